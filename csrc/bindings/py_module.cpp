@@ -1,0 +1,172 @@
+// pybind11 module `_C`: the Python face of the native runtime.
+//
+// Device buffers cross the boundary as raw pointers (ints) plus a raw
+// hipStream_t, so this module does not depend on PyTorch's HIP headers; the
+// Python wrappers in `dmlc.ops` / `dmlc.runtime` pass `tensor.data_ptr()` and
+// `torch.cuda.current_stream().cuda_stream`.
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "../kernels/kernels.h"
+#include "../runtime/engine.h"
+#include "../runtime/ot_io.h"
+
+namespace py = pybind11;
+using namespace dmlc;
+
+namespace {
+
+template <typename T>
+T* P(uintptr_t v) {
+  return reinterpret_cast<T*>(v);
+}
+hipStream_t S(uintptr_t v) { return reinterpret_cast<hipStream_t>(v); }
+
+WeightMap to_weight_map(const py::dict& d) {
+  WeightMap w;
+  for (auto item : d) {
+    auto name = py::cast<std::string>(item.first);
+    auto arr = py::array_t<float, py::array::c_style | py::array::forcecast>::ensure(item.second);
+    if (!arr) throw std::invalid_argument("weight " + name + " is not convertible to float32");
+    HostTensor h;
+    for (py::ssize_t i = 0; i < arr.ndim(); ++i) h.shape.push_back(arr.shape(i));
+    h.data.assign(arr.data(), arr.data() + arr.size());
+    w.emplace(name, std::move(h));
+  }
+  return w;
+}
+
+py::dict from_weight_map(const WeightMap& w) {
+  py::dict d;
+  for (const auto& kv : w) {
+    std::vector<py::ssize_t> shape(kv.second.shape.begin(), kv.second.shape.end());
+    py::array_t<float> a(shape);
+    std::copy(kv.second.data.begin(), kv.second.data.end(), a.mutable_data());
+    d[py::str(kv.first)] = a;
+  }
+  return d;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "dmlc native runtime: CDNA4 HIP kernels, inference engine, .ot I/O";
+
+  // ---------------------------------------------------------------- ops
+  m.def("conv_kpad", &conv_kpad);
+  m.def("conv_npad", &conv_npad);
+  m.def("conv_out_dim", &conv_out_dim);
+  m.def(
+      "conv2d",
+      [](uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t res, uintptr_t y, int B, int H, int W,
+         int Cin, int KH, int KW, int stride, int pad, int N, int Npad, int Kpad, int ldo, bool relu,
+         bool out_f32, int split_k, uintptr_t ws, int tile, uintptr_t stream) {
+        ConvArgs a;
+        a.x = P<void>(x);
+        a.w = P<void>(w);
+        a.bias = P<float>(bias);
+        a.res = P<void>(res);
+        a.y = P<void>(y);
+        a.B = B;
+        a.H = H;
+        a.W = W;
+        a.Cin = Cin;
+        a.KH = KH;
+        a.KW = KW;
+        a.stride = stride;
+        a.pad = pad;
+        a.Ho = conv_out_dim(H, KH, stride, pad);
+        a.Wo = conv_out_dim(W, KW, stride, pad);
+        a.N = N;
+        a.Npad = Npad;
+        a.Kpad = Kpad;
+        a.ldo = ldo;
+        a.relu = relu;
+        a.out_f32 = out_f32;
+        a.split_k = split_k;
+        a.ws = P<float>(ws);
+        a.tile = tile;
+        conv2d_igemm(a, S(stream));
+      },
+      py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("res"), py::arg("y"), py::arg("B"),
+      py::arg("H"), py::arg("W"), py::arg("Cin"), py::arg("KH"), py::arg("KW"), py::arg("stride"),
+      py::arg("pad"), py::arg("N"), py::arg("Npad"), py::arg("Kpad"), py::arg("ldo"),
+      py::arg("relu"), py::arg("out_f32"), py::arg("split_k"), py::arg("ws"), py::arg("tile"),
+      py::arg("stream"));
+  m.def("maxpool2d", [](uintptr_t x, uintptr_t y, int B, int H, int W, int C, int k, int stride,
+                        int pad, uintptr_t stream) {
+    maxpool2d(P<void>(x), P<void>(y), B, H, W, C, conv_out_dim(H, k, stride, pad),
+              conv_out_dim(W, k, stride, pad), k, stride, pad, S(stream));
+  });
+  m.def("avgpool_global", [](uintptr_t x, uintptr_t y, int B, int HW, int C, uintptr_t stream) {
+    avgpool_global(P<void>(x), P<void>(y), B, HW, C, S(stream));
+  });
+  m.def("avgpool_adaptive", [](uintptr_t x, uintptr_t y, int B, int H, int W, int C, int Ho, int Wo,
+                               uintptr_t stream) {
+    avgpool_adaptive(P<void>(x), P<void>(y), B, H, W, C, Ho, Wo, S(stream));
+  });
+  m.def("preprocess_u8", [](uintptr_t x, uintptr_t y, int B, int Hin, int Win, int S_,
+                            uintptr_t stream) {
+    preprocess_u8(P<uint8_t>(x), P<void>(y), B, Hin, Win, S_, S(stream));
+  });
+  m.def("softmax_top1", [](uintptr_t logits, int B, int N, int ld, uintptr_t idx, uintptr_t prob,
+                           uintptr_t stream) {
+    softmax_top1(P<float>(logits), B, N, ld, P<int32_t>(idx), P<float>(prob), S(stream));
+  });
+
+  // ---------------------------------------------------------------- .ot
+  m.def("ot_load", [](const std::string& path) { return from_weight_map(ot_load(path)); });
+  m.def("ot_save", [](const std::string& path, const py::dict& d) { ot_save(path, to_weight_map(d)); });
+
+  // ---------------------------------------------------------------- engine
+  py::class_<Engine>(m, "Engine")
+      .def(py::init([](const std::string& arch, const py::dict& weights, int device, int num_classes,
+                       int image_size) {
+             return new Engine(arch, to_weight_map(weights), device, num_classes, image_size);
+           }),
+           py::arg("arch"), py::arg("weights"), py::arg("device") = 0, py::arg("num_classes") = 1000,
+           py::arg("image_size") = 224)
+      .def_static(
+          "from_ot",
+          [](const std::string& arch, const std::string& path, int device, int num_classes,
+             int image_size) { return new Engine(arch, ot_load(path), device, num_classes, image_size); },
+          py::arg("arch"), py::arg("path"), py::arg("device") = 0, py::arg("num_classes") = 1000,
+          py::arg("image_size") = 224)
+      .def("reserve", &Engine::reserve, py::call_guard<py::gil_scoped_release>())
+      .def(
+          "forward",
+          [](Engine& e, uintptr_t images, int B, int Hin, int Win, uintptr_t idx, uintptr_t prob,
+             uintptr_t logits, uintptr_t stream, bool use_graph) {
+            e.forward(P<uint8_t>(images), B, Hin, Win, P<int32_t>(idx), P<float>(prob), P<float>(logits),
+                      S(stream), use_graph);
+          },
+          py::arg("images"), py::arg("B"), py::arg("Hin"), py::arg("Win"), py::arg("idx"),
+          py::arg("prob"), py::arg("logits"), py::arg("stream"), py::arg("use_graph") = true,
+          py::call_guard<py::gil_scoped_release>())
+      .def("profile",
+           [](Engine& e, uintptr_t images, int B, int Hin, int Win, uintptr_t stream) {
+             return e.profile(P<uint8_t>(images), B, Hin, Win, S(stream));
+           })
+      .def("activation_ptr", [](const Engine& e, int id) { return reinterpret_cast<uintptr_t>(e.activation(id)); })
+      .def("activation_shape",
+           [](const Engine& e, int id) {
+             auto s = e.activation_shape(id);
+             return py::make_tuple(s.H, s.W, s.C, s.f32);
+           })
+      .def("op_list",
+           [](const Engine& e) {
+             py::list l;
+             for (const auto& op : e.ops()) l.append(py::make_tuple(op.name, op.in, op.out, op.res));
+             return l;
+           })
+      .def_property_readonly("num_activations", &Engine::num_activations)
+      .def_property_readonly("arch", &Engine::arch)
+      .def_property_readonly("device", &Engine::device)
+      .def_property_readonly("num_classes", &Engine::num_classes)
+      .def_property_readonly("image_size", &Engine::image_size)
+      .def_property_readonly("max_batch", &Engine::max_batch)
+      .def_property_readonly("weight_bytes", &Engine::weight_bytes)
+      .def_property_readonly("activation_bytes", &Engine::activation_bytes)
+      .def_property_readonly("gflop_per_image", &Engine::gflop_per_image);
+}

@@ -1,0 +1,397 @@
+// Implicit-GEMM convolution on CDNA4 bf16 MFMA (v_mfma_f32_16x16x32_bf16).
+//
+// Replaces the libtorch CPU conv/BN/ReLU/linear ops that the reference runs
+// per query inside `forward_t` (reference: src/services.rs:493, models built at
+// src/services.rs:513-524). GEMM view: M = B*Ho*Wo output pixels, N = Cout,
+// K = KH*KW*Cin with activations in NHWC so every 8-wide k chunk is 16
+// contiguous bytes.
+//
+// Design (gfx950):
+//  * 256-thread workgroups = 4 waves of 64; each wave owns a 64x64 output
+//    sub-tile = 4x4 MFMA 16x16 tiles (16 fp32x4 accumulators).
+//  * The MFMA is issued "swapped": A operand = weight rows (n), B operand =
+//    activation rows (m), so each lane ends with 4 consecutive output
+//    channels of one pixel -> 8-byte packed bf16 stores straight to NHWC.
+//  * Operand tiles are staged global -> VGPR -> LDS, double buffered with one
+//    barrier per K-tile; loads for tile t+1 are issued before the MFMAs of
+//    tile t. LDS rows are XOR-swizzled per 16-B chunk so that the
+//    ds_read_b128 fragment reads (16 rows x same chunk per lane group) are
+//    bank-conflict free (see the derivation next to lds_chunk()).
+//  * Out-of-bounds taps (padding) load zeros; the 3-channel stems use a
+//    packed-tap layout (Cin padded to 4, two taps per 16-B chunk) instead of
+//    padding Cin to 64.
+//  * Epilogue fuses folded-BN bias, residual add and ReLU.
+//  * Optional split-K writes fp32 partials that a small kernel reduces (used
+//    when the tile grid cannot fill the 256 CUs, e.g. batch-1 latency runs
+//    and the AlexNet classifier).
+//  * blockIdx is remapped so consecutive tiles (which share activation rows)
+//    run on the same XCD / L2.
+#include "common.h"
+#include "kernels.h"
+
+#include <algorithm>
+
+namespace dmlc {
+
+namespace {
+
+// Physical 16-B chunk index inside an LDS tile.
+//  128-B rows (BK=64, 8 chunks): phys = chunk ^ ((row>>1)&7). A ds_read_b128
+//  lane group holds 16 distinct rows (mod 16) at chunks c / c+1; the XOR
+//  spreads them over all 16 slots of the 256-B bank row.
+//  64-B rows (BK=32, 4 chunks): phys = chunk ^ g((row>>2)&3), g = {0,2,3,1}.
+template <bool C4>
+__device__ __forceinline__ int lds_chunk(int row, int chunk) {
+  if constexpr (!C4) {
+    return row * 8 + (chunk ^ ((row >> 1) & 7));
+  } else {
+    const int g = (0x1320 >> (((row >> 2) & 3) * 4)) & 3;
+    return row * 4 + (chunk ^ g);
+  }
+}
+
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  // Bijective: blocks b and b+8 share an XCD; give each XCD a contiguous
+  // range of logical tiles.
+  const int q = nwg / 8, r = nwg % 8;
+  const int xcd = bid % 8, local = bid / 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + local;
+}
+
+template <int BM, int BN, int WM, int WN, bool C4>
+__global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a, int kt_per_split,
+                                                         int k_tiles) {
+  constexpr int BK = C4 ? 32 : 64;
+  constexpr int CPR = BK / 8;         // 16-B chunks per LDS row
+  constexpr int RPP = 256 / CPR;      // rows covered by one pass of the block
+  constexpr int PA = BM / RPP;        // activation passes
+  constexpr int PB = BN / RPP;        // weight passes
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int TM = WTM / 16, TN = WTN / 16;
+  static_assert(WM * WN == 4, "4 waves per block");
+  static_assert(PA * RPP == BM && PB * RPP == BN, "tile/pass mismatch");
+  static_assert(TM >= 1 && TN >= 1, "wave tile");
+  constexpr int A_CH = BM * CPR;      // chunks per A buffer
+  constexpr int BUF_CH = (BM + BN) * CPR;
+
+  extern __shared__ __attribute__((aligned(16))) uint4 smem[];  // 2 * BUF_CH chunks
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave % WM, wn = wave / WM;
+
+  const int M = a.B * a.Ho * a.Wo;
+  const int n_tiles = a.Npad / BN;
+  const int m_tiles = (M + BM - 1) / BM;
+  const int nwg = n_tiles * m_tiles;
+  const int tile = xcd_remap(blockIdx.x, nwg);
+  const int mt = tile / n_tiles, nt = tile % n_tiles;
+  const int m0 = mt * BM, n0 = nt * BN;
+
+  const int split = blockIdx.y;
+  const int kt0 = split * kt_per_split;
+  const int kt1 = min(k_tiles, kt0 + kt_per_split);
+  const int nk = kt1 - kt0;
+
+  const bf16* __restrict__ x = (const bf16*)a.x;
+  const bf16* __restrict__ w = (const bf16*)a.w;
+
+  const int cc = tid % CPR;  // chunk column this thread stages
+  const int rr = tid / CPR;  // first row this thread stages
+
+  // Per staged activation row: input origin and base offset.
+  int hi0[PA], wi0[PA], base[PA];
+#pragma unroll
+  for (int p = 0; p < PA; ++p) {
+    const int m = m0 + rr + p * RPP;
+    if (m < M) {
+      const int hw = a.Ho * a.Wo;
+      const int b = m / hw;
+      const int rem = m - b * hw;
+      const int ho = rem / a.Wo;
+      const int wo = rem - ho * a.Wo;
+      hi0[p] = ho * a.stride - a.pad;
+      wi0[p] = wo * a.stride - a.pad;
+      base[p] = ((b * a.H + hi0[p]) * a.W + wi0[p]) * a.Cin;
+    } else {
+      hi0[p] = -(1 << 28);
+      wi0[p] = 0;
+      base[p] = 0;
+    }
+  }
+  const bf16* __restrict__ wbase = w + (size_t)(n0 + rr) * a.Kpad + cc * 8;
+  const int wstride = RPP * a.Kpad;
+
+  uint4 ra[PA], rb[PB];
+
+#define DMLC_LOAD_TILE(t_)                                                                  \
+  do {                                                                                      \
+    const int t = (t_);                                                                     \
+    if constexpr (!C4) {                                                                    \
+      const int ctiles = a.Cin >> 6;                                                        \
+      const int tap = t / ctiles;                                                           \
+      const int c0 = (t - tap * ctiles) << 6;                                               \
+      const int kh = tap / a.KW;                                                            \
+      const int kw = tap - kh * a.KW;                                                       \
+      const int off = (kh * a.W + kw) * a.Cin + c0 + cc * 8;                                \
+      _Pragma("unroll") for (int p = 0; p < PA; ++p) {                                      \
+        const bool ok = (unsigned)(hi0[p] + kh) < (unsigned)a.H &&                          \
+                        (unsigned)(wi0[p] + kw) < (unsigned)a.W;                            \
+        ra[p] = ok ? *(const uint4*)(x + base[p] + off) : make_uint4(0, 0, 0, 0);           \
+      }                                                                                     \
+    } else {                                                                                \
+      const int ntaps = a.KH * a.KW;                                                        \
+      const int tp0 = t * 8 + cc * 2;                                                       \
+      const int kh0 = tp0 / a.KW, kw0 = tp0 - kh0 * a.KW;                                   \
+      const int tp1 = tp0 + 1;                                                              \
+      const int kh1 = tp1 / a.KW, kw1 = tp1 - kh1 * a.KW;                                   \
+      const int off0 = (kh0 * a.W + kw0) * 4, off1 = (kh1 * a.W + kw1) * 4;                 \
+      _Pragma("unroll") for (int p = 0; p < PA; ++p) {                                      \
+        const bool ok0 = tp0 < ntaps && (unsigned)(hi0[p] + kh0) < (unsigned)a.H &&         \
+                         (unsigned)(wi0[p] + kw0) < (unsigned)a.W;                          \
+        const bool ok1 = tp1 < ntaps && (unsigned)(hi0[p] + kh1) < (unsigned)a.H &&         \
+                         (unsigned)(wi0[p] + kw1) < (unsigned)a.W;                          \
+        const uint2 v0 = ok0 ? *(const uint2*)(x + base[p] + off0) : make_uint2(0, 0);      \
+        const uint2 v1 = ok1 ? *(const uint2*)(x + base[p] + off1) : make_uint2(0, 0);      \
+        ra[p] = make_uint4(v0.x, v0.y, v1.x, v1.y);                                         \
+      }                                                                                     \
+    }                                                                                       \
+    const bf16* wt = wbase + t * BK;                                                        \
+    _Pragma("unroll") for (int p = 0; p < PB; ++p) rb[p] = *(const uint4*)(wt + p * wstride); \
+  } while (0)
+
+#define DMLC_STORE_TILE(buf_)                                                               \
+  do {                                                                                      \
+    uint4* sb = smem + (buf_) * BUF_CH;                                                     \
+    _Pragma("unroll") for (int p = 0; p < PA; ++p) sb[lds_chunk<C4>(rr + p * RPP, cc)] = ra[p]; \
+    _Pragma("unroll") for (int p = 0; p < PB; ++p)                                          \
+      sb[A_CH + lds_chunk<C4>(rr + p * RPP, cc)] = rb[p];                                   \
+  } while (0)
+
+  floatx4 acc[TN][TM];
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fq = lane >> 4;
+
+#define DMLC_COMPUTE(buf_)                                                                  \
+  do {                                                                                      \
+    const uint4* sb = smem + (buf_) * BUF_CH;                                               \
+    _Pragma("unroll") for (int ks = 0; ks < BK / 32; ++ks) {                                \
+      bf16x8 af[TN], bm[TM];                                                                \
+      _Pragma("unroll") for (int i = 0; i < TN; ++i) af[i] = __builtin_bit_cast(            \
+          bf16x8, sb[A_CH + lds_chunk<C4>(wn * WTN + i * 16 + fr, ks * 4 + fq)]);           \
+      _Pragma("unroll") for (int j = 0; j < TM; ++j) bm[j] = __builtin_bit_cast(            \
+          bf16x8, sb[lds_chunk<C4>(wm * WTM + j * 16 + fr, ks * 4 + fq)]);                  \
+      _Pragma("unroll") for (int i = 0; i < TN; ++i)                                        \
+        _Pragma("unroll") for (int j = 0; j < TM; ++j)                                      \
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bm[j], acc[i][j], 0, 0, 0); \
+    }                                                                                       \
+  } while (0)
+
+  if (nk > 0) {
+    DMLC_LOAD_TILE(kt0);
+    DMLC_STORE_TILE(0);
+    __syncthreads();
+    int cur = 0;
+    for (int it = 1; it < nk; ++it) {
+      DMLC_LOAD_TILE(kt0 + it);  // global loads in flight under the MFMAs below
+      DMLC_COMPUTE(cur);
+      DMLC_STORE_TILE(cur ^ 1);
+      __syncthreads();
+      cur ^= 1;
+    }
+    DMLC_COMPUTE(cur);
+  }
+
+#undef DMLC_LOAD_TILE
+#undef DMLC_STORE_TILE
+#undef DMLC_COMPUTE
+
+  // Epilogue. Lane holds D[n = 4*fq + r][m = fr] of each 16x16 tile.
+  if (gridDim.y > 1) {
+    float* __restrict__ ws = a.ws + (size_t)split * M * a.Npad;
+#pragma unroll
+    for (int j = 0; j < TM; ++j) {
+      const int m = m0 + wm * WTM + j * 16 + fr;
+      if (m >= M) continue;
+#pragma unroll
+      for (int i = 0; i < TN; ++i) {
+        const int n = n0 + wn * WTN + i * 16 + fq * 4;
+        *(floatx4*)(ws + (size_t)m * a.Npad + n) = acc[i][j];
+      }
+    }
+    return;
+  }
+
+  const bf16* __restrict__ res = (const bf16*)a.res;
+#pragma unroll
+  for (int j = 0; j < TM; ++j) {
+    const int m = m0 + wm * WTM + j * 16 + fr;
+    if (m >= M) continue;
+#pragma unroll
+    for (int i = 0; i < TN; ++i) {
+      const int n = n0 + wn * WTN + i * 16 + fq * 4;
+      if (n >= a.N) continue;
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      if (a.bias) {
+        const floatx4 bb = *(const floatx4*)(a.bias + n);
+        v[0] += bb[0]; v[1] += bb[1]; v[2] += bb[2]; v[3] += bb[3];
+      }
+      const size_t o = (size_t)m * a.ldo + n;
+      if (res) {
+        const uint2 rv = *(const uint2*)(res + o);
+        v[0] += __uint_as_float(rv.x << 16);
+        v[1] += __uint_as_float(rv.x & 0xffff0000u);
+        v[2] += __uint_as_float(rv.y << 16);
+        v[3] += __uint_as_float(rv.y & 0xffff0000u);
+      }
+      if (a.relu) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+      }
+      if (a.out_f32) {
+        *(floatx4*)((float*)a.y + o) = floatx4{v[0], v[1], v[2], v[3]};
+      } else {
+        *(uint2*)((bf16*)a.y + o) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+      }
+    }
+  }
+}
+
+// Split-K reduction + fused epilogue. One thread per 4 output channels.
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(ConvArgs a, int M, int splits) {
+  const int n4 = a.N / 4;
+  const long total = (long)M * n4;
+  for (long idx = blockIdx.x * 256L + threadIdx.x; idx < total; idx += (long)gridDim.x * 256) {
+    const int m = (int)(idx / n4);
+    const int n = (int)(idx - (long)m * n4) * 4;
+    floatx4 s = {0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < splits; ++k) s += *(const floatx4*)(a.ws + ((size_t)k * M + m) * a.Npad + n);
+    if (a.bias) s += *(const floatx4*)(a.bias + n);
+    const size_t o = (size_t)m * a.ldo + n;
+    if (a.res) {
+      const uint2 rv = *(const uint2*)((const bf16*)a.res + o);
+      s[0] += __uint_as_float(rv.x << 16);
+      s[1] += __uint_as_float(rv.x & 0xffff0000u);
+      s[2] += __uint_as_float(rv.y << 16);
+      s[3] += __uint_as_float(rv.y & 0xffff0000u);
+    }
+    if (a.relu) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) s[r] = fmaxf(s[r], 0.f);
+    }
+    if (a.out_f32) {
+      *(floatx4*)((float*)a.y + o) = s;
+    } else {
+      *(uint2*)((bf16*)a.y + o) = make_uint2(pack2(s[0], s[1]), pack2(s[2], s[3]));
+    }
+  }
+}
+
+struct TileCfg {
+  int bm, bn;
+};
+
+// Tile configurations: 0 = 128x128 (2x2 waves), 1 = 256x64 (4x1 waves),
+// 2 = 64x256 (1x4 waves).
+constexpr TileCfg kTiles[3] = {{128, 128}, {256, 64}, {64, 256}};
+
+int pick_tile(const ConvArgs& a) {
+  if (a.tile >= 0) return a.tile;
+  if (a.Npad % 128 != 0) return 1;
+  const long M = (long)a.B * a.Ho * a.Wo;
+  if (M <= 64 && a.Npad % 256 == 0) return 2;
+  return 0;
+}
+
+template <int BM, int BN, int WM, int WN>
+void launch_cfg(const ConvArgs& a, bool c4, int splits, int kt_per, int k_tiles, hipStream_t s) {
+  const int M = a.B * a.Ho * a.Wo;
+  const int tiles = ((M + BM - 1) / BM) * (a.Npad / BN);
+  dim3 grid(tiles, splits);
+  const size_t lds = (size_t)2 * (BM + BN) * (c4 ? 4 : 8) * 16;
+  if (c4)
+    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, true>), grid, dim3(256), lds, s, a, kt_per, k_tiles);
+  else
+    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, false>), grid, dim3(256), lds, s, a, kt_per, k_tiles);
+  DMLC_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace
+
+int conv_out_dim(int in, int k, int stride, int pad) { return (in + 2 * pad - k) / stride + 1; }
+
+int conv_kpad(int Cin, int KH, int KW) {
+  if (Cin == 4) {
+    const int k = KH * KW * 4;
+    return (k + 31) / 32 * 32;
+  }
+  return KH * KW * Cin;  // Cin % 64 == 0
+}
+
+int conv_npad(int N) {
+  if (N <= 64) return 64;
+  if (N % 64 == 0) return N;  // 192, 320, ...: 256x64 tiles, no padding waste
+  return (N + 127) / 128 * 128;
+}
+
+int conv_pick_split_k(const ConvArgs& a, int num_cus) {
+  const int cfg = pick_tile(a);
+  const int BM = kTiles[cfg].bm, BN = kTiles[cfg].bn;
+  const long M = (long)a.B * a.Ho * a.Wo;
+  const long tiles = ((M + BM - 1) / BM) * (a.Npad / BN);
+  const int BK = a.Cin == 4 ? 32 : 64;
+  const int k_tiles = a.Kpad / BK;
+  if (tiles >= num_cus / 2 || k_tiles < 16) return 1;
+  int s = (int)((num_cus + tiles - 1) / tiles);
+  s = std::min(s, k_tiles / 8);
+  s = std::min(s, 16);
+  return std::max(s, 1);
+}
+
+size_t conv_splitk_ws_elems(const ConvArgs& a) {
+  if (a.split_k <= 1) return 0;
+  return (size_t)a.split_k * a.B * a.Ho * a.Wo * a.Npad;
+}
+
+void conv2d_igemm(const ConvArgs& a, hipStream_t s) {
+  const bool c4 = a.Cin == 4;
+  if (!c4 && a.Cin % 64 != 0) throw std::invalid_argument("conv2d_igemm: Cin must be 4 or a multiple of 64");
+  if (a.Kpad != conv_kpad(a.Cin, a.KH, a.KW)) throw std::invalid_argument("conv2d_igemm: bad Kpad");
+  if (a.N % 4 != 0 || a.N > a.Npad || a.ldo < a.N) throw std::invalid_argument("conv2d_igemm: bad N/ldo");
+  if (a.Ho != conv_out_dim(a.H, a.KH, a.stride, a.pad) || a.Wo != conv_out_dim(a.W, a.KW, a.stride, a.pad))
+    throw std::invalid_argument("conv2d_igemm: bad output dims");
+  if (!a.x || !a.w || !a.y) throw std::invalid_argument("conv2d_igemm: null operand");
+  const int cfg = pick_tile(a);
+  const int BN = kTiles[cfg].bn;
+  if (a.Npad % BN != 0) throw std::invalid_argument("conv2d_igemm: Npad not a multiple of BN");
+  const long M = (long)a.B * a.Ho * a.Wo;
+  if (M <= 0) return;
+  if ((long)a.B * a.H * a.W * a.Cin >= (1L << 31) || M * a.ldo >= (1L << 31))
+    throw std::invalid_argument("conv2d_igemm: tensor too large for 32-bit offsets");
+  const int BK = c4 ? 32 : 64;
+  const int k_tiles = a.Kpad / BK;
+  int splits = std::max(1, a.split_k);
+  if (splits > 1 && !a.ws) throw std::invalid_argument("conv2d_igemm: split-K needs a workspace");
+  const int kt_per = (k_tiles + splits - 1) / splits;
+  splits = (k_tiles + kt_per - 1) / kt_per;
+  ConvArgs b = a;
+  b.split_k = splits;
+  switch (cfg) {
+    case 0: launch_cfg<128, 128, 2, 2>(b, c4, splits, kt_per, k_tiles, s); break;
+    case 1: launch_cfg<256, 64, 4, 1>(b, c4, splits, kt_per, k_tiles, s); break;
+    default: launch_cfg<64, 256, 1, 4>(b, c4, splits, kt_per, k_tiles, s); break;
+  }
+  if (splits > 1) {
+    const long total = M * (a.N / 4);
+    const int blocks = (int)std::min<long>((total + 255) / 256, 4096);
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, s, b, (int)M, splits);
+    DMLC_HIP_CHECK(hipGetLastError());
+  }
+}
+
+}  // namespace dmlc

@@ -1,0 +1,73 @@
+// Host-side launch API for the hand-written gfx950 kernels.
+//
+// Every launcher is asynchronous on the given stream, performs no allocation
+// and no synchronisation (so it can be captured into a hipGraph), and checks
+// operand geometry on the host before launching (a bad shape throws instead
+// of faulting the GPU).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdexcept>
+#include <string>
+
+namespace dmlc {
+
+#define DMLC_HIP_CHECK(expr)                                                          \
+  do {                                                                                \
+    hipError_t _e = (expr);                                                           \
+    if (_e != hipSuccess)                                                             \
+      throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(_e) +    \
+                               " at " + __FILE__ + ":" + std::to_string(__LINE__)); \
+  } while (0)
+
+// Implicit-GEMM convolution (also used for fully-connected layers as a 1x1
+// conv on a [B,1,1,C] tensor).
+//   x    : bf16 NHWC [B, H, W, Cin]   (Cin == 4 selects the packed-tap path used
+//          by the 3-channel stems; otherwise Cin % 64 == 0)
+//   w    : bf16 [Npad, Kpad], k = (kh*KW + kw)*Cin + c, zero padded
+//   bias : fp32 [Npad] (BN folded at load time), may be null
+//   res  : bf16 [M, ldo] residual added before the activation, may be null
+//   y    : bf16 (or fp32 if out_f32) [M, ldo], M = B*Ho*Wo
+struct ConvArgs {
+  const void* x = nullptr;
+  const void* w = nullptr;
+  const float* bias = nullptr;
+  const void* res = nullptr;
+  void* y = nullptr;
+  int B = 0, H = 0, W = 0, Cin = 0;
+  int Ho = 0, Wo = 0, KH = 1, KW = 1, stride = 1, pad = 0;
+  int N = 0, Npad = 0, Kpad = 0, ldo = 0;
+  bool relu = false;
+  bool out_f32 = false;
+  int split_k = 1;          // >1: fp32 partial sums into `ws`, reduced by a 2nd kernel
+  float* ws = nullptr;      // split-K workspace, >= split_k * M * Npad floats
+  int tile = -1;            // force a tile config (-1 = heuristic)
+};
+
+int conv_out_dim(int in, int k, int stride, int pad);
+// K length of the packed weight matrix for a given conv geometry.
+int conv_kpad(int Cin, int KH, int KW);
+int conv_npad(int N);
+size_t conv_splitk_ws_elems(const ConvArgs& a);
+int conv_pick_split_k(const ConvArgs& a, int num_cus);
+void conv2d_igemm(const ConvArgs& a, hipStream_t s);
+
+// 3x3/s2-style max pooling, NHWC bf16, C % 8 == 0.
+void maxpool2d(const void* x, void* y, int B, int H, int W, int C, int Ho, int Wo, int k,
+               int stride, int pad, hipStream_t s);
+// Global average pool [B,H,W,C] -> [B,C] bf16, C % 8 == 0.
+void avgpool_global(const void* x, void* y, int B, int HW, int C, hipStream_t s);
+// Adaptive average pool to (Ho,Wo), NHWC bf16 (AlexNet avgpool(6,6)).
+void avgpool_adaptive(const void* x, void* y, int B, int H, int W, int C, int Ho, int Wo,
+                      hipStream_t s);
+
+// u8 HWC images [B,Hin,Win,3] -> bf16 NHWC4 [B,S,S,4] (4th channel zero).
+// Aspect-preserving bilinear resize of the short side to S, centre crop,
+// /255, ImageNet mean/std normalisation. Identity resize when Hin=Win=S.
+void preprocess_u8(const uint8_t* x, void* y, int B, int Hin, int Win, int S, hipStream_t s);
+
+// Row-wise softmax + top-1 over fp32 logits [B, ld] (first N columns).
+void softmax_top1(const float* logits, int B, int N, int ld, int32_t* idx, float* prob,
+                  hipStream_t s);
+
+}  // namespace dmlc

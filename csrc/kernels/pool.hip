@@ -1,0 +1,136 @@
+// NHWC bf16 pooling kernels (max pool, global average pool, adaptive average
+// pool). These replace the libtorch max_pool2d / adaptive_avg_pool2d calls
+// inside tch-rs resnet18/alexnet `forward_t` (reference: src/services.rs:493).
+// Memory-bound: every lane moves 16 B (8 channels) per access.
+#include "common.h"
+#include "kernels.h"
+
+#include <algorithm>
+
+namespace dmlc {
+
+namespace {
+
+__global__ __launch_bounds__(256) void maxpool_kernel(const bf16* __restrict__ x, bf16* __restrict__ y,
+                                                      int B, int H, int W, int C, int Ho, int Wo,
+                                                      int k, int stride, int pad) {
+  const int c8 = C / 8;
+  const long total = (long)B * Ho * Wo * c8;
+  for (long idx = blockIdx.x * 256L + threadIdx.x; idx < total; idx += (long)gridDim.x * 256) {
+    const int cg = (int)(idx % c8);
+    long t = idx / c8;
+    const int wo = (int)(t % Wo);
+    t /= Wo;
+    const int ho = (int)(t % Ho);
+    const int b = (int)(t / Ho);
+    float m[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) m[i] = -INFINITY;
+    const int h0 = ho * stride - pad, w0 = wo * stride - pad;
+    for (int kh = 0; kh < k; ++kh) {
+      const int h = h0 + kh;
+      if ((unsigned)h >= (unsigned)H) continue;
+      for (int kw = 0; kw < k; ++kw) {
+        const int w = w0 + kw;
+        if ((unsigned)w >= (unsigned)W) continue;
+        const uint4 v = *(const uint4*)(x + (((long)b * H + h) * W + w) * C + cg * 8);
+        float f[8];
+        unpack8(v, f);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) m[i] = fmaxf(m[i], f[i]);
+      }
+    }
+    *(uint4*)(y + idx * 8) = pack8(m);
+  }
+}
+
+// One thread per (b, 8-channel group); loops over HW. HW <= 64 for ResNet.
+__global__ __launch_bounds__(256) void avgpool_global_kernel(const bf16* __restrict__ x,
+                                                             bf16* __restrict__ y, int B, int HW,
+                                                             int C) {
+  const int c8 = C / 8;
+  const long total = (long)B * c8;
+  const float inv = 1.f / HW;
+  for (long idx = blockIdx.x * 256L + threadIdx.x; idx < total; idx += (long)gridDim.x * 256) {
+    const int cg = (int)(idx % c8);
+    const int b = (int)(idx / c8);
+    float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const bf16* p = x + (long)b * HW * C + cg * 8;
+    for (int i = 0; i < HW; ++i) {
+      float f[8];
+      unpack8(*(const uint4*)(p + (long)i * C), f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] += f[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s[j] *= inv;
+    *(uint4*)(y + idx * 8) = pack8(s);
+  }
+}
+
+// torch adaptive_avg_pool2d bin rule: [floor(i*H/Ho), ceil((i+1)*H/Ho)).
+__global__ __launch_bounds__(256) void avgpool_adaptive_kernel(const bf16* __restrict__ x,
+                                                               bf16* __restrict__ y, int B, int H,
+                                                               int W, int C, int Ho, int Wo) {
+  const int c8 = C / 8;
+  const long total = (long)B * Ho * Wo * c8;
+  for (long idx = blockIdx.x * 256L + threadIdx.x; idx < total; idx += (long)gridDim.x * 256) {
+    const int cg = (int)(idx % c8);
+    long t = idx / c8;
+    const int wo = (int)(t % Wo);
+    t /= Wo;
+    const int ho = (int)(t % Ho);
+    const int b = (int)(t / Ho);
+    const int hs = (ho * H) / Ho, he = ((ho + 1) * H + Ho - 1) / Ho;
+    const int ws = (wo * W) / Wo, we = ((wo + 1) * W + Wo - 1) / Wo;
+    float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int h = hs; h < he; ++h)
+      for (int w = ws; w < we; ++w) {
+        float f[8];
+        unpack8(*(const uint4*)(x + (((long)b * H + h) * W + w) * C + cg * 8), f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s[j] += f[j];
+      }
+    const float inv = 1.f / ((he - hs) * (we - ws));
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s[j] *= inv;
+    *(uint4*)(y + idx * 8) = pack8(s);
+  }
+}
+
+int grid_for(long work) { return (int)std::max<long>(1, std::min<long>((work + 255) / 256, 8192)); }
+
+}  // namespace
+
+void maxpool2d(const void* x, void* y, int B, int H, int W, int C, int Ho, int Wo, int k, int stride,
+               int pad, hipStream_t s) {
+  if (C % 8 != 0) throw std::invalid_argument("maxpool2d: C % 8 != 0");
+  if (Ho != conv_out_dim(H, k, stride, pad) || Wo != conv_out_dim(W, k, stride, pad))
+    throw std::invalid_argument("maxpool2d: bad output dims");
+  const long work = (long)B * Ho * Wo * (C / 8);
+  if (work == 0) return;
+  hipLaunchKernelGGL(maxpool_kernel, dim3(grid_for(work)), dim3(256), 0, s, (const bf16*)x, (bf16*)y,
+                     B, H, W, C, Ho, Wo, k, stride, pad);
+  DMLC_HIP_CHECK(hipGetLastError());
+}
+
+void avgpool_global(const void* x, void* y, int B, int HW, int C, hipStream_t s) {
+  if (C % 8 != 0) throw std::invalid_argument("avgpool_global: C % 8 != 0");
+  const long work = (long)B * (C / 8);
+  if (work == 0) return;
+  hipLaunchKernelGGL(avgpool_global_kernel, dim3(grid_for(work)), dim3(256), 0, s, (const bf16*)x,
+                     (bf16*)y, B, HW, C);
+  DMLC_HIP_CHECK(hipGetLastError());
+}
+
+void avgpool_adaptive(const void* x, void* y, int B, int H, int W, int C, int Ho, int Wo,
+                      hipStream_t s) {
+  if (C % 8 != 0) throw std::invalid_argument("avgpool_adaptive: C % 8 != 0");
+  const long work = (long)B * Ho * Wo * (C / 8);
+  if (work == 0) return;
+  hipLaunchKernelGGL(avgpool_adaptive_kernel, dim3(grid_for(work)), dim3(256), 0, s, (const bf16*)x,
+                     (bf16*)y, B, H, W, C, Ho, Wo);
+  DMLC_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace dmlc

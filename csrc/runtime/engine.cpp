@@ -1,0 +1,427 @@
+// GPU inference engine implementation (see engine.h).
+//
+// Model definitions follow the torchvision/tch-rs layer naming that the
+// reference's `.ot` checkpoints use (tch::vision::resnet::resnet18 and
+// tch::vision::alexnet::alexnet, constructed at src/services.rs:515,521):
+// conv1/bn1/layer{1..4}.{i}.{conv,bn}{1,2[,3]}/downsample.{0,1}/fc and
+// features.{0,3,6,8,10}/classifier.{1,4,6}.
+#include "engine.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <stdexcept>
+
+namespace dmlc {
+
+namespace {
+
+size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+const HostTensor& need(const WeightMap& w, const std::string& k) {
+  auto it = w.find(k);
+  if (it == w.end()) throw std::runtime_error("missing weight: " + k);
+  return it->second;
+}
+
+const HostTensor* maybe(const WeightMap& w, const std::string& k) {
+  auto it = w.find(k);
+  return it == w.end() ? nullptr : &it->second;
+}
+
+uint16_t f2bf_host(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return 0x7fc0;  // NaN
+  u += 0x7fffu + ((u >> 16) & 1u);                        // round to nearest even
+  return (uint16_t)(u >> 16);
+}
+
+}  // namespace
+
+Engine::Engine(const std::string& arch, const WeightMap& weights, int device, int num_classes,
+               int image_size)
+    : arch_(arch), device_(device), num_classes_(num_classes), image_size_(image_size) {
+  if (num_classes % 4 != 0) throw std::invalid_argument("num_classes must be a multiple of 4");
+  DMLC_HIP_CHECK(hipSetDevice(device_));
+  hipDeviceProp_t prop;
+  DMLC_HIP_CHECK(hipGetDeviceProperties(&prop, device_));
+  num_cus_ = prop.multiProcessorCount;
+
+  if (arch == "resnet18")
+    build_resnet({2, 2, 2, 2}, false);
+  else if (arch == "resnet34")
+    build_resnet({3, 4, 6, 3}, false);
+  else if (arch == "resnet50")
+    build_resnet({3, 4, 6, 3}, true);
+  else if (arch == "alexnet")
+    build_alexnet();
+  else
+    throw std::invalid_argument("unknown arch: " + arch);
+
+  pack_weights(weights);
+  DMLC_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  DMLC_HIP_CHECK(hipEventCreateWithFlags(&ev_in_, hipEventDisableTiming));
+  DMLC_HIP_CHECK(hipEventCreateWithFlags(&ev_out_, hipEventDisableTiming));
+  ws_elems_ = (size_t)16 << 20;  // 64 MB split-K workspace
+  DMLC_HIP_CHECK(hipMalloc(&ws_, ws_elems_ * sizeof(float)));
+}
+
+Engine::~Engine() {
+  hipSetDevice(device_);
+  for (auto& kv : graphs_) hipGraphExecDestroy(kv.second);
+  if (!acts_.empty() && acts_[0]) hipFree(acts_[0]);
+  if (warena_) hipFree(warena_);
+  if (ws_) hipFree(ws_);
+  if (dummy_idx_) hipFree(dummy_idx_);
+  if (ev_in_) hipEventDestroy(ev_in_);
+  if (ev_out_) hipEventDestroy(ev_out_);
+  if (stream_) hipStreamDestroy(stream_);
+}
+
+int Engine::add_act(ActShape s) {
+  shapes_.push_back(s);
+  return (int)shapes_.size() - 1;
+}
+
+int Engine::conv(int in, const std::string& name, const std::string& bn, int cout, int k,
+                 int stride, int pad, bool relu, int res) {
+  const ActShape is = shapes_.at(in);
+  ConvLayer L;
+  L.name = name;
+  L.bn = bn;
+  L.cin_eff = is.C;
+  L.cin = is.C == 4 ? 3 : is.C;
+  L.cout = cout;
+  L.kh = L.kw = k;
+  L.stride = stride;
+  L.pad = pad;
+  L.relu = relu;
+  convs_.push_back(L);
+  ActShape os{conv_out_dim(is.H, k, stride, pad), conv_out_dim(is.W, k, stride, pad), cout, false};
+  const int out = add_act(os);
+  Op op{OpType::Conv, in, out, res, (int)convs_.size() - 1, 0, 0, 0, name};
+  ops_.push_back(op);
+  return out;
+}
+
+int Engine::fc(int in, const std::string& name, int cout, bool relu, bool last) {
+  const ActShape is = shapes_.at(in);
+  ConvLayer L;
+  L.name = name;
+  L.fc = true;
+  L.cin = L.cin_eff = is.H * is.W * is.C;
+  if (is.H * is.W > 1) {
+    L.fc_hwc[0] = is.H;
+    L.fc_hwc[1] = is.W;
+    L.fc_hwc[2] = is.C;
+  }
+  L.cout = cout;
+  L.relu = relu;
+  convs_.push_back(L);
+  const int out = add_act(ActShape{1, 1, cout, last});
+  ops_.push_back(Op{OpType::Conv, in, out, -1, (int)convs_.size() - 1, 0, 0, 0, name});
+  return out;
+}
+
+void Engine::build_resnet(const std::vector<int>& blocks, bool bottleneck) {
+  const int S = image_size_;
+  int x = add_act(ActShape{S, S, 4, false});
+  ops_.push_back(Op{OpType::Preprocess, -1, x, -1, -1, 0, 0, 0, "preprocess"});
+  x = conv(x, "conv1", "bn1", 64, 7, 2, 3, true);
+  {
+    const ActShape s = shapes_[x];
+    const int y = add_act(ActShape{conv_out_dim(s.H, 3, 2, 1), conv_out_dim(s.W, 3, 2, 1), s.C, false});
+    ops_.push_back(Op{OpType::MaxPool, x, y, -1, -1, 3, 2, 1, "maxpool"});
+    x = y;
+  }
+  int inplanes = 64;
+  for (int li = 0; li < 4; ++li) {
+    const int planes = 64 << li;
+    for (int bi = 0; bi < blocks[li]; ++bi) {
+      const int stride = (li > 0 && bi == 0) ? 2 : 1;
+      const std::string p = "layer" + std::to_string(li + 1) + "." + std::to_string(bi);
+      const int outp = bottleneck ? planes * 4 : planes;
+      int identity = x;
+      if (stride != 1 || inplanes != outp)
+        identity = conv(x, p + ".downsample.0", p + ".downsample.1", outp, 1, stride, 0, false);
+      if (!bottleneck) {
+        const int y = conv(x, p + ".conv1", p + ".bn1", planes, 3, stride, 1, true);
+        x = conv(y, p + ".conv2", p + ".bn2", planes, 3, 1, 1, true, identity);
+      } else {
+        int y = conv(x, p + ".conv1", p + ".bn1", planes, 1, 1, 0, true);
+        y = conv(y, p + ".conv2", p + ".bn2", planes, 3, stride, 1, true);
+        x = conv(y, p + ".conv3", p + ".bn3", outp, 1, 1, 0, true, identity);
+      }
+      inplanes = outp;
+    }
+  }
+  {
+    const ActShape s = shapes_[x];
+    const int y = add_act(ActShape{1, 1, s.C, false});
+    ops_.push_back(Op{OpType::AvgPoolGlobal, x, y, -1, -1, 0, 0, 0, "avgpool"});
+    x = y;
+  }
+  logits_act_ = fc(x, "fc", num_classes_, false, true);
+  ops_.push_back(Op{OpType::SoftmaxTop1, logits_act_, -1, -1, -1, 0, 0, 0, "softmax_top1"});
+}
+
+void Engine::build_alexnet() {
+  const int S = image_size_;
+  int x = add_act(ActShape{S, S, 4, false});
+  ops_.push_back(Op{OpType::Preprocess, -1, x, -1, -1, 0, 0, 0, "preprocess"});
+  auto pool = [&](int in, const std::string& n) {
+    const ActShape s = shapes_[in];
+    const int y = add_act(ActShape{conv_out_dim(s.H, 3, 2, 0), conv_out_dim(s.W, 3, 2, 0), s.C, false});
+    ops_.push_back(Op{OpType::MaxPool, in, y, -1, -1, 3, 2, 0, n});
+    return y;
+  };
+  x = conv(x, "features.0", "", 64, 11, 4, 2, true);
+  x = pool(x, "features.2");
+  x = conv(x, "features.3", "", 192, 5, 1, 2, true);
+  x = pool(x, "features.5");
+  x = conv(x, "features.6", "", 384, 3, 1, 1, true);
+  x = conv(x, "features.8", "", 256, 3, 1, 1, true);
+  x = conv(x, "features.10", "", 256, 3, 1, 1, true);
+  x = pool(x, "features.12");
+  {
+    const ActShape s = shapes_[x];
+    if (!(s.H == 6 && s.W == 6)) {
+      const int y = add_act(ActShape{6, 6, s.C, false});
+      ops_.push_back(Op{OpType::AvgPoolAdaptive, x, y, -1, -1, 0, 0, 0, "avgpool"});
+      x = y;
+    }
+  }
+  x = fc(x, "classifier.1", 4096, true, false);
+  x = fc(x, "classifier.4", 4096, true, false);
+  logits_act_ = fc(x, "classifier.6", num_classes_, false, true);
+  ops_.push_back(Op{OpType::SoftmaxTop1, logits_act_, -1, -1, -1, 0, 0, 0, "softmax_top1"});
+}
+
+void Engine::pack_weights(const WeightMap& w) {
+  // Layout pass.
+  size_t off = 0;
+  for (auto& L : convs_) {
+    L.npad = conv_npad(L.cout);
+    L.kpad = conv_kpad(L.cin_eff, L.kh, L.kw);
+    L.w_off = off;
+    off = align_up(off + (size_t)L.npad * L.kpad * 2, 256);
+    L.b_off = off;
+    off = align_up(off + (size_t)L.npad * 4, 256);
+  }
+  weight_bytes_ = off;
+  std::vector<uint8_t> host(off, 0);
+  for (auto& L : convs_) {
+    const HostTensor& W = need(w, L.name + ".weight");
+    const HostTensor* cb = maybe(w, L.name + ".bias");
+    std::vector<float> scale(L.cout, 1.f), bias(L.cout, 0.f);
+    if (cb) {
+      if (cb->numel() != L.cout) throw std::runtime_error("bad bias size: " + L.name);
+      for (int n = 0; n < L.cout; ++n) bias[n] = cb->data[n];
+    }
+    if (!L.bn.empty()) {
+      const HostTensor& g = need(w, L.bn + ".weight");
+      const HostTensor& b = need(w, L.bn + ".bias");
+      const HostTensor& m = need(w, L.bn + ".running_mean");
+      const HostTensor& v = need(w, L.bn + ".running_var");
+      for (int n = 0; n < L.cout; ++n) {
+        const double s = (double)g.data[n] / std::sqrt((double)v.data[n] + 1e-5);
+        scale[n] = (float)s;
+        bias[n] = (float)((double)b.data[n] + ((double)bias[n] - (double)m.data[n]) * s);
+      }
+    }
+    uint16_t* pw = (uint16_t*)(host.data() + L.w_off);
+    float* pb = (float*)(host.data() + L.b_off);
+    if (!L.fc) {
+      if (W.shape.size() != 4 || W.shape[0] != L.cout || W.shape[1] != L.cin || W.shape[2] != L.kh ||
+          W.shape[3] != L.kw)
+        throw std::runtime_error("bad conv weight shape: " + L.name);
+      for (int n = 0; n < L.cout; ++n)
+        for (int c = 0; c < L.cin; ++c)
+          for (int i = 0; i < L.kh; ++i)
+            for (int j = 0; j < L.kw; ++j) {
+              const float v = W.data[(((size_t)n * L.cin + c) * L.kh + i) * L.kw + j] * scale[n];
+              pw[(size_t)n * L.kpad + (size_t)(i * L.kw + j) * L.cin_eff + c] = f2bf_host(v);
+            }
+    } else {
+      if (W.shape.size() != 2 || W.shape[0] != L.cout || W.shape[1] != L.cin)
+        throw std::runtime_error("bad linear weight shape: " + L.name);
+      const int H = L.fc_hwc[0], Wd = L.fc_hwc[1], C = L.fc_hwc[2];
+      for (int n = 0; n < L.cout; ++n)
+        for (int k = 0; k < L.cin; ++k) {
+          int dst = k;
+          if (H > 0) {  // torch flattens NCHW (c,h,w); our activations are NHWC (h,w,c)
+            const int c = k / (H * Wd), hw = k % (H * Wd);
+            dst = hw * C + c;
+          }
+          pw[(size_t)n * L.kpad + dst] = f2bf_host(W.data[(size_t)n * L.cin + k] * scale[n]);
+        }
+    }
+    for (int n = 0; n < L.cout; ++n) pb[n] = bias[n];
+  }
+  DMLC_HIP_CHECK(hipMalloc(&warena_, weight_bytes_));
+  DMLC_HIP_CHECK(hipMemcpy(warena_, host.data(), weight_bytes_, hipMemcpyHostToDevice));
+}
+
+void Engine::reserve(int max_batch) {
+  if (max_batch <= max_batch_) return;
+  DMLC_HIP_CHECK(hipSetDevice(device_));
+  DMLC_HIP_CHECK(hipDeviceSynchronize());
+  for (auto& kv : graphs_) hipGraphExecDestroy(kv.second);
+  graphs_.clear();
+  if (!acts_.empty() && acts_[0]) DMLC_HIP_CHECK(hipFree(acts_[0]));
+  if (dummy_idx_) DMLC_HIP_CHECK(hipFree(dummy_idx_));
+  std::vector<size_t> offs;
+  size_t total = 0;
+  for (const auto& s : shapes_) {
+    offs.push_back(total);
+    total = align_up(total + s.elems_per_image() * max_batch * (s.f32 ? 4 : 2), 256);
+  }
+  void* base = nullptr;
+  DMLC_HIP_CHECK(hipMalloc(&base, total));
+  acts_.clear();
+  for (size_t o : offs) acts_.push_back((uint8_t*)base + o);
+  act_bytes_ = total;
+  DMLC_HIP_CHECK(hipMalloc(&dummy_idx_, (size_t)max_batch * 8));
+  max_batch_ = max_batch;
+}
+
+double Engine::gflop_per_image() const {
+  double f = 0;
+  for (const auto& op : ops_) {
+    if (op.type != OpType::Conv) continue;
+    const ConvLayer& L = convs_[op.conv];
+    const ActShape& o = shapes_[op.out];
+    f += 2.0 * o.H * o.W * L.cout * (double)L.cin * L.kh * L.kw;
+  }
+  return f * 1e-9;
+}
+
+ConvArgs Engine::conv_args(const Op& op, int B, float* logits) const {
+  const ConvLayer& L = convs_[op.conv];
+  const ActShape& is = shapes_[op.in];
+  const ActShape& os = shapes_[op.out];
+  ConvArgs a;
+  a.x = acts_[op.in];
+  a.w = (const uint8_t*)warena_ + L.w_off;
+  a.bias = (const float*)((const uint8_t*)warena_ + L.b_off);
+  a.res = op.res >= 0 ? acts_[op.res] : nullptr;
+  a.y = (os.f32 && logits) ? (void*)logits : acts_[op.out];
+  a.B = B;
+  if (L.fc) {
+    a.H = a.W = 1;
+    a.Cin = L.cin_eff;
+  } else {
+    a.H = is.H;
+    a.W = is.W;
+    a.Cin = is.C;
+  }
+  a.KH = L.kh;
+  a.KW = L.kw;
+  a.stride = L.stride;
+  a.pad = L.pad;
+  a.Ho = os.H;
+  a.Wo = os.W;
+  a.N = L.cout;
+  a.Npad = L.npad;
+  a.Kpad = L.kpad;
+  a.ldo = L.cout;
+  a.relu = L.relu;
+  a.out_f32 = os.f32;
+  int s = conv_pick_split_k(a, num_cus_);
+  const size_t M = (size_t)B * os.H * os.W;
+  while (s > 1 && (size_t)s * M * L.npad > ws_elems_) --s;
+  a.split_k = s;
+  a.ws = ws_;
+  return a;
+}
+
+void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* idx, float* prob,
+                     float* logits, hipStream_t s, std::vector<hipEvent_t>* evs) {
+  size_t ei = 0;
+  if (evs) DMLC_HIP_CHECK(hipEventRecord((*evs)[ei++], s));
+  for (const Op& op : ops_) {
+    switch (op.type) {
+      case OpType::Preprocess:
+        preprocess_u8(images, acts_[op.out], B, Hin, Win, image_size_, s);
+        break;
+      case OpType::Conv:
+        conv2d_igemm(conv_args(op, B, logits), s);
+        break;
+      case OpType::MaxPool: {
+        const ActShape& i = shapes_[op.in];
+        const ActShape& o = shapes_[op.out];
+        maxpool2d(acts_[op.in], acts_[op.out], B, i.H, i.W, i.C, o.H, o.W, op.k, op.stride, op.pad, s);
+        break;
+      }
+      case OpType::AvgPoolGlobal: {
+        const ActShape& i = shapes_[op.in];
+        avgpool_global(acts_[op.in], acts_[op.out], B, i.H * i.W, i.C, s);
+        break;
+      }
+      case OpType::AvgPoolAdaptive: {
+        const ActShape& i = shapes_[op.in];
+        const ActShape& o = shapes_[op.out];
+        avgpool_adaptive(acts_[op.in], acts_[op.out], B, i.H, i.W, i.C, o.H, o.W, s);
+        break;
+      }
+      case OpType::SoftmaxTop1: {
+        const float* lg = logits ? logits : (const float*)acts_[op.in];
+        softmax_top1(lg, B, num_classes_, num_classes_, idx ? idx : dummy_idx_,
+                     prob ? prob : (float*)(dummy_idx_ + max_batch_), s);
+        break;
+      }
+    }
+    if (evs) DMLC_HIP_CHECK(hipEventRecord((*evs)[ei++], s));
+  }
+}
+
+void Engine::forward(const uint8_t* images, int B, int Hin, int Win, int32_t* idx, float* prob,
+                     float* logits, hipStream_t stream, bool use_graph) {
+  if (B <= 0) return;
+  if (B > max_batch_) throw std::invalid_argument("batch exceeds reserved max_batch");
+  if (!images) throw std::invalid_argument("null images");
+  DMLC_HIP_CHECK(hipSetDevice(device_));
+  DMLC_HIP_CHECK(hipEventRecord(ev_in_, stream));
+  DMLC_HIP_CHECK(hipStreamWaitEvent(stream_, ev_in_, 0));
+  if (use_graph) {
+    GraphKey key{images, B, Hin, Win, idx, prob, logits};
+    auto it = graphs_.find(key);
+    if (it == graphs_.end()) {
+      hipGraph_t g;
+      DMLC_HIP_CHECK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
+      run_ops(images, B, Hin, Win, idx, prob, logits, stream_, nullptr);
+      DMLC_HIP_CHECK(hipStreamEndCapture(stream_, &g));
+      hipGraphExec_t ex;
+      DMLC_HIP_CHECK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+      DMLC_HIP_CHECK(hipGraphDestroy(g));
+      it = graphs_.emplace(key, ex).first;
+    }
+    DMLC_HIP_CHECK(hipGraphLaunch(it->second, stream_));
+  } else {
+    run_ops(images, B, Hin, Win, idx, prob, logits, stream_, nullptr);
+  }
+  DMLC_HIP_CHECK(hipEventRecord(ev_out_, stream_));
+  DMLC_HIP_CHECK(hipStreamWaitEvent(stream, ev_out_, 0));
+}
+
+std::vector<std::pair<std::string, float>> Engine::profile(const uint8_t* images, int B, int Hin,
+                                                           int Win, hipStream_t stream) {
+  if (B > max_batch_) throw std::invalid_argument("batch exceeds reserved max_batch");
+  DMLC_HIP_CHECK(hipSetDevice(device_));
+  DMLC_HIP_CHECK(hipStreamSynchronize(stream));
+  std::vector<hipEvent_t> evs(ops_.size() + 1);
+  for (auto& e : evs) DMLC_HIP_CHECK(hipEventCreate(&e));
+  run_ops(images, B, Hin, Win, nullptr, nullptr, nullptr, stream_, &evs);
+  DMLC_HIP_CHECK(hipStreamSynchronize(stream_));
+  std::vector<std::pair<std::string, float>> out;
+  for (size_t i = 0; i < ops_.size(); ++i) {
+    float ms = 0;
+    DMLC_HIP_CHECK(hipEventElapsedTime(&ms, evs[i], evs[i + 1]));
+    out.emplace_back(ops_[i].name, ms);
+  }
+  for (auto& e : evs) hipEventDestroy(e);
+  return out;
+}
+
+}  // namespace dmlc

@@ -1,0 +1,127 @@
+// GPU inference engine: model graph + HBM-resident folded weights + static
+// activation arena + hipGraph replay of the whole forward.
+//
+// Reference counterpart: the member-side model objects built at start-up and
+// executed per query (src/services.rs:475-497, 513-524): `resnet18` / `alexnet`
+// from tch::vision on the CPU with batch 1. Here the forward is batched, runs
+// on the hand-written CDNA4 kernels in csrc/kernels, and the whole launch
+// sequence for a given (batch, buffers) is captured once into a hipGraph.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <map>
+#include <memory>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "../kernels/kernels.h"
+#include "weights.h"
+
+namespace dmlc {
+
+enum class OpType { Preprocess, Conv, MaxPool, AvgPoolGlobal, AvgPoolAdaptive, SoftmaxTop1 };
+
+struct ActShape {
+  int H = 0, W = 0, C = 0;
+  bool f32 = false;
+  size_t elems_per_image() const { return (size_t)H * W * C; }
+};
+
+struct ConvLayer {
+  std::string name;  // weight prefix (e.g. "layer1.0.conv1")
+  std::string bn;    // BN prefix or "" (conv bias used instead)
+  int cin = 0, cin_eff = 0, cout = 0, kh = 1, kw = 1, stride = 1, pad = 0;
+  bool relu = false;
+  bool fc = false;        // linear layer (weight [N,K]) run as a 1x1 conv
+  int fc_hwc[3] = {0, 0, 0};  // for fc after a spatial tensor: (H,W,C) of the flatten
+  int npad = 0, kpad = 0;
+  size_t w_off = 0, b_off = 0;  // offsets (bytes) into the weight arena
+};
+
+struct Op {
+  OpType type;
+  int in = -1, out = -1, res = -1;  // activation ids
+  int conv = -1;
+  int k = 0, stride = 0, pad = 0;
+  std::string name;
+};
+
+class Engine {
+ public:
+  // arch: resnet18 | resnet34 | resnet50 | alexnet
+  Engine(const std::string& arch, const WeightMap& weights, int device, int num_classes = 1000,
+         int image_size = 224);
+  ~Engine();
+  Engine(const Engine&) = delete;
+  Engine& operator=(const Engine&) = delete;
+
+  const std::string& arch() const { return arch_; }
+  int device() const { return device_; }
+  int num_classes() const { return num_classes_; }
+  int image_size() const { return image_size_; }
+  int max_batch() const { return max_batch_; }
+  size_t weight_bytes() const { return weight_bytes_; }
+  size_t activation_bytes() const { return act_bytes_; }
+  double gflop_per_image() const;
+
+  // Allocate the activation arena for batches up to max_batch.
+  void reserve(int max_batch);
+
+  // images: device u8 [B, Hin, Win, 3]. Outputs (device): idx int32 [B],
+  // prob f32 [B], optional logits f32 [B, num_classes].
+  // Ordered after all prior work on `stream`; later work on `stream` sees
+  // the outputs. use_graph: replay a captured hipGraph for this exact
+  // (B, pointers) signature (captured on first use).
+  void forward(const uint8_t* images, int B, int Hin, int Win, int32_t* idx, float* prob,
+               float* logits, hipStream_t stream, bool use_graph);
+
+  // Eager forward with an event pair around every op: (op name, ms).
+  std::vector<std::pair<std::string, float>> profile(const uint8_t* images, int B, int Hin,
+                                                     int Win, hipStream_t stream);
+
+  // Device pointer to a stored activation of the last forward (debug/tests).
+  const void* activation(int id) const { return acts_.at(id); }
+  int num_activations() const { return (int)shapes_.size(); }
+  ActShape activation_shape(int id) const { return shapes_.at(id); }
+  const std::vector<Op>& ops() const { return ops_; }
+
+ private:
+  int add_act(ActShape s);
+  int conv(int in, const std::string& name, const std::string& bn, int cout, int k, int stride,
+           int pad, bool relu, int res = -1);
+  int fc(int in, const std::string& name, int cout, bool relu, bool last);
+  void build_resnet(const std::vector<int>& blocks, bool bottleneck);
+  void build_alexnet();
+  void pack_weights(const WeightMap& w);
+  void run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* idx, float* prob,
+               float* logits, hipStream_t s, std::vector<hipEvent_t>* evs);
+  ConvArgs conv_args(const Op& op, int B, float* logits) const;
+
+  std::string arch_;
+  int device_ = 0;
+  int num_classes_ = 1000;
+  int image_size_ = 224;
+  int num_cus_ = 256;
+  int max_batch_ = 0;
+
+  std::vector<ActShape> shapes_;
+  std::vector<ConvLayer> convs_;
+  std::vector<Op> ops_;
+  int logits_act_ = -1;
+
+  void* warena_ = nullptr;
+  size_t weight_bytes_ = 0;
+  std::vector<void*> acts_;
+  size_t act_bytes_ = 0;
+  float* ws_ = nullptr;
+  size_t ws_elems_ = 0;
+  int32_t* dummy_idx_ = nullptr;
+
+  hipStream_t stream_ = nullptr;
+  hipEvent_t ev_in_ = nullptr, ev_out_ = nullptr;
+  using GraphKey = std::tuple<const void*, int, int, int, void*, void*, void*>;
+  std::map<GraphKey, hipGraphExec_t> graphs_;
+};
+
+}  // namespace dmlc

@@ -1,0 +1,73 @@
+"""Whole-model numerics: GPU engine (HIP kernels, BN folded, bf16) vs the
+fp32 torch.nn reference on CPU, for every architecture in the zoo."""
+import pytest
+import torch
+
+from dmlc.models import build, state_dict_f32
+from dmlc.runtime import InferenceEngine
+
+pytestmark = pytest.mark.gpu
+
+MEAN = torch.tensor([0.485, 0.456, 0.406]).view(1, 3, 1, 1)
+STD = torch.tensor([0.229, 0.224, 0.225]).view(1, 3, 1, 1)
+
+
+def _ref_logits(model, img_u8):
+    x = (img_u8.permute(0, 3, 1, 2).float() / 255 - MEAN) / STD
+    with torch.no_grad():
+        return model(x)
+
+
+@pytest.mark.parametrize("arch", ["resnet18", "alexnet", "resnet50", "resnet34"])
+def test_engine_matches_reference(gpu, arch):
+    model = build(arch, seed=11, randomize_bn=True)
+    eng = InferenceEngine(arch, state_dict_f32(model), max_batch=16)
+    g = torch.Generator().manual_seed(12)
+    img = torch.randint(0, 256, (16, 224, 224, 3), generator=g, dtype=torch.uint8)
+    ref = _ref_logits(model, img)
+    idx, prob, logits = eng.predict(img.to(gpu), return_logits=True, use_graph=False)
+    torch.cuda.synchronize()
+    rel = ((logits.cpu() - ref).norm() / ref.norm()).item()
+    assert rel < 3e-2, rel
+    ref_p = torch.softmax(ref, -1)
+    agree = (idx.cpu().long() == ref.argmax(-1)).float().mean().item()
+    # top-1 may flip only on near-ties under bf16
+    top2 = ref_p.topk(2, -1).values
+    near_tie = (top2[:, 0] - top2[:, 1]) < 1e-2
+    mism = idx.cpu().long() != ref.argmax(-1)
+    assert torch.all(~mism | near_tie), (agree, rel)
+    assert torch.allclose(prob.cpu(), ref_p.max(-1).values, rtol=0.1, atol=2e-3)
+
+
+def test_graph_replay_matches_eager(gpu):
+    eng = InferenceEngine("resnet18", max_batch=32)
+    img = torch.randint(0, 256, (32, 224, 224, 3), dtype=torch.uint8, device=gpu)
+    i0, p0 = eng.predict(img, use_graph=False)
+    i1, p1 = eng.predict(img, use_graph=True)
+    i2, p2 = eng.predict(img, use_graph=True)  # replay
+    torch.cuda.synchronize()
+    assert torch.equal(i0, i1) and torch.equal(i1, i2)
+    assert torch.equal(p1, p2)
+
+
+def test_batch_independence(gpu):
+    """A sample's result does not depend on the batch it is in (no cross-
+    sample leakage through tiling / split-K)."""
+    eng = InferenceEngine("resnet18", max_batch=64)
+    img = torch.randint(0, 256, (64, 224, 224, 3), dtype=torch.uint8, device=gpu)
+    _, _, l_all = eng.predict(img, return_logits=True)
+    _, _, l_one = eng.predict(img[5:6].contiguous(), return_logits=True)
+    torch.cuda.synchronize()
+    assert torch.allclose(l_all[5], l_one[0], rtol=2e-2, atol=2e-2)
+
+
+def test_ot_checkpoint_engine(gpu, tmp_path):
+    from dmlc.utils.ot import write_random_checkpoint
+    p = write_random_checkpoint("alexnet", str(tmp_path / "alexnet.ot"), seed=3)
+    e1 = InferenceEngine("alexnet", p, max_batch=4)
+    e2 = InferenceEngine("alexnet", state_dict_f32(build("alexnet", seed=3)), max_batch=4)
+    img = torch.randint(0, 256, (4, 224, 224, 3), dtype=torch.uint8, device=gpu)
+    a = e1.predict(img, return_logits=True)[2]
+    b = e2.predict(img, return_logits=True)[2]
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)

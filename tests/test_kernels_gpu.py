@@ -1,0 +1,174 @@
+"""Numerics of the hand-written gfx950 kernels vs plain PyTorch fp32 references.
+
+Inputs are rounded to bf16 first so the reference sees exactly what the kernel
+sees; the remaining difference is the bf16 output rounding plus fp32
+accumulation order.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+import dmlc
+from dmlc import ops
+
+pytestmark = pytest.mark.gpu
+
+
+def _nhwc(x):
+    return x.permute(0, 2, 3, 1).contiguous()
+
+
+def _nchw(x):
+    return x.permute(0, 3, 1, 2).contiguous()
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12)).item()
+
+
+def test_native_loaded(gpu):
+    import sys
+    C = dmlc.native()
+    assert C.__file__.endswith(".so")
+    assert any("libdmlc_gpu.so" in l for l in open("/proc/self/maps"))
+    assert "dmlc._C" in sys.modules
+
+
+CONV_CASES = [
+    # B, H, W, Cin, Cout, k, stride, pad, relu, res, tile, split
+    (2, 56, 56, 64, 64, 3, 1, 1, True, False, -1, 1),
+    (2, 56, 56, 64, 128, 3, 2, 1, True, False, -1, 1),
+    (2, 56, 56, 64, 128, 1, 2, 0, False, False, -1, 1),
+    (3, 28, 28, 128, 128, 3, 1, 1, True, True, -1, 1),
+    (1, 7, 7, 512, 512, 3, 1, 1, True, True, -1, 4),
+    (2, 13, 13, 192, 384, 3, 1, 1, True, False, -1, 1),
+    (2, 27, 27, 64, 192, 5, 1, 2, True, False, -1, 1),
+    (2, 14, 14, 256, 256, 3, 1, 1, False, False, 1, 1),
+    (2, 14, 14, 256, 256, 3, 1, 1, False, False, 2, 1),
+    (2, 14, 14, 256, 512, 1, 1, 0, False, False, 0, 3),
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES, ids=[str(c) for c in CONV_CASES])
+def test_conv2d_vs_torch(gpu, case):
+    B, H, W, Cin, Cout, k, s, p, relu, use_res, tile, split = case
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(B, Cin, H, W, generator=g).bfloat16().float()
+    w = (torch.randn(Cout, Cin, k, k, generator=g) / (Cin * k * k) ** 0.5).bfloat16().float()
+    bias = torch.randn(Cout, generator=g) * 0.1
+    ref = F.conv2d(x, w, bias, s, p)
+    Ho, Wo = ref.shape[2], ref.shape[3]
+    res = None
+    if use_res:
+        res_nchw = torch.randn(B, Cout, Ho, Wo, generator=g).bfloat16().float()
+        ref = ref + res_nchw
+        res = _nhwc(res_nchw).bfloat16().to(gpu)
+    if relu:
+        ref = F.relu(ref)
+    wp = ops.pack_conv_weight(w, device=gpu)
+    y = ops.conv2d(_nhwc(x).bfloat16().to(gpu), wp, Cout, k, k, s, p, bias=bias.to(gpu), res=res, relu=relu,
+                   split_k=split, tile=tile)
+    torch.cuda.synchronize()
+    got = _nchw(y.float().cpu())
+    assert got.shape == ref.shape
+    assert _rel(got, ref) < 8e-3, _rel(got, ref)
+
+
+@pytest.mark.parametrize("k,s,p,cout", [(7, 2, 3, 64), (11, 4, 2, 64), (3, 1, 1, 128)])
+def test_conv2d_stem_c4(gpu, k, s, p, cout):
+    """3-channel stem: input padded to 4 channels, two taps per 16-B chunk."""
+    g = torch.Generator().manual_seed(2)
+    B, H, W = 2, 57, 61
+    x = torch.randn(B, 3, H, W, generator=g).bfloat16().float()
+    w = (torch.randn(cout, 3, k, k, generator=g) / (3 * k * k) ** 0.5).bfloat16().float()
+    ref = F.relu(F.conv2d(x, w, None, s, p))
+    x4 = torch.zeros(B, H, W, 4)
+    x4[..., :3] = _nhwc(x)
+    wp = ops.pack_conv_weight(w, cin_eff=4, device=gpu)
+    y = ops.conv2d(x4.bfloat16().to(gpu), wp, cout, k, k, s, p, relu=True)
+    torch.cuda.synchronize()
+    assert _rel(_nchw(y.float().cpu()), ref) < 8e-3
+
+
+def test_linear_fp32_out(gpu):
+    """FC = 1x1 conv on [B,1,1,K]; N=1000 padded to 1024, fp32 logits."""
+    g = torch.Generator().manual_seed(3)
+    B, K, N = 5, 512, 1000
+    x = torch.randn(B, K, generator=g).bfloat16().float()
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).bfloat16().float()
+    b = torch.randn(N, generator=g)
+    ref = x @ w.t() + b
+    wp = ops.pack_conv_weight(w.view(N, K, 1, 1), device=gpu)
+    for split in (1, 4):
+        y = ops.conv2d(x.view(B, 1, 1, K).bfloat16().to(gpu), wp, N, 1, 1, bias=b.to(gpu), out_f32=True,
+                       split_k=split)
+        torch.cuda.synchronize()
+        assert y.dtype == torch.float32
+        assert _rel(y.view(B, N).cpu(), ref) < 5e-3
+
+
+def test_maxpool(gpu):
+    g = torch.Generator().manual_seed(4)
+    x = torch.randn(2, 64, 112, 112, generator=g).bfloat16().float()
+    for k, s, p in [(3, 2, 1), (3, 2, 0)]:
+        ref = F.max_pool2d(x, k, s, p)
+        y = ops.maxpool2d(_nhwc(x).bfloat16().to(gpu), k, s, p)
+        torch.cuda.synchronize()
+        assert torch.equal(_nchw(y.float().cpu()), ref)
+
+
+def test_avgpool(gpu):
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(3, 512, 7, 7, generator=g).bfloat16().float()
+    ref = F.adaptive_avg_pool2d(x, 1).view(3, 512)
+    y = ops.avgpool_global(_nhwc(x).bfloat16().to(gpu))
+    torch.cuda.synchronize()
+    assert _rel(y.float().cpu(), ref) < 5e-3
+    x2 = torch.randn(2, 256, 13, 13, generator=g).bfloat16().float()
+    ref2 = F.adaptive_avg_pool2d(x2, (6, 6))
+    y2 = ops.avgpool_adaptive(_nhwc(x2).bfloat16().to(gpu), 6, 6)
+    torch.cuda.synchronize()
+    assert _rel(_nchw(y2.float().cpu()), ref2) < 5e-3
+
+
+MEAN = torch.tensor([0.485, 0.456, 0.406]).view(1, 3, 1, 1)
+STD = torch.tensor([0.229, 0.224, 0.225]).view(1, 3, 1, 1)
+
+
+def test_preprocess_identity(gpu):
+    g = torch.Generator().manual_seed(6)
+    img = torch.randint(0, 256, (3, 224, 224, 3), generator=g, dtype=torch.uint8)
+    ref = (_nchw(img.float()) / 255 - MEAN) / STD
+    y = ops.preprocess_u8(img.to(gpu), 224)
+    torch.cuda.synchronize()
+    y = y.float().cpu()
+    assert torch.all(y[..., 3] == 0)
+    assert _rel(_nchw(y[..., :3].contiguous()), ref) < 4e-3
+
+
+def test_preprocess_resize(gpu):
+    """Short side -> 224, centre crop, bilinear (half-pixel) = torch
+    interpolate(align_corners=False) on the resized image, then crop."""
+    g = torch.Generator().manual_seed(7)
+    img = torch.randint(0, 256, (2, 300, 400, 3), generator=g, dtype=torch.uint8)
+    h, w = 224, round(400 * 224 / 300)
+    rs = F.interpolate(_nchw(img.float()), size=(h, w), mode="bilinear", align_corners=False)
+    ox = (w - 224) // 2
+    ref = (rs[:, :, :, ox:ox + 224] / 255 - MEAN) / STD
+    y = ops.preprocess_u8(img.to(gpu), 224)
+    torch.cuda.synchronize()
+    got = _nchw(y.float().cpu()[..., :3].contiguous())
+    # sub-pixel crop offset differences are allowed: compare on the interior
+    assert _rel(got[..., 4:-4, 4:-4], ref[..., 4:-4, 4:-4]) < 0.06
+
+
+def test_softmax_top1(gpu):
+    g = torch.Generator().manual_seed(8)
+    logits = torch.randn(37, 1000, generator=g) * 3
+    logits[5, 17] = 100.0
+    p = torch.softmax(logits, -1)
+    pv, pi = p.max(-1)
+    idx, prob = ops.softmax_top1(logits.to(gpu))
+    torch.cuda.synchronize()
+    assert torch.equal(idx.cpu().long(), pi)
+    assert torch.allclose(prob.cpu(), pv, rtol=1e-4, atol=1e-6)

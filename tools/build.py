@@ -1,0 +1,166 @@
+#!/usr/bin/env python3
+"""In-tree native build for the dmlc framework (gfx950 only).
+
+Targets (all written inside the repository so they travel with `gpurun`):
+  * ``<pkg>/libdmlc_gpu.so``   hand-written HIP kernels + GPU engine (hipcc, --offload-arch=gfx950)
+  * ``<pkg>/_C*.so``           pybind11 module (kernels/engine bindings + .ot I/O on libtorch)
+  * ``build/bin/dmlc-node``    C++ control-plane node binary (membership, RPC, SDFS, jobs, CLI)
+
+Incremental: an object is rebuilt when its source or any header under csrc/ is newer.
+Usage: python tools/build.py [-j N] [--clean] [--verbose]
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import glob
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "distributed-machine-learning-cluster_amd")
+CSRC = os.path.join(ROOT, "csrc")
+BUILD = os.path.join(ROOT, "build")
+OBJ = os.path.join(BUILD, "obj")
+BIN = os.path.join(BUILD, "bin")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+ARCH = "gfx950"
+
+
+def _torch_paths():
+    import torch  # noqa: F401  (only for paths)
+    tdir = os.path.dirname(torch.__file__)
+    return (
+        [os.path.join(tdir, "include"), os.path.join(tdir, "include", "torch", "csrc", "api", "include")],
+        os.path.join(tdir, "lib"),
+        int(torch._C._GLIBCXX_USE_CXX11_ABI),
+    )
+
+
+def _pybind_include():
+    import pybind11
+    return pybind11.get_include()
+
+
+def _headers_mtime() -> float:
+    hs = glob.glob(os.path.join(CSRC, "**", "*.h"), recursive=True)
+    return max((os.path.getmtime(h) for h in hs), default=0.0)
+
+
+def _stale(target: str, sources: list[str], hdr_mtime: float) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(s) > t for s in sources) or hdr_mtime > t
+
+
+def _run(cmd: list[str], verbose: bool) -> None:
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stdout + r.stderr)
+        raise RuntimeError(f"build step failed: {' '.join(cmd[:3])} ... {cmd[-1]}")
+
+
+HIPCC_FLAGS = [
+    "-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result",
+    "-munsafe-fp-atomics",
+]
+
+
+def gpu_objects():
+    srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
+    srcs += [os.path.join(CSRC, "runtime", "engine.cpp")]
+    return srcs
+
+
+def build(jobs: int = 8, verbose: bool = False, node: bool = True) -> None:
+    os.makedirs(OBJ, exist_ok=True)
+    os.makedirs(BIN, exist_ok=True)
+    hdr = _headers_mtime()
+    tinc, tlib, abi = _torch_paths()
+    pyinc = sysconfig.get_paths()["include"]
+    ext = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+
+    # ---- 1. HIP objects -> libdmlc_gpu.so
+    steps = []
+    gpu_objs = []
+    for s in gpu_objects():
+        o = os.path.join(OBJ, os.path.relpath(s, CSRC).replace(os.sep, "_") + ".o")
+        gpu_objs.append(o)
+        if _stale(o, [s], hdr):
+            lang = ["-x", "hip"] if s.endswith(".hip") else []
+            steps.append(["hipcc", *HIPCC_FLAGS, *lang, "-c", s, "-o", o])
+
+    host_flags = [
+        "-O2", "-std=c++17", "-fPIC", f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-D__HIP_PLATFORM_AMD__",
+        f"-I{ROCM}/include", "-Wno-deprecated-declarations",
+    ]
+    torch_flags = [f"-I{p}" for p in tinc]
+    # ---- 2. host objects for the python module
+    py_srcs = {
+        os.path.join(CSRC, "bindings", "py_module.cpp"): [f"-I{_pybind_include()}", f"-I{pyinc}"],
+        os.path.join(CSRC, "runtime", "ot_io.cpp"): torch_flags,
+    }
+    py_objs = []
+    for s, extra in py_srcs.items():
+        o = os.path.join(OBJ, os.path.relpath(s, CSRC).replace(os.sep, "_") + ".o")
+        py_objs.append(o)
+        if _stale(o, [s], hdr):
+            steps.append(["g++", *host_flags, *extra, "-c", s, "-o", o])
+
+    # ---- 3. control-plane objects (C++17, no GPU, no torch)
+    node_srcs = sorted(glob.glob(os.path.join(CSRC, "control", "*.cpp")) +
+                       glob.glob(os.path.join(CSRC, "serve", "*.cpp")) +
+                       glob.glob(os.path.join(CSRC, "cli", "*.cpp"))) if node else []
+    node_objs = []
+    for s in node_srcs:
+        o = os.path.join(OBJ, os.path.relpath(s, CSRC).replace(os.sep, "_") + ".o")
+        node_objs.append(o)
+        if _stale(o, [s], hdr):
+            steps.append(["g++", *host_flags, *torch_flags, "-pthread", "-c", s, "-o", o])
+
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        list(ex.map(lambda c: _run(c, verbose), steps))
+
+    libgpu = os.path.join(PKG, "libdmlc_gpu.so")
+    if _stale(libgpu, gpu_objs, 0):
+        _run(["hipcc", "-shared", "-fPIC", f"--offload-arch={ARCH}", *gpu_objs, "-o", libgpu], verbose)
+
+    pymod = os.path.join(PKG, "_C" + ext)
+    if _stale(pymod, py_objs + [libgpu], 0):
+        _run(["g++", "-shared", "-fPIC", *py_objs, "-o", pymod,
+              f"-L{PKG}", "-ldmlc_gpu", "-Wl,-rpath,$ORIGIN",
+              f"-L{tlib}", "-ltorch_cpu", "-lc10", f"-Wl,-rpath,{tlib}",
+              f"-L{tlib}", "-lamdhip64"], verbose)
+
+    if node and node_objs:
+        exe = os.path.join(BIN, "dmlc-node")
+        ot_obj = os.path.join(OBJ, "runtime_ot_io.cpp.o")
+        if _stale(exe, node_objs + [libgpu, ot_obj], 0):
+            _run(["g++", "-pthread", *node_objs, ot_obj, "-o", exe,
+                  f"-L{PKG}", "-ldmlc_gpu", f"-Wl,-rpath,{PKG}",
+                  f"-L{tlib}", "-ltorch_cpu", "-lc10", "-lamdhip64", f"-Wl,-rpath,{tlib}"], verbose)
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("-j", "--jobs", type=int, default=min(8, os.cpu_count() or 8))
+    ap.add_argument("--clean", action="store_true")
+    ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--no-node", action="store_true")
+    a = ap.parse_args()
+    if a.clean:
+        shutil.rmtree(BUILD, ignore_errors=True)
+        for f in glob.glob(os.path.join(PKG, "*.so")):
+            os.remove(f)
+    build(a.jobs, a.verbose, node=not a.no_node)
+    print("build ok")
+
+
+if __name__ == "__main__":
+    main()
