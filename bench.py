@@ -117,6 +117,8 @@ def main():
     ev_start = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + args.warmup)]
     ev_end = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + args.warmup)]
 
+    transfer = distributed and args.input_mode == "scatter"
+
     def run(first, n):
         """Pipelined loop: input of step i+1 is in flight during compute of step i."""
         stream = torch.cuda.current_stream()
@@ -126,11 +128,14 @@ def main():
         for i in range(first, first + n):
             if h is not None:
                 h.wait()
-            if i + 1 < first + n:
+            if i + 1 < first + n and transfer:
+                # the transfer of batch i+1 can start once compute(i-1) is done
                 ev_start[i + 1].record(stream)
                 h = issue_input(i + 1)
             else:
                 h = None
+                if i + 1 < first + n:
+                    ev_start[i + 1].record(stream)  # no transfer: batch i+1 starts after i is issued
             gh = compute(i)
             if gh is not None:
                 gh.wait()

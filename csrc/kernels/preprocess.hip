@@ -6,9 +6,11 @@
 // resize, crop and normalisation run on the GPU and write the 4-channel
 // packed layout consumed by the conv stem (channel 3 = 0).
 //
-// Resize rule: scale the short side to S (aspect preserved), centre-crop SxS,
-// bilinear sampling with half-pixel centres (align_corners=False). When the
-// input is already SxS this is an exact per-pixel normalisation.
+// Resize rule: resize to (RH, RW) with the short side = S and the long side
+// = floor(S * long / short) (aspect preserved), centre-crop SxS at integer
+// offsets ((RH-S)/2, (RW-S)/2), bilinear sampling with half-pixel centres
+// (= torch interpolate(mode="bilinear", align_corners=False, antialias=False)).
+// When the input is already SxS this is an exact per-pixel normalisation.
 #include "common.h"
 #include "kernels.h"
 
@@ -20,8 +22,8 @@ namespace {
 
 __global__ __launch_bounds__(256) void preprocess_kernel(const uint8_t* __restrict__ x,
                                                          bf16* __restrict__ y, int B, int Hin,
-                                                         int Win, int S, float scale, float oy,
-                                                         float ox) {
+                                                         int Win, int S, float sy_scale,
+                                                         float sx_scale, int oy, int ox) {
   const float mean[3] = {0.485f, 0.456f, 0.406f};
   const float istd[3] = {1.f / 0.229f, 1.f / 0.224f, 1.f / 0.225f};
   const long total = (long)B * S * S;
@@ -40,8 +42,8 @@ __global__ __launch_bounds__(256) void preprocess_kernel(const uint8_t* __restri
       c[2] = p[2];
     } else {
       // Source coordinate of this output pixel centre in the resized+cropped image.
-      float sy = (oy_i + oy + 0.5f) * scale - 0.5f;
-      float sx = (ox_i + ox + 0.5f) * scale - 0.5f;
+      float sy = (oy_i + oy + 0.5f) * sy_scale - 0.5f;
+      float sx = (ox_i + ox + 0.5f) * sx_scale - 0.5f;
       sy = fminf(fmaxf(sy, 0.f), (float)(Hin - 1));
       sx = fminf(fmaxf(sx, 0.f), (float)(Win - 1));
       const int y0 = (int)sy, x0 = (int)sx;
@@ -70,14 +72,20 @@ __global__ __launch_bounds__(256) void preprocess_kernel(const uint8_t* __restri
 void preprocess_u8(const uint8_t* x, void* y, int B, int Hin, int Win, int S, hipStream_t s) {
   if (B <= 0) return;
   if (Hin <= 0 || Win <= 0 || S <= 0) throw std::invalid_argument("preprocess_u8: bad dims");
-  // Short side -> S; 'scale' maps resized coordinates back to source pixels.
-  const float scale = (float)std::min(Hin, Win) / (float)S;
-  const float rh = Hin / scale, rw = Win / scale;  // resized dims
-  const float oy = (rh - S) * 0.5f, ox = (rw - S) * 0.5f;
+  int RH, RW;
+  if (Hin <= Win) {
+    RH = S;
+    RW = (int)((long)S * Win / Hin);
+  } else {
+    RW = S;
+    RH = (int)((long)S * Hin / Win);
+  }
+  const int oy = (RH - S) / 2, ox = (RW - S) / 2;
+  const float sy_scale = (float)Hin / RH, sx_scale = (float)Win / RW;
   const long total = (long)B * S * S;
   const int blocks = (int)std::min<long>((total + 255) / 256, 16384);
   hipLaunchKernelGGL(preprocess_kernel, dim3(blocks), dim3(256), 0, s, x, (bf16*)y, B, Hin, Win, S,
-                     scale, oy, ox);
+                     sy_scale, sx_scale, oy, ox);
   DMLC_HIP_CHECK(hipGetLastError());
 }
 
