@@ -134,9 +134,9 @@ def main():
                 h = issue_input(i + 1)
             else:
                 h = None
-                if i + 1 < first + n:
-                    ev_start[i + 1].record(stream)  # no transfer: batch i+1 starts after i is issued
             gh = compute(i)
+            if not transfer and i + 1 < first + n:
+                ev_start[i + 1].record(stream)  # no transfer: batch i+1 starts when compute(i) ends
             if gh is not None:
                 gh.wait()
             ev_end[i].record(stream)

@@ -9,18 +9,23 @@
 // Design (gfx950):
 //  * 256-thread workgroups = 4 waves of 64; each wave owns a 64x64 output
 //    sub-tile = 4x4 MFMA 16x16 tiles (16 fp32x4 accumulators).
+//  * Operand tiles go HBM/L2 -> LDS with global_load_lds_dwordx4 (LDS-DMA,
+//    no VGPR staging, no ds_write): each wave-instruction fills 8 LDS rows of
+//    128 B. Im2col padding is handled by pointing the lanes of out-of-image
+//    taps at a 16-B zero page, so the DMA never needs a per-lane mask.
+//  * LDS rows are XOR-swizzled per 16-B chunk (phys = chunk ^ ((row>>1)&7)) so
+//    the ds_read_b128 fragment reads (16 rows x same chunk per lane group) are
+//    bank-conflict free; because LDS-DMA writes lane-linearly, the swizzle is
+//    applied to the per-lane SOURCE address and undone on the read.
+//  * Two LDS stages, one barrier per 64-deep K-tile: the DMA of tile t+1 is
+//    issued before the MFMAs of tile t.
 //  * The MFMA is issued "swapped": A operand = weight rows (n), B operand =
 //    activation rows (m), so each lane ends with 4 consecutive output
 //    channels of one pixel -> 8-byte packed bf16 stores straight to NHWC.
-//  * Operand tiles are staged global -> VGPR -> LDS, double buffered with one
-//    barrier per K-tile; loads for tile t+1 are issued before the MFMAs of
-//    tile t. LDS rows are XOR-swizzled per 16-B chunk so that the
-//    ds_read_b128 fragment reads (16 rows x same chunk per lane group) are
-//    bank-conflict free (see the derivation next to lds_chunk()).
-//  * Out-of-bounds taps (padding) load zeros; the 3-channel stems use a
-//    packed-tap layout (Cin padded to 4, two taps per 16-B chunk) instead of
-//    padding Cin to 64.
 //  * Epilogue fuses folded-BN bias, residual add and ReLU.
+//  * The 3-channel stems read a "pair image" written by the preprocess
+//    kernel: zero-padded, 16 B per position = two horizontally adjacent RGB0
+//    pixels, so one 16-B chunk = 2 taps and no bounds checks are needed.
 //  * Optional split-K writes fp32 partials that a small kernel reduces (used
 //    when the tile grid cannot fill the 256 CUs, e.g. batch-1 latency runs
 //    and the AlexNet classifier).
@@ -35,20 +40,10 @@ namespace dmlc {
 
 namespace {
 
-// Physical 16-B chunk index inside an LDS tile.
-//  128-B rows (BK=64, 8 chunks): phys = chunk ^ ((row>>1)&7). A ds_read_b128
-//  lane group holds 16 distinct rows (mod 16) at chunks c / c+1; the XOR
-//  spreads them over all 16 slots of the 256-B bank row.
-//  64-B rows (BK=32, 4 chunks): phys = chunk ^ g((row>>2)&3), g = {0,2,3,1}.
-template <bool C4>
-__device__ __forceinline__ int lds_chunk(int row, int chunk) {
-  if constexpr (!C4) {
-    return row * 8 + (chunk ^ ((row >> 1) & 7));
-  } else {
-    const int g = (0x1320 >> (((row >> 2) & 3) * 4)) & 3;
-    return row * 4 + (chunk ^ g);
-  }
-}
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef const __attribute__((address_space(1))) void* gbl_ptr_t;
+
+__device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   // Bijective: blocks b and b+8 share an XCD; give each XCD a contiguous
@@ -58,27 +53,25 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + local;
 }
 
-template <int BM, int BN, int WM, int WN, bool C4>
-__global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a, int kt_per_split,
-                                                         int k_tiles) {
-  constexpr int BK = C4 ? 32 : 64;
-  constexpr int CPR = BK / 8;         // 16-B chunks per LDS row
-  constexpr int RPP = 256 / CPR;      // rows covered by one pass of the block
-  constexpr int PA = BM / RPP;        // activation passes
-  constexpr int PB = BN / RPP;        // weight passes
+template <int BM, int BN, int WM, int WN, bool PAIR>
+__global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a, int kt_per_split, int k_tiles) {
+  constexpr int BK = 64;
+  constexpr int PA = BM / 32;  // A rows per lane (wave covers BM/4 rows = PA instrs of 8 rows)
+  constexpr int PB = BN / 32;
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int TM = WTM / 16, TN = WTN / 16;
   static_assert(WM * WN == 4, "4 waves per block");
-  static_assert(PA * RPP == BM && PB * RPP == BN, "tile/pass mismatch");
-  static_assert(TM >= 1 && TN >= 1, "wave tile");
-  constexpr int A_CH = BM * CPR;      // chunks per A buffer
-  constexpr int BUF_CH = (BM + BN) * CPR;
+  static_assert(BM % 32 == 0 && BN % 32 == 0, "tile");
+  constexpr int ROWB = BK * 2;                       // 128 B per LDS row
+  constexpr int STAGE_B = (BM + BN) * ROWB;          // bytes per stage
+  constexpr int A_CH = BM * 8;                       // chunks in the A part of a stage
+  constexpr int STAGE_CH = (BM + BN) * 8;
 
-  extern __shared__ __attribute__((aligned(16))) uint4 smem[];  // 2 * BUF_CH chunks
+  extern __shared__ __attribute__((aligned(16))) uint4 smem[];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int wave = tid >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave % WM, wn = wave / WM;
 
   const int M = a.B * a.Ho * a.Wo;
@@ -96,78 +89,84 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a, int kt_per_
 
   const bf16* __restrict__ x = (const bf16*)a.x;
   const bf16* __restrict__ w = (const bf16*)a.w;
+  const bf16* zero = (const bf16*)a.zero;
 
-  const int cc = tid % CPR;  // chunk column this thread stages
-  const int rr = tid / CPR;  // first row this thread stages
-
-  // Per staged activation row: input origin and base offset.
-  int hi0[PA], wi0[PA], base[PA];
+  // Rows this lane stages. A: rows wave*BM/4 + p*8 + lane/8, B likewise.
+  const int lrow = lane >> 3;
+  const int pchunk = lane & 7;  // physical chunk written by this lane
+  int hi0[PA], wi0[PA], abase[PA];
+  int lcA[PA];
 #pragma unroll
   for (int p = 0; p < PA; ++p) {
-    const int m = m0 + rr + p * RPP;
+    const int r = wave * (BM / 4) + p * 8 + lrow;
+    const int lc = swz(r, pchunk);
+    lcA[p] = lc;
+    const int m = m0 + r;
     if (m < M) {
       const int hw = a.Ho * a.Wo;
       const int b = m / hw;
       const int rem = m - b * hw;
       const int ho = rem / a.Wo;
       const int wo = rem - ho * a.Wo;
-      hi0[p] = ho * a.stride - a.pad;
-      wi0[p] = wo * a.stride - a.pad;
-      base[p] = ((b * a.H + hi0[p]) * a.W + wi0[p]) * a.Cin;
+      if constexpr (PAIR) {
+        hi0[p] = ho * a.stride;
+        wi0[p] = wo * a.stride;
+        abase[p] = ((b * a.H + hi0[p]) * a.W + wi0[p]) * 8;
+      } else {
+        hi0[p] = ho * a.stride - a.pad;
+        wi0[p] = wo * a.stride - a.pad;
+        abase[p] = ((b * a.H + hi0[p]) * a.W + wi0[p]) * a.Cin + lc * 8;
+      }
     } else {
       hi0[p] = -(1 << 28);
       wi0[p] = 0;
-      base[p] = 0;
+      abase[p] = 0;
     }
   }
-  const bf16* __restrict__ wbase = w + (size_t)(n0 + rr) * a.Kpad + cc * 8;
-  const int wstride = RPP * a.Kpad;
+  int wboff[PB];
+#pragma unroll
+  for (int p = 0; p < PB; ++p) {
+    const int r = wave * (BN / 4) + p * 8 + lrow;
+    wboff[p] = (n0 + r) * a.Kpad + swz(r, pchunk) * 8;
+  }
+  const int KWP = (a.KW + 1) >> 1;
+  const int ntap_pairs = a.KH * KWP;
 
-  uint4 ra[PA], rb[PB];
-
-#define DMLC_LOAD_TILE(t_)                                                                  \
-  do {                                                                                      \
-    const int t = (t_);                                                                     \
-    if constexpr (!C4) {                                                                    \
-      const int ctiles = a.Cin >> 6;                                                        \
-      const int tap = t / ctiles;                                                           \
-      const int c0 = (t - tap * ctiles) << 6;                                               \
-      const int kh = tap / a.KW;                                                            \
-      const int kw = tap - kh * a.KW;                                                       \
-      const int off = (kh * a.W + kw) * a.Cin + c0 + cc * 8;                                \
-      _Pragma("unroll") for (int p = 0; p < PA; ++p) {                                      \
-        const bool ok = (unsigned)(hi0[p] + kh) < (unsigned)a.H &&                          \
-                        (unsigned)(wi0[p] + kw) < (unsigned)a.W;                            \
-        ra[p] = ok ? *(const uint4*)(x + base[p] + off) : make_uint4(0, 0, 0, 0);           \
-      }                                                                                     \
-    } else {                                                                                \
-      const int ntaps = a.KH * a.KW;                                                        \
-      const int tp0 = t * 8 + cc * 2;                                                       \
-      const int kh0 = tp0 / a.KW, kw0 = tp0 - kh0 * a.KW;                                   \
-      const int tp1 = tp0 + 1;                                                              \
-      const int kh1 = tp1 / a.KW, kw1 = tp1 - kh1 * a.KW;                                   \
-      const int off0 = (kh0 * a.W + kw0) * 4, off1 = (kh1 * a.W + kw1) * 4;                 \
-      _Pragma("unroll") for (int p = 0; p < PA; ++p) {                                      \
-        const bool ok0 = tp0 < ntaps && (unsigned)(hi0[p] + kh0) < (unsigned)a.H &&         \
-                         (unsigned)(wi0[p] + kw0) < (unsigned)a.W;                          \
-        const bool ok1 = tp1 < ntaps && (unsigned)(hi0[p] + kh1) < (unsigned)a.H &&         \
-                         (unsigned)(wi0[p] + kw1) < (unsigned)a.W;                          \
-        const uint2 v0 = ok0 ? *(const uint2*)(x + base[p] + off0) : make_uint2(0, 0);      \
-        const uint2 v1 = ok1 ? *(const uint2*)(x + base[p] + off1) : make_uint2(0, 0);      \
-        ra[p] = make_uint4(v0.x, v0.y, v1.x, v1.y);                                         \
-      }                                                                                     \
-    }                                                                                       \
-    const bf16* wt = wbase + t * BK;                                                        \
-    _Pragma("unroll") for (int p = 0; p < PB; ++p) rb[p] = *(const uint4*)(wt + p * wstride); \
-  } while (0)
-
-#define DMLC_STORE_TILE(buf_)                                                               \
-  do {                                                                                      \
-    uint4* sb = smem + (buf_) * BUF_CH;                                                     \
-    _Pragma("unroll") for (int p = 0; p < PA; ++p) sb[lds_chunk<C4>(rr + p * RPP, cc)] = ra[p]; \
-    _Pragma("unroll") for (int p = 0; p < PB; ++p)                                          \
-      sb[A_CH + lds_chunk<C4>(rr + p * RPP, cc)] = rb[p];                                   \
-  } while (0)
+  // Issue the LDS-DMA for K-tile t into stage `st`.
+  auto stage = [&](int t, int st) __attribute__((always_inline)) {
+    char* sbase = (char*)smem + st * STAGE_B;
+    if constexpr (!PAIR) {
+      const int ctiles = a.Cin >> 6;
+      const int tap = t / ctiles;
+      const int c0 = (t - tap * ctiles) << 6;
+      const int kh = tap / a.KW;
+      const int kw = tap - kh * a.KW;
+      const int off = (kh * a.W + kw) * a.Cin + c0;
+#pragma unroll
+      for (int p = 0; p < PA; ++p) {
+        const bool ok = (unsigned)(hi0[p] + kh) < (unsigned)a.H && (unsigned)(wi0[p] + kw) < (unsigned)a.W;
+        const bf16* src = ok ? x + abase[p] + off : zero;
+        __builtin_amdgcn_global_load_lds((gbl_ptr_t)src,
+                                         (lds_ptr_t)(sbase + (wave * (BM / 4) + p * 8) * ROWB), 16, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int p = 0; p < PA; ++p) {
+        const int kt = t * 8 + lcA[p];
+        const int kh = kt / KWP;
+        const int kwp = kt - kh * KWP;
+        const bool ok = kt < ntap_pairs && hi0[p] >= 0;
+        const bf16* src = ok ? x + abase[p] + (kh * a.W + 2 * kwp) * 8 : zero;
+        __builtin_amdgcn_global_load_lds((gbl_ptr_t)src,
+                                         (lds_ptr_t)(sbase + (wave * (BM / 4) + p * 8) * ROWB), 16, 0, 0);
+      }
+    }
+    const bf16* wt = w + t * BK;
+#pragma unroll
+    for (int p = 0; p < PB; ++p)
+      __builtin_amdgcn_global_load_lds((gbl_ptr_t)(wt + wboff[p]),
+                                       (lds_ptr_t)(sbase + (BM + wave * (BN / 4) + p * 8) * ROWB), 16, 0, 0);
+  };
 
   floatx4 acc[TN][TM];
 #pragma unroll
@@ -177,39 +176,43 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a, int kt_per_
 
   const int fr = lane & 15, fq = lane >> 4;
 
-#define DMLC_COMPUTE(buf_)                                                                  \
-  do {                                                                                      \
-    const uint4* sb = smem + (buf_) * BUF_CH;                                               \
-    _Pragma("unroll") for (int ks = 0; ks < BK / 32; ++ks) {                                \
-      bf16x8 af[TN], bm[TM];                                                                \
-      _Pragma("unroll") for (int i = 0; i < TN; ++i) af[i] = __builtin_bit_cast(            \
-          bf16x8, sb[A_CH + lds_chunk<C4>(wn * WTN + i * 16 + fr, ks * 4 + fq)]);           \
-      _Pragma("unroll") for (int j = 0; j < TM; ++j) bm[j] = __builtin_bit_cast(            \
-          bf16x8, sb[lds_chunk<C4>(wm * WTM + j * 16 + fr, ks * 4 + fq)]);                  \
-      _Pragma("unroll") for (int i = 0; i < TN; ++i)                                        \
-        _Pragma("unroll") for (int j = 0; j < TM; ++j)                                      \
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bm[j], acc[i][j], 0, 0, 0); \
-    }                                                                                       \
-  } while (0)
+  auto compute = [&](int st) __attribute__((always_inline)) {
+    const uint4* sb = smem + st * STAGE_CH;
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      bf16x8 af[TN], bm[TM];
+#pragma unroll
+      for (int i = 0; i < TN; ++i) {
+        const int r = wn * WTN + i * 16 + fr;
+        af[i] = __builtin_bit_cast(bf16x8, sb[A_CH + r * 8 + swz(r, ks * 4 + fq)]);
+      }
+#pragma unroll
+      for (int j = 0; j < TM; ++j) {
+        const int r = wm * WTM + j * 16 + fr;
+        bm[j] = __builtin_bit_cast(bf16x8, sb[r * 8 + swz(r, ks * 4 + fq)]);
+      }
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bm[j], acc[i][j], 0, 0, 0);
+    }
+  };
 
   if (nk > 0) {
-    DMLC_LOAD_TILE(kt0);
-    DMLC_STORE_TILE(0);
+    stage(kt0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     int cur = 0;
     for (int it = 1; it < nk; ++it) {
-      DMLC_LOAD_TILE(kt0 + it);  // global loads in flight under the MFMAs below
-      DMLC_COMPUTE(cur);
-      DMLC_STORE_TILE(cur ^ 1);
+      stage(kt0 + it, cur ^ 1);  // DMA of the next tile lands under these MFMAs
+      compute(cur);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       cur ^= 1;
     }
-    DMLC_COMPUTE(cur);
+    compute(cur);
   }
-
-#undef DMLC_LOAD_TILE
-#undef DMLC_STORE_TILE
-#undef DMLC_COMPUTE
 
   // Epilogue. Lane holds D[n = 4*fq + r][m = fr] of each 16x16 tile.
   if (gridDim.y > 1) {
@@ -309,12 +312,12 @@ int pick_tile(const ConvArgs& a) {
 }
 
 template <int BM, int BN, int WM, int WN>
-void launch_cfg(const ConvArgs& a, bool c4, int splits, int kt_per, int k_tiles, hipStream_t s) {
+void launch_cfg(const ConvArgs& a, int splits, int kt_per, int k_tiles, hipStream_t s) {
   const int M = a.B * a.Ho * a.Wo;
   const int tiles = ((M + BM - 1) / BM) * (a.Npad / BN);
   dim3 grid(tiles, splits);
-  const size_t lds = (size_t)2 * (BM + BN) * (c4 ? 4 : 8) * 16;
-  if (c4)
+  const size_t lds = (size_t)2 * (BM + BN) * 128;
+  if (a.pair_stem)
     hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, true>), grid, dim3(256), lds, s, a, kt_per, k_tiles);
   else
     hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, false>), grid, dim3(256), lds, s, a, kt_per, k_tiles);
@@ -325,10 +328,10 @@ void launch_cfg(const ConvArgs& a, bool c4, int splits, int kt_per, int k_tiles,
 
 int conv_out_dim(int in, int k, int stride, int pad) { return (in + 2 * pad - k) / stride + 1; }
 
-int conv_kpad(int Cin, int KH, int KW) {
-  if (Cin == 4) {
-    const int k = KH * KW * 4;
-    return (k + 31) / 32 * 32;
+int conv_kpad(int Cin, int KH, int KW, bool pair_stem) {
+  if (pair_stem) {
+    const int k = KH * ((KW + 1) / 2) * 8;
+    return (k + 63) / 64 * 64;
   }
   return KH * KW * Cin;  // Cin % 64 == 0
 }
@@ -344,8 +347,7 @@ int conv_pick_split_k(const ConvArgs& a, int num_cus) {
   const int BM = kTiles[cfg].bm, BN = kTiles[cfg].bn;
   const long M = (long)a.B * a.Ho * a.Wo;
   const long tiles = ((M + BM - 1) / BM) * (a.Npad / BN);
-  const int BK = a.Cin == 4 ? 32 : 64;
-  const int k_tiles = a.Kpad / BK;
+  const int k_tiles = a.Kpad / 64;
   if (tiles >= num_cus / 2 || k_tiles < 16) return 1;
   int s = (int)((num_cus + tiles - 1) / tiles);
   s = std::min(s, k_tiles / 8);
@@ -359,22 +361,33 @@ size_t conv_splitk_ws_elems(const ConvArgs& a) {
 }
 
 void conv2d_igemm(const ConvArgs& a, hipStream_t s) {
-  const bool c4 = a.Cin == 4;
-  if (!c4 && a.Cin % 64 != 0) throw std::invalid_argument("conv2d_igemm: Cin must be 4 or a multiple of 64");
-  if (a.Kpad != conv_kpad(a.Cin, a.KH, a.KW)) throw std::invalid_argument("conv2d_igemm: bad Kpad");
-  if (a.N % 4 != 0 || a.N > a.Npad || a.ldo < a.N) throw std::invalid_argument("conv2d_igemm: bad N/ldo");
-  if (a.Ho != conv_out_dim(a.H, a.KH, a.stride, a.pad) || a.Wo != conv_out_dim(a.W, a.KW, a.stride, a.pad))
+  if (a.pair_stem) {
+    if (a.Cin != 8) throw std::invalid_argument("conv2d_igemm: pair stem expects Cin == 8 (2 RGB0 pixels)");
+  } else if (a.Cin % 64 != 0) {
+    throw std::invalid_argument("conv2d_igemm: Cin must be a multiple of 64");
+  }
+  if (a.Kpad != conv_kpad(a.Cin, a.KH, a.KW, a.pair_stem)) throw std::invalid_argument("conv2d_igemm: bad Kpad");
+  if (a.N % 4 != 0 || a.N > a.Npad || a.ldo < a.N || a.ldo % 4 != 0)
+    throw std::invalid_argument("conv2d_igemm: bad N/ldo");
+  if (a.pair_stem) {
+    // x is the zero-padded pair image [B, H, W, 8] with H/W already including 2*pad
+    if (a.Ho != (a.H - a.KH) / a.stride + 1 || a.Wo != (a.W - a.KW) / a.stride + 1)
+      throw std::invalid_argument("conv2d_igemm: bad output dims (pair stem)");
+  } else if (a.Ho != conv_out_dim(a.H, a.KH, a.stride, a.pad) || a.Wo != conv_out_dim(a.W, a.KW, a.stride, a.pad)) {
     throw std::invalid_argument("conv2d_igemm: bad output dims");
-  if (!a.x || !a.w || !a.y) throw std::invalid_argument("conv2d_igemm: null operand");
+  }
+  if (!a.x || !a.w || !a.y || !a.zero) throw std::invalid_argument("conv2d_igemm: null operand");
+  if (((uintptr_t)a.x | (uintptr_t)a.w | (uintptr_t)a.zero) & 15)
+    throw std::invalid_argument("conv2d_igemm: operands must be 16-B aligned");
   const int cfg = pick_tile(a);
   const int BN = kTiles[cfg].bn;
   if (a.Npad % BN != 0) throw std::invalid_argument("conv2d_igemm: Npad not a multiple of BN");
   const long M = (long)a.B * a.Ho * a.Wo;
   if (M <= 0) return;
-  if ((long)a.B * a.H * a.W * a.Cin >= (1L << 31) || M * a.ldo >= (1L << 31))
+  if ((long)a.B * a.H * a.W * a.Cin >= (1L << 31) || M * a.ldo >= (1L << 31) ||
+      (long)a.Npad * a.Kpad >= (1L << 31))
     throw std::invalid_argument("conv2d_igemm: tensor too large for 32-bit offsets");
-  const int BK = c4 ? 32 : 64;
-  const int k_tiles = a.Kpad / BK;
+  const int k_tiles = a.Kpad / 64;
   int splits = std::max(1, a.split_k);
   if (splits > 1 && !a.ws) throw std::invalid_argument("conv2d_igemm: split-K needs a workspace");
   const int kt_per = (k_tiles + splits - 1) / splits;
@@ -382,13 +395,12 @@ void conv2d_igemm(const ConvArgs& a, hipStream_t s) {
   ConvArgs b = a;
   b.split_k = splits;
   switch (cfg) {
-    case 0: launch_cfg<128, 128, 2, 2>(b, c4, splits, kt_per, k_tiles, s); break;
-    case 1: launch_cfg<256, 64, 4, 1>(b, c4, splits, kt_per, k_tiles, s); break;
-    default: launch_cfg<64, 256, 1, 4>(b, c4, splits, kt_per, k_tiles, s); break;
+    case 0: launch_cfg<128, 128, 2, 2>(b, splits, kt_per, k_tiles, s); break;
+    case 1: launch_cfg<256, 64, 4, 1>(b, splits, kt_per, k_tiles, s); break;
+    default: launch_cfg<64, 256, 1, 4>(b, splits, kt_per, k_tiles, s); break;
   }
   if (splits > 1) {
-    const long total = M * (a.N / 4);
-    const int blocks = (int)std::min<long>((total + 255) / 256, 4096);
+    const int blocks = (int)std::min<long>((M * (a.N / 4) + 255) / 256, 4096);
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, s, b, (int)M, splits);
     DMLC_HIP_CHECK(hipGetLastError());
   }

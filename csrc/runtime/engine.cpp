@@ -65,6 +65,8 @@ Engine::Engine(const std::string& arch, const WeightMap& weights, int device, in
   DMLC_HIP_CHECK(hipEventCreateWithFlags(&ev_out_, hipEventDisableTiming));
   ws_elems_ = (size_t)16 << 20;  // 64 MB split-K workspace
   DMLC_HIP_CHECK(hipMalloc(&ws_, ws_elems_ * sizeof(float)));
+  DMLC_HIP_CHECK(hipMalloc(&zero_, 256));
+  DMLC_HIP_CHECK(hipMemset(zero_, 0, 256));
 }
 
 Engine::~Engine() {
@@ -73,6 +75,7 @@ Engine::~Engine() {
   if (!acts_.empty() && acts_[0]) hipFree(acts_[0]);
   if (warena_) hipFree(warena_);
   if (ws_) hipFree(ws_);
+  if (zero_) hipFree(zero_);
   if (dummy_idx_) hipFree(dummy_idx_);
   if (ev_in_) hipEventDestroy(ev_in_);
   if (ev_out_) hipEventDestroy(ev_out_);
@@ -84,14 +87,17 @@ int Engine::add_act(ActShape s) {
   return (int)shapes_.size() - 1;
 }
 
+int Engine::op_count_conv() const { return (int)convs_.size(); }
+
 int Engine::conv(int in, const std::string& name, const std::string& bn, int cout, int k,
                  int stride, int pad, bool relu, int res) {
   const ActShape is = shapes_.at(in);
   ConvLayer L;
   L.name = name;
   L.bn = bn;
+  L.pair = (op_count_conv() == 0 && is.C == 8);  // stem reads the preprocess pair image
   L.cin_eff = is.C;
-  L.cin = is.C == 4 ? 3 : is.C;
+  L.cin = L.pair ? 3 : is.C;
   L.cout = cout;
   L.kh = L.kw = k;
   L.stride = stride;
@@ -126,9 +132,9 @@ int Engine::fc(int in, const std::string& name, int cout, bool relu, bool last) 
 
 void Engine::build_resnet(const std::vector<int>& blocks, bool bottleneck) {
   const int S = image_size_;
-  int x = add_act(ActShape{S, S, 4, false});
-  ops_.push_back(Op{OpType::Preprocess, -1, x, -1, -1, 0, 0, 0, "preprocess"});
-  x = conv(x, "conv1", "bn1", 64, 7, 2, 3, true);
+  int x = add_act(ActShape{S + 6, S + 6, 8, false});  // pair image, stem pad 3
+  ops_.push_back(Op{OpType::Preprocess, -1, x, -1, -1, 0, 0, 3, "preprocess"});
+  x = conv(x, "conv1", "bn1", 64, 7, 2, 0, true);
   {
     const ActShape s = shapes_[x];
     const int y = add_act(ActShape{conv_out_dim(s.H, 3, 2, 1), conv_out_dim(s.W, 3, 2, 1), s.C, false});
@@ -168,15 +174,15 @@ void Engine::build_resnet(const std::vector<int>& blocks, bool bottleneck) {
 
 void Engine::build_alexnet() {
   const int S = image_size_;
-  int x = add_act(ActShape{S, S, 4, false});
-  ops_.push_back(Op{OpType::Preprocess, -1, x, -1, -1, 0, 0, 0, "preprocess"});
+  int x = add_act(ActShape{S + 4, S + 4, 8, false});  // pair image, stem pad 2
+  ops_.push_back(Op{OpType::Preprocess, -1, x, -1, -1, 0, 0, 2, "preprocess"});
   auto pool = [&](int in, const std::string& n) {
     const ActShape s = shapes_[in];
     const int y = add_act(ActShape{conv_out_dim(s.H, 3, 2, 0), conv_out_dim(s.W, 3, 2, 0), s.C, false});
     ops_.push_back(Op{OpType::MaxPool, in, y, -1, -1, 3, 2, 0, n});
     return y;
   };
-  x = conv(x, "features.0", "", 64, 11, 4, 2, true);
+  x = conv(x, "features.0", "", 64, 11, 4, 0, true);
   x = pool(x, "features.2");
   x = conv(x, "features.3", "", 192, 5, 1, 2, true);
   x = pool(x, "features.5");
@@ -203,7 +209,7 @@ void Engine::pack_weights(const WeightMap& w) {
   size_t off = 0;
   for (auto& L : convs_) {
     L.npad = conv_npad(L.cout);
-    L.kpad = conv_kpad(L.cin_eff, L.kh, L.kw);
+    L.kpad = conv_kpad(L.cin_eff, L.kh, L.kw, L.pair);
     L.w_off = off;
     off = align_up(off + (size_t)L.npad * L.kpad * 2, 256);
     L.b_off = off;
@@ -241,7 +247,12 @@ void Engine::pack_weights(const WeightMap& w) {
           for (int i = 0; i < L.kh; ++i)
             for (int j = 0; j < L.kw; ++j) {
               const float v = W.data[(((size_t)n * L.cin + c) * L.kh + i) * L.kw + j] * scale[n];
-              pw[(size_t)n * L.kpad + (size_t)(i * L.kw + j) * L.cin_eff + c] = f2bf_host(v);
+              size_t k;
+              if (L.pair)  // k = (kh*KWP + kwp)*8 + half*4 + c, kw = 2*kwp + half
+                k = (size_t)(i * ((L.kw + 1) / 2) + j / 2) * 8 + (j & 1) * 4 + c;
+              else
+                k = (size_t)(i * L.kw + j) * L.cin_eff + c;
+              pw[(size_t)n * L.kpad + k] = f2bf_host(v);
             }
     } else {
       if (W.shape.size() != 2 || W.shape[0] != L.cout || W.shape[1] != L.cin)
@@ -303,6 +314,8 @@ ConvArgs Engine::conv_args(const Op& op, int B, float* logits) const {
   const ActShape& os = shapes_[op.out];
   ConvArgs a;
   a.x = acts_[op.in];
+  a.zero = zero_;
+  a.pair_stem = L.pair;
   a.w = (const uint8_t*)warena_ + L.w_off;
   a.bias = (const float*)((const uint8_t*)warena_ + L.b_off);
   a.res = op.res >= 0 ? acts_[op.res] : nullptr;
@@ -343,7 +356,7 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
   for (const Op& op : ops_) {
     switch (op.type) {
       case OpType::Preprocess:
-        preprocess_u8(images, acts_[op.out], B, Hin, Win, image_size_, s);
+        preprocess_u8(images, acts_[op.out], B, Hin, Win, image_size_, op.pad, s);
         break;
       case OpType::Conv:
         conv2d_igemm(conv_args(op, B, logits), s);

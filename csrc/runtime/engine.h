@@ -34,6 +34,7 @@ struct ConvLayer {
   int cin = 0, cin_eff = 0, cout = 0, kh = 1, kw = 1, stride = 1, pad = 0;
   bool relu = false;
   bool fc = false;        // linear layer (weight [N,K]) run as a 1x1 conv
+  bool pair = false;      // stem conv on the preprocess pair image (2 taps / 16 B)
   int fc_hwc[3] = {0, 0, 0};  // for fc after a spatial tensor: (H,W,C) of the flatten
   int npad = 0, kpad = 0;
   size_t w_off = 0, b_off = 0;  // offsets (bytes) into the weight arena
@@ -88,6 +89,7 @@ class Engine {
 
  private:
   int add_act(ActShape s);
+  int op_count_conv() const;
   int conv(int in, const std::string& name, const std::string& bn, int cout, int k, int stride,
            int pad, bool relu, int res = -1);
   int fc(int in, const std::string& name, int cout, bool relu, bool last);
@@ -115,6 +117,7 @@ class Engine {
   std::vector<void*> acts_;
   size_t act_bytes_ = 0;
   float* ws_ = nullptr;
+  void* zero_ = nullptr;  // 16-B zero page: LDS-DMA source for conv padding taps
   size_t ws_elems_ = 0;
   int32_t* dummy_idx_ = nullptr;
 

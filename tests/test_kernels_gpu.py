@@ -74,19 +74,19 @@ def test_conv2d_vs_torch(gpu, case):
     assert _rel(got, ref) < 8e-3, _rel(got, ref)
 
 
-@pytest.mark.parametrize("k,s,p,cout", [(7, 2, 3, 64), (11, 4, 2, 64), (3, 1, 1, 128)])
-def test_conv2d_stem_c4(gpu, k, s, p, cout):
-    """3-channel stem: input padded to 4 channels, two taps per 16-B chunk."""
+@pytest.mark.parametrize("k,s,p,cout", [(7, 2, 3, 64), (11, 4, 2, 64), (3, 1, 1, 128), (4, 2, 1, 64)])
+def test_conv2d_stem_pair(gpu, k, s, p, cout):
+    """3-channel stem on the padded pair image (two taps per 16-B chunk)."""
     g = torch.Generator().manual_seed(2)
     B, H, W = 2, 57, 61
     x = torch.randn(B, 3, H, W, generator=g).bfloat16().float()
     w = (torch.randn(cout, 3, k, k, generator=g) / (3 * k * k) ** 0.5).bfloat16().float()
     ref = F.relu(F.conv2d(x, w, None, s, p))
-    x4 = torch.zeros(B, H, W, 4)
-    x4[..., :3] = _nhwc(x)
-    wp = ops.pack_conv_weight(w, cin_eff=4, device=gpu)
-    y = ops.conv2d(x4.bfloat16().to(gpu), wp, cout, k, k, s, p, relu=True)
+    xp = ops.pair_image(_nhwc(x), p)
+    wp = ops.pack_conv_weight(w, pair_stem=True, device=gpu)
+    y = ops.conv2d(xp.bfloat16().to(gpu), wp, cout, k, k, s, p, relu=True, pair_stem=True)
     torch.cuda.synchronize()
+    assert y.shape[1:3] == ref.shape[2:4]
     assert _rel(_nchw(y.float().cpu()), ref) < 8e-3
 
 
@@ -139,11 +139,14 @@ def test_preprocess_identity(gpu):
     g = torch.Generator().manual_seed(6)
     img = torch.randint(0, 256, (3, 224, 224, 3), generator=g, dtype=torch.uint8)
     ref = (_nchw(img.float()) / 255 - MEAN) / STD
-    y = ops.preprocess_u8(img.to(gpu), 224)
-    torch.cuda.synchronize()
-    y = y.float().cpu()
-    assert torch.all(y[..., 3] == 0)
-    assert _rel(_nchw(y[..., :3].contiguous()), ref) < 4e-3
+    for pad in (0, 3):
+        y = ops.preprocess_u8(img.to(gpu), 224, pad)
+        torch.cuda.synchronize()
+        y = y.float().cpu()
+        assert y.shape == (3, 224 + 2 * pad, 224 + 2 * pad, 8)
+        exp = ops.pair_image(_nhwc(ref), pad)
+        assert _rel(y, exp) < 4e-3
+        assert torch.all(y[..., 3] == 0) and torch.all(y[..., 7] == 0)
 
 
 def test_preprocess_resize(gpu):
@@ -159,7 +162,7 @@ def test_preprocess_resize(gpu):
         rs = F.interpolate(_nchw(img.float()), size=(rh, rw), mode="bilinear", align_corners=False)
         oy, ox = (rh - 224) // 2, (rw - 224) // 2
         ref = (rs[:, :, oy:oy + 224, ox:ox + 224] / 255 - MEAN) / STD
-        y = ops.preprocess_u8(img.to(gpu), 224)
+        y = ops.preprocess_u8(img.to(gpu), 224, 0)
         torch.cuda.synchronize()
         got = _nchw(y.float().cpu()[..., :3].contiguous())
         assert _rel(got, ref) < 5e-3, (H, W, _rel(got, ref))

@@ -1,0 +1,79 @@
+#!/usr/bin/env python3
+"""Per-layer conv microbenchmark on the GPU (ResNet18 / AlexNet shapes).
+
+Times each distinct conv of the model in isolation with hipEvents (median of
+--iters), for every tile config, and reports TFLOP/s. Used for kernel A/B
+work and for rocprofv3 --pmc runs (one process, interleaved configs).
+"""
+import argparse
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from dmlc import ops  # noqa: E402
+
+RESNET18 = [
+    # name, H, W, Cin, Cout, k, s, p, pair
+    ("conv1", 230, 230, 8, 64, 7, 2, 3, True),
+    ("l1", 56, 56, 64, 64, 3, 1, 1, False),
+    ("l2.ds", 56, 56, 64, 128, 1, 2, 0, False),
+    ("l2.c1", 56, 56, 64, 128, 3, 2, 1, False),
+    ("l2", 28, 28, 128, 128, 3, 1, 1, False),
+    ("l3.c1", 28, 28, 128, 256, 3, 2, 1, False),
+    ("l3", 14, 14, 256, 256, 3, 1, 1, False),
+    ("l4.c1", 14, 14, 256, 512, 3, 2, 1, False),
+    ("l4", 7, 7, 512, 512, 3, 1, 1, False),
+]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--tiles", default="-1,0,1,2")
+    ap.add_argument("--only", default="")
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    B = a.batch
+    tiles = [int(t) for t in a.tiles.split(",")]
+    for name, H, W, Cin, Cout, k, s, p, pair in RESNET18:
+        if a.only and name not in a.only.split(","):
+            continue
+        x = (torch.randn(B, H, W, Cin, device=dev) * 0.5).bfloat16()
+        cin_real = 3 if pair else Cin
+        w = torch.randn(Cout, cin_real, k, k) / (cin_real * k * k) ** 0.5
+        wp = ops.pack_conv_weight(w, pair_stem=pair, device=dev)
+        bias = torch.zeros(Cout, device=dev)
+        Ho = (H + 2 * (0 if pair else p) - k) // s + 1
+        flops = 2.0 * B * Ho * Ho * Cout * cin_real * k * k
+        row = []
+        for t in tiles:
+            if t == 2 and Cout % 256:
+                continue
+            if t in (0, 2) and Cout % 128:
+                continue
+            try:
+                f = lambda: ops.conv2d(x, wp, Cout, k, k, s, p, bias=bias, relu=True, tile=t, pair_stem=pair)
+                f()
+                torch.cuda.synchronize()
+                ts = []
+                for _ in range(a.iters):
+                    e0, e1 = torch.cuda.Event(True), torch.cuda.Event(True)
+                    e0.record()
+                    f()
+                    e1.record()
+                    e1.synchronize()
+                    ts.append(e0.elapsed_time(e1))
+                ms = statistics.median(ts)
+                row.append(f"tile{t}={ms*1e3:7.1f}us {flops/ms/1e9:6.0f}TF")
+            except Exception as e:  # noqa: BLE001
+                row.append(f"tile{t}=ERR({e})")
+        print(f"{name:6s} M={B*Ho*Ho:8d} N={Cout:4d} K={cin_real*k*k:5d}  " + "  ".join(row), flush=True)
+
+
+if __name__ == "__main__":
+    main()
