@@ -53,9 +53,34 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + local;
 }
 
-template <int BM, int BN, int WM, int WN, bool PAIR>
-__global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a, int kt_per_split, int k_tiles) {
+// __launch_bounds__(256, 2): 2 waves/SIMD caps the unified register budget
+// at 256, which keeps the 64 accumulator registers in arch VGPRs. Without
+// it hipcc splits into AGPRs and shuffles ~100 v_accvgpr_* per K-tile
+// (measured: 4.4 VALU per MFMA, 40% of wave cycles in waits).
+// s_waitcnt vmcnt(N) with a compile-time N (the field is an immediate).
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+
+// Leave at most min(D-1, remaining) tiles (G DMA instructions each) of this
+// wave in flight. `remaining` = tiles issued after the one being waited for.
+template <int D, int G>
+__device__ __forceinline__ void wait_tiles(int remaining) {
+  if constexpr (D >= 3) {
+    if (remaining >= 2) { vm_wait<2 * G>(); return; }
+  }
+  if constexpr (D >= 2) {
+    if (remaining >= 1) { vm_wait<G>(); return; }
+  }
+  vm_wait<0>();
+}
+
+template <int BM, int BN, int WM, int WN, int NS, bool PAIR>
+__global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a, int kt_per_split, int k_tiles) {
   constexpr int BK = 64;
+  static_assert(NS >= 2 && NS <= 4, "stages");
   constexpr int PA = BM / 32;  // A rows per lane (wave covers BM/4 rows = PA instrs of 8 rows)
   constexpr int PB = BN / 32;
   constexpr int WTM = BM / WM, WTN = BN / WN;
@@ -199,19 +224,30 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a, int kt_per_
     }
   };
 
+  // NS-stage ring, prefetch distance D = NS-1 tiles. Iteration `it`:
+  //   wait (counted) until this wave's DMA for tile `it` landed, leaving the
+  //   younger tiles in flight; raw s_barrier (no vmcnt(0) drain) so every
+  //   wave's part of tile `it` is visible and every wave has finished reading
+  //   tile it-1; then refill tile it-1's stage with tile it+D and compute.
+  constexpr int D = NS - 1;
+  constexpr int G = PA + PB;  // LDS-DMA instructions per wave per tile
   if (nk > 0) {
-    stage(kt0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    int cur = 0;
-    for (int it = 1; it < nk; ++it) {
-      stage(kt0 + it, cur ^ 1);  // DMA of the next tile lands under these MFMAs
-      compute(cur);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      cur ^= 1;
+#pragma unroll
+    for (int s = 0; s < D; ++s)
+      if (s < nk) stage(kt0 + s, s);
+    int st = 0;
+    for (int it = 0; it < nk; ++it) {
+      wait_tiles<D, G>(min(D - 1, nk - 1 - it));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (it + D < nk) {
+        const int ls = st == 0 ? NS - 1 : st - 1;  // stage of tile it-1 == stage of tile it+D
+        stage(kt0 + it + D, ls);
+      }
+      compute(st);
+      st = st == NS - 1 ? 0 : st + 1;
     }
-    compute(cur);
   }
 
   // Epilogue. Lane holds D[n = 4*fq + r][m = fr] of each 16x16 tile.
@@ -296,31 +332,34 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(ConvArgs a, int M, i
 }
 
 struct TileCfg {
-  int bm, bn;
+  int bm, bn, ns;
 };
 
-// Tile configurations: 0 = 128x128 (2x2 waves), 1 = 256x64 (4x1 waves),
-// 2 = 64x256 (1x4 waves).
-constexpr TileCfg kTiles[3] = {{128, 128}, {256, 64}, {64, 256}};
+// Tile configurations (4 waves each, 64x64 per wave; ns = LDS stages):
+//   0: 128x128 ns2   1: 256x64 ns2   2: 64x256 ns2
+//   3: 128x128 ns3   4: 256x64 ns3   5: 64x256 ns3   6: 128x128 ns4
+constexpr int kNumTiles = 7;
+constexpr TileCfg kTiles[kNumTiles] = {{128, 128, 2}, {256, 64, 2}, {64, 256, 2}, {128, 128, 3},
+                                       {256, 64, 3},  {64, 256, 3}, {128, 128, 4}};
 
 int pick_tile(const ConvArgs& a) {
-  if (a.tile >= 0) return a.tile;
+  if (a.tile >= 0 && a.tile < kNumTiles) return a.tile;
   if (a.Npad % 128 != 0) return 1;
   const long M = (long)a.B * a.Ho * a.Wo;
   if (M <= 64 && a.Npad % 256 == 0) return 2;
   return 0;
 }
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, int NS>
 void launch_cfg(const ConvArgs& a, int splits, int kt_per, int k_tiles, hipStream_t s) {
   const int M = a.B * a.Ho * a.Wo;
   const int tiles = ((M + BM - 1) / BM) * (a.Npad / BN);
   dim3 grid(tiles, splits);
-  const size_t lds = (size_t)2 * (BM + BN) * 128;
+  const size_t lds = (size_t)NS * (BM + BN) * 128;
   if (a.pair_stem)
-    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, true>), grid, dim3(256), lds, s, a, kt_per, k_tiles);
+    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, NS, true>), grid, dim3(256), lds, s, a, kt_per, k_tiles);
   else
-    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, false>), grid, dim3(256), lds, s, a, kt_per, k_tiles);
+    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, NS, false>), grid, dim3(256), lds, s, a, kt_per, k_tiles);
   DMLC_HIP_CHECK(hipGetLastError());
 }
 
@@ -395,9 +434,13 @@ void conv2d_igemm(const ConvArgs& a, hipStream_t s) {
   ConvArgs b = a;
   b.split_k = splits;
   switch (cfg) {
-    case 0: launch_cfg<128, 128, 2, 2>(b, splits, kt_per, k_tiles, s); break;
-    case 1: launch_cfg<256, 64, 4, 1>(b, splits, kt_per, k_tiles, s); break;
-    default: launch_cfg<64, 256, 1, 4>(b, splits, kt_per, k_tiles, s); break;
+    case 0: launch_cfg<128, 128, 2, 2, 2>(b, splits, kt_per, k_tiles, s); break;
+    case 1: launch_cfg<256, 64, 4, 1, 2>(b, splits, kt_per, k_tiles, s); break;
+    case 2: launch_cfg<64, 256, 1, 4, 2>(b, splits, kt_per, k_tiles, s); break;
+    case 3: launch_cfg<128, 128, 2, 2, 3>(b, splits, kt_per, k_tiles, s); break;
+    case 4: launch_cfg<256, 64, 4, 1, 3>(b, splits, kt_per, k_tiles, s); break;
+    case 5: launch_cfg<64, 256, 1, 4, 3>(b, splits, kt_per, k_tiles, s); break;
+    default: launch_cfg<128, 128, 2, 2, 4>(b, splits, kt_per, k_tiles, s); break;
   }
   if (splits > 1) {
     const int blocks = (int)std::min<long>((M * (a.N / 4) + 255) / 256, 4096);

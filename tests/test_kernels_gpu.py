@@ -46,6 +46,14 @@ CONV_CASES = [
     (2, 14, 14, 256, 256, 3, 1, 1, False, False, 1, 1),
     (2, 14, 14, 256, 256, 3, 1, 1, False, False, 2, 1),
     (2, 14, 14, 256, 512, 1, 1, 0, False, False, 0, 3),
+    # multi-stage LDS rings (counted vmcnt + raw barrier)
+    (3, 28, 28, 128, 128, 3, 1, 1, True, True, 3, 1),
+    (2, 56, 56, 64, 64, 3, 1, 1, True, False, 4, 1),
+    (2, 14, 14, 256, 256, 3, 1, 1, False, True, 5, 1),
+    (3, 28, 28, 128, 128, 3, 1, 1, True, True, 6, 1),
+    (1, 7, 7, 512, 512, 3, 1, 1, True, True, 6, 4),
+    (1, 7, 7, 512, 512, 3, 1, 1, True, True, 3, 16),
+    (2, 14, 14, 256, 256, 1, 1, 0, False, False, 3, 1),
 ]
 
 

@@ -34,7 +34,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--tiles", default="-1,0,1,2")
+    ap.add_argument("--tiles", default="-1,0,1,2,3,4,5,6")
     ap.add_argument("--only", default="")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -52,9 +52,9 @@ def main():
         flops = 2.0 * B * Ho * Ho * Cout * cin_real * k * k
         row = []
         for t in tiles:
-            if t == 2 and Cout % 256:
+            if t in (2, 5) and Cout % 256:
                 continue
-            if t in (0, 2) and Cout % 128:
+            if t in (0, 2, 3, 5, 6) and Cout % 128:
                 continue
             try:
                 f = lambda: ops.conv2d(x, wp, Cout, k, k, s, p, bias=bias, relu=True, tile=t, pair_stem=pair)
