@@ -10,6 +10,7 @@
 
 #include "../kernels/kernels.h"
 #include "../runtime/engine.h"
+#include "../runtime/jpeg.h"
 #include "../runtime/ot_io.h"
 
 namespace py = pybind11;
@@ -116,6 +117,19 @@ PYBIND11_MODULE(_C, m) {
   m.def("softmax_top1", [](uintptr_t logits, int B, int N, int ld, uintptr_t idx, uintptr_t prob,
                            uintptr_t stream) {
     softmax_top1(P<float>(logits), B, N, ld, P<int32_t>(idx), P<float>(prob), S(stream));
+  });
+
+  // ---------------------------------------------------------------- jpeg
+  m.def("decode_jpeg", [](py::bytes data) {
+    std::string s = data;
+    Image img;
+    {
+      py::gil_scoped_release nogil;
+      img = decode_jpeg((const uint8_t*)s.data(), s.size());
+    }
+    py::array_t<uint8_t> a({img.height, img.width, 3});
+    std::copy(img.rgb.begin(), img.rgb.end(), a.mutable_data());
+    return a;
   });
 
   // ---------------------------------------------------------------- .ot

@@ -1,0 +1,303 @@
+#include "member.h"
+
+#include <dirent.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <fstream>
+
+#include "common.h"
+
+namespace dmlc {
+namespace ctl {
+
+namespace {
+
+void rm_rf(const std::string& path) {
+  DIR* d = opendir(path.c_str());
+  if (d) {
+    while (dirent* e = readdir(d)) {
+      const std::string n = e->d_name;
+      if (n == "." || n == "..") continue;
+      const std::string p = path + "/" + n;
+      struct stat st;
+      if (lstat(p.c_str(), &st) == 0 && S_ISDIR(st.st_mode))
+        rm_rf(p);
+      else
+        unlink(p.c_str());
+    }
+    closedir(d);
+  }
+  rmdir(path.c_str());
+}
+
+void mkdir_p(const std::string& path) {
+  std::string cur;
+  for (const auto& part : split(path, '/')) {
+    cur += part + "/";
+    if (!part.empty()) mkdir(cur.c_str(), 0755);
+  }
+}
+
+std::vector<std::string> list_dir_sorted(const std::string& path) {
+  std::vector<std::string> out;
+  DIR* d = opendir(path.c_str());
+  if (!d) return out;
+  while (dirent* e = readdir(d)) {
+    const std::string n = e->d_name;
+    if (n != "." && n != "..") out.push_back(n);
+  }
+  closedir(d);
+  std::sort(out.begin(), out.end());
+  return out;
+}
+
+}  // namespace
+
+Labels Labels::load(const std::string& path) {
+  Labels l;
+  std::ifstream f(path);
+  std::string line;
+  while (std::getline(f, line)) {
+    line = trim(line);
+    if (line.empty()) continue;
+    const auto sp = line.find(' ');
+    std::string wnid = sp == std::string::npos ? line : line.substr(0, sp);
+    std::string text = sp == std::string::npos ? "" : trim(line.substr(sp + 1));
+    l.index[wnid] = (int)l.entries.size();
+    l.entries.emplace_back(wnid, text);
+  }
+  return l;
+}
+
+std::string Labels::text(int idx) const {
+  if (idx >= 0 && idx < (int)entries.size()) return entries[idx].second;
+  return "class " + std::to_string(idx);
+}
+
+MemberService::MemberService(MemberConfig cfg, MembershipService* ms, std::unique_ptr<Executor> exec, Labels labels)
+    : cfg_(std::move(cfg)), ms_(ms), exec_(std::move(exec)), labels_(std::move(labels)) {
+  if (cfg_.storage_dir.empty()) cfg_.storage_dir = cfg_.workdir + "/storage";
+  if (cfg_.models_dir.empty()) cfg_.models_dir = cfg_.workdir + "/models";
+  if (!cfg_.leader_candidates.empty()) leader_ = cfg_.leader_candidates[0];
+}
+
+MemberService::~MemberService() { stop(); }
+
+void MemberService::start(int base_port) {
+  rm_rf(cfg_.storage_dir);  // storage is recreated empty at start-up (src/services.rs:504-507)
+  mkdir_p(cfg_.storage_dir);
+  mkdir_p(cfg_.models_dir);
+  server_ = std::make_unique<RpcServer>("member", cfg_.bind_host, member_port(base_port));
+  register_handlers();
+  server_->start();
+  checker_ = std::thread([this] { leader_check_loop(); });
+}
+
+void MemberService::stop() {
+  if (stop_.exchange(true)) return;
+  if (checker_.joinable()) checker_.join();
+  if (server_) server_->stop();
+}
+
+std::string MemberService::leader_address() const {
+  std::lock_guard<std::mutex> g(mu_);
+  return leader_;
+}
+
+std::map<std::string, std::set<int>> MemberService::files() const {
+  std::lock_guard<std::mutex> g(mu_);
+  return files_;
+}
+
+std::string MemberService::resolve_spec(const std::string& spec) const {
+  if (starts_with(spec, "storage:")) return cfg_.storage_dir + "/" + sanitize_filename(spec.substr(8));
+  if (starts_with(spec, "models:")) return cfg_.models_dir + "/" + sanitize_filename(spec.substr(7));
+  if (!spec.empty() && spec[0] == '/') return spec;
+  return cfg_.workdir + "/" + spec;
+}
+
+std::vector<std::pair<double, std::string>> MemberService::predict(const std::string& model,
+                                                                   const std::vector<std::string>& ids, bool* ok) {
+  *ok = false;
+  std::vector<std::pair<double, std::string>> out;
+  if (!exec_ || !exec_->has_model(model)) return out;
+  std::vector<Image> imgs;
+  for (const auto& id : ids) {
+    const std::string dir = cfg_.dataset_dir + "/" + sanitize_filename(id);
+    const auto files = list_dir_sorted(dir);
+    if (files.empty()) continue;  // unknown id: skipped, like a failed read_dir entry
+    imgs.push_back(decode_jpeg_file(dir + "/" + files[0]));
+  }
+  const auto preds = exec_->predict(model, imgs);
+  for (const auto& p : preds) out.emplace_back(p.prob, labels_.text(p.class_idx));
+  *ok = true;
+  return out;
+}
+
+bool MemberService::fetch(const std::string& src_host, int src_port, const std::string& src_spec,
+                          const std::string& dest_spec) {
+  const std::string dest = resolve_spec(dest_spec);
+  const std::string tmp = dest + ".part" + std::to_string(getpid());
+  try {
+    std::ofstream out(tmp, std::ios::binary | std::ios::trunc);
+    if (!out) throw std::runtime_error("cannot open " + tmp);
+    uint64_t off = 0;
+    while (true) {
+      Writer w;
+      w.str(src_spec).u64(off).u32((uint32_t)cfg_.chunk_bytes);
+      const std::string resp = RpcClient::shared().call(src_host, src_port, M_READ_CHUNK, w.data(), 60000);
+      Reader r(resp);
+      const uint64_t total = r.u64();
+      const std::string data = r.str();
+      out.write(data.data(), (std::streamsize)data.size());
+      off += data.size();
+      if (off >= total || data.empty()) break;
+    }
+    out.close();
+    if (rename(tmp.c_str(), dest.c_str()) != 0) throw std::runtime_error("rename failed");
+    DMLC_LOG_INFO("fetch " << src_host << ":" << src_port << ":" << src_spec << " -> " << dest << ": ok (" << off
+                           << " B)");
+    return true;
+  } catch (const std::exception& e) {
+    unlink(tmp.c_str());
+    DMLC_LOG_WARN("fetch " << src_host << ":" << src_port << ":" << src_spec << " -> " << dest
+                           << ": failed: " << e.what());
+    return false;
+  }
+}
+
+void MemberService::register_handlers() {
+  server_->handle(M_GET_LATEST_VERSION, [this](Reader& r) {
+    const std::string f = r.str();
+    Writer w;
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = files_.find(f);
+    if (it == files_.end() || it->second.empty()) {
+      w.boolean(false).i32(0);
+    } else {
+      w.boolean(true).i32(*it->second.rbegin());
+    }
+    return w.take();
+  });
+  server_->handle(M_RECEIVE, [this](Reader& r) {
+    const std::string f = r.str();
+    const int v = r.i32();
+    std::lock_guard<std::mutex> g(mu_);
+    files_[f].insert(v);
+    return std::string();
+  });
+  server_->handle(M_PREDICT, [this](Reader& r) {
+    const std::string model = r.str();
+    const uint32_t n = r.u32();
+    std::vector<std::string> ids(n);
+    for (auto& s : ids) s = r.str();
+    bool ok = false;
+    const auto res = predict(model, ids, &ok);
+    Writer w;
+    w.boolean(ok).u32((uint32_t)res.size());
+    for (const auto& p : res) w.f64(p.first).str(p.second);
+    return w.take();
+  });
+  server_->handle(M_FETCH, [this](Reader& r) {
+    const std::string host = r.str();
+    const int port = r.i32();
+    const std::string src = r.str(), dest = r.str();
+    Writer w;
+    w.boolean(fetch(host, port, src, dest));
+    return w.take();
+  });
+  server_->handle(M_READ_CHUNK, [this](Reader& r) {
+    const std::string spec = r.str();
+    const uint64_t off = r.u64();
+    const uint32_t len = std::min<uint32_t>(r.u32(), 64u << 20);
+    const std::string path = resolve_spec(spec);
+    std::ifstream f(path, std::ios::binary);
+    if (!f) throw std::runtime_error("no such file: " + spec);
+    f.seekg(0, std::ios::end);
+    const uint64_t total = (uint64_t)f.tellg();
+    std::string data;
+    if (off < total) {
+      data.resize((size_t)std::min<uint64_t>(len, total - off));
+      f.seekg((std::streamoff)off);
+      f.read(&data[0], (std::streamsize)data.size());
+    }
+    Writer w;
+    w.u64(total).str(data);
+    return w.take();
+  });
+  server_->handle(M_DELETE_FILE, [this](Reader& r) {
+    const std::string f = r.str();
+    std::set<int> versions;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      auto it = files_.find(f);
+      if (it != files_.end()) versions = it->second;
+      files_.erase(f);
+    }
+    for (int v : versions) unlink((cfg_.storage_dir + "/" + storage_filename(f, v)).c_str());
+    return std::string();
+  });
+  server_->handle(M_LOAD_MODEL, [this](Reader& r) {
+    const std::string model = r.str();
+    const std::string spec = r.str();
+    Writer w;
+    try {
+      if (!exec_) throw std::runtime_error("no executor");
+      exec_->load_model(model, resolve_spec(spec));
+      DMLC_LOG_INFO("loaded model " << model << " from " << resolve_spec(spec));
+      w.boolean(true).str("");
+    } catch (const std::exception& e) {
+      w.boolean(false).str(e.what());
+    }
+    return w.take();
+  });
+  server_->handle(M_INFO, [this](Reader&) {
+    Writer w;
+    w.str(exec_ ? exec_->backend() : "none");
+    std::lock_guard<std::mutex> g(mu_);
+    w.u32((uint32_t)files_.size());
+    return w.take();
+  });
+}
+
+bool MemberService::check_leader(const std::string& addr) {
+  try {
+    const std::string resp = RpcClient::shared().call(host_of(addr), leader_port(port_of(addr)), L_ALIVE, "", 2000);
+    Reader r(resp);
+    return r.boolean();
+  } catch (const std::exception&) {
+    return false;
+  }
+}
+
+void MemberService::leader_check_loop() {
+  while (!stop_.load()) {
+    for (int slept = 0; slept < cfg_.check_ms && !stop_.load(); slept += 50)
+      std::this_thread::sleep_for(std::chrono::milliseconds(50));
+    if (stop_.load() || cfg_.leader_candidates.empty()) break;
+    std::string cur = leader_address();
+    if (check_leader(cur)) continue;
+    // Advance through the candidate list (wrapping, unlike the reference),
+    // at most one full round per check period.
+    const auto& c = cfg_.leader_candidates;
+    size_t idx = std::find(c.begin(), c.end(), cur) - c.begin();
+    for (size_t step = 1; step <= c.size(); ++step) {
+      const std::string next = c[(idx + step) % c.size()];
+      if (next == cur) continue;
+      if (check_leader(next)) {
+        {
+          std::lock_guard<std::mutex> g(mu_);
+          leader_ = next;
+        }
+        DMLC_LOG_WARN("leader " << cur << " unreachable; switched to " << next);
+        break;
+      }
+    }
+  }
+}
+
+}  // namespace ctl
+}  // namespace dmlc

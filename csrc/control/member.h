@@ -1,0 +1,84 @@
+// Member service: replica registry, SDFS data plane, inference, leader
+// pointer.
+//
+// Reference: tarpc `Member` (get_latest_version / receive / predict,
+// src/services.rs:443-497), MemberState::shared (storage wipe, model load,
+// leader health loop, src/services.rs:502-548), check_leader
+// (src/services.rs:571-580). Differences: bulk data moves member-to-member
+// over this RPC (M_FETCH pulls chunks with M_READ_CHUNK) instead of `scp`;
+// `delete` removes replica files; `train` hot-swaps weights (M_LOAD_MODEL);
+// the leader pointer wraps around the candidate list.
+#pragma once
+#include <atomic>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <set>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../serve/executor.h"
+#include "membership.h"
+#include "rpc.h"
+#include "sdfs.h"
+
+namespace dmlc {
+namespace ctl {
+
+struct MemberConfig {
+  std::string bind_host = "0.0.0.0";
+  std::string workdir = ".";
+  std::string storage_dir;  // default <workdir>/storage
+  std::string models_dir;   // default <workdir>/models
+  std::string dataset_dir;  // imagenet_1k/train layout: <dir>/<wnid>/<file>.JPEG
+  std::vector<std::string> leader_candidates;  // base addresses "host:port", in order
+  int check_ms = 3000;
+  int chunk_bytes = 8 << 20;
+};
+
+// Label table: synset_words.txt lines "<wnid> <label text>" (src/services.rs:170-184).
+struct Labels {
+  std::vector<std::pair<std::string, std::string>> entries;
+  std::map<std::string, int> index;
+  static Labels load(const std::string& path);
+  std::string text(int idx) const;
+};
+
+class MemberService {
+ public:
+  MemberService(MemberConfig cfg, MembershipService* ms, std::unique_ptr<Executor> exec, Labels labels);
+  ~MemberService();
+  void start(int base_port);
+  void stop();
+
+  std::string leader_address() const;  // base address of the current leader
+  std::map<std::string, std::set<int>> files() const;
+  std::string resolve_spec(const std::string& spec) const;
+  Executor* executor() { return exec_.get(); }
+  const Labels& labels() const { return labels_; }
+
+  // local implementations (also reachable over RPC)
+  std::vector<std::pair<double, std::string>> predict(const std::string& model, const std::vector<std::string>& ids,
+                                                      bool* ok);
+  bool fetch(const std::string& src_host, int src_port, const std::string& src_spec, const std::string& dest_spec);
+
+ private:
+  void register_handlers();
+  void leader_check_loop();
+  bool check_leader(const std::string& addr);
+
+  MemberConfig cfg_;
+  MembershipService* ms_;
+  std::unique_ptr<Executor> exec_;
+  Labels labels_;
+  std::unique_ptr<RpcServer> server_;
+  mutable std::mutex mu_;
+  std::map<std::string, std::set<int>> files_;
+  std::string leader_;
+  std::atomic<bool> stop_{false};
+  std::thread checker_;
+};
+
+}  // namespace ctl
+}  // namespace dmlc

@@ -1,0 +1,271 @@
+#include "executor.h"
+
+#include <ATen/ATen.h>
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <map>
+#include <stdexcept>
+
+#include "../runtime/engine.h"
+#include "../runtime/ot_io.h"
+
+namespace dmlc {
+
+std::vector<float> preprocess_host(const Image& img, int S) {
+  const int Hin = img.height, Win = img.width;
+  int RH, RW;
+  if (Hin <= Win) {
+    RH = S;
+    RW = (int)((long)S * Win / Hin);
+  } else {
+    RW = S;
+    RH = (int)((long)S * Hin / Win);
+  }
+  const int oy = (RH - S) / 2, ox = (RW - S) / 2;
+  const float sys = (float)Hin / RH, sxs = (float)Win / RW;
+  const bool identity = Hin == S && Win == S;
+  const float mean[3] = {0.485f, 0.456f, 0.406f}, stdv[3] = {0.229f, 0.224f, 0.225f};
+  std::vector<float> out((size_t)3 * S * S);
+  for (int y = 0; y < S; ++y)
+    for (int x = 0; x < S; ++x) {
+      float c[3];
+      if (identity) {
+        const uint8_t* p = &img.rgb[((size_t)y * Win + x) * 3];
+        for (int k = 0; k < 3; ++k) c[k] = p[k];
+      } else {
+        float sy = (y + oy + 0.5f) * sys - 0.5f, sx = (x + ox + 0.5f) * sxs - 0.5f;
+        sy = std::min(std::max(sy, 0.f), (float)(Hin - 1));
+        sx = std::min(std::max(sx, 0.f), (float)(Win - 1));
+        const int y0 = (int)sy, x0 = (int)sx, y1 = std::min(y0 + 1, Hin - 1), x1 = std::min(x0 + 1, Win - 1);
+        const float fy = sy - y0, fx = sx - x0;
+        for (int k = 0; k < 3; ++k) {
+          const float a = img.rgb[((size_t)y0 * Win + x0) * 3 + k], b = img.rgb[((size_t)y0 * Win + x1) * 3 + k];
+          const float d = img.rgb[((size_t)y1 * Win + x0) * 3 + k], e = img.rgb[((size_t)y1 * Win + x1) * 3 + k];
+          const float top = a + (b - a) * fx, bot = d + (e - d) * fx;
+          c[k] = top + (bot - top) * fy;
+        }
+      }
+      for (int k = 0; k < 3; ++k) out[(size_t)k * S * S + (size_t)y * S + x] = (c[k] / 255.f - mean[k]) / stdv[k];
+    }
+  return out;
+}
+
+int hip_device_count() {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+namespace {
+
+// ------------------------------------------------------------------ CPU
+class CpuExecutor : public Executor {
+ public:
+  std::string backend() const override { return "cpu"; }
+
+  void load_model(const std::string& model, const std::string& path) override {
+    load_model_weights(model, ot_load(path));
+  }
+
+  void load_model_weights(const std::string& model, const WeightMap& w) override {
+    std::map<std::string, at::Tensor> t;
+    for (const auto& kv : w)
+      t[kv.first] = at::from_blob(const_cast<float*>(kv.second.data.data()), kv.second.shape, at::kFloat).clone();
+    std::lock_guard<std::mutex> g(mu_);
+    models_[model] = std::move(t);
+  }
+
+  bool has_model(const std::string& model) const override {
+    std::lock_guard<std::mutex> g(mu_);
+    return models_.count(model) > 0;
+  }
+
+  std::vector<Prediction> predict(const std::string& model, const std::vector<Image>& imgs) override {
+    std::lock_guard<std::mutex> g(mu_);  // per-executor model lock, like the reference's Mutex<Box<dyn ModuleT>>
+    auto it = models_.find(model);
+    if (it == models_.end()) throw std::runtime_error("model not loaded: " + model);
+    if (imgs.empty()) return {};
+    const int S = 224;
+    at::Tensor x = at::empty({(int64_t)imgs.size(), 3, S, S}, at::kFloat);
+    for (size_t i = 0; i < imgs.size(); ++i) {
+      auto v = preprocess_host(imgs[i], S);
+      std::memcpy(x[i].data_ptr<float>(), v.data(), v.size() * 4);
+    }
+    at::Tensor logits = forward(model, it->second, x);
+    at::Tensor p = at::softmax(logits, -1);
+    auto mx = p.max(-1);
+    at::Tensor pv = std::get<0>(mx).contiguous(), pi = std::get<1>(mx).contiguous();
+    std::vector<Prediction> out(imgs.size());
+    for (size_t i = 0; i < imgs.size(); ++i) {
+      out[i].prob = pv[i].item<float>();
+      out[i].class_idx = (int)pi[i].item<int64_t>();
+    }
+    return out;
+  }
+
+ private:
+  using TM = std::map<std::string, at::Tensor>;
+  static const at::Tensor& W(const TM& w, const std::string& k) {
+    auto it = w.find(k);
+    if (it == w.end()) throw std::runtime_error("missing weight: " + k);
+    return it->second;
+  }
+  static at::Tensor conv(const TM& w, const at::Tensor& x, const std::string& c, const std::string& bn, int s, int p,
+                         bool relu) {
+    auto bi = w.find(c + ".bias");
+    at::Tensor y = at::conv2d(x, W(w, c + ".weight"), bi == w.end() ? at::Tensor() : bi->second, {s, s}, {p, p});
+    if (!bn.empty())
+      y = at::batch_norm(y, W(w, bn + ".weight"), W(w, bn + ".bias"), W(w, bn + ".running_mean"),
+                         W(w, bn + ".running_var"), false, 0.1, 1e-5, false);
+    return relu ? at::relu(y) : y;
+  }
+  static at::Tensor forward(const std::string& arch, const TM& w, at::Tensor x) {
+    if (arch == "alexnet") {
+      x = conv(w, x, "features.0", "", 4, 2, true);
+      x = at::max_pool2d(x, {3, 3}, {2, 2});
+      x = conv(w, x, "features.3", "", 1, 2, true);
+      x = at::max_pool2d(x, {3, 3}, {2, 2});
+      x = conv(w, x, "features.6", "", 1, 1, true);
+      x = conv(w, x, "features.8", "", 1, 1, true);
+      x = conv(w, x, "features.10", "", 1, 1, true);
+      x = at::max_pool2d(x, {3, 3}, {2, 2});
+      x = at::adaptive_avg_pool2d(x, {6, 6}).flatten(1);
+      x = at::relu(at::linear(x, W(w, "classifier.1.weight"), W(w, "classifier.1.bias")));
+      x = at::relu(at::linear(x, W(w, "classifier.4.weight"), W(w, "classifier.4.bias")));
+      return at::linear(x, W(w, "classifier.6.weight"), W(w, "classifier.6.bias"));
+    }
+    std::vector<int> blocks;
+    bool bottleneck = false;
+    if (arch == "resnet18") blocks = {2, 2, 2, 2};
+    else if (arch == "resnet34") blocks = {3, 4, 6, 3};
+    else if (arch == "resnet50") blocks = {3, 4, 6, 3}, bottleneck = true;
+    else throw std::runtime_error("unknown arch: " + arch);
+    x = conv(w, x, "conv1", "bn1", 2, 3, true);
+    x = at::max_pool2d(x, {3, 3}, {2, 2}, {1, 1});
+    for (int li = 0; li < 4; ++li)
+      for (int bi = 0; bi < blocks[li]; ++bi) {
+        const int stride = (li > 0 && bi == 0) ? 2 : 1;
+        const std::string p = "layer" + std::to_string(li + 1) + "." + std::to_string(bi);
+        at::Tensor idt = x;
+        if (w.count(p + ".downsample.0.weight"))
+          idt = conv(w, x, p + ".downsample.0", p + ".downsample.1", stride, 0, false);
+        at::Tensor y;
+        if (!bottleneck) {
+          y = conv(w, x, p + ".conv1", p + ".bn1", stride, 1, true);
+          y = conv(w, y, p + ".conv2", p + ".bn2", 1, 1, false);
+        } else {
+          y = conv(w, x, p + ".conv1", p + ".bn1", 1, 0, true);
+          y = conv(w, y, p + ".conv2", p + ".bn2", stride, 1, true);
+          y = conv(w, y, p + ".conv3", p + ".bn3", 1, 0, false);
+        }
+        x = at::relu(y + idt);
+      }
+    x = at::adaptive_avg_pool2d(x, {1, 1}).flatten(1);
+    return at::linear(x, W(w, "fc.weight"), W(w, "fc.bias"));
+  }
+
+  mutable std::mutex mu_;
+  std::map<std::string, TM> models_;
+};
+
+// ------------------------------------------------------------------ GPU
+class GpuExecutor : public Executor {
+ public:
+  GpuExecutor(int device, int max_batch) : device_(device), max_batch_(max_batch) {
+    DMLC_HIP_CHECK(hipSetDevice(device_));
+    DMLC_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    DMLC_HIP_CHECK(hipMalloc(&d_out_, (size_t)max_batch_ * 8));
+  }
+  ~GpuExecutor() override {
+    hipSetDevice(device_);
+    engines_.clear();
+    if (d_in_) hipFree(d_in_);
+    if (d_out_) hipFree(d_out_);
+    if (stream_) hipStreamDestroy(stream_);
+  }
+  std::string backend() const override { return "gpu:" + std::to_string(device_); }
+
+  void load_model(const std::string& model, const std::string& path) override {
+    load_model_weights(model, ot_load(path));
+  }
+  void load_model_weights(const std::string& model, const WeightMap& w) override {
+    std::lock_guard<std::mutex> g(mu_);
+    DMLC_HIP_CHECK(hipSetDevice(device_));
+    auto e = std::make_unique<Engine>(model, w, device_);
+    e->reserve(max_batch_);
+    engines_[model] = std::move(e);  // hot-swap: the old engine is freed here
+  }
+  bool has_model(const std::string& model) const override {
+    std::lock_guard<std::mutex> g(mu_);
+    return engines_.count(model) > 0;
+  }
+
+  std::vector<Prediction> predict(const std::string& model, const std::vector<Image>& imgs) override {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = engines_.find(model);
+    if (it == engines_.end()) throw std::runtime_error("model not loaded: " + model);
+    DMLC_HIP_CHECK(hipSetDevice(device_));
+    std::vector<Prediction> out(imgs.size());
+    // Group same-sized images; each group is one batched forward.
+    std::map<std::pair<int, int>, std::vector<size_t>> groups;
+    for (size_t i = 0; i < imgs.size(); ++i) groups[{imgs[i].height, imgs[i].width}].push_back(i);
+    for (const auto& kv : groups) {
+      const int H = kv.first.first, W = kv.first.second;
+      const auto& ids = kv.second;
+      for (size_t s = 0; s < ids.size(); s += (size_t)max_batch_) {
+        const int B = (int)std::min(ids.size() - s, (size_t)max_batch_);
+        const size_t per = (size_t)H * W * 3;
+        ensure_input(per * B);
+        for (int b = 0; b < B; ++b)
+          DMLC_HIP_CHECK(hipMemcpyAsync((uint8_t*)d_in_ + per * b, imgs[ids[s + b]].rgb.data(), per,
+                                        hipMemcpyHostToDevice, stream_));
+        int32_t* d_idx = (int32_t*)d_out_;
+        float* d_prob = (float*)((int32_t*)d_out_ + max_batch_);
+        // graphs only for the fixed-size serving shape; ragged sizes run eager
+        it->second->forward((const uint8_t*)d_in_, B, H, W, d_idx, d_prob, nullptr, stream_,
+                            H == 224 && W == 224);
+        std::vector<int32_t> hi(B);
+        std::vector<float> hp(B);
+        DMLC_HIP_CHECK(hipMemcpyAsync(hi.data(), d_idx, B * 4, hipMemcpyDeviceToHost, stream_));
+        DMLC_HIP_CHECK(hipMemcpyAsync(hp.data(), d_prob, B * 4, hipMemcpyDeviceToHost, stream_));
+        DMLC_HIP_CHECK(hipStreamSynchronize(stream_));
+        for (int b = 0; b < B; ++b) out[ids[s + b]] = Prediction{hp[b], hi[b]};
+      }
+    }
+    return out;
+  }
+
+ private:
+  void ensure_input(size_t bytes) {
+    if (bytes <= in_bytes_) return;
+    DMLC_HIP_CHECK(hipStreamSynchronize(stream_));
+    if (d_in_) DMLC_HIP_CHECK(hipFree(d_in_));
+    DMLC_HIP_CHECK(hipMalloc(&d_in_, bytes));
+    in_bytes_ = bytes;
+  }
+
+  int device_, max_batch_;
+  hipStream_t stream_ = nullptr;
+  void* d_in_ = nullptr;
+  size_t in_bytes_ = 0;
+  void* d_out_ = nullptr;
+  mutable std::mutex mu_;
+  std::map<std::string, std::unique_ptr<Engine>> engines_;
+};
+
+}  // namespace
+
+std::unique_ptr<Executor> make_executor(const std::string& backend, int device, int max_batch) {
+  std::string b = backend;
+  if (b == "auto") b = hip_device_count() > 0 ? "gpu" : "cpu";
+  if (b == "gpu") {
+    if (hip_device_count() <= device) throw std::runtime_error("no HIP device " + std::to_string(device));
+    return std::make_unique<GpuExecutor>(device, max_batch);
+  }
+  if (b == "cpu") return std::make_unique<CpuExecutor>();
+  throw std::invalid_argument("unknown executor backend: " + backend);
+}
+
+}  // namespace dmlc

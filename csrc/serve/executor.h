@@ -1,0 +1,48 @@
+// Inference executors used by the member service's `predict`.
+//
+// Reference: Member::predict (src/services.rs:475-497) decodes each queried
+// image, runs `forward_t` under a per-model mutex on the CPU, applies softmax
+// and takes the top-1 (prob, label). Here an executor classifies a whole
+// batch of decoded images:
+//   * GpuExecutor: the hand-written HIP engine (csrc/runtime/engine.cpp),
+//     images uploaded once as u8, preprocess/forward/top-1 on the GPU.
+//   * CpuExecutor: the same architectures on libtorch CPU ops (fp32); used
+//     on nodes without a GPU (the BASELINE "AlexNet single-image classify on
+//     CPU via libtorch .ot load" plumbing config).
+#pragma once
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../runtime/jpeg.h"
+#include "../runtime/weights.h"
+
+namespace dmlc {
+
+struct Prediction {
+  double prob = 0;
+  int class_idx = -1;
+};
+
+class Executor {
+ public:
+  virtual ~Executor() = default;
+  virtual std::string backend() const = 0;
+  // Loads (or hot-swaps) the weights of `model` (arch name) from a .ot file.
+  virtual void load_model(const std::string& model, const std::string& ot_path) = 0;
+  virtual void load_model_weights(const std::string& model, const WeightMap& w) = 0;
+  virtual bool has_model(const std::string& model) const = 0;
+  virtual std::vector<Prediction> predict(const std::string& model, const std::vector<Image>& imgs) = 0;
+};
+
+// backend: "gpu", "cpu" or "auto" (GPU when a HIP device is visible).
+std::unique_ptr<Executor> make_executor(const std::string& backend, int device, int max_batch);
+int hip_device_count();
+
+// Host-side reference preprocessing (same rule as csrc/kernels/preprocess.hip):
+// short side -> S (long = floor(S*long/short)), centre crop, bilinear
+// align_corners=False, /255, ImageNet mean/std. Output CHW float [3,S,S].
+std::vector<float> preprocess_host(const Image& img, int S);
+
+}  // namespace dmlc

@@ -1,0 +1,81 @@
+#include "job.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+
+namespace dmlc {
+namespace ctl {
+
+void write_job(Writer& w, const Job& j) {
+  w.str(j.model_name);
+  w.i32(j.finished);
+  w.i32(j.correct);
+  w.u32((uint32_t)j.durations_us.size());
+  for (int64_t d : j.durations_us) w.i64(d);
+  w.u32((uint32_t)j.assigned.size());
+  for (const auto& id : j.assigned) write_id(w, id);
+  w.i64(j.started_us);
+  w.i64(j.first_done_us);
+}
+
+Job read_job(Reader& r) {
+  Job j;
+  j.model_name = r.str();
+  j.finished = r.i32();
+  j.correct = r.i32();
+  uint32_t n = r.u32();
+  j.durations_us.resize(n);
+  for (uint32_t i = 0; i < n; ++i) j.durations_us[i] = r.i64();
+  n = r.u32();
+  for (uint32_t i = 0; i < n; ++i) j.assigned.push_back(read_id(r));
+  j.started_us = r.i64();
+  j.first_done_us = r.i64();
+  return j;
+}
+
+double percentile_sorted(const std::vector<double>& s, double q) {
+  if (s.empty()) return 0;
+  const double k = (s.size() - 1) * q / 100.0;
+  const size_t lo = (size_t)k, hi = std::min(lo + 1, s.size() - 1);
+  return s[lo] + (s[hi] - s[lo]) * (k - lo);
+}
+
+LatencyStats latency_stats(const std::vector<int64_t>& d) {
+  LatencyStats st;
+  st.count = d.size();
+  if (d.empty()) return st;
+  std::vector<double> ms(d.size());
+  for (size_t i = 0; i < d.size(); ++i) ms[i] = d[i] / 1000.0;
+  double sum = 0;
+  for (double v : ms) sum += v;
+  st.mean = sum / ms.size();
+  double var = 0;
+  for (double v : ms) var += (v - st.mean) * (v - st.mean);
+  st.stddev = std::sqrt(var / ms.size());
+  std::sort(ms.begin(), ms.end());
+  st.p50 = percentile_sorted(ms, 50);
+  st.p90 = percentile_sorted(ms, 90);
+  st.p95 = percentile_sorted(ms, 95);
+  st.p99 = percentile_sorted(ms, 99);
+  st.max = ms.back();
+  return st;
+}
+
+std::string format_job_report(int n, const Job& j) {
+  const LatencyStats s = latency_stats(j.durations_us);
+  const double acc = j.finished > 0 ? 100.0 * j.correct / j.finished : 0.0;
+  char buf[1024];
+  snprintf(buf, sizeof(buf),
+           "Job %d:\n"
+           "\tModel: %s\n"
+           "\tAccuracy: %d/%d = %.2f%%\n"
+           "\tQueries: %zu total, %.3f ms avg, %.3f ms std, %.3f ms median,\n"
+           "\t\t%.3f ms p90, %.3f ms p95, %.3f ms p99",
+           n, j.model_name.c_str(), j.correct, j.finished, acc, s.count, s.mean, s.stddev, s.p50, s.p90, s.p95,
+           s.p99);
+  return buf;
+}
+
+}  // namespace ctl
+}  // namespace dmlc

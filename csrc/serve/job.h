@@ -1,0 +1,51 @@
+// Inference job bookkeeping and latency statistics.
+//
+// Reference: `Job{model_name, finished_prediction_count,
+// correct_prediction_count, query_durations, assigned_member_ids}` and
+// `add_query_result` (src/services.rs:54-81); the `jobs` report computes
+// accuracy and mean/std/median/p90/p95/p99 with the `histogram` crate at
+// millisecond resolution (src/main.rs:271-314). Here durations are kept in
+// microseconds and percentiles are exact (sorted), reported in ms with
+// sub-millisecond resolution.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../control/membership.h"
+#include "../control/wire.h"
+
+namespace dmlc {
+namespace ctl {
+
+struct Job {
+  std::string model_name;
+  int32_t finished = 0;
+  int32_t correct = 0;
+  std::vector<int64_t> durations_us;
+  std::vector<Id> assigned;
+  int64_t started_us = 0;   // wall clock when the job first issued a query
+  int64_t first_done_us = 0;
+
+  void add_result(bool ok, int64_t dur_us) {
+    ++finished;
+    if (ok) ++correct;
+    durations_us.push_back(dur_us);
+  }
+};
+
+void write_job(Writer& w, const Job& j);
+Job read_job(Reader& r);
+
+struct LatencyStats {
+  size_t count = 0;
+  double mean = 0, stddev = 0, p50 = 0, p90 = 0, p95 = 0, p99 = 0, max = 0;  // ms
+};
+LatencyStats latency_stats(const std::vector<int64_t>& durations_us);
+double percentile_sorted(const std::vector<double>& sorted, double q);
+
+// The `jobs` report block (same fields and layout as src/main.rs:291-309).
+std::string format_job_report(int n, const Job& j);
+
+}  // namespace ctl
+}  // namespace dmlc

@@ -1,0 +1,517 @@
+#include "leader.h"
+
+#include <optional>
+
+#include "../control/common.h"
+
+namespace dmlc {
+namespace ctl {
+
+LeaderService::LeaderService(LeaderConfig cfg, MembershipService* ms, MemberService* member, Labels labels)
+    : cfg_(std::move(cfg)), ms_(ms), member_(member), labels_(std::move(labels)) {
+  for (const auto& m : cfg_.job_models) {
+    Job j;
+    j.model_name = m;
+    jobs_.push_back(j);
+  }
+  running_.assign(jobs_.size(), false);
+}
+
+LeaderService::~LeaderService() { stop(); }
+
+void LeaderService::start(int base_port) {
+  self_ = ms_->id().address;
+  server_ = std::make_unique<RpcServer>("leader", cfg_.bind_host, leader_port(base_port));
+  register_handlers();
+  server_->start();
+  loops_.emplace_back([this] { rereplicate_loop(); });
+  loops_.emplace_back([this] { assign_loop(); });
+  loops_.emplace_back([this] { succession_loop(); });
+}
+
+void LeaderService::stop() {
+  if (stop_.exchange(true)) return;
+  for (auto& t : loops_)
+    if (t.joinable()) t.join();
+  {
+    std::lock_guard<std::mutex> g(runners_mu_);
+    for (auto& t : runners_)
+      if (t.joinable()) t.join();
+  }
+  while (inflight_.load() > 0) std::this_thread::sleep_for(std::chrono::milliseconds(5));
+  if (server_) server_->stop();
+}
+
+bool LeaderService::is_leader() const { return member_->leader_address() == self_; }
+
+void LeaderService::sleep_bg() {
+  for (int slept = 0; slept < cfg_.bg_ms && !stop_.load(); slept += 50)
+    std::this_thread::sleep_for(std::chrono::milliseconds(50));
+}
+
+int LeaderService::latest_version(const std::string& f) const {
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = dir_.find(f);
+  int v = 0;
+  if (it == dir_.end()) return 0;
+  for (const auto& r : it->second)
+    if (!r.second.empty()) v = std::max(v, *r.second.rbegin());
+  return v;
+}
+
+bool LeaderService::copy_to(const Id& src, const std::string& src_spec, const Id& dest, const std::string& dest_spec) {
+  try {
+    Writer w;
+    w.str(src.host()).i32(member_port(src.port())).str(src_spec).str(dest_spec);
+    const std::string resp =
+        RpcClient::shared().call(dest.host(), member_port(dest.port()), M_FETCH, w.data(), 3600 * 1000);
+    Reader r(resp);
+    const bool ok = r.boolean();
+    DMLC_LOG_INFO("copy " << src.address << ":" << src_spec << " -> " << dest.address << ":" << dest_spec << ": "
+                          << (ok ? "ok" : "failed"));
+    return ok;
+  } catch (const std::exception& e) {
+    DMLC_LOG_WARN("copy " << src.address << ":" << src_spec << " -> " << dest.address << ":" << dest_spec
+                          << ": " << e.what());
+    return false;
+  }
+}
+
+std::set<Id> LeaderService::put_version(const Id* src_id, const std::string* src_spec, const std::string& filename,
+                                        int version) {
+  if (version == 0) return {};
+  const std::set<Id> active = ms_->active_ids();
+  if (active.empty()) return {};
+  std::set<Id> current;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = dir_.find(filename);
+    if (it != dir_.end())
+      for (const auto& r : it->second)
+        if (active.count(r.first) && r.second.count(version)) current.insert(r.first);
+  }
+  if ((int)current.size() >= cfg_.replication) return current;
+  Id sid;
+  std::string sspec;
+  if (src_id) {
+    sid = *src_id;
+    sspec = *src_spec;
+  } else if (!current.empty()) {
+    sid = *current.begin();
+    sspec = "storage:" + storage_filename(filename, version);
+  } else {
+    DMLC_LOG_WARN("put_version: no source and no live replica of " << filename << " v" << version
+                                                                   << "; the file may be lost");
+    return current;
+  }
+  std::vector<Id> candidates;
+  for (const auto& id : active)
+    if (!current.count(id)) candidates.push_back(id);
+  if (candidates.empty()) return current;
+  const std::set<Id> targets = choose_replicas(filename, candidates, cfg_.replication - (int)current.size());
+  const std::string dest_spec = "storage:" + storage_filename(filename, version);
+  std::mutex rmu;
+  std::set<Id> received;
+  std::vector<std::thread> ts;
+  for (const Id& d : targets) {
+    ts.emplace_back([&, d] {
+      if (!copy_to(sid, sspec, d, dest_spec)) return;
+      try {
+        Writer w;
+        w.str(filename).i32(version);
+        RpcClient::shared().call(d.host(), member_port(d.port()), M_RECEIVE, w.data(), 10000);
+        std::lock_guard<std::mutex> g(rmu);
+        received.insert(d);
+      } catch (const std::exception& e) {
+        DMLC_LOG_WARN("put_version: receive on " << d.address << " failed: " << e.what());
+      }
+    });
+  }
+  for (auto& t : ts) t.join();
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    auto& m = dir_[filename];
+    for (const auto& id : received) m[id].insert(version);
+  }
+  std::set<Id> all = current;
+  all.insert(received.begin(), received.end());
+  return all;
+}
+
+std::set<Id> LeaderService::put(const Id& src, const std::string& src_path, const std::string& filename) {
+  const int version = latest_version(filename) + 1;
+  return put_version(&src, &src_path, filename, version);
+}
+
+std::optional<Id> LeaderService::get_version(const std::string& filename, int version, const Id& dest,
+                                             const std::string& dest_spec) {
+  if (version == 0) return std::nullopt;
+  std::vector<Id> srcs;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = dir_.find(filename);
+    if (it != dir_.end())
+      for (const auto& r : it->second)
+        if (r.second.count(version)) srcs.push_back(r.first);
+  }
+  for (const auto& s : srcs)
+    if (copy_to(s, "storage:" + storage_filename(filename, version), dest, dest_spec)) return s;
+  return std::nullopt;
+}
+
+int LeaderService::get(const std::string& filename, const Id& dest, const std::string& dest_path) {
+  const int v = latest_version(filename);
+  return get_version(filename, v, dest, dest_path) ? v : 0;
+}
+
+std::set<int> LeaderService::get_versions(const std::string& filename, int count, const Id& dest,
+                                          const std::string& dest_path) {
+  const int latest = latest_version(filename);
+  std::set<int> out;
+  if (latest == 0 || count <= 0) return out;
+  std::mutex omu;
+  std::vector<std::thread> ts;
+  for (int v = latest; v >= 1 && v > latest - count; --v) {
+    ts.emplace_back([&, v] {
+      if (get_version(filename, v, dest, versioned_sibling(dest_path, v))) {
+        std::lock_guard<std::mutex> g(omu);
+        out.insert(v);
+      }
+    });
+  }
+  for (auto& t : ts) t.join();
+  return out;
+}
+
+void LeaderService::del(const std::string& filename) {
+  std::set<Id> holders;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = dir_.find(filename);
+    if (it != dir_.end())
+      for (const auto& r : it->second) holders.insert(r.first);
+    dir_.erase(filename);
+  }
+  for (const auto& id : holders) {  // also drop the replica files (reference kept them)
+    try {
+      Writer w;
+      w.str(filename);
+      RpcClient::shared().call(id.host(), member_port(id.port()), M_DELETE_FILE, w.data(), 5000);
+    } catch (const std::exception&) {
+    }
+  }
+}
+
+std::vector<std::pair<Id, std::vector<int>>> LeaderService::ls(const std::string& filename) {
+  const std::set<Id> active = ms_->active_ids();
+  std::vector<std::pair<Id, std::vector<int>>> out;
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = dir_.find(filename);
+  if (it == dir_.end()) return out;
+  for (const auto& r : it->second)
+    if (active.count(r.first)) out.emplace_back(r.first, std::vector<int>(r.second.begin(), r.second.end()));
+  return out;
+}
+
+void LeaderService::train(const std::string& filename, const std::string& model_name) {
+  const int v = latest_version(filename);
+  if (v == 0) throw std::runtime_error("file not found: " + filename);
+  const std::string spec = "models:" + model_name + ".ot";
+  std::vector<std::thread> ts;
+  std::mutex emu;
+  std::vector<std::string> errors;
+  for (const Id& id : ms_->active_ids()) {
+    ts.emplace_back([&, id] {
+      std::string err;
+      if (!get_version(filename, v, id, spec)) {
+        err = id.address + ": copy failed";
+      } else {
+        try {
+          Writer w;
+          w.str(model_name).str(spec);
+          Reader r(RpcClient::shared().call(id.host(), member_port(id.port()), M_LOAD_MODEL, w.data(), 600000));
+          if (!r.boolean()) err = id.address + ": " + r.str();
+        } catch (const std::exception& e) {
+          err = id.address + ": " + e.what();
+        }
+      }
+      if (!err.empty()) {
+        std::lock_guard<std::mutex> g(emu);
+        errors.push_back(err);
+      }
+    });
+  }
+  for (auto& t : ts) t.join();
+  if (!errors.empty()) {
+    std::string s;
+    for (const auto& e : errors) s += (s.empty() ? "" : "; ") + e;
+    throw std::runtime_error(s);
+  }
+}
+
+void LeaderService::predict() {
+  std::lock_guard<std::mutex> g(runners_mu_);
+  for (size_t j = 0; j < jobs_.size(); ++j) {
+    {
+      std::lock_guard<std::mutex> g2(mu_);
+      if (running_[j]) continue;
+      running_[j] = true;
+    }
+    runners_.emplace_back([this, j] { run_job(j); });
+  }
+}
+
+std::vector<Job> LeaderService::jobs() const {
+  std::lock_guard<std::mutex> g(mu_);
+  return jobs_;
+}
+
+void LeaderService::run_job(size_t j) {
+  std::string model;
+  size_t idx;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    model = jobs_[j].model_name;
+    idx = (size_t)jobs_[j].finished;  // resume point (src/services.rs:410-411)
+  }
+  const auto& L = labels_.entries;
+  const size_t limit = cfg_.job_limit > 0 ? std::min(L.size(), (size_t)cfg_.job_limit) : L.size();
+  auto next_tick = std::chrono::steady_clock::now();
+  while (idx < limit && !stop_.load()) {
+    next_tick += std::chrono::milliseconds(cfg_.query_interval_ms);
+    std::this_thread::sleep_until(next_tick);
+    if (!is_leader()) break;  // leadership moved: the new leader resumes
+    std::vector<Id> pool;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      pool = jobs_[j].assigned;
+    }
+    if (pool.empty()) {
+      auto a = ms_->active_ids();
+      pool.assign(a.begin(), a.end());
+    }
+    if (pool.empty()) continue;
+    Id target;
+    {
+      std::lock_guard<std::mutex> g(rng_mu_);
+      target = pool[std::uniform_int_distribution<size_t>(0, pool.size() - 1)(rng_)];
+    }
+    while (inflight_.load() >= cfg_.max_inflight && !stop_.load())
+      std::this_thread::sleep_for(std::chrono::microseconds(200));
+    const size_t n = std::min((size_t)cfg_.query_batch, limit - idx);
+    const size_t first = idx;
+    idx += n;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      if (jobs_[j].started_us == 0) jobs_[j].started_us = wall_us();
+    }
+    inflight_++;
+    std::thread([this, j, model, target, first, n] {
+      const auto& L = labels_.entries;
+      Writer w;
+      w.str(model).u32((uint32_t)n);
+      for (size_t i = 0; i < n; ++i) w.str(L[first + i].first);
+      const int64_t t0 = steady_us();
+      // A query whose member died is retried on another live member (the
+      // reference dropped it); latency is end to end, retries included.
+      Id tgt = target;
+      std::string resp;
+      bool sent = false;
+      for (int attempt = 0; attempt < 4 && !stop_.load(); ++attempt) {
+        try {
+          resp = RpcClient::shared().call(tgt.host(), member_port(tgt.port()), M_PREDICT, w.data(), 120000);
+          sent = true;
+          break;
+        } catch (const std::exception& e) {
+          DMLC_LOG_WARN("predict " << model << " on " << tgt.address << " failed: " << e.what());
+          std::this_thread::sleep_for(std::chrono::milliseconds(std::min(cfg_.bg_ms, 1000)));
+          auto act = ms_->active_ids();
+          act.erase(tgt);
+          if (act.empty()) break;
+          std::lock_guard<std::mutex> g(rng_mu_);
+          auto it = act.begin();
+          std::advance(it, std::uniform_int_distribution<size_t>(0, act.size() - 1)(rng_));
+          tgt = *it;
+        }
+      }
+      try {
+        if (!sent) throw std::runtime_error("no live member answered");
+        const int64_t dur = steady_us() - t0;
+        Reader r(resp);
+        if (r.boolean()) {
+          const uint32_t m = r.u32();
+          std::vector<std::string> lines;
+          {
+            std::lock_guard<std::mutex> g(mu_);
+            if (jobs_[j].first_done_us == 0) jobs_[j].first_done_us = wall_us();
+            for (uint32_t i = 0; i < m && i < n; ++i) {
+              const double p = r.f64();
+              const std::string label = r.str();
+              const std::string& truth = L[first + i].second;
+              const bool ok = label == truth;
+              jobs_[j].add_result(ok, dur);
+              if (cfg_.print_predictions) {
+                char buf[64];
+                snprintf(buf, sizeof(buf), " (%.2f%%)", p * 100.0);
+                lines.push_back(model + " - " + L[first + i].first + ": " + label + buf +
+                                (ok ? "" : " (should be " + truth + ")"));
+              }
+            }
+          }
+          for (const auto& s : lines) out_line(s);
+        }
+      } catch (const std::exception& e) {
+        DMLC_LOG_WARN("predict " << model << " on " << target.address << " failed: " << e.what());
+      }
+      inflight_--;
+    }).detach();
+  }
+  std::lock_guard<std::mutex> g(mu_);
+  running_[j] = false;
+}
+
+void LeaderService::rereplicate_loop() {
+  while (!stop_.load()) {
+    sleep_bg();
+    if (stop_.load()) break;
+    if (!is_leader()) continue;
+    std::vector<std::string> files;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      for (const auto& kv : dir_) files.push_back(kv.first);
+    }
+    for (const auto& f : files) put_version(nullptr, nullptr, f, latest_version(f));
+  }
+}
+
+void LeaderService::assign_loop() {
+  while (!stop_.load()) {
+    sleep_bg();
+    if (stop_.load()) break;
+    const std::vector<Id> active = ms_->active_sorted();
+    std::lock_guard<std::mutex> g(mu_);
+    const size_t J = jobs_.size(), n = active.size();
+    for (size_t j = 0; j < J; ++j) {
+      const size_t b = j * n / J, e = (j + 1) * n / J;
+      jobs_[j].assigned.assign(active.begin() + b, active.begin() + e);
+    }
+  }
+}
+
+void LeaderService::succession_loop() {
+  std::string last = member_->leader_address();
+  while (!stop_.load()) {
+    sleep_bg();
+    if (stop_.load()) break;
+    const std::string leader = member_->leader_address();
+    if (last != self_ && leader == self_) {
+      bool resume;
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        resume = !jobs_.empty() && !jobs_[0].durations_us.empty();
+      }
+      DMLC_LOG_WARN("became leader" << (resume ? "; resuming jobs" : ""));
+      if (resume) predict();
+    } else if (leader != self_) {
+      try {  // standby: copy job progress AND the SDFS directory from the leader
+        const std::string resp =
+            RpcClient::shared().call(host_of(leader), leader_port(port_of(leader)), L_STATE, "", 5000);
+        Reader r(resp);
+        std::vector<Job> js;
+        const uint32_t nj = r.u32();
+        for (uint32_t i = 0; i < nj; ++i) js.push_back(read_job(r));
+        Directory d = read_directory(r);
+        std::lock_guard<std::mutex> g(mu_);
+        if (js.size() == jobs_.size()) jobs_ = js;
+        dir_ = std::move(d);
+      } catch (const std::exception&) {
+      }
+    }
+    last = leader;
+  }
+}
+
+void LeaderService::register_handlers() {
+  server_->handle(L_ALIVE, [](Reader&) {
+    Writer w;
+    w.boolean(true);
+    return w.take();
+  });
+  server_->handle(L_PUT, [this](Reader& r) {
+    const Id src = read_id(r);
+    const std::string path = r.str(), fname = r.str();
+    const auto ids = put(src, path, fname);
+    Writer w;
+    w.u32((uint32_t)ids.size());
+    for (const auto& id : ids) write_id(w, id);
+    return w.take();
+  });
+  server_->handle(L_GET, [this](Reader& r) {
+    const std::string fname = r.str();
+    const Id dest = read_id(r);
+    const std::string path = r.str();
+    const int v = get(fname, dest, path);
+    Writer w;
+    w.boolean(v > 0).i32(v);
+    return w.take();
+  });
+  server_->handle(L_GET_VERSIONS, [this](Reader& r) {
+    const std::string fname = r.str();
+    const int count = r.i32();
+    const Id dest = read_id(r);
+    const std::string path = r.str();
+    const auto vs = get_versions(fname, count, dest, path);
+    Writer w;
+    w.u32((uint32_t)vs.size());
+    for (int v : vs) w.i32(v);
+    return w.take();
+  });
+  server_->handle(L_DELETE, [this](Reader& r) {
+    del(r.str());
+    return std::string();
+  });
+  server_->handle(L_LS, [this](Reader& r) {
+    const auto res = ls(r.str());
+    Writer w;
+    w.u32((uint32_t)res.size());
+    for (const auto& e : res) {
+      write_id(w, e.first);
+      w.u32((uint32_t)e.second.size());
+      for (int v : e.second) w.i32(v);
+    }
+    return w.take();
+  });
+  server_->handle(L_TRAIN, [this](Reader& r) {
+    const std::string fname = r.str(), model = r.str();
+    Writer w;
+    try {
+      train(fname, model);
+      w.boolean(true).str("");
+    } catch (const std::exception& e) {
+      w.boolean(false).str(e.what());
+    }
+    return w.take();
+  });
+  server_->handle(L_PREDICT, [this](Reader&) {
+    predict();
+    return std::string();
+  });
+  server_->handle(L_JOBS, [this](Reader&) {
+    const auto js = jobs();
+    Writer w;
+    w.u32((uint32_t)js.size());
+    for (const auto& j : js) write_job(w, j);
+    return w.take();
+  });
+  server_->handle(L_STATE, [this](Reader&) {
+    Writer w;
+    std::lock_guard<std::mutex> g(mu_);
+    w.u32((uint32_t)jobs_.size());
+    for (const auto& j : jobs_) write_job(w, j);
+    write_directory(w, dir_);
+    return w.take();
+  });
+}
+
+}  // namespace ctl
+}  // namespace dmlc

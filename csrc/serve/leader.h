@@ -1,0 +1,99 @@
+// Leader service: SDFS metadata + replication, inference job coordinator,
+// fair-share scheduler, fail-over with job resume.
+//
+// Reference: tarpc `Leader` (get, get_versions, put, delete, ls, train,
+// predict, jobs, alive; src/services.rs:38-160), LeaderState::new background
+// loops (re-replication, job assignment, succession/job-state copy;
+// src/services.rs:163-242), put_version/get_version (:283-405) and run_job
+// (:407-433).
+// Differences: bytes move member-to-member over RPC instead
+// of scp; standbys copy the SDFS directory along with the jobs (#5); delete
+// removes replica files (#6); train hot-swaps weights on every member (#7);
+// a job with no assigned member borrows all active members instead of
+// silently skipping queries; queries can be batched (query_batch) and the
+// tick is configurable (reference: 1 query / 0.5 s / job).
+#pragma once
+#include <atomic>
+#include <condition_variable>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <optional>
+#include <random>
+#include <set>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../control/member.h"
+#include "../control/membership.h"
+#include "../control/rpc.h"
+#include "../control/sdfs.h"
+#include "job.h"
+
+namespace dmlc {
+namespace ctl {
+
+struct LeaderConfig {
+  std::string bind_host = "0.0.0.0";
+  int replication = 4;
+  int bg_ms = 3000;
+  int query_interval_ms = 500;
+  int query_batch = 1;
+  int max_inflight = 32;
+  int job_limit = 0;  // queries per job (0 = every label, as the reference)
+  bool print_predictions = true;
+  std::vector<std::string> job_models = {"resnet18", "alexnet"};
+};
+
+class LeaderService {
+ public:
+  LeaderService(LeaderConfig cfg, MembershipService* ms, MemberService* member, Labels labels);
+  ~LeaderService();
+  void start(int base_port);
+  void stop();
+
+  bool is_leader() const;
+  // RPC bodies (also used locally)
+  std::set<Id> put(const Id& src, const std::string& src_path, const std::string& filename);
+  int get(const std::string& filename, const Id& dest, const std::string& dest_path);
+  std::set<int> get_versions(const std::string& filename, int count, const Id& dest, const std::string& dest_path);
+  void del(const std::string& filename);
+  std::vector<std::pair<Id, std::vector<int>>> ls(const std::string& filename);
+  void train(const std::string& filename, const std::string& model_name);
+  void predict();
+  std::vector<Job> jobs() const;
+
+ private:
+  void register_handlers();
+  int latest_version(const std::string& f) const;
+  std::set<Id> put_version(const Id* src_id, const std::string* src_spec, const std::string& filename, int version);
+  bool copy_to(const Id& src, const std::string& src_spec, const Id& dest, const std::string& dest_spec);
+  std::optional<Id> get_version(const std::string& filename, int version, const Id& dest, const std::string& dest_spec);
+  void run_job(size_t j);
+  void rereplicate_loop();
+  void assign_loop();
+  void succession_loop();
+  void sleep_bg();
+
+  LeaderConfig cfg_;
+  MembershipService* ms_;
+  MemberService* member_;
+  Labels labels_;
+  std::unique_ptr<RpcServer> server_;
+  std::string self_;  // base address
+  mutable std::mutex mu_;
+  Directory dir_;
+  std::vector<Job> jobs_;
+  std::vector<bool> running_;
+  std::atomic<bool> stop_{false};
+  std::vector<std::thread> loops_;
+  std::mutex runners_mu_;
+  std::vector<std::thread> runners_;
+  std::atomic<int> inflight_{0};
+  std::mutex rng_mu_;
+  std::mt19937_64 rng_{std::random_device{}()};
+};
+
+}  // namespace ctl
+}  // namespace dmlc

@@ -105,6 +105,7 @@ def build(jobs: int = 8, verbose: bool = False, node: bool = True) -> None:
     py_srcs = {
         os.path.join(CSRC, "bindings", "py_module.cpp"): [f"-I{_pybind_include()}", f"-I{pyinc}"],
         os.path.join(CSRC, "runtime", "ot_io.cpp"): torch_flags,
+        os.path.join(CSRC, "runtime", "jpeg.cpp"): ["-O3"],
     }
     py_objs = []
     for s, extra in py_srcs.items():
@@ -140,9 +141,9 @@ def build(jobs: int = 8, verbose: bool = False, node: bool = True) -> None:
 
     if node and node_objs:
         exe = os.path.join(BIN, "dmlc-node")
-        ot_obj = os.path.join(OBJ, "runtime_ot_io.cpp.o")
-        if _stale(exe, node_objs + [libgpu, ot_obj], 0):
-            _run(["g++", "-pthread", *node_objs, ot_obj, "-o", exe,
+        rt_objs = [os.path.join(OBJ, "runtime_ot_io.cpp.o"), os.path.join(OBJ, "runtime_jpeg.cpp.o")]
+        if _stale(exe, node_objs + [libgpu] + rt_objs, 0):
+            _run(["g++", "-pthread", *node_objs, *rt_objs, "-o", exe,
                   f"-L{PKG}", "-ldmlc_gpu", f"-Wl,-rpath,{PKG}",
                   f"-L{tlib}", "-ltorch_cpu", "-lc10", "-lamdhip64", f"-Wl,-rpath,{tlib}"], verbose)
 
