@@ -1,0 +1,66 @@
+"""dmlc-node with the GPU executor (hand-written HIP engine) on a real GPU:
+classification agrees with the CPU (libtorch) executor, and a two-node
+cluster serves predict jobs from the GPU."""
+import os
+import re
+import subprocess
+import time
+
+import pytest
+
+from dmlc.serve.cluster import NODE_BIN, LocalCluster
+from dmlc.utils.dataset import make_synthetic_dataset, synthetic_labels, write_labels
+from dmlc.utils.ot import write_random_checkpoint
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def env(tmp_path_factory):
+    root = tmp_path_factory.mktemp("gpunode")
+    labels = synthetic_labels(1000)
+    lab = write_labels(str(root / "synset_words.txt"), labels)
+    ds = make_synthetic_dataset(str(root / "train"), labels[:16], size=(300, 400))
+    ckpt = write_random_checkpoint("resnet18", str(root / "resnet18.ot"), seed=4)
+    return {"root": root, "labels": lab, "dataset": ds, "ckpt": ckpt, "entries": labels}
+
+
+def _classify(env, executor, images):
+    r = subprocess.run([NODE_BIN, "classify", "--model", "resnet18", "--weights", env["ckpt"], "--labels",
+                        env["labels"], "--image", ",".join(images), "--executor", executor],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return [int(x) for x in re.findall(r"class=(\d+)", r.stdout)], r.stdout
+
+
+def test_gpu_executor_agrees_with_cpu(gpu, env):
+    imgs = []
+    for wnid, _ in env["entries"][:16]:
+        d = os.path.join(env["dataset"], wnid)
+        imgs.append(os.path.join(d, sorted(os.listdir(d))[0]))
+    g, out = _classify(env, "gpu", imgs)
+    c, _ = _classify(env, "cpu", imgs)
+    assert "[gpu:0]" in out
+    assert len(g) == len(c) == 16
+    agree = sum(a == b for a, b in zip(g, c))
+    assert agree >= 14, (g, c)  # bf16 vs fp32: only near-ties may flip
+
+
+def test_gpu_cluster_predict(gpu, env, tmp_path):
+    cl = LocalCluster(2, 19700, str(tmp_path / "c"), env["labels"], n_leaders=1, executor="gpu",
+                      dataset=env["dataset"], models=f"resnet18={env['ckpt']}",
+                      extra=["--jobs", "resnet18", "--job-limit", "16", "--query-interval-ms", "20",
+                             "--query-batch", "4", "--quiet-predictions"])
+    with cl:
+        n = cl.nodes
+        assert "executor gpu:0" in n[0].cmd("info")
+        n[1].cmd("predict")
+        deadline = time.time() + 60
+        done = 0
+        while time.time() < deadline:
+            m = re.search(r"Accuracy: \d+/(\d+)", n[1].cmd("jobs"))
+            done = int(m.group(1)) if m else 0
+            if done >= 16:
+                break
+            time.sleep(0.5)
+        assert done == 16
