@@ -72,85 +72,37 @@ def main():
     if distributed:
         dist.init_process_group("nccl", device_id=dev)
 
+    from dmlc.models import build, state_dict_f32
+    from dmlc.parallel import DPInference, broadcast_state_dict
     from dmlc.runtime import InferenceEngine
 
     B = args.batch
-    eng = InferenceEngine(args.model, device=local_rank, max_batch=B, seed=0)
+    # Rank 0 owns the weights (random init: the reference's .ot files are LFS
+    # stubs) and broadcasts them over RCCL, like `train` distributing a model.
+    sd = state_dict_f32(build(args.model, seed=0)) if rank == 0 else None
+    sd = broadcast_state_dict(sd, 0, dev) if distributed else sd
+    eng = InferenceEngine(args.model, sd, device=local_rank, max_batch=B)
     use_graph = not args.no_graph
 
-    # Staged input pool on rank 0 (two global batches, distinct synthetic images).
-    g = torch.Generator(device=dev).manual_seed(1234)
-    slots = 2
+    # Staged input pool (two global batches of distinct synthetic images) in
+    # the coordinator's HBM, or every rank's own shard in local mode.
+    g = torch.Generator(device=dev).manual_seed(1234 + rank)
+    pool = None
     if rank == 0 or args.input_mode == "local":
-        n_pool = slots * (B * world if args.input_mode == "scatter" else B)
+        n_pool = 2 * (B * world if args.input_mode == "scatter" else B)
         pool = torch.randint(0, 256, (n_pool, 224, 224, 3), dtype=torch.uint8, device=dev, generator=g)
-    else:
-        pool = None
-    inbuf = [torch.empty(B, 224, 224, 3, dtype=torch.uint8, device=dev) for _ in range(slots)]
-    outbuf = [torch.empty(2, B, dtype=torch.int32, device=dev) for _ in range(slots)]
-    gathered = [[torch.empty(2, B, dtype=torch.int32, device=dev) for _ in range(world)] if rank == 0 else None
-                for _ in range(slots)]
 
-    def shard_list(step):
-        s = step % slots
-        base = s * B * world
-        return [pool[base + r * B: base + (r + 1) * B] for r in range(world)]
-
-    def issue_input(step):
-        s = step % slots
-        if args.input_mode == "local":
-            return None
-        if not distributed:
-            return None
-        return dist.scatter(inbuf[s], shard_list(step) if rank == 0 else None, src=0, async_op=True)
-
-    def compute(step):
-        s = step % slots
-        # single GPU: the coordinator's own shard is already in its HBM
-        src = pool[s * B:(s + 1) * B] if (args.input_mode == "local" or not distributed) else inbuf[s]
-        ob = outbuf[s]
-        eng.predict(src, use_graph=use_graph, out=(ob[0], ob[1].view(torch.float32)))
-        if distributed:
-            return dist.gather(ob, gathered[s] if rank == 0 else None, dst=0, async_op=True)
-        return None
-
-    ev_start = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + args.warmup)]
-    ev_end = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + args.warmup)]
-
-    transfer = distributed and args.input_mode == "scatter"
-
-    def run(first, n):
-        """Pipelined loop: input of step i+1 is in flight during compute of step i."""
-        stream = torch.cuda.current_stream()
-        ev_start[first].record(stream)
-        h = issue_input(first)
-        pending = []
-        for i in range(first, first + n):
-            if h is not None:
-                h.wait()
-            if i + 1 < first + n and transfer:
-                # the transfer of batch i+1 can start once compute(i-1) is done
-                ev_start[i + 1].record(stream)
-                h = issue_input(i + 1)
-            else:
-                h = None
-            gh = compute(i)
-            if not transfer and i + 1 < first + n:
-                ev_start[i + 1].record(stream)  # no transfer: batch i+1 starts when compute(i) ends
-            if gh is not None:
-                gh.wait()
-            ev_end[i].record(stream)
-            pending.append(gh)
-        return pending
+    dp = DPInference(lambda imgs, out: eng.predict(imgs, use_graph=use_graph, out=out), B, dev,
+                     input_mode=args.input_mode)
 
     # Warmup (also captures the hipGraphs and warms RCCL channels).
-    run(0, args.warmup)
+    dp.run(pool, 0, args.warmup)
     torch.cuda.synchronize()
     if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    run(args.warmup, args.steps)
+    dp.run(pool, args.warmup, args.steps)
     torch.cuda.synchronize()
     if distributed:
         dist.barrier()
@@ -161,21 +113,21 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
 
-    batch_lat = [ev_start[i].elapsed_time(ev_end[i]) for i in range(args.warmup, args.warmup + args.steps)]
+    batch_lat = [dp.latency_ms(i) for i in range(args.warmup, args.warmup + args.steps)]
 
-    # Sanity: outputs are valid class ids / probabilities.
-    ob = outbuf[(args.warmup + args.steps - 1) % slots]
-    ids = ob[0].cpu()
-    probs = ob[1].view(torch.float32).cpu()
-    assert int(ids.min()) >= 0 and int(ids.max()) < 1000, "bad class ids"
-    assert float(probs.min()) > 0 and float(probs.max()) <= 1.0001, "bad probabilities"
+    # Sanity: the coordinator's gathered outputs are valid class ids / probabilities.
+    if rank == 0:
+        ids, probs = dp.results(args.warmup + args.steps - 1)
+        assert ids.numel() == B * world
+        assert int(ids.min()) >= 0 and int(ids.max()) < 1000, "bad class ids"
+        assert float(probs.min()) > 0 and float(probs.max()) <= 1.0001, "bad probabilities"
 
     # Batch-1 query latency (hipGraph replay of preprocess+forward+top-1 for
     # one image, host-timed end to end including the D2H of the answer).
     qlat = []
     if rank == 0 and args.latency_queries > 0:
-        q_eng = InferenceEngine(args.model, device=local_rank, max_batch=1, seed=0)
-        qimg = (pool[:1] if pool is not None else inbuf[0][:1]).contiguous()
+        q_eng = InferenceEngine(args.model, sd, device=local_rank, max_batch=1)
+        qimg = pool[:1].contiguous()
         qout = (torch.empty(1, dtype=torch.int32, device=dev), torch.empty(1, dtype=torch.float32, device=dev))
         for i in range(args.latency_queries + 20):
             torch.cuda.synchronize()
@@ -187,8 +139,7 @@ def main():
 
     ops_profile = None
     if rank == 0 and args.profile_ops:
-        src = pool[:B] if pool is not None else inbuf[0]
-        ops_profile = eng.profile(src)
+        ops_profile = eng.profile(pool[:B].contiguous())
 
     if rank == 0:
         n_img = B * world * args.steps

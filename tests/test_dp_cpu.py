@@ -1,0 +1,84 @@
+"""Data-parallel inference coordinator (scatter u8 shards -> per-rank
+forward -> gather top-1) with world_size 2 on the gloo backend (CPU). The
+same code path runs over RCCL on GPUs in bench.py."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from dmlc.models import build, state_dict_f32
+from dmlc.parallel import DPInference, broadcast_state_dict
+
+MEAN = torch.tensor([0.485, 0.456, 0.406]).view(1, 3, 1, 1)
+STD = torch.tensor([0.229, 0.224, 0.225]).view(1, 3, 1, 1)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _predict_fn(model):
+    def f(imgs, out):
+        x = (imgs.permute(0, 3, 1, 2).float() / 255 - MEAN) / STD
+        with torch.no_grad():
+            p = torch.softmax(model(x), -1)
+        v, i = p.max(-1)
+        out[0].copy_(i.int())
+        out[1].copy_(v)
+    return f
+
+
+def _worker(rank, world, port, B, steps, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(2)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        sd = state_dict_f32(build("resnet18", seed=3)) if rank == 0 else None
+        sd = broadcast_state_dict(sd, 0, torch.device("cpu"))
+        model = build("resnet18", seed=None)
+        model.load_state_dict(sd, strict=False)
+        model.eval()
+        dev = torch.device("cpu")
+        pool = None
+        if rank == 0:
+            g = torch.Generator().manual_seed(7)
+            pool = torch.randint(0, 256, (2 * B * world, 64, 64, 3), generator=g, dtype=torch.uint8)
+        dp = DPInference(_predict_fn(model), B, dev, image_shape=(64, 64, 3))
+        dp.run(pool, 0, steps)
+        if rank == 0:
+            res = [dp.results(s) for s in range(steps - 2, steps)]
+            lat = [dp.latency_ms(s) for s in range(steps)]
+            q.put((res, [dp.shards(pool, s) for s in range(steps - 2, steps)], lat))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_scatter_gather_gloo():
+    world, B, steps = 2, 3, 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, B, steps, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res, shards, lat = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    model = build("resnet18", seed=3)
+    f = _predict_fn(model)
+    for (idx, prob), sh in zip(res, shards):
+        imgs = torch.cat(sh)
+        exp = (torch.empty(world * B, dtype=torch.int32), torch.empty(world * B))
+        f(imgs, exp)
+        assert torch.equal(idx, exp[0])
+        assert torch.allclose(prob, exp[1], rtol=1e-5, atol=1e-6)
+    assert all(x > 0 for x in lat)

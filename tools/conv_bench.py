@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--tiles", default="-1,0,1,2,3,4,5,6")
     ap.add_argument("--only", default="")
+    ap.add_argument("--ref", action="store_true", help="also time hipBLASLt GEMM and MIOpen conv on each shape")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     B = a.batch
@@ -72,6 +73,29 @@ def main():
                 row.append(f"tile{t}={ms*1e3:7.1f}us {flops/ms/1e9:6.0f}TF")
             except Exception as e:  # noqa: BLE001
                 row.append(f"tile{t}=ERR({e})")
+        if a.ref:
+            # vendor references on the same shape: plain GEMM (hipBLASLt via
+            # torch.mm) and MIOpen conv (bf16, channels_last)
+            M, K = B * Ho * Ho, cin_real * k * k
+            A = torch.randn(M, K, device=dev).bfloat16()
+            Bm = torch.randn(K, Cout, device=dev).bfloat16()
+            xc = torch.randn(B, cin_real, H - (2 * p if pair else 0), W - (2 * p if pair else 0),
+                             device=dev).bfloat16().to(memory_format=torch.channels_last)
+            wc = torch.randn(Cout, cin_real, k, k, device=dev).bfloat16().to(memory_format=torch.channels_last)
+            for tag, f in (("gemm", lambda: torch.mm(A, Bm)),
+                           ("miopen", lambda: torch.nn.functional.conv2d(xc, wc, None, s, p))):
+                f()
+                torch.cuda.synchronize()
+                ts = []
+                for _ in range(a.iters):
+                    e0, e1 = torch.cuda.Event(True), torch.cuda.Event(True)
+                    e0.record()
+                    f()
+                    e1.record()
+                    e1.synchronize()
+                    ts.append(e0.elapsed_time(e1))
+                ms = statistics.median(ts)
+                row.append(f"{tag}={ms*1e3:7.1f}us {flops/ms/1e9:6.0f}TF")
         print(f"{name:6s} M={B*Ho*Ho:8d} N={Cout:4d} K={cin_real*k*k:5d}  " + "  ".join(row), flush=True)
 
 
