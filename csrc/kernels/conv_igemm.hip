@@ -53,10 +53,6 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + local;
 }
 
-// __launch_bounds__(256, 2): 2 waves/SIMD caps the unified register budget
-// at 256, which keeps the 64 accumulator registers in arch VGPRs. Without
-// it hipcc splits into AGPRs and shuffles ~100 v_accvgpr_* per K-tile
-// (measured: 4.4 VALU per MFMA, 40% of wave cycles in waits).
 // s_waitcnt vmcnt(N) with a compile-time N (the field is an immediate).
 template <int N>
 __device__ __forceinline__ void vm_wait() {
@@ -77,6 +73,10 @@ __device__ __forceinline__ void wait_tiles(int remaining) {
   vm_wait<0>();
 }
 
+// __launch_bounds__(256, 2): 2 waves/SIMD caps the unified register budget
+// at 256, which keeps the 64 accumulator registers in arch VGPRs. Without
+// it hipcc splits into AGPRs and shuffles ~100 v_accvgpr_* per K-tile
+// (measured: 4.4 VALU per MFMA, 40% of wave cycles in waits).
 template <int BM, int BN, int WM, int WN, int NS, bool PAIR>
 __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a, int kt_per_split, int k_tiles) {
   constexpr int BK = 64;
@@ -338,6 +338,9 @@ struct TileCfg {
 // Tile configurations (4 waves each, 64x64 per wave; ns = LDS stages):
 //   0: 128x128 ns2   1: 256x64 ns2   2: 64x256 ns2
 //   3: 128x128 ns3   4: 256x64 ns3   5: 64x256 ns3   6: 128x128 ns4
+// (A register double-buffered fragment schedule on top of ns2 measured
+// within +-3% of these and was dropped; ns3/ns4 lose 30% to the halved
+// occupancy: profiles/r1_conv_bench_stages.log.)
 constexpr int kNumTiles = 7;
 constexpr TileCfg kTiles[kNumTiles] = {{128, 128, 2}, {256, 64, 2}, {64, 256, 2}, {128, 128, 3},
                                        {256, 64, 3},  {64, 256, 3}, {128, 128, 4}};
