@@ -55,19 +55,20 @@ PYBIND11_MODULE(_C, m) {
   m.doc() = "dmlc native runtime: CDNA4 HIP kernels, inference engine, .ot I/O";
 
   // ---------------------------------------------------------------- ops
-  m.def("conv_kpad", &conv_kpad, py::arg("Cin"), py::arg("KH"), py::arg("KW"), py::arg("pair_stem") = false);
+  m.def("conv_kpad", &conv_kpad, py::arg("Cin"), py::arg("KH"), py::arg("KW"), py::arg("stem") = false);
+  m.def("stem_row_width", &stem_row_width);
   m.def("conv_npad", &conv_npad);
   m.def("conv_out_dim", &conv_out_dim);
   m.def(
       "conv2d",
       [](uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t res, uintptr_t y, int B, int H, int W,
          int Cin, int KH, int KW, int stride, int pad, int N, int Npad, int Kpad, int ldo, bool relu,
-         bool out_f32, int split_k, uintptr_t ws, int tile, uintptr_t zero, bool pair_stem,
+         bool out_f32, int split_k, uintptr_t ws, int tile, uintptr_t zero, bool stem, int Ho, int Wo,
          uintptr_t stream) {
         ConvArgs a;
         a.x = P<void>(x);
         a.zero = P<void>(zero);
-        a.pair_stem = pair_stem;
+        a.stem = stem;
         a.w = P<void>(w);
         a.bias = P<float>(bias);
         a.res = P<void>(res);
@@ -80,8 +81,8 @@ PYBIND11_MODULE(_C, m) {
         a.KW = KW;
         a.stride = stride;
         a.pad = pad;
-        a.Ho = conv_out_dim(H, KH, stride, pair_stem ? 0 : pad);
-        a.Wo = conv_out_dim(W, KW, stride, pair_stem ? 0 : pad);
+        a.Ho = Ho > 0 ? Ho : conv_out_dim(H, KH, stride, pad);
+        a.Wo = Wo > 0 ? Wo : conv_out_dim(W, KW, stride, pad);
         a.N = N;
         a.Npad = Npad;
         a.Kpad = Kpad;
@@ -97,7 +98,7 @@ PYBIND11_MODULE(_C, m) {
       py::arg("H"), py::arg("W"), py::arg("Cin"), py::arg("KH"), py::arg("KW"), py::arg("stride"),
       py::arg("pad"), py::arg("N"), py::arg("Npad"), py::arg("Kpad"), py::arg("ldo"),
       py::arg("relu"), py::arg("out_f32"), py::arg("split_k"), py::arg("ws"), py::arg("tile"),
-      py::arg("zero"), py::arg("pair_stem"), py::arg("stream"));
+      py::arg("zero"), py::arg("stem"), py::arg("Ho"), py::arg("Wo"), py::arg("stream"));
   m.def("maxpool2d", [](uintptr_t x, uintptr_t y, int B, int H, int W, int C, int k, int stride,
                         int pad, uintptr_t stream) {
     maxpool2d(P<void>(x), P<void>(y), B, H, W, C, conv_out_dim(H, k, stride, pad),
@@ -110,9 +111,9 @@ PYBIND11_MODULE(_C, m) {
                                uintptr_t stream) {
     avgpool_adaptive(P<void>(x), P<void>(y), B, H, W, C, Ho, Wo, S(stream));
   });
-  m.def("preprocess_u8", [](uintptr_t x, uintptr_t y, int B, int Hin, int Win, int S_, int pad,
+  m.def("preprocess_u8", [](uintptr_t x, uintptr_t y, int B, int Hin, int Win, int S_, int pad, int Wr,
                             uintptr_t stream) {
-    preprocess_u8(P<uint8_t>(x), P<void>(y), B, Hin, Win, S_, pad, S(stream));
+    preprocess_u8(P<uint8_t>(x), P<void>(y), B, Hin, Win, S_, pad, Wr, S(stream));
   });
   m.def("softmax_top1", [](uintptr_t logits, int B, int N, int ld, uintptr_t idx, uintptr_t prob,
                            uintptr_t stream) {

@@ -23,9 +23,12 @@
 //    activation rows (m), so each lane ends with 4 consecutive output
 //    channels of one pixel -> 8-byte packed bf16 stores straight to NHWC.
 //  * Epilogue fuses folded-BN bias, residual add and ReLU.
-//  * The 3-channel stems read a "pair image" written by the preprocess
-//    kernel: zero-padded, 16 B per position = two horizontally adjacent RGB0
-//    pixels, so one 16-B chunk = 2 taps and no bounds checks are needed.
+//  * The 3-channel stems read a zero-padded packed-RGB bf16 image written by
+//    the preprocess kernel: within an input row the KW taps x 3 channels of
+//    one output pixel are contiguous, so k = kh*CPK*8 + kw*3 + c and each
+//    16-B chunk is 8 consecutive (kw, c) values of one row (CPK = ceil(3KW/8)
+//    chunks per kernel row; no bounds checks, 77% useful K for 7x7 instead
+//    of 57% with 4-channel padding).
 //  * Optional split-K writes fp32 partials that a small kernel reduces (used
 //    when the tile grid cannot fill the 256 CUs, e.g. batch-1 latency runs
 //    and the AlexNet classifier).
@@ -136,7 +139,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a, int kt_p
       if constexpr (PAIR) {
         hi0[p] = ho * a.stride;
         wi0[p] = wo * a.stride;
-        abase[p] = ((b * a.H + hi0[p]) * a.W + wi0[p]) * 8;
+        abase[p] = ((b * a.H + hi0[p]) * a.W + wi0[p]) * 3;  // packed RGB row image
       } else {
         hi0[p] = ho * a.stride - a.pad;
         wi0[p] = wo * a.stride - a.pad;
@@ -154,8 +157,8 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a, int kt_p
     const int r = wave * (BN / 4) + p * 8 + lrow;
     wboff[p] = (n0 + r) * a.Kpad + swz(r, pchunk) * 8;
   }
-  const int KWP = (a.KW + 1) >> 1;
-  const int ntap_pairs = a.KH * KWP;
+  const int CPK = (a.KW * 3 + 7) >> 3;  // stem: 16-B chunks per kernel row
+  const int stem_chunks = a.KH * CPK;
 
   // Issue the LDS-DMA for K-tile t into stage `st`.
   auto stage = [&](int t, int st) __attribute__((always_inline)) {
@@ -177,11 +180,12 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a, int kt_p
     } else {
 #pragma unroll
       for (int p = 0; p < PA; ++p) {
-        const int kt = t * 8 + lcA[p];
-        const int kh = kt / KWP;
-        const int kwp = kt - kh * KWP;
-        const bool ok = kt < ntap_pairs && hi0[p] >= 0;
-        const bf16* src = ok ? x + abase[p] + (kh * a.W + 2 * kwp) * 8 : zero;
+        const int q = t * 8 + lcA[p];  // chunk index along K
+        const int kh = q / CPK;
+        const int j = q - kh * CPK;
+        const bool ok = q < stem_chunks && hi0[p] >= 0;
+        // 4-B aligned (wi0 even, row length even): LDS-DMA needs dword alignment
+        const bf16* src = ok ? x + abase[p] + kh * a.W * 3 + j * 8 : zero;
         __builtin_amdgcn_global_load_lds((gbl_ptr_t)src,
                                          (lds_ptr_t)(sbase + (wave * (BM / 4) + p * 8) * ROWB), 16, 0, 0);
       }
@@ -359,7 +363,7 @@ void launch_cfg(const ConvArgs& a, int splits, int kt_per, int k_tiles, hipStrea
   const int tiles = ((M + BM - 1) / BM) * (a.Npad / BN);
   dim3 grid(tiles, splits);
   const size_t lds = (size_t)NS * (BM + BN) * 128;
-  if (a.pair_stem)
+  if (a.stem)
     hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, NS, true>), grid, dim3(256), lds, s, a, kt_per, k_tiles);
   else
     hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, NS, false>), grid, dim3(256), lds, s, a, kt_per, k_tiles);
@@ -370,12 +374,20 @@ void launch_cfg(const ConvArgs& a, int splits, int kt_per, int k_tiles, hipStrea
 
 int conv_out_dim(int in, int k, int stride, int pad) { return (in + 2 * pad - k) / stride + 1; }
 
-int conv_kpad(int Cin, int KH, int KW, bool pair_stem) {
-  if (pair_stem) {
-    const int k = KH * ((KW + 1) / 2) * 8;
+int conv_kpad(int Cin, int KH, int KW, bool stem) {
+  if (stem) {
+    const int k = KH * ((KW * 3 + 7) / 8) * 8;
     return (k + 63) / 64 * 64;
   }
   return KH * KW * Cin;  // Cin % 64 == 0
+}
+
+int stem_row_width(int S, int pad, int KW, int stride) {
+  // columns read by the last output pixel: ((Wo-1)*stride)*3 + CPK*8 values
+  const int Wo = (S + 2 * pad - KW) / stride + 1;
+  const int need = ((Wo - 1) * stride * 3 + ((KW * 3 + 7) / 8) * 8 + 2) / 3;
+  int w = std::max(S + 2 * pad, need);
+  return (w + 7) / 8 * 8;  // multiple of 8 pixels: 48-B aligned rows, even width
 }
 
 int conv_npad(int N) {
@@ -403,18 +415,22 @@ size_t conv_splitk_ws_elems(const ConvArgs& a) {
 }
 
 void conv2d_igemm(const ConvArgs& a, hipStream_t s) {
-  if (a.pair_stem) {
-    if (a.Cin != 8) throw std::invalid_argument("conv2d_igemm: pair stem expects Cin == 8 (2 RGB0 pixels)");
+  if (a.stem) {
+    if (a.Cin != 3) throw std::invalid_argument("conv2d_igemm: stem expects the packed RGB image (Cin == 3)");
   } else if (a.Cin % 64 != 0) {
     throw std::invalid_argument("conv2d_igemm: Cin must be a multiple of 64");
   }
-  if (a.Kpad != conv_kpad(a.Cin, a.KH, a.KW, a.pair_stem)) throw std::invalid_argument("conv2d_igemm: bad Kpad");
+  if (a.Kpad != conv_kpad(a.Cin, a.KH, a.KW, a.stem)) throw std::invalid_argument("conv2d_igemm: bad Kpad");
   if (a.N % 4 != 0 || a.N > a.Npad || a.ldo < a.N || a.ldo % 4 != 0)
     throw std::invalid_argument("conv2d_igemm: bad N/ldo");
-  if (a.pair_stem) {
-    // x is the zero-padded pair image [B, H, W, 8] with H/W already including 2*pad
-    if (a.Ho != (a.H - a.KH) / a.stride + 1 || a.Wo != (a.W - a.KW) / a.stride + 1)
-      throw std::invalid_argument("conv2d_igemm: bad output dims (pair stem)");
+  if (a.stem) {
+    // x = zero-padded packed image [B, H, W, 3] (pad already applied, W = row
+    // width in pixels). Every chunk read must stay inside its row and be
+    // dword aligned: even stride and even row width.
+    const int cpk = (a.KW * 3 + 7) / 8;
+    if (a.Ho <= 0 || a.Wo <= 0 || (a.Ho - 1) * a.stride + a.KH > a.H ||
+        (a.Wo - 1) * a.stride * 3 + cpk * 8 > a.W * 3 || (a.stride & 1) || (a.W & 1))
+      throw std::invalid_argument("conv2d_igemm: stem geometry out of bounds / misaligned");
   } else if (a.Ho != conv_out_dim(a.H, a.KH, a.stride, a.pad) || a.Wo != conv_out_dim(a.W, a.KW, a.stride, a.pad)) {
     throw std::invalid_argument("conv2d_igemm: bad output dims");
   }

@@ -22,11 +22,11 @@ namespace dmlc {
 
 // Implicit-GEMM convolution (also used for fully-connected layers as a 1x1
 // conv on a [B,1,1,C] tensor).
-//   x    : bf16 NHWC [B, H, W, Cin], Cin % 64 == 0; or, with pair_stem, the
-//          zero-padded pair image [B, H+2p, W+2p, 8] written by preprocess_u8
-//          (H/W in ConvArgs are then the padded dims and pad is ignored)
+//   x    : bf16 NHWC [B, H, W, Cin], Cin % 64 == 0; or, with `stem`, the
+//          zero-padded packed RGB image [B, H, W, 3] written by preprocess_u8
+//          (H/W = padded rows / row width; Ho/Wo given; pad ignored)
 //   w    : bf16 [Npad, Kpad], k = (kh*KW + kw)*Cin + c, zero padded; for the
-//          pair stem k = (kh*KWP + kwp)*8 + half*4 + c with kw = 2*kwp + half
+//          stem k = kh*CPK*8 + kw*3 + c, CPK = ceil(3*KW/8)
 //   zero : >= 16 zero bytes (source of the LDS-DMA for padding taps)
 //   bias : fp32 [Npad] (BN folded at load time), may be null
 //   res  : bf16 [M, ldo] residual added before the activation, may be null
@@ -43,7 +43,7 @@ struct ConvArgs {
   int N = 0, Npad = 0, Kpad = 0, ldo = 0;
   bool relu = false;
   bool out_f32 = false;
-  bool pair_stem = false;
+  bool stem = false;
   int split_k = 1;          // >1: fp32 partial sums into `ws`, reduced by a 2nd kernel
   float* ws = nullptr;      // split-K workspace, >= split_k * M * Npad floats
   int tile = -1;            // force a tile config (-1 = heuristic)
@@ -51,7 +51,9 @@ struct ConvArgs {
 
 int conv_out_dim(int in, int k, int stride, int pad);
 // K length of the packed weight matrix for a given conv geometry.
-int conv_kpad(int Cin, int KH, int KW, bool pair_stem = false);
+int conv_kpad(int Cin, int KH, int KW, bool stem = false);
+// Row width (pixels) of the stem's padded packed-RGB image for an SxS input.
+int stem_row_width(int S, int pad, int KW, int stride);
 int conv_npad(int N);
 size_t conv_splitk_ws_elems(const ConvArgs& a);
 int conv_pick_split_k(const ConvArgs& a, int num_cus);
@@ -66,11 +68,12 @@ void avgpool_global(const void* x, void* y, int B, int HW, int C, hipStream_t s)
 void avgpool_adaptive(const void* x, void* y, int B, int H, int W, int C, int Ho, int Wo,
                       hipStream_t s);
 
-// u8 HWC images [B,Hin,Win,3] -> bf16 "pair image" [B, S+2*pad, S+2*pad, 8]:
-// position (h, w) holds the normalised RGB0 pixels (h-pad, w-pad) and
-// (h-pad, w-pad+1), zero outside the SxS image. Aspect-preserving bilinear
-// resize of the short side to S, centre crop, /255, ImageNet mean/std.
-void preprocess_u8(const uint8_t* x, void* y, int B, int Hin, int Win, int S, int pad, hipStream_t s);
+// u8 HWC images [B,Hin,Win,3] -> bf16 packed RGB [B, S+2*pad, Wr, 3] with
+// the SxS image at (pad, pad) and zeros elsewhere (Wr % 8 == 0, >= S+2*pad).
+// Aspect-preserving bilinear resize of the short side to S, centre crop,
+// /255, ImageNet mean/std.
+void preprocess_u8(const uint8_t* x, void* y, int B, int Hin, int Win, int S, int pad, int Wr,
+                   hipStream_t s);
 
 // Row-wise softmax + top-1 over fp32 logits [B, ld] (first N columns).
 void softmax_top1(const float* logits, int B, int N, int ld, int32_t* idx, float* prob,

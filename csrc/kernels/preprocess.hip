@@ -1,12 +1,12 @@
-// On-device image preprocessing: u8 HWC -> normalised bf16 "pair image".
+// On-device image preprocessing: u8 HWC -> normalised, zero-padded packed
+// RGB bf16 (the conv stem's input layout).
 //
 // Reference equivalent: tch `imagenet::load_image_and_resize(path, 224, 224)`
 // called per query at src/services.rs:492 (decode + resize + /255 + ImageNet
 // mean/std normalisation, all on the CPU). Here the host only decodes; the
-// resize, crop and normalisation run on the GPU and write the layout the conv
-// stem consumes: a zero-padded image where each 16-B position (h, w) holds
-// the RGB0 pixels (h-pad, w-pad) and (h-pad, w-pad+1), so one 16-B LDS-DMA
-// of the stem conv fetches two horizontally adjacent taps with no bounds
+// resize, crop and normalisation run on the GPU and write [B, S+2p, Wr, 3]
+// bf16 with the image at (p, p) and zeros elsewhere, so the stem conv reads
+// each kernel row's KW*3 values as contiguous 16-B chunks without bounds
 // checks (csrc/kernels/conv_igemm.hip).
 //
 // Resize rule: resize to (RH, RW) with the short side = S and the long side
@@ -14,6 +14,9 @@
 // offsets ((RH-S)/2, (RW-S)/2), bilinear sampling with half-pixel centres
 // (= torch interpolate(mode="bilinear", align_corners=False, antialias=False)).
 // When the input is already SxS this is an exact per-pixel normalisation.
+//
+// One thread writes 8 consecutive pixels of an output row = 48 B as three
+// 16-B stores (Wr % 8 == 0 keeps every store aligned).
 #include "common.h"
 #include "kernels.h"
 
@@ -24,15 +27,18 @@ namespace dmlc {
 namespace {
 
 struct PreParams {
-  int B, Hin, Win, S, pad, P;  // P = S + 2*pad
+  int B, Hin, Win, S, pad, P, Wr;  // P = S + 2*pad rows, Wr pixels per row
   float sy_scale, sx_scale;
   int oy, ox;
   bool identity;
 };
 
-// Normalised RGB of crop pixel (y, x) packed as bf16 {r,g} {b,0}.
-__device__ __forceinline__ uint2 pixel(const uint8_t* __restrict__ img, const PreParams& p, int y, int x) {
-  if ((unsigned)y >= (unsigned)p.S || (unsigned)x >= (unsigned)p.S) return make_uint2(0, 0);
+__device__ __forceinline__ void pixel(const uint8_t* __restrict__ img, const PreParams& p, int y, int x,
+                                      float* o) {
+  if ((unsigned)y >= (unsigned)p.S || (unsigned)x >= (unsigned)p.S) {
+    o[0] = o[1] = o[2] = 0.f;
+    return;
+  }
   float c[3];
   if (p.identity) {
     const uint8_t* q = img + ((long)y * p.Win + x) * 3;
@@ -58,34 +64,40 @@ __device__ __forceinline__ uint2 pixel(const uint8_t* __restrict__ img, const Pr
       c[k] = top + (bot - top) * fy;
     }
   }
-  const float o0 = (c[0] * (1.f / 255.f) - 0.485f) * (1.f / 0.229f);
-  const float o1 = (c[1] * (1.f / 255.f) - 0.456f) * (1.f / 0.224f);
-  const float o2 = (c[2] * (1.f / 255.f) - 0.406f) * (1.f / 0.225f);
-  return make_uint2(pack2(o0, o1), pack2(o2, 0.f));
+  o[0] = (c[0] * (1.f / 255.f) - 0.485f) * (1.f / 0.229f);
+  o[1] = (c[1] * (1.f / 255.f) - 0.456f) * (1.f / 0.224f);
+  o[2] = (c[2] * (1.f / 255.f) - 0.406f) * (1.f / 0.225f);
 }
 
-__global__ __launch_bounds__(256) void preprocess_pair_kernel(const uint8_t* __restrict__ x,
-                                                              bf16* __restrict__ y, PreParams p) {
-  const long total = (long)p.B * p.P * p.P;
+__global__ __launch_bounds__(256) void preprocess_kernel(const uint8_t* __restrict__ x, bf16* __restrict__ y,
+                                                         PreParams p) {
+  const int groups = p.Wr / 8;
+  const long total = (long)p.B * p.P * groups;
   for (long idx = blockIdx.x * 256L + threadIdx.x; idx < total; idx += (long)gridDim.x * 256) {
-    const int wx = (int)(idx % p.P);
-    long t = idx / p.P;
+    const int g = (int)(idx % groups);
+    long t = idx / groups;
     const int hy = (int)(t % p.P);
     const int b = (int)(t / p.P);
     const uint8_t* img = x + (long)b * p.Hin * p.Win * 3;
-    const int iy = hy - p.pad, ix = wx - p.pad;
-    const uint2 a = pixel(img, p, iy, ix);
-    const uint2 c = pixel(img, p, iy, ix + 1);
-    *(uint4*)(y + idx * 8) = make_uint4(a.x, a.y, c.x, c.y);
+    const int iy = hy - p.pad;
+    float v[24];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) pixel(img, p, iy, g * 8 + i - p.pad, v + 3 * i);
+    uint4* dst = (uint4*)(y + idx * 24);
+    dst[0] = pack8(v);
+    dst[1] = pack8(v + 8);
+    dst[2] = pack8(v + 16);
   }
 }
 
 }  // namespace
 
-void preprocess_u8(const uint8_t* x, void* y, int B, int Hin, int Win, int S, int pad, hipStream_t s) {
+void preprocess_u8(const uint8_t* x, void* y, int B, int Hin, int Win, int S, int pad, int Wr,
+                   hipStream_t s) {
   if (B <= 0) return;
-  if (Hin <= 0 || Win <= 0 || S <= 0 || pad < 0) throw std::invalid_argument("preprocess_u8: bad dims");
-  if (!x || !y) throw std::invalid_argument("preprocess_u8: null operand");
+  if (Hin <= 0 || Win <= 0 || S <= 0 || pad < 0 || Wr < S + 2 * pad || Wr % 8 != 0)
+    throw std::invalid_argument("preprocess_u8: bad dims");
+  if (!x || !y || ((uintptr_t)y & 15)) throw std::invalid_argument("preprocess_u8: null / misaligned operand");
   PreParams p;
   p.B = B;
   p.Hin = Hin;
@@ -93,6 +105,7 @@ void preprocess_u8(const uint8_t* x, void* y, int B, int Hin, int Win, int S, in
   p.S = S;
   p.pad = pad;
   p.P = S + 2 * pad;
+  p.Wr = Wr;
   int RH, RW;
   if (Hin <= Win) {
     RH = S;
@@ -106,9 +119,9 @@ void preprocess_u8(const uint8_t* x, void* y, int B, int Hin, int Win, int S, in
   p.sy_scale = (float)Hin / RH;
   p.sx_scale = (float)Win / RW;
   p.identity = (Hin == S && Win == S);
-  const long total = (long)B * p.P * p.P;
+  const long total = (long)B * p.P * (Wr / 8);
   const int blocks = (int)std::min<long>((total + 255) / 256, 16384);
-  hipLaunchKernelGGL(preprocess_pair_kernel, dim3(blocks), dim3(256), 0, s, x, (bf16*)y, p);
+  hipLaunchKernelGGL(preprocess_kernel, dim3(blocks), dim3(256), 0, s, x, (bf16*)y, p);
   DMLC_HIP_CHECK(hipGetLastError());
 }
 

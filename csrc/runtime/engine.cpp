@@ -95,9 +95,9 @@ int Engine::conv(int in, const std::string& name, const std::string& bn, int cou
   ConvLayer L;
   L.name = name;
   L.bn = bn;
-  L.pair = (op_count_conv() == 0 && is.C == 8);  // stem reads the preprocess pair image
+  L.pair = (op_count_conv() == 0 && is.C == 3);  // stem reads the packed RGB image
   L.cin_eff = is.C;
-  L.cin = L.pair ? 3 : is.C;
+  L.cin = is.C;
   L.cout = cout;
   L.kh = L.kw = k;
   L.stride = stride;
@@ -105,6 +105,10 @@ int Engine::conv(int in, const std::string& name, const std::string& bn, int cou
   L.relu = relu;
   convs_.push_back(L);
   ActShape os{conv_out_dim(is.H, k, stride, pad), conv_out_dim(is.W, k, stride, pad), cout, false};
+  if (L.pair) {  // stem: padding is in the image; its rows are wider than S + 2p
+    os.H = conv_out_dim(image_size_, k, stride, stem_pad_);
+    os.W = os.H;
+  }
   const int out = add_act(os);
   Op op{OpType::Conv, in, out, res, (int)convs_.size() - 1, 0, 0, 0, name};
   ops_.push_back(op);
@@ -132,7 +136,8 @@ int Engine::fc(int in, const std::string& name, int cout, bool relu, bool last) 
 
 void Engine::build_resnet(const std::vector<int>& blocks, bool bottleneck) {
   const int S = image_size_;
-  int x = add_act(ActShape{S + 6, S + 6, 8, false});  // pair image, stem pad 3
+  stem_pad_ = 3;  // packed RGB image with the 7x7/s2 stem's padding built in
+  int x = add_act(ActShape{S + 6, stem_row_width(S, 3, 7, 2), 3, false});
   ops_.push_back(Op{OpType::Preprocess, -1, x, -1, -1, 0, 0, 3, "preprocess"});
   x = conv(x, "conv1", "bn1", 64, 7, 2, 0, true);
   {
@@ -174,7 +179,8 @@ void Engine::build_resnet(const std::vector<int>& blocks, bool bottleneck) {
 
 void Engine::build_alexnet() {
   const int S = image_size_;
-  int x = add_act(ActShape{S + 4, S + 4, 8, false});  // pair image, stem pad 2
+  stem_pad_ = 2;  // packed RGB image with the 11x11/s4 stem's padding built in
+  int x = add_act(ActShape{S + 4, stem_row_width(S, 2, 11, 4), 3, false});
   ops_.push_back(Op{OpType::Preprocess, -1, x, -1, -1, 0, 0, 2, "preprocess"});
   auto pool = [&](int in, const std::string& n) {
     const ActShape s = shapes_[in];
@@ -248,8 +254,8 @@ void Engine::pack_weights(const WeightMap& w) {
             for (int j = 0; j < L.kw; ++j) {
               const float v = W.data[(((size_t)n * L.cin + c) * L.kh + i) * L.kw + j] * scale[n];
               size_t k;
-              if (L.pair)  // k = (kh*KWP + kwp)*8 + half*4 + c, kw = 2*kwp + half
-                k = (size_t)(i * ((L.kw + 1) / 2) + j / 2) * 8 + (j & 1) * 4 + c;
+              if (L.pair)  // stem: k = kh*CPK*8 + kw*3 + c
+                k = (size_t)i * ((L.kw * 3 + 7) / 8) * 8 + j * 3 + c;
               else
                 k = (size_t)(i * L.kw + j) * L.cin_eff + c;
               pw[(size_t)n * L.kpad + k] = f2bf_host(v);
@@ -315,7 +321,7 @@ ConvArgs Engine::conv_args(const Op& op, int B, float* logits) const {
   ConvArgs a;
   a.x = acts_[op.in];
   a.zero = zero_;
-  a.pair_stem = L.pair;
+  a.stem = L.pair;
   a.w = (const uint8_t*)warena_ + L.w_off;
   a.bias = (const float*)((const uint8_t*)warena_ + L.b_off);
   a.res = op.res >= 0 ? acts_[op.res] : nullptr;
@@ -356,7 +362,7 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
   for (const Op& op : ops_) {
     switch (op.type) {
       case OpType::Preprocess:
-        preprocess_u8(images, acts_[op.out], B, Hin, Win, image_size_, op.pad, s);
+        preprocess_u8(images, acts_[op.out], B, Hin, Win, image_size_, op.pad, shapes_[op.out].W, s);
         break;
       case OpType::Conv:
         conv2d_igemm(conv_args(op, B, logits), s);

@@ -34,7 +34,7 @@ struct ConvLayer {
   int cin = 0, cin_eff = 0, cout = 0, kh = 1, kw = 1, stride = 1, pad = 0;
   bool relu = false;
   bool fc = false;        // linear layer (weight [N,K]) run as a 1x1 conv
-  bool pair = false;      // stem conv on the preprocess pair image (2 taps / 16 B)
+  bool pair = false;      // stem conv on the preprocess packed-RGB image (8 (kw,c) values / 16 B)
   int fc_hwc[3] = {0, 0, 0};  // for fc after a spatial tensor: (H,W,C) of the flatten
   int npad = 0, kpad = 0;
   size_t w_off = 0, b_off = 0;  // offsets (bytes) into the weight arena
@@ -106,6 +106,7 @@ class Engine {
   int image_size_ = 224;
   int num_cus_ = 256;
   int max_batch_ = 0;
+  int stem_pad_ = 0;
 
   std::vector<ActShape> shapes_;
   std::vector<ConvLayer> convs_;

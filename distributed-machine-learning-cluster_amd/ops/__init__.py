@@ -28,8 +28,12 @@ def _ptr(t):
     return 0 if t is None else t.data_ptr()
 
 
-def conv_kpad(cin: int, kh: int, kw: int, pair_stem: bool = False) -> int:
-    return native().conv_kpad(cin, kh, kw, pair_stem)
+def conv_kpad(cin: int, kh: int, kw: int, stem: bool = False) -> int:
+    return native().conv_kpad(cin, kh, kw, stem)
+
+
+def stem_row_width(size: int, pad: int, kw: int, stride: int) -> int:
+    return native().stem_row_width(size, pad, kw, stride)
 
 
 def conv_npad(n: int) -> int:
@@ -46,50 +50,51 @@ def _zero_page(device) -> torch.Tensor:
     return z
 
 
-def pack_conv_weight(w: torch.Tensor, scale: torch.Tensor | None = None, pair_stem: bool = False,
+def pack_conv_weight(w: torch.Tensor, scale: torch.Tensor | None = None, stem: bool = False,
                      device=None) -> torch.Tensor:
     """[Cout, Cin, KH, KW] fp32 -> packed bf16 [Npad, Kpad] (per-row scale
     folded in, e.g. a BN scale). k = (kh*KW + kw)*Cin + c; for the 3-channel
-    stem (``pair_stem``) k = (kh*KWP + kw//2)*8 + (kw%2)*4 + c."""
+    stem k = kh*CPK*8 + kw*3 + c with CPK = ceil(3*KW/8)."""
     cout, cin, kh, kw = w.shape
-    kpad, npad = conv_kpad(8 if pair_stem else cin, kh, kw, pair_stem), conv_npad(cout)
+    kpad, npad = conv_kpad(cin, kh, kw, stem), conv_npad(cout)
     w = w.float()
     if scale is not None:
         w = w * scale.float().view(-1, 1, 1, 1)
     out = torch.zeros(npad, kpad)
-    if pair_stem:
-        kwp = (kw + 1) // 2
-        wp = torch.zeros(cout, kh, kwp * 2, 4)
-        wp[:, :, :kw, :cin] = w.permute(0, 2, 3, 1)
-        out[:cout, : kh * kwp * 8] = wp.reshape(cout, -1)
+    if stem:
+        cpk = (kw * 3 + 7) // 8
+        wp = torch.zeros(cout, kh, cpk * 8)
+        wp[:, :, : kw * 3] = w.permute(0, 2, 3, 1).reshape(cout, kh, kw * 3)
+        out[:cout, : kh * cpk * 8] = wp.reshape(cout, -1)
     else:
         out[:cout, : kh * kw * cin] = w.permute(0, 2, 3, 1).reshape(cout, -1)
     return out.to(torch.bfloat16).to(device) if device is not None else out.to(torch.bfloat16)
 
 
-def pair_image(x_nhwc3: torch.Tensor, pad: int) -> torch.Tensor:
-    """Reference construction of the stem's pair image from an NHWC RGB
-    tensor: [B, H+2p, W+2p, 8], position (h,w) = RGB0 of pixels (h-p, w-p)
-    and (h-p, w-p+1), zeros outside the image."""
+def stem_image(x_nhwc3: torch.Tensor, pad: int, row_width: int) -> torch.Tensor:
+    """Reference construction of the stem's input: [B, H+2p, row_width, 3]
+    with the image at (p, p) and zeros elsewhere."""
     B, H, W, _ = x_nhwc3.shape
-    px = torch.zeros(B, H + 2 * pad, W + 2 * pad + 1, 4, dtype=x_nhwc3.dtype, device=x_nhwc3.device)
-    px[:, pad:pad + H, pad:pad + W, :3] = x_nhwc3
-    return torch.cat([px[:, :, :-1], px[:, :, 1:]], dim=-1).contiguous()
+    out = torch.zeros(B, H + 2 * pad, row_width, 3, dtype=x_nhwc3.dtype, device=x_nhwc3.device)
+    out[:, pad:pad + H, pad:pad + W] = x_nhwc3
+    return out.contiguous()
 
 
 def conv2d(x: torch.Tensor, w_packed: torch.Tensor, cout: int, kh: int, kw: int, stride: int = 1,
            pad: int = 0, bias: torch.Tensor | None = None, res: torch.Tensor | None = None,
            relu: bool = False, out_f32: bool = False, split_k: int = 1, tile: int = -1,
-           out: torch.Tensor | None = None, pair_stem: bool = False) -> torch.Tensor:
+           out: torch.Tensor | None = None, stem: bool = False, out_hw: tuple | None = None) -> torch.Tensor:
     """Implicit-GEMM conv on MFMA. x: bf16 NHWC [B,H,W,Cin] (Cin % 64 == 0),
-    or with ``pair_stem`` the padded pair image (``pair_image``; pad ignored).
+    or with ``stem`` the padded packed RGB image (``stem_image``) plus the
+    output size ``out_hw`` (the padding is already in the image).
     Returns [B,Ho,Wo,cout] (bf16, or fp32 if out_f32)."""
     _need_cuda(x, w_packed, bias, res)
     C = native()
     B, H, W, Cin = x.shape
-    if pair_stem:
-        pad = 0
-    Ho, Wo = C.conv_out_dim(H, kh, stride, pad), C.conv_out_dim(W, kw, stride, pad)
+    if stem:
+        Ho, Wo = out_hw
+    else:
+        Ho, Wo = C.conv_out_dim(H, kh, stride, pad), C.conv_out_dim(W, kw, stride, pad)
     if out is None:
         out = torch.empty(B, Ho, Wo, cout, device=x.device, dtype=torch.float32 if out_f32 else torch.bfloat16)
     ws = None
@@ -102,7 +107,7 @@ def conv2d(x: torch.Tensor, w_packed: torch.Tensor, cout: int, kh: int, kw: int,
     C.conv2d(x=_ptr(x.contiguous()), w=_ptr(w_packed), bias=_ptr(bias), res=_ptr(res), y=_ptr(out), B=B, H=H,
              W=W, Cin=Cin, KH=kh, KW=kw, stride=stride, pad=pad, N=cout, Npad=w_packed.shape[0],
              Kpad=w_packed.shape[1], ldo=cout, relu=relu, out_f32=out_f32, split_k=split_k, ws=_ptr(ws),
-             tile=tile, zero=_ptr(_zero_page(x.device)), pair_stem=pair_stem, stream=_stream())
+             tile=tile, zero=_ptr(_zero_page(x.device)), stem=stem, Ho=Ho, Wo=Wo, stream=_stream())
     return out
 
 
@@ -132,16 +137,17 @@ def avgpool_adaptive(x: torch.Tensor, ho: int, wo: int) -> torch.Tensor:
     return y
 
 
-def preprocess_u8(images: torch.Tensor, size: int = 224, pad: int = 0) -> torch.Tensor:
-    """u8 [B,H,W,3] -> bf16 pair image [B,size+2p,size+2p,8] (resize, crop,
-    normalise; see ``pair_image``)."""
+def preprocess_u8(images: torch.Tensor, size: int = 224, pad: int = 0, row_width: int | None = None) -> torch.Tensor:
+    """u8 [B,H,W,3] -> bf16 packed RGB [B, size+2p, row_width, 3] (resize,
+    crop, normalise; zero border; see ``stem_image``)."""
     _need_cuda(images)
     if images.dtype != torch.uint8 or images.dim() != 4 or images.shape[-1] != 3:
         raise ValueError("preprocess_u8 expects uint8 [B,H,W,3]")
     B, H, W, _ = images.shape
     P = size + 2 * pad
-    y = torch.empty(B, P, P, 8, device=images.device, dtype=torch.bfloat16)
-    native().preprocess_u8(_ptr(images.contiguous()), _ptr(y), B, H, W, size, pad, _stream())
+    Wr = row_width or (P + 7) // 8 * 8
+    y = torch.empty(B, P, Wr, 3, device=images.device, dtype=torch.bfloat16)
+    native().preprocess_u8(_ptr(images.contiguous()), _ptr(y), B, H, W, size, pad, Wr, _stream())
     return y
 
 

@@ -82,17 +82,24 @@ def test_conv2d_vs_torch(gpu, case):
     assert _rel(got, ref) < 8e-3, _rel(got, ref)
 
 
-@pytest.mark.parametrize("k,s,p,cout", [(7, 2, 3, 64), (11, 4, 2, 64), (3, 1, 1, 128), (4, 2, 1, 64)])
-def test_conv2d_stem_pair(gpu, k, s, p, cout):
-    """3-channel stem on the padded pair image (two taps per 16-B chunk)."""
+@pytest.mark.parametrize("k,s,p,cout,hw", [(7, 2, 3, 64, (56, 60)), (11, 4, 2, 64, (57, 61)),
+                                           (3, 2, 1, 128, (58, 62)), (4, 2, 1, 64, (57, 61)),
+                                           (7, 2, 3, 64, (224, 224)), (11, 4, 2, 64, (224, 224))])
+def test_conv2d_stem_packed(gpu, k, s, p, cout, hw):
+    """3-channel stem on the zero-padded packed RGB image (8 (kw,c) values
+    per 16-B chunk, k = kh*CPK*8 + kw*3 + c)."""
     g = torch.Generator().manual_seed(2)
-    B, H, W = 2, 57, 61
+    B, (H, W) = 2, hw
     x = torch.randn(B, 3, H, W, generator=g).bfloat16().float()
     w = (torch.randn(cout, 3, k, k, generator=g) / (3 * k * k) ** 0.5).bfloat16().float()
     ref = F.relu(F.conv2d(x, w, None, s, p))
-    xp = ops.pair_image(_nhwc(x), p)
-    wp = ops.pack_conv_weight(w, pair_stem=True, device=gpu)
-    y = ops.conv2d(xp.bfloat16().to(gpu), wp, cout, k, k, s, p, relu=True, pair_stem=True)
+    Ho, Wo = ref.shape[2:4]
+    cpk = (3 * k + 7) // 8
+    need = ((Wo - 1) * s * 3 + cpk * 8 + 2) // 3
+    Wr = (max(W + 2 * p, need) + 7) // 8 * 8
+    xp = ops.stem_image(_nhwc(x), p, Wr)
+    wp = ops.pack_conv_weight(w, stem=True, device=gpu)
+    y = ops.conv2d(xp.bfloat16().to(gpu), wp, cout, k, k, s, p, relu=True, stem=True, out_hw=(Ho, Wo))
     torch.cuda.synchronize()
     assert y.shape[1:3] == ref.shape[2:4]
     assert _rel(_nchw(y.float().cpu()), ref) < 8e-3
@@ -147,14 +154,14 @@ def test_preprocess_identity(gpu):
     g = torch.Generator().manual_seed(6)
     img = torch.randint(0, 256, (3, 224, 224, 3), generator=g, dtype=torch.uint8)
     ref = (_nchw(img.float()) / 255 - MEAN) / STD
-    for pad in (0, 3):
-        y = ops.preprocess_u8(img.to(gpu), 224, pad)
+    for pad, wr in ((0, 224), (3, 232), (2, 240)):
+        y = ops.preprocess_u8(img.to(gpu), 224, pad, wr)
         torch.cuda.synchronize()
         y = y.float().cpu()
-        assert y.shape == (3, 224 + 2 * pad, 224 + 2 * pad, 8)
-        exp = ops.pair_image(_nhwc(ref), pad)
+        assert y.shape == (3, 224 + 2 * pad, wr, 3)
+        exp = ops.stem_image(_nhwc(ref), pad, wr)
         assert _rel(y, exp) < 4e-3
-        assert torch.all(y[..., 3] == 0) and torch.all(y[..., 7] == 0)
+        assert torch.all(y[:, :pad] == 0) and torch.all(y[:, :, 224 + pad:] == 0)
 
 
 def test_preprocess_resize(gpu):

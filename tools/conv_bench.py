@@ -18,7 +18,7 @@ from dmlc import ops  # noqa: E402
 
 RESNET18 = [
     # name, H, W, Cin, Cout, k, s, p, pair
-    ("conv1", 230, 230, 8, 64, 7, 2, 3, True),
+    ("conv1", 230, 232, 3, 64, 7, 2, 3, True),  # packed stem image: 224+2*3 rows, 232-pixel rows
     ("l1", 56, 56, 64, 64, 3, 1, 1, False),
     ("l2.ds", 56, 56, 64, 128, 1, 2, 0, False),
     ("l2.c1", 56, 56, 64, 128, 3, 2, 1, False),
@@ -47,7 +47,7 @@ def main():
         x = (torch.randn(B, H, W, Cin, device=dev) * 0.5).bfloat16()
         cin_real = 3 if pair else Cin
         w = torch.randn(Cout, cin_real, k, k) / (cin_real * k * k) ** 0.5
-        wp = ops.pack_conv_weight(w, pair_stem=pair, device=dev)
+        wp = ops.pack_conv_weight(w, stem=pair, device=dev)
         bias = torch.zeros(Cout, device=dev)
         Ho = (H + 2 * (0 if pair else p) - k) // s + 1
         flops = 2.0 * B * Ho * Ho * Cout * cin_real * k * k
@@ -58,7 +58,8 @@ def main():
             if t in (0, 2, 3, 5, 6) and Cout % 128:
                 continue
             try:
-                f = lambda: ops.conv2d(x, wp, Cout, k, k, s, p, bias=bias, relu=True, tile=t, pair_stem=pair)
+                f = lambda: ops.conv2d(x, wp, Cout, k, k, s, p, bias=bias, relu=True, tile=t, stem=pair,
+                                       out_hw=(Ho, Ho) if pair else None)
                 f()
                 torch.cuda.synchronize()
                 ts = []
