@@ -24,6 +24,7 @@
 #include <set>
 #include <cstdio>
 #include <cstring>
+#include <fstream>
 #include <iostream>
 #include <map>
 #include <memory>
@@ -250,6 +251,26 @@ void handle_line(Node& n, const std::string& line) {
       Reader r(n.call_leader(L_JOBS, "", 30000));
       const uint32_t k = r.u32();
       for (uint32_t i = 0; i < k; ++i) out_line(format_job_report((int)i + 1, read_job(r)));
+    } else if (c == "jobs-dump") {
+      // machine-readable job state (per-query latency and completion time)
+      if (t.size() != 2) return err_line("Invalid jobs-dump command!");
+      Reader r(n.call_leader(L_JOBS, "", 30000));
+      const uint32_t k = r.u32();
+      std::ofstream f(absolutize(t[1]));
+      f << "[";
+      for (uint32_t i = 0; i < k; ++i) {
+        const Job j = read_job(r);
+        f << (i ? "," : "") << "{\"model\":\"" << j.model_name << "\",\"finished\":" << j.finished
+          << ",\"correct\":" << j.correct << ",\"started_us\":" << j.started_us
+          << ",\"first_done_us\":" << j.first_done_us << ",\"assigned\":" << j.assigned.size()
+          << ",\"durations_us\":[";
+        for (size_t q = 0; q < j.durations_us.size(); ++q) f << (q ? "," : "") << j.durations_us[q];
+        f << "],\"done_us\":[";
+        for (size_t q = 0; q < j.done_us.size(); ++q) f << (q ? "," : "") << j.done_us[q];
+        f << "]}";
+      }
+      f << "]\n";
+      out_line("dumped " + std::to_string(k) + " jobs");
     } else if (c == "assign") {
       if (t.size() != 1) return err_line("Invalid assign command!");
       Reader r(n.call_leader(L_JOBS, "", 30000));

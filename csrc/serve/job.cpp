@@ -13,6 +13,8 @@ void write_job(Writer& w, const Job& j) {
   w.i32(j.correct);
   w.u32((uint32_t)j.durations_us.size());
   for (int64_t d : j.durations_us) w.i64(d);
+  w.u32((uint32_t)j.done_us.size());
+  for (int64_t d : j.done_us) w.i64(d);
   w.u32((uint32_t)j.assigned.size());
   for (const auto& id : j.assigned) write_id(w, id);
   w.i64(j.started_us);
@@ -27,6 +29,9 @@ Job read_job(Reader& r) {
   uint32_t n = r.u32();
   j.durations_us.resize(n);
   for (uint32_t i = 0; i < n; ++i) j.durations_us[i] = r.i64();
+  n = r.u32();
+  j.done_us.resize(n);
+  for (uint32_t i = 0; i < n; ++i) j.done_us[i] = r.i64();
   n = r.u32();
   for (uint32_t i = 0; i < n; ++i) j.assigned.push_back(read_id(r));
   j.started_us = r.i64();

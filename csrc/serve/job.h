@@ -23,14 +23,16 @@ struct Job {
   int32_t finished = 0;
   int32_t correct = 0;
   std::vector<int64_t> durations_us;
+  std::vector<int64_t> done_us;  // wall-clock completion time of each query
   std::vector<Id> assigned;
   int64_t started_us = 0;   // wall clock when the job first issued a query
   int64_t first_done_us = 0;
 
-  void add_result(bool ok, int64_t dur_us) {
+  void add_result(bool ok, int64_t dur_us, int64_t done_wall_us = 0) {
     ++finished;
     if (ok) ++correct;
     durations_us.push_back(dur_us);
+    done_us.push_back(done_wall_us);
   }
 };
 

@@ -343,13 +343,14 @@ void LeaderService::run_job(size_t j) {
           std::vector<std::string> lines;
           {
             std::lock_guard<std::mutex> g(mu_);
-            if (jobs_[j].first_done_us == 0) jobs_[j].first_done_us = wall_us();
+            const int64_t now = wall_us();
+            if (jobs_[j].first_done_us == 0) jobs_[j].first_done_us = now;
             for (uint32_t i = 0; i < m && i < n; ++i) {
               const double p = r.f64();
               const std::string label = r.str();
               const std::string& truth = L[first + i].second;
               const bool ok = label == truth;
-              jobs_[j].add_result(ok, dur);
+              jobs_[j].add_result(ok, dur, now);
               if (cfg_.print_predictions) {
                 char buf[64];
                 snprintf(buf, sizeof(buf), " (%.2f%%)", p * 100.0);

@@ -1,0 +1,161 @@
+#!/usr/bin/env python3
+"""Serving benchmark through the whole control plane (BASELINE config:
+"AlexNet + ResNet18 two concurrent predict jobs (fair-share coordinator, jobs
+percentile reporting)").
+
+Starts N `dmlc-node` processes (one per GPU when there are several; all on
+GPU 0 on a one-GPU box), runs the reference's `predict` (both jobs over the
+imagenet_1k-shaped dataset: one JPEG per class, decoded on the member, then
+preprocess/forward/top-1 on the GPU), and reports from the leader's job
+state the quantities the reference publishes (CS425MP4Report.pdf pp.2-3):
+  * per-query latency mean/std (+ p50/p95/p99) per job (ref: ResNet18
+    158.94 ms / AlexNet 149.52 ms mean),
+  * time for the 2nd job to start executing queries (ref: 138.33 ms),
+  * optionally the time to resume normal operation after killing a
+    non-coordinator member (ref: 1.262 s) or the coordinator (ref: 3.593 s).
+
+usage: python tools/bench_jobs.py [--nodes 4] [--executor gpu] [--images 1000]
+         [--interval-ms 50] [--batch 1] [--kill member|leader] [--fast-periods]
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import tempfile
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from dmlc.serve.cluster import LocalCluster  # noqa: E402
+from dmlc.utils.dataset import make_synthetic_dataset, synthetic_labels, write_labels  # noqa: E402
+from dmlc.utils.ot import write_random_checkpoint  # noqa: E402
+
+REF = {"resnet18_mean_ms": 158.94, "alexnet_mean_ms": 149.52, "second_job_start_ms": 138.33,
+       "member_failure_recovery_s": 1.262, "leader_failure_recovery_s": 3.593}
+
+
+def pct(xs, q):
+    xs = sorted(xs)
+    if not xs:
+        return None
+    k = (len(xs) - 1) * q / 100
+    lo, hi = int(k), min(int(k) + 1, len(xs) - 1)
+    return xs[lo] + (xs[hi] - xs[lo]) * (k - lo)
+
+
+def recovery_s(jobs, t_fail_us):
+    """Longest gap between consecutive query completions (any job) after the
+    failure, minus the median gap before it: how long the cluster stopped
+    producing answers."""
+    done = sorted(d for j in jobs for d in j["done_us"] if d > 0)
+    before = [b - a for a, b in zip(done, done[1:]) if b < t_fail_us]
+    after = [b - a for a, b in zip(done, done[1:]) if a >= t_fail_us - 5e6 and b > t_fail_us]
+    if not after:
+        return None
+    base = statistics.median(before) if before else 0
+    return max(0.0, (max(after) - base) / 1e6)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--nodes", type=int, default=4)
+    ap.add_argument("--executor", default="gpu")
+    ap.add_argument("--gpus", type=int, default=0, help="devices to spread nodes over (0 = all visible)")
+    ap.add_argument("--images", type=int, default=1000)
+    ap.add_argument("--interval-ms", type=int, default=50)
+    ap.add_argument("--batch", type=int, default=1)
+    ap.add_argument("--kill", choices=["none", "member", "leader"], default="none")
+    ap.add_argument("--fast-periods", action="store_true", help="200 ms pings, 1.2 s failure timeout, 500 ms loops")
+    ap.add_argument("--port", type=int, default=21000)
+    ap.add_argument("--out", default="")
+    a = ap.parse_args()
+
+    ngpu = a.gpus
+    if a.executor == "gpu" and ngpu == 0:
+        import torch
+        ngpu = torch.cuda.device_count()
+    root = tempfile.mkdtemp(prefix="dmlc_jobs_")
+    labels = synthetic_labels(1000)
+    lab = write_labels(os.path.join(root, "synset_words.txt"), labels)
+    t = time.time()
+    ds = make_synthetic_dataset(os.path.join(root, "train"), labels[:a.images], size=(375, 500))
+    print(f"# dataset: {a.images} JPEGs 500x375 in {time.time() - t:.1f}s", file=sys.stderr)
+    ck = {m: write_random_checkpoint(m, os.path.join(root, f"{m}.ot"), seed=i) for i, m in
+          enumerate(["resnet18", "alexnet"])}
+    models = ",".join(f"{m}={p}" for m, p in ck.items())
+    extra = ["--job-limit", str(a.images), "--query-interval-ms", str(a.interval_ms), "--query-batch",
+             str(a.batch), "--quiet-predictions", "--max-batch", str(max(8, a.batch))]
+    cl = LocalCluster(a.nodes, a.port, os.path.join(root, "c"), lab, n_leaders=2, executor=a.executor,
+                      dataset=ds, models=models, fast=a.fast_periods, extra=extra)
+    if a.kill == "member" and a.nodes < 3:
+        raise SystemExit("--kill member needs >= 3 nodes (2 leader candidates + a member)")
+    nodes = []
+    try:
+        from dmlc.serve.cluster import NodeProcess
+        for i, p in enumerate(cl.ports):
+            ex = list(extra) + (["--device", str(i % ngpu)] if ngpu else [])
+            nodes.append(NodeProcess(p, cl.leaders, os.path.join(cl.root, f"n{p}"), lab, dataset=ds,
+                                     models=models, executor=a.executor, fast=a.fast_periods, extra=ex))
+        cl.nodes = nodes
+        for nd in nodes:
+            nd.expect(r"Address is", 60)
+        for nd in nodes:
+            nd.run(f"join {nodes[0].address}", r"Joined!", 30)
+        cl.wait_members(len(nodes), 60)
+        time.sleep(4 if not a.fast_periods else 1.5)  # one assignment round
+        client = nodes[1]  # standby leader candidate: survives both kill experiments
+        t_predict = time.time()
+        client.cmd("predict")
+        t_fail = None
+        deadline = time.time() + max(300, a.images * a.interval_ms / 1000 * 4)
+        while time.time() < deadline:
+            time.sleep(1.0)
+            try:
+                out = client.cmd("jobs", 30)
+            except Exception:  # noqa: BLE001  (leader switch)
+                continue
+            import re
+            counts = [int(x) for x in re.findall(r"Accuracy: \d+/(\d+)", out)]
+            if a.kill != "none" and t_fail is None and counts and min(counts) >= a.images * 0.3:
+                victim = nodes[0] if a.kill == "leader" else nodes[-1]
+                t_fail = time.time()
+                victim.kill()
+                print(f"# killed {a.kill} {victim.address} at {t_fail - t_predict:.2f}s", file=sys.stderr)
+            if len(counts) == 2 and min(counts) >= a.images:
+                break
+        dump = os.path.join(root, "jobs.json")
+        client.cmd(f"jobs-dump {dump}")
+        jobs = json.load(open(dump))
+    finally:
+        for nd in nodes:
+            nd.stop()
+        for nd in nodes:
+            nd.kill()
+    res = {"bench": "two concurrent predict jobs through the control plane", "nodes": a.nodes,
+           "executor": a.executor, "gpus": ngpu, "images_per_job": a.images, "query_interval_ms": a.interval_ms,
+           "query_batch": a.batch, "data": "synthetic 500x375 JPEGs (imagenet_1k layout), random-init weights",
+           "reference": REF, "jobs": []}
+    for j in jobs:
+        d = [x / 1000 for x in j["durations_us"]]
+        span = (max(j["done_us"]) - j["started_us"]) / 1e6 if j["done_us"] else None
+        res["jobs"].append({"model": j["model"], "finished": j["finished"], "correct": j["correct"],
+                            "mean_ms": round(statistics.mean(d), 3), "std_ms": round(statistics.pstdev(d), 3),
+                            "p50_ms": round(pct(d, 50), 3), "p95_ms": round(pct(d, 95), 3),
+                            "p99_ms": round(pct(d, 99), 3),
+                            "queries_per_s": round(j["finished"] / span, 2) if span else None})
+    fd = sorted(j["first_done_us"] for j in jobs)
+    st = sorted(j["started_us"] for j in jobs)
+    res["second_job_start_ms"] = round((st[-1] - st[0]) / 1000, 3)
+    res["second_job_first_result_ms"] = round((fd[-1] - fd[0]) / 1000, 3)
+    if t_fail is not None:
+        res[f"{a.kill}_failure_recovery_s"] = round(recovery_s(jobs, t_fail * 1e6), 3)
+    line = json.dumps(res)
+    print(line)
+    if a.out:
+        with open(a.out, "w") as f:
+            f.write(line + "\n")
+
+
+if __name__ == "__main__":
+    main()
