@@ -64,7 +64,7 @@ PYBIND11_MODULE(_C, m) {
       [](uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t res, uintptr_t y, int B, int H, int W,
          int Cin, int KH, int KW, int stride, int pad, int N, int Npad, int Kpad, int ldo, bool relu,
          bool out_f32, int split_k, uintptr_t ws, int tile, uintptr_t zero, bool stem, int Ho, int Wo,
-         uintptr_t stream) {
+         int max_blocks, uintptr_t stream) {
         ConvArgs a;
         a.x = P<void>(x);
         a.zero = P<void>(zero);
@@ -92,13 +92,16 @@ PYBIND11_MODULE(_C, m) {
         a.split_k = split_k;
         a.ws = P<float>(ws);
         a.tile = tile;
+        a.persistent = max_blocks > 0;
+        a.max_blocks = max_blocks;
         conv2d_igemm(a, S(stream));
       },
       py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("res"), py::arg("y"), py::arg("B"),
       py::arg("H"), py::arg("W"), py::arg("Cin"), py::arg("KH"), py::arg("KW"), py::arg("stride"),
       py::arg("pad"), py::arg("N"), py::arg("Npad"), py::arg("Kpad"), py::arg("ldo"),
       py::arg("relu"), py::arg("out_f32"), py::arg("split_k"), py::arg("ws"), py::arg("tile"),
-      py::arg("zero"), py::arg("stem"), py::arg("Ho"), py::arg("Wo"), py::arg("stream"));
+      py::arg("zero"), py::arg("stem"), py::arg("Ho"), py::arg("Wo"), py::arg("max_blocks"),
+      py::arg("stream"));
   m.def("maxpool2d", [](uintptr_t x, uintptr_t y, int B, int H, int W, int C, int k, int stride,
                         int pad, uintptr_t stream) {
     maxpool2d(P<void>(x), P<void>(y), B, H, W, C, conv_out_dim(H, k, stride, pad),

@@ -334,7 +334,7 @@ int run_node(const Args& a) {
   std::unique_ptr<Executor> ex;
   try {
     ex = make_executor(a.get("executor", "auto"), a.geti("device", 0), a.geti("max-batch", 64));
-    load_models(ex.get(), a.get("models", ""));
+    if (ex) load_models(ex.get(), a.get("models", ""));
   } catch (const std::exception& e) {
     err_line(std::string("executor unavailable: ") + e.what());
   }
@@ -397,6 +397,7 @@ int run_node(const Args& a) {
 int run_classify(const Args& a) {
   const std::string model = a.get("model", "alexnet");
   auto ex = make_executor(a.get("executor", "cpu"), a.geti("device", 0), 1);
+  if (!ex) throw std::runtime_error("no inference executor in this build");
   ex->load_model(model, a.get("weights"));
   const Labels labels = Labels::load(a.get("labels", "synset_words.txt"));
   std::vector<Image> imgs;

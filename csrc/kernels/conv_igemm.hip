@@ -106,9 +106,13 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a, int kt_p
   const int n_tiles = a.Npad / BN;
   const int m_tiles = (M + BM - 1) / BM;
   const int nwg = n_tiles * m_tiles;
-  const int tile = xcd_remap(blockIdx.x, nwg);
-  const int mt = tile / n_tiles, nt = tile % n_tiles;
-  const int m0 = mt * BM, n0 = nt * BN;
+  // Persistent grids (NS == 2): block b walks tiles b, b+G, b+2G, ... (G =
+  // gridDim.x, a multiple of 8 so b's XCD group is fixed), and the first
+  // K-tile DMA of its next tile is issued before the epilogue of the current
+  // one, so prologue latency and epilogue stores overlap.
+  int tile_iter = blockIdx.x;
+  int tile = xcd_remap(tile_iter, nwg);
+  int m0 = (tile / n_tiles) * BM, n0 = (tile % n_tiles) * BN;
 
   const int split = blockIdx.y;
   const int kt0 = split * kt_per_split;
@@ -124,39 +128,43 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a, int kt_p
   const int pchunk = lane & 7;  // physical chunk written by this lane
   int hi0[PA], wi0[PA], abase[PA];
   int lcA[PA];
-#pragma unroll
-  for (int p = 0; p < PA; ++p) {
-    const int r = wave * (BM / 4) + p * 8 + lrow;
-    const int lc = swz(r, pchunk);
-    lcA[p] = lc;
-    const int m = m0 + r;
-    if (m < M) {
-      const int hw = a.Ho * a.Wo;
-      const int b = m / hw;
-      const int rem = m - b * hw;
-      const int ho = rem / a.Wo;
-      const int wo = rem - ho * a.Wo;
-      if constexpr (PAIR) {
-        hi0[p] = ho * a.stride;
-        wi0[p] = wo * a.stride;
-        abase[p] = ((b * a.H + hi0[p]) * a.W + wi0[p]) * 3;  // packed RGB row image
-      } else {
-        hi0[p] = ho * a.stride - a.pad;
-        wi0[p] = wo * a.stride - a.pad;
-        abase[p] = ((b * a.H + hi0[p]) * a.W + wi0[p]) * a.Cin + lc * 8;
-      }
-    } else {
-      hi0[p] = -(1 << 28);
-      wi0[p] = 0;
-      abase[p] = 0;
-    }
-  }
   int wboff[PB];
+  // Per-tile staging state (input origin of every staged row, weight rows).
+  auto setup_rows = [&](int m0_, int n0_) __attribute__((always_inline)) {
 #pragma unroll
-  for (int p = 0; p < PB; ++p) {
-    const int r = wave * (BN / 4) + p * 8 + lrow;
-    wboff[p] = (n0 + r) * a.Kpad + swz(r, pchunk) * 8;
-  }
+    for (int p = 0; p < PA; ++p) {
+      const int r = wave * (BM / 4) + p * 8 + lrow;
+      const int lc = swz(r, pchunk);
+      lcA[p] = lc;
+      const int m = m0_ + r;
+      if (m < M) {
+        const int hw = a.Ho * a.Wo;
+        const int b = m / hw;
+        const int rem = m - b * hw;
+        const int ho = rem / a.Wo;
+        const int wo = rem - ho * a.Wo;
+        if constexpr (PAIR) {
+          hi0[p] = ho * a.stride;
+          wi0[p] = wo * a.stride;
+          abase[p] = ((b * a.H + hi0[p]) * a.W + wi0[p]) * 3;  // packed RGB row image
+        } else {
+          hi0[p] = ho * a.stride - a.pad;
+          wi0[p] = wo * a.stride - a.pad;
+          abase[p] = ((b * a.H + hi0[p]) * a.W + wi0[p]) * a.Cin + lc * 8;
+        }
+      } else {
+        hi0[p] = -(1 << 28);
+        wi0[p] = 0;
+        abase[p] = 0;
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < PB; ++p) {
+      const int r = wave * (BN / 4) + p * 8 + lrow;
+      wboff[p] = (n0_ + r) * a.Kpad + swz(r, pchunk) * 8;
+    }
+  };
+  setup_rows(m0, n0);
   const int CPK = (a.KW * 3 + 7) >> 3;  // stem: 16-B chunks per kernel row
   const int stem_chunks = a.KH * CPK;
 
@@ -235,7 +243,97 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a, int kt_p
   //   tile it-1; then refill tile it-1's stage with tile it+D and compute.
   constexpr int D = NS - 1;
   constexpr int G = PA + PB;  // LDS-DMA instructions per wave per tile
-  if (nk > 0) {
+
+  // Epilogue. Lane holds D[n = 4*fq + r][m = fr] of each 16x16 tile.
+  auto epilogue = [&](int m0e, int n0e) __attribute__((always_inline)) {
+    if (gridDim.y > 1) {
+      float* __restrict__ ws = a.ws + (size_t)split * M * a.Npad;
+#pragma unroll
+      for (int j = 0; j < TM; ++j) {
+        const int m = m0e + wm * WTM + j * 16 + fr;
+        if (m >= M) continue;
+#pragma unroll
+        for (int i = 0; i < TN; ++i) {
+          const int n = n0e + wn * WTN + i * 16 + fq * 4;
+          *(floatx4*)(ws + (size_t)m * a.Npad + n) = acc[i][j];
+        }
+      }
+      return;
+    }
+    const bf16* __restrict__ res = (const bf16*)a.res;
+#pragma unroll
+    for (int j = 0; j < TM; ++j) {
+      const int m = m0e + wm * WTM + j * 16 + fr;
+      if (m >= M) continue;
+#pragma unroll
+      for (int i = 0; i < TN; ++i) {
+        const int n = n0e + wn * WTN + i * 16 + fq * 4;
+        if (n >= a.N) continue;
+        float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        if (a.bias) {
+          const floatx4 bb = *(const floatx4*)(a.bias + n);
+          v[0] += bb[0]; v[1] += bb[1]; v[2] += bb[2]; v[3] += bb[3];
+        }
+        const size_t o = (size_t)m * a.ldo + n;
+        if (res) {
+          const uint2 rv = *(const uint2*)(res + o);
+          v[0] += __uint_as_float(rv.x << 16);
+          v[1] += __uint_as_float(rv.x & 0xffff0000u);
+          v[2] += __uint_as_float(rv.y << 16);
+          v[3] += __uint_as_float(rv.y & 0xffff0000u);
+        }
+        if (a.relu) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+        }
+        if (a.out_f32) {
+          *(floatx4*)((float*)a.y + o) = floatx4{v[0], v[1], v[2], v[3]};
+        } else {
+          *(uint2*)((bf16*)a.y + o) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+        }
+      }
+    }
+  };
+
+  if (nk <= 0 || tile_iter >= nwg) return;
+
+  if constexpr (NS == 2) {
+    // Flattened (tile, K-tile) stream over this block's tiles; the DMA for
+    // the next item is issued right after each barrier, including across a
+    // tile boundary (the next tile's first K-tile lands during this tile's
+    // last MFMAs and epilogue).
+    stage(kt0, 0);
+    int st = 0;
+    while (true) {
+      int next_iter = -1;
+      int m0c = m0, n0c = n0;
+      for (int it = 0; it < nk; ++it) {
+        vm_wait<0>();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (it + 1 < nk) {
+          stage(kt0 + it + 1, st ^ 1);
+        } else if (a.persistent && tile_iter + (int)gridDim.x < nwg) {
+          next_iter = tile_iter + gridDim.x;
+          tile = xcd_remap(next_iter, nwg);
+          m0 = (tile / n_tiles) * BM;
+          n0 = (tile % n_tiles) * BN;
+          setup_rows(m0, n0);  // the current tile issued all its DMA: safe to overwrite
+          stage(kt0, st ^ 1);
+        }
+        compute(st);
+        st ^= 1;
+      }
+      epilogue(m0c, n0c);
+      if (next_iter < 0) break;
+      tile_iter = next_iter;
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+  } else {
 #pragma unroll
     for (int s = 0; s < D; ++s)
       if (s < nk) stage(kt0 + s, s);
@@ -252,56 +350,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a, int kt_p
       compute(st);
       st = st == NS - 1 ? 0 : st + 1;
     }
-  }
-
-  // Epilogue. Lane holds D[n = 4*fq + r][m = fr] of each 16x16 tile.
-  if (gridDim.y > 1) {
-    float* __restrict__ ws = a.ws + (size_t)split * M * a.Npad;
-#pragma unroll
-    for (int j = 0; j < TM; ++j) {
-      const int m = m0 + wm * WTM + j * 16 + fr;
-      if (m >= M) continue;
-#pragma unroll
-      for (int i = 0; i < TN; ++i) {
-        const int n = n0 + wn * WTN + i * 16 + fq * 4;
-        *(floatx4*)(ws + (size_t)m * a.Npad + n) = acc[i][j];
-      }
-    }
-    return;
-  }
-
-  const bf16* __restrict__ res = (const bf16*)a.res;
-#pragma unroll
-  for (int j = 0; j < TM; ++j) {
-    const int m = m0 + wm * WTM + j * 16 + fr;
-    if (m >= M) continue;
-#pragma unroll
-    for (int i = 0; i < TN; ++i) {
-      const int n = n0 + wn * WTN + i * 16 + fq * 4;
-      if (n >= a.N) continue;
-      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      if (a.bias) {
-        const floatx4 bb = *(const floatx4*)(a.bias + n);
-        v[0] += bb[0]; v[1] += bb[1]; v[2] += bb[2]; v[3] += bb[3];
-      }
-      const size_t o = (size_t)m * a.ldo + n;
-      if (res) {
-        const uint2 rv = *(const uint2*)(res + o);
-        v[0] += __uint_as_float(rv.x << 16);
-        v[1] += __uint_as_float(rv.x & 0xffff0000u);
-        v[2] += __uint_as_float(rv.y << 16);
-        v[3] += __uint_as_float(rv.y & 0xffff0000u);
-      }
-      if (a.relu) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
-      }
-      if (a.out_f32) {
-        *(floatx4*)((float*)a.y + o) = floatx4{v[0], v[1], v[2], v[3]};
-      } else {
-        *(uint2*)((bf16*)a.y + o) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
-      }
-    }
+    epilogue(m0, n0);
   }
 }
 
@@ -345,9 +394,10 @@ struct TileCfg {
 // (A register double-buffered fragment schedule on top of ns2 measured
 // within +-3% of these and was dropped; ns3/ns4 lose 30% to the halved
 // occupancy: profiles/r1_conv_bench_stages.log.)
-constexpr int kNumTiles = 7;
-constexpr TileCfg kTiles[kNumTiles] = {{128, 128, 2}, {256, 64, 2}, {64, 256, 2}, {128, 128, 3},
-                                       {256, 64, 3},  {64, 256, 3}, {128, 128, 4}};
+//   7: 128x64 ns2 (waves 2x2 of 64x32)   8: 64x128 ns2 (waves 2x2 of 32x64)
+constexpr int kNumTiles = 9;
+constexpr TileCfg kTiles[kNumTiles] = {{128, 128, 2}, {256, 64, 2}, {64, 256, 2}, {128, 128, 3}, {256, 64, 3},
+                                       {64, 256, 3},  {128, 128, 4}, {128, 64, 2}, {64, 128, 2}};
 
 int pick_tile(const ConvArgs& a) {
   if (a.tile >= 0 && a.tile < kNumTiles) return a.tile;
@@ -360,13 +410,19 @@ int pick_tile(const ConvArgs& a) {
 template <int BM, int BN, int WM, int WN, int NS>
 void launch_cfg(const ConvArgs& a, int splits, int kt_per, int k_tiles, hipStream_t s) {
   const int M = a.B * a.Ho * a.Wo;
-  const int tiles = ((M + BM - 1) / BM) * (a.Npad / BN);
+  int tiles = ((M + BM - 1) / BM) * (a.Npad / BN);
+  ConvArgs b = a;
+  if (NS == 2 && a.persistent && a.max_blocks >= 8 && tiles > a.max_blocks) {
+    tiles = a.max_blocks / 8 * 8;  // multiple of 8: a block keeps its XCD group
+  } else {
+    b.persistent = false;
+  }
   dim3 grid(tiles, splits);
   const size_t lds = (size_t)NS * (BM + BN) * 128;
   if (a.stem)
-    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, NS, true>), grid, dim3(256), lds, s, a, kt_per, k_tiles);
+    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, NS, true>), grid, dim3(256), lds, s, b, kt_per, k_tiles);
   else
-    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, NS, false>), grid, dim3(256), lds, s, a, kt_per, k_tiles);
+    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, NS, false>), grid, dim3(256), lds, s, b, kt_per, k_tiles);
   DMLC_HIP_CHECK(hipGetLastError());
 }
 
@@ -459,7 +515,9 @@ void conv2d_igemm(const ConvArgs& a, hipStream_t s) {
     case 3: launch_cfg<128, 128, 2, 2, 3>(b, splits, kt_per, k_tiles, s); break;
     case 4: launch_cfg<256, 64, 4, 1, 3>(b, splits, kt_per, k_tiles, s); break;
     case 5: launch_cfg<64, 256, 1, 4, 3>(b, splits, kt_per, k_tiles, s); break;
-    default: launch_cfg<128, 128, 2, 2, 4>(b, splits, kt_per, k_tiles, s); break;
+    case 6: launch_cfg<128, 128, 2, 2, 4>(b, splits, kt_per, k_tiles, s); break;
+    case 7: launch_cfg<128, 64, 2, 2, 2>(b, splits, kt_per, k_tiles, s); break;
+    default: launch_cfg<64, 128, 2, 2, 2>(b, splits, kt_per, k_tiles, s); break;
   }
   if (splits > 1) {
     const int blocks = (int)std::min<long>((M * (a.N / 4) + 255) / 256, 4096);

@@ -47,6 +47,8 @@ struct ConvArgs {
   int split_k = 1;          // >1: fp32 partial sums into `ws`, reduced by a 2nd kernel
   float* ws = nullptr;      // split-K workspace, >= split_k * M * Npad floats
   int tile = -1;            // force a tile config (-1 = heuristic)
+  bool persistent = false;  // cap the grid at max_blocks; blocks walk several tiles
+  int max_blocks = 0;       // persistent grid size (multiple of 8), e.g. 2 * #CUs
 };
 
 int conv_out_dim(int in, int k, int stride, int pad);

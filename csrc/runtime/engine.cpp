@@ -47,6 +47,7 @@ Engine::Engine(const std::string& arch, const WeightMap& weights, int device, in
   hipDeviceProp_t prop;
   DMLC_HIP_CHECK(hipGetDeviceProperties(&prop, device_));
   num_cus_ = prop.multiProcessorCount;
+  if (const char* e = std::getenv("DMLC_PERSISTENT")) persistent_ = std::string(e) != "0";
 
   if (arch == "resnet18")
     build_resnet({2, 2, 2, 2}, false);
@@ -352,6 +353,8 @@ ConvArgs Engine::conv_args(const Op& op, int B, float* logits) const {
   while (s > 1 && (size_t)s * M * L.npad > ws_elems_) --s;
   a.split_k = s;
   a.ws = ws_;
+  a.persistent = persistent_;
+  a.max_blocks = 2 * num_cus_;
   return a;
 }
 

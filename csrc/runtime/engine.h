@@ -107,6 +107,7 @@ class Engine {
   int num_cus_ = 256;
   int max_batch_ = 0;
   int stem_pad_ = 0;
+  bool persistent_ = true;  // persistent conv grids (env DMLC_PERSISTENT=0 disables)
 
   std::vector<ActShape> shapes_;
   std::vector<ConvLayer> convs_;

@@ -83,7 +83,8 @@ def stem_image(x_nhwc3: torch.Tensor, pad: int, row_width: int) -> torch.Tensor:
 def conv2d(x: torch.Tensor, w_packed: torch.Tensor, cout: int, kh: int, kw: int, stride: int = 1,
            pad: int = 0, bias: torch.Tensor | None = None, res: torch.Tensor | None = None,
            relu: bool = False, out_f32: bool = False, split_k: int = 1, tile: int = -1,
-           out: torch.Tensor | None = None, stem: bool = False, out_hw: tuple | None = None) -> torch.Tensor:
+           out: torch.Tensor | None = None, stem: bool = False, out_hw: tuple | None = None,
+           max_blocks: int = 0) -> torch.Tensor:
     """Implicit-GEMM conv on MFMA. x: bf16 NHWC [B,H,W,Cin] (Cin % 64 == 0),
     or with ``stem`` the padded packed RGB image (``stem_image``) plus the
     output size ``out_hw`` (the padding is already in the image).
@@ -107,7 +108,8 @@ def conv2d(x: torch.Tensor, w_packed: torch.Tensor, cout: int, kh: int, kw: int,
     C.conv2d(x=_ptr(x.contiguous()), w=_ptr(w_packed), bias=_ptr(bias), res=_ptr(res), y=_ptr(out), B=B, H=H,
              W=W, Cin=Cin, KH=kh, KW=kw, stride=stride, pad=pad, N=cout, Npad=w_packed.shape[0],
              Kpad=w_packed.shape[1], ldo=cout, relu=relu, out_f32=out_f32, split_k=split_k, ws=_ptr(ws),
-             tile=tile, zero=_ptr(_zero_page(x.device)), stem=stem, Ho=Ho, Wo=Wo, stream=_stream())
+             tile=tile, zero=_ptr(_zero_page(x.device)), stem=stem, Ho=Ho, Wo=Wo, max_blocks=max_blocks,
+             stream=_stream())
     return out
 
 

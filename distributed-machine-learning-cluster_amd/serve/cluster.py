@@ -24,11 +24,11 @@ NODE_BIN = os.path.join(REPO_ROOT, "build", "bin", "dmlc-node")
 class NodeProcess:
     def __init__(self, port: int, leaders: list[str], workdir: str, labels: str, dataset: str = "",
                  models: str = "", executor: str = "cpu", host: str = "127.0.0.1", fast: bool = True,
-                 extra: list[str] | None = None, env: dict | None = None):
+                 extra: list[str] | None = None, env: dict | None = None, binary: str | None = None):
         self.port = port
         self.address = f"{host}:{port}"
         os.makedirs(workdir, exist_ok=True)
-        args = [NODE_BIN, "--host", host, "--port", str(port), "--leaders", ",".join(leaders),
+        args = [binary or os.environ.get("DMLC_NODE_BIN", NODE_BIN), "--host", host, "--port", str(port), "--leaders", ",".join(leaders),
                 "--workdir", workdir, "--labels", labels, "--executor", executor, "--ack"]
         if dataset:
             args += ["--dataset", dataset]

@@ -55,6 +55,36 @@ CONV_CASES = [
     (1, 7, 7, 512, 512, 3, 1, 1, True, True, 3, 16),
     (2, 14, 14, 256, 256, 1, 1, 0, False, False, 3, 1),
 ]
+# persistent grids: a tiny block cap forces every block through many tiles
+PERSIST_CASES = [
+    (3, 28, 28, 128, 128, 3, 1, 1, True, True, 0, 1),
+    (2, 56, 56, 64, 64, 3, 1, 1, True, False, 1, 1),
+    (2, 14, 14, 256, 512, 3, 2, 1, True, False, 2, 1),
+    (5, 13, 13, 192, 384, 3, 1, 1, True, True, 0, 1),
+]
+
+
+@pytest.mark.parametrize("case", PERSIST_CASES, ids=[str(c) for c in PERSIST_CASES])
+@pytest.mark.parametrize("max_blocks", [8, 24])
+def test_conv2d_persistent(gpu, case, max_blocks):
+    B, H, W, Cin, Cout, k, s, p, relu, use_res, tile, split = case
+    g = torch.Generator().manual_seed(9)
+    x = torch.randn(B, Cin, H, W, generator=g).bfloat16().float()
+    w = (torch.randn(Cout, Cin, k, k, generator=g) / (Cin * k * k) ** 0.5).bfloat16().float()
+    bias = torch.randn(Cout, generator=g) * 0.1
+    ref = F.conv2d(x, w, bias, s, p)
+    res = None
+    if use_res:
+        r = torch.randn_like(ref).bfloat16().float()
+        ref = ref + r
+        res = _nhwc(r).bfloat16().to(gpu)
+    if relu:
+        ref = F.relu(ref)
+    wp = ops.pack_conv_weight(w, device=gpu)
+    y = ops.conv2d(_nhwc(x).bfloat16().to(gpu), wp, Cout, k, k, s, p, bias=bias.to(gpu), res=res, relu=relu,
+                   tile=tile, max_blocks=max_blocks)
+    torch.cuda.synchronize()
+    assert _rel(_nchw(y.float().cpu()), ref) < 8e-3
 
 
 @pytest.mark.parametrize("case", CONV_CASES, ids=[str(c) for c in CONV_CASES])

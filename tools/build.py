@@ -115,9 +115,10 @@ def build(jobs: int = 8, verbose: bool = False, node: bool = True) -> None:
             steps.append(["g++", *host_flags, *extra, "-c", s, "-o", o])
 
     # ---- 3. control-plane objects (C++17, no GPU, no torch)
-    node_srcs = sorted(glob.glob(os.path.join(CSRC, "control", "*.cpp")) +
-                       glob.glob(os.path.join(CSRC, "serve", "*.cpp")) +
-                       glob.glob(os.path.join(CSRC, "cli", "*.cpp"))) if node else []
+    ctl_srcs = sorted(glob.glob(os.path.join(CSRC, "control", "*.cpp")) +
+                      glob.glob(os.path.join(CSRC, "serve", "*.cpp")) +
+                      glob.glob(os.path.join(CSRC, "cli", "*.cpp")))
+    node_srcs = [s for s in ctl_srcs if not s.endswith("executor_stub.cpp")] if node else []
     node_objs = []
     for s in node_srcs:
         o = os.path.join(OBJ, os.path.relpath(s, CSRC).replace(os.sep, "_") + ".o")
@@ -125,8 +126,24 @@ def build(jobs: int = 8, verbose: bool = False, node: bool = True) -> None:
         if _stale(o, [s], hdr):
             steps.append(["g++", *host_flags, *torch_flags, "-pthread", "-c", s, "-o", o])
 
+    # ---- 4. ThreadSanitizer build of the control plane (no torch / HIP)
+    tsan_objs = []
+    if node:
+        tsan_srcs = [s for s in ctl_srcs if not s.endswith("executor.cpp")]
+        tsan_srcs.append(os.path.join(CSRC, "runtime", "jpeg.cpp"))
+        for s in tsan_srcs:
+            o = os.path.join(OBJ, "tsan_" + os.path.relpath(s, CSRC).replace(os.sep, "_") + ".o")
+            tsan_objs.append(o)
+            if _stale(o, [s], hdr):
+                steps.append(["g++", "-O1", "-g", "-std=c++17", "-fPIC", "-fsanitize=thread", "-pthread",
+                              "-c", s, "-o", o])
+
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         list(ex.map(lambda c: _run(c, verbose), steps))
+    if tsan_objs:
+        tsan_exe = os.path.join(BIN, "dmlc-node-tsan")
+        if _stale(tsan_exe, tsan_objs, 0):
+            _run(["g++", "-fsanitize=thread", "-pthread", *tsan_objs, "-o", tsan_exe], verbose)
 
     libgpu = os.path.join(PKG, "libdmlc_gpu.so")
     if _stale(libgpu, gpu_objs, 0):

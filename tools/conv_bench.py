@@ -36,6 +36,8 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--tiles", default="-1,0,1,2,3,4,5,6")
     ap.add_argument("--only", default="")
+    ap.add_argument("--persist", type=int, default=0, help="persistent grid size (0 = one block per tile)")
+    ap.add_argument("--split", type=int, default=1, help="split-K factor")
     ap.add_argument("--ref", action="store_true", help="also time hipBLASLt GEMM and MIOpen conv on each shape")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -55,11 +57,12 @@ def main():
         for t in tiles:
             if t in (2, 5) and Cout % 256:
                 continue
-            if t in (0, 2, 3, 5, 6) and Cout % 128:
+            if t in (0, 2, 3, 5, 6, 8) and Cout % 128:
                 continue
             try:
                 f = lambda: ops.conv2d(x, wp, Cout, k, k, s, p, bias=bias, relu=True, tile=t, stem=pair,
-                                       out_hw=(Ho, Ho) if pair else None)
+                                       out_hw=(Ho, Ho) if pair else None, max_blocks=a.persist,
+                                       split_k=a.split)
                 f()
                 torch.cuda.synchronize()
                 ts = []
