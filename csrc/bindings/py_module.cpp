@@ -114,9 +114,17 @@ PYBIND11_MODULE(_C, m) {
                                uintptr_t stream) {
     avgpool_adaptive(P<void>(x), P<void>(y), B, H, W, C, Ho, Wo, S(stream));
   });
-  m.def("preprocess_u8", [](uintptr_t x, uintptr_t y, int B, int Hin, int Win, int S_, int pad, int Wr,
-                            uintptr_t stream) {
-    preprocess_u8(P<uint8_t>(x), P<void>(y), B, Hin, Win, S_, pad, Wr, S(stream));
+  m.def(
+      "preprocess_u8",
+      [](uintptr_t x, uintptr_t y, int B, int Hin, int Win, int S_, int pad, int Wr, uintptr_t stream,
+         bool paired) { preprocess_u8(P<uint8_t>(x), P<void>(y), B, Hin, Win, S_, pad, Wr, S(stream), paired); },
+      py::arg("x"), py::arg("y"), py::arg("B"), py::arg("Hin"), py::arg("Win"), py::arg("S"), py::arg("pad"),
+      py::arg("Wr"), py::arg("stream"), py::arg("paired") = false);
+  m.attr("STEM_POOL_K") = kStemPoolK;
+  m.def("stem_pool_pick_strip", &stem_pool_pick_strip);
+  m.def("stem_conv_pool", [](uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y, int B, int S_, int Wq,
+                             int strip, uintptr_t stream) {
+    stem_conv_pool(P<void>(x), P<void>(w), P<float>(bias), P<void>(y), B, S_, Wq, strip, S(stream));
   });
   m.def("softmax_top1", [](uintptr_t logits, int B, int N, int ld, uintptr_t idx, uintptr_t prob,
                            uintptr_t stream) {

@@ -73,9 +73,21 @@ void avgpool_adaptive(const void* x, void* y, int B, int H, int W, int C, int Ho
 // u8 HWC images [B,Hin,Win,3] -> bf16 packed RGB [B, S+2*pad, Wr, 3] with
 // the SxS image at (pad, pad) and zeros elsewhere (Wr % 8 == 0, >= S+2*pad).
 // Aspect-preserving bilinear resize of the short side to S, centre crop,
-// /255, ImageNet mean/std.
+// /255, ImageNet mean/std. `paired`: each pair of pixels occupies 16 B as
+// [r g b r g b 0 0] (layout [B, S+2*pad, Wr/2, 8]; stem_conv_pool's input).
 void preprocess_u8(const uint8_t* x, void* y, int B, int Hin, int Win, int S, int pad, int Wr,
-                   hipStream_t s);
+                   hipStream_t s, bool paired = false);
+
+// Fused ResNet stem: conv 7x7/s2/p3 (folded BN) + ReLU + maxpool 3x3/s2/p1.
+//   x : paired image [B, S+6, Wq, 8] bf16 (preprocess_u8 pad=3, paired)
+//   w : bf16 [64, 224], k = kh*32 + q*8 + e: chunk q covers kw = 2q, 2q+1,
+//       e = 3*(kw-2q) + c; e = 6,7 and kw = 7 are zero
+//   y : bf16 NHWC [B, S/4, S/4, 64]
+// strip = pooled rows per workgroup (even divisor of S/4).
+constexpr int kStemPoolK = 224;
+int stem_pool_pick_strip(int B, int PH, int num_cus);
+void stem_conv_pool(const void* x, const void* w, const float* bias, void* y, int B, int S, int Wq, int strip,
+                    hipStream_t s);
 
 // Row-wise softmax + top-1 over fp32 logits [B, ld] (first N columns).
 void softmax_top1(const float* logits, int B, int N, int ld, int32_t* idx, float* prob,

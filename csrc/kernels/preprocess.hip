@@ -16,7 +16,9 @@
 // When the input is already SxS this is an exact per-pixel normalisation.
 //
 // One thread writes 8 consecutive pixels of an output row = 48 B as three
-// 16-B stores (Wr % 8 == 0 keeps every store aligned).
+// 16-B stores (Wr % 8 == 0 keeps every store aligned). In the paired layout
+// (input of the fused stem, csrc/kernels/stem_pool.hip) a pixel pair fills a
+// 16-B chunk [r g b r g b 0 0] and the 8 pixels are four 16-B stores.
 #include "common.h"
 #include "kernels.h"
 
@@ -31,6 +33,7 @@ struct PreParams {
   float sy_scale, sx_scale;
   int oy, ox;
   bool identity;
+  bool paired;  // 2 pixels per 16 B: [r g b r g b 0 0]
 };
 
 __device__ __forceinline__ void pixel(const uint8_t* __restrict__ img, const PreParams& p, int y, int x,
@@ -80,20 +83,32 @@ __global__ __launch_bounds__(256) void preprocess_kernel(const uint8_t* __restri
     const int b = (int)(t / p.P);
     const uint8_t* img = x + (long)b * p.Hin * p.Win * 3;
     const int iy = hy - p.pad;
-    float v[24];
+    if (p.paired) {
+      float v[32];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) pixel(img, p, iy, g * 8 + i - p.pad, v + 3 * i);
-    uint4* dst = (uint4*)(y + idx * 24);
-    dst[0] = pack8(v);
-    dst[1] = pack8(v + 8);
-    dst[2] = pack8(v + 16);
+      for (int i = 0; i < 8; ++i) pixel(img, p, iy, g * 8 + i - p.pad, v + 8 * (i >> 1) + 3 * (i & 1));
+      uint4* dst = (uint4*)(y + idx * 32);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        v[8 * q + 6] = v[8 * q + 7] = 0.f;
+        dst[q] = pack8(v + 8 * q);
+      }
+    } else {
+      float v[24];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) pixel(img, p, iy, g * 8 + i - p.pad, v + 3 * i);
+      uint4* dst = (uint4*)(y + idx * 24);
+      dst[0] = pack8(v);
+      dst[1] = pack8(v + 8);
+      dst[2] = pack8(v + 16);
+    }
   }
 }
 
 }  // namespace
 
 void preprocess_u8(const uint8_t* x, void* y, int B, int Hin, int Win, int S, int pad, int Wr,
-                   hipStream_t s) {
+                   hipStream_t s, bool paired) {
   if (B <= 0) return;
   if (Hin <= 0 || Win <= 0 || S <= 0 || pad < 0 || Wr < S + 2 * pad || Wr % 8 != 0)
     throw std::invalid_argument("preprocess_u8: bad dims");
@@ -119,6 +134,7 @@ void preprocess_u8(const uint8_t* x, void* y, int B, int Hin, int Win, int S, in
   p.sy_scale = (float)Hin / RH;
   p.sx_scale = (float)Win / RW;
   p.identity = (Hin == S && Win == S);
+  p.paired = paired;
   const long total = (long)B * p.P * (Wr / 8);
   const int blocks = (int)std::min<long>((total + 255) / 256, 16384);
   hipLaunchKernelGGL(preprocess_kernel, dim3(blocks), dim3(256), 0, s, x, (bf16*)y, p);

@@ -1,0 +1,319 @@
+// Fused ResNet stem: conv 7x7/s2/p3 (BN folded) + ReLU + maxpool 3x3/s2/p1
+// in one kernel, image in, pooled [B, Ho/2, Wo/2, 64] bf16 NHWC out.
+//
+// Reference equivalent: the first four modules of tch::vision::resnet18's
+// forward (conv1, bn1, relu, maxpool) run by `forward_t` per query at
+// src/services.rs:493. As two kernels (implicit-GEMM conv, then maxpool) the
+// stem is the most memory-bound stage of ResNet18: the 112x112x64 conv
+// output is written and re-read (2 x 411 MB at B=256) and the im2col tile
+// re-fetches every input pixel ~12x from L2. Here each workgroup walks a
+// strip of pooled rows of one image top to bottom:
+//
+//  * Input: the "paired" image from preprocess_u8(paired=true): rows of
+//    Wq 16-B chunks, chunk p = padded pixels (2p, 2p+1) as [r g b r g b 0 0].
+//    With stride 2, output column ow reads kernel row kh as the 4 chunks
+//    p = ow..ow+3, so a 32-wide K step is exactly one kernel row and every
+//    MFMA operand is one aligned ds_read_b128 straight from the staged input
+//    row (no im2col copy). K = 7 rows x 32 = 224; weights are zero on the
+//    pad slots (e = 6,7 and kw = 7).
+//  * Staging: input rows go HBM -> LDS with global_load_lds_dwordx4 into a
+//    ring of 21 rows; a step needs 13, the 8 rows of the next step are in
+//    flight while the current one computes.
+//  * Compute: 4 waves, wave w = one conv row, all 64 channels; weights
+//    (64 x 224) live in registers for the whole kernel. D = X x W, so each
+//    lane holds 4 consecutive output columns of one channel.
+//  * Pool: the horizontal 3-max is then mostly lane-local: columns
+//    4g..4g+3 of a lane give pooled columns 2g (plus column 4g-1, fetched
+//    with one ds_bpermute from the lane 16 below) and 2g+1. +bias and ReLU
+//    are applied after the max (both monotone, so they commute with it),
+//    and the results go to a 5-row LDS ring of pooled conv rows ([pw][64 ch],
+//    16-B channel chunks XOR-swizzled by pw so the 4 row groups of a wave
+//    hit different banks). The vertical 3-max over that ring writes two
+//    pooled rows per step as 16-B stores. Post-ReLU values are >= 0, so
+//    bf16 max is an unsigned 16-bit max and the zero row above the image is
+//    neutral.
+//
+// Step t of a strip starting at pooled row ph0 computes conv rows
+// c0 = 2*ph0 - 4 + 4t .. c0+3; step 0 only computes row 2*ph0-1 (the top
+// halo), steps >= 1 emit pooled rows ph0 + 2(t-1) and ph0 + 2(t-1) + 1.
+#include "common.h"
+#include "kernels.h"
+
+#include <algorithm>
+#include <cstdlib>
+#include <string>
+
+namespace dmlc {
+
+namespace {
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef const __attribute__((address_space(1))) void* gbl_ptr_t;
+typedef unsigned short ushort8 __attribute__((ext_vector_type(8)));
+typedef float float2v __attribute__((ext_vector_type(2)));
+typedef short short2v __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+constexpr int kRing = 21;  // staged input rows: 13 for a step + 8 in flight
+constexpr int kHp = 5;     // horizontally pooled conv rows: carried halo + 4
+constexpr int kK = 224;    // 7 kernel rows x 4 chunks x 8
+// Pooled-row LDS layout: [pw][64 ch] with a 144-B column stride (128 + 16 pad):
+// the 4 row groups of a wave write columns 2 apart = 288 B = 8 banks apart,
+// so the 16-bit stores are conflict-free and every address is a per-lane
+// base plus an immediate.
+constexpr int kHpCol = 144;
+
+struct StemArgs {
+  const bf16* x;      // [B, Hp, Wq, 8]
+  const bf16* w;      // [64, 224]
+  const float* bias;  // [64]
+  bf16* y;            // [B, PH, PW, 64]
+  int Hp, Wq, PH, PW, strip;
+};
+
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+
+// LDS address of a pointer into __shared__ memory.
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
+// 16-bit LDS stores issued as inline asm: the compiler's waitcnt pass would
+// otherwise put an s_waitcnt vmcnt(0) in front of every LDS store (it cannot
+// tell them apart from the in-flight LDS-DMA of the input ring), stalling
+// the epilogue on the next step's prefetch. lds_barrier() waits lgkmcnt(0).
+// `off` must fold to a constant (it becomes the instruction's offset field).
+__device__ __forceinline__ void ds_write_lo16(uint32_t addr, uint32_t v, const int off) {
+  asm volatile("ds_write_b16 %0, %1 offset:%2" ::"v"(addr), "v"(v), "i"(off));
+}
+__device__ __forceinline__ void ds_write_hi16(uint32_t addr, uint32_t v, const int off) {
+  asm volatile("ds_write_b16_d16_hi %0, %1 offset:%2" ::"v"(addr), "v"(v), "i"(off));
+}
+
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+}
+
+template <int NF, bool PF>
+__global__ __launch_bounds__(256, 2) void stem_conv_pool_kernel(
+    StemArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint4 smem[];
+  const int RB = a.Wq * 16;  // bytes per staged input row
+  char* ring = (char*)smem;
+  char* hp = ring + kRing * RB;
+  const int HPB = a.PW * kHpCol;  // bytes per pooled conv row
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: row math in SGPRs
+  const int fr = lane & 15, fq = lane >> 4;
+  const int strips = a.PH / a.strip;
+  const int b = blockIdx.x / strips;
+  const int ph0 = (blockIdx.x - b * strips) * a.strip;
+  const int T = a.strip / 2;  // steps 1..T emit pooled rows
+  const bf16* img = a.x + (long)b * a.Hp * a.Wq * 8;
+
+  // This wave's share of a row list [lo, lo+cnt): rows lo+wave, lo+wave+4, ...
+  auto load_rows = [&](int lo, int cnt) __attribute__((always_inline)) {
+    for (int i = wave; i < cnt; i += 4) {
+      const int r = lo + i;
+      if (r < 0) continue;
+      const bf16* src = img + (long)r * a.Wq * 8;
+      char* dst = ring + (r % kRing) * RB;
+      for (int c0 = 0; c0 < a.Wq; c0 += 64) {
+        if (c0 + lane < a.Wq)
+          __builtin_amdgcn_global_load_lds((gbl_ptr_t)(src + (c0 + lane) * 8), (lds_ptr_t)(dst + c0 * 16), 16, 0,
+                                           0);
+      }
+    }
+  };
+
+  // Weights in registers: wf[n][s] = W[16n + fr][32s + 8fq .. +8].
+  bf16x8 wf[4][7];
+#pragma unroll
+  for (int n = 0; n < 4; ++n)
+#pragma unroll
+    for (int s = 0; s < 7; ++s)
+      wf[n][s] = *(const bf16x8*)(a.w + (n * 16 + fr) * kK + s * 32 + fq * 8);
+  float bs[4];
+#pragma unroll
+  for (int n = 0; n < 4; ++n) bs[n] = a.bias[n * 16 + fr];
+
+  // Prologue: rows for step 0 (the 13 rows of c0(0), negative ones skipped).
+  load_rows(4 * ph0 - 8, 13);
+  vm_wait<0>();
+  __builtin_amdgcn_s_barrier();
+
+  for (int t = 0; t <= T; ++t) {
+    const int c0 = 2 * ph0 - 4 + 4 * t;
+    if (t < T) load_rows(2 * c0 + 13, 8);  // next step's new rows
+
+    const int cr = c0 + wave;  // this wave's conv row
+    char* hrow = hp + ((cr + kHp) % kHp) * HPB;
+    if (t > 0 || wave == 3) {
+      if (cr < 0) {  // row above the image: neutral zero row for the max
+        for (int o = lane * 16; o < HPB; o += 64 * 16) *(uint4*)(hrow + o) = make_uint4(0, 0, 0, 0);
+      } else {
+        // Fragment-major: the 28 MFMAs of output columns 16f..16f+15 (7
+        // kernel rows x 4 channel blocks), then that fragment's pooling
+        // epilogue, which the scheduler can overlap with fragment f+1's
+        // MFMAs. Only two fragments' accumulators are ever live.
+        const char* rbase = ring + (fr + fq) * 16;
+        int rows[7];
+#pragma unroll
+        for (int s = 0; s < 7; ++s) rows[s] = ((2 * cr + s) % kRing) * RB;
+        // per-lane store base: column 2g, channel chunk r/8, element r%8
+        const uint32_t hbase = lds_addr(hrow) + fq * 2 * kHpCol + (fr >> 3) * 16 + (fr & 7) * 2;
+        const int nb_addr = ((lane + 48) & 63) << 2;  // read lane (l - 16) mod 64
+        float prev3[4];  // column 16f+15 of the previous fragment, per channel block
+        bf16x8 xf[7], xg[7];
+#pragma unroll
+        for (int s = 0; s < 7; ++s) xf[s] = *(const bf16x8*)(rbase + rows[s]);
+#pragma unroll
+        for (int f = 0; f < NF; ++f) {
+          if (PF && f + 1 < NF) {  // next fragment's operands, in flight during this one's MFMAs
+#pragma unroll
+            for (int s = 0; s < 7; ++s) xg[s] = *(const bf16x8*)(rbase + rows[s] + (f + 1) * 256);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+          floatx4 acc[4];
+#pragma unroll
+          for (int n = 0; n < 4; ++n) acc[n] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int s = 0; s < 7; ++s)
+#pragma unroll
+            for (int n = 0; n < 4; ++n)
+              acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[s], wf[n][s], acc[n], 0, 0, 0);
+          // Horizontal 3-max over columns (2pw-1, 2pw, 2pw+1), + bias, ReLU.
+          // Lane (r, g) holds columns 16f + 4g + i (i = 0..3) of channel
+          // 16n + r: pooled columns 8f + 2g (needs column 16f + 4g - 1, the
+          // i = 3 value of row g-1, or of row 3 of fragment f-1 when g = 0)
+          // and 8f + 2g + 1 (own values only).
+#pragma unroll
+          for (int n = 0; n < 4; ++n) {
+            const floatx4 v = acc[n];
+            const float src = (f > 0 && fq == 3) ? prev3[n] : v[3];
+            float nb = __int_as_float(__builtin_amdgcn_ds_bpermute(nb_addr, __float_as_int(src)));
+            if (f == 0) nb = fq == 0 ? v[0] : nb;  // first image column: no left neighbour
+            float2v p = {fmaxf(fmaxf(nb, v[0]), v[1]), fmaxf(fmaxf(v[1], v[2]), v[3])};
+            p += float2v{bs[n], bs[n]};
+            // ReLU after rounding: bf16 bits as int16, max with 0 (also maps -0 to +0)
+            const short2v q = __builtin_elementwise_max(
+                __builtin_bit_cast(short2v, __builtin_convertvector(p, bf16x2)), short2v{0, 0});
+            const uint32_t packed = __builtin_bit_cast(uint32_t, q);
+            ds_write_lo16(hbase, packed, f * 8 * kHpCol + n * 32);
+            ds_write_hi16(hbase, packed, f * 8 * kHpCol + n * 32 + kHpCol);
+            prev3[n] = v[3];
+          }
+          if (f + 1 < NF) {
+#pragma unroll
+            for (int s = 0; s < 7; ++s)
+              xf[s] = PF ? xg[s] : *(const bf16x8*)(rbase + rows[s] + (f + 1) * 256);
+          }
+        }
+      }
+    }
+    lds_barrier();
+
+    // Stores this wave issues below (wave-uniform: 16*PW items, PW % 8 == 0).
+    const int items = 16 * a.PW;
+    const int nst = t > 0 ? __builtin_amdgcn_readfirstlane(tid < items ? (items - 1 - tid) / 256 + 1 : 0) : 0;
+    if (t > 0) {  // vertical 3-max -> pooled rows ph, ph+1
+      const int ph = ph0 + 2 * (t - 1);
+      const int per_row = a.PW * 8;
+      ushort8 m[4];  // 16*PW <= 1024 items: at most 4 per thread, reads issued together
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int it = tid + j * 256;
+        if (it < 2 * per_row) {
+          const int pr = it >= per_row;
+          const int rem = it - pr * per_row;
+          const int pw = rem >> 3, cg = rem & 7;
+          const int r1 = 2 * (ph + pr) - 1;
+          const int off = pw * kHpCol + cg * 16;
+          const ushort8 v1 = *(const ushort8*)(hp + ((r1 + kHp) % kHp) * HPB + off);
+          const ushort8 v2 = *(const ushort8*)(hp + ((r1 + 1) % kHp) * HPB + off);
+          const ushort8 v3 = *(const ushort8*)(hp + ((r1 + 2) % kHp) * HPB + off);
+          m[j] = __builtin_elementwise_max(__builtin_elementwise_max(v1, v2), v3);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int it = tid + j * 256;
+        if (it < 2 * per_row) {
+          const int pr = it >= per_row;
+          const int rem = it - pr * per_row;
+          *(ushort8*)(a.y + (((long)b * a.PH + ph + pr) * a.PW + (rem >> 3)) * 64 + (rem & 7) * 8) = m[j];
+        }
+      }
+    }
+    // The next step's rows have landed. vmcnt retires in issue order, so
+    // leaving this step's `nst` younger stores in flight still covers the DMA.
+    switch (nst) {
+      case 0: vm_wait<0>(); break;
+      case 1: vm_wait<1>(); break;
+      case 2: vm_wait<2>(); break;
+      case 3: vm_wait<3>(); break;
+      default: vm_wait<4>(); break;
+    }
+    lds_barrier();
+  }
+}
+
+}  // namespace
+
+int stem_pool_pick_strip(int B, int PH, int num_cus) {
+  // Largest even divisor of PH whose grid still gives every CU two
+  // workgroups (2 fit per CU: 256 VGPRs, ~80 KB LDS each at 224x224).
+  int best = 2;
+  for (int s = 2; s <= PH; s += 2) {
+    if (PH % s) continue;
+    if ((long)B * (PH / s) >= 2L * num_cus) best = s;
+  }
+  return best;
+}
+
+void stem_conv_pool(const void* x, const void* w, const float* bias, void* y, int B, int S, int Wq, int strip,
+                    hipStream_t s) {
+  if (B <= 0) return;
+  const int Ho = S / 2, PH = Ho / 2;
+  const int NF = Ho / 16;
+  if (S % 32 != 0 || NF < 4 || NF > 8) throw std::invalid_argument("stem_conv_pool: image size must be 128..256, %32");
+  if (Wq < Ho + 3 || Wq > 512) throw std::invalid_argument("stem_conv_pool: bad paired row width");
+  if (strip < 2 || strip % 2 || PH % strip) throw std::invalid_argument("stem_conv_pool: bad strip");
+  if (!x || !w || !bias || !y || ((uintptr_t)x & 15) || ((uintptr_t)w & 15) || ((uintptr_t)y & 15))
+    throw std::invalid_argument("stem_conv_pool: null / misaligned operand");
+  StemArgs a;
+  a.x = (const bf16*)x;
+  a.w = (const bf16*)w;
+  a.bias = bias;
+  a.y = (bf16*)y;
+  a.Hp = S + 6;
+  a.Wq = Wq;
+  a.PH = PH;
+  a.PW = PH;
+  a.strip = strip;
+  const size_t lds = (size_t)kRing * Wq * 16 + (size_t)kHp * a.PW * kHpCol;
+  const dim3 grid(B * (PH / strip));
+  static const bool pf = [] {
+    const char* e = std::getenv("DMLC_STEM_PREFETCH");
+    return e && std::string(e) == "1";
+  }();
+  switch (NF * 2 + pf) {
+#define DMLC_STEM_CASE(F)                                                                              \
+  case 2 * F: hipLaunchKernelGGL((stem_conv_pool_kernel<F, false>), grid, dim3(256), lds, s, a); break; \
+  case 2 * F + 1: hipLaunchKernelGGL((stem_conv_pool_kernel<F, true>), grid, dim3(256), lds, s, a); break;
+    DMLC_STEM_CASE(4)
+    DMLC_STEM_CASE(5)
+    DMLC_STEM_CASE(6)
+    DMLC_STEM_CASE(7)
+    DMLC_STEM_CASE(8)
+#undef DMLC_STEM_CASE
+  }
+  DMLC_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace dmlc

@@ -48,6 +48,7 @@ Engine::Engine(const std::string& arch, const WeightMap& weights, int device, in
   DMLC_HIP_CHECK(hipGetDeviceProperties(&prop, device_));
   num_cus_ = prop.multiProcessorCount;
   if (const char* e = std::getenv("DMLC_PERSISTENT")) persistent_ = std::string(e) != "0";
+  if (const char* e = std::getenv("DMLC_FUSED_STEM")) fused_stem_ = std::string(e) != "0";
 
   if (arch == "resnet18")
     build_resnet({2, 2, 2, 2}, false);
@@ -138,10 +139,30 @@ int Engine::fc(int in, const std::string& name, int cout, bool relu, bool last) 
 void Engine::build_resnet(const std::vector<int>& blocks, bool bottleneck) {
   const int S = image_size_;
   stem_pad_ = 3;  // packed RGB image with the 7x7/s2 stem's padding built in
-  int x = add_act(ActShape{S + 6, stem_row_width(S, 3, 7, 2), 3, false});
-  ops_.push_back(Op{OpType::Preprocess, -1, x, -1, -1, 0, 0, 3, "preprocess"});
-  x = conv(x, "conv1", "bn1", 64, 7, 2, 0, true);
-  {
+  int x;
+  if (fused_stem_ && S % 32 == 0 && S >= 128 && S <= 256) {
+    // paired image -> one kernel for conv1 + bn1 + relu + maxpool
+    const int pairs = stem_row_width(S, 3, 7, 2) / 2;
+    x = add_act(ActShape{S + 6, pairs, 8, false});
+    ops_.push_back(Op{OpType::Preprocess, -1, x, -1, -1, 1, 0, 3, "preprocess"});
+    ConvLayer L;
+    L.name = "conv1";
+    L.bn = "bn1";
+    L.stem_pool = true;
+    L.cin = L.cin_eff = 3;
+    L.cout = 64;
+    L.kh = L.kw = 7;
+    L.stride = 2;
+    L.pad = 3;
+    L.relu = true;
+    convs_.push_back(L);
+    const int y = add_act(ActShape{S / 4, S / 4, 64, false});
+    ops_.push_back(Op{OpType::StemPool, x, y, -1, (int)convs_.size() - 1, 0, 0, 0, "conv1+maxpool"});
+    x = y;
+  } else {
+    x = add_act(ActShape{S + 6, stem_row_width(S, 3, 7, 2), 3, false});
+    ops_.push_back(Op{OpType::Preprocess, -1, x, -1, -1, 0, 0, 3, "preprocess"});
+    x = conv(x, "conv1", "bn1", 64, 7, 2, 0, true);
     const ActShape s = shapes_[x];
     const int y = add_act(ActShape{conv_out_dim(s.H, 3, 2, 1), conv_out_dim(s.W, 3, 2, 1), s.C, false});
     ops_.push_back(Op{OpType::MaxPool, x, y, -1, -1, 3, 2, 1, "maxpool"});
@@ -216,7 +237,7 @@ void Engine::pack_weights(const WeightMap& w) {
   size_t off = 0;
   for (auto& L : convs_) {
     L.npad = conv_npad(L.cout);
-    L.kpad = conv_kpad(L.cin_eff, L.kh, L.kw, L.pair);
+    L.kpad = L.stem_pool ? kStemPoolK : conv_kpad(L.cin_eff, L.kh, L.kw, L.pair);
     L.w_off = off;
     off = align_up(off + (size_t)L.npad * L.kpad * 2, 256);
     L.b_off = off;
@@ -255,7 +276,9 @@ void Engine::pack_weights(const WeightMap& w) {
             for (int j = 0; j < L.kw; ++j) {
               const float v = W.data[(((size_t)n * L.cin + c) * L.kh + i) * L.kw + j] * scale[n];
               size_t k;
-              if (L.pair)  // stem: k = kh*CPK*8 + kw*3 + c
+              if (L.stem_pool)  // paired stem: chunk (kw/2) of row kh, slot 3*(kw%2) + c
+                k = (size_t)i * 32 + (j / 2) * 8 + (j % 2) * 3 + c;
+              else if (L.pair)  // stem: k = kh*CPK*8 + kw*3 + c
                 k = (size_t)i * ((L.kw * 3 + 7) / 8) * 8 + j * 3 + c;
               else
                 k = (size_t)(i * L.kw + j) * L.cin_eff + c;
@@ -307,9 +330,10 @@ void Engine::reserve(int max_batch) {
 double Engine::gflop_per_image() const {
   double f = 0;
   for (const auto& op : ops_) {
-    if (op.type != OpType::Conv) continue;
+    if (op.type != OpType::Conv && op.type != OpType::StemPool) continue;
     const ConvLayer& L = convs_[op.conv];
-    const ActShape& o = shapes_[op.out];
+    ActShape o = shapes_[op.out];
+    if (op.type == OpType::StemPool) o.H = o.W = image_size_ / 2;  // the conv's (pre-pool) output
     f += 2.0 * o.H * o.W * L.cout * (double)L.cin * L.kh * L.kw;
   }
   return f * 1e-9;
@@ -364,12 +388,22 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
   if (evs) DMLC_HIP_CHECK(hipEventRecord((*evs)[ei++], s));
   for (const Op& op : ops_) {
     switch (op.type) {
-      case OpType::Preprocess:
-        preprocess_u8(images, acts_[op.out], B, Hin, Win, image_size_, op.pad, shapes_[op.out].W, s);
+      case OpType::Preprocess: {
+        const bool paired = op.k == 1;
+        const int Wr = paired ? 2 * shapes_[op.out].W : shapes_[op.out].W;
+        preprocess_u8(images, acts_[op.out], B, Hin, Win, image_size_, op.pad, Wr, s, paired);
         break;
+      }
       case OpType::Conv:
         conv2d_igemm(conv_args(op, B, logits), s);
         break;
+      case OpType::StemPool: {
+        const ConvLayer& L = convs_[op.conv];
+        stem_conv_pool(acts_[op.in], (const uint8_t*)warena_ + L.w_off,
+                       (const float*)((const uint8_t*)warena_ + L.b_off), acts_[op.out], B, image_size_,
+                       shapes_[op.in].W, stem_pool_pick_strip(B, shapes_[op.out].H, num_cus_), s);
+        break;
+      }
       case OpType::MaxPool: {
         const ActShape& i = shapes_[op.in];
         const ActShape& o = shapes_[op.out];

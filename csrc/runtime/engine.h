@@ -20,7 +20,7 @@
 
 namespace dmlc {
 
-enum class OpType { Preprocess, Conv, MaxPool, AvgPoolGlobal, AvgPoolAdaptive, SoftmaxTop1 };
+enum class OpType { Preprocess, Conv, StemPool, MaxPool, AvgPoolGlobal, AvgPoolAdaptive, SoftmaxTop1 };
 
 struct ActShape {
   int H = 0, W = 0, C = 0;
@@ -35,6 +35,7 @@ struct ConvLayer {
   bool relu = false;
   bool fc = false;        // linear layer (weight [N,K]) run as a 1x1 conv
   bool pair = false;      // stem conv on the preprocess packed-RGB image (8 (kw,c) values / 16 B)
+  bool stem_pool = false; // fused ResNet stem (conv+maxpool) on the paired image, K = 224
   int fc_hwc[3] = {0, 0, 0};  // for fc after a spatial tensor: (H,W,C) of the flatten
   int npad = 0, kpad = 0;
   size_t w_off = 0, b_off = 0;  // offsets (bytes) into the weight arena
@@ -44,7 +45,7 @@ struct Op {
   OpType type;
   int in = -1, out = -1, res = -1;  // activation ids
   int conv = -1;
-  int k = 0, stride = 0, pad = 0;
+  int k = 0, stride = 0, pad = 0;  // Preprocess: k = 1 for the paired layout
   std::string name;
 };
 
@@ -108,6 +109,7 @@ class Engine {
   int max_batch_ = 0;
   int stem_pad_ = 0;
   bool persistent_ = true;  // persistent conv grids (env DMLC_PERSISTENT=0 disables)
+  bool fused_stem_ = true;  // conv1+maxpool as one kernel (env DMLC_FUSED_STEM=0 disables)
 
   std::vector<ActShape> shapes_;
   std::vector<ConvLayer> convs_;

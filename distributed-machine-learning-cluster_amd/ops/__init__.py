@@ -139,17 +139,68 @@ def avgpool_adaptive(x: torch.Tensor, ho: int, wo: int) -> torch.Tensor:
     return y
 
 
-def preprocess_u8(images: torch.Tensor, size: int = 224, pad: int = 0, row_width: int | None = None) -> torch.Tensor:
+def preprocess_u8(images: torch.Tensor, size: int = 224, pad: int = 0, row_width: int | None = None,
+                  paired: bool = False) -> torch.Tensor:
     """u8 [B,H,W,3] -> bf16 packed RGB [B, size+2p, row_width, 3] (resize,
-    crop, normalise; zero border; see ``stem_image``)."""
+    crop, normalise; zero border; see ``stem_image``). With ``paired`` the
+    result is [B, size+2p, row_width/2, 8]: pixel pairs as [r g b r g b 0 0]
+    (``paired_image``), the fused stem's input."""
     _need_cuda(images)
     if images.dtype != torch.uint8 or images.dim() != 4 or images.shape[-1] != 3:
         raise ValueError("preprocess_u8 expects uint8 [B,H,W,3]")
     B, H, W, _ = images.shape
     P = size + 2 * pad
     Wr = row_width or (P + 7) // 8 * 8
-    y = torch.empty(B, P, Wr, 3, device=images.device, dtype=torch.bfloat16)
-    native().preprocess_u8(_ptr(images.contiguous()), _ptr(y), B, H, W, size, pad, Wr, _stream())
+    shape = (B, P, Wr // 2, 8) if paired else (B, P, Wr, 3)
+    y = torch.empty(*shape, device=images.device, dtype=torch.bfloat16)
+    native().preprocess_u8(_ptr(images.contiguous()), _ptr(y), B, H, W, size, pad, Wr, _stream(), paired)
+    return y
+
+
+def paired_image(x_nhwc3: torch.Tensor, pad: int = 3, pairs: int | None = None) -> torch.Tensor:
+    """Reference construction of the fused stem's input: the zero-padded
+    image [B, H+2p, 2*pairs, 3] regrouped as [B, H+2p, pairs, 8] with
+    chunk = [r g b r g b 0 0] of pixels (2q, 2q+1)."""
+    B, H, W, _ = x_nhwc3.shape
+    pairs = pairs or ((W + 2 * pad + 7) // 8 * 4)
+    img = stem_image(x_nhwc3, pad, 2 * pairs)
+    out = torch.zeros(B, H + 2 * pad, pairs, 8, dtype=x_nhwc3.dtype, device=x_nhwc3.device)
+    out[..., :6] = img.reshape(B, H + 2 * pad, pairs, 6)
+    return out
+
+
+def pack_stem_pool_weight(w: torch.Tensor, scale: torch.Tensor | None = None, device=None) -> torch.Tensor:
+    """[64, 3, 7, 7] fp32 -> bf16 [64, 224] for ``stem_conv_pool``:
+    k = kh*32 + q*8 + e with kw = 2q + e//3, c = e%3 (e < 6, kw < 7)."""
+    cout, cin, kh, kw = w.shape
+    if (cout, cin, kh, kw) != (64, 3, 7, 7):
+        raise ValueError("stem_conv_pool packs a [64, 3, 7, 7] weight")
+    w = w.float()
+    if scale is not None:
+        w = w * scale.float().view(-1, 1, 1, 1)
+    wk = torch.zeros(64, 7, 8, 3)  # [n, kh, kw (8 slots), c]
+    wk[:, :, :7] = w.permute(0, 2, 3, 1)
+    out = torch.zeros(64, 7, 4, 8)
+    out[..., :6] = wk.reshape(64, 7, 4, 6)
+    out = out.reshape(64, 224).to(torch.bfloat16)
+    return out.to(device) if device is not None else out
+
+
+def stem_conv_pool(x_paired: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, size: int = 224,
+                   strip: int | None = None) -> torch.Tensor:
+    """Fused conv7x7/s2 + bias + ReLU + maxpool3x3/s2/p1 on the paired image
+    (``preprocess_u8(..., pad=3, paired=True)``). Returns [B, size/4, size/4, 64]."""
+    _need_cuda(x_paired, w_packed, bias)
+    C = native()
+    B, P, Wq, eight = x_paired.shape
+    if eight != 8 or P != size + 6:
+        raise ValueError("stem_conv_pool expects a paired [B, size+6, Wq, 8] image")
+    ph = size // 4
+    if strip is None:
+        strip = C.stem_pool_pick_strip(B, ph, torch.cuda.get_device_properties(x_paired.device).multi_processor_count)
+    y = torch.empty(B, ph, ph, 64, device=x_paired.device, dtype=torch.bfloat16)
+    C.stem_conv_pool(_ptr(x_paired.contiguous()), _ptr(w_packed.contiguous()), _ptr(bias.float().contiguous()),
+                     _ptr(y), B, size, Wq, strip, _stream())
     return y
 
 

@@ -135,6 +135,39 @@ def test_conv2d_stem_packed(gpu, k, s, p, cout, hw):
     assert _rel(_nchw(y.float().cpu()), ref) < 8e-3
 
 
+@pytest.mark.parametrize("B,S,strip", [(3, 224, None), (2, 224, 2), (2, 224, 14), (1, 224, 56),
+                                       (2, 128, None), (1, 256, 8), (4, 192, 6)])
+def test_stem_conv_pool(gpu, B, S, strip):
+    """Fused conv7x7/s2/p3 + bias + ReLU + maxpool3x3/s2/p1 (stem_pool.hip)
+    vs torch fp32 on the same bf16-rounded image and weights."""
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(B, 3, S, S, generator=g).bfloat16().float()
+    w = (torch.randn(64, 3, 7, 7, generator=g) / 147 ** 0.5).bfloat16().float()
+    bias = torch.randn(64, generator=g) * 0.1
+    ref = F.max_pool2d(F.relu(F.conv2d(x, w, bias, 2, 3)), 3, 2, 1)
+    xp = ops.paired_image(_nhwc(x), 3).bfloat16().to(gpu)
+    wp = ops.pack_stem_pool_weight(w, device=gpu)
+    y = ops.stem_conv_pool(xp, wp, bias.to(gpu), S, strip)
+    torch.cuda.synchronize()
+    got = _nchw(y.float().cpu())
+    assert got.shape == ref.shape
+    assert _rel(got, ref) < 5e-3, _rel(got, ref)
+    assert (got - ref).abs().max().item() < 0.05
+
+
+def test_preprocess_paired(gpu):
+    g = torch.Generator().manual_seed(12)
+    img = torch.randint(0, 256, (2, 224, 224, 3), generator=g, dtype=torch.uint8)
+    ref = _nhwc((_nchw(img.float()) / 255 - MEAN) / STD)
+    y = ops.preprocess_u8(img.to(gpu), 224, 3, 232, paired=True)
+    torch.cuda.synchronize()
+    assert y.shape == (2, 230, 116, 8)
+    exp = ops.paired_image(ref, 3, 116)
+    y = y.float().cpu()
+    assert _rel(y, exp) < 4e-3
+    assert torch.all(y[..., 6:] == 0)
+
+
 def test_linear_fp32_out(gpu):
     """FC = 1x1 conv on [B,1,1,K]; N=1000 padded to 1024, fp32 logits."""
     g = torch.Generator().manual_seed(3)

@@ -72,6 +72,12 @@ HIPCC_FLAGS = [
 ]
 
 
+# Per-file extra flags. The fused stem's max-pool epilogue works on finite
+# conv outputs; without nnan every fmaxf is preceded by NaN-quieting
+# canonicalisations (2-3 extra VALU per max).
+HIPCC_FILE_FLAGS = {"stem_pool.hip": ["-fno-honor-nans"]}
+
+
 def gpu_objects():
     srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
     srcs += [os.path.join(CSRC, "runtime", "engine.cpp")]
@@ -94,7 +100,8 @@ def build(jobs: int = 8, verbose: bool = False, node: bool = True) -> None:
         gpu_objs.append(o)
         if _stale(o, [s], hdr):
             lang = ["-x", "hip"] if s.endswith(".hip") else []
-            steps.append(["hipcc", *HIPCC_FLAGS, *lang, "-c", s, "-o", o])
+            extra = HIPCC_FILE_FLAGS.get(os.path.basename(s), [])
+            steps.append(["hipcc", *HIPCC_FLAGS, *extra, *lang, "-c", s, "-o", o])
 
     host_flags = [
         "-O2", "-std=c++17", "-fPIC", f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-D__HIP_PLATFORM_AMD__",
