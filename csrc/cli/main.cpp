@@ -9,7 +9,7 @@
 //   predict, jobs, assign
 // and the same output strings. Everything the reference hard-codes (hosts,
 // ports, periods, replication factor, paths) is a flag here, so any number
-// of nodes run on one machine; extra verbs: fault, info, sleep, quit.
+// of nodes run on one machine; extra verbs: fault, info, prefetch, sleep, quit.
 //
 // Sub-commands: `dmlc-node selftest` (C++ unit tests) and
 // `dmlc-node classify --model M --weights W.ot --labels L --image I.JPEG`
@@ -292,6 +292,16 @@ void handle_line(Node& n, const std::string& line) {
       out_line("id " + n.ms->id().address + " leader " + n.member->leader_address() + " executor " +
                (n.member->executor() ? n.member->executor()->backend() : std::string("none")) + " sent " +
                std::to_string(n.ms->sent()) + " received " + std::to_string(n.ms->received()));
+      if (Executor* ex = n.member->executor()) {
+        const CacheStats cs = ex->cache_stats();
+        out_line("cache hits " + std::to_string(cs.hits) + " misses " + std::to_string(cs.misses) + " staged " +
+                 std::to_string(cs.staged) + " evictions " + std::to_string(cs.evictions) + " entries " +
+                 std::to_string(cs.entries) + " bytes " + std::to_string(cs.bytes) + " capacity " +
+                 std::to_string(cs.capacity) + " prefetched " + std::to_string(n.member->prefetched()));
+      }
+    } else if (c == "prefetch") {
+      // stage the dataset's query images into the executor's (HBM) cache
+      out_line(n.member->start_prefetch() ? "prefetch started" : "prefetch unavailable or running");
     } else if (c == "sleep") {
       if (t.size() == 2) std::this_thread::sleep_for(std::chrono::milliseconds(std::stoi(t[1])));
     } else if (c == "quit" || c == "exit") {
@@ -333,7 +343,8 @@ int run_node(const Args& a) {
 
   std::unique_ptr<Executor> ex;
   try {
-    ex = make_executor(a.get("executor", "auto"), a.geti("device", 0), a.geti("max-batch", 64));
+    ex = make_executor(a.get("executor", "auto"), a.geti("device", 0), a.geti("max-batch", 64),
+                       (size_t)a.geti("hbm-cache-mb", 4096) << 20);
     if (ex) load_models(ex.get(), a.get("models", ""));
   } catch (const std::exception& e) {
     err_line(std::string("executor unavailable: ") + e.what());
@@ -347,6 +358,7 @@ int run_node(const Args& a) {
   mcfg.check_ms = a.geti("bg-ms", 3000);
   n->member = std::make_unique<MemberService>(mcfg, n->ms.get(), std::move(ex), labels);
   n->member->start(n->base_port);
+  if (a.has("prefetch")) n->member->start_prefetch();
 
   bool candidate = false;
   for (const auto& l : leaders) candidate |= (l == self);
@@ -426,6 +438,7 @@ int main(int argc, char** argv) {
                  "                 [--rf 4] [--ping-ms 1000] [--fail-ms 3000] [--bg-ms 3000]\n"
                  "                 [--query-interval-ms 500] [--query-batch 1] [--jobs resnet18,alexnet]\n"
                  "                 [--join h:p] [--daemon] [--stay] [--quiet-predictions]\n"
+                 "                 [--max-batch 64] [--hbm-cache-mb 4096] [--prefetch]\n"
                  "       dmlc-node selftest\n"
                  "       dmlc-node classify --model M --weights W.ot --labels L --image I.JPEG [--executor cpu|gpu]\n";
     return 0;

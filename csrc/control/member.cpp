@@ -99,6 +99,7 @@ void MemberService::start(int base_port) {
 void MemberService::stop() {
   if (stop_.exchange(true)) return;
   if (checker_.joinable()) checker_.join();
+  if (prefetcher_.joinable()) prefetcher_.join();
   if (server_) server_->stop();
 }
 
@@ -124,17 +125,41 @@ std::vector<std::pair<double, std::string>> MemberService::predict(const std::st
   *ok = false;
   std::vector<std::pair<double, std::string>> out;
   if (!exec_ || !exec_->has_model(model)) return out;
-  std::vector<Image> imgs;
+  std::vector<std::string> paths;
   for (const auto& id : ids) {
-    const std::string dir = cfg_.dataset_dir + "/" + sanitize_filename(id);
-    const auto files = list_dir_sorted(dir);
-    if (files.empty()) continue;  // unknown id: skipped, like a failed read_dir entry
-    imgs.push_back(decode_jpeg_file(dir + "/" + files[0]));
+    std::string p = query_image(id);
+    if (!p.empty()) paths.push_back(std::move(p));  // unknown id: skipped, like a failed read_dir entry
   }
-  const auto preds = exec_->predict(model, imgs);
+  const auto preds = exec_->predict_files(model, paths);
   for (const auto& p : preds) out.emplace_back(p.prob, labels_.text(p.class_idx));
   *ok = true;
   return out;
+}
+
+std::string MemberService::query_image(const std::string& id) const {
+  // src/services.rs:485-490: the first file of test_files/imagenet_1k/train/<id>/
+  const std::string dir = cfg_.dataset_dir + "/" + sanitize_filename(id);
+  const auto files = list_dir_sorted(dir);
+  return files.empty() ? std::string() : dir + "/" + files[0];
+}
+
+bool MemberService::start_prefetch() {
+  if (!exec_ || prefetching_.exchange(true)) return false;
+  if (prefetcher_.joinable()) prefetcher_.join();
+  prefetcher_ = std::thread([this] {
+    for (size_t i = 0; i < labels_.entries.size() && !stop_; ++i) {
+      const std::string p = query_image(labels_.entries[i].first);
+      if (p.empty()) continue;
+      try {
+        if (!exec_->stage(p)) break;
+        ++prefetched_;
+      } catch (const std::exception& e) {
+        DMLC_LOG_WARN("prefetch of " << p << " failed: " << e.what());
+      }
+    }
+    prefetching_ = false;
+  });
+  return true;
 }
 
 bool MemberService::fetch(const std::string& src_host, int src_port, const std::string& src_spec,

@@ -63,7 +63,15 @@ class MemberService {
                                                       bool* ok);
   bool fetch(const std::string& src_host, int src_port, const std::string& src_spec, const std::string& dest_spec);
 
+  // Stage the dataset's query images (first file of every class directory,
+  // in label order) into the executor's cache on a background thread, so
+  // queries hit HBM-resident images. Returns false if the executor has no
+  // cache or a prefetch is already running.
+  bool start_prefetch();
+  int prefetched() const { return prefetched_.load(); }
+
  private:
+  std::string query_image(const std::string& id) const;
   void register_handlers();
   void leader_check_loop();
   bool check_leader(const std::string& addr);
@@ -78,6 +86,9 @@ class MemberService {
   std::string leader_;
   std::atomic<bool> stop_{false};
   std::thread checker_;
+  std::thread prefetcher_;
+  std::atomic<bool> prefetching_{false};
+  std::atomic<int> prefetched_{0};
 };
 
 }  // namespace ctl

@@ -5,7 +5,9 @@
 
 #include <algorithm>
 #include <cmath>
+#include <list>
 #include <map>
+#include <unordered_map>
 #include <stdexcept>
 
 #include "../runtime/engine.h"
@@ -173,16 +175,21 @@ class CpuExecutor : public Executor {
 // ------------------------------------------------------------------ GPU
 class GpuExecutor : public Executor {
  public:
-  GpuExecutor(int device, int max_batch) : device_(device), max_batch_(max_batch) {
+  GpuExecutor(int device, int max_batch, size_t cache_bytes)
+      : device_(device), max_batch_(max_batch), cache_cap_(cache_bytes) {
     DMLC_HIP_CHECK(hipSetDevice(device_));
     DMLC_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    DMLC_HIP_CHECK(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
     DMLC_HIP_CHECK(hipMalloc(&d_out_, (size_t)max_batch_ * 8));
   }
   ~GpuExecutor() override {
     hipSetDevice(device_);
+    hipDeviceSynchronize();
     engines_.clear();
+    for (auto& kv : cache_) hipFree(kv.second.dev);
     if (d_in_) hipFree(d_in_);
     if (d_out_) hipFree(d_out_);
+    if (side_) hipStreamDestroy(side_);
     if (stream_) hipStreamDestroy(stream_);
   }
   std::string backend() const override { return "gpu:" + std::to_string(device_); }
@@ -204,13 +211,117 @@ class GpuExecutor : public Executor {
 
   std::vector<Prediction> predict(const std::string& model, const std::vector<Image>& imgs) override {
     std::lock_guard<std::mutex> g(mu_);
+    Engine* e = engine(model);
+    std::vector<const void*> src(imgs.size());
+    std::vector<std::pair<int, int>> hw(imgs.size());
+    for (size_t i = 0; i < imgs.size(); ++i) {
+      src[i] = imgs[i].rgb.data();
+      hw[i] = {imgs[i].height, imgs[i].width};
+    }
+    return run(e, src, hw, hipMemcpyHostToDevice);
+  }
+
+  // HBM-resident decoded images: a hit skips the JPEG decode and the H2D
+  // copy; the batch is gathered device-to-device.
+  std::vector<Prediction> predict_files(const std::string& model, const std::vector<std::string>& paths) override {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      engine(model);  // fail fast on an unknown model
+    }
+    for (const auto& p : paths) stage_one(p, /*count_as_miss=*/true);
+    std::lock_guard<std::mutex> g(mu_);
+    Engine* e = engine(model);
+    std::vector<const void*> src(paths.size());
+    std::vector<std::pair<int, int>> hw(paths.size());
+    for (size_t i = 0; i < paths.size(); ++i) {
+      auto it = cache_.find(paths[i]);
+      if (it == cache_.end()) throw std::runtime_error("image evicted before use: " + paths[i]);
+      touch(it);
+      src[i] = it->second.dev;
+      hw[i] = {it->second.h, it->second.w};
+    }
+    return run(e, src, hw, hipMemcpyDeviceToDevice);
+  }
+
+  bool stage(const std::string& path) override {
+    stage_one(path, /*count_as_miss=*/false);
+    return true;
+  }
+
+  CacheStats cache_stats() const override {
+    std::lock_guard<std::mutex> g(mu_);
+    CacheStats c = stats_;
+    c.bytes = cache_bytes_;
+    c.entries = cache_.size();
+    c.capacity = cache_cap_;
+    return c;
+  }
+
+ private:
+  struct Entry {
+    void* dev = nullptr;
+    int h = 0, w = 0;
+    size_t bytes = 0;
+    std::list<std::string>::iterator lru;
+  };
+
+  Engine* engine(const std::string& model) {
     auto it = engines_.find(model);
     if (it == engines_.end()) throw std::runtime_error("model not loaded: " + model);
+    return it->second.get();
+  }
+
+  void touch(std::unordered_map<std::string, Entry>::iterator it) {
+    lru_.splice(lru_.begin(), lru_, it->second.lru);
+  }
+
+  // Decode (outside the lock) and upload on the side stream, so staging
+  // overlaps inference running on the main stream.
+  void stage_one(const std::string& path, bool count_as_miss) {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      auto it = cache_.find(path);
+      if (it != cache_.end()) {
+        if (count_as_miss) ++stats_.hits;
+        touch(it);
+        return;
+      }
+    }
+    const Image img = decode_jpeg_file(path);
+    const size_t bytes = img.rgb.size();
+    std::lock_guard<std::mutex> g(mu_);
+    if (cache_.count(path)) return;  // raced with another stager
+    if (count_as_miss) ++stats_.misses; else ++stats_.staged;
     DMLC_HIP_CHECK(hipSetDevice(device_));
-    std::vector<Prediction> out(imgs.size());
-    // Group same-sized images; each group is one batched forward.
+    while (!lru_.empty() && cache_bytes_ + bytes > cache_cap_) {
+      auto victim = cache_.find(lru_.back());
+      // stream-ordered free: in-flight batches on stream_ may still read it
+      DMLC_HIP_CHECK(hipFreeAsync(victim->second.dev, stream_));
+      cache_bytes_ -= victim->second.bytes;
+      cache_.erase(victim);
+      lru_.pop_back();
+      ++stats_.evictions;
+    }
+    Entry en;
+    en.h = img.height;
+    en.w = img.width;
+    en.bytes = bytes;
+    DMLC_HIP_CHECK(hipMallocAsync(&en.dev, bytes, side_));
+    DMLC_HIP_CHECK(hipMemcpyAsync(en.dev, img.rgb.data(), bytes, hipMemcpyHostToDevice, side_));
+    DMLC_HIP_CHECK(hipStreamSynchronize(side_));  // resident before it is visible
+    lru_.push_front(path);
+    en.lru = lru_.begin();
+    cache_bytes_ += bytes;
+    cache_.emplace(path, en);
+  }
+
+  // Group same-sized images; each group is one batched forward.
+  std::vector<Prediction> run(Engine* e, const std::vector<const void*>& src,
+                              const std::vector<std::pair<int, int>>& hw, hipMemcpyKind kind) {
+    DMLC_HIP_CHECK(hipSetDevice(device_));
+    std::vector<Prediction> out(src.size());
     std::map<std::pair<int, int>, std::vector<size_t>> groups;
-    for (size_t i = 0; i < imgs.size(); ++i) groups[{imgs[i].height, imgs[i].width}].push_back(i);
+    for (size_t i = 0; i < src.size(); ++i) groups[hw[i]].push_back(i);
     for (const auto& kv : groups) {
       const int H = kv.first.first, W = kv.first.second;
       const auto& ids = kv.second;
@@ -219,13 +330,11 @@ class GpuExecutor : public Executor {
         const size_t per = (size_t)H * W * 3;
         ensure_input(per * B);
         for (int b = 0; b < B; ++b)
-          DMLC_HIP_CHECK(hipMemcpyAsync((uint8_t*)d_in_ + per * b, imgs[ids[s + b]].rgb.data(), per,
-                                        hipMemcpyHostToDevice, stream_));
+          DMLC_HIP_CHECK(hipMemcpyAsync((uint8_t*)d_in_ + per * b, src[ids[s + b]], per, kind, stream_));
         int32_t* d_idx = (int32_t*)d_out_;
         float* d_prob = (float*)((int32_t*)d_out_ + max_batch_);
         // graphs only for the fixed-size serving shape; ragged sizes run eager
-        it->second->forward((const uint8_t*)d_in_, B, H, W, d_idx, d_prob, nullptr, stream_,
-                            H == 224 && W == 224);
+        e->forward((const uint8_t*)d_in_, B, H, W, d_idx, d_prob, nullptr, stream_, H == 224 && W == 224);
         std::vector<int32_t> hi(B);
         std::vector<float> hp(B);
         DMLC_HIP_CHECK(hipMemcpyAsync(hi.data(), d_idx, B * 4, hipMemcpyDeviceToHost, stream_));
@@ -237,7 +346,6 @@ class GpuExecutor : public Executor {
     return out;
   }
 
- private:
   void ensure_input(size_t bytes) {
     if (bytes <= in_bytes_) return;
     DMLC_HIP_CHECK(hipStreamSynchronize(stream_));
@@ -247,22 +355,27 @@ class GpuExecutor : public Executor {
   }
 
   int device_, max_batch_;
-  hipStream_t stream_ = nullptr;
+  hipStream_t stream_ = nullptr, side_ = nullptr;
   void* d_in_ = nullptr;
   size_t in_bytes_ = 0;
   void* d_out_ = nullptr;
   mutable std::mutex mu_;
   std::map<std::string, std::unique_ptr<Engine>> engines_;
+  std::unordered_map<std::string, Entry> cache_;
+  std::list<std::string> lru_;
+  size_t cache_bytes_ = 0, cache_cap_;
+  CacheStats stats_;
 };
 
 }  // namespace
 
-std::unique_ptr<Executor> make_executor(const std::string& backend, int device, int max_batch) {
+std::unique_ptr<Executor> make_executor(const std::string& backend, int device, int max_batch,
+                                        size_t cache_bytes) {
   std::string b = backend;
   if (b == "auto") b = hip_device_count() > 0 ? "gpu" : "cpu";
   if (b == "gpu") {
     if (hip_device_count() <= device) throw std::runtime_error("no HIP device " + std::to_string(device));
-    return std::make_unique<GpuExecutor>(device, max_batch);
+    return std::make_unique<GpuExecutor>(device, max_batch, cache_bytes);
   }
   if (b == "cpu") return std::make_unique<CpuExecutor>();
   throw std::invalid_argument("unknown executor backend: " + backend);

@@ -25,6 +25,12 @@ struct Prediction {
   int class_idx = -1;
 };
 
+// Decoded-image cache statistics (GPU executor: images resident in HBM).
+struct CacheStats {
+  uint64_t hits = 0, misses = 0, staged = 0, evictions = 0;
+  uint64_t bytes = 0, entries = 0, capacity = 0;
+};
+
 class Executor {
  public:
   virtual ~Executor() = default;
@@ -34,10 +40,26 @@ class Executor {
   virtual void load_model_weights(const std::string& model, const WeightMap& w) = 0;
   virtual bool has_model(const std::string& model) const = 0;
   virtual std::vector<Prediction> predict(const std::string& model, const std::vector<Image>& imgs) = 0;
+
+  // Classify image files. The default decodes every file on the host; the
+  // GPU executor keeps decoded images resident in HBM and decodes only on a
+  // miss.
+  virtual std::vector<Prediction> predict_files(const std::string& model, const std::vector<std::string>& paths) {
+    std::vector<Image> imgs;
+    imgs.reserve(paths.size());
+    for (const auto& p : paths) imgs.push_back(decode_jpeg_file(p));
+    return predict(model, imgs);
+  }
+  // Make `path` resident ahead of use (side-stream upload); false if the
+  // executor has no cache.
+  virtual bool stage(const std::string& path) { return false; }
+  virtual CacheStats cache_stats() const { return {}; }
 };
 
 // backend: "gpu", "cpu" or "auto" (GPU when a HIP device is visible).
-std::unique_ptr<Executor> make_executor(const std::string& backend, int device, int max_batch);
+// cache_bytes: HBM budget for decoded images (GPU executor).
+std::unique_ptr<Executor> make_executor(const std::string& backend, int device, int max_batch,
+                                        size_t cache_bytes = (size_t)4 << 30);
 int hip_device_count();
 
 // Host-side reference preprocessing (same rule as csrc/kernels/preprocess.hip):

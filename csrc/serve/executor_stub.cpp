@@ -8,6 +8,7 @@
 // the race detector.
 #include <cstdint>
 #include <mutex>
+#include <map>
 #include <set>
 #include <stdexcept>
 
@@ -35,23 +36,62 @@ class DigestExecutor final : public Executor {
   std::vector<Prediction> predict(const std::string& model, const std::vector<Image>& imgs) override {
     if (!has_model(model)) throw std::runtime_error("model not loaded: " + model);
     std::vector<Prediction> out(imgs.size());
-    for (size_t i = 0; i < imgs.size(); ++i) {
-      uint64_t h = 1469598103934665603ull;  // FNV-1a over the pixels
-      for (uint8_t v : imgs[i].rgb) h = (h ^ v) * 1099511628211ull;
-      out[i].class_idx = int(h % 1000);
-      out[i].prob = 1.0;
-    }
+    for (size_t i = 0; i < imgs.size(); ++i) out[i] = Prediction{1.0, digest(imgs[i])};
     return out;
   }
 
+  // Same cache protocol as the GPU executor (hit / miss / staged), with the
+  // digest standing in for the HBM-resident image, so the prefetch thread
+  // and concurrent queries run under the race detector too.
+  std::vector<Prediction> predict_files(const std::string& model, const std::vector<std::string>& paths) override {
+    if (!has_model(model)) throw std::runtime_error("model not loaded: " + model);
+    std::vector<Prediction> out;
+    for (const auto& p : paths) out.push_back(Prediction{1.0, lookup(p, true)});
+    return out;
+  }
+  bool stage(const std::string& path) override {
+    lookup(path, false);
+    return true;
+  }
+  CacheStats cache_stats() const override {
+    std::lock_guard<std::mutex> g(mu_);
+    CacheStats c = stats_;
+    c.entries = cache_.size();
+    return c;
+  }
+
  private:
+  static int digest(const Image& img) {
+    uint64_t h = 1469598103934665603ull;  // FNV-1a over the pixels
+    for (uint8_t v : img.rgb) h = (h ^ v) * 1099511628211ull;
+    return int(h % 1000);
+  }
+  int lookup(const std::string& path, bool query) {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      auto it = cache_.find(path);
+      if (it != cache_.end()) {
+        if (query) ++stats_.hits;
+        return it->second;
+      }
+    }
+    const int d = digest(decode_jpeg_file(path));
+    std::lock_guard<std::mutex> g(mu_);
+    if (cache_.emplace(path, d).second) {
+      if (query) ++stats_.misses; else ++stats_.staged;
+    }
+    return d;
+  }
+
   mutable std::mutex mu_;
   std::set<std::string> models_;
+  std::map<std::string, int> cache_;
+  CacheStats stats_;
 };
 
 }  // namespace
 
-std::unique_ptr<Executor> make_executor(const std::string& backend, int, int) {
+std::unique_ptr<Executor> make_executor(const std::string& backend, int, int, size_t) {
   if (backend == "none") return nullptr;
   if (backend == "digest" || backend == "auto" || backend == "cpu") return std::make_unique<DigestExecutor>();
   throw std::runtime_error("executor '" + backend + "' is not available in the sanitizer build");

@@ -64,3 +64,35 @@ def test_gpu_cluster_predict(gpu, env, tmp_path):
                 break
             time.sleep(0.5)
         assert done == 16
+
+
+def test_gpu_hbm_image_cache(gpu, env, tmp_path):
+    """--prefetch stages every class's query image into HBM on a side
+    stream; the job's queries then hit the resident copies (no JPEG decode,
+    no host->device copy on the query path)."""
+    cl = LocalCluster(1, 19750, str(tmp_path / "c"), env["labels"], n_leaders=1, executor="gpu",
+                      dataset=env["dataset"], models=f"resnet18={env['ckpt']}",
+                      extra=["--jobs", "resnet18", "--job-limit", "16", "--query-interval-ms", "20",
+                             "--query-batch", "4", "--quiet-predictions", "--prefetch"])
+    with cl:
+        n = cl.nodes[0]
+        deadline = time.time() + 60
+        while time.time() < deadline:
+            m = re.search(r"prefetched (\d+)", n.cmd("info"))
+            if m and int(m.group(1)) >= 16:
+                break
+            time.sleep(0.2)
+        info = n.cmd("info")
+        assert re.search(r"staged 16 ", info), info
+        n.cmd("predict")
+        deadline = time.time() + 60
+        done = 0
+        while time.time() < deadline:
+            m = re.search(r"Accuracy: \d+/(\d+)", n.cmd("jobs"))
+            done = int(m.group(1)) if m else 0
+            if done >= 16:
+                break
+            time.sleep(0.5)
+        assert done == 16
+        m = re.search(r"cache hits (\d+) misses (\d+)", n.cmd("info"))
+        assert m and int(m.group(1)) >= 16 and int(m.group(2)) == 0, n.cmd("info")

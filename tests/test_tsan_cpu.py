@@ -54,7 +54,7 @@ def test_tsan_cluster_workload(tsan_bin, tmp_path):
     ds = make_synthetic_dataset(str(tmp_path / "train"), labels[:48], size=(48, 64))
     src = tmp_path / "data.txt"
     src.write_text("payload\n" * 1000)
-    cl = LocalCluster(5, 19700, str(tmp_path / "c"), lab, n_leaders=2, executor="digest", dataset=ds,
+    cl = LocalCluster(5, 19900, str(tmp_path / "c"), lab, n_leaders=2, executor="digest", dataset=ds,
                       models="resnet18=-,alexnet=-", binary=tsan_bin, env=TSAN_ENV,
                       extra=["--job-limit", "40", "--query-interval-ms", "100", "--quiet-predictions"])
     with cl:
@@ -63,8 +63,11 @@ def test_tsan_cluster_workload(tsan_bin, tmp_path):
         assert "Stored on:" in n[3].cmd(f"put {src} a.txt")
         assert "Stored on:" in n[4].cmd(f"put {src} a.txt")
         assert "Retrieved version: 2" in n[2].cmd(f"get a.txt {tmp_path / 'g.txt'}")
-        # predict jobs on all members, then kill a member and the leader mid-run
+        # predict jobs on all members while two of them stage the dataset
+        # into their executor cache; then kill a member and the leader mid-run
+        n[3].cmd("prefetch")
         n[4].cmd("predict")
+        n[1].cmd("prefetch")
         time.sleep(1.0)
         n[2].kill()
         time.sleep(1.0)
@@ -91,6 +94,7 @@ def test_tsan_cluster_workload(tsan_bin, tmp_path):
                 break
             time.sleep(0.5)
         assert sorted(rows) == sorted(nd.address for nd in survivors), rows
+        assert re.search(r"cache hits \d+ misses \d+ staged [1-9]", n[3].cmd("info")), n[3].cmd("info")
         assert "Leaving group" in n[3].cmd("leave")
         cl.wait_members(2, 20, [n[1], n[4]])
     _no_reports(n)
