@@ -82,3 +82,54 @@ def test_dp_scatter_gather_gloo():
         assert torch.equal(idx, exp[0])
         assert torch.allclose(prob, exp[1], rtol=1e-5, atol=1e-6)
     assert all(x > 0 for x in lat)
+
+
+def _elastic_worker(rank, world, port, B, n_images, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(2)
+    import datetime
+    from dmlc.parallel import ElasticDPInference
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=4))
+    model = build("resnet18", seed=5)
+    model.eval()
+    f = _predict_fn(model)
+    calls = [0]
+
+    def predict(imgs, out):
+        calls[0] += 1
+        if rank == world - 1 and calls[0] == 2:
+            os._exit(17)  # this "GPU" dies mid-step: shard received, result never sent
+        f(imgs, out)
+
+    pool = None
+    if rank == 0:
+        g = torch.Generator().manual_seed(9)
+        pool = torch.randint(0, 256, (n_images, 48, 48, 3), generator=g, dtype=torch.uint8)
+    dp = ElasticDPInference(predict, B, torch.device("cpu"), image_shape=(48, 48, 3), timeout_s=4.0)
+    res = dp.run_dataset(pool, n_images)
+    if rank == 0:
+        q.put((res, pool, dp.recoveries, dp.world))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_elastic_dp_survives_rank_loss():
+    """world 3 over gloo; rank 2 dies inside its 2nd step. The survivors
+    rebuild a 2-rank group, redo the uncommitted step and classify every
+    image exactly once."""
+    world, B, n = 3, 2, 19
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_elastic_worker, args=(r, world, port, B, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    (idx, prob), pool, recoveries, final_world = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+    assert [p.exitcode for p in procs] == [0, 0, 17]
+    assert final_world == 2 and len(recoveries) == 1 and recoveries[0]["members"] == [0, 1]
+    exp = (torch.empty(n, dtype=torch.int32), torch.empty(n))
+    _predict_fn(build("resnet18", seed=5).eval())(pool, exp)
+    assert torch.equal(idx, exp[0])
+    assert torch.allclose(prob, exp[1], rtol=1e-4, atol=1e-6)
