@@ -1,5 +1,7 @@
 #include "member.h"
 
+#include "../runtime/trace.h"
+
 #include <dirent.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -125,6 +127,7 @@ std::vector<std::pair<double, std::string>> MemberService::predict(const std::st
   *ok = false;
   std::vector<std::pair<double, std::string>> out;
   if (!exec_ || !exec_->has_model(model)) return out;
+  DMLC_TRACE("member.predict");
   std::vector<std::string> paths;
   for (const auto& id : ids) {
     std::string p = query_image(id);

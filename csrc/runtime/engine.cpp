@@ -10,7 +10,10 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <optional>
 #include <stdexcept>
+
+#include "trace.h"
 
 namespace dmlc {
 
@@ -383,10 +386,12 @@ ConvArgs Engine::conv_args(const Op& op, int B, float* logits) const {
 }
 
 void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* idx, float* prob,
-                     float* logits, hipStream_t s, std::vector<hipEvent_t>* evs) {
+                     float* logits, hipStream_t s, std::vector<hipEvent_t>* evs, bool trace) {
   size_t ei = 0;
   if (evs) DMLC_HIP_CHECK(hipEventRecord((*evs)[ei++], s));
   for (const Op& op : ops_) {
+    std::optional<TraceRange> tr;  // per-op host ranges (not inside a graph capture)
+    if (trace) tr.emplace(op.name.c_str());
     switch (op.type) {
       case OpType::Preprocess: {
         const bool paired = op.k == 1;
@@ -446,16 +451,18 @@ void Engine::forward(const uint8_t* images, int B, int Hin, int Win, int32_t* id
     if (it == graphs_.end()) {
       hipGraph_t g;
       DMLC_HIP_CHECK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
-      run_ops(images, B, Hin, Win, idx, prob, logits, stream_, nullptr);
+      run_ops(images, B, Hin, Win, idx, prob, logits, stream_, nullptr, false);
       DMLC_HIP_CHECK(hipStreamEndCapture(stream_, &g));
       hipGraphExec_t ex;
       DMLC_HIP_CHECK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
       DMLC_HIP_CHECK(hipGraphDestroy(g));
       it = graphs_.emplace(key, ex).first;
     }
+    DMLC_TRACE("engine.forward(graph)");
     DMLC_HIP_CHECK(hipGraphLaunch(it->second, stream_));
   } else {
-    run_ops(images, B, Hin, Win, idx, prob, logits, stream_, nullptr);
+    DMLC_TRACE("engine.forward");
+    run_ops(images, B, Hin, Win, idx, prob, logits, stream_, nullptr, true);
   }
   DMLC_HIP_CHECK(hipEventRecord(ev_out_, stream_));
   DMLC_HIP_CHECK(hipStreamWaitEvent(stream, ev_out_, 0));
@@ -468,7 +475,7 @@ std::vector<std::pair<std::string, float>> Engine::profile(const uint8_t* images
   DMLC_HIP_CHECK(hipStreamSynchronize(stream));
   std::vector<hipEvent_t> evs(ops_.size() + 1);
   for (auto& e : evs) DMLC_HIP_CHECK(hipEventCreate(&e));
-  run_ops(images, B, Hin, Win, nullptr, nullptr, nullptr, stream_, &evs);
+  run_ops(images, B, Hin, Win, nullptr, nullptr, nullptr, stream_, &evs, true);
   DMLC_HIP_CHECK(hipStreamSynchronize(stream_));
   std::vector<std::pair<std::string, float>> out;
   for (size_t i = 0; i < ops_.size(); ++i) {

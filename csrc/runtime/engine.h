@@ -98,7 +98,7 @@ class Engine {
   void build_alexnet();
   void pack_weights(const WeightMap& w);
   void run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* idx, float* prob,
-               float* logits, hipStream_t s, std::vector<hipEvent_t>* evs);
+               float* logits, hipStream_t s, std::vector<hipEvent_t>* evs, bool trace);
   ConvArgs conv_args(const Op& op, int B, float* logits) const;
 
   std::string arch_;

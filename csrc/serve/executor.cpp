@@ -12,6 +12,7 @@
 
 #include "../runtime/engine.h"
 #include "../runtime/ot_io.h"
+#include "../runtime/trace.h"
 
 namespace dmlc {
 
@@ -228,7 +229,10 @@ class GpuExecutor : public Executor {
       std::lock_guard<std::mutex> g(mu_);
       engine(model);  // fail fast on an unknown model
     }
-    for (const auto& p : paths) stage_one(p, /*count_as_miss=*/true);
+    {
+      DMLC_TRACE("executor.stage");
+      for (const auto& p : paths) stage_one(p, /*count_as_miss=*/true);
+    }
     std::lock_guard<std::mutex> g(mu_);
     Engine* e = engine(model);
     std::vector<const void*> src(paths.size());
@@ -318,6 +322,7 @@ class GpuExecutor : public Executor {
   // Group same-sized images; each group is one batched forward.
   std::vector<Prediction> run(Engine* e, const std::vector<const void*>& src,
                               const std::vector<std::pair<int, int>>& hw, hipMemcpyKind kind) {
+    DMLC_TRACE("executor.forward");
     DMLC_HIP_CHECK(hipSetDevice(device_));
     std::vector<Prediction> out(src.size());
     std::map<std::pair<int, int>, std::vector<size_t>> groups;

@@ -1,5 +1,7 @@
 #include "leader.h"
 
+#include "../runtime/trace.h"
+
 #include <optional>
 
 #include "../control/common.h"
@@ -317,6 +319,7 @@ void LeaderService::run_job(size_t j) {
       Id tgt = target;
       std::string resp;
       bool sent = false;
+      DMLC_TRACE("leader.query");
       for (int attempt = 0; attempt < 4 && !stop_.load(); ++attempt) {
         try {
           resp = RpcClient::shared().call(tgt.host(), member_port(tgt.port()), M_PREDICT, w.data(), 120000);

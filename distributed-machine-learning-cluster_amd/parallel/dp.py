@@ -29,6 +29,21 @@ import torch.distributed as dist
 PredictFn = Callable[[torch.Tensor, tuple], None]  # (images u8 [B,H,W,3], (idx_out, prob_out))
 
 
+class _Range:
+    """roctx range (torch.cuda.nvtx maps to roctx on ROCm); no-op on CPU."""
+
+    def __init__(self, name: str, on: bool):
+        self.name, self.on = name, on
+
+    def __enter__(self):
+        if self.on:
+            torch.cuda.nvtx.range_push(self.name)
+
+    def __exit__(self, *exc):
+        if self.on:
+            torch.cuda.nvtx.range_pop()
+
+
 class DPInference:
     def __init__(self, predict_fn: PredictFn, per_rank_batch: int, device: torch.device,
                  image_shape=(224, 224, 3), src: int = 0, slots: int = 2, input_mode: str = "scatter"):
@@ -78,7 +93,8 @@ class DPInference:
             return None
         s = step % self.slots
         shards = self.shards(pool, step) if self.rank == self.src else None
-        return dist.scatter(self.inbuf[s], shards, src=self.src, async_op=True)
+        with _Range("dp.scatter", self.cuda):
+            return dist.scatter(self.inbuf[s], shards, src=self.src, async_op=True)
 
     def _local_input(self, pool, step):
         if self.transfer:
@@ -106,11 +122,13 @@ class DPInference:
                 h = self._issue_input(pool, i + 1)
             s = i % self.slots
             ob = self.outbuf[s]
-            self.predict_fn(self._local_input(pool, i), (ob[0], ob[1].view(torch.float32)))
+            with _Range("dp.predict", self.cuda):
+                self.predict_fn(self._local_input(pool, i), (ob[0], ob[1].view(torch.float32)))
             if self.distributed:
-                g = dist.gather(ob, self.gathered[s] if self.rank == self.src else None, dst=self.src,
-                                async_op=True)
-                g.wait()
+                with _Range("dp.gather", self.cuda):
+                    g = dist.gather(ob, self.gathered[s] if self.rank == self.src else None, dst=self.src,
+                                    async_op=True)
+                    g.wait()
             self._stamp(self.t_end, i)
             if not self.transfer and i + 1 < first + n:
                 self._stamp(self.t_start, i + 1)

@@ -143,7 +143,7 @@ def build(jobs: int = 8, verbose: bool = False, node: bool = True) -> None:
             tsan_objs.append(o)
             if _stale(o, [s], hdr):
                 steps.append(["g++", "-O1", "-g", "-std=c++17", "-fPIC", "-fsanitize=thread", "-pthread",
-                              "-c", s, "-o", o])
+                              "-DDMLC_NO_ROCTX", "-c", s, "-o", o])
 
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         list(ex.map(lambda c: _run(c, verbose), steps))
@@ -154,7 +154,8 @@ def build(jobs: int = 8, verbose: bool = False, node: bool = True) -> None:
 
     libgpu = os.path.join(PKG, "libdmlc_gpu.so")
     if _stale(libgpu, gpu_objs, 0):
-        _run(["hipcc", "-shared", "-fPIC", f"--offload-arch={ARCH}", *gpu_objs, "-o", libgpu], verbose)
+        _run(["hipcc", "-shared", "-fPIC", f"--offload-arch={ARCH}", *gpu_objs, "-o", libgpu,
+              f"-L{ROCM}/lib", "-lrocprofiler-sdk-roctx", f"-Wl,-rpath,{ROCM}/lib"], verbose)
 
     pymod = os.path.join(PKG, "_C" + ext)
     if _stale(pymod, py_objs + [libgpu], 0):
@@ -169,6 +170,7 @@ def build(jobs: int = 8, verbose: bool = False, node: bool = True) -> None:
         if _stale(exe, node_objs + [libgpu] + rt_objs, 0):
             _run(["g++", "-pthread", *node_objs, *rt_objs, "-o", exe,
                   f"-L{PKG}", "-ldmlc_gpu", f"-Wl,-rpath,{PKG}",
+                  f"-L{ROCM}/lib", "-lrocprofiler-sdk-roctx", f"-Wl,-rpath,{ROCM}/lib",
                   f"-L{tlib}", "-ltorch_cpu", "-lc10", "-lamdhip64", f"-Wl,-rpath,{tlib}"], verbose)
 
 
