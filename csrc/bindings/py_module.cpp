@@ -122,6 +122,13 @@ PYBIND11_MODULE(_C, m) {
       py::arg("Wr"), py::arg("stream"), py::arg("paired") = false);
   m.attr("STEM_POOL_K") = kStemPoolK;
   m.def("stem_pool_pick_strip", &stem_pool_pick_strip);
+  m.def("conv3x3_rows_supported", &conv3x3_rows_supported);
+  m.def("conv3x3_rows_pick_strip", &conv3x3_rows_pick_strip);
+  m.def("conv3x3_rows", [](uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t res, uintptr_t y, uintptr_t zero,
+                           int B, int H, int W, int C, bool relu, int strip, uintptr_t stream) {
+    conv3x3_rows(P<void>(x), P<void>(w), P<float>(bias), P<void>(res), P<void>(y), P<void>(zero), B, H, W, C, relu,
+                 strip, S(stream));
+  });
   m.def("stem_conv_pool", [](uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y, int B, int S_, int Wq,
                              int strip, uintptr_t stream) {
     stem_conv_pool(P<void>(x), P<void>(w), P<float>(bias), P<void>(y), B, S_, Wq, strip, S(stream));

@@ -85,6 +85,15 @@ void preprocess_u8(const uint8_t* x, void* y, int B, int Hin, int Win, int S, in
 //   y : bf16 NHWC [B, S/4, S/4, 64]
 // strip = pooled rows per workgroup (even divisor of S/4).
 constexpr int kStemPoolK = 224;
+
+// Direct 3x3/s1/p1 conv for narrow layers (ResNet layer1, 56x56x64 -> 64):
+// weights resident in LDS, input rows streamed once through an LDS ring.
+// Same operand layouts as conv2d_igemm (w [64, 576], bias fp32, optional
+// bf16 residual, NHWC in/out).
+bool conv3x3_rows_supported(int H, int W, int Cin, int Cout);
+int conv3x3_rows_pick_strip(int B, int H, int num_cus);
+void conv3x3_rows(const void* x, const void* w, const float* bias, const void* res, void* y, const void* zero,
+                  int B, int H, int W, int C, bool relu, int strip, hipStream_t s);
 int stem_pool_pick_strip(int B, int PH, int num_cus);
 void stem_conv_pool(const void* x, const void* w, const float* bias, void* y, int B, int S, int Wq, int strip,
                     hipStream_t s);

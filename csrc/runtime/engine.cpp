@@ -52,6 +52,7 @@ Engine::Engine(const std::string& arch, const WeightMap& weights, int device, in
   num_cus_ = prop.multiProcessorCount;
   if (const char* e = std::getenv("DMLC_PERSISTENT")) persistent_ = std::string(e) != "0";
   if (const char* e = std::getenv("DMLC_FUSED_STEM")) fused_stem_ = std::string(e) != "0";
+  if (const char* e = std::getenv("DMLC_ROW_CONV")) row_conv_ = std::string(e) != "0";
 
   if (arch == "resnet18")
     build_resnet({2, 2, 2, 2}, false);
@@ -399,9 +400,20 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
         preprocess_u8(images, acts_[op.out], B, Hin, Win, image_size_, op.pad, Wr, s, paired);
         break;
       }
-      case OpType::Conv:
-        conv2d_igemm(conv_args(op, B, logits), s);
+      case OpType::Conv: {
+        const ConvLayer& L = convs_[op.conv];
+        const ActShape& is = shapes_[op.in];
+        if (row_conv_ && !L.fc && !L.pair && L.kh == 3 && L.kw == 3 && L.stride == 1 && L.pad == 1 &&
+            !shapes_[op.out].f32 && conv3x3_rows_supported(is.H, is.W, is.C, L.cout)) {
+          conv3x3_rows(acts_[op.in], (const uint8_t*)warena_ + L.w_off,
+                       (const float*)((const uint8_t*)warena_ + L.b_off), op.res >= 0 ? acts_[op.res] : nullptr,
+                       acts_[op.out], zero_, B, is.H, is.W, is.C, L.relu, conv3x3_rows_pick_strip(B, is.H, num_cus_),
+                       s);
+        } else {
+          conv2d_igemm(conv_args(op, B, logits), s);
+        }
         break;
+      }
       case OpType::StemPool: {
         const ConvLayer& L = convs_[op.conv];
         stem_conv_pool(acts_[op.in], (const uint8_t*)warena_ + L.w_off,

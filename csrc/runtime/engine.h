@@ -110,6 +110,7 @@ class Engine {
   int stem_pad_ = 0;
   bool persistent_ = true;  // persistent conv grids (env DMLC_PERSISTENT=0 disables)
   bool fused_stem_ = true;  // conv1+maxpool as one kernel (env DMLC_FUSED_STEM=0 disables)
+  bool row_conv_ = true;    // direct row-streaming 3x3 convs where supported (env DMLC_ROW_CONV=0 disables)
 
   std::vector<ActShape> shapes_;
   std::vector<ConvLayer> convs_;

@@ -155,6 +155,28 @@ def test_stem_conv_pool(gpu, B, S, strip):
     assert (got - ref).abs().max().item() < 0.05
 
 
+@pytest.mark.parametrize("B,strip,res", [(2, None, False), (2, None, True), (3, 4, True), (1, 8, False),
+                                         (1, 28, True)])
+def test_conv3x3_rows(gpu, B, strip, res):
+    """Direct row-streaming 3x3 conv (conv3x3_rows.hip) vs torch fp32."""
+    g = torch.Generator().manual_seed(13)
+    x = torch.randn(B, 64, 56, 56, generator=g).bfloat16().float()
+    w = (torch.randn(64, 64, 3, 3, generator=g) / 24).bfloat16().float()
+    bias = torch.randn(64, generator=g) * 0.1
+    r = torch.randn(B, 64, 56, 56, generator=g).bfloat16().float() if res else None
+    ref = F.conv2d(x, w, bias, 1, 1)
+    if res:
+        ref = ref + r
+    ref = F.relu(ref)
+    wp = ops.pack_conv_weight(w, device=gpu)
+    y = ops.conv3x3_rows(_nhwc(x).bfloat16().to(gpu), wp, bias.to(gpu),
+                         _nhwc(r).bfloat16().to(gpu) if res else None, True, strip)
+    torch.cuda.synchronize()
+    got = _nchw(y.float().cpu())
+    assert _rel(got, ref) < 5e-3, _rel(got, ref)
+    assert (got - ref).abs().max().item() < 0.1
+
+
 def test_preprocess_paired(gpu):
     g = torch.Generator().manual_seed(12)
     img = torch.randint(0, 256, (2, 224, 224, 3), generator=g, dtype=torch.uint8)

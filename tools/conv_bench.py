@@ -77,6 +77,22 @@ def main():
                 row.append(f"tile{t}={ms*1e3:7.1f}us {flops/ms/1e9:6.0f}TF")
             except Exception as e:  # noqa: BLE001
                 row.append(f"tile{t}=ERR({e})")
+        if name == "l1":  # direct row-streaming conv (conv3x3_rows.hip)
+            for use_res in (False, True):
+                r = torch.randn(B, H, W, Cout, device=dev).bfloat16() if use_res else None
+                f = lambda: ops.conv3x3_rows(x, wp, bias, r, True)
+                f()
+                torch.cuda.synchronize()
+                ts = []
+                for _ in range(a.iters):
+                    e0, e1 = torch.cuda.Event(True), torch.cuda.Event(True)
+                    e0.record()
+                    f()
+                    e1.record()
+                    e1.synchronize()
+                    ts.append(e0.elapsed_time(e1))
+                ms = statistics.median(ts)
+                row.append(f"rows{'+res' if use_res else ''}={ms*1e3:7.1f}us {flops/ms/1e9:6.0f}TF")
         if a.ref:
             # vendor references on the same shape: plain GEMM (hipBLASLt via
             # torch.mm) and MIOpen conv (bf16, channels_last)
