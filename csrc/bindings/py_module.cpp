@@ -64,7 +64,8 @@ PYBIND11_MODULE(_C, m) {
       [](uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t res, uintptr_t y, int B, int H, int W,
          int Cin, int KH, int KW, int stride, int pad, int N, int Npad, int Kpad, int ldo, bool relu,
          bool out_f32, int split_k, uintptr_t ws, int tile, uintptr_t zero, bool stem, int Ho, int Wo,
-         int max_blocks, uintptr_t stream) {
+         int max_blocks, uintptr_t stream, bool in_fp8, bool out_fp8, uintptr_t alpha, float res_scale,
+         float out_inv_scale) {
         ConvArgs a;
         a.x = P<void>(x);
         a.zero = P<void>(zero);
@@ -94,6 +95,11 @@ PYBIND11_MODULE(_C, m) {
         a.tile = tile;
         a.persistent = max_blocks > 0;
         a.max_blocks = max_blocks;
+        a.in_fp8 = in_fp8;
+        a.out_fp8 = out_fp8;
+        a.alpha = P<float>(alpha);
+        a.res_scale = res_scale;
+        a.out_inv_scale = out_inv_scale;
         conv2d_igemm(a, S(stream));
       },
       py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("res"), py::arg("y"), py::arg("B"),
@@ -101,7 +107,8 @@ PYBIND11_MODULE(_C, m) {
       py::arg("pad"), py::arg("N"), py::arg("Npad"), py::arg("Kpad"), py::arg("ldo"),
       py::arg("relu"), py::arg("out_f32"), py::arg("split_k"), py::arg("ws"), py::arg("tile"),
       py::arg("zero"), py::arg("stem"), py::arg("Ho"), py::arg("Wo"), py::arg("max_blocks"),
-      py::arg("stream"));
+      py::arg("stream"), py::arg("in_fp8") = false, py::arg("out_fp8") = false, py::arg("alpha") = 0,
+      py::arg("res_scale") = 1.f, py::arg("out_inv_scale") = 1.f);
   m.def("maxpool2d", [](uintptr_t x, uintptr_t y, int B, int H, int W, int C, int k, int stride,
                         int pad, uintptr_t stream) {
     maxpool2d(P<void>(x), P<void>(y), B, H, W, C, conv_out_dim(H, k, stride, pad),
@@ -132,6 +139,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("stem_conv_pool", [](uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y, int B, int S_, int Wq,
                              int strip, uintptr_t stream) {
     stem_conv_pool(P<void>(x), P<void>(w), P<float>(bias), P<void>(y), B, S_, Wq, strip, S(stream));
+  });
+  m.def("mfma_fp8_probe", [](uintptr_t a, uintptr_t b, uintptr_t d, uintptr_t stream) {
+    mfma_fp8_probe(P<void>(a), P<void>(b), P<float>(d), S(stream));
   });
   m.def("softmax_top1", [](uintptr_t logits, int B, int N, int ld, uintptr_t idx, uintptr_t prob,
                            uintptr_t stream) {

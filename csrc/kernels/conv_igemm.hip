@@ -38,6 +38,7 @@
 #include "kernels.h"
 
 #include <algorithm>
+#include <type_traits>
 
 namespace dmlc {
 
@@ -47,6 +48,27 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef const __attribute__((address_space(1))) void* gbl_ptr_t;
 
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+
+typedef int v8i __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ v8i cat8(uint4 lo, uint4 hi) {
+  return v8i{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+}
+
+// e4m3 helpers (OCP, gfx950): 4 bytes <-> 4 floats; stores saturate at +-448.
+__device__ __forceinline__ void fp8x4_to_f32(uint32_t u, float* f) {
+  f[0] = __builtin_amdgcn_cvt_f32_fp8((int)u, 0);
+  f[1] = __builtin_amdgcn_cvt_f32_fp8((int)u, 1);
+  f[2] = __builtin_amdgcn_cvt_f32_fp8((int)u, 2);
+  f[3] = __builtin_amdgcn_cvt_f32_fp8((int)u, 3);
+}
+__device__ __forceinline__ uint32_t f32x4_to_fp8(const float* f) {
+  float c[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) c[i] = fminf(fmaxf(f[i], -448.f), 448.f);
+  int v = __builtin_amdgcn_cvt_pk_fp8_f32(c[0], c[1], 0, false);
+  v = __builtin_amdgcn_cvt_pk_fp8_f32(c[2], c[3], v, true);
+  return (uint32_t)v;
+}
 
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   // Bijective: blocks b and b+8 share an XCD; give each XCD a contiguous
@@ -80,9 +102,20 @@ __device__ __forceinline__ void wait_tiles(int remaining) {
 // at 256, which keeps the 64 accumulator registers in arch VGPRs. Without
 // it hipcc splits into AGPRs and shuffles ~100 v_accvgpr_* per K-tile
 // (measured: 4.4 VALU per MFMA, 40% of wave cycles in waits).
-template <int BM, int BN, int WM, int WN, int NS, bool PAIR>
+// fp8 (IN8/OUT8, ResNet50 fp8 path): activations/weights/residual are OCP
+// e4m3 bytes and a 128-B LDS row holds 128 k instead of 64, so one block-
+// scaled v_mfma_scale_f32_16x16x128_f8f6f4 (2x the bf16 MFMA rate) covers a
+// whole K-tile; a lane's A/B fragment is the 32 contiguous bytes of chunks
+// 2*fq, 2*fq+1 of its row (any lane->k map works as long as A and B agree:
+// tests/test_fp8_gpu.py). The epilogue dequantises with a per-channel
+// alpha = s_in * s_w[n], adds bias and the e4m3 residual (x res_scale),
+// applies ReLU and requantises with out_inv_scale (saturating at +-448).
+template <int BM, int BN, int WM, int WN, int NS, bool PAIR, bool IN8 = false, bool OUT8 = false>
 __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a, int kt_per_split, int k_tiles) {
-  constexpr int BK = 64;
+  static_assert(!(PAIR && IN8), "the stem is bf16");
+  using Elem = typename std::conditional<IN8, uint8_t, bf16>::type;
+  constexpr int CE = IN8 ? 16 : 8;  // elements per 16-B chunk
+  constexpr int BK = 8 * CE;        // elements per K-tile (one 128-B LDS row)
   static_assert(NS >= 2 && NS <= 4, "stages");
   constexpr int PA = BM / 32;  // A rows per lane (wave covers BM/4 rows = PA instrs of 8 rows)
   constexpr int PB = BN / 32;
@@ -90,7 +123,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a, int kt_p
   constexpr int TM = WTM / 16, TN = WTN / 16;
   static_assert(WM * WN == 4, "4 waves per block");
   static_assert(BM % 32 == 0 && BN % 32 == 0, "tile");
-  constexpr int ROWB = BK * 2;                       // 128 B per LDS row
+  constexpr int ROWB = 128;                          // bytes per LDS row
   constexpr int STAGE_B = (BM + BN) * ROWB;          // bytes per stage
   constexpr int A_CH = BM * 8;                       // chunks in the A part of a stage
   constexpr int STAGE_CH = (BM + BN) * 8;
@@ -119,9 +152,9 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a, int kt_p
   const int kt1 = min(k_tiles, kt0 + kt_per_split);
   const int nk = kt1 - kt0;
 
-  const bf16* __restrict__ x = (const bf16*)a.x;
-  const bf16* __restrict__ w = (const bf16*)a.w;
-  const bf16* zero = (const bf16*)a.zero;
+  const Elem* __restrict__ x = (const Elem*)a.x;
+  const Elem* __restrict__ w = (const Elem*)a.w;
+  const Elem* zero = (const Elem*)a.zero;
 
   // Rows this lane stages. A: rows wave*BM/4 + p*8 + lane/8, B likewise.
   const int lrow = lane >> 3;
@@ -150,7 +183,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a, int kt_p
         } else {
           hi0[p] = ho * a.stride - a.pad;
           wi0[p] = wo * a.stride - a.pad;
-          abase[p] = ((b * a.H + hi0[p]) * a.W + wi0[p]) * a.Cin + lc * 8;
+          abase[p] = ((b * a.H + hi0[p]) * a.W + wi0[p]) * a.Cin + lc * CE;
         }
       } else {
         hi0[p] = -(1 << 28);
@@ -161,7 +194,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a, int kt_p
 #pragma unroll
     for (int p = 0; p < PB; ++p) {
       const int r = wave * (BN / 4) + p * 8 + lrow;
-      wboff[p] = (n0_ + r) * a.Kpad + swz(r, pchunk) * 8;
+      wboff[p] = (n0_ + r) * a.Kpad + swz(r, pchunk) * CE;
     }
   };
   setup_rows(m0, n0);
@@ -172,16 +205,16 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a, int kt_p
   auto stage = [&](int t, int st) __attribute__((always_inline)) {
     char* sbase = (char*)smem + st * STAGE_B;
     if constexpr (!PAIR) {
-      const int ctiles = a.Cin >> 6;
+      const int ctiles = a.Cin / BK;
       const int tap = t / ctiles;
-      const int c0 = (t - tap * ctiles) << 6;
+      const int c0 = (t - tap * ctiles) * BK;
       const int kh = tap / a.KW;
       const int kw = tap - kh * a.KW;
       const int off = (kh * a.W + kw) * a.Cin + c0;
 #pragma unroll
       for (int p = 0; p < PA; ++p) {
         const bool ok = (unsigned)(hi0[p] + kh) < (unsigned)a.H && (unsigned)(wi0[p] + kw) < (unsigned)a.W;
-        const bf16* src = ok ? x + abase[p] + off : zero;
+        const Elem* src = ok ? x + abase[p] + off : zero;
         __builtin_amdgcn_global_load_lds((gbl_ptr_t)src,
                                          (lds_ptr_t)(sbase + (wave * (BM / 4) + p * 8) * ROWB), 16, 0, 0);
       }
@@ -193,12 +226,12 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a, int kt_p
         const int j = q - kh * CPK;
         const bool ok = q < stem_chunks && hi0[p] >= 0;
         // 4-B aligned (wi0 even, row length even): LDS-DMA needs dword alignment
-        const bf16* src = ok ? x + abase[p] + kh * a.W * 3 + j * 8 : zero;
+        const Elem* src = ok ? x + abase[p] + kh * a.W * 3 + j * 8 : zero;
         __builtin_amdgcn_global_load_lds((gbl_ptr_t)src,
                                          (lds_ptr_t)(sbase + (wave * (BM / 4) + p * 8) * ROWB), 16, 0, 0);
       }
     }
-    const bf16* wt = w + t * BK;
+    const Elem* wt = w + t * BK;
 #pragma unroll
     for (int p = 0; p < PB; ++p)
       __builtin_amdgcn_global_load_lds((gbl_ptr_t)(wt + wboff[p]),
@@ -215,6 +248,26 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a, int kt_p
 
   auto compute = [&](int st) __attribute__((always_inline)) {
     const uint4* sb = smem + st * STAGE_CH;
+    if constexpr (IN8) {
+      // one 128-deep k-step: lane fragment = chunks 2fq, 2fq+1 (32 bytes)
+      v8i af[TN], bm[TM];
+#pragma unroll
+      for (int i = 0; i < TN; ++i) {
+        const int r = wn * WTN + i * 16 + fr;
+        af[i] = cat8(sb[A_CH + r * 8 + swz(r, 2 * fq)], sb[A_CH + r * 8 + swz(r, 2 * fq + 1)]);
+      }
+#pragma unroll
+      for (int j = 0; j < TM; ++j) {
+        const int r = wm * WTM + j * 16 + fr;
+        bm[j] = cat8(sb[r * 8 + swz(r, 2 * fq)], sb[r * 8 + swz(r, 2 * fq + 1)]);
+      }
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j)  // formats 0/0 = e4m3; E8M0 scales 127 = 1.0
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], bm[j], acc[i][j], 0, 0, 0, 127, 0, 127);
+      return;
+    }
 #pragma unroll
     for (int ks = 0; ks < BK / 32; ++ks) {
       bf16x8 af[TN], bm[TM];
@@ -270,23 +323,38 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a, int kt_p
         const int n = n0e + wn * WTN + i * 16 + fq * 4;
         if (n >= a.N) continue;
         float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        if constexpr (IN8) {  // dequantise: s_in * s_w[n]
+          const floatx4 al = *(const floatx4*)(a.alpha + n);
+          v[0] *= al[0]; v[1] *= al[1]; v[2] *= al[2]; v[3] *= al[3];
+        }
         if (a.bias) {
           const floatx4 bb = *(const floatx4*)(a.bias + n);
           v[0] += bb[0]; v[1] += bb[1]; v[2] += bb[2]; v[3] += bb[3];
         }
         const size_t o = (size_t)m * a.ldo + n;
         if (res) {
-          const uint2 rv = *(const uint2*)(res + o);
-          v[0] += __uint_as_float(rv.x << 16);
-          v[1] += __uint_as_float(rv.x & 0xffff0000u);
-          v[2] += __uint_as_float(rv.y << 16);
-          v[3] += __uint_as_float(rv.y & 0xffff0000u);
+          if constexpr (IN8) {
+            float rf[4];
+            fp8x4_to_f32(*(const uint32_t*)((const uint8_t*)a.res + o), rf);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] += rf[r] * a.res_scale;
+          } else {
+            const uint2 rv = *(const uint2*)(res + o);
+            v[0] += __uint_as_float(rv.x << 16);
+            v[1] += __uint_as_float(rv.x & 0xffff0000u);
+            v[2] += __uint_as_float(rv.y << 16);
+            v[3] += __uint_as_float(rv.y & 0xffff0000u);
+          }
         }
         if (a.relu) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
         }
-        if (a.out_f32) {
+        if constexpr (OUT8) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] *= a.out_inv_scale;
+          *(uint32_t*)((uint8_t*)a.y + o) = f32x4_to_fp8(v);
+        } else if (a.out_f32) {
           *(floatx4*)((float*)a.y + o) = floatx4{v[0], v[1], v[2], v[3]};
         } else {
           *(uint2*)((bf16*)a.y + o) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
@@ -407,7 +475,7 @@ int pick_tile(const ConvArgs& a) {
   return 0;
 }
 
-template <int BM, int BN, int WM, int WN, int NS>
+template <int BM, int BN, int WM, int WN, int NS, bool IN8 = false, bool OUT8 = false>
 void launch_cfg(const ConvArgs& a, int splits, int kt_per, int k_tiles, hipStream_t s) {
   const int M = a.B * a.Ho * a.Wo;
   int tiles = ((M + BM - 1) / BM) * (a.Npad / BN);
@@ -419,7 +487,10 @@ void launch_cfg(const ConvArgs& a, int splits, int kt_per, int k_tiles, hipStrea
   }
   dim3 grid(tiles, splits);
   const size_t lds = (size_t)NS * (BM + BN) * 128;
-  if (a.stem)
+  if constexpr (IN8 || OUT8)
+    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, NS, false, IN8, OUT8>), grid, dim3(256), lds, s, b, kt_per,
+                       k_tiles);
+  else if (a.stem)
     hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, NS, true>), grid, dim3(256), lds, s, b, kt_per, k_tiles);
   else
     hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, NS, false>), grid, dim3(256), lds, s, b, kt_per, k_tiles);
@@ -458,7 +529,7 @@ int conv_pick_split_k(const ConvArgs& a, int num_cus) {
   const long M = (long)a.B * a.Ho * a.Wo;
   const long tiles = ((M + BM - 1) / BM) * (a.Npad / BN);
   const int k_tiles = a.Kpad / 64;
-  if (tiles >= num_cus / 2 || k_tiles < 16) return 1;
+  if (a.in_fp8 || a.out_fp8 || tiles >= num_cus / 2 || k_tiles < 16) return 1;
   int s = (int)((num_cus + tiles - 1) / tiles);
   s = std::min(s, k_tiles / 8);
   s = std::min(s, 16);
@@ -473,9 +544,12 @@ size_t conv_splitk_ws_elems(const ConvArgs& a) {
 void conv2d_igemm(const ConvArgs& a, hipStream_t s) {
   if (a.stem) {
     if (a.Cin != 3) throw std::invalid_argument("conv2d_igemm: stem expects the packed RGB image (Cin == 3)");
-  } else if (a.Cin % 64 != 0) {
-    throw std::invalid_argument("conv2d_igemm: Cin must be a multiple of 64");
+  } else if (a.Cin % (a.in_fp8 ? 128 : 64) != 0) {
+    throw std::invalid_argument("conv2d_igemm: Cin must be a multiple of 64 (128 for fp8)");
   }
+  if ((a.in_fp8 || a.out_fp8) && (a.stem || a.split_k > 1 || a.out_f32))
+    throw std::invalid_argument("conv2d_igemm: fp8 has no stem / split-K / fp32-output variant");
+  if (a.in_fp8 && !a.alpha) throw std::invalid_argument("conv2d_igemm: fp8 input needs alpha");
   if (a.Kpad != conv_kpad(a.Cin, a.KH, a.KW, a.stem)) throw std::invalid_argument("conv2d_igemm: bad Kpad");
   if (a.N % 4 != 0 || a.N > a.Npad || a.ldo < a.N || a.ldo % 4 != 0)
     throw std::invalid_argument("conv2d_igemm: bad N/ldo");
@@ -501,13 +575,27 @@ void conv2d_igemm(const ConvArgs& a, hipStream_t s) {
   if ((long)a.B * a.H * a.W * a.Cin >= (1L << 31) || M * a.ldo >= (1L << 31) ||
       (long)a.Npad * a.Kpad >= (1L << 31))
     throw std::invalid_argument("conv2d_igemm: tensor too large for 32-bit offsets");
-  const int k_tiles = a.Kpad / 64;
+  const int k_tiles = a.Kpad / (a.in_fp8 ? 128 : 64);
   int splits = std::max(1, a.split_k);
   if (splits > 1 && !a.ws) throw std::invalid_argument("conv2d_igemm: split-K needs a workspace");
   const int kt_per = (k_tiles + splits - 1) / splits;
   splits = (k_tiles + kt_per - 1) / kt_per;
   ConvArgs b = a;
   b.split_k = splits;
+  if (a.in_fp8 || a.out_fp8) {  // fp8 is built for the 128x128 and 256x64 tiles only
+    const int fcfg = (a.tile == 1 || a.Npad % 128 != 0) ? 1 : 0;
+    if (a.Npad % kTiles[fcfg].bn != 0) throw std::invalid_argument("conv2d_igemm: Npad not a multiple of BN");
+    const int v = (a.in_fp8 ? 2 : 0) + (a.out_fp8 ? 1 : 0) + (fcfg == 1 ? 4 : 0);
+    switch (v) {
+      case 1: launch_cfg<128, 128, 2, 2, 2, false, true>(b, 1, k_tiles, k_tiles, s); break;
+      case 2: launch_cfg<128, 128, 2, 2, 2, true, false>(b, 1, k_tiles, k_tiles, s); break;
+      case 3: launch_cfg<128, 128, 2, 2, 2, true, true>(b, 1, k_tiles, k_tiles, s); break;
+      case 5: launch_cfg<256, 64, 4, 1, 2, false, true>(b, 1, k_tiles, k_tiles, s); break;
+      case 6: launch_cfg<256, 64, 4, 1, 2, true, false>(b, 1, k_tiles, k_tiles, s); break;
+      default: launch_cfg<256, 64, 4, 1, 2, true, true>(b, 1, k_tiles, k_tiles, s); break;
+    }
+    return;
+  }
   switch (cfg) {
     case 0: launch_cfg<128, 128, 2, 2, 2>(b, splits, kt_per, k_tiles, s); break;
     case 1: launch_cfg<256, 64, 4, 1, 2>(b, splits, kt_per, k_tiles, s); break;

@@ -49,6 +49,13 @@ struct ConvArgs {
   int tile = -1;            // force a tile config (-1 = heuristic)
   bool persistent = false;  // cap the grid at max_blocks; blocks walk several tiles
   int max_blocks = 0;       // persistent grid size (multiple of 8), e.g. 2 * #CUs
+  // fp8 (OCP e4m3) path, 128x128 / 256x64 tiles, no split-K:
+  //   in_fp8: x, w and res are e4m3 bytes (Cin % 128 == 0); acc is scaled by
+  //           alpha[n] (= s_in * s_w[n], fp32 [Npad]) and res by res_scale
+  //   out_fp8: y = e4m3(v * out_inv_scale), saturating
+  bool in_fp8 = false, out_fp8 = false;
+  const float* alpha = nullptr;
+  float res_scale = 1.f, out_inv_scale = 1.f;
 };
 
 int conv_out_dim(int in, int k, int stride, int pad);
@@ -97,6 +104,10 @@ void conv3x3_rows(const void* x, const void* w, const float* bias, const void* r
 int stem_pool_pick_strip(int B, int PH, int num_cus);
 void stem_conv_pool(const void* x, const void* w, const float* bias, void* y, int B, int S, int Wq, int strip,
                     hipStream_t s);
+
+// One wave of v_mfma_scale_f32_16x16x128_f8f6f4 (fp8 e4m3, unit scales) on
+// raw per-lane registers: a, b = int32 [64 lanes][8], d = f32 [64 lanes][4].
+void mfma_fp8_probe(const void* a, const void* b, float* d, hipStream_t s);
 
 // Row-wise softmax + top-1 over fp32 logits [B, ld] (first N columns).
 void softmax_top1(const float* logits, int B, int N, int ld, int32_t* idx, float* prob,

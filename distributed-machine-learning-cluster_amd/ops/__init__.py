@@ -131,6 +131,55 @@ def conv3x3_rows(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, re
     return y
 
 
+FP8 = torch.float8_e4m3fn  # OCP e4m3 (gfx950), max 448
+FP8_MAX = 448.0
+
+
+def quantize_fp8(t: torch.Tensor, scale: float) -> torch.Tensor:
+    """e4m3(t / scale), saturating."""
+    return (t.float() / scale).clamp(-FP8_MAX, FP8_MAX).to(FP8)
+
+
+def pack_conv_weight_fp8(w: torch.Tensor, device=None) -> tuple[torch.Tensor, torch.Tensor]:
+    """[Cout, Cin, KH, KW] -> (e4m3 [Npad, Kpad] with a per-output-channel
+    scale, fp32 scales [Npad]); k = (kh*KW + kw)*Cin + c as for bf16."""
+    cout, cin, kh, kw = w.shape
+    kpad, npad = conv_kpad(cin, kh, kw), conv_npad(cout)
+    wk = torch.zeros(npad, kpad)
+    wk[:cout, : kh * kw * cin] = w.float().permute(0, 2, 3, 1).reshape(cout, -1)
+    s = (wk.abs().amax(1) / FP8_MAX).clamp_min(1e-12)
+    q = quantize_fp8(wk / s[:, None], 1.0)
+    return (q.to(device), s.to(device)) if device is not None else (q, s)
+
+
+def conv2d_fp8(x: torch.Tensor, w_q: torch.Tensor, alpha: torch.Tensor, cout: int, kh: int, kw: int,
+               stride: int = 1, pad: int = 0, bias: torch.Tensor | None = None, res: torch.Tensor | None = None,
+               res_scale: float = 1.0, relu: bool = False, out_scale: float | None = None,
+               tile: int = -1) -> torch.Tensor:
+    """fp8 implicit-GEMM conv (block-scaled e4m3 MFMA). x: e4m3 NHWC
+    (Cin % 128 == 0) or bf16 (then w_q is bf16-packed and alpha unused).
+    alpha = s_x * s_w[n]; residual e4m3 scaled by res_scale; output e4m3
+    with scale out_scale (or bf16 when out_scale is None)."""
+    _need_cuda(x, w_q, alpha, bias, res)
+    C = native()
+    B, H, W, Cin = x.shape
+    in8 = x.dtype == FP8
+    Ho, Wo = C.conv_out_dim(H, kh, stride, pad), C.conv_out_dim(W, kw, stride, pad)
+    out8 = out_scale is not None
+    y = torch.empty(B, Ho, Wo, cout, device=x.device, dtype=FP8 if out8 else torch.bfloat16)
+    if bias is not None:
+        bias = bias.float().contiguous()
+        if bias.numel() < w_q.shape[0]:
+            bias = torch.nn.functional.pad(bias, (0, w_q.shape[0] - bias.numel()))
+    al = alpha.float().contiguous() if alpha is not None else None
+    C.conv2d(x=_ptr(x.contiguous()), w=_ptr(w_q), bias=_ptr(bias), res=_ptr(res), y=_ptr(y), B=B, H=H, W=W, Cin=Cin,
+             KH=kh, KW=kw, stride=stride, pad=pad, N=cout, Npad=w_q.shape[0], Kpad=w_q.shape[1], ldo=cout,
+             relu=relu, out_f32=False, split_k=1, ws=0, tile=tile, zero=_ptr(_zero_page(x.device)), stem=False,
+             Ho=Ho, Wo=Wo, max_blocks=0, stream=_stream(), in_fp8=in8, out_fp8=out8, alpha=_ptr(al),
+             res_scale=res_scale, out_inv_scale=(1.0 / out_scale) if out8 else 1.0)
+    return y
+
+
 def maxpool2d(x: torch.Tensor, k: int = 3, stride: int = 2, pad: int = 1) -> torch.Tensor:
     _need_cuda(x)
     C = native()
