@@ -108,8 +108,9 @@ __device__ __forceinline__ void wait_tiles(int remaining) {
 // whole K-tile; a lane's A/B fragment is the 32 contiguous bytes of chunks
 // 2*fq, 2*fq+1 of its row (any lane->k map works as long as A and B agree:
 // tests/test_fp8_gpu.py). The epilogue dequantises with a per-channel
-// alpha = s_in * s_w[n], adds bias and the e4m3 residual (x res_scale),
-// applies ReLU and requantises with out_inv_scale (saturating at +-448).
+// alpha = s_in * s_w[n], adds bias and the residual (e4m3 x res_scale when
+// the output is e4m3: in a ResNet block the residual has the output's
+// dtype), applies ReLU and requantises with out_inv_scale (saturating).
 template <int BM, int BN, int WM, int WN, int NS, bool PAIR, bool IN8 = false, bool OUT8 = false>
 __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a, int kt_per_split, int k_tiles) {
   static_assert(!(PAIR && IN8), "the stem is bf16");
@@ -333,7 +334,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a, int kt_p
         }
         const size_t o = (size_t)m * a.ldo + n;
         if (res) {
-          if constexpr (IN8) {
+          if constexpr (OUT8) {  // the residual is the block's previous output: same dtype as y
             float rf[4];
             fp8x4_to_f32(*(const uint32_t*)((const uint8_t*)a.res + o), rf);
 #pragma unroll

@@ -50,9 +50,10 @@ struct ConvArgs {
   bool persistent = false;  // cap the grid at max_blocks; blocks walk several tiles
   int max_blocks = 0;       // persistent grid size (multiple of 8), e.g. 2 * #CUs
   // fp8 (OCP e4m3) path, 128x128 / 256x64 tiles, no split-K:
-  //   in_fp8: x, w and res are e4m3 bytes (Cin % 128 == 0); acc is scaled by
-  //           alpha[n] (= s_in * s_w[n], fp32 [Npad]) and res by res_scale
-  //   out_fp8: y = e4m3(v * out_inv_scale), saturating
+  //   in_fp8: x and w are e4m3 bytes (Cin % 128 == 0); acc is scaled by
+  //           alpha[n] (= s_in * s_w[n], fp32 [Npad])
+  //   out_fp8: y = e4m3(v * out_inv_scale), saturating; res (if any) is e4m3
+  //           scaled by res_scale (bf16 otherwise)
   bool in_fp8 = false, out_fp8 = false;
   const float* alpha = nullptr;
   float res_scale = 1.f, out_inv_scale = 1.f;
@@ -71,8 +72,10 @@ void conv2d_igemm(const ConvArgs& a, hipStream_t s);
 // 3x3/s2-style max pooling, NHWC bf16, C % 8 == 0.
 void maxpool2d(const void* x, void* y, int B, int H, int W, int C, int Ho, int Wo, int k,
                int stride, int pad, hipStream_t s);
-// Global average pool [B,H,W,C] -> [B,C] bf16, C % 8 == 0.
-void avgpool_global(const void* x, void* y, int B, int HW, int C, hipStream_t s);
+// Global average pool [B,H,W,C] -> [B,C] bf16, C % 8 == 0; in_fp8: e4m3
+// input dequantised by `scale`.
+void avgpool_global(const void* x, void* y, int B, int HW, int C, hipStream_t s, bool in_fp8 = false,
+                    float scale = 1.f);
 // Adaptive average pool to (Ho,Wo), NHWC bf16 (AlexNet avgpool(6,6)).
 void avgpool_adaptive(const void* x, void* y, int B, int H, int W, int C, int Ho, int Wo,
                       hipStream_t s);

@@ -45,20 +45,34 @@ __global__ __launch_bounds__(256) void maxpool_kernel(const bf16* __restrict__ x
 }
 
 // One thread per (b, 8-channel group); loops over HW. HW <= 64 for ResNet.
-__global__ __launch_bounds__(256) void avgpool_global_kernel(const bf16* __restrict__ x,
+// FP8: the input is e4m3 (ResNet50 fp8 path) dequantised by `scale`.
+template <bool FP8>
+__global__ __launch_bounds__(256) void avgpool_global_kernel(const void* __restrict__ xv,
                                                              bf16* __restrict__ y, int B, int HW,
-                                                             int C) {
+                                                             int C, float scale) {
   const int c8 = C / 8;
   const long total = (long)B * c8;
-  const float inv = 1.f / HW;
+  const float inv = (FP8 ? scale : 1.f) / HW;
   for (long idx = blockIdx.x * 256L + threadIdx.x; idx < total; idx += (long)gridDim.x * 256) {
     const int cg = (int)(idx % c8);
     const int b = (int)(idx / c8);
     float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    const bf16* p = x + (long)b * HW * C + cg * 8;
+    const long base = (long)b * HW * C + cg * 8;
     for (int i = 0; i < HW; ++i) {
       float f[8];
-      unpack8(*(const uint4*)(p + (long)i * C), f);
+      if constexpr (FP8) {
+        const uint2 u = *(const uint2*)((const uint8_t*)xv + base + (long)i * C);
+        f[0] = __builtin_amdgcn_cvt_f32_fp8((int)u.x, 0);
+        f[1] = __builtin_amdgcn_cvt_f32_fp8((int)u.x, 1);
+        f[2] = __builtin_amdgcn_cvt_f32_fp8((int)u.x, 2);
+        f[3] = __builtin_amdgcn_cvt_f32_fp8((int)u.x, 3);
+        f[4] = __builtin_amdgcn_cvt_f32_fp8((int)u.y, 0);
+        f[5] = __builtin_amdgcn_cvt_f32_fp8((int)u.y, 1);
+        f[6] = __builtin_amdgcn_cvt_f32_fp8((int)u.y, 2);
+        f[7] = __builtin_amdgcn_cvt_f32_fp8((int)u.y, 3);
+      } else {
+        unpack8(*(const uint4*)((const bf16*)xv + base + (long)i * C), f);
+      }
 #pragma unroll
       for (int j = 0; j < 8; ++j) s[j] += f[j];
     }
@@ -114,12 +128,16 @@ void maxpool2d(const void* x, void* y, int B, int H, int W, int C, int Ho, int W
   DMLC_HIP_CHECK(hipGetLastError());
 }
 
-void avgpool_global(const void* x, void* y, int B, int HW, int C, hipStream_t s) {
+void avgpool_global(const void* x, void* y, int B, int HW, int C, hipStream_t s, bool in_fp8, float scale) {
   if (C % 8 != 0) throw std::invalid_argument("avgpool_global: C % 8 != 0");
   const long work = (long)B * (C / 8);
   if (work == 0) return;
-  hipLaunchKernelGGL(avgpool_global_kernel, dim3(grid_for(work)), dim3(256), 0, s, (const bf16*)x,
-                     (bf16*)y, B, HW, C);
+  if (in_fp8)
+    hipLaunchKernelGGL(avgpool_global_kernel<true>, dim3(grid_for(work)), dim3(256), 0, s, x, (bf16*)y, B, HW, C,
+                       scale);
+  else
+    hipLaunchKernelGGL(avgpool_global_kernel<false>, dim3(grid_for(work)), dim3(256), 0, s, x, (bf16*)y, B, HW, C,
+                       1.f);
   DMLC_HIP_CHECK(hipGetLastError());
 }
 

@@ -40,6 +40,36 @@ uint16_t f2bf_host(float f) {
   return (uint16_t)(u >> 16);
 }
 
+float bf2f_host(uint16_t b) {
+  const uint32_t u = (uint32_t)b << 16;
+  float f;
+  std::memcpy(&f, &u, 4);
+  return f;
+}
+
+// float -> OCP e4m3 (bias 7, max 448, no infinities), round to nearest even,
+// saturating; exact by search over the 127 non-negative finite codes.
+uint8_t f2e4m3_host(float f) {
+  static const std::vector<float> table = [] {
+    std::vector<float> t(127);
+    for (int c = 0; c < 127; ++c) {
+      const int e = c >> 3, m = c & 7;
+      t[c] = e == 0 ? std::ldexp((float)m / 8.f, -6) : std::ldexp(1.f + (float)m / 8.f, e - 7);
+    }
+    return t;
+  }();
+  if (std::isnan(f)) return 0x7f;
+  const uint8_t sign = std::signbit(f) ? 0x80 : 0;
+  const float a = std::fabs(f);
+  if (a >= 448.f) return sign | 0x7e;
+  int c = (int)(std::upper_bound(table.begin(), table.end(), a) - table.begin()) - 1;  // table[c] <= a
+  if (c < 126) {
+    const float lo = table[c], hi = table[c + 1];
+    if (a - lo > hi - a || (a - lo == hi - a && (c & 1))) ++c;
+  }
+  return sign | (uint8_t)c;
+}
+
 }  // namespace
 
 Engine::Engine(const std::string& arch, const WeightMap& weights, int device, int num_classes,
@@ -60,6 +90,12 @@ Engine::Engine(const std::string& arch, const WeightMap& weights, int device, in
     build_resnet({3, 4, 6, 3}, false);
   else if (arch == "resnet50")
     build_resnet({3, 4, 6, 3}, true);
+  else if (arch == "resnet50_fp8") {
+    fp8_ = true;
+    build_resnet({3, 4, 6, 3}, true);
+    mark_fp8();
+    calibrate(weights);
+  }
   else if (arch == "alexnet")
     build_alexnet();
   else
@@ -115,6 +151,7 @@ int Engine::conv(int in, const std::string& name, const std::string& bn, int cou
     os.H = conv_out_dim(image_size_, k, stride, stem_pad_);
     os.W = os.H;
   }
+  convs_.back().in_act = in;
   const int out = add_act(os);
   Op op{OpType::Conv, in, out, res, (int)convs_.size() - 1, 0, 0, 0, name};
   ops_.push_back(op);
@@ -236,16 +273,71 @@ void Engine::build_alexnet() {
   ops_.push_back(Op{OpType::SoftmaxTop1, logits_act_, -1, -1, -1, 0, 0, 0, "softmax_top1"});
 }
 
+// resnet50_fp8: every conv output with a multiple of 128 channels is e4m3:
+// the 256..2048-channel block outputs and residual paths (where the bytes
+// are: layer1's 56x56x256 tensors dominate the traffic) and all of layers
+// 2-4. The stem and layer1's 64-channel inner convs stay bf16 (Cin = 64 is
+// below the fp8 kernel's 128-channel K-tile; the 3x3 runs conv3x3_rows).
+void Engine::mark_fp8() {
+  for (const Op& op : ops_)
+    if (op.type == OpType::Conv && !convs_[op.conv].fc && shapes_[op.out].C % 128 == 0) shapes_[op.out].fp8 = true;
+  for (const Op& op : ops_) {
+    if (op.type != OpType::Conv) continue;
+    if (op.res >= 0 && shapes_[op.res].fp8 != shapes_[op.out].fp8)
+      throw std::runtime_error("mark_fp8: residual and output dtypes differ at " + op.name);
+    if (shapes_[op.in].fp8 && shapes_[op.in].C % 128)
+      throw std::runtime_error("mark_fp8: fp8 conv needs Cin % 128 == 0: " + op.name);
+  }
+}
+
+// Static per-tensor activation scales: run the bf16 model on a synthetic
+// calibration batch and take amax/448 of every tensor that is stored as e4m3.
+void Engine::calibrate(const WeightMap& w) {
+  const int Bc = 8;
+  Engine ref(arch_.substr(0, arch_.find("_fp8")), w, device_, num_classes_, image_size_);
+  if (ref.num_activations() != num_activations()) throw std::runtime_error("calibrate: graph mismatch");
+  ref.reserve(Bc);
+  const size_t img_bytes = (size_t)Bc * image_size_ * image_size_ * 3;
+  std::vector<uint8_t> host(img_bytes);
+  uint32_t st = 12345u;  // fixed-seed xorshift: deterministic scales
+  for (auto& v : host) {
+    st ^= st << 13;
+    st ^= st >> 17;
+    st ^= st << 5;
+    v = (uint8_t)(st >> 24);
+  }
+  uint8_t* d_img = nullptr;
+  DMLC_HIP_CHECK(hipMalloc(&d_img, img_bytes));
+  DMLC_HIP_CHECK(hipMemcpy(d_img, host.data(), img_bytes, hipMemcpyHostToDevice));
+  ref.forward(d_img, Bc, image_size_, image_size_, nullptr, nullptr, nullptr, nullptr, false);
+  DMLC_HIP_CHECK(hipDeviceSynchronize());
+  DMLC_HIP_CHECK(hipFree(d_img));
+  for (int i = 0; i < num_activations(); ++i) {
+    if (!shapes_[i].fp8) continue;
+    const size_t n = shapes_[i].elems_per_image() * Bc;
+    std::vector<uint16_t> a(n);
+    DMLC_HIP_CHECK(hipMemcpy(a.data(), ref.activation(i), n * 2, hipMemcpyDeviceToHost));
+    float amax = 0.f;
+    for (uint16_t v : a) amax = std::max(amax, std::fabs(bf2f_host(v)));
+    shapes_[i].scale = std::max(amax, 1e-6f) / 448.f;
+  }
+}
+
 void Engine::pack_weights(const WeightMap& w) {
   // Layout pass.
   size_t off = 0;
   for (auto& L : convs_) {
     L.npad = conv_npad(L.cout);
     L.kpad = L.stem_pool ? kStemPoolK : conv_kpad(L.cin_eff, L.kh, L.kw, L.pair);
+    L.fp8 = L.in_act >= 0 && shapes_[L.in_act].fp8;
     L.w_off = off;
-    off = align_up(off + (size_t)L.npad * L.kpad * 2, 256);
+    off = align_up(off + (size_t)L.npad * L.kpad * (L.fp8 ? 1 : 2), 256);
     L.b_off = off;
     off = align_up(off + (size_t)L.npad * 4, 256);
+    if (L.fp8) {
+      L.a_off = off;
+      off = align_up(off + (size_t)L.npad * 4, 256);
+    }
   }
   weight_bytes_ = off;
   std::vector<uint8_t> host(off, 0);
@@ -268,7 +360,12 @@ void Engine::pack_weights(const WeightMap& w) {
         bias[n] = (float)((double)b.data[n] + ((double)bias[n] - (double)m.data[n]) * s);
       }
     }
+    std::vector<uint16_t> wbf;
     uint16_t* pw = (uint16_t*)(host.data() + L.w_off);
+    if (L.fp8) {  // fold into a bf16 staging copy first, then quantise per row
+      wbf.assign((size_t)L.npad * L.kpad, 0);
+      pw = wbf.data();
+    }
     float* pb = (float*)(host.data() + L.b_off);
     if (!L.fc) {
       if (W.shape.size() != 4 || W.shape[0] != L.cout || W.shape[1] != L.cin || W.shape[2] != L.kh ||
@@ -303,6 +400,19 @@ void Engine::pack_weights(const WeightMap& w) {
         }
     }
     for (int n = 0; n < L.cout; ++n) pb[n] = bias[n];
+    if (L.fp8) {
+      // e4m3 weights with a per-output-channel scale; alpha = s_in * s_w[n]
+      uint8_t* q = host.data() + L.w_off;
+      float* alpha = (float*)(host.data() + L.a_off);
+      const float s_in = shapes_[L.in_act].scale;
+      for (int n = 0; n < L.npad; ++n) {
+        float amax = 0.f;
+        for (int k = 0; k < L.kpad; ++k) amax = std::max(amax, std::fabs(bf2f_host(pw[(size_t)n * L.kpad + k])));
+        const float sw = amax > 0.f ? amax / 448.f : 1.f;
+        for (int k = 0; k < L.kpad; ++k) q[(size_t)n * L.kpad + k] = f2e4m3_host(bf2f_host(pw[(size_t)n * L.kpad + k]) / sw);
+        alpha[n] = s_in * sw;
+      }
+    }
   }
   DMLC_HIP_CHECK(hipMalloc(&warena_, weight_bytes_));
   DMLC_HIP_CHECK(hipMemcpy(warena_, host.data(), weight_bytes_, hipMemcpyHostToDevice));
@@ -320,7 +430,7 @@ void Engine::reserve(int max_batch) {
   size_t total = 0;
   for (const auto& s : shapes_) {
     offs.push_back(total);
-    total = align_up(total + s.elems_per_image() * max_batch * (s.f32 ? 4 : 2), 256);
+    total = align_up(total + s.elems_per_image() * max_batch * s.elem_bytes(), 256);
   }
   void* base = nullptr;
   DMLC_HIP_CHECK(hipMalloc(&base, total));
@@ -376,6 +486,11 @@ ConvArgs Engine::conv_args(const Op& op, int B, float* logits) const {
   a.ldo = L.cout;
   a.relu = L.relu;
   a.out_f32 = os.f32;
+  a.in_fp8 = L.fp8;
+  a.out_fp8 = os.fp8;
+  if (L.fp8) a.alpha = (const float*)((const uint8_t*)warena_ + L.a_off);
+  if (op.res >= 0 && shapes_[op.res].fp8) a.res_scale = shapes_[op.res].scale;
+  if (os.fp8) a.out_inv_scale = 1.f / os.scale;
   int s = conv_pick_split_k(a, num_cus_);
   const size_t M = (size_t)B * os.H * os.W;
   while (s > 1 && (size_t)s * M * L.npad > ws_elems_) --s;
@@ -403,8 +518,8 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
       case OpType::Conv: {
         const ConvLayer& L = convs_[op.conv];
         const ActShape& is = shapes_[op.in];
-        if (row_conv_ && !L.fc && !L.pair && L.kh == 3 && L.kw == 3 && L.stride == 1 && L.pad == 1 &&
-            !shapes_[op.out].f32 && conv3x3_rows_supported(is.H, is.W, is.C, L.cout)) {
+        if (row_conv_ && !L.fc && !L.pair && !L.fp8 && L.kh == 3 && L.kw == 3 && L.stride == 1 && L.pad == 1 &&
+            !shapes_[op.out].f32 && !shapes_[op.out].fp8 && conv3x3_rows_supported(is.H, is.W, is.C, L.cout)) {
           conv3x3_rows(acts_[op.in], (const uint8_t*)warena_ + L.w_off,
                        (const float*)((const uint8_t*)warena_ + L.b_off), op.res >= 0 ? acts_[op.res] : nullptr,
                        acts_[op.out], zero_, B, is.H, is.W, is.C, L.relu, conv3x3_rows_pick_strip(B, is.H, num_cus_),
@@ -429,7 +544,7 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
       }
       case OpType::AvgPoolGlobal: {
         const ActShape& i = shapes_[op.in];
-        avgpool_global(acts_[op.in], acts_[op.out], B, i.H * i.W, i.C, s);
+        avgpool_global(acts_[op.in], acts_[op.out], B, i.H * i.W, i.C, s, i.fp8, i.scale);
         break;
       }
       case OpType::AvgPoolAdaptive: {

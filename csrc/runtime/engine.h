@@ -25,7 +25,10 @@ enum class OpType { Preprocess, Conv, StemPool, MaxPool, AvgPoolGlobal, AvgPoolA
 struct ActShape {
   int H = 0, W = 0, C = 0;
   bool f32 = false;
+  bool fp8 = false;   // OCP e4m3 with a per-tensor scale (resnet50_fp8)
+  float scale = 1.f;  // value = e4m3 * scale (calibrated)
   size_t elems_per_image() const { return (size_t)H * W * C; }
+  size_t elem_bytes() const { return f32 ? 4 : fp8 ? 1 : 2; }
 };
 
 struct ConvLayer {
@@ -39,6 +42,9 @@ struct ConvLayer {
   int fc_hwc[3] = {0, 0, 0};  // for fc after a spatial tensor: (H,W,C) of the flatten
   int npad = 0, kpad = 0;
   size_t w_off = 0, b_off = 0;  // offsets (bytes) into the weight arena
+  int in_act = -1;              // activation the conv reads
+  bool fp8 = false;             // e4m3 weights (input activation is e4m3)
+  size_t a_off = 0;             // fp8: alpha[n] = s_in * s_w[n] (fp32 [npad])
 };
 
 struct Op {
@@ -51,7 +57,9 @@ struct Op {
 
 class Engine {
  public:
-  // arch: resnet18 | resnet34 | resnet50 | alexnet
+  // arch: resnet18 | resnet34 | resnet50 | alexnet | resnet50_fp8 (layers 2-4
+  // on the block-scaled e4m3 MFMA: per-channel weight scales, per-tensor
+  // activation scales calibrated at load time on a synthetic batch)
   Engine(const std::string& arch, const WeightMap& weights, int device, int num_classes = 1000,
          int image_size = 224);
   ~Engine();
@@ -97,6 +105,8 @@ class Engine {
   void build_resnet(const std::vector<int>& blocks, bool bottleneck);
   void build_alexnet();
   void pack_weights(const WeightMap& w);
+  void mark_fp8();
+  void calibrate(const WeightMap& w);
   void run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* idx, float* prob,
                float* logits, hipStream_t s, std::vector<hipEvent_t>* evs, bool trace);
   ConvArgs conv_args(const Op& op, int B, float* logits) const;
@@ -111,6 +121,7 @@ class Engine {
   bool persistent_ = true;  // persistent conv grids (env DMLC_PERSISTENT=0 disables)
   bool fused_stem_ = true;  // conv1+maxpool as one kernel (env DMLC_FUSED_STEM=0 disables)
   bool row_conv_ = true;    // direct row-streaming 3x3 convs where supported (env DMLC_ROW_CONV=0 disables)
+  bool fp8_ = false;        // resnet50_fp8
 
   std::vector<ActShape> shapes_;
   std::vector<ConvLayer> convs_;

@@ -132,6 +132,7 @@ def build(arch: str, num_classes: int = 1000, seed: int | None = 0, randomize_bn
     git-LFS stubs — pretrained_models/*.ot:1-3 — so every run uses random
     weights of the right architecture). ``randomize_bn`` draws non-trivial
     BN statistics so that BN folding is actually exercised by tests."""
+    arch = arch[:-4] if arch.endswith("_fp8") else arch  # same weights; e4m3 is an engine precision mode
     if arch not in ARCHS:
         raise ValueError(f"unknown arch {arch!r}; choose from {sorted(ARCHS)}")
     g = torch.random.fork_rng() if seed is not None else None

@@ -39,6 +39,35 @@ def test_engine_matches_reference(gpu, arch):
     assert torch.allclose(prob.cpu(), ref_p.max(-1).values, rtol=0.1, atol=2e-3)
 
 
+def test_engine_resnet50_fp8(gpu):
+    """ResNet50 with layers 2-4 on the block-scaled e4m3 MFMA (per-channel
+    weight scales, per-tensor activation scales calibrated at load) vs the
+    fp32 reference: e4m3 keeps 3 mantissa bits, so the bar is looser than the
+    bf16 engine's: logits within 15% (relative L2) and top-1 agreement on
+    all but near-ties."""
+    model = build("resnet50", seed=11, randomize_bn=True)
+    sd = state_dict_f32(model)
+    eng = InferenceEngine("resnet50_fp8", sd, max_batch=16)
+    g = torch.Generator().manual_seed(12)
+    img = torch.randint(0, 256, (16, 224, 224, 3), generator=g, dtype=torch.uint8)
+    ref = _ref_logits(model, img)
+    idx, prob, logits = eng.predict(img.to(gpu), return_logits=True, use_graph=False)
+    torch.cuda.synchronize()
+    rel = ((logits.cpu() - ref).norm() / ref.norm()).item()
+    cos = torch.nn.functional.cosine_similarity(logits.cpu(), ref, dim=-1).min().item()
+    agree = (idx.cpu().long() == ref.argmax(-1)).float().mean().item()
+    print(f"resnet50_fp8 vs fp32: rel {rel:.4f} min-cos {cos:.4f} top1 agree {agree:.3f}")
+    assert rel < 0.15 and cos > 0.98, (rel, cos)
+    ref_p = torch.softmax(ref, -1)
+    top2 = ref_p.topk(2, -1).values
+    near_tie = (top2[:, 0] - top2[:, 1]) < 5e-2
+    mism = idx.cpu().long() != ref.argmax(-1)
+    assert torch.all(~mism | near_tie), (agree, rel)
+    # graph replay gives the same answer
+    i2, p2 = eng.predict(img.to(gpu), use_graph=True)
+    assert torch.equal(i2.cpu(), idx.cpu())
+
+
 def test_graph_replay_matches_eager(gpu):
     eng = InferenceEngine("resnet18", max_batch=32)
     img = torch.randint(0, 256, (32, 224, 224, 3), dtype=torch.uint8, device=gpu)
