@@ -145,7 +145,8 @@ def main():
         n_img = B * world * args.steps
         value = n_img / elapsed
         res = {
-            "metric": "images/sec (whole node) + p50/p95 query latency, ResNet18 ImageNet",
+            "metric": "images/sec (whole node) + p50/p95 query latency, "
+                      + ("ResNet18" if args.model == "resnet18" else args.model) + " ImageNet",
             "value": round(value, 1),
             "unit": "images/s",
             "n_gpus": world,
@@ -154,8 +155,8 @@ def main():
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": round(value / REF_STREAM_IMG_S, 1),
-            "dtype": "bf16",
+            "vs_baseline": round(value / REF_STREAM_IMG_S, 1) if args.model == "resnet18" else None,
+            "dtype": "fp8" if args.model.endswith("_fp8") else "bf16",
             "data": "synthetic u8 224x224x3 images (HBM-staged on rank 0), random-init weights",
             "config": {
                 "model": args.model,
