@@ -464,15 +464,20 @@ struct TileCfg {
 // within +-3% of these and was dropped; ns3/ns4 lose 30% to the halved
 // occupancy: profiles/r1_conv_bench_stages.log.)
 //   7: 128x64 ns2 (waves 2x2 of 64x32)   8: 64x128 ns2 (waves 2x2 of 32x64)
-constexpr int kNumTiles = 9;
+//   9: 128x64 ns3  10: 64x128 ns3 (72 KB: deeper prefetch at 2 blocks per CU)
+constexpr int kNumTiles = 11;
 constexpr TileCfg kTiles[kNumTiles] = {{128, 128, 2}, {256, 64, 2}, {64, 256, 2}, {128, 128, 3}, {256, 64, 3},
-                                       {64, 256, 3},  {128, 128, 4}, {128, 64, 2}, {64, 128, 2}};
+                                       {64, 256, 3},  {128, 128, 4}, {128, 64, 2}, {64, 128, 2}, {128, 64, 3},
+                                       {64, 128, 3}};
 
 int pick_tile(const ConvArgs& a) {
   if (a.tile >= 0 && a.tile < kNumTiles) return a.tile;
   if (a.Npad % 128 != 0) return 1;
   const long M = (long)a.B * a.Ho * a.Wo;
   if (M <= 64 && a.Npad % 256 == 0) return 2;
+  // N = 128 over many pixels (ResNet layer2): 64x128 tiles measured 5-11%
+  // faster than 128x128 (profiles/r1_conv_tiles_ns3.log)
+  if (a.Npad == 128 && M >= 64L * 1024) return 8;
   return 0;
 }
 
@@ -606,7 +611,9 @@ void conv2d_igemm(const ConvArgs& a, hipStream_t s) {
     case 5: launch_cfg<64, 256, 1, 4, 3>(b, splits, kt_per, k_tiles, s); break;
     case 6: launch_cfg<128, 128, 2, 2, 4>(b, splits, kt_per, k_tiles, s); break;
     case 7: launch_cfg<128, 64, 2, 2, 2>(b, splits, kt_per, k_tiles, s); break;
-    default: launch_cfg<64, 128, 2, 2, 2>(b, splits, kt_per, k_tiles, s); break;
+    case 8: launch_cfg<64, 128, 2, 2, 2>(b, splits, kt_per, k_tiles, s); break;
+    case 9: launch_cfg<128, 64, 2, 2, 3>(b, splits, kt_per, k_tiles, s); break;
+    default: launch_cfg<64, 128, 2, 2, 3>(b, splits, kt_per, k_tiles, s); break;
   }
   if (splits > 1) {
     const int blocks = (int)std::min<long>((M * (a.N / 4) + 255) / 256, 4096);

@@ -57,7 +57,7 @@ def main():
         for t in tiles:
             if t in (2, 5) and Cout % 256:
                 continue
-            if t in (0, 2, 3, 5, 6, 8) and Cout % 128:
+            if t in (0, 2, 3, 5, 6, 8, 10) and Cout % 128:
                 continue
             try:
                 f = lambda: ops.conv2d(x, wp, Cout, k, k, s, p, bias=bias, relu=True, tile=t, stem=pair,
