@@ -65,7 +65,7 @@ PYBIND11_MODULE(_C, m) {
          int Cin, int KH, int KW, int stride, int pad, int N, int Npad, int Kpad, int ldo, bool relu,
          bool out_f32, int split_k, uintptr_t ws, int tile, uintptr_t zero, bool stem, int Ho, int Wo,
          int max_blocks, uintptr_t stream, bool in_fp8, bool out_fp8, uintptr_t alpha, float res_scale,
-         float out_inv_scale) {
+         float out_inv_scale, uintptr_t bt_ws, size_t bt_ws_bytes, int bt_splits) {
         ConvArgs a;
         a.x = P<void>(x);
         a.zero = P<void>(zero);
@@ -100,6 +100,11 @@ PYBIND11_MODULE(_C, m) {
         a.alpha = P<float>(alpha);
         a.res_scale = res_scale;
         a.out_inv_scale = out_inv_scale;
+        if (tile >= kConvBigTile0) {  // 8-wave big-tile configs (conv_bigtile.hip)
+          a.tile = -1;
+          conv2d_bigtile(a, tile - kConvBigTile0, bt_splits, P<void>(bt_ws), bt_ws_bytes, S(stream));
+          return;
+        }
         conv2d_igemm(a, S(stream));
       },
       py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("res"), py::arg("y"), py::arg("B"),
@@ -108,7 +113,22 @@ PYBIND11_MODULE(_C, m) {
       py::arg("relu"), py::arg("out_f32"), py::arg("split_k"), py::arg("ws"), py::arg("tile"),
       py::arg("zero"), py::arg("stem"), py::arg("Ho"), py::arg("Wo"), py::arg("max_blocks"),
       py::arg("stream"), py::arg("in_fp8") = false, py::arg("out_fp8") = false, py::arg("alpha") = 0,
-      py::arg("res_scale") = 1.f, py::arg("out_inv_scale") = 1.f);
+      py::arg("res_scale") = 1.f, py::arg("out_inv_scale") = 1.f, py::arg("bt_ws") = 0, py::arg("bt_ws_bytes") = 0,
+      py::arg("bt_splits") = 1);
+  m.def("conv_bigtile_ws_bytes", &conv_bigtile_ws_bytes);
+  m.def("conv_bigtile_ws_header_bytes", &conv_bigtile_ws_header_bytes);
+  m.def(
+      "conv_bigtile_splits",
+      [](int B, int Ho, int Wo, int Npad, int Kpad, int cfg, int num_cus) {
+        ConvArgs a;
+        a.B = B;
+        a.Ho = Ho;
+        a.Wo = Wo;
+        a.Npad = Npad;
+        a.Kpad = Kpad;
+        return conv_bigtile_splits(a, cfg, num_cus);
+      });
+  m.attr("CONV_BIGTILE0") = kConvBigTile0;
   m.def("maxpool2d", [](uintptr_t x, uintptr_t y, int B, int H, int W, int C, int k, int stride,
                         int pad, uintptr_t stream) {
     maxpool2d(P<void>(x), P<void>(y), B, H, W, C, conv_out_dim(H, k, stride, pad),

@@ -69,6 +69,22 @@ size_t conv_splitk_ws_elems(const ConvArgs& a);
 int conv_pick_split_k(const ConvArgs& a, int num_cus);
 void conv2d_igemm(const ConvArgs& a, hipStream_t s);
 
+// Big-tile conv (conv_bigtile.hip): 8-wave 256x256 (cfg 0, Npad % 256 == 0)
+// or 256x128 (cfg 1, Npad == 128) tiles, bf16 in/out, no stem/fp8, with an
+// XCD-local K-lockstep split-K over `splits` slices. ws (needed when
+// splits > 1): conv_bigtile_ws_bytes(slabs) bytes whose first
+// conv_bigtile_ws_header_bytes() are zeroed once at allocation (hand-off
+// flags, left zeroed by every completed launch, then an error word that a
+// timed-out hand-off sets to 1), followed by the fp32 partial-tile slabs.
+// Python/tests select config c with tile = kConvBigTile0 + c.
+constexpr int kConvBigTile0 = 11;
+int conv_bigtile_pick(const ConvArgs& a, int num_cus);  // engine's choice: config, or -1 (old kernel)
+int conv_bigtile_splits(const ConvArgs& a, int cfg, int num_cus);
+long conv_bigtile_slabs(const ConvArgs& a, int cfg, int splits);
+size_t conv_bigtile_ws_bytes(long max_slabs);
+size_t conv_bigtile_ws_header_bytes();
+void conv2d_bigtile(const ConvArgs& a, int cfg, int splits, void* ws, size_t ws_bytes, hipStream_t s);
+
 // 3x3/s2-style max pooling, NHWC bf16, C % 8 == 0.
 void maxpool2d(const void* x, void* y, int B, int H, int W, int C, int Ho, int Wo, int k,
                int stride, int pad, hipStream_t s);

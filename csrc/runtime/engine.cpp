@@ -83,6 +83,7 @@ Engine::Engine(const std::string& arch, const WeightMap& weights, int device, in
   if (const char* e = std::getenv("DMLC_PERSISTENT")) persistent_ = std::string(e) != "0";
   if (const char* e = std::getenv("DMLC_FUSED_STEM")) fused_stem_ = std::string(e) != "0";
   if (const char* e = std::getenv("DMLC_ROW_CONV")) row_conv_ = std::string(e) != "0";
+  if (const char* e = std::getenv("DMLC_BIGTILE")) bigtile_ = std::string(e) != "0";
 
   if (arch == "resnet18")
     build_resnet({2, 2, 2, 2}, false);
@@ -117,6 +118,7 @@ Engine::~Engine() {
   if (!acts_.empty() && acts_[0]) hipFree(acts_[0]);
   if (warena_) hipFree(warena_);
   if (ws_) hipFree(ws_);
+  if (bt_ws_) hipFree(bt_ws_);
   if (zero_) hipFree(zero_);
   if (dummy_idx_) hipFree(dummy_idx_);
   if (ev_in_) hipEventDestroy(ev_in_);
@@ -439,6 +441,18 @@ void Engine::reserve(int max_batch) {
   act_bytes_ = total;
   DMLC_HIP_CHECK(hipMalloc(&dummy_idx_, (size_t)max_batch * 8));
   max_batch_ = max_batch;
+  // big-tile conv split-K slabs for the largest batch
+  long slabs = 0;
+  for (const Op& op : ops_) {
+    if (op.type != OpType::Conv) continue;
+    const ConvArgs a = conv_args(op, max_batch, nullptr);
+    const int cfg = bigtile_ ? conv_bigtile_pick(a, num_cus_) : -1;
+    if (cfg >= 0) slabs = std::max(slabs, conv_bigtile_slabs(a, cfg, conv_bigtile_splits(a, cfg, num_cus_)));
+  }
+  if (bt_ws_) DMLC_HIP_CHECK(hipFree(bt_ws_));
+  bt_ws_bytes_ = conv_bigtile_ws_bytes(slabs);
+  DMLC_HIP_CHECK(hipMalloc(&bt_ws_, bt_ws_bytes_));
+  DMLC_HIP_CHECK(hipMemset(bt_ws_, 0, conv_bigtile_ws_header_bytes()));
 }
 
 double Engine::gflop_per_image() const {
@@ -525,7 +539,15 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
                        acts_[op.out], zero_, B, is.H, is.W, is.C, L.relu, conv3x3_rows_pick_strip(B, is.H, num_cus_),
                        s);
         } else {
-          conv2d_igemm(conv_args(op, B, logits), s);
+          const ConvArgs a = conv_args(op, B, logits);
+          const int bt = bigtile_ ? conv_bigtile_pick(a, num_cus_) : -1;
+          if (bt >= 0) {
+            int splits = conv_bigtile_splits(a, bt, num_cus_);
+            if (conv_bigtile_ws_bytes(conv_bigtile_slabs(a, bt, splits)) > bt_ws_bytes_) splits = 1;
+            conv2d_bigtile(a, bt, splits, bt_ws_, bt_ws_bytes_, s);
+          } else {
+            conv2d_igemm(a, s);
+          }
         }
         break;
       }

@@ -120,6 +120,7 @@ class Engine {
   int stem_pad_ = 0;
   bool persistent_ = true;  // persistent conv grids (env DMLC_PERSISTENT=0 disables)
   bool fused_stem_ = true;  // conv1+maxpool as one kernel (env DMLC_FUSED_STEM=0 disables)
+  bool bigtile_ = true;     // 8-wave big-tile split-K convs where supported (env DMLC_BIGTILE=0 disables)
   bool row_conv_ = true;    // direct row-streaming 3x3 convs where supported (env DMLC_ROW_CONV=0 disables)
   bool fp8_ = false;        // resnet50_fp8
 
@@ -133,6 +134,8 @@ class Engine {
   std::vector<void*> acts_;
   size_t act_bytes_ = 0;
   float* ws_ = nullptr;
+  void* bt_ws_ = nullptr;  // big-tile conv split-K hand-off flags + partial-tile slabs
+  size_t bt_ws_bytes_ = 0;
   void* zero_ = nullptr;  // 16-B zero page: LDS-DMA source for conv padding taps
   size_t ws_elems_ = 0;
   int32_t* dummy_idx_ = nullptr;

@@ -9,6 +9,8 @@ Layout conventions: activations are bf16 NHWC; conv/linear weights are packed
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from .. import native
@@ -98,19 +100,62 @@ def conv2d(x: torch.Tensor, w_packed: torch.Tensor, cout: int, kh: int, kw: int,
         Ho, Wo = C.conv_out_dim(H, kh, stride, pad), C.conv_out_dim(W, kw, stride, pad)
     if out is None:
         out = torch.empty(B, Ho, Wo, cout, device=x.device, dtype=torch.float32 if out_f32 else torch.bfloat16)
-    ws = None
-    if split_k > 1:
-        ws = torch.empty(split_k * B * Ho * Wo * w_packed.shape[0], device=x.device, dtype=torch.float32)
     if bias is not None:
         bias = bias.float().contiguous()
         if bias.numel() < w_packed.shape[0]:
             bias = torch.nn.functional.pad(bias, (0, w_packed.shape[0] - bias.numel()))
+    bt_ws, bt_bytes, bt_splits = None, 0, 1
+    if tile >= C.CONV_BIGTILE0:  # 8-wave big-tile kernel (conv_bigtile.hip); split_k = K slices (0: engine's choice)
+        bt_splits = split_k if split_k > 0 else C.conv_bigtile_splits(
+            B, Ho, Wo, w_packed.shape[0], w_packed.shape[1], tile - C.CONV_BIGTILE0,
+            torch.cuda.get_device_properties(x.device).multi_processor_count)
+        split_k = 1
+        bm, bn = 256, (256 if tile == C.CONV_BIGTILE0 else 128)
+        slabs = -(-B * Ho * Wo // bm) * (w_packed.shape[0] // bn) * (bt_splits - 1)
+        bt_ws = _bigtile_ws(x.device, C.conv_bigtile_ws_bytes(slabs))
+        bt_bytes = bt_ws.numel()
+    ws = None
+    if tile >= C.CONV_BIGTILE0 and int(os.environ.get("DMLC_BT_DEBUG", "0")) & 32:
+        global BT_STAMPS  # per-workgroup phase stamps of the last launch (debug)
+        if BT_STAMPS is None:
+            BT_STAMPS = torch.zeros(1 << 16, dtype=torch.int64, device=x.device)
+        ws = BT_STAMPS
+    if split_k > 1:
+        ws = torch.empty(split_k * B * Ho * Wo * w_packed.shape[0], device=x.device, dtype=torch.float32)
     C.conv2d(x=_ptr(x.contiguous()), w=_ptr(w_packed), bias=_ptr(bias), res=_ptr(res), y=_ptr(out), B=B, H=H,
              W=W, Cin=Cin, KH=kh, KW=kw, stride=stride, pad=pad, N=cout, Npad=w_packed.shape[0],
              Kpad=w_packed.shape[1], ldo=cout, relu=relu, out_f32=out_f32, split_k=split_k, ws=_ptr(ws),
              tile=tile, zero=_ptr(_zero_page(x.device)), stem=stem, Ho=Ho, Wo=Wo, max_blocks=max_blocks,
-             stream=_stream())
+             stream=_stream(), bt_ws=_ptr(bt_ws), bt_ws_bytes=bt_bytes, bt_splits=bt_splits)
     return out
+
+
+_BT_WS: dict = {}
+BT_STAMPS = None
+
+
+def _bigtile_ws(device: torch.device, nbytes: int) -> torch.Tensor:
+    """Per-device big-tile split-K workspace (hand-off flags zeroed once, then
+    fp32 slabs); grown on demand."""
+    C = native()
+    t = _BT_WS.get(device.index)
+    if t is None or t.numel() < nbytes:
+        if t is not None:
+            torch.cuda.synchronize(device)
+        t = torch.empty(max(nbytes, C.conv_bigtile_ws_bytes(0)), dtype=torch.uint8, device=device)
+        t[:C.conv_bigtile_ws_header_bytes()].zero_()
+        _BT_WS[device.index] = t
+    return t
+
+
+def bigtile_error(device: torch.device) -> bool:
+    """True if a big-tile split-K hand-off timed out on `device` (results invalid)."""
+    C = native()
+    t = _BT_WS.get(device.index)
+    if t is None:
+        return False
+    hdr = C.conv_bigtile_ws_header_bytes()
+    return int(t[hdr - 256:hdr - 252].view(torch.int32).item()) != 0
 
 
 def conv3x3_rows(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, res: torch.Tensor | None = None,

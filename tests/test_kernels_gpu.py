@@ -87,6 +87,54 @@ def test_conv2d_persistent(gpu, case, max_blocks):
     assert _rel(_nchw(y.float().cpu()), ref) < 8e-3
 
 
+# 8-wave big-tile kernel (conv_bigtile.hip): tile 11 = 256x256, 12 = 256x128,
+# with the K range cut into `splits` slices (split-K hand-off through slabs
+# when > 1). Shapes cover M not a tile multiple, stride 2, 1x1, uneven
+# slices, more units than CUs and the ResNet layer2-4 geometries.
+BT_CASES = [
+    # B, H, W, Cin, Cout, k, stride, pad, relu, res, tile, splits
+    (4, 7, 7, 512, 512, 3, 1, 1, True, True, 11, 2),      # layer4
+    (4, 7, 7, 512, 512, 3, 1, 1, True, True, 11, 3),
+    (4, 7, 7, 512, 512, 3, 1, 1, False, False, 11, 4),
+    (8, 14, 14, 256, 512, 3, 2, 1, True, False, 11, 2),   # layer4.0.conv1 (stride 2)
+    (6, 14, 14, 256, 256, 3, 1, 1, False, True, 11, 1),   # layer3 (M not a tile multiple)
+    (5, 28, 28, 128, 256, 3, 2, 1, True, False, 11, 2),
+    (3, 28, 28, 128, 128, 3, 1, 1, True, True, 12, 1),    # layer2: 256x128 tiles
+    (3, 56, 56, 64, 128, 3, 2, 1, True, False, 12, 1),
+    (3, 28, 28, 128, 128, 3, 1, 1, True, True, 12, 2),
+    (2, 14, 14, 512, 256, 1, 1, 0, False, False, 11, 1),  # 1x1, K = 512 (8 K-tiles)
+    (2, 13, 13, 384, 256, 3, 1, 1, True, False, 11, 5),   # 54 K-tiles in 5 uneven slices
+    (64, 14, 14, 256, 256, 3, 1, 1, True, True, 11, 2),   # 49 tiles x 2 slices: > 1 unit per XCD slot row
+]
+
+
+@pytest.mark.parametrize("case", BT_CASES, ids=[str(c) for c in BT_CASES])
+def test_conv2d_bigtile(gpu, case):
+    B, H, W, Cin, Cout, k, s, p, relu, use_res, tile, splits = case
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(B, Cin, H, W, generator=g).bfloat16().float()
+    w = (torch.randn(Cout, Cin, k, k, generator=g) / (Cin * k * k) ** 0.5).bfloat16().float()
+    bias = torch.randn(Cout, generator=g) * 0.1
+    ref = F.conv2d(x, w, bias, s, p)
+    res = None
+    if use_res:
+        r = torch.randn_like(ref).bfloat16().float()
+        ref = ref + r
+        res = _nhwc(r).bfloat16().to(gpu)
+    if relu:
+        ref = F.relu(ref)
+    wp = ops.pack_conv_weight(w, device=gpu)
+    xg = _nhwc(x).bfloat16().to(gpu)
+    y = ops.conv2d(xg, wp, Cout, k, k, s, p, bias=bias.to(gpu), res=res, relu=relu, tile=tile, split_k=splits)
+    torch.cuda.synchronize()
+    assert not ops.bigtile_error(gpu), "split-K hand-off timed out"
+    assert _rel(_nchw(y.float().cpu()), ref) < 8e-3
+    # deterministic (fixed hand-off order) and the flags were left clean
+    y2 = ops.conv2d(xg, wp, Cout, k, k, s, p, bias=bias.to(gpu), res=res, relu=relu, tile=tile, split_k=splits)
+    torch.cuda.synchronize()
+    assert torch.equal(y, y2)
+
+
 @pytest.mark.parametrize("case", CONV_CASES, ids=[str(c) for c in CONV_CASES])
 def test_conv2d_vs_torch(gpu, case):
     B, H, W, Cin, Cout, k, s, p, relu, use_res, tile, split = case

@@ -1,9 +1,12 @@
 #!/usr/bin/env python3
 """Per-layer conv microbenchmark on the GPU (ResNet18 / AlexNet shapes).
 
-Times each distinct conv of the model in isolation with hipEvents (median of
---iters), for every tile config, and reports TFLOP/s. Used for kernel A/B
-work and for rocprofv3 --pmc runs (one process, interleaved configs).
+Times each distinct conv of the model in isolation, for every tile config,
+and reports TFLOP/s. Every measurement replays a hipGraph of REP back-to-back
+launches between two hipEvents (median of --iters replays / REP): timing
+single Python-launched kernels between events measures the host launch path
+(a ~40 us floor), not the kernel. Used for kernel A/B work and for rocprofv3
+--pmc runs (one process, interleaved configs).
 """
 import argparse
 import os
@@ -30,6 +33,49 @@ RESNET18 = [
 ]
 
 
+REP = 10
+
+
+def time_us(f, iters):
+    """Median per-launch time (us) of f() replayed from a captured graph."""
+    f()  # allocate workspaces / warm up outside the capture
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        f()
+        torch.cuda.synchronize()
+        with torch.cuda.graph(g, stream=s):
+            for _ in range(REP):
+                f()
+    torch.cuda.synchronize()
+    g.replay()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(iters):
+        e0, e1 = torch.cuda.Event(True), torch.cuda.Event(True)
+        e0.record()
+        g.replay()
+        e1.record()
+        e1.synchronize()
+        ts.append(e0.elapsed_time(e1) * 1e3 / REP)
+    return statistics.median(ts)
+
+
+def _stamps():
+    torch.cuda.synchronize()
+    st = ops.BT_STAMPS.view(-1, 4).cpu()
+    st = st[st[:, 3] > 0].double() / 100.0  # 100 MHz -> us
+    ops.BT_STAMPS.zero_()
+    if st.numel() == 0:
+        return "no stamps"
+    t0 = st[:, 0].min()
+    q = lambda v: f"{v.median().item():.1f}/{v.max().item():.1f}"
+    return (f"[stamps n={st.shape[0]} start {q(st[:, 0] - t0)} pro {q(st[:, 1] - st[:, 0])} "
+            f"loop {q(st[:, 2] - st[:, 1])} epi {q(st[:, 3] - st[:, 2])} end {q(st[:, 3] - t0)}]")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=256)
@@ -37,7 +83,7 @@ def main():
     ap.add_argument("--tiles", default="-1,0,1,2,3,4,5,6")
     ap.add_argument("--only", default="")
     ap.add_argument("--persist", type=int, default=0, help="persistent grid size (0 = one block per tile)")
-    ap.add_argument("--split", type=int, default=1, help="split-K factor")
+    ap.add_argument("--split", type=int, default=1, help="split-K factor (big-tile configs 11/12: K slices, 1 = auto)")
     ap.add_argument("--ref", action="store_true", help="also time hipBLASLt GEMM and MIOpen conv on each shape")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -59,40 +105,25 @@ def main():
                 continue
             if t in (0, 2, 3, 5, 6, 8, 10) and Cout % 128:
                 continue
+            if (t == 11 and Cout % 256) or (t == 12 and Cout != 128) or (t >= 11 and pair):
+                continue
             try:
                 f = lambda: ops.conv2d(x, wp, Cout, k, k, s, p, bias=bias, relu=True, tile=t, stem=pair,
                                        out_hw=(Ho, Ho) if pair else None, max_blocks=a.persist,
-                                       split_k=a.split)
-                f()
-                torch.cuda.synchronize()
-                ts = []
-                for _ in range(a.iters):
-                    e0, e1 = torch.cuda.Event(True), torch.cuda.Event(True)
-                    e0.record()
+                                       split_k=(a.split if a.split != 1 else 0) if t >= 11 else a.split)
+                us = time_us(f, a.iters)
+                row.append(f"tile{t}={us:7.1f}us {flops/us/1e6:6.0f}TF")
+                if t >= 11 and ops.BT_STAMPS is not None:
                     f()
-                    e1.record()
-                    e1.synchronize()
-                    ts.append(e0.elapsed_time(e1))
-                ms = statistics.median(ts)
-                row.append(f"tile{t}={ms*1e3:7.1f}us {flops/ms/1e9:6.0f}TF")
+                    row.append(_stamps())
             except Exception as e:  # noqa: BLE001
                 row.append(f"tile{t}=ERR({e})")
         if name == "l1":  # direct row-streaming conv (conv3x3_rows.hip)
             for use_res in (False, True):
                 r = torch.randn(B, H, W, Cout, device=dev).bfloat16() if use_res else None
                 f = lambda: ops.conv3x3_rows(x, wp, bias, r, True)
-                f()
-                torch.cuda.synchronize()
-                ts = []
-                for _ in range(a.iters):
-                    e0, e1 = torch.cuda.Event(True), torch.cuda.Event(True)
-                    e0.record()
-                    f()
-                    e1.record()
-                    e1.synchronize()
-                    ts.append(e0.elapsed_time(e1))
-                ms = statistics.median(ts)
-                row.append(f"rows{'+res' if use_res else ''}={ms*1e3:7.1f}us {flops/ms/1e9:6.0f}TF")
+                us = time_us(f, a.iters)
+                row.append(f"rows{'+res' if use_res else ''}={us:7.1f}us {flops/us/1e6:6.0f}TF")
         if a.ref:
             # vendor references on the same shape: plain GEMM (hipBLASLt via
             # torch.mm) and MIOpen conv (bf16, channels_last)
@@ -104,18 +135,8 @@ def main():
             wc = torch.randn(Cout, cin_real, k, k, device=dev).bfloat16().to(memory_format=torch.channels_last)
             for tag, f in (("gemm", lambda: torch.mm(A, Bm)),
                            ("miopen", lambda: torch.nn.functional.conv2d(xc, wc, None, s, p))):
-                f()
-                torch.cuda.synchronize()
-                ts = []
-                for _ in range(a.iters):
-                    e0, e1 = torch.cuda.Event(True), torch.cuda.Event(True)
-                    e0.record()
-                    f()
-                    e1.record()
-                    e1.synchronize()
-                    ts.append(e0.elapsed_time(e1))
-                ms = statistics.median(ts)
-                row.append(f"{tag}={ms*1e3:7.1f}us {flops/ms/1e9:6.0f}TF")
+                us = time_us(f, a.iters)
+                row.append(f"{tag}={us:7.1f}us {flops/us/1e6:6.0f}TF")
         print(f"{name:6s} M={B*Ho*Ho:8d} N={Cout:4d} K={cin_real*k*k:5d}  " + "  ".join(row), flush=True)
 
 

@@ -16,7 +16,7 @@ step() {  # name timeout cmd...
 }
 MODE=${1:-all}
 if [ "$MODE" = all ] || [ "$MODE" = test ]; then
-  step pytest_gpu 900 python -m pytest tests -m gpu -x -q
+  step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
 fi
 if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
   step bench1 300 python bench.py --profile-ops
