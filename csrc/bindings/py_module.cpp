@@ -100,6 +100,16 @@ PYBIND11_MODULE(_C, m) {
         a.alpha = P<float>(alpha);
         a.res_scale = res_scale;
         a.out_inv_scale = out_inv_scale;
+        if (tile == kConvBigTile0 + 2) {  // persistent 256x128 big tiles
+          a.tile = -1;
+          hipDeviceProp_t prop;
+          int dev = 0;
+          DMLC_HIP_CHECK(hipGetDevice(&dev));
+          DMLC_HIP_CHECK(hipGetDeviceProperties(&prop, dev));
+          conv2d_bigtile_persistent(a, max_blocks > 0 ? max_blocks : conv_bigtile_persistent_grid(a, prop.multiProcessorCount),
+                                    S(stream));
+          return;
+        }
         if (tile >= kConvBigTile0) {  // 8-wave big-tile configs (conv_bigtile.hip)
           a.tile = -1;
           conv2d_bigtile(a, tile - kConvBigTile0, bt_splits, P<void>(bt_ws), bt_ws_bytes, S(stream));

@@ -242,21 +242,76 @@ __global__ __launch_bounds__(512, 1) void conv_bt_kernel(ConvArgs a, int k_tiles
   // Main loop: NS-stage LDS ring, D = NS-1 sub-tiles in flight. Iteration t:
   // counted wait until this wave's DMA of sub-tile t landed (the younger
   // ones stay in flight), raw barrier (no vmcnt(0) drain: every wave's part
-  // of t is visible and every wave finished reading t-1), refill t-1's stage
-  // with t+D, compute t.
+  // of t is visible and every wave finished reading t-1), then the fragment
+  // reads of t and its MFMAs, with the G LDS-DMA instructions that refill
+  // t-1's stage with t+D spread one per MFMA group: issued in a burst after
+  // the barrier they stall every wave at issue and the DMA and the MFMAs
+  // serialise (measured: loop = DMA-only + MFMA-only time). Past the end of
+  // the slice the refill reads the zero page (harmless: that stage is never
+  // read again), so every iteration issues exactly G and the wait count is
+  // constant; the epilogue's __syncthreads drains them before LDS is reused.
+  static_assert(G <= TN, "at most one DMA per MFMA row group");
+  auto issue_one = [&](int g, char* sbase, int off, int kh, int kw, bool valid, const bf16* wt)
+      __attribute__((always_inline)) {
+    if (g < PA) {
+      const bool ok = valid && (unsigned)(hi0[g] + kh) < (unsigned)a.H && (unsigned)(wi0[g] + kw) < (unsigned)a.W;
+      const bf16* src = ok ? x + abase[g] + off : zero;
+      __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)(sbase + (g * 128 + wave * 16) * ROWB), 16, 0, 0);
+    } else {
+      const int p = g - PA;
+      const bf16* src = valid ? wt + wboff[p] : zero;
+      __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)(sbase + (BM + p * 128 + wave * 16) * ROWB), 16,
+                                       0, 0);
+    }
+  };
 #pragma unroll
-  for (int s2 = 0; s2 < D; ++s2)
-    if (k0 + s2 < k1 && !(dbg & 8)) stage(k0 + s2, s2);
+  for (int s2 = 0; s2 < D; ++s2) {
+    if (dbg & 8) break;
+    const int tn = k0 + s2;
+    const bool valid = tn < k1;
+    const int tap = tn / ctiles, c0 = (tn - tap * ctiles) * BK, kh = tap / a.KW, kw = tap - kh * a.KW;
+    char* sbase = (char*)smem + s2 * STAGE_B;
+#pragma unroll
+    for (int g = 0; g < G; ++g) issue_one(g, sbase, (kh * a.W + kw) * a.Cin + c0, kh, kw, valid, w + tn * BK);
+  }
   int st = 0;
   unsigned long long t_first = 0;
   for (int t = k0; t < k1; ++t) {
-    wait_younger<D, G>(k1 - 1 - t);
+    vm_wait<(D - 1) * G>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (stamps && t == k0) t_first = __builtin_amdgcn_s_memrealtime();
-    if (t + D < k1 && !(dbg & 1)) stage(t + D, st == 0 ? NS - 1 : st - 1);
-    if (!(dbg & 2)) compute(st);
+    const int tn = t + D;
+    const bool valid = tn < k1 && !(dbg & 1);
+    const int tap = tn / ctiles, c0 = (tn - tap * ctiles) * BK, kh = tap / a.KW, kw = tap - kh * a.KW;
+    const int off = (kh * a.W + kw) * a.Cin + c0;
+    char* rbase = (char*)smem + (st == 0 ? NS - 1 : st - 1) * STAGE_B;
+    const bf16* wt = w + tn * BK;
+    const uint4* sb = smem + st * STAGE_CH;
+    bf16x8 af[TN], bm[TM];
+#pragma unroll
+    for (int i = 0; i < TN; ++i) af[i] = __builtin_bit_cast(bf16x8, sb[aoff + i * 64]);
+#pragma unroll
+    for (int j = 0; j < TM; ++j) bm[j] = __builtin_bit_cast(bf16x8, sb[boff + j * 64]);
+#pragma unroll
+    for (int i = 0; i < TN; ++i) {
+      if (i < G) issue_one(i, rbase, off, kh, kw, valid, wt);
+      if (!(dbg & 2)) {
+#pragma unroll
+        for (int j = 0; j < TM; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bm[j], acc[i][j], 0, 0, 0);
+      }
+    }
+    if constexpr (!DBG) {
+      // pin the order: fragment reads, then (1 DMA, TM MFMAs) x TN
+      __builtin_amdgcn_sched_group_barrier(0x100, TN + TM, 0);
+#pragma unroll
+      for (int i = 0; i < TN; ++i) {
+        if (i < G) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, TM, 0);
+      }
+    }
     st = st == NS - 1 ? 0 : st + 1;
   }
 
@@ -367,6 +422,209 @@ __global__ __launch_bounds__(512, 1) void conv_bt_kernel(ConvArgs a, int k_tiles
   }
 }
 
+// Persistent variant for narrow-N convs with many tiles (ResNet layer2: N =
+// 128, 784 tiles of 256x128 at batch 256): workgroup b walks tiles
+// [T*b/G, T*(b+1)/G) (neighbouring tiles share input halo rows in L2/L1).
+// BK = 64 (full 128-B lines per row) in an NS-stage ring that streams across
+// tile boundaries, so the next tile's first K-tiles load during this tile's
+// last MFMAs and its epilogue. The epilogue stages 16 rows x 64 cols of fp32
+// per wave and pass through the stage just consumed (the other stages hold
+// the next tile's prefetch), 4 passes for a 64-row wave tile.
+__device__ __forceinline__ int bp_swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+
+template <int BM, int BN, int WM, int WN, int NS>
+__global__ __launch_bounds__(512, 1) void conv_btp_kernel(ConvArgs a, int k_tiles, int tiles) {
+  constexpr int BK = 64, ROWB = 128;
+  constexpr int PA = BM / 64, PB = BN / 64;  // rows staged per lane (8 waves x 8 rows per DMA instruction)
+  constexpr int G = PA + PB;
+  constexpr int D = NS - 1;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int TM = WTM / 16, TN = WTN / 16;
+  constexpr int STAGE_B = (BM + BN) * ROWB;
+  constexpr int A_CH = BM * 8;
+  constexpr int STAGE_CH = (BM + BN) * 8;
+  static_assert(WM * WN == 8 && WTN == 64 && TM >= 1 && D * G < 64, "config");
+  static_assert(STAGE_B >= 8 * 16 * 64 * 4, "epilogue pass staging must fit in one stage");
+
+  extern __shared__ __attribute__((aligned(16))) uint4 smem[];
+
+  const int G_ = gridDim.x;
+  const int b = blockIdx.x;
+  const int t_lo = (int)((long)tiles * b / G_), t_hi = (int)((long)tiles * (b + 1) / G_);
+  if (t_lo >= t_hi) return;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave % WM, wn = wave / WM;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int M = a.B * a.Ho * a.Wo;
+  const int n_tiles = a.Npad / BN;
+
+  const bf16* __restrict__ x = (const bf16*)a.x;
+  const bf16* __restrict__ w = (const bf16*)a.w;
+  const bf16* zero = (const bf16*)a.zero;
+
+  const int lrow = lane >> 3;
+  const int pchunk = lane & 7;
+  int hi0[PA], wi0[PA], abase[PA];
+  int wboff[PB];
+  auto setup_rows = [&](int tile) __attribute__((always_inline)) {
+    const int m0_ = (tile / n_tiles) * BM, n0_ = (tile % n_tiles) * BN;
+#pragma unroll
+    for (int p = 0; p < PA; ++p) {
+      const int r = p * 64 + wave * 8 + lrow;
+      const int m = m0_ + r;
+      if (m < M) {
+        const int hw = a.Ho * a.Wo;
+        const int bb = m / hw;
+        const int rem = m - bb * hw;
+        const int ho = rem / a.Wo;
+        const int wo = rem - ho * a.Wo;
+        hi0[p] = ho * a.stride - a.pad;
+        wi0[p] = wo * a.stride - a.pad;
+        abase[p] = ((bb * a.H + hi0[p]) * a.W + wi0[p]) * a.Cin + bp_swz(r, pchunk) * 8;
+      } else {
+        hi0[p] = -(1 << 28);
+        wi0[p] = 0;
+        abase[p] = 0;
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < PB; ++p) {
+      const int r = p * 64 + wave * 8 + lrow;
+      wboff[p] = (n0_ + r) * a.Kpad + bp_swz(r, pchunk) * 8;
+    }
+  };
+
+  const int ctiles = a.Cin / BK;
+  auto stage = [&](int t, int st) __attribute__((always_inline)) {
+    char* sbase = (char*)smem + st * STAGE_B;
+    const int tap = t / ctiles;
+    const int c0 = (t - tap * ctiles) * BK;
+    const int kh = tap / a.KW;
+    const int kw = tap - kh * a.KW;
+    const int off = (kh * a.W + kw) * a.Cin + c0;
+#pragma unroll
+    for (int p = 0; p < PA; ++p) {
+      const bool ok = (unsigned)(hi0[p] + kh) < (unsigned)a.H && (unsigned)(wi0[p] + kw) < (unsigned)a.W;
+      const bf16* src = ok ? x + abase[p] + off : zero;
+      __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)(sbase + (p * 64 + wave * 8) * ROWB), 16, 0, 0);
+    }
+    const bf16* wt = w + t * BK;
+#pragma unroll
+    for (int p = 0; p < PB; ++p)
+      __builtin_amdgcn_global_load_lds((gbl_ptr_t)(wt + wboff[p]),
+                                       (lds_ptr_t)(sbase + (BM + p * 64 + wave * 8) * ROWB), 16, 0, 0);
+  };
+
+  floatx4 acc[TN][TM];
+  const int sw = (fr >> 1) & 7;
+  int aoff[2], boff[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    aoff[ks] = A_CH + (wn * WTN + fr) * 8 + ((ks * 4 + fq) ^ sw);
+    boff[ks] = (wm * WTM + fr) * 8 + ((ks * 4 + fq) ^ sw);
+  }
+  auto compute = [&](int st) __attribute__((always_inline)) {
+    const uint4* sb = smem + st * STAGE_CH;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[TN], bm[TM];
+#pragma unroll
+      for (int i = 0; i < TN; ++i) af[i] = __builtin_bit_cast(bf16x8, sb[aoff[ks] + i * 128]);
+#pragma unroll
+      for (int j = 0; j < TM; ++j) bm[j] = __builtin_bit_cast(bf16x8, sb[boff[ks] + j * 128]);
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bm[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  // Flattened (tile, K-tile) stream of this workgroup: item i = (t_lo + i / k_tiles, i % k_tiles).
+  const int items = (t_hi - t_lo) * k_tiles;
+  int issue_tile = t_lo;  // tile whose row state is loaded
+  setup_rows(issue_tile);
+  auto issue = [&](int i, int st) __attribute__((always_inline)) {
+    const int tt = t_lo + i / k_tiles;
+    if (tt != issue_tile) {  // every DMA of the previous tile is issued: its row state can go
+      issue_tile = tt;
+      setup_rows(tt);
+    }
+    stage(i - (tt - t_lo) * k_tiles, st);
+  };
+#pragma unroll
+  for (int s2 = 0; s2 < D; ++s2)
+    if (s2 < items) issue(s2, s2);
+
+  const bf16* __restrict__ res = (const bf16*)a.res;
+  const int q = lane & 7, rr = lane >> 3;
+  int st = 0;
+  for (int tile = t_lo; tile < t_hi; ++tile) {
+#pragma unroll
+    for (int i = 0; i < TN; ++i)
+#pragma unroll
+      for (int j = 0; j < TM; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    const int base = (tile - t_lo) * k_tiles;
+    for (int kk = 0; kk < k_tiles; ++kk) {
+      const int i = base + kk;
+      wait_younger<D, G>(items - 1 - i);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (i + D < items) issue(i + D, st == 0 ? NS - 1 : st - 1);
+      compute(st);
+      st = st == NS - 1 ? 0 : st + 1;
+    }
+    // Epilogue through the stage just consumed (the previous value of st):
+    // after this barrier no wave reads it, and it is refilled only after the
+    // next K-loop barrier, which every wave reaches after its epilogue reads.
+    const int est = st == 0 ? NS - 1 : st - 1;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    float* wl = (float*)((char*)smem + est * STAGE_B) + wave * (16 * 64);
+    const int m0 = (tile / n_tiles) * BM, n0 = (tile % n_tiles) * BN;
+    const int nq = n0 + wn * WTN + q * 8;
+    floatx4 bq0 = {0.f, 0.f, 0.f, 0.f}, bq1 = bq0;
+    if (a.bias && nq < a.N) {
+      bq0 = *(const floatx4*)(a.bias + nq);
+      bq1 = *(const floatx4*)(a.bias + nq + 4);
+    }
+#pragma unroll
+    for (int j = 0; j < TM; ++j) {  // pass j: rows j*16 .. j*16+15 of the wave tile
+#pragma unroll
+      for (int i = 0; i < TN; ++i) *(floatx4*)(wl + fr * 64 + (((i * 4 + fq) ^ fr) * 4)) = acc[i][j];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int g = 0; g < 2; ++g) {
+        const int row = g * 8 + rr;
+        const floatx4 lo = *(const floatx4*)(wl + row * 64 + (((2 * q) ^ row) * 4));
+        const floatx4 hi = *(const floatx4*)(wl + row * 64 + (((2 * q + 1) ^ row) * 4));
+        const int m = m0 + wm * WTM + j * 16 + row;
+        if (m >= M || nq >= a.N) continue;
+        float v[8] = {lo[0] + bq0[0], lo[1] + bq0[1], lo[2] + bq0[2], lo[3] + bq0[3],
+                      hi[0] + bq1[0], hi[1] + bq1[1], hi[2] + bq1[2], hi[3] + bq1[3]};
+        const size_t o = (size_t)m * a.ldo + nq;
+        if (res) {
+          float r[8];
+          unpack8(*(const uint4*)(res + o), r);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += r[e];
+        }
+        if (a.relu) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+        }
+        *(uint4*)((bf16*)a.y + o) = pack8(v);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next pass overwrites
+    }
+  }
+}
+
 struct BtCfg {
   int bm, bn, ns;
 };
@@ -468,6 +726,43 @@ void conv2d_bigtile(const ConvArgs& a, int cfg, int splits, void* ws, size_t ws_
   else
     hipLaunchKernelGGL((conv_bt_kernel<256, 128, 4, 2, 5, false>), g, b, lds, s, a, k_tiles, (int)tiles, splits, slabs,
                        flags, err, 0);
+  DMLC_HIP_CHECK(hipGetLastError());
+}
+
+
+// Persistent big-tile conv (conv_btp_kernel): 256x128 tiles, BK=64, 3 stages.
+bool conv_bigtile_persistent_ok(const ConvArgs& a) {
+  return !(a.stem || a.in_fp8 || a.out_fp8 || a.out_f32) && a.Cin % 64 == 0 && a.Npad % 128 == 0 &&
+         a.N % 8 == 0 && a.ldo % 8 == 0;
+}
+
+int conv_bigtile_persistent_grid(const ConvArgs& a, int num_cus) {
+  // equal tile counts per workgroup: G = tiles / ceil(tiles / CUs)
+  const long M = (long)a.B * a.Ho * a.Wo;
+  const long tiles = ((M + 255) / 256) * (a.Npad / 128);
+  const long per = (tiles + num_cus - 1) / num_cus;
+  return (int)std::max<long>(1, (tiles + per - 1) / per);
+}
+
+void conv2d_bigtile_persistent(const ConvArgs& a, int grid, hipStream_t s) {
+  if (!conv_bigtile_persistent_ok(a)) throw std::invalid_argument("conv2d_bigtile_persistent: unsupported conv");
+  if (a.Kpad != conv_kpad(a.Cin, a.KH, a.KW, false)) throw std::invalid_argument("conv2d_bigtile_persistent: bad Kpad");
+  if (a.N > a.Npad || a.ldo < a.N) throw std::invalid_argument("conv2d_bigtile_persistent: bad N/ldo");
+  if (a.Ho != conv_out_dim(a.H, a.KH, a.stride, a.pad) || a.Wo != conv_out_dim(a.W, a.KW, a.stride, a.pad))
+    throw std::invalid_argument("conv2d_bigtile_persistent: bad output dims");
+  if (!a.x || !a.w || !a.y || !a.zero) throw std::invalid_argument("conv2d_bigtile_persistent: null operand");
+  if (((uintptr_t)a.x | (uintptr_t)a.w | (uintptr_t)a.zero | (uintptr_t)a.y | (uintptr_t)a.res |
+       (uintptr_t)a.bias) & 15)
+    throw std::invalid_argument("conv2d_bigtile_persistent: operands must be 16-B aligned");
+  const long M = (long)a.B * a.Ho * a.Wo;
+  if (M <= 0) return;
+  if ((long)a.B * a.H * a.W * a.Cin >= (1L << 31) || M * a.ldo >= (1L << 31) || (long)a.Npad * a.Kpad >= (1L << 31))
+    throw std::invalid_argument("conv2d_bigtile_persistent: tensor too large for 32-bit offsets");
+  const long tiles = ((M + 255) / 256) * (a.Npad / 128);
+  if (tiles * (a.Kpad / 64) >= (1L << 31)) throw std::invalid_argument("conv2d_bigtile_persistent: too many items");
+  if (grid < 1 || grid > 65536) throw std::invalid_argument("conv2d_bigtile_persistent: bad grid");
+  const size_t lds = (size_t)3 * (256 + 128) * 128;
+  hipLaunchKernelGGL((conv_btp_kernel<256, 128, 4, 2, 3>), dim3(grid), dim3(512), lds, s, a, a.Kpad / 64, (int)tiles);
   DMLC_HIP_CHECK(hipGetLastError());
 }
 

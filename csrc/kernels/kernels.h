@@ -84,6 +84,12 @@ long conv_bigtile_slabs(const ConvArgs& a, int cfg, int splits);
 size_t conv_bigtile_ws_bytes(long max_slabs);
 size_t conv_bigtile_ws_header_bytes();
 void conv2d_bigtile(const ConvArgs& a, int cfg, int splits, void* ws, size_t ws_bytes, hipStream_t s);
+// Persistent 256x128 variant (Npad % 128 == 0): `grid` workgroups walk
+// contiguous tile ranges with the LDS-DMA ring streaming across tiles.
+// Python/tests select it with tile = kConvBigTile0 + 2.
+bool conv_bigtile_persistent_ok(const ConvArgs& a);
+int conv_bigtile_persistent_grid(const ConvArgs& a, int num_cus);
+void conv2d_bigtile_persistent(const ConvArgs& a, int grid, hipStream_t s);
 
 // 3x3/s2-style max pooling, NHWC bf16, C % 8 == 0.
 void maxpool2d(const void* x, void* y, int B, int H, int W, int C, int Ho, int Wo, int k,

@@ -105,7 +105,7 @@ def conv2d(x: torch.Tensor, w_packed: torch.Tensor, cout: int, kh: int, kw: int,
         if bias.numel() < w_packed.shape[0]:
             bias = torch.nn.functional.pad(bias, (0, w_packed.shape[0] - bias.numel()))
     bt_ws, bt_bytes, bt_splits = None, 0, 1
-    if tile >= C.CONV_BIGTILE0:  # 8-wave big-tile kernel (conv_bigtile.hip); split_k = K slices (0: engine's choice)
+    if C.CONV_BIGTILE0 <= tile < C.CONV_BIGTILE0 + 2:  # 8-wave big-tile kernel (conv_bigtile.hip); split_k = K slices (0: engine's choice)
         bt_splits = split_k if split_k > 0 else C.conv_bigtile_splits(
             B, Ho, Wo, w_packed.shape[0], w_packed.shape[1], tile - C.CONV_BIGTILE0,
             torch.cuda.get_device_properties(x.device).multi_processor_count)

@@ -135,6 +135,42 @@ def test_conv2d_bigtile(gpu, case):
     assert torch.equal(y, y2)
 
 
+# persistent 256x128 big tiles (tile 13): small grids force several tiles per
+# workgroup, so the LDS-DMA ring streams across tile boundaries and the
+# epilogue runs on the just-consumed stage while the next tile loads.
+BTP_CASES = [
+    # B, H, W, Cin, Cout, k, stride, pad, relu, res, grid
+    (3, 28, 28, 128, 128, 3, 1, 1, True, True, 0),
+    (3, 28, 28, 128, 128, 3, 1, 1, True, True, 3),
+    (3, 56, 56, 64, 128, 3, 2, 1, True, False, 2),
+    (4, 56, 56, 64, 128, 1, 2, 0, False, False, 5),    # 1x1 downsample, 1 K-tile per tile
+    (2, 14, 14, 256, 256, 3, 1, 1, False, True, 1),    # 2 N-tiles, one workgroup walks all
+    (5, 13, 13, 192, 384, 3, 1, 1, True, False, 4),    # M not a tile multiple, 3 N-tiles
+]
+
+
+@pytest.mark.parametrize("case", BTP_CASES, ids=[str(c) for c in BTP_CASES])
+def test_conv2d_bigtile_persistent(gpu, case):
+    B, H, W, Cin, Cout, k, s, p, relu, use_res, grid = case
+    g = torch.Generator().manual_seed(4)
+    x = torch.randn(B, Cin, H, W, generator=g).bfloat16().float()
+    w = (torch.randn(Cout, Cin, k, k, generator=g) / (Cin * k * k) ** 0.5).bfloat16().float()
+    bias = torch.randn(Cout, generator=g) * 0.1
+    ref = F.conv2d(x, w, bias, s, p)
+    res = None
+    if use_res:
+        r = torch.randn_like(ref).bfloat16().float()
+        ref = ref + r
+        res = _nhwc(r).bfloat16().to(gpu)
+    if relu:
+        ref = F.relu(ref)
+    wp = ops.pack_conv_weight(w, device=gpu)
+    y = ops.conv2d(_nhwc(x).bfloat16().to(gpu), wp, Cout, k, k, s, p, bias=bias.to(gpu), res=res, relu=relu,
+                   tile=13, max_blocks=grid)
+    torch.cuda.synchronize()
+    assert _rel(_nchw(y.float().cpu()), ref) < 8e-3
+
+
 @pytest.mark.parametrize("case", CONV_CASES, ids=[str(c) for c in CONV_CASES])
 def test_conv2d_vs_torch(gpu, case):
     B, H, W, Cin, Cout, k, s, p, relu, use_res, tile, split = case

@@ -105,12 +105,12 @@ def main():
                 continue
             if t in (0, 2, 3, 5, 6, 8, 10) and Cout % 128:
                 continue
-            if (t == 11 and Cout % 256) or (t == 12 and Cout != 128) or (t >= 11 and pair):
+            if (t == 11 and Cout % 256) or (t == 12 and Cout != 128) or (t == 13 and Cout % 128) or (t >= 11 and pair):
                 continue
             try:
                 f = lambda: ops.conv2d(x, wp, Cout, k, k, s, p, bias=bias, relu=True, tile=t, stem=pair,
                                        out_hw=(Ho, Ho) if pair else None, max_blocks=a.persist,
-                                       split_k=(a.split if a.split != 1 else 0) if t >= 11 else a.split)
+                                       split_k=(a.split if a.split != 1 else 0) if t in (11, 12) else a.split)
                 us = time_us(f, a.iters)
                 row.append(f"tile{t}={us:7.1f}us {flops/us/1e6:6.0f}TF")
                 if t >= 11 and ops.BT_STAMPS is not None:
