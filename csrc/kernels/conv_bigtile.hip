@@ -641,15 +641,17 @@ long bt_tiles(const ConvArgs& a, int cfg) {
 int conv_bigtile_pick(const ConvArgs& a, int num_cus) {
   if (a.stem || a.in_fp8 || a.out_fp8 || a.out_f32) return -1;
   if (a.Cin % 64 != 0 || a.Kpad / 64 < 16 || a.N % 8 != 0 || a.ldo % 8 != 0) return -1;
-  // 256x256 tiles when they fill the CUs in one round without a K split
-  // (ResNet18 layer3 at batch 256: 196 tiles on 256 CUs, 74 vs 92 us per
-  // conv, profiles/r1_bigtile_conv.log). The split-K hand-off (+7 us) and
-  // the 256x128 config (narrow N: 85 FLOP per staged byte) measured slower
-  // than conv_igemm's 128x128 tiles at 2 workgroups per CU.
+  // 256x256 tiles only when they fill the CUs in one round without a K
+  // split (ResNet18 layer3 at batch 256: 196 tiles, 69-71 vs 88-92 us per
+  // conv). With 2 K slices (layer4.x.conv2: 98 tiles x 2) the split-K
+  // hand-off costs more than it saves in the model (107 vs 94 us with the
+  // residual epilogue), and the 256x128 configs (narrow N: 85 FLOP per
+  // staged byte) measured slower than conv_igemm's 2-workgroup-per-CU tiles
+  // (profiles/r1_bigtile_conv.log).
   if (a.Npad % 256 != 0) return -1;
   const long tiles = bt_tiles(a, 0);
-  if (tiles > num_cus || tiles * 4 < num_cus * 3) return -1;
-  return 0;
+  if (tiles <= num_cus && tiles * 4 >= num_cus * 3) return 0;
+  return -1;
 }
 
 int conv_bigtile_splits(const ConvArgs& a, int cfg, int num_cus) {
