@@ -129,6 +129,11 @@ void conv3x3_rows(const void* x, const void* w, const float* bias, const void* r
 int stem_pool_pick_strip(int B, int PH, int num_cus);
 void stem_conv_pool(const void* x, const void* w, const float* bias, void* y, int B, int S, int Wq, int strip,
                     hipStream_t s);
+// Same stem with the preprocess fused: u8 HWC SxS images [B, S, S, 3] in
+// (already at the target size: the identity case of preprocess_u8), the
+// paired bf16 rows built in LDS with preprocess_u8's exact arithmetic.
+void stem_conv_pool_u8(const uint8_t* x, const void* w, const float* bias, void* y, int B, int S, int strip,
+                       hipStream_t s);
 
 // One wave of v_mfma_scale_f32_16x16x128_f8f6f4 (fp8 e4m3, unit scales) on
 // raw per-lane registers: a, b = int32 [64 lanes][8], d = f32 [64 lanes][4].

@@ -55,6 +55,11 @@ typedef short short2v __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 
 constexpr int kRing = 21;  // staged input rows: 13 for a step + 8 in flight
+// u8 input (fused preprocess): the 8 rows of the next step arrive as raw u8
+// image rows in a small ring and are converted into the paired bf16 ring only
+// after the current step's MFMAs, so the paired ring needs just 13 rows
+// (and the workgroup still fits 2 per CU: ~73 KB of LDS at 224x224).
+constexpr int kRingU8 = 13;
 constexpr int kHp = 5;     // horizontally pooled conv rows: carried halo + 4
 constexpr int kK = 224;    // 7 kernel rows x 4 chunks x 8
 // Pooled-row LDS layout: [pw][64 ch] with a 144-B column stride (128 + 16 pad):
@@ -65,6 +70,8 @@ constexpr int kHpCol = 144;
 
 struct StemArgs {
   const bf16* x;      // [B, Hp, Wq, 8]
+  const uint8_t* u8;  // fused preprocess: u8 HWC images [B, S, S, 3] (x unused)
+  int S;
   const bf16* w;      // [64, 224]
   const float* bias;  // [64]
   bf16* y;            // [B, PH, PW, 64]
@@ -98,13 +105,16 @@ __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_s_barrier();
 }
 
-template <int NF, bool PF>
+template <int NF, bool PF, bool U8>
 __global__ __launch_bounds__(256, 2) void stem_conv_pool_kernel(
     StemArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint4 smem[];
+  constexpr int RING = U8 ? kRingU8 : kRing;
   const int RB = a.Wq * 16;  // bytes per staged input row
+  const int UB = a.S * 3;    // bytes per raw u8 image row (U8)
   char* ring = (char*)smem;
-  char* hp = ring + kRing * RB;
+  char* hp = ring + RING * RB;
+  char* u8ring = hp + kHp * a.PW * kHpCol;  // U8: raw rows, slot = row % RING
   const int HPB = a.PW * kHpCol;  // bytes per pooled conv row
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -117,16 +127,74 @@ __global__ __launch_bounds__(256, 2) void stem_conv_pool_kernel(
   const bf16* img = a.x + (long)b * a.Hp * a.Wq * 8;
 
   // This wave's share of a row list [lo, lo+cnt): rows lo+wave, lo+wave+4, ...
+  // (U8: padded row r is image row r-3; rows outside the image are not
+  // loaded, convert_rows writes them as zeros.)
+  const uint8_t* uimg = U8 ? a.u8 + (long)b * a.S * a.S * 3 : nullptr;
   auto load_rows = [&](int lo, int cnt) __attribute__((always_inline)) {
     for (int i = wave; i < cnt; i += 4) {
       const int r = lo + i;
       if (r < 0) continue;
-      const bf16* src = img + (long)r * a.Wq * 8;
-      char* dst = ring + (r % kRing) * RB;
-      for (int c0 = 0; c0 < a.Wq; c0 += 64) {
-        if (c0 + lane < a.Wq)
-          __builtin_amdgcn_global_load_lds((gbl_ptr_t)(src + (c0 + lane) * 8), (lds_ptr_t)(dst + c0 * 16), 16, 0,
-                                           0);
+      if constexpr (U8) {
+        const int iy = r - 3;
+        if (iy < 0 || iy >= a.S) continue;
+        const uint8_t* src = uimg + (long)iy * UB;
+        char* dst = u8ring + (r % RING) * UB;
+        for (int c0 = 0; c0 < UB / 4; c0 += 64)
+          if (c0 + lane < UB / 4)
+            __builtin_amdgcn_global_load_lds((gbl_ptr_t)(src + (c0 + lane) * 4), (lds_ptr_t)(dst + c0 * 4), 4, 0, 0);
+      } else {
+        const bf16* src = img + (long)r * a.Wq * 8;
+        char* dst = ring + (r % RING) * RB;
+        for (int c0 = 0; c0 < a.Wq; c0 += 64) {
+          if (c0 + lane < a.Wq)
+            __builtin_amdgcn_global_load_lds((gbl_ptr_t)(src + (c0 + lane) * 8), (lds_ptr_t)(dst + c0 * 16), 16, 0,
+                                             0);
+        }
+      }
+    }
+  };
+  // U8: raw rows [lo, lo+cnt) -> paired bf16 ring rows, exactly the
+  // preprocess_u8(paired) values: chunk p = image columns 2p-3, 2p-2 as
+  // [r g b r g b 0 0], (v/255 - mean)/std, zeros outside the image. A thread
+  // converts 4 chunks (8 pixels = 24 bytes starting at byte 24k-9 of the
+  // row) from 7 aligned dword reads starting at 24k-12.
+  auto convert_rows = [&](int lo, int cnt) __attribute__((always_inline)) {
+    const int G4 = (a.Wq + 3) / 4;
+    const int items = cnt * G4;
+    for (int it = tid; it < items; it += 256) {
+      const int r = lo + it / G4;
+      const int k = it - (it / G4) * G4;
+      if (r < 0) continue;
+      const int iy = r - 3;
+      const bool row_in = iy >= 0 && iy < a.S;
+      const char* srow = u8ring + (r % RING) * UB;
+      const int A = 24 * k - 12;
+      uint32_t d[7];
+#pragma unroll
+      for (int j = 0; j < 7; ++j) {
+        const int o = A + 4 * j;
+        d[j] = (row_in && o >= 0 && o < UB) ? *(const uint32_t*)(srow + o) : 0u;
+      }
+      float v[32];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int ix = 8 * k - 3 + i;
+        const bool in = row_in && ix >= 0 && ix < a.S;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          const int idx = 3 + 3 * i + c;
+          const float cv = (float)((d[idx >> 2] >> (8 * (idx & 3))) & 0xffu);
+          const float nv = c == 0 ? (cv * (1.f / 255.f) - 0.485f) * (1.f / 0.229f)
+                         : c == 1 ? (cv * (1.f / 255.f) - 0.456f) * (1.f / 0.224f)
+                                  : (cv * (1.f / 255.f) - 0.406f) * (1.f / 0.225f);
+          v[8 * (i >> 1) + 3 * (i & 1) + c] = in ? nv : 0.f;
+        }
+      }
+      char* drow = ring + (r % RING) * RB;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        v[8 * q + 6] = v[8 * q + 7] = 0.f;
+        if (4 * k + q < a.Wq) *(uint4*)(drow + (4 * k + q) * 16) = pack8(v + 8 * q);
       }
     }
   };
@@ -146,6 +214,10 @@ __global__ __launch_bounds__(256, 2) void stem_conv_pool_kernel(
   load_rows(4 * ph0 - 8, 13);
   vm_wait<0>();
   __builtin_amdgcn_s_barrier();
+  if constexpr (U8) {
+    convert_rows(4 * ph0 - 8, 13);
+    lds_barrier();
+  }
 
   for (int t = 0; t <= T; ++t) {
     const int c0 = 2 * ph0 - 4 + 4 * t;
@@ -164,7 +236,7 @@ __global__ __launch_bounds__(256, 2) void stem_conv_pool_kernel(
         const char* rbase = ring + (fr + fq) * 16;
         int rows[7];
 #pragma unroll
-        for (int s = 0; s < 7; ++s) rows[s] = ((2 * cr + s) % kRing) * RB;
+        for (int s = 0; s < 7; ++s) rows[s] = ((2 * cr + s) % RING) * RB;
         // per-lane store base: column 2g, channel chunk r/8, element r%8
         const uint32_t hbase = lds_addr(hrow) + fq * 2 * kHpCol + (fr >> 3) * 16 + (fr & 7) * 2;
         const int nb_addr = ((lane + 48) & 63) << 2;  // read lane (l - 16) mod 64
@@ -260,6 +332,12 @@ __global__ __launch_bounds__(256, 2) void stem_conv_pool_kernel(
       default: vm_wait<4>(); break;
     }
     lds_barrier();
+    if constexpr (U8) {
+      if (t < T) {  // the next step's raw rows landed; the rows they replace are no longer read
+        convert_rows(2 * c0 + 13, 8);
+        lds_barrier();
+      }
+    }
   }
 }
 
@@ -276,18 +354,22 @@ int stem_pool_pick_strip(int B, int PH, int num_cus) {
   return best;
 }
 
-void stem_conv_pool(const void* x, const void* w, const float* bias, void* y, int B, int S, int Wq, int strip,
-                    hipStream_t s) {
+namespace {
+void stem_launch(const void* x, const uint8_t* u8, const void* w, const float* bias, void* y, int B, int S, int Wq,
+                 int strip, hipStream_t s) {
   if (B <= 0) return;
   const int Ho = S / 2, PH = Ho / 2;
   const int NF = Ho / 16;
   if (S % 32 != 0 || NF < 4 || NF > 8) throw std::invalid_argument("stem_conv_pool: image size must be 128..256, %32");
   if (Wq < Ho + 3 || Wq > 512) throw std::invalid_argument("stem_conv_pool: bad paired row width");
   if (strip < 2 || strip % 2 || PH % strip) throw std::invalid_argument("stem_conv_pool: bad strip");
-  if (!x || !w || !bias || !y || ((uintptr_t)x & 15) || ((uintptr_t)w & 15) || ((uintptr_t)y & 15))
+  if ((!x && !u8) || !w || !bias || !y || ((uintptr_t)x & 15) || ((uintptr_t)u8 & 3) || ((uintptr_t)w & 15) ||
+      ((uintptr_t)y & 15))
     throw std::invalid_argument("stem_conv_pool: null / misaligned operand");
   StemArgs a;
   a.x = (const bf16*)x;
+  a.u8 = u8;
+  a.S = S;
   a.w = (const bf16*)w;
   a.bias = bias;
   a.y = (bf16*)y;
@@ -296,24 +378,51 @@ void stem_conv_pool(const void* x, const void* w, const float* bias, void* y, in
   a.PH = PH;
   a.PW = PH;
   a.strip = strip;
-  const size_t lds = (size_t)kRing * Wq * 16 + (size_t)kHp * a.PW * kHpCol;
+  const size_t lds = u8 ? (size_t)kRingU8 * Wq * 16 + (size_t)kHp * a.PW * kHpCol + (size_t)kRingU8 * S * 3
+                        : (size_t)kRing * Wq * 16 + (size_t)kHp * a.PW * kHpCol;
   const dim3 grid(B * (PH / strip));
   static const bool pf = [] {
     const char* e = std::getenv("DMLC_STEM_PREFETCH");
     return e && std::string(e) == "1";
   }();
-  switch (NF * 2 + pf) {
-#define DMLC_STEM_CASE(F)                                                                              \
-  case 2 * F: hipLaunchKernelGGL((stem_conv_pool_kernel<F, false>), grid, dim3(256), lds, s, a); break; \
-  case 2 * F + 1: hipLaunchKernelGGL((stem_conv_pool_kernel<F, true>), grid, dim3(256), lds, s, a); break;
-    DMLC_STEM_CASE(4)
-    DMLC_STEM_CASE(5)
-    DMLC_STEM_CASE(6)
-    DMLC_STEM_CASE(7)
-    DMLC_STEM_CASE(8)
+  if (u8) {
+    switch (NF) {
+#define DMLC_STEM_U8_CASE(F) \
+  case F: hipLaunchKernelGGL((stem_conv_pool_kernel<F, false, true>), grid, dim3(256), lds, s, a); break;
+      DMLC_STEM_U8_CASE(4)
+      DMLC_STEM_U8_CASE(5)
+      DMLC_STEM_U8_CASE(6)
+      DMLC_STEM_U8_CASE(7)
+      DMLC_STEM_U8_CASE(8)
+#undef DMLC_STEM_U8_CASE
+    }
+  } else {
+    switch (NF * 2 + pf) {
+#define DMLC_STEM_CASE(F)                                                                                     \
+  case 2 * F: hipLaunchKernelGGL((stem_conv_pool_kernel<F, false, false>), grid, dim3(256), lds, s, a); break; \
+  case 2 * F + 1: hipLaunchKernelGGL((stem_conv_pool_kernel<F, true, false>), grid, dim3(256), lds, s, a); break;
+      DMLC_STEM_CASE(4)
+      DMLC_STEM_CASE(5)
+      DMLC_STEM_CASE(6)
+      DMLC_STEM_CASE(7)
+      DMLC_STEM_CASE(8)
 #undef DMLC_STEM_CASE
+    }
   }
   DMLC_HIP_CHECK(hipGetLastError());
+}
+}  // namespace
+
+void stem_conv_pool(const void* x, const void* w, const float* bias, void* y, int B, int S, int Wq, int strip,
+                    hipStream_t s) {
+  if (!x) throw std::invalid_argument("stem_conv_pool: null input");
+  stem_launch(x, nullptr, w, bias, y, B, S, Wq, strip, s);
+}
+
+void stem_conv_pool_u8(const uint8_t* x, const void* w, const float* bias, void* y, int B, int S, int strip,
+                       hipStream_t s) {
+  if (!x) throw std::invalid_argument("stem_conv_pool_u8: null input");
+  stem_launch(nullptr, x, w, bias, y, B, S, stem_row_width(S, 3, 7, 2) / 2, strip, s);
 }
 
 }  // namespace dmlc

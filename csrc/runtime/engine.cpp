@@ -84,6 +84,7 @@ Engine::Engine(const std::string& arch, const WeightMap& weights, int device, in
   if (const char* e = std::getenv("DMLC_FUSED_STEM")) fused_stem_ = std::string(e) != "0";
   if (const char* e = std::getenv("DMLC_ROW_CONV")) row_conv_ = std::string(e) != "0";
   if (const char* e = std::getenv("DMLC_BIGTILE")) bigtile_ = std::string(e) != "0";
+  if (const char* e = std::getenv("DMLC_FUSED_PREPROCESS")) fused_pre_ = std::string(e) != "0";
 
   if (arch == "resnet18")
     build_resnet({2, 2, 2, 2}, false);
@@ -525,6 +526,8 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
     switch (op.type) {
       case OpType::Preprocess: {
         const bool paired = op.k == 1;
+        // images already SxS feed the fused stem directly (stem_conv_pool_u8)
+        if (paired && fused_pre_ && Hin == image_size_ && Win == image_size_) break;
         const int Wr = paired ? 2 * shapes_[op.out].W : shapes_[op.out].W;
         preprocess_u8(images, acts_[op.out], B, Hin, Win, image_size_, op.pad, Wr, s, paired);
         break;
@@ -553,6 +556,12 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
       }
       case OpType::StemPool: {
         const ConvLayer& L = convs_[op.conv];
+        if (fused_pre_ && Hin == image_size_ && Win == image_size_) {
+          stem_conv_pool_u8(images, (const uint8_t*)warena_ + L.w_off,
+                            (const float*)((const uint8_t*)warena_ + L.b_off), acts_[op.out], B, image_size_,
+                            stem_pool_pick_strip(B, shapes_[op.out].H, num_cus_), s);
+          break;
+        }
         stem_conv_pool(acts_[op.in], (const uint8_t*)warena_ + L.w_off,
                        (const float*)((const uint8_t*)warena_ + L.b_off), acts_[op.out], B, image_size_,
                        shapes_[op.in].W, stem_pool_pick_strip(B, shapes_[op.out].H, num_cus_), s);

@@ -121,6 +121,7 @@ class Engine {
   bool persistent_ = true;  // persistent conv grids (env DMLC_PERSISTENT=0 disables)
   bool fused_stem_ = true;  // conv1+maxpool as one kernel (env DMLC_FUSED_STEM=0 disables)
   bool bigtile_ = true;     // 8-wave big-tile split-K convs where supported (env DMLC_BIGTILE=0 disables)
+  bool fused_pre_ = true;   // SxS u8 images straight into the fused stem (env DMLC_FUSED_PREPROCESS=0 disables)
   bool row_conv_ = true;    // direct row-streaming 3x3 convs where supported (env DMLC_ROW_CONV=0 disables)
   bool fp8_ = false;        // resnet50_fp8
 

@@ -316,6 +316,25 @@ def stem_conv_pool(x_paired: torch.Tensor, w_packed: torch.Tensor, bias: torch.T
     return y
 
 
+def stem_conv_pool_u8(images: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor,
+                      strip: int | None = None) -> torch.Tensor:
+    """The fused stem with the preprocess fused too: u8 [B, S, S, 3] images
+    (already at the model size) -> [B, S/4, S/4, 64]. Same values as
+    ``stem_conv_pool(preprocess_u8(images, S, 3, paired=True), ...)``."""
+    _need_cuda(images, w_packed, bias)
+    if images.dtype != torch.uint8 or images.dim() != 4 or images.shape[-1] != 3 or images.shape[1] != images.shape[2]:
+        raise ValueError("stem_conv_pool_u8 expects uint8 [B, S, S, 3]")
+    C = native()
+    B, S = images.shape[0], images.shape[1]
+    ph = S // 4
+    if strip is None:
+        strip = C.stem_pool_pick_strip(B, ph, torch.cuda.get_device_properties(images.device).multi_processor_count)
+    y = torch.empty(B, ph, ph, 64, device=images.device, dtype=torch.bfloat16)
+    C.stem_conv_pool_u8(_ptr(images.contiguous()), _ptr(w_packed.contiguous()), _ptr(bias.float().contiguous()),
+                        _ptr(y), B, S, strip, _stream())
+    return y
+
+
 def softmax_top1(logits: torch.Tensor, n: int | None = None) -> tuple[torch.Tensor, torch.Tensor]:
     _need_cuda(logits)
     if logits.dtype != torch.float32:

@@ -239,6 +239,24 @@ def test_stem_conv_pool(gpu, B, S, strip):
     assert (got - ref).abs().max().item() < 0.05
 
 
+@pytest.mark.parametrize("B,S,strip", [(3, 224, None), (2, 224, 2), (1, 224, 56), (2, 128, None), (4, 192, 6),
+                                       (1, 256, 8)])
+def test_stem_conv_pool_u8(gpu, B, S, strip):
+    """Stem with the preprocess fused (u8 images in): bit-identical to the
+    two-kernel path preprocess_u8(paired) -> stem_conv_pool."""
+    g = torch.Generator().manual_seed(12)
+    img = torch.randint(0, 256, (B, S, S, 3), dtype=torch.uint8, generator=g).to(gpu)
+    w = (torch.randn(64, 3, 7, 7, generator=g) / 147 ** 0.5).bfloat16().float()
+    bias = (torch.randn(64, generator=g) * 0.1).to(gpu)
+    wp = ops.pack_stem_pool_weight(w, device=gpu)
+    C = dmlc.native()
+    pairs = C.stem_row_width(S, 3, 7, 2) // 2
+    two = ops.stem_conv_pool(ops.preprocess_u8(img, S, 3, 2 * pairs, paired=True), wp, bias, S, strip)
+    one = ops.stem_conv_pool_u8(img, wp, bias, strip)
+    torch.cuda.synchronize()
+    assert torch.equal(one, two)
+
+
 @pytest.mark.parametrize("B,strip,res", [(2, None, False), (2, None, True), (3, 4, True), (1, 8, False),
                                          (1, 28, True)])
 def test_conv3x3_rows(gpu, B, strip, res):
