@@ -81,11 +81,17 @@ __global__ __launch_bounds__(256, 1) void conv3x3_rows_kernel(RowConvArgs a) {
   const int steps = a.strip / R;
   const bf16* img = a.x + (long)b * a.H * W * C;
 
-  // ---- weights -> LDS: chunk i = (ks*C + n)*4 + c' holds w[n][ks*32 + 8*(c' ^ wswz(n))]
+  // ---- weights -> LDS: chunk i = (ks*C + n)*4 + c' holds w[perm(n)][ks*32 + 8*(c' ^ wswz(n))].
+  // perm maps LDS weight row n = 32*wg + 16*nf + r (the MFMA row r of N
+  // fragment nf) to output channel 32*wg + 8*(r>>2) + 4*nf + (r&3): the lane
+  // with accumulator rows 4g..4g+3 of both fragments then holds the 8
+  // consecutive channels 32*wg + 8g .. +7 (16-B output stores and residual
+  // loads instead of two 8-B halves).
+  auto perm = [](int n) { return (n & ~31) + 8 * ((n & 15) >> 2) + 4 * ((n >> 4) & 1) + (n & 3); };
   for (int j = 0; j < WB / 16 / 256; ++j) {
     const int i = j * 256 + tid;
     const int c2 = i & 3, n = (i >> 2) % C, ks = i / (4 * C);
-    const bf16* src = a.w + (long)n * (9 * C) + ks * 32 + 8 * (c2 ^ wswz(n));
+    const bf16* src = a.w + (long)perm(n) * (9 * C) + ks * 32 + 8 * (c2 ^ wswz(n));
     __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)(wl + (j * 256 + wave * 64) * 16), 16, 0, 0);
   }
 
@@ -130,11 +136,12 @@ __global__ __launch_bounds__(256, 1) void conv3x3_rows_kernel(RowConvArgs a) {
   // weight fragment nf of this wave: rows n = wn*32 + 16nf + fr
   const uint32_t wrow = (uint32_t)(wn * 32 + fr) * 64 + ((g ^ wswz(fr)) << 4);
   const char* wbase = wl + wrow;
+  // this lane's 8 output channels (see perm): bias of channel wn*32 + 8g + 4nf + i
   float bs[2][4];
 #pragma unroll
   for (int nf = 0; nf < 2; ++nf)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) bs[nf][i] = a.bias[wn * 32 + nf * 16 + g * 4 + i];
+    for (int i = 0; i < 4; ++i) bs[nf][i] = a.bias[wn * 32 + 8 * g + 4 * nf + i];
 
   for (int s = 0; s < steps; ++s) {
     const int oh0 = oh_first + s * R;
@@ -149,15 +156,12 @@ __global__ __launch_bounds__(256, 1) void conv3x3_rows_kernel(RowConvArgs a) {
 
     // residual of this step's outputs, loaded now so it lands during the MFMAs
     const long base = ((long)b * a.H + oh0) * W * C;
-    uint2 rres[MF][2];
+    uint4 rres[MF];
 #pragma unroll
-    for (int f = 0; f < MF; ++f)
-#pragma unroll
-      for (int nf = 0; nf < 2; ++nf) {
-        const int p = wm * (R * W / 2) + 16 * f + fr;
-        rres[f][nf] = a.res ? *(const uint2*)(a.res + base + (long)p * C + wn * 32 + nf * 16 + g * 4)
-                            : make_uint2(0, 0);
-      }
+    for (int f = 0; f < MF; ++f) {
+      const int p = wm * (R * W / 2) + 16 * f + fr;
+      rres[f] = a.res ? *(const uint4*)(a.res + base + (long)p * C + wn * 32 + 8 * g) : make_uint4(0, 0, 0, 0);
+    }
 
     floatx4 acc[MF][2];
 #pragma unroll
@@ -196,33 +200,31 @@ __global__ __launch_bounds__(256, 1) void conv3x3_rows_kernel(RowConvArgs a) {
       }
     }
 
-    // ---- epilogue: lane holds channels wn*32 + 16nf + 4g + i of pixel (prow, col)
+    // ---- epilogue: lane holds channels wn*32 + 8g .. +7 of pixel (prow, col)
 #pragma unroll
     for (int f = 0; f < MF; ++f) {
       const int p = wm * (R * W / 2) + 16 * f + fr;
+      const long off = base + (long)p * C + wn * 32 + 8 * g;
+      float v[8];
 #pragma unroll
-      for (int nf = 0; nf < 2; ++nf) {
-        const long off = base + (long)p * C + wn * 32 + nf * 16 + g * 4;
-        float v[4];
+      for (int nf = 0; nf < 2; ++nf)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = acc[f][nf][i] + bs[nf][i];
-        if (a.res) {
-          const uint2 r2 = rres[f][nf];
-          v[0] += __uint_as_float(r2.x << 16);
-          v[1] += __uint_as_float(r2.x & 0xffff0000u);
-          v[2] += __uint_as_float(r2.y << 16);
-          v[3] += __uint_as_float(r2.y & 0xffff0000u);
-        }
-        if (a.relu) {
+        for (int i = 0; i < 4; ++i) v[4 * nf + i] = acc[f][nf][i] + bs[nf][i];
+      if (a.res) {
+        float r[8];
+        unpack8(rres[f], r);
 #pragma unroll
-          for (int i = 0; i < 4; ++i) v[i] = fmaxf(v[i], 0.f);
-        }
-        *(uint2*)(a.y + off) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+        for (int e = 0; e < 8; ++e) v[e] += r[e];
       }
+      if (a.relu) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+      }
+      *(uint4*)(a.y + off) = pack8(v);
     }
     // The next step's rows have landed: vmcnt retires in issue order, so the
-    // 2*MF younger stores may stay in flight.
-    vm_wait<2 * MF>();
+    // MF younger stores may stay in flight.
+    vm_wait<MF>();
     __builtin_amdgcn_s_barrier();
   }
 }
@@ -245,8 +247,8 @@ void conv3x3_rows(const void* x, const void* w, const float* bias, const void* r
   if (B <= 0) return;
   if (!conv3x3_rows_supported(H, W, C, C)) throw std::invalid_argument("conv3x3_rows: unsupported shape");
   if (strip <= 0 || strip % 4 || H % strip) throw std::invalid_argument("conv3x3_rows: bad strip");
-  if (!x || !w || !bias || !y || !zero || (((uintptr_t)x | (uintptr_t)w | (uintptr_t)y | (uintptr_t)zero) & 15) ||
-      ((uintptr_t)res & 7))
+  if (!x || !w || !bias || !y || !zero ||
+      (((uintptr_t)x | (uintptr_t)w | (uintptr_t)y | (uintptr_t)zero | (uintptr_t)res) & 15))
     throw std::invalid_argument("conv3x3_rows: null / misaligned operand");
   RowConvArgs a;
   a.x = (const bf16*)x;
