@@ -364,6 +364,57 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a, int kt_p
     }
   };
 
+  // bf16 epilogue staged through LDS (same scheme as conv_bigtile.hip): the
+  // wave writes 16 rows x 64 cols of fp32 accumulators to its 4 KB of the
+  // stage it just consumed (16-B chunks XOR-swizzled by row), then each lane
+  // reads 8 consecutive channels of one row and adds bias and residual with
+  // one 16-B load, applies ReLU and stores 16 B: a wave instruction covers 8
+  // rows x 128 contiguous bytes instead of 16 rows x 32 B. Needs the caller
+  // to have passed a barrier after every wave's last read of that stage.
+  auto epilogue_lds = [&](int m0e, int n0e, int est) __attribute__((always_inline)) {
+    float* wl = (float*)((char*)smem + est * STAGE_B) + wave * (16 * 64);
+    const bf16* __restrict__ res = (const bf16*)a.res;
+    const int q = lane & 7, rr = lane >> 3;
+    const int nq = n0e + wn * WTN + q * 8;
+    floatx4 bq0 = {0.f, 0.f, 0.f, 0.f}, bq1 = bq0;
+    if (a.bias && nq < a.N) {
+      bq0 = *(const floatx4*)(a.bias + nq);
+      bq1 = *(const floatx4*)(a.bias + nq + 4);
+    }
+#pragma unroll
+    for (int j = 0; j < TM; ++j) {
+#pragma unroll
+      for (int i = 0; i < TN; ++i) *(floatx4*)(wl + fr * 64 + (((i * 4 + fq) ^ fr) * 4)) = acc[i][j];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int g = 0; g < 2; ++g) {
+        const int row = g * 8 + rr;
+        const floatx4 lo = *(const floatx4*)(wl + row * 64 + (((2 * q) ^ row) * 4));
+        const floatx4 hi = *(const floatx4*)(wl + row * 64 + (((2 * q + 1) ^ row) * 4));
+        const int m = m0e + wm * WTM + j * 16 + row;
+        if (m >= M || nq >= a.N) continue;
+        float v[8] = {lo[0] + bq0[0], lo[1] + bq0[1], lo[2] + bq0[2], lo[3] + bq0[3],
+                      hi[0] + bq1[0], hi[1] + bq1[1], hi[2] + bq1[2], hi[3] + bq1[3]};
+        const size_t o = (size_t)m * a.ldo + nq;
+        if (res) {
+          float r[8];
+          unpack8(*(const uint4*)(res + o), r);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += r[e];
+        }
+        if (a.relu) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+        }
+        *(uint4*)((bf16*)a.y + o) = pack8(v);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next pass overwrites
+    }
+  };
+  // 16-B rows need N, ldo multiples of 8 and 16-B aligned y / residual
+  const bool lds_epi = !IN8 && !OUT8 && !PAIR && WTN == 64 && gridDim.y == 1 && !a.out_f32 && a.N % 8 == 0 &&
+                       a.ldo % 8 == 0 && (((uintptr_t)a.y | (uintptr_t)a.res) & 15) == 0;
+
   if (nk <= 0 || tile_iter >= nwg) return;
 
   if constexpr (NS == 2) {
@@ -394,7 +445,16 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a, int kt_p
         compute(st);
         st ^= 1;
       }
-      epilogue(m0c, n0c);
+      if (lds_epi) {
+        // every wave has finished reading the stage it just computed (st ^ 1);
+        // the next tile's first K-tile is landing in the other one
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        epilogue_lds(m0c, n0c, st ^ 1);
+      } else {
+        epilogue(m0c, n0c);
+      }
       if (next_iter < 0) break;
       tile_iter = next_iter;
 #pragma unroll
