@@ -85,6 +85,7 @@ Engine::Engine(const std::string& arch, const WeightMap& weights, int device, in
   if (const char* e = std::getenv("DMLC_ROW_CONV")) row_conv_ = std::string(e) != "0";
   if (const char* e = std::getenv("DMLC_BIGTILE")) bigtile_ = std::string(e) != "0";
   if (const char* e = std::getenv("DMLC_FUSED_PREPROCESS")) fused_pre_ = std::string(e) != "0";
+  if (const char* e = std::getenv("DMLC_STREAM_CONV")) stream_conv_ = std::string(e) != "0";
 
   if (arch == "resnet18")
     build_resnet({2, 2, 2, 2}, false);
@@ -535,8 +536,14 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
       case OpType::Conv: {
         const ConvLayer& L = convs_[op.conv];
         const ActShape& is = shapes_[op.in];
-        if (row_conv_ && !L.fc && !L.pair && !L.fp8 && L.kh == 3 && L.kw == 3 && L.stride == 1 && L.pad == 1 &&
-            !shapes_[op.out].f32 && !shapes_[op.out].fp8 && conv3x3_rows_supported(is.H, is.W, is.C, L.cout)) {
+        const bool k3s1 = !L.fc && !L.pair && !L.fp8 && L.kh == 3 && L.kw == 3 && L.stride == 1 && L.pad == 1 &&
+                          !shapes_[op.out].f32 && !shapes_[op.out].fp8;
+        // the stream conv runs 2 workgroups per image: only worth it once the batch fills the CUs
+        if (stream_conv_ && k3s1 && 8 * B >= num_cus_ && conv3x3_stream_supported(is.H, is.W, is.C, L.cout)) {
+          conv3x3_stream(acts_[op.in], (const uint8_t*)warena_ + L.w_off,
+                         (const float*)((const uint8_t*)warena_ + L.b_off), op.res >= 0 ? acts_[op.res] : nullptr,
+                         acts_[op.out], zero_, B, is.H, is.W, is.C, L.relu, s);
+        } else if (row_conv_ && k3s1 && conv3x3_rows_supported(is.H, is.W, is.C, L.cout)) {
           conv3x3_rows(acts_[op.in], (const uint8_t*)warena_ + L.w_off,
                        (const float*)((const uint8_t*)warena_ + L.b_off), op.res >= 0 ? acts_[op.res] : nullptr,
                        acts_[op.out], zero_, B, is.H, is.W, is.C, L.relu, conv3x3_rows_pick_strip(B, is.H, num_cus_),

@@ -122,6 +122,7 @@ class Engine {
   bool fused_stem_ = true;  // conv1+maxpool as one kernel (env DMLC_FUSED_STEM=0 disables)
   bool bigtile_ = true;     // 8-wave big-tile split-K convs where supported (env DMLC_BIGTILE=0 disables)
   bool fused_pre_ = true;   // SxS u8 images straight into the fused stem (env DMLC_FUSED_PREPROCESS=0 disables)
+  bool stream_conv_ = true; // direct 3x3 with streamed weights for 28x28x128 layers (env DMLC_STREAM_CONV=0 disables)
   bool row_conv_ = true;    // direct row-streaming 3x3 convs where supported (env DMLC_ROW_CONV=0 disables)
   bool fp8_ = false;        // resnet50_fp8
 

@@ -176,6 +176,22 @@ def conv3x3_rows(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, re
     return y
 
 
+def conv3x3_stream(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, res: torch.Tensor | None = None,
+                   relu: bool = True) -> torch.Tensor:
+    """Direct 3x3/s1/p1 conv (conv3x3_stream.hip) on NHWC bf16 [B,28,28,128]
+    with the conv2d packed weights [128, 1152]; + bias (+ residual), ReLU."""
+    _need_cuda(x, w_packed, bias, res)
+    C = native()
+    B, H, W, Cin = x.shape
+    if not C.conv3x3_stream_supported(H, W, Cin, w_packed.shape[0]):
+        raise ValueError("conv3x3_stream: unsupported shape")
+    y = torch.empty_like(x)
+    C.conv3x3_stream(_ptr(x.contiguous()), _ptr(w_packed.contiguous()), _ptr(bias.float().contiguous()),
+                     _ptr(None if res is None else res.contiguous()), _ptr(y), _ptr(_zero_page(x.device)), B, H, W,
+                     Cin, relu, _stream())
+    return y
+
+
 FP8 = torch.float8_e4m3fn  # OCP e4m3 (gfx950), max 448
 FP8_MAX = 448.0
 

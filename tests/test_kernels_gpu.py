@@ -257,6 +257,27 @@ def test_stem_conv_pool_u8(gpu, B, S, strip):
     assert torch.equal(one, two)
 
 
+@pytest.mark.parametrize("B,res,relu", [(1, False, True), (3, True, True), (2, True, False), (5, False, False)])
+def test_conv3x3_stream(gpu, B, res, relu):
+    """Direct 3x3 conv with streamed weights (conv3x3_stream.hip, 28x28x128) vs torch fp32."""
+    g = torch.Generator().manual_seed(21)
+    x = torch.randn(B, 128, 28, 28, generator=g).bfloat16().float()
+    w = (torch.randn(128, 128, 3, 3, generator=g) / 1152 ** 0.5).bfloat16().float()
+    bias = torch.randn(128, generator=g) * 0.1
+    ref = F.conv2d(x, w, bias, 1, 1)
+    r = None
+    if res:
+        r_nchw = torch.randn_like(ref).bfloat16().float()
+        ref = ref + r_nchw
+        r = _nhwc(r_nchw).bfloat16().to(gpu)
+    if relu:
+        ref = F.relu(ref)
+    wp = ops.pack_conv_weight(w, device=gpu)
+    y = ops.conv3x3_stream(_nhwc(x).bfloat16().to(gpu), wp, bias.to(gpu), r, relu)
+    torch.cuda.synchronize()
+    assert _rel(_nchw(y.float().cpu()), ref) < 8e-3
+
+
 @pytest.mark.parametrize("B,strip,res", [(2, None, False), (2, None, True), (3, 4, True), (1, 8, False),
                                          (1, 28, True)])
 def test_conv3x3_rows(gpu, B, strip, res):

@@ -118,6 +118,12 @@ def main():
                     row.append(_stamps())
             except Exception as e:  # noqa: BLE001
                 row.append(f"tile{t}=ERR({e})")
+        if name == "l2":  # direct conv with streamed weights (conv3x3_stream.hip)
+            for use_res in (False, True):
+                r = torch.randn(B, H, W, Cout, device=dev).bfloat16() if use_res else None
+                f = lambda: ops.conv3x3_stream(x, wp, bias, r, True)
+                us = time_us(f, a.iters)
+                row.append(f"stream{'+res' if use_res else ''}={us:7.1f}us {flops/us/1e6:6.0f}TF")
         if name == "l1":  # direct row-streaming conv (conv3x3_rows.hip)
             for use_res in (False, True):
                 r = torch.randn(B, H, W, Cout, device=dev).bfloat16() if use_res else None
