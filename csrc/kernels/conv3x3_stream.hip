@@ -54,21 +54,50 @@ struct StreamConvArgs {
   int relu;
 };
 
-template <int H, int W, int C>
+// Weight-row permutation: LDS row n of wave group g = n / WN (WN = 16*NF
+// channels per wave), n_local = 16*nf + r, holds output channel
+// g*WN + 32*(nf>>1) + 8*(r>>2) + 4*(nf&1) + (r&3): the lane with accumulator
+// rows 4fq..4fq+3 of fragments (2j, 2j+1) then owns 8 consecutive channels
+// g*WN + 32j + 8fq .. +7.
+template <int WN>
+__device__ __forceinline__ int perm_row(int n) {
+  const int g = n / WN, nl = n % WN, nf = nl >> 4, r = nl & 15;
+  return g * WN + 32 * (nf >> 1) + 8 * (r >> 2) + 4 * (nf & 1) + (r & 3);
+}
+
+// Weight-stage chunk swizzle (physical 16-B chunk of logical chunk c, row n):
+// 128-B rows (BK = 64): c ^ ((n>>1)&7) as conv_igemm.hip; 64-B rows (BK =
+// 32): c ^ (3*((n>>2)&1)) as conv_bigtile.hip. Both conflict-free for the
+// fragment reads (lane reads chunk fq of row base+fr, base % 16 == 0).
+template <int BK>
+__device__ __forceinline__ int wswz(int n, int c) {
+  if constexpr (BK == 64)
+    return c ^ ((n >> 1) & 7);
+  else
+    return c ^ (3 * ((n >> 2) & 1));
+}
+
+// One workgroup = HS output rows x W columns of one image, all C channels;
+// 8 waves = 2 pixel halves x 4 channel quarters.
+template <int H, int W, int C, int HS, int BK>
 __global__ __launch_bounds__(512, 1) void conv3x3_stream_kernel(StreamConvArgs a) {
-  static_assert(C == 128, "layout below assumes 128 channels (16 chunks per pixel, 4 waves x 32 channels)");
-  constexpr int HR = H / 2;                  // output rows per workgroup (half an image)
-  constexpr int NPIX = HR * W;               // 392 pixels
-  constexpr int MFT = (NPIX + 15) / 16;      // 25 pixel fragments (the last one partly padding)
-  constexpr int MF = (MFT + 1) / 2;          // per wave: 2 pixel halves of 13 fragments
-  constexpr int XR = HR + 2;                 // resident input rows (with the halo)
+  constexpr int NPIX = HS * W;               // output pixels per workgroup
+  constexpr int MFT = (NPIX + 15) / 16;      // pixel fragments (the last one partly padding)
+  constexpr int MF = (MFT + 1) / 2;          // per wave (2 pixel halves)
+  constexpr int WN = C / 4;                  // channels per wave
+  constexpr int NF = WN / 16;                // N fragments per wave
+  constexpr int XR = HS + 2;                 // resident input rows (with the halo)
   constexpr int Q = W + 2;                   // padded columns
+  constexpr int CPX = C / 8;                 // 16-B chunks per pixel
   constexpr int ROWB = Q * C * 2;            // bytes per staged input row
-  constexpr int XI = (Q * 16 + 63) / 64;     // LDS-DMA instructions per input row
-  constexpr int KT = 9 * C / 64;             // 64-deep K-tiles
-  constexpr int WSTAGE = C * 128;            // bytes per weight stage (C rows x 64 k)
-  constexpr int GW = C * 8 / 64 / 8;         // weight DMA instructions per wave per K-tile (2)
-  static_assert(H % 2 == 0, "two halves per image");
+  constexpr int XI = (Q * CPX + 63) / 64;    // LDS-DMA instructions per input row
+  constexpr int KT = 9 * C / BK;             // K-tiles
+  constexpr int CT = C / BK;                 // K-tiles per tap
+  constexpr int WCH = BK / 8;                // 16-B chunks per weight row
+  constexpr int WSTAGE = C * BK * 2;         // bytes per weight stage
+  constexpr int GW = C * WCH / 64 / 8;       // weight DMA instructions per wave per K-tile
+  static_assert(C % 64 == 0 && CPX >= 16 && NF % 2 == 0 && H % HS == 0, "geometry");
+  static_assert(C * WCH % 512 == 0, "weight stage splits into 8 waves x 64 lanes");
 
   extern __shared__ __attribute__((aligned(16))) uint4 smem[];
   char* xs = (char*)smem;
@@ -76,43 +105,42 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream_kernel(StreamConvArgs a
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int mh = wave & 1, wn = wave >> 1;  // pixel half, channel quarter (32 channels)
+  const int mh = wave & 1, wn = wave >> 1;  // pixel half, channel quarter
   const int fr = lane & 15, fq = lane >> 4;
-  const int b = blockIdx.x >> 1, half = blockIdx.x & 1;
-  const int r0 = half * HR;  // first output row
+  constexpr int PARTS = H / HS;
+  const int b = blockIdx.x / PARTS, part = blockIdx.x - b * PARTS;
+  const int r0 = part * HS;  // first output row
   const bf16* img = a.x + (long)b * H * W * C;
 
-  // ---- input rows r0-1 .. r0+HR (outside rows are zeros): instruction k =
-  // row*XI + j goes to wave k % 8
+  // ---- input rows r0-1 .. r0+HS (outside rows/columns are zeros), chunk c of
+  // padded column q at physical chunk c ^ (q & 15): instruction k = row*XI + j
+  // goes to wave k % 8
   for (int k = wave; k < XR * XI; k += 8) {
     const int xr = k / XI, j = k - xr * XI;
     const int r = r0 - 1 + xr;
     const int i = j * 64 + lane;  // chunk of the padded row
-    const int q = i >> 4, pc = i & 15;
+    const int q = i / CPX, pc = i - q * CPX;
     const bool ok = (unsigned)r < (unsigned)H && q >= 1 && q <= W;
     const bf16* src = ok ? img + ((long)r * W + (q - 1)) * C + 8 * (pc ^ (q & 15)) : a.zero;
-    if (i < Q * 16)
+    if (i < Q * CPX)
       __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)(xs + xr * ROWB + j * 1024), 16, 0, 0);
   }
 
-  // ---- weight K-tile t -> stage st. LDS row n = 32wg + 16nf + r holds channel
-  // 32wg + 8(r>>2) + 4nf + (r&3); 16-B chunk c of row n sits at c ^ ((n>>1)&7).
+  // ---- weight K-tile t (k = BK*t ..) -> stage st (rows permuted, chunks swizzled)
   auto load_wtile = [&](int t, int st) __attribute__((always_inline)) {
 #pragma unroll
     for (int p = 0; p < GW; ++p) {
       const int qi = wave * GW + p;  // 1 KB instruction of the stage
       const int i = qi * 64 + lane;
-      const int n = i >> 3, pc = i & 7;
-      const int ch = (n & ~31) + 8 * ((n & 15) >> 2) + 4 * ((n >> 4) & 1) + (n & 3);
-      const bf16* src = a.w + (long)ch * (9 * C) + t * 64 + 8 * (pc ^ ((n >> 1) & 7));
+      const int n = i / WCH, pc = i - n * WCH;
+      const bf16* src = a.w + (long)perm_row<WN>(n) * (9 * C) + t * BK + 8 * wswz<BK>(n, pc);
       __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)(wring + st * WSTAGE + qi * 1024), 16, 0, 0);
     }
   };
   load_wtile(0, 0);
 
-  // ---- per-lane constants: pixel p = 16(mh*MF + f) + fr of the half image
-  // (clamped for padding lanes / the dummy 26th fragment: they compute a
-  // duplicate, never stored)
+  // ---- per-lane constants: pixel p = 16(mh*MF + f) + fr (clamped for padding
+  // lanes / a dummy last fragment: they compute a duplicate, never stored)
   int xoff[MF];  // LDS byte offset of (input row prow, padded column pcol) = tap (0, 0)
   int key[MF];   // padded column of tap (0, 0): the chunk swizzle key is (key + kw) & 15
 #pragma unroll
@@ -122,15 +150,18 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream_kernel(StreamConvArgs a
     xoff[f] = prow * ROWB + pcol * (C * 2);
     key[f] = pcol;
   }
-  const uint32_t wrow = (uint32_t)(32 * wn + fr) * 128;
-  const int wsw = (fr >> 1) & 7;
-  float bs[8];  // bias of this lane's 8 channels 32*wn + 8fq + e
+  const uint32_t wrow = (uint32_t)(WN * wn + fr) * (BK * 2);
+  float bs[NF / 2][8];  // bias of this lane's channels WN*wn + 32j + 8fq + e
 #pragma unroll
-  for (int e = 0; e < 8; ++e) bs[e] = a.bias[32 * wn + 8 * fq + e];
+  for (int j = 0; j < NF / 2; ++j)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bs[j][e] = a.bias[WN * wn + 32 * j + 8 * fq + e];
 
-  floatx4 acc[MF][2];
+  floatx4 acc[MF][NF];
 #pragma unroll
-  for (int f = 0; f < MF; ++f) acc[f][0] = acc[f][1] = floatx4{0.f, 0.f, 0.f, 0.f};
+  for (int f = 0; f < MF; ++f)
+#pragma unroll
+    for (int nf = 0; nf < NF; ++nf) acc[f][nf] = floatx4{0.f, 0.f, 0.f, 0.f};
 
   // ---- K loop: 2-stage weight ring, the DMA of K-tile t+1 issued after the
   // barrier that retires every wave's reads of K-tile t-1
@@ -141,58 +172,63 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream_kernel(StreamConvArgs a
     asm volatile("" ::: "memory");
     if (t + 1 < KT) load_wtile(t + 1, (t + 1) & 1);
 
-    const int tap = t >> 1, c64 = t & 1;
+    const int tap = t / CT, cc = t - tap * CT;
     const int kh = tap / 3, kw = tap - kh * 3;
     const int toff = kh * ROWB + kw * (C * 2);
     const char* ws = wring + (t & 1) * WSTAGE + wrow;
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 wf[2];
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      bf16x8 wf[NF];
 #pragma unroll
-      for (int nf = 0; nf < 2; ++nf)
-        wf[nf] = *(const bf16x8*)(ws + nf * 16 * 128 + (((ks * 4 + fq) ^ wsw) << 4));
-      const int cbase = c64 * 8 + ks * 4 + fq;
+      for (int nf = 0; nf < NF; ++nf)
+        wf[nf] = *(const bf16x8*)(ws + nf * 16 * (BK * 2) + (wswz<BK>(fr, ks * 4 + fq) << 4));
+      const int cbase = cc * WCH + ks * 4 + fq;
 #pragma unroll
       for (int f = 0; f < MF; ++f) {
         const int ch = cbase ^ ((key[f] + kw) & 15);
         const bf16x8 xf = *(const bf16x8*)(xs + xoff[f] + toff + (ch << 4));
 #pragma unroll
-        for (int nf = 0; nf < 2; ++nf)
+        for (int nf = 0; nf < NF; ++nf)
           acc[f][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[nf], xf, acc[f][nf], 0, 0, 0);
       }
     }
   }
 
-  // ---- epilogue: lane holds channels 32*wn + 8fq .. +7 of its pixel
-  const long base = ((long)b * H + r0) * W * C + 32 * wn + 8 * fq;
+  // ---- epilogue: lane holds channels WN*wn + 32j + 8fq .. +7 of its pixel
+  const long base = ((long)b * H + r0) * W * C + WN * wn + 8 * fq;
 #pragma unroll
   for (int f = 0; f < MF; ++f) {
     const int p = 16 * (mh * MF + f) + fr;
     if (p >= NPIX) continue;
-    const long off = base + (long)p * C;
-    float v[8];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      v[e] = acc[f][0][e] + bs[e];
-      v[4 + e] = acc[f][1][e] + bs[4 + e];
-    }
-    if (a.res) {
-      float r[8];
-      unpack8(*(const uint4*)(a.res + off), r);
+    for (int j = 0; j < NF / 2; ++j) {
+      const long off = base + (long)p * C + 32 * j;
+      float v[8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] += r[e];
-    }
-    if (a.relu) {
+      for (int e = 0; e < 4; ++e) {
+        v[e] = acc[f][2 * j][e] + bs[j][e];
+        v[4 + e] = acc[f][2 * j + 1][e] + bs[j][4 + e];
+      }
+      if (a.res) {
+        float r[8];
+        unpack8(*(const uint4*)(a.res + off), r);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+        for (int e = 0; e < 8; ++e) v[e] += r[e];
+      }
+      if (a.relu) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+      }
+      *(uint4*)(a.y + off) = pack8(v);
     }
-    *(uint4*)(a.y + off) = pack8(v);
   }
 }
 
 }  // namespace
 
-bool conv3x3_stream_supported(int H, int W, int Cin, int Cout) { return H == 28 && W == 28 && Cin == 128 && Cout == 128; }
+bool conv3x3_stream_supported(int H, int W, int Cin, int Cout) {
+  return Cin == Cout && ((H == 28 && W == 28 && Cin == 128) || (H == 14 && W == 14 && Cin == 256));
+}
 
 void conv3x3_stream(const void* x, const void* w, const float* bias, const void* res, void* y, const void* zero,
                     int B, int H, int W, int C, bool relu, hipStream_t s) {
@@ -209,8 +245,13 @@ void conv3x3_stream(const void* x, const void* w, const float* bias, const void*
   a.y = (bf16*)y;
   a.zero = (const bf16*)zero;
   a.relu = relu;
-  const size_t lds = (size_t)(14 + 2) * (28 + 2) * 128 * 2 + (size_t)2 * 128 * 128;
-  hipLaunchKernelGGL((conv3x3_stream_kernel<28, 28, 128>), dim3(2 * B), dim3(512), lds, s, a);
+  if (C == 128) {  // layer2: half an image per workgroup (16 x 30 x 256 B rows + 2 x 16 KB weight stages)
+    const size_t lds = (size_t)(14 + 2) * (28 + 2) * 128 * 2 + (size_t)2 * 128 * 64 * 2;
+    hipLaunchKernelGGL((conv3x3_stream_kernel<28, 28, 128, 14, 64>), dim3(2 * B), dim3(512), lds, s, a);
+  } else {  // layer3: a whole image per workgroup (16 x 16 x 512 B rows + 2 x 16 KB weight stages = 160 KB)
+    const size_t lds = (size_t)(14 + 2) * (14 + 2) * 256 * 2 + (size_t)2 * 256 * 32 * 2;
+    hipLaunchKernelGGL((conv3x3_stream_kernel<14, 14, 256, 14, 32>), dim3(B), dim3(512), lds, s, a);
+  }
   DMLC_HIP_CHECK(hipGetLastError());
 }
 

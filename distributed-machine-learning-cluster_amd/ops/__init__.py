@@ -178,8 +178,8 @@ def conv3x3_rows(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, re
 
 def conv3x3_stream(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, res: torch.Tensor | None = None,
                    relu: bool = True) -> torch.Tensor:
-    """Direct 3x3/s1/p1 conv (conv3x3_stream.hip) on NHWC bf16 [B,28,28,128]
-    with the conv2d packed weights [128, 1152]; + bias (+ residual), ReLU."""
+    """Direct 3x3/s1/p1 conv (conv3x3_stream.hip) on NHWC bf16 [B,28,28,128] or
+    [B,14,14,256] with the conv2d packed weights; + bias (+ residual), ReLU."""
     _need_cuda(x, w_packed, bias, res)
     C = native()
     B, H, W, Cin = x.shape

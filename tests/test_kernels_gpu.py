@@ -257,13 +257,17 @@ def test_stem_conv_pool_u8(gpu, B, S, strip):
     assert torch.equal(one, two)
 
 
-@pytest.mark.parametrize("B,res,relu", [(1, False, True), (3, True, True), (2, True, False), (5, False, False)])
-def test_conv3x3_stream(gpu, B, res, relu):
-    """Direct 3x3 conv with streamed weights (conv3x3_stream.hip, 28x28x128) vs torch fp32."""
+@pytest.mark.parametrize("HW,C,B,res,relu", [(28, 128, 1, False, True), (28, 128, 3, True, True),
+                                             (28, 128, 2, True, False), (28, 128, 5, False, False),
+                                             (14, 256, 1, False, True), (14, 256, 3, True, True),
+                                             (14, 256, 2, True, False)])
+def test_conv3x3_stream(gpu, HW, C, B, res, relu):
+    """Direct 3x3 conv with streamed weights (conv3x3_stream.hip: 28x28x128
+    half images, 14x14x256 whole images) vs torch fp32."""
     g = torch.Generator().manual_seed(21)
-    x = torch.randn(B, 128, 28, 28, generator=g).bfloat16().float()
-    w = (torch.randn(128, 128, 3, 3, generator=g) / 1152 ** 0.5).bfloat16().float()
-    bias = torch.randn(128, generator=g) * 0.1
+    x = torch.randn(B, C, HW, HW, generator=g).bfloat16().float()
+    w = (torch.randn(C, C, 3, 3, generator=g) / (9 * C) ** 0.5).bfloat16().float()
+    bias = torch.randn(C, generator=g) * 0.1
     ref = F.conv2d(x, w, bias, 1, 1)
     r = None
     if res:
