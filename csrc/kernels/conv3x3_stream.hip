@@ -1,5 +1,6 @@
-// Direct 3x3 / stride 1 / pad 1 convolution for 128-channel 28x28 layers
-// (ResNet layer2: layer2.0.conv2, layer2.1.conv{1,2}), BN folded, optional
+// Direct 3x3 / stride 1 / pad 1 convolution with the input image resident in
+// LDS, for ResNet18 layer2 (28x28x128: layer2.0.conv2, layer2.1.conv{1,2}) and
+// layer3 (14x14x256: layer3.0.conv2, layer3.1.conv{1,2}), BN folded, optional
 // residual, ReLU.
 //
 // Reference equivalent: those convs + bn + (residual) + relu of
@@ -7,27 +8,29 @@
 // As an implicit GEMM (conv_igemm.hip) every output tile re-fetches its 3x3
 // input window per tap: 9x the input bytes through L2, and in the model the
 // input is cold (written by the previous layer), so these convs ran at 113-128
-// us against 85 us on L2-hot inputs. Here one workgroup owns half an image
-// (14 output rows = 392 pixels = 25 fragments of 16):
+// us against 85 us on L2-hot inputs. Here one workgroup owns HS output rows of
+// one image (layer2: half an image, 392 pixels; layer3: the whole image, 196):
 //
-//  * Its 16 input rows (with the halo; zero rows/columns from a zero page) go
-//    HBM -> LDS once by LDS-DMA and stay resident (120 KB). Pixel rows are
-//    256 B (16 chunks of 8 channels); chunk c of padded column q sits at
-//    physical chunk c ^ (q & 15), so the 16 pixels of a fragment read spread
-//    over all 16 bank slots.
-//  * The folded weights (128 x 1152 bf16 = 295 KB, shared by every CU and
-//    L2-resident) stream once per workgroup through a 2-stage LDS-DMA ring of
-//    64-deep K-tiles (128 rows x 128 B, chunks XOR-swizzled by (row>>1)&7 as
-//    in conv_igemm.hip); a K-tile is 52 MFMAs per wave, 2 waves per SIMD: long enough to hide
-//    the next tile's L2 fetch. (A 4-row step variant re-streamed the weights
-//    7x per image and was L2-bound at 115 us.)
-//  * 8 waves (2 per SIMD: one's LDS reads hide under the other's MFMAs) = 2
-//    pixel halves (13 fragments) x 4 channel quarters (2 N fragments of 16);
-//    with all 25 fragments in one wave the accumulators took 512 registers
-//    and every MFMA pair waited on its own LDS read. D = W x X. The
-//    weight rows are permuted when staged (LDS row 32w + 16nf + r holds
-//    channel 32w + 8(r>>2) + 4nf + (r&3)), so a lane ends with 8 consecutive
-//    output channels of one pixel: 16-B residual loads and output stores.
+//  * Its input rows (the strip plus the halo rows inside the image) go HBM ->
+//    LDS once by LDS-DMA and stay resident; taps that fall outside the image
+//    read one zero pixel instead of staged zero padding. Chunks are XOR-
+//    swizzled per pixel (see the staging loop) so every fragment read is
+//    bank-conflict free and costs one VALU add.
+//  * The folded weights (C x 9C bf16, 295 KB / 1.2 MB, shared by every CU and
+//    L2-resident) stream through LDS in 32-deep K-tiles. Every wave streams
+//    just the 32 output-channel rows it uses through a private 3-stage LDS-DMA
+//    ring and waits only on its own vmcnt: the K loop has no workgroup
+//    barrier. (With one shared ring the per-K-tile barrier, and the LDS read
+//    latency it exposed, held the loop at ~50% MFMA busy: without MFMAs the
+//    barrier/read skeleton alone took 35 of 60 us.)
+//  * 8 waves (2 per SIMD) = WM pixel groups x 8/WM channel groups of 32 (2 N
+//    fragments of 16), 13 pixel fragments each: layer2 WM=2 (its two pixel
+//    halves each stream the channel group's rows), layer3 WM=1. D = W x X. The
+//    weight rows are permuted when staged (row 16nf + r of a wave's tile holds
+//    channel 8(r>>2) + 4nf + (r&3) of its group), so a lane ends with 8
+//    consecutive output channels of one pixel: 16-B residual loads and stores.
+//  * The K loop is software-pipelined: the operands of K-tile t+1 are read
+//    while the MFMAs of t run.
 #include "common.h"
 #include "kernels.h"
 
@@ -35,8 +38,23 @@ namespace dmlc {
 
 namespace {
 
-typedef __attribute__((address_space(3))) void* lds_ptr_t;
-typedef const __attribute__((address_space(1))) void* gbl_ptr_t;
+// 16-B-per-lane LDS-DMA (lane l's 16 bytes land at lds + 16 l), issued as
+// inline asm: with __builtin_amdgcn_global_load_lds in flight the compiler's
+// waitcnt pass turns every LDS-read wait into lgkmcnt(0), which serialised
+// the pipelined K loop on its newest reads. The pass does not see these, so
+// every vmcnt wait on them is explicit (vm_wait), and no compiler-visible
+// memory op is in flight with them except the epilogue's, issued after the
+// last wait.
+__device__ __forceinline__ void dma16(const void* gsrc, const void* lds) {
+  const uint32_t l = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)lds);
+  asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(l), "v"(gsrc) : "memory", "m0");
+}
+
+// Same with a scalar base (saddr form): lane l loads base + voff[l].
+__device__ __forceinline__ void dma16s(const void* sbase, uint32_t voff, const void* lds) {
+  const uint32_t l = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)lds);
+  asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, %2" ::"s"(l), "v"(voff), "s"(sbase) : "memory", "m0");
+}
 
 template <int N>
 __device__ __forceinline__ void vm_wait() {
@@ -52,176 +70,279 @@ struct StreamConvArgs {
   bf16* y;            // [B, H, W, C]
   const bf16* zero;   // >= 16 zero bytes
   int relu;
+  unsigned long long* stamps;  // debug: per-workgroup phase stamps (100 MHz), or null
 };
 
-// Weight-row permutation: LDS row n of wave group g = n / WN (WN = 16*NF
-// channels per wave), n_local = 16*nf + r, holds output channel
-// g*WN + 32*(nf>>1) + 8*(r>>2) + 4*(nf&1) + (r&3): the lane with accumulator
-// rows 4fq..4fq+3 of fragments (2j, 2j+1) then owns 8 consecutive channels
-// g*WN + 32j + 8fq .. +7.
-template <int WN>
-__device__ __forceinline__ int perm_row(int n) {
-  const int g = n / WN, nl = n % WN, nf = nl >> 4, r = nl & 15;
-  return g * WN + 32 * (nf >> 1) + 8 * (r >> 2) + 4 * (nf & 1) + (r & 3);
+// Weight-row permutation inside a wave's 32-row tile: row n = 16nf + r holds
+// channel 8(r>>2) + 4nf + (r&3) of the group, so the lane with accumulator
+// rows 4fq..4fq+3 of fragments 0 and 1 owns the 8 consecutive channels
+// 8fq .. 8fq+7.
+__device__ __forceinline__ int perm32(int n) {
+  const int nf = n >> 4, r = n & 15;
+  return 8 * (r >> 2) + 4 * nf + (r & 3);
 }
 
-// Weight-stage chunk swizzle (physical 16-B chunk of logical chunk c, row n):
-// 128-B rows (BK = 64): c ^ ((n>>1)&7) as conv_igemm.hip; 64-B rows (BK =
-// 32): c ^ (3*((n>>2)&1)) as conv_bigtile.hip. Both conflict-free for the
-// fragment reads (lane reads chunk fq of row base+fr, base % 16 == 0).
-template <int BK>
-__device__ __forceinline__ int wswz(int n, int c) {
-  if constexpr (BK == 64)
-    return c ^ ((n >> 1) & 7);
-  else
-    return c ^ (3 * ((n >> 2) & 1));
-}
+// Weight-tile chunk swizzle (physical 16-B chunk of logical chunk c of a 64-B
+// row n), as conv_bigtile.hip: conflict-free for the fragment reads (lane
+// reads chunk fq of row 16nf + fr).
+__device__ __forceinline__ int wswz(int n, int c) { return c ^ (3 * ((n >> 2) & 1)); }
 
-// One workgroup = HS output rows x W columns of one image, all C channels;
-// 8 waves = 2 pixel halves x 4 channel quarters.
-template <int H, int W, int C, int HS, int BK>
+// Geometry shared by the kernel and its launcher.
+template <int H, int W, int C, int HS, int ND>
+struct StreamGeom {
+  static constexpr int PARTS = H / HS;
+  static constexpr int XR = PARTS == 1 ? H : PARTS == 2 ? HS + 1 : HS + 2;  // max staged rows
+  static constexpr int PXB = C * 2;                    // bytes per pixel
+  static constexpr int ROWB = W * PXB;                 // bytes per staged row
+  static constexpr int ZB = XR * ROWB;                 // zero pixel
+  static constexpr int XBYTES = ZB + PXB;              // input region
+  static constexpr int WST = 32 * 32 * 2;              // a wave's weight stage: 32 rows x 32 k
+  static constexpr size_t LDS = (size_t)XBYTES + (size_t)8 * ND * WST;
+};
+
+// One workgroup = HS output rows x W columns of one image, all C channels.
+template <int H, int W, int C, int HS, int WM, int ND>
 __global__ __launch_bounds__(512, 1) void conv3x3_stream_kernel(StreamConvArgs a) {
+  using G = StreamGeom<H, W, C, HS, ND>;
+  constexpr int BK = 32;                     // K-tile depth = one MFMA k-step
   constexpr int NPIX = HS * W;               // output pixels per workgroup
   constexpr int MFT = (NPIX + 15) / 16;      // pixel fragments (the last one partly padding)
-  constexpr int MF = (MFT + 1) / 2;          // per wave (2 pixel halves)
-  constexpr int WN = C / 4;                  // channels per wave
-  constexpr int NF = WN / 16;                // N fragments per wave
-  constexpr int XR = HS + 2;                 // resident input rows (with the halo)
-  constexpr int Q = W + 2;                   // padded columns
+  constexpr int MF = (MFT + WM - 1) / WM;    // per wave
+  constexpr int WN = 32;                     // channels per wave
+  constexpr int NF = 2;                      // N fragments per wave
+  constexpr int PXB = G::PXB, ROWB = G::ROWB, ZB = G::ZB, WST = G::WST;
   constexpr int CPX = C / 8;                 // 16-B chunks per pixel
-  constexpr int ROWB = Q * C * 2;            // bytes per staged input row
-  constexpr int XI = (Q * CPX + 63) / 64;    // LDS-DMA instructions per input row
+  constexpr int XI = W * CPX / 64;           // LDS-DMA instructions per input row
   constexpr int KT = 9 * C / BK;             // K-tiles
   constexpr int CT = C / BK;                 // K-tiles per tap
-  constexpr int WCH = BK / 8;                // 16-B chunks per weight row
-  constexpr int WSTAGE = C * BK * 2;         // bytes per weight stage
-  constexpr int GW = C * WCH / 64 / 8;       // weight DMA instructions per wave per K-tile
-  static_assert(C % 64 == 0 && CPX >= 16 && NF % 2 == 0 && H % HS == 0, "geometry");
-  static_assert(C * WCH % 512 == 0, "weight stage splits into 8 waves x 64 lanes");
+  constexpr int GW = WST / 1024;             // weight DMA instructions per wave per K-tile
+  static_assert(C == 8 / WM * WN && W * CPX % 64 == 0 && H % HS == 0 && PXB >= 256, "geometry");
+  static_assert(ND == 3 && KT >= ND, "the loop's waits assume a 3-stage ring");
+  static_assert(MF + NF <= 15, "lgkmcnt range of the pipelined loop");
 
   extern __shared__ __attribute__((aligned(16))) uint4 smem[];
   char* xs = (char*)smem;
-  char* wring = xs + XR * ROWB;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int mh = wave & 1, wn = wave >> 1;  // pixel half, channel quarter
+  const int wm = wave % WM, wc = wave / WM;  // pixel group, channel group
   const int fr = lane & 15, fq = lane >> 4;
-  constexpr int PARTS = H / HS;
+  const char* wpriv = xs + G::XBYTES + wave * (ND * WST);
+  constexpr int PARTS = G::PARTS;
   const int b = blockIdx.x / PARTS, part = blockIdx.x - b * PARTS;
-  const int r0 = part * HS;  // first output row
+  const int r0 = part * HS;                                 // first output row
+  const int rs = max(r0 - 1, 0), nrows = min(r0 + HS, H - 1) - rs + 1;  // staged input rows
   const bf16* img = a.x + (long)b * H * W * C;
-
-  // ---- input rows r0-1 .. r0+HS (outside rows/columns are zeros), chunk c of
-  // padded column q at physical chunk c ^ (q & 15): instruction k = row*XI + j
-  // goes to wave k % 8
-  for (int k = wave; k < XR * XI; k += 8) {
-    const int xr = k / XI, j = k - xr * XI;
-    const int r = r0 - 1 + xr;
-    const int i = j * 64 + lane;  // chunk of the padded row
-    const int q = i / CPX, pc = i - q * CPX;
-    const bool ok = (unsigned)r < (unsigned)H && q >= 1 && q <= W;
-    const bf16* src = ok ? img + ((long)r * W + (q - 1)) * C + 8 * (pc ^ (q & 15)) : a.zero;
-    if (i < Q * CPX)
-      __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)(xs + xr * ROWB + j * 1024), 16, 0, 0);
+  // A scalar memory op still pending in the loop (a debug stamp, or a kernel
+  // argument whose s_load the compiler hoists into the loop's preheader) shares
+  // lgkmcnt with the LDS reads and completes out of order, which turns every
+  // counted LDS wait into lgkmcnt(0): consume them here.
+  const int relu = a.relu;
+  asm volatile("" ::"s"(relu));
+  unsigned long long t_start = 0, t_first = 0;
+  if (a.stamps) {
+    t_start = __builtin_amdgcn_s_memrealtime();
+    asm volatile("" ::"s"(t_start));
   }
 
-  // ---- weight K-tile t (k = BK*t ..) -> stage st (rows permuted, chunks swizzled)
+  // ---- input rows rs .. rs+nrows-1. Staged pixel (i, q) has key K = i*W + q,
+  // which for output pixel p at tap (kh, kw) is p + const: consecutive along a
+  // fragment even where it wraps an output row. Chunk c sits at physical chunk
+  // c ^ ((K & 7) << 1). A ds_read_b128 16-lane group holds fragment pixels
+  // 0-3,12-15 at k-group g and 4-11 at g^1 (g even): pixels j and j+8 (one of
+  // each set) share the pair index (c>>1) ^ (K&7) and differ in the low bit,
+  // and the 8 pair indices are distinct: all 16 bank slots for any fragment
+  // offset. (The first layout, padded column & 15 under an XOR, collided
+  // whenever a fragment started at an odd key or wrapped a row: 39% of LDS
+  // cycles were bank conflicts.) A read is one VALU add off a per-tap base.
+  // (Pixels padded by 32 B put chunk c of key K in slot (2K + c) mod 16,
+  // also conflict-free and with reads at immediate offsets, but the fully
+  // unrolled loop that needs spilled registers.) Instruction k = row*XI + j
+  // goes to wave k % 8.
+  for (int k = wave; k < nrows * XI; k += 8) {
+    const int i = k / XI, j = k - i * XI;
+    const int ci = j * 64 + lane;  // chunk of the staged row
+    const int q = ci / CPX, pp = ci - q * CPX;
+    const int pc = pp ^ (((i * W + q) & 7) << 1);  // logical chunk at physical pp
+    dma16(img + ((long)(rs + i) * W + q) * C + 8 * pc, xs + i * ROWB + j * 1024);
+  }
+  if (wave == 0 && lane < CPX) dma16(a.zero, xs + ZB);
+
+  // ---- this wave's 32 weight rows of K-tile t -> its stage st (rows permuted,
+  // chunks swizzled): per-lane byte offsets into the weights, the K-tile
+  // advance in the scalar base
+  uint32_t woff[GW];
+#pragma unroll
+  for (int g = 0; g < GW; ++g) {
+    const int ci = g * 64 + lane, n = ci >> 2, pc = ci & 3;
+    woff[g] = (uint32_t)(((wc * WN + perm32(n)) * (9 * C) + 8 * wswz(n, pc)) * 2);
+  }
+  const bf16* wbase = a.w;
   auto load_wtile = [&](int t, int st) __attribute__((always_inline)) {
 #pragma unroll
-    for (int p = 0; p < GW; ++p) {
-      const int qi = wave * GW + p;  // 1 KB instruction of the stage
-      const int i = qi * 64 + lane;
-      const int n = i / WCH, pc = i - n * WCH;
-      const bf16* src = a.w + (long)perm_row<WN>(n) * (9 * C) + t * BK + 8 * wswz<BK>(n, pc);
-      __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)(wring + st * WSTAGE + qi * 1024), 16, 0, 0);
-    }
+    for (int g = 0; g < GW; ++g) dma16s(wbase + t * BK, woff[g], wpriv + st * WST + g * 1024);
   };
-  load_wtile(0, 0);
+#pragma unroll
+  for (int t = 0; t < ND - 1; ++t) load_wtile(t, t);
 
-  // ---- per-lane constants: pixel p = 16(mh*MF + f) + fr (clamped for padding
-  // lanes / a dummy last fragment: they compute a duplicate, never stored)
-  int xoff[MF];  // LDS byte offset of (input row prow, padded column pcol) = tap (0, 0)
-  int key[MF];   // padded column of tap (0, 0): the chunk swizzle key is (key + kw) & 15
+  // ---- per-lane constants: pixel p = 16(wm*MF + f) + fr (clamped for padding
+  // lanes / a dummy last fragment: they compute a duplicate, never stored).
+  // The swizzle term ((p + const) & 7) << 5 has p & 7 == fr & 7 for every real
+  // pixel (fragments start at multiples of 16), so it is one lane value per
+  // tap for all fragments (clamped lanes read a permuted chunk of their
+  // clamped pixel: in bounds, never stored). The low 4 bits of xoff flag the
+  // image's first/last row and column, whose outside taps read the zero pixel.
+  int xoff[MF];
 #pragma unroll
   for (int f = 0; f < MF; ++f) {
-    const int p = min(16 * (mh * MF + f) + fr, NPIX - 1);
-    const int prow = p / W, pcol = p - prow * W;
-    xoff[f] = prow * ROWB + pcol * (C * 2);
-    key[f] = pcol;
+    const int p = min(16 * (wm * MF + f) + fr, NPIX - 1);
+    const int prow = p / W, pcol = p - prow * W, r = r0 + prow;
+    xoff[f] = ((r - rs) * W + pcol) * PXB | (r == 0 ? 1 : 0) | (r == H - 1 ? 2 : 0) | (pcol == 0 ? 4 : 0) |
+              (pcol == W - 1 ? 8 : 0);
+    asm volatile("" : "+v"(xoff[f]));  // keep it live: rematerialising p / W in the loop cost ~100 VALU per K-tile
   }
-  const uint32_t wrow = (uint32_t)(WN * wn + fr) * (BK * 2);
-  float bs[NF / 2][8];  // bias of this lane's channels WN*wn + 32j + 8fq + e
-#pragma unroll
-  for (int j = 0; j < NF / 2; ++j)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) bs[j][e] = a.bias[WN * wn + 32 * j + 8 * fq + e];
-
   floatx4 acc[MF][NF];
 #pragma unroll
   for (int f = 0; f < MF; ++f)
 #pragma unroll
     for (int nf = 0; nf < NF; ++nf) acc[f][nf] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  // ---- K loop: 2-stage weight ring, the DMA of K-tile t+1 issued after the
-  // barrier that retires every wave's reads of K-tile t-1
-  for (int t = 0; t < KT; ++t) {
-    vm_wait<0>();  // this wave's DMAs of K-tile t (and, at t = 0, of the input rows)
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (t + 1 < KT) load_wtile(t + 1, (t + 1) & 1);
-
-    const int tap = t / CT, cc = t - tap * CT;
+  // per-tap fragment bases xa[f] and lane swizzle tsw = 16 fq ^ ((K & 7) << 5)
+  const int key = 32 * ((fr + (r0 - rs) * W) & 7);
+  int xa[MF], tsw = 0;
+  auto set_tap = [&](int tap) __attribute__((always_inline)) {
     const int kh = tap / 3, kw = tap - kh * 3;
-    const int toff = kh * ROWB + kw * (C * 2);
-    const char* ws = wring + (t & 1) * WSTAGE + wrow;
+    const int tm = (kh == 0 ? 1 : 0) | (kh == 2 ? 2 : 0) | (kw == 0 ? 4 : 0) | (kw == 2 ? 8 : 0);
+    const int toff = ((kh - 1) * W + (kw - 1)) * PXB;
 #pragma unroll
-    for (int ks = 0; ks < BK / 32; ++ks) {
-      bf16x8 wf[NF];
+    for (int f = 0; f < MF; ++f) xa[f] = (xoff[f] & tm) ? ZB : (xoff[f] & ~15) + toff;
+    tsw = (fq << 4) ^ ((key + 32 * ((kh - 1) * W + kw - 1)) & 0xE0);
+  };
+  const uint32_t wlane = fr * (BK * 2) + (wswz(fr, fq) << 4);
+  auto wread = [&](bf16x8* wf, int st) __attribute__((always_inline)) {
 #pragma unroll
-      for (int nf = 0; nf < NF; ++nf)
-        wf[nf] = *(const bf16x8*)(ws + nf * 16 * (BK * 2) + (wswz<BK>(fr, ks * 4 + fq) << 4));
-      const int cbase = cc * WCH + ks * 4 + fq;
+    for (int nf = 0; nf < NF; ++nf) wf[nf] = *(const bf16x8*)(wpriv + st * WST + nf * 16 * (BK * 2) + wlane);
+  };
+  // fragment f of the current tap's K-tile cc (the in-pixel offset is < PXB,
+  // so the add is an OR)
+  auto xread = [&](int f, int cc) __attribute__((always_inline)) {
+    return *(const bf16x8*)(xs + xa[f] + (tsw ^ (cc * BK * 2)));
+  };
+
+  // ---- software-pipelined K loop (one 32-deep k-step per K-tile), no
+  // workgroup barrier: the operands of K-tile t+1 are read while the MFMAs of t
+  // run, each X fragment's next read right after its own MFMAs, the weight
+  // fragments at the start of the tile. Iteration t first waits for the
+  // wave's own DMA of t+1 (issued one iteration earlier), then refills the
+  // stage of t-1 (read during t-2, consumed by t-1's MFMAs) with t+2.
+  set_tap(0);
+  vm_wait<(ND - 2) * GW>();  // own input rows and K-tile 0
+  __builtin_amdgcn_s_barrier();  // every wave's input rows
+  asm volatile("" ::: "memory");
+  if (a.stamps) {
+    t_first = __builtin_amdgcn_s_memrealtime();
+    asm volatile("" ::"s"(t_first));
+  }
+  bf16x8 wf[NF], xf[MF];
+  wread(wf, 0);
+#pragma unroll
+  for (int f = 0; f < MF; ++f) xf[f] = xread(f, 0);
+  int st = 0;
+  for (int tap = 0; tap < 9; ++tap) {
+#pragma unroll
+    for (int cc = 0; cc < CT; ++cc) {
+      const int t = tap * CT + cc;
+      if (t + 1 < KT) vm_wait<0>();
+      if (t + ND - 1 < KT) load_wtile(t + ND - 1, st == 0 ? ND - 1 : st - 1);
+      const int st1 = st == ND - 1 ? 0 : st + 1;
+      // next K-tile's X: same tap at cc+1, or the next tap's first (the
+      // final iteration re-reads a valid tile, unused)
+      if (cc + 1 == CT && tap + 1 < 9) set_tap(tap + 1);
+      const int cn = cc + 1 == CT ? 0 : cc + 1;
+      bf16x8 wn[NF];
+      wread(wn, st1);
+      // everything but the two weight reads just issued: the X fragments (read
+      // during the previous K-tile) have landed. One wait instead of the
+      // compiler's one per fragment.
+      __builtin_amdgcn_s_waitcnt(0xC07F | (NF << 8));
 #pragma unroll
       for (int f = 0; f < MF; ++f) {
-        const int ch = cbase ^ ((key[f] + kw) & 15);
-        const bf16x8 xf = *(const bf16x8*)(xs + xoff[f] + toff + (ch << 4));
 #pragma unroll
         for (int nf = 0; nf < NF; ++nf)
-          acc[f][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[nf], xf, acc[f][nf], 0, 0, 0);
+          acc[f][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[nf], xf[f], acc[f][nf], 0, 0, 0);
+        xf[f] = xread(f, cn);
       }
+      __builtin_amdgcn_sched_group_barrier(0x100, NF, 0);
+#pragma unroll
+      for (int f = 0; f < MF; ++f) {
+        __builtin_amdgcn_sched_group_barrier(0x008, NF, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+#pragma unroll
+      for (int nf = 0; nf < NF; ++nf) wf[nf] = wn[nf];
+      st = st1;
     }
   }
 
-  // ---- epilogue: lane holds channels WN*wn + 32j + 8fq .. +7 of its pixel
-  const long base = ((long)b * H + r0) * W * C + WN * wn + 8 * fq;
+  unsigned long long t_loop = 0;
+  if (a.stamps) {
+    t_loop = __builtin_amdgcn_s_memrealtime();
+    asm volatile("" ::"s"(t_loop));
+  }
+  // ---- epilogue: lane holds channels wc*32 + 8fq .. +7 of its pixel. All
+  // residual loads are issued first (the operand registers are free now):
+  // loaded one per fragment, each waited on before its store, they cost
+  // 4-5 us per workgroup.
+  const long base = ((long)b * H + r0) * W * C + wc * WN + 8 * fq;
+  float bs[8];
 #pragma unroll
-  for (int f = 0; f < MF; ++f) {
-    const int p = 16 * (mh * MF + f) + fr;
-    if (p >= NPIX) continue;
+  for (int e = 0; e < 8; ++e) bs[e] = a.bias[wc * WN + 8 * fq + e];
+  uint4 rv[MF];
+  if (a.res) {
 #pragma unroll
-    for (int j = 0; j < NF / 2; ++j) {
-      const long off = base + (long)p * C + 32 * j;
-      float v[8];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        v[e] = acc[f][2 * j][e] + bs[j][e];
-        v[4 + e] = acc[f][2 * j + 1][e] + bs[j][4 + e];
-      }
-      if (a.res) {
-        float r[8];
-        unpack8(*(const uint4*)(a.res + off), r);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] += r[e];
-      }
-      if (a.relu) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
-      }
-      *(uint4*)(a.y + off) = pack8(v);
+    for (int f = 0; f < MF; ++f) {
+      const int p = min(16 * (wm * MF + f) + fr, NPIX - 1);
+      rv[f] = *(const uint4*)(a.res + base + (long)p * C);
     }
   }
+#pragma unroll
+  for (int f = 0; f < MF; ++f) {
+    const int p = 16 * (wm * MF + f) + fr;
+    if (p >= NPIX) continue;
+    const long off = base + (long)p * C;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v[e] = acc[f][0][e] + bs[e];
+      v[4 + e] = acc[f][1][e] + bs[4 + e];
+    }
+    if (a.res) {
+      float r[8];
+      unpack8(rv[f], r);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += r[e];
+    }
+    if (relu) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+    }
+    *(uint4*)(a.y + off) = pack8(v);
+  }
+  if (a.stamps && tid == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    unsigned long long* sp = a.stamps + blockIdx.x * 4;
+    sp[0] = t_start;
+    sp[1] = t_first;
+    sp[2] = t_loop;
+    sp[3] = __builtin_amdgcn_s_memrealtime();
+  }
+}
+
+template <int H, int W, int C, int HS, int WM>
+void launch_stream(const StreamConvArgs& a, int grid, hipStream_t s) {
+  constexpr size_t lds = StreamGeom<H, W, C, HS, 3>::LDS;
+  static_assert(lds <= 160 * 1024, "LDS budget");
+  hipLaunchKernelGGL((conv3x3_stream_kernel<H, W, C, HS, WM, 3>), dim3(grid), dim3(512), lds, s, a);
 }
 
 }  // namespace
@@ -231,7 +352,7 @@ bool conv3x3_stream_supported(int H, int W, int Cin, int Cout) {
 }
 
 void conv3x3_stream(const void* x, const void* w, const float* bias, const void* res, void* y, const void* zero,
-                    int B, int H, int W, int C, bool relu, hipStream_t s) {
+                    int B, int H, int W, int C, bool relu, hipStream_t s, unsigned long long* stamps) {
   if (B <= 0) return;
   if (!conv3x3_stream_supported(H, W, C, C)) throw std::invalid_argument("conv3x3_stream: unsupported shape");
   if (!x || !w || !bias || !y || !zero ||
@@ -245,13 +366,11 @@ void conv3x3_stream(const void* x, const void* w, const float* bias, const void*
   a.y = (bf16*)y;
   a.zero = (const bf16*)zero;
   a.relu = relu;
-  if (C == 128) {  // layer2: half an image per workgroup (16 x 30 x 256 B rows + 2 x 16 KB weight stages)
-    const size_t lds = (size_t)(14 + 2) * (28 + 2) * 128 * 2 + (size_t)2 * 128 * 64 * 2;
-    hipLaunchKernelGGL((conv3x3_stream_kernel<28, 28, 128, 14, 64>), dim3(2 * B), dim3(512), lds, s, a);
-  } else {  // layer3: a whole image per workgroup (16 x 16 x 512 B rows + 2 x 16 KB weight stages = 160 KB)
-    const size_t lds = (size_t)(14 + 2) * (14 + 2) * 256 * 2 + (size_t)2 * 256 * 32 * 2;
-    hipLaunchKernelGGL((conv3x3_stream_kernel<14, 14, 256, 14, 32>), dim3(B), dim3(512), lds, s, a);
-  }
+  a.stamps = stamps;
+  if (C == 128)  // layer2: half an image per workgroup (15 x 28 x 256 B = 105 KB) + 8 x 3 x 2 KB weight stages
+    launch_stream<28, 28, 128, 14, 2>(a, 2 * B, s);
+  else  // layer3: a whole image per workgroup (14 x 14 x 512 B = 98 KB) + 8 x 3 x 2 KB weight stages
+    launch_stream<14, 14, 256, 14, 1>(a, B, s);
   DMLC_HIP_CHECK(hipGetLastError());
 }
 

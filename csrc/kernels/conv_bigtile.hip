@@ -137,7 +137,14 @@ __global__ __launch_bounds__(512, 1) void conv_bt_kernel(ConvArgs a, int k_tiles
 
   // debug (DMLC_BT_DEBUG & 32): per-workgroup phase stamps (100 MHz clock) into a.ws
   unsigned long long* stamps = (dbg & 32) && a.ws ? (unsigned long long*)a.ws + blockIdx.x * 4 : nullptr;
-  const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+  // (a stamp consumed only at the end would stay a pending scalar-memory op
+  // through the K loop: it shares lgkmcnt with the LDS reads and completes out
+  // of order, which turns every counted LDS wait into lgkmcnt(0))
+  unsigned long long t_start = 0;
+  if (stamps) {
+    t_start = __builtin_amdgcn_s_memrealtime();
+    asm volatile("" ::"s"(t_start));
+  }
   int tile, slice;
   if (!bt_unit(blockIdx.x, tiles, splits, tile, slice)) return;
   tile = __builtin_amdgcn_readfirstlane(tile);  // provably uniform: scalar buffer descriptors, no waterfall loops
@@ -281,7 +288,10 @@ __global__ __launch_bounds__(512, 1) void conv_bt_kernel(ConvArgs a, int k_tiles
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (stamps && t == k0) t_first = __builtin_amdgcn_s_memrealtime();
+    if (stamps && t == k0) {
+      t_first = __builtin_amdgcn_s_memrealtime();
+      asm volatile("" ::"s"(t_first));
+    }
     const int tn = t + D;
     const bool valid = tn < k1 && !(dbg & 1);
     const int tap = tn / ctiles, c0 = (tn - tap * ctiles) * BK, kh = tap / a.KW, kw = tap - kh * a.KW;

@@ -132,7 +132,7 @@ void conv3x3_rows(const void* x, const void* w, const float* bias, const void* r
 // layouts as conv2d_igemm.
 bool conv3x3_stream_supported(int H, int W, int Cin, int Cout);
 void conv3x3_stream(const void* x, const void* w, const float* bias, const void* res, void* y, const void* zero,
-                    int B, int H, int W, int C, bool relu, hipStream_t s);
+                    int B, int H, int W, int C, bool relu, hipStream_t s, unsigned long long* stamps = nullptr);
 int stem_pool_pick_strip(int B, int PH, int num_cus);
 void stem_conv_pool(const void* x, const void* w, const float* bias, void* y, int B, int S, int Wq, int strip,
                     hipStream_t s);

@@ -186,9 +186,15 @@ def conv3x3_stream(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, 
     if not C.conv3x3_stream_supported(H, W, Cin, w_packed.shape[0]):
         raise ValueError("conv3x3_stream: unsupported shape")
     y = torch.empty_like(x)
+    stamps = 0
+    if int(os.environ.get("DMLC_BT_DEBUG", "0")) & 32:  # per-workgroup phase stamps (debug)
+        global BT_STAMPS
+        if BT_STAMPS is None:
+            BT_STAMPS = torch.zeros(1 << 16, dtype=torch.int64, device=x.device)
+        stamps = _ptr(BT_STAMPS)
     C.conv3x3_stream(_ptr(x.contiguous()), _ptr(w_packed.contiguous()), _ptr(bias.float().contiguous()),
                      _ptr(None if res is None else res.contiguous()), _ptr(y), _ptr(_zero_page(x.device)), B, H, W,
-                     Cin, relu, _stream())
+                     Cin, relu, _stream(), stamps)
     return y
 
 

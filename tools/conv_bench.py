@@ -124,6 +124,9 @@ def main():
                 f = lambda: ops.conv3x3_stream(x, wp, bias, r, True)
                 us = time_us(f, a.iters)
                 row.append(f"stream{'+res' if use_res else ''}={us:7.1f}us {flops/us/1e6:6.0f}TF")
+                if ops.BT_STAMPS is not None:
+                    f()
+                    row.append(_stamps())
         if name == "l1":  # direct row-streaming conv (conv3x3_rows.hip)
             for use_res in (False, True):
                 r = torch.randn(B, H, W, Cout, device=dev).bfloat16() if use_res else None
