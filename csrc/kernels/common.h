@@ -37,6 +37,33 @@ __device__ __forceinline__ uint4 pack8(const float* f) {
   return make_uint4(pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]), pack2(f[6], f[7]));
 }
 
+// 16-B-per-lane LDS-DMA (global_load_lds_dwordx4: lane l's 16 bytes land at
+// lds + 16 l; lds must be wave-uniform), issued as inline asm. With
+// __builtin_amdgcn_global_load_lds in flight the compiler's waitcnt pass
+// turns every wait on an LDS read into lgkmcnt(0), so a kernel that keeps
+// DMA in flight under its MFMAs lost the counted waits that let MFMAs start
+// on the first operands to land. The pass does not see these, so every vmcnt
+// wait they need is the kernel's own (s_waitcnt vmcnt asm). Compiler-visible
+// global loads may still be mixed in: vmcnt retires in issue order, so the
+// compiler's counted waits stay correct (they can only wait longer).
+__device__ __forceinline__ void dma16(const void* gsrc, const void* lds) {
+  const uint32_t l =
+      __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)lds);
+  asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(l), "v"(gsrc) : "memory", "m0");
+}
+// 4-B-per-lane form (global_load_lds_dword: lane l's 4 bytes land at lds + 4 l).
+__device__ __forceinline__ void dma4(const void* gsrc, const void* lds) {
+  const uint32_t l =
+      __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)lds);
+  asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dword %1, off" ::"s"(l), "v"(gsrc) : "memory", "m0");
+}
+// Same with a scalar base (saddr form): lane l loads base + voff[l].
+__device__ __forceinline__ void dma16s(const void* sbase, uint32_t voff, const void* lds) {
+  const uint32_t l =
+      __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)lds);
+  asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, %2" ::"s"(l), "v"(voff), "s"(sbase) : "memory", "m0");
+}
+
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));

@@ -31,9 +31,6 @@ namespace dmlc {
 
 namespace {
 
-typedef __attribute__((address_space(3))) void* lds_ptr_t;
-typedef const __attribute__((address_space(1))) void* gbl_ptr_t;
-
 template <int N>
 __device__ __forceinline__ void vm_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
@@ -92,7 +89,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3_rows_kernel(RowConvArgs a) {
     const int i = j * 256 + tid;
     const int c2 = i & 3, n = (i >> 2) % C, ks = i / (4 * C);
     const bf16* src = a.w + (long)perm(n) * (9 * C) + ks * 32 + 8 * (c2 ^ wswz(n));
-    __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)(wl + (j * 256 + wave * 64) * 16), 16, 0, 0);
+    dma16(src, (wl + (j * 256 + wave * 64) * 16));
   }
 
   // ---- one input row (r may be -1 or H: zero row) -> ring slot
@@ -106,7 +103,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3_rows_kernel(RowConvArgs a) {
       const bool ok = inside && q >= 1 && q <= W;
       const bf16* src = ok ? img + ((long)r * W + (q - 1)) * C + 8 * (c2 ^ (q & 7)) : a.zero;
       if (i < ROW_CH)
-        __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)(dst + c0 * 16), 16, 0, 0);
+        dma16(src, (dst + c0 * 16));
     }
   };
   // Rows [lo, lo+n) spread over the 4 waves (each row = ROW_CH/64 instructions).

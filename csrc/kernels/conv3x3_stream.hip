@@ -38,24 +38,6 @@ namespace dmlc {
 
 namespace {
 
-// 16-B-per-lane LDS-DMA (lane l's 16 bytes land at lds + 16 l), issued as
-// inline asm: with __builtin_amdgcn_global_load_lds in flight the compiler's
-// waitcnt pass turns every LDS-read wait into lgkmcnt(0), which serialised
-// the pipelined K loop on its newest reads. The pass does not see these, so
-// every vmcnt wait on them is explicit (vm_wait), and no compiler-visible
-// memory op is in flight with them except the epilogue's, issued after the
-// last wait.
-__device__ __forceinline__ void dma16(const void* gsrc, const void* lds) {
-  const uint32_t l = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)lds);
-  asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(l), "v"(gsrc) : "memory", "m0");
-}
-
-// Same with a scalar base (saddr form): lane l loads base + voff[l].
-__device__ __forceinline__ void dma16s(const void* sbase, uint32_t voff, const void* lds) {
-  const uint32_t l = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)lds);
-  asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, %2" ::"s"(l), "v"(voff), "s"(sbase) : "memory", "m0");
-}
-
 template <int N>
 __device__ __forceinline__ void vm_wait() {
   static_assert(N >= 0 && N < 64, "vmcnt range");

@@ -47,8 +47,6 @@ namespace dmlc {
 
 namespace {
 
-typedef __attribute__((address_space(3))) void* lds_ptr_t;
-typedef const __attribute__((address_space(1))) void* gbl_ptr_t;
 typedef unsigned short ushort8 __attribute__((ext_vector_type(8)));
 typedef float float2v __attribute__((ext_vector_type(2)));
 typedef short short2v __attribute__((ext_vector_type(2)));
@@ -141,14 +139,13 @@ __global__ __launch_bounds__(256, 2) void stem_conv_pool_kernel(
         char* dst = u8ring + (r % RING) * UB;
         for (int c0 = 0; c0 < UB / 4; c0 += 64)
           if (c0 + lane < UB / 4)
-            __builtin_amdgcn_global_load_lds((gbl_ptr_t)(src + (c0 + lane) * 4), (lds_ptr_t)(dst + c0 * 4), 4, 0, 0);
+            dma4(src + (c0 + lane) * 4, dst + c0 * 4);
       } else {
         const bf16* src = img + (long)r * a.Wq * 8;
         char* dst = ring + (r % RING) * RB;
         for (int c0 = 0; c0 < a.Wq; c0 += 64) {
           if (c0 + lane < a.Wq)
-            __builtin_amdgcn_global_load_lds((gbl_ptr_t)(src + (c0 + lane) * 8), (lds_ptr_t)(dst + c0 * 16), 16, 0,
-                                             0);
+            dma16(src + (c0 + lane) * 8, dst + c0 * 16);
         }
       }
     }
