@@ -51,6 +51,7 @@ struct StreamConvArgs {
   const bf16* res;    // [B, H, W, C] or null
   bf16* y;            // [B, H, W, C]
   const bf16* zero;   // >= 16 zero bytes
+  int B;
   int relu;
   unsigned long long* stamps;  // debug: per-workgroup phase stamps (100 MHz), or null
 };
@@ -69,11 +70,14 @@ __device__ __forceinline__ int perm32(int n) {
 // reads chunk fq of row 16nf + fr).
 __device__ __forceinline__ int wswz(int n, int c) { return c ^ (3 * ((n >> 2) & 1)); }
 
-// Geometry shared by the kernel and its launcher.
-template <int H, int W, int C, int HS, int ND>
+// Geometry shared by the kernel and its launcher: a workgroup owns HS output
+// rows of one image (PARTS = H / HS > 1), or IMG whole images (PARTS == 1),
+// and C / NSP of the output channels.
+template <int H, int W, int C, int HS, int IMG, int ND>
 struct StreamGeom {
   static constexpr int PARTS = H / HS;
-  static constexpr int XR = PARTS == 1 ? H : PARTS == 2 ? HS + 1 : HS + 2;  // max staged rows
+  static_assert(PARTS == 1 || IMG == 1, "several images per workgroup only as whole images");
+  static constexpr int XR = PARTS == 1 ? IMG * H : PARTS == 2 ? HS + 1 : HS + 2;  // max staged rows
   static constexpr int PXB = C * 2;                    // bytes per pixel
   static constexpr int ROWB = W * PXB;                 // bytes per staged row
   static constexpr int ZB = XR * ROWB;                 // zero pixel
@@ -82,12 +86,13 @@ struct StreamGeom {
   static constexpr size_t LDS = (size_t)XBYTES + (size_t)8 * ND * WST;
 };
 
-// One workgroup = HS output rows x W columns of one image, all C channels.
-template <int H, int W, int C, int HS, int WM, int ND>
+// One workgroup = HS output rows x W columns of one image (or IMG images),
+// C / NSP output channels.
+template <int H, int W, int C, int HS, int IMG, int NSP, int WM, int ND>
 __global__ __launch_bounds__(512, 1) void conv3x3_stream_kernel(StreamConvArgs a) {
-  using G = StreamGeom<H, W, C, HS, ND>;
+  using G = StreamGeom<H, W, C, HS, IMG, ND>;
   constexpr int BK = 32;                     // K-tile depth = one MFMA k-step
-  constexpr int NPIX = HS * W;               // output pixels per workgroup
+  constexpr int NPIX = IMG * HS * W;         // output pixels per workgroup (the last group may have fewer)
   constexpr int MFT = (NPIX + 15) / 16;      // pixel fragments (the last one partly padding)
   constexpr int MF = (MFT + WM - 1) / WM;    // per wave
   constexpr int WN = 32;                     // channels per wave
@@ -98,7 +103,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream_kernel(StreamConvArgs a
   constexpr int KT = 9 * C / BK;             // K-tiles
   constexpr int CT = C / BK;                 // K-tiles per tap
   constexpr int GW = WST / 1024;             // weight DMA instructions per wave per K-tile
-  static_assert(C == 8 / WM * WN && W * CPX % 64 == 0 && H % HS == 0 && PXB >= 256, "geometry");
+  static_assert(C == 8 / WM * WN * NSP && W * CPX % 64 == 0 && H % HS == 0 && PXB >= 256, "geometry");
   static_assert(ND == 3 && KT >= ND, "the loop's waits assume a 3-stage ring");
   static_assert(MF + NF <= 15, "lgkmcnt range of the pipelined loop");
 
@@ -111,9 +116,16 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream_kernel(StreamConvArgs a
   const int fr = lane & 15, fq = lane >> 4;
   const char* wpriv = xs + G::XBYTES + wave * (ND * WST);
   constexpr int PARTS = G::PARTS;
-  const int b = blockIdx.x / PARTS, part = blockIdx.x - b * PARTS;
+  // channel split fastest: the XCDs (blocks are dealt to them round-robin)
+  // each hold one split's weight rows in their L2
+  const int ns = blockIdx.x % NSP, rest = blockIdx.x / NSP;
+  const int bg = rest / PARTS, part = rest - bg * PARTS;
+  const int b = bg * IMG, nimg = min(IMG, a.B - b);         // first image, images here
   const int r0 = part * HS;                                 // first output row
-  const int rs = max(r0 - 1, 0), nrows = min(r0 + HS, H - 1) - rs + 1;  // staged input rows
+  const int rs = PARTS == 1 ? 0 : max(r0 - 1, 0);
+  const int nrows = PARTS == 1 ? nimg * H : min(r0 + HS, H - 1) - rs + 1;  // staged input rows
+  const int npix = IMG == 1 ? NPIX : nimg * HS * W;
+  const int ch0 = ns * (C / NSP) + wc * WN;                 // this wave's first output channel
   const bf16* img = a.x + (long)b * H * W * C;
   // A scalar memory op still pending in the loop (a debug stamp, or a kernel
   // argument whose s_load the compiler hoists into the loop's preheader) shares
@@ -157,7 +169,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream_kernel(StreamConvArgs a
 #pragma unroll
   for (int g = 0; g < GW; ++g) {
     const int ci = g * 64 + lane, n = ci >> 2, pc = ci & 3;
-    woff[g] = (uint32_t)(((wc * WN + perm32(n)) * (9 * C) + 8 * wswz(n, pc)) * 2);
+    woff[g] = (uint32_t)(((ch0 + perm32(n)) * (9 * C) + 8 * wswz(n, pc)) * 2);
   }
   const bf16* wbase = a.w;
   auto load_wtile = [&](int t, int st) __attribute__((always_inline)) {
@@ -174,12 +186,13 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream_kernel(StreamConvArgs a
   // tap for all fragments (clamped lanes read a permuted chunk of their
   // clamped pixel: in bounds, never stored). The low 4 bits of xoff flag the
   // image's first/last row and column, whose outside taps read the zero pixel.
+  // Several images are staged back to back, so keys stay consecutive.
   int xoff[MF];
 #pragma unroll
   for (int f = 0; f < MF; ++f) {
-    const int p = min(16 * (wm * MF + f) + fr, NPIX - 1);
-    const int prow = p / W, pcol = p - prow * W, r = r0 + prow;
-    xoff[f] = ((r - rs) * W + pcol) * PXB | (r == 0 ? 1 : 0) | (r == H - 1 ? 2 : 0) | (pcol == 0 ? 4 : 0) |
+    const int p = min(16 * (wm * MF + f) + fr, npix - 1);
+    const int pi = p % (HS * W), prow = pi / W, pcol = pi - prow * W, r = r0 + prow;
+    xoff[f] = (p - pi + (r - rs) * W + pcol) * PXB | (r == 0 ? 1 : 0) | (r == H - 1 ? 2 : 0) | (pcol == 0 ? 4 : 0) |
               (pcol == W - 1 ? 8 : 0);
     asm volatile("" : "+v"(xoff[f]));  // keep it live: rematerialising p / W in the loop cost ~100 VALU per K-tile
   }
@@ -271,26 +284,26 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream_kernel(StreamConvArgs a
     t_loop = __builtin_amdgcn_s_memrealtime();
     asm volatile("" ::"s"(t_loop));
   }
-  // ---- epilogue: lane holds channels wc*32 + 8fq .. +7 of its pixel. All
+  // ---- epilogue: lane holds channels ch0 + 8fq .. +7 of its pixel. All
   // residual loads are issued first (the operand registers are free now):
   // loaded one per fragment, each waited on before its store, they cost
   // 4-5 us per workgroup.
-  const long base = ((long)b * H + r0) * W * C + wc * WN + 8 * fq;
+  const long base = ((long)b * H + r0) * W * C + ch0 + 8 * fq;
   float bs[8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) bs[e] = a.bias[wc * WN + 8 * fq + e];
+  for (int e = 0; e < 8; ++e) bs[e] = a.bias[ch0 + 8 * fq + e];
   uint4 rv[MF];
   if (a.res) {
 #pragma unroll
     for (int f = 0; f < MF; ++f) {
-      const int p = min(16 * (wm * MF + f) + fr, NPIX - 1);
+      const int p = min(16 * (wm * MF + f) + fr, npix - 1);
       rv[f] = *(const uint4*)(a.res + base + (long)p * C);
     }
   }
 #pragma unroll
   for (int f = 0; f < MF; ++f) {
     const int p = 16 * (wm * MF + f) + fr;
-    if (p >= NPIX) continue;
+    if (p >= npix) continue;
     const long off = base + (long)p * C;
     float v[8];
 #pragma unroll
@@ -320,17 +333,19 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream_kernel(StreamConvArgs a
   }
 }
 
-template <int H, int W, int C, int HS, int WM>
-void launch_stream(const StreamConvArgs& a, int grid, hipStream_t s) {
-  constexpr size_t lds = StreamGeom<H, W, C, HS, 3>::LDS;
+template <int H, int W, int C, int HS, int IMG, int NSP, int WM>
+void launch_stream(const StreamConvArgs& a, hipStream_t s) {
+  constexpr size_t lds = StreamGeom<H, W, C, HS, IMG, 3>::LDS;
   static_assert(lds <= 160 * 1024, "LDS budget");
-  hipLaunchKernelGGL((conv3x3_stream_kernel<H, W, C, HS, WM, 3>), dim3(grid), dim3(512), lds, s, a);
+  const int grid = (a.B + IMG - 1) / IMG * (H / HS) * NSP;
+  hipLaunchKernelGGL((conv3x3_stream_kernel<H, W, C, HS, IMG, NSP, WM, 3>), dim3(grid), dim3(512), lds, s, a);
 }
 
 }  // namespace
 
 bool conv3x3_stream_supported(int H, int W, int Cin, int Cout) {
-  return Cin == Cout && ((H == 28 && W == 28 && Cin == 128) || (H == 14 && W == 14 && Cin == 256));
+  return Cin == Cout && ((H == 28 && W == 28 && Cin == 128) || (H == 14 && W == 14 && Cin == 256) ||
+                         (H == 7 && W == 7 && Cin == 512));
 }
 
 void conv3x3_stream(const void* x, const void* w, const float* bias, const void* res, void* y, const void* zero,
@@ -347,12 +362,15 @@ void conv3x3_stream(const void* x, const void* w, const float* bias, const void*
   a.res = (const bf16*)res;
   a.y = (bf16*)y;
   a.zero = (const bf16*)zero;
+  a.B = B;
   a.relu = relu;
   a.stamps = stamps;
   if (C == 128)  // layer2: half an image per workgroup (15 x 28 x 256 B = 105 KB) + 8 x 3 x 2 KB weight stages
-    launch_stream<28, 28, 128, 14, 2>(a, 2 * B, s);
-  else  // layer3: a whole image per workgroup (14 x 14 x 512 B = 98 KB) + 8 x 3 x 2 KB weight stages
-    launch_stream<14, 14, 256, 14, 1>(a, B, s);
+    launch_stream<28, 28, 128, 14, 1, 1, 2>(a, s);
+  else if (C == 256)  // layer3: a whole image per workgroup (14 x 14 x 512 B = 98 KB) + 8 x 3 x 2 KB weight stages
+    launch_stream<14, 14, 256, 14, 1, 1, 1>(a, s);
+  else  // layer4: two whole images x half the output channels per workgroup (2 x 49 x 1 KB = 98 KB) + rings
+    launch_stream<7, 7, 512, 7, 2, 2, 1>(a, s);
   DMLC_HIP_CHECK(hipGetLastError());
 }
 

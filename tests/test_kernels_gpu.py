@@ -260,10 +260,12 @@ def test_stem_conv_pool_u8(gpu, B, S, strip):
 @pytest.mark.parametrize("HW,C,B,res,relu", [(28, 128, 1, False, True), (28, 128, 3, True, True),
                                              (28, 128, 2, True, False), (28, 128, 5, False, False),
                                              (14, 256, 1, False, True), (14, 256, 3, True, True),
-                                             (14, 256, 2, True, False)])
+                                             (14, 256, 2, True, False), (7, 512, 1, False, True),
+                                             (7, 512, 3, True, True), (7, 512, 4, True, False)])
 def test_conv3x3_stream(gpu, HW, C, B, res, relu):
     """Direct 3x3 conv with streamed weights (conv3x3_stream.hip: 28x28x128
-    half images, 14x14x256 whole images) vs torch fp32."""
+    half images, 14x14x256 whole images, 7x7x512 image pairs x half the
+    channels; odd B leaves a one-image group) vs torch fp32."""
     g = torch.Generator().manual_seed(21)
     x = torch.randn(B, C, HW, HW, generator=g).bfloat16().float()
     w = (torch.randn(C, C, 3, 3, generator=g) / (9 * C) ** 0.5).bfloat16().float()

@@ -118,7 +118,7 @@ def main():
                     row.append(_stamps())
             except Exception as e:  # noqa: BLE001
                 row.append(f"tile{t}=ERR({e})")
-        if name in ("l2", "l3"):  # direct conv with streamed weights (conv3x3_stream.hip)
+        if name in ("l2", "l3", "l4"):  # direct conv with streamed weights (conv3x3_stream.hip)
             for use_res in (False, True):
                 r = torch.randn(B, H, W, Cout, device=dev).bfloat16() if use_res else None
                 f = lambda: ops.conv3x3_stream(x, wp, bias, r, True)
