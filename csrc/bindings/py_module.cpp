@@ -159,13 +159,16 @@ PYBIND11_MODULE(_C, m) {
       py::arg("Wr"), py::arg("stream"), py::arg("paired") = false);
   m.attr("STEM_POOL_K") = kStemPoolK;
   m.def("stem_pool_pick_strip", &stem_pool_pick_strip);
-  m.def("conv3x3_stream_supported", &conv3x3_stream_supported);
+  m.def("conv3x3_stream_supported", &conv3x3_stream_supported, py::arg("Hin"), py::arg("Win"), py::arg("Cin"),
+        py::arg("Cout"), py::arg("stride") = 1);
   m.def("conv3x3_stream", [](uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t res, uintptr_t y, uintptr_t zero,
-                             int B, int H, int W, int C, bool relu, uintptr_t stream, uintptr_t stamps) {
-    conv3x3_stream(P<void>(x), P<void>(w), P<float>(bias), P<void>(res), P<void>(y), P<void>(zero), B, H, W, C, relu,
-                   S(stream), P<unsigned long long>(stamps));
+                             int B, int H, int W, int Cin, int Cout, int stride, bool relu, uintptr_t stream,
+                             uintptr_t stamps) {
+    conv3x3_stream(P<void>(x), P<void>(w), P<float>(bias), P<void>(res), P<void>(y), P<void>(zero), B, H, W, Cin, Cout,
+                   stride, relu, S(stream), P<unsigned long long>(stamps));
   }, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("res"), py::arg("y"), py::arg("zero"), py::arg("B"),
-        py::arg("H"), py::arg("W"), py::arg("C"), py::arg("relu"), py::arg("stream"), py::arg("stamps") = 0);
+        py::arg("H"), py::arg("W"), py::arg("Cin"), py::arg("Cout"), py::arg("stride"), py::arg("relu"),
+        py::arg("stream"), py::arg("stamps") = 0);
   m.def("conv3x3_rows_supported", &conv3x3_rows_supported);
   m.def("conv3x3_rows_pick_strip", &conv3x3_rows_pick_strip);
   m.def("conv3x3_rows", [](uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t res, uintptr_t y, uintptr_t zero,

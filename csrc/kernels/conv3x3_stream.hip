@@ -1,36 +1,37 @@
-// Direct 3x3 / stride 1 / pad 1 convolution with the input image resident in
-// LDS, for ResNet18 layer2 (28x28x128: layer2.0.conv2, layer2.1.conv{1,2}) and
-// layer3 (14x14x256: layer3.0.conv2, layer3.1.conv{1,2}), BN folded, optional
-// residual, ReLU.
+// Direct 3x3 / pad 1 convolution (stride 1 or 2) with the input image resident
+// in LDS, BN folded, optional residual, ReLU. ResNet18 at batch >= 32 runs
+// every 3x3 conv from layer2 on through it:
+//   stride 1: layer2 (28x28x128), layer3 (14x14x256), layer4 (7x7x512)
+//   stride 2: layer2.0.conv1 (56x56x64 -> 28x28x128), layer3.0.conv1 (28x28x128
+//             -> 14x14x256)
 //
 // Reference equivalent: those convs + bn + (residual) + relu of
 // tch::vision::resnet18, run per query by `forward_t` at src/services.rs:493.
 // As an implicit GEMM (conv_igemm.hip) every output tile re-fetches its 3x3
-// input window per tap: 9x the input bytes through L2, and in the model the
-// input is cold (written by the previous layer), so these convs ran at 113-128
-// us against 85 us on L2-hot inputs. Here one workgroup owns HS output rows of
-// one image (layer2: half an image, 392 pixels; layer3: the whole image, 196):
+// input window per tap (9x the input bytes through L2, from cold inputs in the
+// model) and small-N tiles re-fetch the weights per tile. Here a workgroup owns
+// HS output rows of one image (or IMG whole images) and C_out / NSP channels:
 //
 //  * Its input rows (the strip plus the halo rows inside the image) go HBM ->
 //    LDS once by LDS-DMA and stay resident; taps that fall outside the image
 //    read one zero pixel instead of staged zero padding. Chunks are XOR-
 //    swizzled per pixel (see the staging loop) so every fragment read is
-//    bank-conflict free and costs one VALU add.
-//  * The folded weights (C x 9C bf16, 295 KB / 1.2 MB, shared by every CU and
-//    L2-resident) stream through LDS in 32-deep K-tiles. Every wave streams
-//    just the 32 output-channel rows it uses through a private 3-stage LDS-DMA
-//    ring and waits only on its own vmcnt: the K loop has no workgroup
+//    bank-conflict free and costs one VALU add. Stride 2 stores each input row
+//    with its even columns first, then its odd ones.
+//  * The folded weights stream through LDS in 32-deep K-tiles. Every wave
+//    streams just the 32 output-channel rows it uses through a private 3-stage
+//    LDS-DMA ring and waits only on its own vmcnt: the K loop has no workgroup
 //    barrier. (With one shared ring the per-K-tile barrier, and the LDS read
 //    latency it exposed, held the loop at ~50% MFMA busy: without MFMAs the
 //    barrier/read skeleton alone took 35 of 60 us.)
 //  * 8 waves (2 per SIMD) = WM pixel groups x 8/WM channel groups of 32 (2 N
-//    fragments of 16), 13 pixel fragments each: layer2 WM=2 (its two pixel
-//    halves each stream the channel group's rows), layer3 WM=1. D = W x X. The
-//    weight rows are permuted when staged (row 16nf + r of a wave's tile holds
-//    channel 8(r>>2) + 4nf + (r&3) of its group), so a lane ends with 8
-//    consecutive output channels of one pixel: 16-B residual loads and stores.
+//    fragments of 16). D = W x X. The weight rows are permuted when staged (row
+//    16nf + r of a wave's tile holds channel 8(r>>2) + 4nf + (r&3) of its
+//    group), so a lane ends with 8 consecutive output channels of one pixel:
+//    16-B residual loads and stores.
 //  * The K loop is software-pipelined: the operands of K-tile t+1 are read
 //    while the MFMAs of t run.
+// Design history and measurements: profiles/r1_stream_conv.log.
 #include "common.h"
 #include "kernels.h"
 
@@ -45,11 +46,11 @@ __device__ __forceinline__ void vm_wait() {
 }
 
 struct StreamConvArgs {
-  const bf16* x;      // [B, H, W, C]
-  const bf16* w;      // [C, 9*C], k = (kh*3 + kw)*C + c
-  const float* bias;  // [C]
-  const bf16* res;    // [B, H, W, C] or null
-  bf16* y;            // [B, H, W, C]
+  const bf16* x;      // [B, S*H, S*W, CI]
+  const bf16* w;      // [CO, 9*CI], k = (kh*3 + kw)*CI + c
+  const float* bias;  // [CO]
+  const bf16* res;    // [B, H, W, CO] or null
+  bf16* y;            // [B, H, W, CO]
   const bf16* zero;   // >= 16 zero bytes
   int B;
   int relu;
@@ -70,40 +71,54 @@ __device__ __forceinline__ int perm32(int n) {
 // reads chunk fq of row 16nf + fr).
 __device__ __forceinline__ int wswz(int n, int c) { return c ^ (3 * ((n >> 2) & 1)); }
 
-// Geometry shared by the kernel and its launcher: a workgroup owns HS output
-// rows of one image (PARTS = H / HS > 1), or IMG whole images (PARTS == 1),
-// and C / NSP of the output channels.
-template <int H, int W, int C, int HS, int IMG, int ND>
+// Input chunk swizzle of a staged pixel with key K (see the staging loop).
+template <int CPX>
+__device__ __forceinline__ int xswz(int K) {
+  if constexpr (CPX >= 16)
+    return (K & 7) << 1;
+  else
+    return ((K >> 1) & 3) << 1;
+}
+
+// Geometry shared by the kernel and its launcher: output H x W, stride S, a
+// workgroup owns HS output rows of one image (PARTS = H / HS > 1) or IMG whole
+// images (PARTS == 1).
+template <int H, int W, int CI, int HS, int IMG, int S, int ND>
 struct StreamGeom {
   static constexpr int PARTS = H / HS;
   static_assert(PARTS == 1 || IMG == 1, "several images per workgroup only as whole images");
-  static constexpr int XR = PARTS == 1 ? IMG * H : PARTS == 2 ? HS + 1 : HS + 2;  // max staged rows
-  static constexpr int PXB = C * 2;                    // bytes per pixel
-  static constexpr int ROWB = W * PXB;                 // bytes per staged row
+  static constexpr int HI = S * H, WI = S * W;         // input rows / columns
+  // staged rows: the strip's S*(HS-1)+1 rows plus a halo row above and below,
+  // one of which is outside the image when a stride-1 image has two strips
+  static constexpr int XR = PARTS == 1                 ? IMG * HI
+                            : (S == 1 && PARTS == 2) ? HS + 1
+                            : (S * (HS - 1) + 3 < HI ? S * (HS - 1) + 3 : HI);
+  static constexpr int PXB = CI * 2;                   // bytes per input pixel
+  static constexpr int ROWB = WI * PXB;                // bytes per staged row
   static constexpr int ZB = XR * ROWB;                 // zero pixel
   static constexpr int XBYTES = ZB + PXB;              // input region
   static constexpr int WST = 32 * 32 * 2;              // a wave's weight stage: 32 rows x 32 k
   static constexpr size_t LDS = (size_t)XBYTES + (size_t)8 * ND * WST;
 };
 
-// One workgroup = HS output rows x W columns of one image (or IMG images),
-// C / NSP output channels.
-template <int H, int W, int C, int HS, int IMG, int NSP, int WM, int ND>
+template <int H, int W, int CI, int CO, int HS, int IMG, int NSP, int WM, int S, int ND>
 __global__ __launch_bounds__(512, 1) void conv3x3_stream_kernel(StreamConvArgs a) {
-  using G = StreamGeom<H, W, C, HS, IMG, ND>;
+  using G = StreamGeom<H, W, CI, HS, IMG, S, ND>;
   constexpr int BK = 32;                     // K-tile depth = one MFMA k-step
   constexpr int NPIX = IMG * HS * W;         // output pixels per workgroup (the last group may have fewer)
   constexpr int MFT = (NPIX + 15) / 16;      // pixel fragments (the last one partly padding)
   constexpr int MF = (MFT + WM - 1) / WM;    // per wave
   constexpr int WN = 32;                     // channels per wave
   constexpr int NF = 2;                      // N fragments per wave
+  constexpr int HI = G::HI, WI = G::WI;
   constexpr int PXB = G::PXB, ROWB = G::ROWB, ZB = G::ZB, WST = G::WST;
-  constexpr int CPX = C / 8;                 // 16-B chunks per pixel
-  constexpr int XI = W * CPX / 64;           // LDS-DMA instructions per input row
-  constexpr int KT = 9 * C / BK;             // K-tiles
-  constexpr int CT = C / BK;                 // K-tiles per tap
+  constexpr int CPX = CI / 8;                // 16-B chunks per input pixel
+  constexpr int XI = WI * CPX / 64;          // LDS-DMA instructions per input row
+  constexpr int KT = 9 * CI / BK;            // K-tiles
+  constexpr int CT = CI / BK;                // K-tiles per tap
   constexpr int GW = WST / 1024;             // weight DMA instructions per wave per K-tile
-  static_assert(C == 8 / WM * WN * NSP && W * CPX % 64 == 0 && H % HS == 0 && PXB >= 256, "geometry");
+  static_assert(CO == 8 / WM * WN * NSP && WI * CPX % 64 == 0 && H % HS == 0 && CPX >= 8, "geometry");
+  static_assert(S == 1 || (S == 2 && WI % 4 == 0 && HI % 2 == 0), "stride");
   static_assert(ND == 3 && KT >= ND, "the loop's waits assume a 3-stage ring");
   static_assert(MF + NF <= 15, "lgkmcnt range of the pipelined loop");
 
@@ -122,11 +137,11 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream_kernel(StreamConvArgs a
   const int bg = rest / PARTS, part = rest - bg * PARTS;
   const int b = bg * IMG, nimg = min(IMG, a.B - b);         // first image, images here
   const int r0 = part * HS;                                 // first output row
-  const int rs = PARTS == 1 ? 0 : max(r0 - 1, 0);
-  const int nrows = PARTS == 1 ? nimg * H : min(r0 + HS, H - 1) - rs + 1;  // staged input rows
+  const int rs = PARTS == 1 ? 0 : max(S * r0 - 1, 0);       // first staged input row
+  const int nrows = PARTS == 1 ? nimg * HI : min(S * (r0 + HS - 1) + 1, HI - 1) - rs + 1;
   const int npix = IMG == 1 ? NPIX : nimg * HS * W;
-  const int ch0 = ns * (C / NSP) + wc * WN;                 // this wave's first output channel
-  const bf16* img = a.x + (long)b * H * W * C;
+  const int ch0 = ns * (CO / NSP) + wc * WN;                // this wave's first output channel
+  const bf16* img = a.x + (long)b * HI * WI * CI;
   // A scalar memory op still pending in the loop (a debug stamp, or a kernel
   // argument whose s_load the compiler hoists into the loop's preheader) shares
   // lgkmcnt with the LDS reads and completes out of order, which turns every
@@ -139,26 +154,40 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream_kernel(StreamConvArgs a
     asm volatile("" ::"s"(t_start));
   }
 
-  // ---- input rows rs .. rs+nrows-1. Staged pixel (i, q) has key K = i*W + q,
-  // which for output pixel p at tap (kh, kw) is p + const: consecutive along a
-  // fragment even where it wraps an output row. Chunk c sits at physical chunk
-  // c ^ ((K & 7) << 1). A ds_read_b128 16-lane group holds fragment pixels
-  // 0-3,12-15 at k-group g and 4-11 at g^1 (g even): pixels j and j+8 (one of
-  // each set) share the pair index (c>>1) ^ (K&7) and differ in the low bit,
-  // and the 8 pair indices are distinct: all 16 bank slots for any fragment
-  // offset. (The first layout, padded column & 15 under an XOR, collided
-  // whenever a fragment started at an odd key or wrapped a row: 39% of LDS
-  // cycles were bank conflicts.) A read is one VALU add off a per-tap base.
-  // (Pixels padded by 32 B put chunk c of key K in slot (2K + c) mod 16,
-  // also conflict-free and with reads at immediate offsets, but the fully
-  // unrolled loop that needs spilled registers.) Instruction k = row*XI + j
-  // goes to wave k % 8.
+  // ---- input rows rs .. rs+nrows-1 (several images back to back when
+  // PARTS == 1). Staged pixel = input (y, x) of the workgroup's image i; its
+  // key K is chosen so that for output pixel p at tap (kh, kw) it is p + a tap
+  // constant: consecutive along a fragment even where it wraps an output row.
+  //   stride 1: K = (staged row)*W + x;
+  //   stride 2: K = i*H*W + (((y+1)>>1) - r0)*W + ((x+1)>>1)
+  //             ((y+1)>>1 is the output row for kh 0/1 and one less for kh 2).
+  // Chunk c sits at physical chunk c ^ xswz(K). A ds_read_b128 16-lane group
+  // holds fragment pixels 0-3,12-15 at k-group g and 4-11 at g^1 (g even):
+  //  * pixels of >= 256 B fill a whole 64-bank window; with xswz = (K&7)<<1
+  //    pixels j and j+8 (one of each set) share the pair index (c>>1)^(K&7)
+  //    and differ in the low bit, and the 8 pair indices are distinct;
+  //  * 128-B pixels (64 channels) take the window half given by the pixel's
+  //    parity, which follows K's parity along a fragment (stride 2 stores each
+  //    row's even columns first: consecutive outputs read alternating halves);
+  //    within a half xswz = ((K>>1)&3)<<1 does the same pairing.
+  // All 16 bank slots for any fragment offset. (The first layout, padded
+  // column & 15 under an XOR, collided whenever a fragment started at an odd
+  // key or wrapped a row: 39% of LDS cycles were bank conflicts.)
+  // Instruction k = row*XI + j goes to wave k % 8.
   for (int k = wave; k < nrows * XI; k += 8) {
     const int i = k / XI, j = k - i * XI;
     const int ci = j * 64 + lane;  // chunk of the staged row
-    const int q = ci / CPX, pp = ci - q * CPX;
-    const int pc = pp ^ (((i * W + q) & 7) << 1);  // logical chunk at physical pp
-    dma16(img + ((long)(rs + i) * W + q) * C + 8 * pc, xs + i * ROWB + j * 1024);
+    const int q = ci / CPX, pp = ci - q * CPX;  // physical column, chunk
+    const int x = S == 1 ? q : (q < WI / 2 ? 2 * q : 2 * (q - WI / 2) + 1);
+    int K;
+    if constexpr (S == 1) {
+      K = i * W + x;
+    } else {
+      const int ii = PARTS == 1 ? i / HI : 0, y = PARTS == 1 ? i - ii * HI : rs + i;
+      K = ii * (H * W) + (((y + 1) >> 1) - r0) * W + ((x + 1) >> 1);
+    }
+    const int pc = pp ^ xswz<CPX>(K);  // logical chunk at physical pp
+    dma16(img + ((long)(rs + i) * WI + x) * CI + 8 * pc, xs + i * ROWB + j * 1024);
   }
   if (wave == 0 && lane < CPX) dma16(a.zero, xs + ZB);
 
@@ -169,7 +198,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream_kernel(StreamConvArgs a
 #pragma unroll
   for (int g = 0; g < GW; ++g) {
     const int ci = g * 64 + lane, n = ci >> 2, pc = ci & 3;
-    woff[g] = (uint32_t)(((ch0 + perm32(n)) * (9 * C) + 8 * wswz(n, pc)) * 2);
+    woff[g] = (uint32_t)(((ch0 + perm32(n)) * (9 * CI) + 8 * wswz(n, pc)) * 2);
   }
   const bf16* wbase = a.w;
   auto load_wtile = [&](int t, int st) __attribute__((always_inline)) {
@@ -181,19 +210,17 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream_kernel(StreamConvArgs a
 
   // ---- per-lane constants: pixel p = 16(wm*MF + f) + fr (clamped for padding
   // lanes / a dummy last fragment: they compute a duplicate, never stored).
-  // The swizzle term ((p + const) & 7) << 5 has p & 7 == fr & 7 for every real
-  // pixel (fragments start at multiples of 16), so it is one lane value per
-  // tap for all fragments (clamped lanes read a permuted chunk of their
-  // clamped pixel: in bounds, never stored). The low 4 bits of xoff flag the
-  // image's first/last row and column, whose outside taps read the zero pixel.
-  // Several images are staged back to back, so keys stay consecutive.
+  // xoff = the staged offset of the tap-(1,1) input pixel; its low 4 bits flag
+  // the image's first/last row and column, whose outside taps read the zero
+  // pixel (stride 2 never leaves the image at the bottom or right).
   int xoff[MF];
 #pragma unroll
   for (int f = 0; f < MF; ++f) {
     const int p = min(16 * (wm * MF + f) + fr, npix - 1);
-    const int pi = p % (HS * W), prow = pi / W, pcol = pi - prow * W, r = r0 + prow;
-    xoff[f] = (p - pi + (r - rs) * W + pcol) * PXB | (r == 0 ? 1 : 0) | (r == H - 1 ? 2 : 0) | (pcol == 0 ? 4 : 0) |
-              (pcol == W - 1 ? 8 : 0);
+    const int pi = p % (HS * W), ii = p / (HS * W), prow = pi / W, pcol = pi - prow * W, r = r0 + prow;
+    const int row = ii * HI + S * r - rs;  // (stride 2: even input column 2 pcol sits at slot pcol)
+    xoff[f] = (row * WI + pcol) * PXB | (r == 0 ? 1 : 0) | (S == 1 && r == H - 1 ? 2 : 0) | (pcol == 0 ? 4 : 0) |
+              (S == 1 && pcol == W - 1 ? 8 : 0);
     asm volatile("" : "+v"(xoff[f]));  // keep it live: rematerialising p / W in the loop cost ~100 VALU per K-tile
   }
   floatx4 acc[MF][NF];
@@ -202,16 +229,23 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream_kernel(StreamConvArgs a
 #pragma unroll
     for (int nf = 0; nf < NF; ++nf) acc[f][nf] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  // per-tap fragment bases xa[f] and lane swizzle tsw = 16 fq ^ ((K & 7) << 5)
-  const int key = 32 * ((fr + (r0 - rs) * W) & 7);
+  // per-tap fragment bases xa[f] and lane swizzle tsw = 16 fq ^ 16 xswz(K):
+  // K = p + ktap with p & 15 == fr for every real pixel (fragments start at
+  // multiples of 16), so it is one lane value per tap for all fragments
+  // (clamped lanes read a permuted chunk of their clamped pixel: in bounds,
+  // never stored)
+  const int kbase = fr + (S == 1 ? (r0 - rs) * W : 0);
   int xa[MF], tsw = 0;
   auto set_tap = [&](int tap) __attribute__((always_inline)) {
     const int kh = tap / 3, kw = tap - kh * 3;
     const int tm = (kh == 0 ? 1 : 0) | (kh == 2 ? 2 : 0) | (kw == 0 ? 4 : 0) | (kw == 2 ? 8 : 0);
-    const int toff = ((kh - 1) * W + (kw - 1)) * PXB;
+    // staged column offset of tap column kw (stride 2: odd columns start at WI/2)
+    const int dq = S == 1 ? kw - 1 : (kw == 0 ? WI / 2 - 1 : kw == 1 ? 0 : WI / 2);
+    const int toff = ((kh - 1) * WI + dq) * PXB;
 #pragma unroll
     for (int f = 0; f < MF; ++f) xa[f] = (xoff[f] & tm) ? ZB : (xoff[f] & ~15) + toff;
-    tsw = (fq << 4) ^ ((key + 32 * ((kh - 1) * W + kw - 1)) & 0xE0);
+    const int ktap = S == 1 ? (kh - 1) * W + kw - 1 : (kh == 2 ? W : 0) + (kw == 2 ? 1 : 0);
+    tsw = (fq << 4) ^ (xswz<CPX>(kbase + ktap) << 4);
   };
   const uint32_t wlane = fr * (BK * 2) + (wswz(fr, fq) << 4);
   auto wread = [&](bf16x8* wf, int st) __attribute__((always_inline)) {
@@ -288,7 +322,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream_kernel(StreamConvArgs a
   // residual loads are issued first (the operand registers are free now):
   // loaded one per fragment, each waited on before its store, they cost
   // 4-5 us per workgroup.
-  const long base = ((long)b * H + r0) * W * C + ch0 + 8 * fq;
+  const long base = ((long)b * H + r0) * W * CO + ch0 + 8 * fq;
   float bs[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) bs[e] = a.bias[ch0 + 8 * fq + e];
@@ -297,14 +331,14 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream_kernel(StreamConvArgs a
 #pragma unroll
     for (int f = 0; f < MF; ++f) {
       const int p = min(16 * (wm * MF + f) + fr, npix - 1);
-      rv[f] = *(const uint4*)(a.res + base + (long)p * C);
+      rv[f] = *(const uint4*)(a.res + base + (long)p * CO);
     }
   }
 #pragma unroll
   for (int f = 0; f < MF; ++f) {
     const int p = 16 * (wm * MF + f) + fr;
     if (p >= npix) continue;
-    const long off = base + (long)p * C;
+    const long off = base + (long)p * CO;
     float v[8];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -333,25 +367,32 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream_kernel(StreamConvArgs a
   }
 }
 
-template <int H, int W, int C, int HS, int IMG, int NSP, int WM>
+template <int H, int W, int CI, int CO, int HS, int IMG, int NSP, int WM, int S>
 void launch_stream(const StreamConvArgs& a, hipStream_t s) {
-  constexpr size_t lds = StreamGeom<H, W, C, HS, IMG, 3>::LDS;
+  constexpr size_t lds = StreamGeom<H, W, CI, HS, IMG, S, 3>::LDS;
   static_assert(lds <= 160 * 1024, "LDS budget");
   const int grid = (a.B + IMG - 1) / IMG * (H / HS) * NSP;
-  hipLaunchKernelGGL((conv3x3_stream_kernel<H, W, C, HS, IMG, NSP, WM, 3>), dim3(grid), dim3(512), lds, s, a);
+  hipLaunchKernelGGL((conv3x3_stream_kernel<H, W, CI, CO, HS, IMG, NSP, WM, S, 3>), dim3(grid), dim3(512), lds, s,
+                     a);
 }
 
 }  // namespace
 
-bool conv3x3_stream_supported(int H, int W, int Cin, int Cout) {
-  return Cin == Cout && ((H == 28 && W == 28 && Cin == 128) || (H == 14 && W == 14 && Cin == 256) ||
-                         (H == 7 && W == 7 && Cin == 512));
+bool conv3x3_stream_supported(int Hin, int Win, int Cin, int Cout, int stride) {
+  if (stride == 1)
+    return Cin == Cout && ((Hin == 28 && Win == 28 && Cin == 128) || (Hin == 14 && Win == 14 && Cin == 256) ||
+                           (Hin == 7 && Win == 7 && Cin == 512));
+  if (stride == 2)
+    return Cout == 2 * Cin && ((Hin == 56 && Win == 56 && Cin == 64) || (Hin == 28 && Win == 28 && Cin == 128));
+  return false;
 }
 
 void conv3x3_stream(const void* x, const void* w, const float* bias, const void* res, void* y, const void* zero,
-                    int B, int H, int W, int C, bool relu, hipStream_t s, unsigned long long* stamps) {
+                    int B, int Hin, int Win, int Cin, int Cout, int stride, bool relu, hipStream_t s,
+                    unsigned long long* stamps) {
   if (B <= 0) return;
-  if (!conv3x3_stream_supported(H, W, C, C)) throw std::invalid_argument("conv3x3_stream: unsupported shape");
+  if (!conv3x3_stream_supported(Hin, Win, Cin, Cout, stride))
+    throw std::invalid_argument("conv3x3_stream: unsupported shape");
   if (!x || !w || !bias || !y || !zero ||
       (((uintptr_t)x | (uintptr_t)w | (uintptr_t)y | (uintptr_t)zero | (uintptr_t)res) & 15))
     throw std::invalid_argument("conv3x3_stream: null / misaligned operand");
@@ -365,12 +406,17 @@ void conv3x3_stream(const void* x, const void* w, const float* bias, const void*
   a.B = B;
   a.relu = relu;
   a.stamps = stamps;
-  if (C == 128)  // layer2: half an image per workgroup (15 x 28 x 256 B = 105 KB) + 8 x 3 x 2 KB weight stages
-    launch_stream<28, 28, 128, 14, 1, 1, 2>(a, s);
-  else if (C == 256)  // layer3: a whole image per workgroup (14 x 14 x 512 B = 98 KB) + 8 x 3 x 2 KB weight stages
-    launch_stream<14, 14, 256, 14, 1, 1, 1>(a, s);
-  else  // layer4: two whole images x half the output channels per workgroup (2 x 49 x 1 KB = 98 KB) + rings
-    launch_stream<7, 7, 512, 7, 2, 2, 1>(a, s);
+  // LDS per workgroup: staged input rows + zero pixel + 8 waves x 3 x 2 KB weight stages
+  if (stride == 1 && Cin == 128)  // layer2: half an image (15 x 28 x 256 B = 105 KB)
+    launch_stream<28, 28, 128, 128, 14, 1, 1, 2, 1>(a, s);
+  else if (stride == 1 && Cin == 256)  // layer3: a whole image (14 x 14 x 512 B = 98 KB)
+    launch_stream<14, 14, 256, 256, 14, 1, 1, 1, 1>(a, s);
+  else if (stride == 1)  // layer4: two whole images x half the output channels (2 x 49 x 1 KB = 98 KB)
+    launch_stream<7, 7, 512, 512, 7, 2, 2, 1, 1>(a, s);
+  else if (Cin == 64)  // layer2.0.conv1: a quarter image (15 x 56 x 128 B = 105 KB)
+    launch_stream<28, 28, 64, 128, 7, 1, 1, 2, 2>(a, s);
+  else  // layer3.0.conv1: half an image (15 x 28 x 256 B = 105 KB)
+    launch_stream<14, 14, 128, 256, 7, 1, 1, 1, 2>(a, s);
   DMLC_HIP_CHECK(hipGetLastError());
 }
 

@@ -126,13 +126,14 @@ bool conv3x3_rows_supported(int H, int W, int Cin, int Cout);
 int conv3x3_rows_pick_strip(int B, int H, int num_cus);
 void conv3x3_rows(const void* x, const void* w, const float* bias, const void* res, void* y, const void* zero,
                   int B, int H, int W, int C, bool relu, int strip, hipStream_t s);
-// Direct 3x3/s1/p1 conv for 28x28x128 -> 128 layers (ResNet layer2): one
-// workgroup per image, input rows streamed once through an LDS ring, weights
-// streamed through a 3-stage LDS-DMA ring (conv3x3_stream.hip). Same operand
-// layouts as conv2d_igemm.
-bool conv3x3_stream_supported(int H, int W, int Cin, int Cout);
+// Direct 3x3/p1 conv with the input image resident in LDS and per-wave weight
+// rings (conv3x3_stream.hip): stride 1 on 28x28x128, 14x14x256, 7x7x512;
+// stride 2 on 56x56x64 -> 128 and 28x28x128 -> 256. Hin/Win are the input
+// dims; same operand layouts as conv2d_igemm.
+bool conv3x3_stream_supported(int Hin, int Win, int Cin, int Cout, int stride = 1);
 void conv3x3_stream(const void* x, const void* w, const float* bias, const void* res, void* y, const void* zero,
-                    int B, int H, int W, int C, bool relu, hipStream_t s, unsigned long long* stamps = nullptr);
+                    int B, int Hin, int Win, int Cin, int Cout, int stride, bool relu, hipStream_t s,
+                    unsigned long long* stamps = nullptr);
 int stem_pool_pick_strip(int B, int PH, int num_cus);
 void stem_conv_pool(const void* x, const void* w, const float* bias, void* y, int B, int S, int Wq, int strip,
                     hipStream_t s);

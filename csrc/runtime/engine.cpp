@@ -536,13 +536,16 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
       case OpType::Conv: {
         const ConvLayer& L = convs_[op.conv];
         const ActShape& is = shapes_[op.in];
-        const bool k3s1 = !L.fc && !L.pair && !L.fp8 && L.kh == 3 && L.kw == 3 && L.stride == 1 && L.pad == 1 &&
-                          !shapes_[op.out].f32 && !shapes_[op.out].fp8;
-        // the stream conv runs 2 workgroups per image: only worth it once the batch fills the CUs
-        if (stream_conv_ && k3s1 && 8 * B >= num_cus_ && conv3x3_stream_supported(is.H, is.W, is.C, L.cout)) {
+        const bool k3 = !L.fc && !L.pair && !L.fp8 && L.kh == 3 && L.kw == 3 && L.pad == 1 &&
+                        !shapes_[op.out].f32 && !shapes_[op.out].fp8;
+        const bool k3s1 = k3 && L.stride == 1;
+        // the stream conv runs 1-4 workgroups per image (or image pair): only
+        // worth it once the batch fills the CUs
+        if (stream_conv_ && k3 && 8 * B >= num_cus_ &&
+            conv3x3_stream_supported(is.H, is.W, is.C, L.cout, L.stride)) {
           conv3x3_stream(acts_[op.in], (const uint8_t*)warena_ + L.w_off,
                          (const float*)((const uint8_t*)warena_ + L.b_off), op.res >= 0 ? acts_[op.res] : nullptr,
-                         acts_[op.out], zero_, B, is.H, is.W, is.C, L.relu, s);
+                         acts_[op.out], zero_, B, is.H, is.W, is.C, L.cout, L.stride, L.relu, s);
         } else if (row_conv_ && k3s1 && conv3x3_rows_supported(is.H, is.W, is.C, L.cout)) {
           conv3x3_rows(acts_[op.in], (const uint8_t*)warena_ + L.w_off,
                        (const float*)((const uint8_t*)warena_ + L.b_off), op.res >= 0 ? acts_[op.res] : nullptr,

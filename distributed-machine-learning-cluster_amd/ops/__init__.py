@@ -177,15 +177,18 @@ def conv3x3_rows(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, re
 
 
 def conv3x3_stream(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, res: torch.Tensor | None = None,
-                   relu: bool = True) -> torch.Tensor:
-    """Direct 3x3/s1/p1 conv (conv3x3_stream.hip) on NHWC bf16 [B,28,28,128] or
-    [B,14,14,256] with the conv2d packed weights; + bias (+ residual), ReLU."""
+                   relu: bool = True, stride: int = 1) -> torch.Tensor:
+    """Direct 3x3/p1 conv (conv3x3_stream.hip) on NHWC bf16 with the conv2d
+    packed weights; + bias (+ residual), ReLU. Stride 1: [B,28,28,128],
+    [B,14,14,256], [B,7,7,512]; stride 2: [B,56,56,64] -> 128 channels,
+    [B,28,28,128] -> 256."""
     _need_cuda(x, w_packed, bias, res)
     C = native()
     B, H, W, Cin = x.shape
-    if not C.conv3x3_stream_supported(H, W, Cin, w_packed.shape[0]):
+    Cout = w_packed.shape[0]
+    if not C.conv3x3_stream_supported(H, W, Cin, Cout, stride):
         raise ValueError("conv3x3_stream: unsupported shape")
-    y = torch.empty_like(x)
+    y = torch.empty(B, H // stride, W // stride, Cout, dtype=x.dtype, device=x.device)
     stamps = 0
     if int(os.environ.get("DMLC_BT_DEBUG", "0")) & 32:  # per-workgroup phase stamps (debug)
         global BT_STAMPS
@@ -194,7 +197,7 @@ def conv3x3_stream(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, 
         stamps = _ptr(BT_STAMPS)
     C.conv3x3_stream(_ptr(x.contiguous()), _ptr(w_packed.contiguous()), _ptr(bias.float().contiguous()),
                      _ptr(None if res is None else res.contiguous()), _ptr(y), _ptr(_zero_page(x.device)), B, H, W,
-                     Cin, relu, _stream(), stamps)
+                     Cin, Cout, stride, relu, _stream(), stamps)
     return y
 
 

@@ -284,6 +284,27 @@ def test_conv3x3_stream(gpu, HW, C, B, res, relu):
     assert _rel(_nchw(y.float().cpu()), ref) < 8e-3
 
 
+@pytest.mark.parametrize("HW,Cin,B,relu", [(56, 64, 1, True), (56, 64, 2, False), (28, 128, 1, True),
+                                          (28, 128, 3, False)])
+def test_conv3x3_stream_stride2(gpu, HW, Cin, B, relu):
+    """Stride-2 direct 3x3 conv (conv3x3_stream.hip: 56x56x64 -> 28x28x128 in
+    quarter images, 28x28x128 -> 14x14x256 in half images, even-first column
+    layout) vs torch fp32."""
+    g = torch.Generator().manual_seed(22)
+    Cout = 2 * Cin
+    x = torch.randn(B, Cin, HW, HW, generator=g).bfloat16().float()
+    w = (torch.randn(Cout, Cin, 3, 3, generator=g) / (9 * Cin) ** 0.5).bfloat16().float()
+    bias = torch.randn(Cout, generator=g) * 0.1
+    ref = F.conv2d(x, w, bias, 2, 1)
+    if relu:
+        ref = F.relu(ref)
+    wp = ops.pack_conv_weight(w, device=gpu)
+    y = ops.conv3x3_stream(_nhwc(x).bfloat16().to(gpu), wp, bias.to(gpu), None, relu, stride=2)
+    torch.cuda.synchronize()
+    assert y.shape == (B, HW // 2, HW // 2, Cout)
+    assert _rel(_nchw(y.float().cpu()), ref) < 8e-3
+
+
 @pytest.mark.parametrize("B,strip,res", [(2, None, False), (2, None, True), (3, 4, True), (1, 8, False),
                                          (1, 28, True)])
 def test_conv3x3_rows(gpu, B, strip, res):

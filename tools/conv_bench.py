@@ -118,10 +118,10 @@ def main():
                     row.append(_stamps())
             except Exception as e:  # noqa: BLE001
                 row.append(f"tile{t}=ERR({e})")
-        if name in ("l2", "l3", "l4"):  # direct conv with streamed weights (conv3x3_stream.hip)
-            for use_res in (False, True):
+        if name in ("l2", "l3", "l4", "l2.c1", "l3.c1"):  # direct conv, streamed weights (conv3x3_stream.hip)
+            for use_res in (False, True) if s == 1 else (False,):
                 r = torch.randn(B, H, W, Cout, device=dev).bfloat16() if use_res else None
-                f = lambda: ops.conv3x3_stream(x, wp, bias, r, True)
+                f = lambda: ops.conv3x3_stream(x, wp, bias, r, True, stride=s)
                 us = time_us(f, a.iters)
                 row.append(f"stream{'+res' if use_res else ''}={us:7.1f}us {flops/us/1e6:6.0f}TF")
                 if ops.BT_STAMPS is not None:
