@@ -147,6 +147,15 @@ void stem_conv_pool_u8(const uint8_t* x, const void* w, const float* bias, void*
 // raw per-lane registers: a, b = int32 [64 lanes][8], d = f32 [64 lanes][4].
 void mfma_fp8_probe(const void* a, const void* b, float* d, hipStream_t s);
 
+// Fused ResNet head (head.hip): global avgpool of bf16 x [B, HW, C] + fc
+// (w bf16 [Npad, ldw], bias fp32) -> fp32 logits [B, N] + softmax top-1.
+// ws: head_ws_bytes(max_batch) bytes, zeroed once at allocation.
+bool head_supported(int C, int N, int ldw, int Npad);
+int head_splits(int B, int N, int num_cus);
+size_t head_ws_bytes(int max_batch);
+void head_fused(const void* x, const void* w, const float* bias, int B, int HW, int C, int N, int ldw, int Npad,
+                float* logits, int32_t* idx, float* prob, void* ws, size_t ws_bytes, int num_cus, hipStream_t s);
+
 // Row-wise softmax + top-1 over fp32 logits [B, ld] (first N columns).
 void softmax_top1(const float* logits, int B, int N, int ld, int32_t* idx, float* prob,
                   hipStream_t s);

@@ -86,6 +86,8 @@ Engine::Engine(const std::string& arch, const WeightMap& weights, int device, in
   if (const char* e = std::getenv("DMLC_BIGTILE")) bigtile_ = std::string(e) != "0";
   if (const char* e = std::getenv("DMLC_FUSED_PREPROCESS")) fused_pre_ = std::string(e) != "0";
   if (const char* e = std::getenv("DMLC_STREAM_CONV")) stream_conv_ = std::string(e) != "0";
+  if (const char* e = std::getenv("DMLC_FORK_DS")) fork_ds_ = std::string(e) != "0";
+  if (const char* e = std::getenv("DMLC_FUSED_HEAD")) fused_head_ = std::string(e) != "0";
 
   if (arch == "resnet18")
     build_resnet({2, 2, 2, 2}, false);
@@ -108,6 +110,13 @@ Engine::Engine(const std::string& arch, const WeightMap& weights, int device, in
   DMLC_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
   DMLC_HIP_CHECK(hipEventCreateWithFlags(&ev_in_, hipEventDisableTiming));
   DMLC_HIP_CHECK(hipEventCreateWithFlags(&ev_out_, hipEventDisableTiming));
+  DMLC_HIP_CHECK(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
+  fork_evs_.resize(ops_.size());
+  join_evs_.resize(ops_.size());
+  for (size_t i = 0; i < ops_.size(); ++i) {
+    DMLC_HIP_CHECK(hipEventCreateWithFlags(&fork_evs_[i], hipEventDisableTiming));
+    DMLC_HIP_CHECK(hipEventCreateWithFlags(&join_evs_[i], hipEventDisableTiming));
+  }
   ws_elems_ = (size_t)16 << 20;  // 64 MB split-K workspace
   DMLC_HIP_CHECK(hipMalloc(&ws_, ws_elems_ * sizeof(float)));
   DMLC_HIP_CHECK(hipMalloc(&zero_, 256));
@@ -123,8 +132,12 @@ Engine::~Engine() {
   if (bt_ws_) hipFree(bt_ws_);
   if (zero_) hipFree(zero_);
   if (dummy_idx_) hipFree(dummy_idx_);
+  if (head_ws_) hipFree(head_ws_);
   if (ev_in_) hipEventDestroy(ev_in_);
   if (ev_out_) hipEventDestroy(ev_out_);
+  for (auto e : fork_evs_) hipEventDestroy(e);
+  for (auto e : join_evs_) hipEventDestroy(e);
+  if (side_) hipStreamDestroy(side_);
   if (stream_) hipStreamDestroy(stream_);
 }
 
@@ -221,8 +234,10 @@ void Engine::build_resnet(const std::vector<int>& blocks, bool bottleneck) {
       const std::string p = "layer" + std::to_string(li + 1) + "." + std::to_string(bi);
       const int outp = bottleneck ? planes * 4 : planes;
       int identity = x;
-      if (stride != 1 || inplanes != outp)
+      if (stride != 1 || inplanes != outp) {
         identity = conv(x, p + ".downsample.0", p + ".downsample.1", outp, 1, stride, 0, false);
+        ops_.back().side = true;
+      }
       if (!bottleneck) {
         const int y = conv(x, p + ".conv1", p + ".bn1", planes, 3, stride, 1, true);
         x = conv(y, p + ".conv2", p + ".bn2", planes, 3, 1, 1, true, identity);
@@ -443,6 +458,10 @@ void Engine::reserve(int max_batch) {
   act_bytes_ = total;
   DMLC_HIP_CHECK(hipMalloc(&dummy_idx_, (size_t)max_batch * 8));
   max_batch_ = max_batch;
+  if (head_ws_) DMLC_HIP_CHECK(hipFree(head_ws_));
+  head_ws_bytes_ = head_ws_bytes(max_batch);
+  DMLC_HIP_CHECK(hipMalloc(&head_ws_, head_ws_bytes_));
+  DMLC_HIP_CHECK(hipMemset(head_ws_, 0, head_ws_bytes_));
   // big-tile conv split-K slabs for the largest batch
   long slabs = 0;
   for (const Op& op : ops_) {
@@ -517,11 +536,52 @@ ConvArgs Engine::conv_args(const Op& op, int B, float* logits) const {
   return a;
 }
 
+Engine::ConvPath Engine::conv_path(const Op& op, int B) const {
+  const ConvLayer& L = convs_[op.conv];
+  const ActShape& is = shapes_[op.in];
+  const bool k3 = !L.fc && !L.pair && !L.fp8 && L.kh == 3 && L.kw == 3 && L.pad == 1 && !shapes_[op.out].f32 &&
+                  !shapes_[op.out].fp8;
+  // the stream conv runs 1-4 workgroups per image (or image pair): only
+  // worth it once the batch fills the CUs
+  if (stream_conv_ && k3 && 8 * B >= num_cus_ && conv3x3_stream_supported(is.H, is.W, is.C, L.cout, L.stride))
+    return ConvPath::Stream;
+  if (row_conv_ && k3 && L.stride == 1 && conv3x3_rows_supported(is.H, is.W, is.C, L.cout)) return ConvPath::Rows;
+  if (bigtile_ && conv_bigtile_pick(conv_args(op, B, nullptr), num_cus_) >= 0) return ConvPath::BigTile;
+  return ConvPath::Igemm;
+}
+
+bool Engine::head_fusable(size_t oi) const {
+  if (!fused_head_ || oi + 2 >= ops_.size()) return false;
+  const Op& pool = ops_[oi];
+  const Op& fc = ops_[oi + 1];
+  const Op& sm = ops_[oi + 2];
+  if (pool.type != OpType::AvgPoolGlobal || fc.type != OpType::Conv || sm.type != OpType::SoftmaxTop1) return false;
+  if (shapes_[pool.in].fp8 || fc.in != pool.out || sm.in != fc.out || !shapes_[fc.out].f32) return false;
+  const ConvLayer& L = convs_[fc.conv];
+  return L.fc && !L.fp8 && !L.relu && L.cin == shapes_[pool.in].C && head_supported(L.cin, L.cout, L.kpad, L.npad);
+}
+
+bool Engine::side_safe(int B) const {
+  for (const Op& op : ops_)
+    if (op.type == OpType::Conv && conv_path(op, B) == ConvPath::BigTile) return false;
+  return true;
+}
+
 void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* idx, float* prob,
                      float* logits, hipStream_t s, std::vector<hipEvent_t>* evs, bool trace) {
   size_t ei = 0;
   if (evs) DMLC_HIP_CHECK(hipEventRecord((*evs)[ei++], s));
-  for (const Op& op : ops_) {
+  // per-op event timing keeps every op on one stream
+  const bool side_ready = fork_ds_ && !evs && side_safe(B);
+  std::map<int, hipEvent_t> joined;  // activation -> event its side-stream producer recorded
+  int skip = 0;                      // ops already done by a fused kernel
+  for (size_t oi = 0; oi < ops_.size(); ++oi) {
+    const Op& op = ops_[oi];
+    if (skip > 0) {
+      --skip;
+      if (evs) DMLC_HIP_CHECK(hipEventRecord((*evs)[ei++], s));
+      continue;
+    }
     std::optional<TraceRange> tr;  // per-op host ranges (not inside a graph capture)
     if (trace) tr.emplace(op.name.c_str());
     switch (op.type) {
@@ -536,31 +596,50 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
       case OpType::Conv: {
         const ConvLayer& L = convs_[op.conv];
         const ActShape& is = shapes_[op.in];
-        const bool k3 = !L.fc && !L.pair && !L.fp8 && L.kh == 3 && L.kw == 3 && L.pad == 1 &&
-                        !shapes_[op.out].f32 && !shapes_[op.out].fp8;
-        const bool k3s1 = k3 && L.stride == 1;
-        // the stream conv runs 1-4 workgroups per image (or image pair): only
-        // worth it once the batch fills the CUs
-        if (stream_conv_ && k3 && 8 * B >= num_cus_ &&
-            conv3x3_stream_supported(is.H, is.W, is.C, L.cout, L.stride)) {
-          conv3x3_stream(acts_[op.in], (const uint8_t*)warena_ + L.w_off,
+        // A downsample conv runs on the side stream, concurrently with its
+        // block's conv1 (both read the block input; conv2 joins them through
+        // the residual). Never next to a big-tile conv: its split-K slices
+        // spin on each other and need their CUs.
+        hipStream_t cs = s;
+        if (side_ready && op.side) {
+          DMLC_HIP_CHECK(hipEventRecord(fork_evs_[oi], s));
+          DMLC_HIP_CHECK(hipStreamWaitEvent(side_, fork_evs_[oi], 0));
+          cs = side_;
+        }
+        if (op.res >= 0 && joined.count(op.res)) {
+          DMLC_HIP_CHECK(hipStreamWaitEvent(s, joined[op.res], 0));
+          joined.erase(op.res);
+        }
+        switch (conv_path(op, B)) {
+          case ConvPath::Stream:
+            conv3x3_stream(acts_[op.in], (const uint8_t*)warena_ + L.w_off,
+                           (const float*)((const uint8_t*)warena_ + L.b_off), op.res >= 0 ? acts_[op.res] : nullptr,
+                           acts_[op.out], zero_, B, is.H, is.W, is.C, L.cout, L.stride, L.relu, cs);
+            break;
+          case ConvPath::Rows:
+            conv3x3_rows(acts_[op.in], (const uint8_t*)warena_ + L.w_off,
                          (const float*)((const uint8_t*)warena_ + L.b_off), op.res >= 0 ? acts_[op.res] : nullptr,
-                         acts_[op.out], zero_, B, is.H, is.W, is.C, L.cout, L.stride, L.relu, s);
-        } else if (row_conv_ && k3s1 && conv3x3_rows_supported(is.H, is.W, is.C, L.cout)) {
-          conv3x3_rows(acts_[op.in], (const uint8_t*)warena_ + L.w_off,
-                       (const float*)((const uint8_t*)warena_ + L.b_off), op.res >= 0 ? acts_[op.res] : nullptr,
-                       acts_[op.out], zero_, B, is.H, is.W, is.C, L.relu, conv3x3_rows_pick_strip(B, is.H, num_cus_),
-                       s);
-        } else {
-          const ConvArgs a = conv_args(op, B, logits);
-          const int bt = bigtile_ ? conv_bigtile_pick(a, num_cus_) : -1;
-          if (bt >= 0) {
+                         acts_[op.out], zero_, B, is.H, is.W, is.C, L.relu, conv3x3_rows_pick_strip(B, is.H, num_cus_),
+                         cs);
+            break;
+          case ConvPath::BigTile: {
+            const ConvArgs a = conv_args(op, B, logits);
+            const int bt = conv_bigtile_pick(a, num_cus_);
             int splits = conv_bigtile_splits(a, bt, num_cus_);
             if (conv_bigtile_ws_bytes(conv_bigtile_slabs(a, bt, splits)) > bt_ws_bytes_) splits = 1;
-            conv2d_bigtile(a, bt, splits, bt_ws_, bt_ws_bytes_, s);
-          } else {
-            conv2d_igemm(a, s);
+            conv2d_bigtile(a, bt, splits, bt_ws_, bt_ws_bytes_, cs);
+            break;
           }
+          case ConvPath::Igemm: {
+            ConvArgs a = conv_args(op, B, logits);
+            if (cs != s) a.split_k = 1;  // the split-K workspace belongs to the main stream
+            conv2d_igemm(a, cs);
+            break;
+          }
+        }
+        if (cs != s) {
+          DMLC_HIP_CHECK(hipEventRecord(join_evs_[oi], side_));
+          joined[op.out] = join_evs_[oi];
         }
         break;
       }
@@ -585,6 +664,15 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
       }
       case OpType::AvgPoolGlobal: {
         const ActShape& i = shapes_[op.in];
+        if (head_fusable(oi)) {  // avgpool + fc + softmax/top-1 in one launch
+          const ConvLayer& L = convs_[ops_[oi + 1].conv];
+          head_fused(acts_[op.in], (const uint8_t*)warena_ + L.w_off,
+                     (const float*)((const uint8_t*)warena_ + L.b_off), B, i.H * i.W, i.C, L.cout, L.kpad, L.npad,
+                     logits ? logits : (float*)acts_[ops_[oi + 1].out], idx ? idx : dummy_idx_,
+                     prob ? prob : (float*)(dummy_idx_ + max_batch_), head_ws_, head_ws_bytes_, num_cus_, s);
+          skip = 2;
+          break;
+        }
         avgpool_global(acts_[op.in], acts_[op.out], B, i.H * i.W, i.C, s, i.fp8, i.scale);
         break;
       }

@@ -53,6 +53,7 @@ struct Op {
   int conv = -1;
   int k = 0, stride = 0, pad = 0;  // Preprocess: k = 1 for the paired layout
   std::string name;
+  bool side = false;  // may run on the side stream (downsample conv, joined via the residual)
 };
 
 class Engine {
@@ -110,6 +111,10 @@ class Engine {
   void run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* idx, float* prob,
                float* logits, hipStream_t s, std::vector<hipEvent_t>* evs, bool trace);
   ConvArgs conv_args(const Op& op, int B, float* logits) const;
+  enum class ConvPath { Stream, Rows, BigTile, Igemm };
+  ConvPath conv_path(const Op& op, int B) const;
+  bool side_safe(int B) const;
+  bool head_fusable(size_t oi) const;  // ops oi..oi+2 = avgpool, fc, softmax_top1 -> head_fused  // no big-tile (co-residency-dependent) conv at batch B
 
   std::string arch_;
   int device_ = 0;
@@ -125,6 +130,8 @@ class Engine {
   bool stream_conv_ = true; // direct 3x3 with streamed weights for 28x28x128 layers (env DMLC_STREAM_CONV=0 disables)
   bool row_conv_ = true;    // direct row-streaming 3x3 convs where supported (env DMLC_ROW_CONV=0 disables)
   bool fp8_ = false;        // resnet50_fp8
+  bool fused_head_ = true;  // avgpool+fc+softmax/top-1 as one kernel (env DMLC_FUSED_HEAD=0 disables)
+  bool fork_ds_ = true;     // downsample convs on a side stream (env DMLC_FORK_DS=0 disables)
 
   std::vector<ActShape> shapes_;
   std::vector<ConvLayer> convs_;
@@ -141,9 +148,13 @@ class Engine {
   void* zero_ = nullptr;  // 16-B zero page: LDS-DMA source for conv padding taps
   size_t ws_elems_ = 0;
   int32_t* dummy_idx_ = nullptr;
+  void* head_ws_ = nullptr;  // fused head partials + per-group tickets
+  size_t head_ws_bytes_ = 0;
 
   hipStream_t stream_ = nullptr;
   hipEvent_t ev_in_ = nullptr, ev_out_ = nullptr;
+  hipStream_t side_ = nullptr;                      // downsample branch
+  std::vector<hipEvent_t> fork_evs_, join_evs_;     // per op
   using GraphKey = std::tuple<const void*, int, int, int, void*, void*, void*>;
   std::map<GraphKey, hipGraphExec_t> graphs_;
 };

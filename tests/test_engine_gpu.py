@@ -100,3 +100,31 @@ def test_ot_checkpoint_engine(gpu, tmp_path):
     b = e2.predict(img, return_logits=True)[2]
     torch.cuda.synchronize()
     assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("B", [1, 3, 6, 64, 256])
+def test_fused_head_and_side_stream_match_unfused(gpu, monkeypatch, B):
+    """head.hip (avgpool+fc+softmax/top-1, split over classes with a ticketed
+    last-arriver combine) and the downsample side-stream branch against the
+    three-kernel single-stream path: pooled vectors are bit-identical, the fc
+    sums in a different order, so logits agree to fp32 rounding; replayed
+    twice to check the tickets re-arm."""
+    model = build("resnet18", seed=21, randomize_bn=True)
+    sd = state_dict_f32(model)
+    monkeypatch.setenv("DMLC_FUSED_HEAD", "0")
+    monkeypatch.setenv("DMLC_FORK_DS", "0")
+    ref_eng = InferenceEngine("resnet18", sd, max_batch=B)
+    monkeypatch.setenv("DMLC_FUSED_HEAD", "1")
+    monkeypatch.setenv("DMLC_FORK_DS", "1")
+    eng = InferenceEngine("resnet18", sd, max_batch=B)
+    g = torch.Generator().manual_seed(B)
+    img = torch.randint(0, 256, (B, 224, 224, 3), generator=g, dtype=torch.uint8).to(gpu)
+    ri, rp, rl = ref_eng.predict(img, return_logits=True)
+    for _ in range(2):
+        i, p, lg = eng.predict(img, return_logits=True)
+        torch.cuda.synchronize()
+        assert torch.allclose(lg, rl, rtol=1e-4, atol=1e-4), (lg - rl).abs().max().item()
+        top2 = torch.softmax(rl, -1).topk(2, -1).values
+        near_tie = (top2[:, 0] - top2[:, 1]) < 1e-5
+        assert torch.all((i == ri) | near_tie)
+        assert torch.allclose(p, rp, rtol=1e-4, atol=1e-6)
