@@ -18,13 +18,18 @@
 //  3. logits (+bias) to global fp32 and LDS; per image a wave reduces its
 //     split's (max, argmax, sum exp(x - max)) and stores the partial;
 //  4. the workgroup that draws the last ticket for group g combines the NS
-//     partials (cdna_hip_programming.md §6 Guideline 16 counter recipe:
-//     plain stores -> vmcnt(0) -> barrier -> agent release -> vmcnt(0) ->
-//     relaxed agent fetch_add; reducer: agent acquire -> vmcnt(0) ->
-//     barrier -> loads) and writes (class, prob), then re-arms the counter.
+//     partials (cdna_hip_programming.md §6 Guideline 16 counter recipe, sc1
+//     form: relaxed agent-scope stores of the partials -> vmcnt(0) ->
+//     barrier -> relaxed agent fetch_add; the reducer reads them with relaxed
+//     agent-scope loads; no release/acquire fences, which would write back /
+//     invalidate the XCD's whole L2 in every workgroup) and writes (class,
+//     prob), then re-arms the counter.
 // No workgroup waits on another, so any residency is correct.
 #include "common.h"
 #include "kernels.h"
+
+#include <algorithm>
+#include <cstdlib>
 
 namespace dmlc {
 
@@ -42,92 +47,157 @@ struct HeadArgs {
   float4* part;       // [B, NS] (max, argmax bits, sum, -)
   uint32_t* cnt;      // [ceil(B / kIPW)], zero between launches
   int B, HW, C, N, ldw, tiles_per_split, NS;
+  int ko;  // knock-out bits for timing experiments (env DMLC_HEAD_KO): 1 pool loads, 2 fc loads
 };
 
+// Sum of n (power of two) values in the butterfly order of avgpool_global's
+// xor-shuffle reduce: ((v0+v1)+(v2+v3))+((v4+v5)+(v6+v7)).
+__device__ __forceinline__ float tree_sum(const float* v, int n) {
+  float t[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) t[i] = i < n ? v[i] : 0.f;
+#pragma unroll
+  for (int w = 1; w < 8; w <<= 1)
+#pragma unroll
+    for (int a = 0; a + w < 8; a += 2 * w)
+      if (a + w < n) t[a] = t[a] + t[a + w];
+  return t[0];
+}
+
+template <int TPG>
 __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int C = a.C;
   const int ldp = C + 8;  // pooled row stride (elements): rows 16 B apart in bank space
   bf16* pooled = (bf16*)smem;                                // [kIPW][ldp]
   float* lg = (float*)(smem + kIPW * ldp * 2);               // [kIPW][tiles_per_split*16]
+  float* red = lg;  // pooling partials [TPG][kIPW][C] fp32 (dead before lg is written)
   const int g = blockIdx.x, split = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int b0 = g * kIPW;
   const int nimg = min(kIPW, a.B - b0);
 
-  // ---- 1. average pool
-  {
-    const int c8 = C / 8;
-    const int total = nimg * c8 * 8;
-    const float inv = 1.f / a.HW;
-    for (int t = tid; t < total; t += 256) {
-      const int item = t >> 3, part = t & 7;
-      const int cg = item % c8, i = item / c8;
-      float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  // ---- 1. average pool. avgpool_global's arithmetic: part p (0..7) of a
+  // channel group sums pixels p, p+8, ... in order; the 8 parts combine in
+  // butterfly order. Here TPG threads share a group's 8 parts (PPT each),
+  // every thread issues all its loads of an image before adding, and the
+  // TPG partials meet in LDS.
+  const int c8 = C / 8;
+  constexpr int PPT = 8 / TPG;
+  constexpr int U = PPT >= 8 ? 2 : PPT >= 4 ? 4 : 8;  // pixels per part in flight
+  const float inv = 1.f / a.HW;
+  for (int it = tid; it < ((a.ko & 1) ? 0 : c8 * TPG); it += 256) {
+    const int cg = it % c8, q = it / c8;
+    for (int i = 0; i < nimg; ++i) {
       const bf16* base = a.x + ((long)(b0 + i) * a.HW) * C + cg * 8;
-      constexpr int U = 8;
-      for (int i0 = part; i0 < a.HW; i0 += 8 * U) {
-        float f[U][8];
+      float ps[PPT][8];  // [part][channel]
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const int p = i0 + 8 * u;
-          if (p < a.HW) {
-            unpack8(*(const uint4*)(base + (long)p * C), f[u]);
-          } else {
+      for (int pp = 0; pp < PPT; ++pp)
 #pragma unroll
-            for (int j = 0; j < 8; ++j) f[u][j] = 0.f;
+        for (int j = 0; j < 8; ++j) ps[pp][j] = 0.f;
+      for (int c0 = 0; c0 < a.HW; c0 += 8 * U) {  // U pixels per part per round
+        uint4 v[PPT][U];
+#pragma unroll
+        for (int pp = 0; pp < PPT; ++pp)
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const int pix = c0 + (q * PPT + pp) + 8 * u;
+            v[pp][u] = pix < a.HW ? *(const uint4*)(base + (long)pix * C) : make_uint4(0, 0, 0, 0);
           }
-        }
 #pragma unroll
-        for (int u = 0; u < U; ++u)
+        for (int pp = 0; pp < PPT; ++pp)
 #pragma unroll
-          for (int j = 0; j < 8; ++j) s[j] += f[u][j];
+          for (int u = 0; u < U; ++u) {
+            const int pix = c0 + (q * PPT + pp) + 8 * u;
+            if (pix < a.HW) {
+              float f[8];
+              unpack8(v[pp][u], f);
+#pragma unroll
+              for (int j = 0; j < 8; ++j) ps[pp][j] += f[j];
+            }
+          }
       }
 #pragma unroll
-      for (int o = 1; o < 8; o <<= 1)
+      for (int j = 0; j < 8; ++j) {
+        float col[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) s[j] += __shfl_xor(s[j], o, 64);
-      if (part == 0) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) s[j] *= inv;
-        *(uint4*)(pooled + i * ldp + cg * 8) = pack8(s);
+        for (int pp = 0; pp < 8; ++pp) col[pp] = pp < PPT ? ps[pp][j] : 0.f;
+        red[((long)q * kIPW + i) * C + cg * 8 + j] = tree_sum(col, PPT);
       }
     }
   }
   __syncthreads();
+  for (int it = tid; it < nimg * c8; it += 256) {
+    const int cg = it % c8, i = it / c8;
+    float s[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float col[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) col[q] = q < TPG ? red[((long)q * kIPW + i) * C + cg * 8 + j] : 0.f;
+      s[j] = tree_sum(col, TPG) * inv;
+    }
+    *(uint4*)(pooled + i * ldp + cg * 8) = pack8(s);
+  }
+  __syncthreads();
 
-  // ---- 2./3. fc tiles on MFMA: lane holds D[class row (lane>>4)*4 + r][image lane&15]
+  // ---- 2./3. fc tiles on MFMA: lane holds D[class row (lane>>4)*4 + r][image lane&15].
+  // K in chunks of 512: the chunk's 16 pooled fragments are read once from
+  // LDS, then two tiles' 16 weight fragments each are loaded together so a
+  // wave waits on global latency once per tile pair.
   const int col = lane & 15, kq = lane >> 4;
   const int nsplit = a.tiles_per_split * 16;
   const int n_begin = split * nsplit;
-  for (int t = wave; t < a.tiles_per_split; t += 4) {
+  const bool live = col < nimg;
+  const bf16* prow = pooled + col * ldp + kq * 8;
+  for (int t = wave; t < a.tiles_per_split; t += 8) {
     const int n0 = n_begin + t * 16;
     if (n0 >= a.N) break;
-    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-    const bf16* wrow = a.w + (long)(n0 + col) * a.ldw + kq * 8;
-    const bf16* prow = pooled + col * ldp + kq * 8;
-    const bool live = col < nimg;
-    for (int k0 = 0; k0 < C; k0 += 32 * 4) {
-      bf16x8 wa[4], pb[4];
+    const bool two = t + 4 < a.tiles_per_split && n0 + 64 < a.N;
+    floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+    const bf16* w0 = a.w + (long)(n0 + col) * a.ldw + kq * 8;
+    const bf16* w1 = w0 + 64L * a.ldw;
+    for (int kc = 0; kc < C; kc += 512) {
+      bf16x8 pb[16], wa[16], wb[16];
+      pb[0] = bf16x8{};
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int k = k0 + 32 * u;
+      for (int u = 0; u < 16; ++u) {
+        const int k = kc + 32 * u;
         if (k < C) {
-          wa[u] = *(const bf16x8*)(wrow + k);
-          pb[u] = live ? *(const bf16x8*)(prow + k) : bf16x8{};
+          if (a.ko & 2) {
+            wa[u] = pb[0];
+            wb[u] = pb[0];
+          } else {
+            wa[u] = *(const bf16x8*)(w0 + k);
+            if (two) wb[u] = *(const bf16x8*)(w1 + k);
+          }
         }
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
-        if (k0 + 32 * u < C) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[u], pb[u], acc, 0, 0, 0);
+      for (int u = 0; u < 16; ++u) {
+        const int k = kc + 32 * u;
+        pb[u] = (live && k < C) ? *(const bf16x8*)(prow + k) : bf16x8{};
+      }
+#pragma unroll
+      for (int u = 0; u < 16; ++u)
+        if (kc + 32 * u < C) {
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[u], pb[u], acc0, 0, 0, 0);
+          if (two) acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[u], pb[u], acc1, 0, 0, 0);
+        }
     }
     if (live) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int n = n0 + kq * 4 + r;
-        const float v = acc[r] + a.bias[n];
-        if (n < a.N) a.logits[(long)(b0 + col) * a.N + n] = v;
-        lg[col * nsplit + t * 16 + kq * 4 + r] = v;
+      for (int h = 0; h < 2; ++h) {
+        if (h == 1 && !two) break;
+        const floatx4 acc = h ? acc1 : acc0;
+        const int tt = t + 4 * h;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int n = n_begin + tt * 16 + kq * 4 + r;
+          const float v = acc[r] + a.bias[n];
+          if (n < a.N) a.logits[(long)(b0 + col) * a.N + n] = v;
+          lg[col * nsplit + tt * 16 + kq * 4 + r] = v;
+        }
       }
     }
   }
@@ -164,7 +234,12 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
       }
       return;
     }
-    if (lane == 0) a.part[(long)(b0 + wave) * a.NS + split] = make_float4(best, __int_as_float(bi), s, 0.f);
+    if (lane == 0) {  // relaxed agent-scope atomic stores = sc1 write-through: no release fence needed
+      float* q = (float*)(a.part + (long)(b0 + wave) * a.NS + split);
+      __hip_atomic_store(q, best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(q + 1, __int_as_float(bi), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(q + 2, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
   if (a.NS == 1) return;
 
@@ -173,15 +248,9 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
   __syncthreads();
   int* flag = (int*)lg;  // reuse LDS (every wave is past its lg reads: barrier above)
   if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const uint32_t ticket = __hip_atomic_fetch_add(&a.cnt[g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int last = ticket == (uint32_t)(a.NS - 1);
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(&a.cnt[g], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm (graph replay)
-    }
+    if (last) __hip_atomic_store(&a.cnt[g], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm (graph replay)
     *flag = last;
   }
   __syncthreads();
@@ -191,7 +260,10 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
   const float4* p = a.part + (long)(b0 + wave) * a.NS;
   // every lane walks the NS partials in order (NS is small)
   for (int s = 0; s < a.NS; ++s) {
-    const float4 q = p[s];
+    const float* pq = (const float*)(p + s);  // sc1 loads of the sc1-stored partials
+    const float4 q = make_float4(__hip_atomic_load(pq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                                 __hip_atomic_load(pq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                                 __hip_atomic_load(pq + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), 0.f);
     if (q.z == 0.f) continue;  // empty split (no classes)
     const int qi = __float_as_int(q.y);
     if (q.x > m || (q.x == m && qi < bi)) {
@@ -255,9 +327,18 @@ void head_fused(const void* x, const void* w, const float* bias, int B, int HW, 
   a.C = C;
   a.N = N;
   a.ldw = ldw;
-  const size_t lds = (size_t)kIPW * (C + 8) * 2 + (size_t)kIPW * a.tiles_per_split * 16 * 4;
+  static const int ko = std::getenv("DMLC_HEAD_KO") ? std::atoi(std::getenv("DMLC_HEAD_KO")) : 0;
+  a.ko = ko;
+  const int c8 = C / 8, tpg = c8 >= 256 ? 1 : c8 >= 128 ? 2 : c8 >= 64 ? 4 : 8;
+  const size_t lds = (size_t)kIPW * (C + 8) * 2 +
+                     std::max((size_t)kIPW * a.tiles_per_split * 16 * 4, (size_t)tpg * kIPW * C * 4);
   if (lds > 160 * 1024) throw std::invalid_argument("head_fused: LDS budget exceeded");
-  hipLaunchKernelGGL(head_kernel, dim3(groups, ns), dim3(256), lds, s, a);
+  switch (tpg) {
+    case 1: hipLaunchKernelGGL(head_kernel<1>, dim3(groups, ns), dim3(256), lds, s, a); break;
+    case 2: hipLaunchKernelGGL(head_kernel<2>, dim3(groups, ns), dim3(256), lds, s, a); break;
+    case 4: hipLaunchKernelGGL(head_kernel<4>, dim3(groups, ns), dim3(256), lds, s, a); break;
+    default: hipLaunchKernelGGL(head_kernel<8>, dim3(groups, ns), dim3(256), lds, s, a); break;
+  }
   DMLC_HIP_CHECK(hipGetLastError());
 }
 

@@ -131,7 +131,10 @@ class Engine {
   bool row_conv_ = true;    // direct row-streaming 3x3 convs where supported (env DMLC_ROW_CONV=0 disables)
   bool fp8_ = false;        // resnet50_fp8
   bool fused_head_ = true;  // avgpool+fc+softmax/top-1 as one kernel (env DMLC_FUSED_HEAD=0 disables)
-  bool fork_ds_ = true;     // downsample convs on a side stream (env DMLC_FORK_DS=0 disables)
+  // downsample convs on a side stream (env DMLC_FORK_DS=1 enables): measured
+  // slower (the branch slows its sibling conv1 by 10-12 us and adds ~10 us of
+  // fork/join gaps per block: profiles/r1_fork_ds_timeline.txt)
+  bool fork_ds_ = false;
 
   std::vector<ActShape> shapes_;
   std::vector<ConvLayer> convs_;

@@ -1,3 +1,4 @@
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && export TMPDIR=/tmp
-bash tools/gpu_check.sh test && bash tools/gpu_check.sh bench && \
-timeout -k 10 300 python tools/interference_probe.py > gpurun_out/interference.log 2>&1; echo rc=$?; cat gpurun_out/interference.log | tail -8
+for k in 0 1 2 3; do
+DMLC_HEAD_KO=$k timeout -k 10 120 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/ko$k -o run -- python3 bench.py --steps 20 --warmup 5 --latency-queries 0 > gpurun_out/ko$k.log 2>&1 || exit 1
+done
