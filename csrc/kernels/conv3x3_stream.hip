@@ -3,7 +3,10 @@
 // every 3x3 conv from layer2 on through it:
 //   stride 1: layer2 (28x28x128), layer3 (14x14x256), layer4 (7x7x512)
 //   stride 2: layer2.0.conv1 (56x56x64 -> 28x28x128), layer3.0.conv1 (28x28x128
-//             -> 14x14x256)
+//             -> 14x14x256), layer4.0.conv1 (14x14x256 -> 7x7x512); these also
+//             compute the block's 1x1/s2 downsample conv when asked (its input
+//             is the 3x3's tap (1,1), already resident: one more output, no
+//             second pass over the block input)
 //
 // Reference equivalent: those convs + bn + (residual) + relu of
 // tch::vision::resnet18, run per query by `forward_t` at src/services.rs:493.
@@ -52,6 +55,10 @@ struct StreamConvArgs {
   const bf16* res;    // [B, H, W, CO] or null
   bf16* y;            // [B, H, W, CO]
   const bf16* zero;   // >= 16 zero bytes
+  // fused 1x1 / stride-S downsample (DS kernels): yd = wd x (tap (1,1) input) + bd
+  const bf16* wd;     // [CO, CI]
+  const float* bd;    // [CO]
+  bf16* yd;           // [B, H, W, CO]
   int B;
   int relu;
   unsigned long long* stamps;  // debug: per-workgroup phase stamps (100 MHz), or null
@@ -101,7 +108,7 @@ struct StreamGeom {
   static constexpr size_t LDS = (size_t)XBYTES + (size_t)8 * ND * WST;
 };
 
-template <int H, int W, int CI, int CO, int HS, int IMG, int NSP, int WM, int S, int ND>
+template <int H, int W, int CI, int CO, int HS, int IMG, int NSP, int WM, int S, int ND, bool DS>
 __global__ __launch_bounds__(512, 1) void conv3x3_stream_kernel(StreamConvArgs a) {
   using G = StreamGeom<H, W, CI, HS, IMG, S, ND>;
   constexpr int BK = 32;                     // K-tile depth = one MFMA k-step
@@ -116,9 +123,15 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream_kernel(StreamConvArgs a
   constexpr int XI = WI * CPX / 64;          // LDS-DMA instructions per input row
   constexpr int KT = 9 * CI / BK;            // K-tiles
   constexpr int CT = CI / BK;                // K-tiles per tap
+  // A block's downsample conv reads exactly the 3x3 conv's tap (1,1) input
+  // (x[S r, S c]), which is resident here: its CT K-tiles follow the 3x3's KT
+  // in the same weight stream, on tap (1,1)'s X fragments, into accd.
+  constexpr int KT2 = KT + (DS ? CT : 0);
   constexpr int GW = WST / 1024;             // weight DMA instructions per wave per K-tile
   static_assert(CO == 8 / WM * WN * NSP && WI * CPX % 64 == 0 && H % HS == 0 && CPX >= 8, "geometry");
-  static_assert(S == 1 || (S == 2 && WI % 4 == 0 && HI % 2 == 0), "stride");
+  // (128-B pixels rely on the even/odd column halves starting on the same
+  // window parity; pixels of >= 256 B fill whole bank windows)
+  static_assert(S == 1 || (S == 2 && (WI % 4 == 0 || CPX >= 16) && HI % 2 == 0), "stride");
   static_assert(ND == 3 && KT >= ND, "the loop's waits assume a 3-stage ring");
   static_assert(MF + NF <= 15, "lgkmcnt range of the pipelined loop");
 
@@ -194,16 +207,22 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream_kernel(StreamConvArgs a
   // ---- this wave's 32 weight rows of K-tile t -> its stage st (rows permuted,
   // chunks swizzled): per-lane byte offsets into the weights, the K-tile
   // advance in the scalar base
-  uint32_t woff[GW];
+  uint32_t woff[GW], woffd[GW];
 #pragma unroll
   for (int g = 0; g < GW; ++g) {
     const int ci = g * 64 + lane, n = ci >> 2, pc = ci & 3;
     woff[g] = (uint32_t)(((ch0 + perm32(n)) * (9 * CI) + 8 * wswz(n, pc)) * 2);
+    woffd[g] = (uint32_t)(((ch0 + perm32(n)) * CI + 8 * wswz(n, pc)) * 2);
   }
   const bf16* wbase = a.w;
   auto load_wtile = [&](int t, int st) __attribute__((always_inline)) {
+    if (DS && t >= KT) {
 #pragma unroll
-    for (int g = 0; g < GW; ++g) dma16s(wbase + t * BK, woff[g], wpriv + st * WST + g * 1024);
+      for (int g = 0; g < GW; ++g) dma16s(a.wd + (t - KT) * BK, woffd[g], wpriv + st * WST + g * 1024);
+    } else {
+#pragma unroll
+      for (int g = 0; g < GW; ++g) dma16s(wbase + t * BK, woff[g], wpriv + st * WST + g * 1024);
+    }
   };
 #pragma unroll
   for (int t = 0; t < ND - 1; ++t) load_wtile(t, t);
@@ -223,11 +242,15 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream_kernel(StreamConvArgs a
               (S == 1 && pcol == W - 1 ? 8 : 0);
     asm volatile("" : "+v"(xoff[f]));  // keep it live: rematerialising p / W in the loop cost ~100 VALU per K-tile
   }
-  floatx4 acc[MF][NF];
+  floatx4 acc[MF][NF], accd[DS ? MF : 1][NF];
 #pragma unroll
   for (int f = 0; f < MF; ++f)
 #pragma unroll
     for (int nf = 0; nf < NF; ++nf) acc[f][nf] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int f = 0; f < (DS ? MF : 1); ++f)
+#pragma unroll
+    for (int nf = 0; nf < NF; ++nf) accd[f][nf] = floatx4{0.f, 0.f, 0.f, 0.f};
 
   // per-tap fragment bases xa[f] and lane swizzle tsw = 16 fq ^ 16 xswz(K):
   // K = p + ktap with p & 15 == fr for every real pixel (fragments start at
@@ -281,12 +304,14 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream_kernel(StreamConvArgs a
 #pragma unroll
     for (int cc = 0; cc < CT; ++cc) {
       const int t = tap * CT + cc;
-      if (t + 1 < KT) vm_wait<0>();
-      if (t + ND - 1 < KT) load_wtile(t + ND - 1, st == 0 ? ND - 1 : st - 1);
+      if (t + 1 < KT2) vm_wait<0>();
+      if (t + ND - 1 < KT2) load_wtile(t + ND - 1, st == 0 ? ND - 1 : st - 1);
       const int st1 = st == ND - 1 ? 0 : st + 1;
       // next K-tile's X: same tap at cc+1, or the next tap's first (the
-      // final iteration re-reads a valid tile, unused)
+      // final iteration re-reads a valid tile, unused; with DS it reads the
+      // downsample's first, tap (1,1))
       if (cc + 1 == CT && tap + 1 < 9) set_tap(tap + 1);
+      if (DS && cc + 1 == CT && tap == 8) set_tap(4);
       const int cn = cc + 1 == CT ? 0 : cc + 1;
       bf16x8 wn[NF];
       wread(wn, st1);
@@ -299,6 +324,35 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream_kernel(StreamConvArgs a
 #pragma unroll
         for (int nf = 0; nf < NF; ++nf)
           acc[f][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[nf], xf[f], acc[f][nf], 0, 0, 0);
+        xf[f] = xread(f, cn);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x100, NF, 0);
+#pragma unroll
+      for (int f = 0; f < MF; ++f) {
+        __builtin_amdgcn_sched_group_barrier(0x008, NF, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+#pragma unroll
+      for (int nf = 0; nf < NF; ++nf) wf[nf] = wn[nf];
+      st = st1;
+    }
+  }
+  if constexpr (DS) {  // the downsample's K-tiles, same pipeline
+#pragma unroll
+    for (int cc = 0; cc < CT; ++cc) {
+      const int t = KT + cc;
+      if (t + 1 < KT2) vm_wait<0>();
+      if (t + ND - 1 < KT2) load_wtile(t + ND - 1, st == 0 ? ND - 1 : st - 1);
+      const int st1 = st == ND - 1 ? 0 : st + 1;
+      const int cn = cc + 1 == CT ? 0 : cc + 1;
+      bf16x8 wn[NF];
+      wread(wn, st1);
+      __builtin_amdgcn_s_waitcnt(0xC07F | (NF << 8));
+#pragma unroll
+      for (int f = 0; f < MF; ++f) {
+#pragma unroll
+        for (int nf = 0; nf < NF; ++nf)
+          accd[f][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[nf], xf[f], accd[f][nf], 0, 0, 0);
         xf[f] = xread(f, cn);
       }
       __builtin_amdgcn_sched_group_barrier(0x100, NF, 0);
@@ -357,6 +411,23 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream_kernel(StreamConvArgs a
     }
     *(uint4*)(a.y + off) = pack8(v);
   }
+  if constexpr (DS) {
+    float bd[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bd[e] = a.bd[ch0 + 8 * fq + e];
+#pragma unroll
+    for (int f = 0; f < MF; ++f) {
+      const int p = 16 * (wm * MF + f) + fr;
+      if (p >= npix) continue;
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] = accd[f][0][e] + bd[e];
+        v[4 + e] = accd[f][1][e] + bd[4 + e];
+      }
+      *(uint4*)(a.yd + base + (long)p * CO) = pack8(v);
+    }
+  }
   if (a.stamps && tid == 0) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     unsigned long long* sp = a.stamps + blockIdx.x * 4;
@@ -372,8 +443,15 @@ void launch_stream(const StreamConvArgs& a, hipStream_t s) {
   constexpr size_t lds = StreamGeom<H, W, CI, HS, IMG, S, 3>::LDS;
   static_assert(lds <= 160 * 1024, "LDS budget");
   const int grid = (a.B + IMG - 1) / IMG * (H / HS) * NSP;
-  hipLaunchKernelGGL((conv3x3_stream_kernel<H, W, CI, CO, HS, IMG, NSP, WM, S, 3>), dim3(grid), dim3(512), lds, s,
-                     a);
+  if constexpr (S == 2) {
+    if (a.yd) {
+      hipLaunchKernelGGL((conv3x3_stream_kernel<H, W, CI, CO, HS, IMG, NSP, WM, S, 3, true>), dim3(grid), dim3(512),
+                         lds, s, a);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((conv3x3_stream_kernel<H, W, CI, CO, HS, IMG, NSP, WM, S, 3, false>), dim3(grid), dim3(512), lds,
+                     s, a);
 }
 
 }  // namespace
@@ -383,13 +461,14 @@ bool conv3x3_stream_supported(int Hin, int Win, int Cin, int Cout, int stride) {
     return Cin == Cout && ((Hin == 28 && Win == 28 && Cin == 128) || (Hin == 14 && Win == 14 && Cin == 256) ||
                            (Hin == 7 && Win == 7 && Cin == 512));
   if (stride == 2)
-    return Cout == 2 * Cin && ((Hin == 56 && Win == 56 && Cin == 64) || (Hin == 28 && Win == 28 && Cin == 128));
+    return Cout == 2 * Cin && ((Hin == 56 && Win == 56 && Cin == 64) || (Hin == 28 && Win == 28 && Cin == 128) ||
+                               (Hin == 14 && Win == 14 && Cin == 256));
   return false;
 }
 
 void conv3x3_stream(const void* x, const void* w, const float* bias, const void* res, void* y, const void* zero,
                     int B, int Hin, int Win, int Cin, int Cout, int stride, bool relu, hipStream_t s,
-                    unsigned long long* stamps) {
+                    unsigned long long* stamps, const void* wd, const float* bd, void* yd) {
   if (B <= 0) return;
   if (!conv3x3_stream_supported(Hin, Win, Cin, Cout, stride))
     throw std::invalid_argument("conv3x3_stream: unsupported shape");
@@ -406,6 +485,11 @@ void conv3x3_stream(const void* x, const void* w, const float* bias, const void*
   a.B = B;
   a.relu = relu;
   a.stamps = stamps;
+  a.wd = (const bf16*)wd;
+  a.bd = bd;
+  a.yd = (bf16*)yd;
+  if (yd && (stride != 2 || !wd || !bd || (((uintptr_t)wd | (uintptr_t)yd) & 15)))
+    throw std::invalid_argument("conv3x3_stream: fused downsample needs stride 2 and aligned wd / yd");
   // LDS per workgroup: staged input rows + zero pixel + 8 waves x 3 x 2 KB weight stages
   if (stride == 1 && Cin == 128)  // layer2: half an image (15 x 28 x 256 B = 105 KB)
     launch_stream<28, 28, 128, 128, 14, 1, 1, 2, 1>(a, s);
@@ -415,8 +499,10 @@ void conv3x3_stream(const void* x, const void* w, const float* bias, const void*
     launch_stream<7, 7, 512, 512, 7, 2, 2, 1, 1>(a, s);
   else if (Cin == 64)  // layer2.0.conv1: a quarter image (15 x 56 x 128 B = 105 KB)
     launch_stream<28, 28, 64, 128, 7, 1, 1, 2, 2>(a, s);
-  else  // layer3.0.conv1: half an image (15 x 28 x 256 B = 105 KB)
+  else if (Cin == 128)  // layer3.0.conv1: half an image (15 x 28 x 256 B = 105 KB)
     launch_stream<14, 14, 128, 256, 7, 1, 1, 1, 2>(a, s);
+  else  // layer4.0.conv1: a whole image (14 x 14 x 512 B = 98 KB) x half the output channels
+    launch_stream<7, 7, 256, 512, 7, 1, 2, 1, 2>(a, s);
   DMLC_HIP_CHECK(hipGetLastError());
 }
 

@@ -131,9 +131,12 @@ void conv3x3_rows(const void* x, const void* w, const float* bias, const void* r
 // stride 2 on 56x56x64 -> 128 and 28x28x128 -> 256. Hin/Win are the input
 // dims; same operand layouts as conv2d_igemm.
 bool conv3x3_stream_supported(int Hin, int Win, int Cin, int Cout, int stride = 1);
+// Stride 2 may also compute the block's 1x1/s2 downsample conv (wd [Cout,
+// Cin], bias bd, no ReLU) from the same resident input into yd.
 void conv3x3_stream(const void* x, const void* w, const float* bias, const void* res, void* y, const void* zero,
                     int B, int Hin, int Win, int Cin, int Cout, int stride, bool relu, hipStream_t s,
-                    unsigned long long* stamps = nullptr);
+                    unsigned long long* stamps = nullptr, const void* wd = nullptr, const float* bd = nullptr,
+                    void* yd = nullptr);
 int stem_pool_pick_strip(int B, int PH, int num_cus);
 void stem_conv_pool(const void* x, const void* w, const float* bias, void* y, int B, int S, int Wq, int strip,
                     hipStream_t s);

@@ -88,6 +88,8 @@ Engine::Engine(const std::string& arch, const WeightMap& weights, int device, in
   if (const char* e = std::getenv("DMLC_STREAM_CONV")) stream_conv_ = std::string(e) != "0";
   if (const char* e = std::getenv("DMLC_FORK_DS")) fork_ds_ = std::string(e) != "0";
   if (const char* e = std::getenv("DMLC_FUSED_HEAD")) fused_head_ = std::string(e) != "0";
+  if (const char* e = std::getenv("DMLC_FUSE_DS")) fuse_ds_ = std::string(e) != "0";
+  if (const char* e = std::getenv("DMLC_STREAM_L4S2")) stream_l4s2_ = std::string(e) != "0";
 
   if (arch == "resnet18")
     build_resnet({2, 2, 2, 2}, false);
@@ -543,7 +545,12 @@ Engine::ConvPath Engine::conv_path(const Op& op, int B) const {
                   !shapes_[op.out].fp8;
   // the stream conv runs 1-4 workgroups per image (or image pair): only
   // worth it once the batch fills the CUs
-  if (stream_conv_ && k3 && 8 * B >= num_cus_ && conv3x3_stream_supported(is.H, is.W, is.C, L.cout, L.stride))
+  // 14x14x256 -> 7x7x512 / s2 (layer4.0.conv1) runs 2 rounds of single-image
+  // workgroups with 49 of 64 fragment rows live: 67.9 us with the fused
+  // downsample vs 44.2 + 13.3 us as two implicit GEMMs (profiles/r1_fused_ds.txt)
+  const bool l4s2 = L.stride == 2 && is.H < 28 && !stream_l4s2_;
+  if (stream_conv_ && k3 && !l4s2 && 8 * B >= num_cus_ &&
+      conv3x3_stream_supported(is.H, is.W, is.C, L.cout, L.stride))
     return ConvPath::Stream;
   if (row_conv_ && k3 && L.stride == 1 && conv3x3_rows_supported(is.H, is.W, is.C, L.cout)) return ConvPath::Rows;
   if (bigtile_ && conv_bigtile_pick(conv_args(op, B, nullptr), num_cus_) >= 0) return ConvPath::BigTile;
@@ -561,6 +568,20 @@ bool Engine::head_fusable(size_t oi) const {
   return L.fc && !L.fp8 && !L.relu && L.cin == shapes_[pool.in].C && head_supported(L.cin, L.cout, L.kpad, L.npad);
 }
 
+// ops[oi] is a block's downsample (1x1/s2, BN, no ReLU) and ops[oi+1] the
+// block's 3x3/s2 conv1 on the same input, run by the stream conv.
+bool Engine::ds_fusable(size_t oi, int B) const {
+  if (oi + 1 >= ops_.size()) return false;
+  const Op& d = ops_[oi];
+  const Op& c = ops_[oi + 1];
+  if (d.type != OpType::Conv || c.type != OpType::Conv || d.in != c.in) return false;
+  const ConvLayer& D = convs_[d.conv];
+  const ConvLayer& L = convs_[c.conv];
+  return !D.fc && !D.fp8 && D.kh == 1 && D.kw == 1 && D.stride == 2 && D.pad == 0 && !D.relu && d.res < 0 &&
+         D.cout == L.cout && L.stride == 2 && !shapes_[d.out].fp8 && !shapes_[d.out].f32 &&
+         conv_path(c, B) == ConvPath::Stream;
+}
+
 bool Engine::side_safe(int B) const {
   for (const Op& op : ops_)
     if (op.type == OpType::Conv && conv_path(op, B) == ConvPath::BigTile) return false;
@@ -575,6 +596,7 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
   const bool side_ready = fork_ds_ && !evs && side_safe(B);
   std::map<int, hipEvent_t> joined;  // activation -> event its side-stream producer recorded
   int skip = 0;                      // ops already done by a fused kernel
+  int skip_ds = -1;                  // downsample op left to the next (stream) conv
   for (size_t oi = 0; oi < ops_.size(); ++oi) {
     const Op& op = ops_[oi];
     if (skip > 0) {
@@ -600,6 +622,10 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
         // block's conv1 (both read the block input; conv2 joins them through
         // the residual). Never next to a big-tile conv: its split-K slices
         // spin on each other and need their CUs.
+        if (fuse_ds_ && op.side && ds_fusable(oi, B)) {
+          skip_ds = (int)oi;  // computed by the next op (the block's stride-2 conv1)
+          break;
+        }
         hipStream_t cs = s;
         if (side_ready && op.side) {
           DMLC_HIP_CHECK(hipEventRecord(fork_evs_[oi], s));
@@ -611,11 +637,22 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
           joined.erase(op.res);
         }
         switch (conv_path(op, B)) {
-          case ConvPath::Stream:
+          case ConvPath::Stream: {
+            const ConvLayer* D = nullptr;
+            int yd = -1;
+            if (skip_ds >= 0 && skip_ds + 1 == (int)oi) {
+              D = &convs_[ops_[skip_ds].conv];
+              yd = ops_[skip_ds].out;
+            }
             conv3x3_stream(acts_[op.in], (const uint8_t*)warena_ + L.w_off,
                            (const float*)((const uint8_t*)warena_ + L.b_off), op.res >= 0 ? acts_[op.res] : nullptr,
-                           acts_[op.out], zero_, B, is.H, is.W, is.C, L.cout, L.stride, L.relu, cs);
+                           acts_[op.out], zero_, B, is.H, is.W, is.C, L.cout, L.stride, L.relu, cs, nullptr,
+                           D ? (const uint8_t*)warena_ + D->w_off : nullptr,
+                           D ? (const float*)((const uint8_t*)warena_ + D->b_off) : nullptr,
+                           D ? acts_[yd] : nullptr);
+            skip_ds = -1;
             break;
+          }
           case ConvPath::Rows:
             conv3x3_rows(acts_[op.in], (const uint8_t*)warena_ + L.w_off,
                          (const float*)((const uint8_t*)warena_ + L.b_off), op.res >= 0 ? acts_[op.res] : nullptr,

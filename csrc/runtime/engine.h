@@ -114,7 +114,8 @@ class Engine {
   enum class ConvPath { Stream, Rows, BigTile, Igemm };
   ConvPath conv_path(const Op& op, int B) const;
   bool side_safe(int B) const;
-  bool head_fusable(size_t oi) const;  // ops oi..oi+2 = avgpool, fc, softmax_top1 -> head_fused  // no big-tile (co-residency-dependent) conv at batch B
+  bool head_fusable(size_t oi) const;
+  bool ds_fusable(size_t oi, int B) const;  // ops oi, oi+1 = downsample + stride-2 stream conv1  // ops oi..oi+2 = avgpool, fc, softmax_top1 -> head_fused  // no big-tile (co-residency-dependent) conv at batch B
 
   std::string arch_;
   int device_ = 0;
@@ -130,6 +131,8 @@ class Engine {
   bool stream_conv_ = true; // direct 3x3 with streamed weights for 28x28x128 layers (env DMLC_STREAM_CONV=0 disables)
   bool row_conv_ = true;    // direct row-streaming 3x3 convs where supported (env DMLC_ROW_CONV=0 disables)
   bool fp8_ = false;        // resnet50_fp8
+  bool stream_l4s2_ = false;  // stream conv for 14x14x256 -> 512 / s2 (env DMLC_STREAM_L4S2=1; slower)
+  bool fuse_ds_ = true;     // downsample inside the stride-2 stream conv1 (env DMLC_FUSE_DS=0 disables)
   bool fused_head_ = true;  // avgpool+fc+softmax/top-1 as one kernel (env DMLC_FUSED_HEAD=0 disables)
   // downsample convs on a side stream (env DMLC_FORK_DS=1 enables): measured
   // slower (the branch slows its sibling conv1 by 10-12 us and adds ~10 us of

@@ -177,11 +177,14 @@ def conv3x3_rows(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, re
 
 
 def conv3x3_stream(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, res: torch.Tensor | None = None,
-                   relu: bool = True, stride: int = 1) -> torch.Tensor:
+                   relu: bool = True, stride: int = 1, downsample: tuple | None = None):
     """Direct 3x3/p1 conv (conv3x3_stream.hip) on NHWC bf16 with the conv2d
     packed weights; + bias (+ residual), ReLU. Stride 1: [B,28,28,128],
     [B,14,14,256], [B,7,7,512]; stride 2: [B,56,56,64] -> 128 channels,
-    [B,28,28,128] -> 256."""
+    [B,28,28,128] -> 256, [B,14,14,256] -> 512.
+
+    downsample=(wd_packed [Cout, Cin], bd): stride 2 only; also computes the
+    1x1/s2 conv + bias from the same resident input and returns (y, yd)."""
     _need_cuda(x, w_packed, bias, res)
     C = native()
     B, H, W, Cin = x.shape
@@ -195,10 +198,17 @@ def conv3x3_stream(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, 
         if BT_STAMPS is None:
             BT_STAMPS = torch.zeros(1 << 16, dtype=torch.int64, device=x.device)
         stamps = _ptr(BT_STAMPS)
+    yd = wd = bd = None
+    if downsample is not None:
+        wd, bd = downsample[0].contiguous(), downsample[1].float().contiguous()
+        _need_cuda(wd, bd)
+        if stride != 2 or tuple(wd.shape) != (Cout, Cin):
+            raise ValueError("conv3x3_stream: downsample needs stride 2 and weights [Cout, Cin]")
+        yd = torch.empty_like(y)
     C.conv3x3_stream(_ptr(x.contiguous()), _ptr(w_packed.contiguous()), _ptr(bias.float().contiguous()),
                      _ptr(None if res is None else res.contiguous()), _ptr(y), _ptr(_zero_page(x.device)), B, H, W,
-                     Cin, Cout, stride, relu, _stream(), stamps)
-    return y
+                     Cin, Cout, stride, relu, _stream(), stamps, _ptr(wd), _ptr(bd), _ptr(yd))
+    return y if downsample is None else (y, yd)
 
 
 FP8 = torch.float8_e4m3fn  # OCP e4m3 (gfx950), max 448

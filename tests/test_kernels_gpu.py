@@ -285,7 +285,7 @@ def test_conv3x3_stream(gpu, HW, C, B, res, relu):
 
 
 @pytest.mark.parametrize("HW,Cin,B,relu", [(56, 64, 1, True), (56, 64, 2, False), (28, 128, 1, True),
-                                          (28, 128, 3, False)])
+                                          (28, 128, 3, False), (14, 256, 1, True), (14, 256, 3, False)])
 def test_conv3x3_stream_stride2(gpu, HW, Cin, B, relu):
     """Stride-2 direct 3x3 conv (conv3x3_stream.hip: 56x56x64 -> 28x28x128 in
     quarter images, 28x28x128 -> 14x14x256 in half images, even-first column
@@ -303,6 +303,29 @@ def test_conv3x3_stream_stride2(gpu, HW, Cin, B, relu):
     torch.cuda.synchronize()
     assert y.shape == (B, HW // 2, HW // 2, Cout)
     assert _rel(_nchw(y.float().cpu()), ref) < 8e-3
+
+
+@pytest.mark.parametrize("HW,Cin,B", [(56, 64, 2), (28, 128, 3), (14, 256, 2)])
+def test_conv3x3_stream_fused_downsample(gpu, HW, Cin, B):
+    """Stride-2 stream conv that also computes the block's 1x1/s2 downsample
+    conv from its resident input (extra K-tiles on tap (1,1)) vs torch fp32;
+    the 3x3 output must equal the unfused kernel's bit for bit."""
+    g = torch.Generator().manual_seed(23)
+    Cout = 2 * Cin
+    x = torch.randn(B, Cin, HW, HW, generator=g).bfloat16().float()
+    w = (torch.randn(Cout, Cin, 3, 3, generator=g) / (9 * Cin) ** 0.5).bfloat16().float()
+    wd = (torch.randn(Cout, Cin, 1, 1, generator=g) / Cin ** 0.5).bfloat16().float()
+    bias = torch.randn(Cout, generator=g) * 0.1
+    bd = torch.randn(Cout, generator=g) * 0.1
+    ref_d = F.conv2d(x, wd, bd, 2, 0)
+    xg = _nhwc(x).bfloat16().to(gpu)
+    wp = ops.pack_conv_weight(w, device=gpu)
+    wdp = ops.pack_conv_weight(wd, device=gpu)
+    y0 = ops.conv3x3_stream(xg, wp, bias.to(gpu), None, True, stride=2)
+    y, yd = ops.conv3x3_stream(xg, wp, bias.to(gpu), None, True, stride=2, downsample=(wdp, bd.to(gpu)))
+    torch.cuda.synchronize()
+    assert torch.equal(y, y0)
+    assert _rel(_nchw(yd.float().cpu()), ref_d) < 8e-3
 
 
 @pytest.mark.parametrize("B,strip,res", [(2, None, False), (2, None, True), (3, 4, True), (1, 8, False),
