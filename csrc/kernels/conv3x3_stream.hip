@@ -459,7 +459,7 @@ void launch_stream(const StreamConvArgs& a, hipStream_t s) {
 bool conv3x3_stream_supported(int Hin, int Win, int Cin, int Cout, int stride) {
   if (stride == 1)
     return Cin == Cout && ((Hin == 28 && Win == 28 && Cin == 128) || (Hin == 14 && Win == 14 && Cin == 256) ||
-                           (Hin == 7 && Win == 7 && Cin == 512));
+                           (Hin == 7 && Win == 7 && Cin == 512) || (Hin == 56 && Win == 56 && Cin == 64));
   if (stride == 2)
     return Cout == 2 * Cin && ((Hin == 56 && Win == 56 && Cin == 64) || (Hin == 28 && Win == 28 && Cin == 128) ||
                                (Hin == 14 && Win == 14 && Cin == 256));
@@ -491,7 +491,9 @@ void conv3x3_stream(const void* x, const void* w, const float* bias, const void*
   if (yd && (stride != 2 || !wd || !bd || (((uintptr_t)wd | (uintptr_t)yd) & 15)))
     throw std::invalid_argument("conv3x3_stream: fused downsample needs stride 2 and aligned wd / yd");
   // LDS per workgroup: staged input rows + zero pixel + 8 waves x 3 x 2 KB weight stages
-  if (stride == 1 && Cin == 128)  // layer2: half an image (15 x 28 x 256 B = 105 KB)
+  if (stride == 1 && Cin == 64)  // layer1: 8-row strips (10 x 56 x 128 B = 70 KB), 4 pixel x 2 channel groups
+    launch_stream<56, 56, 64, 64, 8, 1, 1, 4, 1>(a, s);
+  else if (stride == 1 && Cin == 128)  // layer2: half an image (15 x 28 x 256 B = 105 KB)
     launch_stream<28, 28, 128, 128, 14, 1, 1, 2, 1>(a, s);
   else if (stride == 1 && Cin == 256)  // layer3: a whole image (14 x 14 x 512 B = 98 KB)
     launch_stream<14, 14, 256, 256, 14, 1, 1, 1, 1>(a, s);

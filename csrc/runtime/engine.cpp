@@ -90,6 +90,7 @@ Engine::Engine(const std::string& arch, const WeightMap& weights, int device, in
   if (const char* e = std::getenv("DMLC_FUSED_HEAD")) fused_head_ = std::string(e) != "0";
   if (const char* e = std::getenv("DMLC_FUSE_DS")) fuse_ds_ = std::string(e) != "0";
   if (const char* e = std::getenv("DMLC_STREAM_L4S2")) stream_l4s2_ = std::string(e) != "0";
+  if (const char* e = std::getenv("DMLC_STREAM_L1")) stream_l1_ = std::string(e) != "0";
 
   if (arch == "resnet18")
     build_resnet({2, 2, 2, 2}, false);
@@ -549,7 +550,8 @@ Engine::ConvPath Engine::conv_path(const Op& op, int B) const {
   // workgroups with 49 of 64 fragment rows live: 67.9 us with the fused
   // downsample vs 44.2 + 13.3 us as two implicit GEMMs (profiles/r1_fused_ds.txt)
   const bool l4s2 = L.stride == 2 && is.H < 28 && !stream_l4s2_;
-  if (stream_conv_ && k3 && !l4s2 && 8 * B >= num_cus_ &&
+  const bool l1 = L.stride == 1 && is.C == 64 && !stream_l1_;  // layer1: conv3x3_rows unless DMLC_STREAM_L1=1
+  if (stream_conv_ && k3 && !l4s2 && !l1 && 8 * B >= num_cus_ &&
       conv3x3_stream_supported(is.H, is.W, is.C, L.cout, L.stride))
     return ConvPath::Stream;
   if (row_conv_ && k3 && L.stride == 1 && conv3x3_rows_supported(is.H, is.W, is.C, L.cout)) return ConvPath::Rows;

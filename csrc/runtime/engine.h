@@ -131,6 +131,7 @@ class Engine {
   bool stream_conv_ = true; // direct 3x3 with streamed weights for 28x28x128 layers (env DMLC_STREAM_CONV=0 disables)
   bool row_conv_ = true;    // direct row-streaming 3x3 convs where supported (env DMLC_ROW_CONV=0 disables)
   bool fp8_ = false;        // resnet50_fp8
+  bool stream_l1_ = false;    // stream conv for 56x56x64 layer1 (env DMLC_STREAM_L1=1; slower than conv3x3_rows)
   bool stream_l4s2_ = false;  // stream conv for 14x14x256 -> 512 / s2 (env DMLC_STREAM_L4S2=1; slower)
   bool fuse_ds_ = true;     // downsample inside the stride-2 stream conv1 (env DMLC_FUSE_DS=0 disables)
   bool fused_head_ = true;  // avgpool+fc+softmax/top-1 as one kernel (env DMLC_FUSED_HEAD=0 disables)

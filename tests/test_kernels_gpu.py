@@ -261,7 +261,8 @@ def test_stem_conv_pool_u8(gpu, B, S, strip):
                                              (28, 128, 2, True, False), (28, 128, 5, False, False),
                                              (14, 256, 1, False, True), (14, 256, 3, True, True),
                                              (14, 256, 2, True, False), (7, 512, 1, False, True),
-                                             (7, 512, 3, True, True), (7, 512, 4, True, False)])
+                                             (7, 512, 3, True, True), (7, 512, 4, True, False),
+                                             (56, 64, 1, True, True), (56, 64, 2, False, True)])
 def test_conv3x3_stream(gpu, HW, C, B, res, relu):
     """Direct 3x3 conv with streamed weights (conv3x3_stream.hip: 28x28x128
     half images, 14x14x256 whole images, 7x7x512 image pairs x half the
