@@ -163,12 +163,16 @@ PYBIND11_MODULE(_C, m) {
         py::arg("Cout"), py::arg("stride") = 1);
   m.def("conv3x3_stream", [](uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t res, uintptr_t y, uintptr_t zero,
                              int B, int H, int W, int Cin, int Cout, int stride, bool relu, uintptr_t stream,
-                             uintptr_t stamps, uintptr_t wd, uintptr_t bd, uintptr_t yd) {
+                             uintptr_t stamps, uintptr_t wd, uintptr_t bd, uintptr_t yd, uintptr_t wfrag,
+                             uintptr_t wdfrag) {
     conv3x3_stream(P<void>(x), P<void>(w), P<float>(bias), P<void>(res), P<void>(y), P<void>(zero), B, H, W, Cin, Cout,
-                   stride, relu, S(stream), P<unsigned long long>(stamps), P<void>(wd), P<float>(bd), P<void>(yd));
+                   stride, relu, S(stream), P<unsigned long long>(stamps), P<void>(wd), P<float>(bd), P<void>(yd),
+                   P<void>(wfrag), P<void>(wdfrag));
   }, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("res"), py::arg("y"), py::arg("zero"), py::arg("B"),
         py::arg("H"), py::arg("W"), py::arg("Cin"), py::arg("Cout"), py::arg("stride"), py::arg("relu"),
-        py::arg("stream"), py::arg("stamps") = 0, py::arg("wd") = 0, py::arg("bd") = 0, py::arg("yd") = 0);
+        py::arg("stream"), py::arg("stamps") = 0, py::arg("wd") = 0, py::arg("bd") = 0, py::arg("yd") = 0,
+        py::arg("wfrag") = 0, py::arg("wdfrag") = 0);
+  m.def("conv3x3_stream_uses_frag", &conv3x3_stream_uses_frag);
   m.def("conv3x3_rows_supported", &conv3x3_rows_supported);
   m.def("conv3x3_rows_pick_strip", &conv3x3_rows_pick_strip);
   m.def("conv3x3_rows", [](uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t res, uintptr_t y, uintptr_t zero,

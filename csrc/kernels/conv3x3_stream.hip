@@ -59,6 +59,11 @@ struct StreamConvArgs {
   const bf16* wd;     // [CO, CI]
   const float* bd;    // [CO]
   bf16* yd;           // [B, H, W, CO]
+  // WR kernels: weights in fragment order, [CO/32][KT][2][64 lanes][8] (lane l of
+  // fragment nf of channel group g, K-tile t holds channel 32g + perm32(16nf +
+  // (l & 15)), k = 32t + 8(l >> 4) .. +7), loaded straight into VGPRs
+  const bf16* wf;
+  const bf16* wdf;    // WR + DS: the downsample weights in the same order, [CO/32][CI/32][2][64][8]
   int B;
   int relu;
   unsigned long long* stamps;  // debug: per-workgroup phase stamps (100 MHz), or null
@@ -108,7 +113,8 @@ struct StreamGeom {
   static constexpr size_t LDS = (size_t)XBYTES + (size_t)8 * ND * WST;
 };
 
-template <int H, int W, int CI, int CO, int HS, int IMG, int NSP, int WM, int S, int ND, bool DS>
+template <int H, int W, int CI, int CO, int HS, int IMG, int NSP, int WM, int S, int ND, bool DS, bool WR,
+          int PD = 4>
 __global__ __launch_bounds__(512, 1) void conv3x3_stream_kernel(StreamConvArgs a) {
   using G = StreamGeom<H, W, CI, HS, IMG, S, ND>;
   constexpr int BK = 32;                     // K-tile depth = one MFMA k-step
@@ -127,6 +133,9 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream_kernel(StreamConvArgs a
   // (x[S r, S c]), which is resident here: its CT K-tiles follow the 3x3's KT
   // in the same weight stream, on tap (1,1)'s X fragments, into accd.
   constexpr int KT2 = KT + (DS ? CT : 0);
+  // WR: each wave's weight fragments come from HBM/L2 in fragment order
+  // straight into a PD-deep register ring (no LDS stage, no DMA wait)
+  static_assert(!WR || CT % PD == 0, "WR: PD divides the K-tiles per tap");
   constexpr int GW = WST / 1024;             // weight DMA instructions per wave per K-tile
   static_assert(CO == 8 / WM * WN * NSP && WI * CPX % 64 == 0 && H % HS == 0 && CPX >= 8, "geometry");
   // (128-B pixels rely on the even/odd column halves starting on the same
@@ -216,6 +225,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream_kernel(StreamConvArgs a
   }
   const bf16* wbase = a.w;
   auto load_wtile = [&](int t, int st) __attribute__((always_inline)) {
+    if constexpr (WR) return;
     if (DS && t >= KT) {
 #pragma unroll
       for (int g = 0; g < GW; ++g) dma16s(a.wd + (t - KT) * BK, woffd[g], wpriv + st * WST + g * 1024);
@@ -224,8 +234,22 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream_kernel(StreamConvArgs a
       for (int g = 0; g < GW; ++g) dma16s(wbase + t * BK, woff[g], wpriv + st * WST + g * 1024);
     }
   };
+  bf16x8 wq[WR ? PD : 1][NF];
+  const bf16x8* wfp = (const bf16x8*)a.wf + (long)(ch0 / 32) * KT * NF * 64 + lane;
+  const bf16x8* wdfp = (const bf16x8*)a.wdf + (long)(ch0 / 32) * CT * NF * 64 + lane;
+  // fragment nf of K-tile t (the downsample's tiles follow the 3x3's)
+  auto wfrag = [&](int t, int nf) __attribute__((always_inline)) {
+    return (DS && t >= KT) ? wdfp[((t - KT) * NF + nf) * 64] : wfp[(t * NF + nf) * 64];
+  };
+  if constexpr (WR) {
 #pragma unroll
-  for (int t = 0; t < ND - 1; ++t) load_wtile(t, t);
+    for (int t = 0; t < PD - 1; ++t)
+#pragma unroll
+      for (int nf = 0; nf < NF; ++nf) wq[t][nf] = wfp[(t * NF + nf) * 64];
+  } else {
+#pragma unroll
+    for (int t = 0; t < ND - 1; ++t) load_wtile(t, t);
+  }
 
   // ---- per-lane constants: pixel p = 16(wm*MF + f) + fr (clamped for padding
   // lanes / a dummy last fragment: they compute a duplicate, never stored).
@@ -288,7 +312,10 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream_kernel(StreamConvArgs a
   // wave's own DMA of t+1 (issued one iteration earlier), then refills the
   // stage of t-1 (read during t-2, consumed by t-1's MFMAs) with t+2.
   set_tap(0);
-  vm_wait<(ND - 2) * GW>();  // own input rows and K-tile 0
+  if constexpr (WR)
+    vm_wait<(PD - 1) * NF>();  // own input rows (the weight loads were issued after them)
+  else
+    vm_wait<(ND - 2) * GW>();  // own input rows and K-tile 0
   __builtin_amdgcn_s_barrier();  // every wave's input rows
   asm volatile("" ::: "memory");
   if (a.stamps) {
@@ -296,7 +323,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream_kernel(StreamConvArgs a
     asm volatile("" ::"s"(t_first));
   }
   bf16x8 wf[NF], xf[MF];
-  wread(wf, 0);
+  if constexpr (!WR) wread(wf, 0);
 #pragma unroll
   for (int f = 0; f < MF; ++f) xf[f] = xread(f, 0);
   int st = 0;
@@ -304,8 +331,14 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream_kernel(StreamConvArgs a
 #pragma unroll
     for (int cc = 0; cc < CT; ++cc) {
       const int t = tap * CT + cc;
-      if (t + 1 < KT2) vm_wait<0>();
-      if (t + ND - 1 < KT2) load_wtile(t + ND - 1, st == 0 ? ND - 1 : st - 1);
+      if constexpr (WR) {
+        if (t + PD - 1 < KT2)
+#pragma unroll
+          for (int nf = 0; nf < NF; ++nf) wq[(cc + PD - 1) % PD][nf] = wfrag(t + PD - 1, nf);
+      } else {
+        if (t + 1 < KT2) vm_wait<0>();
+        if (t + ND - 1 < KT2) load_wtile(t + ND - 1, st == 0 ? ND - 1 : st - 1);
+      }
       const int st1 = st == ND - 1 ? 0 : st + 1;
       // next K-tile's X: same tap at cc+1, or the next tap's first (the
       // final iteration re-reads a valid tile, unused; with DS it reads the
@@ -314,26 +347,29 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream_kernel(StreamConvArgs a
       if (DS && cc + 1 == CT && tap == 8) set_tap(4);
       const int cn = cc + 1 == CT ? 0 : cc + 1;
       bf16x8 wn[NF];
-      wread(wn, st1);
+      if constexpr (!WR) wread(wn, st1);
       // everything but the two weight reads just issued: the X fragments (read
       // during the previous K-tile) have landed. One wait instead of the
       // compiler's one per fragment.
-      __builtin_amdgcn_s_waitcnt(0xC07F | (NF << 8));
+      __builtin_amdgcn_s_waitcnt(0xC07F | ((WR ? 0 : NF) << 8));
 #pragma unroll
       for (int f = 0; f < MF; ++f) {
 #pragma unroll
         for (int nf = 0; nf < NF; ++nf)
-          acc[f][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[nf], xf[f], acc[f][nf], 0, 0, 0);
+          acc[f][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(WR ? wq[cc % PD][nf] : wf[nf], xf[f], acc[f][nf], 0, 0,
+                                                               0);
         xf[f] = xread(f, cn);
       }
-      __builtin_amdgcn_sched_group_barrier(0x100, NF, 0);
+      if constexpr (!WR) __builtin_amdgcn_sched_group_barrier(0x100, NF, 0);
 #pragma unroll
       for (int f = 0; f < MF; ++f) {
         __builtin_amdgcn_sched_group_barrier(0x008, NF, 0);
         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
       }
+      if constexpr (!WR) {
 #pragma unroll
-      for (int nf = 0; nf < NF; ++nf) wf[nf] = wn[nf];
+        for (int nf = 0; nf < NF; ++nf) wf[nf] = wn[nf];
+      }
       st = st1;
     }
   }
@@ -341,28 +377,37 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream_kernel(StreamConvArgs a
 #pragma unroll
     for (int cc = 0; cc < CT; ++cc) {
       const int t = KT + cc;
-      if (t + 1 < KT2) vm_wait<0>();
-      if (t + ND - 1 < KT2) load_wtile(t + ND - 1, st == 0 ? ND - 1 : st - 1);
+      if constexpr (WR) {  // KT % PD == 0: tile t sits in slot cc % PD
+        if (t + PD - 1 < KT2)
+#pragma unroll
+          for (int nf = 0; nf < NF; ++nf) wq[(cc + PD - 1) % PD][nf] = wfrag(t + PD - 1, nf);
+      } else {
+        if (t + 1 < KT2) vm_wait<0>();
+        if (t + ND - 1 < KT2) load_wtile(t + ND - 1, st == 0 ? ND - 1 : st - 1);
+      }
       const int st1 = st == ND - 1 ? 0 : st + 1;
       const int cn = cc + 1 == CT ? 0 : cc + 1;
       bf16x8 wn[NF];
-      wread(wn, st1);
-      __builtin_amdgcn_s_waitcnt(0xC07F | (NF << 8));
+      if constexpr (!WR) wread(wn, st1);
+      __builtin_amdgcn_s_waitcnt(0xC07F | ((WR ? 0 : NF) << 8));
 #pragma unroll
       for (int f = 0; f < MF; ++f) {
 #pragma unroll
         for (int nf = 0; nf < NF; ++nf)
-          accd[f][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[nf], xf[f], accd[f][nf], 0, 0, 0);
+          accd[f][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(WR ? wq[cc % PD][nf] : wf[nf], xf[f], accd[f][nf], 0,
+                                                                0, 0);
         xf[f] = xread(f, cn);
       }
-      __builtin_amdgcn_sched_group_barrier(0x100, NF, 0);
+      if constexpr (!WR) __builtin_amdgcn_sched_group_barrier(0x100, NF, 0);
 #pragma unroll
       for (int f = 0; f < MF; ++f) {
         __builtin_amdgcn_sched_group_barrier(0x008, NF, 0);
         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
       }
+      if constexpr (!WR) {
 #pragma unroll
-      for (int nf = 0; nf < NF; ++nf) wf[nf] = wn[nf];
+        for (int nf = 0; nf < NF; ++nf) wf[nf] = wn[nf];
+      }
       st = st1;
     }
   }
@@ -438,20 +483,30 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream_kernel(StreamConvArgs a
   }
 }
 
-template <int H, int W, int CI, int CO, int HS, int IMG, int NSP, int WM, int S>
+template <int H, int W, int CI, int CO, int HS, int IMG, int NSP, int WM, int S, bool WR = false, int PD = 4>
 void launch_stream(const StreamConvArgs& a, hipStream_t s) {
-  constexpr size_t lds = StreamGeom<H, W, CI, HS, IMG, S, 3>::LDS;
+  using G = StreamGeom<H, W, CI, HS, IMG, S, 3>;
+  constexpr size_t lds = WR ? (size_t)G::XBYTES : G::LDS;
   static_assert(lds <= 160 * 1024, "LDS budget");
   const int grid = (a.B + IMG - 1) / IMG * (H / HS) * NSP;
+  if constexpr (WR) {
+    if (a.yd)
+      hipLaunchKernelGGL((conv3x3_stream_kernel<H, W, CI, CO, HS, IMG, NSP, WM, S, 3, true, true, PD>), dim3(grid),
+                         dim3(512), lds, s, a);
+    else
+      hipLaunchKernelGGL((conv3x3_stream_kernel<H, W, CI, CO, HS, IMG, NSP, WM, S, 3, false, true, PD>), dim3(grid),
+                         dim3(512), lds, s, a);
+    return;
+  }
   if constexpr (S == 2) {
     if (a.yd) {
-      hipLaunchKernelGGL((conv3x3_stream_kernel<H, W, CI, CO, HS, IMG, NSP, WM, S, 3, true>), dim3(grid), dim3(512),
-                         lds, s, a);
+      hipLaunchKernelGGL((conv3x3_stream_kernel<H, W, CI, CO, HS, IMG, NSP, WM, S, 3, true, false>), dim3(grid),
+                         dim3(512), lds, s, a);
       return;
     }
   }
-  hipLaunchKernelGGL((conv3x3_stream_kernel<H, W, CI, CO, HS, IMG, NSP, WM, S, 3, false>), dim3(grid), dim3(512), lds,
-                     s, a);
+  hipLaunchKernelGGL((conv3x3_stream_kernel<H, W, CI, CO, HS, IMG, NSP, WM, S, 3, false, false>), dim3(grid), dim3(512),
+                     lds, s, a);
 }
 
 }  // namespace
@@ -466,9 +521,20 @@ bool conv3x3_stream_supported(int Hin, int Win, int Cin, int Cout, int stride) {
   return false;
 }
 
+// Register weights only where the LDS-ring variant leaves VGPRs for the ring:
+// the 28x28x128 / 14x14x256 kernels (240 / 248 VGPRs) spill 34-57 VGPRs with
+// even a 2-deep register ring and ran 1.7-2x slower (profiles/r1_stream_conv.log).
+bool conv3x3_stream_uses_frag(int Hin, int Win, int Cin, int Cout, int stride) {
+  // 56x56x64 / s2 (K-tiles per tap = 2, so a 2-deep ring): 83.8 vs 71.0 us
+  // with the LDS ring, not used; 28x28x128 / s2: 48.6 vs 53.6 us
+  if (stride == 2) return Cout == 2 * Cin && Hin == 28 && Win == 28 && Cin == 128;
+  return stride == 1 && Cin == Cout && Hin == 7 && Win == 7 && Cin == 512;
+}
+
 void conv3x3_stream(const void* x, const void* w, const float* bias, const void* res, void* y, const void* zero,
                     int B, int Hin, int Win, int Cin, int Cout, int stride, bool relu, hipStream_t s,
-                    unsigned long long* stamps, const void* wd, const float* bd, void* yd) {
+                    unsigned long long* stamps, const void* wd, const float* bd, void* yd, const void* wfrag,
+                    const void* wdfrag) {
   if (B <= 0) return;
   if (!conv3x3_stream_supported(Hin, Win, Cin, Cout, stride))
     throw std::invalid_argument("conv3x3_stream: unsupported shape");
@@ -488,6 +554,11 @@ void conv3x3_stream(const void* x, const void* w, const float* bias, const void*
   a.wd = (const bf16*)wd;
   a.bd = bd;
   a.yd = (bf16*)yd;
+  a.wf = (const bf16*)wfrag;
+  a.wdf = (const bf16*)wdfrag;
+  if (wfrag && (!conv3x3_stream_uses_frag(Hin, Win, Cin, Cout, stride) || ((uintptr_t)wfrag & 15) ||
+                (yd && (!wdfrag || ((uintptr_t)wdfrag & 15)))))
+    throw std::invalid_argument("conv3x3_stream: no register-weight variant for this call");
   if (yd && (stride != 2 || !wd || !bd || (((uintptr_t)wd | (uintptr_t)yd) & 15)))
     throw std::invalid_argument("conv3x3_stream: fused downsample needs stride 2 and aligned wd / yd");
   // LDS per workgroup: staged input rows + zero pixel + 8 waves x 3 x 2 KB weight stages
@@ -497,10 +568,14 @@ void conv3x3_stream(const void* x, const void* w, const float* bias, const void*
     launch_stream<28, 28, 128, 128, 14, 1, 1, 2, 1>(a, s);
   else if (stride == 1 && Cin == 256)  // layer3: a whole image (14 x 14 x 512 B = 98 KB)
     launch_stream<14, 14, 256, 256, 14, 1, 1, 1, 1>(a, s);
+  else if (stride == 1 && wfrag)  // layer4, weights in fragment order straight into VGPRs
+    launch_stream<7, 7, 512, 512, 7, 2, 2, 1, 1, true>(a, s);
   else if (stride == 1)  // layer4: two whole images x half the output channels (2 x 49 x 1 KB = 98 KB)
     launch_stream<7, 7, 512, 512, 7, 2, 2, 1, 1>(a, s);
   else if (Cin == 64)  // layer2.0.conv1: a quarter image (15 x 56 x 128 B = 105 KB)
     launch_stream<28, 28, 64, 128, 7, 1, 1, 2, 2>(a, s);
+  else if (Cin == 128 && wfrag)
+    launch_stream<14, 14, 128, 256, 7, 1, 1, 1, 2, true>(a, s);
   else if (Cin == 128)  // layer3.0.conv1: half an image (15 x 28 x 256 B = 105 KB)
     launch_stream<14, 14, 128, 256, 7, 1, 1, 1, 2>(a, s);
   else  // layer4.0.conv1: a whole image (14 x 14 x 512 B = 98 KB) x half the output channels

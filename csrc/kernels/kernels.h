@@ -136,7 +136,19 @@ bool conv3x3_stream_supported(int Hin, int Win, int Cin, int Cout, int stride = 
 void conv3x3_stream(const void* x, const void* w, const float* bias, const void* res, void* y, const void* zero,
                     int B, int Hin, int Win, int Cin, int Cout, int stride, bool relu, hipStream_t s,
                     unsigned long long* stamps = nullptr, const void* wd = nullptr, const float* bd = nullptr,
-                    void* yd = nullptr);
+                    void* yd = nullptr, const void* wfrag = nullptr, const void* wdfrag = nullptr);
+// wfrag: the same weights in fragment order (stream_weight_frag_layout), used
+// by the variants that load weights straight into VGPRs (7x7x512 stride 1)
+bool conv3x3_stream_uses_frag(int Hin, int Win, int Cin, int Cout, int stride);
+// [Cout, K] row-major bf16 -> fragment order [Cout/32][K/32][2][64][8]:
+// dst index of (n, k) for n < Cout, k < K (Cout % 32 == 0, K % 32 == 0)
+inline size_t stream_frag_index(int n, int k, int K) {
+  const int g = n / 32, r = n % 32;
+  // inverse of perm32: channel r of the group sits at tile row 16nf + rr
+  const int nf = (r >> 2) & 1, rr = ((r >> 3) << 2) | (r & 3);
+  const int t = k / 32, kk = k % 32, lane = (kk / 8) * 16 + rr, e = kk % 8;
+  return ((((size_t)g * (K / 32) + t) * 2 + nf) * 64 + lane) * 8 + e;
+}
 int stem_pool_pick_strip(int B, int PH, int num_cus);
 void stem_conv_pool(const void* x, const void* w, const float* bias, void* y, int B, int S, int Wq, int strip,
                     hipStream_t s);

@@ -91,6 +91,7 @@ Engine::Engine(const std::string& arch, const WeightMap& weights, int device, in
   if (const char* e = std::getenv("DMLC_FUSE_DS")) fuse_ds_ = std::string(e) != "0";
   if (const char* e = std::getenv("DMLC_STREAM_L4S2")) stream_l4s2_ = std::string(e) != "0";
   if (const char* e = std::getenv("DMLC_STREAM_L1")) stream_l1_ = std::string(e) != "0";
+  if (const char* e = std::getenv("DMLC_STREAM_WREG")) stream_wreg_ = std::string(e) != "0";
 
   if (arch == "resnet18")
     build_resnet({2, 2, 2, 2}, false);
@@ -360,6 +361,15 @@ void Engine::pack_weights(const WeightMap& w) {
       L.a_off = off;
       off = align_up(off + (size_t)L.npad * 4, 256);
     }
+    L.wf_off = 0;
+    // (3x3 convs the register-weight stream conv runs, and the 1x1/s2
+    // downsample it fuses next to a stride-2 one)
+    if (!L.fp8 && !L.fc && !L.pair && !L.stem_pool && L.in_act >= 0 && L.cout % 32 == 0 && L.kpad % 32 == 0 &&
+        ((L.kh == 3 && L.kw == 3) || (L.kh == 1 && L.kw == 1 && L.stride == 2)) &&
+        conv3x3_stream_uses_frag(shapes_[L.in_act].H, shapes_[L.in_act].W, shapes_[L.in_act].C, L.cout, L.stride)) {
+      L.wf_off = off;  // fragment-order copy for the register-weight stream conv
+      off = align_up(off + (size_t)L.cout * L.kpad * 2, 256);
+    }
   }
   weight_bytes_ = off;
   std::vector<uint8_t> host(off, 0);
@@ -422,6 +432,11 @@ void Engine::pack_weights(const WeightMap& w) {
         }
     }
     for (int n = 0; n < L.cout; ++n) pb[n] = bias[n];
+    if (L.wf_off) {
+      uint16_t* pf = (uint16_t*)(host.data() + L.wf_off);
+      for (int n = 0; n < L.cout; ++n)
+        for (int k = 0; k < L.kpad; ++k) pf[stream_frag_index(n, k, L.kpad)] = pw[(size_t)n * L.kpad + k];
+    }
     if (L.fp8) {
       // e4m3 weights with a per-output-channel scale; alpha = s_in * s_w[n]
       uint8_t* q = host.data() + L.w_off;
@@ -651,7 +666,10 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
                            acts_[op.out], zero_, B, is.H, is.W, is.C, L.cout, L.stride, L.relu, cs, nullptr,
                            D ? (const uint8_t*)warena_ + D->w_off : nullptr,
                            D ? (const float*)((const uint8_t*)warena_ + D->b_off) : nullptr,
-                           D ? acts_[yd] : nullptr);
+                           D ? acts_[yd] : nullptr,
+                           (L.wf_off && stream_wreg_ && (!D || D->wf_off)) ? (const uint8_t*)warena_ + L.wf_off
+                                                                          : nullptr,
+                           (D && D->wf_off && stream_wreg_) ? (const uint8_t*)warena_ + D->wf_off : nullptr);
             skip_ds = -1;
             break;
           }

@@ -45,6 +45,7 @@ struct ConvLayer {
   int in_act = -1;              // activation the conv reads
   bool fp8 = false;             // e4m3 weights (input activation is e4m3)
   size_t a_off = 0;             // fp8: alpha[n] = s_in * s_w[n] (fp32 [npad])
+  size_t wf_off = 0;            // weights in stream-conv fragment order (0 = none)
 };
 
 struct Op {
@@ -131,6 +132,7 @@ class Engine {
   bool stream_conv_ = true; // direct 3x3 with streamed weights for 28x28x128 layers (env DMLC_STREAM_CONV=0 disables)
   bool row_conv_ = true;    // direct row-streaming 3x3 convs where supported (env DMLC_ROW_CONV=0 disables)
   bool fp8_ = false;        // resnet50_fp8
+  bool stream_wreg_ = true;   // register-weight stream conv where available (env DMLC_STREAM_WREG=0 disables)
   bool stream_l1_ = false;    // stream conv for 56x56x64 layer1 (env DMLC_STREAM_L1=1; slower than conv3x3_rows)
   bool stream_l4s2_ = false;  // stream conv for 14x14x256 -> 512 / s2 (env DMLC_STREAM_L4S2=1; slower)
   bool fuse_ds_ = true;     // downsample inside the stride-2 stream conv1 (env DMLC_FUSE_DS=0 disables)

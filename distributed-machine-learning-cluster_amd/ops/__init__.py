@@ -176,8 +176,26 @@ def conv3x3_rows(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, re
     return y
 
 
+def stream_weight_frag(w_packed: torch.Tensor, cout: int | None = None) -> torch.Tensor:
+    """Packed conv weights [Npad, K] -> the stream conv's fragment order
+    [Cout/32][K/32][2][64 lanes][8]: lane l of fragment nf of channel group g,
+    K-tile t holds channel 32g + perm32(16nf + (l & 15)), k = 32t + 8(l >> 4)
+    + e, perm32(n) = 8((n & 15) >> 2) + 4(n >> 4) + (n & 3)."""
+    cout = w_packed.shape[0] if cout is None else cout
+    K = w_packed.shape[1]
+    n = torch.arange(32)
+    perm = 8 * ((n & 15) >> 2) + 4 * (n >> 4) + (n & 3)            # tile row -> channel
+    lane = torch.arange(64)
+    rows = perm[(torch.arange(2).view(2, 1) * 16 + (lane & 15).view(1, 64))]  # [nf, lane] -> channel in group
+    w = w_packed[:cout].view(cout // 32, 32, K // 32, 4, 8)          # [g, ch, t, kq, e]
+    kq = (lane >> 4).view(1, 64).expand(2, 64)
+    # advanced indices separated by a slice go first: [nf, lane, g, t, e]
+    out = w[:, rows.to(w.device), :, kq.to(w.device), :]
+    return out.permute(2, 3, 0, 1, 4).contiguous()
+
+
 def conv3x3_stream(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, res: torch.Tensor | None = None,
-                   relu: bool = True, stride: int = 1, downsample: tuple | None = None):
+                   relu: bool = True, stride: int = 1, downsample: tuple | None = None, frag: bool = False):
     """Direct 3x3/p1 conv (conv3x3_stream.hip) on NHWC bf16 with the conv2d
     packed weights; + bias (+ residual), ReLU. Stride 1: [B,28,28,128],
     [B,14,14,256], [B,7,7,512]; stride 2: [B,56,56,64] -> 128 channels,
@@ -205,9 +223,15 @@ def conv3x3_stream(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, 
         if stride != 2 or tuple(wd.shape) != (Cout, Cin):
             raise ValueError("conv3x3_stream: downsample needs stride 2 and weights [Cout, Cin]")
         yd = torch.empty_like(y)
+    wf = None
+    if frag:
+        if not C.conv3x3_stream_uses_frag(H, W, Cin, Cout, stride):
+            raise ValueError("conv3x3_stream: no register-weight variant for this shape")
+        wf = stream_weight_frag(w_packed)
+    wdf = stream_weight_frag(wd) if (frag and wd is not None) else None
     C.conv3x3_stream(_ptr(x.contiguous()), _ptr(w_packed.contiguous()), _ptr(bias.float().contiguous()),
                      _ptr(None if res is None else res.contiguous()), _ptr(y), _ptr(_zero_page(x.device)), B, H, W,
-                     Cin, Cout, stride, relu, _stream(), stamps, _ptr(wd), _ptr(bd), _ptr(yd))
+                     Cin, Cout, stride, relu, _stream(), stamps, _ptr(wd), _ptr(bd), _ptr(yd), _ptr(wf), _ptr(wdf))
     return y if downsample is None else (y, yd)
 
 

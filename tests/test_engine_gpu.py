@@ -128,3 +128,17 @@ def test_fused_head_and_side_stream_match_unfused(gpu, monkeypatch, B):
         near_tie = (top2[:, 0] - top2[:, 1]) < 1e-5
         assert torch.all((i == ri) | near_tie)
         assert torch.allclose(p, rp, rtol=1e-4, atol=1e-6)
+
+
+def test_engine_stream_path_matches_reference(gpu):
+    """B=64 fills the CUs, so the engine takes the stream convs (fused
+    downsample, register-weight layer4) that B=16 does not: vs fp32 torch."""
+    model = build("resnet18", seed=13, randomize_bn=True)
+    eng = InferenceEngine("resnet18", state_dict_f32(model), max_batch=64)
+    g = torch.Generator().manual_seed(14)
+    img = torch.randint(0, 256, (64, 224, 224, 3), generator=g, dtype=torch.uint8)
+    ref = _ref_logits(model, img)
+    idx, prob, logits = eng.predict(img.to(gpu), return_logits=True)
+    torch.cuda.synchronize()
+    rel = ((logits.cpu() - ref).norm() / ref.norm()).item()
+    assert rel < 3e-2, rel

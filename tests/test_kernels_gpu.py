@@ -306,6 +306,31 @@ def test_conv3x3_stream_stride2(gpu, HW, Cin, B, relu):
     assert _rel(_nchw(y.float().cpu()), ref) < 8e-3
 
 
+@pytest.mark.parametrize("HW,C,B,res", [(7, 512, 1, False), (7, 512, 3, True), (7, 512, 4, True)])
+def test_conv3x3_stream_register_weights(gpu, HW, C, B, res):
+    """Stride-1 stream convs with the weights in fragment order loaded
+    straight into VGPRs (WR variants) vs torch fp32, and bit-identical to the
+    LDS-ring variants (same MFMA order)."""
+    g = torch.Generator().manual_seed(24)
+    x = torch.randn(B, C, HW, HW, generator=g).bfloat16().float()
+    w = (torch.randn(C, C, 3, 3, generator=g) / (9 * C) ** 0.5).bfloat16().float()
+    bias = torch.randn(C, generator=g) * 0.1
+    ref = F.conv2d(x, w, bias, 1, 1)
+    r = None
+    if res:
+        r_nchw = torch.randn_like(ref).bfloat16().float()
+        ref = ref + r_nchw
+        r = _nhwc(r_nchw).bfloat16().to(gpu)
+    ref = F.relu(ref)
+    wp = ops.pack_conv_weight(w, device=gpu)
+    xg = _nhwc(x).bfloat16().to(gpu)
+    y = ops.conv3x3_stream(xg, wp, bias.to(gpu), r, True, frag=True)
+    y0 = ops.conv3x3_stream(xg, wp, bias.to(gpu), r, True)
+    torch.cuda.synchronize()
+    assert _rel(_nchw(y.float().cpu()), ref) < 8e-3
+    assert torch.equal(y, y0)
+
+
 @pytest.mark.parametrize("HW,Cin,B", [(56, 64, 2), (28, 128, 3), (14, 256, 2)])
 def test_conv3x3_stream_fused_downsample(gpu, HW, Cin, B):
     """Stride-2 stream conv that also computes the block's 1x1/s2 downsample
@@ -327,6 +352,12 @@ def test_conv3x3_stream_fused_downsample(gpu, HW, Cin, B):
     torch.cuda.synchronize()
     assert torch.equal(y, y0)
     assert _rel(_nchw(yd.float().cpu()), ref_d) < 8e-3
+    if dmlc.native().conv3x3_stream_uses_frag(HW, HW, Cin, Cout, 2):  # register-weight variant: same MFMA order
+        y2, yd2 = ops.conv3x3_stream(xg, wp, bias.to(gpu), None, True, stride=2, downsample=(wdp, bd.to(gpu)),
+                                     frag=True)
+        y3 = ops.conv3x3_stream(xg, wp, bias.to(gpu), None, True, stride=2, frag=True)
+        torch.cuda.synchronize()
+        assert torch.equal(y2, y0) and torch.equal(yd2, yd) and torch.equal(y3, y0)
 
 
 @pytest.mark.parametrize("B,strip,res", [(2, None, False), (2, None, True), (3, 4, True), (1, 8, False),

@@ -101,3 +101,27 @@ def test_stem_pool_lds_reads_conflict_free():
     for f in range(8):
         addr = [(16 * f + (l & 15) + (l >> 4)) * 16 for l in range(64)]
         assert _b128_ways(addr) == 1
+
+
+def test_stream_weight_frag_layout_matches_native_index():
+    """ops.stream_weight_frag (used by the kernel tests) and the engine's
+    stream_frag_index (C++, kernels.h) describe the same permutation: every
+    (channel, k) lands in the lane / element the WR stream conv reads."""
+    import torch
+    from dmlc import ops
+    cout, K = 64, 96
+    w = torch.arange(cout * K, dtype=torch.float32).view(cout, K)
+    f = ops.stream_weight_frag(w).reshape(-1)
+
+    def perm32(n):
+        return 8 * ((n & 15) >> 2) + 4 * (n >> 4) + (n & 3)
+
+    for g in range(cout // 32):
+        for t in range(K // 32):
+            for nf in range(2):
+                for lane in range(64):
+                    for e in range(8):
+                        idx = ((((g * (K // 32) + t) * 2 + nf) * 64 + lane) * 8) + e
+                        n = 32 * g + perm32(16 * nf + (lane & 15))
+                        k = 32 * t + 8 * (lane >> 4) + e
+                        assert f[idx] == w[n, k]
