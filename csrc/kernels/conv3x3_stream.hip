@@ -527,7 +527,7 @@ bool conv3x3_stream_supported(int Hin, int Win, int Cin, int Cout, int stride) {
 bool conv3x3_stream_uses_frag(int Hin, int Win, int Cin, int Cout, int stride) {
   // 56x56x64 / s2 (K-tiles per tap = 2, so a 2-deep ring): 83.8 vs 71.0 us
   // with the LDS ring, not used; 28x28x128 / s2: 48.6 vs 53.6 us
-  if (stride == 2) return Cout == 2 * Cin && Hin == 28 && Win == 28 && Cin == 128;
+  if (stride == 2) return Cout == 2 * Cin && ((Hin == 28 && Win == 28 && Cin == 128) || (Hin == 14 && Cin == 256));
   return stride == 1 && Cin == Cout && Hin == 7 && Win == 7 && Cin == 512;
 }
 
@@ -578,6 +578,8 @@ void conv3x3_stream(const void* x, const void* w, const float* bias, const void*
     launch_stream<14, 14, 128, 256, 7, 1, 1, 1, 2, true>(a, s);
   else if (Cin == 128)  // layer3.0.conv1: half an image (15 x 28 x 256 B = 105 KB)
     launch_stream<14, 14, 128, 256, 7, 1, 1, 1, 2>(a, s);
+  else if (wfrag)
+    launch_stream<7, 7, 256, 512, 7, 1, 2, 1, 2, true>(a, s);
   else  // layer4.0.conv1: a whole image (14 x 14 x 512 B = 98 KB) x half the output channels
     launch_stream<7, 7, 256, 512, 7, 1, 2, 1, 2>(a, s);
   DMLC_HIP_CHECK(hipGetLastError());

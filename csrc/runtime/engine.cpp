@@ -562,9 +562,10 @@ Engine::ConvPath Engine::conv_path(const Op& op, int B) const {
   // the stream conv runs 1-4 workgroups per image (or image pair): only
   // worth it once the batch fills the CUs
   // 14x14x256 -> 7x7x512 / s2 (layer4.0.conv1) runs 2 rounds of single-image
-  // workgroups with 49 of 64 fragment rows live: 67.9 us with the fused
-  // downsample vs 44.2 + 13.3 us as two implicit GEMMs (profiles/r1_fused_ds.txt)
-  const bool l4s2 = L.stride == 2 && is.H < 28 && !stream_l4s2_;
+  // workgroups with 49 of 64 fragment rows live: with the LDS weight ring and
+  // the fused downsample 67.9 us vs 44.2 + 13.3 us as two implicit GEMMs; with
+  // register weights 48.1 vs 13.2 + 46.3 us (profiles/r1_fused_ds.txt)
+  const bool l4s2 = L.stride == 2 && is.H < 28 && !(stream_l4s2_ && stream_wreg_);
   const bool l1 = L.stride == 1 && is.C == 64 && !stream_l1_;  // layer1: conv3x3_rows unless DMLC_STREAM_L1=1
   if (stream_conv_ && k3 && !l4s2 && !l1 && 8 * B >= num_cus_ &&
       conv3x3_stream_supported(is.H, is.W, is.C, L.cout, L.stride))

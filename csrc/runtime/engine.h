@@ -134,7 +134,7 @@ class Engine {
   bool fp8_ = false;        // resnet50_fp8
   bool stream_wreg_ = true;   // register-weight stream conv where available (env DMLC_STREAM_WREG=0 disables)
   bool stream_l1_ = false;    // stream conv for 56x56x64 layer1 (env DMLC_STREAM_L1=1; slower than conv3x3_rows)
-  bool stream_l4s2_ = false;  // stream conv for 14x14x256 -> 512 / s2 (env DMLC_STREAM_L4S2=1; slower)
+  bool stream_l4s2_ = true;   // stream conv for 14x14x256 -> 512 / s2, register weights only (env DMLC_STREAM_L4S2=0)
   bool fuse_ds_ = true;     // downsample inside the stride-2 stream conv1 (env DMLC_FUSE_DS=0 disables)
   bool fused_head_ = true;  // avgpool+fc+softmax/top-1 as one kernel (env DMLC_FUSED_HEAD=0 disables)
   // downsample convs on a side stream (env DMLC_FORK_DS=1 enables): measured
