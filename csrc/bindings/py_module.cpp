@@ -176,10 +176,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv3x3_rows_supported", &conv3x3_rows_supported);
   m.def("conv3x3_rows_pick_strip", &conv3x3_rows_pick_strip);
   m.def("conv3x3_rows", [](uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t res, uintptr_t y, uintptr_t zero,
-                           int B, int H, int W, int C, bool relu, int strip, uintptr_t stream) {
+                           int B, int H, int W, int C, bool relu, int strip, uintptr_t stream, uintptr_t wfrag) {
     conv3x3_rows(P<void>(x), P<void>(w), P<float>(bias), P<void>(res), P<void>(y), P<void>(zero), B, H, W, C, relu,
-                 strip, S(stream));
-  });
+                 strip, S(stream), P<void>(wfrag));
+  }, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("res"), py::arg("y"), py::arg("zero"), py::arg("B"),
+        py::arg("H"), py::arg("W"), py::arg("C"), py::arg("relu"), py::arg("strip"), py::arg("stream"),
+        py::arg("wfrag") = 0);
   m.def("stem_conv_pool_u8", [](uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y, int B, int S_, int strip,
                                 uintptr_t stream) {
     stem_conv_pool_u8(P<uint8_t>(x), P<void>(w), P<float>(bias), P<void>(y), B, S_, strip, S(stream));

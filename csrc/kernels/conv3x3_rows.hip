@@ -47,12 +47,17 @@ struct RowConvArgs {
   const bf16* res;    // [B, H, W, C] or null
   bf16* y;            // [B, H, W, C]
   const bf16* zero;   // >= 16 zero bytes
+  const bf16* wf;     // WR: weights in stream-conv fragment order [C/32][KS][2][64][8] (kernels.h)
   int H, strip;       // strip = output rows per workgroup (multiple of 4)
   int relu;
 };
 
-template <int W, int C>
-__global__ __launch_bounds__(256, 1) void conv3x3_rows_kernel(RowConvArgs a) {
+// WR: the weights are not resident in LDS; every wave streams its fragments
+// from L2 (fragment order, 1 KB coalesced per fragment) through a PD-deep
+// register ring, so the workgroup needs only the input ring (74 KB) and two
+// fit per CU (2 waves per SIMD instead of 1).
+template <int W, int C, bool WR>
+__global__ __launch_bounds__(256, WR ? 2 : 1) void conv3x3_rows_kernel(RowConvArgs a) {
   static_assert(C == 64, "layout below assumes 64 channels (8 chunks per pixel)");
   constexpr int R = 4;                // output rows per step
   constexpr int MF = R * W / 32;      // pixel fragments per wave (2 pixel halves)
@@ -66,7 +71,9 @@ __global__ __launch_bounds__(256, 1) void conv3x3_rows_kernel(RowConvArgs a) {
 
   extern __shared__ __attribute__((aligned(16))) uint4 smem[];
   char* wl = (char*)smem;
-  char* ring = wl + WB;
+  char* ring = wl + (WR ? 0 : WB);
+  constexpr int PD = 3;  // register ring depth (divides KS: the ring is periodic across steps)
+  static_assert(!WR || KS % PD == 0, "PD | KS");
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -85,7 +92,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3_rows_kernel(RowConvArgs a) {
   // consecutive channels 32*wg + 8g .. +7 (16-B output stores and residual
   // loads instead of two 8-B halves).
   auto perm = [](int n) { return (n & ~31) + 8 * ((n & 15) >> 2) + 4 * ((n >> 4) & 1) + (n & 3); };
-  for (int j = 0; j < WB / 16 / 256; ++j) {
+  for (int j = 0; j < (WR ? 0 : WB / 16 / 256); ++j) {
     const int i = j * 256 + tid;
     const int c2 = i & 3, n = (i >> 2) % C, ks = i / (4 * C);
     const bf16* src = a.w + (long)perm(n) * (9 * C) + ks * 32 + 8 * (c2 ^ wswz(n));
@@ -133,6 +140,19 @@ __global__ __launch_bounds__(256, 1) void conv3x3_rows_kernel(RowConvArgs a) {
   // weight fragment nf of this wave: rows n = wn*32 + 16nf + fr
   const uint32_t wrow = (uint32_t)(wn * 32 + fr) * 64 + ((g ^ wswz(fr)) << 4);
   const char* wbase = wl + wrow;
+  // WR: fragment nf of K step ks for this wave's channel group wn
+  // (buffer loads: lane offset in a VGPR, the fragment offset a scalar constant)
+  const __amdgpu_buffer_rsrc_t wrs = wave_rsrc(a.wf + (long)wn * KS * 2 * 64 * 8, KS * 2 * 1024);
+  auto wload = [&](int kf) __attribute__((always_inline)) {
+    return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, lane * 16, kf * 1024, 0));
+  };
+  bf16x8 wq[WR ? PD : 1][2];
+  if constexpr (WR) {
+#pragma unroll
+    for (int ks = 0; ks < PD - 1; ++ks)
+#pragma unroll
+      for (int nf = 0; nf < 2; ++nf) wq[ks][nf] = wload(ks * 2 + nf);
+  }
   // this lane's 8 output channels (see perm): bias of channel wn*32 + 8g + 4nf + i
   float bs[2][4];
 #pragma unroll
@@ -174,7 +194,8 @@ __global__ __launch_bounds__(256, 1) void conv3x3_rows_kernel(RowConvArgs a) {
       const int tap = ks >> 1, h = ks & 1;
       const int kh = tap / 3, kw = tap % 3;
 #pragma unroll
-      for (int nf = 0; nf < 2; ++nf) wd[nf] = *(const bf16x8*)(wbase + (ks * C + nf * 16) * 64);
+      for (int nf = 0; nf < 2; ++nf)
+        if constexpr (!WR) wd[nf] = *(const bf16x8*)(wbase + (ks * C + nf * 16) * 64);
 #pragma unroll
       for (int f = 0; f < MF; ++f) xd[f] = *(const bf16x8*)(ring + roff[f][kh] + colq[f][kw][h]);
     };
@@ -182,12 +203,18 @@ __global__ __launch_bounds__(256, 1) void conv3x3_rows_kernel(RowConvArgs a) {
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       if (ks + 1 < KS) load_k(ks + 1, wn2, xn);
+      if constexpr (WR) {  // K step ks + PD - 1 (wrapping into the next output step's first ones)
+        const int kl = (ks + PD - 1) % KS;
+#pragma unroll
+        for (int nf = 0; nf < 2; ++nf) wq[(ks + PD - 1) % PD][nf] = wload(kl * 2 + nf);
+      }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int f = 0; f < MF; ++f)
 #pragma unroll
         for (int nf = 0; nf < 2; ++nf)
-          acc[f][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wc[nf], xc[f], acc[f][nf], 0, 0, 0);
+          acc[f][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(WR ? wq[ks % PD][nf] : wc[nf], xc[f], acc[f][nf], 0,
+                                                               0, 0);
       __builtin_amdgcn_sched_barrier(0);
       if (ks + 1 < KS) {
 #pragma unroll
@@ -240,7 +267,7 @@ int conv3x3_rows_pick_strip(int B, int H, int num_cus) {
 }
 
 void conv3x3_rows(const void* x, const void* w, const float* bias, const void* res, void* y, const void* zero,
-                  int B, int H, int W, int C, bool relu, int strip, hipStream_t s) {
+                  int B, int H, int W, int C, bool relu, int strip, hipStream_t s, const void* wfrag) {
   if (B <= 0) return;
   if (!conv3x3_rows_supported(H, W, C, C)) throw std::invalid_argument("conv3x3_rows: unsupported shape");
   if (strip <= 0 || strip % 4 || H % strip) throw std::invalid_argument("conv3x3_rows: bad strip");
@@ -257,8 +284,14 @@ void conv3x3_rows(const void* x, const void* w, const float* bias, const void* r
   a.H = H;
   a.strip = strip;
   a.relu = relu;
-  const size_t lds = (size_t)9 * 64 * 64 * 2 + (size_t)10 * (56 + 2) * 64 * 2;
-  hipLaunchKernelGGL((conv3x3_rows_kernel<56, 64>), dim3(B * (H / strip)), dim3(256), lds, s, a);
+  a.wf = (const bf16*)wfrag;
+  if (wfrag && ((uintptr_t)wfrag & 15)) throw std::invalid_argument("conv3x3_rows: misaligned wfrag");
+  const size_t ring = (size_t)10 * (56 + 2) * 64 * 2;
+  if (wfrag)
+    hipLaunchKernelGGL((conv3x3_rows_kernel<56, 64, true>), dim3(B * (H / strip)), dim3(256), ring, s, a);
+  else
+    hipLaunchKernelGGL((conv3x3_rows_kernel<56, 64, false>), dim3(B * (H / strip)), dim3(256),
+                       (size_t)9 * 64 * 64 * 2 + ring, s, a);
   DMLC_HIP_CHECK(hipGetLastError());
 }
 

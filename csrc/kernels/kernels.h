@@ -124,8 +124,11 @@ constexpr int kStemPoolK = 224;
 // bf16 residual, NHWC in/out).
 bool conv3x3_rows_supported(int H, int W, int Cin, int Cout);
 int conv3x3_rows_pick_strip(int B, int H, int num_cus);
+// wfrag: the weights in fragment order (stream_frag_index, K = 9C) -> the
+// register-weight variant (no LDS weights, 2 workgroups per CU; pick the
+// strip for 2 x num_cus workgroups)
 void conv3x3_rows(const void* x, const void* w, const float* bias, const void* res, void* y, const void* zero,
-                  int B, int H, int W, int C, bool relu, int strip, hipStream_t s);
+                  int B, int H, int W, int C, bool relu, int strip, hipStream_t s, const void* wfrag = nullptr);
 // Direct 3x3/p1 conv with the input image resident in LDS and per-wave weight
 // rings (conv3x3_stream.hip): stride 1 on 28x28x128, 14x14x256, 7x7x512;
 // stride 2 on 56x56x64 -> 128 and 28x28x128 -> 256. Hin/Win are the input

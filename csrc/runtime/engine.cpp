@@ -92,6 +92,7 @@ Engine::Engine(const std::string& arch, const WeightMap& weights, int device, in
   if (const char* e = std::getenv("DMLC_STREAM_L4S2")) stream_l4s2_ = std::string(e) != "0";
   if (const char* e = std::getenv("DMLC_STREAM_L1")) stream_l1_ = std::string(e) != "0";
   if (const char* e = std::getenv("DMLC_STREAM_WREG")) stream_wreg_ = std::string(e) != "0";
+  if (const char* e = std::getenv("DMLC_ROWS_WREG")) rows_wreg_ = std::string(e) != "0";
 
   if (arch == "resnet18")
     build_resnet({2, 2, 2, 2}, false);
@@ -365,8 +366,11 @@ void Engine::pack_weights(const WeightMap& w) {
     // (3x3 convs the register-weight stream conv runs, and the 1x1/s2
     // downsample it fuses next to a stride-2 one)
     if (!L.fp8 && !L.fc && !L.pair && !L.stem_pool && L.in_act >= 0 && L.cout % 32 == 0 && L.kpad % 32 == 0 &&
-        ((L.kh == 3 && L.kw == 3) || (L.kh == 1 && L.kw == 1 && L.stride == 2)) &&
-        conv3x3_stream_uses_frag(shapes_[L.in_act].H, shapes_[L.in_act].W, shapes_[L.in_act].C, L.cout, L.stride)) {
+        (((L.kh == 3 && L.kw == 3) || (L.kh == 1 && L.kw == 1 && L.stride == 2)) &&
+             conv3x3_stream_uses_frag(shapes_[L.in_act].H, shapes_[L.in_act].W, shapes_[L.in_act].C, L.cout,
+                                      L.stride) ||
+         (L.kh == 3 && L.kw == 3 && L.stride == 1 && L.pad == 1 &&
+          conv3x3_rows_supported(shapes_[L.in_act].H, shapes_[L.in_act].W, shapes_[L.in_act].C, L.cout)))) {
       L.wf_off = off;  // fragment-order copy for the register-weight stream conv
       off = align_up(off + (size_t)L.cout * L.kpad * 2, 256);
     }
@@ -677,8 +681,9 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
           case ConvPath::Rows:
             conv3x3_rows(acts_[op.in], (const uint8_t*)warena_ + L.w_off,
                          (const float*)((const uint8_t*)warena_ + L.b_off), op.res >= 0 ? acts_[op.res] : nullptr,
-                         acts_[op.out], zero_, B, is.H, is.W, is.C, L.relu, conv3x3_rows_pick_strip(B, is.H, num_cus_),
-                         cs);
+                         acts_[op.out], zero_, B, is.H, is.W, is.C, L.relu,
+                         conv3x3_rows_pick_strip(B, is.H, (L.wf_off && rows_wreg_) ? 2 * num_cus_ : num_cus_), cs,
+                         (L.wf_off && rows_wreg_) ? (const uint8_t*)warena_ + L.wf_off : nullptr);
             break;
           case ConvPath::BigTile: {
             const ConvArgs a = conv_args(op, B, logits);

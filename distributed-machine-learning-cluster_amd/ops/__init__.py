@@ -159,20 +159,23 @@ def bigtile_error(device: torch.device) -> bool:
 
 
 def conv3x3_rows(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, res: torch.Tensor | None = None,
-                 relu: bool = True, strip: int | None = None) -> torch.Tensor:
+                 relu: bool = True, strip: int | None = None, frag: bool = False) -> torch.Tensor:
     """Direct 3x3/s1/p1 conv (conv3x3_rows.hip) on NHWC bf16 [B,56,56,64] with
-    the conv2d packed weights [64, 576]; + bias (+ residual), ReLU."""
+    the conv2d packed weights [64, 576]; + bias (+ residual), ReLU. frag: the
+    register-weight variant (weights in fragment order, 2 workgroups per CU)."""
     _need_cuda(x, w_packed, bias, res)
     C = native()
     B, H, W, Cin = x.shape
     if not C.conv3x3_rows_supported(H, W, Cin, w_packed.shape[0]):
         raise ValueError("conv3x3_rows: unsupported shape")
     if strip is None:
-        strip = C.conv3x3_rows_pick_strip(B, H, torch.cuda.get_device_properties(x.device).multi_processor_count)
+        cus = torch.cuda.get_device_properties(x.device).multi_processor_count
+        strip = C.conv3x3_rows_pick_strip(B, H, 2 * cus if frag else cus)
     y = torch.empty_like(x)
+    wf = stream_weight_frag(w_packed) if frag else None
     C.conv3x3_rows(_ptr(x.contiguous()), _ptr(w_packed.contiguous()), _ptr(bias.float().contiguous()),
                    _ptr(None if res is None else res.contiguous()), _ptr(y), _ptr(_zero_page(x.device)), B, H, W,
-                   Cin, relu, strip, _stream())
+                   Cin, relu, strip, _stream(), _ptr(wf))
     return y
 
 

@@ -380,6 +380,11 @@ def test_conv3x3_rows(gpu, B, strip, res):
     got = _nchw(y.float().cpu())
     assert _rel(got, ref) < 5e-3, _rel(got, ref)
     assert (got - ref).abs().max().item() < 0.1
+    # register-weight variant (weights from L2 in fragment order): same MFMA order
+    y2 = ops.conv3x3_rows(_nhwc(x).bfloat16().to(gpu), wp, bias.to(gpu),
+                          _nhwc(r).bfloat16().to(gpu) if res else None, True, strip, frag=True)
+    torch.cuda.synchronize()
+    assert torch.equal(y2, y)
 
 
 def test_preprocess_paired(gpu):
