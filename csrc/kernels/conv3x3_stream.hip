@@ -235,17 +235,22 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream_kernel(StreamConvArgs a
     }
   };
   bf16x8 wq[WR ? PD : 1][NF];
-  const bf16x8* wfp = (const bf16x8*)a.wf + (long)(ch0 / 32) * KT * NF * 64 + lane;
-  const bf16x8* wdfp = (const bf16x8*)a.wdf + (long)(ch0 / 32) * CT * NF * 64 + lane;
-  // fragment nf of K-tile t (the downsample's tiles follow the 3x3's)
+  // fragment nf of K-tile t (the downsample's tiles follow the 3x3's): buffer
+  // loads, lane offset in a VGPR and the fragment offset a scalar
+  // (non-WR kernels get descriptors of null pointers they never use)
+  const __amdgpu_buffer_rsrc_t wrs = wave_rsrc(a.wf + (long)(ch0 / 32) * KT * NF * 512, WR ? KT * NF * 1024 : 0);
+  const __amdgpu_buffer_rsrc_t wdrs =
+      wave_rsrc(a.wdf + (long)(ch0 / 32) * CT * NF * 512, (WR && DS) ? CT * NF * 1024 : 0);
   auto wfrag = [&](int t, int nf) __attribute__((always_inline)) {
-    return (DS && t >= KT) ? wdfp[((t - KT) * NF + nf) * 64] : wfp[(t * NF + nf) * 64];
+    const bool d = DS && t >= KT;
+    return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
+                                          d ? wdrs : wrs, lane * 16, ((d ? t - KT : t) * NF + nf) * 1024, 0));
   };
   if constexpr (WR) {
 #pragma unroll
     for (int t = 0; t < PD - 1; ++t)
 #pragma unroll
-      for (int nf = 0; nf < NF; ++nf) wq[t][nf] = wfp[(t * NF + nf) * 64];
+      for (int nf = 0; nf < NF; ++nf) wq[t][nf] = wfrag(t, nf);
   } else {
 #pragma unroll
     for (int t = 0; t < ND - 1; ++t) load_wtile(t, t);
@@ -490,10 +495,13 @@ void launch_stream(const StreamConvArgs& a, hipStream_t s) {
   static_assert(lds <= 160 * 1024, "LDS budget");
   const int grid = (a.B + IMG - 1) / IMG * (H / HS) * NSP;
   if constexpr (WR) {
-    if (a.yd)
-      hipLaunchKernelGGL((conv3x3_stream_kernel<H, W, CI, CO, HS, IMG, NSP, WM, S, 3, true, true, PD>), dim3(grid),
-                         dim3(512), lds, s, a);
-    else
+    if constexpr (S == 2) {
+      if (a.yd) {
+        hipLaunchKernelGGL((conv3x3_stream_kernel<H, W, CI, CO, HS, IMG, NSP, WM, S, 3, true, true, PD>), dim3(grid),
+                           dim3(512), lds, s, a);
+        return;
+      }
+    }
       hipLaunchKernelGGL((conv3x3_stream_kernel<H, W, CI, CO, HS, IMG, NSP, WM, S, 3, false, true, PD>), dim3(grid),
                          dim3(512), lds, s, a);
     return;
@@ -522,8 +530,9 @@ bool conv3x3_stream_supported(int Hin, int Win, int Cin, int Cout, int stride) {
 }
 
 // Register weights only where the LDS-ring variant leaves VGPRs for the ring:
-// the 28x28x128 / 14x14x256 kernels (240 / 248 VGPRs) spill 34-57 VGPRs with
-// even a 2-deep register ring and ran 1.7-2x slower (profiles/r1_stream_conv.log).
+// the 28x28x128 / 14x14x256 kernels (240 / 248 VGPRs) spill 17-57 VGPRs with
+// even a 2-deep register ring (pointer or buffer-load addressing) and ran
+// 1.7-2x slower (profiles/r1_stream_conv.log).
 bool conv3x3_stream_uses_frag(int Hin, int Win, int Cin, int Cout, int stride) {
   // 56x56x64 / s2 (K-tiles per tap = 2, so a 2-deep ring): 83.8 vs 71.0 us
   // with the LDS ring, not used; 28x28x128 / s2: 48.6 vs 53.6 us
