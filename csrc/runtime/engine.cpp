@@ -93,6 +93,7 @@ Engine::Engine(const std::string& arch, const WeightMap& weights, int device, in
   if (const char* e = std::getenv("DMLC_STREAM_L1")) stream_l1_ = std::string(e) != "0";
   if (const char* e = std::getenv("DMLC_STREAM_WREG")) stream_wreg_ = std::string(e) != "0";
   if (const char* e = std::getenv("DMLC_ROWS_WREG")) rows_wreg_ = std::string(e) != "0";
+  if (const char* e = std::getenv("DMLC_GRAPH_DIRECT")) graph_direct_ = std::string(e) != "0";
 
   if (arch == "resnet18")
     build_resnet({2, 2, 2, 2}, false);
@@ -762,6 +763,28 @@ void Engine::forward(const uint8_t* images, int B, int Hin, int Win, int32_t* id
   if (B > max_batch_) throw std::invalid_argument("batch exceeds reserved max_batch");
   if (!images) throw std::invalid_argument("null images");
   DMLC_HIP_CHECK(hipSetDevice(device_));
+  if (use_graph && graph_direct_) {
+    // Replays go straight onto the caller's stream: no event hop to the
+    // engine's stream and back (two cross-stream waits cost ~40 us of idle
+    // GPU between back-to-back forwards: profiles/r1_graph_gap.txt). The
+    // engine's own stream is only used to capture.
+    GraphKey key{images, B, Hin, Win, idx, prob, logits};
+    auto it = graphs_.find(key);
+    if (it == graphs_.end()) {
+      DMLC_HIP_CHECK(hipStreamSynchronize(stream));
+      hipGraph_t g;
+      DMLC_HIP_CHECK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
+      run_ops(images, B, Hin, Win, idx, prob, logits, stream_, nullptr, false);
+      DMLC_HIP_CHECK(hipStreamEndCapture(stream_, &g));
+      hipGraphExec_t ex;
+      DMLC_HIP_CHECK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+      DMLC_HIP_CHECK(hipGraphDestroy(g));
+      it = graphs_.emplace(key, ex).first;
+    }
+    DMLC_TRACE("engine.forward(graph)");
+    DMLC_HIP_CHECK(hipGraphLaunch(it->second, stream));
+    return;
+  }
   DMLC_HIP_CHECK(hipEventRecord(ev_in_, stream));
   DMLC_HIP_CHECK(hipStreamWaitEvent(stream_, ev_in_, 0));
   if (use_graph) {

@@ -132,6 +132,7 @@ class Engine {
   bool stream_conv_ = true; // direct 3x3 with streamed weights for 28x28x128 layers (env DMLC_STREAM_CONV=0 disables)
   bool row_conv_ = true;    // direct row-streaming 3x3 convs where supported (env DMLC_ROW_CONV=0 disables)
   bool fp8_ = false;        // resnet50_fp8
+  bool graph_direct_ = true;  // replay graphs on the caller's stream (env DMLC_GRAPH_DIRECT=0: via the engine stream)
   bool rows_wreg_ = true;     // register-weight row conv, 2 workgroups per CU (env DMLC_ROWS_WREG=0 disables)
   bool stream_wreg_ = true;   // register-weight stream conv where available (env DMLC_STREAM_WREG=0 disables)
   bool stream_l1_ = false;    // stream conv for 56x56x64 layer1 (env DMLC_STREAM_L1=1; slower than conv3x3_rows)
