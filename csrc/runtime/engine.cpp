@@ -781,10 +781,17 @@ void Engine::forward(const uint8_t* images, int B, int Hin, int Win, int32_t* id
       DMLC_HIP_CHECK(hipGraphDestroy(g));
       it = graphs_.emplace(key, ex).first;
     }
+    // Forwards share the activation arena: a replay on a different stream
+    // than the previous forward is ordered after it (an event, only then).
+    if (last_stream_valid_ && stream != last_stream_) DMLC_HIP_CHECK(hipStreamWaitEvent(stream, ev_out_, 0));
     DMLC_TRACE("engine.forward(graph)");
     DMLC_HIP_CHECK(hipGraphLaunch(it->second, stream));
+    DMLC_HIP_CHECK(hipEventRecord(ev_out_, stream));
+    last_stream_ = stream;
+    last_stream_valid_ = true;
     return;
   }
+  if (last_stream_valid_ && stream != last_stream_) DMLC_HIP_CHECK(hipStreamWaitEvent(stream, ev_out_, 0));
   DMLC_HIP_CHECK(hipEventRecord(ev_in_, stream));
   DMLC_HIP_CHECK(hipStreamWaitEvent(stream_, ev_in_, 0));
   if (use_graph) {
@@ -808,6 +815,8 @@ void Engine::forward(const uint8_t* images, int B, int Hin, int Win, int32_t* id
   }
   DMLC_HIP_CHECK(hipEventRecord(ev_out_, stream_));
   DMLC_HIP_CHECK(hipStreamWaitEvent(stream, ev_out_, 0));
+  last_stream_ = stream;  // ev_out_ marks the end of this forward
+  last_stream_valid_ = true;
 }
 
 std::vector<std::pair<std::string, float>> Engine::profile(const uint8_t* images, int B, int Hin,

@@ -164,6 +164,8 @@ class Engine {
 
   hipStream_t stream_ = nullptr;
   hipEvent_t ev_in_ = nullptr, ev_out_ = nullptr;
+  hipStream_t last_stream_ = nullptr;  // stream of the last direct graph replay (ev_out_ marks its end)
+  bool last_stream_valid_ = false;
   hipStream_t side_ = nullptr;                      // downsample branch
   std::vector<hipEvent_t> fork_evs_, join_evs_;     // per op
   using GraphKey = std::tuple<const void*, int, int, int, void*, void*, void*>;

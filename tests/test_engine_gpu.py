@@ -142,3 +142,25 @@ def test_engine_stream_path_matches_reference(gpu):
     torch.cuda.synchronize()
     rel = ((logits.cpu() - ref).norm() / ref.norm()).item()
     assert rel < 3e-2, rel
+
+
+def test_graph_replay_on_two_streams_is_ordered(gpu):
+    """Direct graph replays share the activation arena: a replay on a second
+    stream right after one on the first must not overlap it."""
+    model = build("resnet18", seed=31)
+    eng = InferenceEngine("resnet18", state_dict_f32(model), max_batch=8)
+    g = torch.Generator().manual_seed(32)
+    a = torch.randint(0, 256, (8, 224, 224, 3), generator=g, dtype=torch.uint8).to(gpu)
+    b = torch.randint(0, 256, (8, 224, 224, 3), generator=g, dtype=torch.uint8).to(gpu)
+    _, _, la = eng.predict(a, return_logits=True)
+    _, _, lb = eng.predict(b, return_logits=True)
+    torch.cuda.synchronize()
+    la, lb = la.clone(), lb.clone()
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    for _ in range(3):
+        with torch.cuda.stream(s1):
+            _, _, xa = eng.predict(a, return_logits=True)
+        with torch.cuda.stream(s2):
+            _, _, xb = eng.predict(b, return_logits=True)
+        torch.cuda.synchronize()
+        assert torch.equal(xa, la) and torch.equal(xb, lb)
