@@ -535,7 +535,8 @@ bool conv3x3_stream_supported(int Hin, int Win, int Cin, int Cout, int stride) {
 // 1.7-2x slower (profiles/r1_stream_conv.log).
 bool conv3x3_stream_uses_frag(int Hin, int Win, int Cin, int Cout, int stride) {
   // 56x56x64 / s2 (K-tiles per tap = 2, so a 2-deep ring): 83.8 vs 71.0 us
-  // with the LDS ring, not used; 28x28x128 / s2: 48.6 vs 53.6 us
+  // with the LDS ring (a 4-deep ring with all 20 K-tiles unrolled: 73.8),
+  // not used; 28x28x128 / s2: 48.6 vs 53.6 us
   if (stride == 2) return Cout == 2 * Cin && ((Hin == 28 && Win == 28 && Cin == 128) || (Hin == 14 && Cin == 256));
   // (28x28x128 in quarter images and 14x14x256 in 2 channel splits, both 7
   // fragments per wave so the register ring fits, measured 70.2 / 60.2 vs
