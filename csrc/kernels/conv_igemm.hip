@@ -376,10 +376,16 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a, int kt_p
     const bf16* __restrict__ res = (const bf16*)a.res;
     const int q = lane & 7, rr = lane >> 3;
     const int nq = n0e + wn * WTN + q * 8;
-    floatx4 bq0 = {0.f, 0.f, 0.f, 0.f}, bq1 = bq0;
+    floatx4 bq0 = {0.f, 0.f, 0.f, 0.f}, bq1 = bq0, aq0 = {1.f, 1.f, 1.f, 1.f}, aq1 = aq0;
     if (a.bias && nq < a.N) {
       bq0 = *(const floatx4*)(a.bias + nq);
       bq1 = *(const floatx4*)(a.bias + nq + 4);
+    }
+    if constexpr (IN8) {  // dequantise: s_in * s_w[n], before the bias
+      if (nq < a.N) {
+        aq0 = *(const floatx4*)(a.alpha + nq);
+        aq1 = *(const floatx4*)(a.alpha + nq + 4);
+      }
     }
 #pragma unroll
     for (int j = 0; j < TM; ++j) {
@@ -393,27 +399,50 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a, int kt_p
         const floatx4 hi = *(const floatx4*)(wl + row * 64 + (((2 * q + 1) ^ row) * 4));
         const int m = m0e + wm * WTM + j * 16 + row;
         if (m >= M || nq >= a.N) continue;
-        float v[8] = {lo[0] + bq0[0], lo[1] + bq0[1], lo[2] + bq0[2], lo[3] + bq0[3],
-                      hi[0] + bq1[0], hi[1] + bq1[1], hi[2] + bq1[2], hi[3] + bq1[3]};
+        float v[8] = {lo[0] * aq0[0] + bq0[0], lo[1] * aq0[1] + bq0[1], lo[2] * aq0[2] + bq0[2],
+                      lo[3] * aq0[3] + bq0[3], hi[0] * aq1[0] + bq1[0], hi[1] * aq1[1] + bq1[1],
+                      hi[2] * aq1[2] + bq1[2], hi[3] * aq1[3] + bq1[3]};
+        if constexpr (!IN8) {  // (exact: the multiply by 1 is not emitted for bf16 input)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[e] = lo[e] + bq0[e];
+            v[4 + e] = hi[e] + bq1[e];
+          }
+        }
         const size_t o = (size_t)m * a.ldo + nq;
         if (res) {
           float r[8];
-          unpack8(*(const uint4*)(res + o), r);
+          if constexpr (OUT8) {  // the residual is the block's previous output: same dtype as y
+            const uint2 rv = *(const uint2*)((const uint8_t*)a.res + o);
+            fp8x4_to_f32(rv.x, r);
+            fp8x4_to_f32(rv.y, r + 4);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] += r[e];
+            for (int e = 0; e < 8; ++e) v[e] += r[e] * a.res_scale;
+          } else {
+            unpack8(*(const uint4*)(res + o), r);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] += r[e];
+          }
         }
         if (a.relu) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
         }
-        *(uint4*)((bf16*)a.y + o) = pack8(v);
+        if constexpr (OUT8) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] *= a.out_inv_scale;
+          *(uint2*)((uint8_t*)a.y + o) = make_uint2(f32x4_to_fp8(v), f32x4_to_fp8(v + 4));
+        } else {
+          *(uint4*)((bf16*)a.y + o) = pack8(v);
+        }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next pass overwrites
     }
   };
   // 16-B rows need N, ldo multiples of 8 and 16-B aligned y / residual
-  const bool lds_epi = !IN8 && !OUT8 && !PAIR && WTN == 64 && gridDim.y == 1 && !a.out_f32 && a.N % 8 == 0 &&
-                       a.ldo % 8 == 0 && (((uintptr_t)a.y | (uintptr_t)a.res) & 15) == 0;
+  // (fp8 in / out too: alpha before the bias, 8-B e4m3 rows; 16-B bf16 rows)
+  const bool lds_epi = !PAIR && WTN == 64 && gridDim.y == 1 && !a.out_f32 && a.N % 8 == 0 && a.ldo % 8 == 0 &&
+                       (((uintptr_t)a.y | (uintptr_t)a.res) & (OUT8 ? 7 : 15)) == 0;
 
   if (nk <= 0 || tile_iter >= nwg) return;
 

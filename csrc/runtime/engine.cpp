@@ -298,14 +298,28 @@ void Engine::build_alexnet() {
   ops_.push_back(Op{OpType::SoftmaxTop1, logits_act_, -1, -1, -1, 0, 0, 0, "softmax_top1"});
 }
 
-// resnet50_fp8: every conv output with a multiple of 128 channels is e4m3:
-// the 256..2048-channel block outputs and residual paths (where the bytes
-// are: layer1's 56x56x256 tensors dominate the traffic) and all of layers
-// 2-4. The stem and layer1's 64-channel inner convs stay bf16 (Cin = 64 is
-// below the fp8 kernel's 128-channel K-tile; the 3x3 runs conv3x3_rows).
+// resnet50_fp8: conv outputs with a multiple of 128 channels are e4m3: the
+// 256..2048-channel block outputs and residual paths (where the bytes are:
+// layer1's 56x56x256 tensors dominate the traffic), so every 1x1 expand /
+// reduce conv and downsample reads or writes e4m3. The 3x3 convs keep bf16
+// input and output (DMLC_FP8_3X3=1 makes them e4m3 as well): as bf16 they run
+// the direct stream / row convs (LDS-resident input, register weights),
+// which beat the fp8 implicit GEMM on these shapes. The stem and layer1's
+// 64-channel inner convs stay bf16 (Cin = 64 is below the fp8 kernel's
+// 128-channel K-tile).
 void Engine::mark_fp8() {
+  bool fp8_3x3 = false;
+  if (const char* e = std::getenv("DMLC_FP8_3X3")) fp8_3x3 = std::string(e) != "0";
+  std::vector<bool> near_3x3(shapes_.size(), false);  // read or written by a 3x3 conv
   for (const Op& op : ops_)
-    if (op.type == OpType::Conv && !convs_[op.conv].fc && shapes_[op.out].C % 128 == 0) shapes_[op.out].fp8 = true;
+    if (op.type == OpType::Conv && !convs_[op.conv].fc && convs_[op.conv].kh == 3) {
+      near_3x3[op.in] = true;
+      near_3x3[op.out] = true;
+    }
+  for (const Op& op : ops_)
+    if (op.type == OpType::Conv && !convs_[op.conv].fc && shapes_[op.out].C % 128 == 0 &&
+        (fp8_3x3 || !near_3x3[op.out]))
+      shapes_[op.out].fp8 = true;
   for (const Op& op : ops_) {
     if (op.type != OpType::Conv) continue;
     if (op.res >= 0 && shapes_[op.res].fp8 != shapes_[op.out].fp8)
