@@ -102,7 +102,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    dp.run(pool, args.warmup, args.steps)
+    dp.run(pool, args.warmup, args.steps, stamps=False)
     torch.cuda.synchronize()
     if distributed:
         dist.barrier()
@@ -113,11 +113,18 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
 
-    batch_lat = [dp.latency_ms(i) for i in range(args.warmup, args.warmup + args.steps)]
+    # Per-batch latency (scatter issue -> gathered top-1) from event stamps, in
+    # a separate pass: the stamps' stream barriers would otherwise sit inside
+    # the throughput measurement.
+    n_lat = min(args.steps, 50)
+    lat0 = args.warmup + args.steps
+    dp.run(pool, lat0, n_lat)
+    torch.cuda.synchronize()
+    batch_lat = [dp.latency_ms(i) for i in range(lat0, lat0 + n_lat)]
 
     # Sanity: the coordinator's gathered outputs are valid class ids / probabilities.
     if rank == 0:
-        ids, probs = dp.results(args.warmup + args.steps - 1)
+        ids, probs = dp.results(lat0 + n_lat - 1)
         assert ids.numel() == B * world
         assert int(ids.min()) >= 0 and int(ids.max()) < 1000, "bad class ids"
         assert float(probs.min()) > 0 and float(probs.max()) <= 1.0001, "bad probabilities"

@@ -106,10 +106,20 @@ class DPInference:
         return pool[b * self.B:(b + 1) * self.B]
 
     # ---------------------------------------------------------------- run
-    def run(self, pool: torch.Tensor | None, first: int, n: int) -> None:
+    def run(self, pool: torch.Tensor | None, first: int, n: int, stamps: bool = True) -> None:
         """Pipelined steps [first, first+n). `pool` (u8 [N,H,W,3] on this
         rank's device) is needed on the coordinator in scatter mode and on
-        every rank in local mode."""
+        every rank in local mode. stamps=False skips the per-step timing
+        events (each is a release barrier on the stream: ~10 us of idle GPU
+        per step between forwards); latency_ms() then has no entries for
+        these steps."""
+        if not stamps:
+            saved = self._stamp
+            self._stamp = lambda store, step: None
+            try:
+                return self.run(pool, first, n)
+            finally:
+                self._stamp = saved
         self._stamp(self.t_start, first)
         h = self._issue_input(pool, first)
         for i in range(first, first + n):
