@@ -66,6 +66,12 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}; launch N>1 with torchrun")
+    if world > 1:
+        # Under the concurrent RCCL scatter/gather kernels a grid that exactly
+        # fills the CUs loses a whole round when a few slots are taken: finer
+        # row-conv strips (1792 instead of 512 workgroups) cost ~1% alone and
+        # halve that loss (profiles/r1_interference.txt).
+        os.environ.setdefault("DMLC_ROWS_STRIP", "8")
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     distributed = world > 1

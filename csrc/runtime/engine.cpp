@@ -93,6 +93,7 @@ Engine::Engine(const std::string& arch, const WeightMap& weights, int device, in
   if (const char* e = std::getenv("DMLC_STREAM_L1")) stream_l1_ = std::string(e) != "0";
   if (const char* e = std::getenv("DMLC_STREAM_WREG")) stream_wreg_ = std::string(e) != "0";
   if (const char* e = std::getenv("DMLC_ROWS_WREG")) rows_wreg_ = std::string(e) != "0";
+  if (const char* e = std::getenv("DMLC_ROWS_STRIP")) rows_strip_ = std::atoi(e);
   if (const char* e = std::getenv("DMLC_GRAPH_DIRECT")) graph_direct_ = std::string(e) != "0";
 
   if (arch == "resnet18")
@@ -697,7 +698,10 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
             conv3x3_rows(acts_[op.in], (const uint8_t*)warena_ + L.w_off,
                          (const float*)((const uint8_t*)warena_ + L.b_off), op.res >= 0 ? acts_[op.res] : nullptr,
                          acts_[op.out], zero_, B, is.H, is.W, is.C, L.relu,
-                         conv3x3_rows_pick_strip(B, is.H, (L.wf_off && rows_wreg_) ? 2 * num_cus_ : num_cus_), cs,
+                         rows_strip_ > 0 && is.H % rows_strip_ == 0
+                             ? rows_strip_
+                             : conv3x3_rows_pick_strip(B, is.H, (L.wf_off && rows_wreg_) ? 2 * num_cus_ : num_cus_),
+                         cs,
                          (L.wf_off && rows_wreg_) ? (const uint8_t*)warena_ + L.wf_off : nullptr);
             break;
           case ConvPath::BigTile: {

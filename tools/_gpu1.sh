@@ -1,3 +1,2 @@
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && export TMPDIR=/tmp
-timeout -k 10 300 python tools/interference_probe.py > gpurun_out/interference.log 2>&1 || exit 1
-tail -6 gpurun_out/interference.log
+for st in 0 14 8; do echo "strip $st"; DMLC_ROWS_STRIP=$st timeout -k 10 300 python tools/interference_probe.py --modes none,sleep1,sleep4,sleep16 2>&1 | grep forward || exit 1; done
