@@ -1,2 +1,7 @@
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && export TMPDIR=/tmp
-for st in 0 14 8; do echo "strip $st"; DMLC_ROWS_STRIP=$st timeout -k 10 300 python tools/interference_probe.py --modes none,sleep1,sleep4,sleep16 2>&1 | grep forward || exit 1; done
+rm -f gpurun_out/steps.log
+bash tools/gpu_check.sh test || exit 1
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { tail gpurun_out/smoke.log; exit 1; }
+tail -1 gpurun_out/smoke.log
+bash tools/gpu_check.sh bench || exit 1
+bash tools/gpu_check.sh prof || exit 1
