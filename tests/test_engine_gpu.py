@@ -164,3 +164,25 @@ def test_graph_replay_on_two_streams_is_ordered(gpu):
             _, _, xb = eng.predict(b, return_logits=True)
         torch.cuda.synchronize()
         assert torch.equal(xa, la) and torch.equal(xb, lb)
+
+
+@pytest.mark.parametrize("B", [37, 100, 255])
+def test_fast_paths_match_plain_paths_odd_batches(gpu, monkeypatch, B):
+    """Every fast path at odd batch sizes (partial image groups, partial head
+    groups, row-conv strips that do not fill the CUs evenly) against the
+    plain paths: register weights off, downsample unfused, three-kernel head."""
+    model = build("resnet18", seed=41, randomize_bn=True)
+    sd = state_dict_f32(model)
+    for k in ("DMLC_STREAM_WREG", "DMLC_ROWS_WREG", "DMLC_FUSE_DS", "DMLC_FUSED_HEAD"):
+        monkeypatch.setenv(k, "0")
+    ref_eng = InferenceEngine("resnet18", sd, max_batch=B)
+    for k in ("DMLC_STREAM_WREG", "DMLC_ROWS_WREG", "DMLC_FUSE_DS", "DMLC_FUSED_HEAD"):
+        monkeypatch.setenv(k, "1")
+    eng = InferenceEngine("resnet18", sd, max_batch=B)
+    g = torch.Generator().manual_seed(B + 1)
+    img = torch.randint(0, 256, (B, 224, 224, 3), generator=g, dtype=torch.uint8).to(gpu)
+    _, _, rl = ref_eng.predict(img, return_logits=True)
+    i, p, lg = eng.predict(img, return_logits=True)
+    torch.cuda.synchronize()
+    rel = ((lg - rl).norm() / rl.norm()).item()
+    assert rel < 1e-3, rel
