@@ -109,18 +109,18 @@ class DPInference:
     def run(self, pool: torch.Tensor | None, first: int, n: int, stamps: bool = True) -> None:
         """Pipelined steps [first, first+n). `pool` (u8 [N,H,W,3] on this
         rank's device) is needed on the coordinator in scatter mode and on
-        every rank in local mode. stamps=False skips the per-step timing
-        events (each is a release barrier on the stream: ~10 us of idle GPU
-        per step between forwards); latency_ms() then has no entries for
-        these steps."""
-        if not stamps:
-            saved = self._stamp
-            self._stamp = lambda store, step: None
-            try:
-                return self.run(pool, first, n)
-            finally:
-                self._stamp = saved
-        self._stamp(self.t_start, first)
+        every rank in local mode.
+
+        stamps=True records a timing event pair per step (latency_ms) and
+        joins each step's gather into the compute stream right away, so a
+        step's latency is scatter issue -> gathered top-1. stamps=False is
+        the throughput mode: no timing events (each is a release barrier on
+        the stream, ~10 us of idle GPU between forwards) and the gather of
+        step i is joined only before step i + slots reuses its output slot, so
+        no rank's next forward waits for the slowest rank's previous one."""
+        stamp = self._stamp if stamps else (lambda store, step: None)
+        pending = {}  # slot -> gather work not yet joined
+        stamp(self.t_start, first)
         h = self._issue_input(pool, first)
         for i in range(first, first + n):
             if h is not None:
@@ -128,9 +128,11 @@ class DPInference:
             h = None
             if i + 1 < first + n and self.transfer:
                 # batch i+1's transfer may start once compute(i-1) is done
-                self._stamp(self.t_start, i + 1)
+                stamp(self.t_start, i + 1)
                 h = self._issue_input(pool, i + 1)
             s = i % self.slots
+            if s in pending:
+                pending.pop(s).wait()  # gather(i - slots) has read this output slot
             ob = self.outbuf[s]
             with _Range("dp.predict", self.cuda):
                 self.predict_fn(self._local_input(pool, i), (ob[0], ob[1].view(torch.float32)))
@@ -138,10 +140,15 @@ class DPInference:
                 with _Range("dp.gather", self.cuda):
                     g = dist.gather(ob, self.gathered[s] if self.rank == self.src else None, dst=self.src,
                                     async_op=True)
-                    g.wait()
-            self._stamp(self.t_end, i)
+                    if stamps:
+                        g.wait()
+                    else:
+                        pending[s] = g
+            stamp(self.t_end, i)
             if not self.transfer and i + 1 < first + n:
-                self._stamp(self.t_start, i + 1)
+                stamp(self.t_start, i + 1)
+        for g in pending.values():
+            g.wait()
 
     def results(self, step: int) -> tuple[torch.Tensor, torch.Tensor]:
         """Top-1 (class int32 [world*B], prob f32 [world*B]) of `step` at the
