@@ -59,6 +59,8 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--latency-queries", type=int, default=200, help="batch-1 queries for query latency")
     ap.add_argument("--profile-ops", action="store_true", help="print per-op times of one eager forward")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="use the process group (RCCL scatter/gather) even for one rank: rehearses the N>1 path")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -74,7 +76,7 @@ def main():
         os.environ.setdefault("DMLC_ROWS_STRIP", "8")
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
-    distributed = world > 1
+    distributed = world > 1 or args.force_dist
     if distributed:
         dist.init_process_group("nccl", device_id=dev)
 

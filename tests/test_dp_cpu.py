@@ -62,8 +62,12 @@ def _worker(rank, world, port, B, steps, q):
         dist.destroy_process_group()
 
 
-def test_dp_scatter_gather_gloo():
-    world, B, steps = 2, 3, 4
+@pytest.mark.parametrize("world,p2p", [(2, "1"), (3, "1"), (2, "0")])
+def test_dp_scatter_gather_gloo(monkeypatch, world, p2p):
+    """p2p=1: point-to-point sends of the other ranks' shards (the
+    coordinator's own shard read in place); p2p=0: dist.scatter/gather."""
+    monkeypatch.setenv("DMLC_DP_P2P", p2p)
+    B, steps = 3, 4
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
