@@ -810,6 +810,14 @@ void Engine::forward(const uint8_t* images, int B, int Hin, int Win, int32_t* id
     return;
   }
   if (last_stream_valid_ && stream != last_stream_) DMLC_HIP_CHECK(hipStreamWaitEvent(stream, ev_out_, 0));
+  if (!use_graph && graph_direct_) {  // eager launches straight onto the caller's stream too
+    DMLC_TRACE("engine.forward");
+    run_ops(images, B, Hin, Win, idx, prob, logits, stream, nullptr, true);
+    DMLC_HIP_CHECK(hipEventRecord(ev_out_, stream));
+    last_stream_ = stream;
+    last_stream_valid_ = true;
+    return;
+  }
   DMLC_HIP_CHECK(hipEventRecord(ev_in_, stream));
   DMLC_HIP_CHECK(hipStreamWaitEvent(stream_, ev_in_, 0));
   if (use_graph) {
