@@ -6,12 +6,14 @@ to a random member over TCP (src/services.rs:407-433, 2 queries/s/job) and
 every member holds full model replicas (src/services.rs:513-524). Here the
 coordinator (rank 0) holds the staged u8 image pool in HBM and, per step:
 
-  1. scatters one u8 shard [B,224,224,3] to every rank (RCCL grouped
-     send/recv under dist.scatter; the u8 layout is 2x smaller than bf16 and
-     is normalised on the receiving GPU),
+  1. sends one u8 shard [B,224,224,3] to every other rank (one batch of RCCL
+     point-to-point sends, one xGMI link per peer; the u8 layout is 2x
+     smaller than bf16 and is normalised on the receiving GPU) and reads its
+     own shard in place,
   2. every rank classifies its shard (hipGraph-replayed HIP engine),
-  3. (top-1 class, probability) pairs are gathered back to rank 0
-     (8 bytes per image).
+  3. (top-1 class, probability) pairs come back to rank 0 as point-to-point
+     receives (8 bytes per image).
+DMLC_DP_P2P=0 selects dist.scatter / dist.gather instead.
 
 The scatter of step i+1 is issued before the compute of step i and lands in
 the other input slot, so the xGMI transfer overlaps compute; RCCL runs on
