@@ -33,6 +33,17 @@ __device__ __forceinline__ uint32_t pack2(float a, float b) {
   return (uint32_t)__builtin_bit_cast(uint16_t, x) | ((uint32_t)__builtin_bit_cast(uint16_t, y) << 16);
 }
 
+// ImageNet normalisation of a u8-range value of channel c (0=R, 1=G, 2=B):
+// (v/255 - mean)/std as ONE fma, v * 1/(255 std) + (-mean/std). Shared by
+// preprocess.hip and the u8 stem in stem_pool.hip so both produce the same
+// bits (the two-op form costs an extra VALU op per value in the stem's
+// VALU-bound u8 conversion).
+__device__ __forceinline__ float imagenet_norm(int c, float v) {
+  const float sc = c == 0 ? 1.f / (255.f * 0.229f) : c == 1 ? 1.f / (255.f * 0.224f) : 1.f / (255.f * 0.225f);
+  const float sh = c == 0 ? -0.485f / 0.229f : c == 1 ? -0.456f / 0.224f : -0.406f / 0.225f;
+  return __builtin_fmaf(v, sc, sh);
+}
+
 __device__ __forceinline__ uint4 pack8(const float* f) {
   return make_uint4(pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]), pack2(f[6], f[7]));
 }

@@ -67,9 +67,9 @@ __device__ __forceinline__ void pixel(const uint8_t* __restrict__ img, const Pre
       c[k] = top + (bot - top) * fy;
     }
   }
-  o[0] = (c[0] * (1.f / 255.f) - 0.485f) * (1.f / 0.229f);
-  o[1] = (c[1] * (1.f / 255.f) - 0.456f) * (1.f / 0.224f);
-  o[2] = (c[2] * (1.f / 255.f) - 0.406f) * (1.f / 0.225f);
+  o[0] = imagenet_norm(0, c[0]);
+  o[1] = imagenet_norm(1, c[1]);
+  o[2] = imagenet_norm(2, c[2]);
 }
 
 __global__ __launch_bounds__(256) void preprocess_kernel(const uint8_t* __restrict__ x, bf16* __restrict__ y,

@@ -181,9 +181,7 @@ __global__ __launch_bounds__(256, 2) void stem_conv_pool_kernel(
         for (int c = 0; c < 3; ++c) {
           const int idx = 3 + 3 * i + c;
           const float cv = (float)((d[idx >> 2] >> (8 * (idx & 3))) & 0xffu);
-          const float nv = c == 0 ? (cv * (1.f / 255.f) - 0.485f) * (1.f / 0.229f)
-                         : c == 1 ? (cv * (1.f / 255.f) - 0.456f) * (1.f / 0.224f)
-                                  : (cv * (1.f / 255.f) - 0.406f) * (1.f / 0.225f);
+          const float nv = imagenet_norm(c, cv);
           v[8 * (i >> 1) + 3 * (i & 1) + c] = in ? nv : 0.f;
         }
       }

@@ -46,6 +46,9 @@ def main():
     for st in [int(s) for s in a.strips.split(",")]:
         ms = _time(lambda: ops.stem_conv_pool(xp, wp, bias, S, st or None), a.iters)
         print(f"fused strip={st or 'auto'}: {ms * 1e3:7.1f} us  ({flops / ms / 1e9:5.0f} TF conv-equivalent)")
+    for st in [int(s) for s in a.strips.split(",")]:
+        ms = _time(lambda: ops.stem_conv_pool_u8(img, wp, bias, st or None), a.iters)
+        print(f"fused u8 strip={st or 'auto'}: {ms * 1e3:7.1f} us  ({flops / ms / 1e9:5.0f} TF conv-equivalent)")
     wr = ops.stem_row_width(S, 3, 7, 2)
     xr = ops.preprocess_u8(img, S, 3, wr)
     wr_p = ops.pack_conv_weight(w, stem=True, device=dev)
