@@ -370,6 +370,7 @@ int run_node(const Args& a) {
     lc.query_interval_ms = a.geti("query-interval-ms", 500);
     lc.query_batch = a.geti("query-batch", 1);
     lc.max_inflight = a.geti("max-inflight", 32);
+    lc.adaptive_window = a.geti("adaptive-window", 0);
     lc.job_limit = a.geti("job-limit", 0);
     lc.print_predictions = !a.has("quiet-predictions");
     lc.job_models.clear();
@@ -436,7 +437,7 @@ int main(int argc, char** argv) {
     std::cout << "usage: dmlc-node [--host H] [--port P] [--leaders h:p,...] [--workdir D] [--dataset D]\n"
                  "                 [--labels F] [--models name=path,...] [--executor auto|gpu|cpu] [--device N]\n"
                  "                 [--rf 4] [--ping-ms 1000] [--fail-ms 3000] [--bg-ms 3000]\n"
-                 "                 [--query-interval-ms 500] [--query-batch 1] [--jobs resnet18,alexnet]\n"
+                 "                 [--query-interval-ms 500] [--adaptive-window 0] [--query-batch 1] [--jobs resnet18,alexnet]\n"
                  "                 [--join h:p] [--daemon] [--stay] [--quiet-predictions]\n"
                  "                 [--max-batch 64] [--hbm-cache-mb 4096] [--prefetch]\n"
                  "       dmlc-node selftest\n"

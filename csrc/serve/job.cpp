@@ -79,7 +79,13 @@ std::string format_job_report(int n, const Job& j) {
            "\t\t%.3f ms p90, %.3f ms p95, %.3f ms p99",
            n, j.model_name.c_str(), j.correct, j.finished, acc, s.count, s.mean, s.stddev, s.p50, s.p90, s.p95,
            s.p99);
-  return buf;
+  std::string out = buf;
+  if (j.finished > 0 && j.started_us > 0 && !j.done_us.empty() && j.done_us.back() > j.started_us) {
+    const double secs = (j.done_us.back() - j.started_us) * 1e-6;
+    snprintf(buf, sizeof(buf), "\n\tThroughput: %.2f queries/s", j.finished / secs);
+    out += buf;
+  }
+  return out;
 }
 
 }  // namespace ctl

@@ -2,6 +2,7 @@
 
 #include "../runtime/trace.h"
 
+#include <climits>
 #include <optional>
 
 #include "../control/common.h"
@@ -17,6 +18,28 @@ LeaderService::LeaderService(LeaderConfig cfg, MembershipService* ms, MemberServ
     jobs_.push_back(j);
   }
   running_.assign(jobs_.size(), false);
+  job_inflight_.reset(new std::atomic<int>[jobs_.size()]);
+  for (size_t j = 0; j < jobs_.size(); ++j) job_inflight_[j] = 0;
+}
+
+Id LeaderService::pick_target(const std::vector<Id>& pool) {
+  std::lock_guard<std::mutex> g(rng_mu_);
+  if (cfg_.adaptive_window <= 0)  // reference: a random member (src/services.rs:414-416)
+    return pool[std::uniform_int_distribution<size_t>(0, pool.size() - 1)(rng_)];
+  // least outstanding queries; ties broken at random so load spreads evenly
+  int best = INT_MAX;
+  std::vector<size_t> ties;
+  for (size_t i = 0; i < pool.size(); ++i) {
+    auto it = member_inflight_.find(pool[i].address);
+    const int q = it == member_inflight_.end() ? 0 : it->second;
+    if (q < best) {
+      best = q;
+      ties.assign(1, i);
+    } else if (q == best) {
+      ties.push_back(i);
+    }
+  }
+  return pool[ties[std::uniform_int_distribution<size_t>(0, ties.size() - 1)(rng_)]];
 }
 
 LeaderService::~LeaderService() { stop(); }
@@ -280,8 +303,10 @@ void LeaderService::run_job(size_t j) {
   const size_t limit = cfg_.job_limit > 0 ? std::min(L.size(), (size_t)cfg_.job_limit) : L.size();
   auto next_tick = std::chrono::steady_clock::now();
   while (idx < limit && !stop_.load()) {
-    next_tick += std::chrono::milliseconds(cfg_.query_interval_ms);
-    std::this_thread::sleep_until(next_tick);
+    if (cfg_.adaptive_window <= 0) {
+      next_tick += std::chrono::milliseconds(cfg_.query_interval_ms);
+      std::this_thread::sleep_until(next_tick);
+    }
     if (!is_leader()) break;  // leadership moved: the new leader resumes
     std::vector<Id> pool;
     {
@@ -292,12 +317,18 @@ void LeaderService::run_job(size_t j) {
       auto a = ms_->active_ids();
       pool.assign(a.begin(), a.end());
     }
-    if (pool.empty()) continue;
-    Id target;
-    {
-      std::lock_guard<std::mutex> g(rng_mu_);
-      target = pool[std::uniform_int_distribution<size_t>(0, pool.size() - 1)(rng_)];
+    if (pool.empty()) {
+      if (cfg_.adaptive_window > 0) std::this_thread::sleep_for(std::chrono::milliseconds(50));
+      continue;
     }
+    if (cfg_.adaptive_window > 0) {
+      // closed loop: wait for a free slot in this job's window
+      const int window = cfg_.adaptive_window * (int)pool.size();
+      while (job_inflight_[j].load() >= window && !stop_.load())
+        std::this_thread::sleep_for(std::chrono::microseconds(200));
+      if (stop_.load()) break;
+    }
+    const Id target = pick_target(pool);
     while (inflight_.load() >= cfg_.max_inflight && !stop_.load())
       std::this_thread::sleep_for(std::chrono::microseconds(200));
     const size_t n = std::min((size_t)cfg_.query_batch, limit - idx);
@@ -308,6 +339,11 @@ void LeaderService::run_job(size_t j) {
       if (jobs_[j].started_us == 0) jobs_[j].started_us = wall_us();
     }
     inflight_++;
+    job_inflight_[j]++;
+    {
+      std::lock_guard<std::mutex> g(rng_mu_);
+      member_inflight_[target.address]++;
+    }
     std::thread([this, j, model, target, first, n] {
       const auto& L = labels_.entries;
       Writer w;
@@ -367,6 +403,11 @@ void LeaderService::run_job(size_t j) {
       } catch (const std::exception& e) {
         DMLC_LOG_WARN("predict " << model << " on " << target.address << " failed: " << e.what());
       }
+      {
+        std::lock_guard<std::mutex> g(rng_mu_);
+        if (--member_inflight_[target.address] <= 0) member_inflight_.erase(target.address);
+      }
+      job_inflight_[j]--;
       inflight_--;
     }).detach();
   }

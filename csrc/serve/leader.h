@@ -12,6 +12,12 @@
 // a job with no assigned member borrows all active members instead of
 // silently skipping queries; queries can be batched (query_batch) and the
 // tick is configurable (reference: 1 query / 0.5 s / job).
+// Adaptive rate (the report claims the leader adjusts the
+// query rate, the code has a fixed tick): with adaptive_window > 0 a job has
+// no tick; it keeps adaptive_window queries in flight per assigned member and
+// sends each to the member with the fewest of them outstanding, so its rate
+// follows what its members can serve (rate = window / latency) and a slow or
+// overloaded member gets fewer queries.
 #pragma once
 #include <atomic>
 #include <condition_variable>
@@ -41,6 +47,7 @@ struct LeaderConfig {
   int query_interval_ms = 500;
   int query_batch = 1;
   int max_inflight = 32;
+  int adaptive_window = 0;  // >0: closed-loop rate, queries in flight per member
   int job_limit = 0;  // queries per job (0 = every label, as the reference)
   bool print_predictions = true;
   std::vector<std::string> job_models = {"resnet18", "alexnet"};
@@ -91,6 +98,9 @@ class LeaderService {
   std::mutex runners_mu_;
   std::vector<std::thread> runners_;
   std::atomic<int> inflight_{0};
+  std::unique_ptr<std::atomic<int>[]> job_inflight_;  // per job (adaptive window)
+  std::map<std::string, int> member_inflight_;         // per member address, under rng_mu_
+  Id pick_target(const std::vector<Id>& pool);
   std::mutex rng_mu_;
   std::mt19937_64 rng_{std::random_device{}()};
 };

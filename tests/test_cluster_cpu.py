@@ -178,3 +178,30 @@ def test_predict_jobs_assign_and_leader_failover(env, tmp_path):
         assert all(c[2] == c[1] for c in counts)
         rep = n[3].cmd("jobs")
         assert "Model: resnet18" in rep and "Model: alexnet" in rep and "ms p95" in rep
+
+
+def test_adaptive_rate_jobs(env, tmp_path):
+    """--adaptive-window: no tick, each job keeps a window of queries in flight
+    per assigned member (least-outstanding routing), so with a 10 s tick set
+    the jobs still finish at the members' own speed (SURVEY.md §7.6 #12)."""
+    models = f"resnet18={env['models']['resnet18']},alexnet={env['models']['alexnet']}"
+    cl = LocalCluster(4, 19600, str(tmp_path / "c"), env["labels"], n_leaders=1, executor="cpu",
+                      dataset=env["dataset"], models=models,
+                      extra=["--job-limit", "40", "--query-interval-ms", "10000", "--adaptive-window", "2",
+                             "--quiet-predictions"])
+    with cl:
+        n = cl.nodes
+        time.sleep(1.0)  # one assignment round
+        n[0].cmd("predict")
+        deadline = time.time() + 60
+        counts = []
+        while time.time() < deadline:
+            counts = _job_counts(n[0])
+            if len(counts) == 2 and all(c[1] >= 40 for c in counts):
+                break
+            time.sleep(0.5)
+        # a fixed 10 s tick would have finished 6 queries per job by now
+        assert len(counts) == 2 and all(c[1] == 40 and c[2] == 40 for c in counts), counts
+        rep = n[0].cmd("jobs")
+        rates = [float(x) for x in re.findall(r"Throughput: ([\d.]+) queries/s", rep)]
+        assert len(rates) == 2 and all(r > 0.5 for r in rates), rep

@@ -98,3 +98,32 @@ def test_tsan_cluster_workload(tsan_bin, tmp_path):
         assert "Leaving group" in n[3].cmd("leave")
         cl.wait_members(2, 20, [n[1], n[4]])
     _no_reports(n)
+
+
+def test_tsan_adaptive_rate(tsan_bin, tmp_path):
+    """Adaptive-rate jobs (per-job windows, least-outstanding routing over
+    the shared per-member counts) with a member killed mid-run: no races."""
+    labels = synthetic_labels(1000)
+    lab = write_labels(str(tmp_path / "synset_words.txt"), labels)
+    ds = make_synthetic_dataset(str(tmp_path / "train"), labels[:48], size=(48, 64))
+    cl = LocalCluster(4, 19950, str(tmp_path / "c"), lab, n_leaders=1, executor="digest", dataset=ds,
+                      models="resnet18=-,alexnet=-", binary=tsan_bin, env=TSAN_ENV,
+                      extra=["--job-limit", "40", "--adaptive-window", "2", "--quiet-predictions"])
+    with cl:
+        n = cl.nodes
+        time.sleep(1.0)
+        n[0].cmd("predict")
+        time.sleep(0.3)
+        n[3].kill()
+        deadline = time.time() + 90
+        done = False
+        while time.time() < deadline and not done:
+            try:
+                out = n[0].cmd("jobs", 20)
+                tot = [int(q) for q in re.findall(r"Queries: (\d+) total", out)]
+                done = len(tot) == 2 and all(q >= 40 for q in tot)
+            except TimeoutError:
+                pass
+            time.sleep(0.5)
+        assert done, n[0].output()[-4000:]
+    _no_reports(n)
