@@ -65,6 +65,8 @@ def main():
     ap.add_argument("--images", type=int, default=1000)
     ap.add_argument("--interval-ms", type=int, default=50)
     ap.add_argument("--batch", type=int, default=1)
+    ap.add_argument("--adaptive-window", type=int, default=0,
+                    help="closed-loop rate: queries in flight per member (0 = fixed --interval-ms tick)")
     ap.add_argument("--kill", choices=["none", "member", "leader"], default="none")
     ap.add_argument("--fast-periods", action="store_true", help="200 ms pings, 1.2 s failure timeout, 500 ms loops")
     ap.add_argument("--port", type=int, default=21000)
@@ -85,7 +87,8 @@ def main():
           enumerate(["resnet18", "alexnet"])}
     models = ",".join(f"{m}={p}" for m, p in ck.items())
     extra = ["--job-limit", str(a.images), "--query-interval-ms", str(a.interval_ms), "--query-batch",
-             str(a.batch), "--quiet-predictions", "--max-batch", str(max(8, a.batch))]
+             str(a.batch), "--quiet-predictions", "--max-batch", str(max(8, a.batch)),
+             "--adaptive-window", str(a.adaptive_window)]
     cl = LocalCluster(a.nodes, a.port, os.path.join(root, "c"), lab, n_leaders=2, executor=a.executor,
                       dataset=ds, models=models, fast=a.fast_periods, extra=extra)
     if a.kill == "member" and a.nodes < 3:
@@ -134,6 +137,7 @@ def main():
             nd.kill()
     res = {"bench": "two concurrent predict jobs through the control plane", "nodes": a.nodes,
            "executor": a.executor, "gpus": ngpu, "images_per_job": a.images, "query_interval_ms": a.interval_ms,
+           "adaptive_window": a.adaptive_window,
            "query_batch": a.batch, "data": "synthetic 500x375 JPEGs (imagenet_1k layout), random-init weights",
            "reference": REF, "jobs": []}
     for j in jobs:
