@@ -333,6 +333,7 @@ int run_node(const Args& a) {
   mc.detect_ms = a.geti("detect-ms", 1000);
   mc.fail_ms = a.geti("fail-ms", 3000);
   mc.tombstone_ms = a.geti("tombstone-ms", 30000);
+  mc.clock_skew_us = (int64_t)a.geti("clock-skew-ms", 0) * 1000;
   n->ms = std::make_unique<MembershipService>(mc);
   n->ms->start();
 

@@ -132,7 +132,7 @@ static std::string list_table(const MembershipList& l, bool active_only) {
 
 MembershipService::MembershipService(MembershipConfig cfg) : cfg_(std::move(cfg)) {
   id_.address = cfg_.host + ":" + std::to_string(cfg_.port);
-  id_.timestamp = wall_us();
+  id_.timestamp = own_us();
 }
 
 MembershipService::~MembershipService() { stop(); }
@@ -223,7 +223,7 @@ void MembershipService::join(const std::string& introducer) {
   m.type = MsgType::Join;
   {
     std::lock_guard<std::mutex> g(mu_);
-    id_.timestamp = wall_us();  // new incarnation
+    id_.timestamp = own_us();  // new incarnation
     m.sender = id_;
   }
   send(introducer, m);
@@ -236,7 +236,7 @@ void MembershipService::leave() {
   {
     std::lock_guard<std::mutex> g(mu_);
     m.sender = id_;
-    m.last_active = wall_us();
+    m.last_active = own_us();
     const std::string msg = "Leaving group...\nLast membership list:\n" + list_table(list_, false);
     DMLC_LOG_INFO(msg);
     out_line(msg);
@@ -276,7 +276,7 @@ void MembershipService::receiver_loop() {
           Message ack;
           ack.type = MsgType::Ack;
           ack.sender = self;
-          ack.last_active = wall_us();
+          ack.last_active = own_us();
           send(m.sender.address, ack);
         }
         break;
@@ -298,7 +298,7 @@ void MembershipService::receiver_loop() {
           dead_.erase(m.sender);
           list_[m.sender] = Membership{Status::Active, m.sender.timestamp};
           auto it = list_.find(id_);
-          if (it != list_.end()) it->second = Membership{Status::Active, wall_us()};
+          if (it != list_.end()) it->second = Membership{Status::Active, own_us()};
           w.sender = id_;
           w.list = list_;
         }
@@ -329,11 +329,24 @@ void MembershipService::receiver_loop() {
         break;
       }
     }
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      note_heard_locked();
+    }
     for (const auto& c : changes) {
       DMLC_LOG_INFO(c);
       out_line(c);
     }
   }
+}
+
+void MembershipService::note_heard_locked() {
+  const int64_t st = steady_us();
+  for (const auto& kv : list_) {
+    auto& h = heard_[kv.first];
+    if (h.second == 0 || kv.second.last_active > h.first) h = {kv.second.last_active, st};
+  }
+  for (auto it = heard_.begin(); it != heard_.end();) it = list_.count(it->first) ? std::next(it) : heard_.erase(it);
 }
 
 void MembershipService::pinger_loop() {
@@ -346,13 +359,16 @@ void MembershipService::pinger_loop() {
     std::vector<Id> nbrs;
     {
       std::lock_guard<std::mutex> g(mu_);
-      const int64_t now = wall_us();
+      const int64_t now = own_us();
       auto it = list_.find(id_);
       if (it != list_.end()) it->second = Membership{Status::Active, now};
-      // tombstone GC
+      // tombstone GC, aged by the local time since the entry last advanced
+      note_heard_locked();
+      const int64_t st = steady_us();
       for (auto jt = list_.begin(); jt != list_.end();) {
-        if (jt->second.status == Status::Failed && now - jt->second.last_active > (int64_t)cfg_.tombstone_ms * 1000) {
+        if (jt->second.status == Status::Failed && st - heard_[jt->first].second > (int64_t)cfg_.tombstone_ms * 1000) {
           dead_.insert(jt->first);
+          heard_.erase(jt->first);
           jt = list_.erase(jt);
         } else {
           ++jt;
@@ -379,12 +395,13 @@ void MembershipService::detector_loop() {
     std::vector<std::string> msgs;
     {
       std::lock_guard<std::mutex> g(mu_);
-      const int64_t now = wall_us();
+      note_heard_locked();
+      const int64_t now = steady_us();
       if (!paused_.load()) {
         for (const auto& n : last_neighbors_) {
           auto it = list_.find(n);
           if (it == list_.end() || it->second.status != Status::Active) continue;
-          const int64_t el = now - it->second.last_active;
+          const int64_t el = now - heard_[n].second;
           if (el > (int64_t)cfg_.fail_ms * 1000) {
             it->second.status = Status::Failed;
             msgs.push_back("Detected failure of " + n.debug() + " that hasn't been updated for " +

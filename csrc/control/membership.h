@@ -15,7 +15,12 @@
 // neighbours (Leave message) instead of only clearing the list (#1); Failed
 // tombstones are garbage-collected after `tombstone_ms` and GC'd ids are not
 // re-admitted (#2); datagrams up to 64 KB (#2); every port, period and
-// timeout is configurable (#9). Fault-injection hooks (drop rate, pause,
+// timeout is configurable (#9). Failure detection no longer compares a remote
+// wall-clock stamp with the local clock (#3): last_active still orders one
+// node's own heartbeats (LWW), but the detector and tombstone GC age an entry
+// by the LOCAL steady time at which its last_active last advanced (heard_),
+// so clock skew between nodes cannot fail a live node (`--clock-skew-ms`
+// injects skew for the test). Fault-injection hooks (drop rate, pause,
 // partition) make failure tests deterministic on one machine.
 #pragma once
 #include <atomic>
@@ -27,6 +32,7 @@
 #include <thread>
 #include <vector>
 
+#include "common.h"
 #include "net.h"
 #include "wire.h"
 
@@ -86,6 +92,7 @@ struct MembershipConfig {
   int fail_ms = 3000;
   int tombstone_ms = 30000;
   int k = 2;
+  int64_t clock_skew_us = 0;  // fault injection: offset on this node's own wall clock
 };
 
 class MembershipService {
@@ -120,6 +127,8 @@ class MembershipService {
   void detector_loop();
   void send(const std::string& addr, const Message& m);
   bool blocked(const std::string& addr);
+  void note_heard_locked();  // refresh heard_ from list_ (mu_ held)
+  int64_t own_us() const { return wall_us() + cfg_.clock_skew_us; }
 
   MembershipConfig cfg_;
   mutable std::mutex mu_;
@@ -137,6 +146,8 @@ class MembershipService {
   std::mutex rng_mu_;
   std::mt19937_64 rng_{std::random_device{}()};
   std::atomic<uint64_t> sent_{0}, received_{0};
+  // id -> (newest last_active seen, local steady us when it last advanced)
+  std::map<Id, std::pair<int64_t, int64_t>> heard_;
 };
 
 }  // namespace ctl

@@ -205,3 +205,28 @@ def test_adaptive_rate_jobs(env, tmp_path):
         rep = n[0].cmd("jobs")
         rates = [float(x) for x in re.findall(r"Throughput: ([\d.]+) queries/s", rep)]
         assert len(rates) == 2 and all(r > 0.5 for r in rates), rep
+
+
+def test_clock_skew_does_not_fail_live_node(env, tmp_path):
+    """A node whose wall clock is 5 s behind (4x the 1.2 s failure timeout)
+    stays Active: the detector ages entries by the local time since their
+    heartbeat last advanced, not by comparing clocks.
+    A killed node is still detected."""
+    from dmlc.serve.cluster import NodeProcess
+    cl = LocalCluster(2, 19700, str(tmp_path / "c"), env["labels"], n_leaders=1, executor="cpu")
+    with cl:
+        p = 19700 + 20
+        skewed = NodeProcess(p, cl.leaders, str(tmp_path / "c" / f"n{p}"), env["labels"], executor="cpu",
+                             extra=["--clock-skew-ms", "-5000"])
+        cl.nodes.append(skewed)
+        skewed.expect(r"Address is", 20)
+        skewed.run(f"join {cl.nodes[0].address}", r"Joined!", 20)
+        cl.wait_members(3, 20)
+        time.sleep(4.0)
+        for nd in cl.nodes:
+            rows = re.findall(r"\| 127\.0\.0\.1:\d+ .*\| Active", nd.cmd("lm"))
+            assert len(rows) == 3, nd.cmd("lm")
+        flaps = [ln for nd in cl.nodes for ln in nd.lines if "Detected failure" in ln]
+        assert not flaps, flaps
+        cl.nodes[1].kill()
+        cl.wait_members(2, 20, [cl.nodes[0], skewed])
