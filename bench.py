@@ -1,35 +1,40 @@
 #!/usr/bin/env python3
 """Headline benchmark: ResNet18 ImageNet-shaped batch inference, images/s for
-the whole node plus p50/p95 query latency (BASELINE.json metric).
+the whole node plus p50/p95 latency (BASELINE.json metric).
 
-One process per GPU (torchrun for N>1, RCCL = torch.distributed "nccl").
-Each step of the timed loop is the whole serving path of the north star:
+One process per GPU. ``--gpus N`` under torchrun uses the launcher's ranks;
+without a launcher (no WORLD_SIZE in the environment) this script starts the
+N rank processes itself (127.0.0.1 rendezvous) before any GPU call.
+
+The data plane is the native layer in csrc/comm (RCCL over xGMI, driven from
+C++; torch.distributed is used only as a CPU/gloo side channel to hand out
+the RCCL unique ids, for barriers, and for the max over ranks of the timed
+region). Each step of the timed loop is the whole serving path:
 
   rank 0 holds the staged image pool (u8 [*,224,224,3], HBM-resident)
-   -> RCCL scatter of one u8 shard (per_gpu_batch images) to every rank
+   -> grouped ncclSend/ncclRecv of one u8 shard (per_gpu_batch images) to
+      every other rank, one step ahead on a high-priority comm stream
    -> on every GPU: preprocess + ResNet18 (hand-written MFMA kernels,
       hipGraph replay) + fused softmax/top-1
-   -> RCCL gather of (top-1 class, probability) back to rank 0.
+   -> grouped send/recv of (top-1 class, probability) back to rank 0 on a
+      second communicator/stream, then a D2H of the answers.
 
-The scatter of step i+1 is issued before the forward of step i, so the xGMI
-transfer overlaps compute (double-buffered input slots). ``--input-mode local``
-skips the scatter (each rank reads its own HBM-resident shard).
+``--input-mode local`` skips the scatter (each rank reads its own
+HBM-resident shard, e.g. an SDFS replica staged on that GPU).
 
 Reference numbers (CS425MP4Report.pdf p.2): ResNet18 mean query latency
 158.94 ms on CPU VMs, i.e. 6.29 images/s for one query stream; there is no
-published images/s figure, so ``vs_baseline`` divides by that derived rate
-and ``vs_baseline_latency`` compares latency directly.
+published images/s figure, so ``vs_baseline`` divides by that derived rate.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
-
-import torch
-import torch.distributed as dist
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 if ROOT not in sys.path:
@@ -48,97 +53,127 @@ def pct(xs, q):
     return xs[lo] + (xs[hi] - xs[lo]) * (k - lo)
 
 
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def spawn_ranks(n: int) -> int:
+    """Start n rank processes of this script (no GPU touched in the parent)."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env))
+    rc = 0
+    for p in procs:
+        rc = max(rc, p.wait())
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--model", default="resnet18")
     ap.add_argument("--batch", type=int, default=256, help="images per GPU per step")
     ap.add_argument("--input-mode", choices=["scatter", "local"], default="scatter")
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--latency-queries", type=int, default=200, help="batch-1 queries for query latency")
+    ap.add_argument("--latency-steps", type=int, default=50, help="unpipelined steps for the batch latency")
+    ap.add_argument("--latency-queries", type=int, default=200, help="batch-1 GPU queries (GPU-only latency)")
     ap.add_argument("--profile-ops", action="store_true", help="print per-op times of one eager forward")
-    ap.add_argument("--force-dist", action="store_true",
-                    help="use the process group (RCCL scatter/gather) even for one rank: rehearses the N>1 path")
     args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
+
+    import torch
+    import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}; launch N>1 with torchrun")
-    if world > 1:
-        # Under the concurrent RCCL scatter/gather kernels a grid that exactly
-        # fills the CUs loses a whole round when a few slots are taken: finer
-        # row-conv strips (1792 instead of 512 workgroups) cost ~1% alone and
-        # halve that loss (profiles/r1_interference.txt).
-        os.environ.setdefault("DMLC_ROWS_STRIP", "8")
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
-    distributed = world > 1 or args.force_dist
-    if distributed:
-        dist.init_process_group("nccl", device_id=dev)
+    if world > 1:
+        # CPU side channel only: unique ids, barriers, max of the timed region
+        dist.init_process_group("gloo", rank=rank, world_size=world)
 
+    import dmlc
     from dmlc.models import build, state_dict_f32
-    from dmlc.parallel import DPInference, broadcast_state_dict
     from dmlc.runtime import InferenceEngine
 
+    C = dmlc.native()
     B = args.batch
-    # Rank 0 owns the weights (random init: the reference's .ot files are LFS
-    # stubs) and broadcasts them over RCCL, like `train` distributing a model.
-    sd = state_dict_f32(build(args.model, seed=0)) if rank == 0 else None
-    sd = broadcast_state_dict(sd, 0, dev) if distributed else sd
+    scatter = args.input_mode == "scatter"
+    # Random-init weights (the reference's .ot files are LFS stubs); every
+    # rank builds the same seeded model.
+    sd = state_dict_f32(build(args.model, seed=0))
     eng = InferenceEngine(args.model, sd, device=local_rank, max_batch=B)
     use_graph = not args.no_graph
+
+    ids = [b"", b""]
+    if world > 1:
+        box = [[C.rccl_unique_id(), C.rccl_unique_id()] if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0)
+        ids = box[0]
+    runner = C.DpRunner(eng._e, world, rank, ids[0], ids[1], B, scatter=scatter, use_graph=use_graph)
 
     # Staged input pool (two global batches of distinct synthetic images) in
     # the coordinator's HBM, or every rank's own shard in local mode.
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     pool = None
-    if rank == 0 or args.input_mode == "local":
-        n_pool = 2 * (B * world if args.input_mode == "scatter" else B)
+    n_pool = 0
+    if rank == 0 or not scatter:
+        n_pool = 2 * (B * world if scatter else B)
         pool = torch.randint(0, 256, (n_pool, 224, 224, 3), dtype=torch.uint8, device=dev, generator=g)
-
-    dp = DPInference(lambda imgs, out: eng.predict(imgs, use_graph=use_graph, out=out), B, dev,
-                     input_mode=args.input_mode)
-
-    # Warmup (also captures the hipGraphs and warms RCCL channels).
-    dp.run(pool, 0, args.warmup)
+    pool_ptr = pool.data_ptr() if pool is not None else 0
     torch.cuda.synchronize()
-    if distributed:
-        dist.barrier()
-    torch.cuda.synchronize()
+
+    def barrier():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    # Warmup (captures the hipGraphs, warms the RCCL channels).
+    runner.run(pool_ptr, n_pool, 0, args.warmup)
+    barrier()
     t0 = time.perf_counter()
-    dp.run(pool, args.warmup, args.steps, stamps=False)
-    torch.cuda.synchronize()
-    if distributed:
-        dist.barrier()
-    torch.cuda.synchronize()
+    runner.run(pool_ptr, n_pool, args.warmup, args.steps)
+    barrier()
     elapsed = time.perf_counter() - t0
-    if distributed:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
+    per_rank_s = [elapsed]
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        gathered = [torch.zeros(1, dtype=torch.float64) for _ in range(world)]
+        dist.all_gather(gathered, t)
+        per_rank_s = [float(x) for x in gathered]
+        elapsed = max(per_rank_s)
 
-    # Per-batch latency (scatter issue -> gathered top-1) from event stamps, in
-    # a separate pass: the stamps' stream barriers would otherwise sit inside
-    # the throughput measurement.
-    n_lat = min(args.steps, 50)
-    lat0 = args.warmup + args.steps
-    dp.run(pool, lat0, n_lat)
-    torch.cuda.synchronize()
-    batch_lat = [dp.latency_ms(i) for i in range(lat0, lat0 + n_lat)]
+    # Per-batch latency: unpipelined steps, scatter issue -> answers on the
+    # coordinator's host.
+    lat = runner.run(pool_ptr, n_pool, args.warmup + args.steps, args.latency_steps, pipelined=False)
+    batch_lat = lat["step_ms"]
+    barrier()
 
-    # Sanity: the coordinator's gathered outputs are valid class ids / probabilities.
     if rank == 0:
-        ids, probs = dp.results(lat0 + n_lat - 1)
-        assert ids.numel() == B * world
-        assert int(ids.min()) >= 0 and int(ids.max()) < 1000, "bad class ids"
-        assert float(probs.min()) > 0 and float(probs.max()) <= 1.0001, "bad probabilities"
+        idx, prob = runner.last_results()
+        assert len(idx) == B * world
+        assert min(idx) >= 0 and max(idx) < 1000, "bad class ids"
+        assert min(prob) > 0 and max(prob) <= 1.0001, "bad probabilities"
 
-    # Batch-1 query latency (hipGraph replay of preprocess+forward+top-1 for
-    # one image, host-timed end to end including the D2H of the answer).
+    # Batch-1 GPU-only latency (hipGraph replay of preprocess+forward+top-1
+    # for one HBM-resident image, host-timed including the D2H of the
+    # answer). Not the reference's query definition (which includes the RPC
+    # and the JPEG decode): that one is tools/bench_jobs.py's.
     qlat = []
     if rank == 0 and args.latency_queries > 0:
         q_eng = InferenceEngine(args.model, sd, device=local_rank, max_batch=1)
@@ -181,22 +216,25 @@ def main():
                 "image_size": 224,
                 "parallelism": f"dp{world}",
                 "input_mode": args.input_mode,
+                "comm": "native RCCL grouped send/recv (csrc/comm), shards + answers on separate communicators",
+                "rccl_ranks": world,
                 "hipgraph": use_graph,
                 "baseline": "6.29 img/s = one query stream at the reference's 158.94 ms mean ResNet18 latency "
                             "(CS425MP4Report.pdf p.2; no images/s is published)",
             },
+            "per_rank_images_s": [round(B * args.steps / s, 1) for s in per_rank_s],
             "batch_latency_p50_ms": round(pct(batch_lat, 50), 3),
             "batch_latency_p95_ms": round(pct(batch_lat, 95), 3),
-            "query_latency_p50_ms": round(pct(qlat, 50), 4) if qlat else None,
-            "query_latency_p95_ms": round(pct(qlat, 95), 4) if qlat else None,
-            "vs_baseline_latency": round(REF_MEAN_LATENCY_MS / pct(qlat, 50), 1) if qlat else None,
+            "gpu_batch1_latency_p50_ms": round(pct(qlat, 50), 4) if qlat else None,
+            "gpu_batch1_latency_p95_ms": round(pct(qlat, 95), 4) if qlat else None,
             "tflops_effective": round(value * eng.gflop_per_image / 1e3, 1),
         }
         if ops_profile:
             print("# per-op (ms): " + ", ".join(f"{n}={t:.3f}" for n, t in ops_profile), file=sys.stderr)
         print(json.dumps(res), flush=True)
 
-    if distributed:
+    del runner
+    if world > 1:
         dist.barrier()
         dist.destroy_process_group()
 

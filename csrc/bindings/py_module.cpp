@@ -51,6 +51,8 @@ py::dict from_weight_map(const WeightMap& w) {
 
 }  // namespace
 
+void bind_dp(py::module& m);  // py_dp.cpp
+
 PYBIND11_MODULE(_C, m) {
   m.doc() = "dmlc native runtime: CDNA4 HIP kernels, inference engine, .ot I/O";
 
@@ -265,4 +267,7 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("weight_bytes", &Engine::weight_bytes)
       .def_property_readonly("activation_bytes", &Engine::activation_bytes)
       .def_property_readonly("gflop_per_image", &Engine::gflop_per_image);
+
+  // ---------------------------------------------------------------- data parallel
+  bind_dp(m);
 }

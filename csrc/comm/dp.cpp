@@ -1,0 +1,475 @@
+#include "dp.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cstdlib>
+#include <cstring>
+#include <thread>
+
+namespace dmlc {
+namespace dp {
+
+// ------------------------------------------------------------------ host worker
+namespace {
+
+class HostWorker : public Worker {
+ public:
+  HostWorker(int device, int H, int W, int classes) : device_(device), bytes_((size_t)H * W * 3), classes_(classes) {}
+  ~HostWorker() override {
+    for (void* p : live_) std::free(p);
+  }
+  int device() const override { return device_; }
+  void* alloc(size_t bytes) override { return track(std::calloc(1, std::max<size_t>(bytes, 1))); }
+  void dealloc(void* p) override { untrack(p); }
+  void* alloc_host(size_t bytes) override { return alloc(bytes); }
+  void dealloc_host(void* p) override { untrack(p); }
+  Stream stream(int) override { return nullptr; }
+  int new_event() override { return n_events_++; }
+  void record(int, int) override {}
+  void wait(int, int) override {}
+  bool query(int) override { return true; }
+  void sync(int) override {}
+  void sync_all() override {}
+  void classify(const uint8_t* images, int B, int32_t* idx, float* prob) override {
+    for (int b = 0; b < B; ++b) {
+      const uint8_t* img = images + (size_t)b * bytes_;
+      idx[b] = host_class_of(img, bytes_, classes_);
+      prob[b] = host_prob_of(img);
+    }
+  }
+  void copy_d2h(void* dst, const void* src, size_t bytes, int) override { std::memmove(dst, src, bytes); }
+  void copy(void* dst, const void* src, size_t bytes, int) override { std::memmove(dst, src, bytes); }
+  bool healthy() override { return healthy_; }
+  bool healthy_ = true;
+
+ private:
+  void* track(void* p) {
+    if (!p) throw std::bad_alloc();
+    live_.push_back(p);
+    return p;
+  }
+  void untrack(void* p) {
+    auto it = std::find(live_.begin(), live_.end(), p);
+    if (it != live_.end()) {
+      std::free(p);
+      live_.erase(it);
+    }
+  }
+  int device_;
+  size_t bytes_;
+  int classes_;
+  int n_events_ = 0;
+  std::vector<void*> live_;
+};
+
+}  // namespace
+
+std::unique_ptr<Worker> make_host_worker(int device, int H, int W, int classes) {
+  return std::make_unique<HostWorker>(device, H, W, classes);
+}
+
+void host_worker_set_healthy(Worker& w, bool healthy) {
+  auto* h = dynamic_cast<HostWorker*>(&w);
+  if (!h) throw std::invalid_argument("host_worker_set_healthy: not a host worker");
+  h->healthy_ = healthy;
+}
+
+int host_class_of(const uint8_t* img, size_t bytes, int classes) {
+  uint64_t s = 0;
+  for (size_t i = 0; i < bytes; ++i) s += img[i];
+  return (int)(s % (uint64_t)classes);
+}
+
+float host_prob_of(const uint8_t* img) { return (img[0] + 1) / 257.f; }
+
+std::vector<int> shard_counts(int64_t n, int world, int cap) {
+  if (world < 1) throw std::invalid_argument("shard_counts: world < 1");
+  if (n < 0 || n > (int64_t)world * cap) throw std::invalid_argument("shard_counts: n exceeds world * cap");
+  std::vector<int> c(world, (int)(n / world));
+  for (int r = 0; r < (int)(n % world); ++r) ++c[r];
+  return c;
+}
+
+// ------------------------------------------------------------------ rank
+Rank::Rank(Worker* w, int max_per_rank, size_t image_bytes, bool scatter, int slots)
+    : w_(w), max_(max_per_rank), slots_(slots), ib_(image_bytes), scatter_(scatter) {
+  if (max_ < 1 || slots_ < 2) throw std::invalid_argument("dp::Rank: need max_per_rank >= 1 and slots >= 2");
+  w_->activate();
+  for (int s = 0; s < slots_; ++s) {
+    ev_in_.push_back(w_->new_event());
+    ev_comp_.push_back(w_->new_event());
+    ev_out_.push_back(w_->new_event());
+  }
+  inbuf_.assign(slots_, nullptr);
+  ans_.assign(slots_, nullptr);
+  host_ans_.assign(slots_, nullptr);
+  reset();
+}
+
+Rank::~Rank() {
+  w_->activate();
+  w_->sync_all();
+  for (void* p : inbuf_)
+    if (p) w_->dealloc(p);
+  for (void* p : ans_)
+    if (p) w_->dealloc(p);
+  for (void* p : host_ans_)
+    if (p) w_->dealloc_host(p);
+}
+
+void Rank::reset() {
+  in_used_.assign(slots_, false);
+  out_used_.assign(slots_, false);
+}
+
+void Rank::attach(Comm* in, Comm* out) {
+  if ((in == nullptr) != (out == nullptr)) throw std::invalid_argument("dp::Rank::attach: both or no comms");
+  if (in && (in->size() != out->size() || in->rank() != out->rank()))
+    throw std::invalid_argument("dp::Rank::attach: shard and answer communicators disagree");
+  w_->activate();
+  w_->sync_all();  // nothing of the old binding may still be in flight
+  in_ = in;
+  out_ = out;
+  reset();
+  const int world = this->world();
+  if (scatter_ && !root()) {
+    for (auto& p : inbuf_)
+      if (!p) p = w_->alloc((size_t)max_ * ib_);
+  }
+  const int blocks = root() ? world : 1;
+  if (blocks > ans_world_) {
+    for (auto& p : ans_) {
+      if (p) w_->dealloc(p);
+      p = w_->alloc((size_t)blocks * block_bytes());
+    }
+    for (auto& p : host_ans_) {
+      if (p) w_->dealloc_host(p);
+      p = root() ? w_->alloc_host((size_t)blocks * block_bytes()) : nullptr;
+    }
+    ans_world_ = blocks;
+  }
+  if (root())
+    for (auto& p : host_ans_)
+      if (!p) p = w_->alloc_host((size_t)ans_world_ * block_bytes());
+}
+
+void Rank::post_input(const StepPlan& p) {
+  if (!scatter_ || world() == 1) return;
+  const int s = slot(p);
+  if (root()) {
+    if (p.src_event >= 0) w_->wait(Worker::kIn, p.src_event);
+    size_t off = (size_t)p.counts[0];
+    for (int r = 1; r < world(); ++r) {
+      if (p.counts[r] > 0) in_->send(p.src + off * ib_, (size_t)p.counts[r] * ib_, r, w_->stream(Worker::kIn));
+      off += (size_t)p.counts[r];
+    }
+  } else {
+    if (in_used_[s]) w_->wait(Worker::kIn, ev_comp_[s]);  // compute(step - slots) has read this slot
+    const int n = p.counts[rank()];
+    if (n > 0) in_->recv(inbuf_[s], (size_t)n * ib_, 0, w_->stream(Worker::kIn));
+  }
+}
+
+void Rank::after_input(const StepPlan& p) {
+  if (!scatter_ || world() == 1 || root()) return;
+  w_->record(ev_in_[slot(p)], Worker::kIn);
+}
+
+void Rank::compute(const StepPlan& p) {
+  const int s = slot(p);
+  const int n = p.counts.at(rank());
+  if (n > max_) throw std::invalid_argument("dp::Rank::compute: shard larger than max_per_rank");
+  const bool received = scatter_ && !root() && world() > 1;
+  const uint8_t* img = received ? (const uint8_t*)inbuf_[s] : p.src;
+  if (received) w_->wait(Worker::kCompute, ev_in_[s]);
+  else if (root() && p.src_event >= 0) w_->wait(Worker::kCompute, p.src_event);
+  if (out_used_[s]) w_->wait(Worker::kCompute, ev_out_[s]);  // gather(step - slots) has read the answers
+  auto* blk = (uint8_t*)ans_[s];
+  if (n > 0) {
+    if (!img) throw std::invalid_argument("dp::Rank::compute: no images for this rank");
+    w_->classify(img, n, (int32_t*)blk, (float*)(blk + (size_t)max_ * 4));
+  }
+  w_->record(ev_comp_[s], Worker::kCompute);
+  in_used_[s] = true;
+}
+
+void Rank::post_output(const StepPlan& p) {
+  const int s = slot(p);
+  w_->wait(Worker::kOut, ev_comp_[s]);
+  if (world() == 1) return;
+  if (root()) {
+    for (int r = 1; r < world(); ++r)
+      if (p.counts[r] > 0)
+        out_->recv((uint8_t*)ans_[s] + (size_t)r * block_bytes(), block_bytes(), r, w_->stream(Worker::kOut));
+  } else if (p.counts[rank()] > 0) {
+    out_->send(ans_[s], block_bytes(), 0, w_->stream(Worker::kOut));
+  }
+}
+
+void Rank::after_output(const StepPlan& p) {
+  const int s = slot(p);
+  if (root()) w_->copy_d2h(host_ans_[s], ans_[s], (size_t)world() * block_bytes(), Worker::kOut);
+  w_->record(ev_out_[s], Worker::kOut);
+  out_used_[s] = true;
+}
+
+void Rank::wait_step(const StepPlan& p, int timeout_ms) {
+  const int s = slot(p);
+  const auto t0 = std::chrono::steady_clock::now();
+  int spins = 0;
+  while (!w_->query(ev_out_[s])) {
+    if ((in_ && !in_->ok()) || (out_ && !out_->ok())) throw comm::CommError("dp: communicator error while waiting");
+    if (timeout_ms >= 0 &&
+        std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(timeout_ms))
+      throw comm::CommError("dp: step " + std::to_string(p.step) + " timed out");
+    if (++spins > 64) std::this_thread::sleep_for(std::chrono::microseconds(20));
+  }
+}
+
+void Rank::collect(const StepPlan& p, int32_t* idx, float* prob, int timeout_ms) {
+  if (!root()) throw std::logic_error("dp::Rank::collect on a non-coordinator rank");
+  wait_step(p, timeout_ms);
+  const int s = slot(p);
+  const auto* h = (const uint8_t*)host_ans_[s];
+  size_t off = 0;
+  for (int r = 0; r < world(); ++r) {
+    const int n = p.counts[r];
+    const auto* blk = h + (size_t)r * block_bytes();
+    if (n > 0) {
+      std::memcpy(idx + off, blk, (size_t)n * 4);
+      std::memcpy(prob + off, blk + (size_t)max_ * 4, (size_t)n * 4);
+    }
+    off += (size_t)n;
+  }
+}
+
+// ------------------------------------------------------------------ pipeline
+PipelineResult run_pipeline(const std::vector<Rank*>& ranks, int64_t first, int64_t n, const PlanFn& plan,
+                            const ResultFn& on_result, int timeout_ms, bool pipelined) {
+  PipelineResult res;
+  if (n <= 0 || ranks.empty()) return res;
+  Comm* gcomm = ranks.front()->comm_in();  // null for a world of one
+  size_t root_i = ranks.size();
+  for (size_t i = 0; i < ranks.size(); ++i)
+    if (ranks[i]->root()) root_i = i;
+
+  // plans of the steps in flight (at most three)
+  std::vector<std::pair<int64_t, std::vector<StepPlan>>> live;
+  auto plans_of = [&](int64_t step) -> std::vector<StepPlan>& {
+    for (auto& kv : live)
+      if (kv.first == step) return kv.second;
+    std::vector<StepPlan> ps;
+    ps.reserve(ranks.size());
+    for (Rank* r : ranks) ps.push_back(plan(step, *r));  // may throw: nothing of the step is posted yet
+    live.emplace_back(step, std::move(ps));
+    return live.back().second;
+  };
+  auto drop = [&](int64_t step) {
+    live.erase(std::remove_if(live.begin(), live.end(), [&](const auto& kv) { return kv.first == step; }),
+               live.end());
+  };
+  // Groups are thread-wide in both backends: bracketing through one rank's
+  // communicator groups the operations of every rank this thread drives.
+  auto phase = [&](const std::vector<StepPlan>& ps, bool input) {
+    if (gcomm) gcomm->group_start();
+    try {
+      for (size_t i = 0; i < ranks.size(); ++i) input ? ranks[i]->post_input(ps[i]) : ranks[i]->post_output(ps[i]);
+    } catch (...) {
+      if (gcomm) gcomm->group_end();
+      throw;
+    }
+    if (gcomm) gcomm->group_end();
+    for (size_t i = 0; i < ranks.size(); ++i) input ? ranks[i]->after_input(ps[i]) : ranks[i]->after_output(ps[i]);
+  };
+
+  std::vector<int32_t> idx;
+  std::vector<float> prob;
+  auto finish = [&](int64_t step) {
+    auto& ps = plans_of(step);
+    if (root_i < ranks.size()) {
+      const auto& p = ps[root_i];
+      int64_t total = 0;
+      for (int c : p.counts) total += c;
+      idx.resize((size_t)total);
+      prob.resize((size_t)total);
+      ranks[root_i]->collect(p, idx.data(), prob.data(), timeout_ms);
+      res.images += total;
+      if (on_result) on_result(p, idx.data(), prob.data());
+    } else {
+      ranks.front()->wait_step(ps.front(), timeout_ms);  // keep the host one step ahead at most
+    }
+    ++res.steps;
+    drop(step);
+  };
+
+  const int64_t end = first + n;
+  if (!pipelined) {  // latency mode: one step in flight
+    for (int64_t i = first; i < end; ++i) {
+      const auto t0 = std::chrono::steady_clock::now();
+      auto& ps = plans_of(i);
+      phase(ps, true);
+      for (size_t k = 0; k < ranks.size(); ++k) ranks[k]->compute(ps[k]);
+      phase(ps, false);
+      finish(i);
+      res.step_ms.push_back(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    }
+    return res;
+  }
+  phase(plans_of(first), true);
+  for (int64_t i = first; i < end; ++i) {
+    if (i + 1 < end) phase(plans_of(i + 1), true);
+    auto& ps = plans_of(i);
+    for (size_t k = 0; k < ranks.size(); ++k) ranks[k]->compute(ps[k]);
+    phase(ps, false);
+    if (i > first) finish(i - 1);
+  }
+  finish(end - 1);
+  return res;
+}
+
+// ------------------------------------------------------------------ group
+
+namespace {
+// Thrown by the plan function when fault injection drops a member: nothing
+// of the step being planned has been posted yet.
+struct MemberLost {
+  int member;
+};
+}  // namespace
+
+Group::Group(std::vector<Worker*> workers, CommFactory make_comms, int max_per_rank, size_t image_bytes,
+             int timeout_ms)
+    : workers_(std::move(workers)), make_comms_(std::move(make_comms)), max_(max_per_rank), ib_(image_bytes),
+      timeout_ms_(timeout_ms) {
+  if (workers_.empty()) throw std::invalid_argument("dp::Group: no workers");
+  lost_.assign(workers_.size(), false);
+  fail_at_.assign(workers_.size(), -1);
+  fail_abrupt_.assign(workers_.size(), false);
+  for (size_t i = 0; i < workers_.size(); ++i) {
+    members_.push_back((int)i);
+    ranks_.push_back(std::make_unique<Rank>(workers_[i], max_, ib_, /*scatter=*/true));
+  }
+  rebuild();
+}
+
+Group::~Group() {
+  for (auto& r : ranks_) r->worker()->sync_all();
+  ranks_.clear();
+  cin_.clear();
+  cout_.clear();
+}
+
+void Group::rebuild() {
+  cin_.clear();
+  cout_.clear();
+  if (members_.size() > 1) {
+    cin_ = make_comms_(members_);
+    cout_ = make_comms_(members_);
+    if (cin_.size() != members_.size() || cout_.size() != members_.size())
+      throw std::runtime_error("dp::Group: communicator factory returned the wrong number of ranks");
+  }
+  for (size_t i = 0; i < members_.size(); ++i) {
+    Rank& r = *ranks_[members_[i]];
+    if (members_.size() > 1) r.attach(cin_[i].get(), cout_[i].get());
+    else r.attach(nullptr, nullptr);
+  }
+}
+
+void Group::fail(int m, int64_t after_steps, bool abrupt) {
+  if (m <= 0 || m >= (int)workers_.size()) throw std::invalid_argument("dp::Group::fail: bad member (0 is the coordinator)");
+  fail_at_[m] = std::max<int64_t>(0, after_steps);
+  fail_abrupt_[m] = abrupt;
+}
+
+void Group::kill_now(int m) {
+  if (m <= 0 || m >= (int)workers_.size()) throw std::invalid_argument("dp::Group::kill_now: bad member");
+  auto it = std::find(members_.begin(), members_.end(), m);
+  if (it == members_.end()) return;
+  host_worker_set_healthy(*workers_[m], false);
+  const int rank = (int)(it - members_.begin());
+  if (!cin_.empty()) {
+    comm::host_kill(*cin_[0], rank);
+    comm::host_kill(*cout_[0], rank);
+  }
+}
+
+Group::Stats Group::classify(const uint8_t* src, int64_t n, int32_t* idx, float* prob, int src_event,
+                             int32_t* commit_count) {
+  Stats st;
+  int64_t committed = 0;  // answers [0, committed) are final
+  int64_t issued = 0;     // images whose step was planned (posted) in the current attempt
+  while (committed < n) {
+    const int world = (int)members_.size();
+    const int64_t G = (int64_t)max_ * world;
+    const int64_t base = committed;
+    const int64_t steps = (n - base + G - 1) / G;
+    issued = base;
+    std::vector<Rank*> rs;
+    for (int m : members_) rs.push_back(ranks_[m].get());
+    auto plan = [&](int64_t step, const Rank& r) {
+      if (&r == rs.front()) {  // once per step, before anything of it is posted
+        for (int m : members_) {
+          if (fail_at_[m] == 0) {
+            fail_at_[m] = -1;
+            if (!fail_abrupt_[m]) throw MemberLost{m};
+            kill_now(m);  // this step's operations with m fail
+          } else if (fail_at_[m] > 0) {
+            --fail_at_[m];
+          }
+        }
+        issued = std::min<int64_t>(n, base + (step + 1) * G);
+      }
+      StepPlan p;
+      p.step = step;
+      const int64_t start = base + step * G;
+      p.counts = shard_counts(std::min<int64_t>(G, n - start), world, max_);
+      p.src = src + (size_t)start * ib_;
+      p.src_event = r.root() ? src_event : -1;
+      return p;
+    };
+    auto on_result = [&](const StepPlan& p, const int32_t* i, const float* pr) {
+      const int64_t start = base + p.step * G;
+      int64_t total = 0;
+      for (int c : p.counts) total += c;
+      std::memcpy(idx + start, i, (size_t)total * 4);
+      std::memcpy(prob + start, pr, (size_t)total * 4);
+      if (commit_count)
+        for (int64_t k = 0; k < total; ++k) ++commit_count[start + k];
+      committed = start + total;
+      ++st.steps;
+    };
+    std::vector<int> lost;
+    try {
+      run_pipeline(rs, 0, steps, plan, on_result, timeout_ms_);
+      break;
+    } catch (const MemberLost& e) {
+      // injected: the GPU is in fact fine, so everything already posted
+      // completes; drain it, then drop the member
+      for (int m : members_) workers_[m]->sync_all();
+      lost.push_back(e.member);
+    } catch (const comm::CommError&) {
+      for (int m : members_)
+        if (!workers_[m]->healthy()) lost.push_back(m);
+      if (lost.empty()) throw;  // not attributable to a lost GPU
+    }
+    if (std::find(lost.begin(), lost.end(), members_.front()) != lost.end())
+      throw comm::CommError("dp::Group: the coordinator GPU was lost");
+    // abort the broken communicators (RCCL: also ends kernels blocked on
+    // the lost peer), then rebuild over the survivors
+    for (auto& c : cin_) c->abort();
+    for (auto& c : cout_) c->abort();
+    for (int m : members_)
+      if (std::find(lost.begin(), lost.end(), m) == lost.end()) workers_[m]->sync_all();
+    for (int m : lost) lost_[m] = true;
+    members_.erase(std::remove_if(members_.begin(), members_.end(), [&](int m) { return lost_[m]; }),
+                   members_.end());
+    ++st.recoveries;
+    st.redone_images += issued - committed;
+    rebuild();
+  }
+  st.images = n;
+  return st;
+}
+
+}  // namespace dp
+}  // namespace dmlc

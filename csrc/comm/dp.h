@@ -1,0 +1,205 @@
+// Data-parallel batch inference over the GPUs of one node: the coordinator
+// (rank 0) scatters u8 image shards, every rank classifies its shard, and the
+// (class, probability) answers are gathered back to rank 0 — all enqueued on
+// HIP streams so the transfers of one step overlap the compute of another.
+//
+// Reference counterpart: the leader's query fan-out (`run_job`,
+// src/services.rs:407-433: one single-image TCP RPC per 0.5 s tick to a random
+// member) and the member's forward (`Member::predict`, :475-497). SURVEY.md
+// §2.3/§2.6 map that fan-out onto RCCL send/recv over xGMI.
+//
+// Layers:
+//   Worker    one GPU's compute side: streams, events, memory, classify()
+//             (HipWorker: the HIP engine; HostWorker: a CPU stand-in for tests)
+//   Rank      one rank's per-step protocol (double-buffered slots, events)
+//   Pipeline  the issue order of a run for the ranks one thread drives (one
+//             rank per process, or every rank from one thread)
+//   Group     one process owning several GPUs (dmlc-node --gpus N): runs a
+//             classification job over them and survives the loss of a
+//             non-coordinator GPU (abort, rebuild over the survivors, redo
+//             every image whose answer was not yet committed).
+#pragma once
+#include <cstdint>
+#include <functional>
+#include <memory>
+#include <vector>
+
+#include "comm.h"
+
+namespace dmlc {
+class Engine;
+namespace dp {
+
+using comm::Comm;
+using comm::Stream;
+
+class Worker {
+ public:
+  enum StreamId { kCompute = 0, kIn = 1, kOut = 2 };
+  virtual ~Worker() = default;
+  virtual int device() const = 0;
+  virtual void activate() {}                          // make this worker's device current
+  virtual void* alloc(size_t bytes) = 0;              // device memory
+  virtual void dealloc(void* p) = 0;
+  virtual void* alloc_host(size_t bytes) = 0;         // pinned host memory
+  virtual void dealloc_host(void* p) = 0;
+  virtual Stream stream(int id) = 0;
+  virtual int new_event() = 0;
+  virtual void record(int ev, int stream_id) = 0;
+  virtual void wait(int stream_id, int ev) = 0;       // stream waits for the event
+  virtual bool query(int ev) = 0;                     // event reached?
+  virtual void sync(int ev) = 0;
+  virtual void sync_all() = 0;
+  // images: u8 [B, H, W, 3] (worker memory); answers written on kCompute.
+  virtual void classify(const uint8_t* images, int B, int32_t* idx, float* prob) = 0;
+  virtual void copy_d2h(void* dst, const void* src, size_t bytes, int stream_id) = 0;
+  virtual void copy(void* dst, const void* src, size_t bytes, int stream_id) = 0;
+  // False once the device reported an error (a lost GPU); never blocks.
+  virtual bool healthy() { return true; }
+};
+
+// Host stand-in: plain memory, synchronous "streams" (events are no-ops), and
+// a deterministic classifier: class = (sum of the image's bytes) % classes,
+// prob = (first byte + 1) / 257.
+std::unique_ptr<Worker> make_host_worker(int device, int H, int W, int classes = 1000);
+// Test hook: a host worker that reports itself unhealthy (a lost GPU).
+void host_worker_set_healthy(Worker& w, bool healthy);
+// The HIP engine on its device (csrc/comm/hip_worker.cpp): images are u8
+// [B, H, W, 3]; use_graph replays the engine's captured hipGraph.
+std::unique_ptr<Worker> make_hip_worker(Engine* engine, int H, int W, bool use_graph = true);
+int host_class_of(const uint8_t* img, size_t bytes, int classes = 1000);
+float host_prob_of(const uint8_t* img);
+
+// Balanced split of n images over `world` ranks (lower ranks take the
+// remainder), every count <= cap.
+std::vector<int> shard_counts(int64_t n, int world, int cap);
+
+struct StepPlan {
+  int64_t step = 0;          // sequence number; slot = step % slots
+  std::vector<int> counts;   // images per rank (same on every rank)
+  // scatter mode: the step's images on the coordinator (rank r's shard at
+  // image offset sum(counts[0..r))); local mode: this rank's own images.
+  const uint8_t* src = nullptr;
+  int src_event = -1;        // coordinator: event (on kCompute) after which src is valid
+};
+
+class Rank {
+ public:
+  // scatter: the coordinator sends every other rank its shard; otherwise
+  // each rank reads its own images (local mode: no input transfer).
+  Rank(Worker* w, int max_per_rank, size_t image_bytes, bool scatter, int slots = 2);
+  ~Rank();
+  Rank(const Rank&) = delete;
+  Rank& operator=(const Rank&) = delete;
+
+  // (Re)bind to communicators: `in` carries shards, `out` carries answers
+  // (separate communicators on separate streams, so a gather is never queued
+  // behind the next step's scatter). The coordinator is rank 0 of both.
+  void attach(Comm* in, Comm* out);
+  int rank() const { return in_ ? in_->rank() : 0; }
+  int world() const { return in_ ? in_->size() : 1; }
+  bool root() const { return rank() == 0; }
+  Worker* worker() const { return w_; }
+  int max_per_rank() const { return max_; }
+  int slots() const { return slots_; }
+
+  // Phases of one step; post_* go inside a comm group, after_* right after it.
+  void post_input(const StepPlan& p);
+  void after_input(const StepPlan& p);
+  void compute(const StepPlan& p);
+  void post_output(const StepPlan& p);
+  void after_output(const StepPlan& p);
+  // Coordinator: wait for the step's answers (timeout_ms < 0: forever; on a
+  // timeout or a communicator error throws CommError) and copy them in
+  // global image order.
+  void collect(const StepPlan& p, int32_t* idx, float* prob, int timeout_ms = -1);
+  // Wait until the step's answers have left (non-root) / landed (root).
+  void wait_step(const StepPlan& p, int timeout_ms = -1);
+  Comm* comm_in() const { return in_; }
+  Comm* comm_out() const { return out_; }
+  // Forget slot history (after a rebuild every slot is free again).
+  void reset();
+
+ private:
+  int slot(const StepPlan& p) const { return (int)(p.step % slots_); }
+  size_t block_bytes() const { return (size_t)max_ * 8; }  // [idx int32 x max][prob f32 x max]
+  Worker* w_;
+  Comm* in_ = nullptr;
+  Comm* out_ = nullptr;
+  int max_, slots_;
+  size_t ib_;
+  bool scatter_;
+  std::vector<void*> inbuf_;       // non-root scatter: received shards
+  std::vector<void*> ans_;         // answers: root world blocks, others one block
+  std::vector<void*> host_ans_;    // root: pinned copy of the gathered answers
+  std::vector<int> ev_in_, ev_comp_, ev_out_;
+  std::vector<bool> in_used_, out_used_;
+  int ans_world_ = 0;
+};
+
+// Issue order for the ranks one thread drives (all in one comm group per
+// phase): input(first); per step i: input(i+1), compute(i), output(i), then
+// the coordinator collects step i-1 (one step behind, so the host never waits
+// for the step it just issued).
+struct PipelineResult {
+  int64_t steps = 0, images = 0;
+  std::vector<double> step_ms;  // unpipelined runs: input issue -> answers collected, per step (coordinator)
+};
+using PlanFn = std::function<StepPlan(int64_t step, const Rank& r)>;
+using ResultFn = std::function<void(const StepPlan& p, const int32_t* idx, const float* prob)>;
+PipelineResult run_pipeline(const std::vector<Rank*>& ranks, int64_t first, int64_t n, const PlanFn& plan,
+                            const ResultFn& on_result, int timeout_ms = -1, bool pipelined = true);
+
+// One process owning several GPUs.
+class Group {
+ public:
+  using CommFactory = std::function<std::vector<std::unique_ptr<Comm>>(const std::vector<int>& members)>;
+  // workers[0] is the coordinator. make_comms(members) returns one
+  // communicator per member (rank i = members[i]); it is called twice per
+  // (re)build (shards and answers use separate communicators).
+  Group(std::vector<Worker*> workers, CommFactory make_comms, int max_per_rank, size_t image_bytes,
+        int timeout_ms = 30000);
+  ~Group();
+
+  struct Stats {
+    int64_t images = 0, steps = 0;
+    int recoveries = 0;
+    int64_t redone_images = 0;  // images classified again after a loss
+  };
+  // Classify n images stored contiguously at `src` (coordinator memory),
+  // answers in input order. `src_event`: coordinator event after which src
+  // is valid (-1: already valid).
+  // commit_count (optional, n entries): +1 per image each time its answer is
+  // committed (tests check exactly-once).
+  Stats classify(const uint8_t* src, int64_t n, int32_t* idx, float* prob, int src_event = -1,
+                 int32_t* commit_count = nullptr);
+  // Fault injection: member `m` (index into workers, not the coordinator)
+  // is lost before its next step; with after_steps > 0, once that many more
+  // steps have been issued. The lost GPU is dropped without a communicator
+  // error (the operations already posted complete), then the group rebuilds.
+  // abrupt (host communicators only, a test hook): the member dies in the
+  // middle of that step instead — its communicator operations fail and its
+  // worker reports unhealthy — so the recovery runs from a CommError, as
+  // after a real GPU loss.
+  void fail(int m, int64_t after_steps = 0, bool abrupt = false);
+  std::vector<int> members() const { return members_; }
+  int size() const { return (int)members_.size(); }
+
+ private:
+  void rebuild();
+  std::vector<Worker*> workers_;
+  CommFactory make_comms_;
+  int max_;
+  size_t ib_;
+  int timeout_ms_;
+  std::vector<int> members_;  // live workers, coordinator first
+  std::vector<std::unique_ptr<Rank>> ranks_;  // one per worker (index = worker)
+  std::vector<std::unique_ptr<Comm>> cin_, cout_;
+  std::vector<bool> lost_;
+  std::vector<int64_t> fail_at_;  // per worker: steps still to issue before it is lost (-1: never)
+  std::vector<bool> fail_abrupt_;
+  void kill_now(int m);
+};
+
+}  // namespace dp
+}  // namespace dmlc

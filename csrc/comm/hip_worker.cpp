@@ -1,0 +1,103 @@
+// dp::Worker on one MI355X: the HIP engine on a compute stream, and two
+// communication streams (shards in, answers out) created at a higher
+// priority, so the RCCL send/recv kernels of the next step are dispatched
+// promptly next to the running forward instead of queueing behind its
+// workgroups.
+#include <hip/hip_runtime.h>
+
+#include "../kernels/kernels.h"
+#include "../runtime/engine.h"
+#include "dp.h"
+
+namespace dmlc {
+namespace dp {
+namespace {
+
+class HipWorker : public Worker {
+ public:
+  HipWorker(Engine* e, int H, int W, bool use_graph) : e_(e), dev_(e->device()), H_(H), W_(W), graph_(use_graph) {
+    DMLC_HIP_CHECK(hipSetDevice(dev_));
+    int lo = 0, hi = 0;
+    DMLC_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    DMLC_HIP_CHECK(hipStreamCreateWithPriority(&s_[kCompute], hipStreamNonBlocking, lo));
+    DMLC_HIP_CHECK(hipStreamCreateWithPriority(&s_[kIn], hipStreamNonBlocking, hi));
+    DMLC_HIP_CHECK(hipStreamCreateWithPriority(&s_[kOut], hipStreamNonBlocking, hi));
+  }
+  ~HipWorker() override {
+    (void)hipSetDevice(dev_);
+    for (auto s : s_) (void)hipStreamSynchronize(s);
+    for (auto ev : evs_) (void)hipEventDestroy(ev);
+    for (auto s : s_) (void)hipStreamDestroy(s);
+  }
+  int device() const override { return dev_; }
+  void activate() override { DMLC_HIP_CHECK(hipSetDevice(dev_)); }
+  void* alloc(size_t bytes) override {
+    void* p = nullptr;
+    activate();
+    DMLC_HIP_CHECK(hipMalloc(&p, std::max<size_t>(bytes, 256)));
+    return p;
+  }
+  void dealloc(void* p) override {
+    activate();
+    (void)hipFree(p);
+  }
+  void* alloc_host(size_t bytes) override {
+    void* p = nullptr;
+    DMLC_HIP_CHECK(hipHostMalloc(&p, std::max<size_t>(bytes, 256), hipHostMallocDefault));
+    return p;
+  }
+  void dealloc_host(void* p) override { (void)hipHostFree(p); }
+  Stream stream(int id) override { return s_[id]; }
+  int new_event() override {
+    activate();
+    hipEvent_t ev;
+    DMLC_HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    evs_.push_back(ev);
+    return (int)evs_.size() - 1;
+  }
+  void record(int ev, int sid) override { DMLC_HIP_CHECK(hipEventRecord(evs_.at(ev), s_[sid])); }
+  void wait(int sid, int ev) override { DMLC_HIP_CHECK(hipStreamWaitEvent(s_[sid], evs_.at(ev), 0)); }
+  bool query(int ev) override {
+    hipError_t e = hipEventQuery(evs_.at(ev));
+    if (e == hipSuccess) return true;
+    if (e == hipErrorNotReady) return false;
+    throw comm::CommError(std::string("dp: device ") + std::to_string(dev_) + " error: " + hipGetErrorString(e));
+  }
+  void sync(int ev) override { DMLC_HIP_CHECK(hipEventSynchronize(evs_.at(ev))); }
+  void sync_all() override {
+    activate();
+    for (auto s : s_) DMLC_HIP_CHECK(hipStreamSynchronize(s));
+  }
+  void classify(const uint8_t* images, int B, int32_t* idx, float* prob) override {
+    e_->forward(images, B, H_, W_, idx, prob, nullptr, s_[kCompute], graph_);
+  }
+  void copy_d2h(void* dst, const void* src, size_t bytes, int sid) override {
+    DMLC_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s_[sid]));
+  }
+  void copy(void* dst, const void* src, size_t bytes, int sid) override {
+    DMLC_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, s_[sid]));
+  }
+  bool healthy() override {
+    for (auto s : s_) {
+      hipError_t e = hipStreamQuery(s);
+      if (e != hipSuccess && e != hipErrorNotReady) return false;
+    }
+    return true;
+  }
+
+ private:
+  Engine* e_;
+  int dev_, H_, W_;
+  bool graph_;
+  hipStream_t s_[3] = {nullptr, nullptr, nullptr};
+  std::vector<hipEvent_t> evs_;
+};
+
+}  // namespace
+
+std::unique_ptr<Worker> make_hip_worker(Engine* engine, int H, int W, bool use_graph) {
+  return std::make_unique<HipWorker>(engine, H, W, use_graph);
+}
+
+}  // namespace dp
+}  // namespace dmlc

@@ -1,0 +1,100 @@
+"""Native data-parallel layer (csrc/comm/dp.cpp) on the in-process host fake
+communicator: the same Rank / pipeline / Group code that drives RCCL on the
+GPUs, with a deterministic CPU classifier (class = byte sum % 1000).
+
+Checks shard order (every answer lands at its image's position), exactly-once
+commits, ragged last steps, the one-thread-per-rank (multi-process) issue
+order, local mode, and recovery from the loss of a non-coordinator rank —
+both a drained drop and an abrupt death that surfaces as a communicator
+error (reference behaviour being replaced: queries re-sent to a surviving
+member after a failure, src/services.rs:199-211, 407-433)."""
+import numpy as np
+import pytest
+
+import dmlc
+
+C = dmlc.native()
+H = W = 8
+
+
+def _images(n, seed=0):
+    rng = np.random.default_rng(seed)
+    return rng.integers(0, 256, size=(n, H, W, 3), dtype=np.uint8)
+
+
+def _expected(imgs):
+    flat = imgs.reshape(imgs.shape[0], -1).astype(np.int64)
+    return (flat.sum(1) % 1000).astype(np.int32), ((imgs[:, 0, 0, 0].astype(np.float32) + 1) / 257)
+
+
+def _check(out, imgs):
+    ei, ep = _expected(imgs)
+    np.testing.assert_array_equal(out["idx"], ei)
+    np.testing.assert_allclose(out["prob"], ep, rtol=0, atol=0)
+    np.testing.assert_array_equal(out["commits"], np.ones(len(imgs), np.int32))
+
+
+def test_shard_counts():
+    assert C.dp_shard_counts(10, 4, 3) == [3, 3, 2, 2]
+    assert C.dp_shard_counts(8, 8, 1) == [1] * 8
+    assert C.dp_shard_counts(0, 3, 5) == [0, 0, 0]
+    with pytest.raises(ValueError):
+        C.dp_shard_counts(13, 4, 3)
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 5, 8])
+@pytest.mark.parametrize("n", [1, 7, 64, 101])
+def test_group_exactly_once_in_order(world, n):
+    imgs = _images(n, seed=world * 1000 + n)
+    out = C.dp_host_run(imgs, world, 4, mode="group")
+    _check(out, imgs)
+    assert out["stats"]["recoveries"] == 0
+    assert out["stats"]["steps"] == -(-n // (4 * world))
+
+
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
+@pytest.mark.parametrize("scatter", [True, False])
+@pytest.mark.parametrize("pipelined", [True, False])
+def test_threads_one_rank_per_thread(world, scatter, pipelined):
+    """One thread per rank = the multi-process issue order (each rank's
+    pipeline runs independently; groups pair up across threads)."""
+    n = 4 * world * 5 + 3  # ragged last step
+    imgs = _images(n, seed=world)
+    out = C.dp_host_run(imgs, world, 4, mode="threads", scatter=scatter, pipelined=pipelined)
+    _check(out, imgs)
+    assert all(s == out["steps"][0] for s in out["steps"])
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+@pytest.mark.parametrize("abrupt", [False, True])
+@pytest.mark.parametrize("after", [0, 1, 3])
+def test_group_survives_rank_loss(world, abrupt, after):
+    n = 4 * world * 6 + 1
+    imgs = _images(n, seed=7 + world)
+    lost = world - 1 if world > 2 else 1
+    out = C.dp_host_run(imgs, world, 4, mode="group", fail_member=lost, fail_after=after, abrupt=abrupt)
+    _check(out, imgs)
+    st = out["stats"]
+    assert st["recoveries"] == 1
+    assert lost not in out["members"]
+    assert len(out["members"]) == world - 1
+    # the communicators were rebuilt over the survivors, coordinator first
+    # (a lone survivor needs none)
+    if len(out["members"]) > 1:
+        assert out["builds"][-1] == out["members"]
+        assert out["builds"][-1][0] == 0
+    if abrupt:
+        assert st["redone_images"] > 0  # the step that hit the dead rank is redone
+
+
+def test_group_loss_down_to_coordinator_alone():
+    imgs = _images(50, seed=3)
+    out = C.dp_host_run(imgs, 2, 4, mode="group", fail_member=1, fail_after=2, abrupt=True)
+    _check(out, imgs)
+    assert out["members"] == [0]
+
+
+def test_group_rejects_coordinator_failure():
+    imgs = _images(10)
+    with pytest.raises(ValueError):
+        C.dp_host_run(imgs, 3, 4, mode="group", fail_member=0)

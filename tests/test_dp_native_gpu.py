@@ -1,0 +1,61 @@
+"""Native data-parallel layer on a real GPU: the HIP worker (engine on a
+compute stream, answers over the comm streams, pinned D2H) must give the same
+answers as a direct engine forward, for full and ragged steps, pipelined and
+unpipelined. (RCCL send/recv between ranks needs >= 2 GPUs: the driver's
+multi-GPU bench runs that; the protocol itself is covered on CPU by
+tests/test_dp_native_cpu.py.)"""
+import pytest
+import torch
+
+import dmlc
+from dmlc.runtime import InferenceEngine
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    return InferenceEngine("resnet18", device=0, max_batch=64, seed=3)
+
+
+def _pool(n, seed):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    return torch.randint(0, 256, (n, 224, 224, 3), dtype=torch.uint8, device="cuda", generator=g)
+
+
+@pytest.mark.parametrize("pipelined", [True, False])
+def test_runner_world1_matches_engine(gpu, eng, pipelined):
+    C = dmlc.native()
+    pool = _pool(128, 1)
+    torch.cuda.synchronize()
+    r = C.DpRunner(eng._e, 1, 0, b"", b"", 64)
+    out = r.run(pool.data_ptr(), 128, 0, 3, pipelined=pipelined)
+    r.sync()
+    assert out["steps"] == 3 and out["images"] == 3 * 64
+    if not pipelined:
+        assert len(out["step_ms"]) == 3 and all(t > 0 for t in out["step_ms"])
+    idx, prob = r.last_results()
+    # step 2 reads pool batch 2 % 2 = 0
+    ref_i, ref_p = eng.predict(pool[:64].contiguous(), use_graph=False)
+    torch.cuda.synchronize()
+    assert idx == ref_i.cpu().tolist()
+    assert torch.allclose(torch.tensor(prob), ref_p.cpu(), atol=1e-6)
+
+
+def test_group_one_gpu_ragged(gpu, eng):
+    C = dmlc.native()
+    n = 64 * 3 + 17
+    pool = _pool(n, 2)
+    torch.cuda.synchronize()
+    g = C.DpGroup([eng._e], 64)
+    idx, prob, st = g.classify(pool.data_ptr(), n)
+    assert st["images"] == n and st["steps"] == 4 and st["recoveries"] == 0
+    ref_i, ref_p = [], []
+    for s in range(0, n, 64):
+        i, p = eng.predict(pool[s:s + 64].contiguous(), use_graph=False)
+        ref_i.append(i.cpu())
+        ref_p.append(p.cpu())
+    torch.cuda.synchronize()
+    assert idx.tolist() == torch.cat(ref_i).tolist()
+    assert torch.allclose(torch.from_numpy(prob), torch.cat(ref_p), atol=1e-6)
+    assert g.members == [0]

@@ -81,6 +81,7 @@ HIPCC_FILE_FLAGS = {"stem_pool.hip": ["-fno-honor-nans"]}
 def gpu_objects():
     srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
     srcs += [os.path.join(CSRC, "runtime", "engine.cpp")]
+    srcs += sorted(glob.glob(os.path.join(CSRC, "comm", "*.cpp")))
     return srcs
 
 
@@ -111,6 +112,7 @@ def build(jobs: int = 8, verbose: bool = False, node: bool = True) -> None:
     # ---- 2. host objects for the python module
     py_srcs = {
         os.path.join(CSRC, "bindings", "py_module.cpp"): [f"-I{_pybind_include()}", f"-I{pyinc}"],
+        os.path.join(CSRC, "bindings", "py_dp.cpp"): [f"-I{_pybind_include()}", f"-I{pyinc}"],
         os.path.join(CSRC, "runtime", "ot_io.cpp"): torch_flags,
         os.path.join(CSRC, "runtime", "jpeg.cpp"): ["-O3"],
     }
@@ -155,7 +157,7 @@ def build(jobs: int = 8, verbose: bool = False, node: bool = True) -> None:
     libgpu = os.path.join(PKG, "libdmlc_gpu.so")
     if _stale(libgpu, gpu_objs, 0):
         _run(["hipcc", "-shared", "-fPIC", f"--offload-arch={ARCH}", *gpu_objs, "-o", libgpu,
-              f"-L{ROCM}/lib", "-lrocprofiler-sdk-roctx", f"-Wl,-rpath,{ROCM}/lib"], verbose)
+              f"-L{ROCM}/lib", "-lrocprofiler-sdk-roctx", "-lrccl", f"-Wl,-rpath,{ROCM}/lib"], verbose)
 
     pymod = os.path.join(PKG, "_C" + ext)
     if _stale(pymod, py_objs + [libgpu], 0):
