@@ -344,8 +344,17 @@ int run_node(const Args& a) {
 
   std::unique_ptr<Executor> ex;
   try {
-    ex = make_executor(a.get("executor", "auto"), a.geti("device", 0), a.geti("max-batch", 64),
-                       (size_t)a.geti("hbm-cache-mb", 4096) << 20);
+    // --gpus N: this node serves on GPUs device .. device+N-1 (one engine
+    // per GPU, query batches scattered over RCCL); --devices a,b,c lists them
+    std::vector<int> devs;
+    if (!a.get("devices", "").empty()) {
+      for (const auto& d : split(a.get("devices", ""), ','))
+        if (!trim(d).empty()) devs.push_back(std::stoi(trim(d)));
+    } else {
+      for (int i = 0; i < std::max(1, a.geti("gpus", 1)); ++i) devs.push_back(a.geti("device", 0) + i);
+    }
+    ex = make_executor(a.get("executor", "auto"), devs, a.geti("max-batch", 64),
+                       (size_t)a.geti("hbm-cache-mb", 4096) << 20, a.geti("min-shard", 8));
     if (ex) load_models(ex.get(), a.get("models", ""));
   } catch (const std::exception& e) {
     err_line(std::string("executor unavailable: ") + e.what());
@@ -410,12 +419,13 @@ int run_node(const Args& a) {
 
 int run_classify(const Args& a) {
   const std::string model = a.get("model", "alexnet");
-  auto ex = make_executor(a.get("executor", "cpu"), a.geti("device", 0), 1);
+  std::vector<Image> imgs;
+  for (const auto& p : split(a.get("image"), ',')) imgs.push_back(decode_jpeg_file(p));
+  // all images in one batch (one forward on the GPU executor)
+  auto ex = make_executor(a.get("executor", "cpu"), a.geti("device", 0), std::max<int>(1, (int)imgs.size()));
   if (!ex) throw std::runtime_error("no inference executor in this build");
   ex->load_model(model, a.get("weights"));
   const Labels labels = Labels::load(a.get("labels", "synset_words.txt"));
-  std::vector<Image> imgs;
-  for (const auto& p : split(a.get("image"), ',')) imgs.push_back(decode_jpeg_file(p));
   const int64_t t0 = steady_us();
   const auto preds = ex->predict(model, imgs);
   const int64_t dt = steady_us() - t0;
@@ -437,6 +447,7 @@ int main(int argc, char** argv) {
   if (argc >= 2 && (std::string(argv[1]) == "--help" || std::string(argv[1]) == "-h")) {
     std::cout << "usage: dmlc-node [--host H] [--port P] [--leaders h:p,...] [--workdir D] [--dataset D]\n"
                  "                 [--labels F] [--models name=path,...] [--executor auto|gpu|cpu] [--device N]\n"
+                 "                 [--gpus N | --devices a,b,...] [--min-shard 8]\n"
                  "                 [--rf 4] [--ping-ms 1000] [--fail-ms 3000] [--bg-ms 3000]\n"
                  "                 [--query-interval-ms 500] [--adaptive-window 0] [--query-batch 1] [--jobs resnet18,alexnet]\n"
                  "                 [--join h:p] [--daemon] [--stay] [--quiet-predictions]\n"

@@ -422,7 +422,11 @@ Group::Stats Group::classify(const uint8_t* src, int64_t n, int32_t* idx, float*
       StepPlan p;
       p.step = step;
       const int64_t start = base + step * G;
-      p.counts = shard_counts(std::min<int64_t>(G, n - start), world, max_);
+      const int64_t nstep = std::min<int64_t>(G, n - start);
+      const int64_t want = std::max<int64_t>((nstep + min_per_rank_ - 1) / min_per_rank_, (nstep + max_ - 1) / max_);
+      const int used = (int)std::min<int64_t>(world, std::max<int64_t>(1, want));
+      p.counts = shard_counts(nstep, used, max_);
+      p.counts.resize(world, 0);
       p.src = src + (size_t)start * ib_;
       p.src_event = r.root() ? src_event : -1;
       return p;

@@ -19,6 +19,7 @@
 //             non-coordinator GPU (abort, rebuild over the survivors, redo
 //             every image whose answer was not yet committed).
 #pragma once
+#include <algorithm>
 #include <cstdint>
 #include <functional>
 #include <memory>
@@ -184,6 +185,10 @@ class Group {
   void fail(int m, int64_t after_steps = 0, bool abrupt = false);
   std::vector<int> members() const { return members_; }
   int size() const { return (int)members_.size(); }
+  // A step of n images uses ceil(n / min_per_rank) ranks at most (small
+  // query batches stay on few GPUs; default 1 = always all ranks).
+  void set_min_per_rank(int m) { min_per_rank_ = std::max(1, m); }
+  Worker* coordinator() const { return workers_.front(); }
 
  private:
   void rebuild();
@@ -198,6 +203,7 @@ class Group {
   std::vector<bool> lost_;
   std::vector<int64_t> fail_at_;  // per worker: steps still to issue before it is lost (-1: never)
   std::vector<bool> fail_abrupt_;
+  int min_per_rank_ = 1;
   void kill_now(int m);
 };
 

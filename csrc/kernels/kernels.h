@@ -110,6 +110,15 @@ void avgpool_adaptive(const void* x, void* y, int B, int H, int W, int C, int Ho
 void preprocess_u8(const uint8_t* x, void* y, int B, int Hin, int Win, int S, int pad, int Wr,
                    hipStream_t s, bool paired = false);
 
+// Ragged batch: image b = descs[b] (device memory, u8 HWC at its own size)
+// -> out u8 [B, S, S, 3], same resize rule as preprocess_u8, rounded to u8
+// (S % 4 == 0).
+struct ImageDesc {
+  const uint8_t* ptr;
+  int h, w;
+};
+void resize_u8_ragged(const ImageDesc* descs, uint8_t* out, int B, int S, hipStream_t s);
+
 // Fused ResNet stem: conv 7x7/s2/p3 (folded BN) + ReLU + maxpool 3x3/s2/p1.
 //   x : paired image [B, S+6, Wq, 8] bf16 (preprocess_u8 pad=3, paired)
 //   w : bf16 [64, 224], k = kh*32 + q*8 + e: chunk q covers kw = 2q, 2q+1,

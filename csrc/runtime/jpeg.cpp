@@ -8,6 +8,7 @@
 #include <cmath>
 #include <cstring>
 #include <fstream>
+#include <immintrin.h>
 #include <iterator>
 #include <stdexcept>
 
@@ -26,6 +27,10 @@ struct Huff {
   int mincode[17], maxcode[18], valptr[17];
   uint8_t lut_len[256];  // 8-bit lookahead: code length (0 = longer than 8)
   uint8_t lut_sym[256];
+  // AC fast path, kFastBits lookahead: a code AND its value bits resolved in
+  // one lookup. Entry = value << 16 | run << 5 | bits consumed; 0 = slow path.
+  static constexpr int kFastBits = 10;
+  int32_t fast[1 << kFastBits];
   bool present = false;
   void build() {
     int code = 0, k = 0;
@@ -51,6 +56,22 @@ struct Huff {
       }
       code <<= 1;
     }
+    std::memset(fast, 0, sizeof(fast));
+    code = 0;
+    k = 0;
+    for (int l = 1; l <= 16; ++l) {
+      for (int i = 0; i < count[l]; ++i, ++k, ++code) {
+        const int rs = sym[k], r = rs >> 4, sz = rs & 15;
+        if (l > kFastBits || sz == 0 || l + sz > kFastBits) continue;
+        for (int v = 0; v < (1 << sz); ++v) {
+          const int val = v < (1 << (sz - 1)) ? v - (1 << sz) + 1 : v;
+          const int base = ((code << sz) | v) << (kFastBits - l - sz);
+          for (int j = 0; j < (1 << (kFastBits - l - sz)); ++j)
+            fast[base | j] = (int32_t)((uint32_t)val << 16) | (r << 5) | (l + sz);
+        }
+      }
+      code <<= 1;
+    }
     present = true;
   }
 };
@@ -63,6 +84,9 @@ struct Comp {
   int pred = 0;
 };
 
+// Entropy-coded segment reader: a 64-bit accumulator refilled a byte at a
+// time up to 56 bits (byte stuffing 0xFF00 -> 0xFF removed; at a marker it
+// feeds zeros and leaves the marker in place).
 class BitReader {
  public:
   BitReader(const uint8_t* p, const uint8_t* end) : p_(p), end_(end) {}
@@ -71,10 +95,9 @@ class BitReader {
     nbits_ = 0;
     marker_ = false;
   }
-  // Make sure >= n bits (n <= 24) are buffered; past a marker feed zeros.
-  void fill(int n) {
-    while (nbits_ < n) {
-      uint32_t byte = 0;
+  inline void refill() {
+    while (nbits_ <= 56) {
+      uint64_t byte = 0;
       if (!marker_ && p_ < end_) {
         byte = *p_;
         if (byte == 0xFF) {
@@ -89,21 +112,22 @@ class BitReader {
           ++p_;
         }
       }
-      acc_ |= byte << (24 - nbits_);
+      acc_ |= byte << (56 - nbits_);
       nbits_ += 8;
     }
   }
-  uint32_t peek(int n) {
-    fill(n);
-    return acc_ >> (32 - n);
+  // n <= 16 bits
+  inline uint32_t peek(int n) {
+    if (nbits_ < n) refill();
+    return (uint32_t)(acc_ >> (64 - n));
   }
-  void skip(int n) {
+  inline void skip(int n) {
     acc_ <<= n;
     nbits_ -= n;
   }
-  int bits(int n) {
+  inline int bits(int n) {
     if (n == 0) return 0;
-    uint32_t v = peek(n);
+    const uint32_t v = peek(n);
     skip(n);
     return (int)v;
   }
@@ -116,58 +140,275 @@ class BitReader {
  private:
   const uint8_t* p_;
   const uint8_t* end_;
-  uint32_t acc_ = 0;
+  uint64_t acc_ = 0;
   int nbits_ = 0;
   bool marker_ = false;
 };
 
-int decode_huff(const Huff& h, BitReader& br) {
-  const uint32_t look = br.peek(8);
-  if (h.lut_len[look]) {
-    br.skip(h.lut_len[look]);
-    return h.lut_sym[look];
+inline int decode_huff(const Huff& h, BitReader& br) {
+  const uint32_t look = br.peek(16);
+  const uint32_t l8 = look >> 8;
+  if (h.lut_len[l8]) {
+    br.skip(h.lut_len[l8]);
+    return h.lut_sym[l8];
   }
-  int code = 0;
-  for (int l = 1; l <= 16; ++l) {
-    code = (code << 1) | br.bits(1);
-    if (h.maxcode[l] >= 0 && code <= h.maxcode[l] && code >= h.mincode[l])
+  // canonical code longer than 8 bits: its top l bits are <= maxcode[l]
+  for (int l = 9; l <= 16; ++l) {
+    const int code = (int)(look >> (16 - l));
+    if (h.maxcode[l] >= 0 && code <= h.maxcode[l]) {
+      br.skip(l);
       return h.sym[h.valptr[l] + code - h.mincode[l]];
+    }
   }
   throw std::runtime_error("jpeg: bad huffman code");
 }
 
 inline int extend(int v, int t) { return v < (1 << (t - 1)) ? v - (1 << t) + 1 : v; }
 
-struct IdctTable {
-  float c[8][8];
-  IdctTable() {
-    for (int x = 0; x < 8; ++x)
-      for (int u = 0; u < 8; ++u) {
-        const double cu = u == 0 ? std::sqrt(0.5) : 1.0;
-        c[x][u] = (float)(0.5 * cu * std::cos((2 * x + 1) * u * M_PI / 16.0));
-      }
+// AAN (Arai-Agui-Nakajima) scaled 8-point IDCT: 5 multiplies per 1-D
+// transform; the per-coefficient AAN scale factors and the 1/8 of the 2-D
+// transform are folded into the dequantisation table (aan_scale), so a
+// block costs ~80 multiplies instead of the 1,024 of a direct separable
+// transform. Columns first; a column whose AC terms are all zero (the common
+// case after quantisation) is a constant.
+struct AanScale {
+  float f[64];
+  AanScale() {
+    double a[8];
+    a[0] = 1.0;
+    for (int k = 1; k < 8; ++k) a[k] = std::cos(k * M_PI / 16.0) * std::sqrt(2.0);
+    for (int v = 0; v < 8; ++v)
+      for (int u = 0; u < 8; ++u) f[v * 8 + u] = (float)(a[u] * a[v] / 8.0);
   }
 };
+const AanScale kAan;
 
-void idct8x8(const float* in, uint8_t* out, int stride) {
-  static const IdctTable T;
-  float tmp[64];
-  for (int y = 0; y < 8; ++y)  // rows: over u
-    for (int x = 0; x < 8; ++x) {
-      float s = 0;
-      for (int u = 0; u < 8; ++u) s += T.c[x][u] * in[y * 8 + u];
-      tmp[y * 8 + x] = s;
-    }
+// Eight 1-D transforms at once: lane j of every vector is column j (pass 1)
+// or pixel row j (pass 2).
+typedef float v8f __attribute__((vector_size(32)));
+
+#define DMLC_IDCT8_LANES(in, o)                                                    \
+  do {                                                                             \
+    const v8f t10 = in[0] + in[4], t11 = in[0] - in[4];                            \
+    const v8f t13 = in[2] + in[6], t12 = (in[2] - in[6]) * 1.414213562f - t13;     \
+    const v8f e0 = t10 + t13, e3 = t10 - t13, e1 = t11 + t12, e2 = t11 - t12;      \
+    const v8f z13 = in[5] + in[3], z10 = in[5] - in[3];                            \
+    const v8f z11 = in[1] + in[7], z12 = in[1] - in[7];                            \
+    const v8f o7 = z11 + z13;                                                      \
+    const v8f t11b = (z11 - z13) * 1.414213562f;                                   \
+    const v8f z5 = (z10 + z12) * 1.847759065f;                                     \
+    const v8f t10b = z12 * 1.082392200f - z5;                                      \
+    const v8f t12b = z10 * -2.613125930f + z5;                                     \
+    const v8f o6 = t12b - o7;                                                      \
+    const v8f o5 = t11b - o6;                                                      \
+    const v8f o4 = t10b + o5;                                                      \
+    o[0] = e0 + o7;                                                                \
+    o[7] = e0 - o7;                                                                \
+    o[1] = e1 + o6;                                                                \
+    o[6] = e1 - o6;                                                                \
+    o[2] = e2 + o5;                                                                \
+    o[5] = e2 - o5;                                                                \
+    o[4] = e3 + o4;                                                                \
+    o[3] = e3 - o4;                                                                \
+  } while (0)
+
+// AVX2: 8x8 transposes in registers (unpack / shuffle / 128-bit permute),
+// saturating pack to bytes.
+__attribute__((target("avx2,fma"))) void transpose8_avx(__m256* r) {
+  const __m256 t0 = _mm256_unpacklo_ps(r[0], r[1]), t1 = _mm256_unpackhi_ps(r[0], r[1]);
+  const __m256 t2 = _mm256_unpacklo_ps(r[2], r[3]), t3 = _mm256_unpackhi_ps(r[2], r[3]);
+  const __m256 t4 = _mm256_unpacklo_ps(r[4], r[5]), t5 = _mm256_unpackhi_ps(r[4], r[5]);
+  const __m256 t6 = _mm256_unpacklo_ps(r[6], r[7]), t7 = _mm256_unpackhi_ps(r[6], r[7]);
+  const __m256 s0 = _mm256_shuffle_ps(t0, t2, _MM_SHUFFLE(1, 0, 1, 0));
+  const __m256 s1 = _mm256_shuffle_ps(t0, t2, _MM_SHUFFLE(3, 2, 3, 2));
+  const __m256 s2 = _mm256_shuffle_ps(t1, t3, _MM_SHUFFLE(1, 0, 1, 0));
+  const __m256 s3 = _mm256_shuffle_ps(t1, t3, _MM_SHUFFLE(3, 2, 3, 2));
+  const __m256 s4 = _mm256_shuffle_ps(t4, t6, _MM_SHUFFLE(1, 0, 1, 0));
+  const __m256 s5 = _mm256_shuffle_ps(t4, t6, _MM_SHUFFLE(3, 2, 3, 2));
+  const __m256 s6 = _mm256_shuffle_ps(t5, t7, _MM_SHUFFLE(1, 0, 1, 0));
+  const __m256 s7 = _mm256_shuffle_ps(t5, t7, _MM_SHUFFLE(3, 2, 3, 2));
+  r[0] = _mm256_permute2f128_ps(s0, s4, 0x20);
+  r[1] = _mm256_permute2f128_ps(s1, s5, 0x20);
+  r[2] = _mm256_permute2f128_ps(s2, s6, 0x20);
+  r[3] = _mm256_permute2f128_ps(s3, s7, 0x20);
+  r[4] = _mm256_permute2f128_ps(s0, s4, 0x31);
+  r[5] = _mm256_permute2f128_ps(s1, s5, 0x31);
+  r[6] = _mm256_permute2f128_ps(s2, s6, 0x31);
+  r[7] = _mm256_permute2f128_ps(s3, s7, 0x31);
+}
+
+__attribute__((target("avx2,fma"))) void idct8x8_avx2(const float* in, uint8_t* out, int stride) {
+  __m256 a[8], b[8];
+  for (int i = 0; i < 8; ++i) a[i] = _mm256_loadu_ps(in + 8 * i);  // a[v]: lane = u
+  {
+    const v8f* x = (const v8f*)a;
+    v8f* y = (v8f*)b;
+    DMLC_IDCT8_LANES(x, y);  // b[y]: lane = u
+  }
+  transpose8_avx(b);  // b[u]: lane = y
+  {
+    const v8f* x = (const v8f*)b;
+    v8f* y = (v8f*)a;
+    DMLC_IDCT8_LANES(x, y);  // a[x]: lane = y
+  }
+  transpose8_avx(a);  // a[y]: lane = x
+  const __m256 lo = _mm256_setzero_ps(), hi = _mm256_set1_ps(255.f), half = _mm256_set1_ps(128.5f);
+  for (int y = 0; y < 8; ++y) {
+    const __m256 f = _mm256_min_ps(_mm256_max_ps(_mm256_add_ps(a[y], half), lo), hi);
+    const __m256i i32 = _mm256_cvttps_epi32(f);
+    const __m256i i16 = _mm256_packs_epi32(i32, i32);
+    const __m256i u8 = _mm256_packus_epi16(i16, i16);
+    uint32_t w0 = (uint32_t)_mm256_extract_epi32(u8, 0), w1 = (uint32_t)_mm256_extract_epi32(u8, 4);
+    std::memcpy(out + (size_t)y * stride, &w0, 4);
+    std::memcpy(out + (size_t)y * stride + 4, &w1, 4);
+  }
+}
+
+void idct8x8_generic(const float* in, uint8_t* out, int stride) {
+  v8f a[8], b[8];
+  std::memcpy(a, in, sizeof(a));
+  DMLC_IDCT8_LANES(a, b);
+  for (int i = 0; i < 8; ++i)
+    for (int j = 0; j < 8; ++j) a[j][i] = b[i][j];
+  DMLC_IDCT8_LANES(a, b);
   for (int x = 0; x < 8; ++x)
     for (int y = 0; y < 8; ++y) {
-      float s = 0;
-      for (int v = 0; v < 8; ++v) s += T.c[y][v] * tmp[v * 8 + x];
-      const int val = (int)std::lround(s + 128.f);
-      out[y * stride + x] = (uint8_t)std::min(255, std::max(0, val));
+      const float f = b[x][y] + 128.5f;  // round half up; negatives clamp to 0
+      const int i = f <= 0.f ? 0 : (int)f;
+      out[(size_t)y * stride + x] = (uint8_t)(i > 255 ? 255 : i);
     }
 }
 
+bool detect_avx2() {
+  __builtin_cpu_init();  // required before __builtin_cpu_supports in a static initialiser
+  return __builtin_cpu_supports("avx2") && __builtin_cpu_supports("fma");
+}
+const bool kHasAvx2 = detect_avx2();
+
+// in: dequantised, AAN-prescaled coefficients in natural (row-major) order
+inline void idct8x8(const float* in, uint8_t* out, int stride) {
+  if (kHasAvx2) idct8x8_avx2(in, out, stride);
+  else idct8x8_generic(in, out, stride);
+}
+
 uint16_t be16(const uint8_t* p) { return (uint16_t)((p[0] << 8) | p[1]); }
+
+// YCbCr -> RGB in 16.16 fixed point (JFIF full-range coefficients).
+struct ColorTables {
+  int cr_r[256], cb_b[256], cr_g[256], cb_g[256];
+  ColorTables() {
+    for (int i = 0; i < 256; ++i) {
+      const double x = i - 128;
+      cr_r[i] = (int)std::lround(1.402 * x * 65536);
+      cb_b[i] = (int)std::lround(1.772 * x * 65536);
+      cr_g[i] = (int)std::lround(-0.714136 * x * 65536);
+      cb_g[i] = (int)std::lround(-0.344136 * x * 65536);
+    }
+  }
+};
+const ColorTables kColor;
+
+inline uint8_t clamp_fix(int v) {  // 16.16 -> u8, rounded
+  v = (v + 32768) >> 16;
+  return (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v);
+}
+
+// Centred (triangle) upsampling of one chroma row by 1 or 2 per axis into
+// `out` (W values): vertical blend of rows y0/y1 with weights (wa, wb)/4,
+// then horizontal 3:1 blend; result = chroma sample at each output pixel,
+// rounded. Same positions as the generic bilinear path ((x+0.5)/f - 0.5,
+// clamped to the plane's valid area).
+void chroma_row(const Comp& c, int hf, int vf, int y, int W, int H, int hmax, int vmax, uint8_t* out,
+                std::vector<int>& tmp) {
+  const int pw = c.bw * 8;
+  const int cw = (W * c.h + hmax - 1) / hmax, ch = (H * c.v + vmax - 1) / vmax;
+  int y0, y1, wa, wb;  // weights of rows y0, y1 (sum 4)
+  if (vf == 1) {
+    y0 = y1 = y;
+    wa = 4;
+    wb = 0;
+  } else {
+    const int i = y >> 1;
+    if (y & 1) {
+      y0 = i;
+      y1 = std::min(i + 1, ch - 1);
+    } else {
+      y0 = i;
+      y1 = std::max(i - 1, 0);
+    }
+    wa = 3;
+    wb = 1;
+  }
+  const uint8_t* r0 = c.plane.data() + (size_t)y0 * pw;
+  const uint8_t* r1 = c.plane.data() + (size_t)y1 * pw;
+  tmp.resize((size_t)cw);
+  for (int x = 0; x < cw; ++x) tmp[x] = wa * r0[x] + wb * r1[x];  // x4
+  if (hf == 1) {
+    for (int x = 0; x < W; ++x) out[x] = (uint8_t)((tmp[x] + 2) >> 2);
+    return;
+  }
+  for (int x = 0; x < W; ++x) {
+    const int i = x >> 1;
+    const int j = (x & 1) ? std::min(i + 1, cw - 1) : std::max(i - 1, 0);
+    out[x] = (uint8_t)((3 * tmp[i] + tmp[j] + 8) >> 4);  // x16
+  }
+}
+
+// Fast colour conversion for 1 or 3 components with chroma subsampled by 1
+// or 2 per axis (4:4:4, 4:2:2, 4:2:0, 4:4:0 — essentially every JPEG);
+// false for other layouts (the generic float path handles them).
+bool convert_fast(const std::vector<Comp>& comps, int hmax, int vmax, int W, int H, uint8_t* rgb) {
+  const Comp& Yc = comps[0];
+  if (Yc.h != hmax || Yc.v != vmax) return false;
+  const int pw = Yc.bw * 8;
+  if (comps.size() == 1) {
+    for (int y = 0; y < H; ++y) {
+      const uint8_t* yr = Yc.plane.data() + (size_t)y * pw;
+      uint8_t* o = rgb + (size_t)y * W * 3;
+      for (int x = 0; x < W; ++x) o[3 * x] = o[3 * x + 1] = o[3 * x + 2] = yr[x];
+    }
+    return true;
+  }
+  int hf[2], vf[2];
+  for (int k = 0; k < 2; ++k) {
+    const Comp& c = comps[k + 1];
+    if (hmax % c.h || vmax % c.v) return false;
+    hf[k] = hmax / c.h;
+    vf[k] = vmax / c.v;
+    if (hf[k] > 2 || vf[k] > 2) return false;
+  }
+  if (hf[0] == 1 && vf[0] == 1 && hf[1] == 1 && vf[1] == 1) {  // 4:4:4: planes read in place
+    const int cpw = comps[1].bw * 8, rpw = comps[2].bw * 8;
+    for (int y = 0; y < H; ++y) {
+      const uint8_t* yr = Yc.plane.data() + (size_t)y * pw;
+      const uint8_t* br = comps[1].plane.data() + (size_t)y * cpw;
+      const uint8_t* rr = comps[2].plane.data() + (size_t)y * rpw;
+      uint8_t* o = rgb + (size_t)y * W * 3;
+      for (int x = 0; x < W; ++x) {
+        const int Y = yr[x] << 16, b = br[x], r = rr[x];
+        o[3 * x] = clamp_fix(Y + kColor.cr_r[r]);
+        o[3 * x + 1] = clamp_fix(Y + kColor.cb_g[b] + kColor.cr_g[r]);
+        o[3 * x + 2] = clamp_fix(Y + kColor.cb_b[b]);
+      }
+    }
+    return true;
+  }
+  std::vector<uint8_t> cb((size_t)W), cr((size_t)W);
+  std::vector<int> tmp;
+  for (int y = 0; y < H; ++y) {
+    chroma_row(comps[1], hf[0], vf[0], y, W, H, hmax, vmax, cb.data(), tmp);
+    chroma_row(comps[2], hf[1], vf[1], y, W, H, hmax, vmax, cr.data(), tmp);
+    const uint8_t* yr = Yc.plane.data() + (size_t)y * pw;
+    uint8_t* o = rgb + (size_t)y * W * 3;
+    for (int x = 0; x < W; ++x) {
+      const int Y = yr[x] << 16, b = cb[x], r = cr[x];
+      o[3 * x] = clamp_fix(Y + kColor.cr_r[r]);
+      o[3 * x + 1] = clamp_fix(Y + kColor.cb_g[b] + kColor.cr_g[r]);
+      o[3 * x + 2] = clamp_fix(Y + kColor.cb_b[b]);
+    }
+  }
+  return true;
+}
 
 }  // namespace
 
@@ -286,15 +527,30 @@ Image decode_jpeg(const uint8_t* data, size_t size) {
         }
         BitReader br(seg_end, end);
         float blk[64];
+        // dequantisation folded with the AAN scale factors, natural order
+        float qf[4][64];
+        for (int t = 0; t < 4; ++t)
+          for (int k = 0; k < 64; ++k) qf[t][kZigzag[k]] = qt[t][k] * kAan.f[kZigzag[k]];
         int mcus_left = restart;
         auto decode_block = [&](Comp& c, uint8_t* dst, int stride) {
           std::memset(blk, 0, sizeof(blk));
-          const uint16_t* q = qt[c.tq];
+          const float* q = qf[c.tq];
           const int t = decode_huff(dc[c.td], br);
           c.pred += t ? extend(br.bits(t), t) : 0;
-          blk[0] = (float)(c.pred * q[0]);
+          blk[0] = (float)c.pred * q[0];
+          const Huff& ha = ac[c.ta];
           for (int k = 1; k < 64;) {
-            const int rs = decode_huff(ac[c.ta], br);
+            const int32_t fe = ha.fast[br.peek(Huff::kFastBits)];
+            if (fe) {
+              br.skip(fe & 31);
+              k += (fe >> 5) & 15;
+              if (k > 63) break;
+              const int z = kZigzag[k];
+              blk[z] = (float)(fe >> 16) * q[z];
+              ++k;
+              continue;
+            }
+            const int rs = decode_huff(ha, br);
             const int r = rs >> 4, s = rs & 15;
             if (s == 0) {
               if (r != 15) break;
@@ -303,7 +559,8 @@ Image decode_jpeg(const uint8_t* data, size_t size) {
             }
             k += r;
             if (k > 63) break;
-            blk[kZigzag[k]] = (float)(extend(br.bits(s), s) * q[k]);
+            const int z = kZigzag[k];
+            blk[z] = (float)extend(br.bits(s), s) * q[z];
             ++k;
           }
           idct8x8(blk, dst, stride);
@@ -363,6 +620,7 @@ Image decode_jpeg(const uint8_t* data, size_t size) {
   img.width = W;
   img.height = H;
   img.rgb.resize((size_t)W * H * 3);
+  if (convert_fast(comps, hmax, vmax, W, H, img.rgb.data())) return img;
   auto sample = [&](const Comp& c, int x, int y) -> float {
     const int pw = c.bw * 8;
     if (c.h == hmax && c.v == vmax) return c.plane[(size_t)y * pw + x];

@@ -15,6 +15,10 @@
 #include "../runtime/engine.h"
 #include "../runtime/ot_io.h"
 #include "../runtime/trace.h"
+#include "../comm/dp.h"
+#include "../kernels/kernels.h"
+#include <condition_variable>
+#include <cstring>
 
 namespace dmlc {
 
@@ -49,7 +53,9 @@ std::vector<float> preprocess_host(const Image& img, int S) {
           const float a = img.rgb[((size_t)y0 * Win + x0) * 3 + k], b = img.rgb[((size_t)y0 * Win + x1) * 3 + k];
           const float d = img.rgb[((size_t)y1 * Win + x0) * 3 + k], e = img.rgb[((size_t)y1 * Win + x1) * 3 + k];
           const float top = a + (b - a) * fx, bot = d + (e - d) * fx;
-          c[k] = top + (bot - top) * fy;
+          // resized to u8 before normalising, like the GPU path (resize.hip)
+          // and the reference's image-crate resize
+          c[k] = std::min(std::max(std::nearbyint(top + (bot - top) * fy), 0.f), 255.f);
         }
       }
       for (int k = 0; k < 3; ++k) out[(size_t)k * S * S + (size_t)y * S + x] = (c[k] / 255.f - mean[k]) / stdv[k];
@@ -176,66 +182,90 @@ class CpuExecutor : public Executor {
 };
 
 // ------------------------------------------------------------------ GPU
+// One or more GPUs of this node. Per model: an engine on every GPU and a
+// dp::Group over them (GPU 0 coordinates; with more than one GPU the query
+// batch is scattered over RCCL, csrc/comm/dp.h). Decoded images stay resident
+// in GPU 0's HBM at their own sizes (LRU cache); a query's images, whatever
+// their sizes, are resized into one u8 224x224 batch by one kernel
+// (resize.hip) and classified by one graph-replayed forward per GPU.
 class GpuExecutor : public Executor {
  public:
-  GpuExecutor(int device, int max_batch, size_t cache_bytes)
-      : device_(device), max_batch_(max_batch), cache_cap_(cache_bytes) {
-    DMLC_HIP_CHECK(hipSetDevice(device_));
-    DMLC_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
-    DMLC_HIP_CHECK(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
-    DMLC_HIP_CHECK(hipMalloc(&d_out_, (size_t)max_batch_ * 8));
+  GpuExecutor(std::vector<int> devices, int max_batch, size_t cache_bytes, int min_shard)
+      : devices_(std::move(devices)), max_batch_(max_batch), min_shard_(min_shard), cache_cap_(cache_bytes) {
+    if (devices_.empty()) throw std::invalid_argument("GpuExecutor: no devices");
+    DMLC_HIP_CHECK(hipSetDevice(devices_[0]));
+    for (int i = 0; i < kStagers; ++i) {
+      Stager st;
+      DMLC_HIP_CHECK(hipStreamCreateWithFlags(&st.stream, hipStreamNonBlocking));
+      free_stagers_.push_back(st);
+    }
   }
   ~GpuExecutor() override {
-    hipSetDevice(device_);
-    hipDeviceSynchronize();
-    engines_.clear();
-    for (auto& kv : cache_) hipFree(kv.second.dev);
-    if (d_in_) hipFree(d_in_);
-    if (d_out_) hipFree(d_out_);
-    if (side_) hipStreamDestroy(side_);
-    if (stream_) hipStreamDestroy(stream_);
+    (void)hipSetDevice(devices_[0]);
+    (void)hipDeviceSynchronize();
+    {
+      std::lock_guard<std::mutex> g(models_mu_);
+      models_.clear();
+    }
+    (void)hipSetDevice(devices_[0]);
+    for (auto& kv : cache_) (void)hipFree(kv.second.dev);
+    for (auto& st : free_stagers_) {
+      if (st.pinned) (void)hipHostFree(st.pinned);
+      (void)hipStreamDestroy(st.stream);
+    }
   }
-  std::string backend() const override { return "gpu:" + std::to_string(device_); }
+  std::string backend() const override {
+    std::string b = "gpu:" + std::to_string(devices_[0]);
+    for (size_t i = 1; i < devices_.size(); ++i) b += "," + std::to_string(devices_[i]);
+    return b;
+  }
 
   void load_model(const std::string& model, const std::string& path) override {
     load_model_weights(model, ot_load(path));
   }
   void load_model_weights(const std::string& model, const WeightMap& w) override {
-    std::lock_guard<std::mutex> g(mu_);
-    DMLC_HIP_CHECK(hipSetDevice(device_));
-    auto e = std::make_unique<Engine>(model, w, device_);
-    e->reserve(max_batch_);
-    engines_[model] = std::move(e);  // hot-swap: the old engine is freed here
+    // Build the new replicas outside the lock; in-flight queries keep the old
+    // slot alive (shared_ptr) until they finish: a hot swap.
+    auto slot = std::make_shared<ModelSlot>(model, w, devices_, max_batch_, min_shard_);
+    std::lock_guard<std::mutex> g(models_mu_);
+    models_[model] = std::move(slot);
   }
   bool has_model(const std::string& model) const override {
-    std::lock_guard<std::mutex> g(mu_);
-    return engines_.count(model) > 0;
+    std::lock_guard<std::mutex> g(models_mu_);
+    return models_.count(model) > 0;
   }
 
   std::vector<Prediction> predict(const std::string& model, const std::vector<Image>& imgs) override {
-    std::lock_guard<std::mutex> g(mu_);
-    Engine* e = engine(model);
-    std::vector<const void*> src(imgs.size());
-    std::vector<std::pair<int, int>> hw(imgs.size());
+    auto slot = get(model);
+    DMLC_HIP_CHECK(hipSetDevice(devices_[0]));
+    std::vector<ImageDesc> descs(imgs.size());
+    std::vector<void*> bufs;
     for (size_t i = 0; i < imgs.size(); ++i) {
-      src[i] = imgs[i].rgb.data();
-      hw[i] = {imgs[i].height, imgs[i].width};
+      void* d = nullptr;
+      DMLC_HIP_CHECK(hipMalloc(&d, imgs[i].rgb.size()));
+      DMLC_HIP_CHECK(hipMemcpy(d, imgs[i].rgb.data(), imgs[i].rgb.size(), hipMemcpyHostToDevice));
+      bufs.push_back(d);
+      descs[i] = ImageDesc{(const uint8_t*)d, imgs[i].height, imgs[i].width};
     }
-    return run(e, src, hw, hipMemcpyHostToDevice);
+    std::vector<Prediction> out;
+    try {
+      out = slot->run(descs);
+    } catch (...) {
+      for (void* b : bufs) (void)hipFree(b);
+      throw;
+    }
+    for (void* b : bufs) (void)hipFree(b);
+    return out;
   }
 
   // HBM-resident decoded images: a hit skips the JPEG decode and the H2D
-  // copy; the batch is gathered device-to-device.
+  // copy. The query's entries are pinned (not evictable) until its forward
+  // has consumed them.
   std::vector<Prediction> predict_files(const std::string& model, const std::vector<std::string>& paths) override {
+    auto slot = get(model);  // fail fast on an unknown model
     {
-      std::lock_guard<std::mutex> g(mu_);
-      engine(model);  // fail fast on an unknown model
-    }
-    {
-      // A batched query's misses decode in parallel (the host JPEG decode,
-      // ~5 ms for 500x375, was serial and bounded batched queries at ~200
-      // images/s per member); stage_one decodes outside the cache lock.
       DMLC_TRACE("executor.stage");
+      // misses decode in parallel (host JPEG decode dominates a miss)
       const size_t nt = std::min<size_t>(paths.size(), kDecodeThreads);
       if (nt <= 1) {
         for (const auto& p : paths) stage_one(p, /*count_as_miss=*/true);
@@ -255,18 +285,31 @@ class GpuExecutor : public Executor {
           if (e) std::rethrow_exception(e);
       }
     }
-    std::lock_guard<std::mutex> g(mu_);
-    Engine* e = engine(model);
-    std::vector<const void*> src(paths.size());
-    std::vector<std::pair<int, int>> hw(paths.size());
-    for (size_t i = 0; i < paths.size(); ++i) {
-      auto it = cache_.find(paths[i]);
-      if (it == cache_.end()) throw std::runtime_error("image evicted before use: " + paths[i]);
-      touch(it);
-      src[i] = it->second.dev;
-      hw[i] = {it->second.h, it->second.w};
+    std::vector<ImageDesc> descs(paths.size());
+    std::vector<std::string> pinned;
+    {
+      std::lock_guard<std::mutex> g(cache_mu_);
+      for (size_t i = 0; i < paths.size(); ++i) {
+        auto it = cache_.find(paths[i]);
+        if (it == cache_.end()) {
+          for (const auto& p : pinned) --cache_.at(p).pins;
+          throw std::runtime_error("image not resident: " + paths[i]);
+        }
+        touch(it);
+        ++it->second.pins;
+        pinned.push_back(paths[i]);
+        descs[i] = ImageDesc{(const uint8_t*)it->second.dev, it->second.h, it->second.w};
+      }
     }
-    return run(e, src, hw, hipMemcpyDeviceToDevice);
+    std::vector<Prediction> out;
+    try {
+      out = slot->run(descs);
+    } catch (...) {
+      unpin(pinned);
+      throw;
+    }
+    unpin(pinned);
+    return out;
   }
 
   bool stage(const std::string& path) override {
@@ -275,7 +318,7 @@ class GpuExecutor : public Executor {
   }
 
   CacheStats cache_stats() const override {
-    std::lock_guard<std::mutex> g(mu_);
+    std::lock_guard<std::mutex> g(cache_mu_);
     CacheStats c = stats_;
     c.bytes = cache_bytes_;
     c.entries = cache_.size();
@@ -285,28 +328,130 @@ class GpuExecutor : public Executor {
 
  private:
   static constexpr size_t kDecodeThreads = 8;
+  static constexpr int kStagers = 8;
+
+  // One model replicated on every GPU of the executor.
+  struct ModelSlot {
+    ModelSlot(const std::string& arch, const WeightMap& w, const std::vector<int>& devices, int max_batch,
+              int min_shard)
+        : max_batch(max_batch) {
+      for (int d : devices) {
+        DMLC_HIP_CHECK(hipSetDevice(d));
+        engines.push_back(std::make_unique<Engine>(arch, w, d));
+        engines.back()->reserve(max_batch);
+        workers.push_back(dp::make_hip_worker(engines.back().get(), kS, kS, /*use_graph=*/true));
+      }
+      std::vector<dp::Worker*> ws;
+      for (auto& x : workers) ws.push_back(x.get());
+      auto factory = [devices](const std::vector<int>& members) {
+        std::vector<int> devs;
+        for (int m : members) devs.push_back(devices.at(m));
+        return comm::rccl_init_all(devs);
+      };
+      group = std::make_unique<dp::Group>(ws, factory, max_batch, (size_t)kS * kS * 3);
+      group->set_min_per_rank(min_shard);
+      dp::Worker* c = group->coordinator();
+      c->activate();
+      batch = c->alloc((size_t)max_batch * kS * kS * 3);
+      d_descs = c->alloc((size_t)max_batch * sizeof(ImageDesc));
+      h_descs = (ImageDesc*)c->alloc_host((size_t)max_batch * sizeof(ImageDesc));
+      ev_src = c->new_event();
+    }
+    ~ModelSlot() {
+      dp::Worker* c = group->coordinator();
+      c->activate();
+      c->sync_all();
+      c->dealloc(batch);
+      c->dealloc(d_descs);
+      c->dealloc_host(h_descs);
+      group.reset();
+      workers.clear();
+      engines.clear();
+    }
+    // Resize the images into one u8 batch on the coordinator, then classify
+    // it across the group.
+    std::vector<Prediction> run(const std::vector<ImageDesc>& descs) {
+      DMLC_TRACE("executor.forward");
+      std::lock_guard<std::mutex> g(mu);
+      std::vector<Prediction> out(descs.size());
+      dp::Worker* c = group->coordinator();
+      c->activate();
+      auto s = (hipStream_t)c->stream(dp::Worker::kCompute);
+      for (size_t first = 0; first < descs.size(); first += (size_t)max_batch) {
+        const int B = (int)std::min(descs.size() - first, (size_t)max_batch);
+        c->sync(ev_src);  // the previous chunk's resize has read h_descs
+        std::memcpy(h_descs, descs.data() + first, (size_t)B * sizeof(ImageDesc));
+        DMLC_HIP_CHECK(hipMemcpyAsync(d_descs, h_descs, (size_t)B * sizeof(ImageDesc), hipMemcpyHostToDevice, s));
+        resize_u8_ragged((const ImageDesc*)d_descs, (uint8_t*)batch, B, kS, s);
+        c->record(ev_src, dp::Worker::kCompute);
+        std::vector<int32_t> idx(B);
+        std::vector<float> prob(B);
+        group->classify((const uint8_t*)batch, B, idx.data(), prob.data(), ev_src);
+        for (int b = 0; b < B; ++b) out[first + b] = Prediction{prob[b], idx[b]};
+      }
+      return out;
+    }
+    static constexpr int kS = 224;
+    int max_batch;
+    std::vector<std::unique_ptr<Engine>> engines;
+    std::vector<std::unique_ptr<dp::Worker>> workers;
+    std::unique_ptr<dp::Group> group;
+    void* batch = nullptr;
+    void* d_descs = nullptr;
+    ImageDesc* h_descs = nullptr;
+    int ev_src = -1;
+    std::mutex mu;  // one query batch at a time per model
+  };
+
   struct Entry {
     void* dev = nullptr;
     int h = 0, w = 0;
     size_t bytes = 0;
+    int pins = 0;
     std::list<std::string>::iterator lru;
   };
+  struct Stager {
+    hipStream_t stream = nullptr;
+    void* pinned = nullptr;
+    size_t pinned_bytes = 0;
+  };
 
-  Engine* engine(const std::string& model) {
-    auto it = engines_.find(model);
-    if (it == engines_.end()) throw std::runtime_error("model not loaded: " + model);
-    return it->second.get();
+  std::shared_ptr<ModelSlot> get(const std::string& model) const {
+    std::lock_guard<std::mutex> g(models_mu_);
+    auto it = models_.find(model);
+    if (it == models_.end()) throw std::runtime_error("model not loaded: " + model);
+    return it->second;
   }
 
-  void touch(std::unordered_map<std::string, Entry>::iterator it) {
-    lru_.splice(lru_.begin(), lru_, it->second.lru);
+  void touch(std::unordered_map<std::string, Entry>::iterator it) { lru_.splice(lru_.begin(), lru_, it->second.lru); }
+
+  void unpin(const std::vector<std::string>& paths) {
+    std::lock_guard<std::mutex> g(cache_mu_);
+    for (const auto& p : paths) {
+      auto it = cache_.find(p);
+      if (it != cache_.end()) --it->second.pins;
+    }
   }
 
-  // Decode (outside the lock) and upload on the side stream, so staging
-  // overlaps inference running on the main stream.
+  Stager take_stager() {
+    std::unique_lock<std::mutex> g(stager_mu_);
+    stager_cv_.wait(g, [&] { return !free_stagers_.empty(); });
+    Stager s = free_stagers_.back();
+    free_stagers_.pop_back();
+    return s;
+  }
+  void give_stager(const Stager& s) {
+    std::lock_guard<std::mutex> g(stager_mu_);
+    free_stagers_.push_back(s);
+    stager_cv_.notify_one();
+  }
+
+  // Decode and upload without holding the cache lock: the JPEG is decoded on
+  // this thread, copied into the stager's pinned buffer and DMA'd into a new
+  // HBM block on the stager's stream; only the final insert/evict locks.
   void stage_one(const std::string& path, bool count_as_miss) {
     {
-      std::lock_guard<std::mutex> g(mu_);
+      std::lock_guard<std::mutex> g(cache_mu_);
       auto it = cache_.find(path);
       if (it != cache_.end()) {
         if (count_as_miss) ++stats_.hits;
@@ -316,97 +461,86 @@ class GpuExecutor : public Executor {
     }
     const Image img = decode_jpeg_file(path);
     const size_t bytes = img.rgb.size();
-    std::lock_guard<std::mutex> g(mu_);
-    if (cache_.count(path)) return;  // raced with another stager
+    Stager st = take_stager();
+    void* dev = nullptr;
+    try {
+      DMLC_HIP_CHECK(hipSetDevice(devices_[0]));
+      if (st.pinned_bytes < bytes) {
+        if (st.pinned) DMLC_HIP_CHECK(hipHostFree(st.pinned));
+        st.pinned = nullptr;
+        st.pinned_bytes = 0;
+        DMLC_HIP_CHECK(hipHostMalloc(&st.pinned, bytes, hipHostMallocDefault));
+        st.pinned_bytes = bytes;
+      }
+      std::memcpy(st.pinned, img.rgb.data(), bytes);
+      DMLC_HIP_CHECK(hipMallocAsync(&dev, bytes, st.stream));
+      DMLC_HIP_CHECK(hipMemcpyAsync(dev, st.pinned, bytes, hipMemcpyHostToDevice, st.stream));
+      DMLC_HIP_CHECK(hipStreamSynchronize(st.stream));  // resident before it is visible
+    } catch (...) {
+      give_stager(st);
+      throw;
+    }
+    give_stager(st);
+    std::lock_guard<std::mutex> g(cache_mu_);
+    if (cache_.count(path)) {  // raced with another stager
+      (void)hipFree(dev);
+      return;
+    }
     if (count_as_miss) ++stats_.misses; else ++stats_.staged;
-    DMLC_HIP_CHECK(hipSetDevice(device_));
-    while (!lru_.empty() && cache_bytes_ + bytes > cache_cap_) {
-      auto victim = cache_.find(lru_.back());
-      // stream-ordered free: in-flight batches on stream_ may still read it
-      DMLC_HIP_CHECK(hipFreeAsync(victim->second.dev, stream_));
-      cache_bytes_ -= victim->second.bytes;
-      cache_.erase(victim);
-      lru_.pop_back();
+    // evict least-recently-used entries no query has pinned
+    auto victim = lru_.end();
+    while (cache_bytes_ + bytes > cache_cap_ && victim != lru_.begin()) {
+      --victim;
+      auto it = cache_.find(*victim);
+      if (it->second.pins > 0) continue;
+      (void)hipFree(it->second.dev);  // unpinned: no queued kernel reads it
+      cache_bytes_ -= it->second.bytes;
+      cache_.erase(it);
+      victim = lru_.erase(victim);
       ++stats_.evictions;
     }
     Entry en;
+    en.dev = dev;
     en.h = img.height;
     en.w = img.width;
     en.bytes = bytes;
-    DMLC_HIP_CHECK(hipMallocAsync(&en.dev, bytes, side_));
-    DMLC_HIP_CHECK(hipMemcpyAsync(en.dev, img.rgb.data(), bytes, hipMemcpyHostToDevice, side_));
-    DMLC_HIP_CHECK(hipStreamSynchronize(side_));  // resident before it is visible
     lru_.push_front(path);
     en.lru = lru_.begin();
     cache_bytes_ += bytes;
     cache_.emplace(path, en);
   }
 
-  // Group same-sized images; each group is one batched forward.
-  std::vector<Prediction> run(Engine* e, const std::vector<const void*>& src,
-                              const std::vector<std::pair<int, int>>& hw, hipMemcpyKind kind) {
-    DMLC_TRACE("executor.forward");
-    DMLC_HIP_CHECK(hipSetDevice(device_));
-    std::vector<Prediction> out(src.size());
-    std::map<std::pair<int, int>, std::vector<size_t>> groups;
-    for (size_t i = 0; i < src.size(); ++i) groups[hw[i]].push_back(i);
-    for (const auto& kv : groups) {
-      const int H = kv.first.first, W = kv.first.second;
-      const auto& ids = kv.second;
-      for (size_t s = 0; s < ids.size(); s += (size_t)max_batch_) {
-        const int B = (int)std::min(ids.size() - s, (size_t)max_batch_);
-        const size_t per = (size_t)H * W * 3;
-        ensure_input(per * B);
-        for (int b = 0; b < B; ++b)
-          DMLC_HIP_CHECK(hipMemcpyAsync((uint8_t*)d_in_ + per * b, src[ids[s + b]], per, kind, stream_));
-        int32_t* d_idx = (int32_t*)d_out_;
-        float* d_prob = (float*)((int32_t*)d_out_ + max_batch_);
-        // graphs only for the fixed-size serving shape; ragged sizes run eager
-        e->forward((const uint8_t*)d_in_, B, H, W, d_idx, d_prob, nullptr, stream_, H == 224 && W == 224);
-        std::vector<int32_t> hi(B);
-        std::vector<float> hp(B);
-        DMLC_HIP_CHECK(hipMemcpyAsync(hi.data(), d_idx, B * 4, hipMemcpyDeviceToHost, stream_));
-        DMLC_HIP_CHECK(hipMemcpyAsync(hp.data(), d_prob, B * 4, hipMemcpyDeviceToHost, stream_));
-        DMLC_HIP_CHECK(hipStreamSynchronize(stream_));
-        for (int b = 0; b < B; ++b) out[ids[s + b]] = Prediction{hp[b], hi[b]};
-      }
-    }
-    return out;
-  }
-
-  void ensure_input(size_t bytes) {
-    if (bytes <= in_bytes_) return;
-    DMLC_HIP_CHECK(hipStreamSynchronize(stream_));
-    if (d_in_) DMLC_HIP_CHECK(hipFree(d_in_));
-    DMLC_HIP_CHECK(hipMalloc(&d_in_, bytes));
-    in_bytes_ = bytes;
-  }
-
-  int device_, max_batch_;
-  hipStream_t stream_ = nullptr, side_ = nullptr;
-  void* d_in_ = nullptr;
-  size_t in_bytes_ = 0;
-  void* d_out_ = nullptr;
-  mutable std::mutex mu_;
-  std::map<std::string, std::unique_ptr<Engine>> engines_;
+  std::vector<int> devices_;
+  int max_batch_, min_shard_;
+  mutable std::mutex models_mu_;
+  std::map<std::string, std::shared_ptr<ModelSlot>> models_;
+  mutable std::mutex cache_mu_;
   std::unordered_map<std::string, Entry> cache_;
   std::list<std::string> lru_;
   size_t cache_bytes_ = 0, cache_cap_;
   CacheStats stats_;
+  std::mutex stager_mu_;
+  std::condition_variable stager_cv_;
+  std::vector<Stager> free_stagers_;
 };
 
 }  // namespace
 
-std::unique_ptr<Executor> make_executor(const std::string& backend, int device, int max_batch,
-                                        size_t cache_bytes) {
+std::unique_ptr<Executor> make_executor(const std::string& backend, const std::vector<int>& devices, int max_batch,
+                                        size_t cache_bytes, int min_shard) {
   std::string b = backend;
   if (b == "auto") b = hip_device_count() > 0 ? "gpu" : "cpu";
   if (b == "gpu") {
-    if (hip_device_count() <= device) throw std::runtime_error("no HIP device " + std::to_string(device));
-    return std::make_unique<GpuExecutor>(device, max_batch, cache_bytes);
+    for (int d : devices)
+      if (d < 0 || hip_device_count() <= d) throw std::runtime_error("no HIP device " + std::to_string(d));
+    return std::make_unique<GpuExecutor>(devices, max_batch, cache_bytes, min_shard);
   }
   if (b == "cpu") return std::make_unique<CpuExecutor>();
   throw std::invalid_argument("unknown executor backend: " + backend);
+}
+
+std::unique_ptr<Executor> make_executor(const std::string& backend, int device, int max_batch, size_t cache_bytes) {
+  return make_executor(backend, std::vector<int>{device}, max_batch, cache_bytes, 1);
 }
 
 }  // namespace dmlc

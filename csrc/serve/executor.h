@@ -60,6 +60,11 @@ class Executor {
 // cache_bytes: HBM budget for decoded images (GPU executor).
 std::unique_ptr<Executor> make_executor(const std::string& backend, int device, int max_batch,
                                         size_t cache_bytes = (size_t)4 << 30);
+// Several GPUs of this node (GPU executor): one engine per GPU and model; a
+// query batch is resized into one u8 batch on devices[0] and scattered over
+// the GPUs with RCCL (csrc/comm), each GPU taking >= min_shard images.
+std::unique_ptr<Executor> make_executor(const std::string& backend, const std::vector<int>& devices, int max_batch,
+                                        size_t cache_bytes, int min_shard);
 int hip_device_count();
 
 // Host-side reference preprocessing (same rule as csrc/kernels/preprocess.hip):

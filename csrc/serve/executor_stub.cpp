@@ -97,6 +97,11 @@ std::unique_ptr<Executor> make_executor(const std::string& backend, int, int, si
   throw std::runtime_error("executor '" + backend + "' is not available in the sanitizer build");
 }
 
+std::unique_ptr<Executor> make_executor(const std::string& backend, const std::vector<int>& devices, int max_batch,
+                                        size_t cache_bytes, int) {
+  return make_executor(backend, devices.empty() ? 0 : devices[0], max_batch, cache_bytes);
+}
+
 int hip_device_count() { return 0; }
 
 }  // namespace dmlc

@@ -37,11 +37,14 @@ def synthetic_labels(n: int = 1000) -> list[tuple[str, str]]:
 
 def make_synthetic_dataset(root: str, labels: list[tuple[str, str]], size=(375, 500), seed: int = 0,
                            quality: int = 90) -> str:
-    """One smooth random JPEG per wnid (PIL encoder, baseline JPEG)."""
+    """One smooth random JPEG per wnid (PIL encoder, baseline JPEG). `size`
+    is (h, w) or a list of (h, w) used in turn (ragged, like the reference's
+    imagenet_1k with its 344 distinct sizes)."""
     from PIL import Image
     rng = np.random.default_rng(seed)
-    h, w = size
+    sizes = size if isinstance(size, list) else [size]
     for i, (wnid, _) in enumerate(labels):
+        h, w = sizes[i % len(sizes)]
         d = os.path.join(root, wnid)
         os.makedirs(d, exist_ok=True)
         base = rng.integers(0, 256, (h // 16 + 1, w // 16 + 1, 3), dtype=np.uint8)

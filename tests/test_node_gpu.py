@@ -46,6 +46,23 @@ def test_gpu_executor_agrees_with_cpu(gpu, env):
     assert agree >= 14, (g, c)  # bf16 vs fp32: only near-ties may flip
 
 
+def test_gpu_executor_ragged_batch_agrees_with_cpu(gpu, env, tmp_path):
+    """Mixed-size JPEGs in one query: the GPU executor resizes them into one
+    u8 batch (resize.hip) and runs one forward; the CPU executor applies the
+    same resize rule per image."""
+    sizes = [(224, 224), (375, 500), (500, 333), (256, 300), (480, 640), (199, 211), (224, 300), (640, 427)]
+    ds = make_synthetic_dataset(str(tmp_path / "ragged"), env["entries"][:16], size=sizes, seed=9)
+    imgs = []
+    for wnid, _ in env["entries"][:16]:
+        d = os.path.join(ds, wnid)
+        imgs.append(os.path.join(d, sorted(os.listdir(d))[0]))
+    g, _ = _classify(env, "gpu", imgs)
+    c, _ = _classify(env, "cpu", imgs)
+    assert len(g) == len(c) == 16
+    agree = sum(a == b for a, b in zip(g, c))
+    assert agree >= 14, (g, c)
+
+
 def test_gpu_cluster_predict(gpu, env, tmp_path):
     cl = LocalCluster(2, 19700, str(tmp_path / "c"), env["labels"], n_leaders=1, executor="gpu",
                       dataset=env["dataset"], models=f"resnet18={env['ckpt']}",
