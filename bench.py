@@ -87,6 +87,8 @@ def main():
     ap.add_argument("--latency-steps", type=int, default=50, help="unpipelined steps for the batch latency")
     ap.add_argument("--latency-queries", type=int, default=200, help="batch-1 GPU queries (GPU-only latency)")
     ap.add_argument("--profile-ops", action="store_true", help="print per-op times of one eager forward")
+    ap.add_argument("--e2e-queries", type=int, default=200,
+                    help="queries through a dmlc-node cluster for the reference-definition query latency (0: skip)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -187,6 +189,18 @@ def main():
             if i >= 20:
                 qlat.append((time.perf_counter() - t) * 1e3)
 
+    # Query latency with the reference's definition (connect + RPC + JPEG
+    # decode + resize + forward + top-1, one query at a time) through a
+    # one-node dmlc-node cluster on this GPU.
+    e2e = None
+    if rank == 0 and args.e2e_queries > 0:
+        try:
+            from dmlc.serve.e2e import query_latency
+            e2e = query_latency(args.e2e_queries, args.model if args.model in ("resnet18", "alexnet") else "resnet18",
+                                device=local_rank)
+        except Exception as ex:  # noqa: BLE001  (reported, never fails the throughput bench)
+            print(f"# e2e query latency failed: {ex}", file=sys.stderr)
+
     ops_profile = None
     if rank == 0 and args.profile_ops:
         ops_profile = eng.profile(pool[:B].contiguous())
@@ -225,6 +239,13 @@ def main():
             "per_rank_images_s": [round(B * args.steps / s, 1) for s in per_rank_s],
             "batch_latency_p50_ms": round(pct(batch_lat, 50), 3),
             "batch_latency_p95_ms": round(pct(batch_lat, 95), 3),
+            "query_latency_mean_ms": round(e2e["mean_ms"], 3) if e2e else None,
+            "query_latency_p50_ms": round(e2e["p50_ms"], 3) if e2e else None,
+            "query_latency_p95_ms": round(e2e["p95_ms"], 3) if e2e else None,
+            "query_latency_def": "reference definition (src/services.rs:419-424): connect + RPC + JPEG decode + "
+                                 "resize + forward + top-1 through a one-node dmlc-node cluster, one query in flight; "
+                                 + (e2e["data"] if e2e else "not measured"),
+            "vs_baseline_latency": round(REF_MEAN_LATENCY_MS / e2e["mean_ms"], 1) if e2e else None,
             "gpu_batch1_latency_p50_ms": round(pct(qlat, 50), 4) if qlat else None,
             "gpu_batch1_latency_p95_ms": round(pct(qlat, 95), 4) if qlat else None,
             "tflops_effective": round(value * eng.gflop_per_image / 1e3, 1),

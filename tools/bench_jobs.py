@@ -71,6 +71,10 @@ def main():
     ap.add_argument("--fast-periods", action="store_true", help="200 ms pings, 1.2 s failure timeout, 500 ms loops")
     ap.add_argument("--port", type=int, default=21000)
     ap.add_argument("--out", default="")
+    ap.add_argument("--dataset", default="", help="imagenet_1k layout dir (default: synthetic 500x375 JPEGs)")
+    ap.add_argument("--labels", default="", help="synset_words.txt matching --dataset")
+    ap.add_argument("--prefetch", action="store_true", help="stage every query image into HBM before predict")
+    ap.add_argument("--node-gpus", type=int, default=1, help="GPUs per node (RCCL scatter inside a node)")
     a = ap.parse_args()
 
     ngpu = a.gpus
@@ -78,17 +82,25 @@ def main():
         import torch
         ngpu = torch.cuda.device_count()
     root = tempfile.mkdtemp(prefix="dmlc_jobs_")
-    labels = synthetic_labels(1000)
-    lab = write_labels(os.path.join(root, "synset_words.txt"), labels)
-    t = time.time()
-    ds = make_synthetic_dataset(os.path.join(root, "train"), labels[:a.images], size=(375, 500))
-    print(f"# dataset: {a.images} JPEGs 500x375 in {time.time() - t:.1f}s", file=sys.stderr)
+    if a.dataset:
+        ds, lab = os.path.abspath(a.dataset), os.path.abspath(a.labels)
+        n_avail = len(os.listdir(ds))
+        if a.images > n_avail:
+            a.images = n_avail
+        data_desc = f"real imagenet_1k JPEGs from the reference ({a.images} classes, {ds}), random-init weights"
+    else:
+        labels = synthetic_labels(1000)
+        lab = write_labels(os.path.join(root, "synset_words.txt"), labels)
+        t = time.time()
+        ds = make_synthetic_dataset(os.path.join(root, "train"), labels[:a.images], size=(375, 500))
+        print(f"# dataset: {a.images} JPEGs 500x375 in {time.time() - t:.1f}s", file=sys.stderr)
+        data_desc = "synthetic 500x375 JPEGs (imagenet_1k layout), random-init weights"
     ck = {m: write_random_checkpoint(m, os.path.join(root, f"{m}.ot"), seed=i) for i, m in
           enumerate(["resnet18", "alexnet"])}
     models = ",".join(f"{m}={p}" for m, p in ck.items())
     extra = ["--job-limit", str(a.images), "--query-interval-ms", str(a.interval_ms), "--query-batch",
              str(a.batch), "--quiet-predictions", "--max-batch", str(max(8, a.batch)),
-             "--adaptive-window", str(a.adaptive_window)]
+             "--adaptive-window", str(a.adaptive_window)] + (["--prefetch"] if a.prefetch else [])
     cl = LocalCluster(a.nodes, a.port, os.path.join(root, "c"), lab, n_leaders=2, executor=a.executor,
                       dataset=ds, models=models, fast=a.fast_periods, extra=extra)
     if a.kill == "member" and a.nodes < 3:
@@ -97,7 +109,9 @@ def main():
     try:
         from dmlc.serve.cluster import NodeProcess
         for i, p in enumerate(cl.ports):
-            ex = list(extra) + (["--device", str(i % ngpu)] if ngpu else [])
+            ex = list(extra) + (["--device", str((i * a.node_gpus) % ngpu)] if ngpu else [])
+            if a.node_gpus > 1:
+                ex += ["--gpus", str(a.node_gpus)]
             nodes.append(NodeProcess(p, cl.leaders, os.path.join(cl.root, f"n{p}"), lab, dataset=ds,
                                      models=models, executor=a.executor, fast=a.fast_periods, extra=ex))
         cl.nodes = nodes
@@ -138,7 +152,7 @@ def main():
     res = {"bench": "two concurrent predict jobs through the control plane", "nodes": a.nodes,
            "executor": a.executor, "gpus": ngpu, "images_per_job": a.images, "query_interval_ms": a.interval_ms,
            "adaptive_window": a.adaptive_window,
-           "query_batch": a.batch, "data": "synthetic 500x375 JPEGs (imagenet_1k layout), random-init weights",
+           "query_batch": a.batch, "data": data_desc, "prefetch": a.prefetch, "node_gpus": a.node_gpus,
            "reference": REF, "jobs": []}
     for j in jobs:
         d = [x / 1000 for x in j["durations_us"]]
