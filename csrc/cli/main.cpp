@@ -53,6 +53,17 @@ using namespace dmlc::ctl;
 
 namespace {
 
+// Grants peers access to one absolute path for the lifetime of a command.
+struct PathGrant {
+  PathGrant(MemberService& m, std::string p, bool write) : m_(m), p_(std::move(p)), w_(write) {
+    w_ ? m_.allow_write(p_, true) : m_.allow_read(p_, true);
+  }
+  ~PathGrant() { w_ ? m_.allow_write(p_, false) : m_.allow_read(p_, false); }
+  MemberService& m_;
+  std::string p_;
+  bool w_;
+};
+
 struct Args {
   std::map<std::string, std::string> kv;
   std::vector<std::string> pos;
@@ -168,8 +179,10 @@ void handle_line(Node& n, const std::string& line) {
     } else if (c == "put" || c == "p") {
       if (t.size() != 3) return err_line("Invalid put command!");
       Writer w;
+      const std::string src = absolutize(t[1]);
       write_id(w, n.ms->id());
-      w.str(absolutize(t[1])).str(t[2]);
+      w.str(src).str(t[2]);
+      PathGrant grant(*n.member, src, /*write=*/false);  // peers may read it while the put runs
       Reader r(n.call_leader(L_PUT, w.data()));
       std::vector<Id> ids;
       const uint32_t k = r.u32();
@@ -178,9 +191,11 @@ void handle_line(Node& n, const std::string& line) {
     } else if (c == "get" || c == "g") {
       if (t.size() != 3) return err_line("Invalid get command!");
       Writer w;
+      const std::string dest = absolutize(t[2]);
       w.str(t[1]);
       write_id(w, n.ms->id());
-      w.str(absolutize(t[2]));
+      w.str(dest);
+      PathGrant grant(*n.member, dest, /*write=*/true);
       Reader r(n.call_leader(L_GET, w.data()));
       const bool found = r.boolean();
       const int v = r.i32();
@@ -225,6 +240,7 @@ void handle_line(Node& n, const std::string& line) {
       w.str(t[1]).i32(count);
       write_id(w, n.ms->id());
       w.str(dest);
+      PathGrant grant(*n.member, dest, /*write=*/true);  // and its v<N>.<name> siblings
       Reader r(n.call_leader(L_GET_VERSIONS, w.data()));
       std::set<int> vs;
       const uint32_t k = r.u32();

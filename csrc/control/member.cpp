@@ -122,19 +122,68 @@ std::string MemberService::resolve_spec(const std::string& spec) const {
   return cfg_.workdir + "/" + spec;
 }
 
+void MemberService::allow_read(const std::string& p, bool on) {
+  std::lock_guard<std::mutex> g(mu_);
+  if (on) readable_.insert(p);
+  else if (readable_.count(p)) readable_.erase(readable_.find(p));
+}
+
+void MemberService::allow_write(const std::string& p, bool on) {
+  std::lock_guard<std::mutex> g(mu_);
+  if (on) writable_.insert(p);
+  else if (writable_.count(p)) writable_.erase(writable_.find(p));
+}
+
+namespace {
+bool managed_spec(const std::string& spec) { return starts_with(spec, "storage:") || starts_with(spec, "models:"); }
+}  // namespace
+
+std::string MemberService::readable_path(const std::string& spec) const {
+  if (managed_spec(spec)) return resolve_spec(spec);
+  std::lock_guard<std::mutex> g(mu_);
+  if (!spec.empty() && spec[0] == '/' && readable_.count(spec)) return spec;
+  throw std::runtime_error("refused: " + spec + " is not exported by this node");
+}
+
+std::string MemberService::writable_path(const std::string& spec) const {
+  if (managed_spec(spec)) return resolve_spec(spec);
+  std::lock_guard<std::mutex> g(mu_);
+  if (!spec.empty() && spec[0] == '/') {
+    if (writable_.count(spec)) return spec;
+    // get-versions writes v<N>.<name> next to the requested destination
+    const auto slash = spec.rfind('/');
+    const std::string dir = spec.substr(0, slash + 1), base = spec.substr(slash + 1);
+    size_t i = 1;
+    if (base.size() > 2 && base[0] == 'v') {
+      while (i < base.size() && isdigit((unsigned char)base[i])) ++i;
+      if (i > 1 && i < base.size() && base[i] == '.' && writable_.count(dir + base.substr(i + 1))) return spec;
+    }
+  }
+  throw std::runtime_error("refused: " + spec + " is not an expected destination on this node");
+}
+
 std::vector<std::pair<double, std::string>> MemberService::predict(const std::string& model,
                                                                    const std::vector<std::string>& ids, bool* ok) {
   *ok = false;
   std::vector<std::pair<double, std::string>> out;
   if (!exec_ || !exec_->has_model(model)) return out;
   DMLC_TRACE("member.predict");
+  // One answer per requested id, in order: an id without an image (the
+  // reference's read_dir would fail) answers (-1, "") so the leader never
+  // shifts later answers onto the wrong labels.
   std::vector<std::string> paths;
-  for (const auto& id : ids) {
-    std::string p = query_image(id);
-    if (!p.empty()) paths.push_back(std::move(p));  // unknown id: skipped, like a failed read_dir entry
+  std::vector<size_t> where;
+  for (size_t i = 0; i < ids.size(); ++i) {
+    std::string p = query_image(ids[i]);
+    if (!p.empty()) {
+      paths.push_back(std::move(p));
+      where.push_back(i);
+    }
   }
+  out.assign(ids.size(), {-1.0, std::string()});
   const auto preds = exec_->predict_files(model, paths);
-  for (const auto& p : preds) out.emplace_back(p.prob, labels_.text(p.class_idx));
+  for (size_t k = 0; k < preds.size() && k < where.size(); ++k)
+    out[where[k]] = {preds[k].prob, labels_.text(preds[k].class_idx)};
   *ok = true;
   return out;
 }
@@ -167,9 +216,10 @@ bool MemberService::start_prefetch() {
 
 bool MemberService::fetch(const std::string& src_host, int src_port, const std::string& src_spec,
                           const std::string& dest_spec) {
-  const std::string dest = resolve_spec(dest_spec);
-  const std::string tmp = dest + ".part" + std::to_string(getpid());
+  std::string dest, tmp;
   try {
+    dest = writable_path(dest_spec);
+    tmp = dest + ".part" + std::to_string(getpid());
     std::ofstream out(tmp, std::ios::binary | std::ios::trunc);
     if (!out) throw std::runtime_error("cannot open " + tmp);
     uint64_t off = 0;
@@ -190,7 +240,7 @@ bool MemberService::fetch(const std::string& src_host, int src_port, const std::
                            << " B)");
     return true;
   } catch (const std::exception& e) {
-    unlink(tmp.c_str());
+    if (!tmp.empty()) unlink(tmp.c_str());
     DMLC_LOG_WARN("fetch " << src_host << ":" << src_port << ":" << src_spec << " -> " << dest
                            << ": failed: " << e.what());
     return false;
@@ -241,7 +291,7 @@ void MemberService::register_handlers() {
     const std::string spec = r.str();
     const uint64_t off = r.u64();
     const uint32_t len = std::min<uint32_t>(r.u32(), 64u << 20);
-    const std::string path = resolve_spec(spec);
+    const std::string path = readable_path(spec);
     std::ifstream f(path, std::ios::binary);
     if (!f) throw std::runtime_error("no such file: " + spec);
     f.seekg(0, std::ios::end);
@@ -274,6 +324,7 @@ void MemberService::register_handlers() {
     Writer w;
     try {
       if (!exec_) throw std::runtime_error("no executor");
+      if (!managed_spec(spec)) throw std::runtime_error("refused: models load from storage:/models: specs only");
       exec_->load_model(model, resolve_spec(spec));
       DMLC_LOG_INFO("loaded model " << model << " from " << resolve_spec(spec));
       w.boolean(true).str("");

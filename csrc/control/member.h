@@ -63,6 +63,17 @@ class MemberService {
                                                       bool* ok);
   bool fetch(const std::string& src_host, int src_port, const std::string& src_spec, const std::string& dest_spec);
 
+  // What peers may touch through M_READ_CHUNK / M_FETCH / M_LOAD_MODEL:
+  // `storage:` and `models:` specs always; an absolute path only while this
+  // node's own command that needs it runs — the source of a `put`
+  // (readable), the destination of a `get` / `get-versions` (writable, plus
+  // its v<N>.<name> siblings). Everything else is refused, so a peer cannot
+  // read or write arbitrary files.
+  void allow_read(const std::string& abs_path, bool on);
+  void allow_write(const std::string& abs_path, bool on);
+  std::string readable_path(const std::string& spec) const;  // throws if refused
+  std::string writable_path(const std::string& spec) const;  // throws if refused
+
   // Stage the dataset's query images (first file of every class directory,
   // in label order) into the executor's cache on a background thread, so
   // queries hit HBM-resident images. Returns false if the executor has no
@@ -83,6 +94,7 @@ class MemberService {
   std::unique_ptr<RpcServer> server_;
   mutable std::mutex mu_;
   std::map<std::string, std::set<int>> files_;
+  std::multiset<std::string> readable_, writable_;  // under mu_
   std::string leader_;
   std::atomic<bool> stop_{false};
   std::thread checker_;

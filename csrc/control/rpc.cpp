@@ -9,7 +9,7 @@ namespace dmlc {
 namespace ctl {
 
 namespace {
-constexpr uint32_t kMaxFrame = 1u << 30;
+constexpr uint32_t kMaxFrame = 128u << 20;  // > the 64 MiB fetch chunk; bounds what a peer can make us allocate
 
 bool read_frame(int fd, std::string* out) {
   uint32_t len = 0;

@@ -39,6 +39,9 @@ struct Huff {
       mincode[l] = code;
       code += count[l];
       k += count[l];
+      // an over-subscribed table (more codes than 2^l) would overflow the
+      // lookup tables below (found by tests/test_fuzz_cpu.py)
+      if (code > (1 << l)) throw std::runtime_error("jpeg: bad huffman table");
       maxcode[l] = count[l] ? code - 1 : -1;
       code <<= 1;
     }
@@ -475,6 +478,10 @@ Image decode_jpeg(const uint8_t* data, size_t size) {
         W = be16(seg + 3);
         const int nc = seg[5];
         if (W <= 0 || H <= 0 || (nc != 1 && nc != 3)) throw std::runtime_error("jpeg: unsupported frame");
+        // a forged frame header must not allocate gigabytes
+        if (W > 16384 || H > 16384 || (int64_t)W * H > (int64_t)64 << 20)
+          throw std::runtime_error("jpeg: image too large");
+        if (frame) throw std::runtime_error("jpeg: second frame header");
         comps.resize(nc);
         for (int i = 0; i < nc; ++i) {
           comps[i].id = seg[6 + 3 * i];
@@ -522,7 +529,8 @@ Image decode_jpeg(const uint8_t* data, size_t size) {
           if (!c) throw std::runtime_error("jpeg: bad scan component");
           c->td = seg[2 + 2 * i] >> 4;
           c->ta = seg[2 + 2 * i] & 15;
-          if (!dc[c->td & 3].present || !ac[c->ta & 3].present) throw std::runtime_error("jpeg: missing huffman table");
+          if (c->td > 3 || c->ta > 3 || !dc[c->td].present || !ac[c->ta].present)
+            throw std::runtime_error("jpeg: missing huffman table");
           sc.push_back(c);
         }
         BitReader br(seg_end, end);
@@ -536,6 +544,7 @@ Image decode_jpeg(const uint8_t* data, size_t size) {
           std::memset(blk, 0, sizeof(blk));
           const float* q = qf[c.tq];
           const int t = decode_huff(dc[c.td], br);
+          if (t > 15) throw std::runtime_error("jpeg: bad DC magnitude");
           c.pred += t ? extend(br.bits(t), t) : 0;
           blk[0] = (float)c.pred * q[0];
           const Huff& ha = ac[c.ta];

@@ -7,6 +7,16 @@
 namespace dmlc {
 namespace ctl {
 
+namespace {
+// A count read off the wire may not promise more elements than the bytes
+// that are left (a forged count would otherwise allocate gigabytes).
+uint32_t bounded(Reader& r, size_t elem_bytes) {
+  const uint32_t n = r.u32();
+  if ((uint64_t)n * elem_bytes > r.left()) throw WireError("count exceeds message");
+  return n;
+}
+}  // namespace
+
 void write_job(Writer& w, const Job& j) {
   w.str(j.model_name);
   w.i32(j.finished);
@@ -19,6 +29,51 @@ void write_job(Writer& w, const Job& j) {
   for (const auto& id : j.assigned) write_id(w, id);
   w.i64(j.started_us);
   w.i64(j.first_done_us);
+  w.i64(j.elapsed_us);
+}
+
+void write_job_delta(Writer& w, const Job& j, uint32_t from) {
+  if (from > j.durations_us.size() || from > j.done_us.size()) from = 0;
+  w.u32(from);
+  w.str(j.model_name);
+  w.i32(j.finished);
+  w.i32(j.correct);
+  w.u32((uint32_t)(j.durations_us.size() - from));
+  for (size_t i = from; i < j.durations_us.size(); ++i) w.i64(j.durations_us[i]);
+  w.u32((uint32_t)(j.done_us.size() - from));
+  for (size_t i = from; i < j.done_us.size(); ++i) w.i64(j.done_us[i]);
+  w.u32((uint32_t)j.assigned.size());
+  for (const auto& id : j.assigned) write_id(w, id);
+  w.i64(j.started_us);
+  w.i64(j.first_done_us);
+  w.i64(j.elapsed_us);
+}
+
+bool read_job_delta(Reader& r, Job& j) {
+  const uint32_t from = r.u32();
+  Job d;
+  d.model_name = r.str();
+  d.finished = r.i32();
+  d.correct = r.i32();
+  uint32_t n = bounded(r, 8);
+  std::vector<int64_t> dur(n), done;
+  for (uint32_t i = 0; i < n; ++i) dur[i] = r.i64();
+  n = bounded(r, 8);
+  done.resize(n);
+  for (uint32_t i = 0; i < n; ++i) done[i] = r.i64();
+  n = r.u32();
+  for (uint32_t i = 0; i < n; ++i) d.assigned.push_back(read_id(r));
+  d.started_us = r.i64();
+  d.first_done_us = r.i64();
+  d.elapsed_us = r.i64();
+  if (from > 0 && (j.durations_us.size() != from || j.done_us.size() != from || j.model_name != d.model_name))
+    return false;
+  d.durations_us = from ? j.durations_us : std::vector<int64_t>();
+  d.done_us = from ? j.done_us : std::vector<int64_t>();
+  d.durations_us.insert(d.durations_us.end(), dur.begin(), dur.end());
+  d.done_us.insert(d.done_us.end(), done.begin(), done.end());
+  j = std::move(d);
+  return true;
 }
 
 Job read_job(Reader& r) {
@@ -26,16 +81,17 @@ Job read_job(Reader& r) {
   j.model_name = r.str();
   j.finished = r.i32();
   j.correct = r.i32();
-  uint32_t n = r.u32();
+  uint32_t n = bounded(r, 8);
   j.durations_us.resize(n);
   for (uint32_t i = 0; i < n; ++i) j.durations_us[i] = r.i64();
-  n = r.u32();
+  n = bounded(r, 8);
   j.done_us.resize(n);
   for (uint32_t i = 0; i < n; ++i) j.done_us[i] = r.i64();
   n = r.u32();
   for (uint32_t i = 0; i < n; ++i) j.assigned.push_back(read_id(r));
   j.started_us = r.i64();
   j.first_done_us = r.i64();
+  j.elapsed_us = r.i64();
   return j;
 }
 
@@ -80,8 +136,8 @@ std::string format_job_report(int n, const Job& j) {
            n, j.model_name.c_str(), j.correct, j.finished, acc, s.count, s.mean, s.stddev, s.p50, s.p90, s.p95,
            s.p99);
   std::string out = buf;
-  if (j.finished > 0 && j.started_us > 0 && !j.done_us.empty() && j.done_us.back() > j.started_us) {
-    const double secs = (j.done_us.back() - j.started_us) * 1e-6;
+  if (j.finished > 0 && j.elapsed_us > 0) {
+    const double secs = j.elapsed_us * 1e-6;
     snprintf(buf, sizeof(buf), "\n\tThroughput: %.2f queries/s", j.finished / secs);
     out += buf;
   }

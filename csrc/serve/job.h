@@ -27,6 +27,10 @@ struct Job {
   std::vector<Id> assigned;
   int64_t started_us = 0;   // wall clock when the job first issued a query
   int64_t first_done_us = 0;
+  // Time the job has been running, summed over the leaders that ran it,
+  // each measured on its own steady clock (the Throughput line; wall clocks
+  // of different leaders are never subtracted from each other).
+  int64_t elapsed_us = 0;
 
   void add_result(bool ok, int64_t dur_us, int64_t done_wall_us = 0) {
     ++finished;
@@ -38,6 +42,12 @@ struct Job {
 
 void write_job(Writer& w, const Job& j);
 Job read_job(Reader& r);
+// Incremental form for the standby copy: per-query vectors from index
+// `from` on (the standby already holds the first `from`).
+void write_job_delta(Writer& w, const Job& j, uint32_t from);
+// Applies a delta onto `j` (which holds `from` entries); false if `j` does
+// not line up (the standby then asks for everything again).
+bool read_job_delta(Reader& r, Job& j);
 
 struct LatencyStats {
   size_t count = 0;

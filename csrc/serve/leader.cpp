@@ -18,12 +18,18 @@ LeaderService::LeaderService(LeaderConfig cfg, MembershipService* ms, MemberServ
     jobs_.push_back(j);
   }
   running_.assign(jobs_.size(), false);
+  retry_.resize(jobs_.size());
   job_inflight_.reset(new std::atomic<int>[jobs_.size()]);
   for (size_t j = 0; j < jobs_.size(); ++j) job_inflight_[j] = 0;
 }
 
-Id LeaderService::pick_target(const std::vector<Id>& pool) {
+Id LeaderService::pick_target(const std::vector<Id>& all) {
   std::lock_guard<std::mutex> g(rng_mu_);
+  // members benched after a failure sit out unless nobody else is left
+  std::vector<Id> pool;
+  for (const auto& id : all)
+    if (!benched(id.address)) pool.push_back(id);
+  if (pool.empty()) pool = all;
   if (cfg_.adaptive_window <= 0)  // reference: a random member (src/services.rs:414-416)
     return pool[std::uniform_int_distribution<size_t>(0, pool.size() - 1)(rng_)];
   // least outstanding queries; ties broken at random so load spreads evenly
@@ -63,7 +69,13 @@ void LeaderService::stop() {
     for (auto& t : runners_)
       if (t.joinable()) t.join();
   }
-  while (inflight_.load() > 0) std::this_thread::sleep_for(std::chrono::milliseconds(5));
+  {
+    std::lock_guard<std::mutex> g(pool_mu_);
+    pool_stop_ = true;
+  }
+  pool_cv_.notify_all();
+  for (auto& t : workers_)
+    if (t.joinable()) t.join();
   if (server_) server_->stop();
 }
 
@@ -291,18 +303,100 @@ std::vector<Job> LeaderService::jobs() const {
   return jobs_;
 }
 
+// Fixed pool of query workers (instead of one detached thread per query).
+void LeaderService::submit(std::function<void()> task) {
+  std::unique_lock<std::mutex> g(pool_mu_);
+  if (workers_.empty()) {
+    const int n = std::max(1, std::min(cfg_.max_inflight, 256));
+    for (int i = 0; i < n; ++i)
+      workers_.emplace_back([this] {
+        for (;;) {
+          std::function<void()> t;
+          {
+            std::unique_lock<std::mutex> lk(pool_mu_);
+            pool_cv_.wait(lk, [&] { return pool_stop_ || !tasks_.empty(); });
+            if (tasks_.empty()) return;  // stopping and drained
+            t = std::move(tasks_.front());
+            tasks_.pop_front();
+          }
+          t();
+        }
+      });
+  }
+  tasks_.push_back(std::move(task));
+  pool_cv_.notify_one();
+}
+
+bool LeaderService::benched(const std::string& addr) {  // under rng_mu_
+  auto it = bench_until_.find(addr);
+  if (it == bench_until_.end()) return false;
+  if (steady_us() >= it->second) {
+    bench_until_.erase(it);
+    return false;
+  }
+  return true;
+}
+
+std::optional<Id> LeaderService::retry_target(size_t j, const std::set<std::string>& tried) {
+  std::vector<Id> pool;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    pool = jobs_[j].assigned;  // the job's own members first
+  }
+  for (int pass = 0; pass < 2; ++pass) {
+    if (pass == 1) {
+      auto a = ms_->active_ids();
+      pool.assign(a.begin(), a.end());
+    }
+    std::vector<Id> cand;
+    {
+      std::lock_guard<std::mutex> g(rng_mu_);
+      for (const auto& id : pool)
+        if (!tried.count(id.address) && !benched(id.address)) cand.push_back(id);
+    }
+    if (!cand.empty()) return pick_target(cand);
+  }
+  return std::nullopt;
+}
+
 void LeaderService::run_job(size_t j) {
   std::string model;
   size_t idx;
+  int64_t elapsed0;
   {
     std::lock_guard<std::mutex> g(mu_);
     model = jobs_[j].model_name;
     idx = (size_t)jobs_[j].finished;  // resume point (src/services.rs:410-411)
+    elapsed0 = jobs_[j].elapsed_us;
+    retry_[j].clear();
   }
+  const int64_t run0 = steady_us();
   const auto& L = labels_.entries;
   const size_t limit = cfg_.job_limit > 0 ? std::min(L.size(), (size_t)cfg_.job_limit) : L.size();
   auto next_tick = std::chrono::steady_clock::now();
-  while (idx < limit && !stop_.load()) {
+  for (;;) {
+    if (stop_.load()) break;
+    std::pair<size_t, size_t> range{0, 0};  // (first, n): a failed query again, else the next labels
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      if (!retry_[j].empty()) {
+        range = retry_[j].front();
+        retry_[j].pop_front();
+      }
+    }
+    if (range.second == 0) {
+      if (idx >= limit) {
+        // all issued: wait for the stragglers, which may hand a query back
+        if (job_inflight_[j].load() == 0) {
+          std::lock_guard<std::mutex> g(mu_);
+          if (retry_[j].empty()) break;
+        }
+        std::this_thread::sleep_for(std::chrono::milliseconds(1));
+        continue;
+      }
+      range = {idx, std::min((size_t)cfg_.query_batch, limit - idx)};
+      idx += range.second;
+    }
     if (cfg_.adaptive_window <= 0) {
       next_tick += std::chrono::milliseconds(cfg_.query_interval_ms);
       std::this_thread::sleep_until(next_tick);
@@ -318,6 +412,8 @@ void LeaderService::run_job(size_t j) {
       pool.assign(a.begin(), a.end());
     }
     if (pool.empty()) {
+      std::lock_guard<std::mutex> g(mu_);
+      retry_[j].push_front(range);
       if (cfg_.adaptive_window > 0) std::this_thread::sleep_for(std::chrono::milliseconds(50));
       continue;
     }
@@ -331,9 +427,6 @@ void LeaderService::run_job(size_t j) {
     const Id target = pick_target(pool);
     while (inflight_.load() >= cfg_.max_inflight && !stop_.load())
       std::this_thread::sleep_for(std::chrono::microseconds(200));
-    const size_t n = std::min((size_t)cfg_.query_batch, limit - idx);
-    const size_t first = idx;
-    idx += n;
     {
       std::lock_guard<std::mutex> g(mu_);
       if (jobs_[j].started_us == 0) jobs_[j].started_us = wall_us();
@@ -344,75 +437,99 @@ void LeaderService::run_job(size_t j) {
       std::lock_guard<std::mutex> g(rng_mu_);
       member_inflight_[target.address]++;
     }
-    std::thread([this, j, model, target, first, n] {
-      const auto& L = labels_.entries;
-      Writer w;
-      w.str(model).u32((uint32_t)n);
-      for (size_t i = 0; i < n; ++i) w.str(L[first + i].first);
-      const int64_t t0 = steady_us();
-      // A query whose member died is retried on another live member (the
-      // reference dropped it); latency is end to end, retries included.
-      Id tgt = target;
-      std::string resp;
-      bool sent = false;
-      DMLC_TRACE("leader.query");
-      for (int attempt = 0; attempt < 4 && !stop_.load(); ++attempt) {
-        try {
-          resp = RpcClient::shared().call(tgt.host(), member_port(tgt.port()), M_PREDICT, w.data(), 120000);
-          sent = true;
-          break;
-        } catch (const std::exception& e) {
-          DMLC_LOG_WARN("predict " << model << " on " << tgt.address << " failed: " << e.what());
-          std::this_thread::sleep_for(std::chrono::milliseconds(std::min(cfg_.bg_ms, 1000)));
-          auto act = ms_->active_ids();
-          act.erase(tgt);
-          if (act.empty()) break;
-          std::lock_guard<std::mutex> g(rng_mu_);
-          auto it = act.begin();
-          std::advance(it, std::uniform_int_distribution<size_t>(0, act.size() - 1)(rng_));
-          tgt = *it;
-        }
-      }
-      try {
-        if (!sent) throw std::runtime_error("no live member answered");
-        const int64_t dur = steady_us() - t0;
-        Reader r(resp);
-        if (r.boolean()) {
-          const uint32_t m = r.u32();
-          std::vector<std::string> lines;
-          {
-            std::lock_guard<std::mutex> g(mu_);
-            const int64_t now = wall_us();
-            if (jobs_[j].first_done_us == 0) jobs_[j].first_done_us = now;
-            for (uint32_t i = 0; i < m && i < n; ++i) {
-              const double p = r.f64();
-              const std::string label = r.str();
-              const std::string& truth = L[first + i].second;
-              const bool ok = label == truth;
-              jobs_[j].add_result(ok, dur, now);
-              if (cfg_.print_predictions) {
-                char buf[64];
-                snprintf(buf, sizeof(buf), " (%.2f%%)", p * 100.0);
-                lines.push_back(model + " - " + L[first + i].first + ": " + label + buf +
-                                (ok ? "" : " (should be " + truth + ")"));
-              }
-            }
-          }
-          for (const auto& s : lines) out_line(s);
-        }
-      } catch (const std::exception& e) {
-        DMLC_LOG_WARN("predict " << model << " on " << target.address << " failed: " << e.what());
-      }
-      {
-        std::lock_guard<std::mutex> g(rng_mu_);
-        if (--member_inflight_[target.address] <= 0) member_inflight_.erase(target.address);
-      }
-      job_inflight_[j]--;
-      inflight_--;
-    }).detach();
+    submit([this, j, model, target, range, run0, elapsed0] { query(j, model, target, range.first, range.second, run0, elapsed0); });
   }
   std::lock_guard<std::mutex> g(mu_);
   running_[j] = false;
+}
+
+// One query (a batch of `n` labels from `first`). A member that fails (no
+// answer, or ok=false: e.g. it has no such model) is benched for a
+// background period and the query moves to another member of the job's
+// pool (then any live member), with its in-flight count; latency is end to
+// end, retries included. A query no member could answer goes back to the job.
+void LeaderService::query(size_t j, const std::string& model, Id target, size_t first, size_t n, int64_t run0,
+                          int64_t elapsed0) {
+  const auto& L = labels_.entries;
+  Writer w;
+  w.str(model).u32((uint32_t)n);
+  for (size_t i = 0; i < n; ++i) w.str(L[first + i].first);
+  const int64_t t0 = steady_us();
+  Id tgt = target;
+  std::vector<std::pair<double, std::string>> res;
+  bool got = false;
+  std::set<std::string> tried;
+  DMLC_TRACE("leader.query");
+  for (int attempt = 0; attempt < 4 && !stop_.load(); ++attempt) {
+    bool transport = false;
+    std::string why;
+    try {
+      const std::string resp = RpcClient::shared().call(tgt.host(), member_port(tgt.port()), M_PREDICT, w.data(), 120000);
+      Reader r(resp);
+      if (r.boolean()) {
+        const uint32_t m = r.u32();
+        for (uint32_t i = 0; i < m; ++i) {
+          const double p = r.f64();
+          res.emplace_back(p, r.str());
+        }
+        got = true;
+        break;
+      }
+      why = "cannot serve " + model;
+    } catch (const std::exception& e) {
+      transport = true;
+      why = e.what();
+    }
+    DMLC_LOG_WARN("predict " << model << " on " << tgt.address << " failed: " << why << "; benched");
+    tried.insert(tgt.address);
+    {
+      std::lock_guard<std::mutex> g(rng_mu_);
+      bench_until_[tgt.address] = steady_us() + (int64_t)cfg_.bg_ms * 1000;
+    }
+    if (transport) std::this_thread::sleep_for(std::chrono::milliseconds(std::min(cfg_.bg_ms, 200)));
+    auto next = retry_target(j, tried);
+    if (!next) break;
+    {
+      std::lock_guard<std::mutex> g(rng_mu_);
+      if (--member_inflight_[tgt.address] <= 0) member_inflight_.erase(tgt.address);
+      member_inflight_[next->address]++;
+    }
+    tgt = *next;
+  }
+  const int64_t dur = steady_us() - t0;
+  std::vector<std::string> lines;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (got) {
+      const int64_t now = wall_us();
+      if (jobs_[j].first_done_us == 0) jobs_[j].first_done_us = now;
+      for (size_t i = 0; i < n; ++i) {
+        const std::string& truth = L[first + i].second;
+        const bool have = i < res.size() && res[i].first >= 0;
+        const bool ok = have && res[i].second == truth;
+        jobs_[j].add_result(ok, dur, now);
+        if (!have) {
+          lines.push_back(model + " - " + L[first + i].first + ": no image");
+        } else if (cfg_.print_predictions) {
+          char buf[64];
+          snprintf(buf, sizeof(buf), " (%.2f%%)", res[i].first * 100.0);
+          lines.push_back(model + " - " + L[first + i].first + ": " + res[i].second + buf +
+                          (ok ? "" : " (should be " + truth + ")"));
+        }
+      }
+      jobs_[j].elapsed_us = std::max(jobs_[j].elapsed_us, elapsed0 + (steady_us() - run0));
+    } else {
+      retry_[j].push_back({first, n});
+    }
+  }
+  if (!got) DMLC_LOG_WARN("predict " << model << " " << L[first].first << "+" << n << ": no member answered; requeued");
+  for (const auto& l : lines) out_line(l);
+  {
+    std::lock_guard<std::mutex> g(rng_mu_);
+    if (--member_inflight_[tgt.address] <= 0) member_inflight_.erase(tgt.address);
+  }
+  job_inflight_[j]--;
+  inflight_--;
 }
 
 void LeaderService::rereplicate_loop() {
@@ -459,15 +576,30 @@ void LeaderService::succession_loop() {
       if (resume) predict();
     } else if (leader != self_) {
       try {  // standby: copy job progress AND the SDFS directory from the leader
+        // incremental: only the queries completed since the last copy move
+        // (the per-query vectors grow with every query; re-sending them all
+        // each period made the copy cost grow with the job)
+        Writer req;
+        {
+          std::lock_guard<std::mutex> g(mu_);
+          req.u32((uint32_t)jobs_.size());
+          for (const auto& j : jobs_) req.u32((uint32_t)std::min(j.durations_us.size(), j.done_us.size()));
+        }
         const std::string resp =
-            RpcClient::shared().call(host_of(leader), leader_port(port_of(leader)), L_STATE, "", 5000);
+            RpcClient::shared().call(host_of(leader), leader_port(port_of(leader)), L_STATE, req.data(), 5000);
         Reader r(resp);
-        std::vector<Job> js;
         const uint32_t nj = r.u32();
-        for (uint32_t i = 0; i < nj; ++i) js.push_back(read_job(r));
-        Directory d = read_directory(r);
         std::lock_guard<std::mutex> g(mu_);
-        if (js.size() == jobs_.size()) jobs_ = js;
+        std::vector<Job> js = jobs_;
+        bool aligned = nj == js.size();
+        for (uint32_t i = 0; i < nj; ++i) {
+          Job tmp;
+          Job& dst = aligned ? js[i] : tmp;
+          if (!read_job_delta(r, dst)) aligned = false;
+        }
+        Directory d = read_directory(r);
+        if (aligned) jobs_ = std::move(js);
+        else for (auto& j : jobs_) j.durations_us.clear(), j.done_us.clear();  // full copy next time
         dir_ = std::move(d);
       } catch (const std::exception&) {
       }
@@ -548,11 +680,16 @@ void LeaderService::register_handlers() {
     for (const auto& j : js) write_job(w, j);
     return w.take();
   });
-  server_->handle(L_STATE, [this](Reader&) {
+  server_->handle(L_STATE, [this](Reader& r) {
+    std::vector<uint32_t> have;
+    if (r.left() >= 4) {
+      const uint32_t n = r.u32();
+      for (uint32_t i = 0; i < n; ++i) have.push_back(r.u32());
+    }
     Writer w;
     std::lock_guard<std::mutex> g(mu_);
     w.u32((uint32_t)jobs_.size());
-    for (const auto& j : jobs_) write_job(w, j);
+    for (size_t i = 0; i < jobs_.size(); ++i) write_job_delta(w, jobs_[i], i < have.size() ? have[i] : 0);
     write_directory(w, dir_);
     return w.take();
   });

@@ -21,6 +21,8 @@
 #pragma once
 #include <atomic>
 #include <condition_variable>
+#include <deque>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -101,6 +103,17 @@ class LeaderService {
   std::unique_ptr<std::atomic<int>[]> job_inflight_;  // per job (adaptive window)
   std::map<std::string, int> member_inflight_;         // per member address, under rng_mu_
   Id pick_target(const std::vector<Id>& pool);
+  bool benched(const std::string& addr);  // under rng_mu_
+  std::optional<Id> retry_target(size_t j, const std::set<std::string>& tried);
+  void query(size_t j, const std::string& model, Id target, size_t first, size_t n, int64_t run0, int64_t elapsed0);
+  void submit(std::function<void()> task);
+  std::map<std::string, int64_t> bench_until_;          // member -> steady us, under rng_mu_
+  std::vector<std::deque<std::pair<size_t, size_t>>> retry_;  // per job: queries handed back, under mu_
+  std::mutex pool_mu_;
+  std::condition_variable pool_cv_;
+  std::deque<std::function<void()>> tasks_;
+  std::vector<std::thread> workers_;
+  bool pool_stop_ = false;
   std::mutex rng_mu_;
   std::mt19937_64 rng_{std::random_device{}()};
 };

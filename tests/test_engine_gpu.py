@@ -186,3 +186,35 @@ def test_fast_paths_match_plain_paths_odd_batches(gpu, monkeypatch, B):
     torch.cuda.synchronize()
     rel = ((lg - rl).norm() / rl.norm()).item()
     assert rel < 1e-3, rel
+
+
+def test_bench_path_b256_matches_fp32(gpu):
+    """The exact bench.py configuration — ResNet18, B=256, default kernel
+    selection, hipGraph replay, driven by the native DP runner
+    (csrc/comm/dp.cpp) — against fp32 torch.nn: top-1 identical except on
+    near-ties, probabilities within bf16 tolerance, logits (same fast paths
+    with the logits output) within 3% relative L2."""
+    import dmlc
+    torch.set_num_threads(min(16, torch.get_num_threads()))
+    model = build("resnet18", seed=21, randomize_bn=True)
+    eng = InferenceEngine("resnet18", state_dict_f32(model), max_batch=256)
+    g = torch.Generator().manual_seed(22)
+    img = torch.randint(0, 256, (256, 224, 224, 3), generator=g, dtype=torch.uint8)
+    pool = img.to(gpu)
+    torch.cuda.synchronize()
+    r = dmlc.native().DpRunner(eng._e, 1, 0, b"", b"", 256)
+    r.run(pool.data_ptr(), 256, 0, 3)
+    r.sync()
+    idx, prob = r.last_results()
+    idx, prob = torch.tensor(idx), torch.tensor(prob)
+    ref = _ref_logits(model, img)
+    ref_p = torch.softmax(ref, -1)
+    top2 = ref_p.topk(2, -1).values
+    near_tie = (top2[:, 0] - top2[:, 1]) < 1e-2
+    mism = idx.long() != ref.argmax(-1)
+    assert torch.all(~mism | near_tie), mism.sum().item()
+    assert torch.allclose(prob, ref_p.max(-1).values, rtol=0.1, atol=2e-3)
+    _, _, logits = eng.predict(pool, return_logits=True)
+    torch.cuda.synchronize()
+    rel = ((logits.cpu() - ref).norm() / ref.norm()).item()
+    assert rel < 3e-2, rel

@@ -127,7 +127,7 @@ def build(jobs: int = 8, verbose: bool = False, node: bool = True) -> None:
     ctl_srcs = sorted(glob.glob(os.path.join(CSRC, "control", "*.cpp")) +
                       glob.glob(os.path.join(CSRC, "serve", "*.cpp")) +
                       glob.glob(os.path.join(CSRC, "cli", "*.cpp")))
-    node_srcs = [s for s in ctl_srcs if not s.endswith("executor_stub.cpp")] if node else []
+    node_srcs = [s for s in ctl_srcs if not s.endswith(("executor_stub.cpp", "fuzz.cpp"))] if node else []
     node_objs = []
     for s in node_srcs:
         o = os.path.join(OBJ, os.path.relpath(s, CSRC).replace(os.sep, "_") + ".o")
@@ -138,7 +138,7 @@ def build(jobs: int = 8, verbose: bool = False, node: bool = True) -> None:
     # ---- 4. ThreadSanitizer build of the control plane (no torch / HIP)
     tsan_objs = []
     if node:
-        tsan_srcs = [s for s in ctl_srcs if not s.endswith("executor.cpp")]
+        tsan_srcs = [s for s in ctl_srcs if not s.endswith(("executor.cpp", "fuzz.cpp"))]
         tsan_srcs.append(os.path.join(CSRC, "runtime", "jpeg.cpp"))
         for s in tsan_srcs:
             o = os.path.join(OBJ, "tsan_" + os.path.relpath(s, CSRC).replace(os.sep, "_") + ".o")
@@ -147,8 +147,32 @@ def build(jobs: int = 8, verbose: bool = False, node: bool = True) -> None:
                 steps.append(["g++", "-O1", "-g", "-std=c++17", "-fPIC", "-fsanitize=thread", "-pthread",
                               "-DDMLC_NO_ROCTX", "-c", s, "-o", o])
 
+    # ---- 5. AddressSanitizer + UBSan builds: the node (same sources as the
+    # TSan build) and the parser fuzzer (csrc/cli/fuzz.cpp)
+    asan_flags = ["-O1", "-g", "-std=c++17", "-fPIC", "-fsanitize=address,undefined",
+                  "-fno-sanitize-recover=undefined", "-fno-omit-frame-pointer", "-pthread", "-DDMLC_NO_ROCTX"]
+    asan_objs, fuzz_objs = [], []
+    if node:
+        asan_srcs = [s for s in ctl_srcs if not s.endswith("executor.cpp")] + [os.path.join(CSRC, "runtime", "jpeg.cpp")]
+        for s in asan_srcs:
+            o = os.path.join(OBJ, "asan_" + os.path.relpath(s, CSRC).replace(os.sep, "_") + ".o")
+            if _stale(o, [s], hdr):
+                steps.append(["g++", *asan_flags, "-c", s, "-o", o])
+            if s.endswith("fuzz.cpp"):
+                fuzz_objs.append(o)
+                continue
+            asan_objs.append(o)
+            if not s.endswith(("main.cpp", "selftest.cpp")) and "serve" + os.sep + "executor" not in s \
+                    and "control" + os.sep + "member.cpp" not in s and "serve" + os.sep + "leader.cpp" not in s:
+                fuzz_objs.append(o)
+        tsan_objs = [o for o in tsan_objs if not o.endswith("cli_fuzz.cpp.o")]
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         list(ex.map(lambda c: _run(c, verbose), steps))
+    if asan_objs:
+        for exe, objs in ((os.path.join(BIN, "dmlc-node-asan"), asan_objs),
+                          (os.path.join(BIN, "dmlc-fuzz-asan"), fuzz_objs)):
+            if _stale(exe, objs, 0):
+                _run(["g++", "-fsanitize=address,undefined", "-pthread", *objs, "-o", exe], verbose)
     if tsan_objs:
         tsan_exe = os.path.join(BIN, "dmlc-node-tsan")
         if _stale(tsan_exe, tsan_objs, 0):
