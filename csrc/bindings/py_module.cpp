@@ -195,6 +195,15 @@ PYBIND11_MODULE(_C, m) {
   m.def("mfma_fp8_probe", [](uintptr_t a, uintptr_t b, uintptr_t d, uintptr_t stream) {
     mfma_fp8_probe(P<void>(a), P<void>(b), P<float>(d), S(stream));
   });
+  m.def("head_ws_bytes", &head_ws_bytes);
+  m.def("head_pooled", [](uintptr_t pooled, uintptr_t w, uintptr_t bias, int B, int C, int N, int ldw, int Npad,
+                          uintptr_t logits, uintptr_t idx, uintptr_t prob, uintptr_t ws, size_t ws_bytes, int num_cus,
+                          uintptr_t stream, int ns, int ko) {
+    head_pooled(P<float>(pooled), P<void>(w), P<float>(bias), B, C, N, ldw, Npad, P<float>(logits), P<int32_t>(idx),
+                P<float>(prob), P<void>(ws), ws_bytes, num_cus, S(stream), ns, ko);
+  }, py::arg("pooled"), py::arg("w"), py::arg("bias"), py::arg("B"), py::arg("C"), py::arg("N"), py::arg("ldw"),
+        py::arg("Npad"), py::arg("logits"), py::arg("idx"), py::arg("prob"), py::arg("ws"), py::arg("ws_bytes"),
+        py::arg("num_cus"), py::arg("stream"), py::arg("ns") = 0, py::arg("ko") = 0);
   m.def("softmax_top1", [](uintptr_t logits, int B, int N, int ld, uintptr_t idx, uintptr_t prob,
                            uintptr_t stream) {
     softmax_top1(P<float>(logits), B, N, ld, P<int32_t>(idx), P<float>(prob), S(stream));

@@ -67,6 +67,11 @@ struct StreamConvArgs {
   int B;
   int relu;
   unsigned long long* stamps;  // debug: per-workgroup phase stamps (100 MHz), or null
+  // Fused global average pool (whole-image workgroups only): pool[b][c] =
+  // mean over the image's pixels of the (post-ReLU) output; with store_y = 0
+  // the activation itself is not written (nothing else reads it).
+  float* pool;
+  int store_y;
 };
 
 // Weight-row permutation inside a wave's 32-row tile: row n = 16nf + r holds
@@ -438,6 +443,13 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream_kernel(StreamConvArgs a
       rv[f] = *(const uint4*)(a.res + base + (long)p * CO);
     }
   }
+  // fused avgpool: per-lane sums per image of the workgroup (PARTS == 1)
+  constexpr int PIMG = G::PARTS == 1 ? IMG : 1;
+  float psum[PIMG][8];
+#pragma unroll
+  for (int i = 0; i < PIMG; ++i)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) psum[i][e] = 0.f;
 #pragma unroll
   for (int f = 0; f < MF; ++f) {
     const int p = 16 * (wm * MF + f) + fr;
@@ -459,7 +471,45 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream_kernel(StreamConvArgs a
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
     }
-    *(uint4*)(a.y + off) = pack8(v);
+    const uint4 packed = pack8(v);
+    if (a.store_y) *(uint4*)(a.y + off) = packed;
+    if constexpr (G::PARTS == 1) {
+      if (a.pool) {  // the bf16 activation's values, as the unfused avgpool reads them
+        float q[8];
+        unpack8(packed, q);
+        const int im = PIMG == 1 ? 0 : p / (H * W);
+#pragma unroll
+        for (int i = 0; i < PIMG; ++i)
+          if (i == im)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) psum[i][e] += q[e];
+      }
+    }
+  }
+  if constexpr (G::PARTS == 1) {
+    if (a.pool) {  // reduce over the 16 pixel lanes fr of each channel group fq
+#pragma unroll
+      for (int i = 0; i < PIMG; ++i)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float t = psum[i][e];
+          t += __shfl_xor(t, 8, 64);
+          t += __shfl_xor(t, 4, 64);
+          t += __shfl_xor(t, 2, 64);
+          t += __shfl_xor(t, 1, 64);
+          psum[i][e] = t * (1.f / (H * W));
+        }
+      if (fr == 0 && (WM == 1 || wm == 0)) {
+        static_assert(G::PARTS != 1 || WM == 1, "fused pool: one pixel group per wave");
+#pragma unroll
+        for (int i = 0; i < PIMG; ++i)
+          if (i < nimg) {
+            float* dst = a.pool + (long)(b + i) * CO + ch0 + 8 * fq;
+            *(float4*)dst = make_float4(psum[i][0], psum[i][1], psum[i][2], psum[i][3]);
+            *(float4*)(dst + 4) = make_float4(psum[i][4], psum[i][5], psum[i][6], psum[i][7]);
+          }
+      }
+    }
   }
   if constexpr (DS) {
     float bd[8];
@@ -519,6 +569,11 @@ void launch_stream(const StreamConvArgs& a, hipStream_t s) {
 
 }  // namespace
 
+// Whole-image workgroups (the fused avgpool): layer4's 7x7x512 stride-1 conv.
+bool conv3x3_stream_pool_supported(int Hin, int Win, int Cin, int Cout, int stride) {
+  return stride == 1 && Hin == 7 && Win == 7 && Cin == 512 && Cout == 512;
+}
+
 bool conv3x3_stream_supported(int Hin, int Win, int Cin, int Cout, int stride) {
   if (stride == 1)
     return Cin == Cout && ((Hin == 28 && Win == 28 && Cin == 128) || (Hin == 14 && Win == 14 && Cin == 256) ||
@@ -547,8 +602,11 @@ bool conv3x3_stream_uses_frag(int Hin, int Win, int Cin, int Cout, int stride) {
 void conv3x3_stream(const void* x, const void* w, const float* bias, const void* res, void* y, const void* zero,
                     int B, int Hin, int Win, int Cin, int Cout, int stride, bool relu, hipStream_t s,
                     unsigned long long* stamps, const void* wd, const float* bd, void* yd, const void* wfrag,
-                    const void* wdfrag) {
+                    const void* wdfrag, float* pool, bool store_y) {
   if (B <= 0) return;
+  if ((pool || !store_y) && !conv3x3_stream_pool_supported(Hin, Win, Cin, Cout, stride))
+    throw std::invalid_argument("conv3x3_stream: fused avgpool needs whole-image workgroups");
+  if (pool && ((uintptr_t)pool & 15)) throw std::invalid_argument("conv3x3_stream: misaligned pool");
   if (!conv3x3_stream_supported(Hin, Win, Cin, Cout, stride))
     throw std::invalid_argument("conv3x3_stream: unsupported shape");
   if (!x || !w || !bias || !y || !zero ||
@@ -569,6 +627,8 @@ void conv3x3_stream(const void* x, const void* w, const float* bias, const void*
   a.yd = (bf16*)yd;
   a.wf = (const bf16*)wfrag;
   a.wdf = (const bf16*)wdfrag;
+  a.pool = pool;
+  a.store_y = store_y ? 1 : 0;
   if (wfrag && (!conv3x3_stream_uses_frag(Hin, Win, Cin, Cout, stride) || ((uintptr_t)wfrag & 15) ||
                 (yd && (!wdfrag || ((uintptr_t)wdfrag & 15)))))
     throw std::invalid_argument("conv3x3_stream: no register-weight variant for this call");

@@ -35,10 +35,12 @@ namespace dmlc {
 
 namespace {
 
-constexpr int kIPW = 4;  // images per workgroup (one wave each in the softmax)
+constexpr int kIPW = 4;         // images per workgroup, pooling in the kernel (one wave each in the softmax)
+constexpr int kIPWPooled = 16;  // images per workgroup on a pooled input (all 16 MFMA columns)
 
 struct HeadArgs {
   const bf16* x;      // [B, HW, C]
+  const float* pooled;  // POOLED: [B, C] fp32
   const bf16* w;      // [Npad, ldw]
   const float* bias;  // [Npad]
   float* logits;      // [B, N]
@@ -64,9 +66,10 @@ __device__ __forceinline__ float tree_sum(const float* v, int n) {
   return t[0];
 }
 
-template <int TPG>
+template <int TPG, int IPW, bool POOLED>
 __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  constexpr int kIPW = IPW;
   const int C = a.C;
   const int ldp = C + 8;  // pooled row stride (elements): rows 16 B apart in bank space
   bf16* pooled = (bf16*)smem;                                // [kIPW][ldp]
@@ -76,6 +79,18 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int b0 = g * kIPW;
   const int nimg = min(kIPW, a.B - b0);
+  if constexpr (POOLED) {  // the last conv already pooled: fp32 [B, C] -> bf16 rows in LDS
+    const int c8 = C / 8;
+    for (int it = tid; it < nimg * c8; it += 256) {
+      const int i = it / c8, cg = it - i * c8;
+      const float* src = a.pooled + (long)(b0 + i) * C + cg * 8;
+      float v[8];
+      *(float4*)v = *(const float4*)src;
+      *(float4*)(v + 4) = *(const float4*)(src + 4);
+      *(uint4*)(pooled + i * ldp + cg * 8) = pack8(v);
+    }
+    __syncthreads();
+  } else {
 
   // ---- 1. average pool. avgpool_global's arithmetic: part p (0..7) of a
   // channel group sums pixels p, p+8, ... in order; the 8 parts combine in
@@ -140,6 +155,7 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
     *(uint4*)(pooled + i * ldp + cg * 8) = pack8(s);
   }
   __syncthreads();
+  }  // !POOLED
 
   // ---- 2./3. fc tiles on MFMA: lane holds D[class row (lane>>4)*4 + r][image lane&15].
   // K in chunks of 512: the chunk's 16 pooled fragments are read once from
@@ -205,7 +221,8 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
 
   // per image (one wave each): this split's max / argmax / sum exp
   const int n_end = min(a.N, n_begin + nsplit);
-  if (wave < nimg) {
+  for (int im = wave; im < nimg; im += 4) {  // 4 waves
+    const int wave = im;  // image handled by this wave in this round
     float best = -INFINITY;
     int bi = 0x7fffffff;
     for (int n = n_begin + lane; n < n_end; n += 64) {
@@ -232,7 +249,7 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
         a.idx[b0 + wave] = bi;
         a.prob[b0 + wave] = 1.f / s;
       }
-      return;
+      continue;
     }
     if (lane == 0) {  // relaxed agent-scope atomic stores = sc1 write-through: no release fence needed
       float* q = (float*)(a.part + (long)(b0 + wave) * a.NS + split);
@@ -254,7 +271,9 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
     *flag = last;
   }
   __syncthreads();
-  if (!*flag || wave >= nimg) return;
+  if (!*flag) return;
+  for (int im = wave; im < nimg; im += 4) {  // 4 waves
+  const int wave = im;
   float m = -INFINITY, sum = 0.f;
   int bi = 0x7fffffff;
   const float4* p = a.part + (long)(b0 + wave) * a.NS;
@@ -278,17 +297,20 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
     a.idx[b0 + wave] = bi;
     a.prob[b0 + wave] = 1.f / sum;
   }
+  }
 }
 
 }  // namespace
 
-int head_splits(int B, int N, int num_cus) {
-  const int groups = (B + kIPW - 1) / kIPW;
+int head_splits_ipw(int B, int N, int num_cus, int ipw) {
+  const int groups = (B + ipw - 1) / ipw;
   const int tiles = (N + 15) / 16;
   int ns = 1;
   while (ns < 8 && (long)groups * ns * 2 <= num_cus && tiles / (ns * 2) >= 4) ns *= 2;
   return ns;
 }
+
+int head_splits(int B, int N, int num_cus) { return head_splits_ipw(B, N, num_cus, kIPW); }
 
 size_t head_ws_bytes(int max_batch) {
   // partials for up to 8 splits, then the group counters at the very end
@@ -334,11 +356,48 @@ void head_fused(const void* x, const void* w, const float* bias, int B, int HW, 
                      std::max((size_t)kIPW * a.tiles_per_split * 16 * 4, (size_t)tpg * kIPW * C * 4);
   if (lds > 160 * 1024) throw std::invalid_argument("head_fused: LDS budget exceeded");
   switch (tpg) {
-    case 1: hipLaunchKernelGGL(head_kernel<1>, dim3(groups, ns), dim3(256), lds, s, a); break;
-    case 2: hipLaunchKernelGGL(head_kernel<2>, dim3(groups, ns), dim3(256), lds, s, a); break;
-    case 4: hipLaunchKernelGGL(head_kernel<4>, dim3(groups, ns), dim3(256), lds, s, a); break;
-    default: hipLaunchKernelGGL(head_kernel<8>, dim3(groups, ns), dim3(256), lds, s, a); break;
+    case 1: hipLaunchKernelGGL((head_kernel<1, kIPW, false>), dim3(groups, ns), dim3(256), lds, s, a); break;
+    case 2: hipLaunchKernelGGL((head_kernel<2, kIPW, false>), dim3(groups, ns), dim3(256), lds, s, a); break;
+    case 4: hipLaunchKernelGGL((head_kernel<4, kIPW, false>), dim3(groups, ns), dim3(256), lds, s, a); break;
+    default: hipLaunchKernelGGL((head_kernel<8, kIPW, false>), dim3(groups, ns), dim3(256), lds, s, a); break;
   }
+  DMLC_HIP_CHECK(hipGetLastError());
+}
+
+void head_pooled(const float* pooled, const void* w, const float* bias, int B, int C, int N, int ldw, int Npad,
+                 float* logits, int32_t* idx, float* prob, void* ws, size_t ws_bytes, int num_cus, hipStream_t s,
+                 int ns_override, int ko) {
+  if (B <= 0) return;
+  if (!head_supported(C, N, ldw, Npad) || C % 8) throw std::invalid_argument("head_pooled: unsupported C/N/ldw");
+  if (!pooled || !w || !bias || !logits || !idx || !prob || !ws || ((uintptr_t)pooled & 15))
+    throw std::invalid_argument("head_pooled: null / misaligned pointer");
+  constexpr int ipw = kIPWPooled;
+  const int groups = (B + ipw - 1) / ipw;
+  const int tiles = (N + 15) / 16;
+  const int ns = ns_override > 0 ? std::min(ns_override, 8) : head_splits_ipw(B, N, num_cus, ipw);
+  const size_t part_bytes = (size_t)B * ns * sizeof(float4);
+  if (part_bytes + groups * sizeof(uint32_t) > ws_bytes) throw std::invalid_argument("head_pooled: workspace too small");
+  HeadArgs a;
+  a.x = nullptr;
+  a.pooled = pooled;
+  a.w = (const bf16*)w;
+  a.bias = bias;
+  a.logits = logits;
+  a.idx = idx;
+  a.prob = prob;
+  a.NS = ns;
+  a.tiles_per_split = (tiles + ns - 1) / ns;
+  a.part = (float4*)ws;
+  a.cnt = (uint32_t*)((uint8_t*)ws + ws_bytes) - groups;
+  a.B = B;
+  a.HW = 1;
+  a.C = C;
+  a.N = N;
+  a.ldw = ldw;
+  a.ko = ko;
+  const size_t lds = (size_t)ipw * (C + 8) * 2 + (size_t)ipw * a.tiles_per_split * 16 * 4;
+  if (lds > 160 * 1024) throw std::invalid_argument("head_pooled: LDS budget exceeded");
+  hipLaunchKernelGGL((head_kernel<1, kIPWPooled, true>), dim3(groups, ns), dim3(256), lds, s, a);
   DMLC_HIP_CHECK(hipGetLastError());
 }
 

@@ -88,6 +88,7 @@ Engine::Engine(const std::string& arch, const WeightMap& weights, int device, in
   if (const char* e = std::getenv("DMLC_STREAM_CONV")) stream_conv_ = std::string(e) != "0";
   if (const char* e = std::getenv("DMLC_FORK_DS")) fork_ds_ = std::string(e) != "0";
   if (const char* e = std::getenv("DMLC_FUSED_HEAD")) fused_head_ = std::string(e) != "0";
+  if (const char* e = std::getenv("DMLC_FUSED_POOL")) fused_pool_ = std::string(e) != "0";
   if (const char* e = std::getenv("DMLC_FUSE_DS")) fuse_ds_ = std::string(e) != "0";
   if (const char* e = std::getenv("DMLC_STREAM_L4S2")) stream_l4s2_ = std::string(e) != "0";
   if (const char* e = std::getenv("DMLC_STREAM_L1")) stream_l1_ = std::string(e) != "0";
@@ -140,6 +141,7 @@ Engine::~Engine() {
   if (zero_) hipFree(zero_);
   if (dummy_idx_) hipFree(dummy_idx_);
   if (head_ws_) hipFree(head_ws_);
+  if (pooled_) hipFree(pooled_);
   if (ev_in_) hipEventDestroy(ev_in_);
   if (ev_out_) hipEventDestroy(ev_out_);
   for (auto e : fork_evs_) hipEventDestroy(e);
@@ -500,6 +502,13 @@ void Engine::reserve(int max_batch) {
   head_ws_bytes_ = head_ws_bytes(max_batch);
   DMLC_HIP_CHECK(hipMalloc(&head_ws_, head_ws_bytes_));
   DMLC_HIP_CHECK(hipMemset(head_ws_, 0, head_ws_bytes_));
+  // the last conv's fused global average pool: fp32 [max_batch, C]
+  if (pooled_) DMLC_HIP_CHECK(hipFree(pooled_));
+  pooled_ = nullptr;
+  int pool_c = 0;
+  for (const Op& op : ops_)
+    if (op.type == OpType::AvgPoolGlobal) pool_c = std::max(pool_c, shapes_[op.in].C);
+  if (pool_c > 0) DMLC_HIP_CHECK(hipMalloc(&pooled_, (size_t)max_batch * pool_c * sizeof(float)));
   // big-tile conv split-K slabs for the largest batch
   long slabs = 0;
   for (const Op& op : ops_) {
@@ -606,6 +615,23 @@ bool Engine::head_fusable(size_t oi) const {
   return L.fc && !L.fp8 && !L.relu && L.cin == shapes_[pool.in].C && head_supported(L.cin, L.cout, L.kpad, L.npad);
 }
 
+// ops[oi] is the last conv (stream path, whole-image workgroups) and
+// ops[oi+1..oi+3] the fusable head reading only its output: the conv's
+// epilogue computes the global average pool and skips storing the
+// activation; the head then starts from the pooled vectors.
+bool Engine::pool_fusable(size_t oi, int B) const {
+  if (!fused_pool_ || !pooled_ || oi + 1 >= ops_.size()) return false;
+  const Op& c = ops_[oi];
+  const Op& p = ops_[oi + 1];
+  if (c.type != OpType::Conv || p.type != OpType::AvgPoolGlobal || p.in != c.out || !head_fusable(oi + 1)) return false;
+  for (size_t j = 0; j < ops_.size(); ++j)
+    if (j != oi + 1 && (ops_[j].in == c.out || ops_[j].res == c.out)) return false;
+  const ConvLayer& L = convs_[c.conv];
+  const ActShape& is = shapes_[c.in];
+  return !L.fp8 && !shapes_[c.out].fp8 && conv_path(c, B) == ConvPath::Stream &&
+         conv3x3_stream_pool_supported(is.H, is.W, is.C, L.cout, L.stride);
+}
+
 // ops[oi] is a block's downsample (1x1/s2, BN, no ReLU) and ops[oi+1] the
 // block's 3x3/s2 conv1 on the same input, run by the stream conv.
 bool Engine::ds_fusable(size_t oi, int B) const {
@@ -635,6 +661,7 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
   std::map<int, hipEvent_t> joined;  // activation -> event its side-stream producer recorded
   int skip = 0;                      // ops already done by a fused kernel
   int skip_ds = -1;                  // downsample op left to the next (stream) conv
+  bool pooled = false;               // the last conv wrote pooled_ (fused avgpool)
   for (size_t oi = 0; oi < ops_.size(); ++oi) {
     const Op& op = ops_[oi];
     if (skip > 0) {
@@ -682,6 +709,9 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
               D = &convs_[ops_[skip_ds].conv];
               yd = ops_[skip_ds].out;
             }
+            // the fused avgpool keeps the activation for eager/profile runs
+            // (tests read it) and drops it under graph capture
+            const bool fpool = cs == s && pool_fusable(oi, B);
             conv3x3_stream(acts_[op.in], (const uint8_t*)warena_ + L.w_off,
                            (const float*)((const uint8_t*)warena_ + L.b_off), op.res >= 0 ? acts_[op.res] : nullptr,
                            acts_[op.out], zero_, B, is.H, is.W, is.C, L.cout, L.stride, L.relu, cs, nullptr,
@@ -690,7 +720,9 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
                            D ? acts_[yd] : nullptr,
                            (L.wf_off && stream_wreg_ && (!D || D->wf_off)) ? (const uint8_t*)warena_ + L.wf_off
                                                                           : nullptr,
-                           (D && D->wf_off && stream_wreg_) ? (const uint8_t*)warena_ + D->wf_off : nullptr);
+                           (D && D->wf_off && stream_wreg_) ? (const uint8_t*)warena_ + D->wf_off : nullptr,
+                           fpool ? (float*)pooled_ : nullptr, !fpool || trace || evs);
+            pooled = fpool;
             skip_ds = -1;
             break;
           }
@@ -746,6 +778,15 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
       }
       case OpType::AvgPoolGlobal: {
         const ActShape& i = shapes_[op.in];
+        if (pooled && head_fusable(oi)) {  // pooled by the last conv: fc + softmax/top-1
+          const ConvLayer& L = convs_[ops_[oi + 1].conv];
+          head_pooled((const float*)pooled_, (const uint8_t*)warena_ + L.w_off,
+                      (const float*)((const uint8_t*)warena_ + L.b_off), B, i.C, L.cout, L.kpad, L.npad,
+                      logits ? logits : (float*)acts_[ops_[oi + 1].out], idx ? idx : dummy_idx_,
+                      prob ? prob : (float*)(dummy_idx_ + max_batch_), head_ws_, head_ws_bytes_, num_cus_, s);
+          skip = 2;
+          break;
+        }
         if (head_fusable(oi)) {  // avgpool + fc + softmax/top-1 in one launch
           const ConvLayer& L = convs_[ops_[oi + 1].conv];
           head_fused(acts_[op.in], (const uint8_t*)warena_ + L.w_off,

@@ -116,6 +116,7 @@ class Engine {
   ConvPath conv_path(const Op& op, int B) const;
   bool side_safe(int B) const;
   bool head_fusable(size_t oi) const;
+  bool pool_fusable(size_t oi, int B) const;
   bool ds_fusable(size_t oi, int B) const;  // ops oi, oi+1 = downsample + stride-2 stream conv1  // ops oi..oi+2 = avgpool, fc, softmax_top1 -> head_fused  // no big-tile (co-residency-dependent) conv at batch B
 
   std::string arch_;
@@ -140,6 +141,8 @@ class Engine {
   bool stream_l4s2_ = true;   // stream conv for 14x14x256 -> 512 / s2, register weights only (env DMLC_STREAM_L4S2=0)
   bool fuse_ds_ = true;     // downsample inside the stride-2 stream conv1 (env DMLC_FUSE_DS=0 disables)
   bool fused_head_ = true;  // avgpool+fc+softmax/top-1 as one kernel (env DMLC_FUSED_HEAD=0 disables)
+  bool fused_pool_ = true;  // the last conv's epilogue computes the avgpool (env DMLC_FUSED_POOL=0 disables)
+  void* pooled_ = nullptr;  // fp32 [max_batch, C] pooled features of the last conv
   // downsample convs on a side stream (env DMLC_FORK_DS=1 enables): measured
   // slower (the branch slows its sibling conv1 by 10-12 us and adds ~10 us of
   // fork/join gaps per block: profiles/r1_fork_ds_timeline.txt)

@@ -218,3 +218,26 @@ def test_bench_path_b256_matches_fp32(gpu):
     torch.cuda.synchronize()
     rel = ((logits.cpu() - ref).norm() / ref.norm()).item()
     assert rel < 3e-2, rel
+
+
+def test_fused_pool_head_matches_unfused(gpu, monkeypatch):
+    """The last conv's fused global average pool + the pooled head (graph
+    path: the layer4 activation is never stored) against the unfused
+    avgpool+fc+softmax head: identical top-1, logits equal within bf16
+    rounding of the pooled vector."""
+    model = build("resnet18", seed=41, randomize_bn=True)
+    sd = state_dict_f32(model)
+    g = torch.Generator().manual_seed(42)
+    img = torch.randint(0, 256, (96, 224, 224, 3), generator=g, dtype=torch.uint8).to(gpu)
+    monkeypatch.setenv("DMLC_FUSED_POOL", "0")
+    ref_eng = InferenceEngine("resnet18", sd, max_batch=96)
+    monkeypatch.setenv("DMLC_FUSED_POOL", "1")
+    eng = InferenceEngine("resnet18", sd, max_batch=96)
+    ri, rp, rl = ref_eng.predict(img, return_logits=True)
+    fi, fp, fl = eng.predict(img, return_logits=True)  # graph replay: activation not stored
+    i2, p2 = eng.predict(img)                           # the bench's graph (no logits output)
+    torch.cuda.synchronize()
+    rel = ((fl - rl).norm() / rl.norm()).item()
+    assert rel < 1e-2, rel
+    assert torch.equal(fi, ri) and torch.equal(i2, ri)
+    assert torch.allclose(fp, rp, rtol=1e-2, atol=1e-4) and torch.allclose(p2, rp, rtol=1e-2, atol=1e-4)
