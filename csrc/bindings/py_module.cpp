@@ -199,7 +199,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("head_pooled", [](uintptr_t pooled, uintptr_t w, uintptr_t bias, int B, int C, int N, int ldw, int Npad,
                           uintptr_t logits, uintptr_t idx, uintptr_t prob, uintptr_t ws, size_t ws_bytes, int num_cus,
                           uintptr_t stream, int ns, int ko) {
-    head_pooled(P<float>(pooled), P<void>(w), P<float>(bias), B, C, N, ldw, Npad, P<float>(logits), P<int32_t>(idx),
+    head_pooled(P<void>(pooled), P<void>(w), P<float>(bias), B, C, N, ldw, Npad, P<float>(logits), P<int32_t>(idx),
                 P<float>(prob), P<void>(ws), ws_bytes, num_cus, S(stream), ns, ko);
   }, py::arg("pooled"), py::arg("w"), py::arg("bias"), py::arg("B"), py::arg("C"), py::arg("N"), py::arg("ldw"),
         py::arg("Npad"), py::arg("logits"), py::arg("idx"), py::arg("prob"), py::arg("ws"), py::arg("ws_bytes"),

@@ -68,9 +68,10 @@ struct StreamConvArgs {
   int relu;
   unsigned long long* stamps;  // debug: per-workgroup phase stamps (100 MHz), or null
   // Fused global average pool (whole-image workgroups only): pool[b][c] =
-  // mean over the image's pixels of the (post-ReLU) output; with store_y = 0
-  // the activation itself is not written (nothing else reads it).
-  float* pool;
+  // mean over the image's pixels of the (post-ReLU) output, bf16 (what the
+  // unfused avgpool kernel writes); with store_y = 0 the activation itself is
+  // not written (nothing else reads it).
+  bf16* pool;
   int store_y;
 };
 
@@ -504,9 +505,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream_kernel(StreamConvArgs a
 #pragma unroll
         for (int i = 0; i < PIMG; ++i)
           if (i < nimg) {
-            float* dst = a.pool + (long)(b + i) * CO + ch0 + 8 * fq;
-            *(float4*)dst = make_float4(psum[i][0], psum[i][1], psum[i][2], psum[i][3]);
-            *(float4*)(dst + 4) = make_float4(psum[i][4], psum[i][5], psum[i][6], psum[i][7]);
+            *(uint4*)(a.pool + (long)(b + i) * CO + ch0 + 8 * fq) = pack8(psum[i]);
           }
       }
     }
@@ -602,7 +601,7 @@ bool conv3x3_stream_uses_frag(int Hin, int Win, int Cin, int Cout, int stride) {
 void conv3x3_stream(const void* x, const void* w, const float* bias, const void* res, void* y, const void* zero,
                     int B, int Hin, int Win, int Cin, int Cout, int stride, bool relu, hipStream_t s,
                     unsigned long long* stamps, const void* wd, const float* bd, void* yd, const void* wfrag,
-                    const void* wdfrag, float* pool, bool store_y) {
+                    const void* wdfrag, void* pool, bool store_y) {
   if (B <= 0) return;
   if ((pool || !store_y) && !conv3x3_stream_pool_supported(Hin, Win, Cin, Cout, stride))
     throw std::invalid_argument("conv3x3_stream: fused avgpool needs whole-image workgroups");
@@ -627,7 +626,7 @@ void conv3x3_stream(const void* x, const void* w, const float* bias, const void*
   a.yd = (bf16*)yd;
   a.wf = (const bf16*)wfrag;
   a.wdf = (const bf16*)wdfrag;
-  a.pool = pool;
+  a.pool = (bf16*)pool;
   a.store_y = store_y ? 1 : 0;
   if (wfrag && (!conv3x3_stream_uses_frag(Hin, Win, Cin, Cout, stride) || ((uintptr_t)wfrag & 15) ||
                 (yd && (!wdfrag || ((uintptr_t)wdfrag & 15)))))

@@ -40,7 +40,7 @@ constexpr int kIPWPooled = 16;  // images per workgroup on a pooled input (all 1
 
 struct HeadArgs {
   const bf16* x;      // [B, HW, C]
-  const float* pooled;  // POOLED: [B, C] fp32
+  const bf16* pooled;  // POOLED: [B, C] bf16
   const bf16* w;      // [Npad, ldw]
   const float* bias;  // [Npad]
   float* logits;      // [B, N]
@@ -79,15 +79,11 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int b0 = g * kIPW;
   const int nimg = min(kIPW, a.B - b0);
-  if constexpr (POOLED) {  // the last conv already pooled: fp32 [B, C] -> bf16 rows in LDS
+  if constexpr (POOLED) {  // the last conv already pooled: bf16 [B, C] rows -> LDS
     const int c8 = C / 8;
     for (int it = tid; it < nimg * c8; it += 256) {
       const int i = it / c8, cg = it - i * c8;
-      const float* src = a.pooled + (long)(b0 + i) * C + cg * 8;
-      float v[8];
-      *(float4*)v = *(const float4*)src;
-      *(float4*)(v + 4) = *(const float4*)(src + 4);
-      *(uint4*)(pooled + i * ldp + cg * 8) = pack8(v);
+      *(uint4*)(pooled + i * ldp + cg * 8) = *(const uint4*)(a.pooled + (long)(b0 + i) * C + cg * 8);
     }
     __syncthreads();
   } else {
@@ -171,6 +167,13 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
     if (n0 >= a.N) break;
     const bool two = t + 4 < a.tiles_per_split && n0 + 64 < a.N;
     floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+    // bias of this lane's 4 (+4) classes, in flight with the weight loads
+    // (loaded after the MFMAs they cost a dependent round trip per tile)
+    float bv[2][4];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bv[h][r] = (h == 0 || two) ? a.bias[n_begin + (t + 4 * h) * 16 + kq * 4 + r] : 0.f;
     const bf16* w0 = a.w + (long)(n0 + col) * a.ldw + kq * 8;
     const bf16* w1 = w0 + 64L * a.ldw;
     for (int kc = 0; kc < C; kc += 512) {
@@ -210,7 +213,7 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int n = n_begin + tt * 16 + kq * 4 + r;
-          const float v = acc[r] + a.bias[n];
+          const float v = acc[r] + bv[h][r];
           if (n < a.N) a.logits[(long)(b0 + col) * a.N + n] = v;
           lg[col * nsplit + tt * 16 + kq * 4 + r] = v;
         }
@@ -364,7 +367,7 @@ void head_fused(const void* x, const void* w, const float* bias, int B, int HW, 
   DMLC_HIP_CHECK(hipGetLastError());
 }
 
-void head_pooled(const float* pooled, const void* w, const float* bias, int B, int C, int N, int ldw, int Npad,
+void head_pooled(const void* pooled, const void* w, const float* bias, int B, int C, int N, int ldw, int Npad,
                  float* logits, int32_t* idx, float* prob, void* ws, size_t ws_bytes, int num_cus, hipStream_t s,
                  int ns_override, int ko) {
   if (B <= 0) return;
@@ -379,7 +382,7 @@ void head_pooled(const float* pooled, const void* w, const float* bias, int B, i
   if (part_bytes + groups * sizeof(uint32_t) > ws_bytes) throw std::invalid_argument("head_pooled: workspace too small");
   HeadArgs a;
   a.x = nullptr;
-  a.pooled = pooled;
+  a.pooled = (const bf16*)pooled;
   a.w = (const bf16*)w;
   a.bias = bias;
   a.logits = logits;

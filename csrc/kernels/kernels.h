@@ -149,8 +149,8 @@ void conv3x3_stream(const void* x, const void* w, const float* bias, const void*
                     int B, int Hin, int Win, int Cin, int Cout, int stride, bool relu, hipStream_t s,
                     unsigned long long* stamps = nullptr, const void* wd = nullptr, const float* bd = nullptr,
                     void* yd = nullptr, const void* wfrag = nullptr, const void* wdfrag = nullptr,
-                    float* pool = nullptr, bool store_y = true);
-// pool (fp32 [B, Cout]): the global average pool of the output, computed in
+                    void* pool = nullptr, bool store_y = true);
+// pool (bf16 [B, Cout]): the global average pool of the output, computed in
 // the epilogue (whole-image workgroups: the 7x7x512 stride-1 conv); with
 // store_y = false the output activation is not written.
 bool conv3x3_stream_pool_supported(int Hin, int Win, int Cin, int Cout, int stride);
@@ -187,9 +187,9 @@ int head_splits(int B, int N, int num_cus);
 size_t head_ws_bytes(int max_batch);
 void head_fused(const void* x, const void* w, const float* bias, int B, int HW, int C, int N, int ldw, int Npad,
                 float* logits, int32_t* idx, float* prob, void* ws, size_t ws_bytes, int num_cus, hipStream_t s);
-// Same head on an already pooled fp32 [B, C] input (the last conv's fused
+// Same head on an already pooled bf16 [B, C] input (the last conv's fused
 // avgpool): fc + bias + softmax + top-1, 16 images per workgroup.
-void head_pooled(const float* pooled, const void* w, const float* bias, int B, int C, int N, int ldw, int Npad,
+void head_pooled(const void* pooled, const void* w, const float* bias, int B, int C, int N, int ldw, int Npad,
                  float* logits, int32_t* idx, float* prob, void* ws, size_t ws_bytes, int num_cus, hipStream_t s,
                  int ns_override = 0, int ko = 0);
 

@@ -115,6 +115,47 @@ Engine::Engine(const std::string& arch, const WeightMap& weights, int device, in
     throw std::invalid_argument("unknown arch: " + arch);
 
   pack_weights(weights);
+  init_device();
+}
+
+// Same graph, packing and calibration as `src`, on another device, with an
+// uninitialised weight arena: the caller fills it (an RCCL broadcast of the
+// source arena, GpuExecutor::ModelSlot). The host packing runs once per model
+// instead of once per GPU.
+Engine::Engine(const Engine& src, int device)
+    : arch_(src.arch_), device_(device), num_classes_(src.num_classes_), image_size_(src.image_size_) {
+  DMLC_HIP_CHECK(hipSetDevice(device_));
+  hipDeviceProp_t prop;
+  DMLC_HIP_CHECK(hipGetDeviceProperties(&prop, device_));
+  num_cus_ = prop.multiProcessorCount;
+  stem_pad_ = src.stem_pad_;
+  persistent_ = src.persistent_;
+  fused_stem_ = src.fused_stem_;
+  bigtile_ = src.bigtile_;
+  fused_pre_ = src.fused_pre_;
+  stream_conv_ = src.stream_conv_;
+  row_conv_ = src.row_conv_;
+  fp8_ = src.fp8_;
+  graph_direct_ = src.graph_direct_;
+  rows_wreg_ = src.rows_wreg_;
+  rows_strip_ = src.rows_strip_;
+  stream_wreg_ = src.stream_wreg_;
+  stream_l1_ = src.stream_l1_;
+  stream_l4s2_ = src.stream_l4s2_;
+  fuse_ds_ = src.fuse_ds_;
+  fused_head_ = src.fused_head_;
+  fused_pool_ = src.fused_pool_;
+  fork_ds_ = src.fork_ds_;
+  shapes_ = src.shapes_;
+  convs_ = src.convs_;
+  ops_ = src.ops_;
+  logits_act_ = src.logits_act_;
+  weight_bytes_ = src.weight_bytes_;
+  DMLC_HIP_CHECK(hipMalloc(&warena_, weight_bytes_));
+  init_device();
+}
+
+void Engine::init_device() {
   DMLC_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
   DMLC_HIP_CHECK(hipEventCreateWithFlags(&ev_in_, hipEventDisableTiming));
   DMLC_HIP_CHECK(hipEventCreateWithFlags(&ev_out_, hipEventDisableTiming));
@@ -141,7 +182,6 @@ Engine::~Engine() {
   if (zero_) hipFree(zero_);
   if (dummy_idx_) hipFree(dummy_idx_);
   if (head_ws_) hipFree(head_ws_);
-  if (pooled_) hipFree(pooled_);
   if (ev_in_) hipEventDestroy(ev_in_);
   if (ev_out_) hipEventDestroy(ev_out_);
   for (auto e : fork_evs_) hipEventDestroy(e);
@@ -502,13 +542,7 @@ void Engine::reserve(int max_batch) {
   head_ws_bytes_ = head_ws_bytes(max_batch);
   DMLC_HIP_CHECK(hipMalloc(&head_ws_, head_ws_bytes_));
   DMLC_HIP_CHECK(hipMemset(head_ws_, 0, head_ws_bytes_));
-  // the last conv's fused global average pool: fp32 [max_batch, C]
-  if (pooled_) DMLC_HIP_CHECK(hipFree(pooled_));
-  pooled_ = nullptr;
-  int pool_c = 0;
-  for (const Op& op : ops_)
-    if (op.type == OpType::AvgPoolGlobal) pool_c = std::max(pool_c, shapes_[op.in].C);
-  if (pool_c > 0) DMLC_HIP_CHECK(hipMalloc(&pooled_, (size_t)max_batch * pool_c * sizeof(float)));
+
   // big-tile conv split-K slabs for the largest batch
   long slabs = 0;
   for (const Op& op : ops_) {
@@ -616,14 +650,15 @@ bool Engine::head_fusable(size_t oi) const {
 }
 
 // ops[oi] is the last conv (stream path, whole-image workgroups) and
-// ops[oi+1..oi+3] the fusable head reading only its output: the conv's
-// epilogue computes the global average pool and skips storing the
-// activation; the head then starts from the pooled vectors.
+// ops[oi+1] the global average pool, the only reader of its output: the
+// conv's epilogue writes the pooled bf16 vectors straight into the pool's
+// output activation and skips storing its own.
 bool Engine::pool_fusable(size_t oi, int B) const {
-  if (!fused_pool_ || !pooled_ || oi + 1 >= ops_.size()) return false;
+  if (!fused_pool_ || oi + 1 >= ops_.size()) return false;
   const Op& c = ops_[oi];
   const Op& p = ops_[oi + 1];
-  if (c.type != OpType::Conv || p.type != OpType::AvgPoolGlobal || p.in != c.out || !head_fusable(oi + 1)) return false;
+  if (c.type != OpType::Conv || p.type != OpType::AvgPoolGlobal || p.in != c.out) return false;
+  if (shapes_[p.out].fp8 || shapes_[p.out].f32 || shapes_[p.in].fp8) return false;
   for (size_t j = 0; j < ops_.size(); ++j)
     if (j != oi + 1 && (ops_[j].in == c.out || ops_[j].res == c.out)) return false;
   const ConvLayer& L = convs_[c.conv];
@@ -721,7 +756,7 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
                            (L.wf_off && stream_wreg_ && (!D || D->wf_off)) ? (const uint8_t*)warena_ + L.wf_off
                                                                           : nullptr,
                            (D && D->wf_off && stream_wreg_) ? (const uint8_t*)warena_ + D->wf_off : nullptr,
-                           fpool ? (float*)pooled_ : nullptr, !fpool || trace || evs);
+                           fpool ? acts_[ops_[oi + 1].out] : nullptr, !fpool || trace || evs);
             pooled = fpool;
             skip_ds = -1;
             break;
@@ -778,14 +813,16 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
       }
       case OpType::AvgPoolGlobal: {
         const ActShape& i = shapes_[op.in];
-        if (pooled && head_fusable(oi)) {  // pooled by the last conv: fc + softmax/top-1
-          const ConvLayer& L = convs_[ops_[oi + 1].conv];
-          head_pooled((const float*)pooled_, (const uint8_t*)warena_ + L.w_off,
-                      (const float*)((const uint8_t*)warena_ + L.b_off), B, i.C, L.cout, L.kpad, L.npad,
-                      logits ? logits : (float*)acts_[ops_[oi + 1].out], idx ? idx : dummy_idx_,
-                      prob ? prob : (float*)(dummy_idx_ + max_batch_), head_ws_, head_ws_bytes_, num_cus_, s);
-          skip = 2;
-          break;
+        if (pooled) {  // pooled by the last conv's epilogue
+          if (head_fusable(oi)) {  // fc + softmax/top-1 in one launch
+            const ConvLayer& L = convs_[ops_[oi + 1].conv];
+            head_pooled(acts_[op.out], (const uint8_t*)warena_ + L.w_off,
+                        (const float*)((const uint8_t*)warena_ + L.b_off), B, i.C, L.cout, L.kpad, L.npad,
+                        logits ? logits : (float*)acts_[ops_[oi + 1].out], idx ? idx : dummy_idx_,
+                        prob ? prob : (float*)(dummy_idx_ + max_batch_), head_ws_, head_ws_bytes_, num_cus_, s);
+            skip = 2;
+          }
+          break;  // else the fc and softmax ops follow
         }
         if (head_fusable(oi)) {  // avgpool + fc + softmax/top-1 in one launch
           const ConvLayer& L = convs_[ops_[oi + 1].conv];

@@ -64,9 +64,13 @@ class Engine {
   // activation scales calibrated at load time on a synthetic batch)
   Engine(const std::string& arch, const WeightMap& weights, int device, int num_classes = 1000,
          int image_size = 224);
+  // A replica of `src` on `device` (same graph, packing, calibration) whose
+  // weight arena is allocated but not filled: copy src.weight_arena() into
+  // weight_arena() (an RCCL broadcast across the node's GPUs).
+  Engine(const Engine& src, int device);
   ~Engine();
-  Engine(const Engine&) = delete;
   Engine& operator=(const Engine&) = delete;
+  void* weight_arena() const { return warena_; }
 
   const std::string& arch() const { return arch_; }
   int device() const { return device_; }
@@ -107,6 +111,7 @@ class Engine {
   void build_resnet(const std::vector<int>& blocks, bool bottleneck);
   void build_alexnet();
   void pack_weights(const WeightMap& w);
+  void init_device();
   void mark_fp8();
   void calibrate(const WeightMap& w);
   void run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* idx, float* prob,
@@ -142,7 +147,6 @@ class Engine {
   bool fuse_ds_ = true;     // downsample inside the stride-2 stream conv1 (env DMLC_FUSE_DS=0 disables)
   bool fused_head_ = true;  // avgpool+fc+softmax/top-1 as one kernel (env DMLC_FUSED_HEAD=0 disables)
   bool fused_pool_ = true;  // the last conv's epilogue computes the avgpool (env DMLC_FUSED_POOL=0 disables)
-  void* pooled_ = nullptr;  // fp32 [max_batch, C] pooled features of the last conv
   // downsample convs on a side stream (env DMLC_FORK_DS=1 enables): measured
   // slower (the branch slows its sibling conv1 by 10-12 us and adds ~10 us of
   // fork/join gaps per block: profiles/r1_fork_ds_timeline.txt)
