@@ -259,6 +259,35 @@ void handle_line(Node& n, const std::string& line) {
         out_line("Training complete!");
       else
         err_line("Training failed: " + r.str());
+    } else if (c == "predict-shard") {
+      // classify an SDFS u8 shard where a replica lives (HBM-resident on GPU members)
+      if (t.size() < 2 || t.size() > 3) return err_line("Invalid predict-shard command!");
+      Writer w;
+      w.str(t[1]).str(t.size() == 3 ? t[2] : "resnet18");
+      Reader r(n.call_leader(L_PREDICT_SHARD, w.data(), 600000));
+      const std::string holder = r.str();
+      const int v = r.i32();
+      const std::string loc = r.str();
+      const int64_t us = r.i64();
+      const uint32_t k = r.u32();
+      std::map<int, int> hist;
+      std::string head;
+      for (uint32_t i = 0; i < k; ++i) {
+        const int cls = r.i32();
+        const double p = r.f64();
+        ++hist[cls];
+        if (i < 8) head += (head.empty() ? "" : " ") + std::to_string(cls) + ":" + std::to_string((int)(p * 1000) / 10.0).substr(0, 4) + "%";
+      }
+      char buf[256];
+      snprintf(buf, sizeof(buf), "Classified %u images of %s v%d on %s [%s] in %.3f ms (%.1f images/s)", k,
+               t[1].c_str(), v, holder.c_str(), loc.c_str(), us / 1000.0, us > 0 ? k * 1e6 / us : 0.0);
+      out_line(buf);
+      out_line("first: " + head + " | distinct classes: " + std::to_string(hist.size()));
+    } else if (c == "replicas") {  // this node's staged (HBM) shard replicas
+      std::string s;
+      for (const auto& key : n.member->staged_replicas()) s += (s.empty() ? "" : " ") + key;
+      out_line("staged: " + (s.empty() ? std::string("none") : s) + " in " +
+               (n.member->executor() ? n.member->executor()->blob_location() : std::string("-")));
     } else if (c == "predict") {
       if (t.size() != 1) return err_line("Invalid predict command!");
       n.call_leader(L_PREDICT, "", 30000);
@@ -382,6 +411,7 @@ int run_node(const Args& a) {
   mcfg.dataset_dir = a.get("dataset", "test_files/imagenet_1k/train");
   mcfg.leader_candidates = leaders;
   mcfg.check_ms = a.geti("bg-ms", 3000);
+  mcfg.hbm_replicas = !a.has("no-hbm-replicas");
   n->member = std::make_unique<MemberService>(mcfg, n->ms.get(), std::move(ex), labels);
   n->member->start(n->base_port);
   if (a.has("prefetch")) n->member->start_prefetch();

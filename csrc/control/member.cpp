@@ -8,7 +8,9 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstring>
 #include <fstream>
+#include "../serve/shard.h"
 
 #include "common.h"
 
@@ -96,10 +98,78 @@ void MemberService::start(int base_port) {
   register_handlers();
   server_->start();
   checker_ = std::thread([this] { leader_check_loop(); });
+  replicator_ = std::thread([this] { replica_loop(); });
+}
+
+namespace {
+std::string replica_key(const std::string& file, int v) { return file + "@v" + std::to_string(v); }
+}  // namespace
+
+void MemberService::stage_replica(const std::string& file, int version) {
+  if (!exec_) return;
+  const std::string path = cfg_.storage_dir + "/" + storage_filename(file, version);
+  {
+    std::ifstream f(path, std::ios::binary);
+    char magic[8] = {};
+    if (!f.read(magic, 8) || std::memcmp(magic, kShardMagic, 8) != 0) return;  // only u8 shards live in HBM
+  }
+  const std::string key = replica_key(file, version);
+  exec_->stage_blob(key, path);
+  for (const auto& k : exec_->blob_keys())  // older versions of the same file leave HBM
+    if (k != key && k.rfind(file + "@v", 0) == 0) exec_->drop_blob(k);
+  DMLC_LOG_INFO("staged replica " << key << " in " << exec_->blob_location());
+}
+
+void MemberService::replica_loop() {
+  while (!stop_.load()) {
+    std::pair<std::string, int> item;
+    {
+      std::unique_lock<std::mutex> g(rq_mu_);
+      // untimed wait: GCC 11's ThreadSanitizer does not intercept the
+      // pthread_cond_clockwait behind wait_for (false double-lock reports)
+      rq_cv_.wait(g, [&] { return !rq_.empty() || stop_.load(); });
+      if (rq_.empty()) continue;
+      item = rq_.front();
+      rq_.pop_front();
+    }
+    try {
+      stage_replica(item.first, item.second);
+    } catch (const std::exception& e) {
+      DMLC_LOG_WARN("staging replica " << item.first << " v" << item.second << " failed: " << e.what());
+    }
+  }
+}
+
+std::vector<std::string> MemberService::staged_replicas() const {
+  return exec_ ? exec_->blob_keys() : std::vector<std::string>{};
+}
+
+MemberService::ShardResult MemberService::predict_shard(const std::string& file, const std::string& model) {
+  if (!exec_) throw std::runtime_error("no executor");
+  int v = 0;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = files_.find(file);
+    if (it == files_.end() || it->second.empty()) throw std::runtime_error("no replica of " + file + " here");
+    v = *it->second.rbegin();
+  }
+  const std::string key = replica_key(file, v);
+  const auto keys = exec_->blob_keys();
+  if (std::find(keys.begin(), keys.end(), key) == keys.end()) stage_replica(file, v);
+  ShardResult r;
+  r.version = v;
+  r.location = exec_->blob_location() + " -> " + exec_->backend();
+  const int64_t t0 = steady_us();
+  r.preds = exec_->predict_blob(model, key);
+  r.elapsed_us = steady_us() - t0;
+  return r;
 }
 
 void MemberService::stop() {
   if (stop_.exchange(true)) return;
+  { std::lock_guard<std::mutex> g(rq_mu_); }  // a waiter is past its predicate check or asleep: no lost wakeup
+  rq_cv_.notify_all();
+  if (replicator_.joinable()) replicator_.join();
   if (checker_.joinable()) checker_.join();
   if (prefetcher_.joinable()) prefetcher_.join();
   if (server_) server_->stop();
@@ -263,9 +333,24 @@ void MemberService::register_handlers() {
   server_->handle(M_RECEIVE, [this](Reader& r) {
     const std::string f = r.str();
     const int v = r.i32();
-    std::lock_guard<std::mutex> g(mu_);
-    files_[f].insert(v);
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      files_[f].insert(v);
+    }
+    if (cfg_.hbm_replicas && exec_) {  // a u8 shard replica goes resident into HBM
+      std::lock_guard<std::mutex> g(rq_mu_);
+      rq_.emplace_back(f, v);
+      rq_cv_.notify_one();
+    }
     return std::string();
+  });
+  server_->handle(M_PREDICT_SHARD, [this](Reader& r) {
+    const std::string f = r.str(), model = r.str();
+    const ShardResult res = predict_shard(f, model);
+    Writer w;
+    w.i32(res.version).str(res.location).i64(res.elapsed_us).u32((uint32_t)res.preds.size());
+    for (const auto& p : res.preds) w.i32(p.class_idx).f64(p.prob);
+    return w.take();
   });
   server_->handle(M_PREDICT, [this](Reader& r) {
     const std::string model = r.str();
@@ -315,7 +400,10 @@ void MemberService::register_handlers() {
       if (it != files_.end()) versions = it->second;
       files_.erase(f);
     }
-    for (int v : versions) unlink((cfg_.storage_dir + "/" + storage_filename(f, v)).c_str());
+    for (int v : versions) {
+      unlink((cfg_.storage_dir + "/" + storage_filename(f, v)).c_str());
+      if (exec_) exec_->drop_blob(replica_key(f, v));
+    }
     return std::string();
   });
   server_->handle(M_LOAD_MODEL, [this](Reader& r) {

@@ -10,6 +10,8 @@
 // the leader pointer wraps around the candidate list.
 #pragma once
 #include <atomic>
+#include <condition_variable>
+#include <deque>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -35,6 +37,7 @@ struct MemberConfig {
   std::vector<std::string> leader_candidates;  // base addresses "host:port", in order
   int check_ms = 3000;
   int chunk_bytes = 8 << 20;
+  bool hbm_replicas = true;  // stage received u8-shard replicas into the executor's blob store (HBM)
 };
 
 // Label table: synset_words.txt lines "<wnid> <label text>" (src/services.rs:170-184).
@@ -81,6 +84,19 @@ class MemberService {
   bool start_prefetch();
   int prefetched() const { return prefetched_.load(); }
 
+  // Classify the local replica (latest version) of SDFS shard `file` from
+  // the executor's blob store, staging it first if needed. Returns the
+  // version, blob location and per-image predictions.
+  struct ShardResult {
+    int version = 0;
+    std::string location;
+    int64_t elapsed_us = 0;
+    std::vector<Prediction> preds;
+  };
+  ShardResult predict_shard(const std::string& file, const std::string& model);
+  // Keys of the staged replicas ("<file>@v<version>").
+  std::vector<std::string> staged_replicas() const;
+
  private:
   std::string query_image(const std::string& id) const;
   void register_handlers();
@@ -101,6 +117,13 @@ class MemberService {
   std::thread prefetcher_;
   std::atomic<bool> prefetching_{false};
   std::atomic<int> prefetched_{0};
+  // replica staging (received shards -> executor blobs) off the RPC thread
+  void replica_loop();
+  void stage_replica(const std::string& file, int version);
+  std::mutex rq_mu_;
+  std::condition_variable rq_cv_;
+  std::deque<std::pair<std::string, int>> rq_;
+  std::thread replicator_;
 };
 
 }  // namespace ctl

@@ -33,6 +33,7 @@ enum LeaderMethod : uint16_t {
   L_JOBS = 8,
   L_ALIVE = 9,
   L_STATE = 10,  // jobs + SDFS directory snapshot (standby replication)
+  L_PREDICT_SHARD = 11,  // classify an SDFS u8 shard on a replica holder (HBM-resident)
 };
 
 enum MemberMethod : uint16_t {
@@ -44,6 +45,7 @@ enum MemberMethod : uint16_t {
   M_DELETE_FILE = 25,
   M_LOAD_MODEL = 26,  // hot-swap model weights (train)
   M_INFO = 27,
+  M_PREDICT_SHARD = 28,  // classify the local (HBM-staged) replica of a shard
 };
 
 std::string sanitize_filename(const std::string& s);

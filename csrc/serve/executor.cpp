@@ -16,6 +16,8 @@
 #include "../runtime/ot_io.h"
 #include "../runtime/trace.h"
 #include "../comm/dp.h"
+#include "shard.h"
+#include <fstream>
 #include "../kernels/kernels.h"
 #include <condition_variable>
 #include <cstring>
@@ -317,6 +319,80 @@ class GpuExecutor : public Executor {
     return true;
   }
 
+  // ---- SDFS replicas resident in the coordinator GPU's HBM
+  std::string blob_location() const override { return "hbm:gpu" + std::to_string(devices_[0]); }
+
+  void stage_blob(const std::string& key, const std::string& path) override {
+    std::ifstream f(path, std::ios::binary);
+    if (!f) throw std::runtime_error("cannot open " + path);
+    f.seekg(0, std::ios::end);
+    const size_t bytes = (size_t)f.tellg();
+    f.seekg(0);
+    auto b = std::make_shared<HbmBlob>();
+    b->bytes = bytes;
+    b->device = devices_[0];
+    DMLC_HIP_CHECK(hipSetDevice(devices_[0]));
+    DMLC_HIP_CHECK(hipMalloc(&b->dev, std::max<size_t>(bytes, 256)));
+    // pinned bounce buffer, 32 MB chunks, H2D on a stager's side stream
+    Stager st = take_stager();
+    try {
+      constexpr size_t kChunk = (size_t)32 << 20;
+      if (st.pinned_bytes < std::min(kChunk, bytes)) {
+        if (st.pinned) DMLC_HIP_CHECK(hipHostFree(st.pinned));
+        st.pinned = nullptr;
+        st.pinned_bytes = 0;
+        DMLC_HIP_CHECK(hipHostMalloc(&st.pinned, std::min(kChunk, std::max<size_t>(bytes, 256)), hipHostMallocDefault));
+        st.pinned_bytes = std::min(kChunk, std::max<size_t>(bytes, 256));
+      }
+      for (size_t off = 0; off < bytes;) {
+        const size_t n = std::min(st.pinned_bytes, bytes - off);
+        f.read((char*)st.pinned, (std::streamsize)n);
+        if (off == 0 && n >= kShardHeader) std::memcpy(b->head, st.pinned, kShardHeader);
+        DMLC_HIP_CHECK(hipMemcpyAsync((uint8_t*)b->dev + off, st.pinned, n, hipMemcpyHostToDevice, st.stream));
+        DMLC_HIP_CHECK(hipStreamSynchronize(st.stream));
+        off += n;
+      }
+    } catch (...) {
+      give_stager(st);
+      throw;
+    }
+    give_stager(st);
+    std::lock_guard<std::mutex> g(blob_mu_);
+    hbm_blobs_[key] = std::move(b);  // a replaced blob is freed once no query holds it
+  }
+  void drop_blob(const std::string& key) override {
+    std::lock_guard<std::mutex> g(blob_mu_);
+    hbm_blobs_.erase(key);
+  }
+  std::vector<std::string> blob_keys() const override {
+    std::lock_guard<std::mutex> g(blob_mu_);
+    std::vector<std::string> out;
+    for (const auto& kv : hbm_blobs_) out.push_back(kv.first);
+    return out;
+  }
+  std::vector<Prediction> predict_blob(const std::string& model, const std::string& key) override {
+    auto slot = get(model);
+    std::shared_ptr<HbmBlob> b;
+    {
+      std::lock_guard<std::mutex> g(blob_mu_);
+      auto it = hbm_blobs_.find(key);
+      if (it == hbm_blobs_.end()) throw std::runtime_error("blob not staged: " + key);
+      b = it->second;
+    }
+    if (b->bytes < kShardHeader || !is_shard(b->head, kShardHeader)) throw std::runtime_error(key + " is not a u8 shard");
+    ShardInfo si;
+    std::memcpy(&si.n, b->head + 8, 4);
+    std::memcpy(&si.h, b->head + 12, 4);
+    std::memcpy(&si.w, b->head + 16, 4);
+    if (si.h == 0 || si.w == 0 || (uint64_t)si.n * si.image_bytes() + kShardHeader != b->bytes)
+      throw std::runtime_error(key + ": bad shard header");
+    const uint8_t* data = (const uint8_t*)b->dev + kShardHeader;
+    if (si.h == ModelSlot::kS && si.w == ModelSlot::kS) return slot->run_dense(data, si.n);
+    std::vector<ImageDesc> descs(si.n);
+    for (uint32_t i = 0; i < si.n; ++i) descs[i] = ImageDesc{data + (size_t)i * si.image_bytes(), (int)si.h, (int)si.w};
+    return slot->run(descs);
+  }
+
   CacheStats cache_stats() const override {
     std::lock_guard<std::mutex> g(cache_mu_);
     CacheStats c = stats_;
@@ -335,11 +411,24 @@ class GpuExecutor : public Executor {
     ModelSlot(const std::string& arch, const WeightMap& w, const std::vector<int>& devices, int max_batch,
               int min_shard)
         : max_batch(max_batch) {
-      for (int d : devices) {
-        DMLC_HIP_CHECK(hipSetDevice(d));
-        engines.push_back(std::make_unique<Engine>(arch, w, d));
+      // The host packs the weights once (engine 0, one H2D copy); the other
+      // GPUs get replicas whose arenas are filled by one RCCL broadcast over
+      // xGMI (`train` = distribute + hot-swap).
+      for (size_t k = 0; k < devices.size(); ++k) {
+        DMLC_HIP_CHECK(hipSetDevice(devices[k]));
+        if (k == 0) engines.push_back(std::make_unique<Engine>(arch, w, devices[0]));
+        else engines.push_back(std::make_unique<Engine>(*engines[0], devices[k]));
         engines.back()->reserve(max_batch);
         workers.push_back(dp::make_hip_worker(engines.back().get(), kS, kS, /*use_graph=*/true));
+      }
+      if (devices.size() > 1) {
+        auto comms = comm::rccl_init_all(devices);
+        comms[0]->group_start();
+        for (size_t k = 0; k < devices.size(); ++k)
+          comms[k]->broadcast(engines[0]->weight_arena(), engines[k]->weight_arena(), engines[0]->weight_bytes(), 0,
+                              workers[k]->stream(dp::Worker::kIn));
+        comms[0]->group_end();
+        for (auto& wk : workers) wk->sync_all();
       }
       std::vector<dp::Worker*> ws;
       for (auto& x : workers) ws.push_back(x.get());
@@ -391,6 +480,19 @@ class GpuExecutor : public Executor {
       }
       return out;
     }
+    // Images already u8 224x224 in coordinator memory (a staged shard):
+    // straight into the group, no resize copy.
+    std::vector<Prediction> run_dense(const uint8_t* src, int64_t n) {
+      DMLC_TRACE("executor.forward_dense");
+      std::lock_guard<std::mutex> g(mu);
+      std::vector<int32_t> idx(n);
+      std::vector<float> prob(n);
+      group->coordinator()->activate();
+      group->classify(src, n, idx.data(), prob.data());
+      std::vector<Prediction> out(n);
+      for (int64_t i = 0; i < n; ++i) out[i] = Prediction{prob[i], idx[i]};
+      return out;
+    }
     static constexpr int kS = 224;
     int max_batch;
     std::vector<std::unique_ptr<Engine>> engines;
@@ -410,6 +512,19 @@ class GpuExecutor : public Executor {
     int pins = 0;
     std::list<std::string>::iterator lru;
   };
+  struct HbmBlob {
+    void* dev = nullptr;
+    size_t bytes = 0;
+    int device = 0;
+    uint8_t head[kShardHeader] = {};  // host copy of the first bytes (shard header)
+    ~HbmBlob() {
+      if (dev) {
+        (void)hipSetDevice(device);
+        (void)hipFree(dev);
+      }
+    }
+  };
+  std::map<std::string, std::shared_ptr<HbmBlob>> hbm_blobs_;  // under blob_mu_
   struct Stager {
     hipStream_t stream = nullptr;
     void* pinned = nullptr;

@@ -10,6 +10,7 @@
 //     on nodes without a GPU (the BASELINE "AlexNet single-image classify on
 //     CPU via libtorch .ot load" plumbing config).
 #pragma once
+#include <map>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -54,6 +55,22 @@ class Executor {
   // executor has no cache.
   virtual bool stage(const std::string& path) { return false; }
   virtual CacheStats cache_stats() const { return {}; }
+
+  // SDFS replicas resident next to the compute (blobs): the GPU executor
+  // keeps a staged file in the HBM of its coordinator GPU (pinned host buffer
+  // -> hipMemcpyAsync on a side stream); the default keeps it in host memory.
+  // Keys are caller-chosen (the member uses "<sdfs name>@v<version>").
+  virtual void stage_blob(const std::string& key, const std::string& path);
+  virtual void drop_blob(const std::string& key);
+  virtual std::vector<std::string> blob_keys() const;
+  virtual std::string blob_location() const { return "host"; }
+  // Classify every image of a staged u8 shard blob (csrc/serve/shard.h), in
+  // order. GPU: read straight from HBM and scattered over the executor's GPUs.
+  virtual std::vector<Prediction> predict_blob(const std::string& model, const std::string& key);
+
+ protected:
+  mutable std::mutex blob_mu_;
+  std::map<std::string, std::shared_ptr<const std::vector<uint8_t>>> host_blobs_;
 };
 
 // backend: "gpu", "cpu" or "auto" (GPU when a HIP device is visible).

@@ -284,6 +284,17 @@ void LeaderService::train(const std::string& filename, const std::string& model_
     for (const auto& e : errors) s += (s.empty() ? "" : "; ") + e;
     throw std::runtime_error(s);
   }
+  // New weights: that model's job starts over, so the next `predict`
+  // classifies the dataset with them (the reference never reloaded models
+  // after `train`, src/services.rs:139-144 vs :513-524).
+  std::lock_guard<std::mutex> g(mu_);
+  for (size_t j = 0; j < jobs_.size(); ++j)
+    if (jobs_[j].model_name == model_name && !running_[j]) {
+      Job fresh;
+      fresh.model_name = model_name;
+      fresh.assigned = jobs_[j].assigned;
+      jobs_[j] = std::move(fresh);
+    }
 }
 
 void LeaderService::predict() {
@@ -668,6 +679,36 @@ void LeaderService::register_handlers() {
       w.boolean(false).str(e.what());
     }
     return w.take();
+  });
+  server_->handle(L_PREDICT_SHARD, [this](Reader& r) {
+    // a replica holder of the latest version classifies its (HBM-resident)
+    // copy: the shard's bytes never move
+    const std::string f = r.str(), model = r.str();
+    const int v = latest_version(f);
+    if (v == 0) throw std::runtime_error("file not found: " + f);
+    std::vector<Id> holders;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      for (const auto& rep : dir_[f])
+        if (rep.second.count(v)) holders.push_back(rep.first);
+    }
+    const auto active = ms_->active_ids();
+    std::string last_err = "no live holder";
+    for (const Id& h : holders) {
+      if (!active.count(h)) continue;
+      try {
+        Writer w;
+        w.str(f).str(model);
+        const std::string resp = RpcClient::shared().call(h.host(), member_port(h.port()), M_PREDICT_SHARD, w.data(),
+                                                          600000);
+        Writer out;
+        out.str(h.address);
+        return out.take() + resp;
+      } catch (const std::exception& e) {
+        last_err = h.address + ": " + e.what();
+      }
+    }
+    throw std::runtime_error("predict-shard " + f + ": " + last_err);
   });
   server_->handle(L_PREDICT, [this](Reader&) {
     predict();

@@ -113,3 +113,36 @@ def test_gpu_hbm_image_cache(gpu, env, tmp_path):
         assert done == 16
         m = re.search(r"cache hits (\d+) misses (\d+)", n.cmd("info"))
         assert m and int(m.group(1)) >= 16 and int(m.group(2)) == 0, n.cmd("info")
+
+
+def test_gpu_shard_served_from_hbm_without_host_io(gpu, env, tmp_path):
+    """A u8 shard put into the SDFS is staged into the member's HBM when the
+    replica arrives; with the replica FILES deleted from every node's disk,
+    predict-shard still classifies it (from HBM, through the executor's
+    dp::Group) with the same answers as the in-process engine."""
+    import glob
+    import torch
+    from dmlc.runtime import InferenceEngine
+    from dmlc.utils.shards import read_shard, synthetic_shard
+    shard = synthetic_shard(str(tmp_path / "s.u8s"), 40, 224, seed=8)
+    cl = LocalCluster(2, 19800, str(tmp_path / "c"), env["labels"], n_leaders=1, executor="gpu",
+                      dataset=env["dataset"], models=f"resnet18={env['ckpt']}", extra=["--max-batch", "64"])
+    with cl:
+        n = cl.nodes
+        assert "Stored on:" in n[1].cmd(f"put {shard} s.u8s")
+        deadline = time.time() + 60
+        while time.time() < deadline and "s.u8s@v1" not in n[0].cmd("replicas"):
+            time.sleep(0.2)
+        assert re.search(r"s\.u8s@v1 in hbm:gpu0", n[0].cmd("replicas")), n[0].cmd("replicas")
+        removed = [p for p in glob.glob(str(tmp_path / "c" / "*" / "storage" / "v1.s.u8s"))]
+        assert removed
+        for p in removed:
+            os.remove(p)
+        out = n[0].cmd("predict-shard s.u8s resnet18", 120)
+    m = re.search(r"Classified 40 images of s.u8s v1 on (\S+) \[hbm:gpu0 -> gpu:0\]", out)
+    assert m, out
+    got = [int(x) for x in re.findall(r"(\d+):\d", out.split("first:")[1])]
+    eng = InferenceEngine("resnet18", env["ckpt"], device=0, max_batch=64)
+    idx, _ = eng.predict(torch.from_numpy(read_shard(shard).copy()).cuda())
+    torch.cuda.synchronize()
+    assert got == idx[:8].cpu().tolist()
