@@ -193,6 +193,13 @@ void head_pooled(const void* pooled, const void* w, const float* bias, int B, in
                  float* logits, int32_t* idx, float* prob, void* ws, size_t ws_bytes, int num_cus, hipStream_t s,
                  int ns_override = 0, int ko = 0);
 
+// Fully-connected layer at small batch (fc_small.hip): y[b][n] = act(x[b] .
+// w[n] + bias[n]) for B <= 16 as a weight-streaming MFMA GEMV; x bf16
+// [B, ldx], w bf16 [Npad, ldw], y bf16 / fp32 [B, ldo].
+bool fc_small_supported(int B, int K, int ldx, int ldw);
+void fc_small(const void* x, int ldx, const void* w, int ldw, const float* bias, void* y, int ldo, bool out_f32,
+              int B, int K, int N, int Npad, bool relu, hipStream_t s);
+
 // Row-wise softmax + top-1 over fp32 logits [B, ld] (first N columns).
 void softmax_top1(const float* logits, int B, int N, int ld, int32_t* idx, float* prob,
                   hipStream_t s);

@@ -89,6 +89,7 @@ Engine::Engine(const std::string& arch, const WeightMap& weights, int device, in
   if (const char* e = std::getenv("DMLC_FORK_DS")) fork_ds_ = std::string(e) != "0";
   if (const char* e = std::getenv("DMLC_FUSED_HEAD")) fused_head_ = std::string(e) != "0";
   if (const char* e = std::getenv("DMLC_FUSED_POOL")) fused_pool_ = std::string(e) != "0";
+  if (const char* e = std::getenv("DMLC_FC_SMALL")) fc_small_ = std::string(e) != "0";
   if (const char* e = std::getenv("DMLC_FUSE_DS")) fuse_ds_ = std::string(e) != "0";
   if (const char* e = std::getenv("DMLC_STREAM_L4S2")) stream_l4s2_ = std::string(e) != "0";
   if (const char* e = std::getenv("DMLC_STREAM_L1")) stream_l1_ = std::string(e) != "0";
@@ -145,6 +146,7 @@ Engine::Engine(const Engine& src, int device)
   fuse_ds_ = src.fuse_ds_;
   fused_head_ = src.fused_head_;
   fused_pool_ = src.fused_pool_;
+  fc_small_ = src.fc_small_;
   fork_ds_ = src.fork_ds_;
   shapes_ = src.shapes_;
   convs_ = src.convs_;
@@ -542,7 +544,6 @@ void Engine::reserve(int max_batch) {
   head_ws_bytes_ = head_ws_bytes(max_batch);
   DMLC_HIP_CHECK(hipMalloc(&head_ws_, head_ws_bytes_));
   DMLC_HIP_CHECK(hipMemset(head_ws_, 0, head_ws_bytes_));
-
   // big-tile conv split-K slabs for the largest batch
   long slabs = 0;
   for (const Op& op : ops_) {
@@ -735,6 +736,15 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
         if (op.res >= 0 && joined.count(op.res)) {
           DMLC_HIP_CHECK(hipStreamWaitEvent(s, joined[op.res], 0));
           joined.erase(op.res);
+        }
+        if (L.fc && !L.fp8 && !shapes_[op.out].fp8 && fc_small_ && fc_small_supported(B, L.cin, L.cin, L.kpad)) {
+          // query-sized batches: weight-streaming GEMV (AlexNet classifier)
+          const ActShape& os = shapes_[op.out];
+          fc_small(acts_[op.in], L.cin, (const uint8_t*)warena_ + L.w_off, L.kpad,
+                   (const float*)((const uint8_t*)warena_ + L.b_off),
+                   (os.f32 && logits) ? (void*)logits : acts_[op.out], L.cout, os.f32, B, L.cin, L.cout, L.npad,
+                   L.relu, cs);
+          break;
         }
         switch (conv_path(op, B)) {
           case ConvPath::Stream: {

@@ -147,6 +147,7 @@ class Engine {
   bool fuse_ds_ = true;     // downsample inside the stride-2 stream conv1 (env DMLC_FUSE_DS=0 disables)
   bool fused_head_ = true;  // avgpool+fc+softmax/top-1 as one kernel (env DMLC_FUSED_HEAD=0 disables)
   bool fused_pool_ = true;  // the last conv's epilogue computes the avgpool (env DMLC_FUSED_POOL=0 disables)
+  bool fc_small_ = true;    // weight-streaming GEMV for fc layers at B <= 16 (env DMLC_FC_SMALL=0 disables)
   // downsample convs on a side stream (env DMLC_FORK_DS=1 enables): measured
   // slower (the branch slows its sibling conv1 by 10-12 us and adds ~10 us of
   // fork/join gaps per block: profiles/r1_fork_ds_timeline.txt)

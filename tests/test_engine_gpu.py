@@ -241,3 +241,27 @@ def test_fused_pool_head_matches_unfused(gpu, monkeypatch):
     assert rel < 1e-2, rel
     assert torch.equal(fi, ri) and torch.equal(i2, ri)
     assert torch.allclose(fp, rp, rtol=1e-2, atol=1e-4) and torch.allclose(p2, rp, rtol=1e-2, atol=1e-4)
+
+
+@pytest.mark.parametrize("B", [1, 5, 16])
+def test_alexnet_small_batch_fc_matches_reference(gpu, B, monkeypatch):
+    """Query-sized AlexNet batches run the classifier on the weight-streaming
+    split-K GEMV (fc_small.hip): vs fp32 torch.nn, and vs the implicit-GEMM
+    path (DMLC_FC_SMALL=0) on the same inputs."""
+    model = build("alexnet", seed=51, randomize_bn=True)
+    sd = state_dict_f32(model)
+    g = torch.Generator().manual_seed(52 + B)
+    img = torch.randint(0, 256, (B, 224, 224, 3), generator=g, dtype=torch.uint8)
+    eng = InferenceEngine("alexnet", sd, max_batch=B)
+    idx, prob, logits = eng.predict(img.to(gpu), return_logits=True)
+    i2, p2 = eng.predict(img.to(gpu))  # graph replay, no logits output
+    monkeypatch.setenv("DMLC_FC_SMALL", "0")
+    ref_eng = InferenceEngine("alexnet", sd, max_batch=B)
+    _, _, ref_gemm = ref_eng.predict(img.to(gpu), return_logits=True)
+    torch.cuda.synchronize()
+    ref = _ref_logits(model, img)
+    rel = ((logits.cpu() - ref).norm() / ref.norm()).item()
+    assert rel < 3e-2, rel
+    rel2 = ((logits - ref_gemm).norm() / ref_gemm.norm()).item()
+    assert rel2 < 5e-3, rel2
+    assert torch.equal(idx, i2) and torch.allclose(prob, p2)
