@@ -184,6 +184,13 @@ PYBIND11_MODULE(_C, m) {
   }, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("res"), py::arg("y"), py::arg("zero"), py::arg("B"),
         py::arg("H"), py::arg("W"), py::arg("C"), py::arg("relu"), py::arg("strip"), py::arg("stream"),
         py::arg("wfrag") = 0);
+  m.def("conv3x3_block_supported", &conv3x3_block_supported);
+  m.def("conv3x3_block", [](uintptr_t x, uintptr_t wf1, uintptr_t b1, uintptr_t wf2, uintptr_t b2, uintptr_t y,
+                            uintptr_t zero, int B, uintptr_t stream) {
+    conv3x3_block(P<void>(x), P<void>(wf1), P<float>(b1), P<void>(wf2), P<float>(b2), P<void>(y), P<void>(zero), B,
+                  S(stream));
+  }, py::arg("x"), py::arg("wf1"), py::arg("b1"), py::arg("wf2"), py::arg("b2"), py::arg("y"), py::arg("zero"),
+        py::arg("B"), py::arg("stream"));
   m.def("stem_conv_pool_u8", [](uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y, int B, int S_, int strip,
                                 uintptr_t stream) {
     stem_conv_pool_u8(P<uint8_t>(x), P<void>(w), P<float>(bias), P<void>(y), B, S_, strip, S(stream));

@@ -138,6 +138,12 @@ int conv3x3_rows_pick_strip(int B, int H, int num_cus);
 // strip for 2 x num_cus workgroups)
 void conv3x3_rows(const void* x, const void* w, const float* bias, const void* res, void* y, const void* zero,
                   int B, int H, int W, int C, bool relu, int strip, hipStream_t s, const void* wfrag = nullptr);
+// A whole 56x56x64 basic block, relu(conv2(relu(conv1(x))) + x), in one
+// kernel (conv3x3_block.hip): one workgroup per image, the intermediate kept
+// in LDS. wf1/wf2: fragment-order weights (stream_frag_index, K = 576).
+bool conv3x3_block_supported(int H, int W, int C);
+void conv3x3_block(const void* x, const void* wf1, const float* bias1, const void* wf2, const float* bias2, void* y,
+                   const void* zero, int B, hipStream_t s);
 // Direct 3x3/p1 conv with the input image resident in LDS and per-wave weight
 // rings (conv3x3_stream.hip): stride 1 on 28x28x128, 14x14x256, 7x7x512;
 // stride 2 on 56x56x64 -> 128 and 28x28x128 -> 256. Hin/Win are the input

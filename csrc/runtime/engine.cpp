@@ -96,6 +96,7 @@ Engine::Engine(const std::string& arch, const WeightMap& weights, int device, in
   if (const char* e = std::getenv("DMLC_STREAM_WREG")) stream_wreg_ = std::string(e) != "0";
   if (const char* e = std::getenv("DMLC_ROWS_WREG")) rows_wreg_ = std::string(e) != "0";
   if (const char* e = std::getenv("DMLC_ROWS_STRIP")) rows_strip_ = std::atoi(e);
+  if (const char* e = std::getenv("DMLC_FUSED_BLOCK")) fused_block_ = std::string(e) != "0";
   if (const char* e = std::getenv("DMLC_GRAPH_DIRECT")) graph_direct_ = std::string(e) != "0";
 
   if (arch == "resnet18")
@@ -140,6 +141,7 @@ Engine::Engine(const Engine& src, int device)
   graph_direct_ = src.graph_direct_;
   rows_wreg_ = src.rows_wreg_;
   rows_strip_ = src.rows_strip_;
+  fused_block_ = src.fused_block_;
   stream_wreg_ = src.stream_wreg_;
   stream_l1_ = src.stream_l1_;
   stream_l4s2_ = src.stream_l4s2_;
@@ -682,6 +684,33 @@ bool Engine::ds_fusable(size_t oi, int B) const {
          conv_path(c, B) == ConvPath::Stream;
 }
 
+// ops[oi], ops[oi+1] = conv1 (+ReLU) and conv2 (+identity residual, ReLU) of
+// a 56x56x64 basic block, both on the register-weight row conv, and conv1's
+// output read by nothing else: conv3x3_block runs the pair with the
+// intermediate kept in LDS (not written to its activation).
+bool Engine::block_fusable(size_t oi, int B) const {
+  if (!fused_block_ || !rows_wreg_ || oi + 1 >= ops_.size()) return false;
+  // one workgroup per image walks all 56 rows (~100 us per round of num_cus
+  // images at B=256 vs ~2 x 72 us for the two row convs, which split images
+  // into strips): only worth it with rounds that are >= ~70% full (B=1: 86 us
+  // fused vs ~30 us as strips; profiles/r2_block_kernel_stats.txt)
+  const int rounds = (B + num_cus_ - 1) / num_cus_;
+  if (10 * B < 7 * rounds * num_cus_) return false;
+  const Op& c1 = ops_[oi];
+  const Op& c2 = ops_[oi + 1];
+  if (c1.type != OpType::Conv || c2.type != OpType::Conv || c2.in != c1.out || c1.res >= 0 || c2.res != c1.in)
+    return false;
+  if (c1.side || c2.side) return false;
+  for (size_t j = 0; j < ops_.size(); ++j)
+    if (j != oi + 1 && (ops_[j].in == c1.out || ops_[j].res == c1.out)) return false;
+  const ConvLayer& L1 = convs_[c1.conv];
+  const ConvLayer& L2 = convs_[c2.conv];
+  const ActShape& is = shapes_[c1.in];
+  return L1.relu && L2.relu && L1.wf_off && L2.wf_off && conv3x3_block_supported(is.H, is.W, is.C) &&
+         L1.cout == is.C && L2.cout == is.C && !shapes_[c1.in].fp8 && !shapes_[c2.out].fp8 &&
+         conv_path(c1, B) == ConvPath::Rows && conv_path(c2, B) == ConvPath::Rows;
+}
+
 bool Engine::side_safe(int B) const {
   for (const Op& op : ops_)
     if (op.type == OpType::Conv && conv_path(op, B) == ConvPath::BigTile) return false;
@@ -744,6 +773,14 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
                    (const float*)((const uint8_t*)warena_ + L.b_off),
                    (os.f32 && logits) ? (void*)logits : acts_[op.out], L.cout, os.f32, B, L.cin, L.cout, L.npad,
                    L.relu, cs);
+          break;
+        }
+        if (cs == s && block_fusable(oi, B)) {
+          const ConvLayer& L2 = convs_[ops_[oi + 1].conv];
+          const uint8_t* wa = (const uint8_t*)warena_;
+          conv3x3_block(acts_[op.in], wa + L.wf_off, (const float*)(wa + L.b_off), wa + L2.wf_off,
+                        (const float*)(wa + L2.b_off), acts_[ops_[oi + 1].out], zero_, B, s);
+          skip = 1;
           break;
         }
         switch (conv_path(op, B)) {

@@ -122,7 +122,8 @@ class Engine {
   bool side_safe(int B) const;
   bool head_fusable(size_t oi) const;
   bool pool_fusable(size_t oi, int B) const;
-  bool ds_fusable(size_t oi, int B) const;  // ops oi, oi+1 = downsample + stride-2 stream conv1  // ops oi..oi+2 = avgpool, fc, softmax_top1 -> head_fused  // no big-tile (co-residency-dependent) conv at batch B
+  bool ds_fusable(size_t oi, int B) const;     // ops oi, oi+1 = downsample + stride-2 stream conv1
+  bool block_fusable(size_t oi, int B) const;  // ops oi, oi+1 = a layer1 basic block -> conv3x3_block
 
   std::string arch_;
   int device_ = 0;
@@ -139,8 +140,9 @@ class Engine {
   bool row_conv_ = true;    // direct row-streaming 3x3 convs where supported (env DMLC_ROW_CONV=0 disables)
   bool fp8_ = false;        // resnet50_fp8
   bool graph_direct_ = true;  // replay graphs on the caller's stream (env DMLC_GRAPH_DIRECT=0: via the engine stream)
-  bool rows_wreg_ = true;
-  int rows_strip_ = 0;        // row conv output rows per workgroup (env DMLC_ROWS_STRIP; 0 = pick)     // register-weight row conv, 2 workgroups per CU (env DMLC_ROWS_WREG=0 disables)
+  bool rows_wreg_ = true;     // register-weight row conv, 2 workgroups per CU (env DMLC_ROWS_WREG=0 disables)
+  int rows_strip_ = 0;        // row conv output rows per workgroup (env DMLC_ROWS_STRIP; 0 = pick)
+  bool fused_block_ = true;   // layer1 basic blocks as one kernel (env DMLC_FUSED_BLOCK=0 disables)
   bool stream_wreg_ = true;   // register-weight stream conv where available (env DMLC_STREAM_WREG=0 disables)
   bool stream_l1_ = false;    // stream conv for 56x56x64 layer1 (env DMLC_STREAM_L1=1; slower than conv3x3_rows)
   bool stream_l4s2_ = true;   // stream conv for 14x14x256 -> 512 / s2, register weights only (env DMLC_STREAM_L4S2=0)

@@ -179,6 +179,25 @@ def conv3x3_rows(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, re
     return y
 
 
+def conv3x3_block(x: torch.Tensor, w1_packed: torch.Tensor, b1: torch.Tensor, w2_packed: torch.Tensor,
+                  b2: torch.Tensor) -> torch.Tensor:
+    """A whole 56x56x64 basic block (conv3x3_block.hip) on NHWC bf16:
+    relu(conv2(relu(conv1(x) + b1)) + b2 + x), the intermediate kept in LDS
+    (rounded to bf16 like a stored activation). w*_packed: conv2d packed
+    weights [64, 576]."""
+    _need_cuda(x, w1_packed, b1, w2_packed, b2)
+    C = native()
+    B, H, W, Cin = x.shape
+    if not C.conv3x3_block_supported(H, W, Cin) or w1_packed.shape[0] != Cin or w2_packed.shape[0] != Cin:
+        raise ValueError("conv3x3_block: unsupported shape")
+    x = x.contiguous()
+    y = torch.empty_like(x)
+    wf1, wf2 = stream_weight_frag(w1_packed), stream_weight_frag(w2_packed)
+    C.conv3x3_block(_ptr(x), _ptr(wf1), _ptr(b1.float().contiguous()), _ptr(wf2), _ptr(b2.float().contiguous()),
+                    _ptr(y), _ptr(_zero_page(x.device)), B, _stream())
+    return y
+
+
 def stream_weight_frag(w_packed: torch.Tensor, cout: int | None = None) -> torch.Tensor:
     """Packed conv weights [Npad, K] -> the stream conv's fragment order
     [Cout/32][K/32][2][64 lanes][8]: lane l of fragment nf of channel group g,

@@ -243,6 +243,25 @@ def test_fused_pool_head_matches_unfused(gpu, monkeypatch):
     assert torch.allclose(fp, rp, rtol=1e-2, atol=1e-4) and torch.allclose(p2, rp, rtol=1e-2, atol=1e-4)
 
 
+def test_fused_block_matches_unfused(gpu, monkeypatch):
+    """ResNet18's layer1 blocks as one kernel each (conv3x3_block.hip) vs two
+    row convs per block (DMLC_FUSED_BLOCK=0): same MFMA order and bf16
+    intermediate, so the logits are bit-identical."""
+    model = build("resnet18", seed=43, randomize_bn=True)
+    sd = state_dict_f32(model)
+    g = torch.Generator().manual_seed(44)
+    # (fused only once the batch fills >= 70% of the CUs: one image per workgroup)
+    img = torch.randint(0, 256, (192, 224, 224, 3), generator=g, dtype=torch.uint8).to(gpu)
+    monkeypatch.setenv("DMLC_FUSED_BLOCK", "0")
+    ref_eng = InferenceEngine("resnet18", sd, max_batch=192)
+    monkeypatch.setenv("DMLC_FUSED_BLOCK", "1")
+    eng = InferenceEngine("resnet18", sd, max_batch=192)
+    ri, rp, rl = ref_eng.predict(img, return_logits=True)
+    fi, fp, fl = eng.predict(img, return_logits=True)
+    torch.cuda.synchronize()
+    assert torch.equal(fl, rl) and torch.equal(fi, ri)
+
+
 @pytest.mark.parametrize("B", [1, 5, 16])
 def test_alexnet_small_batch_fc_matches_reference(gpu, B, monkeypatch):
     """Query-sized AlexNet batches run the classifier on the weight-streaming

@@ -387,6 +387,30 @@ def test_conv3x3_rows(gpu, B, strip, res):
     assert torch.equal(y2, y)
 
 
+@pytest.mark.parametrize("B", [1, 3])
+def test_conv3x3_block(gpu, B):
+    """Fused layer1 basic block (conv3x3_block.hip: conv1 producer waves ->
+    LDS -> conv2 consumer waves + residual) vs torch fp32, and bit-identical
+    to two register-weight row convs (same MFMA order, bf16 intermediate)."""
+    g = torch.Generator().manual_seed(31)
+    x = torch.randn(B, 64, 56, 56, generator=g).bfloat16().float()
+    w1 = (torch.randn(64, 64, 3, 3, generator=g) / 24).bfloat16().float()
+    w2 = (torch.randn(64, 64, 3, 3, generator=g) / 24).bfloat16().float()
+    b1 = torch.randn(64, generator=g) * 0.1
+    b2 = torch.randn(64, generator=g) * 0.1
+    t = F.relu(F.conv2d(x, w1, b1, 1, 1)).bfloat16().float()
+    ref = F.relu(F.conv2d(t, w2, b2, 1, 1) + x)
+    xg = _nhwc(x).bfloat16().to(gpu)
+    wp1, wp2 = ops.pack_conv_weight(w1, device=gpu), ops.pack_conv_weight(w2, device=gpu)
+    y = ops.conv3x3_block(xg, wp1, b1.to(gpu), wp2, b2.to(gpu))
+    tg = ops.conv3x3_rows(xg, wp1, b1.to(gpu), None, True, frag=True)
+    y2 = ops.conv3x3_rows(tg, wp2, b2.to(gpu), xg, True, frag=True)
+    torch.cuda.synchronize()
+    got = _nchw(y.float().cpu())
+    assert _rel(got, ref) < 5e-3, _rel(got, ref)
+    assert torch.equal(y, y2)
+
+
 def test_preprocess_paired(gpu):
     g = torch.Generator().manual_seed(12)
     img = torch.randint(0, 256, (2, 224, 224, 3), generator=g, dtype=torch.uint8)

@@ -95,6 +95,42 @@ def test_row_conv_lds_reads_conflict_free():
             assert _b128_ways(addr) == 1, (wn, nf)
 
 
+def test_block_conv_lds_layout_conflict_free():
+    """conv3x3_block.hip: staged rows split by K half ([h][q][4 chunks],
+    chunk c of column q holding channels 8*(4h + (c ^ ((q >> 1) & 3)))):
+    the input-fragment reads of both halves (h = 1 at a fixed +3712 B) and
+    the producers' ds_write_b128 of the intermediate are conflict free; the
+    DMA staging order covers every (h, q, chunk) exactly once."""
+    W, R, Q = 56, 4, 58
+    half = Q * 64
+    slot = 2 * half
+    assert slot % 256 == 0
+    for wm in range(2):
+        for f in range(R * W // 32):
+            for kw in range(3):
+                for h in range(2):
+                    addr = []
+                    for l in range(64):
+                        fr, g = l & 15, l >> 4
+                        p = wm * (R * W // 2) + 16 * f + fr
+                        q = p % W + kw
+                        addr.append((p // W) * slot + h * half + q * 64 + ((g ^ ((q >> 1) & 3)) << 4))
+                    assert _b128_ways(addr) == 1, (wm, f, kw, h)
+            for wn in range(2):  # epilogue store of t: channels wn*32 + 8g .. +7 of pixel p
+                addr = []
+                for l in range(64):
+                    fr, g = l & 15, l >> 4
+                    p = wm * (R * W // 2) + 16 * f + fr
+                    q = p % W + 1
+                    addr.append((p // W) * slot + wn * half + q * 64 + ((g ^ ((q >> 1) & 3)) << 4))
+                assert _b128_ways(addr) == 1, (wm, f, wn)
+    seen = set()
+    for i in range(Q * 8):  # load_row: chunk i -> (h, q, c) -> source channel group
+        h, q, c = i // (Q * 4), (i >> 2) % Q, i & 3
+        seen.add((q, 4 * h + (c ^ ((q >> 1) & 3))))
+    assert seen == {(q, cg) for q in range(Q) for cg in range(8)}
+
+
 def test_stem_pool_lds_reads_conflict_free():
     """stem_pool.hip: lane (fr, g) of fragment f reads pair chunk
     16f + fr + g of a staged row; overlapping windows broadcast."""
