@@ -84,6 +84,8 @@ def main():
     ap.add_argument("--batch", type=int, default=256, help="images per GPU per step")
     ap.add_argument("--input-mode", choices=["scatter", "local"], default="scatter")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--lanes", type=int, default=2, choices=[1, 2],
+                    help="model instances per GPU on alternating streams (2: step i+1 starts under step i's tail)")
     ap.add_argument("--latency-steps", type=int, default=50, help="unpipelined steps for the batch latency")
     ap.add_argument("--latency-queries", type=int, default=200, help="batch-1 GPU queries (GPU-only latency)")
     ap.add_argument("--profile-ops", action="store_true", help="print per-op times of one eager forward")
@@ -126,7 +128,8 @@ def main():
         box = [[C.rccl_unique_id(), C.rccl_unique_id()] if rank == 0 else None]
         dist.broadcast_object_list(box, src=0)
         ids = box[0]
-    runner = C.DpRunner(eng._e, world, rank, ids[0], ids[1], B, scatter=scatter, use_graph=use_graph)
+    runner = C.DpRunner(eng._e, world, rank, ids[0], ids[1], B, scatter=scatter, use_graph=use_graph,
+                        lanes=args.lanes)
 
     # Staged input pool (two global batches of distinct synthetic images) in
     # the coordinator's HBM, or every rank's own shard in local mode.
@@ -233,6 +236,7 @@ def main():
                 "comm": "native RCCL grouped send/recv (csrc/comm), shards + answers on separate communicators",
                 "rccl_ranks": world,
                 "hipgraph": use_graph,
+                "lanes": args.lanes,
                 "baseline": "6.29 img/s = one query stream at the reference's 158.94 ms mean ResNet18 latency "
                             "(CS425MP4Report.pdf p.2; no images/s is published)",
             },

@@ -25,9 +25,15 @@ namespace {
 class DpRunner {
  public:
   DpRunner(Engine* e, int world, int rank, const std::string& id_in, const std::string& id_out, int max_per_rank,
-           bool scatter, int image_size, bool use_graph, int timeout_ms)
+           bool scatter, int image_size, bool use_graph, int timeout_ms, int lanes)
       : world_(world), rank_(rank), max_(max_per_rank), scatter_(scatter), S_(image_size), timeout_ms_(timeout_ms) {
-    w_ = dp::make_hip_worker(e, S_, S_, use_graph);
+    if (lanes < 1 || lanes > 2) throw std::invalid_argument("DpRunner: lanes must be 1 or 2");
+    if (lanes == 2) {  // a second instance of the model: consecutive steps overlap
+      lane2_ = std::make_unique<Engine>(*e, e->device());
+      lane2_->copy_weights_from(*e);
+      lane2_->reserve(std::max(e->max_batch(), max_per_rank));
+    }
+    w_ = dp::make_hip_worker(e, S_, S_, use_graph, lane2_.get());
     r_ = std::make_unique<dp::Rank>(w_.get(), max_, ib(), scatter_);
     if (world_ > 1) {
       cin_ = comm::rccl_init_rank(id_in, world_, rank_, e->device());
@@ -39,6 +45,8 @@ class DpRunner {
   }
   ~DpRunner() {
     r_.reset();
+    w_.reset();
+    lane2_.reset();
     cin_.reset();
     cout_.reset();
   }
@@ -86,6 +94,7 @@ class DpRunner {
   int world_, rank_, max_;
   bool scatter_;
   int S_, timeout_ms_;
+  std::unique_ptr<Engine> lane2_;
   std::unique_ptr<dp::Worker> w_;
   std::unique_ptr<dp::Rank> r_;
   std::unique_ptr<comm::Comm> cin_, cout_;
@@ -245,13 +254,13 @@ void bind_dp(py::module& m) {
         py::arg("fail_after") = 0, py::arg("abrupt") = false, py::arg("pipelined") = true);
   py::class_<DpRunner>(m, "DpRunner")
       .def(py::init([](Engine* e, int world, int rank, py::bytes id_in, py::bytes id_out, int max_per_rank,
-                       bool scatter, int image_size, bool use_graph, int timeout_ms) {
+                       bool scatter, int image_size, bool use_graph, int timeout_ms, int lanes) {
              return new DpRunner(e, world, rank, std::string(id_in), std::string(id_out), max_per_rank, scatter,
-                                 image_size, use_graph, timeout_ms);
+                                 image_size, use_graph, timeout_ms, lanes);
            }),
            py::arg("engine"), py::arg("world"), py::arg("rank"), py::arg("id_in"), py::arg("id_out"),
            py::arg("max_per_rank"), py::arg("scatter") = true, py::arg("image_size") = 224,
-           py::arg("use_graph") = true, py::arg("timeout_ms") = -1, py::keep_alive<1, 2>())
+           py::arg("use_graph") = true, py::arg("timeout_ms") = -1, py::arg("lanes") = 1, py::keep_alive<1, 2>())
       .def("run", &DpRunner::run, py::arg("pool"), py::arg("pool_images"), py::arg("first"), py::arg("n"),
            py::arg("pipelined") = true)
       .def("last_results", &DpRunner::last_results)

@@ -30,7 +30,7 @@ class HostWorker : public Worker {
   bool query(int) override { return true; }
   void sync(int) override {}
   void sync_all() override {}
-  void classify(const uint8_t* images, int B, int32_t* idx, float* prob) override {
+  void classify(const uint8_t* images, int B, int32_t* idx, float* prob, int) override {
     for (int b = 0; b < B; ++b) {
       const uint8_t* img = images + (size_t)b * bytes_;
       idx[b] = host_class_of(img, bytes_, classes_);
@@ -181,15 +181,17 @@ void Rank::compute(const StepPlan& p) {
   if (n > max_) throw std::invalid_argument("dp::Rank::compute: shard larger than max_per_rank");
   const bool received = scatter_ && !root() && world() > 1;
   const uint8_t* img = received ? (const uint8_t*)inbuf_[s] : p.src;
-  if (received) w_->wait(Worker::kCompute, ev_in_[s]);
-  else if (root() && p.src_event >= 0) w_->wait(Worker::kCompute, p.src_event);
-  if (out_used_[s]) w_->wait(Worker::kCompute, ev_out_[s]);  // gather(step - slots) has read the answers
+  const int lane = s % w_->lanes();  // slots alternate over the worker's compute lanes
+  const int cs = Worker::compute_stream(lane);
+  if (received) w_->wait(cs, ev_in_[s]);
+  else if (root() && p.src_event >= 0) w_->wait(cs, p.src_event);
+  if (out_used_[s]) w_->wait(cs, ev_out_[s]);  // gather(step - slots) has read the answers
   auto* blk = (uint8_t*)ans_[s];
   if (n > 0) {
     if (!img) throw std::invalid_argument("dp::Rank::compute: no images for this rank");
-    w_->classify(img, n, (int32_t*)blk, (float*)(blk + (size_t)max_ * 4));
+    w_->classify(img, n, (int32_t*)blk, (float*)(blk + (size_t)max_ * 4), lane);
   }
-  w_->record(ev_comp_[s], Worker::kCompute);
+  w_->record(ev_comp_[s], cs);
   in_used_[s] = true;
 }
 

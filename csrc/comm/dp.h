@@ -36,7 +36,9 @@ using comm::Stream;
 
 class Worker {
  public:
-  enum StreamId { kCompute = 0, kIn = 1, kOut = 2 };
+  // kCompute2: the second compute lane's stream (workers with lanes() == 2)
+  enum StreamId { kCompute = 0, kIn = 1, kOut = 2, kCompute2 = 3 };
+  static int compute_stream(int lane) { return lane == 0 ? kCompute : kCompute2; }
   virtual ~Worker() = default;
   virtual int device() const = 0;
   virtual void activate() {}                          // make this worker's device current
@@ -51,8 +53,14 @@ class Worker {
   virtual bool query(int ev) = 0;                     // event reached?
   virtual void sync(int ev) = 0;
   virtual void sync_all() = 0;
-  // images: u8 [B, H, W, 3] (worker memory); answers written on kCompute.
-  virtual void classify(const uint8_t* images, int B, int32_t* idx, float* prob) = 0;
+  // Independent compute lanes (model instances with their own activations,
+  // on their own streams): step slots alternate between them, so one step's
+  // forward may start while the previous one's tail (head kernel, graph
+  // completion) still runs.
+  virtual int lanes() const { return 1; }
+  // images: u8 [B, H, W, 3] (worker memory); answers written on
+  // compute_stream(lane).
+  virtual void classify(const uint8_t* images, int B, int32_t* idx, float* prob, int lane = 0) = 0;
   virtual void copy_d2h(void* dst, const void* src, size_t bytes, int stream_id) = 0;
   virtual void copy(void* dst, const void* src, size_t bytes, int stream_id) = 0;
   // False once the device reported an error (a lost GPU); never blocks.
@@ -67,7 +75,10 @@ std::unique_ptr<Worker> make_host_worker(int device, int H, int W, int classes =
 void host_worker_set_healthy(Worker& w, bool healthy);
 // The HIP engine on its device (csrc/comm/hip_worker.cpp): images are u8
 // [B, H, W, 3]; use_graph replays the engine's captured hipGraph.
-std::unique_ptr<Worker> make_hip_worker(Engine* engine, int H, int W, bool use_graph = true);
+// lane2: a second model instance on the same device (its own activation
+// arena, captured graphs and stream; weights copied from `engine`), owned by
+// the caller like `engine`: lanes() == 2.
+std::unique_ptr<Worker> make_hip_worker(Engine* engine, int H, int W, bool use_graph = true, Engine* lane2 = nullptr);
 int host_class_of(const uint8_t* img, size_t bytes, int classes = 1000);
 float host_prob_of(const uint8_t* img);
 

@@ -2,7 +2,10 @@
 // communication streams (shards in, answers out) created at a higher
 // priority, so the RCCL send/recv kernels of the next step are dispatched
 // promptly next to the running forward instead of queueing behind its
-// workgroups.
+// workgroups. With a second engine instance (lane 2) on its own stream,
+// consecutive steps alternate between the two: step i+1's stem fills the
+// CUs that step i's head kernel (16 workgroups) and the end of its graph
+// leave idle (~40 us per ResNet18 b256 step: profiles/r2_lanes.txt).
 #include <hip/hip_runtime.h>
 
 #include "../kernels/kernels.h"
@@ -15,19 +18,25 @@ namespace {
 
 class HipWorker : public Worker {
  public:
-  HipWorker(Engine* e, int H, int W, bool use_graph) : e_(e), dev_(e->device()), H_(H), W_(W), graph_(use_graph) {
+  HipWorker(Engine* e, int H, int W, bool use_graph, Engine* lane2)
+      : e_{e, lane2}, dev_(e->device()), H_(H), W_(W), graph_(use_graph) {
+    if (lane2 && (lane2->device() != dev_ || lane2->arch() != e->arch()))
+      throw std::invalid_argument("HipWorker: the second lane must be the same model on the same device");
     DMLC_HIP_CHECK(hipSetDevice(dev_));
     int lo = 0, hi = 0;
     DMLC_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
     DMLC_HIP_CHECK(hipStreamCreateWithPriority(&s_[kCompute], hipStreamNonBlocking, lo));
     DMLC_HIP_CHECK(hipStreamCreateWithPriority(&s_[kIn], hipStreamNonBlocking, hi));
     DMLC_HIP_CHECK(hipStreamCreateWithPriority(&s_[kOut], hipStreamNonBlocking, hi));
+    if (lane2) DMLC_HIP_CHECK(hipStreamCreateWithPriority(&s_[kCompute2], hipStreamNonBlocking, lo));
   }
   ~HipWorker() override {
     (void)hipSetDevice(dev_);
-    for (auto s : s_) (void)hipStreamSynchronize(s);
+    for (auto s : s_)
+      if (s) (void)hipStreamSynchronize(s);
     for (auto ev : evs_) (void)hipEventDestroy(ev);
-    for (auto s : s_) (void)hipStreamDestroy(s);
+    for (auto s : s_)
+      if (s) (void)hipStreamDestroy(s);
   }
   int device() const override { return dev_; }
   void activate() override { DMLC_HIP_CHECK(hipSetDevice(dev_)); }
@@ -48,6 +57,7 @@ class HipWorker : public Worker {
   }
   void dealloc_host(void* p) override { (void)hipHostFree(p); }
   Stream stream(int id) override { return s_[id]; }
+  int lanes() const override { return e_[1] ? 2 : 1; }
   int new_event() override {
     activate();
     hipEvent_t ev;
@@ -66,10 +76,12 @@ class HipWorker : public Worker {
   void sync(int ev) override { DMLC_HIP_CHECK(hipEventSynchronize(evs_.at(ev))); }
   void sync_all() override {
     activate();
-    for (auto s : s_) DMLC_HIP_CHECK(hipStreamSynchronize(s));
+    for (auto s : s_)
+      if (s) DMLC_HIP_CHECK(hipStreamSynchronize(s));
   }
-  void classify(const uint8_t* images, int B, int32_t* idx, float* prob) override {
-    e_->forward(images, B, H_, W_, idx, prob, nullptr, s_[kCompute], graph_);
+  void classify(const uint8_t* images, int B, int32_t* idx, float* prob, int lane) override {
+    if (lane < 0 || lane >= lanes()) throw std::invalid_argument("HipWorker: no such compute lane");
+    e_[lane]->forward(images, B, H_, W_, idx, prob, nullptr, s_[compute_stream(lane)], graph_);
   }
   void copy_d2h(void* dst, const void* src, size_t bytes, int sid) override {
     DMLC_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s_[sid]));
@@ -79,6 +91,7 @@ class HipWorker : public Worker {
   }
   bool healthy() override {
     for (auto s : s_) {
+      if (!s) continue;
       hipError_t e = hipStreamQuery(s);
       if (e != hipSuccess && e != hipErrorNotReady) return false;
     }
@@ -86,17 +99,17 @@ class HipWorker : public Worker {
   }
 
  private:
-  Engine* e_;
+  Engine* e_[2];
   int dev_, H_, W_;
   bool graph_;
-  hipStream_t s_[3] = {nullptr, nullptr, nullptr};
+  hipStream_t s_[4] = {nullptr, nullptr, nullptr, nullptr};
   std::vector<hipEvent_t> evs_;
 };
 
 }  // namespace
 
-std::unique_ptr<Worker> make_hip_worker(Engine* engine, int H, int W, bool use_graph) {
-  return std::make_unique<HipWorker>(engine, H, W, use_graph);
+std::unique_ptr<Worker> make_hip_worker(Engine* engine, int H, int W, bool use_graph, Engine* lane2) {
+  return std::make_unique<HipWorker>(engine, H, W, use_graph, lane2);
 }
 
 }  // namespace dp

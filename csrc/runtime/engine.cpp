@@ -159,6 +159,13 @@ Engine::Engine(const Engine& src, int device)
   init_device();
 }
 
+void Engine::copy_weights_from(const Engine& src) {
+  if (src.device_ != device_ || src.weight_bytes_ != weight_bytes_ || src.arch_ != arch_)
+    throw std::invalid_argument("Engine::copy_weights_from: not a same-device replica");
+  DMLC_HIP_CHECK(hipSetDevice(device_));
+  DMLC_HIP_CHECK(hipMemcpy(warena_, src.warena_, weight_bytes_, hipMemcpyDeviceToDevice));
+}
+
 void Engine::init_device() {
   DMLC_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
   DMLC_HIP_CHECK(hipEventCreateWithFlags(&ev_in_, hipEventDisableTiming));

@@ -68,6 +68,9 @@ class Engine {
   // weight arena is allocated but not filled: copy src.weight_arena() into
   // weight_arena() (an RCCL broadcast across the node's GPUs).
   Engine(const Engine& src, int device);
+  // Fill this replica's weight arena from `src` on the same device (a second
+  // compute lane of a dp::Worker).
+  void copy_weights_from(const Engine& src);
   ~Engine();
   Engine& operator=(const Engine&) = delete;
   void* weight_arena() const { return warena_; }
@@ -77,6 +80,7 @@ class Engine {
   int num_classes() const { return num_classes_; }
   int image_size() const { return image_size_; }
   int max_batch() const { return max_batch_; }
+  hipStream_t stream() const { return stream_; }  // the engine's own (capture) stream
   size_t weight_bytes() const { return weight_bytes_; }
   size_t activation_bytes() const { return act_bytes_; }
   double gflop_per_image() const;

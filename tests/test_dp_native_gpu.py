@@ -23,20 +23,22 @@ def _pool(n, seed):
     return torch.randint(0, 256, (n, 224, 224, 3), dtype=torch.uint8, device="cuda", generator=g)
 
 
-@pytest.mark.parametrize("pipelined", [True, False])
-def test_runner_world1_matches_engine(gpu, eng, pipelined):
+@pytest.mark.parametrize("pipelined,lanes", [(True, 1), (False, 1), (True, 2), (False, 2)])
+def test_runner_world1_matches_engine(gpu, eng, pipelined, lanes):
+    """lanes=2: odd steps run on a second model instance on its own stream
+    (weights copied on the device); the last of 4 steps is such a step."""
     C = dmlc.native()
     pool = _pool(128, 1)
     torch.cuda.synchronize()
-    r = C.DpRunner(eng._e, 1, 0, b"", b"", 64)
-    out = r.run(pool.data_ptr(), 128, 0, 3, pipelined=pipelined)
+    r = C.DpRunner(eng._e, 1, 0, b"", b"", 64, lanes=lanes)
+    out = r.run(pool.data_ptr(), 128, 0, 4, pipelined=pipelined)
     r.sync()
-    assert out["steps"] == 3 and out["images"] == 3 * 64
+    assert out["steps"] == 4 and out["images"] == 4 * 64
     if not pipelined:
-        assert len(out["step_ms"]) == 3 and all(t > 0 for t in out["step_ms"])
+        assert len(out["step_ms"]) == 4 and all(t > 0 for t in out["step_ms"])
     idx, prob = r.last_results()
-    # step 2 reads pool batch 2 % 2 = 0
-    ref_i, ref_p = eng.predict(pool[:64].contiguous(), use_graph=False)
+    # step 3 reads pool batch 3 % 2 = 1
+    ref_i, ref_p = eng.predict(pool[64:].contiguous(), use_graph=False)
     torch.cuda.synchronize()
     assert idx == ref_i.cpu().tolist()
     assert torch.allclose(torch.tensor(prob), ref_p.cpu(), atol=1e-6)
