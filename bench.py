@@ -84,7 +84,7 @@ def main():
     ap.add_argument("--batch", type=int, default=256, help="images per GPU per step")
     ap.add_argument("--input-mode", choices=["scatter", "local"], default="scatter")
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--lanes", type=int, default=2, choices=[1, 2],
+    ap.add_argument("--lanes", type=int, default=2, choices=[1, 2, 3, 4],
                     help="model instances per GPU on alternating streams (2: step i+1 starts under step i's tail)")
     ap.add_argument("--latency-steps", type=int, default=50, help="unpipelined steps for the batch latency")
     ap.add_argument("--latency-queries", type=int, default=200, help="batch-1 GPU queries (GPU-only latency)")

@@ -27,14 +27,17 @@ class DpRunner {
   DpRunner(Engine* e, int world, int rank, const std::string& id_in, const std::string& id_out, int max_per_rank,
            bool scatter, int image_size, bool use_graph, int timeout_ms, int lanes)
       : world_(world), rank_(rank), max_(max_per_rank), scatter_(scatter), S_(image_size), timeout_ms_(timeout_ms) {
-    if (lanes < 1 || lanes > 2) throw std::invalid_argument("DpRunner: lanes must be 1 or 2");
-    if (lanes == 2) {  // a second instance of the model: consecutive steps overlap
-      lane2_ = std::make_unique<Engine>(*e, e->device());
-      lane2_->copy_weights_from(*e);
-      lane2_->reserve(std::max(e->max_batch(), max_per_rank));
+    if (lanes < 1 || lanes > dp::Worker::kMaxLanes) throw std::invalid_argument("DpRunner: lanes must be 1..4");
+    std::vector<Engine*> more;
+    for (int l = 1; l < lanes; ++l) {  // further instances of the model: consecutive steps overlap
+      lanes_.push_back(std::make_unique<Engine>(*e, e->device()));
+      lanes_.back()->copy_weights_from(*e);
+      lanes_.back()->reserve(std::max(e->max_batch(), max_per_rank));
+      more.push_back(lanes_.back().get());
     }
-    w_ = dp::make_hip_worker(e, S_, S_, use_graph, lane2_.get());
-    r_ = std::make_unique<dp::Rank>(w_.get(), max_, ib(), scatter_);
+    w_ = dp::make_hip_worker(e, S_, S_, use_graph, more);
+    // one slot per lane (>= 2): that many steps in flight
+    r_ = std::make_unique<dp::Rank>(w_.get(), max_, ib(), scatter_, std::max(2, lanes));
     if (world_ > 1) {
       cin_ = comm::rccl_init_rank(id_in, world_, rank_, e->device());
       cout_ = comm::rccl_init_rank(id_out, world_, rank_, e->device());
@@ -46,7 +49,7 @@ class DpRunner {
   ~DpRunner() {
     r_.reset();
     w_.reset();
-    lane2_.reset();
+    lanes_.clear();
     cin_.reset();
     cout_.reset();
   }
@@ -94,7 +97,7 @@ class DpRunner {
   int world_, rank_, max_;
   bool scatter_;
   int S_, timeout_ms_;
-  std::unique_ptr<Engine> lane2_;
+  std::vector<std::unique_ptr<Engine>> lanes_;
   std::unique_ptr<dp::Worker> w_;
   std::unique_ptr<dp::Rank> r_;
   std::unique_ptr<comm::Comm> cin_, cout_;
@@ -149,7 +152,7 @@ class DpGroupPy {
 // ------------------------------------------------------------------ host
 py::dict dp_host_run(py::array_t<uint8_t, py::array::c_style> images, int world, int max_per_rank,
                      const std::string& mode, bool scatter, int fail_member, int64_t fail_after, bool abrupt,
-                     bool pipelined) {
+                     bool pipelined, int slots) {
   if (images.ndim() != 4 || images.shape(3) != 3) throw std::invalid_argument("images must be u8 [n,H,W,3]");
   const int64_t n = images.shape(0);
   const int H = (int)images.shape(1), W = (int)images.shape(2);
@@ -202,7 +205,7 @@ py::dict dp_host_run(py::array_t<uint8_t, py::array::c_style> images, int world,
         ts.emplace_back([&, r] {
           try {
             auto w = dp::make_host_worker(r, H, W);
-            dp::Rank rank(w.get(), max_per_rank, ib, scatter);
+            dp::Rank rank(w.get(), max_per_rank, ib, scatter, slots);
             if (world > 1) rank.attach(cin[r].get(), cout[r].get());
             else rank.attach(nullptr, nullptr);
             auto plan = [&](int64_t step, const dp::Rank& rk) {
@@ -251,7 +254,7 @@ void bind_dp(py::module& m) {
   m.def("dp_shard_counts", &dp::shard_counts);
   m.def("dp_host_run", &dp_host_run, py::arg("images"), py::arg("world"), py::arg("max_per_rank"),
         py::arg("mode") = "group", py::arg("scatter") = true, py::arg("fail_member") = -1,
-        py::arg("fail_after") = 0, py::arg("abrupt") = false, py::arg("pipelined") = true);
+        py::arg("fail_after") = 0, py::arg("abrupt") = false, py::arg("pipelined") = true, py::arg("slots") = 2);
   py::class_<DpRunner>(m, "DpRunner")
       .def(py::init([](Engine* e, int world, int rank, py::bytes id_in, py::bytes id_out, int max_per_rank,
                        bool scatter, int image_size, bool use_graph, int timeout_ms, int lanes) {

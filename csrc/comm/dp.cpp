@@ -255,7 +255,7 @@ PipelineResult run_pipeline(const std::vector<Rank*>& ranks, int64_t first, int6
   for (size_t i = 0; i < ranks.size(); ++i)
     if (ranks[i]->root()) root_i = i;
 
-  // plans of the steps in flight (at most three)
+  // plans of the steps in flight (at most slots + 1)
   std::vector<std::pair<int64_t, std::vector<StepPlan>>> live;
   auto plans_of = [&](int64_t step) -> std::vector<StepPlan>& {
     for (auto& kv : live)
@@ -317,15 +317,18 @@ PipelineResult run_pipeline(const std::vector<Rank*>& ranks, int64_t first, int6
     }
     return res;
   }
+  // steps in flight = the ranks' slot count (2: the host collects step i-1
+  // after issuing step i)
+  const int64_t depth = ranks.front()->slots();
   phase(plans_of(first), true);
   for (int64_t i = first; i < end; ++i) {
     if (i + 1 < end) phase(plans_of(i + 1), true);
     auto& ps = plans_of(i);
     for (size_t k = 0; k < ranks.size(); ++k) ranks[k]->compute(ps[k]);
     phase(ps, false);
-    if (i > first) finish(i - 1);
+    if (i - first >= depth - 1) finish(i - (depth - 1));
   }
-  finish(end - 1);
+  for (int64_t j = std::max(first, end - (depth - 1)); j < end; ++j) finish(j);
   return res;
 }
 

@@ -36,9 +36,10 @@ using comm::Stream;
 
 class Worker {
  public:
-  // kCompute2: the second compute lane's stream (workers with lanes() == 2)
+  // kCompute2..: the streams of compute lanes 1.. (workers with lanes() > 1)
   enum StreamId { kCompute = 0, kIn = 1, kOut = 2, kCompute2 = 3 };
-  static int compute_stream(int lane) { return lane == 0 ? kCompute : kCompute2; }
+  static constexpr int kMaxLanes = 4;
+  static int compute_stream(int lane) { return lane == 0 ? kCompute : kCompute2 + lane - 1; }
   virtual ~Worker() = default;
   virtual int device() const = 0;
   virtual void activate() {}                          // make this worker's device current
@@ -75,10 +76,11 @@ std::unique_ptr<Worker> make_host_worker(int device, int H, int W, int classes =
 void host_worker_set_healthy(Worker& w, bool healthy);
 // The HIP engine on its device (csrc/comm/hip_worker.cpp): images are u8
 // [B, H, W, 3]; use_graph replays the engine's captured hipGraph.
-// lane2: a second model instance on the same device (its own activation
-// arena, captured graphs and stream; weights copied from `engine`), owned by
-// the caller like `engine`: lanes() == 2.
-std::unique_ptr<Worker> make_hip_worker(Engine* engine, int H, int W, bool use_graph = true, Engine* lane2 = nullptr);
+// more: further instances of the model on the same device (their own
+// activation arenas, captured graphs and streams; weights copied from
+// `engine`), owned by the caller like `engine`: lanes() == 1 + more.size().
+std::unique_ptr<Worker> make_hip_worker(Engine* engine, int H, int W, bool use_graph = true,
+                                        std::vector<Engine*> more = {});
 int host_class_of(const uint8_t* img, size_t bytes, int classes = 1000);
 float host_prob_of(const uint8_t* img);
 
@@ -151,8 +153,9 @@ class Rank {
 
 // Issue order for the ranks one thread drives (all in one comm group per
 // phase): input(first); per step i: input(i+1), compute(i), output(i), then
-// the coordinator collects step i-1 (one step behind, so the host never waits
-// for the step it just issued).
+// the coordinator collects step i-(slots-1) (with 2 slots one step behind,
+// so the host never waits for the step it just issued). All ranks of one
+// call must have the same slot count.
 struct PipelineResult {
   int64_t steps = 0, images = 0;
   std::vector<double> step_ms;  // unpipelined runs: input issue -> answers collected, per step (coordinator)

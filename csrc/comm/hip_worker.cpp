@@ -18,17 +18,23 @@ namespace {
 
 class HipWorker : public Worker {
  public:
-  HipWorker(Engine* e, int H, int W, bool use_graph, Engine* lane2)
-      : e_{e, lane2}, dev_(e->device()), H_(H), W_(W), graph_(use_graph) {
-    if (lane2 && (lane2->device() != dev_ || lane2->arch() != e->arch()))
-      throw std::invalid_argument("HipWorker: the second lane must be the same model on the same device");
+  HipWorker(Engine* e, int H, int W, bool use_graph, std::vector<Engine*> more)
+      : dev_(e->device()), H_(H), W_(W), graph_(use_graph) {
+    e_.push_back(e);
+    for (Engine* x : more) {
+      if (!x || x->device() != dev_ || x->arch() != e->arch())
+        throw std::invalid_argument("HipWorker: every lane must be the same model on the same device");
+      e_.push_back(x);
+    }
+    if ((int)e_.size() > kMaxLanes) throw std::invalid_argument("HipWorker: too many lanes");
     DMLC_HIP_CHECK(hipSetDevice(dev_));
     int lo = 0, hi = 0;
     DMLC_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
     DMLC_HIP_CHECK(hipStreamCreateWithPriority(&s_[kCompute], hipStreamNonBlocking, lo));
     DMLC_HIP_CHECK(hipStreamCreateWithPriority(&s_[kIn], hipStreamNonBlocking, hi));
     DMLC_HIP_CHECK(hipStreamCreateWithPriority(&s_[kOut], hipStreamNonBlocking, hi));
-    if (lane2) DMLC_HIP_CHECK(hipStreamCreateWithPriority(&s_[kCompute2], hipStreamNonBlocking, lo));
+    for (size_t l = 1; l < e_.size(); ++l)
+      DMLC_HIP_CHECK(hipStreamCreateWithPriority(&s_[compute_stream((int)l)], hipStreamNonBlocking, lo));
   }
   ~HipWorker() override {
     (void)hipSetDevice(dev_);
@@ -57,7 +63,7 @@ class HipWorker : public Worker {
   }
   void dealloc_host(void* p) override { (void)hipHostFree(p); }
   Stream stream(int id) override { return s_[id]; }
-  int lanes() const override { return e_[1] ? 2 : 1; }
+  int lanes() const override { return (int)e_.size(); }
   int new_event() override {
     activate();
     hipEvent_t ev;
@@ -99,17 +105,17 @@ class HipWorker : public Worker {
   }
 
  private:
-  Engine* e_[2];
+  std::vector<Engine*> e_;
   int dev_, H_, W_;
   bool graph_;
-  hipStream_t s_[4] = {nullptr, nullptr, nullptr, nullptr};
+  hipStream_t s_[kCompute2 + kMaxLanes - 1] = {};
   std::vector<hipEvent_t> evs_;
 };
 
 }  // namespace
 
-std::unique_ptr<Worker> make_hip_worker(Engine* engine, int H, int W, bool use_graph, Engine* lane2) {
-  return std::make_unique<HipWorker>(engine, H, W, use_graph, lane2);
+std::unique_ptr<Worker> make_hip_worker(Engine* engine, int H, int W, bool use_graph, std::vector<Engine*> more) {
+  return std::make_unique<HipWorker>(engine, H, W, use_graph, std::move(more));
 }
 
 }  // namespace dp

@@ -442,7 +442,7 @@ class GpuExecutor : public Executor {
         lane2.push_back(std::make_unique<Engine>(*engines[k], devices[k]));
         lane2.back()->copy_weights_from(*engines[k]);
         lane2.back()->reserve(max_batch);
-        workers.push_back(dp::make_hip_worker(engines[k].get(), kS, kS, /*use_graph=*/true, lane2.back().get()));
+        workers.push_back(dp::make_hip_worker(engines[k].get(), kS, kS, /*use_graph=*/true, {lane2.back().get()}));
       }
       std::vector<dp::Worker*> ws;
       for (auto& x : workers) ws.push_back(x.get());

@@ -65,6 +65,20 @@ def test_threads_one_rank_per_thread(world, scatter, pipelined):
     assert all(s == out["steps"][0] for s in out["steps"])
 
 
+@pytest.mark.parametrize("world", [1, 2, 4])
+@pytest.mark.parametrize("slots", [3, 4])
+@pytest.mark.parametrize("steps", [1, 2, 3, 7])
+def test_threads_deeper_pipeline(world, slots, steps):
+    """Ranks with 3-4 slots (bench.py --lanes 3/4: that many steps in
+    flight, the host collecting step i-(slots-1)): every image answered
+    exactly once, including runs shorter than the pipeline depth."""
+    n = 4 * world * steps
+    imgs = _images(n, seed=40 + slots + steps)
+    out = C.dp_host_run(imgs, world, 4, mode="threads", slots=slots)
+    _check(out, imgs)
+    assert out["steps"] == [steps] * world
+
+
 @pytest.mark.parametrize("world", [2, 4, 8])
 @pytest.mark.parametrize("abrupt", [False, True])
 @pytest.mark.parametrize("after", [0, 1, 3])
