@@ -15,10 +15,12 @@
 //  2. each wave takes 16-class tiles: A = fc weight rows from global (16 B
 //     per lane), B = pooled^T from LDS (images in MFMA columns 0..3, the
 //     other 12 columns are zero registers), v_mfma_f32_16x16x32_bf16 over K;
-//  3. logits (+bias) to global fp32 and LDS; per image a wave reduces its
-//     split's (max, argmax, sum exp(x - max)) and stores the partial;
-//  4. the workgroup that draws the last ticket for group g combines the NS
-//     partials (cdna_hip_programming.md §6 Guideline 16 counter recipe, sc1
+//  3. logits (+bias) to global fp32 and LDS; 256/IPW threads per image reduce
+//     its split's (max, argmax, sum exp(x - max)), all images of the
+//     workgroup in one pass, and store the partial;
+//  4. the workgroup that draws the last ticket for group g loads all NS
+//     partials of its images at once and merges them with a butterfly
+//     (fixed order) (cdna_hip_programming.md §6 Guideline 16 counter recipe, sc1
 //     form: relaxed agent-scope stores of the partials -> vmcnt(0) ->
 //     barrier -> relaxed agent fetch_add; the reducer reads them with relaxed
 //     agent-scope loads; no release/acquire fences, which would write back /
@@ -37,6 +39,7 @@ namespace {
 
 constexpr int kIPW = 4;         // images per workgroup, pooling in the kernel (one wave each in the softmax)
 constexpr int kIPWPooled = 16;  // images per workgroup on a pooled input (all 16 MFMA columns)
+constexpr int kMaxSplits = 8;   // class splits (workgroups per image group); <= 256 / kIPWPooled
 
 struct HeadArgs {
   const bf16* x;      // [B, HW, C]
@@ -73,7 +76,7 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
   const int C = a.C;
   const int ldp = C + 8;  // pooled row stride (elements): rows 16 B apart in bank space
   bf16* pooled = (bf16*)smem;                                // [kIPW][ldp]
-  float* lg = (float*)(smem + kIPW * ldp * 2);               // [kIPW][tiles_per_split*16]
+  float* lg = (float*)(smem + kIPW * ldp * 2);  // [kIPW][tiles_per_split*16]
   float* red = lg;  // pooling partials [TPG][kIPW][C] fp32 (dead before lg is written)
   const int g = blockIdx.x, split = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -178,14 +181,13 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
     const bf16* w1 = w0 + 64L * a.ldw;
     for (int kc = 0; kc < C; kc += 512) {
       bf16x8 pb[16], wa[16], wb[16];
-      pb[0] = bf16x8{};
 #pragma unroll
       for (int u = 0; u < 16; ++u) {
         const int k = kc + 32 * u;
         if (k < C) {
           if (a.ko & 2) {
-            wa[u] = pb[0];
-            wb[u] = pb[0];
+            wa[u] = bf16x8{};
+            wb[u] = bf16x8{};
           } else {
             wa[u] = *(const bf16x8*)(w0 + k);
             if (two) wb[u] = *(const bf16x8*)(w1 + k);
@@ -222,48 +224,54 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
   }
   __syncthreads();
 
-  // per image (one wave each): this split's max / argmax / sum exp
+  // ---- per image: this split's (max, argmax, sum exp(x - max)). TPI
+  // threads per image (16 with 16 images per workgroup, 64 with 4), all
+  // images in one pass; ties go to the lower class.
+  constexpr int TPI = 256 / kIPW;
+  static_assert(TPI <= 64 && 64 % TPI == 0, "an image's threads must sit in one wave");
+  const int im = tid / TPI, li = tid % TPI;
+  const bool img_live = im < nimg;
   const int n_end = min(a.N, n_begin + nsplit);
-  for (int im = wave; im < nimg; im += 4) {  // 4 waves
-    const int wave = im;  // image handled by this wave in this round
-    float best = -INFINITY;
-    int bi = 0x7fffffff;
-    for (int n = n_begin + lane; n < n_end; n += 64) {
-      const float v = lg[wave * nsplit + (n - n_begin)];
+  float best = -INFINITY, s = 0.f;
+  int bi = 0x7fffffff;
+  if (img_live)
+    for (int n = n_begin + li; n < n_end; n += TPI) {
+      const float v = lg[im * nsplit + (n - n_begin)];
       if (v > best) {
         best = v;
         bi = n;
       }
     }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const float ov = __shfl_xor(best, o, 64);
-      const int oi = __shfl_xor(bi, o, 64);
-      if (ov > best || (ov == best && oi < bi)) {
-        best = ov;
-        bi = oi;
-      }
-    }
-    float s = 0.f;
-    for (int n = n_begin + lane; n < n_end; n += 64) s += __expf(lg[wave * nsplit + (n - n_begin)] - best);
-    s = wave_sum(s);
-    if (a.NS == 1) {
-      if (lane == 0) {
-        a.idx[b0 + wave] = bi;
-        a.prob[b0 + wave] = 1.f / s;
-      }
-      continue;
-    }
-    if (lane == 0) {  // relaxed agent-scope atomic stores = sc1 write-through: no release fence needed
-      float* q = (float*)(a.part + (long)(b0 + wave) * a.NS + split);
-      __hip_atomic_store(q, best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(q + 1, __int_as_float(bi), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(q + 2, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int o = TPI / 2; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(best, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    if (ov > best || (ov == best && oi < bi)) {
+      best = ov;
+      bi = oi;
     }
   }
-  if (a.NS == 1) return;
+  if (img_live)
+    for (int n = n_begin + li; n < n_end; n += TPI) s += __expf(lg[im * nsplit + (n - n_begin)] - best);
+#pragma unroll
+  for (int o = TPI / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if (a.NS == 1) {
+    if (img_live && li == 0) {
+      a.idx[b0 + im] = bi;
+      a.prob[b0 + im] = 1.f / s;
+    }
+    return;
+  }
+  if (img_live && li == 0) {  // relaxed agent-scope atomic stores = sc1 write-through: no release fence needed
+    float* q = (float*)(a.part + (long)(b0 + im) * a.NS + split);
+    __hip_atomic_store(q, best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(q + 1, __int_as_float(bi), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(q + 2, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 
-  // ---- 4. last arriver of group g combines the NS partials
+  // ---- 4. last arriver of group g combines the NS partials: lane li of an
+  // image's TPI threads loads partial li (all loads of the workgroup in
+  // flight together), then a butterfly merge (fixed order: deterministic)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   int* flag = (int*)lg;  // reuse LDS (every wave is past its lg reads: barrier above)
@@ -275,31 +283,38 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
   }
   __syncthreads();
   if (!*flag) return;
-  for (int im = wave; im < nimg; im += 4) {  // 4 waves
-  const int wave = im;
   float m = -INFINITY, sum = 0.f;
-  int bi = 0x7fffffff;
-  const float4* p = a.part + (long)(b0 + wave) * a.NS;
-  // every lane walks the NS partials in order (NS is small)
-  for (int s = 0; s < a.NS; ++s) {
-    const float* pq = (const float*)(p + s);  // sc1 loads of the sc1-stored partials
-    const float4 q = make_float4(__hip_atomic_load(pq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                                 __hip_atomic_load(pq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                                 __hip_atomic_load(pq + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), 0.f);
-    if (q.z == 0.f) continue;  // empty split (no classes)
-    const int qi = __float_as_int(q.y);
-    if (q.x > m || (q.x == m && qi < bi)) {
-      sum = sum * __expf(m - q.x) + q.z;
-      m = q.x;
-      bi = qi;
-    } else {
-      sum += q.z * __expf(q.x - m);
+  int mi = 0x7fffffff;
+  if (img_live && li < a.NS) {
+    const float* pq = (const float*)(a.part + (long)(b0 + im) * a.NS + li);  // sc1 loads of the sc1-stored partials
+    m = __hip_atomic_load(pq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    mi = __float_as_int(__hip_atomic_load(pq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    sum = __hip_atomic_load(pq + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (sum == 0.f) {  // empty split (no classes)
+      m = -INFINITY;
+      mi = 0x7fffffff;
     }
   }
-  if (lane == 0) {
-    a.idx[b0 + wave] = bi;
-    a.prob[b0 + wave] = 1.f / sum;
+#pragma unroll
+  for (int o = 1; o < TPI; o <<= 1) {
+    const float om = __shfl_xor(m, o, 64), os = __shfl_xor(sum, o, 64);
+    const int oi = __shfl_xor(mi, o, 64);
+    if (os == 0.f) continue;
+    if (sum == 0.f) {
+      m = om;
+      mi = oi;
+      sum = os;
+    } else if (om > m || (om == m && oi < mi)) {
+      sum = sum * __expf(m - om) + os;
+      m = om;
+      mi = oi;
+    } else {
+      sum += os * __expf(om - m);
+    }
   }
+  if (img_live && li == 0) {
+    a.idx[b0 + im] = mi;
+    a.prob[b0 + im] = 1.f / sum;
   }
 }
 
@@ -309,16 +324,16 @@ int head_splits_ipw(int B, int N, int num_cus, int ipw) {
   const int groups = (B + ipw - 1) / ipw;
   const int tiles = (N + 15) / 16;
   int ns = 1;
-  while (ns < 8 && (long)groups * ns * 2 <= num_cus && tiles / (ns * 2) >= 4) ns *= 2;
+  while (ns < kMaxSplits && (long)groups * ns * 2 <= num_cus && tiles / (ns * 2) >= 4) ns *= 2;
   return ns;
 }
 
 int head_splits(int B, int N, int num_cus) { return head_splits_ipw(B, N, num_cus, kIPW); }
 
 size_t head_ws_bytes(int max_batch) {
-  // partials for up to 8 splits, then the group counters at the very end
+  // partials for up to kMaxSplits splits, then the group counters at the very end
   const size_t groups = (max_batch + kIPW - 1) / kIPW;
-  return (size_t)max_batch * 8 * sizeof(float4) + ((groups * sizeof(uint32_t) + 255) & ~(size_t)255);
+  return (size_t)max_batch * kMaxSplits * sizeof(float4) + ((groups * sizeof(uint32_t) + 255) & ~(size_t)255);
 }
 
 bool head_supported(int C, int N, int ldw, int Npad) {
@@ -377,7 +392,7 @@ void head_pooled(const void* pooled, const void* w, const float* bias, int B, in
   constexpr int ipw = kIPWPooled;
   const int groups = (B + ipw - 1) / ipw;
   const int tiles = (N + 15) / 16;
-  const int ns = ns_override > 0 ? std::min(ns_override, 8) : head_splits_ipw(B, N, num_cus, ipw);
+  const int ns = ns_override > 0 ? std::min(ns_override, kMaxSplits) : head_splits_ipw(B, N, num_cus, ipw);
   const size_t part_bytes = (size_t)B * ns * sizeof(float4);
   if (part_bytes + groups * sizeof(uint32_t) > ws_bytes) throw std::invalid_argument("head_pooled: workspace too small");
   HeadArgs a;

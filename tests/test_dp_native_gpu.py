@@ -61,3 +61,24 @@ def test_group_one_gpu_ragged(gpu, eng):
     assert idx.tolist() == torch.cat(ref_i).tolist()
     assert torch.allclose(torch.from_numpy(prob), torch.cat(ref_p), atol=1e-6)
     assert g.members == [0]
+
+
+def test_python_wrappers(gpu, eng):
+    """dmlc.parallel.DataParallelRunner / NodeGroup over the same native
+    layer: answers equal a direct engine forward."""
+    from dmlc.parallel import DataParallelRunner, NodeGroup
+    pool = _pool(128, 5)
+    torch.cuda.synchronize()
+    r = DataParallelRunner(eng, 1, 0, batch_per_rank=64, lanes=2)
+    out = r.run(pool, 0, 2)
+    r.synchronize()
+    assert out["steps"] == 2
+    idx, _ = r.last_results()
+    ref_i, _ = eng.predict(pool[64:].contiguous(), use_graph=False)
+    g = NodeGroup([eng], batch_per_rank=64)
+    gi, gp, st = g.classify(pool[:100].contiguous())
+    ref_g, ref_p = eng.predict(pool[:64].contiguous(), use_graph=False)
+    torch.cuda.synchronize()
+    assert idx == ref_i.cpu().tolist()
+    assert gi[:64].tolist() == ref_g.cpu().tolist() and st["images"] == 100
+    assert torch.allclose(gp[:64], ref_p.cpu(), atol=1e-6)
