@@ -8,6 +8,8 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <map>
+
 #include "../kernels/kernels.h"
 #include "../runtime/engine.h"
 #include "../runtime/jpeg.h"
@@ -52,6 +54,14 @@ py::dict from_weight_map(const WeightMap& w) {
 }  // namespace
 
 void bind_dp(py::module& m);  // py_dp.cpp
+
+// {"fused_block": false, ...} -> EngineOptions (unknown names are errors)
+static EngineOptions engine_options(const std::map<std::string, bool>& m) {
+  EngineOptions o;
+  for (const auto& kv : m)
+    if (!o.set(kv.first, kv.second)) throw std::invalid_argument("unknown engine option: " + kv.first);
+  return o;
+}
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "dmlc native runtime: CDNA4 HIP kernels, inference engine, .ot I/O";
@@ -236,17 +246,19 @@ PYBIND11_MODULE(_C, m) {
   // ---------------------------------------------------------------- engine
   py::class_<Engine>(m, "Engine")
       .def(py::init([](const std::string& arch, const py::dict& weights, int device, int num_classes,
-                       int image_size) {
-             return new Engine(arch, to_weight_map(weights), device, num_classes, image_size);
+                       int image_size, const std::map<std::string, bool>& options) {
+             return new Engine(arch, to_weight_map(weights), device, num_classes, image_size, engine_options(options));
            }),
            py::arg("arch"), py::arg("weights"), py::arg("device") = 0, py::arg("num_classes") = 1000,
-           py::arg("image_size") = 224)
+           py::arg("image_size") = 224, py::arg("options") = std::map<std::string, bool>{})
       .def_static(
           "from_ot",
-          [](const std::string& arch, const std::string& path, int device, int num_classes,
-             int image_size) { return new Engine(arch, ot_load(path), device, num_classes, image_size); },
+          [](const std::string& arch, const std::string& path, int device, int num_classes, int image_size,
+             const std::map<std::string, bool>& options) {
+            return new Engine(arch, ot_load(path), device, num_classes, image_size, engine_options(options));
+          },
           py::arg("arch"), py::arg("path"), py::arg("device") = 0, py::arg("num_classes") = 1000,
-          py::arg("image_size") = 224)
+          py::arg("image_size") = 224, py::arg("options") = std::map<std::string, bool>{})
       .def("reserve", &Engine::reserve, py::call_guard<py::gil_scoped_release>())
       .def(
           "forward",

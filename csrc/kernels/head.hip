@@ -52,7 +52,7 @@ struct HeadArgs {
   float4* part;       // [B, NS] (max, argmax bits, sum, -)
   uint32_t* cnt;      // [ceil(B / kIPW)], zero between launches
   int B, HW, C, N, ldw, tiles_per_split, NS;
-  int ko;  // knock-out bits for timing experiments (env DMLC_HEAD_KO): 1 pool loads, 2 fc loads
+  int ko;  // knock-out bits for timing experiments (head_pooled's ko, tools/head_bench.py): 2 = no fc loads
 };
 
 // Sum of n (power of two) values in the butterfly order of avgpool_global's
@@ -367,8 +367,7 @@ void head_fused(const void* x, const void* w, const float* bias, int B, int HW, 
   a.C = C;
   a.N = N;
   a.ldw = ldw;
-  static const int ko = std::getenv("DMLC_HEAD_KO") ? std::atoi(std::getenv("DMLC_HEAD_KO")) : 0;
-  a.ko = ko;
+  a.ko = 0;
   const int c8 = C / 8, tpg = c8 >= 256 ? 1 : c8 >= 128 ? 2 : c8 >= 64 ? 4 : 8;
   const size_t lds = (size_t)kIPW * (C + 8) * 2 +
                      std::max((size_t)kIPW * a.tiles_per_split * 16 * 4, (size_t)tpg * kIPW * C * 4);

@@ -103,7 +103,7 @@ __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_s_barrier();
 }
 
-template <int NF, bool PF, bool U8>
+template <int NF, bool U8>
 __global__ __launch_bounds__(256, 2) void stem_conv_pool_kernel(
     StemArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint4 smem[];
@@ -236,16 +236,11 @@ __global__ __launch_bounds__(256, 2) void stem_conv_pool_kernel(
         const uint32_t hbase = lds_addr(hrow) + fq * 2 * kHpCol + (fr >> 3) * 16 + (fr & 7) * 2;
         const int nb_addr = ((lane + 48) & 63) << 2;  // read lane (l - 16) mod 64
         float prev3[4];  // column 16f+15 of the previous fragment, per channel block
-        bf16x8 xf[7], xg[7];
+        bf16x8 xf[7];
 #pragma unroll
         for (int s = 0; s < 7; ++s) xf[s] = *(const bf16x8*)(rbase + rows[s]);
 #pragma unroll
         for (int f = 0; f < NF; ++f) {
-          if (PF && f + 1 < NF) {  // next fragment's operands, in flight during this one's MFMAs
-#pragma unroll
-            for (int s = 0; s < 7; ++s) xg[s] = *(const bf16x8*)(rbase + rows[s] + (f + 1) * 256);
-            __builtin_amdgcn_sched_barrier(0);
-          }
           floatx4 acc[4];
 #pragma unroll
           for (int n = 0; n < 4; ++n) acc[n] = floatx4{0.f, 0.f, 0.f, 0.f};
@@ -278,7 +273,7 @@ __global__ __launch_bounds__(256, 2) void stem_conv_pool_kernel(
           if (f + 1 < NF) {
 #pragma unroll
             for (int s = 0; s < 7; ++s)
-              xf[s] = PF ? xg[s] : *(const bf16x8*)(rbase + rows[s] + (f + 1) * 256);
+              xf[s] = *(const bf16x8*)(rbase + rows[s] + (f + 1) * 256);
           }
         }
       }
@@ -376,14 +371,10 @@ void stem_launch(const void* x, const uint8_t* u8, const void* w, const float* b
   const size_t lds = u8 ? (size_t)kRingU8 * Wq * 16 + (size_t)kHp * a.PW * kHpCol + (size_t)kRingU8 * S * 3
                         : (size_t)kRing * Wq * 16 + (size_t)kHp * a.PW * kHpCol;
   const dim3 grid(B * (PH / strip));
-  static const bool pf = [] {
-    const char* e = std::getenv("DMLC_STEM_PREFETCH");
-    return e && std::string(e) == "1";
-  }();
   if (u8) {
     switch (NF) {
 #define DMLC_STEM_U8_CASE(F) \
-  case F: hipLaunchKernelGGL((stem_conv_pool_kernel<F, false, true>), grid, dim3(256), lds, s, a); break;
+  case F: hipLaunchKernelGGL((stem_conv_pool_kernel<F, true>), grid, dim3(256), lds, s, a); break;
       DMLC_STEM_U8_CASE(4)
       DMLC_STEM_U8_CASE(5)
       DMLC_STEM_U8_CASE(6)
@@ -392,10 +383,9 @@ void stem_launch(const void* x, const uint8_t* u8, const void* w, const float* b
 #undef DMLC_STEM_U8_CASE
     }
   } else {
-    switch (NF * 2 + pf) {
-#define DMLC_STEM_CASE(F)                                                                                     \
-  case 2 * F: hipLaunchKernelGGL((stem_conv_pool_kernel<F, false, false>), grid, dim3(256), lds, s, a); break; \
-  case 2 * F + 1: hipLaunchKernelGGL((stem_conv_pool_kernel<F, true, false>), grid, dim3(256), lds, s, a); break;
+    switch (NF) {
+#define DMLC_STEM_CASE(F) \
+  case F: hipLaunchKernelGGL((stem_conv_pool_kernel<F, false>), grid, dim3(256), lds, s, a); break;
       DMLC_STEM_CASE(4)
       DMLC_STEM_CASE(5)
       DMLC_STEM_CASE(6)

@@ -72,32 +72,33 @@ uint8_t f2e4m3_host(float f) {
 
 }  // namespace
 
+bool EngineOptions::set(const std::string& name, bool v) {
+  static const std::pair<const char*, bool EngineOptions::*> fields[] = {
+      {"persistent", &EngineOptions::persistent},   {"fused_stem", &EngineOptions::fused_stem},
+      {"fused_preprocess", &EngineOptions::fused_preprocess}, {"row_conv", &EngineOptions::row_conv},
+      {"rows_wreg", &EngineOptions::rows_wreg},     {"fused_block", &EngineOptions::fused_block},
+      {"stream_conv", &EngineOptions::stream_conv}, {"stream_wreg", &EngineOptions::stream_wreg},
+      {"stream_l4s2", &EngineOptions::stream_l4s2}, {"fuse_ds", &EngineOptions::fuse_ds},
+      {"bigtile", &EngineOptions::bigtile},         {"fused_pool", &EngineOptions::fused_pool},
+      {"fused_head", &EngineOptions::fused_head},   {"fc_small", &EngineOptions::fc_small},
+      {"fork_ds", &EngineOptions::fork_ds},         {"fp8_3x3", &EngineOptions::fp8_3x3},
+  };
+  for (const auto& f : fields)
+    if (name == f.first) {
+      this->*(f.second) = v;
+      return true;
+    }
+  return false;
+}
+
 Engine::Engine(const std::string& arch, const WeightMap& weights, int device, int num_classes,
-               int image_size)
-    : arch_(arch), device_(device), num_classes_(num_classes), image_size_(image_size) {
+               int image_size, const EngineOptions& options)
+    : arch_(arch), device_(device), num_classes_(num_classes), image_size_(image_size), opt_(options) {
   if (num_classes % 4 != 0) throw std::invalid_argument("num_classes must be a multiple of 4");
   DMLC_HIP_CHECK(hipSetDevice(device_));
   hipDeviceProp_t prop;
   DMLC_HIP_CHECK(hipGetDeviceProperties(&prop, device_));
   num_cus_ = prop.multiProcessorCount;
-  if (const char* e = std::getenv("DMLC_PERSISTENT")) persistent_ = std::string(e) != "0";
-  if (const char* e = std::getenv("DMLC_FUSED_STEM")) fused_stem_ = std::string(e) != "0";
-  if (const char* e = std::getenv("DMLC_ROW_CONV")) row_conv_ = std::string(e) != "0";
-  if (const char* e = std::getenv("DMLC_BIGTILE")) bigtile_ = std::string(e) != "0";
-  if (const char* e = std::getenv("DMLC_FUSED_PREPROCESS")) fused_pre_ = std::string(e) != "0";
-  if (const char* e = std::getenv("DMLC_STREAM_CONV")) stream_conv_ = std::string(e) != "0";
-  if (const char* e = std::getenv("DMLC_FORK_DS")) fork_ds_ = std::string(e) != "0";
-  if (const char* e = std::getenv("DMLC_FUSED_HEAD")) fused_head_ = std::string(e) != "0";
-  if (const char* e = std::getenv("DMLC_FUSED_POOL")) fused_pool_ = std::string(e) != "0";
-  if (const char* e = std::getenv("DMLC_FC_SMALL")) fc_small_ = std::string(e) != "0";
-  if (const char* e = std::getenv("DMLC_FUSE_DS")) fuse_ds_ = std::string(e) != "0";
-  if (const char* e = std::getenv("DMLC_STREAM_L4S2")) stream_l4s2_ = std::string(e) != "0";
-  if (const char* e = std::getenv("DMLC_STREAM_L1")) stream_l1_ = std::string(e) != "0";
-  if (const char* e = std::getenv("DMLC_STREAM_WREG")) stream_wreg_ = std::string(e) != "0";
-  if (const char* e = std::getenv("DMLC_ROWS_WREG")) rows_wreg_ = std::string(e) != "0";
-  if (const char* e = std::getenv("DMLC_ROWS_STRIP")) rows_strip_ = std::atoi(e);
-  if (const char* e = std::getenv("DMLC_FUSED_BLOCK")) fused_block_ = std::string(e) != "0";
-  if (const char* e = std::getenv("DMLC_GRAPH_DIRECT")) graph_direct_ = std::string(e) != "0";
 
   if (arch == "resnet18")
     build_resnet({2, 2, 2, 2}, false);
@@ -131,25 +132,8 @@ Engine::Engine(const Engine& src, int device)
   DMLC_HIP_CHECK(hipGetDeviceProperties(&prop, device_));
   num_cus_ = prop.multiProcessorCount;
   stem_pad_ = src.stem_pad_;
-  persistent_ = src.persistent_;
-  fused_stem_ = src.fused_stem_;
-  bigtile_ = src.bigtile_;
-  fused_pre_ = src.fused_pre_;
-  stream_conv_ = src.stream_conv_;
-  row_conv_ = src.row_conv_;
+  opt_ = src.opt_;
   fp8_ = src.fp8_;
-  graph_direct_ = src.graph_direct_;
-  rows_wreg_ = src.rows_wreg_;
-  rows_strip_ = src.rows_strip_;
-  fused_block_ = src.fused_block_;
-  stream_wreg_ = src.stream_wreg_;
-  stream_l1_ = src.stream_l1_;
-  stream_l4s2_ = src.stream_l4s2_;
-  fuse_ds_ = src.fuse_ds_;
-  fused_head_ = src.fused_head_;
-  fused_pool_ = src.fused_pool_;
-  fc_small_ = src.fc_small_;
-  fork_ds_ = src.fork_ds_;
   shapes_ = src.shapes_;
   convs_ = src.convs_;
   ops_ = src.ops_;
@@ -168,7 +152,6 @@ void Engine::copy_weights_from(const Engine& src) {
 
 void Engine::init_device() {
   DMLC_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
-  DMLC_HIP_CHECK(hipEventCreateWithFlags(&ev_in_, hipEventDisableTiming));
   DMLC_HIP_CHECK(hipEventCreateWithFlags(&ev_out_, hipEventDisableTiming));
   DMLC_HIP_CHECK(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
   fork_evs_.resize(ops_.size());
@@ -193,7 +176,6 @@ Engine::~Engine() {
   if (zero_) hipFree(zero_);
   if (dummy_idx_) hipFree(dummy_idx_);
   if (head_ws_) hipFree(head_ws_);
-  if (ev_in_) hipEventDestroy(ev_in_);
   if (ev_out_) hipEventDestroy(ev_out_);
   for (auto e : fork_evs_) hipEventDestroy(e);
   for (auto e : join_evs_) hipEventDestroy(e);
@@ -258,7 +240,7 @@ void Engine::build_resnet(const std::vector<int>& blocks, bool bottleneck) {
   const int S = image_size_;
   stem_pad_ = 3;  // packed RGB image with the 7x7/s2 stem's padding built in
   int x;
-  if (fused_stem_ && S % 32 == 0 && S >= 128 && S <= 256) {
+  if (opt_.fused_stem && S % 32 == 0 && S >= 128 && S <= 256) {
     // paired image -> one kernel for conv1 + bn1 + relu + maxpool
     const int pairs = stem_row_width(S, 3, 7, 2) / 2;
     x = add_act(ActShape{S + 6, pairs, 8, false});
@@ -356,14 +338,13 @@ void Engine::build_alexnet() {
 // 256..2048-channel block outputs and residual paths (where the bytes are:
 // layer1's 56x56x256 tensors dominate the traffic), so every 1x1 expand /
 // reduce conv and downsample reads or writes e4m3. The 3x3 convs keep bf16
-// input and output (DMLC_FP8_3X3=1 makes them e4m3 as well): as bf16 they run
+// input and output (EngineOptions::fp8_3x3 makes them e4m3 as well): as bf16 they run
 // the direct stream / row convs (LDS-resident input, register weights),
 // which beat the fp8 implicit GEMM on these shapes. The stem and layer1's
 // 64-channel inner convs stay bf16 (Cin = 64 is below the fp8 kernel's
 // 128-channel K-tile).
 void Engine::mark_fp8() {
-  bool fp8_3x3 = false;
-  if (const char* e = std::getenv("DMLC_FP8_3X3")) fp8_3x3 = std::string(e) != "0";
+  const bool fp8_3x3 = opt_.fp8_3x3;
   std::vector<bool> near_3x3(shapes_.size(), false);  // read or written by a 3x3 conv
   for (const Op& op : ops_)
     if (op.type == OpType::Conv && !convs_[op.conv].fc && convs_[op.conv].kh == 3) {
@@ -558,7 +539,7 @@ void Engine::reserve(int max_batch) {
   for (const Op& op : ops_) {
     if (op.type != OpType::Conv) continue;
     const ConvArgs a = conv_args(op, max_batch, nullptr);
-    const int cfg = bigtile_ ? conv_bigtile_pick(a, num_cus_) : -1;
+    const int cfg = opt_.bigtile ? conv_bigtile_pick(a, num_cus_) : -1;
     if (cfg >= 0) slabs = std::max(slabs, conv_bigtile_slabs(a, cfg, conv_bigtile_splits(a, cfg, num_cus_)));
   }
   if (bt_ws_) DMLC_HIP_CHECK(hipFree(bt_ws_));
@@ -622,7 +603,7 @@ ConvArgs Engine::conv_args(const Op& op, int B, float* logits) const {
   while (s > 1 && (size_t)s * M * L.npad > ws_elems_) --s;
   a.split_k = s;
   a.ws = ws_;
-  a.persistent = persistent_;
+  a.persistent = opt_.persistent;
   a.max_blocks = 2 * num_cus_;
   return a;
 }
@@ -638,18 +619,18 @@ Engine::ConvPath Engine::conv_path(const Op& op, int B) const {
   // workgroups with 49 of 64 fragment rows live: with the LDS weight ring and
   // the fused downsample 67.9 us vs 44.2 + 13.3 us as two implicit GEMMs; with
   // register weights 48.1 vs 13.2 + 46.3 us (profiles/r1_fused_ds.txt)
-  const bool l4s2 = L.stride == 2 && is.H < 28 && !(stream_l4s2_ && stream_wreg_);
-  const bool l1 = L.stride == 1 && is.C == 64 && !stream_l1_;  // layer1: conv3x3_rows unless DMLC_STREAM_L1=1
-  if (stream_conv_ && k3 && !l4s2 && !l1 && 8 * B >= num_cus_ &&
+  const bool l4s2 = L.stride == 2 && is.H < 28 && !(opt_.stream_l4s2 && opt_.stream_wreg);
+  const bool l1 = L.stride == 1 && is.C == 64;  // layer1: conv3x3_rows (the stream conv measured slower there)
+  if (opt_.stream_conv && k3 && !l4s2 && !l1 && 8 * B >= num_cus_ &&
       conv3x3_stream_supported(is.H, is.W, is.C, L.cout, L.stride))
     return ConvPath::Stream;
-  if (row_conv_ && k3 && L.stride == 1 && conv3x3_rows_supported(is.H, is.W, is.C, L.cout)) return ConvPath::Rows;
-  if (bigtile_ && conv_bigtile_pick(conv_args(op, B, nullptr), num_cus_) >= 0) return ConvPath::BigTile;
+  if (opt_.row_conv && k3 && L.stride == 1 && conv3x3_rows_supported(is.H, is.W, is.C, L.cout)) return ConvPath::Rows;
+  if (opt_.bigtile && conv_bigtile_pick(conv_args(op, B, nullptr), num_cus_) >= 0) return ConvPath::BigTile;
   return ConvPath::Igemm;
 }
 
 bool Engine::head_fusable(size_t oi) const {
-  if (!fused_head_ || oi + 2 >= ops_.size()) return false;
+  if (!opt_.fused_head || oi + 2 >= ops_.size()) return false;
   const Op& pool = ops_[oi];
   const Op& fc = ops_[oi + 1];
   const Op& sm = ops_[oi + 2];
@@ -664,7 +645,7 @@ bool Engine::head_fusable(size_t oi) const {
 // conv's epilogue writes the pooled bf16 vectors straight into the pool's
 // output activation and skips storing its own.
 bool Engine::pool_fusable(size_t oi, int B) const {
-  if (!fused_pool_ || oi + 1 >= ops_.size()) return false;
+  if (!opt_.fused_pool || oi + 1 >= ops_.size()) return false;
   const Op& c = ops_[oi];
   const Op& p = ops_[oi + 1];
   if (c.type != OpType::Conv || p.type != OpType::AvgPoolGlobal || p.in != c.out) return false;
@@ -696,7 +677,7 @@ bool Engine::ds_fusable(size_t oi, int B) const {
 // output read by nothing else: conv3x3_block runs the pair with the
 // intermediate kept in LDS (not written to its activation).
 bool Engine::block_fusable(size_t oi, int B) const {
-  if (!fused_block_ || !rows_wreg_ || oi + 1 >= ops_.size()) return false;
+  if (!opt_.fused_block || !opt_.rows_wreg || oi + 1 >= ops_.size()) return false;
   // one workgroup per image walks all 56 rows (~100 us per round of num_cus
   // images at B=256 vs ~2 x 72 us for the two row convs, which split images
   // into strips): only worth it with rounds that are >= ~70% full (B=1: 86 us
@@ -729,7 +710,7 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
   size_t ei = 0;
   if (evs) DMLC_HIP_CHECK(hipEventRecord((*evs)[ei++], s));
   // per-op event timing keeps every op on one stream
-  const bool side_ready = fork_ds_ && !evs && side_safe(B);
+  const bool side_ready = opt_.fork_ds && !evs && side_safe(B);
   std::map<int, hipEvent_t> joined;  // activation -> event its side-stream producer recorded
   int skip = 0;                      // ops already done by a fused kernel
   int skip_ds = -1;                  // downsample op left to the next (stream) conv
@@ -747,7 +728,7 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
       case OpType::Preprocess: {
         const bool paired = op.k == 1;
         // images already SxS feed the fused stem directly (stem_conv_pool_u8)
-        if (paired && fused_pre_ && Hin == image_size_ && Win == image_size_) break;
+        if (paired && opt_.fused_preprocess && Hin == image_size_ && Win == image_size_) break;
         const int Wr = paired ? 2 * shapes_[op.out].W : shapes_[op.out].W;
         preprocess_u8(images, acts_[op.out], B, Hin, Win, image_size_, op.pad, Wr, s, paired);
         break;
@@ -759,7 +740,7 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
         // block's conv1 (both read the block input; conv2 joins them through
         // the residual). Never next to a big-tile conv: its split-K slices
         // spin on each other and need their CUs.
-        if (fuse_ds_ && op.side && ds_fusable(oi, B)) {
+        if (opt_.fuse_ds && op.side && ds_fusable(oi, B)) {
           skip_ds = (int)oi;  // computed by the next op (the block's stride-2 conv1)
           break;
         }
@@ -773,7 +754,7 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
           DMLC_HIP_CHECK(hipStreamWaitEvent(s, joined[op.res], 0));
           joined.erase(op.res);
         }
-        if (L.fc && !L.fp8 && !shapes_[op.out].fp8 && fc_small_ && fc_small_supported(B, L.cin, L.cin, L.kpad)) {
+        if (L.fc && !L.fp8 && !shapes_[op.out].fp8 && opt_.fc_small && fc_small_supported(B, L.cin, L.cin, L.kpad)) {
           // query-sized batches: weight-streaming GEMV (AlexNet classifier)
           const ActShape& os = shapes_[op.out];
           fc_small(acts_[op.in], L.cin, (const uint8_t*)warena_ + L.w_off, L.kpad,
@@ -807,9 +788,9 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
                            D ? (const uint8_t*)warena_ + D->w_off : nullptr,
                            D ? (const float*)((const uint8_t*)warena_ + D->b_off) : nullptr,
                            D ? acts_[yd] : nullptr,
-                           (L.wf_off && stream_wreg_ && (!D || D->wf_off)) ? (const uint8_t*)warena_ + L.wf_off
+                           (L.wf_off && opt_.stream_wreg && (!D || D->wf_off)) ? (const uint8_t*)warena_ + L.wf_off
                                                                           : nullptr,
-                           (D && D->wf_off && stream_wreg_) ? (const uint8_t*)warena_ + D->wf_off : nullptr,
+                           (D && D->wf_off && opt_.stream_wreg) ? (const uint8_t*)warena_ + D->wf_off : nullptr,
                            fpool ? acts_[ops_[oi + 1].out] : nullptr, !fpool || trace || evs);
             pooled = fpool;
             skip_ds = -1;
@@ -819,11 +800,9 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
             conv3x3_rows(acts_[op.in], (const uint8_t*)warena_ + L.w_off,
                          (const float*)((const uint8_t*)warena_ + L.b_off), op.res >= 0 ? acts_[op.res] : nullptr,
                          acts_[op.out], zero_, B, is.H, is.W, is.C, L.relu,
-                         rows_strip_ > 0 && is.H % rows_strip_ == 0
-                             ? rows_strip_
-                             : conv3x3_rows_pick_strip(B, is.H, (L.wf_off && rows_wreg_) ? 2 * num_cus_ : num_cus_),
+                         conv3x3_rows_pick_strip(B, is.H, (L.wf_off && opt_.rows_wreg) ? 2 * num_cus_ : num_cus_),
                          cs,
-                         (L.wf_off && rows_wreg_) ? (const uint8_t*)warena_ + L.wf_off : nullptr);
+                         (L.wf_off && opt_.rows_wreg) ? (const uint8_t*)warena_ + L.wf_off : nullptr);
             break;
           case ConvPath::BigTile: {
             const ConvArgs a = conv_args(op, B, logits);
@@ -848,7 +827,7 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
       }
       case OpType::StemPool: {
         const ConvLayer& L = convs_[op.conv];
-        if (fused_pre_ && Hin == image_size_ && Win == image_size_) {
+        if (opt_.fused_preprocess && Hin == image_size_ && Win == image_size_) {
           stem_conv_pool_u8(images, (const uint8_t*)warena_ + L.w_off,
                             (const float*)((const uint8_t*)warena_ + L.b_off), acts_[op.out], B, image_size_,
                             stem_pool_pick_strip(B, shapes_[op.out].H, num_cus_), s);
@@ -913,7 +892,10 @@ void Engine::forward(const uint8_t* images, int B, int Hin, int Win, int32_t* id
   if (B > max_batch_) throw std::invalid_argument("batch exceeds reserved max_batch");
   if (!images) throw std::invalid_argument("null images");
   DMLC_HIP_CHECK(hipSetDevice(device_));
-  if (use_graph && graph_direct_) {
+  // Forwards share the activation arena: one on a different stream than the
+  // previous forward is ordered after it (an event, only then).
+  if (last_stream_valid_ && stream != last_stream_) DMLC_HIP_CHECK(hipStreamWaitEvent(stream, ev_out_, 0));
+  if (use_graph) {
     // Replays go straight onto the caller's stream: no event hop to the
     // engine's stream and back (two cross-stream waits cost ~40 us of idle
     // GPU between back-to-back forwards: profiles/r1_graph_gap.txt). The
@@ -931,49 +913,14 @@ void Engine::forward(const uint8_t* images, int B, int Hin, int Win, int32_t* id
       DMLC_HIP_CHECK(hipGraphDestroy(g));
       it = graphs_.emplace(key, ex).first;
     }
-    // Forwards share the activation arena: a replay on a different stream
-    // than the previous forward is ordered after it (an event, only then).
-    if (last_stream_valid_ && stream != last_stream_) DMLC_HIP_CHECK(hipStreamWaitEvent(stream, ev_out_, 0));
     DMLC_TRACE("engine.forward(graph)");
     DMLC_HIP_CHECK(hipGraphLaunch(it->second, stream));
-    DMLC_HIP_CHECK(hipEventRecord(ev_out_, stream));
-    last_stream_ = stream;
-    last_stream_valid_ = true;
-    return;
-  }
-  if (last_stream_valid_ && stream != last_stream_) DMLC_HIP_CHECK(hipStreamWaitEvent(stream, ev_out_, 0));
-  if (!use_graph && graph_direct_) {  // eager launches straight onto the caller's stream too
+  } else {  // eager launches straight onto the caller's stream
     DMLC_TRACE("engine.forward");
     run_ops(images, B, Hin, Win, idx, prob, logits, stream, nullptr, true);
-    DMLC_HIP_CHECK(hipEventRecord(ev_out_, stream));
-    last_stream_ = stream;
-    last_stream_valid_ = true;
-    return;
   }
-  DMLC_HIP_CHECK(hipEventRecord(ev_in_, stream));
-  DMLC_HIP_CHECK(hipStreamWaitEvent(stream_, ev_in_, 0));
-  if (use_graph) {
-    GraphKey key{images, B, Hin, Win, idx, prob, logits};
-    auto it = graphs_.find(key);
-    if (it == graphs_.end()) {
-      hipGraph_t g;
-      DMLC_HIP_CHECK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
-      run_ops(images, B, Hin, Win, idx, prob, logits, stream_, nullptr, false);
-      DMLC_HIP_CHECK(hipStreamEndCapture(stream_, &g));
-      hipGraphExec_t ex;
-      DMLC_HIP_CHECK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
-      DMLC_HIP_CHECK(hipGraphDestroy(g));
-      it = graphs_.emplace(key, ex).first;
-    }
-    DMLC_TRACE("engine.forward(graph)");
-    DMLC_HIP_CHECK(hipGraphLaunch(it->second, stream_));
-  } else {
-    DMLC_TRACE("engine.forward");
-    run_ops(images, B, Hin, Win, idx, prob, logits, stream_, nullptr, true);
-  }
-  DMLC_HIP_CHECK(hipEventRecord(ev_out_, stream_));
-  DMLC_HIP_CHECK(hipStreamWaitEvent(stream, ev_out_, 0));
-  last_stream_ = stream;  // ev_out_ marks the end of this forward
+  DMLC_HIP_CHECK(hipEventRecord(ev_out_, stream));
+  last_stream_ = stream;
   last_stream_valid_ = true;
 }
 

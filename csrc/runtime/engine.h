@@ -57,13 +57,45 @@ struct Op {
   bool side = false;  // may run on the side stream (downsample conv, joined via the residual)
 };
 
+// Kernel-path selection. Every field defaults to the fastest measured path;
+// the switches exist so tests can compare each fused / specialised path with
+// the plain one it replaces (tests/test_engine_gpu.py) and so a path can be
+// A/B-timed (profiles/). Python: InferenceEngine(..., options={"fused_block":
+// False}); the names are the field names.
+struct EngineOptions {
+  bool persistent = true;        // persistent (grid-stride) implicit-GEMM conv grids
+  bool fused_stem = true;        // conv1 + BN + ReLU + maxpool in one kernel (stem_pool.hip)
+  bool fused_preprocess = true;  // SxS u8 images straight into the fused stem (no preprocess pass)
+  bool row_conv = true;          // direct row-streaming 3x3 convs (conv3x3_rows.hip) for 56x56x64
+  bool rows_wreg = true;         // ... with register-streamed weights, 2 workgroups per CU
+  bool fused_block = true;       // a 56x56x64 basic block as one kernel (conv3x3_block.hip), B >= 0.7 x CUs
+  bool stream_conv = true;       // direct 3x3 convs with the input resident in LDS (conv3x3_stream.hip)
+  bool stream_wreg = true;       // ... with register-streamed weights where available
+  bool stream_l4s2 = true;       // ... also for 14x14x256 -> 512 / s2 (register weights only)
+  bool fuse_ds = true;           // the block's 1x1/s2 downsample inside the stride-2 stream conv1
+  bool bigtile = true;           // 8-wave big-tile split-K convs where picked (not on the ResNet18 b256 path)
+  bool fused_pool = true;        // the last conv's epilogue computes the global average pool
+  bool fused_head = true;        // avgpool + fc + softmax / top-1 in one kernel (head.hip)
+  bool fc_small = true;          // weight-streaming GEMV for fc layers at B <= 16 (fc_small.hip)
+  // downsample convs on a side stream: measured slower (the branch slows its
+  // sibling conv1 by 10-12 us and adds ~10 us of fork/join gaps per block:
+  // profiles/r1_fork_ds_timeline.txt); kept to test the side-stream path
+  bool fork_ds = false;
+  // resnet50_fp8: the 3x3 convs' inputs / outputs in e4m3 too (default bf16:
+  // the direct bf16 convs beat the fp8 implicit GEMM on those shapes)
+  bool fp8_3x3 = false;
+
+  // Set a field by name; false if there is no such option.
+  bool set(const std::string& name, bool value);
+};
+
 class Engine {
  public:
   // arch: resnet18 | resnet34 | resnet50 | alexnet | resnet50_fp8 (layers 2-4
   // on the block-scaled e4m3 MFMA: per-channel weight scales, per-tensor
   // activation scales calibrated at load time on a synthetic batch)
   Engine(const std::string& arch, const WeightMap& weights, int device, int num_classes = 1000,
-         int image_size = 224);
+         int image_size = 224, const EngineOptions& options = {});
   // A replica of `src` on `device` (same graph, packing, calibration) whose
   // weight arena is allocated but not filled: copy src.weight_arena() into
   // weight_arena() (an RCCL broadcast across the node's GPUs).
@@ -80,6 +112,7 @@ class Engine {
   int num_classes() const { return num_classes_; }
   int image_size() const { return image_size_; }
   int max_batch() const { return max_batch_; }
+  const EngineOptions& options() const { return opt_; }
   hipStream_t stream() const { return stream_; }  // the engine's own (capture) stream
   size_t weight_bytes() const { return weight_bytes_; }
   size_t activation_bytes() const { return act_bytes_; }
@@ -136,28 +169,8 @@ class Engine {
   int num_cus_ = 256;
   int max_batch_ = 0;
   int stem_pad_ = 0;
-  bool persistent_ = true;  // persistent conv grids (env DMLC_PERSISTENT=0 disables)
-  bool fused_stem_ = true;  // conv1+maxpool as one kernel (env DMLC_FUSED_STEM=0 disables)
-  bool bigtile_ = true;     // 8-wave big-tile split-K convs where supported (env DMLC_BIGTILE=0 disables)
-  bool fused_pre_ = true;   // SxS u8 images straight into the fused stem (env DMLC_FUSED_PREPROCESS=0 disables)
-  bool stream_conv_ = true; // direct 3x3 with streamed weights for 28x28x128 layers (env DMLC_STREAM_CONV=0 disables)
-  bool row_conv_ = true;    // direct row-streaming 3x3 convs where supported (env DMLC_ROW_CONV=0 disables)
-  bool fp8_ = false;        // resnet50_fp8
-  bool graph_direct_ = true;  // replay graphs on the caller's stream (env DMLC_GRAPH_DIRECT=0: via the engine stream)
-  bool rows_wreg_ = true;     // register-weight row conv, 2 workgroups per CU (env DMLC_ROWS_WREG=0 disables)
-  int rows_strip_ = 0;        // row conv output rows per workgroup (env DMLC_ROWS_STRIP; 0 = pick)
-  bool fused_block_ = true;   // layer1 basic blocks as one kernel (env DMLC_FUSED_BLOCK=0 disables)
-  bool stream_wreg_ = true;   // register-weight stream conv where available (env DMLC_STREAM_WREG=0 disables)
-  bool stream_l1_ = false;    // stream conv for 56x56x64 layer1 (env DMLC_STREAM_L1=1; slower than conv3x3_rows)
-  bool stream_l4s2_ = true;   // stream conv for 14x14x256 -> 512 / s2, register weights only (env DMLC_STREAM_L4S2=0)
-  bool fuse_ds_ = true;     // downsample inside the stride-2 stream conv1 (env DMLC_FUSE_DS=0 disables)
-  bool fused_head_ = true;  // avgpool+fc+softmax/top-1 as one kernel (env DMLC_FUSED_HEAD=0 disables)
-  bool fused_pool_ = true;  // the last conv's epilogue computes the avgpool (env DMLC_FUSED_POOL=0 disables)
-  bool fc_small_ = true;    // weight-streaming GEMV for fc layers at B <= 16 (env DMLC_FC_SMALL=0 disables)
-  // downsample convs on a side stream (env DMLC_FORK_DS=1 enables): measured
-  // slower (the branch slows its sibling conv1 by 10-12 us and adds ~10 us of
-  // fork/join gaps per block: profiles/r1_fork_ds_timeline.txt)
-  bool fork_ds_ = false;
+  EngineOptions opt_;
+  bool fp8_ = false;  // resnet50_fp8
 
   std::vector<ActShape> shapes_;
   std::vector<ConvLayer> convs_;
@@ -178,7 +191,7 @@ class Engine {
   size_t head_ws_bytes_ = 0;
 
   hipStream_t stream_ = nullptr;
-  hipEvent_t ev_in_ = nullptr, ev_out_ = nullptr;
+  hipEvent_t ev_out_ = nullptr;  // end of the last forward (on last_stream_)
   hipStream_t last_stream_ = nullptr;  // stream of the last direct graph replay (ev_out_ marks its end)
   bool last_stream_valid_ = false;
   hipStream_t side_ = nullptr;                      // downsample branch

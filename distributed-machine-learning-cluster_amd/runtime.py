@@ -23,21 +23,23 @@ class InferenceEngine:
     """Batched classifier on one GPU.
 
     weights: None (random init of ``arch`` with ``seed``), a state dict, or a
-    path to a ``.ot`` checkpoint.
+    path to a ``.ot`` checkpoint. options: kernel-path switches by name
+    (csrc/runtime/engine.h EngineOptions, e.g. {"fused_block": False}); the
+    defaults are the fastest measured paths.
     """
 
     def __init__(self, arch: str = "resnet18", weights=None, device: int = 0, max_batch: int = 256,
-                 num_classes: int = 1000, image_size: int = 224, seed: int = 0):
+                 num_classes: int = 1000, image_size: int = 224, seed: int = 0, options: dict | None = None):
         require_gpu()
         C = native()
         self.arch = arch
         self.device = torch.device("cuda", device)
         if isinstance(weights, str):
-            self._e = C.Engine.from_ot(arch, weights, device, num_classes, image_size)
+            self._e = C.Engine.from_ot(arch, weights, device, num_classes, image_size, dict(options or {}))
         else:
             sd = weights if weights is not None else state_dict_f32(build(arch, num_classes, seed=seed))
             self._e = C.Engine(arch, {k: v.detach().cpu().float().numpy() for k, v in sd.items()},
-                               device, num_classes, image_size)
+                               device, num_classes, image_size, dict(options or {}))
         self._e.reserve(max_batch)
         self.max_batch = max_batch
         self.num_classes = num_classes

@@ -103,7 +103,7 @@ def test_ot_checkpoint_engine(gpu, tmp_path):
 
 
 @pytest.mark.parametrize("B", [1, 3, 6, 64, 256])
-def test_fused_head_and_side_stream_match_unfused(gpu, monkeypatch, B):
+def test_fused_head_and_side_stream_match_unfused(gpu, B):
     """head.hip (avgpool+fc+softmax/top-1, split over classes with a ticketed
     last-arriver combine) and the downsample side-stream branch against the
     three-kernel single-stream path: pooled vectors are bit-identical, the fc
@@ -111,12 +111,8 @@ def test_fused_head_and_side_stream_match_unfused(gpu, monkeypatch, B):
     twice to check the tickets re-arm."""
     model = build("resnet18", seed=21, randomize_bn=True)
     sd = state_dict_f32(model)
-    monkeypatch.setenv("DMLC_FUSED_HEAD", "0")
-    monkeypatch.setenv("DMLC_FORK_DS", "0")
-    ref_eng = InferenceEngine("resnet18", sd, max_batch=B)
-    monkeypatch.setenv("DMLC_FUSED_HEAD", "1")
-    monkeypatch.setenv("DMLC_FORK_DS", "1")
-    eng = InferenceEngine("resnet18", sd, max_batch=B)
+    ref_eng = InferenceEngine("resnet18", sd, max_batch=B, options={"fused_head": False, "fork_ds": False})
+    eng = InferenceEngine("resnet18", sd, max_batch=B, options={"fused_head": True, "fork_ds": True})
     g = torch.Generator().manual_seed(B)
     img = torch.randint(0, 256, (B, 224, 224, 3), generator=g, dtype=torch.uint8).to(gpu)
     ri, rp, rl = ref_eng.predict(img, return_logits=True)
@@ -167,17 +163,14 @@ def test_graph_replay_on_two_streams_is_ordered(gpu):
 
 
 @pytest.mark.parametrize("B", [37, 100, 255])
-def test_fast_paths_match_plain_paths_odd_batches(gpu, monkeypatch, B):
+def test_fast_paths_match_plain_paths_odd_batches(gpu, B):
     """Every fast path at odd batch sizes (partial image groups, partial head
     groups, row-conv strips that do not fill the CUs evenly) against the
     plain paths: register weights off, downsample unfused, three-kernel head."""
     model = build("resnet18", seed=41, randomize_bn=True)
     sd = state_dict_f32(model)
-    for k in ("DMLC_STREAM_WREG", "DMLC_ROWS_WREG", "DMLC_FUSE_DS", "DMLC_FUSED_HEAD"):
-        monkeypatch.setenv(k, "0")
-    ref_eng = InferenceEngine("resnet18", sd, max_batch=B)
-    for k in ("DMLC_STREAM_WREG", "DMLC_ROWS_WREG", "DMLC_FUSE_DS", "DMLC_FUSED_HEAD"):
-        monkeypatch.setenv(k, "1")
+    plain = {k: False for k in ("stream_wreg", "rows_wreg", "fuse_ds", "fused_head", "fused_block", "fused_pool")}
+    ref_eng = InferenceEngine("resnet18", sd, max_batch=B, options=plain)
     eng = InferenceEngine("resnet18", sd, max_batch=B)
     g = torch.Generator().manual_seed(B + 1)
     img = torch.randint(0, 256, (B, 224, 224, 3), generator=g, dtype=torch.uint8).to(gpu)
@@ -220,7 +213,7 @@ def test_bench_path_b256_matches_fp32(gpu):
     assert rel < 3e-2, rel
 
 
-def test_fused_pool_head_matches_unfused(gpu, monkeypatch):
+def test_fused_pool_head_matches_unfused(gpu):
     """The last conv's fused global average pool + the pooled head (graph
     path: the layer4 activation is never stored) against the unfused
     avgpool+fc+softmax head: identical top-1, logits equal within bf16
@@ -229,9 +222,7 @@ def test_fused_pool_head_matches_unfused(gpu, monkeypatch):
     sd = state_dict_f32(model)
     g = torch.Generator().manual_seed(42)
     img = torch.randint(0, 256, (96, 224, 224, 3), generator=g, dtype=torch.uint8).to(gpu)
-    monkeypatch.setenv("DMLC_FUSED_POOL", "0")
-    ref_eng = InferenceEngine("resnet18", sd, max_batch=96)
-    monkeypatch.setenv("DMLC_FUSED_POOL", "1")
+    ref_eng = InferenceEngine("resnet18", sd, max_batch=96, options={"fused_pool": False})
     eng = InferenceEngine("resnet18", sd, max_batch=96)
     ri, rp, rl = ref_eng.predict(img, return_logits=True)
     fi, fp, fl = eng.predict(img, return_logits=True)  # graph replay: activation not stored
@@ -243,18 +234,16 @@ def test_fused_pool_head_matches_unfused(gpu, monkeypatch):
     assert torch.allclose(fp, rp, rtol=1e-2, atol=1e-4) and torch.allclose(p2, rp, rtol=1e-2, atol=1e-4)
 
 
-def test_fused_block_matches_unfused(gpu, monkeypatch):
+def test_fused_block_matches_unfused(gpu):
     """ResNet18's layer1 blocks as one kernel each (conv3x3_block.hip) vs two
-    row convs per block (DMLC_FUSED_BLOCK=0): same MFMA order and bf16
+    row convs per block (options fused_block=False): same MFMA order and bf16
     intermediate, so the logits are bit-identical."""
     model = build("resnet18", seed=43, randomize_bn=True)
     sd = state_dict_f32(model)
     g = torch.Generator().manual_seed(44)
     # (fused only once the batch fills >= 70% of the CUs: one image per workgroup)
     img = torch.randint(0, 256, (192, 224, 224, 3), generator=g, dtype=torch.uint8).to(gpu)
-    monkeypatch.setenv("DMLC_FUSED_BLOCK", "0")
-    ref_eng = InferenceEngine("resnet18", sd, max_batch=192)
-    monkeypatch.setenv("DMLC_FUSED_BLOCK", "1")
+    ref_eng = InferenceEngine("resnet18", sd, max_batch=192, options={"fused_block": False})
     eng = InferenceEngine("resnet18", sd, max_batch=192)
     ri, rp, rl = ref_eng.predict(img, return_logits=True)
     fi, fp, fl = eng.predict(img, return_logits=True)
@@ -263,10 +252,10 @@ def test_fused_block_matches_unfused(gpu, monkeypatch):
 
 
 @pytest.mark.parametrize("B", [1, 5, 16])
-def test_alexnet_small_batch_fc_matches_reference(gpu, B, monkeypatch):
+def test_alexnet_small_batch_fc_matches_reference(gpu, B):
     """Query-sized AlexNet batches run the classifier on the weight-streaming
     split-K GEMV (fc_small.hip): vs fp32 torch.nn, and vs the implicit-GEMM
-    path (DMLC_FC_SMALL=0) on the same inputs."""
+    path (options fc_small=False) on the same inputs."""
     model = build("alexnet", seed=51, randomize_bn=True)
     sd = state_dict_f32(model)
     g = torch.Generator().manual_seed(52 + B)
@@ -274,8 +263,7 @@ def test_alexnet_small_batch_fc_matches_reference(gpu, B, monkeypatch):
     eng = InferenceEngine("alexnet", sd, max_batch=B)
     idx, prob, logits = eng.predict(img.to(gpu), return_logits=True)
     i2, p2 = eng.predict(img.to(gpu))  # graph replay, no logits output
-    monkeypatch.setenv("DMLC_FC_SMALL", "0")
-    ref_eng = InferenceEngine("alexnet", sd, max_batch=B)
+    ref_eng = InferenceEngine("alexnet", sd, max_batch=B, options={"fc_small": False})
     _, _, ref_gemm = ref_eng.predict(img.to(gpu), return_logits=True)
     torch.cuda.synchronize()
     ref = _ref_logits(model, img)
@@ -284,3 +272,8 @@ def test_alexnet_small_batch_fc_matches_reference(gpu, B, monkeypatch):
     rel2 = ((logits - ref_gemm).norm() / ref_gemm.norm()).item()
     assert rel2 < 5e-3, rel2
     assert torch.equal(idx, i2) and torch.allclose(prob, p2)
+
+
+def test_unknown_engine_option_is_an_error(gpu):
+    with pytest.raises(Exception, match="unknown engine option"):
+        InferenceEngine("resnet18", max_batch=1, options={"no_such_path": True})
