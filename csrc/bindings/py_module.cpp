@@ -112,6 +112,20 @@ PYBIND11_MODULE(_C, m) {
         a.alpha = P<float>(alpha);
         a.res_scale = res_scale;
         a.out_inv_scale = out_inv_scale;
+        if (tile == kConv1x1Tile) {  // weight-stationary 1x1 conv (conv1x1.hip)
+          a.tile = -1;
+          hipDeviceProp_t prop;
+          int dev = 0;
+          DMLC_HIP_CHECK(hipGetDevice(&dev));
+          DMLC_HIP_CHECK(hipGetDeviceProperties(&prop, dev));
+          conv1x1(a, prop.multiProcessorCount, S(stream));
+          return;
+        }
+        if (tile == kConv1x1Tile + 1) {  // support query only (no launch): raises if unsupported
+          a.tile = -1;
+          if (!conv1x1_supported(a)) throw std::invalid_argument("conv1x1: unsupported shape");
+          return;
+        }
         if (tile == kConvBigTile0 + 2) {  // persistent 256x128 big tiles
           a.tile = -1;
           hipDeviceProp_t prop;
@@ -151,6 +165,7 @@ PYBIND11_MODULE(_C, m) {
         return conv_bigtile_splits(a, cfg, num_cus);
       });
   m.attr("CONV_BIGTILE0") = kConvBigTile0;
+  m.attr("CONV_1X1") = kConv1x1Tile;
   m.def("maxpool2d", [](uintptr_t x, uintptr_t y, int B, int H, int W, int C, int k, int stride,
                         int pad, uintptr_t stream) {
     maxpool2d(P<void>(x), P<void>(y), B, H, W, C, conv_out_dim(H, k, stride, pad),

@@ -1,0 +1,463 @@
+// Weight-stationary 1x1 convolution for the ResNet50 bottleneck convs
+// (conv1 reduce, conv3 expand, the 1x1/s2 downsample), bf16 or e4m3 in and
+// out, BN folded, optional residual, ReLU.
+//
+// Reference equivalent: the Bottleneck 1x1 convs of tch::vision::resnet50
+// (BASELINE config 5; forward_t per query at src/services.rs:493). At B=256
+// these convs move 100-500 MB each with K = 64..512: as 128x128 implicit-GEMM
+// tiles (conv_igemm.hip) every tile runs 1-4 K-steps between its prologue and
+// a 16-64 KB epilogue, and layer1's expand conv ran at ~1.8 TB/s (280 us vs a
+// ~100 us HBM floor: profiles/r2_resnet50_ops.txt). Here:
+//
+//  * a workgroup owns a 4*NW-channel slice of the output; each of its 4 waves
+//    keeps its NW channels' weights (NW x K, <= 16 KB) in VGPRs for the whole
+//    kernel, so weights are read once per workgroup, not once per tile;
+//  * the workgroup walks 64-pixel blocks of M = B*Ho*Wo (persistent grid,
+//    the slices of one block on the same XCD so its input is fetched from HBM
+//    once), its input rows (K bytes / 2K bytes per pixel) arriving by LDS-DMA
+//    S blocks ahead; the residual of a block is loaded (asm, counted) with its
+//    DMA and consumed in the epilogue;
+//  * D = W x X on v_mfma_f32_16x16x32_bf16 or the block-scaled
+//    v_mfma_scale_f32_16x16x128_f8f6f4 (unit scales): a lane ends with 8
+//    consecutive channels of one pixel (weight rows permuted within 32-channel
+//    groups), stored as one 16-B (bf16) / 8-B (e4m3) write.
+//
+// vmcnt retires in issue order and the compiler cannot see the asm loads, so
+// every wait is explicit: per block a wave issues RES (residual loads), DMA
+// (S-1 blocks ahead; dummy zero-page loads past the end keep the count
+// uniform) and ST (stores); the block's DMA has landed when at most
+// (S-1)(ST+RES+DMA) newer operations are outstanding, its residual when at
+// most DMA are. Only M % 64 == 0 is supported (no partial blocks, so every
+// wave issues the same instruction counts).
+#include "common.h"
+#include "kernels.h"
+
+#include <algorithm>
+#include <type_traits>
+
+namespace dmlc {
+
+namespace {
+
+typedef int v8i __attribute__((ext_vector_type(8)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+
+// LDS reads/writes of this wave done, then the workgroup barrier (no
+// compiler fence: it would add a vmcnt(0) and drain the DMA pipeline)
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+}
+
+// Make the compiler treat v as (re)defined here, after a preceding wait:
+// uses of an asm-loaded register cannot be hoisted above the wait.
+template <typename T>
+__device__ __forceinline__ void pin(T& v) {
+  asm volatile("" : "+v"(v));
+}
+
+
+__device__ __forceinline__ void fp8x4_to_f32(uint32_t u, float* f) {
+  f[0] = __builtin_amdgcn_cvt_f32_fp8((int)u, 0);
+  f[1] = __builtin_amdgcn_cvt_f32_fp8((int)u, 1);
+  f[2] = __builtin_amdgcn_cvt_f32_fp8((int)u, 2);
+  f[3] = __builtin_amdgcn_cvt_f32_fp8((int)u, 3);
+}
+__device__ __forceinline__ uint32_t f32x4_to_fp8(const float* f) {
+  float c[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) c[i] = fminf(fmaxf(f[i], -448.f), 448.f);
+  int v = __builtin_amdgcn_cvt_pk_fp8_f32(c[0], c[1], 0, false);
+  v = __builtin_amdgcn_cvt_pk_fp8_f32(c[2], c[3], v, true);
+  return (uint32_t)v;
+}
+
+// Counted global loads the compiler does not track (no implicit vmcnt(0)
+// waits in front of their uses: the kernel waits for them itself).
+__device__ __forceinline__ u32x2 gload8(const void* p) {
+  u32x2 v;
+  asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+__device__ __forceinline__ u32x4 gload16(const void* p) {
+  u32x4 v;
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+__device__ __forceinline__ uint32_t gload4(const void* p) {
+  uint32_t v;
+  asm volatile("global_load_dword %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+
+// Chunk swizzle of the staged input rows (16-B chunks, RB bytes per pixel):
+// every 16-lane group of the B-fragment reads hits 16 distinct bank groups
+// (tests/test_layouts_cpu.py::test_conv1x1_lds_conflict_free).
+template <int RB, bool IN8>
+__device__ __forceinline__ int swz1(int p) {
+  if constexpr (RB == 128) return IN8 ? ((((p & 7) << 1) | ((p >> 3) & 1)) & 7) : (p & 7);
+  else return p & 15;
+}
+
+struct C1Args {
+  const void* x;       // [B, H, W, K] bf16 or e4m3
+  const void* w;       // [Npad, Kpad] bf16 or e4m3 (BN folded; e4m3 with per-row scales)
+  const float* bias;   // [Npad]
+  const float* alpha;  // e4m3 input: [Npad] = s_in * s_w[n]
+  const void* res;     // [M, N] (the output's dtype) or null
+  void* y;             // [M, N]
+  const void* zero;    // >= 16 zero bytes
+  int B, H, W, Ho, Wo, N, Kpad;
+  int nslices, nblocks;
+  int relu;
+  float res_scale, out_inv_scale;
+};
+
+constexpr int kBM = 64;  // pixels per block
+
+template <bool IN8, bool OUT8, int RB, int NW, int S2, bool RES, int S>
+__global__ __launch_bounds__(256, 2) void conv1x1_kernel(C1Args a) {
+  constexpr int CPR = RB / 16;              // 16-B chunks per staged pixel row
+  constexpr int KS = IN8 ? CPR / 8 : CPR / 4;  // K steps (128 e4m3 / 32 bf16 k each)
+  constexpr int NF = NW / 16;               // N fragments per wave
+  constexpr int NG = NF >= 2 ? NF / 2 : 1;  // 8-channel (or, NF = 1, 4-channel) groups per lane
+  constexpr int CPL = NF >= 2 ? 8 : 4;      // channels per lane per group
+  constexpr int NPF = kBM / 16;             // pixel fragments per block
+  constexpr int STAGE = kBM * RB;
+  constexpr int DT = STAGE / 16 / 64 / 4;   // DMA instructions per wave per block
+  constexpr int RT = RES ? NPF * NG : 0;    // residual loads per wave per block
+  constexpr int ST = NPF * NG;              // stores per wave per block
+  constexpr int N1 = (S - 1) * (ST + RT + DT);
+  static_assert(DT >= 1 && KS >= 1, "tile");
+  using WFrag = typename std::conditional<IN8, v8i, bf16x8>::type;
+
+  extern __shared__ __attribute__((aligned(16))) uint4 smem[];
+  char* stages = (char*)smem;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, g = lane >> 4;
+  // block id -> (slice, first block): the slices of one M block on one XCD
+  const int wgid = blockIdx.x;
+  const int xcd = wgid & 7, r = wgid >> 3;
+  const int slice = r % a.nslices;
+  const int mstart = (r / a.nslices) * 8 + xcd;
+  const int mstride = (int)gridDim.x / a.nslices;
+  const int n0 = slice * 4 * NW + wave * NW;  // this wave's first channel
+
+  // ---- weights -> VGPRs: fragment f row rr = channel ch(f, rr); lane (rr, g)
+  // holds k = 32*ks + 8g .. +8 (bf16) / 128*ks + 32g .. +32 (e4m3)
+  auto ch_of = [](int f, int rr) {
+    if constexpr (NF >= 2) return 32 * (f >> 1) + 8 * (rr >> 2) + 4 * (f & 1) + (rr & 3);
+    else return rr;
+  };
+  WFrag wf[NF][KS];
+  {
+    const uint8_t* wb = (const uint8_t*)a.w;
+    const int esz = IN8 ? 1 : 2;
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      const uint8_t* row = wb + (size_t)(n0 + ch_of(f, fr)) * a.Kpad * esz;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        if constexpr (IN8) {
+          const uint4 lo = *(const uint4*)(row + ks * 128 + g * 32);
+          const uint4 hi = *(const uint4*)(row + ks * 128 + g * 32 + 16);
+          wf[f][ks] = v8i{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+        } else {
+          wf[f][ks] = *(const bf16x8*)(row + (ks * 32 + g * 8) * 2);
+        }
+      }
+    }
+  }
+  // this lane's channels: group j = n0 + 32j + 8g .. +7 (NF = 1: n0 + 4g .. +3)
+  float bs[NG][CPL], al[NG][CPL];
+#pragma unroll
+  for (int j = 0; j < NG; ++j)
+#pragma unroll
+    for (int e = 0; e < CPL; ++e) {
+      const int n = n0 + (NF >= 2 ? 32 * j + 8 * g : 4 * g) + e;
+      bs[j][e] = a.bias[n];
+      al[j][e] = IN8 ? a.alpha[n] : 1.f;
+    }
+
+  // ---- staging: block m -> stage buffer (pixel p's RB bytes, chunk-swizzled)
+  const long rowstride_in = (long)CPR * 16;
+  auto pixel_src = [&](int m) -> const uint8_t* {  // input pixel of output pixel m
+    if constexpr (S2 == 1) {
+      return (const uint8_t*)a.x + (long)m * rowstride_in;
+    } else {
+      const int hw = a.Ho * a.Wo;
+      const int b = m / hw, rem = m - b * hw, oh = rem / a.Wo, ow = rem - oh * a.Wo;
+      return (const uint8_t*)a.x + (((long)b * a.H + 2 * oh) * a.W + 2 * ow) * rowstride_in;
+    }
+  };
+  auto issue_dma = [&](int blk, int st) __attribute__((always_inline)) {
+    char* dst = stages + st * STAGE;
+    const bool live = blk < a.nblocks;
+#pragma unroll
+    for (int d = 0; d < DT; ++d) {
+      const int i = (d * 4 + wave) * 64 + lane;  // chunk index in the stage
+      const int p = i / CPR, pc = i % CPR;
+      const int lc = pc ^ swz1<RB, IN8>(p);  // logical chunk stored at physical pc
+      const void* src = live ? (const void*)(pixel_src(blk * kBM + p) + lc * 16) : a.zero;
+      dma16(src, dst + (d * 4 + wave) * 1024);
+    }
+  };
+  // residual of block blk: lane (fr, g), pixel fragment pf, group j
+  const int out_esz = OUT8 ? 1 : 2;
+  auto res_ptr = [&](int blk, int pf, int j) {
+    const long m = (long)blk * kBM + pf * 16 + fr;
+    const int n = n0 + (NF >= 2 ? 32 * j + 8 * g : 4 * g);
+    return (const uint8_t*)a.res + (m * a.N + n) * out_esz;
+  };
+  typedef typename std::conditional<OUT8, typename std::conditional<(CPL == 8), u32x2, uint32_t>::type,
+                                    typename std::conditional<(CPL == 8), u32x4, u32x2>::type>::type RV;
+  RV rv[NPF][NG];
+
+  // prologue: blocks 0 .. S-2 of this workgroup
+#pragma unroll
+  for (int s = 0; s < S - 1; ++s) issue_dma(mstart + s * mstride, s);
+
+  int it = 0;
+  for (int blk = mstart; blk < a.nblocks; blk += mstride, ++it) {
+    const int st = it % S;
+    lds_barrier();  // every wave is done with stage (it-1) % S: the DMA below reuses it
+    if constexpr (RES) {
+#pragma unroll
+      for (int pf = 0; pf < NPF; ++pf)
+#pragma unroll
+        for (int j = 0; j < NG; ++j) {
+          const void* p = res_ptr(blk, pf, j);
+          if constexpr (OUT8 && CPL == 8) rv[pf][j] = gload8(p);
+          else if constexpr (OUT8) rv[pf][j] = gload4(p);
+          else if constexpr (CPL == 8) rv[pf][j] = gload16(p);
+          else rv[pf][j] = gload8(p);
+        }
+    }
+    issue_dma(blk + (S - 1) * mstride, (it + S - 1) % S);
+    if (it < S - 1) vm_wait<DT>();  // prologue blocks: only this DMA may stay in flight
+    else vm_wait<N1>();
+    lds_barrier();  // every wave's share of block blk's rows has landed
+
+    // ---- MFMAs: acc[pf][f] = D[channel ch(f, 4g+i)][pixel 16pf + fr]
+    const char* sb = stages + st * STAGE;
+    floatx4 acc[NPF][NF];
+#pragma unroll
+    for (int pf = 0; pf < NPF; ++pf)
+#pragma unroll
+      for (int f = 0; f < NF; ++f) acc[pf][f] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      WFrag xb[NPF];
+#pragma unroll
+      for (int pf = 0; pf < NPF; ++pf) {
+        const int p = pf * 16 + fr;
+        const char* row = sb + p * RB;
+        if constexpr (IN8) {
+          const int c0 = ks * 8 + 2 * g;
+          const uint4 lo = *(const uint4*)(row + ((c0 ^ swz1<RB, IN8>(p)) << 4));
+          const uint4 hi = *(const uint4*)(row + (((c0 + 1) ^ swz1<RB, IN8>(p)) << 4));
+          xb[pf] = v8i{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+        } else {
+          xb[pf] = *(const bf16x8*)(row + (((ks * 4 + g) ^ swz1<RB, IN8>(p)) << 4));
+        }
+      }
+#pragma unroll
+      for (int pf = 0; pf < NPF; ++pf)
+#pragma unroll
+        for (int f = 0; f < NF; ++f) {
+          if constexpr (IN8)
+            acc[pf][f] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(wf[f][ks], xb[pf], acc[pf][f], 0, 0, 0,
+                                                                           127, 0, 127);
+          else
+            acc[pf][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[f][ks], xb[pf], acc[pf][f], 0, 0, 0);
+        }
+    }
+
+    // ---- epilogue
+    if constexpr (RES) {
+      vm_wait<DT>();  // this block's residual (only the DMA issued after it may be in flight)
+#pragma unroll
+      for (int pf = 0; pf < NPF; ++pf)
+#pragma unroll
+        for (int j = 0; j < NG; ++j) pin(rv[pf][j]);
+    }
+#pragma unroll
+    for (int pf = 0; pf < NPF; ++pf) {
+      const long m = (long)blk * kBM + pf * 16 + fr;
+#pragma unroll
+      for (int j = 0; j < NG; ++j) {
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < CPL; ++e) {
+          const float raw = NF >= 2 ? acc[pf][2 * j + (e >> 2)][e & 3] : acc[pf][0][e];
+          v[e] = raw * al[j][e] + bs[j][e];
+        }
+        if constexpr (RES) {
+          float rf[8];
+          if constexpr (OUT8) {
+            if constexpr (CPL == 8) {
+              fp8x4_to_f32(rv[pf][j].x, rf);
+              fp8x4_to_f32(rv[pf][j].y, rf + 4);
+            } else {
+              fp8x4_to_f32(rv[pf][j], rf);
+            }
+#pragma unroll
+            for (int e = 0; e < CPL; ++e) v[e] += rf[e] * a.res_scale;
+          } else {
+            if constexpr (CPL == 8) {
+              const u32x4 q = rv[pf][j];
+              unpack8(make_uint4(q.x, q.y, q.z, q.w), rf);
+            } else {
+              const u32x2 q = rv[pf][j];
+              rf[0] = __uint_as_float(q.x << 16);
+              rf[1] = __uint_as_float(q.x & 0xffff0000u);
+              rf[2] = __uint_as_float(q.y << 16);
+              rf[3] = __uint_as_float(q.y & 0xffff0000u);
+            }
+#pragma unroll
+            for (int e = 0; e < CPL; ++e) v[e] += rf[e];
+          }
+        }
+        if (a.relu) {
+#pragma unroll
+          for (int e = 0; e < CPL; ++e) v[e] = fmaxf(v[e], 0.f);
+        }
+        const int n = n0 + (NF >= 2 ? 32 * j + 8 * g : 4 * g);
+        uint8_t* yp = (uint8_t*)a.y + (m * a.N + n) * out_esz;
+        if constexpr (OUT8) {
+#pragma unroll
+          for (int e = 0; e < CPL; ++e) v[e] *= a.out_inv_scale;
+          if constexpr (CPL == 8) *(uint2*)yp = make_uint2(f32x4_to_fp8(v), f32x4_to_fp8(v + 4));
+          else *(uint32_t*)yp = f32x4_to_fp8(v);
+        } else {
+          if constexpr (CPL == 8) *(uint4*)yp = pack8(v);
+          else *(uint2*)yp = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+        }
+      }
+    }
+  }
+  vm_wait<0>();  // no LDS-DMA may outlive the workgroup
+}
+
+// (channels per wave, staged row bytes) for a shape, or {0, 0}
+struct Pick {
+  int nw = 0, rb = 0;
+};
+
+Pick pick(const ConvArgs& a) {
+  Pick p;
+  if (a.KH != 1 || a.KW != 1 || a.pad != 0 || (a.stride != 1 && a.stride != 2) || a.stem || a.out_f32 ||
+      a.split_k > 1)
+    return p;
+  const int esz = a.in_fp8 ? 1 : 2;
+  if (a.Cin != a.Kpad || a.N != a.Npad || a.ldo != a.N) return p;
+  const int rb = a.Cin * esz;
+  if (rb != 128 && rb != 256 && rb != 512) return p;
+  if (a.in_fp8 && a.Cin % 128) return p;
+  const long M = (long)a.B * a.Ho * a.Wo;
+  if (M % kBM) return p;
+  for (int nw : {64, 32, 16}) {
+    if (a.N % (4 * nw)) continue;
+    if ((long)nw * rb > 16 * 1024) continue;  // weights of a wave: <= 64 VGPRs
+    p.nw = nw;
+    p.rb = rb;
+    return p;
+  }
+  return p;
+}
+
+struct L1 {
+  dim3 grid;
+  size_t lds;
+  hipStream_t s;
+  C1Args c;
+  int nw, rb;
+};
+
+template <bool IN8, bool OUT8, int RB, int S2, bool RES>
+void launch_nw(const L1& l) {
+  constexpr int S = RB <= 256 ? 3 : 2;
+  if constexpr (64 * RB <= 16384) {
+    if (l.nw == 64) {
+      hipLaunchKernelGGL((conv1x1_kernel<IN8, OUT8, RB, 64, S2, RES, S>), l.grid, dim3(256), l.lds, l.s, l.c);
+      return;
+    }
+  }
+  if constexpr (32 * RB <= 16384) {
+    if (l.nw == 32) {
+      hipLaunchKernelGGL((conv1x1_kernel<IN8, OUT8, RB, 32, S2, RES, S>), l.grid, dim3(256), l.lds, l.s, l.c);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((conv1x1_kernel<IN8, OUT8, RB, 16, S2, RES, S>), l.grid, dim3(256), l.lds, l.s, l.c);
+}
+
+template <bool IN8, bool OUT8, int S2, bool RES>
+void launch_rb(const L1& l) {
+  if (l.rb == 128) launch_nw<IN8, OUT8, 128, S2, RES>(l);
+  else if (l.rb == 256) launch_nw<IN8, OUT8, 256, S2, RES>(l);
+  else launch_nw<IN8, OUT8, 512, S2, RES>(l);
+}
+
+}  // namespace
+
+bool conv1x1_supported(const ConvArgs& a) { return pick(a).nw > 0; }
+
+void conv1x1(const ConvArgs& a, int num_cus, hipStream_t s) {
+  const Pick pk = pick(a);
+  if (!pk.nw) throw std::invalid_argument("conv1x1: unsupported shape");
+  if (!a.x || !a.w || !a.bias || !a.y || !a.zero || (a.in_fp8 && !a.alpha) ||
+      (((uintptr_t)a.x | (uintptr_t)a.w | (uintptr_t)a.y | (uintptr_t)a.res) & 15))
+    throw std::invalid_argument("conv1x1: null / misaligned operand");
+  C1Args c;
+  c.x = a.x;
+  c.w = a.w;
+  c.bias = a.bias;
+  c.alpha = a.alpha;
+  c.res = a.res;
+  c.y = a.y;
+  c.zero = a.zero;
+  c.B = a.B;
+  c.H = a.H;
+  c.W = a.W;
+  c.Ho = a.Ho;
+  c.Wo = a.Wo;
+  c.N = a.N;
+  c.Kpad = a.Kpad;
+  c.relu = a.relu;
+  c.res_scale = a.res_scale;
+  c.out_inv_scale = a.out_inv_scale;
+  c.nslices = a.N / (4 * pk.nw);
+  c.nblocks = (int)((long)a.B * a.Ho * a.Wo / kBM);
+  // persistent grid: a multiple of 8 * nslices, about 2 workgroups per CU
+  const int q = std::max(1, std::min((c.nblocks + 7) / 8, (2 * num_cus) / (8 * c.nslices)));
+  const dim3 grid(8 * c.nslices * q), block(256);
+  const size_t lds = (size_t)(pk.rb <= 256 ? 3 : 2) * kBM * pk.rb;
+  const bool res = a.res != nullptr;
+  const int key = (a.in_fp8 ? 1 : 0) | (a.out_fp8 ? 2 : 0) | (res ? 4 : 0) | (a.stride == 2 ? 8 : 0);
+  const L1 l{grid, lds, s, c, pk.nw, pk.rb};
+  // the (in, out, residual, stride) combinations ResNet50 needs
+  switch (key) {
+    case 0: launch_rb<false, false, 1, false>(l); break;  // bf16 -> bf16 (reduce convs of the bf16 model)
+    case 4: launch_rb<false, false, 1, true>(l); break;   // bf16 -> bf16 + residual (bf16 expand)
+    case 8: launch_rb<false, false, 2, false>(l); break;  // bf16 downsample
+    case 1: launch_rb<true, false, 1, false>(l); break;   // e4m3 -> bf16 (fp8 reduce convs)
+    case 2: launch_rb<false, true, 1, false>(l); break;   // bf16 -> e4m3 (layer1.0 downsample)
+    case 6: launch_rb<false, true, 1, true>(l); break;    // bf16 -> e4m3 + residual (fp8 expand)
+    case 11: launch_rb<true, true, 2, false>(l); break;   // e4m3 -> e4m3 / s2 (fp8 downsample)
+    case 3: launch_rb<true, true, 1, false>(l); break;    // e4m3 -> e4m3
+    default: throw std::invalid_argument("conv1x1: unsupported dtype / residual / stride combination");
+  }
+  DMLC_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace dmlc

@@ -82,6 +82,7 @@ bool EngineOptions::set(const std::string& name, bool v) {
       {"bigtile", &EngineOptions::bigtile},         {"fused_pool", &EngineOptions::fused_pool},
       {"fused_head", &EngineOptions::fused_head},   {"fc_small", &EngineOptions::fc_small},
       {"fork_ds", &EngineOptions::fork_ds},         {"fp8_3x3", &EngineOptions::fp8_3x3},
+      {"conv1x1", &EngineOptions::conv1x1},
   };
   for (const auto& f : fields)
     if (name == f.first) {
@@ -625,6 +626,11 @@ Engine::ConvPath Engine::conv_path(const Op& op, int B) const {
       conv3x3_stream_supported(is.H, is.W, is.C, L.cout, L.stride))
     return ConvPath::Stream;
   if (opt_.row_conv && k3 && L.stride == 1 && conv3x3_rows_supported(is.H, is.W, is.C, L.cout)) return ConvPath::Rows;
+  if (opt_.conv1x1 && !L.fc && L.kh == 1 && L.kw == 1) {
+    ConvArgs a = conv_args(op, B, nullptr);
+    a.split_k = 1;
+    if (conv1x1_supported(a)) return ConvPath::OneByOne;
+  }
   if (opt_.bigtile && conv_bigtile_pick(conv_args(op, B, nullptr), num_cus_) >= 0) return ConvPath::BigTile;
   return ConvPath::Igemm;
 }
@@ -804,6 +810,12 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
                          cs,
                          (L.wf_off && opt_.rows_wreg) ? (const uint8_t*)warena_ + L.wf_off : nullptr);
             break;
+          case ConvPath::OneByOne: {
+            ConvArgs a = conv_args(op, B, logits);
+            a.split_k = 1;
+            conv1x1(a, num_cus_, cs);
+            break;
+          }
           case ConvPath::BigTile: {
             const ConvArgs a = conv_args(op, B, logits);
             const int bt = conv_bigtile_pick(a, num_cus_);

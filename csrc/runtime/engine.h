@@ -74,6 +74,7 @@ struct EngineOptions {
   bool stream_l4s2 = true;       // ... also for 14x14x256 -> 512 / s2 (register weights only)
   bool fuse_ds = true;           // the block's 1x1/s2 downsample inside the stride-2 stream conv1
   bool bigtile = true;           // 8-wave big-tile split-K convs where picked (not on the ResNet18 b256 path)
+  bool conv1x1 = true;           // weight-stationary 1x1 convs (conv1x1.hip: ResNet50 bottlenecks)
   bool fused_pool = true;        // the last conv's epilogue computes the global average pool
   bool fused_head = true;        // avgpool + fc + softmax / top-1 in one kernel (head.hip)
   bool fc_small = true;          // weight-streaming GEMV for fc layers at B <= 16 (fc_small.hip)
@@ -154,7 +155,7 @@ class Engine {
   void run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* idx, float* prob,
                float* logits, hipStream_t s, std::vector<hipEvent_t>* evs, bool trace);
   ConvArgs conv_args(const Op& op, int B, float* logits) const;
-  enum class ConvPath { Stream, Rows, BigTile, Igemm };
+  enum class ConvPath { Stream, Rows, OneByOne, BigTile, Igemm };
   ConvPath conv_path(const Op& op, int B) const;
   bool side_safe(int B) const;
   bool head_fusable(size_t oi) const;

@@ -122,3 +122,72 @@ def test_conv2d_bf16_in_fp8_out(gpu):
     torch.cuda.synchronize()
     got = _nchw(y.float().cpu() * so)
     assert ((got - ref).norm() / ref.norm()).item() < 0.04
+
+
+@pytest.mark.parametrize("B,H,Cin,Cout,s,in8,out8,res", [
+    (1, 56, 64, 256, 1, False, True, True),     # layer1 expand (bf16 -> e4m3 + e4m3 residual)
+    (1, 56, 64, 256, 1, False, True, False),    # layer1.0 downsample
+    (1, 56, 256, 64, 1, True, False, False),    # layer1 reduce (e4m3 -> bf16)
+    (4, 28, 512, 128, 1, True, False, False),   # layer2 reduce
+    (4, 28, 128, 512, 1, False, True, True),    # layer2 expand
+    (4, 56, 256, 512, 2, True, True, False),    # layer2.0 downsample, stride 2
+    (16, 14, 256, 1024, 1, False, True, True),  # layer3 expand
+    (16, 28, 512, 1024, 2, True, True, False),  # layer3.0 downsample, stride 2
+    (1, 56, 64, 256, 1, False, False, True),    # bf16 model: expand + bf16 residual
+    (4, 56, 256, 512, 2, False, False, False),  # bf16 model: downsample
+])
+def test_conv1x1_weight_stationary(gpu, B, H, Cin, Cout, s, in8, out8, res):
+    """conv1x1.hip (weights in VGPRs, LDS-DMA streamed pixel blocks, counted
+    asm residual loads) on the ResNet50 bottleneck shapes vs torch fp32 on the
+    same (dequantised) operands, and against the implicit-GEMM kernel."""
+    g = torch.Generator().manual_seed(40 + Cin + Cout + s)
+    x = torch.rand(B, Cin, H, H, generator=g) * 4
+    w = torch.randn(Cout, Cin, 1, 1, generator=g) / Cin ** 0.5
+    bias = torch.randn(Cout, generator=g) * 0.1
+    if in8:
+        sx = float(x.abs().max()) / 448
+        xq = ops.quantize_fp8(_nhwc(x), sx)
+        wq, sw = ops.pack_conv_weight_fp8(w)
+        xd = _nchw(xq.float() * sx)
+        wd = (wq.float() * sw[:, None])[:Cout, :Cin].reshape(Cout, Cin, 1, 1)
+        xin, wk, alpha = xq.to(gpu), wq.to(gpu), (sx * sw).to(gpu)
+    else:
+        xd = x.bfloat16().float()
+        wd = w.bfloat16().float()
+        xin, wk, alpha = _nhwc(xd).bfloat16().to(gpu), ops.pack_conv_weight(wd, device=gpu), None
+    ref = F.conv2d(xd, wd, bias, s, 0)
+    rq, rs = None, 1.0
+    if res:
+        r = torch.randn_like(ref)
+        if out8:
+            rs = float(r.abs().max()) / 448
+            rq = ops.quantize_fp8(_nhwc(r), rs)
+            ref = ref + _nchw(rq.float() * rs)
+        else:
+            rq = _nhwc(r).bfloat16()
+            ref = ref + _nchw(rq.float())
+    ref = F.relu(ref)
+    C = dmlc.native()
+    if out8 or in8:
+        so = float(ref.abs().max()) / 448 if out8 else None
+        run = lambda tile: ops.conv2d_fp8(xin, wk, alpha, Cout, 1, 1, s, 0, bias=bias.to(gpu),  # noqa: E731
+                                          res=rq.to(gpu) if res else None, res_scale=rs, relu=True, out_scale=so,
+                                          tile=tile)
+    else:
+        so = None
+        run = lambda tile: ops.conv2d(xin, wk, Cout, 1, 1, s, 0, bias=bias.to(gpu),  # noqa: E731
+                                      res=rq.to(gpu) if res else None, relu=True, tile=tile)
+    y = run(C.CONV_1X1)
+    y0 = run(-1)
+    torch.cuda.synchronize()
+    scale = so if out8 else 1.0
+    got, got0 = _nchw(y.float().cpu() * scale), _nchw(y0.float().cpu() * scale)
+    rel = ((got - ref).norm() / ref.norm()).item()
+    rel0 = ((got - got0).norm() / got0.norm()).item()
+    if out8:
+        assert rel < 0.04, rel
+        assert torch.all((got - ref).abs() <= ref.abs() / 14 + 4 * so * 2 ** -9)
+        assert rel0 < 0.02, rel0
+    else:
+        assert rel < 8e-3, rel
+        assert rel0 < 4e-3, rel0
