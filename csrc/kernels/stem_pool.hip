@@ -103,48 +103,61 @@ __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_s_barrier();
 }
 
+// The whole geometry follows from the image size S = 32 NF (NF = output
+// column fragments): compile-time constants, so the row / ring / column
+// arithmetic is shifts and constant multiplies instead of v_mul_lo_u32 (a
+// quarter-rate VALU op) on runtime sizes.
+template <int NF>
+struct StemGeom {
+  static constexpr int S = 32 * NF, Ho = 16 * NF, PH = 8 * NF, PW = 8 * NF, Hp = S + 6;
+  static constexpr int need = ((Ho - 1) * 6 + 26) / 3;  // stem_row_width(S, 3, 7, 2)
+  static constexpr int Wr = ((S + 6 > need ? S + 6 : need) + 7) / 8 * 8;
+  static constexpr int Wq = Wr / 2;  // paired 16-B chunks per staged row
+};
+
 template <int NF, bool U8>
 __global__ __launch_bounds__(256, 2) void stem_conv_pool_kernel(
     StemArgs a) {
+  using G = StemGeom<NF>;
   extern __shared__ __attribute__((aligned(16))) uint4 smem[];
   constexpr int RING = U8 ? kRingU8 : kRing;
-  const int RB = a.Wq * 16;  // bytes per staged input row
-  const int UB = a.S * 3;    // bytes per raw u8 image row (U8)
+  const int RB = G::Wq * 16;  // bytes per staged input row
+  const int UB = G::S * 3;    // bytes per raw u8 image row (U8)
   char* ring = (char*)smem;
   char* hp = ring + RING * RB;
-  char* u8ring = hp + kHp * a.PW * kHpCol;  // U8: raw rows, slot = row % RING
-  const int HPB = a.PW * kHpCol;  // bytes per pooled conv row
+  char* u8ring = hp + kHp * G::PW * kHpCol;  // U8: raw rows, slot = row % RING
+  const int HPB = G::PW * kHpCol;  // bytes per pooled conv row
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: row math in SGPRs
   const int fr = lane & 15, fq = lane >> 4;
-  const int strips = a.PH / a.strip;
+  const int strips = G::PH / a.strip;
   const int b = blockIdx.x / strips;
   const int ph0 = (blockIdx.x - b * strips) * a.strip;
   const int T = a.strip / 2;  // steps 1..T emit pooled rows
-  const bf16* img = a.x + (long)b * a.Hp * a.Wq * 8;
+  const bf16* img = a.x + (long)b * G::Hp * G::Wq * 8;
 
   // This wave's share of a row list [lo, lo+cnt): rows lo+wave, lo+wave+4, ...
   // (U8: padded row r is image row r-3; rows outside the image are not
   // loaded, convert_rows writes them as zeros.)
-  const uint8_t* uimg = U8 ? a.u8 + (long)b * a.S * a.S * 3 : nullptr;
+  const uint8_t* uimg = U8 ? a.u8 + (long)b * G::S * G::S * 3 : nullptr;
   auto load_rows = [&](int lo, int cnt) __attribute__((always_inline)) {
     for (int i = wave; i < cnt; i += 4) {
       const int r = lo + i;
       if (r < 0) continue;
       if constexpr (U8) {
         const int iy = r - 3;
-        if (iy < 0 || iy >= a.S) continue;
+        if (iy < 0 || iy >= G::S) continue;
         const uint8_t* src = uimg + (long)iy * UB;
         char* dst = u8ring + (r % RING) * UB;
         for (int c0 = 0; c0 < UB / 4; c0 += 64)
           if (c0 + lane < UB / 4)
             dma4(src + (c0 + lane) * 4, dst + c0 * 4);
       } else {
-        const bf16* src = img + (long)r * a.Wq * 8;
+        const bf16* src = img + (long)r * G::Wq * 8;
         char* dst = ring + (r % RING) * RB;
-        for (int c0 = 0; c0 < a.Wq; c0 += 64) {
-          if (c0 + lane < a.Wq)
+        for (int c0 = 0; c0 < G::Wq; c0 += 64) {
+          if (c0 + lane < G::Wq)
             dma16(src + (c0 + lane) * 8, dst + c0 * 16);
         }
       }
@@ -156,14 +169,14 @@ __global__ __launch_bounds__(256, 2) void stem_conv_pool_kernel(
   // converts 4 chunks (8 pixels = 24 bytes starting at byte 24k-9 of the
   // row) from 7 aligned dword reads starting at 24k-12.
   auto convert_rows = [&](int lo, int cnt) __attribute__((always_inline)) {
-    const int G4 = (a.Wq + 3) / 4;
+    const int G4 = (G::Wq + 3) / 4;
     const int items = cnt * G4;
     for (int it = tid; it < items; it += 256) {
       const int r = lo + it / G4;
       const int k = it - (it / G4) * G4;
       if (r < 0) continue;
       const int iy = r - 3;
-      const bool row_in = iy >= 0 && iy < a.S;
+      const bool row_in = iy >= 0 && iy < G::S;
       const char* srow = u8ring + (r % RING) * UB;
       const int A = 24 * k - 12;
       uint32_t d[7];
@@ -176,7 +189,7 @@ __global__ __launch_bounds__(256, 2) void stem_conv_pool_kernel(
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const int ix = 8 * k - 3 + i;
-        const bool in = row_in && ix >= 0 && ix < a.S;
+        const bool in = row_in && ix >= 0 && ix < G::S;
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
           const int idx = 3 + 3 * i + c;
@@ -189,7 +202,7 @@ __global__ __launch_bounds__(256, 2) void stem_conv_pool_kernel(
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         v[8 * q + 6] = v[8 * q + 7] = 0.f;
-        if (4 * k + q < a.Wq) *(uint4*)(drow + (4 * k + q) * 16) = pack8(v + 8 * q);
+        if (4 * k + q < G::Wq) *(uint4*)(drow + (4 * k + q) * 16) = pack8(v + 8 * q);
       }
     }
   };
@@ -281,11 +294,11 @@ __global__ __launch_bounds__(256, 2) void stem_conv_pool_kernel(
     lds_barrier();
 
     // Stores this wave issues below (wave-uniform: 16*PW items, PW % 8 == 0).
-    const int items = 16 * a.PW;
+    const int items = 16 * G::PW;
     const int nst = t > 0 ? __builtin_amdgcn_readfirstlane(tid < items ? (items - 1 - tid) / 256 + 1 : 0) : 0;
     if (t > 0) {  // vertical 3-max -> pooled rows ph, ph+1
       const int ph = ph0 + 2 * (t - 1);
-      const int per_row = a.PW * 8;
+      const int per_row = G::PW * 8;
       ushort8 m[4];  // 16*PW <= 1024 items: at most 4 per thread, reads issued together
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -308,7 +321,7 @@ __global__ __launch_bounds__(256, 2) void stem_conv_pool_kernel(
         if (it < 2 * per_row) {
           const int pr = it >= per_row;
           const int rem = it - pr * per_row;
-          *(ushort8*)(a.y + (((long)b * a.PH + ph + pr) * a.PW + (rem >> 3)) * 64 + (rem & 7) * 8) = m[j];
+          *(ushort8*)(a.y + (((long)b * G::PH + ph + pr) * G::PW + (rem >> 3)) * 64 + (rem & 7) * 8) = m[j];
         }
       }
     }
@@ -351,7 +364,7 @@ void stem_launch(const void* x, const uint8_t* u8, const void* w, const float* b
   const int Ho = S / 2, PH = Ho / 2;
   const int NF = Ho / 16;
   if (S % 32 != 0 || NF < 4 || NF > 8) throw std::invalid_argument("stem_conv_pool: image size must be 128..256, %32");
-  if (Wq < Ho + 3 || Wq > 512) throw std::invalid_argument("stem_conv_pool: bad paired row width");
+  if (Wq != stem_row_width(S, 3, 7, 2) / 2) throw std::invalid_argument("stem_conv_pool: bad paired row width");
   if (strip < 2 || strip % 2 || PH % strip) throw std::invalid_argument("stem_conv_pool: bad strip");
   if ((!x && !u8) || !w || !bias || !y || ((uintptr_t)x & 15) || ((uintptr_t)u8 & 3) || ((uintptr_t)w & 15) ||
       ((uintptr_t)y & 15))
