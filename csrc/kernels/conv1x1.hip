@@ -27,8 +27,8 @@
 // (S-1 blocks ahead; dummy zero-page loads past the end keep the count
 // uniform) and ST (stores); the block's DMA has landed when at most
 // (S-1)(ST+RES+DMA) newer operations are outstanding, its residual when at
-// most DMA are. Only M % 64 == 0 is supported (no partial blocks, so every
-// wave issues the same instruction counts).
+// most DMA are. Only M % BM == 0 is supported (BM = 64, 32 for 1-KB rows: no
+// partial blocks, so every wave issues the same instruction counts).
 #include "common.h"
 #include "kernels.h"
 
@@ -120,10 +120,13 @@ struct C1Args {
   float res_scale, out_inv_scale;
 };
 
-constexpr int kBM = 64;  // pixels per block
+// pixels per block: 64, or 32 for 1-KB input rows (stage = BM x RB bytes)
+template <int RB>
+constexpr int block_m() { return RB <= 512 ? 64 : 32; }
 
 template <bool IN8, bool OUT8, int RB, int NW, int S2, bool RES, int S>
 __global__ __launch_bounds__(256, 2) void conv1x1_kernel(C1Args a) {
+  constexpr int kBM = block_m<RB>();
   constexpr int CPR = RB / 16;              // 16-B chunks per staged pixel row
   constexpr int KS = IN8 ? CPR / 8 : CPR / 4;  // K steps (128 e4m3 / 32 bf16 k each)
   constexpr int NF = NW / 16;               // N fragments per wave
@@ -361,10 +364,13 @@ Pick pick(const ConvArgs& a) {
   const int esz = a.in_fp8 ? 1 : 2;
   if (a.Cin != a.Kpad || a.N != a.Npad || a.ldo != a.N) return p;
   const int rb = a.Cin * esz;
-  if (rb != 128 && rb != 256 && rb != 512) return p;
+  if (rb != 128 && rb != 256 && rb != 512 && rb != 1024) return p;
   if (a.in_fp8 && a.Cin % 128) return p;
   const long M = (long)a.B * a.Ho * a.Wo;
-  if (M % kBM) return p;
+  if (M % (rb <= 512 ? 64 : 32)) return p;
+  // strided 1-KB rows (ResNet50 layer4.0 downsample, 32 channel slices each
+  // re-staging every input block): 72 us vs 57 us on the implicit GEMM
+  if (a.stride == 2 && rb > 512) return p;
   for (int nw : {64, 32, 16}) {
     if (a.N % (4 * nw)) continue;
     if ((long)nw * rb > 16 * 1024) continue;  // weights of a wave: <= 64 VGPRs
@@ -405,7 +411,8 @@ template <bool IN8, bool OUT8, int S2, bool RES>
 void launch_rb(const L1& l) {
   if (l.rb == 128) launch_nw<IN8, OUT8, 128, S2, RES>(l);
   else if (l.rb == 256) launch_nw<IN8, OUT8, 256, S2, RES>(l);
-  else launch_nw<IN8, OUT8, 512, S2, RES>(l);
+  else if (l.rb == 512) launch_nw<IN8, OUT8, 512, S2, RES>(l);
+  else launch_nw<IN8, OUT8, 1024, S2, RES>(l);
 }
 
 }  // namespace
@@ -437,11 +444,12 @@ void conv1x1(const ConvArgs& a, int num_cus, hipStream_t s) {
   c.res_scale = a.res_scale;
   c.out_inv_scale = a.out_inv_scale;
   c.nslices = a.N / (4 * pk.nw);
-  c.nblocks = (int)((long)a.B * a.Ho * a.Wo / kBM);
+  const int bm = pk.rb <= 512 ? 64 : 32;
+  c.nblocks = (int)((long)a.B * a.Ho * a.Wo / bm);
   // persistent grid: a multiple of 8 * nslices, about 2 workgroups per CU
   const int q = std::max(1, std::min((c.nblocks + 7) / 8, (2 * num_cus) / (8 * c.nslices)));
   const dim3 grid(8 * c.nslices * q), block(256);
-  const size_t lds = (size_t)(pk.rb <= 256 ? 3 : 2) * kBM * pk.rb;
+  const size_t lds = (size_t)(pk.rb <= 256 ? 3 : 2) * bm * pk.rb;
   const bool res = a.res != nullptr;
   const int key = (a.in_fp8 ? 1 : 0) | (a.out_fp8 ? 2 : 0) | (res ? 4 : 0) | (a.stride == 2 ? 8 : 0);
   const L1 l{grid, lds, s, c, pk.nw, pk.rb};

@@ -80,8 +80,9 @@ void conv2d_igemm(const ConvArgs& a, hipStream_t s);
 constexpr int kConvBigTile0 = 11;
 // Weight-stationary 1x1 conv (conv1x1.hip): stride 1 or 2, no padding, bf16
 // or e4m3 in/out (ConvArgs fp8 fields), optional residual of the output's
-// dtype; Cin * elem in {128, 256, 512} bytes, N % 64 == 0, N == Npad,
-// B*Ho*Wo % 64 == 0. Python/tests select it with tile = kConv1x1Tile.
+// dtype; Cin * elem in {128, 256, 512, 1024} bytes, N % 64 == 0, N == Npad,
+// B*Ho*Wo % 64 == 0 (% 32 for 1-KB rows). Python/tests select it with
+// tile = kConv1x1Tile.
 constexpr int kConv1x1Tile = 100;
 bool conv1x1_supported(const ConvArgs& a);
 void conv1x1(const ConvArgs& a, int num_cus, hipStream_t s);
