@@ -4,6 +4,7 @@ Each test rebuilds, in plain PyTorch, the exact reads a kernel performs on a
 packed layout and checks that they reproduce the fp32 torch op. A layout bug
 then fails here, on the CPU, before any kernel runs.
 """
+import pytest
 import torch
 import torch.nn.functional as F
 
@@ -161,3 +162,37 @@ def test_stream_weight_frag_layout_matches_native_index():
                         n = 32 * g + perm32(16 * nf + (lane & 15))
                         k = 32 * t + 8 * (lane >> 4) + e
                         assert f[idx] == w[n, k]
+
+
+@pytest.mark.parametrize("rb,fp8", [(128, False), (128, True), (256, False), (256, True), (512, False),
+                                    (512, True), (1024, False), (1024, True)])
+def test_conv1x1_lds_conflict_free(rb, fp8):
+    """conv1x1.hip: staged pixel rows of rb bytes, 16-B chunk c of pixel p at
+    physical chunk c ^ swz(p); the B-fragment reads (bf16: chunk 4ks + g of
+    pixel 16pf + fr; e4m3: chunks 8ks + 2g and 8ks + 2g + 1) are conflict free
+    for every pixel fragment and K step, and the DMA staging order covers
+    every (pixel, chunk) once."""
+    cpr = rb // 16
+    bm = 64 if rb <= 512 else 32
+
+    def swz(p):
+        if rb == 128:
+            return ((((p & 7) << 1) | ((p >> 3) & 1)) & 7) if fp8 else (p & 7)
+        return p & 15
+
+    ks_n = cpr // 8 if fp8 else cpr // 4
+    for pf in range(bm // 16):
+        for ks in range(ks_n):
+            for half in ((0, 1) if fp8 else (0,)):
+                addr = []
+                for l in range(64):
+                    fr, g = l & 15, l >> 4
+                    p = 16 * pf + fr
+                    c = 8 * ks + 2 * g + half if fp8 else 4 * ks + g
+                    addr.append(p * rb + ((c ^ swz(p)) << 4))
+                assert _b128_ways(addr) == 1, (pf, ks, half)
+    seen = set()
+    for i in range(bm * cpr):
+        p, pc = i // cpr, i % cpr
+        seen.add((p, pc ^ swz(p)))
+    assert seen == {(p, c) for p in range(bm) for c in range(cpr)}
