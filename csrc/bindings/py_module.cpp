@@ -216,6 +216,13 @@ PYBIND11_MODULE(_C, m) {
                   S(stream));
   }, py::arg("x"), py::arg("wf1"), py::arg("b1"), py::arg("wf2"), py::arg("b2"), py::arg("y"), py::arg("zero"),
         py::arg("B"), py::arg("stream"));
+  m.def("conv3x3_s2rows_supported", &conv3x3_s2rows_supported);
+  m.def("conv3x3_s2rows", [](uintptr_t x, uintptr_t wf, uintptr_t bias, uintptr_t wdf, uintptr_t bd, uintptr_t y,
+                             uintptr_t yd, uintptr_t zero, int B, bool relu, uintptr_t stream, int dbg) {
+    conv3x3_s2rows(P<void>(x), P<void>(wf), P<float>(bias), P<void>(wdf), P<float>(bd), P<void>(y), P<void>(yd),
+                   P<void>(zero), B, relu, S(stream), dbg);
+  }, py::arg("x"), py::arg("wf"), py::arg("bias"), py::arg("wdf"), py::arg("bd"), py::arg("y"), py::arg("yd"),
+        py::arg("zero"), py::arg("B"), py::arg("relu"), py::arg("stream"), py::arg("dbg") = 0);
   m.def("stem_conv_pool_u8", [](uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y, int B, int S_, int strip,
                                 uintptr_t stream) {
     stem_conv_pool_u8(P<uint8_t>(x), P<void>(w), P<float>(bias), P<void>(y), B, S_, strip, S(stream));

@@ -1,0 +1,243 @@
+// Stride-2 3x3 conv 56x56x64 -> 28x28x128 (BN folded, ReLU) together with the
+// block's 1x1/s2 downsample (BN folded, no ReLU), row-streamed: ResNet18
+// layer2.0.conv1 + layer2.0.downsample.
+//
+// Reference equivalent: layer2.0.{conv1,bn1,relu} and layer2.0.downsample of
+// tch::vision::resnet18, run per query by `forward_t` (src/services.rs:493).
+// As a stream conv (conv3x3_stream.hip: 7-output-row strips with their 15
+// input rows resident in LDS, 1024 workgroups at one per CU) the input
+// staging of every round is exposed: 4 rounds of HBM-bound prologue around
+// ~2 us of MFMAs each, 72 us for 33 GFLOP (profiles/r2_final_resnet18_kernels.txt).
+// Here one workgroup walks one image top to bottom (one round at B = 256),
+// 4 output rows per step, the 8 input rows of the next step arriving by
+// LDS-DMA while the current step computes:
+//
+//  * weight-stationary: 4 waves (one per SIMD), wave w owns output channels
+//    32w .. 32w + 31 and keeps all 20 of their K-step fragments (18 for the
+//    3x3 taps, 2 for the downsample) in registers, so the only global traffic
+//    in the loop is the row DMA (whose vmcnt, being asm, the compiler cannot
+//    see or wait on) and the output stores;
+//  * staged input row: two K-half planes of 57 pixel slots x 64 B (slot 0 =
+//    column -1, zero; 1..28 = odd columns; 29..56 = even columns), so output
+//    pixels c, c+1 read adjacent slots at every tap (kw 0: slot c, kw 1: 29 + c
+//    as an immediate, kw 2: c + 1); rows padded to 7424 B (a bank-row
+//    multiple) in a ring of 17 + 2 guard slots (copies of slots 0, 1) so the
+//    3 kernel rows of a fragment are immediate offsets of one address;
+//  * 16-B chunk c of a K-half of stored pixel (y, x) sits at physical chunk
+//    c ^ ((K >> 1) & 3), K = ((y + 1) >> 1) * 28 + ((x + 1) >> 1): along a
+//    fragment K is the output pixel index plus a tap constant, also where a
+//    fragment wraps an output row, and every ds_read_b128 is conflict free
+//    (tests/test_layouts_cpu.py).
+#include "common.h"
+#include "kernels.h"
+
+namespace dmlc {
+
+namespace {
+
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+
+struct S2Args {
+  const bf16* x;      // [B, 56, 56, 64]
+  const bf16* wf;     // 3x3 weights, fragment order [4][18][2][64][8] (stream_frag_index, K = 576)
+  const bf16* wdf;    // 1x1 weights, fragment order [4][2][2][64][8] (K = 64)
+  const float* bias;  // [128]
+  const float* bd;    // [128]
+  bf16* y;            // [B, 28, 28, 128]
+  bf16* yd;           // [B, 28, 28, 128]
+  const bf16* zero;
+  int relu;
+  int dbg;  // experiment: bit 0 no loop DMA, bit 1 no stores
+};
+
+constexpr int kHI = 56, kWI = 56, kCI = 64, kH = 28, kW = 28, kCO = 128;
+constexpr int kR = 4;                 // output rows per step
+constexpr int kSteps = kH / kR;       // 7
+constexpr int kE0 = 29;               // first even-column slot
+constexpr int kHalf = 3712;           // bytes per K-half plane (58 slots x 64 B)
+constexpr int kRB = 2 * kHalf;        // 7424 B per staged row
+constexpr int kRing = 17;             // rows 2 r0 - 1 .. 2 r0 + 7 in use + 8 in flight
+constexpr int kSlotsAlloc = kRing + 2;
+constexpr int kRowCh = kRB / 16;      // 464 DMA chunks per row
+constexpr int kMF = kR * kW / 16;     // 7 pixel fragments per step
+constexpr int kKT = 18, kCT = 2;      // 3x3 / downsample K steps
+constexpr int kKS = kKT + kCT;
+constexpr int kOffKw1 = kE0 * 64;     // kw = 1 reads slot 29 + c
+
+__device__ __forceinline__ int swz_of(int y, int x) { return ((((y + 1) >> 1) * kW + ((x + 1) >> 1)) >> 1) & 3; }
+
+__global__ __launch_bounds__(256, 1) void conv3x3_s2rows_kernel(S2Args a) {
+  extern __shared__ __attribute__((aligned(16))) uint4 smem[];
+  char* ring = (char*)smem;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, g = lane >> 4;
+  const int b = blockIdx.x;
+  const bf16* img = a.x + (long)b * kHI * kWI * kCI;
+
+  // input row yy (-1: zero row) -> ring slot (yy + 1) % 17, and the guard
+  // slot 17 / 18 too for slots 0 / 1; the 4 waves share the chunks
+  auto load_row = [&](int yy) __attribute__((always_inline)) {
+    const int slot = (yy + 1) % kRing;
+    const bool inside = (unsigned)yy < (unsigned)kHI;
+    for (int c0 = wave * 64; c0 < kRowCh; c0 += 4 * 64) {
+      const int i = c0 + lane;
+      const int h = i >= kRowCh / 2, j = i - h * (kRowCh / 2);
+      const int pos = j >> 2, c = j & 3;
+      const int x = pos == 0 ? -1 : (pos < kE0 ? 2 * pos - 1 : 2 * (pos - kE0));
+      const int lc = 4 * h + (c ^ swz_of(yy, x));
+      const bool ok = inside && x >= 0 && pos <= 2 * kW;
+      const bf16* src = ok ? img + ((long)yy * kWI + x) * kCI + 8 * lc : a.zero;
+      if (i < kRowCh) {
+        dma16(src, ring + slot * kRB + c0 * 16);
+        if (slot < 2) dma16(src, ring + (slot + kRing) * kRB + c0 * 16);
+      }
+    }
+  };
+  for (int yy = -1; yy <= 7; ++yy) load_row(yy);
+
+  // ---- per-lane constants. Fragment f covers tile pixels p = 16 f + fr (row
+  // p / 28 of the step, column c = p % 28). col[f][v]: the in-row byte offset
+  // of K-half 0 for variant v = (kw == 2) + 2 (kh == 2)
+  int prow2[kMF], col[kMF][4];
+#pragma unroll
+  for (int f = 0; f < kMF; ++f) {
+    const int p = 16 * f + fr;
+    prow2[f] = 2 * (p / kW);
+    const int c = p % kW;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int kw2 = v & 1, kh2 = v >> 1;
+      const int s = ((p + kw2 + kW * kh2) >> 1) & 3;  // K of r0 = 0 (r0 is a multiple of 4)
+      col[f][v] = (c + kw2) * 64 + ((g ^ s) << 4);
+    }
+  }
+  const int ch0 = wave * 32;
+  bf16x8 w[kKS][2];
+#pragma unroll
+  for (int t = 0; t < kKS; ++t)
+#pragma unroll
+    for (int nf = 0; nf < 2; ++nf) {
+      const bf16* src = t < kKT ? a.wf + ((((long)wave * kKT + t) * 2 + nf) * 64 + lane) * 8
+                                : a.wdf + ((((long)wave * kCT + (t - kKT)) * 2 + nf) * 64 + lane) * 8;
+      w[t][nf] = *(const bf16x8*)src;
+    }
+  // this lane's 8 output channels ch0 + 8g .. +7 (weight rows permuted, perm32)
+  float bs[8], bsd[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    bs[e] = a.bias[ch0 + 8 * g + e];
+    bsd[e] = a.bd[ch0 + 8 * g + e];
+  }
+  vm_wait<0>();
+  __builtin_amdgcn_s_barrier();
+
+  for (int step = 0; step < kSteps; ++step) {
+    const int r0 = step * kR;  // first output row; input rows 2 r0 - 1 .. 2 r0 + 7
+    if (step + 1 < kSteps && !(a.dbg & 1))
+      for (int yy = 2 * r0 + 8; yy <= 2 * r0 + 15; ++yy) load_row(yy);
+    // ring slot of kernel row 0 of every fragment (+ kh rows: immediate, guard slots)
+    const int sb = (2 * r0) % kRing;
+    int rowoff[kMF];
+#pragma unroll
+    for (int f = 0; f < kMF; ++f) {
+      int sl = sb + prow2[f];
+      sl = sl >= kRing ? sl - kRing : sl;
+      rowoff[f] = sl * kRB;
+    }
+    floatx4 acc[kMF][2], accd[kMF][2];
+#pragma unroll
+    for (int f = 0; f < kMF; ++f)
+#pragma unroll
+      for (int nf = 0; nf < 2; ++nf) {
+        acc[f][nf] = floatx4{0.f, 0.f, 0.f, 0.f};
+        accd[f][nf] = floatx4{0.f, 0.f, 0.f, 0.f};
+      }
+    // K step t: tap = t >> 1 (downsample steps: tap 4 = (1, 1)), K-half h = t & 1
+    auto xread = [&](int t, int f) __attribute__((always_inline)) {
+      const int tap = t < kKT ? t >> 1 : 4, h = t & 1;
+      const int kh = tap / 3, kw = tap % 3;
+      const int v = (kw == 2) + 2 * (kh == 2);
+      const int imm = kh * kRB + (kw == 1 ? kOffKw1 : 0) + h * kHalf;
+      return *(const bf16x8*)(ring + (rowoff[f] + col[f][v]) + imm);
+    };
+    bf16x8 xc[kMF];
+#pragma unroll
+    for (int f = 0; f < kMF; ++f) xc[f] = xread(0, f);
+#pragma unroll
+    for (int t = 0; t < kKS; ++t) {
+#pragma unroll
+      for (int f = 0; f < kMF; ++f) {
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int nf = 0; nf < 2; ++nf) {
+          if (t < kKT)
+            acc[f][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[t][nf], xc[f], acc[f][nf], 0, 0, 0);
+          else
+            accd[f][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[t][nf], xc[f], accd[f][nf], 0, 0, 0);
+        }
+        if (t + 1 < kKS) xc[f] = xread(t + 1, f);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- epilogue: lane holds channels ch0 + 8g .. +7 of tile pixel 16 f + fr
+#pragma unroll
+    for (int f = 0; f < kMF; ++f) {
+      const long o = (((long)b * kH + r0) * kW + 16 * f + fr) * kCO + ch0 + 8 * g;
+      float v[8], vd[8];
+#pragma unroll
+      for (int nf = 0; nf < 2; ++nf)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          v[4 * nf + i] = acc[f][nf][i] + bs[4 * nf + i];
+          vd[4 * nf + i] = accd[f][nf][i] + bsd[4 * nf + i];
+        }
+      if (a.relu) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+      }
+      if (!(a.dbg & 2)) {
+        *(uint4*)(a.y + o) = pack8(v);
+        *(uint4*)(a.yd + o) = pack8(vd);
+      }
+    }
+    // the next step's rows have landed (the 2 kMF stores just issued may
+    // still be in flight: vmcnt retires in order) and every wave is done
+    // reading the rows they replace
+    vm_wait<2 * kMF>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+}
+
+}  // namespace
+
+bool conv3x3_s2rows_supported(int Hin, int Win, int Cin, int Cout) {
+  return Hin == kHI && Win == kWI && Cin == kCI && Cout == kCO;
+}
+
+void conv3x3_s2rows(const void* x, const void* wf, const float* bias, const void* wdf, const float* bd, void* y,
+                    void* yd, const void* zero, int B, bool relu, hipStream_t s, int dbg) {
+  if (B <= 0) return;
+  if (!x || !wf || !bias || !wdf || !bd || !y || !yd || !zero ||
+      (((uintptr_t)x | (uintptr_t)wf | (uintptr_t)wdf | (uintptr_t)y | (uintptr_t)yd | (uintptr_t)zero) & 15))
+    throw std::invalid_argument("conv3x3_s2rows: null / misaligned operand");
+  S2Args a;
+  a.x = (const bf16*)x;
+  a.wf = (const bf16*)wf;
+  a.wdf = (const bf16*)wdf;
+  a.bias = bias;
+  a.bd = bd;
+  a.y = (bf16*)y;
+  a.yd = (bf16*)yd;
+  a.zero = (const bf16*)zero;
+  a.relu = relu;
+  a.dbg = dbg;
+  hipLaunchKernelGGL(conv3x3_s2rows_kernel, dim3(B), dim3(256), (size_t)kSlotsAlloc * kRB, s, a);
+  DMLC_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace dmlc

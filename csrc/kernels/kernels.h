@@ -152,6 +152,14 @@ void conv3x3_rows(const void* x, const void* w, const float* bias, const void* r
 bool conv3x3_block_supported(int H, int W, int C);
 void conv3x3_block(const void* x, const void* wf1, const float* bias1, const void* wf2, const float* bias2, void* y,
                    const void* zero, int B, hipStream_t s);
+// ResNet layer2.0's stride-2 3x3 conv 56x56x64 -> 28x28x128 and its 1x1/s2
+// downsample in one row-streaming, weight-stationary kernel
+// (conv3x3_s2rows.hip): one workgroup per image. wf / wdf: fragment-order
+// weights (stream_frag_index, K = 576 / 64); y = relu?(conv3x3 + bias),
+// yd = downsample + bd.
+bool conv3x3_s2rows_supported(int Hin, int Win, int Cin, int Cout);
+void conv3x3_s2rows(const void* x, const void* wf, const float* bias, const void* wdf, const float* bd, void* y,
+                    void* yd, const void* zero, int B, bool relu, hipStream_t s, int dbg = 0);
 // Direct 3x3/p1 conv with the input image resident in LDS and per-wave weight
 // rings (conv3x3_stream.hip): stride 1 on 28x28x128, 14x14x256, 7x7x512;
 // stride 2 on 56x56x64 -> 128 and 28x28x128 -> 256. Hin/Win are the input

@@ -82,7 +82,7 @@ bool EngineOptions::set(const std::string& name, bool v) {
       {"bigtile", &EngineOptions::bigtile},         {"fused_pool", &EngineOptions::fused_pool},
       {"fused_head", &EngineOptions::fused_head},   {"fc_small", &EngineOptions::fc_small},
       {"fork_ds", &EngineOptions::fork_ds},         {"fp8_3x3", &EngineOptions::fp8_3x3},
-      {"conv1x1", &EngineOptions::conv1x1},
+      {"conv1x1", &EngineOptions::conv1x1},         {"s2rows", &EngineOptions::s2rows},
   };
   for (const auto& f : fields)
     if (name == f.first) {
@@ -418,8 +418,10 @@ void Engine::pack_weights(const WeightMap& w) {
     // downsample it fuses next to a stride-2 one)
     if (!L.fp8 && !L.fc && !L.pair && !L.stem_pool && L.in_act >= 0 && L.cout % 32 == 0 && L.kpad % 32 == 0 &&
         (((L.kh == 3 && L.kw == 3) || (L.kh == 1 && L.kw == 1 && L.stride == 2)) &&
-             conv3x3_stream_uses_frag(shapes_[L.in_act].H, shapes_[L.in_act].W, shapes_[L.in_act].C, L.cout,
-                                      L.stride) ||
+             (conv3x3_stream_uses_frag(shapes_[L.in_act].H, shapes_[L.in_act].W, shapes_[L.in_act].C, L.cout,
+                                       L.stride) ||
+              (L.stride == 2 &&
+               conv3x3_s2rows_supported(shapes_[L.in_act].H, shapes_[L.in_act].W, shapes_[L.in_act].C, L.cout))) ||
          (L.kh == 3 && L.kw == 3 && L.stride == 1 && L.pad == 1 &&
           conv3x3_rows_supported(shapes_[L.in_act].H, shapes_[L.in_act].W, shapes_[L.in_act].C, L.cout)))) {
       L.wf_off = off;  // fragment-order copy for the register-weight stream conv
@@ -705,6 +707,18 @@ bool Engine::block_fusable(size_t oi, int B) const {
          conv_path(c1, B) == ConvPath::Rows && conv_path(c2, B) == ConvPath::Rows;
 }
 
+// The stride-2 conv1 of a block whose downsample it computes (fuse_ds) on
+// the 56x56x64 -> 128 shape: conv3x3_s2rows runs one workgroup per image
+// (59 us at B=256 vs 72 us for the stream conv's 4 rounds of strips,
+// profiles/r2_s2rows.txt); like the fused block only with rounds >= ~70% full.
+bool Engine::s2rows_ok(const Op& op, const ConvLayer& D, int B) const {
+  const ConvLayer& L = convs_[op.conv];
+  const ActShape& is = shapes_[op.in];
+  const int rounds = (B + num_cus_ - 1) / num_cus_;
+  return opt_.s2rows && op.res < 0 && L.wf_off && D.wf_off && 10 * B >= 7 * rounds * num_cus_ &&
+         conv3x3_s2rows_supported(is.H, is.W, is.C, L.cout);
+}
+
 bool Engine::side_safe(int B) const {
   for (const Op& op : ops_)
     if (op.type == OpType::Conv && conv_path(op, B) == ConvPath::BigTile) return false;
@@ -788,15 +802,23 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
             // the fused avgpool keeps the activation for eager/profile runs
             // (tests read it) and drops it under graph capture
             const bool fpool = cs == s && pool_fusable(oi, B);
+            if (D && s2rows_ok(op, *D, B)) {
+              const uint8_t* wa = (const uint8_t*)warena_;
+              conv3x3_s2rows(acts_[op.in], wa + L.wf_off, (const float*)(wa + L.b_off), wa + D->wf_off,
+                             (const float*)(wa + D->b_off), acts_[op.out], acts_[yd], zero_, B, L.relu, cs);
+              skip_ds = -1;
+              break;
+            }
+            // (wf_off may exist for conv3x3_s2rows alone)
+            const bool wreg = L.wf_off && opt_.stream_wreg && (!D || D->wf_off) &&
+                              conv3x3_stream_uses_frag(is.H, is.W, is.C, L.cout, L.stride);
             conv3x3_stream(acts_[op.in], (const uint8_t*)warena_ + L.w_off,
                            (const float*)((const uint8_t*)warena_ + L.b_off), op.res >= 0 ? acts_[op.res] : nullptr,
                            acts_[op.out], zero_, B, is.H, is.W, is.C, L.cout, L.stride, L.relu, cs, nullptr,
                            D ? (const uint8_t*)warena_ + D->w_off : nullptr,
                            D ? (const float*)((const uint8_t*)warena_ + D->b_off) : nullptr,
-                           D ? acts_[yd] : nullptr,
-                           (L.wf_off && opt_.stream_wreg && (!D || D->wf_off)) ? (const uint8_t*)warena_ + L.wf_off
-                                                                          : nullptr,
-                           (D && D->wf_off && opt_.stream_wreg) ? (const uint8_t*)warena_ + D->wf_off : nullptr,
+                           D ? acts_[yd] : nullptr, wreg ? (const uint8_t*)warena_ + L.wf_off : nullptr,
+                           (wreg && D) ? (const uint8_t*)warena_ + D->wf_off : nullptr,
                            fpool ? acts_[ops_[oi + 1].out] : nullptr, !fpool || trace || evs);
             pooled = fpool;
             skip_ds = -1;

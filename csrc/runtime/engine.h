@@ -73,6 +73,8 @@ struct EngineOptions {
   bool stream_wreg = true;       // ... with register-streamed weights where available
   bool stream_l4s2 = true;       // ... also for 14x14x256 -> 512 / s2 (register weights only)
   bool fuse_ds = true;           // the block's 1x1/s2 downsample inside the stride-2 stream conv1
+  bool s2rows = true;            // ... layer2.0 (56x56x64 -> 128): one weight-stationary kernel per image
+                                 // walking its rows (conv3x3_s2rows.hip), B >= 0.7 x CUs
   bool bigtile = true;           // 8-wave big-tile split-K convs where picked (not on the ResNet18 b256 path)
   bool conv1x1 = true;           // weight-stationary 1x1 convs (conv1x1.hip: ResNet50 bottlenecks)
   bool fused_pool = true;        // the last conv's epilogue computes the global average pool
@@ -162,6 +164,7 @@ class Engine {
   bool pool_fusable(size_t oi, int B) const;
   bool ds_fusable(size_t oi, int B) const;     // ops oi, oi+1 = downsample + stride-2 stream conv1
   bool block_fusable(size_t oi, int B) const;  // ops oi, oi+1 = a layer1 basic block -> conv3x3_block
+  bool s2rows_ok(const Op& op, const ConvLayer& D, int B) const;  // layer2.0 conv1 + downsample -> conv3x3_s2rows
 
   std::string arch_;
   int device_ = 0;

@@ -198,6 +198,28 @@ def conv3x3_block(x: torch.Tensor, w1_packed: torch.Tensor, b1: torch.Tensor, w2
     return y
 
 
+def conv3x3_s2rows(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, wd_packed: torch.Tensor,
+                   bd: torch.Tensor, relu: bool = True):
+    """ResNet layer2.0's stride-2 3x3 conv [B,56,56,64] -> [B,28,28,128]
+    and its 1x1/s2 downsample in one row-streaming kernel
+    (conv3x3_s2rows.hip): returns (relu?(conv3x3(x) + bias), conv1x1_s2(x)
+    + bd). w_packed: conv2d packed weights [128, 576]; wd_packed [128, 64]."""
+    _need_cuda(x, w_packed, bias, wd_packed, bd)
+    C = native()
+    B, H, W, Cin = x.shape
+    Cout = w_packed.shape[0]
+    if (not C.conv3x3_s2rows_supported(H, W, Cin, Cout) or tuple(w_packed.shape) != (Cout, 9 * Cin)
+            or tuple(wd_packed.shape) != (Cout, Cin)):
+        raise ValueError("conv3x3_s2rows: unsupported shape")
+    x = x.contiguous()
+    y = torch.empty(B, H // 2, W // 2, Cout, dtype=x.dtype, device=x.device)
+    yd = torch.empty_like(y)
+    wf, wdf = stream_weight_frag(w_packed), stream_weight_frag(wd_packed)
+    C.conv3x3_s2rows(_ptr(x), _ptr(wf), _ptr(bias.float().contiguous()), _ptr(wdf), _ptr(bd.float().contiguous()),
+                     _ptr(y), _ptr(yd), _ptr(_zero_page(x.device)), B, relu, _stream())
+    return y, yd
+
+
 def stream_weight_frag(w_packed: torch.Tensor, cout: int | None = None) -> torch.Tensor:
     """Packed conv weights [Npad, K] -> the stream conv's fragment order
     [Cout/32][K/32][2][64 lanes][8]: lane l of fragment nf of channel group g,

@@ -411,6 +411,30 @@ def test_conv3x3_block(gpu, B):
     assert torch.equal(y, y2)
 
 
+@pytest.mark.parametrize("B", [1, 5])
+def test_conv3x3_s2rows(gpu, B):
+    """Row-streaming weight-stationary layer2.0 conv1 + downsample
+    (conv3x3_s2rows.hip) vs torch fp32 and vs the stream conv's fused
+    downsample variant."""
+    g = torch.Generator().manual_seed(37)
+    x = torch.randn(B, 64, 56, 56, generator=g).bfloat16().float()
+    w = (torch.randn(128, 64, 3, 3, generator=g) / 24).bfloat16().float()
+    wd = (torch.randn(128, 64, 1, 1, generator=g) / 8).bfloat16().float()
+    bias = torch.randn(128, generator=g) * 0.1
+    bd = torch.randn(128, generator=g) * 0.1
+    ref = F.relu(F.conv2d(x, w, bias, 2, 1))
+    ref_d = F.conv2d(x, wd, bd, 2, 0)
+    xg = _nhwc(x).bfloat16().to(gpu)
+    wp, wdp = ops.pack_conv_weight(w, device=gpu), ops.pack_conv_weight(wd, device=gpu)
+    y, yd = ops.conv3x3_s2rows(xg, wp, bias.to(gpu), wdp, bd.to(gpu))
+    y0, yd0 = ops.conv3x3_stream(xg, wp, bias.to(gpu), None, True, stride=2, downsample=(wdp, bd.to(gpu)))
+    torch.cuda.synchronize()
+    assert _rel(_nchw(y.float().cpu()), ref) < 5e-3, _rel(_nchw(y.float().cpu()), ref)
+    assert _rel(_nchw(yd.float().cpu()), ref_d) < 5e-3, _rel(_nchw(yd.float().cpu()), ref_d)
+    assert (y.float() - y0.float()).abs().max().item() < 0.05
+    assert (yd.float() - yd0.float()).abs().max().item() < 0.05
+
+
 def test_preprocess_paired(gpu):
     g = torch.Generator().manual_seed(12)
     img = torch.randint(0, 256, (2, 224, 224, 3), generator=g, dtype=torch.uint8)

@@ -196,3 +196,61 @@ def test_conv1x1_lds_conflict_free(rb, fp8):
         p, pc = i // cpr, i % cpr
         seen.add((p, pc ^ swz(p)))
     assert seen == {(p, c) for p in range(bm) for c in range(cpr)}
+
+
+def _s2rows_pos(x):
+    """conv3x3_s2rows.hip staged-row slot of input column x (-1: the pad)."""
+    return 0 if x == -1 else ((x + 1) // 2 if x & 1 else 29 + x // 2)
+
+
+def _s2rows_swz(y, x):
+    return ((((y + 1) >> 1) * 28 + ((x + 1) >> 1)) >> 1) & 3
+
+
+def test_s2rows_lds_layout():
+    """conv3x3_s2rows.hip: every ds_read_b128 of a 112-pixel step (7
+    fragments x 9 taps x 2 K halves, all 7 steps, through the 17-row ring
+    with its 2 guard slots) is conflict free and reads the channels the
+    weight fragment expects; the DMA staging order of a row covers every
+    (column, channel chunk) once."""
+    RB, HALF, RING = 7424, 3712, 17
+    # ring contents as (row) per slot, guard slots 17/18 mirroring 0/1
+    for r0 in range(0, 28, 4):
+        sb = (2 * r0) % RING
+        for f in range(7):
+            for kh in range(3):
+                for kw in range(3):
+                    for h in range(2):
+                        addr = []
+                        for l in range(64):
+                            fr, g = l & 15, l >> 4
+                            p = 16 * f + fr
+                            r, c = r0 + p // 28, p % 28
+                            y, x = 2 * r + kh - 1, 2 * c + kw - 1
+                            sl = sb + 2 * (p // 28)
+                            sl = sl - RING if sl >= RING else sl
+                            # kernel: rowoff + col[v] + immediate
+                            v = (kw == 2) + 2 * (kh == 2)
+                            s = ((p + (v & 1) + 28 * (v >> 1)) >> 1) & 3
+                            col = (c + (v & 1)) * 64 + ((g ^ s) << 4)
+                            a = sl * RB + col + kh * RB + (29 * 64 if kw == 1 else 0) + h * HALF
+                            addr.append(a)
+                            # the slot holds row y (mod the ring, guards mirror slots 0/1)
+                            slot = a // RB
+                            assert (slot % RING) == (y + 1) % RING and slot < RING + 2
+                            off = a % RB
+                            hh, j = off // HALF, off % HALF
+                            assert hh == h and j // 64 == _s2rows_pos(x)
+                            # stored chunk holds logical chunk 4h + (phys ^ swz(y, x)) == 4h + g
+                            assert ((j % 64) // 16) ^ _s2rows_swz(y, x) == g
+                        assert _b128_ways(addr) == 1, (r0, f, kh, kw, h)
+    seen = set()
+    for i in range(RB // 16):  # load_row: chunk i -> (h, pos, c) -> source column / channel chunk
+        h, j = i // (HALF // 16), i % (HALF // 16)
+        pos, c = j >> 2, j & 3
+        if pos > 56:
+            continue
+        x = -1 if pos == 0 else (2 * pos - 1 if pos < 29 else 2 * (pos - 29))
+        assert _s2rows_pos(x) == pos
+        seen.add((x, 4 * h + (c ^ _s2rows_swz(0, x))))
+    assert seen == {(x, cc) for x in range(-1, 56) for cc in range(8)}
