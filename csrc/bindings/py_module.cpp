@@ -223,6 +223,12 @@ PYBIND11_MODULE(_C, m) {
                    P<void>(zero), B, relu, S(stream), dbg);
   }, py::arg("x"), py::arg("wf"), py::arg("bias"), py::arg("wdf"), py::arg("bd"), py::arg("y"), py::arg("yd"),
         py::arg("zero"), py::arg("B"), py::arg("relu"), py::arg("stream"), py::arg("dbg") = 0);
+  m.def("conv3x3_rows28_supported", &conv3x3_rows28_supported);
+  m.def("conv3x3_rows28", [](uintptr_t x, uintptr_t wf, uintptr_t bias, uintptr_t res, uintptr_t y, int B, bool relu,
+                             uintptr_t stream, int dbg) {
+    conv3x3_rows28(P<void>(x), P<void>(wf), P<float>(bias), P<void>(res), P<void>(y), B, relu, S(stream), dbg);
+  }, py::arg("x"), py::arg("wf"), py::arg("bias"), py::arg("res"), py::arg("y"), py::arg("B"), py::arg("relu"),
+        py::arg("stream"), py::arg("dbg") = 0);
   m.def("stem_conv_pool_u8", [](uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y, int B, int S_, int strip,
                                 uintptr_t stream) {
     stem_conv_pool_u8(P<uint8_t>(x), P<void>(w), P<float>(bias), P<void>(y), B, S_, strip, S(stream));

@@ -58,7 +58,7 @@ constexpr int kQ = kW + 2;             // staged columns
 constexpr int kHalf = kQ * 64;         // one K half (32 channels) of a staged row: 3712 B
 constexpr int kSlot = 2 * kHalf;       // 7424 B per staged row
 constexpr int kRing = 10;
-constexpr int kRowCh = kQ * kC / 8;    // 464 16-B chunks per row
+constexpr int kRun = 4 * kW;           // 224 DMA chunks per K half of a row (q = 1..56)
 constexpr int kSteps = kH / kR + 2;    // 16
 
 // One role's whole pipeline (PROD: conv1 producer, else conv2 consumer).
@@ -80,21 +80,30 @@ __device__ __forceinline__ void block_role(const BlockArgs& a, char* xring, char
   // 57. The h = 1 fragment of a tap is the h = 0 one + kHalf (an immediate
   // ds_read offset), and every 16-lane group of a ds_read_b128 / ds_write_b128
   // hits 16 distinct bank groups (tests/test_layouts_cpu.py). Producers only.
+  // The pad columns q = 0, 57 and the zero row -1 are zeroed once (kernel
+  // start) and never DMA'd: a zero page read by every workgroup's pad lanes
+  // is one hot L2 channel per XCD (conv3x3_s2rows.hip measured 7 us of it).
+  // Row 56 reuses a ring slot, so its data chunks are written as zeros.
+  // Per K half the chunks of q = 1..56 are one contiguous run of 224;
+  // wave rw DMAs chunks 64 rw .. 64 rw + 63 of both runs.
   auto load_row = [&](int r) __attribute__((always_inline)) {
-    char* dst = xring + ((r + kRing) % kRing) * kSlot;
-    const bool inside = (unsigned)r < (unsigned)kH;
-    for (int c0 = rw * 64; c0 < kRowCh; c0 += 4 * 64) {
-      const int i = c0 + lane;
-      const int h = i / (kQ * 4), q = (i >> 2) % kQ, c = i & 3;
-      const bool ok = inside && q >= 1 && q <= kW;
-      const bf16* src = ok ? img + ((long)r * kW + (q - 1)) * kC + 8 * (4 * h + (c ^ ((q >> 1) & 3))) : a.zero;
-      if (i < kRowCh) dma16(src, dst + c0 * 16);
+    char* dst = xring + ((r + kRing) % kRing) * kSlot + 64 + rw * 1024;
+    const int k = rw * 64 + lane;
+    const int q = 1 + (k >> 2), c = k & 3;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (k < kRun) {
+        if (r < kH)
+          dma16(img + ((long)r * kW + (q - 1)) * kC + 8 * (4 * h + (c ^ ((q >> 1) & 3))), dst + h * kHalf);
+        else
+          *(uint4*)(dst + h * kHalf + lane * 16) = make_uint4(0, 0, 0, 0);
+      }
     }
   };
   // x rows -1 .. 5: P_-1 needs x rows -2..1 (row -2 only feeds t row -1,
   // which is written as zeros), P_0 needs rows 0..5
   if constexpr (PROD)
-    for (int r = -1; r <= 5; ++r) load_row(r);
+    for (int r = 0; r <= 5; ++r) load_row(r);
 
   // ---- per-lane constants (4-row tile, 2 pixel halves)
   // fragment f, lane fr: pixel p = wm*112 + 16f + fr of the tile, in tile row
@@ -247,8 +256,11 @@ __global__ __launch_bounds__(512, 1) void conv3x3_block_kernel(BlockArgs a) {
   char* tring = xring + kRing * kSlot;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  // zero the t ring (pad columns stay zero; halo rows are written as zeros)
-  for (int i = tid; i < kRing * kSlot / 16; i += 512) ((uint4*)tring)[i] = make_uint4(0, 0, 0, 0);
+  // zero both rings (pad columns stay zero; x row -1 is the zeroed slot 9;
+  // t halo rows are written as zeros), before any x-row DMA lands
+  for (int i = tid; i < 2 * kRing * kSlot / 16; i += 512) ((uint4*)xring)[i] = make_uint4(0, 0, 0, 0);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
   if (wave < 4)
     block_role<true, PD, DMA_KS>(a, xring, tring, wave & 3, lane);
   else

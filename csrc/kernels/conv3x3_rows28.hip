@@ -1,0 +1,270 @@
+// Weight-stationary row-streaming 3x3/s1/p1 conv for 28x28x128 -> 128 (BN
+// folded, optional residual, ReLU): ResNet18 layer2's stride-1 convs
+// (layer2.0.conv2, layer2.1.conv1, layer2.1.conv2).
+//
+// Reference equivalent: those convs + bn (+ residual) + relu of
+// tch::vision::resnet18, run per query by `forward_t` (src/services.rs:493).
+// As a stream conv (conv3x3_stream.hip) these run 2 rounds of half-image
+// workgroups whose 15-row input prologue is exposed each round, with the
+// weights streamed from L2 through a register ring (64-70 us at B=256,
+// profiles/r2_final_resnet18_kernels.txt). The 32 x 1152 bf16 weights of
+// one wave's 32 output channels are 288 VGPRs: with one wave per SIMD the
+// whole 128 x 1152 weight matrix fits in one workgroup's registers, so here
+// a workgroup walks one image (one round at B = 256) with no weight traffic
+// in its loop, the same scheme as conv3x3_s2rows.hip:
+//
+//  * 4 waves; wave w owns output channels 32w .. 32w + 31 (2 N fragments)
+//    for all 112 pixels (7 fragments) of a 4-output-row step; 36 K steps
+//    (9 taps x 4 channel quarters) x 14 MFMAs per step;
+//  * staged input row: 4 channel-quarter planes of 30 pixel slots x 64 B
+//    (slot 0 / 29 = columns -1 / 28, zero; slot x + 1 = column x), rows
+//    7680 B (a bank-row multiple) in a ring of 10 + 2 guard slots (copies of
+//    slots 0, 1) so a fragment's 3 kernel rows and 4 quarters are immediate
+//    offsets of one address per (fragment, kw);
+//  * 16-B chunk c of a quarter of stored pixel (y, x) sits at physical chunk
+//    c ^ ((K >> 1) & 3), K = 28 y + x: along a fragment K is the output pixel
+//    index plus a tap constant, also across a row wrap, and every
+//    ds_read_b128 is conflict free (tests/test_layouts_cpu.py); kernel rows
+//    0 and 2 differ from row 1 by 28 in K, an XOR of 2 on the chunk;
+//  * the pad slots are zeroed once (no zero-page DMA: one hot L2 channel
+//    per XCD); the 4 rows of the next step arrive by LDS-DMA (wave w: its
+//    own quarter plane) while the current step computes.
+#include "common.h"
+#include "kernels.h"
+
+namespace dmlc {
+
+namespace {
+
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+
+struct R28Args {
+  const bf16* x;      // [B, 28, 28, 128]
+  const bf16* wf;     // weights, fragment order [4][36][2][64][8] (stream_frag_index, K = 1152)
+  const float* bias;  // [128]
+  const bf16* res;    // [B, 28, 28, 128] or null
+  bf16* y;            // [B, 28, 28, 128]
+  int relu;
+};
+
+constexpr int kH = 28, kW = 28, kC = 128;
+constexpr int kR = 4;                 // output rows per step
+constexpr int kSteps = kH / kR;       // 7
+constexpr int kPlane = 30 * 64;       // one channel quarter of a staged row: 1920 B
+constexpr int kRB = 4 * kPlane;       // 7680 B per staged row
+constexpr int kRing = 10;             // rows r0 - 1 .. r0 + 4 in use + 4 in flight
+constexpr int kSlotsAlloc = kRing + 2;
+constexpr int kRun = 4 * kW;          // 112 DMA chunks per quarter plane (slots 1..28)
+constexpr int kMF = kR * kW / 16;     // 7 pixel fragments per step
+constexpr int kKS = 9 * kC / 32;      // 36 K steps
+constexpr int kResCh = kMF * 16 * 16;  // residual chunks per step (112 pixels x 16)
+
+__device__ __forceinline__ int swz_of(int y, int x) { return ((kW * y + x) >> 1) & 3; }
+
+// DBG (experiments): bit 0 no row DMA in the loop, bit 1 no LDS reads in the
+// K loop, bit 2 no epilogue, bit 3 prologue only
+template <bool RES, int DBG = 0>
+__global__ __launch_bounds__(256, 1) void conv3x3_rows28_kernel(R28Args a) {
+  extern __shared__ __attribute__((aligned(16))) uint4 smem[];
+  char* ring = (char*)smem;
+  char* resbuf = ring + kSlotsAlloc * kRB;  // RES: [112 pixels][16 chunks]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, g = lane >> 4;
+  const int b = blockIdx.x;
+  const bf16* img = a.x + (long)b * kH * kW * kC;
+
+  for (int o = tid * 16; o < kSlotsAlloc * kRB; o += 256 * 16) *(uint4*)(ring + o) = make_uint4(0, 0, 0, 0);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  // input row yy -> ring slot (yy + 1) % 10 (+ guard slot 10 / 11 for slots
+  // 0 / 1); wave w stages quarter plane w: chunks 0..63 and 64..111 of its run.
+  // Row 28 (below the image) reuses a slot: its run is written as zeros.
+  auto load_row = [&](int yy) __attribute__((always_inline)) {
+    const int slot = (yy + 1) % kRing;
+    char* dst = ring + wave * kPlane + 64;
+#pragma unroll
+    for (int i0 = 0; i0 < kRun; i0 += 64) {
+      const int k = i0 + lane;
+      const int x = k >> 2, c = k & 3;
+      if (k < kRun) {
+        if (yy < kH) {
+          const bf16* src = img + ((long)((DBG & 32) ? 0 : yy) * kW + x) * kC + 32 * wave + 8 * (c ^ swz_of(yy, x));
+          dma16(src, dst + slot * kRB + i0 * 16);
+          if (slot < 2) dma16(src, dst + (slot + kRing) * kRB + i0 * 16);
+        } else {
+          *(uint4*)(dst + slot * kRB + k * 16) = make_uint4(0, 0, 0, 0);
+        }
+      }
+    }
+  };
+  for (int yy = 0; yy <= 4; ++yy) load_row(yy);
+
+  // ---- per-lane constants: fragment f = tile pixels p = 16 f + fr (row
+  // p / 28 of the step, column p % 28). col[f][kw]: in-row byte offset of
+  // quarter 0 for kernel row 1; rows 0 / 2 flip chunk bit 1 (XOR 32).
+  int prow[kMF], col[kMF][3];
+#pragma unroll
+  for (int f = 0; f < kMF; ++f) {
+    const int p = 16 * f + fr;
+    prow[f] = p / kW;
+    const int c = p % kW;
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) {
+      const int s = ((p + kw - 1) >> 1) & 3;  // K & ... of (r0 + prow, c + kw - 1), r0 % 4 == 0
+      col[f][kw] = (c + kw) * 64 + ((g ^ s) << 4);
+    }
+  }
+  const int ch0 = wave * 32;
+  bf16x8 w[kKS][2];
+#pragma unroll
+  for (int t = 0; t < kKS; ++t)
+#pragma unroll
+    for (int nf = 0; nf < 2; ++nf)
+      w[t][nf] = *(const bf16x8*)(a.wf + ((((long)wave * kKS + t) * 2 + nf) * 64 + lane) * 8);
+  // this lane's 8 output channels ch0 + 8g .. +7 (weight rows permuted, perm32)
+  float bs[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) bs[e] = a.bias[ch0 + 8 * g + e];
+  vm_wait<0>();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+
+  for (int step = 0; step < ((DBG & 8) ? 0 : kSteps); ++step) {
+    const int r0 = step * kR;  // output rows r0 .. r0 + 3; input rows r0 - 1 .. r0 + 4
+    if (step + 1 < kSteps && !(DBG & 1))
+      for (int yy = r0 + 5; yy <= r0 + 8; ++yy) load_row(yy);
+    // residual of this step's 112 output pixels -> LDS (lands during the K
+    // loop; registers are full of weights): 16-B chunk c of pixel p at
+    // physical chunk c ^ (p & 15), so the epilogue's reads are conflict free
+    const long obase = ((long)b * kH + r0) * kW * kC + ch0 + 8 * g;
+    if constexpr (RES) {
+      const bf16* rimg = a.res + ((long)b * kH + r0) * kW * kC;
+#pragma unroll
+      for (int j = 0; j < kResCh / 256; ++j) {
+        const int i = j * 256 + wave * 64 + lane;
+        const int p = i >> 4, c = i & 15;
+        dma16(rimg + (long)p * kC + 8 * (c ^ (p & 15)), resbuf + (j * 256 + wave * 64) * 16);
+      }
+    }
+    // ring slot of kernel row 0 of each fragment (+ kh rows: immediate, guard slots)
+    int rowoff[kMF];
+#pragma unroll
+    for (int f = 0; f < kMF; ++f) {
+      int sl = r0 % kRing + prow[f];  // slot of input row r0 + prow - 1
+      sl = sl >= kRing ? sl - kRing : sl;
+      rowoff[f] = sl * kRB;
+    }
+    floatx4 acc[kMF][2];
+#pragma unroll
+    for (int f = 0; f < kMF; ++f)
+#pragma unroll
+      for (int nf = 0; nf < 2; ++nf) acc[f][nf] = floatx4{0.f, 0.f, 0.f, 0.f};
+    // K step t: tap = t >> 2 (kh = tap / 3, kw = tap % 3), quarter q = t & 3
+    // tb[f]: fragment f's address for the current tap (quarter 0, kernel row
+    // 0's slot; kh and the quarter are immediates). Computed by volatile asm
+    // at its point of use, so the compiler neither hoists nor keeps the 63
+    // per-(fragment, tap) sums live (the weights hold 288 registers).
+    int tb[kMF];
+    auto tap_addr = [&](int tap, int f) __attribute__((always_inline)) {
+      const int kh = tap / 3, kw = tap % 3;
+      if (kh == 1)
+        asm volatile("v_add_u32 %0, %1, %2" : "=v"(tb[f]) : "v"(rowoff[f]), "v"(col[f][kw]));
+      else
+        asm volatile("v_xor_b32 %0, 32, %1\n\tv_add_u32 %0, %2, %0" : "=&v"(tb[f]) : "v"(col[f][kw]), "v"(rowoff[f]));
+    };
+    auto xread = [&](int t, int f) __attribute__((always_inline)) {
+      const int tap = t >> 2, q = t & 3;
+      if (q == 0) tap_addr(tap, f);
+      return *(const bf16x8*)(ring + tb[f] + (tap / 3) * kRB + q * kPlane);
+    };
+    bf16x8 xc[kMF];
+#pragma unroll
+    for (int f = 0; f < kMF; ++f) xc[f] = xread(0, f);
+#pragma unroll
+    for (int t = 0; t < kKS; ++t) {
+#pragma unroll
+      for (int f = 0; f < kMF; ++f) {
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int nf = 0; nf < 2; ++nf)
+          acc[f][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[t][nf], xc[f], acc[f][nf], 0, 0, 0);
+        if (t + 1 < kKS && !(DBG & 2)) xc[f] = xread(t + 1, f);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (RES) {  // this wave's residual DMAs (the youngest VMEM ops) have landed; and everyone's
+      vm_wait<0>();
+      __builtin_amdgcn_s_barrier();
+    }
+    // ---- epilogue: lane holds channels ch0 + 8g .. +7 of tile pixel 16 f + fr
+#pragma unroll
+    for (int f = 0; f < ((DBG & 4) ? 0 : kMF); ++f) {
+      float v[8];
+#pragma unroll
+      for (int nf = 0; nf < 2; ++nf)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[4 * nf + i] = acc[f][nf][i] + bs[4 * nf + i];
+      if constexpr (RES) {
+        float r[8];
+        unpack8(*(const uint4*)(resbuf + (16 * f + fr) * 256 + (((4 * wave + g) ^ fr) << 4)), r);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += r[e];
+      }
+      if (a.relu) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+      }
+      *(uint4*)(a.y + obase + (long)(16 * f + fr) * kC) = pack8(v);
+    }
+    // the next step's rows have landed (older than the kMF stores just
+    // issued: vmcnt retires in order) and every wave is done with the rows
+    // they replace
+    if constexpr (!(DBG & 16)) vm_wait<kMF>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+}
+
+}  // namespace
+
+bool conv3x3_rows28_supported(int H, int W, int Cin, int Cout) {
+  return H == kH && W == kW && Cin == kC && Cout == kC;
+}
+
+void conv3x3_rows28(const void* x, const void* wf, const float* bias, const void* res, void* y, int B, bool relu,
+                    hipStream_t s, int dbg) {
+  if (B <= 0) return;
+  if (!x || !wf || !bias || !y ||
+      (((uintptr_t)x | (uintptr_t)wf | (uintptr_t)res | (uintptr_t)y) & 15))
+    throw std::invalid_argument("conv3x3_rows28: null / misaligned operand");
+  if (x == y || (res && res == y)) throw std::invalid_argument("conv3x3_rows28: in-place not supported");
+  R28Args a;
+  a.x = (const bf16*)x;
+  a.wf = (const bf16*)wf;
+  a.bias = bias;
+  a.res = (const bf16*)res;
+  a.y = (bf16*)y;
+  a.relu = relu;
+  const size_t lds = (size_t)kSlotsAlloc * kRB + (res ? (size_t)kResCh * 16 : 0);  // 90 / 118 KB
+  switch (dbg) {
+    case 1: hipLaunchKernelGGL((conv3x3_rows28_kernel<false, 1>), dim3(B), dim3(256), lds, s, a); break;
+    case 2: hipLaunchKernelGGL((conv3x3_rows28_kernel<false, 2>), dim3(B), dim3(256), lds, s, a); break;
+    case 4: hipLaunchKernelGGL((conv3x3_rows28_kernel<false, 4>), dim3(B), dim3(256), lds, s, a); break;
+    case 7: hipLaunchKernelGGL((conv3x3_rows28_kernel<false, 7>), dim3(B), dim3(256), lds, s, a); break;
+    case 8: hipLaunchKernelGGL((conv3x3_rows28_kernel<false, 8>), dim3(B), dim3(256), lds, s, a); break;
+    case 16: hipLaunchKernelGGL((conv3x3_rows28_kernel<false, 16>), dim3(B), dim3(256), lds, s, a); break;
+    case 32: hipLaunchKernelGGL((conv3x3_rows28_kernel<false, 32>), dim3(B), dim3(256), lds, s, a); break;
+    default:
+      if (res)
+        hipLaunchKernelGGL(conv3x3_rows28_kernel<true>, dim3(B), dim3(256), lds, s, a);
+      else
+        hipLaunchKernelGGL(conv3x3_rows28_kernel<false>, dim3(B), dim3(256), lds, s, a);
+  }
+  DMLC_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace dmlc

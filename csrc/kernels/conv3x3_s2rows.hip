@@ -61,7 +61,7 @@ constexpr int kHalf = 3712;           // bytes per K-half plane (58 slots x 64 B
 constexpr int kRB = 2 * kHalf;        // 7424 B per staged row
 constexpr int kRing = 17;             // rows 2 r0 - 1 .. 2 r0 + 7 in use + 8 in flight
 constexpr int kSlotsAlloc = kRing + 2;
-constexpr int kRowCh = kRB / 16;      // 464 DMA chunks per row
+constexpr int kRun = 4 * 2 * kW;      // 224 DMA chunks per K-half plane (slots 1..56)
 constexpr int kMF = kR * kW / 16;     // 7 pixel fragments per step
 constexpr int kKT = 18, kCT = 2;      // 3x3 / downsample K steps
 constexpr int kKS = kKT + kCT;
@@ -78,26 +78,33 @@ __global__ __launch_bounds__(256, 1) void conv3x3_s2rows_kernel(S2Args a) {
   const int b = blockIdx.x;
   const bf16* img = a.x + (long)b * kHI * kWI * kCI;
 
-  // input row yy (-1: zero row) -> ring slot (yy + 1) % 17, and the guard
-  // slot 17 / 18 too for slots 0 / 1; the 4 waves share the chunks
+  // Every slot's pad column (slot 0 of each K-half plane), its spare slot
+  // and the zero row y = -1 are zeroed once here and never DMA'd over (a
+  // shared zero page read by every workgroup's pad lanes is one hot L2
+  // channel per XCD).
+  for (int o = tid * 16; o < kSlotsAlloc * kRB; o += 256 * 16) *(uint4*)(ring + o) = make_uint4(0, 0, 0, 0);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  // input row yy >= 0 -> ring slot (yy + 1) % 17, and guard slot 17 / 18 too
+  // for slots 0 / 1: per K-half plane the 224 chunks of slots 1..56 are one
+  // contiguous run; wave w DMAs chunks 64 w .. 64 w + 63 of both runs
   auto load_row = [&](int yy) __attribute__((always_inline)) {
     const int slot = (yy + 1) % kRing;
-    const bool inside = (unsigned)yy < (unsigned)kHI;
-    for (int c0 = wave * 64; c0 < kRowCh; c0 += 4 * 64) {
-      const int i = c0 + lane;
-      const int h = i >= kRowCh / 2, j = i - h * (kRowCh / 2);
-      const int pos = j >> 2, c = j & 3;
-      const int x = pos == 0 ? -1 : (pos < kE0 ? 2 * pos - 1 : 2 * (pos - kE0));
-      const int lc = 4 * h + (c ^ swz_of(yy, x));
-      const bool ok = inside && x >= 0 && pos <= 2 * kW;
-      const bf16* src = ok ? img + ((long)yy * kWI + x) * kCI + 8 * lc : a.zero;
-      if (i < kRowCh) {
-        dma16(src, ring + slot * kRB + c0 * 16);
-        if (slot < 2) dma16(src, ring + (slot + kRing) * kRB + c0 * 16);
+    const int k = wave * 64 + lane;
+    const int pos = 1 + (k >> 2), c = k & 3;
+    const int x = pos < kE0 ? 2 * pos - 1 : 2 * (pos - kE0);
+    const int sw = swz_of(yy, x);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const bf16* src = img + ((long)yy * kWI + x) * kCI + 8 * (4 * h + (c ^ sw));
+      char* dst = ring + h * kHalf + 64 + wave * 1024;
+      if (k < kRun) {
+        dma16(src, dst + slot * kRB);
+        if (slot < 2) dma16(src, dst + (slot + kRing) * kRB);
       }
     }
   };
-  for (int yy = -1; yy <= 7; ++yy) load_row(yy);
+  for (int yy = 0; yy <= 7; ++yy) load_row(yy);
 
   // ---- per-lane constants. Fragment f covers tile pixels p = 16 f + fr (row
   // p / 28 of the step, column c = p % 28). col[f][v]: the in-row byte offset

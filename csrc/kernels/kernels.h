@@ -160,6 +160,12 @@ void conv3x3_block(const void* x, const void* wf1, const float* bias1, const voi
 bool conv3x3_s2rows_supported(int Hin, int Win, int Cin, int Cout);
 void conv3x3_s2rows(const void* x, const void* wf, const float* bias, const void* wdf, const float* bd, void* y,
                     void* yd, const void* zero, int B, bool relu, hipStream_t s, int dbg = 0);
+// Weight-stationary row-streaming 3x3/s1/p1 conv for 28x28x128 -> 128
+// (conv3x3_rows28.hip): one workgroup per image, the weights in registers.
+// wf: fragment-order weights (stream_frag_index, K = 1152); res optional.
+bool conv3x3_rows28_supported(int H, int W, int Cin, int Cout);
+void conv3x3_rows28(const void* x, const void* wf, const float* bias, const void* res, void* y, int B, bool relu,
+                    hipStream_t s, int dbg = 0);
 // Direct 3x3/p1 conv with the input image resident in LDS and per-wave weight
 // rings (conv3x3_stream.hip): stride 1 on 28x28x128, 14x14x256, 7x7x512;
 // stride 2 on 56x56x64 -> 128 and 28x28x128 -> 256. Hin/Win are the input

@@ -83,6 +83,7 @@ bool EngineOptions::set(const std::string& name, bool v) {
       {"fused_head", &EngineOptions::fused_head},   {"fc_small", &EngineOptions::fc_small},
       {"fork_ds", &EngineOptions::fork_ds},         {"fp8_3x3", &EngineOptions::fp8_3x3},
       {"conv1x1", &EngineOptions::conv1x1},         {"s2rows", &EngineOptions::s2rows},
+      {"rows28", &EngineOptions::rows28},
   };
   for (const auto& f : fields)
     if (name == f.first) {
@@ -421,7 +422,9 @@ void Engine::pack_weights(const WeightMap& w) {
              (conv3x3_stream_uses_frag(shapes_[L.in_act].H, shapes_[L.in_act].W, shapes_[L.in_act].C, L.cout,
                                        L.stride) ||
               (L.stride == 2 &&
-               conv3x3_s2rows_supported(shapes_[L.in_act].H, shapes_[L.in_act].W, shapes_[L.in_act].C, L.cout))) ||
+               conv3x3_s2rows_supported(shapes_[L.in_act].H, shapes_[L.in_act].W, shapes_[L.in_act].C, L.cout)) ||
+              (L.kh == 3 && L.stride == 1 && L.pad == 1 &&
+               conv3x3_rows28_supported(shapes_[L.in_act].H, shapes_[L.in_act].W, shapes_[L.in_act].C, L.cout))) ||
          (L.kh == 3 && L.kw == 3 && L.stride == 1 && L.pad == 1 &&
           conv3x3_rows_supported(shapes_[L.in_act].H, shapes_[L.in_act].W, shapes_[L.in_act].C, L.cout)))) {
       L.wf_off = off;  // fragment-order copy for the register-weight stream conv
@@ -624,6 +627,13 @@ Engine::ConvPath Engine::conv_path(const Op& op, int B) const {
   // register weights 48.1 vs 13.2 + 46.3 us (profiles/r1_fused_ds.txt)
   const bool l4s2 = L.stride == 2 && is.H < 28 && !(opt_.stream_l4s2 && opt_.stream_wreg);
   const bool l1 = L.stride == 1 && is.C == 64;  // layer1: conv3x3_rows (the stream conv measured slower there)
+  // layer2's stride-1 convs: one weight-stationary workgroup per image walking
+  // its rows (59-60 us vs 62-66 us for the stream conv at B=256,
+  // profiles/r2_rows28.txt), once the batch fills >= ~70% of one round
+  const int rounds = (B + num_cus_ - 1) / num_cus_;
+  if (opt_.rows28 && k3 && L.stride == 1 && L.wf_off && 10 * B >= 7 * rounds * num_cus_ &&
+      conv3x3_rows28_supported(is.H, is.W, is.C, L.cout))
+    return ConvPath::Rows28;
   if (opt_.stream_conv && k3 && !l4s2 && !l1 && 8 * B >= num_cus_ &&
       conv3x3_stream_supported(is.H, is.W, is.C, L.cout, L.stride))
     return ConvPath::Stream;
@@ -824,6 +834,11 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
             skip_ds = -1;
             break;
           }
+          case ConvPath::Rows28:
+            conv3x3_rows28(acts_[op.in], (const uint8_t*)warena_ + L.wf_off,
+                           (const float*)((const uint8_t*)warena_ + L.b_off), op.res >= 0 ? acts_[op.res] : nullptr,
+                           acts_[op.out], B, L.relu, cs);
+            break;
           case ConvPath::Rows:
             conv3x3_rows(acts_[op.in], (const uint8_t*)warena_ + L.w_off,
                          (const float*)((const uint8_t*)warena_ + L.b_off), op.res >= 0 ? acts_[op.res] : nullptr,

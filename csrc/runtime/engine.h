@@ -75,6 +75,7 @@ struct EngineOptions {
   bool fuse_ds = true;           // the block's 1x1/s2 downsample inside the stride-2 stream conv1
   bool s2rows = true;            // ... layer2.0 (56x56x64 -> 128): one weight-stationary kernel per image
                                  // walking its rows (conv3x3_s2rows.hip), B >= 0.7 x CUs
+  bool rows28 = true;            // layer2's stride-1 convs the same way (conv3x3_rows28.hip), B >= 0.7 x CUs
   bool bigtile = true;           // 8-wave big-tile split-K convs where picked (not on the ResNet18 b256 path)
   bool conv1x1 = true;           // weight-stationary 1x1 convs (conv1x1.hip: ResNet50 bottlenecks)
   bool fused_pool = true;        // the last conv's epilogue computes the global average pool
@@ -157,7 +158,7 @@ class Engine {
   void run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* idx, float* prob,
                float* logits, hipStream_t s, std::vector<hipEvent_t>* evs, bool trace);
   ConvArgs conv_args(const Op& op, int B, float* logits) const;
-  enum class ConvPath { Stream, Rows, OneByOne, BigTile, Igemm };
+  enum class ConvPath { Stream, Rows, Rows28, OneByOne, BigTile, Igemm };
   ConvPath conv_path(const Op& op, int B) const;
   bool side_safe(int B) const;
   bool head_fusable(size_t oi) const;

@@ -220,6 +220,26 @@ def conv3x3_s2rows(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, 
     return y, yd
 
 
+def conv3x3_rows28(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, res: torch.Tensor | None = None,
+                   relu: bool = True) -> torch.Tensor:
+    """Weight-stationary row-streaming 3x3/s1/p1 conv on [B,28,28,128] ->
+    128 channels (conv3x3_rows28.hip): relu?(conv(x) + bias (+ res)).
+    w_packed: conv2d packed weights [128, 1152]."""
+    _need_cuda(x, w_packed, bias, res)
+    C = native()
+    B, H, W, Cin = x.shape
+    Cout = w_packed.shape[0]
+    if not C.conv3x3_rows28_supported(H, W, Cin, Cout) or tuple(w_packed.shape) != (Cout, 9 * Cin):
+        raise ValueError("conv3x3_rows28: unsupported shape")
+    if res is not None and tuple(res.shape) != (B, H, W, Cout):
+        raise ValueError("conv3x3_rows28: residual shape")
+    x = x.contiguous()
+    y = torch.empty_like(x)
+    C.conv3x3_rows28(_ptr(x), _ptr(stream_weight_frag(w_packed)), _ptr(bias.float().contiguous()),
+                     _ptr(None if res is None else res.contiguous()), _ptr(y), B, relu, _stream())
+    return y
+
+
 def stream_weight_frag(w_packed: torch.Tensor, cout: int | None = None) -> torch.Tensor:
     """Packed conv weights [Npad, K] -> the stream conv's fragment order
     [Cout/32][K/32][2][64 lanes][8]: lane l of fragment nf of channel group g,

@@ -251,16 +251,18 @@ def test_fused_block_matches_unfused(gpu):
     assert torch.equal(fl, rl) and torch.equal(fi, ri)
 
 
-def test_s2rows_matches_stream(gpu):
-    """ResNet18's layer2.0 conv1 + downsample as one row-streaming kernel
-    (conv3x3_s2rows.hip) vs the stream conv with the fused downsample
-    (options s2rows=False): different accumulation order, so logits agree to
-    bf16 rounding, not bit for bit."""
+@pytest.mark.parametrize("option", ["s2rows", "rows28"])
+def test_weight_stationary_rows_match_stream(gpu, option):
+    """ResNet18's layer2 convs as weight-stationary row-streaming kernels
+    (s2rows: layer2.0 conv1 + downsample, conv3x3_s2rows.hip; rows28: the
+    stride-1 convs, conv3x3_rows28.hip) vs the stream conv (the option off):
+    different accumulation order, so logits agree to bf16 rounding, not bit
+    for bit."""
     model = build("resnet18", seed=45, randomize_bn=True)
     sd = state_dict_f32(model)
     g = torch.Generator().manual_seed(46)
     img = torch.randint(0, 256, (192, 224, 224, 3), generator=g, dtype=torch.uint8).to(gpu)
-    ref_eng = InferenceEngine("resnet18", sd, max_batch=192, options={"s2rows": False})
+    ref_eng = InferenceEngine("resnet18", sd, max_batch=192, options={option: False})
     eng = InferenceEngine("resnet18", sd, max_batch=192)
     ri, _, rl = ref_eng.predict(img, return_logits=True)
     fi, _, fl = eng.predict(img, return_logits=True)

@@ -435,6 +435,30 @@ def test_conv3x3_s2rows(gpu, B):
     assert (yd.float() - yd0.float()).abs().max().item() < 0.05
 
 
+@pytest.mark.parametrize("B,res", [(1, False), (3, True), (2, False)])
+def test_conv3x3_rows28(gpu, B, res):
+    """Weight-stationary row-streaming layer2 conv (conv3x3_rows28.hip) vs
+    torch fp32, and vs the stream conv on the same operands."""
+    g = torch.Generator().manual_seed(41)
+    x = torch.randn(B, 128, 28, 28, generator=g).bfloat16().float()
+    w = (torch.randn(128, 128, 3, 3, generator=g) / 34).bfloat16().float()
+    bias = torch.randn(128, generator=g) * 0.1
+    r = torch.randn(B, 128, 28, 28, generator=g).bfloat16().float() if res else None
+    ref = F.conv2d(x, w, bias, 1, 1)
+    if res:
+        ref = ref + r
+    ref = F.relu(ref)
+    xg = _nhwc(x).bfloat16().to(gpu)
+    rg = _nhwc(r).bfloat16().to(gpu) if res else None
+    wp = ops.pack_conv_weight(w, device=gpu)
+    y = ops.conv3x3_rows28(xg, wp, bias.to(gpu), rg, True)
+    y0 = ops.conv3x3_stream(xg, wp, bias.to(gpu), rg, True)
+    torch.cuda.synchronize()
+    got = _nchw(y.float().cpu())
+    assert _rel(got, ref) < 5e-3, _rel(got, ref)
+    assert (y.float() - y0.float()).abs().max().item() < 0.05
+
+
 def test_preprocess_paired(gpu):
     g = torch.Generator().manual_seed(12)
     img = torch.randint(0, 256, (2, 224, 224, 3), generator=g, dtype=torch.uint8)

@@ -101,7 +101,7 @@ def test_block_conv_lds_layout_conflict_free():
     chunk c of column q holding channels 8*(4h + (c ^ ((q >> 1) & 3)))):
     the input-fragment reads of both halves (h = 1 at a fixed +3712 B) and
     the producers' ds_write_b128 of the intermediate are conflict free; the
-    DMA staging order covers every (h, q, chunk) exactly once."""
+    DMA staging order covers every in-image (h, q, chunk) exactly once."""
     W, R, Q = 56, 4, 58
     half = Q * 64
     slot = 2 * half
@@ -125,11 +125,16 @@ def test_block_conv_lds_layout_conflict_free():
                     q = p % W + 1
                     addr.append((p // W) * slot + wn * half + q * 64 + ((g ^ ((q >> 1) & 3)) << 4))
                 assert _b128_ways(addr) == 1, (wm, f, wn)
-    seen = set()
-    for i in range(Q * 8):  # load_row: chunk i -> (h, q, c) -> source channel group
-        h, q, c = i // (Q * 4), (i >> 2) % Q, i & 3
-        seen.add((q, 4 * h + (c ^ ((q >> 1) & 3))))
-    assert seen == {(q, cg) for q in range(Q) for cg in range(8)}
+    seen, dst = set(), set()
+    for h in range(2):  # load_row: chunk k of K half h's run (q = 1..56) -> LDS chunk, source channel group
+        for k in range(4 * W):
+            q, c = 1 + k // 4, k % 4
+            dst.add(h * half // 16 + 4 + k)
+            seen.add((q, 4 * h + (c ^ ((q >> 1) & 3))))
+    assert seen == {(q, cg) for q in range(1, W + 1) for cg in range(8)}
+    # never DMA'd (zeroed at kernel start): the pad columns q = 0, 57 of both halves
+    assert {i for i in range(slot // 16) if i not in dst} == {h * half // 16 + j for h in range(2)
+                                                               for j in (0, 1, 2, 3, 228, 229, 230, 231)}
 
 
 def test_stem_pool_lds_reads_conflict_free():
@@ -244,13 +249,63 @@ def test_s2rows_lds_layout():
                             # stored chunk holds logical chunk 4h + (phys ^ swz(y, x)) == 4h + g
                             assert ((j % 64) // 16) ^ _s2rows_swz(y, x) == g
                         assert _b128_ways(addr) == 1, (r0, f, kh, kw, h)
-    seen = set()
-    for i in range(RB // 16):  # load_row: chunk i -> (h, pos, c) -> source column / channel chunk
-        h, j = i // (HALF // 16), i % (HALF // 16)
-        pos, c = j >> 2, j & 3
-        if pos > 56:
-            continue
-        x = -1 if pos == 0 else (2 * pos - 1 if pos < 29 else 2 * (pos - 29))
-        assert _s2rows_pos(x) == pos
-        seen.add((x, 4 * h + (c ^ _s2rows_swz(0, x))))
-    assert seen == {(x, cc) for x in range(-1, 56) for cc in range(8)}
+    seen, dst = set(), set()
+    for h in range(2):  # load_row: chunk k of K-half h's run -> LDS chunk, source column / channel chunk
+        for k in range(224):
+            pos, c = 1 + k // 4, k % 4
+            x = 2 * pos - 1 if pos < 29 else 2 * (pos - 29)
+            assert _s2rows_pos(x) == pos
+            dst.add(h * HALF // 16 + 4 + k)
+            seen.add((x, 4 * h + (c ^ _s2rows_swz(0, x))))
+    assert seen == {(x, cc) for x in range(56) for cc in range(8)}
+    # the chunks never DMA'd (pad slot 0 and spare slot 57 of each plane) stay zero
+    assert {i for i in range(RB // 16) if i not in dst} == {h * HALF // 16 + j for h in range(2) for j in (0, 1, 2, 3, 228, 229, 230, 231)}
+
+
+def test_rows28_lds_layout():
+    """conv3x3_rows28.hip: every ds_read_b128 of a 112-pixel step (7
+    fragments x 9 taps x 4 channel quarters, all 7 steps, through the
+    10-row ring with its 2 guard slots) is conflict free and reads the
+    channels its weight fragment expects; the per-wave DMA runs cover every
+    (column, channel chunk) once and leave the pad slots alone."""
+    RB, PLANE, RING = 7680, 1920, 10
+
+    def swz(y, x):
+        return ((28 * y + x) >> 1) & 3
+
+    for r0 in range(0, 28, 4):
+        for f in range(7):
+            for kh in range(3):
+                for kw in range(3):
+                    for q in range(4):
+                        addr = []
+                        for l in range(64):
+                            fr, g = l & 15, l >> 4
+                            p = 16 * f + fr
+                            y, x = r0 + p // 28 + kh - 1, p % 28 + kw - 1
+                            sl = r0 % RING + p // 28
+                            sl = sl - RING if sl >= RING else sl
+                            s = ((p + kw - 1) >> 1) & 3
+                            col = (p % 28 + kw) * 64 + ((g ^ s) << 4)
+                            a = sl * RB + (col ^ (0 if kh == 1 else 32)) + kh * RB + q * PLANE
+                            addr.append(a)
+                            assert a // RB % RING == (y + 1) % RING and a // RB < RING + 2
+                            off = a % RB
+                            assert off // PLANE == q and (off % PLANE) // 64 == x + 1
+                            if 0 <= x < 28:
+                                assert ((off % 64) // 16) ^ swz(y, x) == g
+                        assert _b128_ways(addr) == 1, (r0, f, kh, kw, q)
+    seen, dst = set(), set()
+    for wave in range(4):
+        for k in range(112):
+            x, c = k >> 2, k & 3
+            dst.add(wave * PLANE // 16 + 4 + k)
+            seen.add((x, 4 * wave + (c ^ swz(3, x))))
+    assert seen == {(x, cc) for x in range(28) for cc in range(16)}
+    assert {i for i in range(RB // 16) if i not in dst} == {w * PLANE // 16 + j for w in range(4)
+                                                             for j in (0, 1, 2, 3, 116, 117, 118, 119)}
+    # epilogue residual reads: chunk (4 wave + g) ^ fr of pixel 16 f + fr
+    for f in range(7):
+        for wave in range(4):
+            addr = [(16 * f + (l & 15)) * 256 + (((4 * wave + (l >> 4)) ^ (l & 15)) << 4) for l in range(64)]
+            assert _b128_ways(addr) == 1
