@@ -24,7 +24,7 @@
 //    lane holds 4 consecutive output columns of one channel.
 //  * Pool: the horizontal 3-max is then mostly lane-local: columns
 //    4g..4g+3 of a lane give pooled columns 2g (plus column 4g-1, fetched
-//    with one ds_bpermute from the lane 16 below) and 2g+1. +bias and ReLU
+//    from the lane 16 below with two row-swap permutes) and 2g+1. +bias and ReLU
 //    are applied after the max (both monotone, so they commute with it),
 //    and the results go to a 5-row LDS ring of pooled conv rows ([pw][64 ch],
 //    16-B channel chunks XOR-swizzled by pw so the 4 row groups of a wave
@@ -101,6 +101,22 @@ __device__ __forceinline__ void ds_write_hi16(uint32_t addr, uint32_t v, const i
 __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
+}
+
+// y[l] = x[(l - 16) mod 64]: rotate the wave's four 16-lane rows down by one
+// with the gfx950 row-swap permutes (VALU only; a ds_bpermute here made each
+// of the 4 channel blocks of a fragment epilogue wait a full LDS round trip,
+// and its lgkmcnt wait also drained the epilogue's own LDS stores).
+// permlane32_swap(x, x): [0] = rows (0,1,0,1), [1] = rows (2,3,2,3);
+// z = rows (2,3,0,1); permlane16_swap(z, x): [0] = (2,0,0,2), [1] = (3,1,1,3):
+// odd rows from [0], even rows from [1].
+// Semantics checked on the GPU by tools/probes/permlane_probe.hip.
+__device__ __forceinline__ float rot_rows_down1(float x, int lane) {
+  const unsigned u = __float_as_uint(x);
+  const auto p32 = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  const unsigned z = lane < 32 ? p32[1] : p32[0];
+  const auto p16 = __builtin_amdgcn_permlane16_swap(z, u, false, false);
+  return __uint_as_float((lane & 16) ? p16[0] : p16[1]);
 }
 
 // The whole geometry follows from the image size S = 32 NF (NF = output
@@ -247,7 +263,6 @@ __global__ __launch_bounds__(256, 2) void stem_conv_pool_kernel(
         for (int s = 0; s < 7; ++s) rows[s] = ((2 * cr + s) % RING) * RB;
         // per-lane store base: column 2g, channel chunk r/8, element r%8
         const uint32_t hbase = lds_addr(hrow) + fq * 2 * kHpCol + (fr >> 3) * 16 + (fr & 7) * 2;
-        const int nb_addr = ((lane + 48) & 63) << 2;  // read lane (l - 16) mod 64
         float prev3[4];  // column 16f+15 of the previous fragment, per channel block
         bf16x8 xf[7];
 #pragma unroll
@@ -262,6 +277,13 @@ __global__ __launch_bounds__(256, 2) void stem_conv_pool_kernel(
 #pragma unroll
             for (int n = 0; n < 4; ++n)
               acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[s], wf[n][s], acc[n], 0, 0, 0);
+          // The next fragment's operands go out before this epilogue so the
+          // reads land under it.
+          if (f + 1 < NF) {
+#pragma unroll
+            for (int s = 0; s < 7; ++s)
+              xf[s] = *(const bf16x8*)(rbase + rows[s] + (f + 1) * 256);
+          }
           // Horizontal 3-max over columns (2pw-1, 2pw, 2pw+1), + bias, ReLU.
           // Lane (r, g) holds columns 16f + 4g + i (i = 0..3) of channel
           // 16n + r: pooled columns 8f + 2g (needs column 16f + 4g - 1, the
@@ -271,7 +293,7 @@ __global__ __launch_bounds__(256, 2) void stem_conv_pool_kernel(
           for (int n = 0; n < 4; ++n) {
             const floatx4 v = acc[n];
             const float src = (f > 0 && fq == 3) ? prev3[n] : v[3];
-            float nb = __int_as_float(__builtin_amdgcn_ds_bpermute(nb_addr, __float_as_int(src)));
+            float nb = rot_rows_down1(src, lane);
             if (f == 0) nb = fq == 0 ? v[0] : nb;  // first image column: no left neighbour
             float2v p = {fmaxf(fmaxf(nb, v[0]), v[1]), fmaxf(fmaxf(v[1], v[2]), v[3])};
             p += float2v{bs[n], bs[n]};
@@ -282,11 +304,6 @@ __global__ __launch_bounds__(256, 2) void stem_conv_pool_kernel(
             ds_write_lo16(hbase, packed, f * 8 * kHpCol + n * 32);
             ds_write_hi16(hbase, packed, f * 8 * kHpCol + n * 32 + kHpCol);
             prev3[n] = v[3];
-          }
-          if (f + 1 < NF) {
-#pragma unroll
-            for (int s = 0; s < 7; ++s)
-              xf[s] = *(const bf16x8*)(rbase + rows[s] + (f + 1) * 256);
           }
         }
       }
