@@ -308,11 +308,12 @@ __global__ __launch_bounds__(256, 2) void stem_conv_pool_kernel(
         }
       }
     }
+    // One barrier between the MFMA phase and the pooled-row / conversion
+    // phase: the next step's rows (issued at the top of the step) have landed
+    // by now, so the wait for them moves ahead of it and the vertical max and
+    // the u8 conversion share one phase (they touch disjoint LDS).
+    vm_wait<0>();
     lds_barrier();
-
-    // Stores this wave issues below (wave-uniform: 16*PW items, PW % 8 == 0).
-    const int items = 16 * G::PW;
-    const int nst = t > 0 ? __builtin_amdgcn_readfirstlane(tid < items ? (items - 1 - tid) / 256 + 1 : 0) : 0;
     if (t > 0) {  // vertical 3-max -> pooled rows ph, ph+1
       const int ph = ph0 + 2 * (t - 1);
       const int per_row = G::PW * 8;
@@ -342,22 +343,14 @@ __global__ __launch_bounds__(256, 2) void stem_conv_pool_kernel(
         }
       }
     }
-    // The next step's rows have landed. vmcnt retires in issue order, so
-    // leaving this step's `nst` younger stores in flight still covers the DMA.
-    switch (nst) {
-      case 0: vm_wait<0>(); break;
-      case 1: vm_wait<1>(); break;
-      case 2: vm_wait<2>(); break;
-      case 3: vm_wait<3>(); break;
-      default: vm_wait<4>(); break;
-    }
-    lds_barrier();
     if constexpr (U8) {
-      if (t < T) {  // the next step's raw rows landed; the rows they replace are no longer read
-        convert_rows(2 * c0 + 13, 8);
-        lds_barrier();
-      }
+      // the next step's raw rows landed; the paired rows they replace were
+      // last read by this step's MFMAs (before the barrier above)
+      if (t < T) convert_rows(2 * c0 + 13, 8);
     }
+    // the next step's MFMAs overwrite pooled rows read above and read the
+    // converted rows
+    lds_barrier();
   }
 }
 
