@@ -6,11 +6,13 @@
 //                      multi-GPU serving, elastic on GPU loss)
 //   dp_host_run        the same protocol over the host fake (CPU tests:
 //                      shard order, exactly-once answers, rank loss)
+#include <hip/hip_runtime.h>
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
 #include <thread>
+#include <vector>
 
 #include "../comm/comm.h"
 #include "../comm/dp.h"
@@ -40,7 +42,8 @@ class DpRunner {
     r_ = std::make_unique<dp::Rank>(w_.get(), max_, ib(), scatter_, std::max(2, lanes));
     if (world_ > 1) {
       cin_ = comm::rccl_init_rank(id_in, world_, rank_, e->device());
-      cout_ = comm::rccl_init_rank(id_out, world_, rank_, e->device());
+      // answers: 8 B per image, one CTA (comm::rccl_init_rank's max_ctas)
+      cout_ = comm::rccl_init_rank(id_out, world_, rank_, e->device(), 1);
       r_->attach(cin_.get(), cout_.get());
     } else {
       r_->attach(nullptr, nullptr);
@@ -247,9 +250,42 @@ py::dict dp_host_run(py::array_t<uint8_t, py::array::c_style> images, int world,
   return out;
 }
 
+// One-rank RCCL communicator on `device` (optionally CTA-capped) moving
+// `bytes` to itself with a grouped send/recv and a broadcast: exercises the
+// RcclComm wrapper and librccl on a one-GPU box (tests/test_dp_native_gpu.py).
+bool rccl_loopback(int device, size_t bytes, int max_ctas) {
+  if (hipSetDevice(device) != hipSuccess) throw std::runtime_error("rccl_loopback: hipSetDevice");
+  auto c = comm::rccl_init_rank(comm::rccl_unique_id(), 1, 0, device, max_ctas);
+  hipStream_t s;
+  uint8_t *a, *b, *d;
+  if (hipStreamCreate(&s) != hipSuccess || hipMalloc(&a, bytes) != hipSuccess || hipMalloc(&b, bytes) != hipSuccess ||
+      hipMalloc(&d, bytes) != hipSuccess)
+    throw std::runtime_error("rccl_loopback: allocation");
+  std::vector<uint8_t> h(bytes), g(bytes), g2(bytes);
+  for (size_t i = 0; i < bytes; ++i) h[i] = (uint8_t)(i * 131 + 7);
+  bool ok = hipMemcpy(a, h.data(), bytes, hipMemcpyHostToDevice) == hipSuccess &&
+            hipMemset(b, 0, bytes) == hipSuccess && hipMemset(d, 0, bytes) == hipSuccess;
+  c->group_start();
+  c->send(a, bytes, 0, s);
+  c->recv(b, bytes, 0, s);
+  c->group_end();
+  c->broadcast(a, d, bytes, 0, s);
+  ok = ok && hipStreamSynchronize(s) == hipSuccess && c->ok();
+  ok = ok && hipMemcpy(g.data(), b, bytes, hipMemcpyDeviceToHost) == hipSuccess &&
+       hipMemcpy(g2.data(), d, bytes, hipMemcpyDeviceToHost) == hipSuccess;
+  ok = ok && g == h && g2 == h;
+  c.reset();
+  (void)hipFree(a);
+  (void)hipFree(b);
+  (void)hipFree(d);
+  (void)hipStreamDestroy(s);
+  return ok;
+}
+
 }  // namespace
 
 void bind_dp(py::module& m) {
+  m.def("rccl_loopback", &rccl_loopback, py::arg("device") = 0, py::arg("bytes") = 1 << 20, py::arg("max_ctas") = 0);
   m.def("rccl_unique_id", []() { return py::bytes(comm::rccl_unique_id()); });
   m.def("dp_shard_counts", &dp::shard_counts);
   m.def("dp_host_run", &dp_host_run, py::arg("images"), py::arg("world"), py::arg("max_per_rank"),

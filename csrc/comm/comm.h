@@ -85,7 +85,8 @@ constexpr size_t kUniqueIdBytes = 128;  // NCCL_UNIQUE_ID_BYTES
 std::string rccl_unique_id();
 // One rank of an nranks communicator on HIP device `device` (one process
 // per GPU).
-std::unique_ptr<Comm> rccl_init_rank(const std::string& unique_id, int nranks, int rank, int device);
+std::unique_ptr<Comm> rccl_init_rank(const std::string& unique_id, int nranks, int rank, int device,
+                                     int max_ctas = 0);
 // Communicators for several GPUs driven by one process (ncclCommInitAll):
 // result[i] is rank i on devices[i].
 std::vector<std::unique_ptr<Comm>> rccl_init_all(const std::vector<int>& devices);

@@ -83,14 +83,26 @@ std::string rccl_unique_id() {
   return std::string(id.internal, sizeof(id.internal));
 }
 
-std::unique_ptr<Comm> rccl_init_rank(const std::string& unique_id, int nranks, int rank, int device) {
+std::unique_ptr<Comm> rccl_init_rank(const std::string& unique_id, int nranks, int rank, int device, int max_ctas) {
   if (unique_id.size() != kUniqueIdBytes) throw std::invalid_argument("rccl_init_rank: unique id must be 128 bytes");
   if (rank < 0 || rank >= nranks) throw std::invalid_argument("rccl_init_rank: bad rank");
   ncclUniqueId id;
   std::memcpy(id.internal, unique_id.data(), kUniqueIdBytes);
   if (hipSetDevice(device) != hipSuccess) throw CommError("rccl_init_rank: hipSetDevice failed");
   ncclComm_t c = nullptr;
-  check(ncclCommInitRank(&c, nranks, id, rank), "ncclCommInitRank");
+  if (max_ctas > 0) {
+    // Cap the CTAs (= CUs held while an operation runs) of this
+    // communicator's kernels: the answer gather moves 8 B per image and needs
+    // one, and every CU it does not hold is one the forward keeps (its convs
+    // run one workgroup per CU: a CU held by a comm kernel delays a whole
+    // workgroup of them, profiles/r1_interference.txt).
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.minCTAs = 1;
+    cfg.maxCTAs = max_ctas;
+    check(ncclCommInitRankConfig(&c, nranks, id, rank, &cfg), "ncclCommInitRankConfig");
+  } else {
+    check(ncclCommInitRank(&c, nranks, id, rank), "ncclCommInitRank");
+  }
   return std::make_unique<RcclComm>(c, device);
 }
 

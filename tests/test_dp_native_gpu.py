@@ -1,9 +1,10 @@
 """Native data-parallel layer on a real GPU: the HIP worker (engine on a
 compute stream, answers over the comm streams, pinned D2H) must give the same
 answers as a direct engine forward, for full and ragged steps, pipelined and
-unpipelined. (RCCL send/recv between ranks needs >= 2 GPUs: the driver's
-multi-GPU bench runs that; the protocol itself is covered on CPU by
-tests/test_dp_native_cpu.py.)"""
+unpipelined. librccl itself runs here through one-rank loopback
+communicators (test_rccl_loopback); RCCL send/recv between ranks needs >= 2
+GPUs: the driver's multi-GPU bench runs that, and the protocol itself is
+covered on CPU by tests/test_dp_native_cpu.py."""
 import pytest
 import torch
 
@@ -82,3 +83,12 @@ def test_python_wrappers(gpu, eng):
     assert idx == ref_i.cpu().tolist()
     assert gi[:64].tolist() == ref_g.cpu().tolist() and st["images"] == 100
     assert torch.allclose(gp[:64], ref_p.cpu(), atol=1e-6)
+
+
+@pytest.mark.parametrize("max_ctas,nbytes", [(0, 1 << 20), (1, 1 << 20), (1, 2048), (4, 38535168)])
+def test_rccl_loopback(gpu, max_ctas, nbytes):
+    """librccl through the RcclComm wrapper on one GPU: a one-rank
+    communicator (plain, or CTA-capped as the answer communicator is) moves a
+    buffer to itself by grouped send/recv and by broadcast, bit-exact
+    (38.5 MB = one 256-image u8 shard)."""
+    assert dmlc.native().rccl_loopback(0, nbytes, max_ctas)
