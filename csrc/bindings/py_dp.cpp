@@ -96,6 +96,26 @@ class DpRunner {
     py::gil_scoped_release nogil;
     w_->sync_all();
   }
+  // Stage shards into every rank's HBM before a run (SDFS replicas placed
+  // where they are served): the coordinator's `images` images per rank at
+  // src (rank r's at image offset r * images) go to dst on rank r over the
+  // shard communicator (its own part by a device copy); blocks until done.
+  void stage(uintptr_t src, uintptr_t dst, int64_t images) {
+    const size_t bytes = (size_t)images * ib();
+    py::gil_scoped_release nogil;
+    w_->activate();
+    if (rank_ == 0) w_->copy((void*)dst, (const void*)src, bytes, dp::Worker::kIn);
+    if (world_ > 1) {
+      cin_->group_start();
+      if (rank_ == 0) {
+        for (int r = 1; r < world_; ++r) cin_->send((const void*)(src + r * bytes), bytes, r, w_->stream(dp::Worker::kIn));
+      } else {
+        cin_->recv((void*)dst, bytes, 0, w_->stream(dp::Worker::kIn));
+      }
+      cin_->group_end();
+    }
+    w_->sync_all();
+  }
 
   int world_, rank_, max_;
   bool scatter_;
@@ -282,9 +302,34 @@ bool rccl_loopback(int device, size_t bytes, int max_ctas) {
   return ok;
 }
 
+// A one-rank RCCL communicator that issues self send/recv groups on a given
+// stream without waiting: real RCCL kernels (their CTAs, LDS and register
+// footprint) next to the forward on one GPU, for tools/interference_probe.py
+// (what the coordinator's scatter does to its own compute at N > 1).
+class RcclLoop {
+ public:
+  RcclLoop(int device, int max_ctas) : c_(comm::rccl_init_rank(comm::rccl_unique_id(), 1, 0, device, max_ctas)) {}
+  // `legs` grouped send/recv pairs of `bytes` each, src -> dst + i * bytes
+  void issue(uintptr_t stream, uintptr_t src, uintptr_t dst, size_t bytes, int legs) {
+    c_->group_start();
+    for (int i = 0; i < legs; ++i) {
+      c_->send((const void*)(src + i * bytes), bytes, 0, (comm::Stream)stream);
+      c_->recv((void*)(dst + i * bytes), bytes, 0, (comm::Stream)stream);
+    }
+    c_->group_end();
+  }
+
+ private:
+  std::unique_ptr<comm::Comm> c_;
+};
+
 }  // namespace
 
 void bind_dp(py::module& m) {
+  py::class_<RcclLoop>(m, "RcclLoop")
+      .def(py::init<int, int>(), py::arg("device") = 0, py::arg("max_ctas") = 0)
+      .def("issue", &RcclLoop::issue, py::arg("stream"), py::arg("src"), py::arg("dst"), py::arg("bytes"),
+           py::arg("legs") = 7);
   m.def("rccl_loopback", &rccl_loopback, py::arg("device") = 0, py::arg("bytes") = 1 << 20, py::arg("max_ctas") = 0);
   m.def("rccl_unique_id", []() { return py::bytes(comm::rccl_unique_id()); });
   m.def("dp_shard_counts", &dp::shard_counts);
@@ -304,7 +349,8 @@ void bind_dp(py::module& m) {
            py::arg("pipelined") = true)
       .def("last_results", &DpRunner::last_results)
       .def("compute_stream", &DpRunner::compute_stream)
-      .def("sync", &DpRunner::sync);
+      .def("sync", &DpRunner::sync)
+      .def("stage", &DpRunner::stage, py::arg("src"), py::arg("dst"), py::arg("images"));
   py::class_<DpGroupPy>(m, "DpGroup")
       .def(py::init([](std::vector<Engine*> engines, int max_per_rank, int image_size, bool use_graph,
                        int timeout_ms) { return new DpGroupPy(engines, max_per_rank, image_size, use_graph, timeout_ms); }),

@@ -10,6 +10,10 @@ Modes, each timed over graph-replayed b256 forwards:
            like a long-lived RCCL p2p kernel with K blocks
   copy     a side-stream D2D copy of 7 x 38.5 MB per forward (HBM traffic of
            the coordinator's u8 shards at N=8)
+  rcclK    real RCCL kernels: a one-rank communicator (CTA cap K, 0 = RCCL's
+           default) moves 7 x 38.5 MB to itself by grouped send/recv on a
+           high-priority side stream per forward -- the coordinator's
+           scatter legs, with their CTA/LDS footprint, minus the xGMI hop
 """
 import argparse
 import os
@@ -28,6 +32,7 @@ def main():
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--modes", default="none,sleep1,sleep4,sleep16,sleep32,copy")
     args = ap.parse_args()
+    import dmlc
     from dmlc.runtime import InferenceEngine
     dev = torch.device("cuda", 0)
     eng = InferenceEngine("resnet18", None, device=0, max_batch=args.batch)
@@ -38,6 +43,8 @@ def main():
     side = [torch.cuda.Stream() for _ in range(32)]
     src = torch.empty(7 * B * 224 * 224 * 3, dtype=torch.uint8, device=dev)
     dst = torch.empty_like(src)
+    hi = torch.cuda.Stream(priority=-1)
+    loops = {}
 
     def fwd():
         eng.predict(img, out=out)
@@ -66,6 +73,22 @@ def main():
                     side[j].wait_event(ev)
                     with torch.cuda.stream(side[j]):
                         torch.cuda._sleep(int(cyc_per_ms * 1.3))
+            elif mode.startswith("rccl"):
+                k = int(mode[4:])
+                if k not in loops:
+                    loops[k] = dmlc.native().RcclLoop(0, k)
+                    ts = []
+                    for _ in range(6):  # the legs alone
+                        x0, x1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                        x0.record(hi)
+                        loops[k].issue(hi.cuda_stream, src.data_ptr(), dst.data_ptr(), B * 224 * 224 * 3, 7)
+                        x1.record(hi)
+                        torch.cuda.synchronize()
+                        ts.append(x0.elapsed_time(x1))
+                    print(f"{mode:8s} 7 x {B * 224 * 224 * 3 / 1e6:.1f} MB self send/recv alone: "
+                          f"{sorted(ts[1:])[2]:.3f} ms", flush=True)
+                hi.wait_event(ev)
+                loops[k].issue(hi.cuda_stream, src.data_ptr(), dst.data_ptr(), B * 224 * 224 * 3, 7)
             elif mode == "copy":
                 side[0].wait_event(ev)
                 with torch.cuda.stream(side[0]):
