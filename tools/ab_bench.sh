@@ -11,11 +11,11 @@ CMD=$1
 shift
 PKG=distributed-machine-learning-cluster_amd
 mkdir -p gpurun_out
-cp "$PKG/libdmlc_gpu.so" /tmp/libdmlc_gpu.tree.so
-restore() { cp /tmp/libdmlc_gpu.tree.so "$PKG/libdmlc_gpu.so"; }
+mkdir -p /tmp/ab_tree && cp "$PKG"/libdmlc_gpu.so "$PKG"/_C*.so /tmp/ab_tree/
+restore() { cp /tmp/ab_tree/*.so "$PKG/"; }
 trap restore EXIT
 for name in "$@"; do
-  cp "build/ab/$name/libdmlc_gpu.so" "$PKG/libdmlc_gpu.so"
+  cp "build/ab/$name/"*.so "$PKG/"
   echo "== $name"
   timeout -k 10 300 bash -c "$CMD" > "gpurun_out/ab_$name.log" 2>&1
   rc=$?
