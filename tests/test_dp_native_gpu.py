@@ -92,3 +92,24 @@ def test_rccl_loopback(gpu, max_ctas, nbytes):
     buffer to itself by grouped send/recv and by broadcast, bit-exact
     (38.5 MB = one 256-image u8 shard)."""
     assert dmlc.native().rccl_loopback(0, nbytes, max_ctas)
+
+
+def test_runner_stage_then_local_run(gpu, eng):
+    """bench.py's default input mode: DpRunner.stage copies the coordinator's
+    shard into the rank's own HBM pool (world 1: a device copy; at N > 1 the
+    other shards go over the shard communicator), then a local-mode run
+    classifies it like a direct forward."""
+    C = dmlc.native()
+    src = _pool(64, 5)
+    dst = torch.zeros_like(src)
+    torch.cuda.synchronize()
+    r = C.DpRunner(eng._e, 1, 0, b"", b"", 64, scatter=False, lanes=1)
+    r.stage(src.data_ptr(), dst.data_ptr(), 64)
+    assert torch.equal(dst, src)
+    out = r.run(dst.data_ptr(), 64, 0, 2)
+    r.sync()
+    assert out["images"] == 2 * 64
+    idx, prob = r.last_results()
+    ref_i, _ = eng.predict(src, use_graph=False)
+    torch.cuda.synchronize()
+    assert idx == ref_i.cpu().tolist()

@@ -309,3 +309,30 @@ def test_rows28_lds_layout():
         for wave in range(4):
             addr = [(16 * f + (l & 15)) * 256 + (((4 * wave + (l >> 4)) ^ (l & 15)) << 4) for l in range(64)]
             assert _b128_ways(addr) == 1
+
+
+def _permlane32_swap(a, b):
+    """gfx950 v_permlane32_swap_b32 as measured on the GPU
+    (tools/probes/permlane_probe.hip, profiles/r2_stem_permlane_ab.txt):
+    [0] = rows (a0, a1, b0, b1), [1] = rows (a2, a3, b2, b3), 16-lane rows."""
+    r = lambda v, i: v[16 * i:16 * i + 16]  # noqa: E731
+    return r(a, 0) + r(a, 1) + r(b, 0) + r(b, 1), r(a, 2) + r(a, 3) + r(b, 2) + r(b, 3)
+
+
+def _permlane16_swap(a, b):
+    """v_permlane16_swap_b32, measured: [0] = rows (a0, b0, a2, b2), [1] = rows (a1, b1, a3, b3)."""
+    r = lambda v, i: v[16 * i:16 * i + 16]  # noqa: E731
+    return r(a, 0) + r(b, 0) + r(a, 2) + r(b, 2), r(a, 1) + r(b, 1) + r(a, 3) + r(b, 3)
+
+
+def test_stem_row_rotation_from_permlane_swaps():
+    """stem_pool.hip rot_rows_down1: lane l must receive lane (l - 16) mod 64's
+    value (the pooling window's left neighbour column lives in the row group
+    below). Emulates the two swaps with their measured semantics and the
+    kernel's two lane selects."""
+    x = list(range(64))
+    p32 = _permlane32_swap(x, x)
+    z = [p32[1][l] if l < 32 else p32[0][l] for l in range(64)]
+    p16 = _permlane16_swap(z, x)
+    y = [p16[0][l] if (l & 16) else p16[1][l] for l in range(64)]
+    assert y == [(l - 16) % 64 for l in range(64)]
