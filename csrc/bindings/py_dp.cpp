@@ -27,7 +27,7 @@ namespace {
 class DpRunner {
  public:
   DpRunner(Engine* e, int world, int rank, const std::string& id_in, const std::string& id_out, int max_per_rank,
-           bool scatter, int image_size, bool use_graph, int timeout_ms, int lanes)
+           bool scatter, int image_size, bool use_graph, int timeout_ms, int lanes, int slots)
       : world_(world), rank_(rank), max_(max_per_rank), scatter_(scatter), S_(image_size), timeout_ms_(timeout_ms) {
     if (lanes < 1 || lanes > dp::Worker::kMaxLanes) throw std::invalid_argument("DpRunner: lanes must be 1..4");
     std::vector<Engine*> more;
@@ -39,7 +39,14 @@ class DpRunner {
     }
     w_ = dp::make_hip_worker(e, S_, S_, use_graph, more);
     // one slot per lane (>= 2): that many steps in flight
-    r_ = std::make_unique<dp::Rank>(w_.get(), max_, ib(), scatter_, std::max(2, lanes));
+    // Steps in flight (slots). Step i reuses slot i - slots, so its forward
+    // waits for that step's answers to have left; with slots = 2 that was the
+    // step just before on the same lane, and the answer copy's latency sat
+    // between a lane's consecutive forwards (bench: 268k vs 276k img/s with 4
+    // slots, the bare two-lane loop 276.7k: tools/pipeline_probe.py).
+    if (slots <= 0) slots = 2 * std::max(2, lanes);
+    if (slots < 2) throw std::invalid_argument("DpRunner: slots must be >= 2");
+    r_ = std::make_unique<dp::Rank>(w_.get(), max_, ib(), scatter_, slots);
     if (world_ > 1) {
       cin_ = comm::rccl_init_rank(id_in, world_, rank_, e->device());
       // answers: 8 B per image, one CTA (comm::rccl_init_rank's max_ctas)
@@ -338,13 +345,14 @@ void bind_dp(py::module& m) {
         py::arg("fail_after") = 0, py::arg("abrupt") = false, py::arg("pipelined") = true, py::arg("slots") = 2);
   py::class_<DpRunner>(m, "DpRunner")
       .def(py::init([](Engine* e, int world, int rank, py::bytes id_in, py::bytes id_out, int max_per_rank,
-                       bool scatter, int image_size, bool use_graph, int timeout_ms, int lanes) {
+                       bool scatter, int image_size, bool use_graph, int timeout_ms, int lanes, int slots) {
              return new DpRunner(e, world, rank, std::string(id_in), std::string(id_out), max_per_rank, scatter,
-                                 image_size, use_graph, timeout_ms, lanes);
+                                 image_size, use_graph, timeout_ms, lanes, slots);
            }),
            py::arg("engine"), py::arg("world"), py::arg("rank"), py::arg("id_in"), py::arg("id_out"),
            py::arg("max_per_rank"), py::arg("scatter") = true, py::arg("image_size") = 224,
-           py::arg("use_graph") = true, py::arg("timeout_ms") = -1, py::arg("lanes") = 1, py::keep_alive<1, 2>())
+           py::arg("use_graph") = true, py::arg("timeout_ms") = -1, py::arg("lanes") = 1, py::arg("slots") = 0,
+           py::keep_alive<1, 2>())
       .def("run", &DpRunner::run, py::arg("pool"), py::arg("pool_images"), py::arg("first"), py::arg("n"),
            py::arg("pipelined") = true)
       .def("last_results", &DpRunner::last_results)

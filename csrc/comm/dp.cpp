@@ -181,7 +181,9 @@ void Rank::compute(const StepPlan& p) {
   if (n > max_) throw std::invalid_argument("dp::Rank::compute: shard larger than max_per_rank");
   const bool received = scatter_ && !root() && world() > 1;
   const uint8_t* img = received ? (const uint8_t*)inbuf_[s] : p.src;
-  const int lane = s % w_->lanes();  // slots alternate over the worker's compute lanes
+  // consecutive steps alternate over the worker's compute lanes (whatever the
+  // slot count)
+  const int lane = (int)(p.step % w_->lanes());
   const int cs = Worker::compute_stream(lane);
   if (received) w_->wait(cs, ev_in_[s]);
   else if (root() && p.src_event >= 0) w_->wait(cs, p.src_event);

@@ -89,8 +89,14 @@ class HipWorker : public Worker {
     if (lane < 0 || lane >= lanes()) throw std::invalid_argument("HipWorker: no such compute lane");
     e_[lane]->forward(images, B, H_, W_, idx, prob, nullptr, s_[compute_stream(lane)], graph_);
   }
+  // dst is pinned host memory (alloc_host). A plain DeviceToHost copy runs as
+  // a blit kernel (__amd_rocclr_copyBuffer, ~4 us): on the high-priority
+  // answer stream it takes a CU slot while the forward's one-workgroup-per-CU
+  // convs launch, and a displaced workgroup costs that conv a second round.
+  // The NoCU kind goes through a copy engine (tools/probes/nocu_copy_probe.hip:
+  // exact, no kernel in the trace).
   void copy_d2h(void* dst, const void* src, size_t bytes, int sid) override {
-    DMLC_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s_[sid]));
+    DMLC_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDeviceNoCU, s_[sid]));
   }
   void copy(void* dst, const void* src, size_t bytes, int sid) override {
     DMLC_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, s_[sid]));
