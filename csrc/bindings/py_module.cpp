@@ -69,12 +69,6 @@ PYBIND11_MODULE(_C, m) {
   // ---------------------------------------------------------------- ops
   m.def("conv_kpad", &conv_kpad, py::arg("Cin"), py::arg("KH"), py::arg("KW"), py::arg("stem") = false);
   m.def("stem_row_width", &stem_row_width);
-  m.def("cu_masked_stream", [](int device, std::vector<uint32_t> mask) {  // EXPERIMENT
-    hipStream_t st;
-    DMLC_HIP_CHECK(hipSetDevice(device));
-    DMLC_HIP_CHECK(hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()));
-    return (uintptr_t)st;
-  });
   m.def("conv_npad", &conv_npad);
   m.def("conv_out_dim", &conv_out_dim);
   m.def(

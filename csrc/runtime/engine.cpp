@@ -101,7 +101,6 @@ Engine::Engine(const std::string& arch, const WeightMap& weights, int device, in
   hipDeviceProp_t prop;
   DMLC_HIP_CHECK(hipGetDeviceProperties(&prop, device_));
   num_cus_ = prop.multiProcessorCount;
-  if (const char* e = std::getenv("DMLC_EXP_NUM_CUS")) num_cus_ = std::atoi(e);  // EXPERIMENT
 
   if (arch == "resnet18")
     build_resnet({2, 2, 2, 2}, false);
@@ -134,7 +133,6 @@ Engine::Engine(const Engine& src, int device)
   hipDeviceProp_t prop;
   DMLC_HIP_CHECK(hipGetDeviceProperties(&prop, device_));
   num_cus_ = prop.multiProcessorCount;
-  if (const char* e = std::getenv("DMLC_EXP_NUM_CUS")) num_cus_ = std::atoi(e);  // EXPERIMENT
   stem_pad_ = src.stem_pad_;
   opt_ = src.opt_;
   fp8_ = src.fp8_;
