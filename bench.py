@@ -268,8 +268,8 @@ def main():
                             "(CS425MP4Report.pdf p.2; no images/s is published)",
             },
             "per_rank_images_s": [round(B * args.steps / s, 1) for s in per_rank_s],
-            "batch_latency_p50_ms": round(pct(batch_lat, 50), 3),
-            "batch_latency_p95_ms": round(pct(batch_lat, 95), 3),
+            "batch_latency_p50_ms": round(pct(batch_lat, 50), 3) if batch_lat else None,
+            "batch_latency_p95_ms": round(pct(batch_lat, 95), 3) if batch_lat else None,
             "query_latency_mean_ms": round(e2e["mean_ms"], 3) if e2e else None,
             "query_latency_p50_ms": round(e2e["p50_ms"], 3) if e2e else None,
             "query_latency_p95_ms": round(e2e["p95_ms"], 3) if e2e else None,

@@ -200,6 +200,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("stream"), py::arg("stamps") = 0, py::arg("wd") = 0, py::arg("bd") = 0, py::arg("yd") = 0,
         py::arg("wfrag") = 0, py::arg("wdfrag") = 0);
   m.def("conv3x3_stream_uses_frag", &conv3x3_stream_uses_frag);
+  m.def("conv3x3_stream_set_variant", &conv3x3_stream_set_variant);
   m.def("conv3x3_rows_supported", &conv3x3_rows_supported);
   m.def("conv3x3_rows_pick_strip", &conv3x3_rows_pick_strip);
   m.def("conv3x3_rows", [](uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t res, uintptr_t y, uintptr_t zero,

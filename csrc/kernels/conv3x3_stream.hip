@@ -120,15 +120,19 @@ struct StreamGeom {
 };
 
 template <int H, int W, int CI, int CO, int HS, int IMG, int NSP, int WM, int S, int ND, bool DS, bool WR,
-          int PD = 4>
+          int PD = 4, int NG = 1>
 __global__ __launch_bounds__(512, 1) void conv3x3_stream_kernel(StreamConvArgs a) {
   using G = StreamGeom<H, W, CI, HS, IMG, S, ND>;
   constexpr int BK = 32;                     // K-tile depth = one MFMA k-step
   constexpr int NPIX = IMG * HS * W;         // output pixels per workgroup (the last group may have fewer)
   constexpr int MFT = (NPIX + 15) / 16;      // pixel fragments (the last one partly padding)
   constexpr int MF = (MFT + WM - 1) / WM;    // per wave
-  constexpr int WN = 32;                     // channels per wave
-  constexpr int NF = 2;                      // N fragments per wave
+  // NG = 2 (register weights only): a wave owns two 32-channel groups, so each
+  // X fragment read from LDS feeds 4 MFMAs instead of 2 (the LDS read skeleton
+  // alone was ~24 of the 14x14x256 conv's 43 us loop, profiles/r1_stream_conv.log)
+  static_assert(NG == 1 || (NG == 2 && WR), "two channel groups per wave need the register weights");
+  constexpr int WN = 32 * NG;                // channels per wave
+  constexpr int NF = 2 * NG;                 // N fragments per wave
   constexpr int HI = G::HI, WI = G::WI;
   constexpr int PXB = G::PXB, ROWB = G::ROWB, ZB = G::ZB, WST = G::WST;
   constexpr int CPX = CI / 8;                // 16-B chunks per input pixel
@@ -244,13 +248,17 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream_kernel(StreamConvArgs a
   // fragment nf of K-tile t (the downsample's tiles follow the 3x3's): buffer
   // loads, lane offset in a VGPR and the fragment offset a scalar
   // (non-WR kernels get descriptors of null pointers they never use)
-  const __amdgpu_buffer_rsrc_t wrs = wave_rsrc(a.wf + (long)(ch0 / 32) * KT * NF * 512, WR ? KT * NF * 1024 : 0);
+  // (a wave's NG groups are consecutive in the fragment-order array: group j
+  // of the wave starts j * KT * 2 fragments after the first)
+  const __amdgpu_buffer_rsrc_t wrs = wave_rsrc(a.wf + (long)(ch0 / 32) * KT * 2 * 512, WR ? NG * KT * 2 * 1024 : 0);
   const __amdgpu_buffer_rsrc_t wdrs =
-      wave_rsrc(a.wdf + (long)(ch0 / 32) * CT * NF * 512, (WR && DS) ? CT * NF * 1024 : 0);
+      wave_rsrc(a.wdf + (long)(ch0 / 32) * CT * 2 * 512, (WR && DS) ? NG * CT * 2 * 1024 : 0);
   auto wfrag = [&](int t, int nf) __attribute__((always_inline)) {
     const bool d = DS && t >= KT;
+    const int kt = d ? CT : KT, tt = d ? t - KT : t;
     return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
-                                          d ? wdrs : wrs, lane * 16, ((d ? t - KT : t) * NF + nf) * 1024, 0));
+                                          d ? wdrs : wrs, lane * 16, ((nf >> 1) * kt * 2 + tt * 2 + (nf & 1)) * 1024,
+                                          0));
   };
   if constexpr (WR) {
 #pragma unroll
@@ -432,99 +440,117 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream_kernel(StreamConvArgs a
   // residual loads are issued first (the operand registers are free now):
   // loaded one per fragment, each waited on before its store, they cost
   // 4-5 us per workgroup.
+  // (NG = 2: the same for channel group j at +32 j, fragments 2j, 2j+1)
   const long base = ((long)b * H + r0) * W * CO + ch0 + 8 * fq;
-  float bs[8];
+  float bs[NG][8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) bs[e] = a.bias[ch0 + 8 * fq + e];
-  uint4 rv[MF];
+  for (int j = 0; j < NG; ++j)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bs[j][e] = a.bias[ch0 + 32 * j + 8 * fq + e];
+  uint4 rv[MF][NG];
   if (a.res) {
 #pragma unroll
     for (int f = 0; f < MF; ++f) {
       const int p = min(16 * (wm * MF + f) + fr, npix - 1);
-      rv[f] = *(const uint4*)(a.res + base + (long)p * CO);
+#pragma unroll
+      for (int j = 0; j < NG; ++j) rv[f][j] = *(const uint4*)(a.res + base + 32 * j + (long)p * CO);
     }
   }
   // fused avgpool: per-lane sums per image of the workgroup (PARTS == 1)
+  // (whole images with one pixel group per wave: a wave's lanes see every
+  // pixel of its images; the host allows the pool only on such variants)
+  constexpr bool POOLABLE = G::PARTS == 1 && WM == 1;
   constexpr int PIMG = G::PARTS == 1 ? IMG : 1;
-  float psum[PIMG][8];
+  float psum[NG][PIMG][8];
 #pragma unroll
-  for (int i = 0; i < PIMG; ++i)
+  for (int j = 0; j < NG; ++j)
 #pragma unroll
-    for (int e = 0; e < 8; ++e) psum[i][e] = 0.f;
+    for (int i = 0; i < PIMG; ++i)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) psum[j][i][e] = 0.f;
 #pragma unroll
   for (int f = 0; f < MF; ++f) {
     const int p = 16 * (wm * MF + f) + fr;
     if (p >= npix) continue;
-    const long off = base + (long)p * CO;
-    float v[8];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      v[e] = acc[f][0][e] + bs[e];
-      v[4 + e] = acc[f][1][e] + bs[4 + e];
-    }
-    if (a.res) {
-      float r[8];
-      unpack8(rv[f], r);
+    for (int j = 0; j < NG; ++j) {
+      const long off = base + 32 * j + (long)p * CO;
+      float v[8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] += r[e];
-    }
-    if (relu) {
+      for (int e = 0; e < 4; ++e) {
+        v[e] = acc[f][2 * j][e] + bs[j][e];
+        v[4 + e] = acc[f][2 * j + 1][e] + bs[j][4 + e];
+      }
+      if (a.res) {
+        float r[8];
+        unpack8(rv[f][j], r);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
-    }
-    const uint4 packed = pack8(v);
-    if (a.store_y) *(uint4*)(a.y + off) = packed;
-    if constexpr (G::PARTS == 1) {
-      if (a.pool) {  // the bf16 activation's values, as the unfused avgpool reads them
-        float q[8];
-        unpack8(packed, q);
-        const int im = PIMG == 1 ? 0 : p / (H * W);
+        for (int e = 0; e < 8; ++e) v[e] += r[e];
+      }
+      if (relu) {
 #pragma unroll
-        for (int i = 0; i < PIMG; ++i)
-          if (i == im)
+        for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+      }
+      const uint4 packed = pack8(v);
+      if (a.store_y) *(uint4*)(a.y + off) = packed;
+      if constexpr (POOLABLE) {
+        if (a.pool) {  // the bf16 activation's values, as the unfused avgpool reads them
+          float q[8];
+          unpack8(packed, q);
+          const int im = PIMG == 1 ? 0 : p / (H * W);
 #pragma unroll
-            for (int e = 0; e < 8; ++e) psum[i][e] += q[e];
+          for (int i = 0; i < PIMG; ++i)
+            if (i == im)
+#pragma unroll
+              for (int e = 0; e < 8; ++e) psum[j][i][e] += q[e];
+        }
       }
     }
   }
-  if constexpr (G::PARTS == 1) {
+  if constexpr (POOLABLE) {
     if (a.pool) {  // reduce over the 16 pixel lanes fr of each channel group fq
 #pragma unroll
-      for (int i = 0; i < PIMG; ++i)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          float t = psum[i][e];
-          t += __shfl_xor(t, 8, 64);
-          t += __shfl_xor(t, 4, 64);
-          t += __shfl_xor(t, 2, 64);
-          t += __shfl_xor(t, 1, 64);
-          psum[i][e] = t * (1.f / (H * W));
-        }
-      if (fr == 0 && (WM == 1 || wm == 0)) {
-        static_assert(G::PARTS != 1 || WM == 1, "fused pool: one pixel group per wave");
+      for (int j = 0; j < NG; ++j)
 #pragma unroll
         for (int i = 0; i < PIMG; ++i)
-          if (i < nimg) {
-            *(uint4*)(a.pool + (long)(b + i) * CO + ch0 + 8 * fq) = pack8(psum[i]);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            float t = psum[j][i][e];
+            t += __shfl_xor(t, 8, 64);
+            t += __shfl_xor(t, 4, 64);
+            t += __shfl_xor(t, 2, 64);
+            t += __shfl_xor(t, 1, 64);
+            psum[j][i][e] = t * (1.f / (H * W));
           }
+      if (fr == 0 && (WM == 1 || wm == 0)) {
+#pragma unroll
+        for (int j = 0; j < NG; ++j)
+#pragma unroll
+          for (int i = 0; i < PIMG; ++i)
+            if (i < nimg) {
+              *(uint4*)(a.pool + (long)(b + i) * CO + ch0 + 32 * j + 8 * fq) = pack8(psum[j][i]);
+            }
       }
     }
   }
   if constexpr (DS) {
-    float bd[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) bd[e] = a.bd[ch0 + 8 * fq + e];
+    for (int j = 0; j < NG; ++j) {
+      float bd[8];
 #pragma unroll
-    for (int f = 0; f < MF; ++f) {
-      const int p = 16 * (wm * MF + f) + fr;
-      if (p >= npix) continue;
-      float v[8];
+      for (int e = 0; e < 8; ++e) bd[e] = a.bd[ch0 + 32 * j + 8 * fq + e];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        v[e] = accd[f][0][e] + bd[e];
-        v[4 + e] = accd[f][1][e] + bd[4 + e];
+      for (int f = 0; f < MF; ++f) {
+        const int p = 16 * (wm * MF + f) + fr;
+        if (p >= npix) continue;
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = accd[f][2 * j][e] + bd[e];
+          v[4 + e] = accd[f][2 * j + 1][e] + bd[4 + e];
+        }
+        *(uint4*)(a.yd + base + 32 * j + (long)p * CO) = pack8(v);
       }
-      *(uint4*)(a.yd + base + (long)p * CO) = pack8(v);
     }
   }
   if (a.stamps && tid == 0) {
@@ -537,7 +563,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream_kernel(StreamConvArgs a
   }
 }
 
-template <int H, int W, int CI, int CO, int HS, int IMG, int NSP, int WM, int S, bool WR = false, int PD = 4>
+template <int H, int W, int CI, int CO, int HS, int IMG, int NSP, int WM, int S, bool WR = false, int PD = 4,
+          int NG = 1>
 void launch_stream(const StreamConvArgs& a, hipStream_t s) {
   using G = StreamGeom<H, W, CI, HS, IMG, S, 3>;
   constexpr size_t lds = WR ? (size_t)G::XBYTES : G::LDS;
@@ -546,27 +573,34 @@ void launch_stream(const StreamConvArgs& a, hipStream_t s) {
   if constexpr (WR) {
     if constexpr (S == 2) {
       if (a.yd) {
-        hipLaunchKernelGGL((conv3x3_stream_kernel<H, W, CI, CO, HS, IMG, NSP, WM, S, 3, true, true, PD>), dim3(grid),
+        hipLaunchKernelGGL((conv3x3_stream_kernel<H, W, CI, CO, HS, IMG, NSP, WM, S, 3, true, true, PD, NG>),
+                           dim3(grid), dim3(512), lds, s, a);
+        return;
+      }
+    }
+      hipLaunchKernelGGL((conv3x3_stream_kernel<H, W, CI, CO, HS, IMG, NSP, WM, S, 3, false, true, PD, NG>),
+                         dim3(grid), dim3(512), lds, s, a);
+    return;
+  } else {
+    if constexpr (S == 2) {
+      if (a.yd) {
+        hipLaunchKernelGGL((conv3x3_stream_kernel<H, W, CI, CO, HS, IMG, NSP, WM, S, 3, true, false>), dim3(grid),
                            dim3(512), lds, s, a);
         return;
       }
     }
-      hipLaunchKernelGGL((conv3x3_stream_kernel<H, W, CI, CO, HS, IMG, NSP, WM, S, 3, false, true, PD>), dim3(grid),
-                         dim3(512), lds, s, a);
-    return;
+    hipLaunchKernelGGL((conv3x3_stream_kernel<H, W, CI, CO, HS, IMG, NSP, WM, S, 3, false, false>), dim3(grid),
+                       dim3(512), lds, s, a);
   }
-  if constexpr (S == 2) {
-    if (a.yd) {
-      hipLaunchKernelGGL((conv3x3_stream_kernel<H, W, CI, CO, HS, IMG, NSP, WM, S, 3, true, false>), dim3(grid),
-                         dim3(512), lds, s, a);
-      return;
-    }
-  }
-  hipLaunchKernelGGL((conv3x3_stream_kernel<H, W, CI, CO, HS, IMG, NSP, WM, S, 3, false, false>), dim3(grid), dim3(512),
-                     lds, s, a);
 }
 
+// Tuning hook for tools/conv_bench.py A/B runs (0 = the default kernels):
+// 1 = the 14x14x256 register-weight kernel with a 2-deep weight ring (PD 2).
+int g_stream_variant = 0;
+
 }  // namespace
+
+void conv3x3_stream_set_variant(int v) { g_stream_variant = v; }
 
 // Whole-image workgroups (the fused avgpool): layer4's 7x7x512 stride-1 conv.
 bool conv3x3_stream_pool_supported(int Hin, int Win, int Cin, int Cout, int stride) {
@@ -595,7 +629,9 @@ bool conv3x3_stream_uses_frag(int Hin, int Win, int Cin, int Cout, int stride) {
   // (28x28x128 in quarter images and 14x14x256 in 2 channel splits, both 7
   // fragments per wave so the register ring fits, measured 70.2 / 60.2 vs
   // 67.9 / 56.4 us with the LDS ring: kept out)
-  return stride == 1 && Cin == Cout && Hin == 7 && Win == 7 && Cin == 512;
+  // 14x14x256 with two channel groups per wave (NG = 2: WM = 2 pixel halves x
+  // 4 x 64 channels, 7 fragments per wave, X reads per MFMA halved)
+  return stride == 1 && Cin == Cout && ((Hin == 7 && Win == 7 && Cin == 512) || (Hin == 14 && Win == 14 && Cin == 256));
 }
 
 void conv3x3_stream(const void* x, const void* w, const float* bias, const void* res, void* y, const void* zero,
@@ -638,10 +674,19 @@ void conv3x3_stream(const void* x, const void* w, const float* bias, const void*
     launch_stream<56, 56, 64, 64, 8, 1, 1, 4, 1>(a, s);
   else if (stride == 1 && Cin == 128)  // layer2: half an image (15 x 28 x 256 B = 105 KB)
     launch_stream<28, 28, 128, 128, 14, 1, 1, 2, 1>(a, s);
+  else if (stride == 1 && Cin == 256 && wfrag) {  // layer3, register weights, 2 pixel halves x 4 groups of 64 channels
+    if (g_stream_variant == 1)
+      launch_stream<14, 14, 256, 256, 14, 1, 1, 2, 1, true, 2, 2>(a, s);
+    else
+      launch_stream<14, 14, 256, 256, 14, 1, 1, 2, 1, true, 4, 2>(a, s);
+  }
   else if (stride == 1 && Cin == 256)  // layer3: a whole image (14 x 14 x 512 B = 98 KB)
     launch_stream<14, 14, 256, 256, 14, 1, 1, 1, 1>(a, s);
-  else if (stride == 1 && wfrag)  // layer4, weights in fragment order straight into VGPRs
+  else if (stride == 1 && wfrag) {  // layer4, weights in fragment order straight into VGPRs
+    // (two 64-channel groups per wave measured slower here: 2 images x 2
+    // pixel halves 58.7 us, 1 image x 8 groups 60.9 us vs 53.0 us)
     launch_stream<7, 7, 512, 512, 7, 2, 2, 1, 1, true>(a, s);
+  }
   else if (stride == 1)  // layer4: two whole images x half the output channels (2 x 49 x 1 KB = 98 KB)
     launch_stream<7, 7, 512, 512, 7, 2, 2, 1, 1>(a, s);
   else if (Cin == 64)  // layer2.0.conv1: a quarter image (15 x 56 x 128 B = 105 KB)

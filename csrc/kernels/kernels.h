@@ -185,6 +185,8 @@ bool conv3x3_stream_pool_supported(int Hin, int Win, int Cin, int Cout, int stri
 // wfrag: the same weights in fragment order (stream_weight_frag_layout), used
 // by the variants that load weights straight into VGPRs (7x7x512 stride 1)
 bool conv3x3_stream_uses_frag(int Hin, int Win, int Cin, int Cout, int stride);
+// A/B tuning hook (tools/conv_bench.py): picks alternative register-weight kernels
+void conv3x3_stream_set_variant(int v);
 // [Cout, K] row-major bf16 -> fragment order [Cout/32][K/32][2][64][8]:
 // dst index of (n, k) for n < Cout, k < K (Cout % 32 == 0, K % 32 == 0)
 inline size_t stream_frag_index(int n, int k, int K) {

@@ -259,7 +259,8 @@ def stream_weight_frag(w_packed: torch.Tensor, cout: int | None = None) -> torch
 
 
 def conv3x3_stream(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, res: torch.Tensor | None = None,
-                   relu: bool = True, stride: int = 1, downsample: tuple | None = None, frag: bool = False):
+                   relu: bool = True, stride: int = 1, downsample: tuple | None = None,
+                   frag: bool | torch.Tensor = False):
     """Direct 3x3/p1 conv (conv3x3_stream.hip) on NHWC bf16 with the conv2d
     packed weights; + bias (+ residual), ReLU. Stride 1: [B,28,28,128],
     [B,14,14,256], [B,7,7,512]; stride 2: [B,56,56,64] -> 128 channels,
@@ -288,11 +289,11 @@ def conv3x3_stream(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, 
             raise ValueError("conv3x3_stream: downsample needs stride 2 and weights [Cout, Cin]")
         yd = torch.empty_like(y)
     wf = None
-    if frag:
+    if frag is not False and frag is not None:  # True, or the fragment-order weights (graph capture)
         if not C.conv3x3_stream_uses_frag(H, W, Cin, Cout, stride):
             raise ValueError("conv3x3_stream: no register-weight variant for this shape")
-        wf = stream_weight_frag(w_packed)
-    wdf = stream_weight_frag(wd) if (frag and wd is not None) else None
+        wf = frag if isinstance(frag, torch.Tensor) else stream_weight_frag(w_packed)
+    wdf = stream_weight_frag(wd) if (wf is not None and wd is not None) else None
     C.conv3x3_stream(_ptr(x.contiguous()), _ptr(w_packed.contiguous()), _ptr(bias.float().contiguous()),
                      _ptr(None if res is None else res.contiguous()), _ptr(y), _ptr(_zero_page(x.device)), B, H, W,
                      Cin, Cout, stride, relu, _stream(), stamps, _ptr(wd), _ptr(bd), _ptr(yd), _ptr(wf), _ptr(wdf))

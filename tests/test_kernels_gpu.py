@@ -306,11 +306,22 @@ def test_conv3x3_stream_stride2(gpu, HW, Cin, B, relu):
     assert _rel(_nchw(y.float().cpu()), ref) < 8e-3
 
 
-@pytest.mark.parametrize("HW,C,B,res", [(7, 512, 1, False), (7, 512, 3, True), (7, 512, 4, True)])
-def test_conv3x3_stream_register_weights(gpu, HW, C, B, res):
+@pytest.mark.parametrize("HW,C,B,res,variant", [(7, 512, 1, False, 0), (7, 512, 3, True, 0), (7, 512, 4, True, 0),
+                                                (14, 256, 1, False, 0), (14, 256, 3, True, 0), (14, 256, 2, True, 1)])
+def test_conv3x3_stream_register_weights(gpu, HW, C, B, res, variant):
     """Stride-1 stream convs with the weights in fragment order loaded
-    straight into VGPRs (WR variants) vs torch fp32, and bit-identical to the
-    LDS-ring variants (same MFMA order)."""
+    straight into VGPRs (WR variants; 14x14x256 with two 32-channel groups
+    per wave, ring depth 4 or 2 by variant) vs torch fp32, and bit-identical to the
+    LDS-ring variants (same MFMA order per output)."""
+    nat = dmlc.native()
+    nat.conv3x3_stream_set_variant(variant)
+    try:
+        _stream_register_weights(gpu, HW, C, B, res)
+    finally:
+        nat.conv3x3_stream_set_variant(0)
+
+
+def _stream_register_weights(gpu, HW, C, B, res):
     g = torch.Generator().manual_seed(24)
     x = torch.randn(B, C, HW, HW, generator=g).bfloat16().float()
     w = (torch.randn(C, C, 3, 3, generator=g) / (9 * C) ** 0.5).bfloat16().float()

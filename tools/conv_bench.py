@@ -84,6 +84,7 @@ def main():
     ap.add_argument("--only", default="")
     ap.add_argument("--persist", type=int, default=0, help="persistent grid size (0 = one block per tile)")
     ap.add_argument("--split", type=int, default=1, help="split-K factor (big-tile configs 11/12: K slices, 1 = auto)")
+    ap.add_argument("--variants", default="0", help="register-weight stream conv variants to time (A/B hook)")
     ap.add_argument("--ref", action="store_true", help="also time hipBLASLt GEMM and MIOpen conv on each shape")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -127,6 +128,20 @@ def main():
                 if ops.BT_STAMPS is not None:
                     f()
                     row.append(_stamps())
+                # register-weight kernels (fragment-order weights), per A/B variant
+                nat = ops.C if hasattr(ops, "C") else __import__("dmlc").native()
+                if nat.conv3x3_stream_uses_frag(H, W, Cin, Cout, s) and s == 1:
+                    for v in [int(t) for t in a.variants.split(",")]:
+                        nat.conv3x3_stream_set_variant(v)
+                        try:
+                            wf = ops.stream_weight_frag(wp, Cout)
+                            f = lambda: ops.conv3x3_stream(x, wp, bias, r, True, stride=s, frag=wf)
+                            us = time_us(f, a.iters)
+                            row.append(f"wr{v}{'+res' if use_res else ''}={us:7.1f}us {flops/us/1e6:6.0f}TF")
+                        except Exception as e:  # noqa: BLE001
+                            row.append(f"wr{v}=ERR({e})")
+                        finally:
+                            nat.conv3x3_stream_set_variant(0)
         if name == "l1":  # direct row-streaming conv (conv3x3_rows.hip)
             for use_res in (False, True):
                 r = torch.randn(B, H, W, Cout, device=dev).bfloat16() if use_res else None
