@@ -296,33 +296,101 @@ inline void idct8x8(const float* in, uint8_t* out, int stride) {
 
 uint16_t be16(const uint8_t* p) { return (uint16_t)((p[0] << 8) | p[1]); }
 
-// YCbCr -> RGB in 16.16 fixed point (JFIF full-range coefficients).
-struct ColorTables {
-  int cr_r[256], cb_b[256], cr_g[256], cb_g[256];
-  ColorTables() {
-    for (int i = 0; i < 256; ++i) {
-      const double x = i - 128;
-      cr_r[i] = (int)std::lround(1.402 * x * 65536);
-      cb_b[i] = (int)std::lround(1.772 * x * 65536);
-      cr_g[i] = (int)std::lround(-0.714136 * x * 65536);
-      cb_g[i] = (int)std::lround(-0.344136 * x * 65536);
-    }
-  }
-};
-const ColorTables kColor;
+// YCbCr -> RGB in 16.16 fixed point (JFIF full-range coefficients, each
+// rounded once to a 16.16 constant as libjpeg's FIX() does), e.g.
+// R = (Y * 2^16 + kCrR * (Cr - 128) + 2^15) >> 16, clamped to [0, 255]. The
+// scalar and AVX2 paths compute exactly this, so they are bit-identical.
+constexpr int kCrR = 91881;    // 1.402    * 65536
+constexpr int kCbB = 116130;   // 1.772    * 65536
+constexpr int kCrG = -46802;   // -0.714136 * 65536
+constexpr int kCbG = -22554;   // -0.344136 * 65536
 
 inline uint8_t clamp_fix(int v) {  // 16.16 -> u8, rounded
   v = (v + 32768) >> 16;
   return (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v);
 }
 
+inline void ycc_pixel(int y, int cb, int cr, uint8_t* o) {
+  const int Y = y << 16, b = cb - 128, r = cr - 128;
+  o[0] = clamp_fix(Y + kCrR * r);
+  o[1] = clamp_fix(Y + kCbG * b + kCrG * r);
+  o[2] = clamp_fix(Y + kCbB * b);
+}
+
+void ycc_row_scalar(const uint8_t* y, const uint8_t* cb, const uint8_t* cr, uint8_t* o, int x0, int W) {
+  for (int x = x0; x < W; ++x) ycc_pixel(y[x], cb[x], cr[x], o + 3 * x);
+}
+
+// 2 x 8 int32 -> 16 u8 in pixel order, saturating (packs work per 128-bit lane)
+__attribute__((target("avx2"))) inline __m128i pack16_avx2(__m256i a, __m256i b) {
+  const __m256i w = _mm256_permute4x64_epi64(_mm256_packs_epi32(a, b), 0xD8);  // 16 x i16, in order
+  return _mm_packus_epi16(_mm256_castsi256_si128(w), _mm256_extracti128_si256(w, 1));
+}
+
+// R, G, B of 16 pixels (bytes of y/cb/cr at p), 32-bit fixed-point lanes
+__attribute__((target("avx2"))) inline void ycc16_avx2(const uint8_t* y, const uint8_t* cb, const uint8_t* cr,
+                                                       __m128i* R, __m128i* G, __m128i* B) {
+  const __m256i c128 = _mm256_set1_epi32(128), half = _mm256_set1_epi32(32768);
+  __m256i rr[2], gg[2], bb[2];
+  for (int h = 0; h < 2; ++h) {
+    const __m256i Y =
+        _mm256_add_epi32(_mm256_slli_epi32(_mm256_cvtepu8_epi32(_mm_loadl_epi64((const __m128i*)(y + 8 * h))), 16),
+                         half);
+    const __m256i b = _mm256_sub_epi32(_mm256_cvtepu8_epi32(_mm_loadl_epi64((const __m128i*)(cb + 8 * h))), c128);
+    const __m256i r = _mm256_sub_epi32(_mm256_cvtepu8_epi32(_mm_loadl_epi64((const __m128i*)(cr + 8 * h))), c128);
+    rr[h] = _mm256_srai_epi32(_mm256_add_epi32(Y, _mm256_mullo_epi32(r, _mm256_set1_epi32(kCrR))), 16);
+    gg[h] = _mm256_srai_epi32(_mm256_add_epi32(Y, _mm256_add_epi32(_mm256_mullo_epi32(b, _mm256_set1_epi32(kCbG)),
+                                                                   _mm256_mullo_epi32(r, _mm256_set1_epi32(kCrG)))),
+                              16);
+    bb[h] = _mm256_srai_epi32(_mm256_add_epi32(Y, _mm256_mullo_epi32(b, _mm256_set1_epi32(kCbB))), 16);
+  }
+  *R = pack16_avx2(rr[0], rr[1]);
+  *G = pack16_avx2(gg[0], gg[1]);
+  *B = pack16_avx2(bb[0], bb[1]);
+}
+
+// 16 pixels per iteration, the three planar byte vectors interleaved into 48
+// RGB bytes with pshufb. Returns the first pixel it did not convert.
+__attribute__((target("avx2"))) int ycc_row_avx2(const uint8_t* y, const uint8_t* cb, const uint8_t* cr, uint8_t* o,
+                                                 int W) {
+  // output byte j of each 16-byte third takes channel j % 3 of pixel j / 3
+  alignas(16) static const int8_t m[3][3][16] = {
+      {{0, -1, -1, 1, -1, -1, 2, -1, -1, 3, -1, -1, 4, -1, -1, 5},
+       {-1, 0, -1, -1, 1, -1, -1, 2, -1, -1, 3, -1, -1, 4, -1, -1},
+       {-1, -1, 0, -1, -1, 1, -1, -1, 2, -1, -1, 3, -1, -1, 4, -1}},
+      {{-1, -1, 6, -1, -1, 7, -1, -1, 8, -1, -1, 9, -1, -1, 10, -1},
+       {5, -1, -1, 6, -1, -1, 7, -1, -1, 8, -1, -1, 9, -1, -1, 10},
+       {-1, 5, -1, -1, 6, -1, -1, 7, -1, -1, 8, -1, -1, 9, -1, -1}},
+      {{-1, 11, -1, -1, 12, -1, -1, 13, -1, -1, 14, -1, -1, 15, -1, -1},
+       {-1, -1, 11, -1, -1, 12, -1, -1, 13, -1, -1, 14, -1, -1, 15, -1},
+       {10, -1, -1, 11, -1, -1, 12, -1, -1, 13, -1, -1, 14, -1, -1, 15}}};
+  int x = 0;
+  for (; x + 16 <= W; x += 16) {
+    __m128i R, G, B;
+    ycc16_avx2(y + x, cb + x, cr + x, &R, &G, &B);
+    for (int k = 0; k < 3; ++k) {
+      const __m128i v = _mm_or_si128(_mm_or_si128(_mm_shuffle_epi8(R, _mm_load_si128((const __m128i*)m[k][0])),
+                                                  _mm_shuffle_epi8(G, _mm_load_si128((const __m128i*)m[k][1]))),
+                                     _mm_shuffle_epi8(B, _mm_load_si128((const __m128i*)m[k][2])));
+      _mm_storeu_si128((__m128i*)(o + 3 * x + 16 * k), v);
+    }
+  }
+  return x;
+}
+
+void ycc_row(const uint8_t* y, const uint8_t* cb, const uint8_t* cr, uint8_t* o, int W) {
+  const int x0 = kHasAvx2 ? ycc_row_avx2(y, cb, cr, o, W) : 0;
+  ycc_row_scalar(y, cb, cr, o, x0, W);
+}
+
 // Centred (triangle) upsampling of one chroma row by 1 or 2 per axis into
 // `out` (W values): vertical blend of rows y0/y1 with weights (wa, wb)/4,
 // then horizontal 3:1 blend; result = chroma sample at each output pixel,
 // rounded. Same positions as the generic bilinear path ((x+0.5)/f - 0.5,
-// clamped to the plane's valid area).
+// clamped to the plane's valid area). The interior loops are branch-free
+// (the edge samples are handled apart) so the compiler vectorises them.
 void chroma_row(const Comp& c, int hf, int vf, int y, int W, int H, int hmax, int vmax, uint8_t* out,
-                std::vector<int>& tmp) {
+                std::vector<uint16_t>& tmp) {
   const int pw = c.bw * 8;
   const int cw = (W * c.h + hmax - 1) / hmax, ch = (H * c.v + vmax - 1) / vmax;
   int y0, y1, wa, wb;  // weights of rows y0, y1 (sum 4)
@@ -345,16 +413,36 @@ void chroma_row(const Comp& c, int hf, int vf, int y, int W, int H, int hmax, in
   const uint8_t* r0 = c.plane.data() + (size_t)y0 * pw;
   const uint8_t* r1 = c.plane.data() + (size_t)y1 * pw;
   tmp.resize((size_t)cw);
-  for (int x = 0; x < cw; ++x) tmp[x] = wa * r0[x] + wb * r1[x];  // x4
+  uint16_t* t = tmp.data();
+  for (int x = 0; x < cw; ++x) t[x] = (uint16_t)(wa * r0[x] + wb * r1[x]);  // x4
   if (hf == 1) {
-    for (int x = 0; x < W; ++x) out[x] = (uint8_t)((tmp[x] + 2) >> 2);
+    for (int x = 0; x < W; ++x) out[x] = (uint8_t)((t[x] + 2) >> 2);
     return;
   }
-  for (int x = 0; x < W; ++x) {
-    const int i = x >> 1;
-    const int j = (x & 1) ? std::min(i + 1, cw - 1) : std::max(i - 1, 0);
-    out[x] = (uint8_t)((3 * tmp[i] + tmp[j] + 8) >> 4);  // x16
+  // out[2i] blends t[i] with t[i-1], out[2i+1] with t[i+1] (clamped at the ends)
+  auto even = [&](int i) { return (uint8_t)((3 * t[i] + t[std::max(i - 1, 0)] + 8) >> 4); };
+  auto odd = [&](int i) { return (uint8_t)((3 * t[i] + t[std::min(i + 1, cw - 1)] + 8) >> 4); };
+  const int n = W / 2;  // complete (even, odd) pairs; W odd leaves a last even sample
+  if (n >= 2) {
+    out[0] = even(0);
+    out[1] = odd(0);
+    const int last = std::min(n - 1, cw - 2);  // interior pairs: i-1 >= 0 and i+1 <= cw-1
+    for (int i = 1; i <= last; ++i) {
+      const int m3 = 3 * t[i];
+      out[2 * i] = (uint8_t)((m3 + t[i - 1] + 8) >> 4);
+      out[2 * i + 1] = (uint8_t)((m3 + t[i + 1] + 8) >> 4);
+    }
+    for (int i = last + 1; i < n; ++i) {
+      out[2 * i] = even(i);
+      out[2 * i + 1] = odd(i);
+    }
+  } else {
+    for (int i = 0; i < n; ++i) {
+      out[2 * i] = even(i);
+      out[2 * i + 1] = odd(i);
+    }
   }
+  if (W & 1) out[W - 1] = even(n);
 }
 
 // Fast colour conversion for 1 or 3 components with chroma subsampled by 1
@@ -382,33 +470,17 @@ bool convert_fast(const std::vector<Comp>& comps, int hmax, int vmax, int W, int
   }
   if (hf[0] == 1 && vf[0] == 1 && hf[1] == 1 && vf[1] == 1) {  // 4:4:4: planes read in place
     const int cpw = comps[1].bw * 8, rpw = comps[2].bw * 8;
-    for (int y = 0; y < H; ++y) {
-      const uint8_t* yr = Yc.plane.data() + (size_t)y * pw;
-      const uint8_t* br = comps[1].plane.data() + (size_t)y * cpw;
-      const uint8_t* rr = comps[2].plane.data() + (size_t)y * rpw;
-      uint8_t* o = rgb + (size_t)y * W * 3;
-      for (int x = 0; x < W; ++x) {
-        const int Y = yr[x] << 16, b = br[x], r = rr[x];
-        o[3 * x] = clamp_fix(Y + kColor.cr_r[r]);
-        o[3 * x + 1] = clamp_fix(Y + kColor.cb_g[b] + kColor.cr_g[r]);
-        o[3 * x + 2] = clamp_fix(Y + kColor.cb_b[b]);
-      }
-    }
+    for (int y = 0; y < H; ++y)
+      ycc_row(Yc.plane.data() + (size_t)y * pw, comps[1].plane.data() + (size_t)y * cpw,
+              comps[2].plane.data() + (size_t)y * rpw, rgb + (size_t)y * W * 3, W);
     return true;
   }
   std::vector<uint8_t> cb((size_t)W), cr((size_t)W);
-  std::vector<int> tmp;
+  std::vector<uint16_t> tmp;
   for (int y = 0; y < H; ++y) {
     chroma_row(comps[1], hf[0], vf[0], y, W, H, hmax, vmax, cb.data(), tmp);
     chroma_row(comps[2], hf[1], vf[1], y, W, H, hmax, vmax, cr.data(), tmp);
-    const uint8_t* yr = Yc.plane.data() + (size_t)y * pw;
-    uint8_t* o = rgb + (size_t)y * W * 3;
-    for (int x = 0; x < W; ++x) {
-      const int Y = yr[x] << 16, b = cb[x], r = cr[x];
-      o[3 * x] = clamp_fix(Y + kColor.cr_r[r]);
-      o[3 * x + 1] = clamp_fix(Y + kColor.cb_g[b] + kColor.cr_g[r]);
-      o[3 * x + 2] = clamp_fix(Y + kColor.cb_b[b]);
-    }
+    ycc_row(Yc.plane.data() + (size_t)y * pw, cb.data(), cr.data(), rgb + (size_t)y * W * 3, W);
   }
   return true;
 }
