@@ -612,8 +612,10 @@ bool conv3x3_stream_supported(int Hin, int Win, int Cin, int Cout, int stride) {
     return Cin == Cout && ((Hin == 28 && Win == 28 && Cin == 128) || (Hin == 14 && Win == 14 && Cin == 256) ||
                            (Hin == 7 && Win == 7 && Cin == 512) || (Hin == 56 && Win == 56 && Cin == 64));
   if (stride == 2)
-    return Cout == 2 * Cin && ((Hin == 56 && Win == 56 && Cin == 64) || (Hin == 28 && Win == 28 && Cin == 128) ||
-                               (Hin == 14 && Win == 14 && Cin == 256));
+    return (Cout == 2 * Cin && ((Hin == 56 && Win == 56 && Cin == 64) || (Hin == 28 && Win == 28 && Cin == 128) ||
+                                (Hin == 14 && Win == 14 && Cin == 256))) ||
+           // ResNet50 layer2.0.conv2 (the bottleneck's strided 3x3)
+           (Cout == Cin && Hin == 56 && Win == 56 && Cin == 128);
   return false;
 }
 
@@ -625,7 +627,9 @@ bool conv3x3_stream_uses_frag(int Hin, int Win, int Cin, int Cout, int stride) {
   // 56x56x64 / s2 (K-tiles per tap = 2, so a 2-deep ring): 83.8 vs 71.0 us
   // with the LDS ring (a 4-deep ring with all 20 K-tiles unrolled: 73.8),
   // not used; 28x28x128 / s2: 48.6 vs 53.6 us
-  if (stride == 2) return Cout == 2 * Cin && ((Hin == 28 && Win == 28 && Cin == 128) || (Hin == 14 && Cin == 256));
+  if (stride == 2)
+    return (Cout == 2 * Cin && ((Hin == 28 && Win == 28 && Cin == 128) || (Hin == 14 && Cin == 256))) ||
+           (Cout == Cin && Hin == 56 && Win == 56 && Cin == 128);
   // (28x28x128 in quarter images and 14x14x256 in 2 channel splits, both 7
   // fragments per wave so the register ring fits, measured 70.2 / 60.2 vs
   // 67.9 / 56.4 us with the LDS ring: kept out)
@@ -689,6 +693,10 @@ void conv3x3_stream(const void* x, const void* w, const float* bias, const void*
   }
   else if (stride == 1)  // layer4: two whole images x half the output channels (2 x 49 x 1 KB = 98 KB)
     launch_stream<7, 7, 512, 512, 7, 2, 2, 1, 1>(a, s);
+  else if (Cin == 128 && Hin == 56 && wfrag)  // ResNet50 layer2.0.conv2: 4 output rows (9 x 56 x 256 B = 129 KB)
+    launch_stream<28, 28, 128, 128, 4, 1, 1, 2, 2, true>(a, s);
+  else if (Cin == 128 && Hin == 56)  // the same with the LDS weight ring: 2 output rows (5 rows = 72 KB + 48 KB)
+    launch_stream<28, 28, 128, 128, 2, 1, 1, 2, 2>(a, s);
   else if (Cin == 64)  // layer2.0.conv1: a quarter image (15 x 56 x 128 B = 105 KB)
     launch_stream<28, 28, 64, 128, 7, 1, 1, 2, 2>(a, s);
   else if (Cin == 128 && wfrag)

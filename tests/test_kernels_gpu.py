@@ -285,14 +285,16 @@ def test_conv3x3_stream(gpu, HW, C, B, res, relu):
     assert _rel(_nchw(y.float().cpu()), ref) < 8e-3
 
 
-@pytest.mark.parametrize("HW,Cin,B,relu", [(56, 64, 1, True), (56, 64, 2, False), (28, 128, 1, True),
-                                          (28, 128, 3, False), (14, 256, 1, True), (14, 256, 3, False)])
-def test_conv3x3_stream_stride2(gpu, HW, Cin, B, relu):
+@pytest.mark.parametrize("HW,Cin,B,relu,cmul", [(56, 64, 1, True, 2), (56, 64, 2, False, 2), (28, 128, 1, True, 2),
+                                               (28, 128, 3, False, 2), (14, 256, 1, True, 2), (14, 256, 3, False, 2),
+                                               (56, 128, 1, True, 1), (56, 128, 3, False, 1)])
+def test_conv3x3_stream_stride2(gpu, HW, Cin, B, relu, cmul):
     """Stride-2 direct 3x3 conv (conv3x3_stream.hip: 56x56x64 -> 28x28x128 in
-    quarter images, 28x28x128 -> 14x14x256 in half images, even-first column
-    layout) vs torch fp32."""
+    quarter images, 28x28x128 -> 14x14x256 in half images, ResNet50's
+    56x56x128 -> 28x28x128 in 2-row strips (LDS weight ring) and 4-row strips
+    (register weights, bit-identical), even-first column layout) vs torch fp32."""
     g = torch.Generator().manual_seed(22)
-    Cout = 2 * Cin
+    Cout = cmul * Cin
     x = torch.randn(B, Cin, HW, HW, generator=g).bfloat16().float()
     w = (torch.randn(Cout, Cin, 3, 3, generator=g) / (9 * Cin) ** 0.5).bfloat16().float()
     bias = torch.randn(Cout, generator=g) * 0.1
@@ -304,6 +306,10 @@ def test_conv3x3_stream_stride2(gpu, HW, Cin, B, relu):
     torch.cuda.synchronize()
     assert y.shape == (B, HW // 2, HW // 2, Cout)
     assert _rel(_nchw(y.float().cpu()), ref) < 8e-3
+    if cmul == 1:  # the register-weight variant: same MFMA order per output
+        yw = ops.conv3x3_stream(_nhwc(x).bfloat16().to(gpu), wp, bias.to(gpu), None, relu, stride=2, frag=True)
+        torch.cuda.synchronize()
+        assert torch.equal(y, yw)
 
 
 @pytest.mark.parametrize("HW,C,B,res,variant", [(7, 512, 1, False, 0), (7, 512, 3, True, 0), (7, 512, 4, True, 0),
