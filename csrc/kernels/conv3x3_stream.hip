@@ -35,6 +35,8 @@
 //  * The K loop is software-pipelined: the operands of K-tile t+1 are read
 //    while the MFMAs of t run.
 // Design history and measurements: profiles/r1_stream_conv.log.
+#include <atomic>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -596,7 +598,7 @@ void launch_stream(const StreamConvArgs& a, hipStream_t s) {
 
 // Tuning hook for tools/conv_bench.py A/B runs (0 = the default kernels):
 // 1 = the 14x14x256 register-weight kernel with a 2-deep weight ring (PD 2).
-int g_stream_variant = 0;
+std::atomic<int> g_stream_variant{0};
 
 }  // namespace
 

@@ -17,6 +17,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
+import dmlc  # noqa: E402
 from dmlc import ops  # noqa: E402
 
 RESNET18 = [
@@ -129,7 +130,7 @@ def main():
                     f()
                     row.append(_stamps())
                 # register-weight kernels (fragment-order weights), per A/B variant
-                nat = ops.C if hasattr(ops, "C") else __import__("dmlc").native()
+                nat = dmlc.native()
                 if nat.conv3x3_stream_uses_frag(H, W, Cin, Cout, s) and s == 1:
                     for v in [int(t) for t in a.variants.split(",")]:
                         nat.conv3x3_stream_set_variant(v)
