@@ -8,6 +8,7 @@
 #include <cmath>
 #include <cstring>
 #include <fstream>
+#include <functional>
 #include <immintrin.h>
 #include <iterator>
 #include <stdexcept>
@@ -505,7 +506,8 @@ bool convert_fast(const std::vector<Comp>& comps, int hmax, int vmax, int W, int
 
 }  // namespace
 
-Image decode_jpeg(const uint8_t* data, size_t size) {
+// Decodes into the buffer out(W, H) returns (W * H * 3 bytes).
+static void decode_jpeg_impl(const uint8_t* data, size_t size, const std::function<uint8_t*(int, int)>& out) {
   const uint8_t* p = data;
   const uint8_t* end = data + size;
   if (size < 4 || p[0] != 0xFF || p[1] != 0xD8) throw std::runtime_error("jpeg: missing SOI");
@@ -715,11 +717,8 @@ Image decode_jpeg(const uint8_t* data, size_t size) {
   }
   if (!frame || !scanned) throw std::runtime_error("jpeg: no image data");
 
-  Image img;
-  img.width = W;
-  img.height = H;
-  img.rgb.resize((size_t)W * H * 3);
-  if (convert_fast(comps, hmax, vmax, W, H, img.rgb.data())) return img;
+  uint8_t* rgb = out(W, H);
+  if (convert_fast(comps, hmax, vmax, W, H, rgb)) return;
   auto sample = [&](const Comp& c, int x, int y) -> float {
     const int pw = c.bw * 8;
     if (c.h == hmax && c.v == vmax) return c.plane[(size_t)y * pw + x];
@@ -738,7 +737,7 @@ Image decode_jpeg(const uint8_t* data, size_t size) {
   auto clamp8 = [](float v) { return (uint8_t)std::min(255.f, std::max(0.f, std::round(v))); };
   for (int y = 0; y < H; ++y)
     for (int x = 0; x < W; ++x) {
-      uint8_t* o = &img.rgb[((size_t)y * W + x) * 3];
+      uint8_t* o = rgb + ((size_t)y * W + x) * 3;
       const float Y = sample(comps[0], x, y);
       if (comps.size() == 1) {
         o[0] = o[1] = o[2] = clamp8(Y);
@@ -749,7 +748,21 @@ Image decode_jpeg(const uint8_t* data, size_t size) {
         o[2] = clamp8(Y + 1.772f * cb);
       }
     }
+}
+
+Image decode_jpeg(const uint8_t* data, size_t size) {
+  Image img;
+  decode_jpeg_impl(data, size, [&](int w, int h) {
+    img.width = w;
+    img.height = h;
+    img.rgb.resize((size_t)w * h * 3);
+    return img.rgb.data();
+  });
   return img;
+}
+
+void decode_jpeg_into(const uint8_t* data, size_t size, const std::function<uint8_t*(int, int)>& out) {
+  decode_jpeg_impl(data, size, out);
 }
 
 Image decode_jpeg_file(const std::string& path) {

@@ -9,6 +9,7 @@
 // rejected with an error.
 #pragma once
 #include <cstdint>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -22,5 +23,9 @@ struct Image {
 // Throws std::runtime_error on malformed / unsupported input.
 Image decode_jpeg(const uint8_t* data, size_t size);
 Image decode_jpeg_file(const std::string& path);
+// Decodes straight into a caller-provided buffer: out(width, height) returns
+// width * height * 3 writable bytes (e.g. pinned staging memory for the H2D
+// copy; saves the Image vector's zero-fill and a copy per query image).
+void decode_jpeg_into(const uint8_t* data, size_t size, const std::function<uint8_t*(int, int)>& out);
 
 }  // namespace dmlc

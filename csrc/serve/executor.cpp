@@ -404,7 +404,7 @@ class GpuExecutor : public Executor {
 
  private:
   static constexpr size_t kDecodeThreads = 8;
-  static constexpr int kStagers = 8;
+  static constexpr int kStagers = 16;  // held through a miss's decode (it decodes into the pinned buffer)
 
   // One model replicated on every GPU of the executor.
   struct ModelSlot {
@@ -590,20 +590,35 @@ class GpuExecutor : public Executor {
         return;
       }
     }
-    const Image img = decode_jpeg_file(path);
-    const size_t bytes = img.rgb.size();
+    std::vector<uint8_t> jpeg;
+    {
+      std::ifstream f(path, std::ios::binary);
+      if (!f) throw std::runtime_error("cannot open " + path);
+      jpeg.assign(std::istreambuf_iterator<char>(f), std::istreambuf_iterator<char>());
+    }
+    // (kStagers = 2 x the decode threads of one query: holding a stager through
+    // the decode leaves concurrent queries' misses decoding in parallel)
     Stager st = take_stager();
     void* dev = nullptr;
+    int img_h = 0, img_w = 0;
+    size_t bytes = 0;
     try {
       DMLC_HIP_CHECK(hipSetDevice(devices_[0]));
-      if (st.pinned_bytes < bytes) {
-        if (st.pinned) DMLC_HIP_CHECK(hipHostFree(st.pinned));
-        st.pinned = nullptr;
-        st.pinned_bytes = 0;
-        DMLC_HIP_CHECK(hipHostMalloc(&st.pinned, bytes, hipHostMallocDefault));
-        st.pinned_bytes = bytes;
-      }
-      std::memcpy(st.pinned, img.rgb.data(), bytes);
+      // decoded straight into the stager's pinned buffer: no RGB vector to
+      // zero-fill and copy per query image
+      decode_jpeg_into(jpeg.data(), jpeg.size(), [&](int w, int h) {
+        img_w = w;
+        img_h = h;
+        bytes = (size_t)w * h * 3;
+        if (st.pinned_bytes < bytes) {
+          if (st.pinned) DMLC_HIP_CHECK(hipHostFree(st.pinned));
+          st.pinned = nullptr;
+          st.pinned_bytes = 0;
+          DMLC_HIP_CHECK(hipHostMalloc(&st.pinned, bytes, hipHostMallocDefault));
+          st.pinned_bytes = bytes;
+        }
+        return (uint8_t*)st.pinned;
+      });
       DMLC_HIP_CHECK(hipMallocAsync(&dev, bytes, st.stream));
       DMLC_HIP_CHECK(hipMemcpyAsync(dev, st.pinned, bytes, hipMemcpyHostToDevice, st.stream));
       DMLC_HIP_CHECK(hipStreamSynchronize(st.stream));  // resident before it is visible
@@ -632,8 +647,8 @@ class GpuExecutor : public Executor {
     }
     Entry en;
     en.dev = dev;
-    en.h = img.height;
-    en.w = img.width;
+    en.h = img_h;
+    en.w = img_w;
     en.bytes = bytes;
     lru_.push_front(path);
     en.lru = lru_.begin();
