@@ -30,7 +30,12 @@ class HipWorker : public Worker {
     DMLC_HIP_CHECK(hipSetDevice(dev_));
     int lo = 0, hi = 0;
     DMLC_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
-    DMLC_HIP_CHECK(hipStreamCreateWithPriority(&s_[kCompute], hipStreamNonBlocking, lo));
+    // With two lanes, lane 0 runs at high priority: its workgroups dispatch
+    // first as CUs free up and lane 1 fills the gaps (its kernels' tails and
+    // the one-workgroup-per-CU convs' partial last rounds), instead of the two
+    // forwards contending evenly: +0.6-1.1% img/s in two same-box interleaved
+    // A/Bs (profiles/r2_lanes.txt)
+    DMLC_HIP_CHECK(hipStreamCreateWithPriority(&s_[kCompute], hipStreamNonBlocking, e_.size() > 1 ? hi : lo));
     DMLC_HIP_CHECK(hipStreamCreateWithPriority(&s_[kIn], hipStreamNonBlocking, hi));
     DMLC_HIP_CHECK(hipStreamCreateWithPriority(&s_[kOut], hipStreamNonBlocking, hi));
     for (size_t l = 1; l < e_.size(); ++l)
