@@ -20,18 +20,19 @@ region). The serving path (scatter mode runs all of it every step):
       second communicator/stream, then a D2H of the answers.
 
 Input modes (--input-mode):
-  staged (default)  rank 0's images are scattered to the ranks over RCCL once,
+  scatter (default) the per-step scatter above: every step moves each rank's
+                    u8 shard (38.5 MB at 256 images) from rank 0's HBM over
+                    RCCL, one step ahead of its forward. Rank 0 drives all the
+                    send legs, and RCCL's copy kernels next to a forward slow
+                    it ~1.2x (they hold CUs the one-workgroup-per-CU convs
+                    need, profiles/r2_rccl_interference.txt), so rank 0 takes
+                    --coord-weight of a fair share and the other ranks split
+                    the rest (global batch unchanged: per_gpu_batch x N).
+  staged            rank 0's images are scattered to the ranks over RCCL once,
                     before timing (SDFS shard replicas placed in the HBM of the
                     GPU that serves them, as predict-shard does); every timed
                     step classifies the rank's HBM-resident shard and gathers
                     the answers to rank 0 over RCCL (8 B per image, one CTA).
-  scatter           the per-step scatter above: every step also moves each
-                    rank's 38.5 MB shard from rank 0 over RCCL. Measured on one
-                    GPU, RCCL's copy kernels running next to the forward slow
-                    it ~1.2x (they hold CUs the one-workgroup-per-CU convs
-                    need; a copy-engine copy of the same bytes: 1.04x,
-                    profiles/r2_rccl_interference.txt), and at N > 1 both the
-                    coordinator and every receiver run them each step.
   local             each rank generates its own shard (no transfer at all).
 At N = 1 all three run the same forward.
 
@@ -55,6 +56,9 @@ if ROOT not in sys.path:
 
 REF_MEAN_LATENCY_MS = 158.94  # ResNet18, CS425MP4Report.pdf p.2 §1a
 REF_STREAM_IMG_S = 1000.0 / REF_MEAN_LATENCY_MS
+# rank 0's share in scatter mode (it also runs the 7 send legs): its forward
+# next to RCCL kernels is ~1.2x slower (profiles/r2_rccl_interference.txt)
+COORD_WEIGHT = 0.85
 
 
 def pct(xs, q):
@@ -95,7 +99,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--model", default="resnet18")
     ap.add_argument("--batch", type=int, default=256, help="images per GPU per step")
-    ap.add_argument("--input-mode", choices=["staged", "scatter", "local"], default="staged")
+    ap.add_argument("--input-mode", choices=["staged", "scatter", "local"], default="scatter")
+    ap.add_argument("--coord-weight", type=float, default=None,
+                    help="rank 0's share of a step as a fraction of a fair share (scatter mode; default "
+                         f"{COORD_WEIGHT} at N > 1, 1 at N = 1)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--lanes", type=int, default=2, choices=[1, 2, 3, 4],
                     help="model instances per GPU on alternating streams (2: step i+1 starts under step i's tail)")
@@ -144,8 +151,13 @@ def main():
         box = [[C.rccl_unique_id(), C.rccl_unique_id()] if rank == 0 else None]
         dist.broadcast_object_list(box, src=0)
         ids = box[0]
+    coord_weight = args.coord_weight if args.coord_weight is not None else (COORD_WEIGHT if world > 1 else 1.0)
+    if not scatter:
+        coord_weight = 1.0  # nothing to send per step: an even split
     runner = C.DpRunner(eng._e, world, rank, ids[0], ids[1], B, scatter=scatter, use_graph=use_graph,
-                        lanes=args.lanes)
+                        lanes=args.lanes, coord_weight=coord_weight)
+    counts = runner.counts  # images per rank per step (sum = B * world)
+    M = runner.max_per_rank
 
     # Input pool: two global batches of distinct synthetic images, in the
     # coordinator's HBM (scatter), staged from there into every rank's HBM
@@ -154,16 +166,16 @@ def main():
     pool = None
     n_pool = 0
     if args.input_mode == "staged":
-        n_pool = 2 * B
+        n_pool = 2 * M  # two per-rank batches at a stride of max_per_rank images
         pool = torch.empty((n_pool, 224, 224, 3), dtype=torch.uint8, device=dev)
         src = torch.randint(0, 256, (2, world * B, 224, 224, 3), dtype=torch.uint8, device=dev,
                             generator=g) if rank == 0 else None
         torch.cuda.synchronize()
-        for k in range(2):  # batch k: rank r's shard = images [r*B, (r+1)*B) of src[k]
-            runner.stage(src[k].data_ptr() if rank == 0 else 0, pool[k * B].data_ptr(), B)
+        for k in range(2):  # batch k: rank r's shard = its count's images of src[k]
+            runner.stage(src[k].data_ptr() if rank == 0 else 0, pool[k * M].data_ptr())
         del src
     elif rank == 0 or not scatter:
-        n_pool = 2 * (B * world if scatter else B)
+        n_pool = 2 * (B * world if scatter else M)
         pool = torch.randint(0, 256, (n_pool, 224, 224, 3), dtype=torch.uint8, device=dev, generator=g)
     pool_ptr = pool.data_ptr() if pool is not None else 0
     torch.cuda.synchronize()
@@ -259,15 +271,18 @@ def main():
                     + {"staged": "generated on rank 0, shards scattered to the ranks' HBM over RCCL before timing",
                        "scatter": "HBM-resident on rank 0, scattered over RCCL every step",
                        "local": "generated in every rank's HBM"}[args.input_mode],
+            "prime_steps": args.prime_steps,
             "config": {
                 "model": args.model,
                 "global_batch": B * world,
                 "per_gpu_batch": B,
+                "per_rank_counts": counts,
+                "coord_weight": coord_weight,
                 "seq_len": None,
                 "image_size": 224,
                 "parallelism": f"dp{world}",
                 "input_mode": args.input_mode,
-                "comm": "native RCCL grouped send/recv (csrc/comm), shards + answers on separate communicators"
+                "comm": "native RCCL grouped send/recv (csrc/comm/runner.h), shards + answers on separate communicators"
                     + ("" if scatter else "; per step: answers only"),
                 "rccl_ranks": world,
                 "hipgraph": use_graph,
@@ -276,14 +291,15 @@ def main():
                 "baseline": "6.29 img/s = one query stream at the reference's 158.94 ms mean ResNet18 latency "
                             "(CS425MP4Report.pdf p.2; no images/s is published)",
             },
-            "per_rank_images_s": [round(B * args.steps / s, 1) for s in per_rank_s],
+            "per_rank_images_s": [round(c * args.steps / s, 1) for c, s in zip(counts, per_rank_s)],
             "batch_latency_p50_ms": round(pct(batch_lat, 50), 3) if batch_lat else None,
             "batch_latency_p95_ms": round(pct(batch_lat, 95), 3) if batch_lat else None,
             "query_latency_mean_ms": round(e2e["mean_ms"], 3) if e2e else None,
             "query_latency_p50_ms": round(e2e["p50_ms"], 3) if e2e else None,
             "query_latency_p95_ms": round(e2e["p95_ms"], 3) if e2e else None,
-            "query_latency_def": "reference definition (src/services.rs:419-424): connect + RPC + JPEG decode + "
-                                 "resize + forward + top-1 through a one-node dmlc-node cluster, one query in flight; "
+            "query_latency_def": "reference definition (src/services.rs:419-424): a new TCP connection per query "
+                                 "(--new-conn-per-query) + RPC + JPEG decode + resize + forward + top-1 through a "
+                                 "one-node dmlc-node cluster, one query in flight; "
                                  + (e2e["data"] if e2e else "not measured"),
             "vs_baseline_latency": round(REF_MEAN_LATENCY_MS / e2e["mean_ms"], 1) if e2e else None,
             "gpu_batch1_latency_p50_ms": round(pct(qlat, 50), 4) if qlat else None,

@@ -16,6 +16,13 @@
 
 #include "../comm/comm.h"
 #include "../comm/dp.h"
+#include "../comm/fleet.h"
+#include "../comm/runner.h"
+#include <atomic>
+#include <map>
+#include <mutex>
+#include <set>
+#include <tuple>
 #include "../runtime/engine.h"
 
 namespace py = pybind11;
@@ -24,72 +31,44 @@ using namespace dmlc;
 namespace {
 
 // ------------------------------------------------------------------ runner
+// bench.py's rank (csrc/comm/runner.h) on the HIP engine and RCCL.
 class DpRunner {
  public:
   DpRunner(Engine* e, int world, int rank, const std::string& id_in, const std::string& id_out, int max_per_rank,
-           bool scatter, int image_size, bool use_graph, int timeout_ms, int lanes, int slots)
-      : world_(world), rank_(rank), max_(max_per_rank), scatter_(scatter), S_(image_size), timeout_ms_(timeout_ms) {
+           bool scatter, int image_size, bool use_graph, int timeout_ms, int lanes, int slots, double coord_weight,
+           std::vector<int> counts)
+      : S_(image_size) {
     if (lanes < 1 || lanes > dp::Worker::kMaxLanes) throw std::invalid_argument("DpRunner: lanes must be 1..4");
+    if (counts.empty()) counts = dp::weighted_counts(max_per_rank, world, coord_weight);
+    int mx = 0;
+    for (int c : counts) mx = std::max(mx, c);
+    e->reserve(mx);
     std::vector<Engine*> more;
     for (int l = 1; l < lanes; ++l) {  // further instances of the model: consecutive steps overlap
       lanes_.push_back(std::make_unique<Engine>(*e, e->device()));
       lanes_.back()->copy_weights_from(*e);
-      lanes_.back()->reserve(std::max(e->max_batch(), max_per_rank));
+      lanes_.back()->reserve(std::max(e->max_batch(), mx));
       more.push_back(lanes_.back().get());
     }
-    w_ = dp::make_hip_worker(e, S_, S_, use_graph, more);
-    // one slot per lane (>= 2): that many steps in flight
-    // Steps in flight (slots). Step i reuses slot i - slots, so its forward
-    // waits for that step's answers to have left; with slots = 2 that was the
-    // step just before on the same lane, and the answer copy's latency sat
-    // between a lane's consecutive forwards (bench: 268k vs 276k img/s with 4
-    // slots, the bare two-lane loop 276.7k: tools/pipeline_probe.py).
-    if (slots <= 0) slots = 2 * std::max(2, lanes);
-    if (slots < 2) throw std::invalid_argument("DpRunner: slots must be >= 2");
-    r_ = std::make_unique<dp::Rank>(w_.get(), max_, ib(), scatter_, slots);
-    if (world_ > 1) {
-      cin_ = comm::rccl_init_rank(id_in, world_, rank_, e->device());
+    std::unique_ptr<comm::Comm> cin, cout;
+    if (world > 1) {
+      cin = comm::rccl_init_rank(id_in, world, rank, e->device());
       // answers: 8 B per image, one CTA (comm::rccl_init_rank's max_ctas)
-      cout_ = comm::rccl_init_rank(id_out, world_, rank_, e->device(), 1);
-      r_->attach(cin_.get(), cout_.get());
-    } else {
-      r_->attach(nullptr, nullptr);
+      cout = comm::rccl_init_rank(id_out, world, rank, e->device(), 1);
     }
+    r_ = std::make_unique<dp::Runner>(dp::make_hip_worker(e, S_, S_, use_graph, more), std::move(cin),
+                                      std::move(cout), world, rank, counts, scatter, (size_t)S_ * S_ * 3, timeout_ms,
+                                      slots);
   }
   ~DpRunner() {
     r_.reset();
-    w_.reset();
     lanes_.clear();
-    cin_.reset();
-    cout_.reset();
   }
-  size_t ib() const { return (size_t)S_ * S_ * 3; }
-
-  // Steps [first, first+n) over a staged pool: scatter mode reads global
-  // batches (max*world images) from the coordinator's pool; local mode reads
-  // per-rank batches from this rank's own pool.
   py::dict run(uintptr_t pool, int64_t pool_images, int64_t first, int64_t n, bool pipelined) {
-    const int64_t G = (int64_t)max_ * world_;
-    const int64_t per = scatter_ ? G : max_;
-    const bool has_pool = scatter_ ? rank_ == 0 : true;
-    if (has_pool && pool_images < per) throw std::invalid_argument("DpRunner.run: pool smaller than one batch");
-    const int64_t nb = has_pool ? pool_images / per : 1;
-    auto counts = dp::shard_counts(G, world_, max_);
-    auto plan = [&](int64_t step, const dp::Rank&) {
-      dp::StepPlan p;
-      p.step = step;
-      p.counts = counts;
-      p.src = has_pool ? (const uint8_t*)pool + (size_t)((step % nb) * per) * ib() : nullptr;
-      return p;
-    };
-    auto on_result = [&](const dp::StepPlan&, const int32_t* i, const float* pr) {
-      last_idx_.assign(i, i + G);
-      last_prob_.assign(pr, pr + G);
-    };
     dp::PipelineResult res;
     {
       py::gil_scoped_release nogil;
-      res = dp::run_pipeline({r_.get()}, first, n, plan, on_result, timeout_ms_, pipelined);
+      res = r_->run((const uint8_t*)pool, pool_images, first, n, pipelined);
     }
     py::dict d;
     d["steps"] = res.steps;
@@ -97,43 +76,94 @@ class DpRunner {
     d["step_ms"] = res.step_ms;
     return d;
   }
-  py::tuple last_results() const { return py::make_tuple(last_idx_, last_prob_); }
-  uintptr_t compute_stream() { return (uintptr_t)w_->stream(dp::Worker::kCompute); }
+  py::tuple last_results() const { return py::make_tuple(r_->last_idx(), r_->last_prob()); }
+  uintptr_t compute_stream() { return (uintptr_t)r_->worker()->stream(dp::Worker::kCompute); }
   void sync() {
     py::gil_scoped_release nogil;
-    w_->sync_all();
+    r_->worker()->sync_all();
   }
-  // Stage shards into every rank's HBM before a run (SDFS replicas placed
-  // where they are served): the coordinator's `images` images per rank at
-  // src (rank r's at image offset r * images) go to dst on rank r over the
-  // shard communicator (its own part by a device copy); blocks until done.
-  void stage(uintptr_t src, uintptr_t dst, int64_t images) {
-    const size_t bytes = (size_t)images * ib();
+  // SDFS replicas placed where they are served: this global batch's shards
+  // into every rank's HBM before a run (csrc/comm/runner.h stage()).
+  void stage(uintptr_t src, uintptr_t dst) {
     py::gil_scoped_release nogil;
-    w_->activate();
-    if (rank_ == 0) w_->copy((void*)dst, (const void*)src, bytes, dp::Worker::kIn);
-    if (world_ > 1) {
-      cin_->group_start();
-      if (rank_ == 0) {
-        for (int r = 1; r < world_; ++r) cin_->send((const void*)(src + r * bytes), bytes, r, w_->stream(dp::Worker::kIn));
-      } else {
-        cin_->recv((void*)dst, bytes, 0, w_->stream(dp::Worker::kIn));
-      }
-      cin_->group_end();
-    }
-    w_->sync_all();
+    r_->stage((const uint8_t*)src, (uint8_t*)dst);
   }
-
-  int world_, rank_, max_;
-  bool scatter_;
-  int S_, timeout_ms_;
+  int S_;
   std::vector<std::unique_ptr<Engine>> lanes_;
-  std::unique_ptr<dp::Worker> w_;
-  std::unique_ptr<dp::Rank> r_;
-  std::unique_ptr<comm::Comm> cin_, cout_;
-  std::vector<int32_t> last_idx_;
-  std::vector<float> last_prob_;
+  std::unique_ptr<dp::Runner> r_;
 };
+
+// bench.py's exact per-rank call sequence (stage, prime, warmup, timed,
+// unpipelined latency) on host workers and the rendezvous host
+// communicator, one thread per rank (= one process per GPU). `pool`: two
+// global batches on the coordinator. Returns per rank the steps of each run
+// and on rank 0 whether the last step's answers match its images.
+py::dict dp_host_bench(py::array_t<uint8_t, py::array::c_style> pool, int world, int per_rank, double coord_weight,
+                       const std::string& input_mode, int lanes, int prime, int warmup, int steps, int latency) {
+  if (pool.ndim() != 4 || pool.shape(3) != 3) throw std::invalid_argument("pool must be u8 [n,H,W,3]");
+  const int H = (int)pool.shape(1), W = (int)pool.shape(2);
+  const size_t ib = (size_t)H * W * 3;
+  const auto counts = dp::weighted_counts(per_rank, world, coord_weight);
+  int64_t G = 0;
+  for (int c : counts) G += c;
+  if (pool.shape(0) != 2 * G) throw std::invalid_argument("pool must hold two global batches");
+  const bool scatter = input_mode == "scatter";
+  if (!scatter && input_mode != "staged") throw std::invalid_argument("input_mode: scatter | staged");
+  const uint8_t* src = pool.data();
+  auto cin = comm::host_world(world, 5000), cout = comm::host_world(world, 5000);
+  std::vector<std::string> errs(world);
+  std::vector<std::vector<int64_t>> done(world);
+  std::vector<int32_t> last_idx;
+  std::vector<float> last_prob;
+  int64_t last_step = -1;
+  {
+    py::gil_scoped_release nogil;
+    std::vector<std::thread> ts;
+    for (int r = 0; r < world; ++r)
+      ts.emplace_back([&, r] {
+        try {
+          dp::Runner run(dp::make_host_worker(r, H, W, 1000, lanes), world > 1 ? std::move(cin[r]) : nullptr,
+                         world > 1 ? std::move(cout[r]) : nullptr, world, r, counts, scatter, ib, 5000);
+          std::vector<uint8_t> mine;
+          const uint8_t* p = r == 0 ? src : nullptr;
+          int64_t np = r == 0 ? 2 * G : 0;
+          if (!scatter) {  // staged: two per-rank batches at a stride of max_per_rank images
+            mine.resize((size_t)2 * run.max_per_rank() * ib);
+            for (int k = 0; k < 2; ++k)
+              run.stage(r == 0 ? src + (size_t)k * G * ib : nullptr, mine.data() + (size_t)k * run.max_per_rank() * ib);
+            p = mine.data();
+            np = 2 * run.max_per_rank();
+          }
+          std::vector<int64_t> d;
+          d.push_back(run.run(p, np, 0, prime).steps);
+          d.push_back(run.run(p, np, 0, warmup).steps);
+          d.push_back(run.run(p, np, warmup, steps).steps);
+          d.push_back(run.run(p, np, warmup + steps, latency, /*pipelined=*/false).steps);
+          done[r] = d;
+          if (r == 0) {
+            last_idx = run.last_idx();
+            last_prob = run.last_prob();
+            last_step = warmup + steps + latency - 1;
+          }
+        } catch (const std::exception& e) {
+          errs[r] = e.what();
+        }
+      });
+    for (auto& t : ts) t.join();
+  }
+  for (int r = 0; r < world; ++r)
+    if (!errs[r].empty()) throw std::runtime_error("rank " + std::to_string(r) + ": " + errs[r]);
+  // the last step read global batch (last_step % 2): answers in image order
+  bool ok = last_idx.size() == (size_t)G;
+  const uint8_t* b = src + (size_t)(last_step % 2) * G * ib;
+  for (int64_t i = 0; ok && i < G; ++i)
+    ok = last_idx[i] == dp::host_class_of(b + i * ib, ib) && last_prob[i] == dp::host_prob_of(b + i * ib);
+  py::dict out;
+  out["steps"] = done;
+  out["counts"] = counts;
+  out["answers_ok"] = ok;
+  return out;
+}
 
 // ------------------------------------------------------------------ group
 class DpGroupPy {
@@ -277,6 +307,212 @@ py::dict dp_host_run(py::array_t<uint8_t, py::array::c_style> images, int world,
   return out;
 }
 
+// ------------------------------------------------------------------ host fleet
+// The serving fleet (csrc/comm/fleet.h) over host workers and the rendezvous
+// host communicator: the partition rule, rebalancing after a GPU loss, the
+// weight broadcast into moved GPUs, per-query routing under concurrency and
+// exactly-once answers, all on the CPU (tests/test_fleet_cpu.py).
+// Every communicator world the fleet creates is tracked: worlds alive at the
+// same time must cover identical or disjoint device sets (two models never
+// hold communicators on one device).
+class HostFleet {
+ public:
+  HostFleet(std::vector<int> devices, int H, int W, int lanes, int delay_us, int max_per_rank, int min_shard,
+            std::map<std::string, uint32_t> seeds)
+      : H_(H), W_(W), seeds_(std::move(seeds)) {
+    dp::FleetOptions o;
+    o.max_per_rank = max_per_rank;
+    o.image_bytes = (size_t)H * W * 3;
+    o.min_shard = min_shard;
+    o.aux_bytes = 64;
+    o.timeout_ms = 5000;
+    auto wf = [this, lanes, delay_us](const std::string& m, int d, dp::Worker* rep) {
+      std::lock_guard<std::mutex> g(mu_);
+      auto it = seeds_.find(m);
+      if (it == seeds_.end()) throw std::runtime_error("HostFleet: unknown model " + m);
+      builds_.push_back({m, d, rep != nullptr});
+      // a replica starts with an empty arena: only the broadcast makes it right
+      return dp::make_host_worker(d, H_, W_, 1000, lanes, rep ? 0u : it->second, delay_us);
+    };
+    auto cf = [this](const std::vector<int>& devs) {
+      std::vector<std::unique_ptr<comm::Comm>> out;
+      auto world = std::make_shared<int>(0);
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        for (auto& w : worlds_) {
+          if (w.second.expired()) continue;
+          std::set<int> a(w.first.begin(), w.first.end()), b(devs.begin(), devs.end());
+          bool overlap = false;
+          for (int x : b) overlap |= a.count(x) > 0;
+          if (overlap && a != b) overlaps_.push_back(w.first), overlaps_.push_back(devs);
+        }
+        worlds_.emplace_back(devs, world);
+        comm_builds_.push_back(devs);
+      }
+      for (auto& c : comm::host_world((int)devs.size(), 5000)) out.push_back(std::make_unique<Tracked>(std::move(c), world));
+      return out;
+    };
+    f_ = std::make_unique<dp::Fleet>(devices, wf, cf, o);
+  }
+  void set_jobs(const std::vector<std::string>& j) {
+    py::gil_scoped_release nogil;
+    f_->set_jobs(j);
+  }
+  void load(const std::string& m) {
+    py::gil_scoped_release nogil;
+    f_->load(m);
+  }
+  void lose(int d) {
+    py::gil_scoped_release nogil;
+    f_->lose(d);
+  }
+  // new "host weights" for `model` (then load() = a hot swap, as `train`)
+  void set_seed(const std::string& m, uint32_t seed) {
+    std::lock_guard<std::mutex> g(mu_);
+    seeds_[m] = seed;
+  }
+  // abrupt: every instance on `d` starts failing (found by the next query)
+  void fail(int d) {
+    for (const auto& kv : f_->partitions())
+      if (dp::Worker* w = f_->worker(kv.first, d)) dp::host_worker_set_healthy(*w, false);
+  }
+  // queries: (model, first, count) over `images`; run by `threads` threads.
+  py::dict run(py::array_t<uint8_t, py::array::c_style> images, std::vector<std::tuple<std::string, int64_t, int64_t>> qs,
+               int threads) {
+    const size_t ib = (size_t)H_ * W_ * 3;
+    const uint8_t* src = images.data();
+    const int64_t total = images.shape(0);
+    std::vector<std::vector<int32_t>> idx(qs.size());
+    std::vector<std::vector<float>> prob(qs.size());
+    std::vector<dp::Fleet::Route> routes(qs.size());
+    std::vector<std::string> errs(qs.size());
+    {
+      py::gil_scoped_release nogil;
+      std::atomic<size_t> next{0};
+      std::vector<std::thread> ts;
+      for (int t = 0; t < std::max(1, threads); ++t)
+        ts.emplace_back([&] {
+          for (size_t q = next++; q < qs.size(); q = next++) {
+            const auto& [model, first, count] = qs[q];
+            try {
+              if (first < 0 || first + count > total) throw std::invalid_argument("query out of range");
+              idx[q].assign(count, -1);
+              prob[q].assign(count, 0.f);
+              auto stage = [&, first = first](const dp::StageCtx& c, int64_t off, int64_t n) -> const uint8_t* {
+                if (n > c.capacity) throw std::logic_error("stage: more images than the batch holds");
+                std::memcpy(c.batch, src + (size_t)(first + off) * ib, (size_t)n * ib);
+                return (const uint8_t*)c.batch;
+              };
+              routes[q] = f_->classify(model, count, stage, idx[q].data(), prob[q].data());
+            } catch (const std::exception& e) {
+              errs[q] = e.what();
+            }
+          }
+        });
+      for (auto& t : ts) t.join();
+    }
+    py::list out_idx, out_prob, out_route;
+    for (size_t q = 0; q < qs.size(); ++q) {
+      out_idx.append(py::array_t<int32_t>(idx[q].size(), idx[q].data()));
+      out_prob.append(py::array_t<float>(prob[q].size(), prob[q].data()));
+      py::dict r;
+      r["device"] = routes[q].device;
+      r["scattered"] = routes[q].scattered;
+      r["devices_used"] = routes[q].devices_used;
+      r["retries"] = routes[q].retries;
+      out_route.append(r);
+    }
+    py::dict d;
+    d["idx"] = out_idx;
+    d["prob"] = out_prob;
+    d["routes"] = out_route;
+    d["errors"] = errs;
+    return d;
+  }
+  py::dict state() {
+    py::dict d;
+    d["partitions"] = f_->partitions();
+    d["live"] = f_->live();
+    d["rebalances"] = f_->rebalances();
+    std::map<std::string, std::map<int, int64_t>> served;
+    for (const auto& kv : f_->partitions()) served[kv.first] = f_->served(kv.first);
+    d["served"] = served;
+    std::lock_guard<std::mutex> g(mu_);
+    d["comm_builds"] = comm_builds_;
+    d["overlapping_worlds"] = overlaps_;
+    py::list b;
+    for (const auto& x : builds_) b.append(py::make_tuple(std::get<0>(x), std::get<1>(x), std::get<2>(x)));
+    d["worker_builds"] = b;
+    return d;
+  }
+
+ private:
+  // a host communicator that keeps its world's liveness token alive
+  struct Tracked : comm::Comm {
+    Tracked(std::unique_ptr<comm::Comm> c, std::shared_ptr<int> t) : c_(std::move(c)), t_(std::move(t)) {}
+    int rank() const override { return c_->rank(); }
+    int size() const override { return c_->size(); }
+    std::string backend() const override { return c_->backend(); }
+    void group_start() override { c_->group_start(); }
+    void group_end() override { c_->group_end(); }
+    void send(const void* b, size_t n, int p, comm::Stream s) override { c_->send(b, n, p, s); }
+    void recv(void* b, size_t n, int p, comm::Stream s) override { c_->recv(b, n, p, s); }
+    void broadcast(const void* sb, void* rb, size_t n, int root, comm::Stream s) override {
+      c_->broadcast(sb, rb, n, root, s);
+    }
+    bool ok() override { return c_->ok(); }
+    void abort() override { c_->abort(); }
+    std::unique_ptr<comm::Comm> c_;
+    std::shared_ptr<int> t_;
+  };
+  int H_, W_;
+  std::map<std::string, uint32_t> seeds_;
+  std::unique_ptr<dp::Fleet> f_;
+  std::mutex mu_;
+  std::vector<std::pair<std::vector<int>, std::weak_ptr<int>>> worlds_;
+  std::vector<std::vector<int>> comm_builds_, overlaps_;
+  std::vector<std::tuple<std::string, int, bool>> builds_;
+};
+
+// A deliberately mis-ordered exchange on the host fake: with `bad`, both
+// ranks send before they receive (each in its own group); RCCL would hang,
+// the rendezvous fake must time out. Without it, the well-ordered exchange
+// completes and nothing is left pending.
+py::dict host_order_probe(bool bad, int timeout_ms) {
+  auto cs = comm::host_world(2, timeout_ms);
+  std::vector<uint8_t> a(64, 1), b(64, 2), ra(64, 0), rb(64, 0);
+  std::string e0, e1;
+  {
+    py::gil_scoped_release nogil;
+    std::thread t1([&] {
+      try {
+        if (bad) {
+          cs[1]->send(b.data(), 64, 0, nullptr);
+          cs[1]->recv(rb.data(), 64, 0, nullptr);
+        } else {
+          cs[1]->recv(rb.data(), 64, 0, nullptr);
+          cs[1]->send(b.data(), 64, 0, nullptr);
+        }
+      } catch (const std::exception& e) {
+        e1 = e.what();
+      }
+    });
+    try {
+      cs[0]->send(a.data(), 64, 1, nullptr);
+      cs[0]->recv(ra.data(), 64, 1, nullptr);
+    } catch (const std::exception& e) {
+      e0 = e.what();
+    }
+    t1.join();
+  }
+  py::dict d;
+  d["err0"] = e0;
+  d["err1"] = e1;
+  d["ok"] = ra == b && rb == a;
+  d["pending"] = comm::host_pending(*cs[0]);
+  return d;
+}
+
 // One-rank RCCL communicator on `device` (optionally CTA-capped) moving
 // `bytes` to itself with a grouped send/recv and a broadcast: exercises the
 // RcclComm wrapper and librccl on a one-GPU box (tests/test_dp_native_gpu.py).
@@ -333,6 +569,19 @@ class RcclLoop {
 }  // namespace
 
 void bind_dp(py::module& m) {
+  m.def("dp_partition_devices", &dp::partition_devices, py::arg("live"), py::arg("jobs"));
+  m.def("host_order_probe", &host_order_probe, py::arg("bad"), py::arg("timeout_ms") = 500);
+  py::class_<HostFleet>(m, "HostFleet")
+      .def(py::init<std::vector<int>, int, int, int, int, int, int, std::map<std::string, uint32_t>>(),
+           py::arg("devices"), py::arg("H"), py::arg("W"), py::arg("lanes"), py::arg("delay_us"),
+           py::arg("max_per_rank"), py::arg("min_shard"), py::arg("seeds"))
+      .def("set_jobs", &HostFleet::set_jobs)
+      .def("load", &HostFleet::load)
+      .def("lose", &HostFleet::lose)
+      .def("fail", &HostFleet::fail)
+      .def("set_seed", &HostFleet::set_seed)
+      .def("run", &HostFleet::run, py::arg("images"), py::arg("queries"), py::arg("threads") = 1)
+      .def("state", &HostFleet::state);
   py::class_<RcclLoop>(m, "RcclLoop")
       .def(py::init<int, int>(), py::arg("device") = 0, py::arg("max_ctas") = 0)
       .def("issue", &RcclLoop::issue, py::arg("stream"), py::arg("src"), py::arg("dst"), py::arg("bytes"),
@@ -340,25 +589,32 @@ void bind_dp(py::module& m) {
   m.def("rccl_loopback", &rccl_loopback, py::arg("device") = 0, py::arg("bytes") = 1 << 20, py::arg("max_ctas") = 0);
   m.def("rccl_unique_id", []() { return py::bytes(comm::rccl_unique_id()); });
   m.def("dp_shard_counts", &dp::shard_counts);
+  m.def("dp_weighted_counts", &dp::weighted_counts, py::arg("per_rank"), py::arg("world"), py::arg("coord_weight"));
+  m.def("dp_host_bench", &dp_host_bench, py::arg("pool"), py::arg("world"), py::arg("per_rank"),
+        py::arg("coord_weight") = 1.0, py::arg("input_mode") = "scatter", py::arg("lanes") = 2, py::arg("prime") = 3,
+        py::arg("warmup") = 2, py::arg("steps") = 5, py::arg("latency") = 3);
   m.def("dp_host_run", &dp_host_run, py::arg("images"), py::arg("world"), py::arg("max_per_rank"),
         py::arg("mode") = "group", py::arg("scatter") = true, py::arg("fail_member") = -1,
         py::arg("fail_after") = 0, py::arg("abrupt") = false, py::arg("pipelined") = true, py::arg("slots") = 2);
   py::class_<DpRunner>(m, "DpRunner")
       .def(py::init([](Engine* e, int world, int rank, py::bytes id_in, py::bytes id_out, int max_per_rank,
-                       bool scatter, int image_size, bool use_graph, int timeout_ms, int lanes, int slots) {
+                       bool scatter, int image_size, bool use_graph, int timeout_ms, int lanes, int slots,
+                       double coord_weight, std::vector<int> counts) {
              return new DpRunner(e, world, rank, std::string(id_in), std::string(id_out), max_per_rank, scatter,
-                                 image_size, use_graph, timeout_ms, lanes, slots);
+                                 image_size, use_graph, timeout_ms, lanes, slots, coord_weight, counts);
            }),
            py::arg("engine"), py::arg("world"), py::arg("rank"), py::arg("id_in"), py::arg("id_out"),
            py::arg("max_per_rank"), py::arg("scatter") = true, py::arg("image_size") = 224,
            py::arg("use_graph") = true, py::arg("timeout_ms") = -1, py::arg("lanes") = 1, py::arg("slots") = 0,
-           py::keep_alive<1, 2>())
+           py::arg("coord_weight") = 1.0, py::arg("counts") = std::vector<int>{}, py::keep_alive<1, 2>())
       .def("run", &DpRunner::run, py::arg("pool"), py::arg("pool_images"), py::arg("first"), py::arg("n"),
            py::arg("pipelined") = true)
       .def("last_results", &DpRunner::last_results)
       .def("compute_stream", &DpRunner::compute_stream)
       .def("sync", &DpRunner::sync)
-      .def("stage", &DpRunner::stage, py::arg("src"), py::arg("dst"), py::arg("images"));
+      .def("stage", &DpRunner::stage, py::arg("src"), py::arg("dst"))
+      .def_property_readonly("counts", [](const DpRunner& r) { return r.r_->counts(); })
+      .def_property_readonly("max_per_rank", [](const DpRunner& r) { return r.r_->max_per_rank(); });
   py::class_<DpGroupPy>(m, "DpGroup")
       .def(py::init([](std::vector<Engine*> engines, int max_per_rank, int image_size, bool use_graph,
                        int timeout_ms) { return new DpGroupPy(engines, max_per_rank, image_size, use_graph, timeout_ms); }),

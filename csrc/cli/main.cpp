@@ -289,8 +289,20 @@ void handle_line(Node& n, const std::string& line) {
       out_line("staged: " + (s.empty() ? std::string("none") : s) + " in " +
                (n.member->executor() ? n.member->executor()->blob_location() : std::string("-")));
     } else if (c == "predict") {
-      if (t.size() != 1) return err_line("Invalid predict command!");
-      n.call_leader(L_PREDICT, "", 30000);
+      // predict                 start / resume the jobs (reference: no arguments)
+      // predict <shard> ...     the jobs classify these labelled SDFS u8 shards
+      //                         (resident in the replica holders' HBM) instead
+      // predict dataset         back to the dataset's per-label JPEGs
+      if (t.size() == 1) {
+        n.call_leader(L_PREDICT, "", 30000);
+      } else {
+        Writer w;
+        const bool dataset = t.size() == 2 && t[1] == "dataset";
+        w.u32(dataset ? 0u : (uint32_t)(t.size() - 1));
+        if (!dataset)
+          for (size_t i = 1; i < t.size(); ++i) w.str(t[i]);
+        n.call_leader(L_PREDICT, w.data(), 30000);
+      }
     } else if (c == "jobs") {
       if (t.size() != 1) return err_line("Invalid jobs command!");
       Reader r(n.call_leader(L_JOBS, "", 30000));
@@ -325,12 +337,13 @@ void handle_line(Node& n, const std::string& line) {
         out_line("Job " + std::to_string(i + 1) + ":\n" + id_rows_table(j.assigned));
       }
     } else if (c == "fault") {
-      // fault drop <p> | pause | resume | partition <addr> | heal
+      // fault drop <p> | pause | resume | partition <addr> | heal | gpu <device>
       if (t.size() >= 3 && t[1] == "drop") n.ms->set_drop_rate(std::stod(t[2]));
       else if (t.size() == 2 && t[1] == "pause") n.ms->set_paused(true);
       else if (t.size() == 2 && t[1] == "resume") n.ms->set_paused(false);
       else if (t.size() == 3 && t[1] == "partition") n.ms->partition(t[2]);
       else if (t.size() == 2 && t[1] == "heal") n.ms->heal();
+      else if (t.size() == 3 && t[1] == "gpu" && n.member->executor()) n.member->executor()->lose_device(std::stoi(t[2]));
       else return err_line("Invalid fault command!");
       out_line("ok");
     } else if (c == "info") {
@@ -338,6 +351,7 @@ void handle_line(Node& n, const std::string& line) {
                (n.member->executor() ? n.member->executor()->backend() : std::string("none")) + " sent " +
                std::to_string(n.ms->sent()) + " received " + std::to_string(n.ms->received()));
       if (Executor* ex = n.member->executor()) {
+        out_line("placement " + ex->placement());
         const CacheStats cs = ex->cache_stats();
         out_line("cache hits " + std::to_string(cs.hits) + " misses " + std::to_string(cs.misses) + " staged " +
                  std::to_string(cs.staged) + " evictions " + std::to_string(cs.evictions) + " entries " +
@@ -399,8 +413,16 @@ int run_node(const Args& a) {
       for (int i = 0; i < std::max(1, a.geti("gpus", 1)); ++i) devs.push_back(a.geti("device", 0) + i);
     }
     ex = make_executor(a.get("executor", "auto"), devs, a.geti("max-batch", 64),
-                       (size_t)a.geti("hbm-cache-mb", 4096) << 20, a.geti("min-shard", 8));
-    if (ex) load_models(ex.get(), a.get("models", ""));
+                       (size_t)a.geti("hbm-cache-mb", 4096) << 20, a.geti("min-shard", 32), a.geti("lanes", 2));
+    if (ex) {
+      // the GPUs are split between the jobs in this order (first floor(n/2)
+      // to the first job, src/services.rs:199-211)
+      std::vector<std::string> jobs;
+      for (const auto& m : split(a.get("jobs", "resnet18,alexnet"), ','))
+        if (!trim(m).empty()) jobs.push_back(trim(m));
+      ex->set_jobs(jobs);
+      load_models(ex.get(), a.get("models", ""));
+    }
   } catch (const std::exception& e) {
     err_line(std::string("executor unavailable: ") + e.what());
   }
@@ -429,6 +451,8 @@ int run_node(const Args& a) {
     lc.adaptive_window = a.geti("adaptive-window", 0);
     lc.job_limit = a.geti("job-limit", 0);
     lc.print_predictions = !a.has("quiet-predictions");
+    lc.new_conn_per_query = a.has("new-conn-per-query");
+    lc.max_attempts = a.geti("max-attempts", 3);
     lc.job_models.clear();
     for (const auto& m : split(a.get("jobs", "resnet18,alexnet"), ','))
       if (!trim(m).empty()) lc.job_models.push_back(trim(m));
@@ -493,10 +517,11 @@ int main(int argc, char** argv) {
   if (argc >= 2 && (std::string(argv[1]) == "--help" || std::string(argv[1]) == "-h")) {
     std::cout << "usage: dmlc-node [--host H] [--port P] [--leaders h:p,...] [--workdir D] [--dataset D]\n"
                  "                 [--labels F] [--models name=path,...] [--executor auto|gpu|cpu] [--device N]\n"
-                 "                 [--gpus N | --devices a,b,...] [--min-shard 8]\n"
+                 "                 [--gpus N | --devices a,b,...] [--min-shard 32] [--lanes 2]\n"
                  "                 [--rf 4] [--ping-ms 1000] [--fail-ms 3000] [--bg-ms 3000]\n"
                  "                 [--query-interval-ms 500] [--adaptive-window 0] [--query-batch 1] [--jobs resnet18,alexnet]\n"
-                 "                 [--join h:p] [--daemon] [--stay] [--quiet-predictions]\n"
+                 "                 [--join h:p] [--daemon] [--stay] [--quiet-predictions] [--new-conn-per-query]\n"
+                 "                 [--max-attempts 3]\n"
                  "                 [--max-batch 64] [--hbm-cache-mb 4096] [--prefetch]\n"
                  "       dmlc-node selftest\n"
                  "       dmlc-node classify --model M --weights W.ot --labels L --image I.JPEG [--executor cpu|gpu]\n";

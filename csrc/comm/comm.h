@@ -15,10 +15,12 @@
 //     stream; one communicator per rank, built either per process from a
 //     unique id (one process per GPU) or for all local GPUs of one process
 //     (ncclCommInitAll).
-//   * HostComm  (host_comm.cpp): an in-process fake over host memory with the
-//     same grouping semantics, plus fault injection (a rank can be declared
-//     lost). It runs the data-parallel coordinator's shard/gather/recovery
-//     logic on CPU in tests (tests/test_dp_native_cpu.py).
+//   * HostComm  (host_comm.cpp): an in-process fake over host memory with
+//     RCCL's rendezvous, per-pair FIFO and grouping semantics, plus fault
+//     injection (a rank can be declared lost). It runs the data-parallel
+//     coordinator's shard/gather/recovery logic and the serving fleet's
+//     partitions on CPU in tests (tests/test_dp_native_cpu.py,
+//     tests/test_fleet_cpu.py).
 #pragma once
 #include <cstddef>
 #include <cstdint>
@@ -97,9 +99,12 @@ class HostWorld;  // shared mailbox state of one fake communicator
 // may be driven from one thread per rank or from one thread for all ranks.
 // recv gives up after `timeout_ms` (a hang would otherwise stall the test).
 std::vector<std::unique_ptr<Comm>> host_world(int n, int timeout_ms = 10000);
-// Fault injection on a host communicator: every later operation of `rank`
-// throws, and peers' receives from it throw CommError.
+// Fault injection on a host communicator: every pending and later operation
+// that involves `rank` fails with CommError.
 void host_kill(Comm& any_member_of_world, int rank);
+// Operations posted on the fake world but not matched yet (0 after every
+// well-formed exchange: nothing is buffered).
+size_t host_pending(Comm& any_member_of_world);
 
 }  // namespace comm
 }  // namespace dmlc

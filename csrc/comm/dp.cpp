@@ -1,7 +1,9 @@
 #include "dp.h"
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <mutex>
 #include <cstdlib>
 #include <cstring>
 #include <thread>
@@ -14,7 +16,12 @@ namespace {
 
 class HostWorker : public Worker {
  public:
-  HostWorker(int device, int H, int W, int classes) : device_(device), bytes_((size_t)H * W * 3), classes_(classes) {}
+  HostWorker(int device, int H, int W, int classes, int lanes, uint32_t seed, int delay_us)
+      : device_(device), bytes_((size_t)H * W * 3), classes_(classes), lanes_(std::max(1, lanes)),
+        delay_us_(delay_us), busy_(lanes_) {
+    for (auto& b : busy_) b = false;
+    std::memcpy(arena_, &seed, 4);
+  }
   ~HostWorker() override {
     for (void* p : live_) std::free(p);
   }
@@ -30,25 +37,38 @@ class HostWorker : public Worker {
   bool query(int) override { return true; }
   void sync(int) override {}
   void sync_all() override {}
-  void classify(const uint8_t* images, int B, int32_t* idx, float* prob, int) override {
+  int lanes() const override { return lanes_; }
+  void classify(const uint8_t* images, int B, int32_t* idx, float* prob, int lane) override {
+    if (!healthy_) throw comm::CommError("host worker " + std::to_string(device_) + ": device lost");
+    if (lane < 0 || lane >= lanes_) throw std::invalid_argument("host worker: no such lane");
+    // a lane runs one forward at a time (a stream): concurrent use is a bug
+    if (busy_[lane].exchange(true)) throw std::logic_error("host worker: lane used concurrently");
+    uint32_t w;
+    std::memcpy(&w, arena_, 4);
+    if (delay_us_ > 0) std::this_thread::sleep_for(std::chrono::microseconds(delay_us_));
     for (int b = 0; b < B; ++b) {
       const uint8_t* img = images + (size_t)b * bytes_;
-      idx[b] = host_class_of(img, bytes_, classes_);
+      idx[b] = (int32_t)(((uint64_t)host_class_of(img, bytes_, 1 << 30) + w) % (uint64_t)classes_);
       prob[b] = host_prob_of(img);
     }
+    busy_[lane] = false;
   }
   void copy_d2h(void* dst, const void* src, size_t bytes, int) override { std::memmove(dst, src, bytes); }
   void copy(void* dst, const void* src, size_t bytes, int) override { std::memmove(dst, src, bytes); }
   bool healthy() override { return healthy_; }
-  bool healthy_ = true;
+  void* weight_arena() override { return arena_; }
+  size_t weight_bytes() const override { return sizeof(arena_); }
+  std::atomic<bool> healthy_{true};
 
  private:
   void* track(void* p) {
     if (!p) throw std::bad_alloc();
+    std::lock_guard<std::mutex> g(mu_);
     live_.push_back(p);
     return p;
   }
   void untrack(void* p) {
+    std::lock_guard<std::mutex> g(mu_);
     auto it = std::find(live_.begin(), live_.end(), p);
     if (it != live_.end()) {
       std::free(p);
@@ -57,15 +77,19 @@ class HostWorker : public Worker {
   }
   int device_;
   size_t bytes_;
-  int classes_;
-  int n_events_ = 0;
+  int classes_, lanes_, delay_us_;
+  std::vector<std::atomic<bool>> busy_;
+  uint8_t arena_[16] = {};
+  std::atomic<int> n_events_{0};
+  std::mutex mu_;
   std::vector<void*> live_;
 };
 
 }  // namespace
 
-std::unique_ptr<Worker> make_host_worker(int device, int H, int W, int classes) {
-  return std::make_unique<HostWorker>(device, H, W, classes);
+std::unique_ptr<Worker> make_host_worker(int device, int H, int W, int classes, int lanes, uint32_t seed,
+                                         int delay_us) {
+  return std::make_unique<HostWorker>(device, H, W, classes, lanes, seed, delay_us);
 }
 
 void host_worker_set_healthy(Worker& w, bool healthy) {
@@ -107,8 +131,12 @@ Rank::Rank(Worker* w, int max_per_rank, size_t image_bytes, bool scatter, int sl
 }
 
 Rank::~Rank() {
-  w_->activate();
-  w_->sync_all();
+  // teardown never throws: the device may be the lost one
+  try {
+    w_->activate();
+  } catch (...) {
+  }
+  w_->sync_all_noexcept();
   for (void* p : inbuf_)
     if (p) w_->dealloc(p);
   for (void* p : ans_)
@@ -360,7 +388,10 @@ Group::Group(std::vector<Worker*> workers, CommFactory make_comms, int max_per_r
 }
 
 Group::~Group() {
-  for (auto& r : ranks_) r->worker()->sync_all();
+  // a lost member is skipped (its device may not answer), and nothing here
+  // throws: the group is torn down after a GPU loss (fleet rebalance, hot swap)
+  for (size_t i = 0; i < ranks_.size(); ++i)
+    if (!lost_[i]) ranks_[i]->worker()->sync_all_noexcept();
   ranks_.clear();
   cin_.clear();
   cout_.clear();
@@ -403,6 +434,7 @@ void Group::kill_now(int m) {
 Group::Stats Group::classify(const uint8_t* src, int64_t n, int32_t* idx, float* prob, int src_event,
                              int32_t* commit_count) {
   Stats st;
+  st.per_worker.assign(workers_.size(), 0);
   int64_t committed = 0;  // answers [0, committed) are final
   int64_t issued = 0;     // images whose step was planned (posted) in the current attempt
   while (committed < n) {
@@ -430,7 +462,9 @@ Group::Stats Group::classify(const uint8_t* src, int64_t n, int32_t* idx, float*
       p.step = step;
       const int64_t start = base + step * G;
       const int64_t nstep = std::min<int64_t>(G, n - start);
-      const int64_t want = std::max<int64_t>((nstep + min_per_rank_ - 1) / min_per_rank_, (nstep + max_ - 1) / max_);
+      // as many ranks as can each take min_per_rank images (at least enough
+      // to stay under max_ per rank)
+      const int64_t want = std::max<int64_t>(nstep / min_per_rank_, (nstep + max_ - 1) / max_);
       const int used = (int)std::min<int64_t>(world, std::max<int64_t>(1, want));
       p.counts = shard_counts(nstep, used, max_);
       p.counts.resize(world, 0);
@@ -446,6 +480,12 @@ Group::Stats Group::classify(const uint8_t* src, int64_t n, int32_t* idx, float*
       std::memcpy(prob + start, pr, (size_t)total * 4);
       if (commit_count)
         for (int64_t k = 0; k < total; ++k) ++commit_count[start + k];
+      int used = 0;
+      for (size_t i = 0; i < p.counts.size() && i < members_.size(); ++i) {
+        st.per_worker[members_[i]] += p.counts[i];
+        used += p.counts[i] > 0;
+      }
+      st.ranks_used = std::max(st.ranks_used, used);
       committed = start + total;
       ++st.steps;
     };

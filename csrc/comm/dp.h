@@ -66,12 +66,31 @@ class Worker {
   virtual void copy(void* dst, const void* src, size_t bytes, int stream_id) = 0;
   // False once the device reported an error (a lost GPU); never blocks.
   virtual bool healthy() { return true; }
+  // The model's packed weights in worker memory (lane 0's): the fleet fills
+  // a new replica's arena with an RCCL broadcast from a live instance of the
+  // same model, then calls weights_updated() so the other lanes copy it.
+  virtual void* weight_arena() { return nullptr; }
+  virtual size_t weight_bytes() const { return 0; }
+  virtual void weights_updated() {}
+  // Never throws: used on teardown paths, where the device may be lost.
+  virtual void sync_all_noexcept() noexcept {
+    try {
+      sync_all();
+    } catch (...) {
+    }
+  }
 };
 
 // Host stand-in: plain memory, synchronous "streams" (events are no-ops), and
-// a deterministic classifier: class = (sum of the image's bytes) % classes,
-// prob = (first byte + 1) / 257.
-std::unique_ptr<Worker> make_host_worker(int device, int H, int W, int classes = 1000);
+// a deterministic classifier: class = (sum of the image's bytes + w) %
+// classes, prob = (first byte + 1) / 257, where w is the u32 at the start of
+// its weight arena (`seed` for a worker built from "host weights"; 0 for a
+// replica until the fleet broadcasts the arena into it).
+// lanes: concurrent classify() calls it accepts (one per lane); delay_us:
+// time one classify() takes (so concurrent queries overlap in tests).
+// An unhealthy host worker's classify() throws CommError (a lost GPU).
+std::unique_ptr<Worker> make_host_worker(int device, int H, int W, int classes = 1000, int lanes = 1,
+                                         uint32_t seed = 0, int delay_us = 0);
 // Test hook: a host worker that reports itself unhealthy (a lost GPU).
 void host_worker_set_healthy(Worker& w, bool healthy);
 // The HIP engine on its device (csrc/comm/hip_worker.cpp): images are u8
@@ -81,6 +100,12 @@ void host_worker_set_healthy(Worker& w, bool healthy);
 // `engine`), owned by the caller like `engine`: lanes() == 1 + more.size().
 std::unique_ptr<Worker> make_hip_worker(Engine* engine, int H, int W, bool use_graph = true,
                                         std::vector<Engine*> more = {});
+// The same, owning its engines (engines[0] = lane 0): the serving fleet's
+// per-(model, GPU) instances.
+std::unique_ptr<Worker> make_owned_hip_worker(std::vector<std::unique_ptr<Engine>> engines, int H, int W,
+                                              bool use_graph = true);
+// Lane `lane`'s engine of a HIP worker (throws for other workers).
+Engine* hip_worker_engine(Worker& w, int lane = 0);
 int host_class_of(const uint8_t* img, size_t bytes, int classes = 1000);
 float host_prob_of(const uint8_t* img);
 
@@ -180,6 +205,8 @@ class Group {
     int64_t images = 0, steps = 0;
     int recoveries = 0;
     int64_t redone_images = 0;  // images classified again after a loss
+    std::vector<int64_t> per_worker;  // images answered by each worker (index into workers)
+    int ranks_used = 0;               // most ranks one step used
   };
   // Classify n images stored contiguously at `src` (coordinator memory),
   // answers in input order. `src_event`: coordinator event after which src

@@ -106,6 +106,15 @@ class HipWorker : public Worker {
   void copy(void* dst, const void* src, size_t bytes, int sid) override {
     DMLC_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, s_[sid]));
   }
+  void* weight_arena() override { return e_[0]->weight_arena(); }
+  size_t weight_bytes() const override { return e_[0]->weight_bytes(); }
+  void weights_updated() override {
+    for (size_t l = 1; l < e_.size(); ++l) e_[l]->copy_weights_from(*e_[0]);
+  }
+  Engine* engine(int lane) const { return e_.at(lane); }
+  // engines this worker owns (make_owned_hip_worker), destroyed after it
+  std::vector<std::unique_ptr<Engine>> owned_;
+
   bool healthy() override {
     for (auto s : s_) {
       if (!s) continue;
@@ -127,6 +136,22 @@ class HipWorker : public Worker {
 
 std::unique_ptr<Worker> make_hip_worker(Engine* engine, int H, int W, bool use_graph, std::vector<Engine*> more) {
   return std::make_unique<HipWorker>(engine, H, W, use_graph, std::move(more));
+}
+
+std::unique_ptr<Worker> make_owned_hip_worker(std::vector<std::unique_ptr<Engine>> engines, int H, int W,
+                                              bool use_graph) {
+  if (engines.empty()) throw std::invalid_argument("make_owned_hip_worker: no engines");
+  std::vector<Engine*> more;
+  for (size_t l = 1; l < engines.size(); ++l) more.push_back(engines[l].get());
+  auto w = std::make_unique<HipWorker>(engines[0].get(), H, W, use_graph, std::move(more));
+  w->owned_ = std::move(engines);
+  return w;
+}
+
+Engine* hip_worker_engine(Worker& w, int lane) {
+  auto* h = dynamic_cast<HipWorker*>(&w);
+  if (!h) throw std::invalid_argument("hip_worker_engine: not a HIP worker");
+  return h->engine(lane);
 }
 
 }  // namespace dp

@@ -1,12 +1,26 @@
 // In-process fake communicator (host memory): the data-parallel coordinator's
-// shard / gather / rank-loss logic runs on it in CPU tests. Semantics match
-// what the coordinator relies on from RCCL:
-//   * point-to-point messages between a (src, dst) pair are delivered in the
-//     order they were posted;
-//   * a group posts all of its sends before it blocks on any receive, so one
-//     thread may drive several ranks inside one group, and a rank may send
-//     and receive in the same group without deadlock;
-//   * a receive from a lost peer (host_kill) fails with CommError.
+// shard / gather / rank-loss logic and the serving fleet's partition logic
+// run on it in CPU tests. It models what RCCL point-to-point does, not what
+// is convenient:
+//   * rendezvous: a send completes only when the matching receive has been
+//     posted (the bytes are copied straight from the sender's buffer into the
+//     receiver's); nothing is buffered, so an issue order that would leave
+//     two RCCL ranks each waiting on the other (rank 0 sends to 1 while 1
+//     sends to 0, each before receiving) times out here too instead of
+//     passing;
+//   * FIFO per (src, dst) pair and communicator: the k-th send a -> b meets
+//     the k-th receive at b from a, whichever threads post them, and the sizes
+//     must agree;
+//   * groups: every operation posted between a thread's outermost
+//     group_start and group_end is posted at once when the group ends, and
+//     group_end returns when all of them have completed (the host stand-in
+//     for "the stream reached the end of the group's kernel"). One thread may
+//     drive several ranks inside one group, and a rank may send and receive
+//     in the same group;
+//   * a lost peer (host_kill) or an abort fails every pending and later
+//     operation that involves it with CommError; a timed-out group withdraws
+//     its still-unmatched operations before it throws, so no later match
+//     touches a buffer the caller has given up on.
 #include <chrono>
 #include <condition_variable>
 #include <cstring>
@@ -19,47 +33,64 @@
 namespace dmlc {
 namespace comm {
 
+namespace {
+// One posted operation; owned by the group_end call that posted it (its
+// stack frame outlives the op's presence in the world's queues).
+struct Op {
+  bool is_send = false;
+  int self = 0, peer = 0;
+  const void* sbuf = nullptr;
+  void* rbuf = nullptr;
+  size_t bytes = 0;
+  bool done = false;
+  std::string error;  // set with done = true on failure
+};
+}  // namespace
+
 class HostWorld {
  public:
   HostWorld(int n, int timeout_ms) : n_(n), timeout_ms_(timeout_ms), dead_(n, false) {}
 
-  void put(int src, int dst, const void* buf, size_t bytes) {
-    std::lock_guard<std::mutex> g(mu_);
-    if (aborted_ || dead_[src]) throw CommError("host comm: rank " + std::to_string(src) + " is lost");
-    auto& q = box_[{src, dst}];
-    q.emplace_back((const uint8_t*)buf, (const uint8_t*)buf + bytes);
-    cv_.notify_all();
-  }
-
-  void take(int src, int dst, void* buf, size_t bytes) {
+  // Post every op (matching what it can), then wait for all of them.
+  // Throws CommError on failure or timeout (after withdrawing unmatched ops).
+  void run(std::vector<Op*>& ops) {
     std::unique_lock<std::mutex> g(mu_);
-    auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms_);
+    for (Op* o : ops) post(o);
+    const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms_);
     for (;;) {
-      if (aborted_ || dead_[dst]) throw CommError("host comm: rank " + std::to_string(dst) + " is lost");
-      auto it = box_.find({src, dst});
-      if (it != box_.end() && !it->second.empty()) {
-        auto& m = it->second.front();
-        if (m.size() != bytes)
-          throw CommError("host comm: size mismatch " + std::to_string(m.size()) + " vs " + std::to_string(bytes) +
-                          " from rank " + std::to_string(src));
-        if (bytes) std::memcpy(buf, m.data(), bytes);
-        it->second.pop_front();
-        return;
+      bool all = true;
+      for (Op* o : ops) all &= o->done;
+      if (all) break;
+      if (cv_.wait_until(g, deadline) == std::cv_status::timeout) {
+        bool all2 = true;
+        for (Op* o : ops) all2 &= o->done;
+        if (all2) break;
+        for (Op* o : ops)
+          if (!o->done) {
+            withdraw(o);
+            o->done = true;
+            o->error = std::string("host comm: ") + (o->is_send ? "send to " : "recv from ") +
+                       std::to_string(o->peer) + " timed out (no matching " + (o->is_send ? "recv" : "send") +
+                       " posted)";
+          }
+        break;
       }
-      if (dead_[src]) throw CommError("host comm: peer " + std::to_string(src) + " is lost");
-      if (cv_.wait_until(g, deadline) == std::cv_status::timeout)
-        throw CommError("host comm: recv from " + std::to_string(src) + " timed out");
     }
+    for (Op* o : ops)
+      if (!o->error.empty()) throw CommError(o->error);
   }
 
   void kill(int r) {
     std::lock_guard<std::mutex> g(mu_);
     dead_.at(r) = true;
+    fail_where([&](const Op* o) { return o->self == r || o->peer == r; },
+               "host comm: rank " + std::to_string(r) + " is lost");
     cv_.notify_all();
   }
   void abort_all() {
     std::lock_guard<std::mutex> g(mu_);
     aborted_ = true;
+    fail_where([](const Op*) { return true; }, "host comm: communicator aborted");
     cv_.notify_all();
   }
   bool healthy(int r) {
@@ -70,36 +101,109 @@ class HostWorld {
     return true;
   }
   int size() const { return n_; }
+  // operations posted but not matched yet (tests: nothing may be left over)
+  size_t pending() {
+    std::lock_guard<std::mutex> g(mu_);
+    size_t k = 0;
+    for (auto& kv : sends_) k += kv.second.size();
+    for (auto& kv : recvs_) k += kv.second.size();
+    return k;
+  }
 
  private:
+  using Key = std::pair<int, int>;  // (src, dst)
+  void post(Op* o) {
+    if (aborted_) return fail(o, "host comm: communicator aborted");
+    if (dead_[o->self] || dead_[o->peer])
+      return fail(o, "host comm: rank " + std::to_string(dead_[o->self] ? o->self : o->peer) + " is lost");
+    const Key k = o->is_send ? Key{o->self, o->peer} : Key{o->peer, o->self};
+    auto& mine = o->is_send ? sends_[k] : recvs_[k];
+    auto& theirs = o->is_send ? recvs_[k] : sends_[k];
+    if (!theirs.empty() && mine.empty()) {
+      Op* other = theirs.front();
+      theirs.pop_front();
+      Op* s = o->is_send ? o : other;
+      Op* r = o->is_send ? other : o;
+      if (s->bytes != r->bytes) {
+        const std::string e = "host comm: size mismatch " + std::to_string(s->bytes) + " vs " +
+                              std::to_string(r->bytes) + " from rank " + std::to_string(s->self) + " to " +
+                              std::to_string(r->self);
+        fail(s, e);
+        fail(r, e);
+        return;
+      }
+      if (s->bytes) std::memcpy(r->rbuf, s->sbuf, s->bytes);
+      s->done = r->done = true;
+      cv_.notify_all();
+      return;
+    }
+    mine.push_back(o);
+  }
+  void fail(Op* o, const std::string& e) {
+    o->done = true;
+    o->error = e;
+    cv_.notify_all();
+  }
+  void withdraw(Op* o) {
+    for (auto* m : {&sends_, &recvs_})
+      for (auto& kv : *m) {
+        auto& q = kv.second;
+        for (auto it = q.begin(); it != q.end(); ++it)
+          if (*it == o) {
+            q.erase(it);
+            return;
+          }
+      }
+  }
+  template <class Pred>
+  void fail_where(Pred p, const std::string& e) {
+    for (auto* m : {&sends_, &recvs_})
+      for (auto& kv : *m) {
+        auto& q = kv.second;
+        for (auto it = q.begin(); it != q.end();) {
+          if (p(*it)) {
+            fail(*it, e);
+            it = q.erase(it);
+          } else {
+            ++it;
+          }
+        }
+      }
+  }
+
   int n_, timeout_ms_;
   std::mutex mu_;
   std::condition_variable cv_;
-  std::map<std::pair<int, int>, std::deque<std::vector<uint8_t>>> box_;
+  std::map<Key, std::deque<Op*>> sends_, recvs_;  // posted, unmatched, FIFO per pair
   std::vector<bool> dead_;
   bool aborted_ = false;
 };
 
 namespace {
 
-struct PendingOp {
+struct Pending {
   HostWorld* world;
-  bool is_send;
-  int self, peer;
-  const void* sbuf;
-  void* rbuf;
-  size_t bytes;
+  Op op;
 };
 
 // Thread-wide group state, like RCCL's.
 thread_local int t_depth = 0;
-thread_local std::vector<PendingOp> t_ops;
+thread_local std::vector<Pending> t_ops;
 
-void run_ops(std::vector<PendingOp>& ops) {
-  for (auto& o : ops)
-    if (o.is_send) o.world->put(o.self, o.peer, o.sbuf, o.bytes);
-  for (auto& o : ops)
-    if (!o.is_send) o.world->take(o.peer, o.self, o.rbuf, o.bytes);
+void run_ops(std::vector<Pending>& ops) {
+  // one HostWorld::run per world, all posted before any waits: a group may
+  // span several communicators (RCCL groups do), so post everything first.
+  std::map<HostWorld*, std::vector<Op*>> by_world;
+  for (auto& p : ops) by_world[p.world].push_back(&p.op);
+  if (by_world.empty()) return;
+  if (by_world.size() == 1) {
+    by_world.begin()->first->run(by_world.begin()->second);
+    return;
+  }
+  // several worlds: run them one after another would deadlock if a peer's
+  // matching group posts them in another order; the protocols here never mix
+  // communicators in one group, so refuse instead of guessing.
+  throw std::logic_error("host comm: a group may not span several communicators");
 }
 
 class HostComm : public Comm {
@@ -113,15 +217,26 @@ class HostComm : public Comm {
   void group_end() override {
     if (t_depth <= 0) throw std::logic_error("host comm: group_end without group_start");
     if (--t_depth > 0) return;
-    std::vector<PendingOp> ops;
+    std::vector<Pending> ops;
     ops.swap(t_ops);
     run_ops(ops);
   }
   void send(const void* buf, size_t bytes, int peer, Stream) override {
-    post({w_.get(), true, rank_, check_peer(peer), buf, nullptr, bytes});
+    Op o;
+    o.is_send = true;
+    o.self = rank_;
+    o.peer = check_peer(peer);
+    o.sbuf = buf;
+    o.bytes = bytes;
+    post(o);
   }
   void recv(void* buf, size_t bytes, int peer, Stream) override {
-    post({w_.get(), false, rank_, check_peer(peer), nullptr, buf, bytes});
+    Op o;
+    o.self = rank_;
+    o.peer = check_peer(peer);
+    o.rbuf = buf;
+    o.bytes = bytes;
+    post(o);
   }
   void broadcast(const void* sendbuf, void* recvbuf, size_t bytes, int root, Stream s) override {
     group_start();
@@ -144,11 +259,11 @@ class HostComm : public Comm {
     if (p < 0 || p >= size() || p == rank_) throw std::invalid_argument("host comm: bad peer " + std::to_string(p));
     return p;
   }
-  void post(PendingOp op) {
+  void post(const Op& op) {
     if (t_depth > 0) {
-      t_ops.push_back(op);
+      t_ops.push_back({w_.get(), op});
     } else {
-      std::vector<PendingOp> one{op};
+      std::vector<Pending> one{{w_.get(), op}};
       run_ops(one);
     }
   }
@@ -170,6 +285,12 @@ void host_kill(Comm& c, int rank) {
   auto* h = dynamic_cast<HostComm*>(&c);
   if (!h) throw std::invalid_argument("host_kill: not a host communicator");
   h->world()->kill(rank);
+}
+
+size_t host_pending(Comm& c) {
+  auto* h = dynamic_cast<HostComm*>(&c);
+  if (!h) throw std::invalid_argument("host_pending: not a host communicator");
+  return h->world()->pending();
 }
 
 }  // namespace comm

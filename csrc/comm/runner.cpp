@@ -1,0 +1,110 @@
+#include "runner.h"
+
+#include <cmath>
+#include <numeric>
+#include <stdexcept>
+
+namespace dmlc {
+namespace dp {
+
+std::vector<int> weighted_counts(int per_rank, int world, double coord_weight) {
+  if (world < 1 || per_rank < 1) throw std::invalid_argument("weighted_counts: need world >= 1 and per_rank >= 1");
+  if (!(coord_weight > 0.0) || coord_weight > (double)world)
+    throw std::invalid_argument("weighted_counts: coord_weight must be in (0, world]");
+  const int64_t total = (int64_t)per_rank * world;
+  if (world == 1) return {per_rank};
+  const int c0 = std::max(1, std::min<int>((int)std::lround(per_rank * coord_weight), (int)total - (world - 1)));
+  std::vector<int> c(world);
+  c[0] = c0;
+  const int64_t rest = total - c0;
+  for (int r = 1; r < world; ++r) c[r] = (int)(rest / (world - 1));
+  for (int r = 1; r <= (int)(rest % (world - 1)); ++r) ++c[r];
+  return c;
+}
+
+Runner::Runner(std::unique_ptr<Worker> w, std::unique_ptr<Comm> in, std::unique_ptr<Comm> out, int world, int rank,
+               std::vector<int> counts, bool scatter, size_t image_bytes, int timeout_ms, int slots)
+    : w_(std::move(w)), in_(std::move(in)), out_(std::move(out)), world_(world), rank_(rank),
+      counts_(std::move(counts)), scatter_(scatter), ib_(image_bytes), timeout_ms_(timeout_ms) {
+  if ((int)counts_.size() != world_) throw std::invalid_argument("dp::Runner: one count per rank");
+  max_ = 0;
+  for (int c : counts_) {
+    if (c < 0) throw std::invalid_argument("dp::Runner: negative count");
+    max_ = std::max(max_, c);
+  }
+  if (max_ < 1) throw std::invalid_argument("dp::Runner: empty step");
+  // Steps in flight (slots). Step i reuses slot i - slots, so its forward
+  // waits for that step's answers to have left; with slots = 2 that was the
+  // step just before on the same lane, and the answer copy's latency sat
+  // between a lane's consecutive forwards (bench: 268k vs 276k img/s with 4
+  // slots, the bare two-lane loop 276.7k: tools/pipeline_probe.py).
+  if (slots <= 0) slots = 2 * std::max(2, w_->lanes());
+  r_ = std::make_unique<Rank>(w_.get(), max_, ib_, scatter_, slots);
+  if (world_ > 1) {
+    if (!in_ || !out_ || in_->size() != world_ || in_->rank() != rank_)
+      throw std::invalid_argument("dp::Runner: communicators do not match world/rank");
+    r_->attach(in_.get(), out_.get());
+  } else {
+    r_->attach(nullptr, nullptr);
+  }
+}
+
+Runner::~Runner() {
+  r_.reset();
+  w_->sync_all_noexcept();
+  in_.reset();
+  out_.reset();
+  w_.reset();
+}
+
+int64_t Runner::global_batch() const { return std::accumulate(counts_.begin(), counts_.end(), (int64_t)0); }
+
+PipelineResult Runner::run(const uint8_t* pool, int64_t pool_images, int64_t first, int64_t n, bool pipelined) {
+  const int64_t G = global_batch();
+  const int64_t per = scatter_ ? G : max_;  // pool stride of one step's images
+  const bool has_pool = scatter_ ? rank_ == 0 : true;
+  if (has_pool && (!pool || pool_images < (scatter_ ? G : counts_[rank_])))
+    throw std::invalid_argument("dp::Runner::run: pool smaller than one batch");
+  const int64_t nb = has_pool ? std::max<int64_t>(1, pool_images / per) : 1;
+  auto plan = [&](int64_t step, const Rank&) {
+    StepPlan p;
+    p.step = step;
+    p.counts = counts_;
+    p.src = has_pool ? pool + (size_t)((step % nb) * per) * ib_ : nullptr;
+    return p;
+  };
+  auto on_result = [&](const StepPlan&, const int32_t* i, const float* pr) {
+    last_idx_.assign(i, i + G);
+    last_prob_.assign(pr, pr + G);
+  };
+  return run_pipeline({r_.get()}, first, n, plan, on_result, timeout_ms_, pipelined);
+}
+
+void Runner::stage(const uint8_t* src, uint8_t* dst) {
+  w_->activate();
+  const size_t mine = (size_t)counts_[rank_] * ib_;
+  if (rank_ == 0 && mine) w_->copy(dst, src, mine, Worker::kIn);
+  if (world_ > 1) {
+    in_->group_start();
+    try {
+      if (rank_ == 0) {
+        size_t off = (size_t)counts_[0] * ib_;
+        for (int r = 1; r < world_; ++r) {
+          const size_t b = (size_t)counts_[r] * ib_;
+          if (b) in_->send(src + off, b, r, w_->stream(Worker::kIn));
+          off += b;
+        }
+      } else if (mine) {
+        in_->recv(dst, mine, 0, w_->stream(Worker::kIn));
+      }
+    } catch (...) {
+      in_->group_end();
+      throw;
+    }
+    in_->group_end();
+  }
+  w_->sync_all();
+}
+
+}  // namespace dp
+}  // namespace dmlc

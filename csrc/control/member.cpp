@@ -114,6 +114,18 @@ void MemberService::stage_replica(const std::string& file, int version) {
     if (!f.read(magic, 8) || std::memcmp(magic, kShardMagic, 8) != 0) return;  // only u8 shards live in HBM
   }
   const std::string key = replica_key(file, version);
+  {
+    std::ifstream f(path, std::ios::binary | std::ios::ate);
+    const size_t bytes = (size_t)f.tellg();
+    f.seekg(0);
+    uint8_t head[kShardHeader] = {};
+    if (!f.read((char*)head, kShardHeader)) throw std::runtime_error(path + ": short shard");
+    ShardMeta m;
+    m.version = version;
+    m.info = parse_shard(head, bytes);  // validates the header before anything is staged
+    std::lock_guard<std::mutex> g(mu_);
+    shard_meta_[file] = m;
+  }
   exec_->stage_blob(key, path);
   for (const auto& k : exec_->blob_keys())  // older versions of the same file leave HBM
     if (k != key && k.rfind(file + "@v", 0) == 0) exec_->drop_blob(k);
@@ -163,6 +175,43 @@ MemberService::ShardResult MemberService::predict_shard(const std::string& file,
   r.preds = exec_->predict_blob(model, key);
   r.elapsed_us = steady_us() - t0;
   return r;
+}
+
+MemberService::ShardMeta MemberService::shard_meta(const std::string& file) {
+  int v = 0;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = files_.find(file);
+    if (it == files_.end() || it->second.empty()) throw std::runtime_error("no replica of " + file + " here");
+    v = *it->second.rbegin();
+    auto m = shard_meta_.find(file);
+    if (m != shard_meta_.end() && m->second.version == v) return m->second;
+  }
+  const std::string path = cfg_.storage_dir + "/" + storage_filename(file, v);
+  std::ifstream f(path, std::ios::binary | std::ios::ate);
+  if (!f) throw std::runtime_error("replica of " + file + " v" + std::to_string(v) + " is neither staged nor on disk");
+  const size_t bytes = (size_t)f.tellg();
+  f.seekg(0);
+  uint8_t head[kShardHeader] = {};
+  if (!f.read((char*)head, kShardHeader)) throw std::runtime_error(file + " is not a u8 shard");
+  ShardMeta m;
+  m.version = v;
+  m.info = parse_shard(head, bytes);
+  std::lock_guard<std::mutex> g(mu_);
+  shard_meta_[file] = m;
+  return m;
+}
+
+std::vector<Prediction> MemberService::predict_range(const std::string& file, const std::string& model, int64_t first,
+                                                     int64_t n) {
+  if (!exec_) throw std::runtime_error("no executor");
+  const ShardMeta m = shard_meta(file);
+  if (first < 0 || n < 0 || first + n > (int64_t)m.info.n) throw std::runtime_error(file + ": range out of bounds");
+  const std::string key = replica_key(file, m.version);
+  const auto keys = exec_->blob_keys();
+  if (std::find(keys.begin(), keys.end(), key) == keys.end()) stage_replica(file, m.version);
+  DMLC_TRACE("member.predict_range");
+  return exec_->predict_blob_range(model, key, first, n);
 }
 
 void MemberService::stop() {
@@ -350,6 +399,26 @@ void MemberService::register_handlers() {
     Writer w;
     w.i32(res.version).str(res.location).i64(res.elapsed_us).u32((uint32_t)res.preds.size());
     for (const auto& p : res.preds) w.i32(p.class_idx).f64(p.prob);
+    return w.take();
+  });
+  server_->handle(M_SHARD_INFO, [this](Reader& r) {
+    const ShardMeta m = shard_meta(r.str());
+    Writer w;
+    w.i32(m.version).u32(m.info.n).u32(m.info.h).u32(m.info.w).u32(m.info.label0).boolean(m.info.labelled);
+    return w.take();
+  });
+  server_->handle(M_PREDICT_RANGE, [this](Reader& r) {
+    const std::string model = r.str(), file = r.str();
+    const int64_t first = (int64_t)r.u64();
+    const uint32_t n = r.u32();
+    Writer w;
+    if (!exec_ || !exec_->has_model(model)) {
+      w.boolean(false).u32(0);
+      return w.take();
+    }
+    const auto preds = predict_range(file, model, first, n);
+    w.boolean(true).u32((uint32_t)preds.size());
+    for (const auto& p : preds) w.i32(p.class_idx).f64(p.prob);
     return w.take();
   });
   server_->handle(M_PREDICT, [this](Reader& r) {

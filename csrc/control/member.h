@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "../serve/executor.h"
+#include "../serve/shard.h"
 #include "membership.h"
 #include "rpc.h"
 #include "sdfs.h"
@@ -94,6 +95,16 @@ class MemberService {
     std::vector<Prediction> preds;
   };
   ShardResult predict_shard(const std::string& file, const std::string& model);
+  // Header of the local replica (latest version) of shard `file`; recorded
+  // when the replica is staged, so it survives the file's removal from disk.
+  struct ShardMeta {
+    int version = 0;
+    ShardInfo info;
+  };
+  ShardMeta shard_meta(const std::string& file);
+  // Images [first, first + n) of the local replica of `file` (a shard job's
+  // query, csrc/serve/leader.cpp): read in place from the executor's blob.
+  std::vector<Prediction> predict_range(const std::string& file, const std::string& model, int64_t first, int64_t n);
   // Keys of the staged replicas ("<file>@v<version>").
   std::vector<std::string> staged_replicas() const;
 
@@ -110,6 +121,7 @@ class MemberService {
   std::unique_ptr<RpcServer> server_;
   mutable std::mutex mu_;
   std::map<std::string, std::set<int>> files_;
+  std::map<std::string, ShardMeta> shard_meta_;  // under mu_
   std::multiset<std::string> readable_, writable_;  // under mu_
   std::string leader_;
   std::atomic<bool> stop_{false};

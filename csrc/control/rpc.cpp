@@ -119,7 +119,7 @@ RpcClient& RpcClient::shared() {
 }
 
 std::string RpcClient::call(const std::string& host, int port, uint16_t method, const std::string& payload,
-                            int timeout_ms) {
+                            int timeout_ms, bool fresh) {
   const std::string key = host + ":" + std::to_string(port);
   std::string body;
   body.append((const char*)&method, 2);
@@ -129,7 +129,7 @@ std::string RpcClient::call(const std::string& host, int port, uint16_t method, 
   for (int attempt = 0; attempt < 2; ++attempt) {
     int fd = -1;
     bool pooled = false;
-    if (attempt == 0) {
+    if (attempt == 0 && !fresh) {
       std::lock_guard<std::mutex> g(mu_);
       auto& v = idle_[key];
       if (!v.empty()) {
@@ -155,7 +155,7 @@ std::string RpcClient::call(const std::string& host, int port, uint16_t method, 
     }
     if (resp.empty()) throw RpcError("empty response");
     const uint8_t status = (uint8_t)resp[0];
-    {
+    if (!fresh) {
       std::lock_guard<std::mutex> g(mu_);
       auto& v = idle_[key];
       if (v.size() < 16) v.push_back(conn.release());

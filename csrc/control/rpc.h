@@ -60,8 +60,11 @@ class RpcClient {
  public:
   static RpcClient& shared();
   // Synchronous call; throws RpcError / NetError. timeout covers the whole call.
+  // fresh: a new TCP connection for this call, closed after it (the
+  // reference's per-query connect, src/services.rs:420,583-588; the default
+  // reuses pooled connections).
   std::string call(const std::string& host, int port, uint16_t method, const std::string& payload,
-                   int timeout_ms = 10000);
+                   int timeout_ms = 10000, bool fresh = false);
   void drop(const std::string& host, int port);  // close pooled connections
   void clear();
 

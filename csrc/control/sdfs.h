@@ -29,7 +29,7 @@ enum LeaderMethod : uint16_t {
   L_DELETE = 4,
   L_LS = 5,
   L_TRAIN = 6,
-  L_PREDICT = 7,
+  L_PREDICT = 7,  // payload: optional u32 count + SDFS shard names (jobs over shards)
   L_JOBS = 8,
   L_ALIVE = 9,
   L_STATE = 10,  // jobs + SDFS directory snapshot (standby replication)
@@ -46,6 +46,8 @@ enum MemberMethod : uint16_t {
   M_LOAD_MODEL = 26,  // hot-swap model weights (train)
   M_INFO = 27,
   M_PREDICT_SHARD = 28,  // classify the local (HBM-staged) replica of a shard
+  M_SHARD_INFO = 29,     // header of the local replica of a shard (n, h, w, labels)
+  M_PREDICT_RANGE = 30,  // classify images [first, first+n) of the local replica of a shard
 };
 
 std::string sanitize_filename(const std::string& s);

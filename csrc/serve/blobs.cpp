@@ -32,6 +32,11 @@ std::vector<std::string> Executor::blob_keys() const {
 }
 
 std::vector<Prediction> Executor::predict_blob(const std::string& model, const std::string& key) {
+  return predict_blob_range(model, key, 0, -1);
+}
+
+std::vector<Prediction> Executor::predict_blob_range(const std::string& model, const std::string& key, int64_t first,
+                                                     int64_t count) {
   std::shared_ptr<const std::vector<uint8_t>> b;
   {
     std::lock_guard<std::mutex> g(blob_mu_);
@@ -40,11 +45,13 @@ std::vector<Prediction> Executor::predict_blob(const std::string& model, const s
     b = it->second;
   }
   const ShardInfo s = parse_shard(b->data(), b->size());
-  std::vector<Image> imgs(s.n);
-  for (uint32_t i = 0; i < s.n; ++i) {
+  if (count < 0) count = (int64_t)s.n - first;
+  if (first < 0 || count < 0 || first + count > (int64_t)s.n) throw std::runtime_error(key + ": image range out of bounds");
+  std::vector<Image> imgs(count);
+  for (int64_t i = 0; i < count; ++i) {
     imgs[i].height = (int)s.h;
     imgs[i].width = (int)s.w;
-    const uint8_t* p = b->data() + kShardHeader + (size_t)i * s.image_bytes();
+    const uint8_t* p = b->data() + kShardHeader + (size_t)(first + i) * s.image_bytes();
     imgs[i].rgb.assign(p, p + s.image_bytes());
   }
   return predict(model, imgs);

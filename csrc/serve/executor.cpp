@@ -16,6 +16,10 @@
 #include "../runtime/ot_io.h"
 #include "../runtime/trace.h"
 #include "../comm/dp.h"
+#include "../comm/fleet.h"
+#include <atomic>
+#include <climits>
+#include <set>
 #include "shard.h"
 #include <fstream>
 #include "../kernels/kernels.h"
@@ -184,87 +188,111 @@ class CpuExecutor : public Executor {
 };
 
 // ------------------------------------------------------------------ GPU
-// One or more GPUs of this node. Per model: an engine on every GPU and a
-// dp::Group over them (GPU 0 coordinates; with more than one GPU the query
-// batch is scattered over RCCL, csrc/comm/dp.h). Decoded images stay resident
-// in GPU 0's HBM at their own sizes (LRU cache); a query's images, whatever
-// their sizes, are resized into one u8 224x224 batch by one kernel
-// (resize.hip) and classified by one graph-replayed forward per GPU.
+// The GPUs of this node as one serving fleet (csrc/comm/fleet.h): the GPUs
+// are split between the loaded models with the reference's fair-share rule,
+// every model has an instance (engine x compute lanes) on each GPU of its
+// partition, a query of a few images runs on the least-loaded GPU of the
+// partition, and a large batch is scattered over the partition with RCCL.
+//
+// Data placement (HBM, 288 GB per GPU):
+//   * decoded query images: an LRU cache spread over the GPUs (each new entry
+//     on the GPU holding the fewest cached bytes); a query on GPU d resizes
+//     them (resize.hip) straight from wherever they live, over xGMI peer
+//     access (a copy-engine peer copy where peer access is unavailable);
+//   * SDFS u8 shard replicas: split into one slice per live GPU when they
+//     arrive, streamed from disk through two pinned buffers on per-GPU side
+//     streams (the read of chunk i+1 overlaps the DMA of chunk i); a shard
+//     query runs on the GPU holding its slice when that GPU is in the model's
+//     partition, reading the slice in place.
 class GpuExecutor : public Executor {
  public:
-  GpuExecutor(std::vector<int> devices, int max_batch, size_t cache_bytes, int min_shard)
-      : devices_(std::move(devices)), max_batch_(max_batch), min_shard_(min_shard), cache_cap_(cache_bytes) {
+  GpuExecutor(std::vector<int> devices, int max_batch, size_t cache_bytes, int min_shard, int lanes)
+      : devices_(std::move(devices)), max_batch_(max_batch), lanes_(std::max(1, std::min(lanes, 4))),
+        cache_cap_(cache_bytes) {
     if (devices_.empty()) throw std::invalid_argument("GpuExecutor: no devices");
-    DMLC_HIP_CHECK(hipSetDevice(devices_[0]));
-    for (int i = 0; i < kStagers; ++i) {
-      Stager st;
-      DMLC_HIP_CHECK(hipStreamCreateWithFlags(&st.stream, hipStreamNonBlocking));
-      free_stagers_.push_back(st);
-    }
+    for (int d : devices_) cache_bytes_dev_[d] = 0;
+    if (devices_.size() > 1) enable_peers();
+    for (int i = 0; i < kStagers; ++i) free_stagers_.push_back(std::make_shared<Stager>());
+    dp::FleetOptions o;
+    o.max_per_rank = max_batch_;
+    o.image_bytes = (size_t)kS * kS * 3;
+    o.min_shard = std::max(1, min_shard);
+    o.aux_bytes = (size_t)max_batch_ * sizeof(ImageDesc);
+    fleet_ = std::make_unique<dp::Fleet>(
+        devices_, [this](const std::string& m, int d, dp::Worker* rep) { return make_worker(m, d, rep); },
+        [](const std::vector<int>& devs) { return comm::rccl_init_all(devs); }, o);
   }
   ~GpuExecutor() override {
-    (void)hipSetDevice(devices_[0]);
-    (void)hipDeviceSynchronize();
+    fleet_.reset();
     {
-      std::lock_guard<std::mutex> g(models_mu_);
-      models_.clear();
+      std::lock_guard<std::mutex> g(blob_mu_);
+      hbm_blobs_.clear();
     }
-    (void)hipSetDevice(devices_[0]);
-    for (auto& kv : cache_) (void)hipFree(kv.second.dev);
-    for (auto& st : free_stagers_) {
-      if (st.pinned) (void)hipHostFree(st.pinned);
-      (void)hipStreamDestroy(st.stream);
+    for (auto& kv : cache_) {
+      (void)hipSetDevice(kv.second.device);
+      (void)hipFree(kv.second.dev);
     }
+    free_stagers_.clear();
   }
   std::string backend() const override {
     std::string b = "gpu:" + std::to_string(devices_[0]);
     for (size_t i = 1; i < devices_.size(); ++i) b += "," + std::to_string(devices_[i]);
     return b;
   }
+  std::string placement() const override {
+    std::string s;
+    for (const auto& kv : fleet_->partitions()) {
+      s += (s.empty() ? "" : " ") + kv.first + "=gpu";
+      for (size_t i = 0; i < kv.second.size(); ++i) s += (i ? "," : "") + std::to_string(kv.second[i]);
+      if (kv.second.empty()) s += "-";
+    }
+    return s.empty() ? "none" : s;
+  }
+  void set_jobs(const std::vector<std::string>& models) override { fleet_->set_jobs(models); }
+  void lose_device(int device) override { fleet_->lose(device); }
 
   void load_model(const std::string& model, const std::string& path) override {
     load_model_weights(model, ot_load(path));
   }
   void load_model_weights(const std::string& model, const WeightMap& w) override {
-    // Build the new replicas outside the lock; in-flight queries keep the old
-    // slot alive (shared_ptr) until they finish: a hot swap.
-    auto slot = std::make_shared<ModelSlot>(model, w, devices_, max_batch_, min_shard_);
-    std::lock_guard<std::mutex> g(models_mu_);
-    models_[model] = std::move(slot);
+    {
+      std::lock_guard<std::mutex> g(weights_mu_);
+      weights_[model] = std::make_shared<const WeightMap>(w);
+    }
+    fleet_->load(model);  // first load: partitions recomputed; later: hot swap
   }
-  bool has_model(const std::string& model) const override {
-    std::lock_guard<std::mutex> g(models_mu_);
-    return models_.count(model) > 0;
-  }
+  bool has_model(const std::string& model) const override { return fleet_->has(model); }
 
+  // Host images (decoded): uploaded to the chosen GPU inside the stage.
   std::vector<Prediction> predict(const std::string& model, const std::vector<Image>& imgs) override {
-    auto slot = get(model);
-    DMLC_HIP_CHECK(hipSetDevice(devices_[0]));
-    std::vector<ImageDesc> descs(imgs.size());
-    std::vector<void*> bufs;
-    for (size_t i = 0; i < imgs.size(); ++i) {
-      void* d = nullptr;
-      DMLC_HIP_CHECK(hipMalloc(&d, imgs[i].rgb.size()));
-      DMLC_HIP_CHECK(hipMemcpy(d, imgs[i].rgb.data(), imgs[i].rgb.size(), hipMemcpyHostToDevice));
-      bufs.push_back(d);
-      descs[i] = ImageDesc{(const uint8_t*)d, imgs[i].height, imgs[i].width};
-    }
-    std::vector<Prediction> out;
-    try {
-      out = slot->run(descs);
-    } catch (...) {
-      for (void* b : bufs) (void)hipFree(b);
-      throw;
-    }
-    for (void* b : bufs) (void)hipFree(b);
-    return out;
+    const int64_t n = (int64_t)imgs.size();
+    std::vector<int32_t> idx(n);
+    std::vector<float> prob(n);
+    auto stage = [&](const dp::StageCtx& c, int64_t first, int64_t cnt) -> const uint8_t* {
+      auto s = (hipStream_t)c.worker->stream(c.stream);
+      auto* hd = (ImageDesc*)c.aux_host;
+      std::vector<void*> tmp;
+      for (int64_t i = 0; i < cnt; ++i) {
+        const Image& im = imgs[first + i];
+        void* d = nullptr;
+        DMLC_HIP_CHECK(hipMallocAsync(&d, std::max<size_t>(im.rgb.size(), 1), s));
+        DMLC_HIP_CHECK(hipMemcpyAsync(d, im.rgb.data(), im.rgb.size(), hipMemcpyHostToDevice, s));
+        tmp.push_back(d);
+        hd[i] = ImageDesc{(const uint8_t*)d, im.height, im.width};
+      }
+      resize_into(c, hd, cnt, s);
+      for (void* d : tmp) DMLC_HIP_CHECK(hipFreeAsync(d, s));
+      return (const uint8_t*)c.batch;
+    };
+    fleet_->classify(model, n, stage, idx.data(), prob.data());
+    return to_preds(idx, prob);
   }
 
   // HBM-resident decoded images: a hit skips the JPEG decode and the H2D
   // copy. The query's entries are pinned (not evictable) until its forward
   // has consumed them.
   std::vector<Prediction> predict_files(const std::string& model, const std::vector<std::string>& paths) override {
-    auto slot = get(model);  // fail fast on an unknown model
+    if (!fleet_->has(model)) throw std::runtime_error("model not loaded: " + model);
     {
       DMLC_TRACE("executor.stage");
       // misses decode in parallel (host JPEG decode dominates a miss)
@@ -287,7 +315,11 @@ class GpuExecutor : public Executor {
           if (e) std::rethrow_exception(e);
       }
     }
-    std::vector<ImageDesc> descs(paths.size());
+    struct Src {
+      const uint8_t* dev;
+      int device, h, w;
+    };
+    std::vector<Src> src(paths.size());
     std::vector<std::string> pinned;
     {
       std::lock_guard<std::mutex> g(cache_mu_);
@@ -300,18 +332,51 @@ class GpuExecutor : public Executor {
         touch(it);
         ++it->second.pins;
         pinned.push_back(paths[i]);
-        descs[i] = ImageDesc{(const uint8_t*)it->second.dev, it->second.h, it->second.w};
+        src[i] = Src{(const uint8_t*)it->second.dev, it->second.device, it->second.h, it->second.w};
       }
     }
-    std::vector<Prediction> out;
+    const int64_t n = (int64_t)paths.size();
+    std::vector<int32_t> idx(n);
+    std::vector<float> prob(n);
+    // the GPU already holding most of the query's images, for locality
+    std::map<int, int> where;
+    for (const auto& x : src) ++where[x.device];
+    int prefer = -1, most = 0;
+    for (const auto& kv : where)
+      if (kv.second > most) most = kv.second, prefer = kv.first;
+    auto stage = [&](const dp::StageCtx& c, int64_t first, int64_t cnt) -> const uint8_t* {
+      auto s = (hipStream_t)c.worker->stream(c.stream);
+      auto* hd = (ImageDesc*)c.aux_host;
+      std::vector<void*> tmp;
+      for (int64_t i = 0; i < cnt; ++i) {
+        const Src& x = src[first + i];
+        const uint8_t* p = x.dev;
+        if (x.device != c.device && !peer(c.device, x.device)) {
+          // no peer mapping: a copy-engine copy over xGMI into a temporary
+          const size_t bytes = (size_t)x.h * x.w * 3;
+          void* d = nullptr;
+          DMLC_HIP_CHECK(hipMallocAsync(&d, bytes, s));
+          DMLC_HIP_CHECK(hipMemcpyPeerAsync(d, c.device, x.dev, x.device, bytes, s));
+          tmp.push_back(d);
+          p = (const uint8_t*)d;
+        }
+        hd[i] = ImageDesc{p, x.h, x.w};
+      }
+      resize_into(c, hd, cnt, s);
+      for (void* d : tmp) DMLC_HIP_CHECK(hipFreeAsync(d, s));
+      return (const uint8_t*)c.batch;
+    };
+    dp::Fleet::QueryOptions q;
+    q.prefer_device = prefer;
     try {
-      out = slot->run(descs);
+      DMLC_TRACE("executor.forward");
+      fleet_->classify(model, n, stage, idx.data(), prob.data(), q);
     } catch (...) {
       unpin(pinned);
       throw;
     }
     unpin(pinned);
-    return out;
+    return to_preds(idx, prob);
   }
 
   bool stage(const std::string& path) override {
@@ -319,8 +384,12 @@ class GpuExecutor : public Executor {
     return true;
   }
 
-  // ---- SDFS replicas resident in the coordinator GPU's HBM
-  std::string blob_location() const override { return "hbm:gpu" + std::to_string(devices_[0]); }
+  // ---- SDFS shard replicas, one slice per live GPU
+  std::string blob_location() const override {
+    std::string s = "hbm:gpu";
+    for (size_t i = 0; i < devices_.size(); ++i) s += (i ? "," : "") + std::to_string(devices_[i]);
+    return s;
+  }
 
   void stage_blob(const std::string& key, const std::string& path) override {
     std::ifstream f(path, std::ios::binary);
@@ -328,30 +397,65 @@ class GpuExecutor : public Executor {
     f.seekg(0, std::ios::end);
     const size_t bytes = (size_t)f.tellg();
     f.seekg(0);
+    uint8_t head[kShardHeader] = {};
+    if (bytes < kShardHeader || !f.read((char*)head, kShardHeader)) throw std::runtime_error(path + ": not a u8 shard");
     auto b = std::make_shared<HbmBlob>();
-    b->bytes = bytes;
-    b->device = devices_[0];
-    DMLC_HIP_CHECK(hipSetDevice(devices_[0]));
-    DMLC_HIP_CHECK(hipMalloc(&b->dev, std::max<size_t>(bytes, 256)));
-    // pinned bounce buffer, 32 MB chunks, H2D on a stager's side stream
-    Stager st = take_stager();
+    b->si = parse_shard(head, bytes);  // validates h, w <= 4096 and n * h * w * 3 == size
+    const size_t ib = b->si.image_bytes();
+    std::vector<int> live = fleet_->live();
+    if (live.empty()) throw std::runtime_error("no live GPU to stage " + key);
+    const int64_t n = b->si.n;
+    const int P = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)live.size(), n));
+    for (int k = 0; k < P; ++k) {
+      HbmBlob::Piece pc;
+      pc.device = live[k];
+      pc.first = n * k / P;
+      pc.n = n * (k + 1) / P - pc.first;
+      DMLC_HIP_CHECK(hipSetDevice(pc.device));
+      DMLC_HIP_CHECK(hipMalloc(&pc.dev, std::max<size_t>((size_t)pc.n * ib, 256)));
+      b->pieces.push_back(pc);
+    }
+    // Stream the images through two pinned buffers: the file read of one
+    // chunk overlaps the DMA of the previous one (each slice's DMA on a side
+    // stream of its GPU); a buffer is refilled only once its copies are done.
+    auto st = take_stager();
     try {
       constexpr size_t kChunk = (size_t)32 << 20;
-      if (st.pinned_bytes < std::min(kChunk, bytes)) {
-        if (st.pinned) DMLC_HIP_CHECK(hipHostFree(st.pinned));
-        st.pinned = nullptr;
-        st.pinned_bytes = 0;
-        DMLC_HIP_CHECK(hipHostMalloc(&st.pinned, std::min(kChunk, std::max<size_t>(bytes, 256)), hipHostMallocDefault));
-        st.pinned_bytes = std::min(kChunk, std::max<size_t>(bytes, 256));
+      const size_t chunk = std::max(ib, kChunk / ib * ib);  // whole images per chunk
+      st->ensure_pinned(std::min(chunk, std::max<size_t>((size_t)n * ib, 256)));
+      const size_t cap = st->pinned_bytes / ib * ib;
+      if (cap == 0) throw std::runtime_error("stage_blob: staging buffer too small");
+      std::vector<hipEvent_t> pending[2];
+      int buf = 0;
+      for (int64_t img = 0; img < n;) {
+        for (hipEvent_t e : pending[buf]) {
+          DMLC_HIP_CHECK(hipEventSynchronize(e));
+          DMLC_HIP_CHECK(hipEventDestroy(e));
+        }
+        pending[buf].clear();
+        const int64_t cnt = std::min<int64_t>(n - img, (int64_t)(cap / ib));
+        uint8_t* hb = (uint8_t*)st->pinned[buf];
+        if (!f.read((char*)hb, (std::streamsize)((size_t)cnt * ib))) throw std::runtime_error(path + ": short read");
+        for (const auto& pc : b->pieces) {
+          const int64_t lo = std::max(img, pc.first), hi = std::min(img + cnt, pc.first + pc.n);
+          if (lo >= hi) continue;
+          DMLC_HIP_CHECK(hipSetDevice(pc.device));
+          hipStream_t s = st->stream(pc.device);
+          DMLC_HIP_CHECK(hipMemcpyAsync((uint8_t*)pc.dev + (size_t)(lo - pc.first) * ib, hb + (size_t)(lo - img) * ib,
+                                        (size_t)(hi - lo) * ib, hipMemcpyHostToDevice, s));
+          hipEvent_t e;
+          DMLC_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+          DMLC_HIP_CHECK(hipEventRecord(e, s));
+          pending[buf].push_back(e);
+        }
+        img += cnt;
+        buf ^= 1;
       }
-      for (size_t off = 0; off < bytes;) {
-        const size_t n = std::min(st.pinned_bytes, bytes - off);
-        f.read((char*)st.pinned, (std::streamsize)n);
-        if (off == 0 && n >= kShardHeader) std::memcpy(b->head, st.pinned, kShardHeader);
-        DMLC_HIP_CHECK(hipMemcpyAsync((uint8_t*)b->dev + off, st.pinned, n, hipMemcpyHostToDevice, st.stream));
-        DMLC_HIP_CHECK(hipStreamSynchronize(st.stream));
-        off += n;
-      }
+      for (auto& v : pending)
+        for (hipEvent_t e : v) {
+          DMLC_HIP_CHECK(hipEventSynchronize(e));  // resident before it is visible
+          DMLC_HIP_CHECK(hipEventDestroy(e));
+        }
     } catch (...) {
       give_stager(st);
       throw;
@@ -370,27 +474,48 @@ class GpuExecutor : public Executor {
     for (const auto& kv : hbm_blobs_) out.push_back(kv.first);
     return out;
   }
+
+  // Every image of a shard: slice-aligned chunks of at most max_batch images,
+  // run concurrently as direct queries, each preferring the GPU that holds
+  // its slice (the data is already spread over the GPUs: no scatter).
   std::vector<Prediction> predict_blob(const std::string& model, const std::string& key) override {
-    auto slot = get(model);
-    std::shared_ptr<HbmBlob> b;
-    {
-      std::lock_guard<std::mutex> g(blob_mu_);
-      auto it = hbm_blobs_.find(key);
-      if (it == hbm_blobs_.end()) throw std::runtime_error("blob not staged: " + key);
-      b = it->second;
-    }
-    if (b->bytes < kShardHeader || !is_shard(b->head, kShardHeader)) throw std::runtime_error(key + " is not a u8 shard");
-    ShardInfo si;
-    std::memcpy(&si.n, b->head + 8, 4);
-    std::memcpy(&si.h, b->head + 12, 4);
-    std::memcpy(&si.w, b->head + 16, 4);
-    if (si.h == 0 || si.w == 0 || (uint64_t)si.n * si.image_bytes() + kShardHeader != b->bytes)
-      throw std::runtime_error(key + ": bad shard header");
-    const uint8_t* data = (const uint8_t*)b->dev + kShardHeader;
-    if (si.h == ModelSlot::kS && si.w == ModelSlot::kS) return slot->run_dense(data, si.n);
-    std::vector<ImageDesc> descs(si.n);
-    for (uint32_t i = 0; i < si.n; ++i) descs[i] = ImageDesc{data + (size_t)i * si.image_bytes(), (int)si.h, (int)si.w};
-    return slot->run(descs);
+    auto b = blob(key);
+    const int64_t n = b->si.n;
+    std::vector<int32_t> idx(n);
+    std::vector<float> prob(n);
+    std::vector<std::pair<int64_t, int64_t>> chunks;
+    for (const auto& pc : b->pieces)
+      for (int64_t f = pc.first; f < pc.first + pc.n; f += max_batch_)
+        chunks.emplace_back(f, std::min<int64_t>(max_batch_, pc.first + pc.n - f));
+    const auto parts = fleet_->partitions();
+    const size_t width = parts.count(model) ? std::max<size_t>(1, parts.at(model).size() * lanes_) : 1;
+    std::atomic<size_t> next{0};
+    std::vector<std::exception_ptr> errs(std::min(width, std::max<size_t>(1, chunks.size())));
+    std::vector<std::thread> ts;
+    for (size_t t = 0; t < errs.size(); ++t)
+      ts.emplace_back([&, t] {
+        try {
+          for (size_t c = next++; c < chunks.size(); c = next++)
+            classify_range(model, b, chunks[c].first, chunks[c].second, idx.data() + chunks[c].first,
+                           prob.data() + chunks[c].first);
+        } catch (...) {
+          errs[t] = std::current_exception();
+        }
+      });
+    for (auto& th : ts) th.join();
+    for (auto& e : errs)
+      if (e) std::rethrow_exception(e);
+    return to_preds(idx, prob);
+  }
+  std::vector<Prediction> predict_blob_range(const std::string& model, const std::string& key, int64_t first,
+                                             int64_t n) override {
+    auto b = blob(key);
+    if (n < 0) n = (int64_t)b->si.n - first;
+    if (first < 0 || n < 0 || first + n > (int64_t)b->si.n) throw std::runtime_error(key + ": image range out of bounds");
+    std::vector<int32_t> idx(n);
+    std::vector<float> prob(n);
+    classify_range(model, b, first, n, idx.data(), prob.data());
+    return to_preds(idx, prob);
   }
 
   CacheStats cache_stats() const override {
@@ -403,155 +528,184 @@ class GpuExecutor : public Executor {
   }
 
  private:
+  static constexpr int kS = 224;
   static constexpr size_t kDecodeThreads = 8;
   static constexpr int kStagers = 16;  // held through a miss's decode (it decodes into the pinned buffer)
 
-  // One model replicated on every GPU of the executor.
-  struct ModelSlot {
-    ModelSlot(const std::string& arch, const WeightMap& w, const std::vector<int>& devices, int max_batch,
-              int min_shard)
-        : max_batch(max_batch) {
-      // The host packs the weights once (engine 0, one H2D copy); the other
-      // GPUs get replicas whose arenas are filled by one RCCL broadcast over
-      // xGMI (`train` = distribute + hot-swap).
-      for (size_t k = 0; k < devices.size(); ++k) {
-        DMLC_HIP_CHECK(hipSetDevice(devices[k]));
-        if (k == 0) engines.push_back(std::make_unique<Engine>(arch, w, devices[0]));
-        else engines.push_back(std::make_unique<Engine>(*engines[0], devices[k]));
-        engines.back()->reserve(max_batch);
+  // A pinned bounce buffer pair and one side stream per GPU it has uploaded to.
+  struct Stager {
+    void* pinned[2] = {nullptr, nullptr};
+    size_t pinned_bytes = 0;
+    std::map<int, hipStream_t> streams;
+    void ensure_pinned(size_t bytes) {
+      if (pinned_bytes >= bytes) return;
+      for (auto& p : pinned) {
+        if (p) DMLC_HIP_CHECK(hipHostFree(p));
+        p = nullptr;
       }
-      if (devices.size() > 1) {
-        auto comms = comm::rccl_init_all(devices);
-        comms[0]->group_start();
-        for (size_t k = 0; k < devices.size(); ++k) {
-          DMLC_HIP_CHECK(hipSetDevice(devices[k]));
-          comms[k]->broadcast(engines[0]->weight_arena(), engines[k]->weight_arena(), engines[0]->weight_bytes(), 0,
-                              engines[k]->stream());
-        }
-        comms[0]->group_end();
-        for (size_t k = 0; k < devices.size(); ++k) {
-          DMLC_HIP_CHECK(hipSetDevice(devices[k]));
-          DMLC_HIP_CHECK(hipStreamSynchronize(engines[k]->stream()));
-        }
+      pinned_bytes = 0;
+      for (auto& p : pinned) DMLC_HIP_CHECK(hipHostMalloc(&p, bytes, hipHostMallocDefault));
+      pinned_bytes = bytes;
+    }
+    hipStream_t stream(int device) {
+      auto it = streams.find(device);
+      if (it != streams.end()) return it->second;
+      hipStream_t s;
+      DMLC_HIP_CHECK(hipSetDevice(device));
+      DMLC_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+      streams[device] = s;
+      return s;
+    }
+    ~Stager() {
+      for (auto& kv : streams) {
+        (void)hipSetDevice(kv.first);
+        (void)hipStreamSynchronize(kv.second);
+        (void)hipStreamDestroy(kv.second);
       }
-      // Two compute lanes per GPU (dp::Worker::lanes): a second instance of
-      // the model whose forward overlaps the previous step's tail (+9% at
-      // ResNet18 b256: profiles/r2_lanes.txt).
-      for (size_t k = 0; k < devices.size(); ++k) {
-        DMLC_HIP_CHECK(hipSetDevice(devices[k]));
-        lane2.push_back(std::make_unique<Engine>(*engines[k], devices[k]));
-        lane2.back()->copy_weights_from(*engines[k]);
-        lane2.back()->reserve(max_batch);
-        workers.push_back(dp::make_hip_worker(engines[k].get(), kS, kS, /*use_graph=*/true, {lane2.back().get()}));
-      }
-      std::vector<dp::Worker*> ws;
-      for (auto& x : workers) ws.push_back(x.get());
-      auto factory = [devices](const std::vector<int>& members) {
-        std::vector<int> devs;
-        for (int m : members) devs.push_back(devices.at(m));
-        return comm::rccl_init_all(devs);
-      };
-      group = std::make_unique<dp::Group>(ws, factory, max_batch, (size_t)kS * kS * 3);
-      group->set_min_per_rank(min_shard);
-      dp::Worker* c = group->coordinator();
-      c->activate();
-      batch = c->alloc((size_t)max_batch * kS * kS * 3);
-      d_descs = c->alloc((size_t)max_batch * sizeof(ImageDesc));
-      h_descs = (ImageDesc*)c->alloc_host((size_t)max_batch * sizeof(ImageDesc));
-      ev_src = c->new_event();
+      for (auto p : pinned)
+        if (p) (void)hipHostFree(p);
     }
-    ~ModelSlot() {
-      dp::Worker* c = group->coordinator();
-      c->activate();
-      c->sync_all();
-      c->dealloc(batch);
-      c->dealloc(d_descs);
-      c->dealloc_host(h_descs);
-      group.reset();
-      workers.clear();
-      lane2.clear();
-      engines.clear();
-    }
-    // Resize the images into one u8 batch on the coordinator, then classify
-    // it across the group.
-    std::vector<Prediction> run(const std::vector<ImageDesc>& descs) {
-      DMLC_TRACE("executor.forward");
-      std::lock_guard<std::mutex> g(mu);
-      std::vector<Prediction> out(descs.size());
-      dp::Worker* c = group->coordinator();
-      c->activate();
-      auto s = (hipStream_t)c->stream(dp::Worker::kCompute);
-      for (size_t first = 0; first < descs.size(); first += (size_t)max_batch) {
-        const int B = (int)std::min(descs.size() - first, (size_t)max_batch);
-        c->sync(ev_src);  // the previous chunk's resize has read h_descs
-        std::memcpy(h_descs, descs.data() + first, (size_t)B * sizeof(ImageDesc));
-        DMLC_HIP_CHECK(hipMemcpyAsync(d_descs, h_descs, (size_t)B * sizeof(ImageDesc), hipMemcpyHostToDevice, s));
-        resize_u8_ragged((const ImageDesc*)d_descs, (uint8_t*)batch, B, kS, s);
-        c->record(ev_src, dp::Worker::kCompute);
-        std::vector<int32_t> idx(B);
-        std::vector<float> prob(B);
-        group->classify((const uint8_t*)batch, B, idx.data(), prob.data(), ev_src);
-        for (int b = 0; b < B; ++b) out[first + b] = Prediction{prob[b], idx[b]};
-      }
-      return out;
-    }
-    // Images already u8 224x224 in coordinator memory (a staged shard):
-    // straight into the group, no resize copy.
-    std::vector<Prediction> run_dense(const uint8_t* src, int64_t n) {
-      DMLC_TRACE("executor.forward_dense");
-      std::lock_guard<std::mutex> g(mu);
-      std::vector<int32_t> idx(n);
-      std::vector<float> prob(n);
-      group->coordinator()->activate();
-      group->classify(src, n, idx.data(), prob.data());
-      std::vector<Prediction> out(n);
-      for (int64_t i = 0; i < n; ++i) out[i] = Prediction{prob[i], idx[i]};
-      return out;
-    }
-    static constexpr int kS = 224;
-    int max_batch;
-    std::vector<std::unique_ptr<Engine>> engines;
-    std::vector<std::unique_ptr<Engine>> lane2;  // second compute lane per GPU
-    std::vector<std::unique_ptr<dp::Worker>> workers;
-    std::unique_ptr<dp::Group> group;
-    void* batch = nullptr;
-    void* d_descs = nullptr;
-    ImageDesc* h_descs = nullptr;
-    int ev_src = -1;
-    std::mutex mu;  // one query batch at a time per model
   };
 
   struct Entry {
     void* dev = nullptr;
+    int device = 0;
     int h = 0, w = 0;
     size_t bytes = 0;
     int pins = 0;
     std::list<std::string>::iterator lru;
   };
   struct HbmBlob {
-    void* dev = nullptr;
-    size_t bytes = 0;
-    int device = 0;
-    uint8_t head[kShardHeader] = {};  // host copy of the first bytes (shard header)
+    ShardInfo si;
+    struct Piece {
+      int device = 0;
+      void* dev = nullptr;
+      int64_t first = 0, n = 0;
+    };
+    std::vector<Piece> pieces;
     ~HbmBlob() {
-      if (dev) {
-        (void)hipSetDevice(device);
-        (void)hipFree(dev);
-      }
+      for (auto& p : pieces)
+        if (p.dev) {
+          (void)hipSetDevice(p.device);
+          (void)hipFree(p.dev);
+        }
     }
   };
-  std::map<std::string, std::shared_ptr<HbmBlob>> hbm_blobs_;  // under blob_mu_
-  struct Stager {
-    hipStream_t stream = nullptr;
-    void* pinned = nullptr;
-    size_t pinned_bytes = 0;
-  };
 
-  std::shared_ptr<ModelSlot> get(const std::string& model) const {
-    std::lock_guard<std::mutex> g(models_mu_);
-    auto it = models_.find(model);
-    if (it == models_.end()) throw std::runtime_error("model not loaded: " + model);
+  std::unique_ptr<dp::Worker> make_worker(const std::string& model, int device, dp::Worker* replica_of) {
+    std::shared_ptr<const WeightMap> w;
+    if (!replica_of) {
+      std::lock_guard<std::mutex> g(weights_mu_);
+      auto it = weights_.find(model);
+      if (it == weights_.end()) throw std::runtime_error("no weights for " + model);
+      w = it->second;
+    }
+    DMLC_HIP_CHECK(hipSetDevice(device));
+    std::vector<std::unique_ptr<Engine>> es;
+    if (replica_of) es.push_back(std::make_unique<Engine>(*dp::hip_worker_engine(*replica_of, 0), device));
+    else es.push_back(std::make_unique<Engine>(model, *w, device));
+    es[0]->reserve(max_batch_);
+    // further compute lanes: more instances on the same GPU (their own
+    // activations, graphs and streams), so concurrent queries overlap
+    for (int l = 1; l < lanes_; ++l) {
+      es.push_back(std::make_unique<Engine>(*es[0], device));
+      if (!replica_of) es.back()->copy_weights_from(*es[0]);  // a replica's lanes copy after the broadcast
+      es.back()->reserve(max_batch_);
+    }
+    return dp::make_owned_hip_worker(std::move(es), kS, kS, /*use_graph=*/true);
+  }
+
+  void enable_peers() {
+    for (int a : devices_)
+      for (int b : devices_) {
+        if (a == b) continue;
+        int can = 0;
+        if (hipDeviceCanAccessPeer(&can, a, b) != hipSuccess || !can) continue;
+        DMLC_HIP_CHECK(hipSetDevice(a));
+        const hipError_t e = hipDeviceEnablePeerAccess(b, 0);
+        if (e == hipSuccess || e == hipErrorPeerAccessAlreadyEnabled) peers_.insert({a, b});
+        (void)hipGetLastError();
+      }
+  }
+  // kernels on `reader` may dereference memory of `owner`
+  bool peer(int reader, int owner) const { return reader == owner || peers_.count({reader, owner}) > 0; }
+
+  // descriptors (pinned host) -> the stage's device scratch -> one u8 batch
+  void resize_into(const dp::StageCtx& c, const ImageDesc* hd, int64_t cnt, hipStream_t s) {
+    if (cnt > c.capacity) throw std::logic_error("resize_into: more images than the stage buffer holds");
+    for (int64_t i = 0; i < cnt; ++i)
+      if (hd[i].h <= 0 || hd[i].w <= 0 || hd[i].h > 4096 || hd[i].w > 4096)
+        throw std::runtime_error("resize_into: bad image size");
+    DMLC_HIP_CHECK(hipMemcpyAsync(c.aux, hd, (size_t)cnt * sizeof(ImageDesc), hipMemcpyHostToDevice, s));
+    resize_u8_ragged((const ImageDesc*)c.aux, (uint8_t*)c.batch, (int)cnt, kS, s);
+  }
+
+  std::shared_ptr<HbmBlob> blob(const std::string& key) const {
+    std::lock_guard<std::mutex> g(blob_mu_);
+    auto it = hbm_blobs_.find(key);
+    if (it == hbm_blobs_.end()) throw std::runtime_error("blob not staged: " + key);
     return it->second;
+  }
+
+  // Images [first, first + n) of a staged shard through the fleet (no scatter:
+  // the slices are already spread over the GPUs; the query prefers the GPU
+  // holding its first image).
+  void classify_range(const std::string& model, const std::shared_ptr<HbmBlob>& b, int64_t first, int64_t n,
+                      int32_t* idx, float* prob) {
+    const size_t ib = b->si.image_bytes();
+    const bool dense = b->si.h == (uint32_t)kS && b->si.w == (uint32_t)kS;
+    int prefer = -1;
+    for (const auto& pc : b->pieces)
+      if (first >= pc.first && first < pc.first + pc.n) prefer = pc.device;
+    auto stage = [&](const dp::StageCtx& c, int64_t off, int64_t cnt) -> const uint8_t* {
+      const int64_t g0 = first + off;
+      auto s = (hipStream_t)c.worker->stream(c.stream);
+      if (dense) {
+        for (const auto& pc : b->pieces)  // in place: the whole range in a slice on this GPU
+          if (pc.device == c.device && g0 >= pc.first && g0 + cnt <= pc.first + pc.n)
+            return (const uint8_t*)pc.dev + (size_t)(g0 - pc.first) * ib;
+        for (const auto& pc : b->pieces) {  // gather the range into the stage buffer
+          const int64_t lo = std::max(g0, pc.first), hi = std::min(g0 + cnt, pc.first + pc.n);
+          if (lo >= hi) continue;
+          uint8_t* dst = (uint8_t*)c.batch + (size_t)(lo - g0) * ib;
+          const uint8_t* srcp = (const uint8_t*)pc.dev + (size_t)(lo - pc.first) * ib;
+          if (pc.device == c.device)
+            DMLC_HIP_CHECK(hipMemcpyAsync(dst, srcp, (size_t)(hi - lo) * ib, hipMemcpyDeviceToDevice, s));
+          else
+            DMLC_HIP_CHECK(hipMemcpyPeerAsync(dst, c.device, srcp, pc.device, (size_t)(hi - lo) * ib, s));
+        }
+        return (const uint8_t*)c.batch;
+      }
+      // other sizes: resized on the GPU like query images
+      auto* hd = (ImageDesc*)c.aux_host;
+      std::vector<void*> tmp;
+      for (const auto& pc : b->pieces) {
+        const int64_t lo = std::max(g0, pc.first), hi = std::min(g0 + cnt, pc.first + pc.n);
+        if (lo >= hi) continue;
+        const uint8_t* base = (const uint8_t*)pc.dev + (size_t)(lo - pc.first) * ib;
+        if (!peer(c.device, pc.device)) {
+          void* d = nullptr;
+          DMLC_HIP_CHECK(hipMallocAsync(&d, (size_t)(hi - lo) * ib, s));
+          DMLC_HIP_CHECK(hipMemcpyPeerAsync(d, c.device, base, pc.device, (size_t)(hi - lo) * ib, s));
+          tmp.push_back(d);
+          base = (const uint8_t*)d;
+        }
+        for (int64_t i = lo; i < hi; ++i) hd[i - g0] = ImageDesc{base + (size_t)(i - lo) * ib, (int)b->si.h, (int)b->si.w};
+      }
+      resize_into(c, hd, cnt, s);
+      for (void* d : tmp) DMLC_HIP_CHECK(hipFreeAsync(d, s));
+      return (const uint8_t*)c.batch;
+    };
+    dp::Fleet::QueryOptions q;
+    q.prefer_device = prefer;
+    q.allow_scatter = false;
+    fleet_->classify(model, n, stage, idx, prob, q);
+  }
+
+  static std::vector<Prediction> to_preds(const std::vector<int32_t>& idx, const std::vector<float>& prob) {
+    std::vector<Prediction> out(idx.size());
+    for (size_t i = 0; i < idx.size(); ++i) out[i] = Prediction{prob[i], idx[i]};
+    return out;
   }
 
   void touch(std::unordered_map<std::string, Entry>::iterator it) { lru_.splice(lru_.begin(), lru_, it->second.lru); }
@@ -564,23 +718,25 @@ class GpuExecutor : public Executor {
     }
   }
 
-  Stager take_stager() {
+  std::shared_ptr<Stager> take_stager() {
     std::unique_lock<std::mutex> g(stager_mu_);
     stager_cv_.wait(g, [&] { return !free_stagers_.empty(); });
-    Stager s = free_stagers_.back();
+    auto s = free_stagers_.back();
     free_stagers_.pop_back();
     return s;
   }
-  void give_stager(const Stager& s) {
+  void give_stager(const std::shared_ptr<Stager>& s) {
     std::lock_guard<std::mutex> g(stager_mu_);
     free_stagers_.push_back(s);
     stager_cv_.notify_one();
   }
 
   // Decode and upload without holding the cache lock: the JPEG is decoded on
-  // this thread, copied into the stager's pinned buffer and DMA'd into a new
-  // HBM block on the stager's stream; only the final insert/evict locks.
+  // this thread into the stager's pinned buffer and DMA'd into a new HBM
+  // block on the GPU holding the fewest cached bytes; only the final
+  // insert/evict locks.
   void stage_one(const std::string& path, bool count_as_miss) {
+    int home;
     {
       std::lock_guard<std::mutex> g(cache_mu_);
       auto it = cache_.find(path);
@@ -589,6 +745,11 @@ class GpuExecutor : public Executor {
         touch(it);
         return;
       }
+      home = devices_[0];
+      size_t least = SIZE_MAX;
+      const auto live = fleet_->live();
+      for (int d : live)
+        if (cache_bytes_dev_[d] < least) least = cache_bytes_dev_[d], home = d;
     }
     std::vector<uint8_t> jpeg;
     {
@@ -598,37 +759,34 @@ class GpuExecutor : public Executor {
     }
     // (kStagers = 2 x the decode threads of one query: holding a stager through
     // the decode leaves concurrent queries' misses decoding in parallel)
-    Stager st = take_stager();
+    auto st = take_stager();
     void* dev = nullptr;
     int img_h = 0, img_w = 0;
     size_t bytes = 0;
     try {
-      DMLC_HIP_CHECK(hipSetDevice(devices_[0]));
-      // decoded straight into the stager's pinned buffer: no RGB vector to
-      // zero-fill and copy per query image
       decode_jpeg_into(jpeg.data(), jpeg.size(), [&](int w, int h) {
         img_w = w;
         img_h = h;
         bytes = (size_t)w * h * 3;
-        if (st.pinned_bytes < bytes) {
-          if (st.pinned) DMLC_HIP_CHECK(hipHostFree(st.pinned));
-          st.pinned = nullptr;
-          st.pinned_bytes = 0;
-          DMLC_HIP_CHECK(hipHostMalloc(&st.pinned, bytes, hipHostMallocDefault));
-          st.pinned_bytes = bytes;
-        }
-        return (uint8_t*)st.pinned;
+        st->ensure_pinned(bytes);
+        return (uint8_t*)st->pinned[0];
       });
-      DMLC_HIP_CHECK(hipMallocAsync(&dev, bytes, st.stream));
-      DMLC_HIP_CHECK(hipMemcpyAsync(dev, st.pinned, bytes, hipMemcpyHostToDevice, st.stream));
-      DMLC_HIP_CHECK(hipStreamSynchronize(st.stream));  // resident before it is visible
+      hipStream_t s = st->stream(home);
+      DMLC_HIP_CHECK(hipSetDevice(home));
+      // plain hipMalloc: peer-mapped for the other GPUs' resize kernels
+      // (stream-ordered pool memory would need per-pool access grants)
+      DMLC_HIP_CHECK(hipMalloc(&dev, std::max<size_t>(bytes, 256)));
+      DMLC_HIP_CHECK(hipMemcpyAsync(dev, st->pinned[0], bytes, hipMemcpyHostToDevice, s));
+      DMLC_HIP_CHECK(hipStreamSynchronize(s));  // resident before it is visible
     } catch (...) {
       give_stager(st);
+      if (dev) (void)hipFree(dev);
       throw;
     }
     give_stager(st);
     std::lock_guard<std::mutex> g(cache_mu_);
     if (cache_.count(path)) {  // raced with another stager
+      (void)hipSetDevice(home);
       (void)hipFree(dev);
       return;
     }
@@ -639,54 +797,62 @@ class GpuExecutor : public Executor {
       --victim;
       auto it = cache_.find(*victim);
       if (it->second.pins > 0) continue;
+      (void)hipSetDevice(it->second.device);
       (void)hipFree(it->second.dev);  // unpinned: no queued kernel reads it
       cache_bytes_ -= it->second.bytes;
+      cache_bytes_dev_[it->second.device] -= it->second.bytes;
       cache_.erase(it);
       victim = lru_.erase(victim);
       ++stats_.evictions;
     }
     Entry en;
     en.dev = dev;
+    en.device = home;
     en.h = img_h;
     en.w = img_w;
     en.bytes = bytes;
     lru_.push_front(path);
     en.lru = lru_.begin();
     cache_bytes_ += bytes;
+    cache_bytes_dev_[home] += bytes;
     cache_.emplace(path, en);
   }
 
   std::vector<int> devices_;
-  int max_batch_, min_shard_;
-  mutable std::mutex models_mu_;
-  std::map<std::string, std::shared_ptr<ModelSlot>> models_;
+  int max_batch_, lanes_;
+  std::set<std::pair<int, int>> peers_;  // (reader, owner) with peer access enabled
+  std::unique_ptr<dp::Fleet> fleet_;
+  std::mutex weights_mu_;
+  std::map<std::string, std::shared_ptr<const WeightMap>> weights_;  // host copies (fresh instances build from them)
+  std::map<std::string, std::shared_ptr<HbmBlob>> hbm_blobs_;  // under blob_mu_
   mutable std::mutex cache_mu_;
   std::unordered_map<std::string, Entry> cache_;
   std::list<std::string> lru_;
   size_t cache_bytes_ = 0, cache_cap_;
+  std::map<int, size_t> cache_bytes_dev_;
   CacheStats stats_;
   std::mutex stager_mu_;
   std::condition_variable stager_cv_;
-  std::vector<Stager> free_stagers_;
+  std::vector<std::shared_ptr<Stager>> free_stagers_;
 };
 
 }  // namespace
 
 std::unique_ptr<Executor> make_executor(const std::string& backend, const std::vector<int>& devices, int max_batch,
-                                        size_t cache_bytes, int min_shard) {
+                                        size_t cache_bytes, int min_shard, int lanes) {
   std::string b = backend;
   if (b == "auto") b = hip_device_count() > 0 ? "gpu" : "cpu";
   if (b == "gpu") {
     for (int d : devices)
       if (d < 0 || hip_device_count() <= d) throw std::runtime_error("no HIP device " + std::to_string(d));
-    return std::make_unique<GpuExecutor>(devices, max_batch, cache_bytes, min_shard);
+    return std::make_unique<GpuExecutor>(devices, max_batch, cache_bytes, min_shard, lanes);
   }
   if (b == "cpu") return std::make_unique<CpuExecutor>();
   throw std::invalid_argument("unknown executor backend: " + backend);
 }
 
 std::unique_ptr<Executor> make_executor(const std::string& backend, int device, int max_batch, size_t cache_bytes) {
-  return make_executor(backend, std::vector<int>{device}, max_batch, cache_bytes, 1);
+  return make_executor(backend, std::vector<int>{device}, max_batch, cache_bytes, 32, 2);
 }
 
 }  // namespace dmlc

@@ -13,6 +13,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <stdexcept>
 #include <string>
 #include <vector>
 
@@ -65,8 +66,23 @@ class Executor {
   virtual std::vector<std::string> blob_keys() const;
   virtual std::string blob_location() const { return "host"; }
   // Classify every image of a staged u8 shard blob (csrc/serve/shard.h), in
-  // order. GPU: read straight from HBM and scattered over the executor's GPUs.
+  // order. GPU: read in place from the HBM slices of the blob, each slice on
+  // the partition GPU that holds it where possible.
   virtual std::vector<Prediction> predict_blob(const std::string& model, const std::string& key);
+  // Images [first, first + n) of a staged shard blob (a shard job's query).
+  virtual std::vector<Prediction> predict_blob_range(const std::string& model, const std::string& key, int64_t first,
+                                                     int64_t n);
+
+  // Several GPUs (GPU executor): the job order for the partition rule
+  // (reference: first floor(n/2) GPUs to the first job,
+  // src/services.rs:199-211), a human-readable placement, and declaring a GPU
+  // lost (the fleet rebalances over the survivors).
+  virtual void set_jobs(const std::vector<std::string>& models) { (void)models; }
+  virtual std::string placement() const { return backend(); }
+  virtual void lose_device(int device) {
+    (void)device;
+    throw std::runtime_error("lose_device: not a multi-GPU executor");
+  }
 
  protected:
   mutable std::mutex blob_mu_;
@@ -77,11 +93,13 @@ class Executor {
 // cache_bytes: HBM budget for decoded images (GPU executor).
 std::unique_ptr<Executor> make_executor(const std::string& backend, int device, int max_batch,
                                         size_t cache_bytes = (size_t)4 << 30);
-// Several GPUs of this node (GPU executor): one engine per GPU and model; a
-// query batch is resized into one u8 batch on devices[0] and scattered over
-// the GPUs with RCCL (csrc/comm), each GPU taking >= min_shard images.
+// Several GPUs of this node (GPU executor, csrc/comm/fleet.h): the GPUs are
+// split between the loaded models; a query goes to the least-loaded GPU of
+// its model's partition, and a batch of >= 2 x min_shard images is scattered
+// over the partition with RCCL instead.
+// lanes: concurrent forwards per GPU and model (one model instance each).
 std::unique_ptr<Executor> make_executor(const std::string& backend, const std::vector<int>& devices, int max_batch,
-                                        size_t cache_bytes, int min_shard);
+                                        size_t cache_bytes, int min_shard, int lanes = 2);
 int hip_device_count();
 
 // Host-side reference preprocessing (same rule as csrc/kernels/preprocess.hip):

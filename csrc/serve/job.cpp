@@ -15,6 +15,17 @@ uint32_t bounded(Reader& r, size_t elem_bytes) {
   if ((uint64_t)n * elem_bytes > r.left()) throw WireError("count exceeds message");
   return n;
 }
+void write_tail(Writer& w, const Job& j) {
+  w.u32((uint32_t)j.source.size());
+  for (const auto& s : j.source) w.str(s);
+  w.i32(j.failed);
+}
+void read_tail(Reader& r, Job& j) {
+  const uint32_t n = bounded(r, 4);
+  j.source.clear();
+  for (uint32_t i = 0; i < n; ++i) j.source.push_back(r.str());
+  j.failed = r.i32();
+}
 }  // namespace
 
 void write_job(Writer& w, const Job& j) {
@@ -30,6 +41,7 @@ void write_job(Writer& w, const Job& j) {
   w.i64(j.started_us);
   w.i64(j.first_done_us);
   w.i64(j.elapsed_us);
+  write_tail(w, j);
 }
 
 void write_job_delta(Writer& w, const Job& j, uint32_t from) {
@@ -47,6 +59,7 @@ void write_job_delta(Writer& w, const Job& j, uint32_t from) {
   w.i64(j.started_us);
   w.i64(j.first_done_us);
   w.i64(j.elapsed_us);
+  write_tail(w, j);
 }
 
 bool read_job_delta(Reader& r, Job& j) {
@@ -66,7 +79,9 @@ bool read_job_delta(Reader& r, Job& j) {
   d.started_us = r.i64();
   d.first_done_us = r.i64();
   d.elapsed_us = r.i64();
-  if (from > 0 && (j.durations_us.size() != from || j.done_us.size() != from || j.model_name != d.model_name))
+  read_tail(r, d);
+  if (from > 0 && (j.durations_us.size() != from || j.done_us.size() != from || j.model_name != d.model_name ||
+                   j.source != d.source))
     return false;
   d.durations_us = from ? j.durations_us : std::vector<int64_t>();
   d.done_us = from ? j.done_us : std::vector<int64_t>();
@@ -92,6 +107,7 @@ Job read_job(Reader& r) {
   j.started_us = r.i64();
   j.first_done_us = r.i64();
   j.elapsed_us = r.i64();
+  read_tail(r, j);
   return j;
 }
 
@@ -136,6 +152,12 @@ std::string format_job_report(int n, const Job& j) {
            n, j.model_name.c_str(), j.correct, j.finished, acc, s.count, s.mean, s.stddev, s.p50, s.p90, s.p95,
            s.p99);
   std::string out = buf;
+  if (!j.source.empty()) {
+    std::string src;
+    for (const auto& x : j.source) src += (src.empty() ? "" : ", ") + x;
+    out += "\n\tData: SDFS shards " + src;
+  }
+  if (j.failed > 0) out += "\n\tUnanswered: " + std::to_string(j.failed) + " images (dropped after retries)";
   if (j.finished > 0 && j.elapsed_us > 0) {
     const double secs = j.elapsed_us * 1e-6;
     snprintf(buf, sizeof(buf), "\n\tThroughput: %.2f queries/s", j.finished / secs);

@@ -31,6 +31,11 @@ struct Job {
   // each measured on its own steady clock (the Throughput line; wall clocks
   // of different leaders are never subtracted from each other).
   int64_t elapsed_us = 0;
+  // Where the queries come from: empty = the dataset's label list (the
+  // reference, src/services.rs:410-411); else SDFS shard names, in order
+  // (labelled u8 shards, csrc/serve/shard.h: BASELINE config 3).
+  std::vector<std::string> source;
+  int32_t failed = 0;  // images of queries no member answered after every retry (dropped)
 
   void add_result(bool ok, int64_t dur_us, int64_t done_wall_us = 0) {
     ++finished;

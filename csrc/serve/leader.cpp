@@ -19,6 +19,7 @@ LeaderService::LeaderService(LeaderConfig cfg, MembershipService* ms, MemberServ
   }
   running_.assign(jobs_.size(), false);
   retry_.resize(jobs_.size());
+  segs_.resize(jobs_.size());
   job_inflight_.reset(new std::atomic<int>[jobs_.size()]);
   for (size_t j = 0; j < jobs_.size(); ++j) job_inflight_[j] = 0;
 }
@@ -297,16 +298,83 @@ void LeaderService::train(const std::string& filename, const std::string& model_
     }
 }
 
-void LeaderService::predict() {
+void LeaderService::predict(const std::vector<std::string>* shards) {
   std::lock_guard<std::mutex> g(runners_mu_);
   for (size_t j = 0; j < jobs_.size(); ++j) {
     {
       std::lock_guard<std::mutex> g2(mu_);
       if (running_[j]) continue;
+      if (shards && jobs_[j].source != *shards) {  // another data source: the job starts over
+        Job fresh;
+        fresh.model_name = jobs_[j].model_name;
+        fresh.assigned = jobs_[j].assigned;
+        fresh.source = *shards;
+        jobs_[j] = std::move(fresh);
+      }
       running_[j] = true;
     }
     runners_.emplace_back([this, j] { run_job(j); });
   }
+}
+
+std::vector<Id> LeaderService::shard_holders(const std::string& file) {
+  const int v = latest_version(file);
+  const auto active = ms_->active_ids();
+  std::vector<Id> out;
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = dir_.find(file);
+  if (it == dir_.end()) return out;
+  for (const auto& rep : it->second)
+    if (rep.second.count(v) && active.count(rep.first)) out.push_back(rep.first);
+  return out;
+}
+
+// The job's shards: size and first label of each, from a live replica holder
+// (M_SHARD_INFO); the job's index space is the shards back to back.
+bool LeaderService::load_segments(size_t j, const std::vector<std::string>& source) {
+  std::vector<Seg> segs;
+  size_t start = 0;
+  for (const auto& f : source) {
+    bool got = false;
+    std::string why = "no live replica holder";
+    for (const Id& h : shard_holders(f)) {
+      try {
+        Writer w;
+        w.str(f);
+        Reader r(RpcClient::shared().call(h.host(), member_port(h.port()), M_SHARD_INFO, w.data(), 10000));
+        (void)r.i32();  // version
+        Seg sg;
+        sg.file = f;
+        sg.start = start;
+        sg.n = r.u32();
+        (void)r.u32();
+        (void)r.u32();
+        sg.label0 = r.u32();
+        if (!r.boolean()) {
+          why = "not a labelled shard";
+          break;
+        }
+        if ((size_t)sg.label0 + sg.n > labels_.entries.size()) {
+          why = "labels beyond the label table";
+          break;
+        }
+        start += sg.n;
+        segs.push_back(sg);
+        got = true;
+        break;
+      } catch (const std::exception& e) {
+        why = h.address + ": " + e.what();
+      }
+    }
+    if (!got) {
+      DMLC_LOG_WARN("job over shards: " << f << ": " << why);
+      out_line("predict: shard " + f + ": " + why);
+      return false;
+    }
+  }
+  std::lock_guard<std::mutex> g(mu_);
+  segs_[j] = std::move(segs);
+  return true;
 }
 
 std::vector<Job> LeaderService::jobs() const {
@@ -348,16 +416,27 @@ bool LeaderService::benched(const std::string& addr) {  // under rng_mu_
   return true;
 }
 
-std::optional<Id> LeaderService::retry_target(size_t j, const std::set<std::string>& tried) {
+std::optional<Id> LeaderService::retry_target(size_t j, const std::set<std::string>& tried,
+                                               const std::vector<Id>* only) {
   std::vector<Id> pool;
   {
     std::lock_guard<std::mutex> g(mu_);
     pool = jobs_[j].assigned;  // the job's own members first
   }
+  if (only) {  // shard queries: replica holders only, the job's own first
+    std::vector<Id> mine;
+    for (const auto& id : *only)
+      if (std::find(pool.begin(), pool.end(), id) != pool.end()) mine.push_back(id);
+    pool = mine;
+  }
   for (int pass = 0; pass < 2; ++pass) {
     if (pass == 1) {
-      auto a = ms_->active_ids();
-      pool.assign(a.begin(), a.end());
+      if (only) {
+        pool = *only;
+      } else {
+        auto a = ms_->active_ids();
+        pool.assign(a.begin(), a.end());
+      }
     }
     std::vector<Id> cand;
     {
@@ -374,20 +453,36 @@ void LeaderService::run_job(size_t j) {
   std::string model;
   size_t idx;
   int64_t elapsed0;
+  std::vector<std::string> source;
   {
     std::lock_guard<std::mutex> g(mu_);
     model = jobs_[j].model_name;
-    idx = (size_t)jobs_[j].finished;  // resume point (src/services.rs:410-411)
+    // resume point (src/services.rs:410-411): queries answered or dropped
+    idx = (size_t)jobs_[j].finished + (size_t)jobs_[j].failed;
     elapsed0 = jobs_[j].elapsed_us;
+    source = jobs_[j].source;
     retry_[j].clear();
+    segs_[j].clear();
+  }
+  if (!source.empty() && !load_segments(j, source)) {
+    std::lock_guard<std::mutex> g(mu_);
+    running_[j] = false;
+    return;
+  }
+  std::vector<Seg> segs;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    segs = segs_[j];
   }
   const int64_t run0 = steady_us();
   const auto& L = labels_.entries;
-  const size_t limit = cfg_.job_limit > 0 ? std::min(L.size(), (size_t)cfg_.job_limit) : L.size();
+  size_t total = L.size();
+  if (!source.empty()) total = segs.empty() ? 0 : segs.back().start + segs.back().n;
+  const size_t limit = cfg_.job_limit > 0 ? std::min(total, (size_t)cfg_.job_limit) : total;
   auto next_tick = std::chrono::steady_clock::now();
   for (;;) {
     if (stop_.load()) break;
-    std::pair<size_t, size_t> range{0, 0};  // (first, n): a failed query again, else the next labels
+    Range range;  // a failed query again, else the next labels / shard images
     {
       std::lock_guard<std::mutex> g(mu_);
       if (!retry_[j].empty()) {
@@ -395,7 +490,7 @@ void LeaderService::run_job(size_t j) {
         retry_[j].pop_front();
       }
     }
-    if (range.second == 0) {
+    if (range.n == 0) {
       if (idx >= limit) {
         // all issued: wait for the stragglers, which may hand a query back
         if (job_inflight_[j].load() == 0) {
@@ -405,8 +500,11 @@ void LeaderService::run_job(size_t j) {
         std::this_thread::sleep_for(std::chrono::milliseconds(1));
         continue;
       }
-      range = {idx, std::min((size_t)cfg_.query_batch, limit - idx)};
-      idx += range.second;
+      range.first = idx;
+      range.n = std::min((size_t)cfg_.query_batch, limit - idx);
+      for (const auto& sg : segs)  // a shard query never spans two shards
+        if (idx >= sg.start && idx < sg.start + sg.n) range.n = std::min(range.n, sg.start + sg.n - idx);
+      idx += range.n;
     }
     if (cfg_.adaptive_window <= 0) {
       next_tick += std::chrono::milliseconds(cfg_.query_interval_ms);
@@ -418,13 +516,24 @@ void LeaderService::run_job(size_t j) {
       std::lock_guard<std::mutex> g(mu_);
       pool = jobs_[j].assigned;
     }
-    if (pool.empty()) {
+    if (!segs.empty()) {
+      // a shard query goes to a replica holder (its bytes are resident there),
+      // one of the job's own members when it can
+      const Seg* sg = nullptr;
+      for (const auto& x : segs)
+        if (range.first >= x.start && range.first < x.start + x.n) sg = &x;
+      const std::vector<Id> holders = sg ? shard_holders(sg->file) : std::vector<Id>{};
+      std::vector<Id> mine;
+      for (const auto& h : holders)
+        if (std::find(pool.begin(), pool.end(), h) != pool.end()) mine.push_back(h);
+      pool = mine.empty() ? holders : mine;
+    } else if (pool.empty()) {
       auto a = ms_->active_ids();
       pool.assign(a.begin(), a.end());
     }
     if (pool.empty()) {
       std::lock_guard<std::mutex> g(mu_);
-      retry_[j].push_front(range);
+      retry_[j].push_front(range);  // no member at all: not an attempt
       if (cfg_.adaptive_window > 0) std::this_thread::sleep_for(std::chrono::milliseconds(50));
       continue;
     }
@@ -448,26 +557,49 @@ void LeaderService::run_job(size_t j) {
       std::lock_guard<std::mutex> g(rng_mu_);
       member_inflight_[target.address]++;
     }
-    submit([this, j, model, target, range, run0, elapsed0] { query(j, model, target, range.first, range.second, run0, elapsed0); });
+    submit([this, j, model, target, range, run0, elapsed0] { query(j, model, target, range, run0, elapsed0); });
   }
   std::lock_guard<std::mutex> g(mu_);
   running_[j] = false;
 }
 
-// One query (a batch of `n` labels from `first`). A member that fails (no
-// answer, or ok=false: e.g. it has no such model) is benched for a
-// background period and the query moves to another member of the job's
-// pool (then any live member), with its in-flight count; latency is end to
-// end, retries included. A query no member could answer goes back to the job.
-void LeaderService::query(size_t j, const std::string& model, Id target, size_t first, size_t n, int64_t run0,
+// One query (a batch of `n` labels / shard images from `first`). A member
+// that fails (no answer, or ok=false: e.g. it has no such model) is benched
+// for a background period and the query moves to another member of the
+// job's pool (then any live member; for a shard query, any live replica
+// holder), with its in-flight count; latency is end to end, retries
+// included. A query no member could answer goes back to the job, with a
+// back-off, at most max_attempts times in all; then it is dropped (the
+// reference dropped failed queries) and counted as unanswered.
+void LeaderService::query(size_t j, const std::string& model, Id target, Range range, int64_t run0,
                           int64_t elapsed0) {
   const auto& L = labels_.entries;
+  const size_t first = range.first, n = range.n;
+  const Seg* sg = nullptr;
+  std::vector<Seg> segs;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    segs = segs_[j];
+  }
+  for (const auto& x : segs)
+    if (first >= x.start && first < x.start + x.n) sg = &x;
+  if (range.attempts > 0)  // a requeued query: back off before sending it again
+    std::this_thread::sleep_for(std::chrono::milliseconds(std::min(cfg_.bg_ms, 50 * range.attempts)));
   Writer w;
-  w.str(model).u32((uint32_t)n);
-  for (size_t i = 0; i < n; ++i) w.str(L[first + i].first);
+  std::vector<Id> holders;
+  if (sg) {
+    w.str(model).str(sg->file).u64(first - sg->start).u32((uint32_t)n);
+    holders = shard_holders(sg->file);
+  } else {
+    w.str(model).u32((uint32_t)n);
+    for (size_t i = 0; i < n; ++i) w.str(L[first + i].first);
+  }
+  // truth of image i: its label index
+  auto truth_of = [&](size_t i) -> size_t { return sg ? sg->label0 + (first - sg->start) + i : first + i; };
   const int64_t t0 = steady_us();
   Id tgt = target;
   std::vector<std::pair<double, std::string>> res;
+  std::vector<int> cls;
   bool got = false;
   std::set<std::string> tried;
   DMLC_TRACE("leader.query");
@@ -475,13 +607,24 @@ void LeaderService::query(size_t j, const std::string& model, Id target, size_t 
     bool transport = false;
     std::string why;
     try {
-      const std::string resp = RpcClient::shared().call(tgt.host(), member_port(tgt.port()), M_PREDICT, w.data(), 120000);
+      // the reference connects anew for every query (src/services.rs:420); by
+      // default the pooled connection is reused (--new-conn-per-query: fresh)
+      const std::string resp = RpcClient::shared().call(tgt.host(), member_port(tgt.port()),
+                                                        sg ? M_PREDICT_RANGE : M_PREDICT, w.data(), 120000,
+                                                        cfg_.new_conn_per_query);
       Reader r(resp);
       if (r.boolean()) {
         const uint32_t m = r.u32();
         for (uint32_t i = 0; i < m; ++i) {
-          const double p = r.f64();
-          res.emplace_back(p, r.str());
+          if (sg) {
+            const int c = r.i32();
+            const double p = r.f64();
+            cls.push_back(c);
+            res.emplace_back(p, labels_.text(c));
+          } else {
+            const double p = r.f64();
+            res.emplace_back(p, r.str());
+          }
         }
         got = true;
         break;
@@ -498,7 +641,7 @@ void LeaderService::query(size_t j, const std::string& model, Id target, size_t 
       bench_until_[tgt.address] = steady_us() + (int64_t)cfg_.bg_ms * 1000;
     }
     if (transport) std::this_thread::sleep_for(std::chrono::milliseconds(std::min(cfg_.bg_ms, 200)));
-    auto next = retry_target(j, tried);
+    auto next = retry_target(j, tried, sg ? &holders : nullptr);
     if (!next) break;
     {
       std::lock_guard<std::mutex> g(rng_mu_);
@@ -509,31 +652,38 @@ void LeaderService::query(size_t j, const std::string& model, Id target, size_t 
   }
   const int64_t dur = steady_us() - t0;
   std::vector<std::string> lines;
+  bool dropped = false;
   {
     std::lock_guard<std::mutex> g(mu_);
     if (got) {
       const int64_t now = wall_us();
       if (jobs_[j].first_done_us == 0) jobs_[j].first_done_us = now;
       for (size_t i = 0; i < n; ++i) {
-        const std::string& truth = L[first + i].second;
+        const size_t t = truth_of(i);
+        const std::string& truth = L[t].second;
         const bool have = i < res.size() && res[i].first >= 0;
-        const bool ok = have && res[i].second == truth;
+        const bool ok = have && (sg ? cls[i] == (int)t : res[i].second == truth);
         jobs_[j].add_result(ok, dur, now);
         if (!have) {
-          lines.push_back(model + " - " + L[first + i].first + ": no image");
+          lines.push_back(model + " - " + L[t].first + ": no image");
         } else if (cfg_.print_predictions) {
           char buf[64];
           snprintf(buf, sizeof(buf), " (%.2f%%)", res[i].first * 100.0);
-          lines.push_back(model + " - " + L[first + i].first + ": " + res[i].second + buf +
+          lines.push_back(model + " - " + L[t].first + ": " + res[i].second + buf +
                           (ok ? "" : " (should be " + truth + ")"));
         }
       }
       jobs_[j].elapsed_us = std::max(jobs_[j].elapsed_us, elapsed0 + (steady_us() - run0));
+    } else if (range.attempts + 1 >= std::max(1, cfg_.max_attempts)) {
+      jobs_[j].failed += (int32_t)n;
+      dropped = true;
     } else {
-      retry_[j].push_back({first, n});
+      retry_[j].push_back({first, n, range.attempts + 1});
     }
   }
-  if (!got) DMLC_LOG_WARN("predict " << model << " " << L[first].first << "+" << n << ": no member answered; requeued");
+  if (!got)
+    DMLC_LOG_WARN("predict " << model << " " << L[truth_of(0)].first << "+" << n << ": no member answered; "
+                             << (dropped ? "dropped" : "requeued"));
   for (const auto& l : lines) out_line(l);
   {
     std::lock_guard<std::mutex> g(rng_mu_);
@@ -710,8 +860,16 @@ void LeaderService::register_handlers() {
     }
     throw std::runtime_error("predict-shard " + f + ": " + last_err);
   });
-  server_->handle(L_PREDICT, [this](Reader&) {
-    predict();
+  server_->handle(L_PREDICT, [this](Reader& r) {
+    if (r.left() >= 4) {  // `predict <shard>...` / `predict dataset`
+      const uint32_t k = r.u32();
+      if (k > 4096) throw std::runtime_error("predict: too many shards");
+      std::vector<std::string> shards;
+      for (uint32_t i = 0; i < k; ++i) shards.push_back(r.str());
+      predict(&shards);
+    } else {
+      predict();
+    }
     return std::string();
   });
   server_->handle(L_JOBS, [this](Reader&) {

@@ -52,6 +52,8 @@ struct LeaderConfig {
   int adaptive_window = 0;  // >0: closed-loop rate, queries in flight per member
   int job_limit = 0;  // queries per job (0 = every label, as the reference)
   bool print_predictions = true;
+  bool new_conn_per_query = false;  // the reference's per-query TCP connect (src/services.rs:420)
+  int max_attempts = 3;  // sends of one query (across members and requeues) before it is dropped
   std::vector<std::string> job_models = {"resnet18", "alexnet"};
 };
 
@@ -70,7 +72,10 @@ class LeaderService {
   void del(const std::string& filename);
   std::vector<std::pair<Id, std::vector<int>>> ls(const std::string& filename);
   void train(const std::string& filename, const std::string& model_name);
-  void predict();
+  // Start the jobs that are not running. shards == nullptr: each job keeps
+  // its source (resume); otherwise the jobs take their queries from these
+  // SDFS shards (empty: the dataset's labels), starting over if that changes.
+  void predict(const std::vector<std::string>* shards = nullptr);
   std::vector<Job> jobs() const;
 
  private:
@@ -79,7 +84,21 @@ class LeaderService {
   std::set<Id> put_version(const Id* src_id, const std::string* src_spec, const std::string& filename, int version);
   bool copy_to(const Id& src, const std::string& src_spec, const Id& dest, const std::string& dest_spec);
   std::optional<Id> get_version(const std::string& filename, int version, const Id& dest, const std::string& dest_spec);
+  // One query's images: [first, first + n) of the job's index space, sent
+  // `attempts` times so far.
+  struct Range {
+    size_t first = 0, n = 0;
+    int attempts = 0;
+  };
+  // A labelled shard of a job's source: global indices [start, start + n).
+  struct Seg {
+    std::string file;
+    size_t start = 0, n = 0;
+    uint32_t label0 = 0;
+  };
   void run_job(size_t j);
+  bool load_segments(size_t j, const std::vector<std::string>& source);
+  std::vector<Id> shard_holders(const std::string& file);
   void rereplicate_loop();
   void assign_loop();
   void succession_loop();
@@ -104,11 +123,12 @@ class LeaderService {
   std::map<std::string, int> member_inflight_;         // per member address, under rng_mu_
   Id pick_target(const std::vector<Id>& pool);
   bool benched(const std::string& addr);  // under rng_mu_
-  std::optional<Id> retry_target(size_t j, const std::set<std::string>& tried);
-  void query(size_t j, const std::string& model, Id target, size_t first, size_t n, int64_t run0, int64_t elapsed0);
+  std::optional<Id> retry_target(size_t j, const std::set<std::string>& tried, const std::vector<Id>* only);
+  void query(size_t j, const std::string& model, Id target, Range range, int64_t run0, int64_t elapsed0);
   void submit(std::function<void()> task);
   std::map<std::string, int64_t> bench_until_;          // member -> steady us, under rng_mu_
-  std::vector<std::deque<std::pair<size_t, size_t>>> retry_;  // per job: queries handed back, under mu_
+  std::vector<std::deque<Range>> retry_;  // per job: queries handed back, under mu_
+  std::vector<std::vector<Seg>> segs_;    // per job: shard segments of its source, under mu_
   std::mutex pool_mu_;
   std::condition_variable pool_cv_;
   std::deque<std::function<void()>> tasks_;

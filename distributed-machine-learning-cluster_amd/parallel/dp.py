@@ -52,6 +52,10 @@ class DataParallelRunner:
         scatter mode; every rank's own pool in local mode). Returns
         {steps, images, step_ms} (step_ms: unpipelined runs only)."""
         ptr, count = (pool.data_ptr(), pool.shape[0]) if pool is not None else (0, 0)
+        if pool is not None:
+            # the native streams do not wait on torch's: whatever produced
+            # the pool on the current stream must be done first
+            torch.cuda.current_stream(pool.device).synchronize()
         return self._r.run(ptr, count, first, n, pipelined=pipelined)
 
     def last_results(self) -> tuple[list[int], list[float]]:
@@ -77,6 +81,8 @@ class NodeGroup:
         Returns (idx int32 [N], prob f32 [N], stats dict)."""
         if not images.is_contiguous() or images.dtype != torch.uint8:
             raise ValueError("images must be contiguous uint8 [N, S, S, 3]")
+        # the native streams do not wait on torch's current stream
+        torch.cuda.current_stream(images.device).synchronize()
         idx, prob, st = self._g.classify(images.data_ptr(), images.shape[0])
         return torch.from_numpy(idx), torch.from_numpy(prob), st
 

@@ -5,7 +5,8 @@ until its answer is back: connect + RPC + JPEG decode + resize + forward +
 softmax/top-1 (``Instant`` around ``MemberClient::spawn(..).predict(..)``,
 src/services.rs:419-424; published mean 158.94 ms for ResNet18,
 CS425MP4Report.pdf p.2). This runs the same thing through this framework: a
-one-node cluster (leader + member with the GPU executor) runs a ResNet18
+one-node cluster (a new TCP connection per query, as the reference's
+``MemberClient::spawn``; the default reuses pooled connections) (leader + member with the GPU executor) runs a ResNet18
 predict job with one query in flight at a time (``--adaptive-window 1``,
 batch 1), over JPEGs that are decoded per query (no HBM prefetch), and the
 leader records every query's latency exactly as the reference's job does.
@@ -56,7 +57,7 @@ def query_latency(n: int = 200, model: str = "resnet18", device: int = 0, port: 
             desc = f"synthetic 500x375 JPEGs ({n})"
         ckpt = write_random_checkpoint(model, os.path.join(root, f"{model}.ot"), seed=0)
         extra = ["--jobs", model, "--job-limit", str(n), "--adaptive-window", "1", "--query-batch", "1",
-                 "--quiet-predictions", "--device", str(device), "--max-batch", "8"]
+                 "--quiet-predictions", "--device", str(device), "--max-batch", "8", "--new-conn-per-query"]
         cl = LocalCluster(1, port, os.path.join(root, "c"), labels, n_leaders=1, executor=executor,
                           dataset=dataset, models=f"{model}={ckpt}", extra=extra)
         with cl:

@@ -112,3 +112,51 @@ def test_group_rejects_coordinator_failure():
     imgs = _images(10)
     with pytest.raises(ValueError):
         C.dp_host_run(imgs, 3, 4, mode="group", fail_member=0)
+
+
+# ---- the host fake behaves like RCCL point-to-point, not like a mailbox
+
+def test_fake_is_rendezvous_a_misordered_exchange_times_out():
+    """Both ranks send before they receive: RCCL would hang (a send needs its
+    receive posted), and so must the fake (it used to buffer the sends and
+    pass). Both sides fail with a timeout and nothing is left posted."""
+    bad = C.host_order_probe(bad=True, timeout_ms=300)
+    assert "timed out" in bad["err0"] and "timed out" in bad["err1"], bad
+    assert not bad["ok"]
+    assert bad["pending"] == 0
+    good = C.host_order_probe(bad=False, timeout_ms=2000)
+    assert good["err0"] == "" and good["err1"] == "" and good["ok"], good
+    assert good["pending"] == 0
+
+
+# ---- bench.py's per-rank protocol, one thread per rank (= one process per GPU)
+
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
+@pytest.mark.parametrize("mode", ["scatter", "staged"])
+@pytest.mark.parametrize("weight", [1.0, 0.85])
+def test_bench_protocol(world, mode, weight):
+    """stage (staged mode), prime run, warmup, timed run and the unpipelined
+    latency run, exactly as bench.py issues them, with the coordinator's
+    shard weighted down (--coord-weight): every rank runs every step and the
+    coordinator's last answers are its images' classes in global order."""
+    per = 6
+    counts = C.dp_weighted_counts(per, world, weight)
+    G = sum(counts)
+    assert G == per * world
+    pool = np.random.default_rng(world).integers(0, 256, size=(2 * G, H, W, 3), dtype=np.uint8)
+    out = C.dp_host_bench(pool, world, per, coord_weight=weight, input_mode=mode, lanes=2, prime=4, warmup=3,
+                          steps=7, latency=2)
+    assert out["answers_ok"]
+    assert out["steps"] == [[4, 3, 7, 2]] * world
+    assert out["counts"] == counts
+
+
+@pytest.mark.parametrize("per,world,w,want", [
+    (256, 8, 1.0, [256] * 8),
+    (256, 8, 0.85, [218] + [262] * 3 + [261] * 4),
+    (256, 2, 0.5, [128, 384]),
+    (10, 1, 0.5, [10]),
+])
+def test_weighted_counts(per, world, w, want):
+    got = C.dp_weighted_counts(per, world, w)
+    assert got == want and sum(got) == per * world

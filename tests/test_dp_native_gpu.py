@@ -104,7 +104,7 @@ def test_runner_stage_then_local_run(gpu, eng):
     dst = torch.zeros_like(src)
     torch.cuda.synchronize()
     r = C.DpRunner(eng._e, 1, 0, b"", b"", 64, scatter=False, lanes=1)
-    r.stage(src.data_ptr(), dst.data_ptr(), 64)
+    r.stage(src.data_ptr(), dst.data_ptr())
     assert torch.equal(dst, src)
     out = r.run(dst.data_ptr(), 64, 0, 2)
     r.sync()

@@ -183,32 +183,39 @@ def test_fast_paths_match_plain_paths_odd_batches(gpu, B):
 
 def test_bench_path_b256_matches_fp32(gpu):
     """The exact bench.py configuration — ResNet18, B=256, default kernel
-    selection, hipGraph replay, driven by the native DP runner
-    (csrc/comm/dp.cpp) — against fp32 torch.nn: top-1 identical except on
-    near-ties, probabilities within bf16 tolerance, logits (same fast paths
-    with the logits output) within 3% relative L2."""
+    selection, hipGraph replay, two compute lanes (the second a copied
+    engine on its own stream), primed pipeline, driven by the native DP
+    runner (csrc/comm/runner.cpp) — against fp32 torch.nn: top-1 identical
+    except on near-ties, probabilities within bf16 tolerance, for a step on
+    each lane; logits (same fast paths with the logits output) within 3%
+    relative L2."""
     import dmlc
-    torch.set_num_threads(min(16, torch.get_num_threads()))
     model = build("resnet18", seed=21, randomize_bn=True)
     eng = InferenceEngine("resnet18", state_dict_f32(model), max_batch=256)
     g = torch.Generator().manual_seed(22)
-    img = torch.randint(0, 256, (256, 224, 224, 3), generator=g, dtype=torch.uint8)
+    img = torch.randint(0, 256, (512, 224, 224, 3), generator=g, dtype=torch.uint8)
     pool = img.to(gpu)
     torch.cuda.synchronize()
-    r = dmlc.native().DpRunner(eng._e, 1, 0, b"", b"", 256)
-    r.run(pool.data_ptr(), 256, 0, 3)
-    r.sync()
-    idx, prob = r.last_results()
-    idx, prob = torch.tensor(idx), torch.tensor(prob)
-    ref = _ref_logits(model, img)
-    ref_p = torch.softmax(ref, -1)
-    top2 = ref_p.topk(2, -1).values
-    near_tie = (top2[:, 0] - top2[:, 1]) < 1e-2
-    mism = idx.long() != ref.argmax(-1)
-    assert torch.all(~mism | near_tie), mism.sum().item()
-    assert torch.allclose(prob, ref_p.max(-1).values, rtol=0.1, atol=2e-3)
-    _, _, logits = eng.predict(pool, return_logits=True)
+    r = dmlc.native().DpRunner(eng._e, 1, 0, b"", b"", 256, lanes=2)
+    torch.set_num_threads(min(16, torch.get_num_threads()))
+    ref_model = model  # fp32 on the CPU: no reduced-precision GPU conv in the reference
+    # prime as bench.py does (every slot's graph captured, both lanes used)
+    r.run(pool.data_ptr(), 512, 0, 9)
+    for first, batch in ((9, 1), (10, 0)):  # step 9: lane 1 on batch 1; step 10: lane 0 on batch 0
+        r.run(pool.data_ptr(), 512, first, 1)
+        r.sync()
+        idx, prob = r.last_results()
+        idx, prob = torch.tensor(idx), torch.tensor(prob)
+        ref = _ref_logits(ref_model, img[batch * 256:(batch + 1) * 256])
+        ref_p = torch.softmax(ref, -1)
+        top2 = ref_p.topk(2, -1).values
+        near_tie = (top2[:, 0] - top2[:, 1]) < 1e-2
+        mism = idx.long() != ref.argmax(-1)
+        assert torch.all(~mism | near_tie), (first, mism.sum().item())
+        assert torch.allclose(prob, ref_p.max(-1).values, rtol=0.1, atol=2e-3), first
+    _, _, logits = eng.predict(pool[:256], return_logits=True)
     torch.cuda.synchronize()
+    ref = _ref_logits(ref_model, img[:256])
     rel = ((logits.cpu() - ref).norm() / ref.norm()).item()
     assert rel < 3e-2, rel
 
