@@ -6,6 +6,7 @@
 // `torch.cuda.current_stream().cuda_stream`.
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
+#include "../serve/shard.h"
 #include <pybind11/stl.h>
 
 #include <map>
@@ -271,6 +272,12 @@ PYBIND11_MODULE(_C, m) {
   // ---------------------------------------------------------------- .ot
   m.def("ot_load", [](const std::string& path) { return from_weight_map(ot_load(path)); });
   m.def("ot_save", [](const std::string& path, const py::dict& d) { ot_save(path, to_weight_map(d)); });
+  // where a staged shard replica's images live (csrc/serve/shard.h)
+  m.def("shard_slices", [](int64_t n, const std::vector<int>& devices) {
+    py::list out;
+    for (const auto& s : shard_slices(n, devices)) out.append(py::make_tuple(s.device, s.first, s.n));
+    return out;
+  });
 
   // ---------------------------------------------------------------- engine
   py::class_<Engine>(m, "Engine")

@@ -405,12 +405,11 @@ class GpuExecutor : public Executor {
     std::vector<int> live = fleet_->live();
     if (live.empty()) throw std::runtime_error("no live GPU to stage " + key);
     const int64_t n = b->si.n;
-    const int P = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)live.size(), n));
-    for (int k = 0; k < P; ++k) {
+    for (const ShardSlice& sl : shard_slices(n, live)) {
       HbmBlob::Piece pc;
-      pc.device = live[k];
-      pc.first = n * k / P;
-      pc.n = n * (k + 1) / P - pc.first;
+      pc.device = sl.device;
+      pc.first = sl.first;
+      pc.n = sl.n;
       DMLC_HIP_CHECK(hipSetDevice(pc.device));
       DMLC_HIP_CHECK(hipMalloc(&pc.dev, std::max<size_t>((size_t)pc.n * ib, 256)));
       b->pieces.push_back(pc);

@@ -10,9 +10,11 @@
 // dmlc.utils.shards.write_shard.
 #pragma once
 #include <cstdint>
+#include <algorithm>
 #include <cstring>
 #include <stdexcept>
 #include <string>
+#include <vector>
 
 namespace dmlc {
 
@@ -43,6 +45,27 @@ inline ShardInfo parse_shard(const uint8_t* p, size_t bytes) {
   if (s.h == 0 || s.w == 0 || s.h > 4096 || s.w > 4096) throw std::runtime_error("shard: bad image size");
   if ((uint64_t)s.n * s.image_bytes() != bytes - kShardHeader) throw std::runtime_error("shard: size mismatch");
   return s;
+}
+
+// Placement of a shard replica's images over the GPUs of a node: one
+// contiguous slice per live GPU (in the order given), as even as possible,
+// never an empty slice (fewer images than GPUs: the first n GPUs get one).
+struct ShardSlice {
+  int device = 0;
+  int64_t first = 0, n = 0;
+};
+inline std::vector<ShardSlice> shard_slices(int64_t n, const std::vector<int>& devices) {
+  if (devices.empty()) throw std::runtime_error("shard_slices: no device");
+  const int64_t P = std::max<int64_t>(1, std::min<int64_t>((int64_t)devices.size(), n));
+  std::vector<ShardSlice> out;
+  for (int64_t k = 0; k < P; ++k) {
+    ShardSlice s;
+    s.device = devices[k];
+    s.first = n * k / P;
+    s.n = n * (k + 1) / P - s.first;
+    out.push_back(s);
+  }
+  return out;
 }
 
 }  // namespace dmlc

@@ -35,9 +35,11 @@ def load_ot_jit(path: str) -> dict[str, torch.Tensor]:
     return out
 
 
-def write_random_checkpoint(arch: str, path: str, seed: int = 0, num_classes: int = 1000) -> str:
+def write_random_checkpoint(arch: str, path: str, seed: int = 0, num_classes: int = 1000,
+                            randomize_bn: bool = False) -> str:
     """Random-init weights of ``arch`` written as ``.ot`` (the reference's real
-    weights are git-LFS pointer stubs, pretrained_models/*.ot:1-3)."""
+    weights are git-LFS pointer stubs, pretrained_models/*.ot:1-3).
+    randomize_bn: non-trivial BN statistics, so predictions vary by image."""
     from ..models import build, state_dict_f32
-    save_ot(path, state_dict_f32(build(arch, num_classes, seed=seed)))
+    save_ot(path, state_dict_f32(build(arch, num_classes, seed=seed, randomize_bn=randomize_bn)))
     return path

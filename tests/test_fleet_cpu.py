@@ -63,6 +63,21 @@ def _small_queries(n_imgs, k, seed=0, models=("resnet18", "alexnet"), max_n=3):
     return qs
 
 
+@pytest.mark.parametrize("n,devices,want", [
+    (1000, list(range(8)), [(d, 125 * d, 125) for d in range(8)]),
+    (10, [0, 1, 2, 4], [(0, 0, 2), (1, 2, 3), (2, 5, 2), (4, 7, 3)]),   # after a loss: the live GPUs only
+    (3, list(range(8)), [(0, 0, 1), (1, 1, 1), (2, 2, 1)]),             # no empty slice
+    (7, [5], [(5, 0, 7)]),
+])
+def test_shard_replica_slices_one_per_live_gpu(n, devices, want):
+    """A staged shard replica lives in HBM as one contiguous slice per live
+    GPU (csrc/serve/shard.h shard_slices, used by the GPU executor's
+    stage_blob); shard queries then prefer the GPU holding their slice."""
+    got = C.shard_slices(n, devices)
+    assert got == want
+    assert sum(c for _, _, c in got) == n
+
+
 @pytest.mark.parametrize("live,jobs,want", [
     (list(range(8)), 2, [[0, 1, 2, 3], [4, 5, 6, 7]]),
     ([0, 1, 2, 4, 5, 6, 7], 2, [[0, 1, 2], [4, 5, 6, 7]]),   # first floor(7/2) to job 1

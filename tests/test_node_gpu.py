@@ -22,7 +22,10 @@ def env(tmp_path_factory):
     lab = write_labels(str(root / "synset_words.txt"), labels)
     ds = make_synthetic_dataset(str(root / "train"), labels[:16], size=(300, 400))
     ckpt = write_random_checkpoint("resnet18", str(root / "resnet18.ot"), seed=4)
-    return {"root": root, "labels": lab, "dataset": ds, "ckpt": ckpt, "entries": labels}
+    ckpt_a = write_random_checkpoint("alexnet", str(root / "alexnet.ot"), seed=5)
+    ckpt_rb = write_random_checkpoint("resnet18", str(root / "resnet18_rb.ot"), seed=6, randomize_bn=True)
+    return {"root": root, "labels": lab, "dataset": ds, "ckpt": ckpt, "ckpt_a": ckpt_a, "ckpt_rb": ckpt_rb,
+            "entries": labels}
 
 
 def _classify(env, executor, images):
@@ -146,3 +149,57 @@ def test_gpu_shard_served_from_hbm_without_host_io(gpu, env, tmp_path):
     idx, _ = eng.predict(torch.from_numpy(read_shard(shard).copy()).cuda())
     torch.cuda.synchronize()
     assert got == idx[:8].cpu().tolist()
+
+
+def test_gpu_jobs_over_hbm_shard(gpu, env, tmp_path):
+    """Both jobs over a labelled SDFS shard (`predict <shard>`): every query
+    is a range of the shard classified in place from its HBM slice on the
+    replica holder (no JPEG decode, no host I/O: the replica files are
+    deleted first). The report's accuracy must equal the count of images the
+    in-process engine puts in their label class, and every printed
+    prediction must be the engine's."""
+    import glob
+    import torch
+    from dmlc.runtime import InferenceEngine
+    from dmlc.utils.shards import synthetic_shard, read_shard, write_shard
+    label0, n = 0, 48
+    imgs = read_shard(synthetic_shard(str(tmp_path / "raw.u8s"), n, 224, seed=21))
+    shard = write_shard(str(tmp_path / "val.u8s"), imgs, label0=label0)
+    cl = LocalCluster(1, 19850, str(tmp_path / "c"), env["labels"], n_leaders=1, executor="gpu",
+                      dataset=env["dataset"], models=f"resnet18={env['ckpt_rb']},alexnet={env['ckpt_a']}",
+                      extra=["--max-batch", "16", "--query-batch", "8", "--adaptive-window", "2"])
+    with cl:
+        nd = cl.nodes[0]
+        assert re.search(r"placement alexnet=gpu0 resnet18=gpu0", nd.cmd("info")), nd.cmd("info")
+        assert "Stored on:" in nd.cmd(f"put {shard} val.u8s")
+        deadline = time.time() + 60
+        while time.time() < deadline and "val.u8s@v1" not in nd.cmd("replicas"):
+            time.sleep(0.2)
+        for p in glob.glob(str(tmp_path / "c" / "*" / "storage" / "v1.val.u8s")):
+            os.remove(p)
+        mark = nd.mark()
+        nd.cmd("predict val.u8s")
+        deadline = time.time() + 120
+        out = ""
+        while time.time() < deadline:
+            out = nd.cmd("jobs")
+            if len(re.findall(rf"Accuracy: \d+/{n} ", out)) == 2:
+                break
+            time.sleep(0.5)
+        text = nd.output(mark)
+    # the oracle at the queries' batch size (8): the same kernel paths
+    eng = InferenceEngine("resnet18", env["ckpt_rb"], device=0, max_batch=8)
+    x = torch.from_numpy(imgs.copy()).cuda()
+    idx = []
+    for s in range(0, n, 8):
+        i, _ = eng.predict(x[s:s + 8].contiguous())
+        idx += i.cpu().tolist()
+    correct = sum(int(c == label0 + i) for i, c in enumerate(idx))
+    m = re.search(rf"Model: resnet18\n\tAccuracy: (\d+)/{n} ", out)
+    assert m and int(m.group(1)) == correct, out
+    assert re.search(r"Data: SDFS shards val\.u8s", out)
+    got = dict(re.findall(r"^resnet18 - (n\d+): (.*?) \(\d", text, re.M))
+    wnids = [w for w, _ in env["entries"]]
+    texts = dict(env["entries"])
+    for i in range(n):
+        assert got[wnids[label0 + i]] == texts[wnids[idx[i]]], i
