@@ -14,6 +14,11 @@ Modes, each timed over graph-replayed b256 forwards:
            default) moves 7 x 38.5 MB to itself by grouped send/recv on a
            high-priority side stream per forward -- the coordinator's
            scatter legs, with their CTA/LDS footprint, minus the xGMI hop
+  rcclK:L  the same with L legs (L = 1: what a receiving rank runs per step)
+
+--batches b1,b2,...: every mode at each forward batch (the coordinator's
+weighted share vs a worker's full batch: bench.py --coord-weight).
+--leg-images: images per leg (default: the batch).
 """
 import argparse
 import os
@@ -31,17 +36,25 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--modes", default="none,sleep1,sleep4,sleep16,sleep32,copy")
+    ap.add_argument("--batches", default="")
+    ap.add_argument("--leg-images", type=int, default=0)
     args = ap.parse_args()
+    for b in ([int(x) for x in args.batches.split(",")] if args.batches else [args.batch]):
+        print(f"## batch {b}", flush=True)
+        run(args, b)
+
+
+def run(args, B):
     import dmlc
     from dmlc.runtime import InferenceEngine
     dev = torch.device("cuda", 0)
-    eng = InferenceEngine("resnet18", None, device=0, max_batch=args.batch)
-    B = args.batch
+    eng = InferenceEngine("resnet18", None, device=0, max_batch=B)
+    LB = args.leg_images or B
     img = torch.randint(0, 256, (B, 224, 224, 3), dtype=torch.uint8, device=dev)
     out = (torch.empty(B, dtype=torch.int32, device=dev), torch.empty(B, dtype=torch.float32, device=dev))
     main_s = torch.cuda.current_stream()
     side = [torch.cuda.Stream() for _ in range(32)]
-    src = torch.empty(7 * B * 224 * 224 * 3, dtype=torch.uint8, device=dev)
+    src = torch.empty(7 * LB * 224 * 224 * 3, dtype=torch.uint8, device=dev)
     dst = torch.empty_like(src)
     hi = torch.cuda.Stream(priority=-1)
     loops = {}
@@ -74,21 +87,25 @@ def main():
                     with torch.cuda.stream(side[j]):
                         torch.cuda._sleep(int(cyc_per_ms * 1.3))
             elif mode.startswith("rccl"):
-                k = int(mode[4:])
+                spec = mode[4:].split(":")
+                k = int(spec[0])
+                legs = int(spec[1]) if len(spec) > 1 else 7
                 if k not in loops:
                     loops[k] = dmlc.native().RcclLoop(0, k)
+                if mode not in loops:
+                    loops[mode] = True
                     ts = []
                     for _ in range(6):  # the legs alone
                         x0, x1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                         x0.record(hi)
-                        loops[k].issue(hi.cuda_stream, src.data_ptr(), dst.data_ptr(), B * 224 * 224 * 3, 7)
+                        loops[k].issue(hi.cuda_stream, src.data_ptr(), dst.data_ptr(), LB * 224 * 224 * 3, legs)
                         x1.record(hi)
                         torch.cuda.synchronize()
                         ts.append(x0.elapsed_time(x1))
-                    print(f"{mode:8s} 7 x {B * 224 * 224 * 3 / 1e6:.1f} MB self send/recv alone: "
+                    print(f"{mode:8s} {legs} x {LB * 224 * 224 * 3 / 1e6:.1f} MB self send/recv alone: "
                           f"{sorted(ts[1:])[2]:.3f} ms", flush=True)
                 hi.wait_event(ev)
-                loops[k].issue(hi.cuda_stream, src.data_ptr(), dst.data_ptr(), B * 224 * 224 * 3, 7)
+                loops[k].issue(hi.cuda_stream, src.data_ptr(), dst.data_ptr(), LB * 224 * 224 * 3, legs)
             elif mode == "copy":
                 side[0].wait_event(ev)
                 with torch.cuda.stream(side[0]):
