@@ -1,0 +1,235 @@
+// Fused AlexNet stem: u8 image -> ImageNet normalisation -> conv 11x11/s4/p2
+// (+bias) -> ReLU -> maxpool 3x3/s2, one workgroup per image, the 55x55x64
+// conv output never leaves LDS. [B, 224, 224, 3] u8 in, [B, 27, 27, 64] bf16
+// NHWC out.
+//
+// Reference equivalent: tch::vision::alexnet's features.0 (conv), .1 (relu),
+// .2 (maxpool) after imagenet::load_image_and_resize's normalisation, run per
+// query by `forward_t` (src/services.rs:492-493). As three kernels
+// (preprocess_u8, the packed-RGB implicit GEMM, maxpool2d) the stem took
+// 41 + 157 + ~20 us at B = 256 (profiles/r2_alexnet_b256_kernel_stats.txt):
+// the implicit GEMM's 11x11 im2col re-reads every input pixel ~30x and its
+// 64-wide N tile leaves most of each MFMA tile idle.
+//
+//  * Paired rows: padded pixel column j (image column j - 2) pairs into 16-B
+//    chunks p = (2p, 2p+1) as bf16 [r g b r g b 0 0]. With stride 4, output
+//    column ow reads padded columns 4ow .. 4ow+10 = chunks 2ow .. 2ow+5 of
+//    each kernel row, so K = 11 rows x 6 chunks x 8 = 528 (+16 zero) = 17
+//    MFMA k-steps of 32, and every B operand is one aligned ds_read_b128 from
+//    the staged row (no im2col). Weights are zero on the pad slots (e = 6, 7,
+//    kw = 11, kh = 11).
+//  * Rows stream through LDS: the raw u8 rows of conv row oh+4 arrive by
+//    LDS-DMA during conv row oh, and are converted into the paired ring during
+//    conv row oh+1 for conv row oh+3 (beside the MFMAs of the SIMD's other
+//    wave), so each conv row costs one barrier.
+//  * 8 waves: wave w = pixel fragment w & 3 (16 output columns) x output
+//    channels 32 (w >> 2) .. +31 (two n-blocks), D = W x X with the weight
+//    rows permuted (perm32) so a lane ends with 8 consecutive channels of one
+//    pixel; all 17 x 2 weight fragments stay in VGPRs.
+//  * + bias, ReLU, bf16 -> a 4-slot ring of conv rows [55][64] in LDS (16-B
+//    chunks XOR-swizzled by pixel: conflict-free stores and reads); every
+//    second conv row the 3x3/s2 max of the three latest rows is stored as one
+//    pooled row (post-ReLU values are >= 0: bf16 max = unsigned 16-bit max).
+#include "common.h"
+#include "kernels.h"
+
+namespace dmlc {
+
+namespace {
+
+typedef unsigned short ushort8 __attribute__((ext_vector_type(8)));
+
+constexpr int kS = 224;         // input image size
+constexpr int kHo = 55;         // conv output size
+constexpr int kPH = 27;         // pooled output size
+constexpr int kC = 64;          // output channels
+constexpr int kChunks = 114;    // paired chunks per padded row (228 padded pixels)
+constexpr int kRowB = 136 * 16; // staged paired row: chunks >= 114 stay zero (fragment padding reads up to 131)
+constexpr int kRing = 32;       // paired rows (power of two): 11 in use + 8 converted ahead
+constexpr int kKS = 17;         // K steps of 32 (68 chunks, 66 used)
+constexpr int kU8B = kS * 3;    // 672 bytes per raw image row
+constexpr int kU8Slot = 704;    // raw ring slot (16-B aligned)
+constexpr int kU8Ring = 8;
+constexpr int kConvB = kHo * 128;  // one conv row [55][64] bf16
+constexpr int kConvRing = 4;
+constexpr size_t kLds = (size_t)kRing * kRowB + (size_t)kConvRing * kConvB + (size_t)kU8Ring * kU8Slot;
+
+struct AlexStemArgs {
+  const uint8_t* x;    // [B, 224, 224, 3]
+  const bf16* w;       // [64][544] paired-chunk K order (alex_stem_k)
+  const float* bias;   // [64]
+  bf16* y;             // [B, 27, 27, 64]
+};
+
+__device__ __forceinline__ int perm32(int n) {
+  const int nf = n >> 4, r = n & 15;
+  return 8 * (r >> 2) + 4 * nf + (r & 3);
+}
+
+// conv-ring byte offset of 16-B channel chunk c of pixel px
+__device__ __forceinline__ int conv_off(int px, int c) { return px * 128 + ((c ^ (px & 7)) << 4); }
+
+__global__ __launch_bounds__(512, 1) void alex_stem_kernel(AlexStemArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint4 smem[];
+  char* ring = (char*)smem;
+  char* conv = ring + kRing * kRowB;
+  char* raw = conv + kConvRing * kConvB;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fq = lane >> 4;
+  const int b = blockIdx.x;
+  const uint8_t* img = a.x + (long)b * kS * kU8B;
+
+  // zero the paired ring once: out-of-image rows and the fragment-padding
+  // chunks must read as finite zeros (they meet zero weights)
+  for (int o = tid * 16; o < kRing * kRowB; o += 512 * 16) *(uint4*)(ring + o) = make_uint4(0, 0, 0, 0);
+
+  // paired chunk p of padded row pr from 6 bytes of the raw row (image row
+  // pr - 2): the exact values preprocess_u8 would produce (imagenet_norm)
+  auto convert_chunk = [&](int pr, int p, const uint8_t* src_row) __attribute__((always_inline)) {
+    const int iy = pr - 2;
+    float v[8];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int ix = 2 * p - 2 + q;
+      const bool in = iy >= 0 && iy < kS && ix >= 0 && ix < kS;
+      const int ixc = ix < 0 ? 0 : ix >= kS ? kS - 1 : ix;  // never an out-of-row address
+#pragma unroll
+      for (int c = 0; c < 3; ++c) v[3 * q + c] = in ? imagenet_norm(c, (float)src_row[3 * ixc + c]) : 0.f;
+    }
+    v[6] = v[7] = 0.f;
+    *(uint4*)(ring + (pr & (kRing - 1)) * kRowB + p * 16) = pack8(v);
+  };
+  // raw image row of padded row pr -> raw ring (LDS-DMA, one wave, 42 lanes)
+  auto dma_row = [&](int pr) __attribute__((always_inline)) {
+    const int iy = pr - 2;
+    if (iy < 0 || iy >= kS) return;
+    if (lane < kU8B / 16) dma16(img + (long)iy * kU8B + lane * 16, raw + (pr % kU8Ring) * kU8Slot);
+  };
+
+  // weights: wave's channel group 32 (w >> 2), n-blocks nf = 0, 1 (rows permuted)
+  const int ch0 = 32 * (wave >> 2);
+  bf16x8 wr[kKS][2];
+#pragma unroll
+  for (int nf = 0; nf < 2; ++nf) {
+    const bf16* row = a.w + (long)(ch0 + perm32(16 * nf + fr)) * (kKS * 32);
+#pragma unroll
+    for (int ks = 0; ks < kKS; ++ks) wr[ks][nf] = *(const bf16x8*)(row + ks * 32 + fq * 8);
+  }
+  float bs[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) bs[e] = a.bias[ch0 + 8 * fq + e];
+
+  // per-lane B-operand constants: chunk c = 4 ks + fq = (kh, cc); kh = 11
+  // (the two pad chunks) reads row 10 (finite values x zero weights)
+  const int f = wave & 3;
+  const int ow = 16 * f + fr;
+  int kh_of[kKS], col_of[kKS];
+#pragma unroll
+  for (int ks = 0; ks < kKS; ++ks) {
+    const int c = 4 * ks + fq;
+    const int kh = c / 6, cc = c - 6 * (c / 6);
+    kh_of[ks] = kh < 11 ? kh : 10;
+    col_of[ks] = (2 * ow + cc) * 16;
+  }
+
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  // prologue: padded rows 0..18 (conv rows 0, 1, 2) straight from global;
+  // raw rows 19..22 (conv row 3) by DMA
+  for (int it = tid; it < 19 * kChunks; it += 512) {
+    const int pr = it / kChunks, p = it - pr * kChunks;
+    const int iy = pr - 2;
+    convert_chunk(pr, p, img + (long)(iy < 0 ? 0 : iy >= kS ? kS - 1 : iy) * kU8B);
+  }
+  if (wave < 4) dma_row(19 + wave);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  for (int oh = 0; oh <= kHo; ++oh) {
+    if (oh < kHo) {
+      // rows of conv row oh+4 go out now (the raw ring slot they fill was
+      // converted at the previous iteration, before its barrier)
+      if (wave < 4 && oh + 4 < kHo) dma_row(4 * oh + 23 + wave);
+      // convert conv row oh+3's new rows (padded 4oh+19 .. 4oh+22; raw rows
+      // landed before the last barrier); disjoint from the rows read below
+      if (oh + 3 < kHo && tid < 4 * kChunks) {
+        const int pr = 4 * oh + 19 + tid / kChunks, p = tid - (tid / kChunks) * kChunks;
+        convert_chunk(pr, p, (const uint8_t*)raw + (pr % kU8Ring) * kU8Slot);
+      }
+      // ---- conv row oh: 17 k-steps x 2 n-blocks
+      floatx4 acc[2] = {floatx4{0.f, 0.f, 0.f, 0.f}, floatx4{0.f, 0.f, 0.f, 0.f}};
+      const int pr0 = 4 * oh;
+      bf16x8 xb = *(const bf16x8*)(ring + ((pr0 + kh_of[0]) & (kRing - 1)) * kRowB + col_of[0]);
+#pragma unroll
+      for (int ks = 0; ks < kKS; ++ks) {
+        bf16x8 xn;
+        if (ks + 1 < kKS) xn = *(const bf16x8*)(ring + ((pr0 + kh_of[ks + 1]) & (kRing - 1)) * kRowB + col_of[ks + 1]);
+        acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[ks][0], xb, acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[ks][1], xb, acc[1], 0, 0, 0);
+        if (ks + 1 < kKS) xb = xn;
+      }
+      // lane: channels ch0 + 8 fq .. +7 of pixel ow (nf 0: +0..3, nf 1: +4..7)
+      if (ow < kHo) {
+        float v[8];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          v[i] = fmaxf(acc[0][i] + bs[i], 0.f);
+          v[4 + i] = fmaxf(acc[1][i] + bs[4 + i], 0.f);
+        }
+        *(uint4*)(conv + (oh & (kConvRing - 1)) * kConvB + conv_off(ow, ch0 / 8 + fq)) = pack8(v);
+      }
+    }
+    // pooled row ph = (oh - 3) / 2 from conv rows oh-3 .. oh-1 (visible since
+    // the last barrier; this iteration wrote slot oh % 4, a different one)
+    if (oh >= 3 && (oh & 1)) {
+      const int ph = (oh - 3) >> 1;
+      if (tid < kPH * 8) {
+        const int pw = tid >> 3, cg = tid & 7;
+        ushort8 m = ushort8{0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int dy = 0; dy < 3; ++dy) {
+          const char* row = conv + ((2 * ph + dy) & (kConvRing - 1)) * kConvB;
+#pragma unroll
+          for (int dx = 0; dx < 3; ++dx)
+            m = __builtin_elementwise_max(m, *(const ushort8*)(row + conv_off(2 * pw + dx, cg)));
+        }
+        *(ushort8*)(a.y + (((long)b * kPH + ph) * kPH + pw) * kC + cg * 8) = m;
+      }
+    }
+    // this iteration's DMA (conv row oh+4's raw rows, issued before the
+    // MFMAs) has had the whole MFMA phase to land; the next iteration
+    // converts it, so it must be in LDS before the barrier
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+}
+
+}  // namespace
+
+size_t alex_stem_lds_bytes() { return kLds; }
+
+bool alex_stem_supported(int S) { return S == kS; }
+
+// K index of weight (kh, kw, c) in the paired-chunk order (544 per channel).
+int alex_stem_k(int kh, int kw, int c) {
+  const int cc = kw / 2, q = kw % 2;
+  return (kh * 6 + cc) * 8 + q * 3 + c;
+}
+
+void alex_stem_u8(const uint8_t* x, const void* w, const float* bias, void* y, int B, hipStream_t s) {
+  if (B <= 0) return;
+  if (!x || !w || !bias || !y || ((uintptr_t)x & 15) || ((uintptr_t)w & 15) || ((uintptr_t)y & 15))
+    throw std::invalid_argument("alex_stem_u8: null / misaligned operand");
+  AlexStemArgs a;
+  a.x = x;
+  a.w = (const bf16*)w;
+  a.bias = bias;
+  a.y = (bf16*)y;
+  hipLaunchKernelGGL(alex_stem_kernel, dim3(B), dim3(512), kLds, s, a);
+  DMLC_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace dmlc

@@ -204,6 +204,13 @@ void stem_conv_pool(const void* x, const void* w, const float* bias, void* y, in
 // paired bf16 rows built in LDS with preprocess_u8's exact arithmetic.
 void stem_conv_pool_u8(const uint8_t* x, const void* w, const float* bias, void* y, int B, int S, int strip,
                        hipStream_t s);
+// AlexNet features.0-2 fused (alex_stem.hip): u8 [B, 224, 224, 3] ->
+// normalise -> conv 11x11/s4/p2 + bias -> ReLU -> maxpool 3x3/s2 ->
+// [B, 27, 27, 64] bf16. w: [64][544] bf16 in alex_stem_k order.
+bool alex_stem_supported(int S);
+int alex_stem_k(int kh, int kw, int c);
+constexpr int kAlexStemK = 544;
+void alex_stem_u8(const uint8_t* x, const void* w, const float* bias, void* y, int B, hipStream_t s);
 
 // One wave of v_mfma_scale_f32_16x16x128_f8f6f4 (fp8 e4m3, unit scales) on
 // raw per-lane registers: a, b = int32 [64 lanes][8], d = f32 [64 lanes][4].

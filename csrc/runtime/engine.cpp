@@ -315,6 +315,9 @@ void Engine::build_alexnet() {
     return y;
   };
   x = conv(x, "features.0", "", 64, 11, 4, 0, true);
+  // 224x224 u8 batches skip preprocess + features.0 + features.2: one fused
+  // kernel (alex_stem.hip) writes features.2's output
+  convs_.back().alex_stem = opt_.fused_stem && alex_stem_supported(S);
   x = pool(x, "features.2");
   x = conv(x, "features.3", "", 192, 5, 1, 2, true);
   x = pool(x, "features.5");
@@ -430,6 +433,10 @@ void Engine::pack_weights(const WeightMap& w) {
       L.wf_off = off;  // fragment-order copy for the register-weight stream conv
       off = align_up(off + (size_t)L.cout * L.kpad * 2, 256);
     }
+    if (L.alex_stem) {  // paired-chunk K order for alex_stem.hip
+      L.wf_off = off;
+      off = align_up(off + (size_t)L.cout * kAlexStemK * 2, 256);
+    }
   }
   weight_bytes_ = off;
   std::vector<uint8_t> host(off, 0);
@@ -492,7 +499,15 @@ void Engine::pack_weights(const WeightMap& w) {
         }
     }
     for (int n = 0; n < L.cout; ++n) pb[n] = bias[n];
-    if (L.wf_off) {
+    if (L.alex_stem) {
+      uint16_t* pf = (uint16_t*)(host.data() + L.wf_off);
+      for (int n = 0; n < L.cout; ++n)
+        for (int c = 0; c < L.cin; ++c)
+          for (int i = 0; i < L.kh; ++i)
+            for (int j = 0; j < L.kw; ++j)
+              pf[(size_t)n * kAlexStemK + alex_stem_k(i, j, c)] =
+                  f2bf_host(W.data[(((size_t)n * L.cin + c) * L.kh + i) * L.kw + j] * scale[n]);
+    } else if (L.wf_off) {
       uint16_t* pf = (uint16_t*)(host.data() + L.wf_off);
       for (int n = 0; n < L.cout; ++n)
         for (int k = 0; k < L.kpad; ++k) pf[stream_frag_index(n, k, L.kpad)] = pw[(size_t)n * L.kpad + k];
@@ -757,6 +772,16 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
     switch (op.type) {
       case OpType::Preprocess: {
         const bool paired = op.k == 1;
+        // AlexNet: 224x224 u8 images -> features.2's output in one kernel
+        if (oi + 2 < ops_.size() && ops_[oi + 1].type == OpType::Conv && ops_[oi + 2].type == OpType::MaxPool &&
+            convs_[ops_[oi + 1].conv].alex_stem && opt_.fused_preprocess && Hin == image_size_ &&
+            Win == image_size_) {
+          const ConvLayer& L = convs_[ops_[oi + 1].conv];
+          const uint8_t* wa = (const uint8_t*)warena_;
+          alex_stem_u8(images, wa + L.wf_off, (const float*)(wa + L.b_off), acts_[ops_[oi + 2].out], B, s);
+          skip = 2;
+          break;
+        }
         // images already SxS feed the fused stem directly (stem_conv_pool_u8)
         if (paired && opt_.fused_preprocess && Hin == image_size_ && Win == image_size_) break;
         const int Wr = paired ? 2 * shapes_[op.out].W : shapes_[op.out].W;

@@ -39,6 +39,7 @@ struct ConvLayer {
   bool fc = false;        // linear layer (weight [N,K]) run as a 1x1 conv
   bool pair = false;      // stem conv on the preprocess packed-RGB image (8 (kw,c) values / 16 B)
   bool stem_pool = false; // fused ResNet stem (conv+maxpool) on the paired image, K = 224
+  bool alex_stem = false; // AlexNet features.0: also packed for alex_stem.hip (u8 -> conv+relu+pool) at wf_off
   int fc_hwc[3] = {0, 0, 0};  // for fc after a spatial tensor: (H,W,C) of the flatten
   int npad = 0, kpad = 0;
   size_t w_off = 0, b_off = 0;  // offsets (bytes) into the weight arena

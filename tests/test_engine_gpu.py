@@ -181,6 +181,34 @@ def test_fast_paths_match_plain_paths_odd_batches(gpu, B):
     assert rel < 1e-3, rel
 
 
+@pytest.mark.parametrize("B", [3, 64, 256])
+def test_alexnet_fused_stem_matches_unfused(gpu, B):
+    """alex_stem.hip (u8 -> normalise -> conv 11x11/s4 + ReLU -> maxpool in
+    one kernel) against the three-kernel path it replaces (preprocess_u8, the
+    packed-RGB implicit GEMM, maxpool2d): the same bf16 math, so logits agree
+    to accumulation-order rounding and top-1 is identical but for near-ties;
+    and against fp32 torch.nn at B=3."""
+    model = build("alexnet", seed=31)
+    sd = state_dict_f32(model)
+    g = torch.Generator().manual_seed(B)
+    img = torch.randint(0, 256, (B, 224, 224, 3), generator=g, dtype=torch.uint8)
+    x = img.to(gpu)
+    ref_eng = InferenceEngine("alexnet", sd, max_batch=B, options={"fused_stem": False})
+    eng = InferenceEngine("alexnet", sd, max_batch=B)
+    ri, _, rl = ref_eng.predict(x, return_logits=True, use_graph=False)
+    fi, _, fl = eng.predict(x, return_logits=True)
+    torch.cuda.synchronize()
+    rel = ((fl - rl).norm() / rl.norm()).item()
+    assert rel < 1e-2, rel
+    p = torch.softmax(rl.float().cpu(), -1)
+    top2 = p.topk(2, -1).values
+    near = (top2[:, 0] - top2[:, 1]) < 1e-2
+    assert torch.all((fi.cpu() == ri.cpu()) | near)
+    if B == 3:
+        ref = _ref_logits(model, img)
+        assert ((fl.cpu() - ref).norm() / ref.norm()).item() < 3e-2
+
+
 def test_bench_path_b256_matches_fp32(gpu):
     """The exact bench.py configuration — ResNet18, B=256, default kernel
     selection, hipGraph replay, two compute lanes (the second a copied

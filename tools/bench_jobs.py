@@ -14,8 +14,15 @@ state the quantities the reference publishes (CS425MP4Report.pdf pp.2-3):
   * optionally the time to resume normal operation after killing a
     non-coordinator member (ref: 1.262 s) or the coordinator (ref: 3.593 s).
 
+With --shards DIR (labelled u8 shards, tools/make_shards.py) the jobs run
+over SDFS-staged shards instead (BASELINE config 3): the shards are `put`
+into the SDFS, every replica holder stages its copy into HBM (one slice per
+GPU), and `predict <shard>...` sends each query (a range of one shard) to a
+replica holder, which classifies it in place: no JPEG decode, no host I/O.
+
 usage: python tools/bench_jobs.py [--nodes 4] [--executor gpu] [--images 1000]
          [--interval-ms 50] [--batch 1] [--kill member|leader] [--fast-periods]
+         [--shards data/shards]
 """
 import argparse
 import json
@@ -75,14 +82,27 @@ def main():
     ap.add_argument("--labels", default="", help="synset_words.txt matching --dataset")
     ap.add_argument("--prefetch", action="store_true", help="stage every query image into HBM before predict")
     ap.add_argument("--node-gpus", type=int, default=1, help="GPUs per node (RCCL scatter inside a node)")
+    ap.add_argument("--shards", default="", help="dir of labelled u8 shards: the jobs run over them from the SDFS")
     a = ap.parse_args()
+    shards = sorted(f for f in os.listdir(a.shards) if f.endswith(".u8s")) if a.shards else []
+    if shards:
+        from dmlc.utils.shards import shard_info
+        a.images = sum(shard_info(os.path.join(a.shards, f))["n"] for f in shards)
 
     ngpu = a.gpus
     if a.executor == "gpu" and ngpu == 0:
         import torch
         ngpu = torch.cuda.device_count()
     root = tempfile.mkdtemp(prefix="dmlc_jobs_")
-    if a.dataset:
+    if shards:  # the jobs read the shards; the members need no JPEG dataset
+        ds = os.path.join(root, "empty")
+        os.makedirs(ds)
+        if a.labels:
+            lab = os.path.abspath(a.labels)
+        else:
+            lab = write_labels(os.path.join(root, "synset_words.txt"), synthetic_labels(1000))
+        data_desc = "shards"
+    elif a.dataset:
         ds, lab = os.path.abspath(a.dataset), os.path.abspath(a.labels)
         n_avail = len(os.listdir(ds))
         if a.images > n_avail:
@@ -122,8 +142,23 @@ def main():
         cl.wait_members(len(nodes), 60)
         time.sleep(4 if not a.fast_periods else 1.5)  # one assignment round
         client = nodes[1]  # standby leader candidate: survives both kill experiments
+        if shards:
+            t = time.time()
+            for f in shards:
+                out = client.cmd(f"put {os.path.abspath(os.path.join(a.shards, f))} {f}", 600)
+                assert "Stored on:" in out, out
+            want = min(len(nodes), 4)  # replication factor 4
+            deadline = time.time() + 600
+            while time.time() < deadline:
+                staged = sum(all(f"{f}@v1" in nd.cmd("replicas", 30) for f in shards) for nd in nodes)
+                if staged >= want:
+                    break
+                time.sleep(1.0)
+            print(f"# {len(shards)} shards put and staged in HBM in {time.time() - t:.1f}s", file=sys.stderr)
+            data_desc = (f"SDFS-staged labelled u8 shards ({a.images} images in {len(shards)} shards from "
+                         f"{os.path.abspath(a.shards)}), random-init weights")
         t_predict = time.time()
-        client.cmd("predict")
+        client.cmd("predict " + " ".join(shards) if shards else "predict")
         t_fail = None
         deadline = time.time() + max(300, a.images * a.interval_ms / 1000 * 4)
         while time.time() < deadline:
@@ -153,11 +188,13 @@ def main():
            "executor": a.executor, "gpus": ngpu, "images_per_job": a.images, "query_interval_ms": a.interval_ms,
            "adaptive_window": a.adaptive_window,
            "query_batch": a.batch, "data": data_desc, "prefetch": a.prefetch, "node_gpus": a.node_gpus,
+           "source": "shards" if shards else "jpeg",
            "reference": REF, "jobs": []}
     for j in jobs:
         d = [x / 1000 for x in j["durations_us"]]
         span = (max(j["done_us"]) - j["started_us"]) / 1e6 if j["done_us"] else None
         res["jobs"].append({"model": j["model"], "finished": j["finished"], "correct": j["correct"],
+                            "images_per_s": round(j["finished"] / span, 1) if span else None,
                             "mean_ms": round(statistics.mean(d), 3), "std_ms": round(statistics.pstdev(d), 3),
                             "p50_ms": round(pct(d, 50), 3), "p95_ms": round(pct(d, 95), 3),
                             "p99_ms": round(pct(d, 99), 3),
