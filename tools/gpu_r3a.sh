@@ -19,3 +19,5 @@ step interference 300 python tools/interference_probe.py --batches 256,218 --mod
 step bench_alexnet 300 python bench.py --model alexnet --steps 40 --warmup 10 --latency-queries 50 --e2e-queries 0
 step prof_alexnet 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_alex -o run -- python3 bench.py --model alexnet --steps 20 --warmup 5 --latency-queries 0 --e2e-queries 0
 step shard_jobs 600 python tools/bench_jobs.py --nodes 1 --executor gpu --shards bench_data/shards --labels bench_data/synset_words.txt --batch 64 --adaptive-window 4 --fast-periods --out gpurun_out/shard_jobs.json
+step r50fp8_b256 300 python bench.py --model resnet50_fp8 --steps 20 --warmup 5 --latency-queries 0 --e2e-queries 0
+step r50fp8_b128 300 python bench.py --model resnet50_fp8 --batch 128 --steps 40 --warmup 5 --latency-queries 0 --e2e-queries 0
