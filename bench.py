@@ -25,9 +25,11 @@ Input modes (--input-mode):
                     RCCL, one step ahead of its forward. Rank 0 drives all the
                     send legs, and RCCL's copy kernels next to a forward slow
                     it ~1.2x (they hold CUs the one-workgroup-per-CU convs
-                    need, profiles/r2_rccl_interference.txt), so rank 0 takes
-                    --coord-weight of a fair share and the other ranks split
-                    the rest (global batch unchanged: per_gpu_batch x N).
+                    need, profiles/r2_rccl_interference.txt), so rank 0
+                    classifies --coord-weight x per_gpu_batch images and every
+                    other rank per_gpu_batch (never more: 256 = the CU count,
+                    and the one-workgroup-per-image kernels would run a second
+                    round); global_batch = the sum, in the JSON.
   staged            rank 0's images are scattered to the ranks over RCCL once,
                     before timing (SDFS shard replicas placed in the HBM of the
                     GPU that serves them, as predict-shard does); every timed
@@ -252,7 +254,7 @@ def main():
         ops_profile = eng.profile(pool[:B].contiguous())
 
     if rank == 0:
-        n_img = B * world * args.steps
+        n_img = sum(counts) * args.steps
         value = n_img / elapsed
         res = {
             "metric": "images/sec (whole node) + p50/p95 query latency, "
@@ -274,7 +276,7 @@ def main():
             "prime_steps": args.prime_steps,
             "config": {
                 "model": args.model,
-                "global_batch": B * world,
+                "global_batch": sum(counts),
                 "per_gpu_batch": B,
                 "per_rank_counts": counts,
                 "coord_weight": coord_weight,

@@ -9,16 +9,13 @@ namespace dp {
 
 std::vector<int> weighted_counts(int per_rank, int world, double coord_weight) {
   if (world < 1 || per_rank < 1) throw std::invalid_argument("weighted_counts: need world >= 1 and per_rank >= 1");
-  if (!(coord_weight > 0.0) || coord_weight > (double)world)
-    throw std::invalid_argument("weighted_counts: coord_weight must be in (0, world]");
-  const int64_t total = (int64_t)per_rank * world;
-  if (world == 1) return {per_rank};
-  const int c0 = std::max(1, std::min<int>((int)std::lround(per_rank * coord_weight), (int)total - (world - 1)));
-  std::vector<int> c(world);
-  c[0] = c0;
-  const int64_t rest = total - c0;
-  for (int r = 1; r < world; ++r) c[r] = (int)(rest / (world - 1));
-  for (int r = 1; r <= (int)(rest % (world - 1)); ++r) ++c[r];
+  if (!(coord_weight > 0.0) || coord_weight > 1.0)
+    throw std::invalid_argument("weighted_counts: coord_weight must be in (0, 1]");
+  // the other ranks keep exactly per_rank: a batch above it would push the
+  // one-workgroup-per-image kernels (per_rank = 256 = the CU count) into a
+  // second, nearly empty round
+  std::vector<int> c(world, per_rank);
+  if (world > 1) c[0] = std::max(1, std::min(per_rank, (int)std::lround(per_rank * coord_weight)));
   return c;
 }
 

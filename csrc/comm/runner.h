@@ -20,10 +20,12 @@
 namespace dmlc {
 namespace dp {
 
-// Per-rank image counts of a global batch of `per_rank * world` images in
-// which rank 0 (the coordinator, which also drives every scatter leg) takes
-// `coord_weight` of a fair share and the other ranks split the rest evenly
-// (lower ranks take any remainder). coord_weight = 1: an even split.
+// Per-rank image counts of one step: every rank classifies `per_rank` images
+// except rank 0 (the coordinator, which also drives every scatter leg), which
+// takes round(coord_weight x per_rank) (coord_weight in (0, 1]; 1: an even
+// split). The other ranks are never raised above per_rank: at per_rank = 256
+// (the CU count) the one-workgroup-per-image kernels would run a second,
+// nearly empty round.
 std::vector<int> weighted_counts(int per_rank, int world, double coord_weight);
 
 class Runner {

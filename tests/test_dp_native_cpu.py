@@ -142,7 +142,7 @@ def test_bench_protocol(world, mode, weight):
     per = 6
     counts = C.dp_weighted_counts(per, world, weight)
     G = sum(counts)
-    assert G == per * world
+    assert counts[1:] == [per] * (world - 1) and counts[0] == (per if world == 1 or weight == 1.0 else 5)
     pool = np.random.default_rng(world).integers(0, 256, size=(2 * G, H, W, 3), dtype=np.uint8)
     out = C.dp_host_bench(pool, world, per, coord_weight=weight, input_mode=mode, lanes=2, prime=4, warmup=3,
                           steps=7, latency=2)
@@ -153,10 +153,14 @@ def test_bench_protocol(world, mode, weight):
 
 @pytest.mark.parametrize("per,world,w,want", [
     (256, 8, 1.0, [256] * 8),
-    (256, 8, 0.85, [218] + [262] * 3 + [261] * 4),
-    (256, 2, 0.5, [128, 384]),
+    (256, 8, 0.85, [218] + [256] * 7),   # the others never above 256: no second, nearly empty round
+    (256, 2, 0.5, [128, 256]),
     (10, 1, 0.5, [10]),
 ])
 def test_weighted_counts(per, world, w, want):
-    got = C.dp_weighted_counts(per, world, w)
-    assert got == want and sum(got) == per * world
+    assert C.dp_weighted_counts(per, world, w) == want
+
+
+def test_weighted_counts_rejects_raising_the_coordinator():
+    with pytest.raises(ValueError):
+        C.dp_weighted_counts(256, 8, 1.2)
