@@ -141,7 +141,7 @@ def main():
             nd.run(f"join {nodes[0].address}", r"Joined!", 30)
         cl.wait_members(len(nodes), 60)
         time.sleep(4 if not a.fast_periods else 1.5)  # one assignment round
-        client = nodes[1]  # standby leader candidate: survives both kill experiments
+        client = nodes[min(1, len(nodes) - 1)]  # standby leader candidate: survives both kill experiments
         if shards:
             t = time.time()
             for f in shards:
