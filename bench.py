@@ -106,6 +106,8 @@ def main():
                     help="rank 0's share of a step as a fraction of a fair share (scatter mode; default "
                          f"{COORD_WEIGHT} at N > 1, 1 at N = 1)")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--engine-opt", action="append", default=[], metavar="NAME=0|1",
+                    help="engine kernel-path switch (EngineOptions field), for A/B runs; repeatable")
     ap.add_argument("--lanes", type=int, default=2, choices=[1, 2, 3, 4],
                     help="model instances per GPU on alternating streams (2: step i+1 starts under step i's tail)")
     ap.add_argument("--prime-steps", type=int, default=40,
@@ -145,7 +147,8 @@ def main():
     # Random-init weights (the reference's .ot files are LFS stubs); every
     # rank builds the same seeded model.
     sd = state_dict_f32(build(args.model, seed=0))
-    eng = InferenceEngine(args.model, sd, device=local_rank, max_batch=B)
+    opts = {k: bool(int(v)) for k, v in (o.split("=", 1) for o in args.engine_opt)}
+    eng = InferenceEngine(args.model, sd, device=local_rank, max_batch=B, options=opts)
     use_graph = not args.no_graph
 
     ids = [b"", b""]

@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "../kernels/kernels.h"
+#include "blaslt.h"
 #include "weights.h"
 
 namespace dmlc {
@@ -82,6 +83,7 @@ struct EngineOptions {
   bool fused_pool = true;        // the last conv's epilogue computes the global average pool
   bool fused_head = true;        // avgpool + fc + softmax / top-1 in one kernel (head.hip)
   bool fc_small = true;          // weight-streaming GEMV for fc layers at B <= 16 (fc_small.hip)
+  bool blaslt_fc = true;         // bf16 fc layers above that on hipBLASLt (blaslt.h; AlexNet classifier)
   // downsample convs on a side stream: measured slower (the branch slows its
   // sibling conv1 by 10-12 us and adds ~10 us of fork/join gaps per block:
   // profiles/r1_fork_ds_timeline.txt); kept to test the side-stream path
@@ -122,6 +124,7 @@ class Engine {
   size_t weight_bytes() const { return weight_bytes_; }
   size_t activation_bytes() const { return act_bytes_; }
   double gflop_per_image() const;
+  int blaslt_plans() const { return blaslt_ ? blaslt_->plans() : 0; }  // fc shapes on hipBLASLt (tests)
 
   // Allocate the activation arena for batches up to max_batch.
   void reserve(int max_batch);
@@ -167,6 +170,8 @@ class Engine {
   bool ds_fusable(size_t oi, int B) const;     // ops oi, oi+1 = downsample + stride-2 stream conv1
   bool block_fusable(size_t oi, int B) const;  // ops oi, oi+1 = a layer1 basic block -> conv3x3_block
   bool s2rows_ok(const Op& op, const ConvLayer& D, int B) const;  // layer2.0 conv1 + downsample -> conv3x3_s2rows
+  bool fc_blaslt(const Op& op, int B) const;  // this fc op runs on hipBLASLt at batch B
+  void prepare_fc(int B, float* logits, hipStream_t s);  // pick hipBLASLt algorithms (outside capture)
 
   std::string arch_;
   int device_ = 0;
@@ -195,6 +200,8 @@ class Engine {
   int32_t* dummy_idx_ = nullptr;
   void* head_ws_ = nullptr;  // fused head partials + per-group tickets
   size_t head_ws_bytes_ = 0;
+
+  std::unique_ptr<BlasLt> blaslt_;  // created on first use (fc layers at B > 16)
 
   hipStream_t stream_ = nullptr;
   hipEvent_t ev_out_ = nullptr;  // end of the last forward (on last_stream_)

@@ -176,6 +176,8 @@ def main():
                 print(f"# killed {a.kill} {victim.address} at {t_fail - t_predict:.2f}s", file=sys.stderr)
             if len(counts) == 2 and min(counts) >= a.images:
                 break
+            if int(time.time() - t_predict) % 10 == 0:  # progress (a silent run looks hung)
+                print(f"# {time.time() - t_predict:.0f}s: answered {counts}", file=sys.stderr, flush=True)
         dump = os.path.join(root, "jobs.json")
         client.cmd(f"jobs-dump {dump}")
         jobs = json.load(open(dump))
