@@ -218,6 +218,14 @@ PYBIND11_MODULE(_C, m) {
                   S(stream));
   }, py::arg("x"), py::arg("wf1"), py::arg("b1"), py::arg("wf2"), py::arg("b2"), py::arg("y"), py::arg("zero"),
         py::arg("B"), py::arg("stream"));
+  m.def("bottleneck56", [](uintptr_t x, uintptr_t w1, uintptr_t a1, uintptr_t b1, uintptr_t wf2, uintptr_t b2,
+                           uintptr_t wf3, uintptr_t b3, uintptr_t y, float res_scale, float out_inv_scale, int B,
+                           uintptr_t stream, int dbg) {
+    bottleneck56(P<void>(x), P<void>(w1), P<float>(a1), P<float>(b1), P<void>(wf2), P<float>(b2), P<void>(wf3),
+                 P<float>(b3), P<void>(y), res_scale, out_inv_scale, B, S(stream), dbg);
+  }, py::arg("x"), py::arg("w1"), py::arg("a1"), py::arg("b1"), py::arg("wf2"), py::arg("b2"), py::arg("wf3"),
+     py::arg("b3"), py::arg("y"), py::arg("res_scale"), py::arg("out_inv_scale"), py::arg("B"), py::arg("stream") = 0,
+     py::arg("dbg") = 0);
   m.def("conv3x3_s2rows_supported", &conv3x3_s2rows_supported);
   m.def("conv3x3_s2rows", [](uintptr_t x, uintptr_t wf, uintptr_t bias, uintptr_t wdf, uintptr_t bd, uintptr_t y,
                              uintptr_t yd, uintptr_t zero, int B, bool relu, uintptr_t stream, int dbg) {

@@ -1,0 +1,378 @@
+// Fused ResNet50 identity bottleneck for layer1 (resnet50_fp8: layer1.1 and
+// layer1.2), 56x56x256 e4m3 in and out:
+//   t1 = relu(bn1(conv1x1 256->64 (x)))          e4m3 MFMA, t1 bf16 in LDS
+//   t2 = relu(bn2(conv3x3 64->64 (t1)))          bf16 MFMA, t2 bf16 in LDS
+//   y  = relu(bn3(conv1x1 64->256 (t2)) + x)     bf16 MFMA, y e4m3
+// in ONE kernel: x is read once (conv1 operand, then the residual as an L2
+// hit), y written once, and the two 64-channel intermediates never leave LDS.
+//
+// Reference equivalent: torchvision Bottleneck.forward (conv1/bn1/relu,
+// conv2/bn2/relu, conv3/bn3, += identity, relu) of tch::vision::resnet50, run
+// per query by `forward_t` (src/services.rs:493; BASELINE config 5). As three
+// conv1x1 / conv3x3 launches one layer1 block moved ~1.6 GB at B=256 (the
+// 256-channel input read twice, the 64-channel intermediates written and read
+// back) and took ~245 us (profiles/r2_resnet50_fp8_ops_conv1x1.txt); fused it
+// moves ~0.4 GB.
+//
+// One workgroup = one image, 8 waves, 4 output rows (224 pixels = 14 pixel
+// fragments of 16) per step. Per step k (output rows 4k .. 4k+3):
+//   phase 1: conv1 -> t1 rows 4k+1 .. 4k+4 (a 6-row LDS ring; rows -1 and 56
+//            are conv2's zero padding), X fragments straight from HBM/L2
+//   phase 2: conv2 over t1 rows 4k-1 .. 4k+4 -> t2 (224 x 64, LDS)
+//   phase 3: conv3 over t2 + residual -> y rows 4k .. 4k+3
+// with a workgroup barrier after phases 1 and 2 (phase 3 of step k and phase
+// 1 of step k+1 touch disjoint LDS). A prologue phase 1 writes t1 rows -3..0.
+// Wave w: channel half wn = w & 1 (32 channels, 2 N fragments with the perm32
+// row order, so a lane ends with 8 consecutive channels of one pixel) of conv1
+// and conv2 (128 channels of conv3), and a pixel-fragment set: waves 0-3 take
+// fragments {0..3} / {7..10}, waves 4-7 {4..6} / {11..13}, so the two waves
+// sharing a SIMD (w, w+4) together always own 7 fragments.
+#include "common.h"
+#include "kernels.h"
+
+namespace dmlc {
+
+namespace {
+
+typedef int v8i __attribute__((ext_vector_type(8)));
+
+struct BnArgs {
+  const uint8_t* x;    // [B, 56, 56, 256] e4m3 (value = e4m3 * res_scale)
+  const uint8_t* w1;   // [64][256] e4m3 (per-row scales folded into a1)
+  const float* a1;     // [64] s_x * s_w1[n]
+  const float* b1;     // [64]
+  const bf16* wf2;     // conv2 weights, fragment order [2][18][2][64][8] (stream_frag_index, K = 576)
+  const float* b2;     // [64]
+  const bf16* wf3;     // conv3 weights, fragment order [8][2][2][64][8] (K = 64)
+  const float* b3;     // [256]
+  uint8_t* y;          // [B, 56, 56, 256] e4m3
+  float res_scale;     // s_x
+  float out_inv_scale; // 1 / s_y
+  int dbg;             // experiments (tools/bottleneck_bench.py): bit 0 no y stores (kept live), bit 1 no
+                       // residual loads, bit 2 no conv1 X loads, bit 3 no conv2 K loop
+};
+
+constexpr int kH = 56, kW = 56, kC = 256, kM = 64;
+constexpr int kR = 4;                    // output rows per step
+constexpr int kPix = kR * kW;            // 224 pixels per step
+constexpr int kSteps = kH / kR;          // 14
+constexpr int kHalf = (kW + 2) * 64;     // t1 slot: one 32-channel half, 58 columns x 64 B = 3712 B
+constexpr int kSlot = 2 * kHalf;         // 7424 B per t1 row
+constexpr int kRing = 6;                 // t1 rows 4k-1 .. 4k+4
+constexpr int kT2 = kPix * kM * 2;       // 28672 B
+constexpr int kKS2 = 9 * kM / 32;        // 18 conv2 K steps
+constexpr int kPD = 6;                   // conv2 weight register ring depth (divides kKS2)
+constexpr size_t kLds = (size_t)kRing * kSlot + kT2;
+
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+}
+
+__device__ __forceinline__ uint32_t f32x4_to_fp8(const float* f) {
+  float c[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) c[i] = fminf(fmaxf(f[i], -448.f), 448.f);
+  int v = __builtin_amdgcn_cvt_pk_fp8_f32(c[0], c[1], 0, false);
+  v = __builtin_amdgcn_cvt_pk_fp8_f32(c[2], c[3], v, true);
+  return (uint32_t)v;
+}
+
+__device__ __forceinline__ void fp8x4_to_f32(uint32_t u, float* f) {
+  f[0] = __builtin_amdgcn_cvt_f32_fp8((int)u, 0);
+  f[1] = __builtin_amdgcn_cvt_f32_fp8((int)u, 1);
+  f[2] = __builtin_amdgcn_cvt_f32_fp8((int)u, 2);
+  f[3] = __builtin_amdgcn_cvt_f32_fp8((int)u, 3);
+}
+
+// t1 ring address of (row slot byte base, staged column q, channel half h,
+// 16-B chunk g): the conv3x3_block.hip layout (chunk c of (h, q) holds
+// channels 8 (4h + (c ^ ((q >> 1) & 3))); pad columns q = 0, 57 stay zero)
+__device__ __forceinline__ int t1_off(int q, int h, int g) { return h * kHalf + q * 64 + ((g ^ ((q >> 1) & 3)) << 4); }
+// t2: pixel p's 8 chunks of 8 channels, chunk c at physical c ^ ((p >> 1) & 7)
+// (every 16-lane group of a fragment read hits 16 distinct bank slots)
+__device__ __forceinline__ int t2_off(int p, int c) { return p * 128 + ((c ^ ((p >> 1) & 7)) << 4); }
+
+// One wave's share of the whole kernel: fragments F0 .. F0+NFR-1.
+template <int F0, int NFR>
+__device__ __forceinline__ void bn_wave(const BnArgs& a, char* ring, char* t2, int wn, int lane) {
+  const int fr = lane & 15, g = lane >> 4;
+  const int b = blockIdx.x;
+  const uint8_t* xim = a.x + (long)b * kH * kW * kC;
+  uint8_t* yim = a.y + (long)b * kH * kW * kC;
+
+  // per-lane pixel geometry: fragment f's lane pixel p = 16 (F0 + f) + fr sits
+  // in tile row tr[f] = base row TB(f) (compile time) + hi bit
+  int col[NFR], hi = 0;
+#pragma unroll
+  for (int f = 0; f < NFR; ++f) {
+    const int p = 16 * (F0 + f) + fr;
+    col[f] = p % kW;
+    hi |= (p / kW - (16 * (F0 + f)) / kW) << f;
+  }
+  // this lane's 8 channels of a 32-channel group: 8g .. 8g+7 (perm32);
+  // per-channel constants and the conv1 weights are (re)loaded in their phase
+  // (L1/L2 hits) instead of held in VGPRs through the whole kernel
+  const int c1 = 32 * wn + 8 * g;  // conv1 / conv2 output channels
+  auto load8 = [](const float* p, float* v) __attribute__((always_inline)) {
+    const float4 lo = *(const float4*)p, h4 = *(const float4*)(p + 4);
+    v[0] = lo.x, v[1] = lo.y, v[2] = lo.z, v[3] = lo.w, v[4] = h4.x, v[5] = h4.y, v[6] = h4.z, v[7] = h4.w;
+  };
+  // conv2 weight ring (fragment order, this wave's 32-channel group)
+  const __amdgpu_buffer_rsrc_t w2rs = wave_rsrc(a.wf2 + (long)wn * kKS2 * 2 * 512, kKS2 * 2 * 1024);
+  auto w2load = [&](int kf) __attribute__((always_inline)) {
+    return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(w2rs, lane * 16, kf * 1024, 0));
+  };
+  bf16x8 wq[kPD][2];
+#pragma unroll
+  for (int ks = 0; ks < kPD - 1; ++ks)
+#pragma unroll
+    for (int nf = 0; nf < 2; ++nf) wq[ks][nf] = w2load(ks * 2 + nf);
+  // conv3 weights: groups 4 wn + gi (gi = 0..3), [group][ks][nf][64][8]
+  const __amdgpu_buffer_rsrc_t w3rs = wave_rsrc(a.wf3 + (long)wn * 4 * 2 * 2 * 512, 4 * 2 * 2 * 1024);
+
+  // ---- phase 1: conv1 -> t1 rows 4j+1 .. 4j+4 (rows outside the image: zeros)
+  auto conv1 = [&](int j) __attribute__((always_inline)) {
+    // conv1 weights, fragment nf row rr = channel 32 wn + perm32(16 nf + rr):
+    // lane (rr, g) holds k = 128 ks + 32 g .. +32 (e4m3)
+    v8i w1f[2][2];
+#pragma unroll
+    for (int nf = 0; nf < 2; ++nf) {
+      const int ch = 32 * wn + 8 * (fr >> 2) + 4 * nf + (fr & 3);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const uint4 lo = *(const uint4*)(a.w1 + ch * kC + ks * 128 + g * 32);
+        const uint4 h4 = *(const uint4*)(a.w1 + ch * kC + ks * 128 + g * 32 + 16);
+        w1f[nf][ks] = v8i{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)h4.x, (int)h4.y, (int)h4.z, (int)h4.w};
+      }
+    }
+    float a1v[8], b1v[8];
+    load8(a.a1 + c1, a1v);
+    load8(a.b1 + c1, b1v);
+    v8i xb[NFR][2];
+#pragma unroll
+    for (int f = 0; f < NFR; ++f) {
+      const int r = 4 * j + 1 + (16 * (F0 + f)) / kW + ((hi >> f) & 1);
+      const int rc = min(max(r, 0), kH - 1);
+      const uint8_t* src = xim + ((long)rc * kW + col[f]) * kC + g * 32;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        uint4 lo = make_uint4(0x38383838u, 0, 0, 0), h4 = make_uint4(0, 0, 0, 0);
+        if (!(a.dbg & 4)) {
+          lo = *(const uint4*)(src + ks * 128);
+          h4 = *(const uint4*)(src + ks * 128 + 16);
+        }
+        xb[f][ks] = v8i{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)h4.x, (int)h4.y, (int)h4.z, (int)h4.w};
+      }
+    }
+#pragma unroll
+    for (int f = 0; f < NFR; ++f) {
+      floatx4 acc[2] = {floatx4{0.f, 0.f, 0.f, 0.f}, floatx4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int nf = 0; nf < 2; ++nf)
+          acc[nf] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(w1f[nf][ks], xb[f][ks], acc[nf], 0, 0, 0, 127,
+                                                                     0, 127);
+      const int r = 4 * j + 1 + (16 * (F0 + f)) / kW + ((hi >> f) & 1);
+      const bool outside = (unsigned)r >= (unsigned)kH;
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float raw = acc[e >> 2][e & 3];
+        v[e] = outside ? 0.f : fmaxf(raw * a1v[e] + b1v[e], 0.f);
+      }
+      const int q = col[f] + 1;
+      *(uint4*)(ring + ((r + kRing) % kRing) * kSlot + t1_off(q, wn, g)) = pack8(v);
+    }
+  };
+
+  conv1(-1);
+  lds_barrier();
+  for (int k = 0; k < kSteps; ++k) {
+    conv1(k);
+    lds_barrier();
+
+    // ---- phase 2: conv2 over t1 rows 4k-1 .. 4k+4 -> t2
+    {
+      // slot byte offsets of t1 rows 4k-1+i (wave-uniform)
+      // (named scalars, not an array: a per-lane select between array elements
+      // becomes a dynamically indexed private array in scratch)
+      const int s0 = ((4 * k - 1 + kRing) % kRing) * kSlot;
+      auto sl = [&](int i) __attribute__((always_inline)) {  // i compile time
+        const int v = s0 + i * kSlot;
+        return v >= kRing * kSlot ? v - kRing * kSlot : v;
+      };
+      floatx4 acc[NFR][2];
+#pragma unroll
+      for (int f = 0; f < NFR; ++f) acc[f][0] = acc[f][1] = floatx4{0.f, 0.f, 0.f, 0.f};
+      bf16x8 xc[NFR], xn[NFR];
+      auto load_k = [&](int ks, bf16x8* xd) __attribute__((always_inline)) {
+        const int tap = ks >> 1, h = ks & 1;
+        const int kh = tap / 3, kw = tap % 3;
+#pragma unroll
+        for (int f = 0; f < NFR; ++f) {
+          const int tb = (16 * (F0 + f)) / kW + kh;  // ring index of the fragment's base row (+0 / +1 per lane)
+          const int so = ((hi >> f) & 1) ? sl(tb + 1) : sl(tb);
+          xd[f] = *(const bf16x8*)(ring + so + t1_off(col[f] + kw, h, g));
+        }
+      };
+      load_k(0, xc);
+      const int nks = (a.dbg & 8) ? 1 : kKS2;
+#pragma unroll
+      for (int ks = 0; ks < kKS2; ++ks) {
+        if (ks >= nks) break;
+        if (ks + 1 < kKS2) load_k(ks + 1, xn);
+        {  // K step ks + PD - 1, wrapping into the next step's first ones
+          const int kl = (ks + kPD - 1) % kKS2;
+#pragma unroll
+          for (int nf = 0; nf < 2; ++nf) wq[(ks + kPD - 1) % kPD][nf] = w2load(kl * 2 + nf);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int f = 0; f < NFR; ++f)
+#pragma unroll
+          for (int nf = 0; nf < 2; ++nf)
+            acc[f][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wq[ks % kPD][nf], xc[f], acc[f][nf], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (ks + 1 < kKS2) {
+#pragma unroll
+          for (int f = 0; f < NFR; ++f) xc[f] = xn[f];
+        }
+      }
+      float b2v[8];
+      load8(a.b2 + c1, b2v);
+#pragma unroll
+      for (int f = 0; f < NFR; ++f) {
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = fmaxf(acc[f][e >> 2][e & 3] + b2v[e], 0.f);
+        const int p = 16 * (F0 + f) + fr;
+        *(uint4*)(t2 + t2_off(p, 4 * wn + g)) = pack8(v);
+      }
+    }
+    lds_barrier();
+
+    // ---- phase 3: conv3 over t2 + residual -> y rows 4k .. 4k+3
+    {
+      bf16x8 xt[NFR][2];
+#pragma unroll
+      for (int f = 0; f < NFR; ++f) {
+        const int p = 16 * (F0 + f) + fr;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) xt[f][ks] = *(const bf16x8*)(t2 + t2_off(p, 4 * ks + g));
+      }
+      constexpr int GP = 1;  // 32-channel groups per pass (VGPRs: accumulators + weights + residuals)
+#pragma unroll
+      for (int pass = 0; pass < 4 / GP; ++pass) {
+        // groups gi = GP pass .. of this wave's 4: channels 128 wn + 32 gi + 8 g .. +7
+        bf16x8 w3[GP][2][2];  // [group][ks][nf]
+#pragma unroll
+        for (int gg = 0; gg < GP; ++gg)
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int nf = 0; nf < 2; ++nf)
+              w3[gg][ks][nf] = __builtin_bit_cast(
+                  bf16x8, __builtin_amdgcn_raw_buffer_load_b128(w3rs, lane * 16,
+                                                                (((GP * pass + gg) * 2 + ks) * 2 + nf) * 1024, 0));
+        uint2 rv[NFR][GP];
+        long pix[NFR];
+#pragma unroll
+        for (int f = 0; f < NFR; ++f) {
+          const int o = 4 * k + (16 * (F0 + f)) / kW + ((hi >> f) & 1);
+          pix[f] = ((long)o * kW + col[f]) * kC;
+#pragma unroll
+          for (int gg = 0; gg < GP; ++gg)
+            rv[f][gg] = (a.dbg & 2) ? make_uint2(0, 0)
+                                    : *(const uint2*)(xim + pix[f] + 128 * wn + 32 * (GP * pass + gg) + 8 * g);
+        }
+        floatx4 acc[NFR][GP][2];
+#pragma unroll
+        for (int f = 0; f < NFR; ++f)
+#pragma unroll
+          for (int gg = 0; gg < GP; ++gg) acc[f][gg][0] = acc[f][gg][1] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int f = 0; f < NFR; ++f)
+#pragma unroll
+            for (int gg = 0; gg < GP; ++gg)
+#pragma unroll
+              for (int nf = 0; nf < 2; ++nf)
+                acc[f][gg][nf] =
+                    __builtin_amdgcn_mfma_f32_16x16x32_bf16(w3[gg][ks][nf], xt[f][ks], acc[f][gg][nf], 0, 0, 0);
+#pragma unroll
+        for (int gg = 0; gg < GP; ++gg) {
+          const int c3 = 128 * wn + 32 * (GP * pass + gg) + 8 * g;
+          float b3v[8];
+          load8(a.b3 + c3, b3v);
+#pragma unroll
+          for (int f = 0; f < NFR; ++f) {
+            float v[8], rf[8];
+            fp8x4_to_f32(rv[f][gg].x, rf);
+            fp8x4_to_f32(rv[f][gg].y, rf + 4);
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              v[e] = fmaxf(acc[f][gg][e >> 2][e & 3] + b3v[e] + rf[e] * a.res_scale, 0.f) * a.out_inv_scale;
+            const uint2 q = make_uint2(f32x4_to_fp8(v), f32x4_to_fp8(v + 4));
+            if (!(a.dbg & 1) || q.x == 0x12345678u) *(uint2*)(yim + pix[f] + c3) = q;
+          }
+        }
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(512, 1) void bottleneck56_kernel(BnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint4 smem[];
+  char* ring = (char*)smem;
+  char* t2 = ring + kRing * kSlot;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // zero the t1 ring (its pad columns stay zero for the whole kernel)
+  for (int i = tid; i < kRing * kSlot / 16; i += 512) ((uint4*)ring)[i] = make_uint4(0, 0, 0, 0);
+  lds_barrier();
+  const int wn = wave & 1;
+  switch (wave >> 1) {
+    case 0: bn_wave<0, 4>(a, ring, t2, wn, lane); break;
+    case 1: bn_wave<7, 4>(a, ring, t2, wn, lane); break;
+    case 2: bn_wave<4, 3>(a, ring, t2, wn, lane); break;
+    default: bn_wave<11, 3>(a, ring, t2, wn, lane); break;
+  }
+}
+
+}  // namespace
+
+bool bottleneck56_supported(int H, int W, int C, int Cm) { return H == kH && W == kW && C == kC && Cm == kM; }
+
+void bottleneck56(const void* x, const void* w1, const float* a1, const float* b1, const void* wf2, const float* b2,
+                  const void* wf3, const float* b3, void* y, float res_scale, float out_inv_scale, int B,
+                  hipStream_t s, int dbg) {
+  if (B <= 0) return;
+  if (!x || !w1 || !a1 || !b1 || !wf2 || !b2 || !wf3 || !b3 || !y ||
+      (((uintptr_t)x | (uintptr_t)w1 | (uintptr_t)wf2 | (uintptr_t)wf3 | (uintptr_t)y) & 15))
+    throw std::invalid_argument("bottleneck56: null / misaligned operand");
+  if (x == y) throw std::invalid_argument("bottleneck56: in-place not supported (the residual is re-read)");
+  BnArgs a;
+  a.x = (const uint8_t*)x;
+  a.w1 = (const uint8_t*)w1;
+  a.a1 = a1;
+  a.b1 = b1;
+  a.wf2 = (const bf16*)wf2;
+  a.b2 = b2;
+  a.wf3 = (const bf16*)wf3;
+  a.b3 = b3;
+  a.y = (uint8_t*)y;
+  a.res_scale = res_scale;
+  a.out_inv_scale = out_inv_scale;
+  a.dbg = dbg;
+  hipLaunchKernelGGL(bottleneck56_kernel, dim3(B), dim3(512), kLds, s, a);
+  DMLC_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace dmlc

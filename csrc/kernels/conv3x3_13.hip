@@ -1,0 +1,214 @@
+// Direct 3x3 / stride 1 / pad 1 convolution on 13x13 images with the whole
+// input image resident in LDS (AlexNet features.6 / .8 / .10: 13x13x192 ->
+// 384, 384 -> 256, 256 -> 256), bias (+ ReLU), bf16 NHWC in and out.
+//
+// Reference equivalent: those Conv2d + ReLU modules of tch::vision::alexnet,
+// run per query by `forward_t` (src/services.rs:493). As implicit-GEMM tiles
+// (conv_igemm.hip, 128x128) every tile re-gathers its 3x3 windows through L2
+// and the three convs ran at 680-870 TFLOP/s (66 / 105 / 75 us at B=256,
+// profiles/r3_alexnet_ops_blaslt.txt). Here one workgroup = one image:
+//
+//  * the image (169 pixels, 75-130 KB) goes HBM -> LDS once by LDS-DMA, its
+//    16-B chunks XOR-swizzled per pixel (the conv3x3_stream.hip scheme: every
+//    16-lane group of a fragment read hits 16 distinct bank slots); pixels are
+//    padded to a multiple of 256 B; taps outside the image read one zero pixel;
+//  * a wave owns 32 output channels (2 N fragments, perm32 row order: a lane
+//    ends with 8 consecutive channels of one pixel) for all 11 pixel
+//    fragments, so each weight fragment feeds 11 MFMAs and each X fragment 2;
+//    the weights stream from L2 in fragment order (stream_frag_index) through
+//    a PD-deep register ring, no LDS stage and no barrier in the K loop;
+//  * Cout / 32 channel groups over 8 waves: 8 groups (Cout 256) one per wave;
+//    12 (Cout 384): waves 0-3 take two, so every SIMD (waves w, w + 4) runs 3.
+#include "common.h"
+#include "kernels.h"
+
+namespace dmlc {
+
+namespace {
+
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+
+struct D13Args {
+  const bf16* x;      // [B, 13, 13, CI]
+  const bf16* wf;     // [CO/32][KT][2][64][8] fragment order (stream_frag_index, K = 9 CI)
+  const float* bias;  // [CO]
+  bf16* y;            // [B, 13, 13, CO]
+  const bf16* zero;   // >= 16 zero bytes
+  int relu;
+};
+
+constexpr int kH = 13, kW = 13, kNPix = kH * kW;  // 169
+constexpr int kMF = (kNPix + 15) / 16;             // 11 pixel fragments
+
+// chunk swizzle of a staged pixel with key K (its pixel index): >= 256-B
+// pixels, as conv3x3_stream.hip's xswz for CPX >= 16
+__device__ __forceinline__ int swz13(int K) { return (K & 7) << 1; }
+
+template <int CI>
+struct D13Geom {
+  static constexpr int CPX = CI / 8;                    // 16-B chunks per pixel
+  static constexpr int PXC = (CPX + 15) / 16 * 16;      // padded chunks per staged pixel
+  static constexpr int PXB = PXC * 16;                  // bytes per staged pixel
+  static constexpr int ZB = kNPix * PXB;                // zero pixel
+  static constexpr size_t LDS = (size_t)ZB + PXB;
+};
+
+template <int CI, int CO, int PD>
+__global__ __launch_bounds__(512, 1) void conv3x3_13_kernel(D13Args a) {
+  using G = D13Geom<CI>;
+  constexpr int CPX = G::CPX, PXC = G::PXC, PXB = G::PXB, ZB = G::ZB;
+  constexpr int CT = CI / 32;       // K steps per tap
+  constexpr int KT = 9 * CT;        // K steps
+  constexpr int NGRP = CO / 32;     // channel groups (tasks)
+  static_assert(CT % PD == 0, "the weight ring's slot must be a compile-time function of the K step in a tap");
+  static_assert(NGRP == 8 || NGRP == 12, "channel groups: one per wave, or 3 per SIMD");
+  extern __shared__ __attribute__((aligned(16))) uint4 smem[];
+  char* xs = (char*)smem;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, g = lane >> 4;
+  const int b = blockIdx.x;
+  const bf16* img = a.x + (long)b * kNPix * CI;
+
+  // ---- stage the image: physical slot ps = K * PXC + pc holds logical chunk
+  // pc ^ swz(K) of pixel K (slots whose logical chunk is past CPX: padding,
+  // loaded from the zero page); one LDS-DMA instruction = 64 slots
+  constexpr int NSLOT = kNPix * PXC;
+  for (int i = wave; i * 64 < NSLOT; i += 8) {
+    const int ps = i * 64 + lane;
+    if (ps < NSLOT) {
+      const int K = ps / PXC, pc = ps - K * PXC;
+      const int lc = pc ^ swz13(K);
+      dma16(lc < CPX ? (const void*)(img + (long)K * CI + lc * 8) : (const void*)a.zero, xs + i * 1024);
+    }
+  }
+  if (tid < PXB / 16) ((uint4*)(xs + ZB))[tid] = make_uint4(0, 0, 0, 0);
+
+  // ---- per-lane pixel constants: p = 16 f + fr (clamped for the padding lanes
+  // of the last fragment: they compute a duplicate, never stored); xoff = the
+  // staged offset of the pixel, low 4 bits = first/last row/column flags
+  int xoff[kMF];
+#pragma unroll
+  for (int f = 0; f < kMF; ++f) {
+    const int p = min(16 * f + fr, kNPix - 1);
+    const int r = p / kW, c = p - r * kW;
+    xoff[f] = p * PXB | (r == 0 ? 1 : 0) | (r == kH - 1 ? 2 : 0) | (c == 0 ? 4 : 0) | (c == kW - 1 ? 8 : 0);
+    asm volatile("" : "+v"(xoff[f]));  // keep it live (no rematerialised divides in the loop)
+  }
+  int xa[kMF], tsw = 0;
+  auto set_tap = [&](int tap) __attribute__((always_inline)) {
+    const int kh = tap / 3, kw = tap - kh * 3;
+    const int tm = (kh == 0 ? 1 : 0) | (kh == 2 ? 2 : 0) | (kw == 0 ? 4 : 0) | (kw == 2 ? 8 : 0);
+    const int ktap = (kh - 1) * kW + kw - 1;
+#pragma unroll
+    for (int f = 0; f < kMF; ++f) xa[f] = (xoff[f] & tm) ? ZB : (xoff[f] & ~15) + ktap * PXB;
+    // K = p + ktap with p & 15 == fr for every real pixel: one swizzle per tap
+    tsw = (g << 4) ^ (swz13(fr + ktap) << 4);
+  };
+  auto xread = [&](int f, int cc) __attribute__((always_inline)) {
+    return *(const bf16x8*)(xs + xa[f] + (tsw ^ (cc * 64)));
+  };
+
+  vm_wait<0>();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+
+#pragma nounroll
+  for (int grp = wave; grp < NGRP; grp += 8) {
+    const __amdgpu_buffer_rsrc_t wrs = wave_rsrc(a.wf + (long)grp * KT * 2 * 512, KT * 2 * 1024);
+    auto wfrag = [&](int t, int nf) __attribute__((always_inline)) {
+      return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, lane * 16, (t * 2 + nf) * 1024, 0));
+    };
+    bf16x8 wq[PD][2];
+#pragma unroll
+    for (int t = 0; t < PD - 1; ++t)
+#pragma unroll
+      for (int nf = 0; nf < 2; ++nf) wq[t][nf] = wfrag(t, nf);
+    floatx4 acc[kMF][2];
+#pragma unroll
+    for (int f = 0; f < kMF; ++f) acc[f][0] = acc[f][1] = floatx4{0.f, 0.f, 0.f, 0.f};
+    set_tap(0);
+    bf16x8 xf[kMF];
+#pragma unroll
+    for (int f = 0; f < kMF; ++f) xf[f] = xread(f, 0);
+#pragma nounroll
+    for (int tap = 0; tap < 9; ++tap) {
+#pragma unroll
+      for (int cc = 0; cc < CT; ++cc) {
+        const int t = tap * CT + cc;
+        if (t + PD - 1 < KT)
+#pragma unroll
+          for (int nf = 0; nf < 2; ++nf) wq[(cc + PD - 1) % PD][nf] = wfrag(t + PD - 1, nf);
+        // next K step's X: same tap at cc + 1, or the next tap's first (the
+        // final step re-reads a valid tile, unused)
+        if (cc + 1 == CT && tap + 1 < 9) set_tap(tap + 1);
+        const int cn = cc + 1 == CT ? 0 : cc + 1;
+#pragma unroll
+        for (int f = 0; f < kMF; ++f) {
+#pragma unroll
+          for (int nf = 0; nf < 2; ++nf)
+            acc[f][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wq[cc % PD][nf], xf[f], acc[f][nf], 0, 0, 0);
+          xf[f] = xread(f, cn);
+        }
+      }
+    }
+    // ---- epilogue: lane holds channels 32 grp + 8 g .. +7 of pixel 16 f + fr
+    const int ch = 32 * grp + 8 * g;
+    float bs[8];
+    {
+      const float4 lo = *(const float4*)(a.bias + ch), hi = *(const float4*)(a.bias + ch + 4);
+      bs[0] = lo.x, bs[1] = lo.y, bs[2] = lo.z, bs[3] = lo.w, bs[4] = hi.x, bs[5] = hi.y, bs[6] = hi.z, bs[7] = hi.w;
+    }
+    bf16* yim = a.y + (long)b * kNPix * CO;
+#pragma unroll
+    for (int f = 0; f < kMF; ++f) {
+      const int p = 16 * f + fr;
+      if (p < kNPix) {
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          v[e] = acc[f][e >> 2][e & 3] + bs[e];
+          if (a.relu) v[e] = fmaxf(v[e], 0.f);
+        }
+        *(uint4*)(yim + (long)p * CO + ch) = pack8(v);
+      }
+    }
+  }
+}
+
+template <int CI, int CO, int PD>
+void launch13(const D13Args& a, int B, hipStream_t s) {
+  hipLaunchKernelGGL((conv3x3_13_kernel<CI, CO, PD>), dim3(B), dim3(512), D13Geom<CI>::LDS, s, a);
+}
+
+}  // namespace
+
+bool conv3x3_13_supported(int H, int W, int Cin, int Cout) {
+  return H == kH && W == kW &&
+         ((Cin == 192 && Cout == 384) || (Cin == 384 && Cout == 256) || (Cin == 256 && Cout == 256));
+}
+
+void conv3x3_13(const void* x, const void* wf, const float* bias, void* y, const void* zero, int B, int Cin, int Cout,
+                bool relu, hipStream_t s) {
+  if (B <= 0) return;
+  if (!conv3x3_13_supported(kH, kW, Cin, Cout)) throw std::invalid_argument("conv3x3_13: unsupported channels");
+  if (!x || !wf || !bias || !y || !zero || (((uintptr_t)x | (uintptr_t)wf | (uintptr_t)y | (uintptr_t)zero) & 15))
+    throw std::invalid_argument("conv3x3_13: null / misaligned operand");
+  D13Args a;
+  a.x = (const bf16*)x;
+  a.wf = (const bf16*)wf;
+  a.bias = bias;
+  a.y = (bf16*)y;
+  a.zero = (const bf16*)zero;
+  a.relu = relu ? 1 : 0;
+  if (Cin == 192) launch13<192, 384, 3>(a, B, s);
+  else if (Cin == 384) launch13<384, 256, 4>(a, B, s);
+  else launch13<256, 256, 4>(a, B, s);
+  DMLC_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace dmlc

@@ -152,6 +152,20 @@ void conv3x3_rows(const void* x, const void* w, const float* bias, const void* r
 bool conv3x3_block_supported(int H, int W, int C);
 void conv3x3_block(const void* x, const void* wf1, const float* bias1, const void* wf2, const float* bias2, void* y,
                    const void* zero, int B, hipStream_t s);
+// Direct 3x3/s1/p1 conv on 13x13 images, the whole image in LDS
+// (conv3x3_13.hip): AlexNet features.6/.8/.10 (192->384, 384->256,
+// 256->256). wf: fragment-order weights (stream_frag_index, K = 9 Cin).
+bool conv3x3_13_supported(int H, int W, int Cin, int Cout);
+void conv3x3_13(const void* x, const void* wf, const float* bias, void* y, const void* zero, int B, int Cin, int Cout,
+                bool relu, hipStream_t s);
+// ResNet50 layer1 identity bottleneck (resnet50_fp8 layer1.1 / 1.2) in one
+// kernel (bottleneck56.hip): x, y e4m3 [B,56,56,256]; w1 e4m3 [64][256] with
+// a1 = s_x * s_w1; wf2 / wf3: fragment-order bf16 weights (stream_frag_index,
+// K = 576 / 64); y = relu(conv3(relu(conv2(relu(conv1(x))))) + x) / s_y.
+bool bottleneck56_supported(int H, int W, int C, int Cm);
+void bottleneck56(const void* x, const void* w1, const float* a1, const float* b1, const void* wf2, const float* b2,
+                  const void* wf3, const float* b3, void* y, float res_scale, float out_inv_scale, int B,
+                  hipStream_t s, int dbg = 0);
 // ResNet layer2.0's stride-2 3x3 conv 56x56x64 -> 28x28x128 and its 1x1/s2
 // downsample in one row-streaming, weight-stationary kernel
 // (conv3x3_s2rows.hip): one workgroup per image. wf / wdf: fragment-order

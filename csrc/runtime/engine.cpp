@@ -77,11 +77,12 @@ bool EngineOptions::set(const std::string& name, bool v) {
       {"persistent", &EngineOptions::persistent},   {"fused_stem", &EngineOptions::fused_stem},
       {"fused_preprocess", &EngineOptions::fused_preprocess}, {"row_conv", &EngineOptions::row_conv},
       {"rows_wreg", &EngineOptions::rows_wreg},     {"fused_block", &EngineOptions::fused_block},
+      {"fused_bottleneck", &EngineOptions::fused_bottleneck},
       {"stream_conv", &EngineOptions::stream_conv}, {"stream_wreg", &EngineOptions::stream_wreg},
       {"stream_l4s2", &EngineOptions::stream_l4s2}, {"fuse_ds", &EngineOptions::fuse_ds},
       {"bigtile", &EngineOptions::bigtile},         {"fused_pool", &EngineOptions::fused_pool},
       {"fused_head", &EngineOptions::fused_head},   {"fc_small", &EngineOptions::fc_small},
-      {"blaslt_fc", &EngineOptions::blaslt_fc},
+      {"blaslt_fc", &EngineOptions::blaslt_fc},     {"direct13", &EngineOptions::direct13},
       {"fork_ds", &EngineOptions::fork_ds},         {"fp8_3x3", &EngineOptions::fp8_3x3},
       {"conv1x1", &EngineOptions::conv1x1},         {"s2rows", &EngineOptions::s2rows},
       {"rows28", &EngineOptions::rows28},
@@ -434,6 +435,10 @@ void Engine::pack_weights(const WeightMap& w) {
       L.wf_off = off;  // fragment-order copy for the register-weight stream conv
       off = align_up(off + (size_t)L.cout * L.kpad * 2, 256);
     }
+    if (bottleneck_conv3(L)) {  // fragment-order copy for bottleneck56.hip's expand conv
+      L.wf_off = off;
+      off = align_up(off + (size_t)L.cout * L.kpad * 2, 256);
+    }
     if (L.alex_stem) {  // paired-chunk K order for alex_stem.hip
       L.wf_off = off;
       off = align_up(off + (size_t)L.cout * kAlexStemK * 2, 256);
@@ -650,6 +655,8 @@ Engine::ConvPath Engine::conv_path(const Op& op, int B) const {
   if (opt_.rows28 && k3 && L.stride == 1 && L.wf_off && 10 * B >= 7 * rounds * num_cus_ &&
       conv3x3_rows28_supported(is.H, is.W, is.C, L.cout))
     return ConvPath::Rows28;
+  if (opt_.direct13 && k3 && L.stride == 1 && L.wf_off && conv3x3_13_supported(is.H, is.W, is.C, L.cout))
+    return ConvPath::Direct13;
   if (opt_.stream_conv && k3 && !l4s2 && !l1 && 8 * B >= num_cus_ &&
       conv3x3_stream_supported(is.H, is.W, is.C, L.cout, L.stride))
     return ConvPath::Stream;
@@ -731,6 +738,45 @@ bool Engine::block_fusable(size_t oi, int B) const {
   return L1.relu && L2.relu && L1.wf_off && L2.wf_off && conv3x3_block_supported(is.H, is.W, is.C) &&
          L1.cout == is.C && L2.cout == is.C && !shapes_[c1.in].fp8 && !shapes_[c2.out].fp8 &&
          conv_path(c1, B) == ConvPath::Rows && conv_path(c2, B) == ConvPath::Rows;
+}
+
+// A resnet50_fp8 layer1 identity bottleneck's expand conv (1x1, 64 -> 256 on
+// 56x56, bf16 in, e4m3 out): bottleneck56.hip reads its weights in fragment order.
+bool Engine::bottleneck_conv3(const ConvLayer& L) const {
+  if (L.fc || L.fp8 || L.pair || L.stem_pool || L.in_act < 0 || L.kh != 1 || L.kw != 1 || L.stride != 1) return false;
+  const ActShape& is = shapes_[L.in_act];
+  return fp8_ && is.C == 64 && L.cout == 256 && L.kpad == 64 && bottleneck56_supported(is.H, is.W, 256, 64);
+}
+
+// ops[oi..oi+2] = conv1 (1x1 256 -> 64, e4m3 in) + conv2 (3x3 64 -> 64) +
+// conv3 (1x1 64 -> 256 + the block input as residual, e4m3 out) of a
+// resnet50_fp8 layer1 identity block, the intermediates read by nothing else.
+bool Engine::bottleneck_fusable(size_t oi) const {
+  if (!opt_.fused_bottleneck || !fp8_ || oi + 2 >= ops_.size()) return false;
+  const Op& c1 = ops_[oi];
+  const Op& c2 = ops_[oi + 1];
+  const Op& c3 = ops_[oi + 2];
+  if (c1.type != OpType::Conv || c2.type != OpType::Conv || c3.type != OpType::Conv) return false;
+  if (c1.side || c2.side || c3.side || c2.in != c1.out || c3.in != c2.out || c1.res >= 0 || c2.res >= 0 ||
+      c3.res != c1.in)
+    return false;
+  const ConvLayer& L1 = convs_[c1.conv];
+  const ConvLayer& L2 = convs_[c2.conv];
+  const ConvLayer& L3 = convs_[c3.conv];
+  const ActShape& xs = shapes_[c1.in];
+  if (!xs.fp8 || !shapes_[c3.out].fp8 || shapes_[c1.out].fp8 || shapes_[c2.out].fp8) return false;
+  if (!bottleneck56_supported(xs.H, xs.W, xs.C, L1.cout) || !L1.fp8 || L1.kh != 1 || L1.stride != 1 || !L1.relu ||
+      L1.kpad != 256 || L1.npad != 64)
+    return false;
+  if (L2.kh != 3 || L2.kw != 3 || L2.stride != 1 || L2.pad != 1 || !L2.relu || L2.cout != 64 || !L2.wf_off ||
+      L2.kpad != 576)
+    return false;
+  if (!bottleneck_conv3(L3) || !L3.wf_off || !L3.relu) return false;
+  for (size_t j = 0; j < ops_.size(); ++j) {
+    if (j != oi + 1 && (ops_[j].in == c1.out || ops_[j].res == c1.out)) return false;
+    if (j != oi + 2 && (ops_[j].in == c2.out || ops_[j].res == c2.out)) return false;
+  }
+  return true;
 }
 
 // The stride-2 conv1 of a block whose downsample it computes (fuse_ds) on
@@ -854,6 +900,16 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
             break;
           }
         }
+        if (cs == s && bottleneck_fusable(oi)) {
+          const ConvLayer& L2 = convs_[ops_[oi + 1].conv];
+          const ConvLayer& L3 = convs_[ops_[oi + 2].conv];
+          const uint8_t* wa = (const uint8_t*)warena_;
+          bottleneck56(acts_[op.in], wa + L.w_off, (const float*)(wa + L.a_off), (const float*)(wa + L.b_off),
+                       wa + L2.wf_off, (const float*)(wa + L2.b_off), wa + L3.wf_off, (const float*)(wa + L3.b_off),
+                       acts_[ops_[oi + 2].out], shapes_[op.in].scale, 1.f / shapes_[ops_[oi + 2].out].scale, B, s);
+          skip = 2;
+          break;
+        }
         if (cs == s && block_fusable(oi, B)) {
           const ConvLayer& L2 = convs_[ops_[oi + 1].conv];
           const uint8_t* wa = (const uint8_t*)warena_;
@@ -895,6 +951,11 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
             skip_ds = -1;
             break;
           }
+          case ConvPath::Direct13:
+            conv3x3_13(acts_[op.in], (const uint8_t*)warena_ + L.wf_off,
+                       (const float*)((const uint8_t*)warena_ + L.b_off), acts_[op.out], zero_, B, is.C, L.cout,
+                       L.relu, cs);
+            break;
           case ConvPath::Rows28:
             conv3x3_rows28(acts_[op.in], (const uint8_t*)warena_ + L.wf_off,
                            (const float*)((const uint8_t*)warena_ + L.b_off), op.res >= 0 ? acts_[op.res] : nullptr,

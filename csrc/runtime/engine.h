@@ -71,6 +71,7 @@ struct EngineOptions {
   bool row_conv = true;          // direct row-streaming 3x3 convs (conv3x3_rows.hip) for 56x56x64
   bool rows_wreg = true;         // ... with register-streamed weights, 2 workgroups per CU
   bool fused_block = true;       // a 56x56x64 basic block as one kernel (conv3x3_block.hip), B >= 0.7 x CUs
+  bool fused_bottleneck = true;  // resnet50_fp8 layer1 identity bottlenecks as one kernel (bottleneck56.hip)
   bool stream_conv = true;       // direct 3x3 convs with the input resident in LDS (conv3x3_stream.hip)
   bool stream_wreg = true;       // ... with register-streamed weights where available
   bool stream_l4s2 = true;       // ... also for 14x14x256 -> 512 / s2 (register weights only)
@@ -82,8 +83,11 @@ struct EngineOptions {
   bool conv1x1 = true;           // weight-stationary 1x1 convs (conv1x1.hip: ResNet50 bottlenecks)
   bool fused_pool = true;        // the last conv's epilogue computes the global average pool
   bool fused_head = true;        // avgpool + fc + softmax / top-1 in one kernel (head.hip)
+  bool direct13 = true;          // AlexNet's 13x13 3x3 convs with the image resident in LDS (conv3x3_13.hip)
   bool fc_small = true;          // weight-streaming GEMV for fc layers at B <= 16 (fc_small.hip)
-  bool blaslt_fc = true;         // bf16 fc layers above that on hipBLASLt (blaslt.h; AlexNet classifier)
+  // bf16 fc layers above that on hipBLASLt (blaslt.h): faster alone, slower in the two-lane bench
+  // (472-485k vs 518-528k img/s AlexNet, profiles/r3_alexnet_blaslt_ab.txt), so off by default
+  bool blaslt_fc = false;
   // downsample convs on a side stream: measured slower (the branch slows its
   // sibling conv1 by 10-12 us and adds ~10 us of fork/join gaps per block:
   // profiles/r1_fork_ds_timeline.txt); kept to test the side-stream path
@@ -162,13 +166,15 @@ class Engine {
   void run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* idx, float* prob,
                float* logits, hipStream_t s, std::vector<hipEvent_t>* evs, bool trace);
   ConvArgs conv_args(const Op& op, int B, float* logits) const;
-  enum class ConvPath { Stream, Rows, Rows28, OneByOne, BigTile, Igemm };
+  enum class ConvPath { Stream, Rows, Rows28, Direct13, OneByOne, BigTile, Igemm };
   ConvPath conv_path(const Op& op, int B) const;
   bool side_safe(int B) const;
   bool head_fusable(size_t oi) const;
   bool pool_fusable(size_t oi, int B) const;
   bool ds_fusable(size_t oi, int B) const;     // ops oi, oi+1 = downsample + stride-2 stream conv1
   bool block_fusable(size_t oi, int B) const;  // ops oi, oi+1 = a layer1 basic block -> conv3x3_block
+  bool bottleneck_fusable(size_t oi) const;    // ops oi..oi+2 = a layer1 identity bottleneck -> bottleneck56
+  bool bottleneck_conv3(const ConvLayer& L) const;  // L is such a block's expand conv (fragment-order weights)
   bool s2rows_ok(const Op& op, const ConvLayer& D, int B) const;  // layer2.0 conv1 + downsample -> conv3x3_s2rows
   bool fc_blaslt(const Op& op, int B) const;  // this fc op runs on hipBLASLt at batch B
   void prepare_fc(int B, float* logits, hipStream_t s);  // pick hipBLASLt algorithms (outside capture)

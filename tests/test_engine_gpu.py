@@ -311,7 +311,7 @@ def test_weight_stationary_rows_match_stream(gpu, option):
 def test_alexnet_small_batch_fc_matches_reference(gpu, B):
     """Query-sized AlexNet batches run the classifier on the weight-streaming
     split-K GEMV (fc_small.hip): vs fp32 torch.nn, and vs the throughput
-    path (options fc_small=False: hipBLASLt) on the same inputs."""
+    path (options fc_small=False: the implicit GEMM) on the same inputs."""
     model = build("alexnet", seed=51, randomize_bn=True)
     sd = state_dict_f32(model)
     g = torch.Generator().manual_seed(52 + B)
@@ -341,7 +341,7 @@ def test_alexnet_blaslt_fc_matches_reference(gpu, B):
     g = torch.Generator().manual_seed(54 + B)
     img = torch.randint(0, 256, (B, 224, 224, 3), generator=g, dtype=torch.uint8)
     x = img.to(gpu)
-    eng = InferenceEngine("alexnet", sd, max_batch=B)
+    eng = InferenceEngine("alexnet", sd, max_batch=B, options={"blaslt_fc": True})
     idx, prob, logits = eng.predict(x, return_logits=True)
     i2, p2 = eng.predict(x)
     _, _, le = eng.predict(x, return_logits=True, use_graph=False)
@@ -358,6 +358,73 @@ def test_alexnet_blaslt_fc_matches_reference(gpu, B):
     ref = _ref_logits(model, img[:n])
     rel = ((logits[:n].cpu() - ref).norm() / ref.norm()).item()
     assert rel < 3e-2, rel
+
+
+@pytest.mark.parametrize("B", [5, 256])
+def test_alexnet_direct13_matches_igemm(gpu, B):
+    """AlexNet's 13x13 convs (features.6/.8/.10) on the LDS-resident direct
+    conv (conv3x3_13.hip) vs the implicit GEMM (direct13 off): both bf16 MFMA
+    with fp32 accumulation, different K order, so logits agree to bf16
+    rounding; and vs fp32 torch.nn on a few images. The direct kernel is the
+    one that ran: features.8 takes well under the implicit GEMM's time."""
+    model = build("alexnet", seed=57, randomize_bn=True)
+    sd = state_dict_f32(model)
+    g = torch.Generator().manual_seed(58 + B)
+    img = torch.randint(0, 256, (B, 224, 224, 3), generator=g, dtype=torch.uint8)
+    x = img.to(gpu)
+    eng = InferenceEngine("alexnet", sd, max_batch=B)
+    ref_eng = InferenceEngine("alexnet", sd, max_batch=B, options={"direct13": False})
+    fi, _, fl = eng.predict(x, return_logits=True)
+    ri, _, rl = ref_eng.predict(x, return_logits=True)
+    torch.cuda.synchronize()
+    rel = ((fl - rl).norm() / rl.norm()).item()
+    assert rel < 1e-2, rel
+    p = torch.softmax(rl.float().cpu(), -1)
+    top2 = p.topk(2, -1).values
+    near = (top2[:, 0] - top2[:, 1]) < 1e-2
+    assert torch.all((fi.cpu() == ri.cpu()) | near)
+    n = min(B, 8)
+    ref = _ref_logits(model, img[:n])
+    assert ((fl[:n].cpu() - ref).norm() / ref.norm()).item() < 3e-2
+    if B == 256:
+        prof = dict(eng._e.profile(x.data_ptr(), B, 224, 224, 0))
+        rprof = dict(ref_eng._e.profile(x.data_ptr(), B, 224, 224, 0))
+        print("direct13 vs igemm (ms):", {k: (prof[k], rprof[k]) for k in ("features.6", "features.8", "features.10")})
+        assert prof["features.8"] < rprof["features.8"], (prof, rprof)
+
+
+def test_resnet50_fp8_fused_bottleneck_matches_unfused(gpu):
+    """resnet50_fp8's layer1 identity blocks (layer1.1, layer1.2) as one kernel
+    each (bottleneck56.hip: conv1 e4m3 MFMA -> t1 in LDS -> conv2 -> t2 in LDS
+    -> conv3 + residual -> e4m3) vs the three-kernel path (fused_bottleneck
+    off): the same e4m3 / bf16 roundings, different accumulation order in
+    conv2, so logits agree to a few e4m3 ulps, top-1 on all but near-ties; and
+    the fused kernel is the one that ran (its conv2/conv3 ops take no time of
+    their own in the per-op profile)."""
+    model = build("resnet50", seed=61, randomize_bn=True)
+    sd = state_dict_f32(model)
+    g = torch.Generator().manual_seed(62)
+    img = torch.randint(0, 256, (32, 224, 224, 3), generator=g, dtype=torch.uint8)
+    x = img.to(gpu)
+    eng = InferenceEngine("resnet50_fp8", sd, max_batch=32)
+    ref_eng = InferenceEngine("resnet50_fp8", sd, max_batch=32, options={"fused_bottleneck": False})
+    fi, fp, fl = eng.predict(x, return_logits=True, use_graph=False)
+    gi, gp = eng.predict(x)
+    ri, rp, rl = ref_eng.predict(x, return_logits=True, use_graph=False)
+    torch.cuda.synchronize()
+    rel = ((fl - rl).norm() / rl.norm()).item()
+    assert rel < 5e-2, rel
+    p = torch.softmax(rl.float().cpu(), -1)
+    top2 = p.topk(2, -1).values
+    near = (top2[:, 0] - top2[:, 1]) < 5e-2
+    assert torch.all((fi.cpu() == ri.cpu()) | near)
+    assert torch.equal(fi, gi)
+    ref = _ref_logits(model, img[:8])
+    assert ((fl[:8].cpu() - ref).norm() / ref.norm()).item() < 0.15
+    prof = dict(eng._e.profile(x.data_ptr(), 32, 224, 224, 0))
+    rprof = dict(ref_eng._e.profile(x.data_ptr(), 32, 224, 224, 0))
+    for blk in ("layer1.1", "layer1.2"):
+        assert prof[blk + ".conv3"] < 0.3 * rprof[blk + ".conv3"], (blk, prof, rprof)
 
 
 def test_unknown_engine_option_is_an_error(gpu):

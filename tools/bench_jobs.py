@@ -165,7 +165,9 @@ def main():
             time.sleep(1.0)
             try:
                 out = client.cmd("jobs", 30)
-            except Exception:  # noqa: BLE001  (leader switch)
+            except Exception as e:  # noqa: BLE001  (leader switch)
+                print(f"# {time.time() - t_predict:.0f}s: jobs command failed: {str(e)[-3000:]}", file=sys.stderr,
+                      flush=True)
                 continue
             import re
             counts = [int(x) for x in re.findall(r"Accuracy: \d+/(\d+)", out)]

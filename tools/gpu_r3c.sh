@@ -1,5 +1,5 @@
 #!/bin/bash
-# AlexNet hipBLASLt classifier A/B on one box + shard-job benchmark (progress printed every 10 s)
+# Fused ResNet50 bottleneck check + bench A/B, AlexNet hipBLASLt classifier A/B, shard-job benchmark
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -12,6 +12,12 @@ step() {
   tail -3 "gpurun_out/$name.log"
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
 }
+step bn_tests 300 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_engine_gpu.py -k "resnet50"
+grep -q "failed" gpurun_out/bn_tests.log && { echo "bottleneck tests failed: stopping"; exit 1; }
+R="python bench.py --model resnet50_fp8 --latency-queries 0 --e2e-queries 0 --latency-steps 10 --steps 100"
+step r50_fused 200 $R
+step r50_unfused 200 $R --engine-opt fused_bottleneck=0
+step r50_ops 200 $R --steps 5 --warmup 2 --prime-steps 5 --profile-ops
 B="python bench.py --model alexnet --latency-queries 0 --e2e-queries 0 --latency-steps 10"
 step alex_blaslt_a 200 $B
 step alex_igemm_a 200 $B --engine-opt blaslt_fc=0
