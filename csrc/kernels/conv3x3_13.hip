@@ -12,13 +12,14 @@
 //    16-B chunks XOR-swizzled per pixel (the conv3x3_stream.hip scheme: every
 //    16-lane group of a fragment read hits 16 distinct bank slots); pixels are
 //    padded to a multiple of 256 B; taps outside the image read one zero pixel;
-//  * a wave owns 32 output channels (2 N fragments, perm32 row order: a lane
-//    ends with 8 consecutive channels of one pixel) for all 11 pixel
-//    fragments, so each weight fragment feeds 11 MFMAs and each X fragment 2;
-//    the weights stream from L2 in fragment order (stream_frag_index) through
-//    a PD-deep register ring, no LDS stage and no barrier in the K loop;
-//  * Cout / 32 channel groups over 8 waves: 8 groups (Cout 256) one per wave;
-//    12 (Cout 384): waves 0-3 take two, so every SIMD (waves w, w + 4) runs 3.
+//  * 4 waves, one per SIMD with up to 512 registers each: a wave owns Cout/4
+//    output channels (2 N fragments per 32-channel group, perm32 row order: a
+//    lane ends with 8 consecutive channels of one pixel) for all 11 pixel
+//    fragments, so each weight fragment feeds 11 MFMAs and each X fragment
+//    4-6; the weights stream from L2 in fragment order (stream_frag_index)
+//    through a PD-deep register ring, no LDS stage and no barrier in the K
+//    loop. (8 waves of 256 registers
+//    spilled the ring: the compiler double-buffers the X fragments.)
 #include "common.h"
 #include "kernels.h"
 
@@ -30,7 +31,6 @@ template <int N>
 __device__ __forceinline__ void vm_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
 }
-
 struct D13Args {
   const bf16* x;      // [B, 13, 13, CI]
   const bf16* wf;     // [CO/32][KT][2][64][8] fragment order (stream_frag_index, K = 9 CI)
@@ -56,15 +56,17 @@ struct D13Geom {
   static constexpr size_t LDS = (size_t)ZB + PXB;
 };
 
-template <int CI, int CO, int PD>
-__global__ __launch_bounds__(512, 1) void conv3x3_13_kernel(D13Args a) {
+template <int CI, int CO, int PD, int GPP>
+__global__ __launch_bounds__(256, 1) void conv3x3_13_kernel(D13Args a) {
   using G = D13Geom<CI>;
   constexpr int CPX = G::CPX, PXC = G::PXC, PXB = G::PXB, ZB = G::ZB;
   constexpr int CT = CI / 32;       // K steps per tap
   constexpr int KT = 9 * CT;        // K steps
-  constexpr int NGRP = CO / 32;     // channel groups (tasks)
+  constexpr int NGW = CO / 32 / 4;  // 32-channel groups per wave (4 waves, one per SIMD)
+  constexpr int NF = 2 * GPP;       // N fragments per pass (GPP groups: the accumulators of one pass)
+  static_assert(NGW % GPP == 0, "passes");
   static_assert(CT % PD == 0, "the weight ring's slot must be a compile-time function of the K step in a tap");
-  static_assert(NGRP == 8 || NGRP == 12, "channel groups: one per wave, or 3 per SIMD");
+  static_assert(CO % 128 == 0, "channel groups over 4 waves");
   extern __shared__ __attribute__((aligned(16))) uint4 smem[];
   char* xs = (char*)smem;
 
@@ -78,7 +80,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_13_kernel(D13Args a) {
   // pc ^ swz(K) of pixel K (slots whose logical chunk is past CPX: padding,
   // loaded from the zero page); one LDS-DMA instruction = 64 slots
   constexpr int NSLOT = kNPix * PXC;
-  for (int i = wave; i * 64 < NSLOT; i += 8) {
+  for (int i = wave; i * 64 < NSLOT; i += 4) {
     const int ps = i * 64 + lane;
     if (ps < NSLOT) {
       const int K = ps / PXC, pc = ps - K * PXC;
@@ -86,26 +88,23 @@ __global__ __launch_bounds__(512, 1) void conv3x3_13_kernel(D13Args a) {
       dma16(lc < CPX ? (const void*)(img + (long)K * CI + lc * 8) : (const void*)a.zero, xs + i * 1024);
     }
   }
-  if (tid < PXB / 16) ((uint4*)(xs + ZB))[tid] = make_uint4(0, 0, 0, 0);
+  for (int i = tid; i < PXB / 16; i += 256) ((uint4*)(xs + ZB))[i] = make_uint4(0, 0, 0, 0);
 
-  // ---- per-lane pixel constants: p = 16 f + fr (clamped for the padding lanes
-  // of the last fragment: they compute a duplicate, never stored); xoff = the
-  // staged offset of the pixel, low 4 bits = first/last row/column flags
-  int xoff[kMF];
-#pragma unroll
-  for (int f = 0; f < kMF; ++f) {
-    const int p = min(16 * f + fr, kNPix - 1);
-    const int r = p / kW, c = p - r * kW;
-    xoff[f] = p * PXB | (r == 0 ? 1 : 0) | (r == kH - 1 ? 2 : 0) | (c == 0 ? 4 : 0) | (c == kW - 1 ? 8 : 0);
-    asm volatile("" : "+v"(xoff[f]));  // keep it live (no rematerialised divides in the loop)
-  }
+  // ---- per-lane pixel geometry, recomputed per tap (held across the K loop
+  // it cost 11 VGPRs the loop needs): p = 16 f + fr (clamped for the padding
+  // lanes of the last fragment: they compute a duplicate, never stored)
   int xa[kMF], tsw = 0;
   auto set_tap = [&](int tap) __attribute__((always_inline)) {
     const int kh = tap / 3, kw = tap - kh * 3;
-    const int tm = (kh == 0 ? 1 : 0) | (kh == 2 ? 2 : 0) | (kw == 0 ? 4 : 0) | (kw == 2 ? 8 : 0);
     const int ktap = (kh - 1) * kW + kw - 1;
 #pragma unroll
-    for (int f = 0; f < kMF; ++f) xa[f] = (xoff[f] & tm) ? ZB : (xoff[f] & ~15) + ktap * PXB;
+    for (int f = 0; f < kMF; ++f) {
+      const int p = min(16 * f + fr, kNPix - 1);
+      const int r = (p * 79) >> 10, c = p - r * kW;  // p / 13 for p < 169
+      const bool out = (kh == 0 && r == 0) || (kh == 2 && r == kH - 1) || (kw == 0 && c == 0) ||
+                       (kw == 2 && c == kW - 1);
+      xa[f] = out ? ZB : (p + ktap) * PXB;
+    }
     // K = p + ktap with p & 15 == fr for every real pixel: one swizzle per tap
     tsw = (g << 4) ^ (swz13(fr + ktap) << 4);
   };
@@ -118,19 +117,31 @@ __global__ __launch_bounds__(512, 1) void conv3x3_13_kernel(D13Args a) {
   __builtin_amdgcn_s_barrier();
 
 #pragma nounroll
-  for (int grp = wave; grp < NGRP; grp += 8) {
-    const __amdgpu_buffer_rsrc_t wrs = wave_rsrc(a.wf + (long)grp * KT * 2 * 512, KT * 2 * 1024);
-    auto wfrag = [&](int t, int nf) __attribute__((always_inline)) {
-      return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, lane * 16, (t * 2 + nf) * 1024, 0));
+  for (int pass = 0; pass < NGW / GPP; ++pass) {
+    const int grp0 = wave * NGW + pass * GPP;  // first 32-channel group of this pass
+    // this pass's groups grp0 .. grp0 + GPP - 1 are consecutive in the
+    // fragment-order array: fragment nf (group nf / 2) of K step t at
+    // base + ((nf / 2) KT + t) 2 KB + (nf % 2) KB, lane l's 16 B at 16 l;
+    // steps past the end re-load step 0 (uniform load counts for the waits)
+    // (compiler-visible buffer loads: untracked asm loads into a register
+    // ring raced the register allocator at 254 VGPRs -- an in-flight load
+    // landed in a reused register and faulted a later address)
+    const __amdgpu_buffer_rsrc_t wrs = wave_rsrc(a.wf + (long)grp0 * KT * 2 * 512, GPP * KT * 2 * 1024);
+    auto wfetch = [&](int t, bf16x8* dst) __attribute__((always_inline)) {
+      const int tt = t < KT ? t : 0;
+#pragma unroll
+      for (int nf = 0; nf < NF; ++nf)
+        dst[nf] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
+                                                 wrs, lane * 16, (nf >> 1) * KT * 2048 + tt * 2048 + (nf & 1) * 1024, 0));
     };
-    bf16x8 wq[PD][2];
+    bf16x8 wq[PD][NF];
 #pragma unroll
-    for (int t = 0; t < PD - 1; ++t)
+    for (int t = 0; t < PD - 1; ++t) wfetch(t, wq[t]);
+    floatx4 acc[kMF][NF];
 #pragma unroll
-      for (int nf = 0; nf < 2; ++nf) wq[t][nf] = wfrag(t, nf);
-    floatx4 acc[kMF][2];
+    for (int f = 0; f < kMF; ++f)
 #pragma unroll
-    for (int f = 0; f < kMF; ++f) acc[f][0] = acc[f][1] = floatx4{0.f, 0.f, 0.f, 0.f};
+      for (int nf = 0; nf < NF; ++nf) acc[f][nf] = floatx4{0.f, 0.f, 0.f, 0.f};
     set_tap(0);
     bf16x8 xf[kMF];
 #pragma unroll
@@ -140,49 +151,58 @@ __global__ __launch_bounds__(512, 1) void conv3x3_13_kernel(D13Args a) {
 #pragma unroll
       for (int cc = 0; cc < CT; ++cc) {
         const int t = tap * CT + cc;
-        if (t + PD - 1 < KT)
-#pragma unroll
-          for (int nf = 0; nf < 2; ++nf) wq[(cc + PD - 1) % PD][nf] = wfrag(t + PD - 1, nf);
+        wfetch(t + PD - 1, wq[(cc + PD - 1) % PD]);
         // next K step's X: same tap at cc + 1, or the next tap's first (the
         // final step re-reads a valid tile, unused)
         if (cc + 1 == CT && tap + 1 < 9) set_tap(tap + 1);
         const int cn = cc + 1 == CT ? 0 : cc + 1;
+        // the X fragments (read during the previous step) landed: one wait
+        // instead of the compiler's one per fragment
+        __builtin_amdgcn_s_waitcnt(0xC07F);
 #pragma unroll
         for (int f = 0; f < kMF; ++f) {
 #pragma unroll
-          for (int nf = 0; nf < 2; ++nf)
+          for (int nf = 0; nf < NF; ++nf)
             acc[f][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wq[cc % PD][nf], xf[f], acc[f][nf], 0, 0, 0);
           xf[f] = xread(f, cn);
+        }
+#pragma unroll
+        for (int f = 0; f < kMF; ++f) {
+          __builtin_amdgcn_sched_group_barrier(0x008, NF, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
         }
       }
     }
     // ---- epilogue: lane holds channels 32 grp + 8 g .. +7 of pixel 16 f + fr
-    const int ch = 32 * grp + 8 * g;
-    float bs[8];
-    {
-      const float4 lo = *(const float4*)(a.bias + ch), hi = *(const float4*)(a.bias + ch + 4);
-      bs[0] = lo.x, bs[1] = lo.y, bs[2] = lo.z, bs[3] = lo.w, bs[4] = hi.x, bs[5] = hi.y, bs[6] = hi.z, bs[7] = hi.w;
-    }
     bf16* yim = a.y + (long)b * kNPix * CO;
 #pragma unroll
-    for (int f = 0; f < kMF; ++f) {
-      const int p = 16 * f + fr;
-      if (p < kNPix) {
-        float v[8];
+    for (int j = 0; j < GPP; ++j) {
+      const int ch = 32 * (grp0 + j) + 8 * g;
+      float bs[8];
+      {
+        const float4 lo = *(const float4*)(a.bias + ch), hi = *(const float4*)(a.bias + ch + 4);
+        bs[0] = lo.x, bs[1] = lo.y, bs[2] = lo.z, bs[3] = lo.w, bs[4] = hi.x, bs[5] = hi.y, bs[6] = hi.z, bs[7] = hi.w;
+      }
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          v[e] = acc[f][e >> 2][e & 3] + bs[e];
-          if (a.relu) v[e] = fmaxf(v[e], 0.f);
+      for (int f = 0; f < kMF; ++f) {
+        const int p = 16 * f + fr;
+        if (p < kNPix) {
+          float v[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            v[e] = acc[f][2 * j + (e >> 2)][e & 3] + bs[e];
+            if (a.relu) v[e] = fmaxf(v[e], 0.f);
+          }
+          *(uint4*)(yim + (long)p * CO + ch) = pack8(v);
         }
-        *(uint4*)(yim + (long)p * CO + ch) = pack8(v);
       }
     }
   }
 }
 
-template <int CI, int CO, int PD>
+template <int CI, int CO, int PD, int GPP>
 void launch13(const D13Args& a, int B, hipStream_t s) {
-  hipLaunchKernelGGL((conv3x3_13_kernel<CI, CO, PD>), dim3(B), dim3(512), D13Geom<CI>::LDS, s, a);
+  hipLaunchKernelGGL((conv3x3_13_kernel<CI, CO, PD, GPP>), dim3(B), dim3(256), D13Geom<CI>::LDS, s, a);
 }
 
 }  // namespace
@@ -205,9 +225,10 @@ void conv3x3_13(const void* x, const void* wf, const float* bias, void* y, const
   a.y = (bf16*)y;
   a.zero = (const bf16*)zero;
   a.relu = relu ? 1 : 0;
-  if (Cin == 192) launch13<192, 384, 3>(a, B, s);
-  else if (Cin == 384) launch13<384, 256, 4>(a, B, s);
-  else launch13<256, 256, 4>(a, B, s);
+  // (ring depth / groups per pass: the largest without spills)
+  if (Cin == 192) launch13<192, 384, 3, 1>(a, B, s);
+  else if (Cin == 384) launch13<384, 256, 3, 2>(a, B, s);
+  else launch13<256, 256, 2, 2>(a, B, s);
   DMLC_HIP_CHECK(hipGetLastError());
 }
 

@@ -431,7 +431,8 @@ void Engine::pack_weights(const WeightMap& w) {
               (L.kh == 3 && L.stride == 1 && L.pad == 1 &&
                conv3x3_rows28_supported(shapes_[L.in_act].H, shapes_[L.in_act].W, shapes_[L.in_act].C, L.cout))) ||
          (L.kh == 3 && L.kw == 3 && L.stride == 1 && L.pad == 1 &&
-          conv3x3_rows_supported(shapes_[L.in_act].H, shapes_[L.in_act].W, shapes_[L.in_act].C, L.cout)))) {
+          (conv3x3_rows_supported(shapes_[L.in_act].H, shapes_[L.in_act].W, shapes_[L.in_act].C, L.cout) ||
+           conv3x3_13_supported(shapes_[L.in_act].H, shapes_[L.in_act].W, shapes_[L.in_act].C, L.cout))))) {
       L.wf_off = off;  // fragment-order copy for the register-weight stream conv
       off = align_up(off + (size_t)L.cout * L.kpad * 2, 256);
     }
