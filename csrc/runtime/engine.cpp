@@ -83,6 +83,7 @@ bool EngineOptions::set(const std::string& name, bool v) {
       {"bigtile", &EngineOptions::bigtile},         {"fused_pool", &EngineOptions::fused_pool},
       {"fused_head", &EngineOptions::fused_head},   {"fc_small", &EngineOptions::fc_small},
       {"blaslt_fc", &EngineOptions::blaslt_fc},     {"direct13", &EngineOptions::direct13},
+      {"direct27", &EngineOptions::direct27},
       {"fork_ds", &EngineOptions::fork_ds},         {"fp8_3x3", &EngineOptions::fp8_3x3},
       {"conv1x1", &EngineOptions::conv1x1},         {"s2rows", &EngineOptions::s2rows},
       {"rows28", &EngineOptions::rows28},
@@ -436,6 +437,11 @@ void Engine::pack_weights(const WeightMap& w) {
       L.wf_off = off;  // fragment-order copy for the register-weight stream conv
       off = align_up(off + (size_t)L.cout * L.kpad * 2, 256);
     }
+    if (!L.fp8 && !L.fc && L.in_act >= 0 && L.kh == 5 && L.kw == 5 && L.stride == 1 &&
+        conv5x5_27_supported(shapes_[L.in_act].H, shapes_[L.in_act].W, shapes_[L.in_act].C, L.cout, L.pad)) {
+      L.wf_off = off;  // fragment-order copy for conv5x5_27.hip
+      off = align_up(off + (size_t)L.cout * L.kpad * 2, 256);
+    }
     if (bottleneck_conv3(L)) {  // fragment-order copy for bottleneck56.hip's expand conv
       L.wf_off = off;
       off = align_up(off + (size_t)L.cout * L.kpad * 2, 256);
@@ -658,6 +664,9 @@ Engine::ConvPath Engine::conv_path(const Op& op, int B) const {
     return ConvPath::Rows28;
   if (opt_.direct13 && k3 && L.stride == 1 && L.wf_off && conv3x3_13_supported(is.H, is.W, is.C, L.cout))
     return ConvPath::Direct13;
+  if (opt_.direct27 && !L.fc && !L.fp8 && L.kh == 5 && L.kw == 5 && L.stride == 1 && L.relu && L.wf_off &&
+      L.kpad == 1600 && !shapes_[op.out].f32 && conv5x5_27_supported(is.H, is.W, is.C, L.cout, L.pad))
+    return ConvPath::Direct27;
   if (opt_.stream_conv && k3 && !l4s2 && !l1 && 8 * B >= num_cus_ &&
       conv3x3_stream_supported(is.H, is.W, is.C, L.cout, L.stride))
     return ConvPath::Stream;
@@ -956,6 +965,10 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
             conv3x3_13(acts_[op.in], (const uint8_t*)warena_ + L.wf_off,
                        (const float*)((const uint8_t*)warena_ + L.b_off), acts_[op.out], zero_, B, is.C, L.cout,
                        L.relu, cs);
+            break;
+          case ConvPath::Direct27:
+            conv5x5_27(acts_[op.in], (const uint8_t*)warena_ + L.wf_off,
+                       (const float*)((const uint8_t*)warena_ + L.b_off), acts_[op.out], zero_, B, cs);
             break;
           case ConvPath::Rows28:
             conv3x3_rows28(acts_[op.in], (const uint8_t*)warena_ + L.wf_off,

@@ -84,6 +84,7 @@ struct EngineOptions {
   bool fused_pool = true;        // the last conv's epilogue computes the global average pool
   bool fused_head = true;        // avgpool + fc + softmax / top-1 in one kernel (head.hip)
   bool direct13 = true;          // AlexNet's 13x13 3x3 convs with the image resident in LDS (conv3x3_13.hip)
+  bool direct27 = true;          // AlexNet's 5x5 conv on 27x27x64 the same way (conv5x5_27.hip)
   bool fc_small = true;          // weight-streaming GEMV for fc layers at B <= 16 (fc_small.hip)
   // bf16 fc layers above that on hipBLASLt (blaslt.h): faster alone, slower in the two-lane bench
   // (472-485k vs 518-528k img/s AlexNet, profiles/r3_alexnet_blaslt_ab.txt), so off by default
@@ -166,7 +167,7 @@ class Engine {
   void run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* idx, float* prob,
                float* logits, hipStream_t s, std::vector<hipEvent_t>* evs, bool trace);
   ConvArgs conv_args(const Op& op, int B, float* logits) const;
-  enum class ConvPath { Stream, Rows, Rows28, Direct13, OneByOne, BigTile, Igemm };
+  enum class ConvPath { Stream, Rows, Rows28, Direct13, Direct27, OneByOne, BigTile, Igemm };
   ConvPath conv_path(const Op& op, int B) const;
   bool side_safe(int B) const;
   bool head_fusable(size_t oi) const;

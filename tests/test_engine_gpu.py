@@ -362,8 +362,9 @@ def test_alexnet_blaslt_fc_matches_reference(gpu, B):
 
 @pytest.mark.parametrize("B", [5, 256])
 def test_alexnet_direct13_matches_igemm(gpu, B):
-    """AlexNet's 13x13 convs (features.6/.8/.10) on the LDS-resident direct
-    conv (conv3x3_13.hip) vs the implicit GEMM (direct13 off): both bf16 MFMA
+    """AlexNet's 13x13 convs (features.6/.8/.10) and its 5x5 conv (features.3)
+    on the LDS-resident direct convs (conv3x3_13.hip, conv5x5_27.hip) vs the
+    implicit GEMM (direct13 / direct27 off): both bf16 MFMA
     with fp32 accumulation, different K order, so logits agree to bf16
     rounding; and vs fp32 torch.nn on a few images. The direct kernel is the
     one that ran: features.8 takes well under the implicit GEMM's time."""
@@ -373,7 +374,7 @@ def test_alexnet_direct13_matches_igemm(gpu, B):
     img = torch.randint(0, 256, (B, 224, 224, 3), generator=g, dtype=torch.uint8)
     x = img.to(gpu)
     eng = InferenceEngine("alexnet", sd, max_batch=B)
-    ref_eng = InferenceEngine("alexnet", sd, max_batch=B, options={"direct13": False})
+    ref_eng = InferenceEngine("alexnet", sd, max_batch=B, options={"direct13": False, "direct27": False})
     fi, _, fl = eng.predict(x, return_logits=True)
     ri, _, rl = ref_eng.predict(x, return_logits=True)
     torch.cuda.synchronize()
@@ -389,8 +390,10 @@ def test_alexnet_direct13_matches_igemm(gpu, B):
     if B == 256:
         prof = dict(eng._e.profile(x.data_ptr(), B, 224, 224, 0))
         rprof = dict(ref_eng._e.profile(x.data_ptr(), B, 224, 224, 0))
-        print("direct13 vs igemm (ms):", {k: (prof[k], rprof[k]) for k in ("features.6", "features.8", "features.10")})
+        print("direct vs igemm (ms):",
+              {k: (prof[k], rprof[k]) for k in ("features.3", "features.6", "features.8", "features.10")})
         assert prof["features.8"] < rprof["features.8"], (prof, rprof)
+        assert prof["features.3"] < rprof["features.3"], (prof, rprof)
 
 
 def test_resnet50_fp8_fused_bottleneck_matches_unfused(gpu):

@@ -1,0 +1,24 @@
+#!/bin/bash
+# AlexNet direct 5x5 conv check + bench; ResNet18 lanes sweep
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+step() {
+  local name=$1 to=$2; shift 2
+  echo "== $name" | tee -a gpurun_out/steps.log
+  timeout -k 10 "$to" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "   rc=$rc" | tee -a gpurun_out/steps.log
+  tail -3 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+}
+step d27_tests 300 python -u -m pytest -x -v -s --timeout 200 --timeout-method thread tests/test_engine_gpu.py -k "alexnet"
+grep -q " failed" gpurun_out/d27_tests.log && { echo "alexnet tests failed: stopping"; exit 1; }
+B="python bench.py --model alexnet --latency-queries 0 --e2e-queries 0 --latency-steps 10"
+step alex_d27 200 $B
+step alex_d27_ops 200 $B --steps 5 --warmup 2 --prime-steps 5 --profile-ops
+step alex_nod27 200 $B --engine-opt direct27=0
+R="python bench.py --latency-queries 0 --e2e-queries 0 --latency-steps 10"
+step r18_l2 200 $R
+step r18_l3 200 $R --lanes 3
+step r18_l4 200 $R --lanes 4
