@@ -18,10 +18,12 @@
 //    MFMA k-steps of 32, and every B operand is one aligned ds_read_b128 from
 //    the staged row (no im2col). Weights are zero on the pad slots (e = 6, 7,
 //    kw = 11, kh = 11).
-//  * Rows stream through LDS: the raw u8 rows of conv row oh+4 arrive by
-//    LDS-DMA during conv row oh, and are converted into the paired ring during
-//    conv row oh+1 for conv row oh+3 (beside the MFMAs of the SIMD's other
-//    wave), so each conv row costs one barrier.
+//  * Rows stream through LDS: the raw u8 rows of conv row oh+5 go out by
+//    LDS-DMA during conv row oh and are converted into the paired ring during
+//    conv row oh+2 (for conv row oh+5, beside the MFMAs of the SIMD's other
+//    wave), so each conv row costs one barrier and the DMA has two conv rows
+//    to land (with one row of slack the per-row vmcnt(0) exposed the HBM
+//    latency: 85-88 us at B=256).
 //  * 8 waves: wave w = pixel fragment w & 3 (16 output columns) x output
 //    channels 32 (w >> 2) .. +31 (two n-blocks), D = W x X with the weight
 //    rows permuted (perm32) so a lane ends with 8 consecutive channels of one
@@ -49,7 +51,7 @@ constexpr int kRing = 32;       // paired rows (power of two): 11 in use + 8 con
 constexpr int kKS = 17;         // K steps of 32 (68 chunks, 66 used)
 constexpr int kU8B = kS * 3;    // 672 bytes per raw image row
 constexpr int kU8Slot = 704;    // raw ring slot (16-B aligned)
-constexpr int kU8Ring = 8;
+constexpr int kU8Ring = 16;     // raw rows: 4 converting + 8 in flight (DMA two conv rows ahead)
 constexpr int kConvB = kHo * 128;  // one conv row [55][64] bf16
 constexpr int kConvRing = 4;
 constexpr size_t kLds = (size_t)kRing * kRowB + (size_t)kConvRing * kConvB + (size_t)kU8Ring * kU8Slot;
@@ -106,6 +108,8 @@ __global__ __launch_bounds__(512, 1) void alex_stem_kernel(AlexStemArgs a) {
     if (iy < 0 || iy >= kS) return;
     if (lane < kU8B / 16) dma16(img + (long)iy * kU8B + lane * 16, raw + (pr % kU8Ring) * kU8Slot);
   };
+  // (wave-uniform) does dma_row(pr) issue a load
+  auto dma_issues = [](int pr) { return pr - 2 >= 0 && pr - 2 < kS; };
 
   // weights: wave's channel group 32 (w >> 2), n-blocks nf = 0, 1 (rows permuted)
   const int ch0 = 32 * (wave >> 2);
@@ -135,40 +139,47 @@ __global__ __launch_bounds__(512, 1) void alex_stem_kernel(AlexStemArgs a) {
 
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __syncthreads();
-  // prologue: padded rows 0..18 (conv rows 0, 1, 2) straight from global;
-  // raw rows 19..22 (conv row 3) by DMA
-  for (int it = tid; it < 19 * kChunks; it += 512) {
+  // prologue: padded rows 0..22 (conv rows 0..3) straight from global; raw
+  // rows 23..26 and 27..30 (conv rows 4, 5) by DMA, converted at iterations
+  // 0 and 1
+  for (int it = tid; it < 23 * kChunks; it += 512) {
     const int pr = it / kChunks, p = it - pr * kChunks;
     const int iy = pr - 2;
     convert_chunk(pr, p, img + (long)(iy < 0 ? 0 : iy >= kS ? kS - 1 : iy) * kU8B);
   }
-  if (wave < 4) dma_row(19 + wave);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (wave < 4) {
+    dma_row(23 + wave);
+    dma_row(27 + wave);
+    asm volatile("s_waitcnt vmcnt(1)" ::: "memory");  // conv row 4's rows; conv row 5's may stay in flight
+  }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __syncthreads();
 
   for (int oh = 0; oh <= kHo; ++oh) {
     if (oh < kHo) {
-      // rows of conv row oh+4 go out now (the raw ring slot they fill was
-      // converted at the previous iteration, before its barrier)
-      if (wave < 4 && oh + 4 < kHo) dma_row(4 * oh + 23 + wave);
-      // convert conv row oh+3's new rows (padded 4oh+19 .. 4oh+22; raw rows
+      // rows of conv row oh+6 go out now (padded 4oh+31 .. 4oh+34; the raw
+      // ring slots they fill were converted two iterations ago, before a
+      // barrier)
+      if (wave < 4 && oh + 6 < kHo) dma_row(4 * oh + 31 + wave);
+      // convert conv row oh+4's new rows (padded 4oh+23 .. 4oh+26; raw rows
       // landed before the last barrier); disjoint from the rows read below
-      if (oh + 3 < kHo && tid < 4 * kChunks) {
-        const int pr = 4 * oh + 19 + tid / kChunks, p = tid - (tid / kChunks) * kChunks;
+      if (oh + 4 < kHo && tid < 4 * kChunks) {
+        const int pr = 4 * oh + 23 + tid / kChunks, p = tid - (tid / kChunks) * kChunks;
         convert_chunk(pr, p, (const uint8_t*)raw + (pr % kU8Ring) * kU8Slot);
       }
       // ---- conv row oh: 17 k-steps x 2 n-blocks
       floatx4 acc[2] = {floatx4{0.f, 0.f, 0.f, 0.f}, floatx4{0.f, 0.f, 0.f, 0.f}};
       const int pr0 = 4 * oh;
-      bf16x8 xb = *(const bf16x8*)(ring + ((pr0 + kh_of[0]) & (kRing - 1)) * kRowB + col_of[0]);
+      // all 17 B operands issued up front (one read fed only 2 MFMAs: read
+      // one step ahead, its LDS latency was exposed every step)
+      bf16x8 xb[kKS];
+#pragma unroll
+      for (int ks = 0; ks < kKS; ++ks)
+        xb[ks] = *(const bf16x8*)(ring + ((pr0 + kh_of[ks]) & (kRing - 1)) * kRowB + col_of[ks]);
 #pragma unroll
       for (int ks = 0; ks < kKS; ++ks) {
-        bf16x8 xn;
-        if (ks + 1 < kKS) xn = *(const bf16x8*)(ring + ((pr0 + kh_of[ks + 1]) & (kRing - 1)) * kRowB + col_of[ks + 1]);
-        acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[ks][0], xb, acc[0], 0, 0, 0);
-        acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[ks][1], xb, acc[1], 0, 0, 0);
-        if (ks + 1 < kKS) xb = xn;
+        acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[ks][0], xb[ks], acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[ks][1], xb[ks], acc[1], 0, 0, 0);
       }
       // lane: channels ch0 + 8 fq .. +7 of pixel ow (nf 0: +0..3, nf 1: +4..7)
       if (ow < kHo) {
@@ -198,10 +209,13 @@ __global__ __launch_bounds__(512, 1) void alex_stem_kernel(AlexStemArgs a) {
         *(ushort8*)(a.y + (((long)b * kPH + ph) * kPH + pw) * kC + cg * 8) = m;
       }
     }
-    // this iteration's DMA (conv row oh+4's raw rows, issued before the
-    // MFMAs) has had the whole MFMA phase to land; the next iteration
-    // converts it, so it must be in LDS before the barrier
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // the next iteration converts conv row oh+5's raw rows (issued one
+    // iteration ago, or in the prologue): they must be in LDS before the
+    // barrier; this iteration's DMA (conv row oh+6) may stay in flight
+    if (wave < 4 && oh + 6 < kHo && dma_issues(4 * oh + 31 + wave))
+      asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __syncthreads();
   }

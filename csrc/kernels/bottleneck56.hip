@@ -49,7 +49,7 @@ struct BnArgs {
   float res_scale;     // s_x
   float out_inv_scale; // 1 / s_y
   int dbg;             // experiments (tools/bottleneck_bench.py): bit 0 no y stores (kept live), bit 1 no
-                       // residual loads, bit 2 no conv1 X loads, bit 3 no conv2 K loop
+                       // residual loads, bit 2 no conv1 X loads
 };
 
 constexpr int kH = 56, kW = 56, kC = 256, kM = 64;
@@ -222,10 +222,8 @@ __device__ __forceinline__ void bn_wave(const BnArgs& a, char* ring, char* t2, i
         }
       };
       load_k(0, xc);
-      const int nks = (a.dbg & 8) ? 1 : kKS2;
 #pragma unroll
       for (int ks = 0; ks < kKS2; ++ks) {
-        if (ks >= nks) break;
         if (ks + 1 < kKS2) load_k(ks + 1, xn);
         {  // K step ks + PD - 1, wrapping into the next step's first ones
           const int kl = (ks + kPD - 1) % kKS2;

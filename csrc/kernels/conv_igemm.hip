@@ -626,6 +626,11 @@ int conv_pick_split_k(const ConvArgs& a, int num_cus) {
   const int k_tiles = a.Kpad / 64;
   if (a.in_fp8 || a.out_fp8 || tiles >= num_cus / 2 || k_tiles < 16) return 1;
   int s = (int)((num_cus + tiles - 1) / tiles);
+  // fc layers at throughput batches (AlexNet classifier, M = B <= 256: 64 / 16
+  // tiles): 8 K slices (two rounds of workgroups) beat the one-round pick --
+  // classifier.1 55 -> 47 us, classifier.6 28 -> 23 us at B=256; 16 is slower
+  // again (profiles/r3_alexnet_fc_splitk.txt)
+  if (a.H == 1 && a.W == 1 && a.KH == 1 && a.KW == 1 && a.Kpad >= 4096) s = std::max(s, 8);
   s = std::min(s, k_tiles / 8);
   s = std::min(s, 16);
   return std::max(s, 1);

@@ -71,7 +71,9 @@ struct EngineOptions {
   bool row_conv = true;          // direct row-streaming 3x3 convs (conv3x3_rows.hip) for 56x56x64
   bool rows_wreg = true;         // ... with register-streamed weights, 2 workgroups per CU
   bool fused_block = true;       // a 56x56x64 basic block as one kernel (conv3x3_block.hip), B >= 0.7 x CUs
-  bool fused_bottleneck = true;  // resnet50_fp8 layer1 identity bottlenecks as one kernel (bottleneck56.hip)
+  // resnet50_fp8 layer1 identity bottlenecks as one kernel (bottleneck56.hip): at parity with
+  // the three-kernel path so far (248 vs 245 us per block), off by default
+  bool fused_bottleneck = false;
   bool stream_conv = true;       // direct 3x3 convs with the input resident in LDS (conv3x3_stream.hip)
   bool stream_wreg = true;       // ... with register-streamed weights where available
   bool stream_l4s2 = true;       // ... also for 14x14x256 -> 512 / s2 (register weights only)

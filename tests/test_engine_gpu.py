@@ -409,7 +409,7 @@ def test_resnet50_fp8_fused_bottleneck_matches_unfused(gpu):
     g = torch.Generator().manual_seed(62)
     img = torch.randint(0, 256, (32, 224, 224, 3), generator=g, dtype=torch.uint8)
     x = img.to(gpu)
-    eng = InferenceEngine("resnet50_fp8", sd, max_batch=32)
+    eng = InferenceEngine("resnet50_fp8", sd, max_batch=32, options={"fused_bottleneck": True})
     ref_eng = InferenceEngine("resnet50_fp8", sd, max_batch=32, options={"fused_bottleneck": False})
     fi, fp, fl = eng.predict(x, return_logits=True, use_graph=False)
     gi, gp = eng.predict(x)

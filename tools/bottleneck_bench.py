@@ -19,7 +19,7 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--iters", type=int, default=15)
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--dbg", default="0,1,2,4,8,3,15")
+    ap.add_argument("--dbg", default="0,1,2,4,3,7")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     B = args.batch

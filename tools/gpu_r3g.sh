@@ -1,0 +1,21 @@
+#!/bin/bash
+# AlexNet stem DMA pipeline + FC split-K: tests, bench, per-op
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+step() {
+  local name=$1 to=$2; shift 2
+  echo "== $name" | tee -a gpurun_out/steps.log
+  timeout -k 10 "$to" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "   rc=$rc" | tee -a gpurun_out/steps.log
+  tail -3 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+}
+step alex_tests 300 python -u -m pytest -x -v -s --timeout 200 --timeout-method thread tests/test_engine_gpu.py -k "alexnet"
+grep -q " failed" gpurun_out/alex_tests.log && { echo "alexnet tests failed: stopping"; exit 1; }
+B="python bench.py --model alexnet --latency-queries 0 --e2e-queries 0 --latency-steps 10"
+step alex_bench 200 $B
+step alex_ops 200 $B --steps 5 --warmup 2 --prime-steps 5 --profile-ops
+step alex_bench2 200 $B
+step prof_r18 300 rocprofv3 --kernel-trace -d gpurun_out/prof_r18 -o run -- python3 bench.py --steps 100 --warmup 5 --latency-queries 0 --e2e-queries 0 --latency-steps 3
