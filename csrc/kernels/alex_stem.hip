@@ -18,12 +18,11 @@
 //    MFMA k-steps of 32, and every B operand is one aligned ds_read_b128 from
 //    the staged row (no im2col). Weights are zero on the pad slots (e = 6, 7,
 //    kw = 11, kh = 11).
-//  * Rows stream through LDS: the raw u8 rows of conv row oh+5 go out by
-//    LDS-DMA during conv row oh and are converted into the paired ring during
-//    conv row oh+2 (for conv row oh+5, beside the MFMAs of the SIMD's other
-//    wave), so each conv row costs one barrier and the DMA has two conv rows
-//    to land (with one row of slack the per-row vmcnt(0) exposed the HBM
-//    latency: 85-88 us at B=256).
+//  * Two conv rows per iteration and one barrier (one row per barrier: 87 us
+//    at B=256, ~2,000 cycles of phase overhead per row beside ~1,100 of
+//    MFMA per SIMD). The raw u8 rows of conv rows r0+8, r0+9 go out by
+//    LDS-DMA during iteration r0 and are converted into the paired ring two
+//    iterations later (beside the MFMAs of the SIMD's other wave).
 //  * 8 waves: wave w = pixel fragment w & 3 (16 output columns) x output
 //    channels 32 (w >> 2) .. +31 (two n-blocks), D = W x X with the weight
 //    rows permuted (perm32) so a lane ends with 8 consecutive channels of one
@@ -47,13 +46,13 @@ constexpr int kPH = 27;         // pooled output size
 constexpr int kC = 64;          // output channels
 constexpr int kChunks = 114;    // paired chunks per padded row (228 padded pixels)
 constexpr int kRowB = 136 * 16; // staged paired row: chunks >= 114 stay zero (fragment padding reads up to 131)
-constexpr int kRing = 32;       // paired rows (power of two): 11 in use + 8 converted ahead
+constexpr int kRing = 32;       // paired rows (power of two): 15 in use + 16 converted ahead
 constexpr int kKS = 17;         // K steps of 32 (68 chunks, 66 used)
 constexpr int kU8B = kS * 3;    // 672 bytes per raw image row
 constexpr int kU8Slot = 704;    // raw ring slot (16-B aligned)
-constexpr int kU8Ring = 16;     // raw rows: 4 converting + 8 in flight (DMA two conv rows ahead)
+constexpr int kU8Ring = 32;     // raw rows: 8 converting + 16 in flight (DMA two iterations ahead)
 constexpr int kConvB = kHo * 128;  // one conv row [55][64] bf16
-constexpr int kConvRing = 4;
+constexpr int kConvRing = 8;    // conv rows: 3 pooled + 2 written per iteration
 constexpr size_t kLds = (size_t)kRing * kRowB + (size_t)kConvRing * kConvB + (size_t)kU8Ring * kU8Slot;
 
 struct AlexStemArgs {
@@ -86,18 +85,32 @@ __global__ __launch_bounds__(512, 1) void alex_stem_kernel(AlexStemArgs a) {
   // chunks must read as finite zeros (they meet zero weights)
   for (int o = tid * 16; o < kRing * kRowB; o += 512 * 16) *(uint4*)(ring + o) = make_uint4(0, 0, 0, 0);
 
-  // paired chunk p of padded row pr from 6 bytes of the raw row (image row
-  // pr - 2): the exact values preprocess_u8 would produce (imagenet_norm)
-  auto convert_chunk = [&](int pr, int p, const uint8_t* src_row) __attribute__((always_inline)) {
+  // paired chunk p of padded row pr from the raw ring (image row pr - 2,
+  // columns 2p-2, 2p-1 = bytes 6p-6 .. 6p-1): the exact values preprocess_u8
+  // would produce (imagenet_norm). Branch-free: two dword reads issued
+  // together (a byte read per value, each under its own branch and wait,
+  // was most of this kernel's time), the bytes picked by shifts, out-of-image
+  // values selected to zero.
+  auto convert_chunk = [&](int pr, int p) __attribute__((always_inline)) {
     const int iy = pr - 2;
+    const bool row_in = iy >= 0 && iy < kS;
+    const int pc = p < 1 ? 1 : p > kChunks - 2 ? kChunks - 2 : p;  // in-row address for the edge chunks
+    const int start = 6 * pc - 6;                                  // byte offset, even
+    const uint32_t* src = (const uint32_t*)(raw + (pr % kU8Ring) * kU8Slot + (start & ~3));
+    const uint32_t d0 = src[0], d1 = src[1], d2 = src[2];
+    // 64-bit window starting at the first wanted byte
+    const uint64_t w = (start & 2) ? ((uint64_t)d2 << 48 | (uint64_t)d1 << 16 | (d0 >> 16))
+                                   : ((uint64_t)d1 << 32 | d0);
     float v[8];
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const int ix = 2 * p - 2 + q;
-      const bool in = iy >= 0 && iy < kS && ix >= 0 && ix < kS;
-      const int ixc = ix < 0 ? 0 : ix >= kS ? kS - 1 : ix;  // never an out-of-row address
+      const bool in = row_in && ix >= 0 && ix < kS;
 #pragma unroll
-      for (int c = 0; c < 3; ++c) v[3 * q + c] = in ? imagenet_norm(c, (float)src_row[3 * ixc + c]) : 0.f;
+      for (int c = 0; c < 3; ++c) {
+        const float raw_v = (float)(uint32_t)((w >> (8 * (3 * q + c))) & 0xffu);
+        v[3 * q + c] = in ? imagenet_norm(c, raw_v) : 0.f;
+      }
     }
     v[6] = v[7] = 0.f;
     *(uint4*)(ring + (pr & (kRing - 1)) * kRowB + p * 16) = pack8(v);
@@ -139,80 +152,90 @@ __global__ __launch_bounds__(512, 1) void alex_stem_kernel(AlexStemArgs a) {
 
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __syncthreads();
-  // prologue: padded rows 0..22 (conv rows 0..3) straight from global; raw
-  // rows 23..26 and 27..30 (conv rows 4, 5) by DMA, converted at iterations
-  // 0 and 1
+  // prologue: raw rows of padded rows 0..22 (conv rows 0..3) by DMA into the
+  // raw ring, converted here; then the raw rows of conv rows 4, 5 (padded
+  // 23..30) and 6, 7 (31..38), one row per wave, converted at iterations 0
+  // and 1 (31..38 reuse the slots of rows 0..6, converted by then)
+  for (int pr = wave; pr < 23; pr += 8) dma_row(pr);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
   for (int it = tid; it < 23 * kChunks; it += 512) {
     const int pr = it / kChunks, p = it - pr * kChunks;
-    const int iy = pr - 2;
-    convert_chunk(pr, p, img + (long)(iy < 0 ? 0 : iy >= kS ? kS - 1 : iy) * kU8B);
-  }
-  if (wave < 4) {
-    dma_row(23 + wave);
-    dma_row(27 + wave);
-    asm volatile("s_waitcnt vmcnt(1)" ::: "memory");  // conv row 4's rows; conv row 5's may stay in flight
+    convert_chunk(pr, p);
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __syncthreads();
+  dma_row(23 + wave);
+  dma_row(31 + wave);
+  asm volatile("s_waitcnt vmcnt(1)" ::: "memory");  // conv rows 4, 5; 6, 7 may stay in flight
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();
 
-  for (int oh = 0; oh <= kHo; ++oh) {
-    if (oh < kHo) {
-      // rows of conv row oh+6 go out now (padded 4oh+31 .. 4oh+34; the raw
-      // ring slots they fill were converted two iterations ago, before a
-      // barrier)
-      if (wave < 4 && oh + 6 < kHo) dma_row(4 * oh + 31 + wave);
-      // convert conv row oh+4's new rows (padded 4oh+23 .. 4oh+26; raw rows
-      // landed before the last barrier); disjoint from the rows read below
-      if (oh + 4 < kHo && tid < 4 * kChunks) {
-        const int pr = 4 * oh + 23 + tid / kChunks, p = tid - (tid / kChunks) * kChunks;
-        convert_chunk(pr, p, (const uint8_t*)raw + (pr % kU8Ring) * kU8Slot);
+  // iteration i: conv rows r0 = 2i, r0 + 1; pooled row i - 2
+  for (int i = 0; i <= (kHo + 1) / 2; ++i) {
+    const int r0 = 2 * i;
+    // pooled row ph = i - 2 from conv rows 2ph .. 2ph+2 (written before the
+    // last barrier; this iteration writes slots r0, r0+1, different ones).
+    // First in the iteration: its global store is then older than this
+    // iteration's DMA, so the closing vmcnt(1) does not wait for the DMA.
+    const int ph = i - 2;
+    if (ph >= 0 && ph < kPH && tid < kPH * 8) {
+      const int pw = tid >> 3, cg = tid & 7;
+      ushort8 m = ushort8{0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+      for (int dy = 0; dy < 3; ++dy) {
+        const char* row = conv + ((2 * ph + dy) & (kConvRing - 1)) * kConvB;
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx)
+          m = __builtin_elementwise_max(m, *(const ushort8*)(row + conv_off(2 * pw + dx, cg)));
       }
-      // ---- conv row oh: 17 k-steps x 2 n-blocks
-      floatx4 acc[2] = {floatx4{0.f, 0.f, 0.f, 0.f}, floatx4{0.f, 0.f, 0.f, 0.f}};
-      const int pr0 = 4 * oh;
-      // all 17 B operands issued up front (one read fed only 2 MFMAs: read
-      // one step ahead, its LDS latency was exposed every step)
-      bf16x8 xb[kKS];
+      *(ushort8*)(a.y + (((long)b * kPH + ph) * kPH + pw) * kC + cg * 8) = m;
+    }
+    // raw rows of conv rows r0+8, r0+9 (padded 4r0+39 .. 4r0+46, one per
+    // wave; their raw ring slots were converted two iterations ago)
+    const int dpr = 4 * r0 + 39 + wave;
+    const bool dma_now = r0 + 8 + (wave >> 2) < kHo && dma_issues(dpr);
+    if (dma_now) dma_row(dpr);
+    // convert conv rows r0+4, r0+5's new rows (padded 4r0+23 .. 4r0+30; raw
+    // rows landed before the last barrier); disjoint from the rows read below
+    for (int it = tid; it < 8 * kChunks; it += 512) {
+      const int q = it / kChunks, p = it - q * kChunks;
+      const int pr = 4 * r0 + 23 + q;
+      if (r0 + 4 + (q >> 2) < kHo) convert_chunk(pr, p);
+    }
+    // ---- conv rows r0, r0 + 1: 17 k-steps x 2 n-blocks each
 #pragma unroll
-      for (int ks = 0; ks < kKS; ++ks)
-        xb[ks] = *(const bf16x8*)(ring + ((pr0 + kh_of[ks]) & (kRing - 1)) * kRowB + col_of[ks]);
+    for (int rr = 0; rr < 2; ++rr) {
+      const int oh = r0 + rr;
+      if (oh < kHo) {
+        floatx4 acc[2] = {floatx4{0.f, 0.f, 0.f, 0.f}, floatx4{0.f, 0.f, 0.f, 0.f}};
+        const int pr0 = 4 * oh;
+        // all 17 B operands issued up front (one read fed only 2 MFMAs)
+        bf16x8 xb[kKS];
 #pragma unroll
-      for (int ks = 0; ks < kKS; ++ks) {
-        acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[ks][0], xb[ks], acc[0], 0, 0, 0);
-        acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[ks][1], xb[ks], acc[1], 0, 0, 0);
-      }
-      // lane: channels ch0 + 8 fq .. +7 of pixel ow (nf 0: +0..3, nf 1: +4..7)
-      if (ow < kHo) {
-        float v[8];
+        for (int ks = 0; ks < kKS; ++ks)
+          xb[ks] = *(const bf16x8*)(ring + ((pr0 + kh_of[ks]) & (kRing - 1)) * kRowB + col_of[ks]);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          v[i] = fmaxf(acc[0][i] + bs[i], 0.f);
-          v[4 + i] = fmaxf(acc[1][i] + bs[4 + i], 0.f);
+        for (int ks = 0; ks < kKS; ++ks) {
+          acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[ks][0], xb[ks], acc[0], 0, 0, 0);
+          acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[ks][1], xb[ks], acc[1], 0, 0, 0);
         }
-        *(uint4*)(conv + (oh & (kConvRing - 1)) * kConvB + conv_off(ow, ch0 / 8 + fq)) = pack8(v);
+        // lane: channels ch0 + 8 fq .. +7 of pixel ow (nf 0: +0..3, nf 1: +4..7)
+        if (ow < kHo) {
+          float v[8];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[e] = fmaxf(acc[0][e] + bs[e], 0.f);
+            v[4 + e] = fmaxf(acc[1][e] + bs[4 + e], 0.f);
+          }
+          *(uint4*)(conv + (oh & (kConvRing - 1)) * kConvB + conv_off(ow, ch0 / 8 + fq)) = pack8(v);
+        }
       }
     }
-    // pooled row ph = (oh - 3) / 2 from conv rows oh-3 .. oh-1 (visible since
-    // the last barrier; this iteration wrote slot oh % 4, a different one)
-    if (oh >= 3 && (oh & 1)) {
-      const int ph = (oh - 3) >> 1;
-      if (tid < kPH * 8) {
-        const int pw = tid >> 3, cg = tid & 7;
-        ushort8 m = ushort8{0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
-        for (int dy = 0; dy < 3; ++dy) {
-          const char* row = conv + ((2 * ph + dy) & (kConvRing - 1)) * kConvB;
-#pragma unroll
-          for (int dx = 0; dx < 3; ++dx)
-            m = __builtin_elementwise_max(m, *(const ushort8*)(row + conv_off(2 * pw + dx, cg)));
-        }
-        *(ushort8*)(a.y + (((long)b * kPH + ph) * kPH + pw) * kC + cg * 8) = m;
-      }
-    }
-    // the next iteration converts conv row oh+5's raw rows (issued one
-    // iteration ago, or in the prologue): they must be in LDS before the
-    // barrier; this iteration's DMA (conv row oh+6) may stay in flight
-    if (wave < 4 && oh + 6 < kHo && dma_issues(4 * oh + 31 + wave))
+    // the next iteration converts conv rows r0+6, r0+7 (DMA'd one iteration
+    // ago, or in the prologue): in LDS before the barrier; this iteration's
+    // DMA may stay in flight
+    if (dma_now)
       asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -38,6 +38,9 @@ struct D13Args {
   bf16* y;            // [B, 13, 13, CO]
   const bf16* zero;   // >= 16 zero bytes
   int relu;
+  // fused 3x3/s2 max-pool (AlexNet features.12 after features.10): [B, 6, 6, CO]
+  // written instead of y (one pass per wave, ReLU on)
+  bf16* ypool;
 };
 
 constexpr int kH = 13, kW = 13, kNPix = kH * kW;  // 169
@@ -174,6 +177,56 @@ __global__ __launch_bounds__(256, 1) void conv3x3_13_kernel(D13Args a) {
       }
     }
     // ---- epilogue: lane holds channels 32 grp + 8 g .. +7 of pixel 16 f + fr
+    if constexpr (NGW == GPP) {
+      if (a.ypool) {
+        // fused max-pool: every wave is done with the staged image, so this
+        // wave's 169 x 32 GPP-channel output tile goes into its own quarter of
+        // that LDS (chunks XOR-swizzled by pixel), then the wave pools its own
+        // channels: nothing crosses waves after the barrier
+        __syncthreads();
+        constexpr int TB = GPP * 64;  // bytes per pixel of a wave's tile
+        char* tile = xs + wave * (kNPix * TB);
+#pragma unroll
+        for (int j = 0; j < GPP; ++j) {
+          const int ch = 32 * (grp0 + j) + 8 * g;
+          float bs[8];
+          {
+            const float4 lo = *(const float4*)(a.bias + ch), hi = *(const float4*)(a.bias + ch + 4);
+            bs[0] = lo.x, bs[1] = lo.y, bs[2] = lo.z, bs[3] = lo.w, bs[4] = hi.x, bs[5] = hi.y, bs[6] = hi.z,
+            bs[7] = hi.w;
+          }
+#pragma unroll
+          for (int f = 0; f < kMF; ++f) {
+            const int p = 16 * f + fr;
+            if (p < kNPix) {
+              float v[8];
+#pragma unroll
+              for (int e = 0; e < 8; ++e) v[e] = fmaxf(acc[f][2 * j + (e >> 2)][e & 3] + bs[e], 0.f);
+              *(uint4*)(tile + p * TB + (((4 * j + g) ^ (p & (4 * GPP - 1))) << 4)) = pack8(v);
+            }
+          }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        // 6 x 6 pooled pixels x 4 GPP chunks of 8 channels; post-ReLU bf16 >= 0,
+        // so the max is an unsigned 16-bit max
+        typedef unsigned short ushort8 __attribute__((ext_vector_type(8)));
+        constexpr int NC = 4 * GPP;
+        for (int it = lane; it < 36 * NC; it += 64) {
+          const int pp = it / NC, c = it - pp * NC;
+          const int ph = pp / 6, pw = pp - ph * 6;
+          ushort8 m = ushort8{0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+          for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+            for (int dx = 0; dx < 3; ++dx) {
+              const int q = (2 * ph + dy) * kW + 2 * pw + dx;
+              m = __builtin_elementwise_max(m, *(const ushort8*)(tile + q * TB + ((c ^ (q & (NC - 1))) << 4)));
+            }
+          *(ushort8*)(a.ypool + ((long)b * 36 + pp) * CO + 32 * grp0 + 8 * c) = m;
+        }
+        continue;
+      }
+    }
     bf16* yim = a.y + (long)b * kNPix * CO;
 #pragma unroll
     for (int j = 0; j < GPP; ++j) {
@@ -207,13 +260,16 @@ void launch13(const D13Args& a, int B, hipStream_t s) {
 
 }  // namespace
 
+// the fused max-pool needs one pass per wave (the 256 -> 256 variant)
+bool conv3x3_13_pool_supported(int Cin, int Cout) { return Cin == 256 && Cout == 256; }
+
 bool conv3x3_13_supported(int H, int W, int Cin, int Cout) {
   return H == kH && W == kW &&
          ((Cin == 192 && Cout == 384) || (Cin == 384 && Cout == 256) || (Cin == 256 && Cout == 256));
 }
 
 void conv3x3_13(const void* x, const void* wf, const float* bias, void* y, const void* zero, int B, int Cin, int Cout,
-                bool relu, hipStream_t s) {
+                bool relu, hipStream_t s, void* ypool) {
   if (B <= 0) return;
   if (!conv3x3_13_supported(kH, kW, Cin, Cout)) throw std::invalid_argument("conv3x3_13: unsupported channels");
   if (!x || !wf || !bias || !y || !zero || (((uintptr_t)x | (uintptr_t)wf | (uintptr_t)y | (uintptr_t)zero) & 15))
@@ -225,6 +281,9 @@ void conv3x3_13(const void* x, const void* wf, const float* bias, void* y, const
   a.y = (bf16*)y;
   a.zero = (const bf16*)zero;
   a.relu = relu ? 1 : 0;
+  a.ypool = (bf16*)ypool;
+  if (ypool && (!relu || !conv3x3_13_pool_supported(Cin, Cout) || ((uintptr_t)ypool & 15)))
+    throw std::invalid_argument("conv3x3_13: fused pool needs ReLU, Cin = Cout = 256, aligned output");
   // (ring depth / groups per pass: the largest without spills)
   if (Cin == 192) launch13<192, 384, 3, 1>(a, B, s);
   else if (Cin == 384) launch13<384, 256, 3, 2>(a, B, s);

@@ -39,13 +39,17 @@ struct D27Args {
   const float* bias;  // [192]
   bf16* y;            // [B, 27, 27, 192]
   const bf16* zero;   // >= 16 zero bytes
+  // fused 3x3/s2 max-pool (features.5): [B, 13, 13, 192] written instead of y
+  bf16* ypool;
 };
 
 constexpr int kH = 27, kW = 27, kNPix = kH * kW;  // 729
 constexpr int kCI = 64, kCO = 192, kKS = 5, kPad = 2;
 constexpr int kPXB = kCI * 2;                      // 128 B per staged pixel
 constexpr int kZB = kNPix * kPXB;                  // zero pixel
+constexpr int kTile = kNPix * 64;                  // fused pool: one 32-channel group's output [729][32]
 constexpr size_t kLds = (size_t)kZB + kPXB;
+constexpr size_t kLdsPool = kLds + kTile;
 constexpr int kWaves = 8;                          // 2 per SIMD
 constexpr int kFPW = 6;                            // pixel fragments per wave (46 real over 8 waves)
 constexpr int kCT = kCI / 32;                      // 2 K steps per tap
@@ -165,6 +169,50 @@ __global__ __launch_bounds__(512, 1) void conv5x5_27_kernel(D27Args a) {
       }
     }
     // ---- epilogue: lane holds channels 32 grp + 8 g .. +7 of pixel 16 (f0 + f) + fr
+    if (a.ypool) {
+      // fused max-pool, one 32-channel group at a time through an LDS tile
+      // after the staged image ([729][32] bf16, 16-B chunks XOR-swizzled by
+      // pixel): every wave writes its pixels, then all 512 threads pool
+      typedef unsigned short ushort8 __attribute__((ext_vector_type(8)));
+      char* tile = xs + kLds;
+#pragma unroll
+      for (int j = 0; j < kGPP; ++j) {
+        const int ch = 32 * (grp0 + j) + 8 * g;
+        float bs[8];
+        {
+          const float4 lo = *(const float4*)(a.bias + ch), hi = *(const float4*)(a.bias + ch + 4);
+          bs[0] = lo.x, bs[1] = lo.y, bs[2] = lo.z, bs[3] = lo.w, bs[4] = hi.x, bs[5] = hi.y, bs[6] = hi.z,
+          bs[7] = hi.w;
+        }
+        __syncthreads();  // the previous group's pooling reads are done
+#pragma unroll
+        for (int f = 0; f < kFPW; ++f) {
+          const int p = 16 * (f0 + f) + fr;
+          if (p < kNPix) {
+            float v[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = fmaxf(acc[f][2 * j + (e >> 2)][e & 3] + bs[e], 0.f);
+            *(uint4*)(tile + p * 64 + ((g ^ (p & 3)) << 4)) = pack8(v);
+          }
+        }
+        __syncthreads();
+        // 13 x 13 pooled pixels x 4 chunks; post-ReLU bf16 >= 0: unsigned max
+        for (int it = threadIdx.x; it < 169 * 4; it += 64 * kWaves) {
+          const int pp = it >> 2, c = it & 3;
+          const int ph = (pp * 79) >> 10, pw = pp - ph * 13;  // pp / 13 for pp < 169
+          ushort8 m = ushort8{0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+          for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+            for (int dx = 0; dx < 3; ++dx) {
+              const int q = (2 * ph + dy) * kW + 2 * pw + dx;
+              m = __builtin_elementwise_max(m, *(const ushort8*)(tile + q * 64 + ((c ^ (q & 3)) << 4)));
+            }
+          *(ushort8*)(a.ypool + ((long)b * 169 + pp) * kCO + 32 * (grp0 + j) + 8 * c) = m;
+        }
+      }
+      continue;
+    }
     bf16* yim = a.y + (long)b * kNPix * kCO;
 #pragma unroll
     for (int j = 0; j < kGPP; ++j) {
@@ -194,7 +242,8 @@ bool conv5x5_27_supported(int H, int W, int Cin, int Cout, int pad) {
   return H == kH && W == kW && Cin == kCI && Cout == kCO && pad == kPad;
 }
 
-void conv5x5_27(const void* x, const void* wf, const float* bias, void* y, const void* zero, int B, hipStream_t s) {
+void conv5x5_27(const void* x, const void* wf, const float* bias, void* y, const void* zero, int B, hipStream_t s,
+                void* ypool) {
   if (B <= 0) return;
   if (!x || !wf || !bias || !y || !zero || (((uintptr_t)x | (uintptr_t)wf | (uintptr_t)y | (uintptr_t)zero) & 15))
     throw std::invalid_argument("conv5x5_27: null / misaligned operand");
@@ -204,7 +253,9 @@ void conv5x5_27(const void* x, const void* wf, const float* bias, void* y, const
   a.bias = bias;
   a.y = (bf16*)y;
   a.zero = (const bf16*)zero;
-  hipLaunchKernelGGL(conv5x5_27_kernel, dim3(B), dim3(64 * kWaves), kLds, s, a);
+  a.ypool = (bf16*)ypool;
+  if ((uintptr_t)ypool & 15) throw std::invalid_argument("conv5x5_27: misaligned pooled output");
+  hipLaunchKernelGGL(conv5x5_27_kernel, dim3(B), dim3(64 * kWaves), ypool ? kLdsPool : kLds, s, a);
   DMLC_HIP_CHECK(hipGetLastError());
 }
 

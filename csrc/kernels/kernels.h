@@ -156,13 +156,18 @@ void conv3x3_block(const void* x, const void* wf1, const float* bias1, const voi
 // (conv3x3_13.hip): AlexNet features.6/.8/.10 (192->384, 384->256,
 // 256->256). wf: fragment-order weights (stream_frag_index, K = 9 Cin).
 bool conv3x3_13_supported(int H, int W, int Cin, int Cout);
+// ypool: also fuse the following 3x3/s2 max-pool (13 -> 6), written instead of
+// y (256 -> 256 with ReLU only: conv3x3_13_pool_supported).
+bool conv3x3_13_pool_supported(int Cin, int Cout);
 void conv3x3_13(const void* x, const void* wf, const float* bias, void* y, const void* zero, int B, int Cin, int Cout,
-                bool relu, hipStream_t s);
+                bool relu, hipStream_t s, void* ypool = nullptr);
 // Direct 5x5/s1/p2 conv 27x27x64 -> 192 with the image in LDS
 // (conv5x5_27.hip): AlexNet features.3. wf: fragment-order weights
 // (stream_frag_index, K = 1600); bias + ReLU.
 bool conv5x5_27_supported(int H, int W, int Cin, int Cout, int pad);
-void conv5x5_27(const void* x, const void* wf, const float* bias, void* y, const void* zero, int B, hipStream_t s);
+// ypool: also fuse the following 3x3/s2 max-pool (27 -> 13), written instead of y.
+void conv5x5_27(const void* x, const void* wf, const float* bias, void* y, const void* zero, int B, hipStream_t s,
+                void* ypool = nullptr);
 // ResNet50 layer1 identity bottleneck (resnet50_fp8 layer1.1 / 1.2) in one
 // kernel (bottleneck56.hip): x, y e4m3 [B,56,56,256]; w1 e4m3 [64][256] with
 // a1 = s_x * s_w1; wf2 / wf3: fragment-order bf16 weights (stream_frag_index,

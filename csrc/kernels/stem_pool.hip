@@ -58,6 +58,11 @@ constexpr int kRing = 21;  // staged input rows: 13 for a step + 8 in flight
 // after the current step's MFMAs, so the paired ring needs just 13 rows
 // (and the workgroup still fits 2 per CU: ~73 KB of LDS at 224x224).
 constexpr int kRingU8 = 13;
+// raw u8 ring slot: the row at byte 16, zero pads before (16) and after (64)
+// it, so the conversion's 28-byte windows (which start 12 bytes before the
+// row and end up to 16 after it) read in-slot zeros at the edges: no
+// per-dword bounds checks
+constexpr int kU8Front = 16, kU8Pad = 80;
 constexpr int kHp = 5;     // horizontally pooled conv rows: carried halo + 4
 constexpr int kK = 224;    // 7 kernel rows x 4 chunks x 8
 // Pooled-row LDS layout: [pw][64 ch] with a 144-B column stride (128 + 16 pad):
@@ -129,6 +134,8 @@ struct StemGeom {
   static constexpr int need = ((Ho - 1) * 6 + 26) / 3;  // stem_row_width(S, 3, 7, 2)
   static constexpr int Wr = ((S + 6 > need ? S + 6 : need) + 7) / 8 * 8;
   static constexpr int Wq = Wr / 2;  // paired 16-B chunks per staged row
+  // the u8 conversion's last 28-byte window ends this far past the raw row
+  static_assert(24 * ((Wq + 3) / 4) - 8 - 3 * S <= kU8Pad - kU8Front, "raw ring pad");
 };
 
 template <int NF, bool U8>
@@ -139,6 +146,7 @@ __global__ __launch_bounds__(256, 2) void stem_conv_pool_kernel(
   constexpr int RING = U8 ? kRingU8 : kRing;
   const int RB = G::Wq * 16;  // bytes per staged input row
   const int UB = G::S * 3;    // bytes per raw u8 image row (U8)
+  const int UBS = UB + kU8Pad;  // raw ring slot
   char* ring = (char*)smem;
   char* hp = ring + RING * RB;
   char* u8ring = hp + kHp * G::PW * kHpCol;  // U8: raw rows, slot = row % RING
@@ -165,7 +173,7 @@ __global__ __launch_bounds__(256, 2) void stem_conv_pool_kernel(
         const int iy = r - 3;
         if (iy < 0 || iy >= G::S) continue;
         const uint8_t* src = uimg + (long)iy * UB;
-        char* dst = u8ring + (r % RING) * UB;
+        char* dst = u8ring + (r % RING) * UBS + kU8Front;
         for (int c0 = 0; c0 < UB / 4; c0 += 64)
           if (c0 + lane < UB / 4)
             dma4(src + (c0 + lane) * 4, dst + c0 * 4);
@@ -193,14 +201,14 @@ __global__ __launch_bounds__(256, 2) void stem_conv_pool_kernel(
       if (r < 0) continue;
       const int iy = r - 3;
       const bool row_in = iy >= 0 && iy < G::S;
-      const char* srow = u8ring + (r % RING) * UB;
+      const char* srow = u8ring + (r % RING) * UBS + kU8Front;
       const int A = 24 * k - 12;
+      // all 7 reads unconditional from one base (the slot's zero pads cover
+      // the window's overhang at the row ends; a guarded read per dword had
+      // compiled to an exec-masked branch each, the first with its own wait)
       uint32_t d[7];
 #pragma unroll
-      for (int j = 0; j < 7; ++j) {
-        const int o = A + 4 * j;
-        d[j] = (row_in && o >= 0 && o < UB) ? *(const uint32_t*)(srow + o) : 0u;
-      }
+      for (int j = 0; j < 7; ++j) d[j] = row_in ? *(const uint32_t*)(srow + A + 4 * j) : 0u;
       float v[32];
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
@@ -234,6 +242,11 @@ __global__ __launch_bounds__(256, 2) void stem_conv_pool_kernel(
 #pragma unroll
   for (int n = 0; n < 4; ++n) bs[n] = a.bias[n * 16 + fr];
 
+  if constexpr (U8) {  // the raw ring's pads stay zero (the DMA writes rows only)
+    for (int o = tid * 16; o < RING * UBS; o += 256 * 16) *(uint4*)(u8ring + o) = make_uint4(0, 0, 0, 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
   // Prologue: rows for step 0 (the 13 rows of c0(0), negative ones skipped).
   load_rows(4 * ph0 - 8, 13);
   vm_wait<0>();
@@ -391,7 +404,7 @@ void stem_launch(const void* x, const uint8_t* u8, const void* w, const float* b
   a.PH = PH;
   a.PW = PH;
   a.strip = strip;
-  const size_t lds = u8 ? (size_t)kRingU8 * Wq * 16 + (size_t)kHp * a.PW * kHpCol + (size_t)kRingU8 * S * 3
+  const size_t lds = u8 ? (size_t)kRingU8 * Wq * 16 + (size_t)kHp * a.PW * kHpCol + (size_t)kRingU8 * (S * 3 + kU8Pad)
                         : (size_t)kRing * Wq * 16 + (size_t)kHp * a.PW * kHpCol;
   const dim3 grid(B * (PH / strip));
   if (u8) {

@@ -961,15 +961,45 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
             skip_ds = -1;
             break;
           }
-          case ConvPath::Direct13:
+          case ConvPath::Direct13: {
+            // AlexNet features.10 + features.12: the 3x3/s2 max-pool in the
+            // conv's epilogue when the pool is the conv output's only reader
+            void* ypool = nullptr;
+            if (opt_.fused_pool && cs == s && oi + 1 < ops_.size() && L.relu &&
+                conv3x3_13_pool_supported(is.C, L.cout)) {
+              const Op& mp = ops_[oi + 1];
+              bool only = mp.type == OpType::MaxPool && mp.in == op.out && mp.k == 3 && mp.stride == 2 &&
+                          mp.pad == 0 && shapes_[mp.out].H == 6 && shapes_[mp.out].W == 6;
+              for (size_t j = 0; only && j < ops_.size(); ++j)
+                if (j != oi + 1 && (ops_[j].in == op.out || ops_[j].res == op.out)) only = false;
+              if (only) {
+                ypool = acts_[mp.out];
+                skip = 1;
+              }
+            }
             conv3x3_13(acts_[op.in], (const uint8_t*)warena_ + L.wf_off,
                        (const float*)((const uint8_t*)warena_ + L.b_off), acts_[op.out], zero_, B, is.C, L.cout,
-                       L.relu, cs);
+                       L.relu, cs, ypool);
             break;
-          case ConvPath::Direct27:
+          }
+          case ConvPath::Direct27: {
+            // AlexNet features.3 + features.5: the max-pool in the conv's epilogue
+            void* ypool = nullptr;
+            if (opt_.fused_pool && cs == s && oi + 1 < ops_.size()) {
+              const Op& mp = ops_[oi + 1];
+              bool only = mp.type == OpType::MaxPool && mp.in == op.out && mp.k == 3 && mp.stride == 2 &&
+                          mp.pad == 0 && shapes_[mp.out].H == 13 && shapes_[mp.out].W == 13;
+              for (size_t j = 0; only && j < ops_.size(); ++j)
+                if (j != oi + 1 && (ops_[j].in == op.out || ops_[j].res == op.out)) only = false;
+              if (only) {
+                ypool = acts_[mp.out];
+                skip = 1;
+              }
+            }
             conv5x5_27(acts_[op.in], (const uint8_t*)warena_ + L.wf_off,
-                       (const float*)((const uint8_t*)warena_ + L.b_off), acts_[op.out], zero_, B, cs);
+                       (const float*)((const uint8_t*)warena_ + L.b_off), acts_[op.out], zero_, B, cs, ypool);
             break;
+          }
           case ConvPath::Rows28:
             conv3x3_rows28(acts_[op.in], (const uint8_t*)warena_ + L.wf_off,
                            (const float*)((const uint8_t*)warena_ + L.b_off), op.res >= 0 ? acts_[op.res] : nullptr,

@@ -1,5 +1,4 @@
 #!/bin/bash
-# AlexNet stem DMA pipeline + FC split-K: tests, bench, per-op
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -17,4 +16,5 @@ grep -q " failed" gpurun_out/alex_tests.log && { echo "alexnet tests failed: sto
 B="python bench.py --model alexnet --latency-queries 0 --e2e-queries 0 --latency-steps 10"
 step alex_bench 200 $B
 step alex_ops 200 $B --steps 5 --warmup 2 --prime-steps 5 --profile-ops
-step alex_bench2 200 $B
+step alex_nopool 200 $B --engine-opt fused_pool=0
+bash tools/gpu_r3h.sh

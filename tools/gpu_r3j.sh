@@ -1,5 +1,5 @@
 #!/bin/bash
-# AlexNet stem DMA pipeline + FC split-K: tests, bench, per-op
+# stems: branch-free u8 conversion (AlexNet + ResNet18): engine tests, benches, per-op, PMC
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -12,9 +12,11 @@ step() {
   tail -3 "gpurun_out/$name.log"
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
 }
-step alex_tests 300 python -u -m pytest -x -v -s --timeout 200 --timeout-method thread tests/test_engine_gpu.py -k "alexnet"
-grep -q " failed" gpurun_out/alex_tests.log && { echo "alexnet tests failed: stopping"; exit 1; }
+step eng_tests 400 python -u -m pytest -x -v -s --timeout 200 --timeout-method thread tests/test_engine_gpu.py tests/test_kernels_gpu.py
+grep -q " failed" gpurun_out/eng_tests.log && { echo "engine tests failed: stopping"; exit 1; }
 B="python bench.py --model alexnet --latency-queries 0 --e2e-queries 0 --latency-steps 10"
 step alex_bench 200 $B
 step alex_ops 200 $B --steps 5 --warmup 2 --prime-steps 5 --profile-ops
-step alex_bench2 200 $B
+R="python bench.py --latency-queries 0 --e2e-queries 0 --latency-steps 10"
+step r18_bench 200 $R
+step r18_ops 200 $R --steps 5 --warmup 2 --prime-steps 5 --profile-ops
