@@ -243,6 +243,7 @@ PYBIND11_MODULE(_C, m) {
                                 uintptr_t stream) {
     stem_conv_pool_u8(P<uint8_t>(x), P<void>(w), P<float>(bias), P<void>(y), B, S_, strip, S(stream));
   });
+  m.def("stem_conv_pool_set_dbg", &stem_conv_pool_set_dbg);
   m.def("stem_conv_pool", [](uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y, int B, int S_, int Wq,
                              int strip, uintptr_t stream) {
     stem_conv_pool(P<void>(x), P<void>(w), P<float>(bias), P<void>(y), B, S_, Wq, strip, S(stream));

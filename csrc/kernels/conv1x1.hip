@@ -118,6 +118,8 @@ struct C1Args {
   int nslices, nblocks;
   int relu;
   float res_scale, out_inv_scale;
+  const void* x2;  // second input (K chunks cpr1 .. CPR-1 of a pixel), or null
+  int cpr1;        // 16-B chunks of a pixel from x
 };
 
 // pixels per block: 64, or 32 for 1-KB input rows (stage = BM x RB bytes)
@@ -192,7 +194,7 @@ __global__ __launch_bounds__(256, 2) void conv1x1_kernel(C1Args a) {
     }
 
   // ---- staging: block m -> stage buffer (pixel p's RB bytes, chunk-swizzled)
-  const long rowstride_in = (long)CPR * 16;
+  const long rowstride_in = (long)a.cpr1 * 16;  // x's pixel stride (all of K without x2)
   auto pixel_src = [&](int m) -> const uint8_t* {  // input pixel of output pixel m
     if constexpr (S2 == 1) {
       return (const uint8_t*)a.x + (long)m * rowstride_in;
@@ -210,7 +212,13 @@ __global__ __launch_bounds__(256, 2) void conv1x1_kernel(C1Args a) {
       const int i = (d * 4 + wave) * 64 + lane;  // chunk index in the stage
       const int p = i / CPR, pc = i % CPR;
       const int lc = pc ^ swz1<RB, IN8>(p);  // logical chunk stored at physical pc
-      const void* src = live ? (const void*)(pixel_src(blk * kBM + p) + lc * 16) : a.zero;
+      const void* src = a.zero;
+      if (live) {
+        if (lc < a.cpr1)
+          src = pixel_src(blk * kBM + p) + lc * 16;
+        else  // concatenated second input (stride 1: same pixel index)
+          src = (const uint8_t*)a.x2 + ((long)(blk * kBM + p) * (CPR - a.cpr1) + (lc - a.cpr1)) * 16;
+      }
       dma16(src, dst + (d * 4 + wave) * 1024);
     }
   };
@@ -362,8 +370,9 @@ Pick pick(const ConvArgs& a) {
       a.split_k > 1)
     return p;
   const int esz = a.in_fp8 ? 1 : 2;
-  if (a.Cin != a.Kpad || a.N != a.Npad || a.ldo != a.N) return p;
-  const int rb = a.Cin * esz;
+  if (a.x2 && (a.in_fp8 || a.stride != 1 || a.cin2 <= 0 || a.cin2 % 8)) return p;
+  if (a.Cin + (a.x2 ? a.cin2 : 0) != a.Kpad || a.N != a.Npad || a.ldo != a.N) return p;
+  const int rb = a.Kpad * esz;
   if (rb != 128 && rb != 256 && rb != 512 && rb != 1024) return p;
   if (a.in_fp8 && a.Cin % 128) return p;
   const long M = (long)a.B * a.Ho * a.Wo;
@@ -427,6 +436,9 @@ void conv1x1(const ConvArgs& a, int num_cus, hipStream_t s) {
     throw std::invalid_argument("conv1x1: null / misaligned operand");
   C1Args c;
   c.x = a.x;
+  c.x2 = a.x2;
+  c.cpr1 = a.Cin * (a.in_fp8 ? 1 : 2) / 16;
+  if (a.x2 && ((uintptr_t)a.x2 & 15)) throw std::invalid_argument("conv1x1: misaligned second input");
   c.w = a.w;
   c.bias = a.bias;
   c.alpha = a.alpha;

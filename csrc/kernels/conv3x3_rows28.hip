@@ -55,8 +55,15 @@ constexpr int kR = 4;                 // output rows per step
 constexpr int kSteps = kH / kR;       // 7
 constexpr int kPlane = 30 * 64;       // one channel quarter of a staged row: 1920 B
 constexpr int kRB = 4 * kPlane;       // 7680 B per staged row
-constexpr int kRing = 10;             // rows r0 - 1 .. r0 + 4 in use + 4 in flight
-constexpr int kSlotsAlloc = kRing + 2;
+// Input rows are DMA'd AH steps ahead: rows r0 - 1 .. r0 + 4 in use + 4 AH
+// in flight. One step ahead (the default, 10-row ring) measured faster than
+// two (14-row ring): 48.2-48.9 vs 51.5-52.0 us at B = 256 with warm clocks
+// (profiles/r3_rows28_ahead.txt).
+template <int AH>
+struct R28Ring {
+  static constexpr int kRing = 6 + 4 * AH;
+  static constexpr int kSlotsAlloc = kRing + 2;  // + guard copies of slots 0, 1
+};
 constexpr int kRun = 4 * kW;          // 112 DMA chunks per quarter plane (slots 1..28)
 constexpr int kMF = kR * kW / 16;     // 7 pixel fragments per step
 constexpr int kKS = 9 * kC / 32;      // 36 K steps
@@ -64,10 +71,26 @@ constexpr int kResCh = kMF * 16 * 16;  // residual chunks per step (112 pixels x
 
 __device__ __forceinline__ int swz_of(int y, int x) { return ((kW * y + x) >> 1) & 3; }
 
+// s_waitcnt vmcnt(base + n) for a wave-uniform runtime n in [0, 24]
+template <int BASE>
+__device__ __forceinline__ void vm_wait_plus(int n) {
+  switch (n) {
+#define DMLC_VMW(N) \
+  case N: vm_wait<BASE + N>(); break;
+    DMLC_VMW(0) DMLC_VMW(1) DMLC_VMW(2) DMLC_VMW(3) DMLC_VMW(4) DMLC_VMW(5) DMLC_VMW(6) DMLC_VMW(7) DMLC_VMW(8)
+    DMLC_VMW(9) DMLC_VMW(10) DMLC_VMW(11) DMLC_VMW(12) DMLC_VMW(13) DMLC_VMW(14) DMLC_VMW(15) DMLC_VMW(16)
+    DMLC_VMW(17) DMLC_VMW(18) DMLC_VMW(19) DMLC_VMW(20) DMLC_VMW(21) DMLC_VMW(22) DMLC_VMW(23) DMLC_VMW(24)
+#undef DMLC_VMW
+    default: vm_wait<BASE>(); break;  // never: counts above 24 do not occur (wait longer)
+  }
+}
+
 // DBG (experiments): bit 0 no row DMA in the loop, bit 1 no LDS reads in the
 // K loop, bit 2 no epilogue, bit 3 prologue only
-template <bool RES, int DBG = 0>
+template <bool RES, int DBG = 0, int AH = 1>
 __global__ __launch_bounds__(256, 1) void conv3x3_rows28_kernel(R28Args a) {
+  constexpr int kRing = R28Ring<AH>::kRing, kSlotsAlloc = R28Ring<AH>::kSlotsAlloc;
+  static_assert(AH == 1 || AH == 2, "rows DMA'd one or two steps ahead");
   extern __shared__ __attribute__((aligned(16))) uint4 smem[];
   char* ring = (char*)smem;
   char* resbuf = ring + kSlotsAlloc * kRB;  // RES: [112 pixels][16 chunks]
@@ -80,9 +103,11 @@ __global__ __launch_bounds__(256, 1) void conv3x3_rows28_kernel(R28Args a) {
   for (int o = tid * 16; o < kSlotsAlloc * kRB; o += 256 * 16) *(uint4*)(ring + o) = make_uint4(0, 0, 0, 0);
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
-  // input row yy -> ring slot (yy + 1) % 10 (+ guard slot 10 / 11 for slots
-  // 0 / 1); wave w stages quarter plane w: chunks 0..63 and 64..111 of its run.
-  // Row 28 (below the image) reuses a slot: its run is written as zeros.
+  // input row yy -> ring slot (yy + 1) % kRing (+ guard slot kRing / kRing+1
+  // for slots 0 / 1); wave w stages quarter plane w: chunks 0..63 and
+  // 64..111 of its run. Row 28 (below the image) reuses a slot: its run is
+  // written as zeros. row_dmas(yy) = the DMA instructions load_row(yy) issues
+  // (wave-uniform; the vmcnt waits below count them).
   auto load_row = [&](int yy) __attribute__((always_inline)) {
     const int slot = (yy + 1) % kRing;
     char* dst = ring + wave * kPlane + 64;
@@ -97,10 +122,21 @@ __global__ __launch_bounds__(256, 1) void conv3x3_rows28_kernel(R28Args a) {
           if (slot < 2) dma16(src, dst + (slot + kRing) * kRB + i0 * 16);
         } else {
           *(uint4*)(dst + slot * kRB + k * 16) = make_uint4(0, 0, 0, 0);
+          if (slot < 2) *(uint4*)(dst + (slot + kRing) * kRB + k * 16) = make_uint4(0, 0, 0, 0);
         }
       }
     }
   };
+  auto row_dmas = [&](int yy) __attribute__((always_inline)) {
+    return yy < kH ? ((yy + 1) % kRing < 2 ? 4 : 2) : 0;
+  };
+  // this lane's 8 output channels ch0 + 8g .. +7 (weight rows permuted,
+  // perm32); loaded before the row DMAs so the prologue wait below can leave
+  // exactly the weight loads in flight
+  const int ch0 = wave * 32;
+  float bs[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) bs[e] = a.bias[ch0 + 8 * g + e];
   for (int yy = 0; yy <= 4; ++yy) load_row(yy);
 
   // ---- per-lane constants: fragment f = tile pixels p = 16 f + fr (row
@@ -118,28 +154,29 @@ __global__ __launch_bounds__(256, 1) void conv3x3_rows28_kernel(R28Args a) {
       col[f][kw] = (c + kw) * 64 + ((g ^ s) << 4);
     }
   }
-  const int ch0 = wave * 32;
   bf16x8 w[kKS][2];
 #pragma unroll
   for (int t = 0; t < kKS; ++t)
 #pragma unroll
     for (int nf = 0; nf < 2; ++nf)
       w[t][nf] = *(const bf16x8*)(a.wf + ((((long)wave * kKS + t) * 2 + nf) * 64 + lane) * 8);
-  // this lane's 8 output channels ch0 + 8g .. +7 (weight rows permuted, perm32)
-  float bs[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) bs[e] = a.bias[ch0 + 8 * g + e];
-  vm_wait<0>();
+  // the prologue rows (DMA'd before the weights) have landed; the weights
+  // (72 loads, 288 KB per workgroup from L2) may still be in flight: the
+  // first step's MFMAs wait for each K step's own fragments (the compiler's
+  // counted waits), so the load overlaps the first step instead of preceding it
+  vm_wait<63>();
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
 
-  for (int step = 0; step < ((DBG & 8) ? 0 : kSteps); ++step) {
+  // step 0 is peeled (a separate copy of the body): at a loop header the
+  // compiler waits for every outstanding load (vmcnt(0)), which would put the
+  // whole weight load back in front of the first MFMA
+  auto step_body = [&](const int step) __attribute__((always_inline)) {
     const int r0 = step * kR;  // output rows r0 .. r0 + 3; input rows r0 - 1 .. r0 + 4
-    if (step + 1 < kSteps && !(DBG & 1))
-      for (int yy = r0 + 5; yy <= r0 + 8; ++yy) load_row(yy);
     // residual of this step's 112 output pixels -> LDS (lands during the K
     // loop; registers are full of weights): 16-B chunk c of pixel p at
-    // physical chunk c ^ (p & 15), so the epilogue's reads are conflict free
+    // physical chunk c ^ (p & 15), so the epilogue's reads are conflict free.
+    // Issued before this step's row DMAs: its wait leaves those in flight.
     const long obase = ((long)b * kH + r0) * kW * kC + ch0 + 8 * g;
     if constexpr (RES) {
       const bf16* rimg = a.res + ((long)b * kH + r0) * kW * kC;
@@ -149,6 +186,16 @@ __global__ __launch_bounds__(256, 1) void conv3x3_rows28_kernel(R28Args a) {
         const int p = i >> 4, c = i & 15;
         dma16(rimg + (long)p * kC + 8 * (c ^ (p & 15)), resbuf + (j * 256 + wave * 64) * 16);
       }
+    }
+    // rows of step + AH (step 0 also issues those of steps 1 .. AH - 1)
+    int ndma = 0;
+    if (!(DBG & 1)) {
+      const int s_lo = step == 0 ? 1 : step + AH, s_hi = step + AH;
+      for (int s2 = s_lo; s2 <= s_hi && s2 < kSteps; ++s2)
+        for (int yy = 4 * s2 + 1; yy <= 4 * s2 + 4; ++yy) {
+          load_row(yy);
+          ndma += row_dmas(yy);
+        }
     }
     // ring slot of kernel row 0 of each fragment (+ kh rows: immediate, guard slots)
     int rowoff[kMF];
@@ -196,8 +243,11 @@ __global__ __launch_bounds__(256, 1) void conv3x3_rows28_kernel(R28Args a) {
       }
     }
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (RES) {  // this wave's residual DMAs (the youngest VMEM ops) have landed; and everyone's
-      vm_wait<0>();
+    if constexpr (RES) {  // this wave's residual DMAs (older than this step's row DMAs) have landed; and everyone's
+      if (AH == 1 || step == 0)
+        vm_wait<0>();
+      else
+        vm_wait_plus<0>(ndma);
       __builtin_amdgcn_s_barrier();
     }
     // ---- epilogue: lane holds channels ch0 + 8g .. +7 of tile pixel 16 f + fr
@@ -220,12 +270,24 @@ __global__ __launch_bounds__(256, 1) void conv3x3_rows28_kernel(R28Args a) {
       }
       *(uint4*)(a.y + obase + (long)(16 * f + fr) * kC) = pack8(v);
     }
-    // the next step's rows have landed (older than the kMF stores just
-    // issued: vmcnt retires in order) and every wave is done with the rows
-    // they replace
-    if constexpr (!(DBG & 16)) vm_wait<kMF>();
+    // the next step's rows have landed and every wave is done with the rows
+    // they replace. vmcnt retires in order; younger than those rows: AH = 1
+    // this step's kMF stores; AH = 2 the previous step's stores, this step's
+    // row DMAs and stores (step 0: its K loop already drained every load,
+    // the compiler's waits on the weights; RES: the residual wait before the
+    // epilogue covered them, and this step's row DMAs stay in flight)
+    if constexpr (!(DBG & 16)) {
+      if (AH == 1 || step == 0)
+        vm_wait<kMF>();
+      else if (!RES)
+        vm_wait_plus<2 * kMF>(ndma);
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
+  };
+  if constexpr (!(DBG & 8)) {
+    step_body(0);
+    for (int step = 1; step < kSteps; ++step) step_body(step);
   }
 }
 
@@ -249,8 +311,13 @@ void conv3x3_rows28(const void* x, const void* wf, const float* bias, const void
   a.res = (const bf16*)res;
   a.y = (bf16*)y;
   a.relu = relu;
-  const size_t lds = (size_t)kSlotsAlloc * kRB + (res ? (size_t)kResCh * 16 : 0);  // 90 / 118 KB
+  const int ah = (dbg == 64 || dbg == 65) ? 2 : 1;
+  const size_t lds = (size_t)(ah == 2 ? R28Ring<2>::kSlotsAlloc : R28Ring<1>::kSlotsAlloc) * kRB +
+                     (res ? (size_t)kResCh * 16 : 0);  // 90 / 118 KB (two ahead: 123 / 151 KB)
+  static_assert(R28Ring<2>::kSlotsAlloc * kRB + kResCh * 16 <= 160 * 1024, "LDS budget");
   switch (dbg) {
+    case 64: hipLaunchKernelGGL((conv3x3_rows28_kernel<false, 0, 2>), dim3(B), dim3(256), lds, s, a); break;
+    case 65: hipLaunchKernelGGL((conv3x3_rows28_kernel<true, 0, 2>), dim3(B), dim3(256), lds, s, a); break;
     case 1: hipLaunchKernelGGL((conv3x3_rows28_kernel<false, 1>), dim3(B), dim3(256), lds, s, a); break;
     case 2: hipLaunchKernelGGL((conv3x3_rows28_kernel<false, 2>), dim3(B), dim3(256), lds, s, a); break;
     case 4: hipLaunchKernelGGL((conv3x3_rows28_kernel<false, 4>), dim3(B), dim3(256), lds, s, a); break;

@@ -104,6 +104,16 @@ __global__ __launch_bounds__(256, 1) void conv3x3_s2rows_kernel(S2Args a) {
       }
     }
   };
+  // this lane's 8 output channels ch0 + 8g .. +7 (weight rows permuted,
+  // perm32); loaded before the row DMAs so the prologue wait below can leave
+  // exactly the weight loads in flight
+  const int ch0 = wave * 32;
+  float bs[8], bsd[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    bs[e] = a.bias[ch0 + 8 * g + e];
+    bsd[e] = a.bd[ch0 + 8 * g + e];
+  }
   for (int yy = 0; yy <= 7; ++yy) load_row(yy);
 
   // ---- per-lane constants. Fragment f covers tile pixels p = 16 f + fr (row
@@ -122,7 +132,6 @@ __global__ __launch_bounds__(256, 1) void conv3x3_s2rows_kernel(S2Args a) {
       col[f][v] = (c + kw2) * 64 + ((g ^ s) << 4);
     }
   }
-  const int ch0 = wave * 32;
   bf16x8 w[kKS][2];
 #pragma unroll
   for (int t = 0; t < kKS; ++t)
@@ -132,17 +141,17 @@ __global__ __launch_bounds__(256, 1) void conv3x3_s2rows_kernel(S2Args a) {
                                 : a.wdf + ((((long)wave * kCT + (t - kKT)) * 2 + nf) * 64 + lane) * 8;
       w[t][nf] = *(const bf16x8*)src;
     }
-  // this lane's 8 output channels ch0 + 8g .. +7 (weight rows permuted, perm32)
-  float bs[8], bsd[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    bs[e] = a.bias[ch0 + 8 * g + e];
-    bsd[e] = a.bd[ch0 + 8 * g + e];
-  }
-  vm_wait<0>();
+  // the prologue rows (DMA'd before the weights) have landed; the weights may
+  // still be in flight: the first step's MFMAs wait for each K step's own
+  // fragments (the compiler's counted waits), so the 160 KB weight load from
+  // L2 overlaps the first step instead of preceding it
+  vm_wait<2 * kKS>();
   __builtin_amdgcn_s_barrier();
 
-  for (int step = 0; step < kSteps; ++step) {
+  // step 0 is peeled (a separate copy of the body): at a loop header the
+  // compiler waits for every outstanding load (vmcnt(0)), which would put the
+  // whole weight load back in front of the first MFMA
+  auto step_body = [&](const int step) __attribute__((always_inline)) {
     const int r0 = step * kR;  // first output row; input rows 2 r0 - 1 .. 2 r0 + 7
     if (step + 1 < kSteps && !(a.dbg & 1))
       for (int yy = 2 * r0 + 8; yy <= 2 * r0 + 15; ++yy) load_row(yy);
@@ -217,7 +226,9 @@ __global__ __launch_bounds__(256, 1) void conv3x3_s2rows_kernel(S2Args a) {
     vm_wait<2 * kMF>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-  }
+  };
+  step_body(0);
+  for (int step = 1; step < kSteps; ++step) step_body(step);
 }
 
 }  // namespace

@@ -596,8 +596,11 @@ void launch_stream(const StreamConvArgs& a, hipStream_t s) {
   }
 }
 
-// Tuning hook for tools/conv_bench.py A/B runs (0 = the default kernels):
-// 1 = the 14x14x256 register-weight kernel with a 2-deep weight ring (PD 2).
+// Tuning hook for tools/conv_bench.py A/B runs (0 = the default kernels), bits:
+// 1 = the 14x14x256 register-weight kernel with a 2-deep weight ring (PD 2);
+// 2 = the stride-2 register-weight 28x28x128 kernel with two channel groups
+// per wave (NG 2); 4 = the stride-2 14x14x256 one with one (NG 1, half the
+// channels per workgroup).
 std::atomic<int> g_stream_variant{0};
 
 }  // namespace
@@ -681,7 +684,7 @@ void conv3x3_stream(const void* x, const void* w, const float* bias, const void*
   else if (stride == 1 && Cin == 128)  // layer2: half an image (15 x 28 x 256 B = 105 KB)
     launch_stream<28, 28, 128, 128, 14, 1, 1, 2, 1>(a, s);
   else if (stride == 1 && Cin == 256 && wfrag) {  // layer3, register weights, 2 pixel halves x 4 groups of 64 channels
-    if (g_stream_variant == 1)
+    if (g_stream_variant & 1)
       launch_stream<14, 14, 256, 256, 14, 1, 1, 2, 1, true, 2, 2>(a, s);
     else
       launch_stream<14, 14, 256, 256, 14, 1, 1, 2, 1, true, 4, 2>(a, s);
@@ -701,12 +704,26 @@ void conv3x3_stream(const void* x, const void* w, const float* bias, const void*
     launch_stream<28, 28, 128, 128, 2, 1, 1, 2, 2>(a, s);
   else if (Cin == 64)  // layer2.0.conv1: a quarter image (15 x 56 x 128 B = 105 KB)
     launch_stream<28, 28, 64, 128, 7, 1, 1, 2, 2>(a, s);
-  else if (Cin == 128 && wfrag)
-    launch_stream<14, 14, 128, 256, 7, 1, 1, 1, 2, true>(a, s);
+  else if (Cin == 128 && wfrag) {
+    // variant bit 2: two 32-channel groups per wave (2 pixel halves x 4 x 64
+    // channels, an X fragment read feeds 4 MFMAs instead of 2; 8 fragments
+    // for the 7 of a half image): 50.7 vs 49.4 us at B = 256, not used
+    if (g_stream_variant & 2)
+      launch_stream<14, 14, 128, 256, 7, 1, 1, 2, 2, true, 4, 2>(a, s);
+    else
+      launch_stream<14, 14, 128, 256, 7, 1, 1, 1, 2, true>(a, s);
+  }
   else if (Cin == 128)  // layer3.0.conv1: half an image (15 x 28 x 256 B = 105 KB)
     launch_stream<14, 14, 128, 256, 7, 1, 1, 1, 2>(a, s);
-  else if (wfrag)
-    launch_stream<7, 7, 256, 512, 7, 1, 2, 1, 2, true>(a, s);
+  else if (wfrag) {
+    // a whole image x all 512 channels, 64 per wave (NG 2): 43.0 vs 49.0 us
+    // at B = 256 with the fused downsample for half the channels per
+    // workgroup, 32 per wave (variant bit 4; profiles/r3_stream_s2_ng2.txt)
+    if (g_stream_variant & 4)
+      launch_stream<7, 7, 256, 512, 7, 1, 2, 1, 2, true>(a, s);
+    else
+      launch_stream<7, 7, 256, 512, 7, 1, 1, 1, 2, true, 4, 2>(a, s);
+  }
   else  // layer4.0.conv1: a whole image (14 x 14 x 512 B = 98 KB) x half the output channels
     launch_stream<7, 7, 256, 512, 7, 1, 2, 1, 2>(a, s);
   DMLC_HIP_CHECK(hipGetLastError());

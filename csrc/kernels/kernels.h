@@ -57,6 +57,11 @@ struct ConvArgs {
   bool in_fp8 = false, out_fp8 = false;
   const float* alpha = nullptr;
   float res_scale = 1.f, out_inv_scale = 1.f;
+  // conv1x1 only: a second bf16 input concatenated along K (same pixels,
+  // stride 1): K = Cin channels of x, then cin2 channels of x2 (a bottleneck's
+  // expand conv with its stride-1 downsample folded in: w = [W3 | Wd])
+  const void* x2 = nullptr;
+  int cin2 = 0;
 };
 
 int conv_out_dim(int in, int k, int stride, int pad);
@@ -226,6 +231,8 @@ void stem_conv_pool(const void* x, const void* w, const float* bias, void* y, in
 // Same stem with the preprocess fused: u8 HWC SxS images [B, S, S, 3] in
 // (already at the target size: the identity case of preprocess_u8), the
 // paired bf16 rows built in LDS with preprocess_u8's exact arithmetic.
+// timing knock-outs of the 224x224 u8 stem (0 = off; see stem_pool.hip DBG)
+void stem_conv_pool_set_dbg(int dbg);
 void stem_conv_pool_u8(const uint8_t* x, const void* w, const float* bias, void* y, int B, int S, int strip,
                        hipStream_t s);
 // AlexNet features.0-2 fused (alex_stem.hip): u8 [B, 224, 224, 3] ->

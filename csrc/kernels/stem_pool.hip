@@ -79,7 +79,15 @@ struct StemArgs {
   const float* bias;  // [64]
   bf16* y;            // [B, PH, PW, 64]
   int Hp, Wq, PH, PW, strip;
+  // The second half of the grid (at 2 workgroups per CU: each CU's second
+  // workgroup) starts stagger x ~2048 cycles late. The two workgroups of a CU
+  // otherwise run in lockstep: both in their MFMA phase, then both in the
+  // barrier-separated VALU phase (vertical max, u8 conversion) with the
+  // matrix pipes idle. 100.9 -> 93.0 us at B = 256 with 2
+  // (profiles/r3_stem_knockouts.txt).
+  int stagger;
 };
+constexpr int kStemStagger = 2;
 
 template <int N>
 __device__ __forceinline__ void vm_wait() {
@@ -138,7 +146,10 @@ struct StemGeom {
   static_assert(24 * ((Wq + 3) / 4) - 8 - 3 * S <= kU8Pad - kU8Front, "raw ring pad");
 };
 
-template <int NF, bool U8>
+// DBG (timing experiments, tools/stem_knockouts.py): bit 0 no horizontal-pool
+// epilogue (one store of the accumulators per fragment instead), bit 1 no u8
+// conversion, bit 2 no vertical max / output stores, bit 3 no MFMAs
+template <int NF, bool U8, int DBG = 0>
 __global__ __launch_bounds__(256, 2) void stem_conv_pool_kernel(
     StemArgs a) {
   using G = StemGeom<NF>;
@@ -242,6 +253,8 @@ __global__ __launch_bounds__(256, 2) void stem_conv_pool_kernel(
 #pragma unroll
   for (int n = 0; n < 4; ++n) bs[n] = a.bias[n * 16 + fr];
 
+  if (a.stagger && blockIdx.x >= gridDim.x / 2)  // (a wave-uniform scalar loop)
+    for (int i = 0; i < a.stagger; ++i) __builtin_amdgcn_s_sleep(32);  // ~2048 cycles each
   if constexpr (U8) {  // the raw ring's pads stay zero (the DMA writes rows only)
     for (int o = tid * 16; o < RING * UBS; o += 256 * 16) *(uint4*)(u8ring + o) = make_uint4(0, 0, 0, 0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -285,17 +298,29 @@ __global__ __launch_bounds__(256, 2) void stem_conv_pool_kernel(
           floatx4 acc[4];
 #pragma unroll
           for (int n = 0; n < 4; ++n) acc[n] = floatx4{0.f, 0.f, 0.f, 0.f};
+          if constexpr (DBG & 8) {
+#pragma unroll
+            for (int n = 0; n < 4; ++n) acc[n][0] = (float)xf[n][0] + (float)wf[n][0][0];
+          } else {
 #pragma unroll
           for (int s = 0; s < 7; ++s)
 #pragma unroll
             for (int n = 0; n < 4; ++n)
               acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[s], wf[n][s], acc[n], 0, 0, 0);
+          }
           // The next fragment's operands go out before this epilogue so the
           // reads land under it.
           if (f + 1 < NF) {
 #pragma unroll
             for (int s = 0; s < 7; ++s)
               xf[s] = *(const bf16x8*)(rbase + rows[s] + (f + 1) * 256);
+          }
+          if constexpr (DBG & 1) {
+            float t = 0.f;
+#pragma unroll
+            for (int n = 0; n < 4; ++n) t += acc[n][0] + acc[n][1] + acc[n][2] + acc[n][3];
+            ds_write_lo16(hbase, __float_as_uint(t), f * 8 * kHpCol);
+            continue;
           }
           // Horizontal 3-max over columns (2pw-1, 2pw, 2pw+1), + bias, ReLU.
           // Lane (r, g) holds columns 16f + 4g + i (i = 0..3) of channel
@@ -327,7 +352,7 @@ __global__ __launch_bounds__(256, 2) void stem_conv_pool_kernel(
     // the u8 conversion share one phase (they touch disjoint LDS).
     vm_wait<0>();
     lds_barrier();
-    if (t > 0) {  // vertical 3-max -> pooled rows ph, ph+1
+    if (t > 0 && !(DBG & 4)) {  // vertical 3-max -> pooled rows ph, ph+1
       const int ph = ph0 + 2 * (t - 1);
       const int per_row = G::PW * 8;
       ushort8 m[4];  // 16*PW <= 1024 items: at most 4 per thread, reads issued together
@@ -359,7 +384,7 @@ __global__ __launch_bounds__(256, 2) void stem_conv_pool_kernel(
     if constexpr (U8) {
       // the next step's raw rows landed; the paired rows they replace were
       // last read by this step's MFMAs (before the barrier above)
-      if (t < T) convert_rows(2 * c0 + 13, 8);
+      if (t < T && !(DBG & 2)) convert_rows(2 * c0 + 13, 8);
     }
     // the next step's MFMAs overwrite pooled rows read above and read the
     // converted rows
@@ -381,6 +406,8 @@ int stem_pool_pick_strip(int B, int PH, int num_cus) {
 }
 
 namespace {
+int g_stem_dbg = 0;  // knock-out variant of the 224x224 u8 kernel (tools/stem_knockouts.py)
+
 void stem_launch(const void* x, const uint8_t* u8, const void* w, const float* bias, void* y, int B, int S, int Wq,
                  int strip, hipStream_t s) {
   if (B <= 0) return;
@@ -404,10 +431,25 @@ void stem_launch(const void* x, const uint8_t* u8, const void* w, const float* b
   a.PH = PH;
   a.PW = PH;
   a.strip = strip;
+  a.stagger = (g_stem_dbg >> 8) ? (g_stem_dbg >> 8) - 1 : ((long)B * (PH / strip) >= 512 ? kStemStagger : 0);
   const size_t lds = u8 ? (size_t)kRingU8 * Wq * 16 + (size_t)kHp * a.PW * kHpCol + (size_t)kRingU8 * (S * 3 + kU8Pad)
                         : (size_t)kRing * Wq * 16 + (size_t)kHp * a.PW * kHpCol;
   const dim3 grid(B * (PH / strip));
-  if (u8) {
+  if (u8 && NF == 7 && (g_stem_dbg & 255)) {
+    switch (g_stem_dbg & 255) {
+#define DMLC_STEM_DBG_CASE(D) \
+  case D: hipLaunchKernelGGL((stem_conv_pool_kernel<7, true, D>), grid, dim3(256), lds, s, a); break;
+      DMLC_STEM_DBG_CASE(1)
+      DMLC_STEM_DBG_CASE(2)
+      DMLC_STEM_DBG_CASE(4)
+      DMLC_STEM_DBG_CASE(6)
+      DMLC_STEM_DBG_CASE(7)
+      DMLC_STEM_DBG_CASE(8)
+      DMLC_STEM_DBG_CASE(14)
+#undef DMLC_STEM_DBG_CASE
+      default: throw std::invalid_argument("stem_conv_pool: unknown debug variant");
+    }
+  } else if (u8) {
     switch (NF) {
 #define DMLC_STEM_U8_CASE(F) \
   case F: hipLaunchKernelGGL((stem_conv_pool_kernel<F, true>), grid, dim3(256), lds, s, a); break;
@@ -433,6 +475,8 @@ void stem_launch(const void* x, const uint8_t* u8, const void* w, const float* b
   DMLC_HIP_CHECK(hipGetLastError());
 }
 }  // namespace
+
+void stem_conv_pool_set_dbg(int dbg) { g_stem_dbg = dbg; }
 
 void stem_conv_pool(const void* x, const void* w, const float* bias, void* y, int B, int S, int Wq, int strip,
                     hipStream_t s) {

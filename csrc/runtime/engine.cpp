@@ -78,6 +78,7 @@ bool EngineOptions::set(const std::string& name, bool v) {
       {"fused_preprocess", &EngineOptions::fused_preprocess}, {"row_conv", &EngineOptions::row_conv},
       {"rows_wreg", &EngineOptions::rows_wreg},     {"fused_block", &EngineOptions::fused_block},
       {"fused_bottleneck", &EngineOptions::fused_bottleneck},
+      {"ds_into_expand", &EngineOptions::ds_into_expand},
       {"stream_conv", &EngineOptions::stream_conv}, {"stream_wreg", &EngineOptions::stream_wreg},
       {"stream_l4s2", &EngineOptions::stream_l4s2}, {"fuse_ds", &EngineOptions::fuse_ds},
       {"bigtile", &EngineOptions::bigtile},         {"fused_pool", &EngineOptions::fused_pool},
@@ -376,7 +377,12 @@ void Engine::mark_fp8() {
 // calibration batch and take amax/448 of every tensor that is stored as e4m3.
 void Engine::calibrate(const WeightMap& w) {
   const int Bc = 8;
-  Engine ref(arch_.substr(0, arch_.find("_fp8")), w, device_, num_classes_, image_size_);
+  // every activation must be materialised: no path that computes one inside
+  // its reader (the layer1.0 downsample inside the expand conv)
+  EngineOptions ro;
+  ro.ds_into_expand = false;
+  ro.fused_bottleneck = false;
+  Engine ref(arch_.substr(0, arch_.find("_fp8")), w, device_, num_classes_, image_size_, ro);
   if (ref.num_activations() != num_activations()) throw std::runtime_error("calibrate: graph mismatch");
   ref.reserve(Bc);
   const size_t img_bytes = (size_t)Bc * image_size_ * image_size_ * 3;
@@ -449,6 +455,28 @@ void Engine::pack_weights(const WeightMap& w) {
     if (L.alex_stem) {  // paired-chunk K order for alex_stem.hip
       L.wf_off = off;
       off = align_up(off + (size_t)L.cout * kAlexStemK * 2, 256);
+    }
+  }
+  // bottleneck expand convs that can take their stride-1 downsample as a
+  // second K block (conv1x1 with x2): both bf16 in, 1x1, same output
+  for (size_t j = 0; j < ops_.size(); ++j) {
+    const Op& c3 = ops_[j];
+    if (c3.type != OpType::Conv || c3.res < 0) continue;
+    ConvLayer& L3 = convs_[c3.conv];
+    for (size_t i = 0; i < j; ++i) {
+      const Op& d = ops_[i];
+      if (d.type != OpType::Conv || d.out != c3.res) continue;
+      const ConvLayer& D = convs_[d.conv];
+      if (D.fc || L3.fc || D.kh != 1 || D.kw != 1 || D.stride != 1 || D.relu || !L3.relu || L3.kh != 1 ||
+          L3.kw != 1 || L3.stride != 1 || D.fp8 || L3.fp8 || shapes_[d.in].fp8 || shapes_[c3.in].fp8 ||
+          D.cout != L3.cout || D.npad != L3.npad || shapes_[d.in].H != shapes_[c3.in].H ||
+          shapes_[d.in].W != shapes_[c3.in].W || D.kpad != D.cin || L3.kpad != L3.cin)
+        continue;
+      L3.cat_ds = d.conv;
+      L3.cat_off = off;
+      off = align_up(off + (size_t)L3.npad * (L3.kpad + D.kpad) * 2, 256);
+      L3.cat_b_off = off;
+      off = align_up(off + (size_t)L3.npad * 4, 256);
     }
   }
   weight_bytes_ = off;
@@ -538,6 +566,22 @@ void Engine::pack_weights(const WeightMap& w) {
         alpha[n] = s_in * sw;
       }
     }
+  }
+  for (auto& L : convs_) {  // [W3 | Wd] and b3 + bd from the folded bf16 copies above
+    if (L.cat_ds < 0) continue;
+    const ConvLayer& D = convs_[L.cat_ds];
+    const int K = L.kpad + D.kpad;
+    uint16_t* cw = (uint16_t*)(host.data() + L.cat_off);
+    const uint16_t* w3 = (const uint16_t*)(host.data() + L.w_off);
+    const uint16_t* wd = (const uint16_t*)(host.data() + D.w_off);
+    for (int n = 0; n < L.npad; ++n) {
+      std::copy(w3 + (size_t)n * L.kpad, w3 + (size_t)(n + 1) * L.kpad, cw + (size_t)n * K);
+      std::copy(wd + (size_t)n * D.kpad, wd + (size_t)(n + 1) * D.kpad, cw + (size_t)n * K + L.kpad);
+    }
+    float* cb = (float*)(host.data() + L.cat_b_off);
+    const float* b3 = (const float*)(host.data() + L.b_off);
+    const float* bd = (const float*)(host.data() + D.b_off);
+    for (int n = 0; n < L.npad; ++n) cb[n] = b3[n] + bd[n];
   }
   DMLC_HIP_CHECK(hipMalloc(&warena_, weight_bytes_));
   DMLC_HIP_CHECK(hipMemcpy(warena_, host.data(), weight_bytes_, hipMemcpyHostToDevice));
@@ -789,6 +833,32 @@ bool Engine::bottleneck_fusable(size_t oi) const {
   return true;
 }
 
+// ops[oi] is a downsample whose only reader is a later expand conv that
+// computes it itself (its cat_ds): that op's index, else -1.
+int Engine::ds_expand_op(size_t oi) const {
+  if (!opt_.ds_into_expand || ops_[oi].type != OpType::Conv) return -1;
+  const Op& d = ops_[oi];
+  int reader = -1;
+  for (size_t j = 0; j < ops_.size(); ++j) {
+    if (j == oi) continue;
+    if (ops_[j].in == d.out) return -1;
+    if (ops_[j].res == d.out) {
+      if (reader >= 0) return -1;
+      reader = (int)j;
+    }
+  }
+  if (reader < 0) return -1;
+  const ConvLayer& L3 = convs_[ops_[reader].conv];
+  if (L3.cat_ds != d.conv || !L3.cat_off) return -1;
+  ConvArgs a = conv_args(ops_[reader], 1, nullptr);
+  a.split_k = 1;
+  a.res = nullptr;
+  a.x2 = acts_.empty() ? (const void*)16 : acts_[d.in];
+  a.cin2 = convs_[d.conv].cin;
+  a.Kpad = L3.kpad + convs_[d.conv].kpad;
+  return conv1x1_supported(a) ? reader : -1;
+}
+
 // The stride-2 conv1 of a block whose downsample it computes (fuse_ds) on
 // the 56x56x64 -> 128 shape: conv3x3_s2rows runs one workgroup per image
 // (59 us at B=256 vs 72 us for the stream conv's 4 rounds of strips,
@@ -877,6 +947,7 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
         // block's conv1 (both read the block input; conv2 joins them through
         // the residual). Never next to a big-tile conv: its split-K slices
         // spin on each other and need their CUs.
+        if (ds_expand_op(oi) >= 0) break;  // computed by its expand conv (conv1x1 x2)
         if (opt_.fuse_ds && op.side && ds_fusable(oi, B)) {
           skip_ds = (int)oi;  // computed by the next op (the block's stride-2 conv1)
           break;
@@ -907,6 +978,26 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
             blaslt_->fc(acts_[op.in], L.cin, wa + L.w_off, L.kpad, (const float*)(wa + L.b_off),
                         (os.f32 && logits) ? (void*)logits : acts_[op.out], L.cout, os.f32, B, L.cout, L.cin, L.relu,
                         cs);
+            break;
+          }
+        }
+        if (L.cat_off && op.res >= 0) {
+          // expand conv + its stride-1 downsample as one K-concatenated GEMM
+          int ds_op = -1;
+          for (size_t i = 0; i < oi; ++i)
+            if (ops_[i].type == OpType::Conv && ops_[i].conv == L.cat_ds && ds_expand_op(i) == (int)oi) ds_op = (int)i;
+          if (ds_op >= 0) {
+            if (joined.count(op.res)) joined.erase(op.res);
+            ConvArgs a = conv_args(op, B, logits);
+            const ConvLayer& D = convs_[L.cat_ds];
+            a.split_k = 1;
+            a.res = nullptr;
+            a.x2 = acts_[ops_[ds_op].in];
+            a.cin2 = D.cin;
+            a.Kpad = L.kpad + D.kpad;
+            a.w = (const uint8_t*)warena_ + L.cat_off;
+            a.bias = (const float*)((const uint8_t*)warena_ + L.cat_b_off);
+            conv1x1(a, num_cus_, cs);
             break;
           }
         }

@@ -48,6 +48,10 @@ struct ConvLayer {
   bool fp8 = false;             // e4m3 weights (input activation is e4m3)
   size_t a_off = 0;             // fp8: alpha[n] = s_in * s_w[n] (fp32 [npad])
   size_t wf_off = 0;            // weights in stream-conv fragment order (0 = none)
+  // bottleneck expand conv with its stride-1 downsample folded in (conv1x1 x2):
+  // [cout][kpad + ds kpad] bf16 = [W3 | Wd] and bias b3 + bd (0 = none)
+  int cat_ds = -1;              // convs_ index of that downsample
+  size_t cat_off = 0, cat_b_off = 0;
 };
 
 struct Op {
@@ -74,6 +78,7 @@ struct EngineOptions {
   // resnet50_fp8 layer1 identity bottlenecks as one kernel (bottleneck56.hip): at parity with
   // the three-kernel path so far (248 vs 245 us per block), off by default
   bool fused_bottleneck = false;
+  bool ds_into_expand = true;    // ResNet50 layer1.0: the 1x1 downsample computed inside conv3 (one K-concat GEMM)
   bool stream_conv = true;       // direct 3x3 convs with the input resident in LDS (conv3x3_stream.hip)
   bool stream_wreg = true;       // ... with register-streamed weights where available
   bool stream_l4s2 = true;       // ... also for 14x14x256 -> 512 / s2 (register weights only)
@@ -178,6 +183,7 @@ class Engine {
   bool block_fusable(size_t oi, int B) const;  // ops oi, oi+1 = a layer1 basic block -> conv3x3_block
   bool bottleneck_fusable(size_t oi) const;    // ops oi..oi+2 = a layer1 identity bottleneck -> bottleneck56
   bool bottleneck_conv3(const ConvLayer& L) const;  // L is such a block's expand conv (fragment-order weights)
+  int ds_expand_op(size_t oi) const;  // ops[oi] = a downsample folded into a later expand conv: that op, or -1
   bool s2rows_ok(const Op& op, const ConvLayer& D, int B) const;  // layer2.0 conv1 + downsample -> conv3x3_s2rows
   bool fc_blaslt(const Op& op, int B) const;  // this fc op runs on hipBLASLt at batch B
   void prepare_fc(int B, float* logits, hipStream_t s);  // pick hipBLASLt algorithms (outside capture)

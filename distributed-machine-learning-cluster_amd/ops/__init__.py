@@ -266,8 +266,10 @@ def conv3x3_stream(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, 
     [B,14,14,256], [B,7,7,512]; stride 2: [B,56,56,64] -> 128 channels,
     [B,28,28,128] -> 256, [B,14,14,256] -> 512.
 
-    downsample=(wd_packed [Cout, Cin], bd): stride 2 only; also computes the
-    1x1/s2 conv + bias from the same resident input and returns (y, yd)."""
+    downsample=(wd_packed [Cout, Cin], bd[, wd_frag]): stride 2 only; also
+    computes the 1x1/s2 conv + bias from the same resident input and returns
+    (y, yd); wd_frag = stream_weight_frag(wd_packed), precomputed for graph
+    capture."""
     _need_cuda(x, w_packed, bias, res)
     C = native()
     B, H, W, Cin = x.shape
@@ -293,7 +295,9 @@ def conv3x3_stream(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, 
         if not C.conv3x3_stream_uses_frag(H, W, Cin, Cout, stride):
             raise ValueError("conv3x3_stream: no register-weight variant for this shape")
         wf = frag if isinstance(frag, torch.Tensor) else stream_weight_frag(w_packed)
-    wdf = stream_weight_frag(wd) if (wf is not None and wd is not None) else None
+    wdf = None
+    if wf is not None and wd is not None:
+        wdf = downsample[2] if len(downsample) > 2 else stream_weight_frag(wd)
     C.conv3x3_stream(_ptr(x.contiguous()), _ptr(w_packed.contiguous()), _ptr(bias.float().contiguous()),
                      _ptr(None if res is None else res.contiguous()), _ptr(y), _ptr(_zero_page(x.device)), B, H, W,
                      Cin, Cout, stride, relu, _stream(), stamps, _ptr(wd), _ptr(bd), _ptr(yd), _ptr(wf), _ptr(wdf))

@@ -396,6 +396,44 @@ def test_alexnet_direct13_matches_igemm(gpu, B):
         assert prof["features.3"] < rprof["features.3"], (prof, rprof)
 
 
+@pytest.mark.parametrize("arch", ["resnet50", "resnet50_fp8"])
+def test_resnet50_downsample_in_expand_matches_separate(gpu, arch):
+    """layer1.0's 1x1 downsample folded into its expand conv (one conv1x1
+    GEMM over K = [conv2 output | block input] with weights [W3 | Wd], bias
+    b3 + bd) vs the two convs + residual add (ds_into_expand off): the same
+    products, the residual no longer rounded to the activation dtype first, so
+    logits agree to that rounding; and the fused engine is the faster one on
+    layer1.0."""
+    model = build("resnet50", seed=63, randomize_bn=True)
+    sd = state_dict_f32(model)
+    g = torch.Generator().manual_seed(64)
+    img = torch.randint(0, 256, (64, 224, 224, 3), generator=g, dtype=torch.uint8)
+    x = img.to(gpu)
+    eng = InferenceEngine(arch, sd, max_batch=64)
+    ref_eng = InferenceEngine(arch, sd, max_batch=64, options={"ds_into_expand": False})
+    fi, _, fl = eng.predict(x, return_logits=True)
+    ri, _, rl = ref_eng.predict(x, return_logits=True)
+    torch.cuda.synchronize()
+    # both against fp32 (the fp8 engine's activation scales are calibrated with
+    # every activation materialised, whichever paths it runs), then each other
+    ref = _ref_logits(model, img[:16])
+    for lg in (fl, rl):
+        r = ((lg[:16].float().cpu() - ref).norm() / ref.norm()).item()
+        assert r < (0.15 if arch.endswith("fp8") else 3e-2), r
+    rel = ((fl - rl).norm() / rl.norm()).item()
+    assert rel < (5e-2 if arch.endswith("fp8") else 1e-2), rel
+    p = torch.softmax(rl.float().cpu(), -1)
+    top2 = p.topk(2, -1).values
+    near = (top2[:, 0] - top2[:, 1]) < 5e-2
+    assert torch.all((fi.cpu() == ri.cpu()) | near)
+    prof = dict(eng._e.profile(x.data_ptr(), 64, 224, 224, 0))
+    rprof = dict(ref_eng._e.profile(x.data_ptr(), 64, 224, 224, 0))
+    fused = prof["layer1.0.downsample.0"] + prof["layer1.0.conv3"]
+    sep = rprof["layer1.0.downsample.0"] + rprof["layer1.0.conv3"]
+    print(arch, "layer1.0 ds + conv3 (ms): fused", fused, "separate", sep)
+    assert fused < 0.8 * sep  # (the skipped downsample op profiles at the ~5 us empty-op floor)
+
+
 def test_resnet50_fp8_fused_bottleneck_matches_unfused(gpu):
     """resnet50_fp8's layer1 identity blocks (layer1.1, layer1.2) as one kernel
     each (bottleneck56.hip: conv1 e4m3 MFMA -> t1 in LDS -> conv2 -> t2 in LDS

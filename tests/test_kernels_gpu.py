@@ -375,6 +375,16 @@ def test_conv3x3_stream_fused_downsample(gpu, HW, Cin, B):
         y3 = ops.conv3x3_stream(xg, wp, bias.to(gpu), None, True, stride=2, frag=True)
         torch.cuda.synchronize()
         assert torch.equal(y2, y0) and torch.equal(yd2, yd) and torch.equal(y3, y0)
+        nat = dmlc.native()
+        for v in (2, 4):  # one / two channel groups per wave: same MFMA order per output
+            nat.conv3x3_stream_set_variant(v)
+            try:
+                y4, yd4 = ops.conv3x3_stream(xg, wp, bias.to(gpu), None, True, stride=2,
+                                             downsample=(wdp, bd.to(gpu)), frag=True)
+                torch.cuda.synchronize()
+            finally:
+                nat.conv3x3_stream_set_variant(0)
+            assert torch.equal(y4, y0) and torch.equal(yd4, yd)
 
 
 @pytest.mark.parametrize("B,strip,res", [(2, None, False), (2, None, True), (3, 4, True), (1, 8, False),

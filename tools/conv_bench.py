@@ -37,6 +37,20 @@ RESNET18 = [
 REP = 10
 
 
+def warm_gpu(seconds=1.0):
+    """Run bf16 GEMMs for ~seconds first: measurements taken right after start
+    caught the clocks still ramping (the first variant timed read ~10-15%
+    slow, whichever it was)."""
+    import time
+    a = torch.randn(8192, 8192, device="cuda").bfloat16()
+    torch.cuda.synchronize()
+    t0 = time.time()
+    while time.time() - t0 < seconds:
+        for _ in range(20):
+            a @ a
+        torch.cuda.synchronize()
+
+
 def time_us(f, iters):
     """Median per-launch time (us) of f() replayed from a captured graph."""
     f()  # allocate workspaces / warm up outside the capture
@@ -91,6 +105,7 @@ def main():
     dev = torch.device("cuda", 0)
     B = a.batch
     tiles = [int(t) for t in a.tiles.split(",")]
+    warm_gpu()
     for name, H, W, Cin, Cout, k, s, p, pair in RESNET18:
         if a.only and name not in a.only.split(","):
             continue
@@ -120,7 +135,7 @@ def main():
                     row.append(_stamps())
             except Exception as e:  # noqa: BLE001
                 row.append(f"tile{t}=ERR({e})")
-        if name in ("l2", "l3", "l4", "l2.c1", "l3.c1"):  # direct conv, streamed weights (conv3x3_stream.hip)
+        if name in ("l2", "l3", "l4", "l2.c1", "l3.c1", "l4.c1"):  # direct conv, streamed weights (conv3x3_stream.hip)
             for use_res in (False, True) if s == 1 else (False,):
                 r = torch.randn(B, H, W, Cout, device=dev).bfloat16() if use_res else None
                 f = lambda: ops.conv3x3_stream(x, wp, bias, r, True, stride=s)
@@ -131,6 +146,24 @@ def main():
                     row.append(_stamps())
                 # register-weight kernels (fragment-order weights), per A/B variant
                 nat = dmlc.native()
+                if nat.conv3x3_stream_uses_frag(H, W, Cin, Cout, s) and s == 2:
+                    # stride 2 as the engine runs it: with the fused downsample
+                    wdp = ops.pack_conv_weight(torch.randn(Cout, Cin, 1, 1) / Cin ** 0.5, device=dev)
+                    ds = (wdp, bias, ops.stream_weight_frag(wdp, Cout))
+                    wf = ops.stream_weight_frag(wp, Cout)
+                    for v in [int(t) for t in a.variants.split(",")]:
+                        nat.conv3x3_stream_set_variant(v)
+                        try:
+                            f = lambda: ops.conv3x3_stream(x, wp, bias, None, True, stride=2, downsample=ds, frag=wf)
+                            us = time_us(f, a.iters)
+                            row.append(f"wr{v}+ds={us:7.1f}us {flops/us/1e6:6.0f}TF")
+                            if ops.BT_STAMPS is not None:
+                                f()
+                                row.append(_stamps())
+                        except Exception as e:  # noqa: BLE001
+                            row.append(f"wr{v}=ERR({e})")
+                        finally:
+                            nat.conv3x3_stream_set_variant(0)
                 if nat.conv3x3_stream_uses_frag(H, W, Cin, Cout, s) and s == 1:
                     for v in [int(t) for t in a.variants.split(",")]:
                         nat.conv3x3_stream_set_variant(v)
@@ -139,6 +172,9 @@ def main():
                             f = lambda: ops.conv3x3_stream(x, wp, bias, r, True, stride=s, frag=wf)
                             us = time_us(f, a.iters)
                             row.append(f"wr{v}{'+res' if use_res else ''}={us:7.1f}us {flops/us/1e6:6.0f}TF")
+                            if ops.BT_STAMPS is not None:
+                                f()
+                                row.append(_stamps())
                         except Exception as e:  # noqa: BLE001
                             row.append(f"wr{v}=ERR({e})")
                         finally:
