@@ -187,6 +187,7 @@ PYBIND11_MODULE(_C, m) {
       py::arg("Wr"), py::arg("stream"), py::arg("paired") = false);
   m.attr("STEM_POOL_K") = kStemPoolK;
   m.def("stem_pool_pick_strip", &stem_pool_pick_strip);
+  m.def("stem_pool_u8_pick_strip", &stem_pool_u8_pick_strip);
   m.def("conv3x3_stream_supported", &conv3x3_stream_supported, py::arg("Hin"), py::arg("Win"), py::arg("Cin"),
         py::arg("Cout"), py::arg("stride") = 1);
   m.def("conv3x3_stream", [](uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t res, uintptr_t y, uintptr_t zero,

@@ -225,10 +225,10 @@ __global__ __launch_bounds__(512, 1) void alex_stem_kernel(AlexStemArgs a) {
           float v[8];
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            v[e] = fmaxf(acc[0][e] + bs[e], 0.f);
-            v[4 + e] = fmaxf(acc[1][e] + bs[4 + e], 0.f);
+            v[e] = acc[0][e] + bs[e];
+            v[4 + e] = acc[1][e] + bs[4 + e];
           }
-          *(uint4*)(conv + (oh & (kConvRing - 1)) * kConvB + conv_off(ow, ch0 / 8 + fq)) = pack8(v);
+          *(uint4*)(conv + (oh & (kConvRing - 1)) * kConvB + conv_off(ow, ch0 / 8 + fq)) = relu_bf16x8(pack8(v));
         }
       }
     }

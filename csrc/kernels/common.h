@@ -48,6 +48,21 @@ __device__ __forceinline__ uint4 pack8(const float* f) {
   return make_uint4(pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]), pack2(f[6], f[7]));
 }
 
+// ReLU on 8 packed bf16: max with 0 as int16 (negative bf16 bit patterns are
+// negative int16; -0 becomes +0), 4 v_pk_max_i16. Rounding is monotone and
+// keeps the sign, so relu-after-rounding equals rounding-after-fmaxf bit for
+// bit, at a quarter of the VALU: fmaxf(v, 0) compiles to two v_max_f32 per
+// value (a NaN-canonicalising max first), 16 per 8 channels.
+__device__ __forceinline__ uint4 relu_bf16x8(uint4 u) {
+  typedef short short8v __attribute__((ext_vector_type(8)));
+  const short8v z = {0, 0, 0, 0, 0, 0, 0, 0};
+  return __builtin_bit_cast(uint4, __builtin_elementwise_max(__builtin_bit_cast(short8v, u), z));
+}
+__device__ __forceinline__ uint4 pack8_relu(const float* f, bool relu) {
+  const uint4 p = pack8(f);
+  return relu ? relu_bf16x8(p) : p;
+}
+
 // 16-B-per-lane LDS-DMA (global_load_lds_dwordx4: lane l's 16 bytes land at
 // lds + 16 l; lds must be wave-uniform), issued as inline asm. With
 // __builtin_amdgcn_global_load_lds in flight the compiler's waitcnt pass

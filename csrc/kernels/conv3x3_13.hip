@@ -201,8 +201,8 @@ __global__ __launch_bounds__(256, 1) void conv3x3_13_kernel(D13Args a) {
             if (p < kNPix) {
               float v[8];
 #pragma unroll
-              for (int e = 0; e < 8; ++e) v[e] = fmaxf(acc[f][2 * j + (e >> 2)][e & 3] + bs[e], 0.f);
-              *(uint4*)(tile + p * TB + (((4 * j + g) ^ (p & (4 * GPP - 1))) << 4)) = pack8(v);
+              for (int e = 0; e < 8; ++e) v[e] = acc[f][2 * j + (e >> 2)][e & 3] + bs[e];
+              *(uint4*)(tile + p * TB + (((4 * j + g) ^ (p & (4 * GPP - 1))) << 4)) = relu_bf16x8(pack8(v));
             }
           }
         }
@@ -244,9 +244,8 @@ __global__ __launch_bounds__(256, 1) void conv3x3_13_kernel(D13Args a) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
             v[e] = acc[f][2 * j + (e >> 2)][e & 3] + bs[e];
-            if (a.relu) v[e] = fmaxf(v[e], 0.f);
           }
-          *(uint4*)(yim + (long)p * CO + ch) = pack8(v);
+          *(uint4*)(yim + (long)p * CO + ch) = pack8_relu(v, a.relu);
         }
       }
     }

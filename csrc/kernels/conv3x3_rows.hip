@@ -240,11 +240,7 @@ __global__ __launch_bounds__(256, WR ? 2 : 1) void conv3x3_rows_kernel(RowConvAr
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] += r[e];
       }
-      if (a.relu) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
-      }
-      *(uint4*)(a.y + off) = pack8(v);
+      *(uint4*)(a.y + off) = pack8_relu(v, a.relu);
     }
     // The next step's rows have landed: vmcnt retires in issue order, so the
     // MF younger stores may stay in flight.

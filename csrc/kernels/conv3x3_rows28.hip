@@ -32,6 +32,8 @@
 #include "common.h"
 #include "kernels.h"
 
+#include <type_traits>
+
 namespace dmlc {
 
 namespace {
@@ -87,8 +89,15 @@ __device__ __forceinline__ void vm_wait_plus(int n) {
 
 // DBG (experiments): bit 0 no row DMA in the loop, bit 1 no LDS reads in the
 // K loop, bit 2 no epilogue, bit 3 prologue only
-template <bool RES, int DBG = 0, int AH = 1>
-__global__ __launch_bounds__(256, 1) void conv3x3_rows28_kernel(R28Args a) {
+// NW: 4 waves (one per SIMD) x 32 output channels, 288 weight registers per
+// wave (their AGPR / VGPR split costs ~0.6 register moves per MFMA), or 8
+// waves (two per SIMD) x 16 channels, 144 weight registers, every X fragment
+// read feeding one MFMA instead of two.
+template <bool RES, int DBG = 0, int AH = 1, int NW = 4>
+__global__ __launch_bounds__(64 * NW, 1) void conv3x3_rows28_kernel(R28Args a) {
+  static_assert(NW == 4 || NW == 8, "4 or 8 waves");
+  constexpr int NF = NW == 4 ? 2 : 1;  // N fragments (16 channels) per wave
+  constexpr int NT = 64 * NW;
   constexpr int kRing = R28Ring<AH>::kRing, kSlotsAlloc = R28Ring<AH>::kSlotsAlloc;
   static_assert(AH == 1 || AH == 2, "rows DMA'd one or two steps ahead");
   extern __shared__ __attribute__((aligned(16))) uint4 smem[];
@@ -100,24 +109,25 @@ __global__ __launch_bounds__(256, 1) void conv3x3_rows28_kernel(R28Args a) {
   const int b = blockIdx.x;
   const bf16* img = a.x + (long)b * kH * kW * kC;
 
-  for (int o = tid * 16; o < kSlotsAlloc * kRB; o += 256 * 16) *(uint4*)(ring + o) = make_uint4(0, 0, 0, 0);
+  for (int o = tid * 16; o < kSlotsAlloc * kRB; o += NT * 16) *(uint4*)(ring + o) = make_uint4(0, 0, 0, 0);
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   // input row yy -> ring slot (yy + 1) % kRing (+ guard slot kRing / kRing+1
-  // for slots 0 / 1); wave w stages quarter plane w: chunks 0..63 and
-  // 64..111 of its run. Row 28 (below the image) reuses a slot: its run is
+  // for slots 0 / 1); wave w stages quarter plane w & 3: chunks 0..63 and
+  // 64..111 of its run (NW = 8: wave w the half w >> 2). Row 28 (below the image) reuses a slot: its run is
   // written as zeros. row_dmas(yy) = the DMA instructions load_row(yy) issues
   // (wave-uniform; the vmcnt waits below count them).
+  const int qp = wave & 3;  // the quarter plane this wave stages
   auto load_row = [&](int yy) __attribute__((always_inline)) {
     const int slot = (yy + 1) % kRing;
-    char* dst = ring + wave * kPlane + 64;
+    char* dst = ring + qp * kPlane + 64;
 #pragma unroll
-    for (int i0 = 0; i0 < kRun; i0 += 64) {
+    for (int i0 = NW == 8 ? 64 * (wave >> 2) : 0; i0 < kRun; i0 += 64 * (NW / 4)) {
       const int k = i0 + lane;
       const int x = k >> 2, c = k & 3;
       if (k < kRun) {
         if (yy < kH) {
-          const bf16* src = img + ((long)((DBG & 32) ? 0 : yy) * kW + x) * kC + 32 * wave + 8 * (c ^ swz_of(yy, x));
+          const bf16* src = img + ((long)((DBG & 32) ? 0 : yy) * kW + x) * kC + 32 * qp + 8 * (c ^ swz_of(yy, x));
           dma16(src, dst + slot * kRB + i0 * 16);
           if (slot < 2) dma16(src, dst + (slot + kRing) * kRB + i0 * 16);
         } else {
@@ -128,15 +138,18 @@ __global__ __launch_bounds__(256, 1) void conv3x3_rows28_kernel(R28Args a) {
     }
   };
   auto row_dmas = [&](int yy) __attribute__((always_inline)) {
-    return yy < kH ? ((yy + 1) % kRing < 2 ? 4 : 2) : 0;
+    return yy < kH ? ((yy + 1) % kRing < 2 ? 2 : 1) * (NW == 4 ? 2 : 1) : 0;
   };
   // this lane's 8 output channels ch0 + 8g .. +7 (weight rows permuted,
-  // perm32); loaded before the row DMAs so the prologue wait below can leave
-  // exactly the weight loads in flight
-  const int ch0 = wave * 32;
-  float bs[8];
+  // perm32; NW = 8: the 4 channels ch0 + 8g + 4 nf0 .. +3 of fragment nf0 of
+  // 32-channel group wave / 2); loaded before the row DMAs so the prologue
+  // wait below can leave exactly the weight loads in flight
+  const int cg = NW == 4 ? wave : wave >> 1, nf0 = NW == 4 ? 0 : wave & 1;
+  const int ch0 = cg * 32;
+  constexpr int CPL = 4 * NF;  // output channels per lane
+  float bs[CPL];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) bs[e] = a.bias[ch0 + 8 * g + e];
+  for (int e = 0; e < CPL; ++e) bs[e] = a.bias[ch0 + 8 * g + 4 * nf0 + e];
   for (int yy = 0; yy <= 4; ++yy) load_row(yy);
 
   // ---- per-lane constants: fragment f = tile pixels p = 16 f + fr (row
@@ -154,12 +167,12 @@ __global__ __launch_bounds__(256, 1) void conv3x3_rows28_kernel(R28Args a) {
       col[f][kw] = (c + kw) * 64 + ((g ^ s) << 4);
     }
   }
-  bf16x8 w[kKS][2];
+  bf16x8 w[kKS][NF];
 #pragma unroll
   for (int t = 0; t < kKS; ++t)
 #pragma unroll
-    for (int nf = 0; nf < 2; ++nf)
-      w[t][nf] = *(const bf16x8*)(a.wf + ((((long)wave * kKS + t) * 2 + nf) * 64 + lane) * 8);
+    for (int nf = 0; nf < NF; ++nf)
+      w[t][nf] = *(const bf16x8*)(a.wf + ((((long)cg * kKS + t) * 2 + nf + nf0) * 64 + lane) * 8);
   // the prologue rows (DMA'd before the weights) have landed; the weights
   // (72 loads, 288 KB per workgroup from L2) may still be in flight: the
   // first step's MFMAs wait for each K step's own fragments (the compiler's
@@ -177,14 +190,17 @@ __global__ __launch_bounds__(256, 1) void conv3x3_rows28_kernel(R28Args a) {
     // loop; registers are full of weights): 16-B chunk c of pixel p at
     // physical chunk c ^ (p & 15), so the epilogue's reads are conflict free.
     // Issued before this step's row DMAs: its wait leaves those in flight.
-    const long obase = ((long)b * kH + r0) * kW * kC + ch0 + 8 * g;
+    const long obase = ((long)b * kH + r0) * kW * kC + ch0 + 8 * g + 4 * nf0;
     if constexpr (RES) {
       const bf16* rimg = a.res + ((long)b * kH + r0) * kW * kC;
 #pragma unroll
-      for (int j = 0; j < kResCh / 256; ++j) {
-        const int i = j * 256 + wave * 64 + lane;
-        const int p = i >> 4, c = i & 15;
-        dma16(rimg + (long)p * kC + 8 * (c ^ (p & 15)), resbuf + (j * 256 + wave * 64) * 16);
+      for (int j = 0; j < (kResCh + NT - 1) / NT; ++j) {
+        const int i0 = j * NT + wave * 64;
+        if (i0 < kResCh) {  // (wave-uniform: kResCh is a multiple of 64)
+          const int i = i0 + lane;
+          const int p = i >> 4, c = i & 15;
+          dma16(rimg + (long)p * kC + 8 * (c ^ (p & 15)), resbuf + i0 * 16);
+        }
       }
     }
     // rows of step + AH (step 0 also issues those of steps 1 .. AH - 1)
@@ -205,11 +221,6 @@ __global__ __launch_bounds__(256, 1) void conv3x3_rows28_kernel(R28Args a) {
       sl = sl >= kRing ? sl - kRing : sl;
       rowoff[f] = sl * kRB;
     }
-    floatx4 acc[kMF][2];
-#pragma unroll
-    for (int f = 0; f < kMF; ++f)
-#pragma unroll
-      for (int nf = 0; nf < 2; ++nf) acc[f][nf] = floatx4{0.f, 0.f, 0.f, 0.f};
     // K step t: tap = t >> 2 (kh = tap / 3, kw = tap % 3), quarter q = t & 3
     // tb[f]: fragment f's address for the current tap (quarter 0, kernel row
     // 0's slot; kh and the quarter are immediates). Computed by volatile asm
@@ -228,47 +239,75 @@ __global__ __launch_bounds__(256, 1) void conv3x3_rows28_kernel(R28Args a) {
       if (q == 0) tap_addr(tap, f);
       return *(const bf16x8*)(ring + tb[f] + (tap / 3) * kRB + q * kPlane);
     };
-    bf16x8 xc[kMF];
+    // fragments [FB, FE) of the step: the K loop, then their epilogue (NW = 8
+    // runs the step as two such passes: half the accumulator and operand
+    // registers, the weights reused)
+    auto pass = [&](auto fb_, auto fe_) __attribute__((always_inline)) {
+      constexpr int FB = decltype(fb_)::value, FE = decltype(fe_)::value, PF = FE - FB;
+      floatx4 acc[PF][NF];
 #pragma unroll
-    for (int f = 0; f < kMF; ++f) xc[f] = xread(0, f);
+      for (int f = 0; f < PF; ++f)
 #pragma unroll
-    for (int t = 0; t < kKS; ++t) {
+        for (int nf = 0; nf < NF; ++nf) acc[f][nf] = floatx4{0.f, 0.f, 0.f, 0.f};
+      bf16x8 xc[PF];
 #pragma unroll
-      for (int f = 0; f < kMF; ++f) {
-        __builtin_amdgcn_sched_barrier(0);
+      for (int f = 0; f < PF; ++f) xc[f] = xread(0, FB + f);
 #pragma unroll
-        for (int nf = 0; nf < 2; ++nf)
-          acc[f][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[t][nf], xc[f], acc[f][nf], 0, 0, 0);
-        if (t + 1 < kKS && !(DBG & 2)) xc[f] = xread(t + 1, f);
+      for (int t = 0; t < kKS; ++t) {
+#pragma unroll
+        for (int f = 0; f < PF; ++f) {
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int nf = 0; nf < NF; ++nf)
+            acc[f][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[t][nf], xc[f], acc[f][nf], 0, 0, 0);
+          if (t + 1 < kKS && !(DBG & 2)) xc[f] = xread(t + 1, FB + f);
+        }
       }
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr (RES) {  // this wave's residual DMAs (older than this step's row DMAs) have landed; and everyone's
-      if (AH == 1 || step == 0)
-        vm_wait<0>();
-      else
-        vm_wait_plus<0>(ndma);
-      __builtin_amdgcn_s_barrier();
-    }
-    // ---- epilogue: lane holds channels ch0 + 8g .. +7 of tile pixel 16 f + fr
-#pragma unroll
-    for (int f = 0; f < ((DBG & 4) ? 0 : kMF); ++f) {
-      float v[8];
-#pragma unroll
-      for (int nf = 0; nf < 2; ++nf)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) v[4 * nf + i] = acc[f][nf][i] + bs[4 * nf + i];
-      if constexpr (RES) {
-        float r[8];
-        unpack8(*(const uint4*)(resbuf + (16 * f + fr) * 256 + (((4 * wave + g) ^ fr) << 4)), r);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] += r[e];
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (RES && FB == 0) {  // this wave's residual DMAs (older than this step's row DMAs) have landed; and everyone's
+        if (AH == 1 || step == 0)
+          vm_wait<0>();
+        else
+          vm_wait_plus<0>(ndma);
+        __builtin_amdgcn_s_barrier();
       }
-      if (a.relu) {
+      // ---- epilogue: lane holds channels ch0 + 8g .. +7 of tile pixel 16 f + fr
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+      for (int f = 0; f < ((DBG & 4) ? 0 : PF); ++f) {
+        const int ff = FB + f;
+        float v[8];
+#pragma unroll
+        for (int nf = 0; nf < NF; ++nf)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[4 * nf + i] = acc[f][nf][i] + bs[4 * nf + i];
+        const char* rp = resbuf + (16 * ff + fr) * 256 + (((4 * cg + g) ^ fr) << 4);
+        if constexpr (NW == 4) {
+          if constexpr (RES) {
+            float r[8];
+            unpack8(*(const uint4*)rp, r);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] += r[e];
+          }
+          *(uint4*)(a.y + obase + (long)(16 * ff + fr) * kC) = pack8_relu(v, a.relu);
+        } else {
+          if constexpr (RES) {
+            const uint2 rr = *(const uint2*)(rp + 8 * nf0);
+            float r[8];
+            unpack8(make_uint4(rr.x, rr.y, 0u, 0u), r);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] += r[e];
+          }
+          v[4] = v[5] = v[6] = v[7] = 0.f;
+          const uint4 pk = pack8_relu(v, a.relu);
+          *(uint2*)(a.y + obase + (long)(16 * ff + fr) * kC) = make_uint2(pk.x, pk.y);
+        }
       }
-      *(uint4*)(a.y + obase + (long)(16 * f + fr) * kC) = pack8(v);
+    };
+    if constexpr (NW == 4) {
+      pass(std::integral_constant<int, 0>{}, std::integral_constant<int, kMF>{});
+    } else {
+      pass(std::integral_constant<int, 0>{}, std::integral_constant<int, 4>{});
+      pass(std::integral_constant<int, 4>{}, std::integral_constant<int, kMF>{});
     }
     // the next step's rows have landed and every wave is done with the rows
     // they replace. vmcnt retires in order; younger than those rows: AH = 1
@@ -318,6 +357,8 @@ void conv3x3_rows28(const void* x, const void* wf, const float* bias, const void
   switch (dbg) {
     case 64: hipLaunchKernelGGL((conv3x3_rows28_kernel<false, 0, 2>), dim3(B), dim3(256), lds, s, a); break;
     case 65: hipLaunchKernelGGL((conv3x3_rows28_kernel<true, 0, 2>), dim3(B), dim3(256), lds, s, a); break;
+    case 128: hipLaunchKernelGGL((conv3x3_rows28_kernel<false, 0, 1, 8>), dim3(B), dim3(512), lds, s, a); break;
+    case 129: hipLaunchKernelGGL((conv3x3_rows28_kernel<true, 0, 1, 8>), dim3(B), dim3(512), lds, s, a); break;
     case 1: hipLaunchKernelGGL((conv3x3_rows28_kernel<false, 1>), dim3(B), dim3(256), lds, s, a); break;
     case 2: hipLaunchKernelGGL((conv3x3_rows28_kernel<false, 2>), dim3(B), dim3(256), lds, s, a); break;
     case 4: hipLaunchKernelGGL((conv3x3_rows28_kernel<false, 4>), dim3(B), dim3(256), lds, s, a); break;

@@ -211,12 +211,8 @@ __global__ __launch_bounds__(256, 1) void conv3x3_s2rows_kernel(S2Args a) {
           v[4 * nf + i] = acc[f][nf][i] + bs[4 * nf + i];
           vd[4 * nf + i] = accd[f][nf][i] + bsd[4 * nf + i];
         }
-      if (a.relu) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
-      }
       if (!(a.dbg & 2)) {
-        *(uint4*)(a.y + o) = pack8(v);
+        *(uint4*)(a.y + o) = pack8_relu(v, a.relu);
         *(uint4*)(a.yd + o) = pack8(vd);
       }
     }

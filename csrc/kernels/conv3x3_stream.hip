@@ -489,11 +489,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream_kernel(StreamConvArgs a
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] += r[e];
       }
-      if (relu) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
-      }
-      const uint4 packed = pack8(v);
+      const uint4 packed = pack8_relu(v, relu);
       if (a.store_y) *(uint4*)(a.y + off) = packed;
       if constexpr (POOLABLE) {
         if (a.pool) {  // the bf16 activation's values, as the unfused avgpool reads them

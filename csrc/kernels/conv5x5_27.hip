@@ -191,8 +191,8 @@ __global__ __launch_bounds__(512, 1) void conv5x5_27_kernel(D27Args a) {
           if (p < kNPix) {
             float v[8];
 #pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] = fmaxf(acc[f][2 * j + (e >> 2)][e & 3] + bs[e], 0.f);
-            *(uint4*)(tile + p * 64 + ((g ^ (p & 3)) << 4)) = pack8(v);
+            for (int e = 0; e < 8; ++e) v[e] = acc[f][2 * j + (e >> 2)][e & 3] + bs[e];
+            *(uint4*)(tile + p * 64 + ((g ^ (p & 3)) << 4)) = relu_bf16x8(pack8(v));
           }
         }
         __syncthreads();
@@ -228,8 +228,8 @@ __global__ __launch_bounds__(512, 1) void conv5x5_27_kernel(D27Args a) {
         if (p < kNPix) {
           float v[8];
 #pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = fmaxf(acc[f][2 * j + (e >> 2)][e & 3] + bs[e], 0.f);
-          *(uint4*)(yim + (long)p * kCO + ch) = pack8(v);
+          for (int e = 0; e < 8; ++e) v[e] = acc[f][2 * j + (e >> 2)][e & 3] + bs[e];
+          *(uint4*)(yim + (long)p * kCO + ch) = relu_bf16x8(pack8(v));
         }
       }
     }

@@ -406,11 +406,7 @@ __global__ __launch_bounds__(512, 1) void conv_bt_kernel(ConvArgs a, int k_tiles
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] += r[e];
       }
-      if (a.relu) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
-      }
-      const uint4 pv = pack8(v);
+      const uint4 pv = pack8_relu(v, a.relu);
       if (dbg & 16)
         asm volatile("" ::"v"(pv.x), "v"(pv.y), "v"(pv.z), "v"(pv.w));
       else
@@ -624,11 +620,7 @@ __global__ __launch_bounds__(512, 1) void conv_btp_kernel(ConvArgs a, int k_tile
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] += r[e];
         }
-        if (a.relu) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
-        }
-        *(uint4*)((bf16*)a.y + o) = pack8(v);
+        *(uint4*)((bf16*)a.y + o) = pack8_relu(v, a.relu);
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next pass overwrites
     }

@@ -226,6 +226,9 @@ inline size_t stream_frag_index(int n, int k, int K) {
   return ((((size_t)g * (K / 32) + t) * 2 + nf) * 64 + lane) * 8 + e;
 }
 int stem_pool_pick_strip(int B, int PH, int num_cus);
+// u8 images in: strip = PH (one workgroup per image, role-split waves) when
+// B >= num_cus, else stem_pool_pick_strip
+int stem_pool_u8_pick_strip(int B, int PH, int num_cus);
 void stem_conv_pool(const void* x, const void* w, const float* bias, void* y, int B, int S, int Wq, int strip,
                     hipStream_t s);
 // Same stem with the preprocess fused: u8 HWC SxS images [B, S, S, 3] in

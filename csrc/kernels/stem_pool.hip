@@ -392,7 +392,245 @@ __global__ __launch_bounds__(256, 2) void stem_conv_pool_kernel(
   }
 }
 
+
+// ---- Role-split stem (one workgroup per image, B >= the CU count): the same
+// arithmetic as stem_conv_pool_kernel<NF, true>, but the VALU phase no longer
+// stalls the matrix pipes. In the strip kernel every step is [MFMA +
+// horizontal pool] | barrier | [vertical max + stores + u8 conversion] |
+// barrier, and the VALU phase (~30% of the kernel by knock-outs,
+// profiles/r3_stem_knockouts.txt) runs with the matrix pipes idle. Here 8
+// waves: waves 0-3 (one per SIMD) only compute conv rows and their
+// horizontal max into the hp ring; waves 4-7 (their SIMD partners) DMA raw
+// rows, convert them for the next step and do the vertical max and stores of
+// the previous step. One barrier per step:
+//   step t (0..T+1, T = PH/2 steps of 4 conv rows):
+//     MFMA waves (t <= T): conv rows 4t-4 .. 4t-1 (t = 0: only the zero row -1)
+//       from paired rows 8t-8 .. 8t+4 -> hp rows;
+//     helper waves: raw rows 8t+21 .. 8t+28 DMA'd (converted at t+2), pooled
+//       rows 2(t-2), 2(t-2)+1 = max of hp rows 4t-9 .. 4t-5 (t >= 2) -> y,
+//       paired rows 8t+5 .. 8t+12 converted (read by step t+1; t < T); then
+//       each waits for its DMAs of step t-1 only (the stores and this step's
+//       DMAs stay in flight).
+// Rings: paired 21 rows (13 read + 8 written), hp 9 rows (4 written + 5
+// read), raw 24 rows (8 converted + 16 in flight): 130 KB at 224x224.
+constexpr int kRolesPairRing = 21, kRolesHpRing = 9, kRolesRawRing = 24;
+
+// s_waitcnt vmcnt(n) for a wave-uniform runtime n (n > 15 waits for 15)
+__device__ __forceinline__ void vm_wait_dyn(int n) {
+  switch (n) {
+#define DMLC_VMW(N) \
+  case N: vm_wait<N>(); break;
+    DMLC_VMW(1) DMLC_VMW(2) DMLC_VMW(3) DMLC_VMW(4) DMLC_VMW(5) DMLC_VMW(6) DMLC_VMW(7) DMLC_VMW(8) DMLC_VMW(9)
+    DMLC_VMW(10) DMLC_VMW(11) DMLC_VMW(12) DMLC_VMW(13) DMLC_VMW(14)
+#undef DMLC_VMW
+    case 0: vm_wait<0>(); break;
+    default: vm_wait<15>(); break;
+  }
+}
+
+template <int NF>
+__global__ __launch_bounds__(512, 1) void stem_roles_kernel(StemArgs a) {
+  using G = StemGeom<NF>;
+  extern __shared__ __attribute__((aligned(16))) uint4 smem[];
+  constexpr int RB = G::Wq * 16;      // bytes per paired row
+  constexpr int UB = G::S * 3;        // bytes per raw image row
+  constexpr int UBS = UB + kU8Pad;    // raw ring slot
+  constexpr int HPB = G::PW * kHpCol;  // bytes per horizontally pooled conv row
+  constexpr int T = G::PH / 2;
+  char* ring = (char*)smem;
+  char* hp = ring + kRolesPairRing * RB;
+  char* u8ring = hp + kRolesHpRing * HPB;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool mfma_wave = wave < 4;
+  const int hw = wave & 3, htid = tid & 255;  // helper wave / thread index among the helpers
+  const int fr = lane & 15, fq = lane >> 4;
+  const int b = blockIdx.x;
+  const uint8_t* uimg = a.u8 + (long)b * G::S * G::S * 3;
+
+  // raw padded rows [lo, lo+cnt) (image row = padded row - 3) -> raw ring, by the helpers
+  auto load_rows = [&](int lo, int cnt) __attribute__((always_inline)) {
+    for (int i = hw; i < cnt; i += 4) {
+      const int r = lo + i, iy = r - 3;
+      if (iy < 0 || iy >= G::S) continue;
+      const uint8_t* src = uimg + (long)iy * UB;
+      char* dst = u8ring + (r % kRolesRawRing) * UBS + kU8Front;
+      for (int c0 = 0; c0 < UB / 4; c0 += 64)
+        if (c0 + lane < UB / 4) dma4(src + (c0 + lane) * 4, dst + c0 * 4);
+    }
+  };
+  // raw rows [lo, lo+cnt) -> paired bf16 rows (stem_conv_pool_kernel's
+  // convert_rows, over nthr threads)
+  auto convert_rows = [&](int lo, int cnt, int t0, int nthr) __attribute__((always_inline)) {
+    const int G4 = (G::Wq + 3) / 4;
+    const int items = cnt * G4;
+    for (int it = t0; it < items; it += nthr) {
+      const int r = lo + it / G4;
+      const int k = it - (it / G4) * G4;
+      if (r < 0) continue;
+      const int iy = r - 3;
+      const bool row_in = iy >= 0 && iy < G::S;
+      const char* srow = u8ring + (r % kRolesRawRing) * UBS + kU8Front;
+      const int A = 24 * k - 12;
+      uint32_t d[7];
+#pragma unroll
+      for (int j = 0; j < 7; ++j) d[j] = row_in ? *(const uint32_t*)(srow + A + 4 * j) : 0u;
+      float v[32];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int ix = 8 * k - 3 + i;
+        const bool in = row_in && ix >= 0 && ix < G::S;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          const int idx = 3 + 3 * i + c;
+          const float cv = (float)((d[idx >> 2] >> (8 * (idx & 3))) & 0xffu);
+          const float nv = imagenet_norm(c, cv);
+          v[8 * (i >> 1) + 3 * (i & 1) + c] = in ? nv : 0.f;
+        }
+      }
+      char* drow = ring + (r % kRolesPairRing) * RB;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        v[8 * q + 6] = v[8 * q + 7] = 0.f;
+        if (4 * k + q < G::Wq) *(uint4*)(drow + (4 * k + q) * 16) = pack8(v + 8 * q);
+      }
+    }
+  };
+
+  bf16x8 wf[4][7];
+  float bs[4];
+  if (mfma_wave) {
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+      for (int s = 0; s < 7; ++s) wf[n][s] = *(const bf16x8*)(a.w + (n * 16 + fr) * kK + s * 32 + fq * 8);
+#pragma unroll
+    for (int n = 0; n < 4; ++n) bs[n] = a.bias[n * 16 + fr];
+  }
+  // raw ring pads stay zero; prologue: raw rows 0..20 (converted before step
+  // 0 and at steps 0, 1), rows 0..4 converted by everyone (step 0 reads
+  // paired rows -8..4)
+  for (int o = tid * 16; o < kRolesRawRing * UBS; o += 512 * 16) *(uint4*)(u8ring + o) = make_uint4(0, 0, 0, 0);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if (!mfma_wave) load_rows(0, 21);
+  vm_wait<0>();
+  __builtin_amdgcn_s_barrier();
+  convert_rows(0, 5, tid, 512);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+
+  for (int t = 0; t <= T + 1; ++t) {
+    if (mfma_wave) {
+      if (t <= T) {
+        const int c0 = 4 * t - 4;
+        const int cr = c0 + wave;
+        char* hrow = hp + ((cr + kRolesHpRing) % kRolesHpRing) * HPB;
+        if (cr < 0) {
+          if (wave == 3)
+            for (int o = lane * 16; o < HPB; o += 64 * 16) *(uint4*)(hrow + o) = make_uint4(0, 0, 0, 0);
+        } else {
+          const char* rbase = ring + (fr + fq) * 16;
+          int rows[7];
+#pragma unroll
+          for (int s = 0; s < 7; ++s) rows[s] = ((2 * cr + s) % kRolesPairRing) * RB;
+          const uint32_t hbase = lds_addr(hrow) + fq * 2 * kHpCol + (fr >> 3) * 16 + (fr & 7) * 2;
+          float prev3[4];
+          bf16x8 xf[7];
+#pragma unroll
+          for (int s = 0; s < 7; ++s) xf[s] = *(const bf16x8*)(rbase + rows[s]);
+#pragma unroll
+          for (int f = 0; f < NF; ++f) {
+            floatx4 acc[4];
+#pragma unroll
+            for (int n = 0; n < 4; ++n) acc[n] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < 7; ++s)
+#pragma unroll
+              for (int n = 0; n < 4; ++n)
+                acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[s], wf[n][s], acc[n], 0, 0, 0);
+            if (f + 1 < NF) {
+#pragma unroll
+              for (int s = 0; s < 7; ++s) xf[s] = *(const bf16x8*)(rbase + rows[s] + (f + 1) * 256);
+            }
+#pragma unroll
+            for (int n = 0; n < 4; ++n) {
+              const floatx4 v = acc[n];
+              const float src = (f > 0 && fq == 3) ? prev3[n] : v[3];
+              float nb = rot_rows_down1(src, lane);
+              if (f == 0) nb = fq == 0 ? v[0] : nb;
+              float2v p = {fmaxf(fmaxf(nb, v[0]), v[1]), fmaxf(fmaxf(v[1], v[2]), v[3])};
+              p += float2v{bs[n], bs[n]};
+              const short2v q = __builtin_elementwise_max(
+                  __builtin_bit_cast(short2v, __builtin_convertvector(p, bf16x2)), short2v{0, 0});
+              const uint32_t packed = __builtin_bit_cast(uint32_t, q);
+              ds_write_lo16(hbase, packed, f * 8 * kHpCol + n * 32);
+              ds_write_hi16(hbase, packed, f * 8 * kHpCol + n * 32 + kHpCol);
+              prev3[n] = v[3];
+            }
+          }
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    } else {
+      // DMA the raw rows step t+2's conversion reads: this wave's rows
+      // 8t+21+hw and 8t+25+hw, DPR instructions each (rows outside the image
+      // are not loaded)
+      constexpr int DPR = (UB / 4 + 63) / 64;
+      int nwait = 0;
+      if (t + 2 < T) {
+        load_rows(8 * t + 21, 8);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) nwait += (8 * t + 21 + hw + 4 * i - 3 < G::S) ? DPR : 0;
+      }
+      if (t >= 2) {  // vertical 3-max of step t-1's conv rows -> pooled rows ph, ph+1
+        const int ph = 2 * (t - 2);
+        constexpr int per_row = G::PW * 8;
+        ushort8 m[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int it = htid + j * 256;
+          if (it < 2 * per_row) {
+            const int pr = it >= per_row;
+            const int rem = it - pr * per_row;
+            const int pw = rem >> 3, cg = rem & 7;
+            const int r1 = 2 * (ph + pr) - 1;
+            const int off = pw * kHpCol + cg * 16;
+            const ushort8 v1 = *(const ushort8*)(hp + ((r1 + kRolesHpRing) % kRolesHpRing) * HPB + off);
+            const ushort8 v2 = *(const ushort8*)(hp + ((r1 + 1) % kRolesHpRing) * HPB + off);
+            const ushort8 v3 = *(const ushort8*)(hp + ((r1 + 2) % kRolesHpRing) * HPB + off);
+            m[j] = __builtin_elementwise_max(__builtin_elementwise_max(v1, v2), v3);
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int it = htid + j * 256;
+          if (it < 2 * per_row) {
+            const int pr = it >= per_row;
+            const int rem = it - pr * per_row;
+            *(ushort8*)(a.y + (((long)b * G::PH + ph + pr) * G::PW + (rem >> 3)) * 64 + (rem & 7) * 8) = m[j];
+          }
+          nwait += (64 * hw + 256 * j < 2 * per_row) ? 1 : 0;  // a store instruction of this wave
+        }
+      }
+      if (t < T) convert_rows(8 * t + 5, 8, htid, 256);
+      // step t-1's DMAs (converted at t+1) have landed: everything but this
+      // step's DMAs and stores (vmcnt retires in issue order)
+      vm_wait_dyn(nwait);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+  }
+}
+
 }  // namespace
+
+int stem_pool_u8_pick_strip(int B, int PH, int num_cus) {
+  // one image per workgroup (the role-split kernel: 89 vs 100-104 us at
+  // B = 256, profiles/r3_stem_knockouts.txt) once that fills the CUs
+  return B >= num_cus ? PH : stem_pool_pick_strip(B, PH, num_cus);
+}
 
 int stem_pool_pick_strip(int B, int PH, int num_cus) {
   // Largest even divisor of PH whose grid still gives every CU two
@@ -431,7 +669,9 @@ void stem_launch(const void* x, const uint8_t* u8, const void* w, const float* b
   a.PH = PH;
   a.PW = PH;
   a.strip = strip;
-  a.stagger = (g_stem_dbg >> 8) ? (g_stem_dbg >> 8) - 1 : ((long)B * (PH / strip) >= 512 ? kStemStagger : 0);
+  // g_stem_dbg: bits 0-7 knock-outs, 512 force the role-split kernel, 1024
+  // forbid it, bits 16+ stagger + 1 (0 = the default)
+  a.stagger = (g_stem_dbg >> 16) ? (g_stem_dbg >> 16) - 1 : ((long)B * (PH / strip) >= 512 ? kStemStagger : 0);
   const size_t lds = u8 ? (size_t)kRingU8 * Wq * 16 + (size_t)kHp * a.PW * kHpCol + (size_t)kRingU8 * (S * 3 + kU8Pad)
                         : (size_t)kRing * Wq * 16 + (size_t)kHp * a.PW * kHpCol;
   const dim3 grid(B * (PH / strip));
@@ -448,6 +688,22 @@ void stem_launch(const void* x, const uint8_t* u8, const void* w, const float* b
       DMLC_STEM_DBG_CASE(14)
 #undef DMLC_STEM_DBG_CASE
       default: throw std::invalid_argument("stem_conv_pool: unknown debug variant");
+    }
+  } else if (u8 && ((g_stem_dbg & 512) || (strip == PH && !(g_stem_dbg & 1024)))) {
+    // one workgroup per image, role-split waves (stem_pool_u8_pick_strip picks
+    // strip = PH once the batch gives every CU an image)
+    const size_t lds_roles = (size_t)kRolesPairRing * Wq * 16 + (size_t)kRolesHpRing * a.PW * kHpCol +
+                             (size_t)kRolesRawRing * (S * 3 + kU8Pad);
+    if (lds_roles > 160 * 1024) throw std::invalid_argument("stem_conv_pool: role-split LDS budget");
+    switch (NF) {
+#define DMLC_STEM_ROLES_CASE(F) \
+  case F: hipLaunchKernelGGL((stem_roles_kernel<F>), dim3(B), dim3(512), lds_roles, s, a); break;
+      DMLC_STEM_ROLES_CASE(4)
+      DMLC_STEM_ROLES_CASE(5)
+      DMLC_STEM_ROLES_CASE(6)
+      DMLC_STEM_ROLES_CASE(7)
+      DMLC_STEM_ROLES_CASE(8)
+#undef DMLC_STEM_ROLES_CASE
     }
   } else if (u8) {
     switch (NF) {

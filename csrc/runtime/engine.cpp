@@ -87,7 +87,7 @@ bool EngineOptions::set(const std::string& name, bool v) {
       {"direct27", &EngineOptions::direct27},
       {"fork_ds", &EngineOptions::fork_ds},         {"fp8_3x3", &EngineOptions::fp8_3x3},
       {"conv1x1", &EngineOptions::conv1x1},         {"s2rows", &EngineOptions::s2rows},
-      {"rows28", &EngineOptions::rows28},
+      {"rows28", &EngineOptions::rows28},           {"stem_roles", &EngineOptions::stem_roles},
   };
   for (const auto& f : fields)
     if (name == f.first) {
@@ -1136,7 +1136,9 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
         if (opt_.fused_preprocess && Hin == image_size_ && Win == image_size_) {
           stem_conv_pool_u8(images, (const uint8_t*)warena_ + L.w_off,
                             (const float*)((const uint8_t*)warena_ + L.b_off), acts_[op.out], B, image_size_,
-                            stem_pool_pick_strip(B, shapes_[op.out].H, num_cus_), s);
+                            opt_.stem_roles ? stem_pool_u8_pick_strip(B, shapes_[op.out].H, num_cus_)
+                                            : stem_pool_pick_strip(B, shapes_[op.out].H, num_cus_),
+                            s);
           break;
         }
         stem_conv_pool(acts_[op.in], (const uint8_t*)warena_ + L.w_off,

@@ -456,7 +456,7 @@ def stem_conv_pool_u8(images: torch.Tensor, w_packed: torch.Tensor, bias: torch.
     B, S = images.shape[0], images.shape[1]
     ph = S // 4
     if strip is None:
-        strip = C.stem_pool_pick_strip(B, ph, torch.cuda.get_device_properties(images.device).multi_processor_count)
+        strip = C.stem_pool_u8_pick_strip(B, ph, torch.cuda.get_device_properties(images.device).multi_processor_count)
     y = torch.empty(B, ph, ph, 64, device=images.device, dtype=torch.bfloat16)
     C.stem_conv_pool_u8(_ptr(images.contiguous()), _ptr(w_packed.contiguous()), _ptr(bias.float().contiguous()),
                         _ptr(y), B, S, strip, _stream())

@@ -253,8 +253,14 @@ def test_stem_conv_pool_u8(gpu, B, S, strip):
     pairs = C.stem_row_width(S, 3, 7, 2) // 2
     two = ops.stem_conv_pool(ops.preprocess_u8(img, S, 3, 2 * pairs, paired=True), wp, bias, S, strip)
     one = ops.stem_conv_pool_u8(img, wp, bias, strip)
+    C.stem_conv_pool_set_dbg(512)  # one workgroup per image, MFMA / helper waves: same arithmetic
+    try:
+        roles = ops.stem_conv_pool_u8(img, wp, bias, strip)
+    finally:
+        C.stem_conv_pool_set_dbg(0)
     torch.cuda.synchronize()
     assert torch.equal(one, two)
+    assert torch.equal(roles, two)
 
 
 @pytest.mark.parametrize("HW,C,B,res,relu", [(28, 128, 1, False, True), (28, 128, 3, True, True),
@@ -484,6 +490,16 @@ def test_conv3x3_rows28(gpu, B, res):
     got = _nchw(y.float().cpu())
     assert _rel(got, ref) < 5e-3, _rel(got, ref)
     assert (y.float() - y0.float()).abs().max().item() < 0.05
+    # the experiment variants (dbg): inputs two steps ahead, and 8 waves x 16
+    # channels: the same MFMA order per output, bit for bit
+    C = dmlc.native()
+    wf = ops.stream_weight_frag(wp)
+    for dbg in (64, 128):
+        y2 = torch.empty_like(y)
+        C.conv3x3_rows28(ops._ptr(xg), ops._ptr(wf), ops._ptr(bias.to(gpu)), ops._ptr(rg), ops._ptr(y2), B, True,
+                         ops._stream(), dbg + (1 if res else 0))
+        torch.cuda.synchronize()
+        assert torch.equal(y2, y), dbg
 
 
 def test_preprocess_paired(gpu):

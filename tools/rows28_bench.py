@@ -64,6 +64,7 @@ def main():
         return run
 
     runs = [("rows28", rows(None)), ("rows28+res", rows(r)), ("ahead2", rows(None, 64)), ("ahead2+res", rows(r, 65)),
+            ("8 waves", rows(None, 128)), ("8 waves+res", rows(r, 129)),
             ("stream", stream(None)), ("stream+res", stream(r))]
     if args.dbg:
         runs += [("no DMA", rows(None, 1)), ("no LDS rd", rows(None, 2)), ("no DMA wait", rows(None, 16)),

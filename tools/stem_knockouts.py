@@ -41,17 +41,25 @@ def main():
     for d in [int(t) for t in args.dbg.split(",")] * 2:
         C.stem_conv_pool_set_dbg(d)
         try:
-            us = time_us(lambda: ops.stem_conv_pool_u8(img, wp, bias), args.iters)
+            us = time_us(lambda: ops.stem_conv_pool_u8(img, wp, bias, 28), args.iters)
         finally:
             C.stem_conv_pool_set_dbg(0)
         print(f"u8 dbg={d:2d} {NAMES.get(d, ''):22s} {us:7.1f} us  {flop / us / 1e6:6.0f} TFLOP/s (147-deep K)", flush=True)
     for st in [int(t) for t in args.stagger.split(",")]:  # second half of the grid started ~st us late
-        C.stem_conv_pool_set_dbg((st + 1) << 8)  # (0 = the default stagger)
+        C.stem_conv_pool_set_dbg(((st + 1) << 16) | 1024)  # (0 = the default stagger)
         try:
-            us = time_us(lambda: ops.stem_conv_pool_u8(img, wp, bias), args.iters)
+            us = time_us(lambda: ops.stem_conv_pool_u8(img, wp, bias, 28), args.iters)
         finally:
             C.stem_conv_pool_set_dbg(0)
         print(f"u8 stagger={st:2d} {us:7.1f} us", flush=True)
+    us = time_us(lambda: ops.stem_conv_pool_u8(img, wp, bias), args.iters)
+    print(f"u8 default (role-split, one workgroup per image at B >= CUs) {us:7.1f} us", flush=True)
+    C.stem_conv_pool_set_dbg(1024)
+    try:
+        us = time_us(lambda: ops.stem_conv_pool_u8(img, wp, bias, 28), args.iters)
+    finally:
+        C.stem_conv_pool_set_dbg(0)
+    print(f"u8 strip kernel (strip 28, 2 workgroups per CU, staggered) {us:7.1f} us", flush=True)
     xp = ops.preprocess_u8(img, 224, 3, paired=True)
     us = time_us(lambda: ops.stem_conv_pool(xp, wp, bias), args.iters)
     print(f"bf16 paired input          {us:7.1f} us", flush=True)
