@@ -126,8 +126,12 @@ struct C1Args {
 template <int RB>
 constexpr int block_m() { return RB <= 512 ? 64 : 32; }
 
-template <bool IN8, bool OUT8, int RB, int NW, int S2, bool RES, int S>
-__global__ __launch_bounds__(256, 2) void conv1x1_kernel(C1Args a) {
+// WV waves per workgroup: 4 (two workgroups per CU, <= 64 weight VGPRs per
+// wave) or 8 (one per CU, <= 128 weight VGPRs per wave: twice the channels
+// per wave and per workgroup, so a wide layer restages its input for fewer
+// channel slices)
+template <bool IN8, bool OUT8, int RB, int NW, int S2, bool RES, int S, int WV>
+__global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void conv1x1_kernel(C1Args a) {
   constexpr int kBM = block_m<RB>();
   constexpr int CPR = RB / 16;              // 16-B chunks per staged pixel row
   constexpr int KS = IN8 ? CPR / 8 : CPR / 4;  // K steps (128 e4m3 / 32 bf16 k each)
@@ -136,7 +140,7 @@ __global__ __launch_bounds__(256, 2) void conv1x1_kernel(C1Args a) {
   constexpr int CPL = NF >= 2 ? 8 : 4;      // channels per lane per group
   constexpr int NPF = kBM / 16;             // pixel fragments per block
   constexpr int STAGE = kBM * RB;
-  constexpr int DT = STAGE / 16 / 64 / 4;   // DMA instructions per wave per block
+  constexpr int DT = STAGE / 16 / 64 / WV;  // DMA instructions per wave per block
   constexpr int RT = RES ? NPF * NG : 0;    // residual loads per wave per block
   constexpr int ST = NPF * NG;              // stores per wave per block
   constexpr int N1 = (S - 1) * (ST + RT + DT);
@@ -155,7 +159,7 @@ __global__ __launch_bounds__(256, 2) void conv1x1_kernel(C1Args a) {
   const int slice = r % a.nslices;
   const int mstart = (r / a.nslices) * 8 + xcd;
   const int mstride = (int)gridDim.x / a.nslices;
-  const int n0 = slice * 4 * NW + wave * NW;  // this wave's first channel
+  const int n0 = slice * WV * NW + wave * NW;  // this wave's first channel
 
   // ---- weights -> VGPRs: fragment f row rr = channel ch(f, rr); lane (rr, g)
   // holds k = 32*ks + 8g .. +8 (bf16) / 128*ks + 32g .. +32 (e4m3)
@@ -209,7 +213,7 @@ __global__ __launch_bounds__(256, 2) void conv1x1_kernel(C1Args a) {
     const bool live = blk < a.nblocks;
 #pragma unroll
     for (int d = 0; d < DT; ++d) {
-      const int i = (d * 4 + wave) * 64 + lane;  // chunk index in the stage
+      const int i = (d * WV + wave) * 64 + lane;  // chunk index in the stage
       const int p = i / CPR, pc = i % CPR;
       const int lc = pc ^ swz1<RB, IN8>(p);  // logical chunk stored at physical pc
       const void* src = a.zero;
@@ -219,7 +223,7 @@ __global__ __launch_bounds__(256, 2) void conv1x1_kernel(C1Args a) {
         else  // concatenated second input (stride 1: same pixel index)
           src = (const uint8_t*)a.x2 + ((long)(blk * kBM + p) * (CPR - a.cpr1) + (lc - a.cpr1)) * 16;
       }
-      dma16(src, dst + (d * 4 + wave) * 1024);
+      dma16(src, dst + (d * WV + wave) * 1024);
     }
   };
   // residual of block blk: lane (fr, g), pixel fragment pf, group j
@@ -359,9 +363,20 @@ __global__ __launch_bounds__(256, 2) void conv1x1_kernel(C1Args a) {
   vm_wait<0>();  // no LDS-DMA may outlive the workgroup
 }
 
-// (channels per wave, staged row bytes) for a shape, or {0, 0}
+// Register-resident weights of a wave: NW x RB bytes <= 16 KB (64 VGPRs),
+// and with 8 waves also the 32 KB of 32 bf16 1-KB rows (128 VGPRs: ResNet50
+// layer4's expand conv). Other 32 KB forms spilled (fp8 1-KB rows at 32
+// channels, 512-B rows at 64 channels).
+constexpr bool weights_fit(int wv, bool in8, int rb, int nw) {
+  return nw * rb <= 16384 || (wv == 8 && !in8 && rb == 1024 && nw == 32);
+}
+
+// (waves per workgroup, channels per wave, staged row bytes) for a shape, or
+// nw = 0. The fewest channel slices win (every slice restages the whole
+// input: ResNet50 layer4's expand conv ran 32 slices at 4 waves x 16
+// channels); at equal slices the 4-wave form (two workgroups per CU).
 struct Pick {
-  int nw = 0, rb = 0;
+  int wv = 4, nw = 0, rb = 0;
 };
 
 Pick pick(const ConvArgs& a) {
@@ -380,13 +395,20 @@ Pick pick(const ConvArgs& a) {
   // strided 1-KB rows (ResNet50 layer4.0 downsample, 32 channel slices each
   // re-staging every input block): 72 us vs 57 us on the implicit GEMM
   if (a.stride == 2 && rb > 512) return p;
-  for (int nw : {64, 32, 16}) {
-    if (a.N % (4 * nw)) continue;
-    if ((long)nw * rb > 16 * 1024) continue;  // weights of a wave: <= 64 VGPRs
-    p.nw = nw;
-    p.rb = rb;
-    return p;
-  }
+  int best = 0;
+  for (int wv : {4, 8})
+    for (int nw : {64, 32, 16}) {
+      if (a.N % (wv * nw)) continue;
+      if (!weights_fit(wv, a.in_fp8, rb, nw)) continue;
+      const int slices = a.N / (wv * nw);
+      if (!best || slices < best) {
+        best = slices;
+        p.wv = wv;
+        p.nw = nw;
+        p.rb = rb;
+      }
+      break;  // the widest nw that fits this wave count
+    }
   return p;
 }
 
@@ -395,25 +417,32 @@ struct L1 {
   size_t lds;
   hipStream_t s;
   C1Args c;
-  int nw, rb;
+  int wv, nw, rb;
 };
+
+template <bool IN8, bool OUT8, int RB, int S2, bool RES, int WV>
+void launch_wv(const L1& l) {
+  constexpr int S = RB <= 256 ? 3 : 2;
+  const dim3 block(64 * WV);
+  if constexpr (weights_fit(WV, IN8, RB, 64)) {
+    if (l.nw == 64) {
+      hipLaunchKernelGGL((conv1x1_kernel<IN8, OUT8, RB, 64, S2, RES, S, WV>), l.grid, block, l.lds, l.s, l.c);
+      return;
+    }
+  }
+  if constexpr (weights_fit(WV, IN8, RB, 32)) {
+    if (l.nw == 32) {
+      hipLaunchKernelGGL((conv1x1_kernel<IN8, OUT8, RB, 32, S2, RES, S, WV>), l.grid, block, l.lds, l.s, l.c);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((conv1x1_kernel<IN8, OUT8, RB, 16, S2, RES, S, WV>), l.grid, block, l.lds, l.s, l.c);
+}
 
 template <bool IN8, bool OUT8, int RB, int S2, bool RES>
 void launch_nw(const L1& l) {
-  constexpr int S = RB <= 256 ? 3 : 2;
-  if constexpr (64 * RB <= 16384) {
-    if (l.nw == 64) {
-      hipLaunchKernelGGL((conv1x1_kernel<IN8, OUT8, RB, 64, S2, RES, S>), l.grid, dim3(256), l.lds, l.s, l.c);
-      return;
-    }
-  }
-  if constexpr (32 * RB <= 16384) {
-    if (l.nw == 32) {
-      hipLaunchKernelGGL((conv1x1_kernel<IN8, OUT8, RB, 32, S2, RES, S>), l.grid, dim3(256), l.lds, l.s, l.c);
-      return;
-    }
-  }
-  hipLaunchKernelGGL((conv1x1_kernel<IN8, OUT8, RB, 16, S2, RES, S>), l.grid, dim3(256), l.lds, l.s, l.c);
+  if (l.wv == 8) launch_wv<IN8, OUT8, RB, S2, RES, 8>(l);
+  else launch_wv<IN8, OUT8, RB, S2, RES, 4>(l);
 }
 
 template <bool IN8, bool OUT8, int S2, bool RES>
@@ -455,16 +484,18 @@ void conv1x1(const ConvArgs& a, int num_cus, hipStream_t s) {
   c.relu = a.relu;
   c.res_scale = a.res_scale;
   c.out_inv_scale = a.out_inv_scale;
-  c.nslices = a.N / (4 * pk.nw);
+  c.nslices = a.N / (pk.wv * pk.nw);
   const int bm = pk.rb <= 512 ? 64 : 32;
   c.nblocks = (int)((long)a.B * a.Ho * a.Wo / bm);
-  // persistent grid: a multiple of 8 * nslices, about 2 workgroups per CU
-  const int q = std::max(1, std::min((c.nblocks + 7) / 8, (2 * num_cus) / (8 * c.nslices)));
-  const dim3 grid(8 * c.nslices * q), block(256);
+  // persistent grid: a multiple of 8 * nslices, about 2 (4 waves) or 1 (8
+  // waves) workgroups per CU
+  const int per_cu = pk.wv == 4 ? 2 : 1;
+  const int q = std::max(1, std::min((c.nblocks + 7) / 8, (per_cu * num_cus) / (8 * c.nslices)));
+  const dim3 grid(8 * c.nslices * q);
   const size_t lds = (size_t)(pk.rb <= 256 ? 3 : 2) * bm * pk.rb;
   const bool res = a.res != nullptr;
   const int key = (a.in_fp8 ? 1 : 0) | (a.out_fp8 ? 2 : 0) | (res ? 4 : 0) | (a.stride == 2 ? 8 : 0);
-  const L1 l{grid, lds, s, c, pk.nw, pk.rb};
+  const L1 l{grid, lds, s, c, pk.wv, pk.nw, pk.rb};
   // the (in, out, residual, stride) combinations ResNet50 needs
   switch (key) {
     case 0: launch_rb<false, false, 1, false>(l); break;  // bf16 -> bf16 (reduce convs of the bf16 model)
