@@ -70,6 +70,12 @@ __device__ __forceinline__ void fp8x4_to_f32(uint32_t u, float* f) {
   f[2] = __builtin_amdgcn_cvt_f32_fp8((int)u, 2);
   f[3] = __builtin_amdgcn_cvt_f32_fp8((int)u, 3);
 }
+// values already within +-448
+__device__ __forceinline__ uint32_t f32x4_to_fp8_sat(const float* f) {
+  int v = __builtin_amdgcn_cvt_pk_fp8_f32(f[0], f[1], 0, false);
+  v = __builtin_amdgcn_cvt_pk_fp8_f32(f[2], f[3], v, true);
+  return (uint32_t)v;
+}
 __device__ __forceinline__ uint32_t f32x4_to_fp8(const float* f) {
   float c[4];
 #pragma unroll
@@ -186,15 +192,21 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void conv1x1_kernel(C1Arg
       }
     }
   }
-  // this lane's channels: group j = n0 + 32j + 8g .. +7 (NF = 1: n0 + 4g .. +3)
+  // this lane's channels: group j = n0 + 32j + 8g .. +7 (NF = 1: n0 + 4g .. +3).
+  // e4m3 output: the 1 / s_out quantisation scale is folded into alpha, the
+  // bias and the residual scale here, so an output value costs one fma (+ one
+  // for the residual) and one med3 (ReLU and the +-448 saturation together)
+  const float osc = OUT8 ? a.out_inv_scale : 1.f;
+  const float rsc = a.res_scale * osc;
+  const float relu_lo = a.relu ? 0.f : -448.f;  // e4m3 output: med3(v, relu_lo, 448)
   float bs[NG][CPL], al[NG][CPL];
 #pragma unroll
   for (int j = 0; j < NG; ++j)
 #pragma unroll
     for (int e = 0; e < CPL; ++e) {
       const int n = n0 + (NF >= 2 ? 32 * j + 8 * g : 4 * g) + e;
-      bs[j][e] = a.bias[n];
-      al[j][e] = IN8 ? a.alpha[n] : 1.f;
+      bs[j][e] = a.bias[n] * osc;
+      al[j][e] = (IN8 ? a.alpha[n] : 1.f) * osc;
     }
 
   // ---- staging: block m -> stage buffer (pixel p's RB bytes, chunk-swizzled)
@@ -314,7 +326,7 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void conv1x1_kernel(C1Arg
 #pragma unroll
         for (int e = 0; e < CPL; ++e) {
           const float raw = NF >= 2 ? acc[pf][2 * j + (e >> 2)][e & 3] : acc[pf][0][e];
-          v[e] = raw * al[j][e] + bs[j][e];
+          v[e] = IN8 || OUT8 ? __builtin_fmaf(raw, al[j][e], bs[j][e]) : raw + bs[j][e];
         }
         if constexpr (RES) {
           float rf[8];
@@ -326,7 +338,7 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void conv1x1_kernel(C1Arg
               fp8x4_to_f32(rv[pf][j], rf);
             }
 #pragma unroll
-            for (int e = 0; e < CPL; ++e) v[e] += rf[e] * a.res_scale;
+            for (int e = 0; e < CPL; ++e) v[e] = __builtin_fmaf(rf[e], rsc, v[e]);
           } else {
             if constexpr (CPL == 8) {
               const u32x4 q = rv[pf][j];
@@ -342,20 +354,21 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void conv1x1_kernel(C1Arg
             for (int e = 0; e < CPL; ++e) v[e] += rf[e];
           }
         }
-        if (a.relu) {
-#pragma unroll
-          for (int e = 0; e < CPL; ++e) v[e] = fmaxf(v[e], 0.f);
-        }
         const int n = n0 + (NF >= 2 ? 32 * j + 8 * g : 4 * g);
         uint8_t* yp = (uint8_t*)a.y + (m * a.N + n) * out_esz;
-        if constexpr (OUT8) {
+        if constexpr (OUT8) {  // (already scaled by 1 / s_out)
 #pragma unroll
-          for (int e = 0; e < CPL; ++e) v[e] *= a.out_inv_scale;
-          if constexpr (CPL == 8) *(uint2*)yp = make_uint2(f32x4_to_fp8(v), f32x4_to_fp8(v + 4));
-          else *(uint32_t*)yp = f32x4_to_fp8(v);
+          for (int e = 0; e < CPL; ++e) v[e] = __builtin_amdgcn_fmed3f(v[e], relu_lo, 448.f);
+          if constexpr (CPL == 8) *(uint2*)yp = make_uint2(f32x4_to_fp8_sat(v), f32x4_to_fp8_sat(v + 4));
+          else *(uint32_t*)yp = f32x4_to_fp8_sat(v);
+        } else if constexpr (CPL == 8) {
+          *(uint4*)yp = pack8_relu(v, a.relu);  // ReLU on the packed bf16
         } else {
-          if constexpr (CPL == 8) *(uint4*)yp = pack8(v);
-          else *(uint2*)yp = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+          if (a.relu) {
+#pragma unroll
+            for (int e = 0; e < CPL; ++e) v[e] = __builtin_amdgcn_fmed3f(v[e], 0.f, __builtin_inff());
+          }
+          *(uint2*)yp = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
         }
       }
     }
