@@ -17,16 +17,27 @@
 // One workgroup = one image, 8 waves, 4 output rows (224 pixels = 14 pixel
 // fragments of 16) per step. Per step k (output rows 4k .. 4k+3):
 //   phase 1: conv1 -> t1 rows 4k+1 .. 4k+4 (a 6-row LDS ring; rows -1 and 56
-//            are conv2's zero padding), X fragments straight from HBM/L2
+//            are conv2's zero padding) from x rows staged in LDS by DMA
+//            during the previous step
 //   phase 2: conv2 over t1 rows 4k-1 .. 4k+4 -> t2 (224 x 64, LDS)
-//   phase 3: conv3 over t2 + residual -> y rows 4k .. 4k+3
-// with a workgroup barrier after phases 1 and 2 (phase 3 of step k and phase
-// 1 of step k+1 touch disjoint LDS). A prologue phase 1 writes t1 rows -3..0.
-// Wave w: channel half wn = w & 1 (32 channels, 2 N fragments with the perm32
-// row order, so a lane ends with 8 consecutive channels of one pixel) of conv1
-// and conv2 (128 channels of conv3), and a pixel-fragment set: waves 0-3 take
-// fragments {0..3} / {7..10}, waves 4-7 {4..6} / {11..13}, so the two waves
-// sharing a SIMD (w, w+4) together always own 7 fragments.
+//   phase 3: conv3 over t2 (weights LDS-resident) + residual -> y rows
+//            4k .. 4k+3; issues the DMA of the next step's x rows
+// with a workgroup barrier after each phase. A prologue phase 1 writes t1
+// rows -3..0. Wave w: channel half wn = w & 1 (32 channels, 2 N fragments
+// with the perm32 row order, so a lane ends with 8 consecutive channels of
+// one pixel) of conv1 and conv2 (128 channels of conv3), and a
+// pixel-fragment set: waves 0-3 take fragments {0..3} / {7..10}, waves 4-7
+// {4..6} / {11..13}, so the two waves sharing a SIMD (w, w+4) together
+// always own 7 fragments.
+//
+// v1 loaded x, the conv1 weights, the BN constants and the conv3 weights
+// from HBM/L2 in the phase that used them, each behind the previous step's
+// y stores (vmcnt retires in order): 257-273 us per block at B = 256, 111 us
+// with every memory access knocked out. v2 (this file) stages x by DMA one
+// step ahead and keeps the weights and constants on chip: 193-210 us,
+// resnet50_fp8 101.2k -> 104.3k img/s (profiles/r3_bottleneck_v2.txt). Its
+// y stores and residual loads are still exposed (144 / 161 us without
+// them): conv2's weight-ring loads wait behind the stores.
 #include "common.h"
 #include "kernels.h"
 
@@ -49,7 +60,7 @@ struct BnArgs {
   float res_scale;     // s_x
   float out_inv_scale; // 1 / s_y
   int dbg;             // experiments (tools/bottleneck_bench.py): bit 0 no y stores (kept live), bit 1 no
-                       // residual loads, bit 2 no conv1 X loads
+                       // residual loads
 };
 
 constexpr int kH = 56, kW = 56, kC = 256, kM = 64;
@@ -60,9 +71,14 @@ constexpr int kHalf = (kW + 2) * 64;     // t1 slot: one 32-channel half, 58 col
 constexpr int kSlot = 2 * kHalf;         // 7424 B per t1 row
 constexpr int kRing = 6;                 // t1 rows 4k-1 .. 4k+4
 constexpr int kT2 = kPix * kM * 2;       // 28672 B
+constexpr int kXB = kPix * kC;           // 57344 B: conv1's 4 x rows (e4m3)
+constexpr int kW3 = 8 * 2 * 2 * 1024;    // 32768 B: conv3 weights, fragment order [8][2][2][64 lanes][16 B]
 constexpr int kKS2 = 9 * kM / 32;        // 18 conv2 K steps
-constexpr int kPD = 6;                   // conv2 weight register ring depth (divides kKS2)
-constexpr size_t kLds = (size_t)kRing * kSlot + kT2;
+constexpr int kPD = 2;                   // conv2 weight register ring depth (divides kKS2; 3 spilled)
+constexpr int kXDma = kXB / 1024 / 8;    // 7 LDS-DMA instructions per wave per step
+constexpr int kC1 = 2 * kM * 4;          // 512 B: conv1's alpha and bias (64 + 64 floats)
+constexpr size_t kLds = (size_t)kRing * kSlot + kT2 + kXB + kW3 + kC1;  // 163840 B = 160 KiB
+static_assert(kLds <= 160 * 1024, "LDS budget");
 
 template <int N>
 __device__ __forceinline__ void vm_wait() {
@@ -96,10 +112,30 @@ __device__ __forceinline__ int t1_off(int q, int h, int g) { return h * kHalf + 
 // t2: pixel p's 8 chunks of 8 channels, chunk c at physical c ^ ((p >> 1) & 7)
 // (every 16-lane group of a fragment read hits 16 distinct bank slots)
 __device__ __forceinline__ int t2_off(int p, int c) { return p * 128 + ((c ^ ((p >> 1) & 7)) << 4); }
+// x staging buffer: tile pixel p's 16 chunks of 16 channels, chunk c at
+// physical c ^ (p & 15) (a fragment's 16 pixels, p & 15 = lane row: every
+// 16-lane group of a ds_read_b128 covers the 16 chunk slots of a bank row)
+__device__ __forceinline__ int xb_off(int p, int c) { return p * 256 + ((c ^ (p & 15)) << 4); }
 
-// One wave's share of the whole kernel: fragments F0 .. F0+NFR-1.
+// One wave's share of the whole kernel: fragments F0 .. F0+NFR-1 of every
+// 4-row step, channel half wn of conv1 / conv2 (32 channels), 128 channels
+// of conv3.
+//
+// Step k (output rows 4k .. 4k+3), every wave:
+//   wait for the x rows 4k+1 .. 4k+4 (LDS-DMA issued during step k-1)
+//   conv1: x (LDS) -> t1 rows 4k+1 .. 4k+4 (LDS ring)          | barrier
+//   conv2: t1 rows 4k-1 .. 4k+4 -> t2 (LDS)                    | barrier
+//   conv3: residual + bias loads, then the DMA of step k+1's x rows, then
+//          t2 + conv3 weights (LDS) + residual -> y stores
+// Memory ordering: vmcnt retires in issue order and stores count in it, so
+// no load may be waited on behind a store: the residual and bias loads go
+// out before the DMA and the stores, the conv3 weights live in LDS, the
+// conv1 weights and BN constants in registers (v1 loaded them per step from
+// L2 after the previous step's stores, and without the memory traffic it
+// ran 111 us vs 257-273 us: profiles/r3_bottleneck_v2.txt).
 template <int F0, int NFR>
-__device__ __forceinline__ void bn_wave(const BnArgs& a, char* ring, char* t2, int wn, int lane) {
+__device__ __forceinline__ void bn_wave(const BnArgs& a, char* ring, char* t2, char* xb, const char* w3l,
+                                        const float* c1l, int wn, int wave, int lane) {
   const int fr = lane & 15, g = lane >> 4;
   const int b = blockIdx.x;
   const uint8_t* xim = a.x + (long)b * kH * kW * kC;
@@ -114,14 +150,28 @@ __device__ __forceinline__ void bn_wave(const BnArgs& a, char* ring, char* t2, i
     col[f] = p % kW;
     hi |= (p / kW - (16 * (F0 + f)) / kW) << f;
   }
-  // this lane's 8 channels of a 32-channel group: 8g .. 8g+7 (perm32);
-  // per-channel constants and the conv1 weights are (re)loaded in their phase
-  // (L1/L2 hits) instead of held in VGPRs through the whole kernel
-  const int c1 = 32 * wn + 8 * g;  // conv1 / conv2 output channels
   auto load8 = [](const float* p, float* v) __attribute__((always_inline)) {
     const float4 lo = *(const float4*)p, h4 = *(const float4*)(p + 4);
     v[0] = lo.x, v[1] = lo.y, v[2] = lo.z, v[3] = lo.w, v[4] = h4.x, v[5] = h4.y, v[6] = h4.z, v[7] = h4.w;
   };
+  // this lane's 8 channels of a 32-channel group: 8g .. 8g+7 (perm32)
+  const int c1 = 32 * wn + 8 * g;  // conv1 / conv2 output channels
+  // ---- resident: conv1 weights (fragment nf row rr = channel 32 wn +
+  // perm32(16 nf + rr); lane (rr, g) holds k = 128 ks + 32 g .. +32, e4m3)
+  // and the conv1 / conv2 per-channel constants
+  v8i w1f[2][2];
+#pragma unroll
+  for (int nf = 0; nf < 2; ++nf) {
+    const int ch = 32 * wn + 8 * (fr >> 2) + 4 * nf + (fr & 3);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const uint4 lo = *(const uint4*)(a.w1 + ch * kC + ks * 128 + g * 32);
+      const uint4 h4 = *(const uint4*)(a.w1 + ch * kC + ks * 128 + g * 32 + 16);
+      w1f[nf][ks] = v8i{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)h4.x, (int)h4.y, (int)h4.z, (int)h4.w};
+    }
+  }
+  float b2v[8];  // (conv1's alpha and bias are read from LDS per fragment)
+  load8(a.b2 + c1, b2v);
   // conv2 weight ring (fragment order, this wave's 32-channel group)
   const __amdgpu_buffer_rsrc_t w2rs = wave_rsrc(a.wf2 + (long)wn * kKS2 * 2 * 512, kKS2 * 2 * 1024);
   auto w2load = [&](int kf) __attribute__((always_inline)) {
@@ -132,54 +182,48 @@ __device__ __forceinline__ void bn_wave(const BnArgs& a, char* ring, char* t2, i
   for (int ks = 0; ks < kPD - 1; ++ks)
 #pragma unroll
     for (int nf = 0; nf < 2; ++nf) wq[ks][nf] = w2load(ks * 2 + nf);
-  // conv3 weights: groups 4 wn + gi (gi = 0..3), [group][ks][nf][64][8]
-  const __amdgpu_buffer_rsrc_t w3rs = wave_rsrc(a.wf3 + (long)wn * 4 * 2 * 2 * 512, 4 * 2 * 2 * 1024);
 
-  // ---- phase 1: conv1 -> t1 rows 4j+1 .. 4j+4 (rows outside the image: zeros)
+  // ---- x rows 4j+1 .. 4j+4 (clamped into the image: rows outside it feed
+  // t1 rows that are written as zeros) -> x staging buffer, by LDS-DMA:
+  // instruction i = wave + 8d covers tile pixels 4i .. 4i+3, which share an
+  // image row (56 % 4 == 0): the row and first column go in the scalar base,
+  // the lane's pixel (lane >> 4) and swizzled chunk in one per-wave offset
+  // ((4i) & 15 = (4 wave) & 15 for every d)
+  const uint32_t xvoff = (uint32_t)((lane >> 4) * kC + 16 * ((lane & 15) ^ ((4 * wave + (lane >> 4)) & 15)));
+  auto dma_x = [&](int j) __attribute__((always_inline)) {
+#pragma unroll
+    for (int d = 0; d < kXDma; ++d) {
+      const int i = wave + 8 * d, p0 = 4 * i;
+      const int r = min(max(4 * j + 1 + p0 / kW, 0), kH - 1);
+      const int off = __builtin_amdgcn_readfirstlane((r * kW + p0 % kW) * kC);
+      dma16s(xim + off, xvoff, xb + i * 1024);
+    }
+  };
+
+  // ---- conv1 -> t1 rows 4j+1 .. 4j+4 (rows outside the image: zeros)
   auto conv1 = [&](int j) __attribute__((always_inline)) {
-    // conv1 weights, fragment nf row rr = channel 32 wn + perm32(16 nf + rr):
-    // lane (rr, g) holds k = 128 ks + 32 g .. +32 (e4m3)
-    v8i w1f[2][2];
-#pragma unroll
-    for (int nf = 0; nf < 2; ++nf) {
-      const int ch = 32 * wn + 8 * (fr >> 2) + 4 * nf + (fr & 3);
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const uint4 lo = *(const uint4*)(a.w1 + ch * kC + ks * 128 + g * 32);
-        const uint4 h4 = *(const uint4*)(a.w1 + ch * kC + ks * 128 + g * 32 + 16);
-        w1f[nf][ks] = v8i{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)h4.x, (int)h4.y, (int)h4.z, (int)h4.w};
-      }
-    }
-    float a1v[8], b1v[8];
-    load8(a.a1 + c1, a1v);
-    load8(a.b1 + c1, b1v);
-    v8i xb[NFR][2];
 #pragma unroll
     for (int f = 0; f < NFR; ++f) {
-      const int r = 4 * j + 1 + (16 * (F0 + f)) / kW + ((hi >> f) & 1);
-      const int rc = min(max(r, 0), kH - 1);
-      const uint8_t* src = xim + ((long)rc * kW + col[f]) * kC + g * 32;
+      const int p = 16 * (F0 + f) + fr;
+      v8i xv[2];
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        uint4 lo = make_uint4(0x38383838u, 0, 0, 0), h4 = make_uint4(0, 0, 0, 0);
-        if (!(a.dbg & 4)) {
-          lo = *(const uint4*)(src + ks * 128);
-          h4 = *(const uint4*)(src + ks * 128 + 16);
-        }
-        xb[f][ks] = v8i{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)h4.x, (int)h4.y, (int)h4.z, (int)h4.w};
+        const uint4 lo = *(const uint4*)(xb + xb_off(p, 8 * ks + 2 * g));
+        const uint4 h4 = *(const uint4*)(xb + xb_off(p, 8 * ks + 2 * g + 1));
+        xv[ks] = v8i{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)h4.x, (int)h4.y, (int)h4.z, (int)h4.w};
       }
-    }
-#pragma unroll
-    for (int f = 0; f < NFR; ++f) {
       floatx4 acc[2] = {floatx4{0.f, 0.f, 0.f, 0.f}, floatx4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
         for (int nf = 0; nf < 2; ++nf)
-          acc[nf] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(w1f[nf][ks], xb[f][ks], acc[nf], 0, 0, 0, 127,
-                                                                     0, 127);
+          acc[nf] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(w1f[nf][ks], xv[ks], acc[nf], 0, 0, 0, 127, 0,
+                                                                     127);
       const int r = 4 * j + 1 + (16 * (F0 + f)) / kW + ((hi >> f) & 1);
       const bool outside = (unsigned)r >= (unsigned)kH;
+      float a1v[8], b1v[8];
+      load8(c1l + c1, a1v);
+      load8(c1l + kM + c1, b1v);
       float v[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
@@ -191,13 +235,24 @@ __device__ __forceinline__ void bn_wave(const BnArgs& a, char* ring, char* t2, i
     }
   };
 
-  conv1(-1);
+  // prologue: t1 rows -3 .. 0 (only rows -1 = zero padding and 0 matter),
+  // then the x rows of step 0
+  dma_x(-1);
+  vm_wait<0>();
   lds_barrier();
+  conv1(-1);
+  lds_barrier();  // every wave is done with the staging buffer
+  dma_x(0);
   for (int k = 0; k < kSteps; ++k) {
+    // this step's x rows (DMA'd during the previous step, or the prologue):
+    // only the previous step's y stores (issued after the DMA) may be pending
+    if (k == 0) vm_wait<0>();
+    else vm_wait<NFR * 4>();
+    lds_barrier();
     conv1(k);
     lds_barrier();
 
-    // ---- phase 2: conv2 over t1 rows 4k-1 .. 4k+4 -> t2
+    // ---- conv2 over t1 rows 4k-1 .. 4k+4 -> t2
     {
       // slot byte offsets of t1 rows 4k-1+i (wave-uniform)
       // (named scalars, not an array: a per-lane select between array elements
@@ -242,8 +297,6 @@ __device__ __forceinline__ void bn_wave(const BnArgs& a, char* ring, char* t2, i
           for (int f = 0; f < NFR; ++f) xc[f] = xn[f];
         }
       }
-      float b2v[8];
-      load8(a.b2 + c1, b2v);
 #pragma unroll
       for (int f = 0; f < NFR; ++f) {
         float v[8];
@@ -255,92 +308,89 @@ __device__ __forceinline__ void bn_wave(const BnArgs& a, char* ring, char* t2, i
     }
     lds_barrier();
 
-    // ---- phase 3: conv3 over t2 + residual -> y rows 4k .. 4k+3
+    // ---- conv3 over t2 + residual -> y rows 4k .. 4k+3
     {
-      bf16x8 xt[NFR][2];
+      // residual and bias of all 4 passes first (no load after a store)
+      uint2 rv[NFR][4];
+      auto pix = [&](int f) __attribute__((always_inline)) {  // byte offset of fragment f's lane pixel
+        const int o = 4 * k + (16 * (F0 + f)) / kW + ((hi >> f) & 1);
+        return (o * kW + col[f]) * kC;
+      };
 #pragma unroll
-      for (int f = 0; f < NFR; ++f) {
-        const int p = 16 * (F0 + f) + fr;
+      for (int f = 0; f < NFR; ++f)
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) xt[f][ks] = *(const bf16x8*)(t2 + t2_off(p, 4 * ks + g));
-      }
-      constexpr int GP = 1;  // 32-channel groups per pass (VGPRs: accumulators + weights + residuals)
+        for (int pass = 0; pass < 4; ++pass)
+          rv[f][pass] = (a.dbg & 2) ? make_uint2(0, 0) : *(const uint2*)(xim + pix(f) + 128 * wn + 32 * pass + 8 * g);
+      float b3v[4][8];
 #pragma unroll
-      for (int pass = 0; pass < 4 / GP; ++pass) {
-        // groups gi = GP pass .. of this wave's 4: channels 128 wn + 32 gi + 8 g .. +7
-        bf16x8 w3[GP][2][2];  // [group][ks][nf]
+      for (int pass = 0; pass < 4; ++pass) load8(a.b3 + 128 * wn + 32 * pass + 8 * g, b3v[pass]);
+      // then the x rows of the next step (in flight under this conv3 and the
+      // next step's barrier)
+      if (k + 1 < kSteps) dma_x(k + 1);
 #pragma unroll
-        for (int gg = 0; gg < GP; ++gg)
+      for (int pass = 0; pass < 4; ++pass) {
+        // channels 128 wn + 32 pass + 8 g .. +7: weight group 4 wn + pass
+        bf16x8 w3[2][2];  // [ks][nf]
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int nf = 0; nf < 2; ++nf)
+            w3[ks][nf] = *(const bf16x8*)(w3l + (((4 * wn + pass) * 2 + ks) * 2 + nf) * 1024 + lane * 16);
+        const int c3 = 128 * wn + 32 * pass + 8 * g;
+        // one fragment at a time (t2 operands re-read per pass from LDS:
+        // the registers hold the prefetched residuals and biases instead)
+#pragma unroll
+        for (int f = 0; f < NFR; ++f) {
+          const int p = 16 * (F0 + f) + fr;
+          bf16x8 xt[2];
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks) xt[ks] = *(const bf16x8*)(t2 + t2_off(p, 4 * ks + g));
+          floatx4 acc[2] = {floatx4{0.f, 0.f, 0.f, 0.f}, floatx4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
           for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
             for (int nf = 0; nf < 2; ++nf)
-              w3[gg][ks][nf] = __builtin_bit_cast(
-                  bf16x8, __builtin_amdgcn_raw_buffer_load_b128(w3rs, lane * 16,
-                                                                (((GP * pass + gg) * 2 + ks) * 2 + nf) * 1024, 0));
-        uint2 rv[NFR][GP];
-        long pix[NFR];
+              acc[nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w3[ks][nf], xt[ks], acc[nf], 0, 0, 0);
+          float v[8], rf[8];
+          fp8x4_to_f32(rv[f][pass].x, rf);
+          fp8x4_to_f32(rv[f][pass].y, rf + 4);
 #pragma unroll
-        for (int f = 0; f < NFR; ++f) {
-          const int o = 4 * k + (16 * (F0 + f)) / kW + ((hi >> f) & 1);
-          pix[f] = ((long)o * kW + col[f]) * kC;
-#pragma unroll
-          for (int gg = 0; gg < GP; ++gg)
-            rv[f][gg] = (a.dbg & 2) ? make_uint2(0, 0)
-                                    : *(const uint2*)(xim + pix[f] + 128 * wn + 32 * (GP * pass + gg) + 8 * g);
-        }
-        floatx4 acc[NFR][GP][2];
-#pragma unroll
-        for (int f = 0; f < NFR; ++f)
-#pragma unroll
-          for (int gg = 0; gg < GP; ++gg) acc[f][gg][0] = acc[f][gg][1] = floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-          for (int f = 0; f < NFR; ++f)
-#pragma unroll
-            for (int gg = 0; gg < GP; ++gg)
-#pragma unroll
-              for (int nf = 0; nf < 2; ++nf)
-                acc[f][gg][nf] =
-                    __builtin_amdgcn_mfma_f32_16x16x32_bf16(w3[gg][ks][nf], xt[f][ks], acc[f][gg][nf], 0, 0, 0);
-#pragma unroll
-        for (int gg = 0; gg < GP; ++gg) {
-          const int c3 = 128 * wn + 32 * (GP * pass + gg) + 8 * g;
-          float b3v[8];
-          load8(a.b3 + c3, b3v);
-#pragma unroll
-          for (int f = 0; f < NFR; ++f) {
-            float v[8], rf[8];
-            fp8x4_to_f32(rv[f][gg].x, rf);
-            fp8x4_to_f32(rv[f][gg].y, rf + 4);
-#pragma unroll
-            for (int e = 0; e < 8; ++e)
-              v[e] = fmaxf(acc[f][gg][e >> 2][e & 3] + b3v[e] + rf[e] * a.res_scale, 0.f) * a.out_inv_scale;
-            const uint2 q = make_uint2(f32x4_to_fp8(v), f32x4_to_fp8(v + 4));
-            if (!(a.dbg & 1) || q.x == 0x12345678u) *(uint2*)(yim + pix[f] + c3) = q;
-          }
+          for (int e = 0; e < 8; ++e)
+            v[e] = fmaxf(acc[e >> 2][e & 3] + b3v[pass][e] + rf[e] * a.res_scale, 0.f) * a.out_inv_scale;
+          const uint2 q = make_uint2(f32x4_to_fp8(v), f32x4_to_fp8(v + 4));
+          if (!(a.dbg & 1) || q.x == 0x12345678u) *(uint2*)(yim + pix(f) + c3) = q;
         }
       }
     }
   }
+  vm_wait<0>();  // no LDS-DMA may outlive the workgroup
 }
 
 __global__ __launch_bounds__(512, 1) void bottleneck56_kernel(BnArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint4 smem[];
   char* ring = (char*)smem;
   char* t2 = ring + kRing * kSlot;
+  char* xb = t2 + kT2;
+  char* w3l = xb + kXB;
+  float* c1l = (float*)(w3l + kW3);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  // zero the t1 ring (its pad columns stay zero for the whole kernel)
+  // zero the t1 ring (its pad columns stay zero for the whole kernel); the
+  // conv3 weights -> LDS (read by every step)
   for (int i = tid; i < kRing * kSlot / 16; i += 512) ((uint4*)ring)[i] = make_uint4(0, 0, 0, 0);
+  for (int i = tid; i < kW3 / 16; i += 512) ((uint4*)w3l)[i] = ((const uint4*)a.wf3)[i];
+  if (tid < kM) {
+    c1l[tid] = a.a1[tid];
+    c1l[kM + tid] = a.b1[tid];
+  }
+  vm_wait<0>();
   lds_barrier();
   const int wn = wave & 1;
   switch (wave >> 1) {
-    case 0: bn_wave<0, 4>(a, ring, t2, wn, lane); break;
-    case 1: bn_wave<7, 4>(a, ring, t2, wn, lane); break;
-    case 2: bn_wave<4, 3>(a, ring, t2, wn, lane); break;
-    default: bn_wave<11, 3>(a, ring, t2, wn, lane); break;
+    case 0: bn_wave<0, 4>(a, ring, t2, xb, w3l, c1l, wn, wave, lane); break;
+    case 1: bn_wave<7, 4>(a, ring, t2, xb, w3l, c1l, wn, wave, lane); break;
+    case 2: bn_wave<4, 3>(a, ring, t2, xb, w3l, c1l, wn, wave, lane); break;
+    default: bn_wave<11, 3>(a, ring, t2, xb, w3l, c1l, wn, wave, lane); break;
   }
 }
 
