@@ -14,30 +14,31 @@
 // back) and took ~245 us (profiles/r2_resnet50_fp8_ops_conv1x1.txt); fused it
 // moves ~0.4 GB.
 //
-// One workgroup = one image, 8 waves, 4 output rows (224 pixels = 14 pixel
-// fragments of 16) per step. Per step k (output rows 4k .. 4k+3):
-//   phase 1: conv1 -> t1 rows 4k+1 .. 4k+4 (a 6-row LDS ring; rows -1 and 56
-//            are conv2's zero padding) from x rows staged in LDS by DMA
-//            during the previous step
-//   phase 2: conv2 over t1 rows 4k-1 .. 4k+4 -> t2 (224 x 64, LDS)
-//   phase 3: conv3 over t2 (weights LDS-resident) + residual -> y rows
-//            4k .. 4k+3; issues the DMA of the next step's x rows
-// with a workgroup barrier after each phase. A prologue phase 1 writes t1
-// rows -3..0. Wave w: channel half wn = w & 1 (32 channels, 2 N fragments
-// with the perm32 row order, so a lane ends with 8 consecutive channels of
-// one pixel) of conv1 and conv2 (128 channels of conv3), and a
-// pixel-fragment set: waves 0-3 take fragments {0..3} / {7..10}, waves 4-7
-// {4..6} / {11..13}, so the two waves sharing a SIMD (w, w+4) together
-// always own 7 fragments.
+// One workgroup = one image, 8 waves in two roles, 4 output rows (224
+// pixels = 14 pixel fragments of 16) per step; the schedule is at the kernel
+// (two workgroup barriers per step):
+//  * compute waves 0-3 (tile half wm, channel half wn): conv1 -> t1 rows
+//    4k+1 .. 4k+4 (a 6-row LDS ring; rows -1 and 56 are conv2's zero
+//    padding) from x rows staged in LDS, then conv2 over t1 rows 4k-1 .. 4k+4
+//    -> t2 (two LDS buffers); conv1 weights in registers, conv2 weights
+//    through a register ring (their only global loads);
+//  * memory waves 4-7 (tile half, 128-channel half): the LDS-DMA of the
+//    next step's x rows, conv3 of the previous step's t2 with the weights in
+//    registers, + residual (loaded a step ahead) -> y stores, 16 channels
+//    per lane (16-B e4m3 accesses).
+// A memory wave shares its SIMD with a compute wave, and its vmcnt queue is
+// its own: the compute waves never wait behind a store.
 //
-// v1 loaded x, the conv1 weights, the BN constants and the conv3 weights
-// from HBM/L2 in the phase that used them, each behind the previous step's
-// y stores (vmcnt retires in order): 257-273 us per block at B = 256, 111 us
-// with every memory access knocked out. v2 (this file) stages x by DMA one
-// step ahead and keeps the weights and constants on chip: 193-210 us,
-// resnet50_fp8 101.2k -> 104.3k img/s (profiles/r3_bottleneck_v2.txt). Its
-// y stores and residual loads are still exposed (144 / 161 us without
-// them): conv2's weight-ring loads wait behind the stores.
+// History (tools/bottleneck_bench.py, B = 256, same-box resnet50_fp8 bench;
+// profiles/r3_bottleneck_v2.txt, profiles/r3_bottleneck_v3.txt):
+//  v1: every wave all three convs, x / weights / constants loaded from
+//      HBM/L2 in the phase that used them, behind the previous stores:
+//      257-273 us per block (111 us with every memory access knocked out),
+//      at parity with the three unfused kernels;
+//  v2: x staged by DMA a step ahead, weights and constants on chip:
+//      193-210 us (+3% img/s with the fused kernel on);
+//  v3: the two roles, 16-B residual / y accesses, residual a step ahead:
+//      156-177 us; resnet50_fp8 103.2k -> 109.5-109.8k img/s fused.
 #include "common.h"
 #include "kernels.h"
 
@@ -67,17 +68,18 @@ constexpr int kH = 56, kW = 56, kC = 256, kM = 64;
 constexpr int kR = 4;                    // output rows per step
 constexpr int kPix = kR * kW;            // 224 pixels per step
 constexpr int kSteps = kH / kR;          // 14
+constexpr int kMF = kPix / 32;           // 7 pixel fragments per wave (half a step)
 constexpr int kHalf = (kW + 2) * 64;     // t1 slot: one 32-channel half, 58 columns x 64 B = 3712 B
 constexpr int kSlot = 2 * kHalf;         // 7424 B per t1 row
 constexpr int kRing = 6;                 // t1 rows 4k-1 .. 4k+4
-constexpr int kT2 = kPix * kM * 2;       // 28672 B
+constexpr int kT2 = kPix * kM * 2;       // 28672 B per t2 buffer (two)
 constexpr int kXB = kPix * kC;           // 57344 B: conv1's 4 x rows (e4m3)
-constexpr int kW3 = 8 * 2 * 2 * 1024;    // 32768 B: conv3 weights, fragment order [8][2][2][64 lanes][16 B]
 constexpr int kKS2 = 9 * kM / 32;        // 18 conv2 K steps
-constexpr int kPD = 2;                   // conv2 weight register ring depth (divides kKS2; 3 spilled)
-constexpr int kXDma = kXB / 1024 / 8;    // 7 LDS-DMA instructions per wave per step
-constexpr int kC1 = 2 * kM * 4;          // 512 B: conv1's alpha and bias (64 + 64 floats)
-constexpr size_t kLds = (size_t)kRing * kSlot + kT2 + kXB + kW3 + kC1;  // 163840 B = 160 KiB
+constexpr int kPD = 3;                   // conv2 weight register ring depth (divides kKS2)
+constexpr int kXDma = kXB / 1024 / 4;    // 14 LDS-DMA instructions per memory wave per step
+constexpr int kCst = 7 * kM * 4;         // a1, b1, b2 (64 floats each), b3 (256): 1792 B
+constexpr int kST = kMF * 2;             // y stores per memory wave per step
+constexpr size_t kLds = (size_t)kRing * kSlot + 2 * kT2 + kXB + kCst;  // 161024 B
 static_assert(kLds <= 160 * 1024, "LDS budget");
 
 template <int N>
@@ -105,9 +107,27 @@ __device__ __forceinline__ void fp8x4_to_f32(uint32_t u, float* f) {
   f[3] = __builtin_amdgcn_cvt_f32_fp8((int)u, 3);
 }
 
-// t1 ring address of (row slot byte base, staged column q, channel half h,
-// 16-B chunk g): the conv3x3_block.hip layout (chunk c of (h, q) holds
-// channels 8 (4h + (c ^ ((q >> 1) & 3))); pad columns q = 0, 57 stay zero)
+// 16-B global load the compiler does not track: its wait is the kernel's own
+// (counted vm_wait + pin), so no compiler wait lands behind a later DMA
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ u32x4 gload16(const void* p) {
+  u32x4 v;
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+template <typename T>
+__device__ __forceinline__ void pin(T& v) {
+  asm volatile("" : "+v"(v));
+}
+
+__device__ __forceinline__ void load8(const float* p, float* v) {
+  const float4 lo = *(const float4*)p, h4 = *(const float4*)(p + 4);
+  v[0] = lo.x, v[1] = lo.y, v[2] = lo.z, v[3] = lo.w, v[4] = h4.x, v[5] = h4.y, v[6] = h4.z, v[7] = h4.w;
+}
+
+// t1 ring address of (staged column q, channel half h, 16-B chunk g): the
+// conv3x3_block.hip layout (chunk c of (h, q) holds channels
+// 8 (4h + (c ^ ((q >> 1) & 3))); pad columns q = 0, 57 stay zero)
 __device__ __forceinline__ int t1_off(int q, int h, int g) { return h * kHalf + q * 64 + ((g ^ ((q >> 1) & 3)) << 4); }
 // t2: pixel p's 8 chunks of 8 channels, chunk c at physical c ^ ((p >> 1) & 7)
 // (every 16-lane group of a fragment read hits 16 distinct bank slots)
@@ -117,94 +137,69 @@ __device__ __forceinline__ int t2_off(int p, int c) { return p * 128 + ((c ^ ((p
 // 16-lane group of a ds_read_b128 covers the 16 chunk slots of a bank row)
 __device__ __forceinline__ int xb_off(int p, int c) { return p * 256 + ((c ^ (p & 15)) << 4); }
 
-// One wave's share of the whole kernel: fragments F0 .. F0+NFR-1 of every
-// 4-row step, channel half wn of conv1 / conv2 (32 channels), 128 channels
-// of conv3.
-//
-// Step k (output rows 4k .. 4k+3), every wave:
-//   wait for the x rows 4k+1 .. 4k+4 (LDS-DMA issued during step k-1)
-//   conv1: x (LDS) -> t1 rows 4k+1 .. 4k+4 (LDS ring)          | barrier
-//   conv2: t1 rows 4k-1 .. 4k+4 -> t2 (LDS)                    | barrier
-//   conv3: residual + bias loads, then the DMA of step k+1's x rows, then
-//          t2 + conv3 weights (LDS) + residual -> y stores
-// Memory ordering: vmcnt retires in issue order and stores count in it, so
-// no load may be waited on behind a store: the residual and bias loads go
-// out before the DMA and the stores, the conv3 weights live in LDS, the
-// conv1 weights and BN constants in registers (v1 loaded them per step from
-// L2 after the previous step's stores, and without the memory traffic it
-// ran 111 us vs 257-273 us: profiles/r3_bottleneck_v2.txt).
-template <int F0, int NFR>
-__device__ __forceinline__ void bn_wave(const BnArgs& a, char* ring, char* t2, char* xb, const char* w3l,
-                                        const float* c1l, int wn, int wave, int lane) {
-  const int fr = lane & 15, g = lane >> 4;
-  const int b = blockIdx.x;
-  const uint8_t* xim = a.x + (long)b * kH * kW * kC;
-  uint8_t* yim = a.y + (long)b * kH * kW * kC;
-
-  // per-lane pixel geometry: fragment f's lane pixel p = 16 (F0 + f) + fr sits
-  // in tile row tr[f] = base row TB(f) (compile time) + hi bit
-  int col[NFR], hi = 0;
+// Lane geometry shared by both roles: wave half wm owns the step's tile
+// pixels 112 wm .. 112 wm + 111 (tile rows 2 wm, 2 wm + 1) as fragments
+// f = 0..6, lane pixel p = 112 wm + 16 f + fr in tile row 2 wm + bit f of hi.
+struct Geo {
+  int col[kMF];
+  int hi;
+  __device__ __forceinline__ Geo(int wm, int fr) {
+    hi = 0;
 #pragma unroll
-  for (int f = 0; f < NFR; ++f) {
-    const int p = 16 * (F0 + f) + fr;
-    col[f] = p % kW;
-    hi |= (p / kW - (16 * (F0 + f)) / kW) << f;
-  }
-  auto load8 = [](const float* p, float* v) __attribute__((always_inline)) {
-    const float4 lo = *(const float4*)p, h4 = *(const float4*)(p + 4);
-    v[0] = lo.x, v[1] = lo.y, v[2] = lo.z, v[3] = lo.w, v[4] = h4.x, v[5] = h4.y, v[6] = h4.z, v[7] = h4.w;
-  };
-  // this lane's 8 channels of a 32-channel group: 8g .. 8g+7 (perm32)
-  const int c1 = 32 * wn + 8 * g;  // conv1 / conv2 output channels
-  // ---- resident: conv1 weights (fragment nf row rr = channel 32 wn +
-  // perm32(16 nf + rr); lane (rr, g) holds k = 128 ks + 32 g .. +32, e4m3)
-  // and the conv1 / conv2 per-channel constants
-  v8i w1f[2][2];
-#pragma unroll
-  for (int nf = 0; nf < 2; ++nf) {
-    const int ch = 32 * wn + 8 * (fr >> 2) + 4 * nf + (fr & 3);
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const uint4 lo = *(const uint4*)(a.w1 + ch * kC + ks * 128 + g * 32);
-      const uint4 h4 = *(const uint4*)(a.w1 + ch * kC + ks * 128 + g * 32 + 16);
-      w1f[nf][ks] = v8i{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)h4.x, (int)h4.y, (int)h4.z, (int)h4.w};
+    for (int f = 0; f < kMF; ++f) {
+      const int q = 16 * f + fr;  // pixel within the half tile
+      col[f] = (112 * wm + q) % kW;
+      hi |= (q / kW) << f;
     }
   }
-  float b2v[8];  // (conv1's alpha and bias are read from LDS per fragment)
-  load8(a.b2 + c1, b2v);
-  // conv2 weight ring (fragment order, this wave's 32-channel group)
-  const __amdgpu_buffer_rsrc_t w2rs = wave_rsrc(a.wf2 + (long)wn * kKS2 * 2 * 512, kKS2 * 2 * 1024);
-  auto w2load = [&](int kf) __attribute__((always_inline)) {
-    return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(w2rs, lane * 16, kf * 1024, 0));
-  };
+};
+
+// ---- compute role (waves 0-3: wave cw = 2 wm + wn): conv1 -> t1 ring,
+// conv2 -> t2, on tile half wm and channel half wn (32 channels, perm32
+// rows). Its only global loads are the conv2 weight ring's (no store ever
+// sits in front of them in its vmcnt queue).
+struct Compute {
+  const BnArgs& a;
+  char* ring;
+  const char* xb;
+  const float* cst;
+  int wm, wn, fr, g, lane;
+  Geo geo;
+  v8i w1f[2][2];  // conv1 weights, resident (lane (rr, g): k = 128 ks + 32 g .. +32 of channel 32 wn + perm32(16 nf + rr))
   bf16x8 wq[kPD][2];
-#pragma unroll
-  for (int ks = 0; ks < kPD - 1; ++ks)
-#pragma unroll
-    for (int nf = 0; nf < 2; ++nf) wq[ks][nf] = w2load(ks * 2 + nf);
+  __amdgpu_buffer_rsrc_t w2rs;
 
-  // ---- x rows 4j+1 .. 4j+4 (clamped into the image: rows outside it feed
-  // t1 rows that are written as zeros) -> x staging buffer, by LDS-DMA:
-  // instruction i = wave + 8d covers tile pixels 4i .. 4i+3, which share an
-  // image row (56 % 4 == 0): the row and first column go in the scalar base,
-  // the lane's pixel (lane >> 4) and swizzled chunk in one per-wave offset
-  // ((4i) & 15 = (4 wave) & 15 for every d)
-  const uint32_t xvoff = (uint32_t)((lane >> 4) * kC + 16 * ((lane & 15) ^ ((4 * wave + (lane >> 4)) & 15)));
-  auto dma_x = [&](int j) __attribute__((always_inline)) {
+  __device__ __forceinline__ Compute(const BnArgs& a_, char* ring_, const char* xb_, const float* cst_, int cw, int lane_)
+      : a(a_), ring(ring_), xb(xb_), cst(cst_), wm(cw >> 1), wn(cw & 1), fr(lane_ & 15), g(lane_ >> 4), lane(lane_),
+        geo(cw >> 1, lane_ & 15) {
 #pragma unroll
-    for (int d = 0; d < kXDma; ++d) {
-      const int i = wave + 8 * d, p0 = 4 * i;
-      const int r = min(max(4 * j + 1 + p0 / kW, 0), kH - 1);
-      const int off = __builtin_amdgcn_readfirstlane((r * kW + p0 % kW) * kC);
-      dma16s(xim + off, xvoff, xb + i * 1024);
+    for (int nf = 0; nf < 2; ++nf) {
+      const int ch = 32 * wn + 8 * (fr >> 2) + 4 * nf + (fr & 3);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const uint4 lo = *(const uint4*)(a.w1 + ch * kC + ks * 128 + g * 32);
+        const uint4 h4 = *(const uint4*)(a.w1 + ch * kC + ks * 128 + g * 32 + 16);
+        w1f[nf][ks] = v8i{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)h4.x, (int)h4.y, (int)h4.z, (int)h4.w};
+      }
     }
-  };
-
-  // ---- conv1 -> t1 rows 4j+1 .. 4j+4 (rows outside the image: zeros)
-  auto conv1 = [&](int j) __attribute__((always_inline)) {
+    w2rs = wave_rsrc(a.wf2 + (long)wn * kKS2 * 2 * 512, kKS2 * 2 * 1024);
 #pragma unroll
-    for (int f = 0; f < NFR; ++f) {
-      const int p = 16 * (F0 + f) + fr;
+    for (int ks = 0; ks < kPD - 1; ++ks)
+#pragma unroll
+      for (int nf = 0; nf < 2; ++nf) wq[ks][nf] = w2load(ks * 2 + nf);
+  }
+  __device__ __forceinline__ bf16x8 w2load(int kf) {
+    return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(w2rs, lane * 16, kf * 1024, 0));
+  }
+
+  // t1 rows 4j+1 .. 4j+4 (rows outside the image: zeros) from the staged x rows
+  __device__ __forceinline__ void conv1(int j) {
+    float a1v[8], b1v[8];
+    load8(cst + 32 * wn + 8 * g, a1v);
+    load8(cst + kM + 32 * wn + 8 * g, b1v);
+#pragma unroll
+    for (int f = 0; f < kMF; ++f) {
+      const int p = 112 * wm + 16 * f + fr;
       v8i xv[2];
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
@@ -219,178 +214,254 @@ __device__ __forceinline__ void bn_wave(const BnArgs& a, char* ring, char* t2, c
         for (int nf = 0; nf < 2; ++nf)
           acc[nf] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(w1f[nf][ks], xv[ks], acc[nf], 0, 0, 0, 127, 0,
                                                                      127);
-      const int r = 4 * j + 1 + (16 * (F0 + f)) / kW + ((hi >> f) & 1);
+      const int r = 4 * j + 1 + 2 * wm + ((geo.hi >> f) & 1);
       const bool outside = (unsigned)r >= (unsigned)kH;
-      float a1v[8], b1v[8];
-      load8(c1l + c1, a1v);
-      load8(c1l + kM + c1, b1v);
       float v[8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float raw = acc[e >> 2][e & 3];
-        v[e] = outside ? 0.f : fmaxf(raw * a1v[e] + b1v[e], 0.f);
-      }
-      const int q = col[f] + 1;
-      *(uint4*)(ring + ((r + kRing) % kRing) * kSlot + t1_off(q, wn, g)) = pack8(v);
+      for (int e = 0; e < 8; ++e) v[e] = outside ? 0.f : fmaxf(acc[e >> 2][e & 3] * a1v[e] + b1v[e], 0.f);
+      *(uint4*)(ring + ((r + kRing) % kRing) * kSlot + t1_off(geo.col[f] + 1, wn, g)) = pack8(v);
     }
-  };
+  }
 
-  // prologue: t1 rows -3 .. 0 (only rows -1 = zero padding and 0 matter),
-  // then the x rows of step 0
-  dma_x(-1);
-  vm_wait<0>();
-  lds_barrier();
-  conv1(-1);
-  lds_barrier();  // every wave is done with the staging buffer
-  dma_x(0);
-  for (int k = 0; k < kSteps; ++k) {
-    // this step's x rows (DMA'd during the previous step, or the prologue):
-    // only the previous step's y stores (issued after the DMA) may be pending
-    if (k == 0) vm_wait<0>();
-    else vm_wait<NFR * 4>();
-    lds_barrier();
-    conv1(k);
-    lds_barrier();
-
-    // ---- conv2 over t1 rows 4k-1 .. 4k+4 -> t2
-    {
-      // slot byte offsets of t1 rows 4k-1+i (wave-uniform)
-      // (named scalars, not an array: a per-lane select between array elements
-      // becomes a dynamically indexed private array in scratch)
-      const int s0 = ((4 * k - 1 + kRing) % kRing) * kSlot;
-      auto sl = [&](int i) __attribute__((always_inline)) {  // i compile time
-        const int v = s0 + i * kSlot;
-        return v >= kRing * kSlot ? v - kRing * kSlot : v;
-      };
-      floatx4 acc[NFR][2];
+  // conv2 over t1 rows 4k-1 .. 4k+4 -> t2 buffer
+  __device__ __forceinline__ void conv2(int k, char* t2) {
+    // slot byte offsets of t1 rows 4k-1+i (wave-uniform; named scalars, not
+    // an array: a per-lane select between array elements becomes a
+    // dynamically indexed private array in scratch)
+    const int s0 = ((4 * k - 1 + kRing) % kRing) * kSlot;
+    auto sl = [&](int i) __attribute__((always_inline)) {  // i compile time
+      const int v = s0 + i * kSlot;
+      return v >= kRing * kSlot ? v - kRing * kSlot : v;
+    };
+    floatx4 acc[kMF][2];
 #pragma unroll
-      for (int f = 0; f < NFR; ++f) acc[f][0] = acc[f][1] = floatx4{0.f, 0.f, 0.f, 0.f};
-      bf16x8 xc[NFR], xn[NFR];
-      auto load_k = [&](int ks, bf16x8* xd) __attribute__((always_inline)) {
-        const int tap = ks >> 1, h = ks & 1;
-        const int kh = tap / 3, kw = tap % 3;
+    for (int f = 0; f < kMF; ++f) acc[f][0] = acc[f][1] = floatx4{0.f, 0.f, 0.f, 0.f};
+    bf16x8 xc[kMF], xn[kMF];
+    auto load_k = [&](int ks, bf16x8* xd) __attribute__((always_inline)) {
+      const int tap = ks >> 1, h = ks & 1;
+      const int kh = tap / 3, kw = tap % 3;
 #pragma unroll
-        for (int f = 0; f < NFR; ++f) {
-          const int tb = (16 * (F0 + f)) / kW + kh;  // ring index of the fragment's base row (+0 / +1 per lane)
-          const int so = ((hi >> f) & 1) ? sl(tb + 1) : sl(tb);
-          xd[f] = *(const bf16x8*)(ring + so + t1_off(col[f] + kw, h, g));
-        }
-      };
-      load_k(0, xc);
-#pragma unroll
-      for (int ks = 0; ks < kKS2; ++ks) {
-        if (ks + 1 < kKS2) load_k(ks + 1, xn);
-        {  // K step ks + PD - 1, wrapping into the next step's first ones
-          const int kl = (ks + kPD - 1) % kKS2;
-#pragma unroll
-          for (int nf = 0; nf < 2; ++nf) wq[(ks + kPD - 1) % kPD][nf] = w2load(kl * 2 + nf);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int f = 0; f < NFR; ++f)
-#pragma unroll
-          for (int nf = 0; nf < 2; ++nf)
-            acc[f][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wq[ks % kPD][nf], xc[f], acc[f][nf], 0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);
-        if (ks + 1 < kKS2) {
-#pragma unroll
-          for (int f = 0; f < NFR; ++f) xc[f] = xn[f];
-        }
+      for (int f = 0; f < kMF; ++f) {
+        const int so = ((geo.hi >> f) & 1) ? sl(2 * wm + kh + 1) : sl(2 * wm + kh);
+        xd[f] = *(const bf16x8*)(ring + so + t1_off(geo.col[f] + kw, h, g));
       }
+    };
+    load_k(0, xc);
 #pragma unroll
-      for (int f = 0; f < NFR; ++f) {
-        float v[8];
+    for (int ks = 0; ks < kKS2; ++ks) {
+      if (ks + 1 < kKS2) load_k(ks + 1, xn);
+      {  // K step ks + PD - 1, wrapping into the next step's first ones
+        const int kl = (ks + kPD - 1) % kKS2;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = fmaxf(acc[f][e >> 2][e & 3] + b2v[e], 0.f);
-        const int p = 16 * (F0 + f) + fr;
-        *(uint4*)(t2 + t2_off(p, 4 * wn + g)) = pack8(v);
+        for (int nf = 0; nf < 2; ++nf) wq[(ks + kPD - 1) % kPD][nf] = w2load(kl * 2 + nf);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int f = 0; f < kMF; ++f)
+#pragma unroll
+        for (int nf = 0; nf < 2; ++nf)
+          acc[f][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wq[ks % kPD][nf], xc[f], acc[f][nf], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (ks + 1 < kKS2) {
+#pragma unroll
+        for (int f = 0; f < kMF; ++f) xc[f] = xn[f];
       }
     }
-    lds_barrier();
+    float b2v[8];
+    load8(cst + 2 * kM + 32 * wn + 8 * g, b2v);
+#pragma unroll
+    for (int f = 0; f < kMF; ++f) {
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = fmaxf(acc[f][e >> 2][e & 3] + b2v[e], 0.f);
+      *(uint4*)(t2 + t2_off(112 * wm + 16 * f + fr, 4 * wn + g)) = pack8(v);
+    }
+  }
+};
 
-    // ---- conv3 over t2 + residual -> y rows 4k .. 4k+3
-    {
-      // residual and bias of all 4 passes first (no load after a store)
-      uint2 rv[NFR][4];
-      auto pix = [&](int f) __attribute__((always_inline)) {  // byte offset of fragment f's lane pixel
-        const int o = 4 * k + (16 * (F0 + f)) / kW + ((hi >> f) & 1);
-        return (o * kW + col[f]) * kC;
-      };
+// ---- memory role (waves 4-7: wave mw = 2 wm + cb): the x-row DMA, the
+// residual loads, conv3 (t2 of tile half wm -> 128 channels 128 cb .. +127,
+// weights resident) and the y stores. Its vmcnt queue per step: residual
+// loads, then the DMA, then the stores.
+struct Memory {
+  const BnArgs& a;
+  char* xb;
+  const float* cst;
+  int mw, wm, cb, fr, g, lane;
+  Geo geo;
+  const uint8_t* xim;
+  uint8_t* yim;
+  uint32_t xvoff;
+  bf16x8 w3[2][2][4];  // [channel pair-pass P][ks][nf]: channels 128 cb + 64 P .. +63
+
+  __device__ __forceinline__ Memory(const BnArgs& a_, char* xb_, const float* cst_, int mw_, int lane_)
+      : a(a_), xb(xb_), cst(cst_), mw(mw_), wm(mw_ >> 1), cb(mw_ & 1), fr(lane_ & 15), g(lane_ >> 4), lane(lane_),
+        geo(mw_ >> 1, lane_ & 15) {
+    xim = a.x + (long)blockIdx.x * kH * kW * kC;
+    yim = a.y + (long)blockIdx.x * kH * kW * kC;
+    // DMA instruction i = mw + 4d covers tile pixels 4i .. 4i+3 (one image
+    // row: 56 % 4 == 0); lane: pixel 4i + (lane >> 4), physical chunk
+    // lane & 15 = logical chunk (lane & 15) ^ ((4i + (lane >> 4)) & 15),
+    // (4i) & 15 = (4 mw) & 15 for every d
+    xvoff = (uint32_t)((lane >> 4) * kC + 16 * ((lane & 15) ^ ((4 * mw + (lane >> 4)) & 15)));
+    // conv3 weights in the perm64 row order: row r of N fragment nf of
+    // channel pair-pass P is channel 128 cb + 64 P + 16 (r >> 2) + 4 nf +
+    // (r & 3), so a lane's 16 accumulators are 16 consecutive channels (16-B
+    // e4m3 residual loads and y stores, 64 B per pixel per wave instruction).
+    // Gathered from the perm32 fragment-order array (wf3: channel 8 (r' >> 2)
+    // + 4 nf' + (r' & 3) of a 32-channel group at lane r' + 16 k-group).
 #pragma unroll
-      for (int f = 0; f < NFR; ++f)
+    for (int P = 0; P < 2; ++P)
 #pragma unroll
-        for (int pass = 0; pass < 4; ++pass)
-          rv[f][pass] = (a.dbg & 2) ? make_uint2(0, 0) : *(const uint2*)(xim + pix(f) + 128 * wn + 32 * pass + 8 * g);
-      float b3v[4][8];
+      for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-      for (int pass = 0; pass < 4; ++pass) load8(a.b3 + 128 * wn + 32 * pass + 8 * g, b3v[pass]);
-      // then the x rows of the next step (in flight under this conv3 and the
-      // next step's barrier)
-      if (k + 1 < kSteps) dma_x(k + 1);
+        for (int nf = 0; nf < 4; ++nf) {
+          const int c = 128 * cb + 64 * P + 16 * (fr >> 2) + 4 * nf + (fr & 3);
+          const int grp = c >> 5, cc = c & 31;
+          const int r0 = 4 * (cc >> 3) + (cc & 3), nf0 = (cc >> 2) & 1;
+          w3[P][ks][nf] =
+              *(const bf16x8*)((const char*)a.wf3 + ((grp * 2 + ks) * 2 + nf0) * 1024 + ((g << 4) | r0) * 16);
+        }
+  }
+
+  // x rows 4j+1 .. 4j+4 (clamped into the image: rows outside it feed t1
+  // rows that are written as zeros) -> staging buffer
+  __device__ __forceinline__ void dma_x(int j) {
 #pragma unroll
-      for (int pass = 0; pass < 4; ++pass) {
-        // channels 128 wn + 32 pass + 8 g .. +7: weight group 4 wn + pass
-        bf16x8 w3[2][2];  // [ks][nf]
+    for (int d = 0; d < kXDma; ++d) {
+      const int i = mw + 4 * d, p0 = 4 * i;
+      const int r = min(max(4 * j + 1 + p0 / kW, 0), kH - 1);
+      const int off = __builtin_amdgcn_readfirstlane((r * kW + p0 % kW) * kC);
+      dma16s(xim + off, xvoff, xb + i * 1024);
+    }
+  }
+
+  __device__ __forceinline__ int pix(int k, int f) const {  // byte offset of fragment f's lane pixel, output rows 4k..
+    return ((4 * k + 2 * wm + ((geo.hi >> f) & 1)) * kW + geo.col[f]) * kC;
+  }
+
+  u32x4 rv[kMF][2];  // residual of the next conv3 (loaded a step ahead)
+  static constexpr int kRL = kMF * 2;  // residual loads per step
+
+  // the residual of y rows 4k .. 4k+3 (16 channels per lane and pair-pass)
+  __device__ __forceinline__ void load_rv(int k) {
+#pragma unroll
+    for (int f = 0; f < kMF; ++f)
+#pragma unroll
+      for (int P = 0; P < 2; ++P) rv[f][P] = gload16(xim + pix(k, f) + 128 * cb + 64 * P + 16 * g);
+  }
+
+  // conv3 over t2 -> y rows 4k .. 4k+3 (its residual landed: the caller's wait)
+  __device__ __forceinline__ void conv3(int k, const char* t2) {
+#pragma unroll
+    for (int f = 0; f < kMF; ++f)
+#pragma unroll
+      for (int P = 0; P < 2; ++P) {
+        pin(rv[f][P]);
+        if (a.dbg & 2) rv[f][P] = u32x4{0, 0, 0, 0};
+      }
+#pragma unroll
+    for (int P = 0; P < 2; ++P) {
+      const int c3 = 128 * cb + 64 * P + 16 * g;  // this lane's 16 channels
+      float b3v[16];
+      load8(cst + 3 * kM + c3, b3v);
+      load8(cst + 3 * kM + c3 + 8, b3v + 8);
+#pragma unroll
+      for (int f = 0; f < kMF; ++f) {
+        const int p = 112 * wm + 16 * f + fr;
+        bf16x8 xt[2];
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) xt[ks] = *(const bf16x8*)(t2 + t2_off(p, 4 * ks + g));
+        floatx4 acc[4];
+#pragma unroll
+        for (int nf = 0; nf < 4; ++nf) acc[nf] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-          for (int nf = 0; nf < 2; ++nf)
-            w3[ks][nf] = *(const bf16x8*)(w3l + (((4 * wn + pass) * 2 + ks) * 2 + nf) * 1024 + lane * 16);
-        const int c3 = 128 * wn + 32 * pass + 8 * g;
-        // one fragment at a time (t2 operands re-read per pass from LDS:
-        // the registers hold the prefetched residuals and biases instead)
+          for (int nf = 0; nf < 4; ++nf)
+            acc[nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w3[P][ks][nf], xt[ks], acc[nf], 0, 0, 0);
+        const uint32_t rw[4] = {rv[f][P].x, rv[f][P].y, rv[f][P].z, rv[f][P].w};
+        uint32_t q[4];
 #pragma unroll
-        for (int f = 0; f < NFR; ++f) {
-          const int p = 16 * (F0 + f) + fr;
-          bf16x8 xt[2];
+        for (int h = 0; h < 4; ++h) {  // channels c3 + 4h .. +3 = acc[h]
+          float v[4], rf[4];
+          fp8x4_to_f32(rw[h], rf);
 #pragma unroll
-          for (int ks = 0; ks < 2; ++ks) xt[ks] = *(const bf16x8*)(t2 + t2_off(p, 4 * ks + g));
-          floatx4 acc[2] = {floatx4{0.f, 0.f, 0.f, 0.f}, floatx4{0.f, 0.f, 0.f, 0.f}};
-#pragma unroll
-          for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-            for (int nf = 0; nf < 2; ++nf)
-              acc[nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w3[ks][nf], xt[ks], acc[nf], 0, 0, 0);
-          float v[8], rf[8];
-          fp8x4_to_f32(rv[f][pass].x, rf);
-          fp8x4_to_f32(rv[f][pass].y, rf + 4);
-#pragma unroll
-          for (int e = 0; e < 8; ++e)
-            v[e] = fmaxf(acc[e >> 2][e & 3] + b3v[pass][e] + rf[e] * a.res_scale, 0.f) * a.out_inv_scale;
-          const uint2 q = make_uint2(f32x4_to_fp8(v), f32x4_to_fp8(v + 4));
-          if (!(a.dbg & 1) || q.x == 0x12345678u) *(uint2*)(yim + pix(f) + c3) = q;
+          for (int i = 0; i < 4; ++i)
+            v[i] = fmaxf(acc[h][i] + b3v[4 * h + i] + rf[i] * a.res_scale, 0.f) * a.out_inv_scale;
+          q[h] = f32x4_to_fp8(v);
         }
+        if (!(a.dbg & 1) || q[0] == 0x12345678u) *(uint4*)(yim + pix(k, f) + c3) = make_uint4(q[0], q[1], q[2], q[3]);
       }
     }
   }
-  vm_wait<0>();  // no LDS-DMA may outlive the workgroup
-}
+};
 
+// Step k = 0 .. 14, two workgroup barriers each (S1 mid-step, S2 at the end):
+//   compute: conv1(k) [x rows staged during step k-1]  | S1 | conv2(k) -> t2[k & 1] | S2
+//   memory:                                           | S1 | residual loads, DMA of
+//            conv1(k+1)'s x rows, conv3(k-1) over t2[(k-1) & 1], y stores, wait for the DMA | S2
+// The x buffer is read before S1 and written after it; the two t2 buffers
+// alternate; t1 rows written by conv1(k+1) replace rows conv2(k) finished
+// with before S2.
 __global__ __launch_bounds__(512, 1) void bottleneck56_kernel(BnArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint4 smem[];
   char* ring = (char*)smem;
-  char* t2 = ring + kRing * kSlot;
-  char* xb = t2 + kT2;
-  char* w3l = xb + kXB;
-  float* c1l = (float*)(w3l + kW3);
+  char* t2 = ring + kRing * kSlot;  // two buffers of kT2
+  char* xb = t2 + 2 * kT2;
+  float* cst = (float*)(xb + kXB);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   // zero the t1 ring (its pad columns stay zero for the whole kernel); the
-  // conv3 weights -> LDS (read by every step)
+  // per-channel constants -> LDS
   for (int i = tid; i < kRing * kSlot / 16; i += 512) ((uint4*)ring)[i] = make_uint4(0, 0, 0, 0);
-  for (int i = tid; i < kW3 / 16; i += 512) ((uint4*)w3l)[i] = ((const uint4*)a.wf3)[i];
   if (tid < kM) {
-    c1l[tid] = a.a1[tid];
-    c1l[kM + tid] = a.b1[tid];
+    cst[tid] = a.a1[tid];
+    cst[kM + tid] = a.b1[tid];
+    cst[2 * kM + tid] = a.b2[tid];
   }
-  vm_wait<0>();
-  lds_barrier();
-  const int wn = wave & 1;
-  switch (wave >> 1) {
-    case 0: bn_wave<0, 4>(a, ring, t2, xb, w3l, c1l, wn, wave, lane); break;
-    case 1: bn_wave<7, 4>(a, ring, t2, xb, w3l, c1l, wn, wave, lane); break;
-    case 2: bn_wave<4, 3>(a, ring, t2, xb, w3l, c1l, wn, wave, lane); break;
-    default: bn_wave<11, 3>(a, ring, t2, xb, w3l, c1l, wn, wave, lane); break;
+  if (tid < 4 * kM) cst[3 * kM + tid] = a.b3[tid];
+  if (wave < 4) {
+    Compute c(a, ring, xb, cst, wave, lane);
+    lds_barrier();  // B0: x rows of conv1(-1) staged (memory waves)
+    c.conv1(-1);
+    lds_barrier();  // B1
+    lds_barrier();  // B2: x rows of conv1(0) staged
+    for (int k = 0; k <= kSteps; ++k) {
+      if (k < kSteps) c.conv1(k);
+      lds_barrier();  // S1
+      if (k < kSteps) c.conv2(k, t2 + (k & 1) * kT2);
+      lds_barrier();  // S2
+    }
+  } else {
+    Memory m(a, xb, cst, wave - 4, lane);
+    m.dma_x(-1);
+    vm_wait<0>();
+    lds_barrier();  // B0
+    lds_barrier();  // B1: conv1(-1) is done with the x buffer
+    m.dma_x(0);
+    vm_wait<0>();
+    lds_barrier();  // B2
+    for (int k = 0; k <= kSteps; ++k) {
+      lds_barrier();  // S1: conv1(k) is done with the x buffer
+      // vmcnt queue of a step: [this step's residual, loaded last step]
+      // [DMA of conv1(k+1)'s x rows] [conv3(k-1)'s stores] [next residual]
+      const bool dma = k + 1 < kSteps;
+      if (dma) m.dma_x(k + 1);
+      if (k >= 1) {
+        if (dma) vm_wait<kXDma>();  // the residual (older than the DMA)
+        else vm_wait<0>();
+        m.conv3(k - 1, t2 + ((k - 1) & 1) * kT2);
+      }
+      if (k < kSteps) m.load_rv(k);
+      if (dma) {  // the DMA has landed (the stores and the next residual may be in flight)
+        if (a.dbg & 1) vm_wait<0>();
+        else if (k >= 1) vm_wait<kST + Memory::kRL>();
+        else vm_wait<Memory::kRL>();
+      }
+      lds_barrier();  // S2
+    }
+    vm_wait<0>();  // no LDS-DMA may outlive the workgroup
   }
 }
 
