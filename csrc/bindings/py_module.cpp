@@ -214,11 +214,11 @@ PYBIND11_MODULE(_C, m) {
         py::arg("wfrag") = 0);
   m.def("conv3x3_block_supported", &conv3x3_block_supported);
   m.def("conv3x3_block", [](uintptr_t x, uintptr_t wf1, uintptr_t b1, uintptr_t wf2, uintptr_t b2, uintptr_t y,
-                            uintptr_t zero, int B, uintptr_t stream) {
+                            uintptr_t zero, int B, uintptr_t stream, int dbg) {
     conv3x3_block(P<void>(x), P<void>(wf1), P<float>(b1), P<void>(wf2), P<float>(b2), P<void>(y), P<void>(zero), B,
-                  S(stream));
+                  S(stream), dbg);
   }, py::arg("x"), py::arg("wf1"), py::arg("b1"), py::arg("wf2"), py::arg("b2"), py::arg("y"), py::arg("zero"),
-        py::arg("B"), py::arg("stream"));
+        py::arg("B"), py::arg("stream"), py::arg("dbg") = 0);
   m.def("bottleneck56", [](uintptr_t x, uintptr_t w1, uintptr_t a1, uintptr_t b1, uintptr_t wf2, uintptr_t b2,
                            uintptr_t wf3, uintptr_t b3, uintptr_t y, float res_scale, float out_inv_scale, int B,
                            uintptr_t stream, int dbg) {

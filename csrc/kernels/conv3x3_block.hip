@@ -67,7 +67,9 @@ constexpr int kSteps = kH / kR + 2;    // 16
 // DMA_KS: K step at which producers issue the next step's x-row DMA (vmcnt
 // retires in order: a weight load issued after the DMA cannot be waited on
 // without waiting for the DMA too).
-template <bool PROD, int PD, int DMA_KS>
+// DBG (tools/block_bench.py knock-outs): bit 0 no x-row DMA in the loop, bit 1
+// no residual loads, bit 2 no y stores (results wrong, timing only)
+template <bool PROD, int PD, int DMA_KS, int DBG = 0>
 __device__ __forceinline__ void block_role(const BlockArgs& a, char* xring, char* tring, int rw, int lane) {
   const int wm = rw & 1, wn = rw >> 1;
   const int fr = lane & 15, g = lane >> 4;
@@ -154,7 +156,7 @@ __device__ __forceinline__ void block_role(const BlockArgs& a, char* xring, char
     // producers: DMA the new x rows of the next producer step (its t rows
     // nb..nb+3 need x rows nb-1..nb+4; up to nb are here already)
     auto issue_dma = [&]() __attribute__((always_inline)) {
-      if (PROD && step + 1 <= kH / kR) {
+      if (PROD && !(DBG & 1) && step + 1 <= kH / kR) {
         const int nb = step == 0 ? 1 : base + 4;
         for (int r = nb + 1; r <= nb + 4; ++r)
           if (r >= 6) load_row(r);
@@ -176,7 +178,7 @@ __device__ __forceinline__ void block_role(const BlockArgs& a, char* xring, char
 #pragma unroll
         for (int f = 0; f < kMF; ++f) {
           const int p = wm * (kR * kW / 2) + 16 * f + fr;
-          rres[f] = *(const uint4*)(a.x + obase + (long)p * kC + wn * 32 + 8 * g);
+          rres[f] = (DBG & 2) ? make_uint4(0, 0, 0, 0) : *(const uint4*)(a.x + obase + (long)p * kC + wn * 32 + 8 * g);
         }
       }
       floatx4 acc[kMF][2];
@@ -237,7 +239,8 @@ __device__ __forceinline__ void block_role(const BlockArgs& a, char* xring, char
           unpack8(rres[f], r);
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e] + r[e], 0.f);
-          *(uint4*)(a.y + obase + (long)p * kC + wn * 32 + 8 * g) = pack8(v);
+          const uint4 pk = pack8(v);
+          if (!(DBG & 4) || pk.x == 0x12345678u) *(uint4*)(a.y + obase + (long)p * kC + wn * 32 + 8 * g) = pk;
         }
       }
     }
@@ -249,7 +252,7 @@ __device__ __forceinline__ void block_role(const BlockArgs& a, char* xring, char
   }
 }
 
-template <int PD, int DMA_KS>
+template <int PD, int DMA_KS, int DBG = 0>
 __global__ __launch_bounds__(512, 1) void conv3x3_block_kernel(BlockArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint4 smem[];
   char* xring = (char*)smem;
@@ -262,9 +265,9 @@ __global__ __launch_bounds__(512, 1) void conv3x3_block_kernel(BlockArgs a) {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   if (wave < 4)
-    block_role<true, PD, DMA_KS>(a, xring, tring, wave & 3, lane);
+    block_role<true, PD, DMA_KS, DBG>(a, xring, tring, wave & 3, lane);
   else
-    block_role<false, PD, DMA_KS>(a, xring, tring, wave & 3, lane);
+    block_role<false, PD, DMA_KS, DBG>(a, xring, tring, wave & 3, lane);
 }
 
 }  // namespace
@@ -272,7 +275,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_block_kernel(BlockArgs a) {
 bool conv3x3_block_supported(int H, int W, int C) { return H == kH && W == kW && C == kC; }
 
 void conv3x3_block(const void* x, const void* wf1, const float* bias1, const void* wf2, const float* bias2, void* y,
-                   const void* zero, int B, hipStream_t s) {
+                   const void* zero, int B, hipStream_t s, int dbg) {
   if (B <= 0) return;
   if (!x || !wf1 || !wf2 || !bias1 || !bias2 || !y || !zero ||
       (((uintptr_t)x | (uintptr_t)wf1 | (uintptr_t)wf2 | (uintptr_t)y | (uintptr_t)zero) & 15))
@@ -289,7 +292,13 @@ void conv3x3_block(const void* x, const void* wf1, const float* bias1, const voi
   const size_t lds = (size_t)2 * kRing * kSlot;  // 148.5 KB
   // PD 6: 5 K steps of weight lookahead (PD 3 and a mid-step DMA measured
   // the same, 116-120 us at B=256); tools/block_bench.py
-  hipLaunchKernelGGL((conv3x3_block_kernel<6, 0>), dim3(B), dim3(512), lds, s, a);
+  switch (dbg) {  // knock-outs / variants for tools/block_bench.py
+    case 1: hipLaunchKernelGGL((conv3x3_block_kernel<6, 0, 1>), dim3(B), dim3(512), lds, s, a); break;
+    case 2: hipLaunchKernelGGL((conv3x3_block_kernel<6, 0, 2>), dim3(B), dim3(512), lds, s, a); break;
+    case 4: hipLaunchKernelGGL((conv3x3_block_kernel<6, 0, 4>), dim3(B), dim3(512), lds, s, a); break;
+    case 7: hipLaunchKernelGGL((conv3x3_block_kernel<6, 0, 7>), dim3(B), dim3(512), lds, s, a); break;
+    default: hipLaunchKernelGGL((conv3x3_block_kernel<6, 0>), dim3(B), dim3(512), lds, s, a);
+  }
   DMLC_HIP_CHECK(hipGetLastError());
 }
 

@@ -156,7 +156,7 @@ void conv3x3_rows(const void* x, const void* w, const float* bias, const void* r
 // in LDS. wf1/wf2: fragment-order weights (stream_frag_index, K = 576).
 bool conv3x3_block_supported(int H, int W, int C);
 void conv3x3_block(const void* x, const void* wf1, const float* bias1, const void* wf2, const float* bias2, void* y,
-                   const void* zero, int B, hipStream_t s);
+                   const void* zero, int B, hipStream_t s, int dbg = 0);
 // Direct 3x3/s1/p1 conv on 13x13 images, the whole image in LDS
 // (conv3x3_13.hip): AlexNet features.6/.8/.10 (192->384, 384->256,
 // 256->256). wf: fragment-order weights (stream_frag_index, K = 9 Cin).
