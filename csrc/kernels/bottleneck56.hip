@@ -61,7 +61,7 @@ struct BnArgs {
   float res_scale;     // s_x
   float out_inv_scale; // 1 / s_y
   int dbg;             // experiments (tools/bottleneck_bench.py): bit 0 no y stores (kept live), bit 1 no
-                       // residual loads
+                       // residual loads, bit 2 plain (not non-temporal) y stores
 };
 
 constexpr int kH = 56, kW = 56, kC = 256, kM = 64;
@@ -391,7 +391,10 @@ struct Memory {
             v[i] = fmaxf(acc[h][i] + b3v[4 * h + i] + rf[i] * a.res_scale, 0.f) * a.out_inv_scale;
           q[h] = f32x4_to_fp8(v);
         }
-        if (!(a.dbg & 1) || q[0] == 0x12345678u) *(uint4*)(yim + pix(k, f) + c3) = make_uint4(q[0], q[1], q[2], q[3]);
+        if (!(a.dbg & 4))  // non-temporal y stores (L2 kept for the x re-reads); dbg bit 2: plain stores
+          __builtin_nontemporal_store(u32x4{q[0], q[1], q[2], q[3]}, (u32x4*)(yim + pix(k, f) + c3));
+        else if (!(a.dbg & 1) || q[0] == 0x12345678u)
+          *(uint4*)(yim + pix(k, f) + c3) = make_uint4(q[0], q[1], q[2], q[3]);
       }
     }
   }
