@@ -142,8 +142,12 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void conv1x1_kernel(C1Arg
   constexpr int CPR = RB / 16;              // 16-B chunks per staged pixel row
   constexpr int KS = IN8 ? CPR / 8 : CPR / 4;  // K steps (128 e4m3 / 32 bf16 k each)
   constexpr int NF = NW / 16;               // N fragments per wave
-  constexpr int NG = NF >= 2 ? NF / 2 : 1;  // 8-channel (or, NF = 1, 4-channel) groups per lane
-  constexpr int CPL = NF >= 2 ? 8 : 4;      // channels per lane per group
+  // e4m3 output with >= 4 N fragments: weight rows in the perm64 order, so a
+  // lane's accumulators are 16 consecutive channels (16-B residual loads and
+  // y stores, 64 B per pixel per wave instruction, instead of 8 B / 32 B)
+  constexpr bool W16 = OUT8 && NF >= 4;
+  constexpr int NG = W16 ? NF / 4 : NF >= 2 ? NF / 2 : 1;  // channel groups per lane
+  constexpr int CPL = W16 ? 16 : NF >= 2 ? 8 : 4;          // channels per lane per group
   constexpr int NPF = kBM / 16;             // pixel fragments per block
   constexpr int STAGE = kBM * RB;
   constexpr int DT = STAGE / 16 / 64 / WV;  // DMA instructions per wave per block
@@ -170,9 +174,12 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void conv1x1_kernel(C1Arg
   // ---- weights -> VGPRs: fragment f row rr = channel ch(f, rr); lane (rr, g)
   // holds k = 32*ks + 8g .. +8 (bf16) / 128*ks + 32g .. +32 (e4m3)
   auto ch_of = [](int f, int rr) {
-    if constexpr (NF >= 2) return 32 * (f >> 1) + 8 * (rr >> 2) + 4 * (f & 1) + (rr & 3);
+    if constexpr (W16) return 64 * (f >> 2) + 16 * (rr >> 2) + 4 * (f & 3) + (rr & 3);
+    else if constexpr (NF >= 2) return 32 * (f >> 1) + 8 * (rr >> 2) + 4 * (f & 1) + (rr & 3);
     else return rr;
   };
+  // first channel of lane group j
+  auto grp_ch = [&](int j) { return W16 ? 64 * j + 16 * g : NF >= 2 ? 32 * j + 8 * g : 4 * g; };
   WFrag wf[NF][KS];
   {
     const uint8_t* wb = (const uint8_t*)a.w;
@@ -204,7 +211,7 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void conv1x1_kernel(C1Arg
   for (int j = 0; j < NG; ++j)
 #pragma unroll
     for (int e = 0; e < CPL; ++e) {
-      const int n = n0 + (NF >= 2 ? 32 * j + 8 * g : 4 * g) + e;
+      const int n = n0 + grp_ch(j) + e;
       bs[j][e] = a.bias[n] * osc;
       al[j][e] = (IN8 ? a.alpha[n] : 1.f) * osc;
     }
@@ -242,11 +249,12 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void conv1x1_kernel(C1Arg
   const int out_esz = OUT8 ? 1 : 2;
   auto res_ptr = [&](int blk, int pf, int j) {
     const long m = (long)blk * kBM + pf * 16 + fr;
-    const int n = n0 + (NF >= 2 ? 32 * j + 8 * g : 4 * g);
+    const int n = n0 + grp_ch(j);
     return (const uint8_t*)a.res + (m * a.N + n) * out_esz;
   };
-  typedef typename std::conditional<OUT8, typename std::conditional<(CPL == 8), u32x2, uint32_t>::type,
-                                    typename std::conditional<(CPL == 8), u32x4, u32x2>::type>::type RV;
+  typedef typename std::conditional<
+      OUT8, typename std::conditional<(CPL == 16), u32x4, typename std::conditional<(CPL == 8), u32x2, uint32_t>::type>::type,
+      typename std::conditional<(CPL == 8), u32x4, u32x2>::type>::type RV;
   RV rv[NPF][NG];
 
   // prologue: blocks 0 .. S-2 of this workgroup
@@ -263,7 +271,8 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void conv1x1_kernel(C1Arg
 #pragma unroll
         for (int j = 0; j < NG; ++j) {
           const void* p = res_ptr(blk, pf, j);
-          if constexpr (OUT8 && CPL == 8) rv[pf][j] = gload8(p);
+          if constexpr (OUT8 && CPL == 16) rv[pf][j] = gload16(p);
+          else if constexpr (OUT8 && CPL == 8) rv[pf][j] = gload8(p);
           else if constexpr (OUT8) rv[pf][j] = gload4(p);
           else if constexpr (CPL == 8) rv[pf][j] = gload16(p);
           else rv[pf][j] = gload8(p);
@@ -322,16 +331,21 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void conv1x1_kernel(C1Arg
       const long m = (long)blk * kBM + pf * 16 + fr;
 #pragma unroll
       for (int j = 0; j < NG; ++j) {
-        float v[8];
+        float v[CPL];
 #pragma unroll
         for (int e = 0; e < CPL; ++e) {
-          const float raw = NF >= 2 ? acc[pf][2 * j + (e >> 2)][e & 3] : acc[pf][0][e];
+          const float raw = W16 ? acc[pf][4 * j + (e >> 2)][e & 3] : NF >= 2 ? acc[pf][2 * j + (e >> 2)][e & 3] : acc[pf][0][e];
           v[e] = IN8 || OUT8 ? __builtin_fmaf(raw, al[j][e], bs[j][e]) : raw + bs[j][e];
         }
         if constexpr (RES) {
-          float rf[8];
+          float rf[CPL];
           if constexpr (OUT8) {
-            if constexpr (CPL == 8) {
+            if constexpr (CPL == 16) {
+              fp8x4_to_f32(rv[pf][j].x, rf);
+              fp8x4_to_f32(rv[pf][j].y, rf + 4);
+              fp8x4_to_f32(rv[pf][j].z, rf + 8);
+              fp8x4_to_f32(rv[pf][j].w, rf + 12);
+            } else if constexpr (CPL == 8) {
               fp8x4_to_f32(rv[pf][j].x, rf);
               fp8x4_to_f32(rv[pf][j].y, rf + 4);
             } else {
@@ -354,12 +368,15 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void conv1x1_kernel(C1Arg
             for (int e = 0; e < CPL; ++e) v[e] += rf[e];
           }
         }
-        const int n = n0 + (NF >= 2 ? 32 * j + 8 * g : 4 * g);
+        const int n = n0 + grp_ch(j);
         uint8_t* yp = (uint8_t*)a.y + (m * a.N + n) * out_esz;
         if constexpr (OUT8) {  // (already scaled by 1 / s_out)
 #pragma unroll
           for (int e = 0; e < CPL; ++e) v[e] = __builtin_amdgcn_fmed3f(v[e], relu_lo, 448.f);
-          if constexpr (CPL == 8) *(uint2*)yp = make_uint2(f32x4_to_fp8_sat(v), f32x4_to_fp8_sat(v + 4));
+          if constexpr (CPL == 16)
+            *(uint4*)yp = make_uint4(f32x4_to_fp8_sat(v), f32x4_to_fp8_sat(v + 4), f32x4_to_fp8_sat(v + 8),
+                                     f32x4_to_fp8_sat(v + 12));
+          else if constexpr (CPL == 8) *(uint2*)yp = make_uint2(f32x4_to_fp8_sat(v), f32x4_to_fp8_sat(v + 4));
           else *(uint32_t*)yp = f32x4_to_fp8_sat(v);
         } else if constexpr (CPL == 8) {
           *(uint4*)yp = pack8_relu(v, a.relu);  // ReLU on the packed bf16
