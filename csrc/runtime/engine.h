@@ -75,8 +75,8 @@ struct EngineOptions {
   bool row_conv = true;          // direct row-streaming 3x3 convs (conv3x3_rows.hip) for 56x56x64
   bool rows_wreg = true;         // ... with register-streamed weights, 2 workgroups per CU
   bool fused_block = true;       // a 56x56x64 basic block as one kernel (conv3x3_block.hip), B >= 0.7 x CUs
-  // resnet50_fp8 layer1 identity bottlenecks as one kernel (bottleneck56.hip): at parity with
-  // the three-kernel path so far (248 vs 245 us per block), off by default
+  // resnet50_fp8 layer1 identity bottlenecks as one kernel (bottleneck56.hip, compute / memory
+  // wave roles): 156-177 vs ~245 us per block, +6% img/s (profiles/r3_bottleneck_v3.txt)
   bool fused_bottleneck = true;
   bool ds_into_expand = true;    // ResNet50 layer1.0: the 1x1 downsample computed inside conv3 (one K-concat GEMM)
   bool stream_conv = true;       // direct 3x3 convs with the input resident in LDS (conv3x3_stream.hip)
