@@ -42,6 +42,8 @@
 #include "common.h"
 #include "kernels.h"
 
+#include <type_traits>
+
 namespace dmlc {
 
 namespace {
@@ -136,6 +138,9 @@ __device__ __forceinline__ int t2_off(int p, int c) { return p * 128 + ((c ^ ((p
 // physical c ^ (p & 15) (a fragment's 16 pixels, p & 15 = lane row: every
 // 16-lane group of a ds_read_b128 covers the 16 chunk slots of a bank row)
 __device__ __forceinline__ int xb_off(int p, int c) { return p * 256 + ((c ^ (p & 15)) << 4); }
+// head kernel (bf16 64-channel x, 128-B rows): chunk c of pixel p at physical
+// c ^ (p & 7) (conv1x1.hip's 128-B bf16 layout, tests/test_layouts_cpu.py)
+__device__ __forceinline__ int xb_off_ds(int p, int c) { return p * 128 + ((c ^ (p & 7)) << 4); }
 
 // Lane geometry shared by both roles: wave half wm owns the step's tile
 // pixels 112 wm .. 112 wm + 111 (tile rows 2 wm, 2 wm + 1) as fragments
@@ -158,6 +163,7 @@ struct Geo {
 // conv2 -> t2, on tile half wm and channel half wn (32 channels, perm32
 // rows). Its only global loads are the conv2 weight ring's (no store ever
 // sits in front of them in its vmcnt queue).
+template <bool DS = false>
 struct Compute {
   const BnArgs& a;
   char* ring;
@@ -165,7 +171,9 @@ struct Compute {
   const float* cst;
   int wm, wn, fr, g, lane;
   Geo geo;
-  v8i w1f[2][2];  // conv1 weights, resident (lane (rr, g): k = 128 ks + 32 g .. +32 of channel 32 wn + perm32(16 nf + rr))
+  // conv1 weights, resident: lane (rr, g) of fragment nf holds channel 32 wn +
+  // perm32(16 nf + rr), k = 128 ks + 32 g .. +32 (e4m3) / DS: 32 ks + 8 g .. +8 (bf16)
+  typename std::conditional<DS, bf16x8, v8i>::type w1f[2][2];
   bf16x8 wq[kPD][2];
   __amdgpu_buffer_rsrc_t w2rs;
 
@@ -177,9 +185,13 @@ struct Compute {
       const int ch = 32 * wn + 8 * (fr >> 2) + 4 * nf + (fr & 3);
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        const uint4 lo = *(const uint4*)(a.w1 + ch * kC + ks * 128 + g * 32);
-        const uint4 h4 = *(const uint4*)(a.w1 + ch * kC + ks * 128 + g * 32 + 16);
-        w1f[nf][ks] = v8i{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)h4.x, (int)h4.y, (int)h4.z, (int)h4.w};
+        if constexpr (DS) {
+          w1f[nf][ks] = *(const bf16x8*)(a.w1 + (ch * kM + ks * 32 + g * 8) * 2);
+        } else {
+          const uint4 lo = *(const uint4*)(a.w1 + ch * kC + ks * 128 + g * 32);
+          const uint4 h4 = *(const uint4*)(a.w1 + ch * kC + ks * 128 + g * 32 + 16);
+          w1f[nf][ks] = v8i{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)h4.x, (int)h4.y, (int)h4.z, (int)h4.w};
+        }
       }
     }
     w2rs = wave_rsrc(a.wf2 + (long)wn * kKS2 * 2 * 512, kKS2 * 2 * 1024);
@@ -200,20 +212,31 @@ struct Compute {
 #pragma unroll
     for (int f = 0; f < kMF; ++f) {
       const int p = 112 * wm + 16 * f + fr;
-      v8i xv[2];
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const uint4 lo = *(const uint4*)(xb + xb_off(p, 8 * ks + 2 * g));
-        const uint4 h4 = *(const uint4*)(xb + xb_off(p, 8 * ks + 2 * g + 1));
-        xv[ks] = v8i{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)h4.x, (int)h4.y, (int)h4.z, (int)h4.w};
-      }
       floatx4 acc[2] = {floatx4{0.f, 0.f, 0.f, 0.f}, floatx4{0.f, 0.f, 0.f, 0.f}};
+      if constexpr (DS) {
+        bf16x8 xv[2];
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
+        for (int ks = 0; ks < 2; ++ks) xv[ks] = *(const bf16x8*)(xb + xb_off_ds(p, 4 * ks + g));
 #pragma unroll
-        for (int nf = 0; nf < 2; ++nf)
-          acc[nf] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(w1f[nf][ks], xv[ks], acc[nf], 0, 0, 0, 127, 0,
-                                                                     127);
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int nf = 0; nf < 2; ++nf)
+            acc[nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1f[nf][ks], xv[ks], acc[nf], 0, 0, 0);
+      } else {
+        v8i xv[2];
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const uint4 lo = *(const uint4*)(xb + xb_off(p, 8 * ks + 2 * g));
+          const uint4 h4 = *(const uint4*)(xb + xb_off(p, 8 * ks + 2 * g + 1));
+          xv[ks] = v8i{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)h4.x, (int)h4.y, (int)h4.z, (int)h4.w};
+        }
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int nf = 0; nf < 2; ++nf)
+            acc[nf] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(w1f[nf][ks], xv[ks], acc[nf], 0, 0, 0, 127, 0,
+                                                                       127);
+      }
       const int r = 4 * j + 1 + 2 * wm + ((geo.hi >> f) & 1);
       const bool outside = (unsigned)r >= (unsigned)kH;
       float v[8];
@@ -425,7 +448,7 @@ __global__ __launch_bounds__(512, 1) void bottleneck56_kernel(BnArgs a) {
   }
   if (tid < 4 * kM) cst[3 * kM + tid] = a.b3[tid];
   if (wave < 4) {
-    Compute c(a, ring, xb, cst, wave, lane);
+    Compute<> c(a, ring, xb, cst, wave, lane);
     lds_barrier();  // B0: x rows of conv1(-1) staged (memory waves)
     c.conv1(-1);
     lds_barrier();  // B1
@@ -468,6 +491,107 @@ __global__ __launch_bounds__(512, 1) void bottleneck56_kernel(BnArgs a) {
   }
 }
 
+
+// ---- ResNet50 layer1.0's reduce + 3x3 convs as one kernel ("head"): x bf16
+// [B,56,56,64] (the stem's output), t1 = relu(conv1x1 64->64 (x) + b1) and
+// t2 = relu(conv3x3 64->64 (t1) + b2) with t1 in LDS, t2 (bf16 [B,56,56,64])
+// stored for the block's expand conv (conv1x1.hip with the downsample as its
+// second K block). The compute waves are bottleneck56's (bf16 conv1); the
+// memory waves DMA the next step's x rows (128-B pixels, 8 per instruction)
+// and copy the previous step's t2 from LDS to memory. Saves t1's round trip
+// through HBM (2 x 103 MB at B = 256) and a launch.
+constexpr int kXBh = kPix * kM * 2;         // 28672 B: 4 x rows of 64 bf16 channels
+constexpr int kXDmah = kXBh / 1024 / 4;     // 7 LDS-DMA instructions per memory wave per step
+constexpr int kSTh = kPix * 8 / 256;        // 7 t2 chunks (16 B) per memory lane per step
+constexpr size_t kLdsH = (size_t)kRing * kSlot + 2 * kT2 + kXBh + kCst;  // 132352 B
+
+struct HeadMemory {
+  const BnArgs& a;
+  char* xb;
+  int mw, lane;
+  const uint8_t* xim;
+  uint8_t* yim;
+  uint32_t xvoff;
+  __device__ __forceinline__ HeadMemory(const BnArgs& a_, char* xb_, int mw_, int lane_)
+      : a(a_), xb(xb_), mw(mw_), lane(lane_) {
+    xim = a.x + (long)blockIdx.x * kH * kW * kM * 2;
+    yim = a.y + (long)blockIdx.x * kH * kW * kM * 2;
+    // instruction i covers pixels 8i .. 8i+7 of one image row (56 % 8 == 0);
+    // lane: pixel 8i + (lane >> 3), physical chunk lane & 7 = logical
+    // (lane & 7) ^ (lane >> 3)
+    xvoff = (uint32_t)((lane >> 3) * 128 + 16 * ((lane & 7) ^ (lane >> 3)));
+  }
+  __device__ __forceinline__ void dma_x(int j) {  // x rows 4j+1 .. 4j+4 (clamped)
+#pragma unroll
+    for (int d = 0; d < kXDmah; ++d) {
+      const int i = mw + 4 * d, p0 = 8 * i;
+      const int r = min(max(4 * j + 1 + p0 / kW, 0), kH - 1);
+      const int off = __builtin_amdgcn_readfirstlane((r * kW + p0 % kW) * 128);
+      dma16s(xim + off, xvoff, xb + i * 1024);
+    }
+  }
+  // t2 of output rows 4k .. 4k+3 (LDS, swizzled) -> y
+  __device__ __forceinline__ void copy_t2(int k, const char* t2) {
+#pragma unroll
+    for (int i = 0; i < kSTh; ++i) {
+      const int id = (i * 4 + mw) * 64 + lane;
+      const int p = id >> 3, c = id & 7;
+      const uint4 v = *(const uint4*)(t2 + t2_off(p, c));
+      *(uint4*)(yim + ((4 * k + p / kW) * kW + p % kW) * 128 + c * 16) = v;
+    }
+  }
+};
+
+__global__ __launch_bounds__(512, 1) void bottleneck56_head_kernel(BnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint4 smem[];
+  char* ring = (char*)smem;
+  char* t2 = ring + kRing * kSlot;  // two buffers of kT2
+  char* xb = t2 + 2 * kT2;
+  float* cst = (float*)(xb + kXBh);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  for (int i = tid; i < kRing * kSlot / 16; i += 512) ((uint4*)ring)[i] = make_uint4(0, 0, 0, 0);
+  if (tid < kM) {
+    cst[tid] = 1.f;  // (no conv1 alpha: bf16 weights carry the BN scale)
+    cst[kM + tid] = a.b1[tid];
+    cst[2 * kM + tid] = a.b2[tid];
+  }
+  if (wave < 4) {
+    Compute<true> c(a, ring, xb, cst, wave, lane);
+    lds_barrier();  // B0: x rows of conv1(-1) staged
+    c.conv1(-1);
+    lds_barrier();  // B1
+    lds_barrier();  // B2: x rows of conv1(0) staged
+    for (int k = 0; k <= kSteps; ++k) {
+      if (k < kSteps) c.conv1(k);
+      lds_barrier();  // S1
+      if (k < kSteps) c.conv2(k, t2 + (k & 1) * kT2);
+      lds_barrier();  // S2
+    }
+  } else {
+    HeadMemory m(a, xb, wave - 4, lane);
+    m.dma_x(-1);
+    vm_wait<0>();
+    lds_barrier();  // B0
+    lds_barrier();  // B1: conv1(-1) is done with the x buffer
+    m.dma_x(0);
+    vm_wait<0>();
+    lds_barrier();  // B2
+    for (int k = 0; k <= kSteps; ++k) {
+      lds_barrier();  // S1: conv1(k) is done with the x buffer
+      const bool dma = k + 1 < kSteps;
+      if (dma) m.dma_x(k + 1);
+      if (k >= 1) m.copy_t2(k - 1, t2 + ((k - 1) & 1) * kT2);
+      if (dma) {  // the DMA has landed (this step's t2 stores may be in flight)
+        if (k >= 1) vm_wait<kSTh>();
+        else vm_wait<0>();
+      }
+      lds_barrier();  // S2
+    }
+    vm_wait<0>();  // no LDS-DMA may outlive the workgroup
+  }
+}
+
 }  // namespace
 
 bool bottleneck56_supported(int H, int W, int C, int Cm) { return H == kH && W == kW && C == kC && Cm == kM; }
@@ -494,6 +618,23 @@ void bottleneck56(const void* x, const void* w1, const float* a1, const float* b
   a.out_inv_scale = out_inv_scale;
   a.dbg = dbg;
   hipLaunchKernelGGL(bottleneck56_kernel, dim3(B), dim3(512), kLds, s, a);
+  DMLC_HIP_CHECK(hipGetLastError());
+}
+
+void bottleneck56_head(const void* x, const void* w1, const float* b1, const void* wf2, const float* b2, void* y,
+                       int B, hipStream_t s) {
+  if (B <= 0) return;
+  if (!x || !w1 || !b1 || !wf2 || !b2 || !y || (((uintptr_t)x | (uintptr_t)w1 | (uintptr_t)wf2 | (uintptr_t)y) & 15))
+    throw std::invalid_argument("bottleneck56_head: null / misaligned operand");
+  if (x == y) throw std::invalid_argument("bottleneck56_head: in-place not supported");
+  BnArgs a = {};
+  a.x = (const uint8_t*)x;
+  a.w1 = (const uint8_t*)w1;
+  a.b1 = b1;
+  a.wf2 = (const bf16*)wf2;
+  a.b2 = b2;
+  a.y = (uint8_t*)y;
+  hipLaunchKernelGGL(bottleneck56_head_kernel, dim3(B), dim3(512), kLdsH, s, a);
   DMLC_HIP_CHECK(hipGetLastError());
 }
 

@@ -181,6 +181,11 @@ bool bottleneck56_supported(int H, int W, int C, int Cm);
 void bottleneck56(const void* x, const void* w1, const float* a1, const float* b1, const void* wf2, const float* b2,
                   const void* wf3, const float* b3, void* y, float res_scale, float out_inv_scale, int B,
                   hipStream_t s, int dbg = 0);
+// ResNet50 layer1.0's reduce 1x1 (64 -> 64) + 3x3 (64 -> 64) as one kernel
+// (bottleneck56.hip, t1 in LDS): x bf16 [B,56,56,64], w1 bf16 [64][64] (BN
+// folded), b1, wf2 / b2 as above, y = t2 bf16 [B,56,56,64].
+void bottleneck56_head(const void* x, const void* w1, const float* b1, const void* wf2, const float* b2, void* y,
+                       int B, hipStream_t s);
 // ResNet layer2.0's stride-2 3x3 conv 56x56x64 -> 28x28x128 and its 1x1/s2
 // downsample in one row-streaming, weight-stationary kernel
 // (conv3x3_s2rows.hip): one workgroup per image. wf / wdf: fragment-order

@@ -833,6 +833,32 @@ bool Engine::bottleneck_fusable(size_t oi) const {
   return true;
 }
 
+// ops[oi..oi+1] = conv1 (1x1 64 -> 64) + conv2 (3x3 64 -> 64) on a bf16
+// 56x56x64 input (ResNet50 layer1.0: the stem's output), conv1's output read
+// by conv2 alone: one bottleneck56_head kernel, t1 kept in LDS.
+bool Engine::bottleneck_head_fusable(size_t oi) const {
+  if (!opt_.fused_bottleneck || oi + 1 >= ops_.size()) return false;
+  const Op& c1 = ops_[oi];
+  const Op& c2 = ops_[oi + 1];
+  if (c1.type != OpType::Conv || c2.type != OpType::Conv || c1.side || c2.side || c2.in != c1.out || c1.res >= 0 ||
+      c2.res >= 0)
+    return false;
+  const ConvLayer& L1 = convs_[c1.conv];
+  const ConvLayer& L2 = convs_[c2.conv];
+  const ActShape& xs = shapes_[c1.in];
+  if (xs.fp8 || xs.f32 || shapes_[c1.out].fp8 || shapes_[c2.out].fp8 || shapes_[c2.out].f32) return false;
+  if (!bottleneck56_supported(xs.H, xs.W, 256, 64) || xs.C != 64) return false;
+  if (L1.fc || L1.fp8 || L1.pair || L1.stem_pool || L1.kh != 1 || L1.kw != 1 || L1.stride != 1 || !L1.relu ||
+      L1.cout != 64 || L1.kpad != 64 || L1.npad != 64)
+    return false;
+  if (L2.fp8 || L2.kh != 3 || L2.kw != 3 || L2.stride != 1 || L2.pad != 1 || !L2.relu || L2.cout != 64 ||
+      !L2.wf_off || L2.kpad != 576)
+    return false;
+  for (size_t j = 0; j < ops_.size(); ++j)
+    if (j != oi + 1 && (ops_[j].in == c1.out || ops_[j].res == c1.out)) return false;
+  return true;
+}
+
 // ops[oi] is a downsample whose only reader is a later expand conv that
 // computes it itself (its cat_ds): that op's index, else -1.
 int Engine::ds_expand_op(size_t oi) const {
@@ -1009,6 +1035,14 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
                        wa + L2.wf_off, (const float*)(wa + L2.b_off), wa + L3.wf_off, (const float*)(wa + L3.b_off),
                        acts_[ops_[oi + 2].out], shapes_[op.in].scale, 1.f / shapes_[ops_[oi + 2].out].scale, B, s);
           skip = 2;
+          break;
+        }
+        if (cs == s && bottleneck_head_fusable(oi)) {
+          const ConvLayer& L2 = convs_[ops_[oi + 1].conv];
+          const uint8_t* wa = (const uint8_t*)warena_;
+          bottleneck56_head(acts_[op.in], wa + L.w_off, (const float*)(wa + L.b_off), wa + L2.wf_off,
+                            (const float*)(wa + L2.b_off), acts_[ops_[oi + 1].out], B, s);
+          skip = 1;
           break;
         }
         if (cs == s && block_fusable(oi, B)) {

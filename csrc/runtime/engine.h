@@ -183,6 +183,7 @@ class Engine {
   bool ds_fusable(size_t oi, int B) const;     // ops oi, oi+1 = downsample + stride-2 stream conv1
   bool block_fusable(size_t oi, int B) const;  // ops oi, oi+1 = a layer1 basic block -> conv3x3_block
   bool bottleneck_fusable(size_t oi) const;    // ops oi..oi+2 = a layer1 identity bottleneck -> bottleneck56
+  bool bottleneck_head_fusable(size_t oi) const;  // ops oi, oi+1 = layer1.0's reduce + 3x3 -> bottleneck56_head
   bool bottleneck_conv3(const ConvLayer& L) const;  // L is such a block's expand conv (fragment-order weights)
   int ds_expand_op(size_t oi) const;  // ops[oi] = a downsample folded into a later expand conv: that op, or -1
   bool s2rows_ok(const Op& op, const ConvLayer& D, int B) const;  // layer2.0 conv1 + downsample -> conv3x3_s2rows

@@ -464,6 +464,8 @@ def test_resnet50_fp8_fused_bottleneck_matches_unfused(gpu):
     assert ((fl[:8].cpu() - ref).norm() / ref.norm()).item() < 0.15
     prof = dict(eng._e.profile(x.data_ptr(), 32, 224, 224, 0))
     rprof = dict(ref_eng._e.profile(x.data_ptr(), 32, 224, 224, 0))
+    # layer1.0's reduce + 3x3 run as one bottleneck56_head kernel in its conv1 op
+    assert prof["layer1.0.conv2"] < 0.6 * rprof["layer1.0.conv2"], (prof, rprof)
     for blk in ("layer1.1", "layer1.2"):
         # (the fused path's conv3 op is an empty op at the ~5-7 us launch
         # floor; the unfused expand conv takes ~17 us at B = 32)
