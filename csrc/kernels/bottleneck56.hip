@@ -93,6 +93,12 @@ __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_s_barrier();
 }
 
+// values already within +-448
+__device__ __forceinline__ uint32_t f32x4_to_fp8_sat(const float* f) {
+  int v = __builtin_amdgcn_cvt_pk_fp8_f32(f[0], f[1], 0, false);
+  v = __builtin_amdgcn_cvt_pk_fp8_f32(f[2], f[3], v, true);
+  return (uint32_t)v;
+}
 __device__ __forceinline__ uint32_t f32x4_to_fp8(const float* f) {
   float c[4];
 #pragma unroll
@@ -386,9 +392,16 @@ struct Memory {
 #pragma unroll
     for (int P = 0; P < 2; ++P) {
       const int c3 = 128 * cb + 64 * P + 16 * g;  // this lane's 16 channels
+      // 1 / s_y folded into the bias and the residual scale: an output value
+      // is two fma, one med3 (ReLU and the e4m3 saturation) and a quarter of
+      // a packed convert (the memory waves' VALU shares the SIMDs with the
+      // compute waves' MFMAs)
+      const float inv = a.out_inv_scale, rsi = a.res_scale * inv;
       float b3v[16];
       load8(cst + 3 * kM + c3, b3v);
       load8(cst + 3 * kM + c3 + 8, b3v + 8);
+#pragma unroll
+      for (int e = 0; e < 16; ++e) b3v[e] *= inv;
 #pragma unroll
       for (int f = 0; f < kMF; ++f) {
         const int p = 112 * wm + 16 * f + fr;
@@ -411,8 +424,9 @@ struct Memory {
           fp8x4_to_f32(rw[h], rf);
 #pragma unroll
           for (int i = 0; i < 4; ++i)
-            v[i] = fmaxf(acc[h][i] + b3v[4 * h + i] + rf[i] * a.res_scale, 0.f) * a.out_inv_scale;
-          q[h] = f32x4_to_fp8(v);
+            v[i] = __builtin_amdgcn_fmed3f(__builtin_fmaf(rf[i], rsi, __builtin_fmaf(acc[h][i], inv, b3v[4 * h + i])),
+                                           0.f, 448.f);
+          q[h] = f32x4_to_fp8_sat(v);
         }
         if (!(a.dbg & 4))  // non-temporal y stores (L2 kept for the x re-reads); dbg bit 2: plain stores
           __builtin_nontemporal_store(u32x4{q[0], q[1], q[2], q[3]}, (u32x4*)(yim + pix(k, f) + c3));
