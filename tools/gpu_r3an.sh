@@ -1,5 +1,5 @@
 #!/bin/bash
-# fused bottleneck with the slim conv3 epilogue (bnep) vs HEAD (base): test, microbench, resnet50_fp8 bench
+# fused bottleneck epilogue A/B: bnep (candidate) vs base (HEAD): test, microbench, resnet50_fp8 bench
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
