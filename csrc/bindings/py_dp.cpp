@@ -318,16 +318,22 @@ py::dict dp_host_run(py::array_t<uint8_t, py::array::c_style> images, int world,
 class HostFleet {
  public:
   HostFleet(std::vector<int> devices, int H, int W, int lanes, int delay_us, int max_per_rank, int min_shard,
-            std::map<std::string, uint32_t> seeds)
+            std::map<std::string, uint32_t> seeds, int batch_window_us, bool eager_when_idle)
       : H_(H), W_(W), seeds_(std::move(seeds)) {
     dp::FleetOptions o;
     o.max_per_rank = max_per_rank;
     o.image_bytes = (size_t)H * W * 3;
     o.min_shard = min_shard;
-    o.aux_bytes = 64;
+    o.aux_bytes = 8;
     o.timeout_ms = 5000;
+    o.batch_window_us = batch_window_us;
+    o.eager_when_idle = eager_when_idle;
     auto wf = [this, lanes, delay_us](const std::string& m, int d, dp::Worker* rep) {
       std::lock_guard<std::mutex> g(mu_);
+      if (fail_builds_ > 0) {  // fault injection: a worker build that fails (OOM, HIP error)
+        --fail_builds_;
+        throw std::runtime_error("HostFleet: injected worker build failure");
+      }
       auto it = seeds_.find(m);
       if (it == seeds_.end()) throw std::runtime_error("HostFleet: unknown model " + m);
       builds_.push_back({m, d, rep != nullptr});
@@ -370,6 +376,11 @@ class HostFleet {
   void set_seed(const std::string& m, uint32_t seed) {
     std::lock_guard<std::mutex> g(mu_);
     seeds_[m] = seed;
+  }
+  // the next n worker builds throw
+  void fail_next_builds(int n) {
+    std::lock_guard<std::mutex> g(mu_);
+    fail_builds_ = n;
   }
   // abrupt: every instance on `d` starts failing (found by the next query)
   void fail(int d) {
@@ -437,6 +448,9 @@ class HostFleet {
     std::map<std::string, std::map<int, int64_t>> served;
     for (const auto& kv : f_->partitions()) served[kv.first] = f_->served(kv.first);
     d["served"] = served;
+    std::map<std::string, std::map<int, int64_t>> fwd;
+    for (const auto& kv : f_->partitions()) fwd[kv.first] = f_->forwards(kv.first);
+    d["forwards"] = fwd;
     std::lock_guard<std::mutex> g(mu_);
     d["comm_builds"] = comm_builds_;
     d["overlapping_worlds"] = overlaps_;
@@ -467,6 +481,7 @@ class HostFleet {
   };
   int H_, W_;
   std::map<std::string, uint32_t> seeds_;
+  int fail_builds_ = 0;
   std::unique_ptr<dp::Fleet> f_;
   std::mutex mu_;
   std::vector<std::pair<std::vector<int>, std::weak_ptr<int>>> worlds_;
@@ -572,14 +587,16 @@ void bind_dp(py::module& m) {
   m.def("dp_partition_devices", &dp::partition_devices, py::arg("live"), py::arg("jobs"));
   m.def("host_order_probe", &host_order_probe, py::arg("bad"), py::arg("timeout_ms") = 500);
   py::class_<HostFleet>(m, "HostFleet")
-      .def(py::init<std::vector<int>, int, int, int, int, int, int, std::map<std::string, uint32_t>>(),
+      .def(py::init<std::vector<int>, int, int, int, int, int, int, std::map<std::string, uint32_t>, int, bool>(),
            py::arg("devices"), py::arg("H"), py::arg("W"), py::arg("lanes"), py::arg("delay_us"),
-           py::arg("max_per_rank"), py::arg("min_shard"), py::arg("seeds"))
+           py::arg("max_per_rank"), py::arg("min_shard"), py::arg("seeds"), py::arg("batch_window_us") = 200,
+           py::arg("eager_when_idle") = true)
       .def("set_jobs", &HostFleet::set_jobs)
       .def("load", &HostFleet::load)
       .def("lose", &HostFleet::lose)
       .def("fail", &HostFleet::fail)
       .def("set_seed", &HostFleet::set_seed)
+      .def("fail_next_builds", &HostFleet::fail_next_builds)
       .def("run", &HostFleet::run, py::arg("images"), py::arg("queries"), py::arg("threads") = 1)
       .def("state", &HostFleet::state);
   py::class_<RcclLoop>(m, "RcclLoop")

@@ -340,8 +340,7 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("max_batch", &Engine::max_batch)
       .def_property_readonly("weight_bytes", &Engine::weight_bytes)
       .def_property_readonly("activation_bytes", &Engine::activation_bytes)
-      .def_property_readonly("gflop_per_image", &Engine::gflop_per_image)
-      .def_property_readonly("blaslt_plans", &Engine::blaslt_plans);
+      .def_property_readonly("gflop_per_image", &Engine::gflop_per_image);
 
   // ---------------------------------------------------------------- data parallel
   bind_dp(m);

@@ -412,8 +412,9 @@ int run_node(const Args& a) {
     } else {
       for (int i = 0; i < std::max(1, a.geti("gpus", 1)); ++i) devs.push_back(a.geti("device", 0) + i);
     }
-    ex = make_executor(a.get("executor", "auto"), devs, a.geti("max-batch", 64),
-                       (size_t)a.geti("hbm-cache-mb", 4096) << 20, a.geti("min-shard", 32), a.geti("lanes", 2));
+    ex = make_executor(a.get("executor", "auto"), devs, a.geti("max-batch", 256),
+                       (size_t)a.geti("hbm-cache-mb", 4096) << 20, a.geti("min-shard", 32), a.geti("lanes", 2),
+                       a.geti("batch-window-us", 200));
     if (ex) {
       // the GPUs are split between the jobs in this order (first floor(n/2)
       // to the first job, src/services.rs:199-211)
@@ -522,7 +523,7 @@ int main(int argc, char** argv) {
                  "                 [--query-interval-ms 500] [--adaptive-window 0] [--query-batch 1] [--jobs resnet18,alexnet]\n"
                  "                 [--join h:p] [--daemon] [--stay] [--quiet-predictions] [--new-conn-per-query]\n"
                  "                 [--max-attempts 3]\n"
-                 "                 [--max-batch 64] [--hbm-cache-mb 4096] [--prefetch]\n"
+                 "                 [--max-batch 256] [--batch-window-us 200] [--hbm-cache-mb 4096] [--prefetch]\n"
                  "       dmlc-node selftest\n"
                  "       dmlc-node classify --model M --weights W.ot --labels L --image I.JPEG [--executor cpu|gpu]\n";
     return 0;

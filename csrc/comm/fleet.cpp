@@ -1,7 +1,9 @@
 #include "fleet.h"
 
 #include <algorithm>
+#include <chrono>
 #include <climits>
+#include <deque>
 #include <cstring>
 #include <stdexcept>
 
@@ -26,8 +28,9 @@ std::vector<std::vector<int>> partition_devices(std::vector<int> live, int jobs)
 
 // ------------------------------------------------------------------ instance
 // One model on one GPU: its worker, and per compute lane a staging batch,
-// scratch and answer buffers. A direct query holds one lane; a scattered
-// query claims every lane of every instance of the partition.
+// scratch and answer buffers. Direct queries queue here as requests and are
+// coalesced into forwards (one lane each); a scattered query claims every
+// lane of every instance of the partition for one group step at a time.
 struct Fleet::Instance {
   struct Lane {
     void* batch = nullptr;
@@ -37,27 +40,47 @@ struct Fleet::Instance {
     void* ans_host = nullptr;
     int ev = -1;
   };
+  // A chunk (<= max images) of one direct query, queued for a forward.
+  struct Req {
+    const StageFn* stage = nullptr;
+    int64_t first = 0;         // images [first, first + n) of its query
+    int n = 0;
+    int32_t* idx = nullptr;    // the caller's answers for this chunk
+    float* prob = nullptr;
+    std::chrono::steady_clock::time_point t0;
+    int state = 0;             // 0 queued, 1 in a forward, 2 answered, 3 failed
+    bool lost = false;         // failed because the device is lost (the query is redone)
+    std::exception_ptr err;    // failed for another reason (rethrown to the caller)
+    int off = 0;               // its first image's slot in the forward's batch
+  };
   std::string model;
   int device;
   int max;
+  size_t ib, aux_pi;
   std::unique_ptr<Worker> w;
   std::vector<Lane> lanes;
   std::mutex mu;
   std::condition_variable cv;
   std::vector<int> free;
   int claims = 0;
+  std::deque<Req*> q;        // queued direct requests, oldest first (under mu)
+  int64_t q_images = 0;
+  int busy = 0;              // lanes running a direct forward (under mu)
+  bool dead = false;         // a forward failed on an unhealthy device (under mu)
   std::atomic<int> outstanding{0};
   std::atomic<int64_t> served{0};
+  std::atomic<int64_t> forwards{0};
 
   Instance(std::string m, int d, std::unique_ptr<Worker> worker, const FleetOptions& o)
-      : model(std::move(m)), device(d), max(o.max_per_rank), w(std::move(worker)) {
+      : model(std::move(m)), device(d), max(o.max_per_rank), ib(o.image_bytes), aux_pi(o.aux_bytes),
+        w(std::move(worker)) {
     w->activate();
     for (int l = 0; l < w->lanes(); ++l) {
       Lane L;
       L.batch = w->alloc((size_t)max * o.image_bytes);
       if (o.aux_bytes) {
-        L.aux = w->alloc(o.aux_bytes);
-        L.aux_host = w->alloc_host(o.aux_bytes);
+        L.aux = w->alloc(o.aux_bytes * max);
+        L.aux_host = w->alloc_host(o.aux_bytes * max);
       }
       L.ans = w->alloc((size_t)max * 8);
       L.ans_host = w->alloc_host((size_t)max * 8);
@@ -80,21 +103,12 @@ struct Fleet::Instance {
       w->dealloc_host(L.ans_host);
     }
   }
-  int acquire_one() {
-    std::unique_lock<std::mutex> g(mu);
-    cv.wait(g, [&] { return claims == 0 && !free.empty(); });
-    const int l = free.back();
-    free.pop_back();
-    return l;
-  }
-  void release_one(int l) {
-    std::lock_guard<std::mutex> g(mu);
-    free.push_back(l);
-    cv.notify_all();
-  }
+  // Scatter steps: queued direct requests go first (bounded, so a steady
+  // stream of small queries cannot starve a scatter), then every lane.
   void claim_all() {
     std::unique_lock<std::mutex> g(mu);
-    ++claims;  // new direct queries wait from here on: no starvation
+    cv.wait_for(g, std::chrono::milliseconds(5), [&] { return q.empty() || dead; });
+    ++claims;  // no new direct forward starts from here on
     cv.wait(g, [&] { return free.size() == lanes.size(); });
   }
   void release_all() {
@@ -201,6 +215,14 @@ std::map<std::string, std::vector<int>> Fleet::partitions() const {
   return out;
 }
 
+std::map<int, int64_t> Fleet::forwards(const std::string& model) const {
+  std::shared_lock<std::shared_mutex> lk(plan_mu_);
+  const Model& m = get(model);
+  std::map<int, int64_t> out;
+  for (const auto& i : m.inst) out[i->device] += i->forwards.load();
+  return out;
+}
+
 std::map<int, int64_t> Fleet::served(const std::string& model) const {
   std::shared_lock<std::shared_mutex> lk(plan_mu_);
   const Model& m = get(model);
@@ -263,10 +285,13 @@ void Fleet::apply_locked(Model& m, const std::vector<int>& devs, std::vector<std
     std::lock_guard<std::mutex> g(lost_mu_);
     lost = lost_;
   }
-  bool same = fresh.empty() && devs == m.devices && m.inst.size() == devs.size();
+  bool same = fresh.empty() && devs == m.devices && m.inst.size() == devs.size() &&
+              (devs.size() < 2 || (m.group && m.gcap > 0));
   for (const auto& i : m.inst) same = same && !lost.count(i->device);
   if (same) return;
 
+  // Nothing of `m` changes until the new instances exist (a failed build or
+  // broadcast leaves the old plan in place, marked dirty by rebalance()).
   if (!m.inst.empty()) m.drop_group(opt_);
   std::vector<std::shared_ptr<Instance>> next(devs.size());
   if (!fresh.empty()) {
@@ -313,8 +338,8 @@ void Fleet::apply_locked(Model& m, const std::vector<int>& devs, std::vector<std
     m.gcap = (int64_t)opt_.max_per_rank * (int64_t)devs.size();
     m.gbatch = w->alloc((size_t)m.gcap * opt_.image_bytes);
     if (opt_.aux_bytes) {
-      m.gaux = w->alloc(opt_.aux_bytes * devs.size());
-      m.gaux_host = w->alloc_host(opt_.aux_bytes * devs.size());
+      m.gaux = w->alloc(opt_.aux_bytes * (size_t)m.gcap);
+      m.gaux_host = w->alloc_host(opt_.aux_bytes * (size_t)m.gcap);
     }
     m.gev = w->new_event();
   }
@@ -323,16 +348,23 @@ void Fleet::apply_locked(Model& m, const std::vector<int>& devs, std::vector<std
 void Fleet::rebalance() {
   std::unique_lock<std::shared_mutex> lk(plan_mu_);
   dirty_ = false;
-  const auto order = order_locked();
-  const auto plan = partition_devices(live(), (int)order.size());
-  // every group whose partition changes goes first, so the broadcast of a
-  // moved GPU's new weights never shares a device with a live group of
-  // another model
-  for (size_t j = 0; j < order.size(); ++j) {
-    Model& m = *models_.at(order[j]);
-    if (m.devices != plan[j] && !m.inst.empty()) m.drop_group(opt_);
+  try {
+    const auto order = order_locked();
+    const auto plan = partition_devices(live(), (int)order.size());
+    // every group whose partition changes goes first, so the broadcast of a
+    // moved GPU's new weights never shares a device with a live group of
+    // another model
+    for (size_t j = 0; j < order.size(); ++j) {
+      Model& m = *models_.at(order[j]);
+      if (m.devices != plan[j] && !m.inst.empty()) m.drop_group(opt_);
+    }
+    for (size_t j = 0; j < order.size(); ++j) apply_locked(*models_.at(order[j]), plan[j]);
+  } catch (...) {
+    // a model whose instances or group could not be (re)built keeps its old
+    // instances without a group (queries run direct); the next query retries
+    dirty_ = true;
+    throw;
   }
-  for (size_t j = 0; j < order.size(); ++j) apply_locked(*models_.at(order[j]), plan[j]);
   ++rebalances_;
 }
 
@@ -414,7 +446,8 @@ Fleet::Route Fleet::classify(const std::string& model, int64_t n, const StageFn&
       std::shared_lock<std::shared_mutex> lk(plan_mu_);
       Model& m = get(model);
       if (m.inst.empty()) throw std::runtime_error("fleet: no live GPU serves " + model);
-      const bool scatter = q.allow_scatter && m.inst.size() > 1 && n >= 2 * (int64_t)opt_.min_shard;
+      const bool scatter =
+          q.allow_scatter && m.inst.size() > 1 && m.group && m.gcap > 0 && n >= 2 * (int64_t)opt_.min_shard;
       r = scatter ? scattered(m, n, stage, idx, prob) : direct(m, n, stage, idx, prob, q.prefer_device);
     } catch (const DeviceLost&) {
       if (++retries > (int)devices_.size()) throw std::runtime_error("fleet: query failed on every GPU");
@@ -425,6 +458,15 @@ Fleet::Route Fleet::classify(const std::string& model, int64_t n, const StageFn&
     return r;
   }
 }
+
+namespace {
+// Smallest power of two >= b, at most max (bounded graph set per lane).
+int bucket_of(int b, int max) {
+  int p = 1;
+  while (p < b) p <<= 1;
+  return std::min(p, max);
+}
+}  // namespace
 
 Fleet::Route Fleet::direct(Model& m, int64_t n, const StageFn& stage, int32_t* idx, float* prob, int prefer) {
   // least outstanding queries; ties rotate so equal load spreads evenly; the
@@ -442,62 +484,200 @@ Fleet::Route Fleet::direct(Model& m, int64_t n, const StageFn& stage, int32_t* i
   }
   for (auto& c : m.inst)
     if (c->device == prefer && c->outstanding.load() <= bq) best = c.get();
-  ++best->outstanding;
+  Instance& in = *best;
+  ++in.outstanding;
   struct Dec {
     std::atomic<int>& a;
     ~Dec() { --a; }
-  } dec{best->outstanding};
-  Worker* w = best->w.get();
-  const int max = best->max;
-  for (int64_t first = 0; first < n; first += max) {
-    const int c = (int)std::min<int64_t>(max, n - first);
-    const int lane = best->acquire_one();
-    try {
-      w->activate();
-      const int cs = Worker::compute_stream(lane);
-      auto& L = best->lanes[lane];
-      StageCtx ctx;
-      ctx.worker = w;
-      ctx.device = best->device;
-      ctx.stream = cs;
-      ctx.batch = L.batch;
-      ctx.capacity = max;
-      ctx.aux = L.aux;
-      ctx.aux_host = L.aux_host;
-      const uint8_t* img = stage(ctx, first, c);
-      auto* a = (uint8_t*)L.ans;
-      w->classify(img, c, (int32_t*)a, (float*)(a + (size_t)max * 4), lane);
-      w->copy_d2h(L.ans_host, L.ans, (size_t)max * 8, cs);
-      w->record(L.ev, cs);
-      w->sync(L.ev);
-      const auto* h = (const uint8_t*)L.ans_host;
-      std::memcpy(idx + first, h, (size_t)c * 4);
-      std::memcpy(prob + first, h + (size_t)max * 4, (size_t)c * 4);
-    } catch (...) {
-      best->release_one(lane);
-      if (!w->healthy()) {
-        mark_lost(best->device);
-        throw DeviceLost{best->device};
-      }
-      throw;
-    }
-    best->release_one(lane);
+  } dec{in.outstanding};
+  Worker* w = in.w.get();
+  const int max = in.max;
+  const auto window = std::chrono::microseconds(std::max(0, opt_.batch_window_us));
+
+  using Req = Instance::Req;
+  std::vector<Req> reqs((size_t)((n + max - 1) / max));
+  const auto now0 = std::chrono::steady_clock::now();
+  for (size_t k = 0; k < reqs.size(); ++k) {
+    Req& r = reqs[k];
+    r.stage = &stage;
+    r.first = (int64_t)k * max;
+    r.n = (int)std::min<int64_t>(max, n - r.first);
+    r.idx = idx + r.first;
+    r.prob = prob + r.first;
+    r.t0 = now0;
   }
-  best->served += n;
+  struct Flight {
+    int lane;
+    std::vector<Req*> batch;
+  };
+  std::deque<Flight> mine;  // forwards this caller issued, oldest first; it finishes every one of them
+
+  std::unique_lock<std::mutex> g(in.mu);
+  for (Req& r : reqs) {
+    in.q.push_back(&r);
+    in.q_images += r.n;
+  }
+  in.cv.notify_all();
+  auto fail_queue = [&]() {  // the device is gone: every queued request is redone elsewhere
+    for (Req* r : in.q) {
+      r->state = 3;
+      r->lost = true;
+    }
+    in.q.clear();
+    in.q_images = 0;
+    in.cv.notify_all();
+  };
+  auto ready = [&]() {
+    if (in.q.empty() || in.claims > 0 || in.free.empty() || in.dead) return false;
+    return in.q_images >= max || window.count() == 0 || (opt_.eager_when_idle && in.busy == 0) ||
+           std::chrono::steady_clock::now() >= in.q.front()->t0 + window;
+  };
+  auto all_done = [&]() {
+    for (const Req& r : reqs)
+      if (r.state < 2) return false;
+    return true;
+  };
+
+  for (;;) {
+    if (in.dead) fail_queue();
+    // issue every ready forward, each on its own free lane
+    while (ready()) {
+      Flight f;
+      f.lane = in.free.back();
+      in.free.pop_back();
+      ++in.busy;
+      int B = 0;
+      while (!in.q.empty() && B + in.q.front()->n <= max) {
+        Req* r = in.q.front();
+        in.q.pop_front();
+        in.q_images -= r->n;
+        r->state = 1;
+        r->off = B;
+        B += r->n;
+        f.batch.push_back(r);
+      }
+      g.unlock();
+      // stage every request into the lane's batch back to back, then one
+      // forward and one answer copy for all of them
+      auto& L = in.lanes[f.lane];
+      const int cs = Worker::compute_stream(f.lane);
+      bool issued = false;
+      try {
+        w->activate();
+        int off = 0;
+        for (Req* r : f.batch) {
+          StageCtx ctx;
+          ctx.worker = w;
+          ctx.device = in.device;
+          ctx.stream = cs;
+          ctx.batch = (uint8_t*)L.batch + (size_t)off * in.ib;
+          ctx.capacity = max - off;
+          ctx.aux = L.aux ? (uint8_t*)L.aux + (size_t)off * in.aux_pi : nullptr;
+          ctx.aux_host = L.aux_host ? (uint8_t*)L.aux_host + (size_t)off * in.aux_pi : nullptr;
+          const uint8_t* p = nullptr;
+          try {
+            p = (*r->stage)(ctx, r->first, r->n);
+          } catch (...) {
+            if (!w->healthy()) throw;
+            r->err = std::current_exception();  // this request only
+            r->state = 3;
+            continue;
+          }
+          // the lane's own buffer, so the graph key (batch address, bucket) is fixed per lane
+          if (p != ctx.batch) w->copy(ctx.batch, p, (size_t)r->n * in.ib, cs);
+          r->off = off;
+          off += r->n;
+        }
+        if (off > 0) {
+          const int Bf = opt_.bucket_batches ? bucket_of(off, max) : off;
+          auto* a = (uint8_t*)L.ans;
+          w->classify((const uint8_t*)L.batch, Bf, (int32_t*)a, (float*)(a + (size_t)max * 4), f.lane);
+          w->copy_d2h(L.ans_host, L.ans, (size_t)max * 8, cs);
+          in.forwards++;
+        }
+        w->record(L.ev, cs);
+        issued = true;
+      } catch (...) {
+        const bool lost = !w->healthy();
+        const auto err = std::current_exception();
+        g.lock();
+        for (Req* r : f.batch)
+          if (r->state == 1) {
+            r->state = 3;
+            r->lost = lost;
+            if (!lost) r->err = err;
+          }
+        if (lost) in.dead = true;
+        in.free.push_back(f.lane);
+        --in.busy;
+        in.cv.notify_all();
+        continue;
+      }
+      g.lock();
+      if (issued) mine.push_back(std::move(f));
+    }
+    if (!mine.empty()) {  // finish my oldest forward
+      Flight f = std::move(mine.front());
+      mine.pop_front();
+      g.unlock();
+      auto& L = in.lanes[f.lane];
+      bool lost = false;
+      std::exception_ptr err;
+      try {
+        w->sync(L.ev);
+        const auto* h = (const uint8_t*)L.ans_host;
+        for (Req* r : f.batch)
+          if (r->state == 1) {
+            std::memcpy(r->idx, h + (size_t)r->off * 4, (size_t)r->n * 4);
+            std::memcpy(r->prob, h + (size_t)max * 4 + (size_t)r->off * 4, (size_t)r->n * 4);
+          }
+      } catch (...) {
+        lost = !w->healthy();
+        err = std::current_exception();
+      }
+      g.lock();
+      int64_t answered = 0;
+      for (Req* r : f.batch)
+        if (r->state == 1) {
+          if (err) {
+            r->state = 3;
+            r->lost = lost;
+            if (!lost) r->err = err;
+          } else {
+            r->state = 2;
+            answered += r->n;
+          }
+        }
+      in.served += answered;
+      if (lost) in.dead = true;
+      in.free.push_back(f.lane);
+      --in.busy;
+      in.cv.notify_all();
+      continue;
+    }
+    if (all_done()) break;
+    // wait for: a lane, my requests answered by another caller's forward, or
+    // the batching window of the oldest queued request
+    if (!in.q.empty() && in.claims == 0 && !in.free.empty() && !in.dead)
+      in.cv.wait_until(g, in.q.front()->t0 + window);
+    else
+      in.cv.wait(g);
+  }
+  g.unlock();
+  for (const Req& r : reqs)
+    if (r.lost) {
+      mark_lost(in.device);
+      throw DeviceLost{in.device};
+    }
+  for (const Req& r : reqs)
+    if (r.err) std::rethrow_exception(r.err);
   Route r;
-  r.device = best->device;
+  r.device = in.device;
   return r;
 }
 
 Fleet::Route Fleet::scattered(Model& m, int64_t n, const StageFn& stage, int32_t* idx, float* prob) {
   std::lock_guard<std::mutex> g(m.group_mu);
-  for (auto& i : m.inst) i->claim_all();
-  struct Release {
-    Model& m;
-    ~Release() {
-      for (auto& i : m.inst) i->release_all();
-    }
-  } rel{m};
   Instance& c = *m.inst.front();
   Worker* w = c.w.get();
   Route r;
@@ -505,7 +685,17 @@ Fleet::Route Fleet::scattered(Model& m, int64_t n, const StageFn& stage, int32_t
   r.device = c.device;
   r.devices_used = 0;
   try {
+    // one group classify (<= gcap images: one step per lane of each GPU) at
+    // a time, every lane claimed only for it: direct queries queued
+    // meanwhile run between the steps of a long scatter
     for (int64_t first = 0; first < n; first += m.gcap) {
+      for (auto& i : m.inst) i->claim_all();
+      struct Release {
+        Model& m;
+        ~Release() {
+          for (auto& i : m.inst) i->release_all();
+        }
+      } rel{m};
       const int64_t cnt = std::min<int64_t>(m.gcap, n - first);
       w->activate();
       StageCtx ctx;

@@ -17,6 +17,20 @@
 //   * a batch large enough to shard (>= 2 x min_shard images) is scattered
 //     over the partition with RCCL instead (dp::Group: grouped send/recv over
 //     xGMI, elastic on the loss of a GPU).
+//   * the reference serialises concurrent queries per model behind a mutex
+//     and runs each as its own batch-1 forward (`Member::predict`,
+//     src/services.rs:475-497). Here concurrent direct queries routed to the
+//     same (model, GPU) instance are COALESCED: they queue on the instance,
+//     and whichever caller finds a free compute lane and a ready queue (full
+//     batch, or the oldest request waited batch_window_us) stages every queued
+//     request into that lane's batch buffer back to back and runs ONE
+//     forward for all of them (real batching). A query
+//     larger than max_per_rank is cut into max_per_rank chunks that queue the
+//     same way, so its chunks run on several lanes at once (issued together,
+//     synchronised oldest first) instead of one lane with a host sync per
+//     chunk. The batch size of a forward is rounded up to a bucket (1, 2, 4,
+//     ..., max_per_rank), so each lane replays one captured hipGraph per
+//     bucket.
 //
 // Invariants:
 //   * partitions are disjoint whenever there are at least as many live GPUs
@@ -51,11 +65,21 @@ namespace dp {
 std::vector<std::vector<int>> partition_devices(std::vector<int> live, int jobs);
 
 struct FleetOptions {
-  int max_per_rank = 64;          // images per GPU per forward
+  int max_per_rank = 256;         // images per GPU per forward (= the CU count: one round of the big-batch kernels)
   size_t image_bytes = 224 * 224 * 3;
   int min_shard = 32;             // scatter only batches of >= 2*min_shard, >= min_shard per GPU
-  size_t aux_bytes = 0;           // per-lane scratch handed to the stage function
+  size_t aux_bytes = 0;           // scratch PER IMAGE handed to the stage function (a lane holds max_per_rank x it)
   int timeout_ms = 30000;         // dp::Group step timeout
+  // Coalescing of direct queries: a queued request waits at most this long
+  // for more requests to join its forward (0: a free lane takes whatever is
+  // queued at once).
+  int batch_window_us = 200;
+  // ... except on an idle instance (no forward running): the first request
+  // goes at once, later ones batch while it runs.
+  bool eager_when_idle = true;
+  // Round a forward's batch up to a power of two (max_per_rank at most): a
+  // bounded set of captured graphs per lane.
+  bool bucket_batches = true;
 };
 
 // Where the stage function puts a query's images for a chosen worker.
@@ -119,6 +143,9 @@ class Fleet {
   void lose(int device);
   // Images served per device for `model` (direct and scattered).
   std::map<int, int64_t> served(const std::string& model) const;
+  // Direct-path forwards run per device for `model` (each may carry several
+  // coalesced queries).
+  std::map<int, int64_t> forwards(const std::string& model) const;
   int rebalances() const { return rebalances_.load(); }
   // The instance of `model` on `device` (nullptr if none): tests, hooks.
   Worker* worker(const std::string& model, int device) const;

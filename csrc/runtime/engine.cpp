@@ -83,7 +83,7 @@ bool EngineOptions::set(const std::string& name, bool v) {
       {"stream_l4s2", &EngineOptions::stream_l4s2}, {"fuse_ds", &EngineOptions::fuse_ds},
       {"bigtile", &EngineOptions::bigtile},         {"fused_pool", &EngineOptions::fused_pool},
       {"fused_head", &EngineOptions::fused_head},   {"fc_small", &EngineOptions::fc_small},
-      {"blaslt_fc", &EngineOptions::blaslt_fc},     {"direct13", &EngineOptions::direct13},
+      {"direct13", &EngineOptions::direct13},
       {"direct27", &EngineOptions::direct27},
       {"fork_ds", &EngineOptions::fork_ds},         {"fp8_3x3", &EngineOptions::fp8_3x3},
       {"conv1x1", &EngineOptions::conv1x1},         {"s2rows", &EngineOptions::s2rows},
@@ -897,31 +897,6 @@ bool Engine::s2rows_ok(const Op& op, const ConvLayer& D, int B) const {
          conv3x3_s2rows_supported(is.H, is.W, is.C, L.cout);
 }
 
-bool Engine::fc_blaslt(const Op& op, int B) const {
-  if (op.type != OpType::Conv) return false;
-  const ConvLayer& L = convs_[op.conv];
-  return opt_.blaslt_fc && L.fc && !L.fp8 && !shapes_[op.in].fp8 && !shapes_[op.out].fp8 &&
-         !(opt_.fc_small && fc_small_supported(B, L.cin, L.cin, L.kpad));
-}
-
-// hipBLASLt plans for this batch's fc layers, picked by timing the heuristic
-// candidates on the real operands: this synchronises, so it runs before a
-// graph capture (and before the first eager forward at a new B). A shape
-// without a plan stays on the implicit-GEMM path.
-void Engine::prepare_fc(int B, float* logits, hipStream_t s) {
-  for (size_t oi = 0; oi < ops_.size(); ++oi) {
-    const Op& op = ops_[oi];
-    if (!fc_blaslt(op, B) || (oi > 0 && head_fusable(oi - 1))) continue;
-    const ConvLayer& L = convs_[op.conv];
-    const ActShape& os = shapes_[op.out];
-    if (!blaslt_) blaslt_ = std::make_unique<BlasLt>(device_);
-    if (blaslt_->ready(B, L.cout, L.cin, L.cin, L.kpad, L.cout, os.f32, L.relu)) continue;
-    const uint8_t* wa = (const uint8_t*)warena_;
-    blaslt_->prepare(B, L.cout, L.cin, L.cin, L.kpad, L.cout, os.f32, L.relu, acts_[op.in], wa + L.w_off,
-                     (const float*)(wa + L.b_off), (os.f32 && logits) ? (void*)logits : acts_[op.out], s);
-  }
-}
-
 bool Engine::side_safe(int B) const {
   for (const Op& op : ops_)
     if (op.type == OpType::Conv && conv_path(op, B) == ConvPath::BigTile) return false;
@@ -996,16 +971,6 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
                    (os.f32 && logits) ? (void*)logits : acts_[op.out], L.cout, os.f32, B, L.cin, L.cout, L.npad,
                    L.relu, cs);
           break;
-        }
-        if (blaslt_ && fc_blaslt(op, B)) {
-          const ActShape& os = shapes_[op.out];
-          if (blaslt_->ready(B, L.cout, L.cin, L.cin, L.kpad, L.cout, os.f32, L.relu)) {
-            const uint8_t* wa = (const uint8_t*)warena_;
-            blaslt_->fc(acts_[op.in], L.cin, wa + L.w_off, L.kpad, (const float*)(wa + L.b_off),
-                        (os.f32 && logits) ? (void*)logits : acts_[op.out], L.cout, os.f32, B, L.cout, L.cin, L.relu,
-                        cs);
-            break;
-          }
         }
         if (L.cat_off && op.res >= 0) {
           // expand conv + its stride-1 downsample as one K-concatenated GEMM
@@ -1245,7 +1210,6 @@ void Engine::forward(const uint8_t* images, int B, int Hin, int Win, int32_t* id
     GraphKey key{images, B, Hin, Win, idx, prob, logits};
     auto it = graphs_.find(key);
     if (it == graphs_.end()) {
-      prepare_fc(B, logits, stream);
       DMLC_HIP_CHECK(hipStreamSynchronize(stream));
       hipGraph_t g;
       DMLC_HIP_CHECK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
@@ -1260,7 +1224,6 @@ void Engine::forward(const uint8_t* images, int B, int Hin, int Win, int32_t* id
     DMLC_HIP_CHECK(hipGraphLaunch(it->second, stream));
   } else {  // eager launches straight onto the caller's stream
     DMLC_TRACE("engine.forward");
-    prepare_fc(B, logits, stream);
     run_ops(images, B, Hin, Win, idx, prob, logits, stream, nullptr, true);
   }
   DMLC_HIP_CHECK(hipEventRecord(ev_out_, stream));
@@ -1273,7 +1236,6 @@ std::vector<std::pair<std::string, float>> Engine::profile(const uint8_t* images
   if (B > max_batch_) throw std::invalid_argument("batch exceeds reserved max_batch");
   DMLC_HIP_CHECK(hipSetDevice(device_));
   DMLC_HIP_CHECK(hipStreamSynchronize(stream));
-  prepare_fc(B, nullptr, stream_);
   std::vector<hipEvent_t> evs(ops_.size() + 1);
   for (auto& e : evs) DMLC_HIP_CHECK(hipEventCreate(&e));
   run_ops(images, B, Hin, Win, nullptr, nullptr, nullptr, stream_, &evs, true);

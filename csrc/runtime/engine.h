@@ -16,7 +16,6 @@
 #include <vector>
 
 #include "../kernels/kernels.h"
-#include "blaslt.h"
 #include "weights.h"
 
 namespace dmlc {
@@ -94,9 +93,6 @@ struct EngineOptions {
   bool direct13 = true;          // AlexNet's 13x13 3x3 convs with the image resident in LDS (conv3x3_13.hip)
   bool direct27 = true;          // AlexNet's 5x5 conv on 27x27x64 the same way (conv5x5_27.hip)
   bool fc_small = true;          // weight-streaming GEMV for fc layers at B <= 16 (fc_small.hip)
-  // bf16 fc layers above that on hipBLASLt (blaslt.h): faster alone, slower in the two-lane bench
-  // (472-485k vs 518-528k img/s AlexNet, profiles/r3_alexnet_blaslt_ab.txt), so off by default
-  bool blaslt_fc = false;
   // downsample convs on a side stream: measured slower (the branch slows its
   // sibling conv1 by 10-12 us and adds ~10 us of fork/join gaps per block:
   // profiles/r1_fork_ds_timeline.txt); kept to test the side-stream path
@@ -137,7 +133,6 @@ class Engine {
   size_t weight_bytes() const { return weight_bytes_; }
   size_t activation_bytes() const { return act_bytes_; }
   double gflop_per_image() const;
-  int blaslt_plans() const { return blaslt_ ? blaslt_->plans() : 0; }  // fc shapes on hipBLASLt (tests)
 
   // Allocate the activation arena for batches up to max_batch.
   void reserve(int max_batch);
@@ -187,8 +182,6 @@ class Engine {
   bool bottleneck_conv3(const ConvLayer& L) const;  // L is such a block's expand conv (fragment-order weights)
   int ds_expand_op(size_t oi) const;  // ops[oi] = a downsample folded into a later expand conv: that op, or -1
   bool s2rows_ok(const Op& op, const ConvLayer& D, int B) const;  // layer2.0 conv1 + downsample -> conv3x3_s2rows
-  bool fc_blaslt(const Op& op, int B) const;  // this fc op runs on hipBLASLt at batch B
-  void prepare_fc(int B, float* logits, hipStream_t s);  // pick hipBLASLt algorithms (outside capture)
 
   std::string arch_;
   int device_ = 0;
@@ -218,7 +211,6 @@ class Engine {
   void* head_ws_ = nullptr;  // fused head partials + per-group tickets
   size_t head_ws_bytes_ = 0;
 
-  std::unique_ptr<BlasLt> blaslt_;  // created on first use (fc layers at B > 16)
 
   hipStream_t stream_ = nullptr;
   hipEvent_t ev_out_ = nullptr;  // end of the last forward (on last_stream_)

@@ -206,7 +206,7 @@ class CpuExecutor : public Executor {
 //     partition, reading the slice in place.
 class GpuExecutor : public Executor {
  public:
-  GpuExecutor(std::vector<int> devices, int max_batch, size_t cache_bytes, int min_shard, int lanes)
+  GpuExecutor(std::vector<int> devices, int max_batch, size_t cache_bytes, int min_shard, int lanes, int batch_window_us)
       : devices_(std::move(devices)), max_batch_(max_batch), lanes_(std::max(1, std::min(lanes, 4))),
         cache_cap_(cache_bytes) {
     if (devices_.empty()) throw std::invalid_argument("GpuExecutor: no devices");
@@ -217,7 +217,8 @@ class GpuExecutor : public Executor {
     o.max_per_rank = max_batch_;
     o.image_bytes = (size_t)kS * kS * 3;
     o.min_shard = std::max(1, min_shard);
-    o.aux_bytes = (size_t)max_batch_ * sizeof(ImageDesc);
+    o.aux_bytes = sizeof(ImageDesc);  // per image: a coalesced request's descriptors at its batch offset
+    o.batch_window_us = batch_window_us;
     fleet_ = std::make_unique<dp::Fleet>(
         devices_, [this](const std::string& m, int d, dp::Worker* rep) { return make_worker(m, d, rep); },
         [](const std::vector<int>& devs) { return comm::rccl_init_all(devs); }, o);
@@ -838,13 +839,13 @@ class GpuExecutor : public Executor {
 }  // namespace
 
 std::unique_ptr<Executor> make_executor(const std::string& backend, const std::vector<int>& devices, int max_batch,
-                                        size_t cache_bytes, int min_shard, int lanes) {
+                                        size_t cache_bytes, int min_shard, int lanes, int batch_window_us) {
   std::string b = backend;
   if (b == "auto") b = hip_device_count() > 0 ? "gpu" : "cpu";
   if (b == "gpu") {
     for (int d : devices)
       if (d < 0 || hip_device_count() <= d) throw std::runtime_error("no HIP device " + std::to_string(d));
-    return std::make_unique<GpuExecutor>(devices, max_batch, cache_bytes, min_shard, lanes);
+    return std::make_unique<GpuExecutor>(devices, max_batch, cache_bytes, min_shard, lanes, batch_window_us);
   }
   if (b == "cpu") return std::make_unique<CpuExecutor>();
   throw std::invalid_argument("unknown executor backend: " + backend);

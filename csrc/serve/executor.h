@@ -98,8 +98,11 @@ std::unique_ptr<Executor> make_executor(const std::string& backend, int device, 
 // its model's partition, and a batch of >= 2 x min_shard images is scattered
 // over the partition with RCCL instead.
 // lanes: concurrent forwards per GPU and model (one model instance each).
+// batch_window_us: concurrent queries to one (model, GPU) instance are
+// coalesced into one forward of up to max_batch images; a queued query waits
+// at most this long for others to join (dp::FleetOptions).
 std::unique_ptr<Executor> make_executor(const std::string& backend, const std::vector<int>& devices, int max_batch,
-                                        size_t cache_bytes, int min_shard, int lanes = 2);
+                                        size_t cache_bytes, int min_shard, int lanes = 2, int batch_window_us = 200);
 int hip_device_count();
 
 // Host-side reference preprocessing (same rule as csrc/kernels/preprocess.hip):

@@ -98,7 +98,7 @@ std::unique_ptr<Executor> make_executor(const std::string& backend, int, int, si
 }
 
 std::unique_ptr<Executor> make_executor(const std::string& backend, const std::vector<int>& devices, int max_batch,
-                                        size_t cache_bytes, int, int) {
+                                        size_t cache_bytes, int, int, int) {
   return make_executor(backend, devices.empty() ? 0 : devices[0], max_batch, cache_bytes);
 }
 

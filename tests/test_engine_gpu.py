@@ -330,36 +330,6 @@ def test_alexnet_small_batch_fc_matches_reference(gpu, B):
     assert torch.equal(idx, i2) and torch.allclose(prob, p2)
 
 
-@pytest.mark.parametrize("B", [64, 256])
-def test_alexnet_blaslt_fc_matches_reference(gpu, B):
-    """Throughput batches run the classifier on hipBLASLt (csrc/runtime/blaslt.cpp,
-    bias + ReLU epilogue, fp32 logits for the last layer): all three fc layers
-    get a plan, and the logits match the implicit-GEMM path (blaslt_fc=False)
-    to bf16 rounding and fp32 torch.nn within 3%, eager and graph replay."""
-    model = build("alexnet", seed=53, randomize_bn=True)
-    sd = state_dict_f32(model)
-    g = torch.Generator().manual_seed(54 + B)
-    img = torch.randint(0, 256, (B, 224, 224, 3), generator=g, dtype=torch.uint8)
-    x = img.to(gpu)
-    eng = InferenceEngine("alexnet", sd, max_batch=B, options={"blaslt_fc": True})
-    idx, prob, logits = eng.predict(x, return_logits=True)
-    i2, p2 = eng.predict(x)
-    _, _, le = eng.predict(x, return_logits=True, use_graph=False)
-    assert eng._e.blaslt_plans >= 3
-    ref_eng = InferenceEngine("alexnet", sd, max_batch=B, options={"blaslt_fc": False})
-    ri, _, rl = ref_eng.predict(x, return_logits=True)
-    assert ref_eng._e.blaslt_plans == 0
-    torch.cuda.synchronize()
-    assert torch.equal(logits, le)
-    rel = ((logits - rl).norm() / rl.norm()).item()
-    assert rel < 1e-2, rel
-    assert torch.equal(idx, i2) and torch.allclose(prob, p2)
-    n = min(B, 32)
-    ref = _ref_logits(model, img[:n])
-    rel = ((logits[:n].cpu() - ref).norm() / ref.norm()).item()
-    assert rel < 3e-2, rel
-
-
 @pytest.mark.parametrize("B", [5, 256])
 def test_alexnet_direct13_matches_igemm(gpu, B):
     """AlexNet's 13x13 convs (features.6/.8/.10) and its 5x5 conv (features.3)

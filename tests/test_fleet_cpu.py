@@ -240,3 +240,106 @@ def test_hot_swap_broadcasts_new_weights_to_every_gpu_of_the_partition():
     finally:
         SEEDS.update(SEEDS_OLD)
     assert f.state()["partitions"] == {"resnet18": [0, 1, 2, 3], "alexnet": [4, 5, 6, 7]}
+
+
+# ---------------------------------------------------------------- coalescing
+# The reference runs each query as its own batch-1 forward under the model's
+# mutex (src/services.rs:475-497); SURVEY.md §7.6 #12 asks for real batching.
+# Concurrent direct queries to one (model, GPU) instance queue there and
+# share forwards of up to max_per_rank images.
+
+def _coalescing_fleet(devices=1, jobs=("resnet18",), max_per_rank=16, window_us=50000, eager=False, delay_us=2000,
+                      lanes=2):
+    f = C.HostFleet(list(range(devices)), H, W, lanes, delay_us, max_per_rank, 4, SEEDS,
+                    batch_window_us=window_us, eager_when_idle=eager)
+    f.set_jobs(list(jobs))
+    for m in jobs:
+        f.load(m)
+    return f
+
+
+@pytest.mark.parametrize("n", [16, 40, 64])
+def test_concurrent_single_image_queries_share_forwards(n):
+    """n concurrent 1-image queries on one GPU: at most ceil(n / max) forwards,
+    every answer exactly once and in order."""
+    f = _coalescing_fleet()
+    imgs = _imgs(n, seed=20)
+    qs = [("resnet18", i, 1) for i in range(n)]
+    out = f.run(imgs, qs, threads=n)
+    _check(out, imgs, qs)
+    st = f.state()
+    assert st["served"]["resnet18"][0] == n
+    assert st["forwards"]["resnet18"][0] <= -(-n // 16), st["forwards"]
+
+
+def test_eager_idle_first_query_goes_alone_then_batches():
+    """Serving default: an idle instance runs the first query at once (no
+    batching delay for a lone query); queries arriving while it runs batch."""
+    f = _coalescing_fleet(eager=True, window_us=20000, delay_us=20000)
+    imgs = _imgs(33, seed=21)
+    qs = [("resnet18", i, 1) for i in range(33)]
+    out = f.run(imgs, qs, threads=33)
+    _check(out, imgs, qs)
+    fw = f.state()["forwards"]["resnet18"][0]
+    assert fw <= 1 + -(-32 // 16) + 1, fw  # the lone first, the rest in (nearly) full batches
+    # a lone query on an idle instance: one forward, no window wait
+    out = f.run(imgs, [("resnet18", 3, 1)], threads=1)
+    _check(out, imgs, [("resnet18", 3, 1)])
+
+
+def test_large_query_chunks_run_on_every_lane():
+    """A direct query bigger than max_per_rank is cut into max-sized chunks
+    queued together: one forward per chunk, issued on both lanes at once."""
+    f = _coalescing_fleet(window_us=0, delay_us=1000)
+    imgs = _imgs(5 * 16 + 3, seed=22)
+    qs = [("resnet18", 0, 5 * 16 + 3)]
+    out = f.run(imgs, qs, threads=1)
+    _check(out, imgs, qs)
+    assert f.state()["forwards"]["resnet18"][0] == 6
+
+
+def test_coalesced_queries_mixed_sizes_exactly_once_in_order():
+    f = _coalescing_fleet(devices=4, jobs=("resnet18", "alexnet"), window_us=2000, delay_us=1500)
+    imgs = _imgs(400, seed=23)
+    qs = _small_queries(400, 200, seed=24, max_n=12)
+    out = f.run(imgs, qs, threads=48)
+    _check(out, imgs, qs)
+    st = f.state()
+    for model in ("resnet18", "alexnet"):
+        imgs_model = sum(c for m, _, c in qs if m == model)
+        assert sum(st["served"][model].values()) == imgs_model
+        assert sum(st["forwards"][model].values()) < sum(1 for m, _, _ in qs if m == model)  # some shared
+
+
+def test_coalesced_queries_survive_gpu_failure_exactly_once():
+    """A GPU dies while coalesced batches are queued and running on it: every
+    query is still answered exactly once and in order (the lost GPU's
+    requests are redone on the rebalanced fleet)."""
+    f = _coalescing_fleet(devices=4, jobs=("resnet18", "alexnet"), window_us=3000, delay_us=2000)
+    imgs = _imgs(300, seed=25)
+    qs = [("resnet18" if i % 3 else "alexnet", (7 * i) % 290, 1 + i % 4) for i in range(150)]
+    f.fail(1)
+    out = f.run(imgs, qs, threads=40)
+    _check(out, imgs, qs)
+    st = f.state()
+    assert 1 not in st["live"]
+    assert any(r["retries"] > 0 for r in out["routes"])
+    assert st["partitions"] == {"resnet18": [0], "alexnet": [2, 3]}
+
+
+def test_failed_worker_build_keeps_serving_and_retries():
+    """A worker build that fails during a rebalance (OOM, HIP error) leaves
+    the model on its old GPUs without a group: queries still run (direct, no
+    scatter through a half-built group) and the next query retries the
+    rebalance (fleet.cpp:270)."""
+    f = _fleet(delay_us=0)
+    f.fail_next_builds(1)
+    with pytest.raises(Exception):
+        f.lose(5)  # GPU 3 moves to alexnet: its replica build fails
+    imgs = _imgs(200, seed=26)
+    qs = [("alexnet", 0, 100), ("resnet18", 10, 3), ("alexnet", 5, 2)]
+    out = f.run(imgs, qs, threads=3)  # rebalances again first (build succeeds now)
+    _check(out, imgs, qs)
+    st = f.state()
+    assert st["partitions"] == {"resnet18": [0, 1, 2], "alexnet": [3, 4, 6, 7]}
+    assert st["overlapping_worlds"] == []

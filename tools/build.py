@@ -107,7 +107,7 @@ HIPCC_FILE_FLAGS = {"stem_pool.hip": ["-fno-honor-nans"]}
 
 def gpu_objects():
     srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
-    srcs += [os.path.join(CSRC, "runtime", "engine.cpp"), os.path.join(CSRC, "runtime", "blaslt.cpp")]
+    srcs += [os.path.join(CSRC, "runtime", "engine.cpp")]
     srcs += sorted(glob.glob(os.path.join(CSRC, "comm", "*.cpp")))
     return srcs
 
@@ -209,7 +209,7 @@ def build(jobs: int = 8, verbose: bool = False, node: bool = True) -> None:
     libgpu = os.path.join(PKG, "libdmlc_gpu.so")
     if _stale(libgpu, gpu_objs, 0):
         _run(["hipcc", "-shared", "-fPIC", f"--offload-arch={ARCH}", *gpu_objs, "-o", libgpu,
-              f"-L{ROCM}/lib", "-lrocprofiler-sdk-roctx", "-lrccl", "-lhipblaslt", f"-Wl,-rpath,{ROCM}/lib"], verbose)
+              f"-L{ROCM}/lib", "-lrocprofiler-sdk-roctx", "-lrccl", f"-Wl,-rpath,{ROCM}/lib"], verbose)
 
     pymod = os.path.join(PKG, "_C" + ext)
     if _stale(pymod, py_objs + [libgpu], 0):
