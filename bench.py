@@ -59,7 +59,11 @@ if ROOT not in sys.path:
 REF_MEAN_LATENCY_MS = 158.94  # ResNet18, CS425MP4Report.pdf p.2 §1a
 REF_STREAM_IMG_S = 1000.0 / REF_MEAN_LATENCY_MS
 # rank 0's share in scatter mode (it also runs the 7 send legs): its forward
-# next to RCCL kernels is ~1.2x slower (profiles/r2_rccl_interference.txt)
+# next to RCCL kernels is ~1.2x slower (profiles/r2_rccl_interference.txt).
+# That was measured with one rank; at N > 1 bench.py starts from it and
+# calibrates (--coord-weight auto, csrc/comm/runner.h Runner::calibrate):
+# rounds of pipelined steps, every rank's forward time all-gathered, rank 0's
+# count re-solved until its forward time matches the slowest other rank's.
 COORD_WEIGHT = 0.85
 
 
@@ -102,9 +106,11 @@ def main():
     ap.add_argument("--model", default="resnet18")
     ap.add_argument("--batch", type=int, default=256, help="images per GPU per step")
     ap.add_argument("--input-mode", choices=["staged", "scatter", "local"], default="scatter")
-    ap.add_argument("--coord-weight", type=float, default=None,
-                    help="rank 0's share of a step as a fraction of a fair share (scatter mode; default "
-                         f"{COORD_WEIGHT} at N > 1, 1 at N = 1)")
+    ap.add_argument("--coord-weight", default="auto",
+                    help="rank 0's share of a step as a fraction of a fair share (scatter mode): a number, or "
+                         f"'auto' (N > 1: calibrated during the prime steps starting from {COORD_WEIGHT}; N = 1: 1)")
+    ap.add_argument("--calib-rounds", type=int, default=5, help="coordinator-share calibration rounds (auto)")
+    ap.add_argument("--calib-steps", type=int, default=8, help="pipelined steps per calibration round")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--engine-opt", action="append", default=[], metavar="NAME=0|1",
                     help="engine kernel-path switch (EngineOptions field), for A/B runs; repeatable")
@@ -156,7 +162,11 @@ def main():
         box = [[C.rccl_unique_id(), C.rccl_unique_id()] if rank == 0 else None]
         dist.broadcast_object_list(box, src=0)
         ids = box[0]
-    coord_weight = args.coord_weight if args.coord_weight is not None else (COORD_WEIGHT if world > 1 else 1.0)
+    auto_weight = args.coord_weight == "auto" and world > 1 and scatter
+    if args.coord_weight == "auto":
+        coord_weight = COORD_WEIGHT if world > 1 else 1.0
+    else:
+        coord_weight = float(args.coord_weight)
     if not scatter:
         coord_weight = 1.0  # nothing to send per step: an even split
     runner = C.DpRunner(eng._e, world, rank, ids[0], ids[1], B, scatter=scatter, use_graph=use_graph,
@@ -194,8 +204,20 @@ def main():
     # Setup: prime the pipeline (hipGraph capture of every slot, RCCL
     # channels, and ~35 ms of load so the GPU leaves its idle clocks; a fixed
     # step count, the same on every rank), then the W warmup steps.
+    calibration = None
     if args.prime_steps > 0:
         runner.run(pool_ptr, n_pool, 0, args.prime_steps)
+        barrier()
+    if auto_weight and args.calib_rounds > 0:
+        def allgather(x):
+            t = torch.tensor([x], dtype=torch.float64)
+            out = [torch.zeros(1, dtype=torch.float64) for _ in range(world)]
+            dist.all_gather(out, t)
+            return [float(v) for v in out]
+        calibration = runner.calibrate(pool_ptr, n_pool, args.prime_steps, args.calib_steps, args.calib_rounds,
+                                       0.05, allgather)
+        coord_weight = calibration["weight"]
+        counts = runner.counts
         barrier()
     runner.run(pool_ptr, n_pool, 0, args.warmup)
     barrier()
@@ -219,7 +241,7 @@ def main():
 
     if rank == 0:
         idx, prob = runner.last_results()
-        assert len(idx) == B * world
+        assert len(idx) == sum(counts)
         assert min(idx) >= 0 and max(idx) < 1000, "bad class ids"
         assert min(prob) > 0 and max(prob) <= 1.0001, "bad probabilities"
 
@@ -282,7 +304,8 @@ def main():
                 "global_batch": sum(counts),
                 "per_gpu_batch": B,
                 "per_rank_counts": counts,
-                "coord_weight": coord_weight,
+                "coord_weight": round(coord_weight, 4),
+                "coord_weight_mode": "calibrated" if calibration else ("fixed" if world > 1 else "n/a"),
                 "seq_len": None,
                 "image_size": 224,
                 "parallelism": f"dp{world}",
@@ -311,6 +334,9 @@ def main():
             "gpu_batch1_latency_p95_ms": round(pct(qlat, 95), 4) if qlat else None,
             "tflops_effective": round(value * eng.gflop_per_image / 1e3, 1),
         }
+        if calibration:
+            res["calibration"] = [{k: (round(v, 4) if isinstance(v, float) else v) for k, v in r.items()}
+                                  for r in calibration["rounds"]]
         if ops_profile:
             print("# per-op (ms): " + ", ".join(f"{n}={t:.3f}" for n, t in ops_profile), file=sys.stderr)
         print(json.dumps(res), flush=True)

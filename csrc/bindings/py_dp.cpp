@@ -74,6 +74,40 @@ class DpRunner {
     d["steps"] = res.steps;
     d["images"] = res.images;
     d["step_ms"] = res.step_ms;
+    d["busy_ms"] = res.busy_ms;
+    return d;
+  }
+  void set_counts(const std::vector<int>& c) { r_->set_counts(c); }
+  // allgather: Python callable, float -> list of every rank's float (bench.py:
+  // torch.distributed over gloo); called with the GIL held
+  py::dict calibrate(uintptr_t pool, int64_t pool_images, int64_t first, int64_t steps, int rounds, double tol,
+                     py::function allgather, double min_weight) {
+    dp::Runner::AllGather ag = [&allgather](double x) {
+      py::gil_scoped_acquire gil;
+      return allgather(x).cast<std::vector<double>>();
+    };
+    dp::Runner::Calibration c;
+    {
+      py::gil_scoped_release nogil;
+      c = r_->calibrate((const uint8_t*)pool, pool_images, first, steps, rounds, tol, ag, min_weight);
+    }
+    return calib_dict(c);
+  }
+  static py::dict calib_dict(const dp::Runner::Calibration& c) {
+    py::dict d;
+    d["weight"] = c.weight;
+    d["steps"] = c.steps;
+    py::list rs;
+    for (const auto& r : c.rounds) {
+      py::dict x;
+      x["weight"] = r.weight;
+      x["coord_count"] = r.coord_count;
+      x["busy_coord_ms"] = r.busy_coord;
+      x["busy_worker_ms"] = r.busy_worker;
+      x["rate"] = r.rate();
+      rs.append(x);
+    }
+    d["rounds"] = rs;
     return d;
   }
   py::tuple last_results() const { return py::make_tuple(r_->last_idx(), r_->last_prob()); }
@@ -98,8 +132,37 @@ class DpRunner {
 // communicator, one thread per rank (= one process per GPU). `pool`: two
 // global batches on the coordinator. Returns per rank the steps of each run
 // and on rank 0 whether the last step's answers match its images.
+// All-gather of one double per thread-rank (the host stand-in for bench.py's
+// gloo all_gather): every rank's call returns once all have contributed.
+class ThreadAllGather {
+ public:
+  explicit ThreadAllGather(int world) : world_(world), vals_(world) {}
+  std::vector<double> operator()(int rank, double x) {
+    std::unique_lock<std::mutex> g(mu_);
+    const int64_t gen = gen_;
+    vals_[rank] = x;
+    if (++arrived_ == world_) {
+      out_ = vals_;
+      arrived_ = 0;
+      ++gen_;
+      cv_.notify_all();
+    } else {
+      cv_.wait(g, [&] { return gen_ != gen; });
+    }
+    return out_;
+  }
+
+ private:
+  int world_, arrived_ = 0;
+  int64_t gen_ = 0;
+  std::vector<double> vals_, out_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+};
+
 py::dict dp_host_bench(py::array_t<uint8_t, py::array::c_style> pool, int world, int per_rank, double coord_weight,
-                       const std::string& input_mode, int lanes, int prime, int warmup, int steps, int latency) {
+                       const std::string& input_mode, int lanes, int prime, int warmup, int steps, int latency,
+                       int us_per_image, int coord_extra_us, int calib_rounds, int calib_steps) {
   if (pool.ndim() != 4 || pool.shape(3) != 3) throw std::invalid_argument("pool must be u8 [n,H,W,3]");
   const int H = (int)pool.shape(1), W = (int)pool.shape(2);
   const size_t ib = (size_t)H * W * 3;
@@ -116,14 +179,18 @@ py::dict dp_host_bench(py::array_t<uint8_t, py::array::c_style> pool, int world,
   std::vector<int32_t> last_idx;
   std::vector<float> last_prob;
   int64_t last_step = -1;
+  std::vector<int> final_counts;
+  dp::Runner::Calibration calib;
+  ThreadAllGather ag(world);
   {
     py::gil_scoped_release nogil;
     std::vector<std::thread> ts;
     for (int r = 0; r < world; ++r)
       ts.emplace_back([&, r] {
         try {
-          dp::Runner run(dp::make_host_worker(r, H, W, 1000, lanes), world > 1 ? std::move(cin[r]) : nullptr,
-                         world > 1 ? std::move(cout[r]) : nullptr, world, r, counts, scatter, ib, 5000);
+          dp::Runner run(dp::make_host_worker(r, H, W, 1000, lanes, 0, 0, us_per_image, r == 0 ? coord_extra_us : 0),
+                         world > 1 ? std::move(cin[r]) : nullptr, world > 1 ? std::move(cout[r]) : nullptr, world, r,
+                         counts, scatter, ib, 5000);
           std::vector<uint8_t> mine;
           const uint8_t* p = r == 0 ? src : nullptr;
           int64_t np = r == 0 ? 2 * G : 0;
@@ -136,6 +203,11 @@ py::dict dp_host_bench(py::array_t<uint8_t, py::array::c_style> pool, int world,
           }
           std::vector<int64_t> d;
           d.push_back(run.run(p, np, 0, prime).steps);
+          if (calib_rounds > 0) {
+            auto c = run.calibrate(p, np, prime, calib_steps, calib_rounds, 0.05,
+                                   [&](double x) { return ag(r, x); });
+            if (r == 0) calib = c;
+          }
           d.push_back(run.run(p, np, 0, warmup).steps);
           d.push_back(run.run(p, np, warmup, steps).steps);
           d.push_back(run.run(p, np, warmup + steps, latency, /*pipelined=*/false).steps);
@@ -144,6 +216,7 @@ py::dict dp_host_bench(py::array_t<uint8_t, py::array::c_style> pool, int world,
             last_idx = run.last_idx();
             last_prob = run.last_prob();
             last_step = warmup + steps + latency - 1;
+            final_counts = run.counts();
           }
         } catch (const std::exception& e) {
           errs[r] = e.what();
@@ -153,15 +226,20 @@ py::dict dp_host_bench(py::array_t<uint8_t, py::array::c_style> pool, int world,
   }
   for (int r = 0; r < world; ++r)
     if (!errs[r].empty()) throw std::runtime_error("rank " + std::to_string(r) + ": " + errs[r]);
-  // the last step read global batch (last_step % 2): answers in image order
-  bool ok = last_idx.size() == (size_t)G;
-  const uint8_t* b = src + (size_t)(last_step % 2) * G * ib;
-  for (int64_t i = 0; ok && i < G; ++i)
+  // the last step read global batch (last_step % nb) at a stride of the
+  // final counts' total (calibration may have lowered the coordinator's)
+  int64_t Gf = 0;
+  for (int c : final_counts) Gf += c;
+  const int64_t nb = scatter ? std::max<int64_t>(1, 2 * G / std::max<int64_t>(1, Gf)) : 2;
+  bool ok = (int64_t)last_idx.size() == Gf;
+  const uint8_t* b = src + (size_t)(scatter ? (last_step % nb) * Gf : (last_step % 2) * G) * ib;
+  for (int64_t i = 0; ok && i < Gf; ++i)
     ok = last_idx[i] == dp::host_class_of(b + i * ib, ib) && last_prob[i] == dp::host_prob_of(b + i * ib);
   py::dict out;
   out["steps"] = done;
-  out["counts"] = counts;
+  out["counts"] = final_counts;
   out["answers_ok"] = ok;
+  out["calibration"] = DpRunner::calib_dict(calib);
   return out;
 }
 
@@ -212,7 +290,7 @@ class DpGroupPy {
 // ------------------------------------------------------------------ host
 py::dict dp_host_run(py::array_t<uint8_t, py::array::c_style> images, int world, int max_per_rank,
                      const std::string& mode, bool scatter, int fail_member, int64_t fail_after, bool abrupt,
-                     bool pipelined, int slots) {
+                     bool pipelined, int slots, int us_per_image, int coord_extra_us, int repeats, bool auto_balance) {
   if (images.ndim() != 4 || images.shape(3) != 3) throw std::invalid_argument("images must be u8 [n,H,W,3]");
   const int64_t n = images.shape(0);
   const int H = (int)images.shape(1), W = (int)images.shape(2);
@@ -231,7 +309,7 @@ py::dict dp_host_run(py::array_t<uint8_t, py::array::c_style> images, int world,
     std::vector<std::unique_ptr<dp::Worker>> owned;
     std::vector<dp::Worker*> ws;
     for (int r = 0; r < world; ++r) {
-      owned.push_back(dp::make_host_worker(r, H, W));
+      owned.push_back(dp::make_host_worker(r, H, W, 1000, 1, 0, 0, us_per_image, r == 0 ? coord_extra_us : 0));
       ws.push_back(owned.back().get());
     }
     std::vector<std::vector<int>> builds;
@@ -241,13 +319,20 @@ py::dict dp_host_run(py::array_t<uint8_t, py::array::c_style> images, int world,
     };
     dp::Group::Stats st;
     std::vector<int> members;
+    std::vector<double> weights;
     {
       py::gil_scoped_release nogil;
       dp::Group g(ws, factory, max_per_rank, ib, 5000);
+      g.set_coord_weight(1.0, auto_balance);
       if (fail_member >= 0) g.fail(fail_member, fail_after, abrupt);
-      st = g.classify(src, n, pi, pp, -1, pc);
+      for (int k = 0; k < std::max(1, repeats); ++k) {
+        if (k > 0) std::fill(pc, pc + n, 0);
+        st = g.classify(src, n, pi, pp, -1, pc);
+        weights.push_back(g.coord_weight());
+      }
       members = g.members();
     }
+    out["coord_weights"] = weights;
     out["stats"] = DpGroupPy::stats(st);
     out["members"] = members;
     out["builds"] = builds;
@@ -609,10 +694,22 @@ void bind_dp(py::module& m) {
   m.def("dp_weighted_counts", &dp::weighted_counts, py::arg("per_rank"), py::arg("world"), py::arg("coord_weight"));
   m.def("dp_host_bench", &dp_host_bench, py::arg("pool"), py::arg("world"), py::arg("per_rank"),
         py::arg("coord_weight") = 1.0, py::arg("input_mode") = "scatter", py::arg("lanes") = 2, py::arg("prime") = 3,
-        py::arg("warmup") = 2, py::arg("steps") = 5, py::arg("latency") = 3);
+        py::arg("warmup") = 2, py::arg("steps") = 5, py::arg("latency") = 3, py::arg("us_per_image") = 0,
+        py::arg("coord_extra_us") = 0, py::arg("calib_rounds") = 0, py::arg("calib_steps") = 4);
+  m.def("dp_weighted_shards", &dp::weighted_shards, py::arg("n"), py::arg("world"), py::arg("cap"), py::arg("w0"));
+  m.def("dp_next_coord_weight",
+        [](double w, double b0, double bw, int c0, int per, int world, double min_w) {
+          dp::CalibRound r;
+          r.weight = w, r.busy_coord = b0, r.busy_worker = bw, r.coord_count = c0, r.per_rank = per, r.world = world;
+          return dp::next_coord_weight(r, min_w);
+        },
+        py::arg("weight"), py::arg("busy_coord"), py::arg("busy_worker"), py::arg("coord_count"), py::arg("per_rank"),
+        py::arg("world"), py::arg("min_weight") = 0.5);
   m.def("dp_host_run", &dp_host_run, py::arg("images"), py::arg("world"), py::arg("max_per_rank"),
         py::arg("mode") = "group", py::arg("scatter") = true, py::arg("fail_member") = -1,
-        py::arg("fail_after") = 0, py::arg("abrupt") = false, py::arg("pipelined") = true, py::arg("slots") = 2);
+        py::arg("fail_after") = 0, py::arg("abrupt") = false, py::arg("pipelined") = true, py::arg("slots") = 2,
+        py::arg("us_per_image") = 0, py::arg("coord_extra_us") = 0, py::arg("repeats") = 1,
+        py::arg("auto_balance") = true);
   py::class_<DpRunner>(m, "DpRunner")
       .def(py::init([](Engine* e, int world, int rank, py::bytes id_in, py::bytes id_out, int max_per_rank,
                        bool scatter, int image_size, bool use_graph, int timeout_ms, int lanes, int slots,
@@ -630,6 +727,9 @@ void bind_dp(py::module& m) {
       .def("compute_stream", &DpRunner::compute_stream)
       .def("sync", &DpRunner::sync)
       .def("stage", &DpRunner::stage, py::arg("src"), py::arg("dst"))
+      .def("set_counts", &DpRunner::set_counts, py::arg("counts"))
+      .def("calibrate", &DpRunner::calibrate, py::arg("pool"), py::arg("pool_images"), py::arg("first"),
+           py::arg("steps"), py::arg("rounds"), py::arg("tol"), py::arg("allgather"), py::arg("min_weight") = 0.5)
       .def_property_readonly("counts", [](const DpRunner& r) { return r.r_->counts(); })
       .def_property_readonly("max_per_rank", [](const DpRunner& r) { return r.r_->max_per_rank(); });
   py::class_<DpGroupPy>(m, "DpGroup")

@@ -3,6 +3,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cmath>
 #include <mutex>
 #include <cstdlib>
 #include <cstring>
@@ -16,9 +17,10 @@ namespace {
 
 class HostWorker : public Worker {
  public:
-  HostWorker(int device, int H, int W, int classes, int lanes, uint32_t seed, int delay_us)
+  HostWorker(int device, int H, int W, int classes, int lanes, uint32_t seed, int delay_us, int us_per_image,
+             int extra_us)
       : device_(device), bytes_((size_t)H * W * 3), classes_(classes), lanes_(std::max(1, lanes)),
-        delay_us_(delay_us), busy_(lanes_) {
+        delay_us_(delay_us), us_per_image_(us_per_image), extra_us_(extra_us), busy_(lanes_) {
     for (auto& b : busy_) b = false;
     std::memcpy(arena_, &seed, 4);
   }
@@ -31,8 +33,20 @@ class HostWorker : public Worker {
   void* alloc_host(size_t bytes) override { return alloc(bytes); }
   void dealloc_host(void* p) override { untrack(p); }
   Stream stream(int) override { return nullptr; }
-  int new_event() override { return n_events_++; }
-  void record(int, int) override {}
+  int new_event() override {
+    std::lock_guard<std::mutex> g(mu_);
+    stamps_.emplace_back();
+    return n_events_++;
+  }
+  // synchronous "streams": an event's time is the time it was recorded
+  void record(int ev, int) override {
+    std::lock_guard<std::mutex> g(mu_);
+    stamps_.at(ev) = std::chrono::steady_clock::now();
+  }
+  double elapsed_ms(int a, int b) override {
+    std::lock_guard<std::mutex> g(mu_);
+    return std::chrono::duration<double, std::milli>(stamps_.at(b) - stamps_.at(a)).count();
+  }
   void wait(int, int) override {}
   bool query(int) override { return true; }
   void sync(int) override {}
@@ -45,7 +59,8 @@ class HostWorker : public Worker {
     if (busy_[lane].exchange(true)) throw std::logic_error("host worker: lane used concurrently");
     uint32_t w;
     std::memcpy(&w, arena_, 4);
-    if (delay_us_ > 0) std::this_thread::sleep_for(std::chrono::microseconds(delay_us_));
+    const int64_t us = delay_us_ + (int64_t)us_per_image_ * B + extra_us_;
+    if (us > 0) std::this_thread::sleep_for(std::chrono::microseconds(us));
     for (int b = 0; b < B; ++b) {
       const uint8_t* img = images + (size_t)b * bytes_;
       idx[b] = (int32_t)(((uint64_t)host_class_of(img, bytes_, 1 << 30) + w) % (uint64_t)classes_);
@@ -77,10 +92,11 @@ class HostWorker : public Worker {
   }
   int device_;
   size_t bytes_;
-  int classes_, lanes_, delay_us_;
+  int classes_, lanes_, delay_us_, us_per_image_, extra_us_;
   std::vector<std::atomic<bool>> busy_;
   uint8_t arena_[16] = {};
-  std::atomic<int> n_events_{0};
+  int n_events_ = 0;
+  std::vector<std::chrono::steady_clock::time_point> stamps_;
   std::mutex mu_;
   std::vector<void*> live_;
 };
@@ -88,8 +104,8 @@ class HostWorker : public Worker {
 }  // namespace
 
 std::unique_ptr<Worker> make_host_worker(int device, int H, int W, int classes, int lanes, uint32_t seed,
-                                         int delay_us) {
-  return std::make_unique<HostWorker>(device, H, W, classes, lanes, seed, delay_us);
+                                         int delay_us, int us_per_image, int extra_us) {
+  return std::make_unique<HostWorker>(device, H, W, classes, lanes, seed, delay_us, us_per_image, extra_us);
 }
 
 void host_worker_set_healthy(Worker& w, bool healthy) {
@@ -105,6 +121,47 @@ int host_class_of(const uint8_t* img, size_t bytes, int classes) {
 }
 
 float host_prob_of(const uint8_t* img) { return (img[0] + 1) / 257.f; }
+
+double CalibRound::rate() const {
+  const double pace = std::max(busy_coord, busy_worker);
+  const double images = coord_count + (double)per_rank * (world - 1);
+  return pace > 0.0 ? images / pace : 0.0;
+}
+
+double next_coord_weight(const CalibRound& r, double min_weight) {
+  if (!(r.busy_coord > 0.0) || !(r.busy_worker > 0.0)) return r.weight;
+  const double w = r.weight * r.busy_worker / r.busy_coord;
+  return std::max(min_weight, std::min(1.0, w));
+}
+
+double best_coord_weight(const std::vector<CalibRound>& rounds) {
+  double best = 1.0, rate = -1.0;
+  for (const auto& r : rounds) {
+    const double x = r.rate();
+    if (x > rate * 1.0005 || (x >= rate * 0.9995 && r.weight > best)) {
+      rate = std::max(rate, x);
+      best = r.weight;
+    }
+  }
+  return best;
+}
+
+std::vector<int> weighted_shards(int64_t n, int world, int cap, double w0) {
+  if (world <= 1 || w0 >= 1.0) return shard_counts(n, world, cap);
+  if (!(w0 > 0.0)) throw std::invalid_argument("weighted_shards: w0 must be in (0, 1]");
+  const int cap0 = std::max(1, std::min(cap, (int)std::lround(cap * w0)));
+  const int64_t room = (int64_t)cap0 + (int64_t)cap * (world - 1);
+  if (n < 0 || n > room) throw std::invalid_argument("weighted_shards: n exceeds the step's capacity");
+  int64_t c0 = std::min<int64_t>(cap0, std::llround((double)n * w0 / (w0 + world - 1)));
+  int64_t rest = n - c0;
+  if (rest > (int64_t)cap * (world - 1)) {  // the others are full: the coordinator takes the overflow
+    c0 += rest - (int64_t)cap * (world - 1);
+    rest = (int64_t)cap * (world - 1);
+  }
+  std::vector<int> out{(int)c0};
+  for (int c : shard_counts(rest, world - 1, cap)) out.push_back(c);
+  return out;
+}
 
 std::vector<int> shard_counts(int64_t n, int world, int cap) {
   if (world < 1) throw std::invalid_argument("shard_counts: world < 1");
@@ -123,7 +180,10 @@ Rank::Rank(Worker* w, int max_per_rank, size_t image_bytes, bool scatter, int sl
     ev_in_.push_back(w_->new_event());
     ev_comp_.push_back(w_->new_event());
     ev_out_.push_back(w_->new_event());
+    ev_t0_.push_back(w_->new_timing_event());
+    ev_t1_.push_back(w_->new_timing_event());
   }
+  slot_n_.assign(slots_, -1);
   inbuf_.assign(slots_, nullptr);
   ans_.assign(slots_, nullptr);
   host_ans_.assign(slots_, nullptr);
@@ -148,6 +208,7 @@ Rank::~Rank() {
 void Rank::reset() {
   in_used_.assign(slots_, false);
   out_used_.assign(slots_, false);
+  slot_n_.assign(slots_, -1);
 }
 
 void Rank::attach(Comm* in, Comm* out) {
@@ -179,6 +240,16 @@ void Rank::attach(Comm* in, Comm* out) {
   if (root())
     for (auto& p : host_ans_)
       if (!p) p = w_->alloc_host((size_t)ans_world_ * block_bytes());
+}
+
+void Rank::settle_busy() {
+  for (int s = 0; s < slots_; ++s)
+    if (slot_n_[s] > 0 && w_->query(ev_t1_[s])) {
+      busy_ms_ += w_->elapsed_ms(ev_t0_[s], ev_t1_[s]);
+      ++busy_steps_;
+      busy_images_ += slot_n_[s];
+      slot_n_[s] = -1;
+    }
 }
 
 void Rank::post_input(const StepPlan& p) {
@@ -219,8 +290,11 @@ void Rank::compute(const StepPlan& p) {
   auto* blk = (uint8_t*)ans_[s];
   if (n > 0) {
     if (!img) throw std::invalid_argument("dp::Rank::compute: no images for this rank");
+    w_->record(ev_t0_[s], cs);
     w_->classify(img, n, (int32_t*)blk, (float*)(blk + (size_t)max_ * 4), lane);
+    w_->record(ev_t1_[s], cs);
   }
+  slot_n_[s] = n > 0 ? n : -1;
   w_->record(ev_comp_[s], cs);
   in_used_[s] = true;
 }
@@ -256,6 +330,12 @@ void Rank::wait_step(const StepPlan& p, int timeout_ms) {
       throw comm::CommError("dp: step " + std::to_string(p.step) + " timed out");
     if (++spins > 64) std::this_thread::sleep_for(std::chrono::microseconds(20));
   }
+  if (slot_n_[s] > 0) {  // the step's forward is complete: account its time
+    busy_ms_ += w_->elapsed_ms(ev_t0_[s], ev_t1_[s]);
+    ++busy_steps_;
+    busy_images_ += slot_n_[s];
+    slot_n_[s] = -1;
+  }
 }
 
 void Rank::collect(const StepPlan& p, int32_t* idx, float* prob, int timeout_ms) {
@@ -280,6 +360,13 @@ PipelineResult run_pipeline(const std::vector<Rank*>& ranks, int64_t first, int6
                             const ResultFn& on_result, int timeout_ms, bool pipelined) {
   PipelineResult res;
   if (n <= 0 || ranks.empty()) return res;
+  Rank* timed = ranks.front();
+  const double busy0 = timed->busy_ms();
+  const int64_t bsteps0 = timed->busy_steps();
+  auto busy_mean = [&]() {
+    const int64_t k = timed->busy_steps() - bsteps0;
+    return k > 0 ? (timed->busy_ms() - busy0) / (double)k : 0.0;
+  };
   Comm* gcomm = ranks.front()->comm_in();  // null for a world of one
   size_t root_i = ranks.size();
   for (size_t i = 0; i < ranks.size(); ++i)
@@ -345,6 +432,7 @@ PipelineResult run_pipeline(const std::vector<Rank*>& ranks, int64_t first, int6
       finish(i);
       res.step_ms.push_back(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
     }
+    res.busy_ms = busy_mean();
     return res;
   }
   // steps in flight = the ranks' slot count (2: the host collects step i-1
@@ -359,6 +447,7 @@ PipelineResult run_pipeline(const std::vector<Rank*>& ranks, int64_t first, int6
     if (i - first >= depth - 1) finish(i - (depth - 1));
   }
   for (int64_t j = std::max(first, end - (depth - 1)); j < end; ++j) finish(j);
+  res.busy_ms = busy_mean();
   return res;
 }
 
@@ -431,6 +520,31 @@ void Group::kill_now(int m) {
   }
 }
 
+void Group::set_coord_weight(double w, bool auto_balance) {
+  if (!(w > 0.0) || w > 1.0) throw std::invalid_argument("dp::Group: coord_weight must be in (0, 1]");
+  coord_weight_ = w;
+  auto_balance_ = auto_balance;
+}
+
+// Per-image forward time of the coordinator vs the slowest other rank over
+// the last run: the weight that equalises them under a time ~ images model,
+// half-way from the current one (serving batches vary; a step's fixed costs
+// are not linear in its images).
+void Group::rebalance_coord(const std::vector<Rank*>& rs) {
+  for (Rank* r : rs) r->settle_busy();
+  auto per_image = [](const Rank* r) {
+    return r->busy_images() > 0 ? r->busy_ms() / (double)r->busy_images() : 0.0;
+  };
+  const double t0 = per_image(rs.front());
+  double tw = 0.0;
+  for (size_t i = 1; i < rs.size(); ++i) tw = std::max(tw, per_image(rs[i]));
+  if (t0 > 0.0 && tw > 0.0) {
+    const double target = std::max(0.5, std::min(1.0, tw / t0));
+    coord_weight_ = std::max(0.5, std::min(1.0, 0.5 * coord_weight_ + 0.5 * target));
+  }
+  for (Rank* r : rs) r->reset_busy();
+}
+
 Group::Stats Group::classify(const uint8_t* src, int64_t n, int32_t* idx, float* prob, int src_event,
                              int32_t* commit_count) {
   Stats st;
@@ -439,7 +553,8 @@ Group::Stats Group::classify(const uint8_t* src, int64_t n, int32_t* idx, float*
   int64_t issued = 0;     // images whose step was planned (posted) in the current attempt
   while (committed < n) {
     const int world = (int)members_.size();
-    const int64_t G = (int64_t)max_ * world;
+    const double w0 = world > 1 ? coord_weight_ : 1.0;
+    const int64_t G = (int64_t)max_ * (world - 1) + std::max(1, std::min(max_, (int)std::lround(max_ * w0)));
     const int64_t base = committed;
     const int64_t steps = (n - base + G - 1) / G;
     issued = base;
@@ -466,7 +581,10 @@ Group::Stats Group::classify(const uint8_t* src, int64_t n, int32_t* idx, float*
       // to stay under max_ per rank)
       const int64_t want = std::max<int64_t>(nstep / min_per_rank_, (nstep + max_ - 1) / max_);
       const int used = (int)std::min<int64_t>(world, std::max<int64_t>(1, want));
-      p.counts = shard_counts(nstep, used, max_);
+      // (with fewer ranks than the group, the step may not fit their caps
+      // weighted: an even split then)
+      const bool weighted = used == world && w0 < 1.0;
+      p.counts = weighted ? weighted_shards(nstep, used, max_, w0) : shard_counts(nstep, used, max_);
       p.counts.resize(world, 0);
       p.src = src + (size_t)start * ib_;
       p.src_event = r.root() ? src_event : -1;
@@ -492,6 +610,7 @@ Group::Stats Group::classify(const uint8_t* src, int64_t n, int32_t* idx, float*
     std::vector<int> lost;
     try {
       run_pipeline(rs, 0, steps, plan, on_result, timeout_ms_);
+      if (auto_balance_ && world > 1 && steps >= 2) rebalance_coord(rs);
       break;
     } catch (const MemberLost& e) {
       // injected: the GPU is in fact fine, so everything already posted

@@ -54,6 +54,10 @@ class Worker {
   virtual bool query(int ev) = 0;                     // event reached?
   virtual void sync(int ev) = 0;
   virtual void sync_all() = 0;
+  // Events that carry a timestamp (the coordinator-share calibration times
+  // every rank's forward): elapsed_ms(a, b) once both have completed.
+  virtual int new_timing_event() { return new_event(); }
+  virtual double elapsed_ms(int ev_a, int ev_b) { (void)ev_a, (void)ev_b; return 0.0; }
   // Independent compute lanes (model instances with their own activations,
   // on their own streams): step slots alternate between them, so one step's
   // forward may start while the previous one's tail (head kernel, graph
@@ -89,8 +93,12 @@ class Worker {
 // lanes: concurrent classify() calls it accepts (one per lane); delay_us:
 // time one classify() takes (so concurrent queries overlap in tests).
 // An unhealthy host worker's classify() throws CommError (a lost GPU).
+// us_per_image / extra_us (calibration tests): a classify of B images takes
+// delay_us + B x us_per_image + extra_us; extra_us on the coordinator stands
+// for the CUs its scatter legs' copy kernels take from its forward on a GPU.
 std::unique_ptr<Worker> make_host_worker(int device, int H, int W, int classes = 1000, int lanes = 1,
-                                         uint32_t seed = 0, int delay_us = 0);
+                                         uint32_t seed = 0, int delay_us = 0, int us_per_image = 0,
+                                         int extra_us = 0);
 // Test hook: a host worker that reports itself unhealthy (a lost GPU).
 void host_worker_set_healthy(Worker& w, bool healthy);
 // The HIP engine on its device (csrc/comm/hip_worker.cpp): images are u8
@@ -112,6 +120,30 @@ float host_prob_of(const uint8_t* img);
 // Balanced split of n images over `world` ranks (lower ranks take the
 // remainder), every count <= cap.
 std::vector<int> shard_counts(int64_t n, int world, int cap);
+
+// Coordinator-share calibration. The coordinator drives every scatter leg
+// next to its own forward (on a GPU, RCCL's copy kernels hold CUs its
+// one-workgroup-per-CU convs need), so with an even split the whole job runs
+// at its pace. One round: a run at weight w (its share of a fair per-rank
+// batch) measures the coordinator's forward busy time b0 and the slowest
+// other rank's bw (ms per step).
+struct CalibRound {
+  double weight = 1.0;
+  double busy_coord = 0.0, busy_worker = 0.0;
+  int coord_count = 0, per_rank = 0, world = 1;
+  // images per ms of the job at this weight, if the step runs at the pace of
+  // its slowest rank
+  double rate() const;
+};
+// Next weight to try: the coordinator's count scaled by bw / b0 (equal busy
+// times under a time ~ count model), within [min_weight, 1].
+double next_coord_weight(const CalibRound& r, double min_weight = 0.5);
+// The measured weight with the highest rate (ties: the larger weight).
+double best_coord_weight(const std::vector<CalibRound>& rounds);
+// A step's split of n images with the coordinator weighted: rank 0 takes a
+// w0 share relative to each other rank (at most round(w0 x cap)), the others
+// a balanced split of the rest (at most cap each).
+std::vector<int> weighted_shards(int64_t n, int world, int cap, double w0);
 
 struct StepPlan {
   int64_t step = 0;          // sequence number; slot = step % slots
@@ -154,6 +186,15 @@ class Rank {
   void collect(const StepPlan& p, int32_t* idx, float* prob, int timeout_ms = -1);
   // Wait until the step's answers have left (non-root) / landed (root).
   void wait_step(const StepPlan& p, int timeout_ms = -1);
+  // Forward time of the steps completed since reset_busy() (timing events
+  // around each classify on its compute stream): total ms, steps, images.
+  double busy_ms() const { return busy_ms_; }
+  int64_t busy_steps() const { return busy_steps_; }
+  int64_t busy_images() const { return busy_images_; }
+  void reset_busy() { busy_ms_ = 0.0, busy_steps_ = 0, busy_images_ = 0; }
+  // Account every step whose forward has completed but was not waited on
+  // through this rank (a group's non-coordinator ranks, after a run).
+  void settle_busy();
   Comm* comm_in() const { return in_; }
   Comm* comm_out() const { return out_; }
   // Forget slot history (after a rebuild every slot is free again).
@@ -172,6 +213,10 @@ class Rank {
   std::vector<void*> ans_;         // answers: root world blocks, others one block
   std::vector<void*> host_ans_;    // root: pinned copy of the gathered answers
   std::vector<int> ev_in_, ev_comp_, ev_out_;
+  std::vector<int> ev_t0_, ev_t1_;  // timing: around the slot's classify
+  std::vector<int> slot_n_;         // images of the slot's step (-1: no timing pending)
+  double busy_ms_ = 0.0;
+  int64_t busy_steps_ = 0, busy_images_ = 0;
   std::vector<bool> in_used_, out_used_;
   int ans_world_ = 0;
 };
@@ -184,6 +229,7 @@ class Rank {
 struct PipelineResult {
   int64_t steps = 0, images = 0;
   std::vector<double> step_ms;  // unpipelined runs: input issue -> answers collected, per step (coordinator)
+  double busy_ms = 0.0;         // this rank's mean forward time per step (the first rank this thread drives)
 };
 using PlanFn = std::function<StepPlan(int64_t step, const Rank& r)>;
 using ResultFn = std::function<void(const StepPlan& p, const int32_t* idx, const float* prob)>;
@@ -230,6 +276,12 @@ class Group {
   // query batches stay on few GPUs; default 1 = always all ranks).
   void set_min_per_rank(int m) { min_per_rank_ = std::max(1, m); }
   Worker* coordinator() const { return workers_.front(); }
+  // The coordinator's share of a step relative to the other ranks (it drives
+  // every scatter leg). With auto_balance (the default) each classify() of
+  // two or more steps re-estimates it from the ranks' forward time per image
+  // (smoothed), so the coordinator stops setting the pace of every step.
+  double coord_weight() const { return coord_weight_; }
+  void set_coord_weight(double w, bool auto_balance);
 
  private:
   void rebuild();
@@ -245,7 +297,10 @@ class Group {
   std::vector<int64_t> fail_at_;  // per worker: steps still to issue before it is lost (-1: never)
   std::vector<bool> fail_abrupt_;
   int min_per_rank_ = 1;
+  double coord_weight_ = 1.0;
+  bool auto_balance_ = true;
   void kill_now(int m);
+  void rebalance_coord(const std::vector<Rank*>& rs);
 };
 
 }  // namespace dp

@@ -76,6 +76,18 @@ class HipWorker : public Worker {
     evs_.push_back(ev);
     return (int)evs_.size() - 1;
   }
+  int new_timing_event() override {
+    activate();
+    hipEvent_t ev;
+    DMLC_HIP_CHECK(hipEventCreate(&ev));
+    evs_.push_back(ev);
+    return (int)evs_.size() - 1;
+  }
+  double elapsed_ms(int a, int b) override {
+    float ms = 0.f;
+    DMLC_HIP_CHECK(hipEventElapsedTime(&ms, evs_.at(a), evs_.at(b)));
+    return ms;
+  }
   void record(int ev, int sid) override { DMLC_HIP_CHECK(hipEventRecord(evs_.at(ev), s_[sid])); }
   void wait(int sid, int ev) override { DMLC_HIP_CHECK(hipStreamWaitEvent(s_[sid], evs_.at(ev), 0)); }
   bool query(int ev) override {

@@ -77,6 +77,50 @@ PipelineResult Runner::run(const uint8_t* pool, int64_t pool_images, int64_t fir
   return run_pipeline({r_.get()}, first, n, plan, on_result, timeout_ms_, pipelined);
 }
 
+void Runner::set_counts(const std::vector<int>& counts) {
+  if ((int)counts.size() != world_) throw std::invalid_argument("dp::Runner::set_counts: one count per rank");
+  int64_t total = 0;
+  for (int c : counts) {
+    if (c < 0 || c > max_) throw std::invalid_argument("dp::Runner::set_counts: count outside [0, max_per_rank]");
+    total += c;
+  }
+  if (total < 1) throw std::invalid_argument("dp::Runner::set_counts: empty step");
+  counts_ = counts;
+}
+
+Runner::Calibration Runner::calibrate(const uint8_t* pool, int64_t pool_images, int64_t first, int64_t steps,
+                                      int rounds, double tol, const AllGather& allgather, double min_weight) {
+  Calibration out;
+  if (world_ < 2 || !scatter_ || steps < 1 || rounds < 1) {
+    out.weight = world_ > 1 ? (double)counts_[0] / counts_[1] : 1.0;
+    return out;
+  }
+  const int per = counts_[1];
+  double w = (double)counts_[0] / per;
+  for (int k = 0; k < rounds; ++k) {
+    const PipelineResult res = run(pool, pool_images, first + out.steps, steps);
+    out.steps += steps;
+    const std::vector<double> b = allgather(res.busy_ms);
+    if ((int)b.size() != world_) throw std::runtime_error("dp::Runner::calibrate: all-gather returned the wrong size");
+    CalibRound r;
+    r.weight = w;
+    r.busy_coord = b[0];
+    for (int i = 1; i < world_; ++i) r.busy_worker = std::max(r.busy_worker, b[i]);
+    r.coord_count = counts_[0];
+    r.per_rank = per;
+    r.world = world_;
+    out.rounds.push_back(r);
+    if (r.busy_worker > 0.0 && std::fabs(r.busy_coord / r.busy_worker - 1.0) <= tol) break;
+    const double nw = next_coord_weight(r, min_weight);
+    if (weighted_counts(per, world_, nw) == counts_) break;  // the count would not change
+    w = nw;
+    set_counts(weighted_counts(per, world_, w));
+  }
+  out.weight = best_coord_weight(out.rounds);
+  set_counts(weighted_counts(per, world_, out.weight));
+  return out;
+}
+
 void Runner::stage(const uint8_t* src, uint8_t* dst) {
   w_->activate();
   const size_t mine = (size_t)counts_[rank_] * ib_;

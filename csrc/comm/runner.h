@@ -12,6 +12,7 @@
 // Reference counterpart: the leader's fan-out of queries to members
 // (src/services.rs:414-421) and the replies.
 #pragma once
+#include <functional>
 #include <memory>
 #include <vector>
 
@@ -46,6 +47,27 @@ class Runner {
   // on rank r over the shard communicator (rank 0's own part by a device
   // copy). Blocks until done.
   void stage(const uint8_t* src, uint8_t* dst);
+
+  // New per-rank counts between runs (every rank the same vector, each count
+  // <= max_per_rank()): the coordinator share after a calibration.
+  void set_counts(const std::vector<int>& counts);
+
+  // Coordinator-share calibration (scatter mode, world > 1): up to `rounds`
+  // runs of `steps` pipelined steps; after each, every rank's mean forward
+  // time per step is all-gathered (allgather: this rank's value -> every
+  // rank's, in rank order; every rank calls it the same number of times) and
+  // the coordinator's count re-solved (next_coord_weight) until its forward
+  // time is within `tol` of the slowest other rank's. Ends on the measured
+  // weight with the best rate (best_coord_weight); every rank computes the
+  // same decisions from the same gathered values.
+  struct Calibration {
+    double weight = 1.0;
+    std::vector<CalibRound> rounds;
+    int64_t steps = 0;
+  };
+  using AllGather = std::function<std::vector<double>(double)>;
+  Calibration calibrate(const uint8_t* pool, int64_t pool_images, int64_t first, int64_t steps, int rounds,
+                        double tol, const AllGather& allgather, double min_weight = 0.5);
 
   Worker* worker() const { return w_.get(); }
   int world() const { return world_; }

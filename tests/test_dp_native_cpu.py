@@ -164,3 +164,67 @@ def test_weighted_counts(per, world, w, want):
 def test_weighted_counts_rejects_raising_the_coordinator():
     with pytest.raises(ValueError):
         C.dp_weighted_counts(256, 8, 1.2)
+
+
+# ---- coordinator share calibration (bench.py at N > 1, and dp::Group)
+
+def test_calibration_equalises_coordinator_and_worker_forward_times():
+    """bench.py's calibration on the host fake: the coordinator's forward is
+    slowed by a fixed 1.5 ms per step (standing for the CUs its scatter legs'
+    copy kernels take on a GPU) on top of 0.2 ms per image. Starting from an
+    even split, the calibration rounds converge to the count whose forward
+    time matches the other ranks' within 5%, and the timed run then uses it
+    (every rank computing the same counts from the gathered times)."""
+    world, per = 4, 20
+    counts = C.dp_weighted_counts(per, world, 1.0)
+    pool = np.random.default_rng(5).integers(0, 256, size=(2 * sum(counts), H, W, 3), dtype=np.uint8)
+    out = C.dp_host_bench(pool, world, per, coord_weight=1.0, input_mode="scatter", lanes=2, prime=2, warmup=2,
+                          steps=4, latency=1, us_per_image=200, coord_extra_us=1500, calib_rounds=6, calib_steps=4)
+    assert out["answers_ok"]
+    cal = out["calibration"]
+    rounds = cal["rounds"]
+    assert rounds[0]["weight"] == 1.0 and rounds[0]["busy_coord_ms"] > 1.25 * rounds[0]["busy_worker_ms"]
+    # equal forward times at c0 * 0.2 + 1.5 = 20 * 0.2 -> c0 = 12.5 (weight 0.625)
+    assert 0.55 <= cal["weight"] <= 0.75, rounds
+    best = max(rounds, key=lambda r: r["rate"])
+    assert abs(best["busy_coord_ms"] / best["busy_worker_ms"] - 1) < 0.12, rounds
+    assert out["counts"][0] == round(per * cal["weight"]) and out["counts"][1:] == [per] * (world - 1)
+    assert all(len(s) == 4 and s == out["steps"][0] for s in out["steps"])
+
+
+def test_calibration_keeps_an_even_split_without_interference():
+    world, per = 3, 12
+    pool = np.random.default_rng(6).integers(0, 256, size=(2 * per * world, H, W, 3), dtype=np.uint8)
+    out = C.dp_host_bench(pool, world, per, coord_weight=1.0, lanes=2, prime=2, warmup=1, steps=3, latency=1,
+                          us_per_image=300, coord_extra_us=0, calib_rounds=4, calib_steps=3)
+    assert out["answers_ok"]
+    assert out["calibration"]["weight"] >= 0.9
+    assert out["counts"][0] >= 11
+
+
+@pytest.mark.parametrize("n,world,cap,w0,want", [
+    (64, 4, 16, 1.0, [16, 16, 16, 16]),
+    (59, 4, 16, 0.75, [12, 16, 16, 15]),
+    (20, 4, 16, 0.5, [3, 6, 6, 5]),
+    (60, 4, 16, 0.75, [12, 16, 16, 16]),
+])
+def test_weighted_shards(n, world, cap, w0, want):
+    got = C.dp_weighted_shards(n, world, cap, w0)
+    assert sum(got) == n and all(0 <= c <= cap for c in got)
+    assert got == want
+
+
+def test_group_auto_balances_the_coordinator_share():
+    """Serving scatters (dp::Group): each classify re-estimates the
+    coordinator's share from per-image forward times; with the coordinator
+    slowed as above the weight falls from 1.0 towards the equal-time point
+    (0.53 here) and every answer is still committed exactly once."""
+    imgs = _images(16 * 4 * 4, seed=31)
+    out = C.dp_host_run(imgs, 4, 16, mode="group", us_per_image=200, coord_extra_us=1500, repeats=6)
+    _check(out, imgs)
+    w = out["coord_weights"]
+    assert w[0] < 0.95 and all(b <= a + 1e-9 for a, b in zip(w, w[1:])), w
+    assert 0.5 <= w[-1] <= 0.7, w
+    flat = C.dp_host_run(imgs, 4, 16, mode="group", us_per_image=200, coord_extra_us=0, repeats=3)
+    _check(flat, imgs)
+    assert flat["coord_weights"][-1] >= 0.9, flat["coord_weights"]
