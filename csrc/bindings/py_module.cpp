@@ -288,6 +288,12 @@ PYBIND11_MODULE(_C, m) {
     for (const auto& s : shard_slices(n, devices)) out.append(py::make_tuple(s.device, s.first, s.n));
     return out;
   });
+  m.def("shard_placement", [](int64_t n, const std::vector<std::vector<int>>& parts) {
+    py::list out;
+    for (const auto& p : shard_placement(n, parts))
+      out.append(py::make_tuple(p.copy, p.slice.device, p.slice.first, p.slice.n));
+    return out;
+  });
 
   // ---------------------------------------------------------------- engine
   py::class_<Engine>(m, "Engine")

@@ -293,15 +293,21 @@ void handle_line(Node& n, const std::string& line) {
       // predict <shard> ...     the jobs classify these labelled SDFS u8 shards
       //                         (resident in the replica holders' HBM) instead
       // predict dataset         back to the dataset's per-label JPEGs
+      std::string resp;
       if (t.size() == 1) {
-        n.call_leader(L_PREDICT, "", 30000);
+        resp = n.call_leader(L_PREDICT, "", 30000);
       } else {
         Writer w;
         const bool dataset = t.size() == 2 && t[1] == "dataset";
         w.u32(dataset ? 0u : (uint32_t)(t.size() - 1));
         if (!dataset)
           for (size_t i = 1; i < t.size(); ++i) w.str(t[i]);
-        n.call_leader(L_PREDICT, w.data(), 30000);
+        resp = n.call_leader(L_PREDICT, w.data(), 30000);
+      }
+      if (resp.size() >= 4) {  // notes: e.g. a running job kept its source
+        Reader r(resp);
+        const uint32_t k = r.u32();
+        for (uint32_t i = 0; i < k && i < 64; ++i) out_line("predict: " + r.str());
       }
     } else if (c == "jobs") {
       if (t.size() != 1) return err_line("Invalid jobs command!");

@@ -122,7 +122,7 @@ struct StreamGeom {
 };
 
 template <int H, int W, int CI, int CO, int HS, int IMG, int NSP, int WM, int S, int ND, bool DS, bool WR,
-          int PD = 4, int NG = 1>
+          int PD = 4, int NG = 1, int PRIO = 0>
 __global__ __launch_bounds__(512, 1) void conv3x3_stream_kernel(StreamConvArgs a) {
   using G = StreamGeom<H, W, CI, HS, IMG, S, ND>;
   constexpr int BK = 32;                     // K-tile depth = one MFMA k-step
@@ -332,6 +332,10 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream_kernel(StreamConvArgs a
   // fragments at the start of the tile. Iteration t first waits for the
   // wave's own DMA of t+1 (issued one iteration earlier), then refills the
   // stage of t-1 (read during t-2, consumed by t-1's MFMAs) with t+2.
+  // PRIO (A/B): waves 4-7 (the second-dispatched half, the arbitration
+  // loser of every SIMD pair) at priority 1 for the whole K loop
+  if constexpr (PRIO)
+    if (wave >= 4) __builtin_amdgcn_s_setprio(1);
   set_tap(0);
   if constexpr (WR)
     vm_wait<(PD - 1) * NF>();  // own input rows (the weight loads were issued after them)
@@ -562,7 +566,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream_kernel(StreamConvArgs a
 }
 
 template <int H, int W, int CI, int CO, int HS, int IMG, int NSP, int WM, int S, bool WR = false, int PD = 4,
-          int NG = 1>
+          int NG = 1, int PRIO = 0>
 void launch_stream(const StreamConvArgs& a, hipStream_t s) {
   using G = StreamGeom<H, W, CI, HS, IMG, S, 3>;
   constexpr size_t lds = WR ? (size_t)G::XBYTES : G::LDS;
@@ -571,12 +575,12 @@ void launch_stream(const StreamConvArgs& a, hipStream_t s) {
   if constexpr (WR) {
     if constexpr (S == 2) {
       if (a.yd) {
-        hipLaunchKernelGGL((conv3x3_stream_kernel<H, W, CI, CO, HS, IMG, NSP, WM, S, 3, true, true, PD, NG>),
+        hipLaunchKernelGGL((conv3x3_stream_kernel<H, W, CI, CO, HS, IMG, NSP, WM, S, 3, true, true, PD, NG, PRIO>),
                            dim3(grid), dim3(512), lds, s, a);
         return;
       }
     }
-      hipLaunchKernelGGL((conv3x3_stream_kernel<H, W, CI, CO, HS, IMG, NSP, WM, S, 3, false, true, PD, NG>),
+      hipLaunchKernelGGL((conv3x3_stream_kernel<H, W, CI, CO, HS, IMG, NSP, WM, S, 3, false, true, PD, NG, PRIO>),
                          dim3(grid), dim3(512), lds, s, a);
     return;
   } else {
@@ -596,7 +600,9 @@ void launch_stream(const StreamConvArgs& a, hipStream_t s) {
 // 1 = the 14x14x256 register-weight kernel with a 2-deep weight ring (PD 2);
 // 2 = the stride-2 register-weight 28x28x128 kernel with two channel groups
 // per wave (NG 2); 4 = the stride-2 14x14x256 one with one (NG 1, half the
-// channels per workgroup).
+// channels per workgroup); 8 = the 7x7x512 stride-1 register-weight kernel
+// with an 8-deep weight ring (16 deep spills); 32 = waves 4-7 at priority 1 in
+// the register-weight kernels of layers 3-4.
 std::atomic<int> g_stream_variant{0};
 
 }  // namespace
@@ -682,6 +688,8 @@ void conv3x3_stream(const void* x, const void* w, const float* bias, const void*
   else if (stride == 1 && Cin == 256 && wfrag) {  // layer3, register weights, 2 pixel halves x 4 groups of 64 channels
     if (g_stream_variant & 1)
       launch_stream<14, 14, 256, 256, 14, 1, 1, 2, 1, true, 2, 2>(a, s);
+    else if (g_stream_variant & 32)
+      launch_stream<14, 14, 256, 256, 14, 1, 1, 2, 1, true, 4, 2, 1>(a, s);
     else
       launch_stream<14, 14, 256, 256, 14, 1, 1, 2, 1, true, 4, 2>(a, s);
   }
@@ -690,7 +698,12 @@ void conv3x3_stream(const void* x, const void* w, const float* bias, const void*
   else if (stride == 1 && wfrag) {  // layer4, weights in fragment order straight into VGPRs
     // (two 64-channel groups per wave measured slower here: 2 images x 2
     // pixel halves 58.7 us, 1 image x 8 groups 60.9 us vs 53.0 us)
-    launch_stream<7, 7, 512, 512, 7, 2, 2, 1, 1, true>(a, s);
+    if (g_stream_variant & 8)
+      launch_stream<7, 7, 512, 512, 7, 2, 2, 1, 1, true, 8>(a, s);
+    else if (g_stream_variant & 32)
+      launch_stream<7, 7, 512, 512, 7, 2, 2, 1, 1, true, 4, 1, 1>(a, s);
+    else
+      launch_stream<7, 7, 512, 512, 7, 2, 2, 1, 1, true>(a, s);
   }
   else if (stride == 1)  // layer4: two whole images x half the output channels (2 x 49 x 1 KB = 98 KB)
     launch_stream<7, 7, 512, 512, 7, 2, 2, 1, 1>(a, s);
@@ -717,6 +730,8 @@ void conv3x3_stream(const void* x, const void* w, const float* bias, const void*
     // workgroup, 32 per wave (variant bit 4; profiles/r3_stream_s2_ng2.txt)
     if (g_stream_variant & 4)
       launch_stream<7, 7, 256, 512, 7, 1, 2, 1, 2, true>(a, s);
+    else if (g_stream_variant & 32)
+      launch_stream<7, 7, 256, 512, 7, 1, 1, 1, 2, true, 4, 2, 1>(a, s);
     else
       launch_stream<7, 7, 256, 512, 7, 1, 1, 1, 2, true, 4, 2>(a, s);
   }

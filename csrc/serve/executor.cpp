@@ -250,7 +250,28 @@ class GpuExecutor : public Executor {
     return s.empty() ? "none" : s;
   }
   void set_jobs(const std::vector<std::string>& models) override { fleet_->set_jobs(models); }
-  void lose_device(int device) override { fleet_->lose(device); }
+  void lose_device(int device) override {
+    fleet_->lose(device);
+    // the partitions moved: every staged shard is placed for the new ones now
+    std::vector<std::pair<std::string, std::shared_ptr<HbmBlob>>> bs;
+    {
+      std::lock_guard<std::mutex> g(blob_mu_);
+      for (const auto& kv : hbm_blobs_) bs.emplace_back(kv.first, kv.second);
+    }
+    for (auto& kv : bs) current_blob(kv.first, kv.second);
+    // decoded query images homed on the lost GPU are gone with it
+    std::lock_guard<std::mutex> g(cache_mu_);
+    for (auto it = cache_.begin(); it != cache_.end();) {
+      if (it->second.device == device && it->second.pins == 0) {
+        cache_bytes_ -= it->second.bytes;
+        cache_bytes_dev_[device] -= it->second.bytes;
+        lru_.erase(it->second.lru);
+        it = cache_.erase(it);  // (its memory went with the device)
+      } else {
+        ++it;
+      }
+    }
+  }
 
   void load_model(const std::string& model, const std::string& path) override {
     load_model_weights(model, ot_load(path));
@@ -392,75 +413,11 @@ class GpuExecutor : public Executor {
     return s;
   }
 
+  // SDFS u8 shard replica -> HBM: one full copy per serving partition, each
+  // sliced over that partition's GPUs (shard.h shard_placement), so every
+  // model reads the images of its queries in place from a GPU it serves on.
   void stage_blob(const std::string& key, const std::string& path) override {
-    std::ifstream f(path, std::ios::binary);
-    if (!f) throw std::runtime_error("cannot open " + path);
-    f.seekg(0, std::ios::end);
-    const size_t bytes = (size_t)f.tellg();
-    f.seekg(0);
-    uint8_t head[kShardHeader] = {};
-    if (bytes < kShardHeader || !f.read((char*)head, kShardHeader)) throw std::runtime_error(path + ": not a u8 shard");
-    auto b = std::make_shared<HbmBlob>();
-    b->si = parse_shard(head, bytes);  // validates h, w <= 4096 and n * h * w * 3 == size
-    const size_t ib = b->si.image_bytes();
-    std::vector<int> live = fleet_->live();
-    if (live.empty()) throw std::runtime_error("no live GPU to stage " + key);
-    const int64_t n = b->si.n;
-    for (const ShardSlice& sl : shard_slices(n, live)) {
-      HbmBlob::Piece pc;
-      pc.device = sl.device;
-      pc.first = sl.first;
-      pc.n = sl.n;
-      DMLC_HIP_CHECK(hipSetDevice(pc.device));
-      DMLC_HIP_CHECK(hipMalloc(&pc.dev, std::max<size_t>((size_t)pc.n * ib, 256)));
-      b->pieces.push_back(pc);
-    }
-    // Stream the images through two pinned buffers: the file read of one
-    // chunk overlaps the DMA of the previous one (each slice's DMA on a side
-    // stream of its GPU); a buffer is refilled only once its copies are done.
-    auto st = take_stager();
-    try {
-      constexpr size_t kChunk = (size_t)32 << 20;
-      const size_t chunk = std::max(ib, kChunk / ib * ib);  // whole images per chunk
-      st->ensure_pinned(std::min(chunk, std::max<size_t>((size_t)n * ib, 256)));
-      const size_t cap = st->pinned_bytes / ib * ib;
-      if (cap == 0) throw std::runtime_error("stage_blob: staging buffer too small");
-      std::vector<hipEvent_t> pending[2];
-      int buf = 0;
-      for (int64_t img = 0; img < n;) {
-        for (hipEvent_t e : pending[buf]) {
-          DMLC_HIP_CHECK(hipEventSynchronize(e));
-          DMLC_HIP_CHECK(hipEventDestroy(e));
-        }
-        pending[buf].clear();
-        const int64_t cnt = std::min<int64_t>(n - img, (int64_t)(cap / ib));
-        uint8_t* hb = (uint8_t*)st->pinned[buf];
-        if (!f.read((char*)hb, (std::streamsize)((size_t)cnt * ib))) throw std::runtime_error(path + ": short read");
-        for (const auto& pc : b->pieces) {
-          const int64_t lo = std::max(img, pc.first), hi = std::min(img + cnt, pc.first + pc.n);
-          if (lo >= hi) continue;
-          DMLC_HIP_CHECK(hipSetDevice(pc.device));
-          hipStream_t s = st->stream(pc.device);
-          DMLC_HIP_CHECK(hipMemcpyAsync((uint8_t*)pc.dev + (size_t)(lo - pc.first) * ib, hb + (size_t)(lo - img) * ib,
-                                        (size_t)(hi - lo) * ib, hipMemcpyHostToDevice, s));
-          hipEvent_t e;
-          DMLC_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-          DMLC_HIP_CHECK(hipEventRecord(e, s));
-          pending[buf].push_back(e);
-        }
-        img += cnt;
-        buf ^= 1;
-      }
-      for (auto& v : pending)
-        for (hipEvent_t e : v) {
-          DMLC_HIP_CHECK(hipEventSynchronize(e));  // resident before it is visible
-          DMLC_HIP_CHECK(hipEventDestroy(e));
-        }
-    } catch (...) {
-      give_stager(st);
-      throw;
-    }
-    give_stager(st);
+    auto b = load_blob(path);
     std::lock_guard<std::mutex> g(blob_mu_);
     hbm_blobs_[key] = std::move(b);  // a replaced blob is freed once no query holds it
   }
@@ -479,14 +436,16 @@ class GpuExecutor : public Executor {
   // run concurrently as direct queries, each preferring the GPU that holds
   // its slice (the data is already spread over the GPUs: no scatter).
   std::vector<Prediction> predict_blob(const std::string& model, const std::string& key) override {
-    auto b = blob(key);
+    auto b = current_blob(key, blob(key));
     const int64_t n = b->si.n;
     std::vector<int32_t> idx(n);
     std::vector<float> prob(n);
     std::vector<std::pair<int64_t, int64_t>> chunks;
+    const int copy = std::max(0, copy_of(*b, model));
     for (const auto& pc : b->pieces)
-      for (int64_t f = pc.first; f < pc.first + pc.n; f += max_batch_)
-        chunks.emplace_back(f, std::min<int64_t>(max_batch_, pc.first + pc.n - f));
+      if (pc.copy == copy)
+        for (int64_t f = pc.first; f < pc.first + pc.n; f += max_batch_)
+          chunks.emplace_back(f, std::min<int64_t>(max_batch_, pc.first + pc.n - f));
     const auto parts = fleet_->partitions();
     const size_t width = parts.count(model) ? std::max<size_t>(1, parts.at(model).size() * lanes_) : 1;
     std::atomic<size_t> next{0};
@@ -496,7 +455,7 @@ class GpuExecutor : public Executor {
       ts.emplace_back([&, t] {
         try {
           for (size_t c = next++; c < chunks.size(); c = next++)
-            classify_range(model, b, chunks[c].first, chunks[c].second, idx.data() + chunks[c].first,
+            classify_range(model, b, key, chunks[c].first, chunks[c].second, idx.data() + chunks[c].first,
                            prob.data() + chunks[c].first);
         } catch (...) {
           errs[t] = std::current_exception();
@@ -514,7 +473,7 @@ class GpuExecutor : public Executor {
     if (first < 0 || n < 0 || first + n > (int64_t)b->si.n) throw std::runtime_error(key + ": image range out of bounds");
     std::vector<int32_t> idx(n);
     std::vector<float> prob(n);
-    classify_range(model, b, first, n, idx.data(), prob.data());
+    classify_range(model, b, key, first, n, idx.data(), prob.data());
     return to_preds(idx, prob);
   }
 
@@ -577,8 +536,11 @@ class GpuExecutor : public Executor {
   };
   struct HbmBlob {
     ShardInfo si;
+    std::string path;                     // the replica file (re-staging after a partition change)
+    std::vector<std::vector<int>> parts;  // the partitions it was placed for (one copy each)
     struct Piece {
       int device = 0;
+      int copy = 0;
       void* dev = nullptr;
       int64_t first = 0, n = 0;
     };
@@ -647,16 +609,159 @@ class GpuExecutor : public Executor {
     return it->second;
   }
 
+  std::shared_ptr<HbmBlob> load_blob(const std::string& path) {
+    std::ifstream f(path, std::ios::binary);
+    if (!f) throw std::runtime_error("cannot open " + path);
+    f.seekg(0, std::ios::end);
+    const size_t bytes = (size_t)f.tellg();
+    f.seekg(0);
+    uint8_t head[kShardHeader] = {};
+    if (bytes < kShardHeader || !f.read((char*)head, kShardHeader)) throw std::runtime_error(path + ": not a u8 shard");
+    auto b = std::make_shared<HbmBlob>();
+    b->si = parse_shard(head, bytes);  // validates h, w <= 4096 and n * h * w * 3 == size
+    b->path = path;
+    const size_t ib = b->si.image_bytes();
+    b->parts = partition_sets();
+    if (b->parts.empty()) throw std::runtime_error("no live GPU to stage " + path);
+    const int64_t n = b->si.n;
+    for (const PlacedSlice& ps : shard_placement(n, b->parts)) {
+      HbmBlob::Piece pc;
+      pc.device = ps.slice.device;
+      pc.copy = ps.copy;
+      pc.first = ps.slice.first;
+      pc.n = ps.slice.n;
+      DMLC_HIP_CHECK(hipSetDevice(pc.device));
+      DMLC_HIP_CHECK(hipMalloc(&pc.dev, std::max<size_t>((size_t)pc.n * ib, 256)));
+      b->pieces.push_back(pc);
+    }
+    // Stream the images through two pinned buffers: the file read of one
+    // chunk overlaps the DMA of the previous one (each slice's DMA on a side
+    // stream of its GPU); a buffer is refilled only once its copies are done.
+    auto st = take_stager();
+    try {
+      constexpr size_t kChunk = (size_t)32 << 20;
+      const size_t chunk = std::max(ib, kChunk / ib * ib);  // whole images per chunk
+      st->ensure_pinned(std::min(chunk, std::max<size_t>((size_t)n * ib, 256)));
+      const size_t cap = st->pinned_bytes / ib * ib;
+      if (cap == 0) throw std::runtime_error("stage_blob: staging buffer too small");
+      std::vector<hipEvent_t> pending[2];
+      int buf = 0;
+      for (int64_t img = 0; img < n;) {
+        for (hipEvent_t e : pending[buf]) {
+          DMLC_HIP_CHECK(hipEventSynchronize(e));
+          DMLC_HIP_CHECK(hipEventDestroy(e));
+        }
+        pending[buf].clear();
+        const int64_t cnt = std::min<int64_t>(n - img, (int64_t)(cap / ib));
+        uint8_t* hb = (uint8_t*)st->pinned[buf];
+        if (!f.read((char*)hb, (std::streamsize)((size_t)cnt * ib))) throw std::runtime_error(path + ": short read");
+        for (const auto& pc : b->pieces) {
+          const int64_t lo = std::max(img, pc.first), hi = std::min(img + cnt, pc.first + pc.n);
+          if (lo >= hi) continue;
+          DMLC_HIP_CHECK(hipSetDevice(pc.device));
+          hipStream_t s = st->stream(pc.device);
+          DMLC_HIP_CHECK(hipMemcpyAsync((uint8_t*)pc.dev + (size_t)(lo - pc.first) * ib, hb + (size_t)(lo - img) * ib,
+                                        (size_t)(hi - lo) * ib, hipMemcpyHostToDevice, s));
+          hipEvent_t e;
+          DMLC_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+          DMLC_HIP_CHECK(hipEventRecord(e, s));
+          pending[buf].push_back(e);
+        }
+        img += cnt;
+        buf ^= 1;
+      }
+      for (auto& v : pending)
+        for (hipEvent_t e : v) {
+          DMLC_HIP_CHECK(hipEventSynchronize(e));  // resident before it is visible
+          DMLC_HIP_CHECK(hipEventDestroy(e));
+        }
+    } catch (...) {
+      give_stager(st);
+      throw;
+    }
+    give_stager(st);
+    return b;
+  }
+  // The distinct GPU sets of the current partitions (sorted), the copies a
+  // staged blob holds.
+  std::vector<std::vector<int>> partition_sets() const {
+    std::vector<std::vector<int>> out;
+    for (auto kv : fleet_->partitions()) {
+      if (kv.second.empty()) continue;
+      std::sort(kv.second.begin(), kv.second.end());
+      if (std::find(out.begin(), out.end(), kv.second) == out.end()) out.push_back(kv.second);
+    }
+    if (out.empty()) {  // no model loaded yet: one copy over the live GPUs
+      auto l = fleet_->live();
+      if (!l.empty()) out.push_back(l);
+    }
+    std::sort(out.begin(), out.end());
+    return out;
+  }
+  // A blob placed for other partitions, or with a piece on a lost GPU (a GPU
+  // loss rebalanced the fleet), is staged again from its file for the
+  // current ones (the lost GPU's slices used to fail every query
+  // that touched them).
+  std::shared_ptr<HbmBlob> current_blob(const std::string& key, std::shared_ptr<HbmBlob> b) {
+    auto ok = [&](const HbmBlob& x) {
+      if (x.parts != partition_sets()) return false;
+      const auto live = fleet_->live();
+      for (const auto& pc : x.pieces)
+        if (std::find(live.begin(), live.end(), pc.device) == live.end()) return false;
+      return true;
+    };
+    if (ok(*b)) return b;
+    std::lock_guard<std::mutex> rg(restage_mu_);
+    {
+      std::lock_guard<std::mutex> g(blob_mu_);
+      auto it = hbm_blobs_.find(key);
+      if (it != hbm_blobs_.end() && it->second != b && ok(*it->second)) return it->second;  // done meanwhile
+    }
+    auto nb = load_blob(b->path);
+    std::lock_guard<std::mutex> g(blob_mu_);
+    hbm_blobs_[key] = nb;
+    return nb;
+  }
+
   // Images [first, first + n) of a staged shard through the fleet (no scatter:
   // the slices are already spread over the GPUs; the query prefers the GPU
   // holding its first image).
-  void classify_range(const std::string& model, const std::shared_ptr<HbmBlob>& b, int64_t first, int64_t n,
-                      int32_t* idx, float* prob) {
+  // The copy of a blob placed for `model`'s partition (-1: none matches).
+  int copy_of(const HbmBlob& b, const std::string& model) const {
+    const auto parts = fleet_->partitions();
+    auto it = parts.find(model);
+    if (it == parts.end()) return -1;
+    auto mine = it->second;
+    std::sort(mine.begin(), mine.end());
+    for (size_t c = 0; c < b.parts.size(); ++c)
+      if (b.parts[c] == mine) return (int)c;
+    return -1;
+  }
+  // The piece that holds image `pos` best for a reader on `device`: one on
+  // that device, else one of copy `copy`, else any (a peer read).
+  static const HbmBlob::Piece* piece_for(const HbmBlob& b, int64_t pos, int device, int copy) {
+    const HbmBlob::Piece* best = nullptr;
+    int score = -1;
+    for (const auto& pc : b.pieces) {
+      if (pos < pc.first || pos >= pc.first + pc.n) continue;
+      const int sc = pc.device == device ? 2 : pc.copy == copy ? 1 : 0;
+      if (sc > score) score = sc, best = &pc;
+    }
+    return best;
+  }
+
+  // Images [first, first + n) of a staged shard through the fleet (no scatter:
+  // the slices are already spread over the partition's GPUs; the query
+  // prefers the GPU holding its first image in the model's copy, and reads
+  // it there in place).
+  void classify_range(const std::string& model, std::shared_ptr<HbmBlob> b, const std::string& key, int64_t first,
+                      int64_t n, int32_t* idx, float* prob) {
+    b = current_blob(key, b);
     const size_t ib = b->si.image_bytes();
     const bool dense = b->si.h == (uint32_t)kS && b->si.w == (uint32_t)kS;
+    const int copy = copy_of(*b, model);
     int prefer = -1;
-    for (const auto& pc : b->pieces)
-      if (first >= pc.first && first < pc.first + pc.n) prefer = pc.device;
+    if (const auto* pc = piece_for(*b, first, -1, copy)) prefer = pc->device;
     auto stage = [&](const dp::StageCtx& c, int64_t off, int64_t cnt) -> const uint8_t* {
       const int64_t g0 = first + off;
       auto s = (hipStream_t)c.worker->stream(c.stream);
@@ -664,33 +769,38 @@ class GpuExecutor : public Executor {
         for (const auto& pc : b->pieces)  // in place: the whole range in a slice on this GPU
           if (pc.device == c.device && g0 >= pc.first && g0 + cnt <= pc.first + pc.n)
             return (const uint8_t*)pc.dev + (size_t)(g0 - pc.first) * ib;
-        for (const auto& pc : b->pieces) {  // gather the range into the stage buffer
-          const int64_t lo = std::max(g0, pc.first), hi = std::min(g0 + cnt, pc.first + pc.n);
-          if (lo >= hi) continue;
-          uint8_t* dst = (uint8_t*)c.batch + (size_t)(lo - g0) * ib;
-          const uint8_t* srcp = (const uint8_t*)pc.dev + (size_t)(lo - pc.first) * ib;
-          if (pc.device == c.device)
-            DMLC_HIP_CHECK(hipMemcpyAsync(dst, srcp, (size_t)(hi - lo) * ib, hipMemcpyDeviceToDevice, s));
+        for (int64_t pos = g0; pos < g0 + cnt;) {  // gather the range into the stage buffer
+          const auto* pc = piece_for(*b, pos, c.device, copy);
+          if (!pc) throw std::runtime_error("blob: image not staged");
+          const int64_t hi = std::min(g0 + cnt, pc->first + pc->n);
+          uint8_t* dst = (uint8_t*)c.batch + (size_t)(pos - g0) * ib;
+          const uint8_t* srcp = (const uint8_t*)pc->dev + (size_t)(pos - pc->first) * ib;
+          if (pc->device == c.device)
+            DMLC_HIP_CHECK(hipMemcpyAsync(dst, srcp, (size_t)(hi - pos) * ib, hipMemcpyDeviceToDevice, s));
           else
-            DMLC_HIP_CHECK(hipMemcpyPeerAsync(dst, c.device, srcp, pc.device, (size_t)(hi - lo) * ib, s));
+            DMLC_HIP_CHECK(hipMemcpyPeerAsync(dst, c.device, srcp, pc->device, (size_t)(hi - pos) * ib, s));
+          pos = hi;
         }
         return (const uint8_t*)c.batch;
       }
       // other sizes: resized on the GPU like query images
       auto* hd = (ImageDesc*)c.aux_host;
       std::vector<void*> tmp;
-      for (const auto& pc : b->pieces) {
-        const int64_t lo = std::max(g0, pc.first), hi = std::min(g0 + cnt, pc.first + pc.n);
-        if (lo >= hi) continue;
-        const uint8_t* base = (const uint8_t*)pc.dev + (size_t)(lo - pc.first) * ib;
-        if (!peer(c.device, pc.device)) {
+      for (int64_t pos = g0; pos < g0 + cnt;) {
+        const auto* pc = piece_for(*b, pos, c.device, copy);
+        if (!pc) throw std::runtime_error("blob: image not staged");
+        const int64_t hi = std::min(g0 + cnt, pc->first + pc->n);
+        const uint8_t* base = (const uint8_t*)pc->dev + (size_t)(pos - pc->first) * ib;
+        if (!peer(c.device, pc->device)) {
           void* d = nullptr;
-          DMLC_HIP_CHECK(hipMallocAsync(&d, (size_t)(hi - lo) * ib, s));
-          DMLC_HIP_CHECK(hipMemcpyPeerAsync(d, c.device, base, pc.device, (size_t)(hi - lo) * ib, s));
+          DMLC_HIP_CHECK(hipMallocAsync(&d, (size_t)(hi - pos) * ib, s));
+          DMLC_HIP_CHECK(hipMemcpyPeerAsync(d, c.device, base, pc->device, (size_t)(hi - pos) * ib, s));
           tmp.push_back(d);
           base = (const uint8_t*)d;
         }
-        for (int64_t i = lo; i < hi; ++i) hd[i - g0] = ImageDesc{base + (size_t)(i - lo) * ib, (int)b->si.h, (int)b->si.w};
+        for (int64_t i = pos; i < hi; ++i)
+          hd[i - g0] = ImageDesc{base + (size_t)(i - pos) * ib, (int)b->si.h, (int)b->si.w};
+        pos = hi;
       }
       resize_into(c, hd, cnt, s);
       for (void* d : tmp) DMLC_HIP_CHECK(hipFreeAsync(d, s));
@@ -825,6 +935,7 @@ class GpuExecutor : public Executor {
   std::mutex weights_mu_;
   std::map<std::string, std::shared_ptr<const WeightMap>> weights_;  // host copies (fresh instances build from them)
   std::map<std::string, std::shared_ptr<HbmBlob>> hbm_blobs_;  // under blob_mu_
+  std::mutex restage_mu_;  // one re-staging at a time
   mutable std::mutex cache_mu_;
   std::unordered_map<std::string, Entry> cache_;
   std::list<std::string> lru_;

@@ -298,12 +298,17 @@ void LeaderService::train(const std::string& filename, const std::string& model_
     }
 }
 
-void LeaderService::predict(const std::vector<std::string>* shards) {
+std::vector<std::string> LeaderService::predict(const std::vector<std::string>* shards) {
   std::lock_guard<std::mutex> g(runners_mu_);
+  std::vector<std::string> notes;
   for (size_t j = 0; j < jobs_.size(); ++j) {
     {
       std::lock_guard<std::mutex> g2(mu_);
-      if (running_[j]) continue;
+      if (running_[j]) {
+        if (shards && jobs_[j].source != *shards)
+          notes.push_back("job " + jobs_[j].model_name + " is still running on its previous source; it keeps it");
+        continue;
+      }
       if (shards && jobs_[j].source != *shards) {  // another data source: the job starts over
         Job fresh;
         fresh.model_name = jobs_[j].model_name;
@@ -315,6 +320,7 @@ void LeaderService::predict(const std::vector<std::string>* shards) {
     }
     runners_.emplace_back([this, j] { run_job(j); });
   }
+  return notes;
 }
 
 std::vector<Id> LeaderService::shard_holders(const std::string& file) {
@@ -478,7 +484,12 @@ void LeaderService::run_job(size_t j) {
   const auto& L = labels_.entries;
   size_t total = L.size();
   if (!source.empty()) total = segs.empty() ? 0 : segs.back().start + segs.back().n;
-  const size_t limit = cfg_.job_limit > 0 ? std::min(total, (size_t)cfg_.job_limit) : total;
+  // a label job stops after the label table (the reference's 1,000 queries);
+  // a shard job's --job-limit may exceed its shards' images: it loops over
+  // them (sustained throughput runs, tools/bench_jobs.py --job-limit)
+  const size_t limit = cfg_.job_limit > 0 ? (source.empty() ? std::min(total, (size_t)cfg_.job_limit)
+                                                            : (total ? (size_t)cfg_.job_limit : 0))
+                                          : total;
   auto next_tick = std::chrono::steady_clock::now();
   for (;;) {
     if (stop_.load()) break;
@@ -502,8 +513,9 @@ void LeaderService::run_job(size_t j) {
       }
       range.first = idx;
       range.n = std::min((size_t)cfg_.query_batch, limit - idx);
+      const size_t di = total ? idx % total : idx;  // data index (a looping shard job wraps)
       for (const auto& sg : segs)  // a shard query never spans two shards
-        if (idx >= sg.start && idx < sg.start + sg.n) range.n = std::min(range.n, sg.start + sg.n - idx);
+        if (di >= sg.start && di < sg.start + sg.n) range.n = std::min(range.n, sg.start + sg.n - di);
       idx += range.n;
     }
     if (cfg_.adaptive_window <= 0) {
@@ -520,8 +532,9 @@ void LeaderService::run_job(size_t j) {
       // a shard query goes to a replica holder (its bytes are resident there),
       // one of the job's own members when it can
       const Seg* sg = nullptr;
+      const size_t di = range.first % total;
       for (const auto& x : segs)
-        if (range.first >= x.start && range.first < x.start + x.n) sg = &x;
+        if (di >= x.start && di < x.start + x.n) sg = &x;
       const std::vector<Id> holders = sg ? shard_holders(sg->file) : std::vector<Id>{};
       std::vector<Id> mine;
       for (const auto& h : holders)
@@ -533,8 +546,19 @@ void LeaderService::run_job(size_t j) {
     }
     if (pool.empty()) {
       std::lock_guard<std::mutex> g(mu_);
-      retry_[j].push_front(range);  // no member at all: not an attempt
-      if (cfg_.adaptive_window > 0) std::this_thread::sleep_for(std::chrono::milliseconds(50));
+      if (segs.empty()) {
+        retry_[j].push_front(range);  // no member at all: not an attempt
+      } else if (range.attempts + 1 >= std::max(1, cfg_.max_attempts)) {
+        // a shard with no live replica holder: an attempt like a failed query
+        // (it used to be requeued forever and the job never finished: ADVICE r3)
+        jobs_[j].failed += (int32_t)range.n;
+        DMLC_LOG_WARN("job " << jobs_[j].model_name << ": images " << range.first << "+" << range.n
+                             << ": no live replica holder; dropped");
+      } else {
+        range.attempts += 1;
+        retry_[j].push_back(range);
+      }
+      if (cfg_.adaptive_window > 0 || !segs.empty()) std::this_thread::sleep_for(std::chrono::milliseconds(50));
       continue;
     }
     if (cfg_.adaptive_window > 0) {
@@ -574,13 +598,16 @@ void LeaderService::run_job(size_t j) {
 void LeaderService::query(size_t j, const std::string& model, Id target, Range range, int64_t run0,
                           int64_t elapsed0) {
   const auto& L = labels_.entries;
-  const size_t first = range.first, n = range.n;
+  const size_t n = range.n;
   const Seg* sg = nullptr;
   std::vector<Seg> segs;
   {
     std::lock_guard<std::mutex> g(mu_);
     segs = segs_[j];
   }
+  // data index of the query's first image (a shard job may loop over its shards)
+  const size_t total = segs.empty() ? 0 : segs.back().start + segs.back().n;
+  const size_t first = total ? range.first % total : range.first;
   for (const auto& x : segs)
     if (first >= x.start && first < x.start + x.n) sg = &x;
   if (range.attempts > 0)  // a requeued query: back off before sending it again
@@ -861,16 +888,20 @@ void LeaderService::register_handlers() {
     throw std::runtime_error("predict-shard " + f + ": " + last_err);
   });
   server_->handle(L_PREDICT, [this](Reader& r) {
+    std::vector<std::string> notes;
     if (r.left() >= 4) {  // `predict <shard>...` / `predict dataset`
       const uint32_t k = r.u32();
       if (k > 4096) throw std::runtime_error("predict: too many shards");
       std::vector<std::string> shards;
       for (uint32_t i = 0; i < k; ++i) shards.push_back(r.str());
-      predict(&shards);
+      notes = predict(&shards);
     } else {
-      predict();
+      notes = predict();
     }
-    return std::string();
+    Writer w;
+    w.u32((uint32_t)notes.size());
+    for (const auto& x : notes) w.str(x);
+    return w.take();
   });
   server_->handle(L_JOBS, [this](Reader&) {
     const auto js = jobs();

@@ -75,7 +75,9 @@ class LeaderService {
   // Start the jobs that are not running. shards == nullptr: each job keeps
   // its source (resume); otherwise the jobs take their queries from these
   // SDFS shards (empty: the dataset's labels), starting over if that changes.
-  void predict(const std::vector<std::string>* shards = nullptr);
+  // Returns notes for the caller: a job still running keeps its source
+  // (a different one is not applied until it is idle).
+  std::vector<std::string> predict(const std::vector<std::string>* shards = nullptr);
   std::vector<Job> jobs() const;
 
  private:

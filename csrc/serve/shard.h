@@ -68,4 +68,32 @@ inline std::vector<ShardSlice> shard_slices(int64_t n, const std::vector<int>& d
   return out;
 }
 
+// Placement of a shard replica over the node's serving partitions (the GPU
+// sets dp::Fleet gives each model): one full copy per distinct partition,
+// sliced over that partition's GPUs with shard_slices, so every model finds
+// every image of the shard in the HBM of a GPU it serves from (both jobs run
+// over the same shards: a single copy spread over all GPUs had each model
+// read half its ranges over xGMI). Identical partitions (fewer GPUs than
+// models: the models share their GPU) share one copy; a device listed in
+// several partitions holds one slice per copy it is part of. copy = index of
+// the partition copy the slice belongs to.
+struct PlacedSlice {
+  int copy = 0;
+  ShardSlice slice;
+};
+inline std::vector<PlacedSlice> shard_placement(int64_t n, const std::vector<std::vector<int>>& partitions) {
+  std::vector<std::vector<int>> copies;
+  for (auto p : partitions) {
+    if (p.empty()) continue;
+    std::sort(p.begin(), p.end());
+    p.erase(std::unique(p.begin(), p.end()), p.end());
+    if (std::find(copies.begin(), copies.end(), p) == copies.end()) copies.push_back(p);
+  }
+  if (copies.empty()) throw std::runtime_error("shard_placement: no partition");
+  std::vector<PlacedSlice> out;
+  for (size_t c = 0; c < copies.size(); ++c)
+    for (const ShardSlice& s : shard_slices(n, copies[c])) out.push_back(PlacedSlice{(int)c, s});
+  return out;
+}
+
 }  // namespace dmlc

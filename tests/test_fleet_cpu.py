@@ -343,3 +343,29 @@ def test_failed_worker_build_keeps_serving_and_retries():
     st = f.state()
     assert st["partitions"] == {"resnet18": [0, 1, 2], "alexnet": [3, 4, 6, 7]}
     assert st["overlapping_worlds"] == []
+
+
+# ------------------------------------------------- shard replica placement
+@pytest.mark.parametrize("n,parts,want", [
+    # two jobs on disjoint halves: one full copy per partition, sliced over its GPUs
+    (1000, [[0, 1, 2, 3], [4, 5, 6, 7]],
+     [(0, d, 250 * d, 250) for d in range(4)] + [(1, 4 + d, 250 * d, 250) for d in range(4)]),
+    # after a loss the partitions are uneven (first floor(7/2) to job 1)
+    (10, [[0, 1, 2], [3, 4, 6, 7]], [(0, 0, 0, 3), (0, 1, 3, 3), (0, 2, 6, 4),
+                                     (1, 3, 0, 2), (1, 4, 2, 3), (1, 6, 5, 2), (1, 7, 7, 3)]),
+    # fewer GPUs than jobs: both models share GPU 0 -> one copy
+    (7, [[0], [0]], [(0, 0, 0, 7)]),
+    # a partition's GPUs are taken in sorted order; copies follow the partitions
+    (4, [[3, 2], [1, 0]], [(0, 2, 0, 2), (0, 3, 2, 2), (1, 0, 0, 2), (1, 1, 2, 2)]),
+])
+def test_shard_placement_one_copy_per_partition(n, parts, want):
+    """A staged shard replica is held in HBM once per serving partition,
+    sliced over that partition's GPUs, so each model reads every image of
+    its queries from a GPU it serves on (GPU executor stage_blob; both jobs
+    run over the same shards)."""
+    got = C.shard_placement(n, parts)
+    assert got == want
+    for c in {p[0] for p in got}:  # every copy covers the shard exactly once
+        cover = sorted((f, k) for cc, _, f, k in got if cc == c)
+        assert cover[0][0] == 0 and all(a[0] + a[1] == b[0] for a, b in zip(cover, cover[1:]))
+        assert cover[-1][0] + cover[-1][1] == n

@@ -438,10 +438,12 @@ def test_conv3x3_block(gpu, B):
     y = ops.conv3x3_block(xg, wp1, b1.to(gpu), wp2, b2.to(gpu))
     tg = ops.conv3x3_rows(xg, wp1, b1.to(gpu), None, True, frag=True)
     y2 = ops.conv3x3_rows(tg, wp2, b2.to(gpu), xg, True, frag=True)
+    y_ws = ops.conv3x3_block(xg, wp1, b1.to(gpu), wp2, b2.to(gpu), variant=16)  # weight-stationary roles
     torch.cuda.synchronize()
     got = _nchw(y.float().cpu())
     assert _rel(got, ref) < 5e-3, _rel(got, ref)
     assert torch.equal(y, y2)
+    assert torch.equal(y_ws, y)
 
 
 @pytest.mark.parametrize("B", [1, 5])

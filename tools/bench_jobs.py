@@ -83,11 +83,18 @@ def main():
     ap.add_argument("--prefetch", action="store_true", help="stage every query image into HBM before predict")
     ap.add_argument("--node-gpus", type=int, default=1, help="GPUs per node (RCCL scatter inside a node)")
     ap.add_argument("--shards", default="", help="dir of labelled u8 shards: the jobs run over them from the SDFS")
+    ap.add_argument("--job-limit", type=int, default=0,
+                    help="images per job (shard jobs loop over their shards to reach it; default: one pass)")
+    ap.add_argument("--max-batch", type=int, default=256, help="dmlc-node --max-batch (coalesced forward size)")
+    ap.add_argument("--warm-frac", type=float, default=0.1,
+                    help="steady state: the first this fraction of each job's queries is excluded")
     a = ap.parse_args()
     shards = sorted(f for f in os.listdir(a.shards) if f.endswith(".u8s")) if a.shards else []
     if shards:
         from dmlc.utils.shards import shard_info
         a.images = sum(shard_info(os.path.join(a.shards, f))["n"] for f in shards)
+        if a.job_limit > 0:
+            a.images = a.job_limit
 
     ngpu = a.gpus
     if a.executor == "gpu" and ngpu == 0:
@@ -119,7 +126,7 @@ def main():
           enumerate(["resnet18", "alexnet"])}
     models = ",".join(f"{m}={p}" for m, p in ck.items())
     extra = ["--job-limit", str(a.images), "--query-interval-ms", str(a.interval_ms), "--query-batch",
-             str(a.batch), "--quiet-predictions", "--max-batch", str(max(8, a.batch)),
+             str(a.batch), "--quiet-predictions", "--max-batch", str(max(a.max_batch, a.batch)),
              "--adaptive-window", str(a.adaptive_window)] + (["--prefetch"] if a.prefetch else [])
     cl = LocalCluster(a.nodes, a.port, os.path.join(root, "c"), lab, n_leaders=2, executor=a.executor,
                       dataset=ds, models=models, fast=a.fast_periods, extra=extra)
@@ -197,8 +204,19 @@ def main():
     for j in jobs:
         d = [x / 1000 for x in j["durations_us"]]
         span = (max(j["done_us"]) - j["started_us"]) / 1e6 if j["done_us"] else None
+        # steady state: queries (equal-sized: --batch images, but a shard query
+        # never spans two shards) completed after the first warm_frac of them
+        done = sorted(x for x in j["done_us"] if x > 0)
+        k0 = int(len(done) * a.warm_frac)
+        steady = None
+        if len(done) - k0 >= 2 and done[-1] > done[k0]:
+            steady = round(j["finished"] * (len(done) - 1 - k0) / len(done) / ((done[-1] - done[k0]) / 1e6), 1)
+        ds = d[int(len(d) * a.warm_frac):]
         res["jobs"].append({"model": j["model"], "finished": j["finished"], "correct": j["correct"],
                             "images_per_s": round(j["finished"] / span, 1) if span else None,
+                            "steady_images_per_s": steady,
+                            "steady_p50_ms": round(pct(ds, 50), 3) if ds else None,
+                            "steady_p95_ms": round(pct(ds, 95), 3) if ds else None,
                             "mean_ms": round(statistics.mean(d), 3), "std_ms": round(statistics.pstdev(d), 3),
                             "p50_ms": round(pct(d, 50), 3), "p95_ms": round(pct(d, 95), 3),
                             "p99_ms": round(pct(d, 99), 3),

@@ -66,7 +66,11 @@ def _run(cmd: list[str], verbose: bool) -> None:
         sys.stderr.write(r.stdout + r.stderr)
         raise RuntimeError(f"build step failed: {' '.join(cmd[:3])} ... {cmd[-1]}")
     if SCRATCH_REMARK in cmd:
-        _check_scratch(r.stderr, cmd[-1])
+        try:
+            _check_scratch(r.stderr, cmd[-1])
+        except RuntimeError:
+            os.remove(cmd[-1])  # never leave the rejected object up to date for the next build
+            raise
 
 
 # Every hand-written kernel is register-resident by design: a spill to scratch

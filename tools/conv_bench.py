@@ -104,7 +104,7 @@ def main():
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     B = a.batch
-    tiles = [int(t) for t in a.tiles.split(",")]
+    tiles = [] if a.tiles == "none" else [int(t) for t in a.tiles.split(",")]
     warm_gpu()
     for name, H, W, Cin, Cout, k, s, p, pair in RESNET18:
         if a.only and name not in a.only.split(","):
