@@ -613,6 +613,43 @@ py::dict host_order_probe(bool bad, int timeout_ms) {
   return d;
 }
 
+// One group spanning two communicators, posted by the two ranks in opposite
+// communicator order (rank 0: send on A, recv on B; rank 1: send on B, recv
+// on A): valid for RCCL, so the host fake must complete it too.
+py::dict host_multi_world_probe(int timeout_ms) {
+  auto A = comm::host_world(2, timeout_ms), B = comm::host_world(2, timeout_ms);
+  std::vector<uint8_t> a(64, 1), b(64, 2), ra(64, 0), rb(64, 0);
+  std::string e0, e1;
+  {
+    py::gil_scoped_release nogil;
+    std::thread t1([&] {
+      try {
+        A[1]->group_start();
+        B[1]->send(b.data(), 64, 0, nullptr);
+        A[1]->recv(rb.data(), 64, 0, nullptr);
+        A[1]->group_end();
+      } catch (const std::exception& e) {
+        e1 = e.what();
+      }
+    });
+    try {
+      A[0]->group_start();
+      A[0]->send(a.data(), 64, 1, nullptr);
+      B[0]->recv(ra.data(), 64, 1, nullptr);
+      A[0]->group_end();
+    } catch (const std::exception& e) {
+      e0 = e.what();
+    }
+    t1.join();
+  }
+  py::dict d;
+  d["err0"] = e0;
+  d["err1"] = e1;
+  d["ok"] = ra == b && rb == a;
+  d["pending"] = comm::host_pending(*A[0]) + comm::host_pending(*B[0]);
+  return d;
+}
+
 // One-rank RCCL communicator on `device` (optionally CTA-capped) moving
 // `bytes` to itself with a grouped send/recv and a broadcast: exercises the
 // RcclComm wrapper and librccl on a one-GPU box (tests/test_dp_native_gpu.py).
@@ -671,6 +708,7 @@ class RcclLoop {
 void bind_dp(py::module& m) {
   m.def("dp_partition_devices", &dp::partition_devices, py::arg("live"), py::arg("jobs"));
   m.def("host_order_probe", &host_order_probe, py::arg("bad"), py::arg("timeout_ms") = 500);
+  m.def("host_multi_world_probe", &host_multi_world_probe, py::arg("timeout_ms") = 2000);
   py::class_<HostFleet>(m, "HostFleet")
       .def(py::init<std::vector<int>, int, int, int, int, int, int, std::map<std::string, uint32_t>, int, bool>(),
            py::arg("devices"), py::arg("H"), py::arg("W"), py::arg("lanes"), py::arg("delay_us"),

@@ -54,8 +54,17 @@ class HostWorld {
   // Post every op (matching what it can), then wait for all of them.
   // Throws CommError on failure or timeout (after withdrawing unmatched ops).
   void run(std::vector<Op*>& ops) {
-    std::unique_lock<std::mutex> g(mu_);
+    post_ops(ops);
+    wait_ops(ops);
+  }
+  // The two halves of run(): a group spanning several worlds posts into all
+  // of them before it waits on any (as an RCCL group spanning communicators).
+  void post_ops(std::vector<Op*>& ops) {
+    std::lock_guard<std::mutex> g(mu_);
     for (Op* o : ops) post(o);
+  }
+  void wait_ops(std::vector<Op*>& ops) {
+    std::unique_lock<std::mutex> g(mu_);
     const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms_);
     for (;;) {
       bool all = true;
@@ -200,10 +209,20 @@ void run_ops(std::vector<Pending>& ops) {
     by_world.begin()->first->run(by_world.begin()->second);
     return;
   }
-  // several worlds: run them one after another would deadlock if a peer's
-  // matching group posts them in another order; the protocols here never mix
-  // communicators in one group, so refuse instead of guessing.
-  throw std::logic_error("host comm: a group may not span several communicators");
+  // several worlds: post into every one before waiting on any (waiting world
+  // by world after posting all cannot deadlock: a peer's matching group has
+  // posted its side of every world too); the first error is rethrown once
+  // every world's ops are done or withdrawn
+  for (auto& kv : by_world) kv.first->post_ops(kv.second);
+  std::exception_ptr err;
+  for (auto& kv : by_world) {
+    try {
+      kv.first->wait_ops(kv.second);
+    } catch (...) {
+      if (!err) err = std::current_exception();
+    }
+  }
+  if (err) std::rethrow_exception(err);
 }
 
 class HostComm : public Comm {
