@@ -52,6 +52,7 @@ struct HeadArgs {
   float4* part;       // [B, NS] (max, argmax bits, sum, -)
   uint32_t* cnt;      // [ceil(B / kIPW)], zero between launches
   int B, HW, C, N, ldw, tiles_per_split, NS;
+  float scale;  // FP8 input: the e4m3 activation's dequantisation scale
   int ko;  // knock-out bits for timing experiments (head_pooled's ko, tools/head_bench.py): 2 = no fc loads
 };
 
@@ -69,7 +70,7 @@ __device__ __forceinline__ float tree_sum(const float* v, int n) {
   return t[0];
 }
 
-template <int TPG, int IPW, bool POOLED>
+template <int TPG, int IPW, bool POOLED, bool FP8 = false>
 __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   constexpr int kIPW = IPW;
@@ -99,11 +100,13 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
   const int c8 = C / 8;
   constexpr int PPT = 8 / TPG;
   constexpr int U = PPT >= 8 ? 2 : PPT >= 4 ? 4 : 8;  // pixels per part in flight
-  const float inv = 1.f / a.HW;
+  const float inv = (FP8 ? a.scale : 1.f) / a.HW;  // (avgpool_global's factor)
   for (int it = tid; it < ((a.ko & 1) ? 0 : c8 * TPG); it += 256) {
     const int cg = it % c8, q = it / c8;
     for (int i = 0; i < nimg; ++i) {
-      const bf16* base = a.x + ((long)(b0 + i) * a.HW) * C + cg * 8;
+      const long eoff = ((long)(b0 + i) * a.HW) * C + cg * 8;  // element offset
+      const bf16* base = a.x + eoff;
+      const uint8_t* base8 = (const uint8_t*)a.x + eoff;
       float ps[PPT][8];  // [part][channel]
 #pragma unroll
       for (int pp = 0; pp < PPT; ++pp)
@@ -116,7 +119,12 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
 #pragma unroll
           for (int u = 0; u < U; ++u) {
             const int pix = c0 + (q * PPT + pp) + 8 * u;
-            v[pp][u] = pix < a.HW ? *(const uint4*)(base + (long)pix * C) : make_uint4(0, 0, 0, 0);
+            if constexpr (FP8) {  // 8 e4m3 channels
+              const uint2 q8 = pix < a.HW ? *(const uint2*)(base8 + (long)pix * C) : make_uint2(0, 0);
+              v[pp][u] = make_uint4(q8.x, q8.y, 0, 0);
+            } else {
+              v[pp][u] = pix < a.HW ? *(const uint4*)(base + (long)pix * C) : make_uint4(0, 0, 0, 0);
+            }
           }
 #pragma unroll
         for (int pp = 0; pp < PPT; ++pp)
@@ -125,7 +133,19 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
             const int pix = c0 + (q * PPT + pp) + 8 * u;
             if (pix < a.HW) {
               float f[8];
-              unpack8(v[pp][u], f);
+              if constexpr (FP8) {
+                const int lo8 = (int)v[pp][u].x, hi8 = (int)v[pp][u].y;
+                f[0] = __builtin_amdgcn_cvt_f32_fp8(lo8, 0);
+                f[1] = __builtin_amdgcn_cvt_f32_fp8(lo8, 1);
+                f[2] = __builtin_amdgcn_cvt_f32_fp8(lo8, 2);
+                f[3] = __builtin_amdgcn_cvt_f32_fp8(lo8, 3);
+                f[4] = __builtin_amdgcn_cvt_f32_fp8(hi8, 0);
+                f[5] = __builtin_amdgcn_cvt_f32_fp8(hi8, 1);
+                f[6] = __builtin_amdgcn_cvt_f32_fp8(hi8, 2);
+                f[7] = __builtin_amdgcn_cvt_f32_fp8(hi8, 3);
+              } else {
+                unpack8(v[pp][u], f);
+              }
 #pragma unroll
               for (int j = 0; j < 8; ++j) ps[pp][j] += f[j];
             }
@@ -341,7 +361,8 @@ bool head_supported(int C, int N, int ldw, int Npad) {
 }
 
 void head_fused(const void* x, const void* w, const float* bias, int B, int HW, int C, int N, int ldw, int Npad,
-                float* logits, int32_t* idx, float* prob, void* ws, size_t ws_bytes, int num_cus, hipStream_t s) {
+                float* logits, int32_t* idx, float* prob, void* ws, size_t ws_bytes, int num_cus, hipStream_t s,
+                bool in_fp8, float scale) {
   if (B <= 0) return;
   if (!head_supported(C, N, ldw, Npad)) throw std::invalid_argument("head_fused: unsupported C/N/ldw");
   if (!x || !w || !bias || !logits || !idx || !prob || !ws) throw std::invalid_argument("head_fused: null pointer");
@@ -368,10 +389,17 @@ void head_fused(const void* x, const void* w, const float* bias, int B, int HW, 
   a.N = N;
   a.ldw = ldw;
   a.ko = 0;
+  a.scale = scale;
   const int c8 = C / 8, tpg = c8 >= 256 ? 1 : c8 >= 128 ? 2 : c8 >= 64 ? 4 : 8;
   const size_t lds = (size_t)kIPW * (C + 8) * 2 +
                      std::max((size_t)kIPW * a.tiles_per_split * 16 * 4, (size_t)tpg * kIPW * C * 4);
   if (lds > 160 * 1024) throw std::invalid_argument("head_fused: LDS budget exceeded");
+  if (in_fp8) {  // ResNet50 e4m3: the last bottleneck's output pooled straight from e4m3
+    if (tpg != 1) throw std::invalid_argument("head_fused: e4m3 input needs C >= 2048");
+    hipLaunchKernelGGL((head_kernel<1, kIPW, false, true>), dim3(groups, ns), dim3(256), lds, s, a);
+    DMLC_HIP_CHECK(hipGetLastError());
+    return;
+  }
   switch (tpg) {
     case 1: hipLaunchKernelGGL((head_kernel<1, kIPW, false>), dim3(groups, ns), dim3(256), lds, s, a); break;
     case 2: hipLaunchKernelGGL((head_kernel<2, kIPW, false>), dim3(groups, ns), dim3(256), lds, s, a); break;

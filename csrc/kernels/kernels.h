@@ -262,7 +262,8 @@ bool head_supported(int C, int N, int ldw, int Npad);
 int head_splits(int B, int N, int num_cus);
 size_t head_ws_bytes(int max_batch);
 void head_fused(const void* x, const void* w, const float* bias, int B, int HW, int C, int N, int ldw, int Npad,
-                float* logits, int32_t* idx, float* prob, void* ws, size_t ws_bytes, int num_cus, hipStream_t s);
+                float* logits, int32_t* idx, float* prob, void* ws, size_t ws_bytes, int num_cus, hipStream_t s,
+                bool in_fp8 = false, float scale = 1.f);  // in_fp8: x is e4m3 dequantised by scale (C >= 2048)
 // Same head on an already pooled bf16 [B, C] input (the last conv's fused
 // avgpool): fc + bias + softmax + top-1, 16 images per workgroup.
 void head_pooled(const void* pooled, const void* w, const float* bias, int B, int C, int N, int ldw, int Npad,

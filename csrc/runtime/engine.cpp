@@ -730,8 +730,10 @@ bool Engine::head_fusable(size_t oi) const {
   const Op& fc = ops_[oi + 1];
   const Op& sm = ops_[oi + 2];
   if (pool.type != OpType::AvgPoolGlobal || fc.type != OpType::Conv || sm.type != OpType::SoftmaxTop1) return false;
-  if (shapes_[pool.in].fp8 || fc.in != pool.out || sm.in != fc.out || !shapes_[fc.out].f32) return false;
+  if (fc.in != pool.out || sm.in != fc.out || !shapes_[fc.out].f32 || shapes_[pool.out].fp8) return false;
   const ConvLayer& L = convs_[fc.conv];
+  // (an e4m3 pool input, ResNet50 fp8: pooled from e4m3 in the head, C >= 2048)
+  if (shapes_[pool.in].fp8 && shapes_[pool.in].C < 2048) return false;
   return L.fc && !L.fp8 && !L.relu && L.cin == shapes_[pool.in].C && head_supported(L.cin, L.cout, L.kpad, L.npad);
 }
 
@@ -1169,7 +1171,8 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
           head_fused(acts_[op.in], (const uint8_t*)warena_ + L.w_off,
                      (const float*)((const uint8_t*)warena_ + L.b_off), B, i.H * i.W, i.C, L.cout, L.kpad, L.npad,
                      logits ? logits : (float*)acts_[ops_[oi + 1].out], idx ? idx : dummy_idx_,
-                     prob ? prob : (float*)(dummy_idx_ + max_batch_), head_ws_, head_ws_bytes_, num_cus_, s);
+                     prob ? prob : (float*)(dummy_idx_ + max_batch_), head_ws_, head_ws_bytes_, num_cus_, s, i.fp8,
+                     i.scale);
           skip = 2;
           break;
         }

@@ -68,6 +68,29 @@ def test_engine_resnet50_fp8(gpu):
     assert torch.equal(i2.cpu(), idx.cpu())
 
 
+@pytest.mark.parametrize("B", [16, 64])
+def test_resnet50_fp8_fused_head_matches_unfused(gpu, B):
+    """The fused head reads ResNet50 e4m3's last activation directly (pool
+    from e4m3 + dequantisation scale, fc, softmax/top-1) instead of three
+    launches (fp8 avgpool, fc, softmax): pooled vectors bit-identical to the
+    fp8 avgpool kernel's, the fc summed in another order, so logits agree to
+    fp32 rounding; replayed twice (the combine tickets re-arm)."""
+    model = build("resnet50", seed=13, randomize_bn=True)
+    sd = state_dict_f32(model)
+    ref_eng = InferenceEngine("resnet50_fp8", sd, max_batch=B, options={"fused_head": False})
+    eng = InferenceEngine("resnet50_fp8", sd, max_batch=B, options={"fused_head": True})
+    g = torch.Generator().manual_seed(70 + B)
+    img = torch.randint(0, 256, (B, 224, 224, 3), generator=g, dtype=torch.uint8).to(gpu)
+    ri, rp, rl = ref_eng.predict(img, return_logits=True)
+    for _ in range(2):
+        i, p, lg = eng.predict(img, return_logits=True)
+        torch.cuda.synchronize()
+        assert torch.allclose(lg, rl, rtol=1e-4, atol=1e-4), (lg - rl).abs().max().item()
+        top2 = torch.softmax(rl, -1).topk(2, -1).values
+        assert torch.all((i == ri) | ((top2[:, 0] - top2[:, 1]) < 1e-5))
+        assert torch.allclose(p, rp, rtol=1e-4, atol=1e-6)
+
+
 def test_graph_replay_matches_eager(gpu):
     eng = InferenceEngine("resnet18", max_batch=32)
     img = torch.randint(0, 256, (32, 224, 224, 3), dtype=torch.uint8, device=gpu)

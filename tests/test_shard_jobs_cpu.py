@@ -158,3 +158,32 @@ def test_unservable_queries_are_dropped_not_retried_forever(tsan_bin, tmp_path):
         assert re.search(r"Model: resnet18\n\tAccuracy: \d+/6", out), out
         assert re.search(r"Model: alexnet\n\tAccuracy: 0/0 .*\n.*\n.*\n\tUnanswered: 6 images", out), out
     _no_reports(nd)
+
+
+def test_shard_job_loops_to_job_limit(tsan_bin, tmp_path):
+    """Sustained runs (tools/bench_jobs.py --job-limit): a shard job whose
+    --job-limit exceeds its shards' images loops over them, each image scored
+    against its own label on every pass: 40 queries over the 16-image shard
+    = 2.5 passes, 12 + 12 + 6 right."""
+    labels = synthetic_labels(1000)
+    lab = write_labels(str(tmp_path / "synset_words.txt"), labels)
+    ds = make_synthetic_dataset(str(tmp_path / "train"), labels[:4], size=(48, 64))
+    rng = np.random.default_rng(6)
+    label0, n = 200, 16
+    targets = [label0 + i if i % 4 else (label0 + i + 500) % 1000 for i in range(n)]
+    imgs = np.stack([_craft(t, rng) for t in targets])
+    shard = write_shard(str(tmp_path / "loop.u8s"), imgs, label0=label0)
+    cl = LocalCluster(2, 20820, str(tmp_path / "c"), lab, n_leaders=1, executor="digest", dataset=ds,
+                      models="resnet18=-,alexnet=-", binary=tsan_bin, env=TSAN_ENV,
+                      extra=["--query-batch", "3", "--adaptive-window", "2", "--job-limit", "40",
+                             "--quiet-predictions"])
+    with cl:
+        nd = cl.nodes
+        assert "Stored on:" in nd[1].cmd(f"put {shard} loop.u8s")
+        deadline = time.time() + 30
+        while time.time() < deadline and not all("loop.u8s@v1" in x.cmd("replicas") for x in nd):
+            time.sleep(0.2)
+        nd[0].cmd("predict loop.u8s")
+        out = _wait_jobs(nd[0], [40, 40])
+        assert len(re.findall(r"Accuracy: 30/40 = 75\.00%", out)) == 2, out
+    _no_reports(nd)

@@ -30,8 +30,21 @@ def main():
     ap.add_argument("--per", type=int, default=250, help="images per shard")
     ap.add_argument("--limit", type=int, default=0, help="only the first N classes")
     ap.add_argument("--name", default="imagenet_1k")
+    ap.add_argument("--synthetic", type=int, default=0,
+                    help="N random 224x224 images (labels 0..N-1) instead of a dataset (throughput runs on a box "
+                         "without the reference's JPEGs)")
     a = ap.parse_args()
     from dmlc.utils.shards import decode_resize, write_shard
+    if a.synthetic:
+        import numpy as np
+        os.makedirs(a.out, exist_ok=True)
+        rng = np.random.default_rng(0)
+        for k, s in enumerate(range(0, a.synthetic, a.per)):
+            n = min(a.per, a.synthetic - s)
+            imgs = rng.integers(0, 256, size=(n, 224, 224, 3), dtype=np.uint8)
+            p = write_shard(os.path.join(a.out, f"{a.name}.{k}.u8s"), imgs, label0=s)
+            print(f"{p}: synthetic images {s}..{s + n - 1}", flush=True)
+        return
     wnids = sorted(os.listdir(a.src))
     if a.limit:
         wnids = wnids[:a.limit]
