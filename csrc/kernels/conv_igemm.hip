@@ -519,8 +519,27 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(ConvArgs a, int M, i
   for (long idx = blockIdx.x * 256L + threadIdx.x; idx < total; idx += (long)gridDim.x * 256) {
     const int m = (int)(idx / n4);
     const int n = (int)(idx - (long)m * n4) * 4;
+    // all of a group's partial loads in flight at once (a plain loop waited
+    // on each in turn: one L2 round trip per split, ~5 us per reduce at B=1)
     floatx4 s = {0.f, 0.f, 0.f, 0.f};
-    for (int k = 0; k < splits; ++k) s += *(const floatx4*)(a.ws + ((size_t)k * M + m) * a.Npad + n);
+    const float* wp = a.ws + (size_t)m * a.Npad + n;
+    const size_t sstride = (size_t)M * a.Npad;
+    int k = 0;
+    for (; k + 8 <= splits; k += 8) {
+      floatx4 t[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) t[u] = *(const floatx4*)(wp + (size_t)(k + u) * sstride);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += t[u];
+    }
+    for (; k + 4 <= splits; k += 4) {
+      floatx4 t[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) t[u] = *(const floatx4*)(wp + (size_t)(k + u) * sstride);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) s += t[u];
+    }
+    for (; k < splits; ++k) s += *(const floatx4*)(wp + (size_t)k * sstride);
     if (a.bias) s += *(const floatx4*)(a.bias + n);
     const size_t o = (size_t)m * a.ldo + n;
     if (a.res) {

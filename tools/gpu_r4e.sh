@@ -3,7 +3,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 240 python tools/b1_sweep.py > gpurun_out/r4e_b1.log 2>&1 || { tail -20 gpurun_out/r4e_b1.log; exit 1; }
+timeout -k 10 240 python tools/b1_sweep.py --tiles 0,2,3,5,6,7,8,9,10 --splits 1,2,4,8,16,32 > gpurun_out/r4e_b1.log 2>&1 || { tail -20 gpurun_out/r4e_b1.log; exit 1; }
 grep -v amdgpu.ids gpurun_out/r4e_b1.log | cut -c1-200
 timeout -k 10 120 python tools/make_shards.py --synthetic 1000 --per 250 --out /tmp/shards > gpurun_out/r4e_mk.log 2>&1 || { tail -5 gpurun_out/r4e_mk.log; exit 1; }
 for cfg in "64 4" "128 4"; do
