@@ -41,7 +41,7 @@ def main():
         d = collections.defaultdict(list)
         for s, e, name, g, w in ph:
             d[name].append((e - s) / 1000.0)
-        nf = n or max(len(v) for v in d.values())
+        nf = n or max(1, sum(len(v) for k, v in d.items() if "stem" in k))  # one stem per forward
         print(f"## {title}: per forward ({nf} forwards)")
         tot = 0.0
         for name, v in sorted(d.items(), key=lambda kv: -sum(kv[1])):
