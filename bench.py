@@ -251,7 +251,7 @@ def main():
     # and the JPEG decode): that one is tools/bench_jobs.py's.
     qlat = []
     if rank == 0 and args.latency_queries > 0:
-        q_eng = InferenceEngine(args.model, sd, device=local_rank, max_batch=1)
+        q_eng = InferenceEngine(args.model, sd, device=local_rank, max_batch=1, options=opts)
         qimg = pool[:1].contiguous()
         qout = (torch.empty(1, dtype=torch.int32, device=dev), torch.empty(1, dtype=torch.float32, device=dev))
         for i in range(args.latency_queries + 20):

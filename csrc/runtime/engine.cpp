@@ -88,6 +88,7 @@ bool EngineOptions::set(const std::string& name, bool v) {
       {"fork_ds", &EngineOptions::fork_ds},         {"fp8_3x3", &EngineOptions::fp8_3x3},
       {"conv1x1", &EngineOptions::conv1x1},         {"s2rows", &EngineOptions::s2rows},
       {"rows28", &EngineOptions::rows28},           {"stem_roles", &EngineOptions::stem_roles},
+      {"igemm_small_m", &EngineOptions::igemm_small_m},
   };
   for (const auto& f : fields)
     if (name == f.first) {
@@ -678,6 +679,14 @@ ConvArgs Engine::conv_args(const Op& op, int B, float* logits) const {
   if (os.fp8) a.out_inv_scale = 1.f / os.scale;
   int s = conv_pick_split_k(a, num_cus_);
   const size_t M = (size_t)B * os.H * os.W;
+  if (opt_.igemm_small_m && M <= 1024 && !L.pair && !L.fc && !L.fp8 && !os.fp8 && !os.f32 && L.npad % 128 == 0) {
+    // 64x256 ns3 for the narrowest outputs, else 128x128 ns3 (conv_igemm.hip tile table)
+    a.tile = (M <= 64 && L.npad % 256 == 0) ? 5 : 3;
+    const int bm = a.tile == 5 ? 64 : 128, bn = a.tile == 5 ? 256 : 128;
+    const int tiles = (int)((M + bm - 1) / bm) * (L.npad / bn);
+    const int k_tiles = L.kpad / 64;
+    s = std::max(1, std::min({k_tiles / 2, (num_cus_ / 2 + tiles - 1) / tiles, 32}));
+  }
   while (s > 1 && (size_t)s * M * L.npad > ws_elems_) --s;
   a.split_k = s;
   a.ws = ws_;

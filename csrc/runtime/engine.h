@@ -69,6 +69,11 @@ struct Op {
 // False}); the names are the field names.
 struct EngineOptions {
   bool persistent = true;        // persistent (grid-stride) implicit-GEMM conv grids
+  // query-sized implicit GEMMs (M = B*Ho*Wo <= 1024, e.g. batch 1): 3-stage
+  // tiles and enough K slices to put ~half the CUs to work (the 2-stage tile
+  // with <= 9 slices ran 12 us per conv at batch 1, latency of one K tile
+  // at a time: profiles/r4_resnet18_b256_kernel_stats_baseline.txt)
+  bool igemm_small_m = true;
   bool fused_stem = true;        // conv1 + BN + ReLU + maxpool in one kernel (stem_pool.hip)
   bool fused_preprocess = true;  // SxS u8 images straight into the fused stem (no preprocess pass)
   bool row_conv = true;          // direct row-streaming 3x3 convs (conv3x3_rows.hip) for 56x56x64
