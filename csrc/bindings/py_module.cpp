@@ -234,6 +234,17 @@ PYBIND11_MODULE(_C, m) {
                    P<void>(zero), B, relu, S(stream), dbg);
   }, py::arg("x"), py::arg("wf"), py::arg("bias"), py::arg("wdf"), py::arg("bd"), py::arg("y"), py::arg("yd"),
         py::arg("zero"), py::arg("B"), py::arg("relu"), py::arg("stream"), py::arg("dbg") = 0);
+  m.def("conv_small_supported", &conv_small_supported);
+  m.def("conv_small_pick_mf", &conv_small_pick_mf);
+  m.def("conv_small_set_mf", &conv_small_set_mf);
+  m.def("conv_small", [](uintptr_t x, uintptr_t wf, uintptr_t bias, uintptr_t res, uintptr_t y, int B, int H, int W,
+                         int CI, int CO, int stride, bool relu, int mf, uintptr_t stream, uintptr_t wdf, uintptr_t bd,
+                         uintptr_t yd) {
+    conv_small(P<void>(x), P<void>(wf), P<float>(bias), P<void>(res), P<void>(y), B, H, W, CI, CO, stride, relu, mf,
+               S(stream), P<void>(wdf), P<float>(bd), P<void>(yd));
+  }, py::arg("x"), py::arg("wf"), py::arg("bias"), py::arg("res"), py::arg("y"), py::arg("B"), py::arg("H"),
+        py::arg("W"), py::arg("CI"), py::arg("CO"), py::arg("stride"), py::arg("relu"), py::arg("mf"),
+        py::arg("stream"), py::arg("wdf") = 0, py::arg("bd") = 0, py::arg("yd") = 0);
   m.def("conv3x3_rows28_supported", &conv3x3_rows28_supported);
   m.def("conv3x3_rows28", [](uintptr_t x, uintptr_t wf, uintptr_t bias, uintptr_t res, uintptr_t y, int B, bool relu,
                              uintptr_t stream, int dbg) {

@@ -200,6 +200,18 @@ void conv3x3_s2rows(const void* x, const void* wf, const float* bias, const void
 bool conv3x3_rows28_supported(int H, int W, int Cin, int Cout);
 void conv3x3_rows28(const void* x, const void* wf, const float* bias, const void* res, void* y, int B, bool relu,
                     hipStream_t s, int dbg = 0);
+// Query-batch 3x3/p1 conv (conv_small.hip) for B <= a few images: one launch
+// per conv, no split-K. x [B,H,W,CI] bf16 NHWC (CI in 64..512), wf: fragment-
+// order weights (stream_frag_index, K = 9 CI), y = relu?(conv + bias (+ res)).
+// Stride 2 with wdf/bd/yd also computes the block's 1x1/s2 downsample
+// (fragment-order weights, K = CI) into yd. mf: pixel fragments of 16 per
+// workgroup (1, 2 or 4; conv_small_pick_mf).
+bool conv_small_supported(int H, int W, int CI, int CO, int stride);
+int conv_small_pick_mf(int B, int H, int W, int CI, int CO, int stride, int num_cus);
+void conv_small_set_mf(int mf);  // A/B override of the pick (0 = heuristic)
+void conv_small(const void* x, const void* wf, const float* bias, const void* res, void* y, int B, int H, int W,
+                int CI, int CO, int stride, bool relu, int mf, hipStream_t s, const void* wdf = nullptr,
+                const float* bd = nullptr, void* yd = nullptr);
 // Direct 3x3/p1 conv with the input image resident in LDS and per-wave weight
 // rings (conv3x3_stream.hip): stride 1 on 28x28x128, 14x14x256, 7x7x512;
 // stride 2 on 56x56x64 -> 128 and 28x28x128 -> 256. Hin/Win are the input

@@ -89,6 +89,7 @@ bool EngineOptions::set(const std::string& name, bool v) {
       {"conv1x1", &EngineOptions::conv1x1},         {"s2rows", &EngineOptions::s2rows},
       {"rows28", &EngineOptions::rows28},           {"stem_roles", &EngineOptions::stem_roles},
       {"igemm_small_m", &EngineOptions::igemm_small_m},
+      {"small_conv", &EngineOptions::small_conv},
   };
   for (const auto& f : fields)
     if (name == f.first) {
@@ -430,7 +431,13 @@ void Engine::pack_weights(const WeightMap& w) {
     L.wf_off = 0;
     // (3x3 convs the register-weight stream conv runs, and the 1x1/s2
     // downsample it fuses next to a stride-2 one)
-    if (!L.fp8 && !L.fc && !L.pair && !L.stem_pool && L.in_act >= 0 && L.cout % 32 == 0 && L.kpad % 32 == 0 &&
+    // (and every 3x3/p1 conv and 1x1/s2 downsample the query-batch conv can
+    // run: conv_small.hip)
+    const bool small =
+        !L.fp8 && !L.fc && !L.pair && !L.stem_pool && L.in_act >= 0 && L.cout % 32 == 0 &&
+        ((L.kh == 3 && L.kw == 3 && L.pad == 1) || (L.kh == 1 && L.kw == 1 && L.stride == 2 && L.pad == 0)) &&
+        conv_small_supported(shapes_[L.in_act].H, shapes_[L.in_act].W, shapes_[L.in_act].C, L.cout, L.stride);
+    if (small || (!L.fp8 && !L.fc && !L.pair && !L.stem_pool && L.in_act >= 0 && L.cout % 32 == 0 && L.kpad % 32 == 0 &&
         (((L.kh == 3 && L.kw == 3) || (L.kh == 1 && L.kw == 1 && L.stride == 2)) &&
              (conv3x3_stream_uses_frag(shapes_[L.in_act].H, shapes_[L.in_act].W, shapes_[L.in_act].C, L.cout,
                                        L.stride) ||
@@ -440,7 +447,7 @@ void Engine::pack_weights(const WeightMap& w) {
                conv3x3_rows28_supported(shapes_[L.in_act].H, shapes_[L.in_act].W, shapes_[L.in_act].C, L.cout))) ||
          (L.kh == 3 && L.kw == 3 && L.stride == 1 && L.pad == 1 &&
           (conv3x3_rows_supported(shapes_[L.in_act].H, shapes_[L.in_act].W, shapes_[L.in_act].C, L.cout) ||
-           conv3x3_13_supported(shapes_[L.in_act].H, shapes_[L.in_act].W, shapes_[L.in_act].C, L.cout))))) {
+           conv3x3_13_supported(shapes_[L.in_act].H, shapes_[L.in_act].W, shapes_[L.in_act].C, L.cout)))))) {
       L.wf_off = off;  // fragment-order copy for the register-weight stream conv
       off = align_up(off + (size_t)L.cout * L.kpad * 2, 256);
     }
@@ -712,6 +719,11 @@ Engine::ConvPath Engine::conv_path(const Op& op, int B) const {
   // its rows (59-60 us vs 62-66 us for the stream conv at B=256,
   // profiles/r2_rows28.txt), once the batch fills >= ~70% of one round
   const int rounds = (B + num_cus_ - 1) / num_cus_;
+  // query batches: one launch per conv, no split-K (conv_small.hip)
+  if (opt_.small_conv && k3 && L.wf_off && B <= kSmallConvMaxB &&
+      conv_small_supported(is.H, is.W, is.C, L.cout, L.stride) &&
+      !(opt_.direct13 && conv3x3_13_supported(is.H, is.W, is.C, L.cout)))  // (AlexNet keeps its fused pools)
+    return ConvPath::Small;
   if (opt_.rows28 && k3 && L.stride == 1 && L.wf_off && 10 * B >= 7 * rounds * num_cus_ &&
       conv3x3_rows28_supported(is.H, is.W, is.C, L.cout))
     return ConvPath::Rows28;
@@ -775,7 +787,7 @@ bool Engine::ds_fusable(size_t oi, int B) const {
   const ConvLayer& L = convs_[c.conv];
   return !D.fc && !D.fp8 && D.kh == 1 && D.kw == 1 && D.stride == 2 && D.pad == 0 && !D.relu && d.res < 0 &&
          D.cout == L.cout && L.stride == 2 && !shapes_[d.out].fp8 && !shapes_[d.out].f32 &&
-         conv_path(c, B) == ConvPath::Stream;
+         (conv_path(c, B) == ConvPath::Stream || (conv_path(c, B) == ConvPath::Small && D.wf_off));
 }
 
 // ops[oi], ops[oi+1] = conv1 (+ReLU) and conv2 (+identity residual, ReLU) of
@@ -1099,6 +1111,22 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
             }
             conv5x5_27(acts_[op.in], (const uint8_t*)warena_ + L.wf_off,
                        (const float*)((const uint8_t*)warena_ + L.b_off), acts_[op.out], zero_, B, cs, ypool);
+            break;
+          }
+          case ConvPath::Small: {
+            const uint8_t* wa = (const uint8_t*)warena_;
+            const ConvLayer* D = nullptr;
+            int yd = -1;
+            if (skip_ds >= 0 && skip_ds + 1 == (int)oi) {
+              D = &convs_[ops_[skip_ds].conv];
+              yd = ops_[skip_ds].out;
+            }
+            conv_small(acts_[op.in], wa + L.wf_off, (const float*)(wa + L.b_off), op.res >= 0 ? acts_[op.res] : nullptr,
+                       acts_[op.out], B, is.H, is.W, is.C, L.cout, L.stride, L.relu,
+                       conv_small_pick_mf(B, is.H, is.W, is.C, L.cout, L.stride, num_cus_), cs,
+                       D ? wa + D->wf_off : nullptr, D ? (const float*)(wa + D->b_off) : nullptr,
+                       D ? acts_[yd] : nullptr);
+            skip_ds = -1;
             break;
           }
           case ConvPath::Rows28:

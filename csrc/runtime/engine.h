@@ -67,6 +67,8 @@ struct Op {
 // the plain one it replaces (tests/test_engine_gpu.py) and so a path can be
 // A/B-timed (profiles/). Python: InferenceEngine(..., options={"fused_block":
 // False}); the names are the field names.
+constexpr int kSmallConvMaxB = 4;  // largest batch on the query-batch conv path
+
 struct EngineOptions {
   bool persistent = true;        // persistent (grid-stride) implicit-GEMM conv grids
   // query-sized implicit GEMMs (M = B*Ho*Wo <= 1024, e.g. batch 1): 3-stage
@@ -74,6 +76,9 @@ struct EngineOptions {
   // with <= 9 slices ran 12 us per conv at batch 1, latency of one K tile
   // at a time: profiles/r4_resnet18_b256_kernel_stats_baseline.txt)
   bool igemm_small_m = true;
+  // query batches (B <= kSmallConvMaxB): every 3x3 conv (+ its block's 1x1/s2
+  // downsample) as one conv_small.hip launch, no split-K reduction kernels
+  bool small_conv = true;
   bool fused_stem = true;        // conv1 + BN + ReLU + maxpool in one kernel (stem_pool.hip)
   bool fused_preprocess = true;  // SxS u8 images straight into the fused stem (no preprocess pass)
   bool row_conv = true;          // direct row-streaming 3x3 convs (conv3x3_rows.hip) for 56x56x64
@@ -175,7 +180,7 @@ class Engine {
   void run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* idx, float* prob,
                float* logits, hipStream_t s, std::vector<hipEvent_t>* evs, bool trace);
   ConvArgs conv_args(const Op& op, int B, float* logits) const;
-  enum class ConvPath { Stream, Rows, Rows28, Direct13, Direct27, OneByOne, BigTile, Igemm };
+  enum class ConvPath { Stream, Rows, Rows28, Direct13, Direct27, OneByOne, BigTile, Igemm, Small };
   ConvPath conv_path(const Op& op, int B) const;
   bool side_safe(int B) const;
   bool head_fusable(size_t oi) const;

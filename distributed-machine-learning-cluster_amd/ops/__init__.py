@@ -220,6 +220,37 @@ def conv3x3_s2rows(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, 
     return y, yd
 
 
+def conv_small(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, res: torch.Tensor | None = None,
+               relu: bool = True, stride: int = 1, wd_packed: torch.Tensor | None = None,
+               bd: torch.Tensor | None = None, mf: int | None = None):
+    """Query-batch 3x3/p1 conv (conv_small.hip) on NHWC bf16 [B,H,W,CI]:
+    relu?(conv3x3(x) + bias (+ res)). w_packed: conv2d packed weights
+    [Cout, 9 CI]. With stride 2 and wd_packed [Cout, CI] / bd also returns the
+    1x1/s2 downsample conv1x1_s2(x) + bd: (y, yd)."""
+    _need_cuda(x, w_packed, bias, res, wd_packed, bd)
+    C = native()
+    B, H, W, Cin = x.shape
+    Cout = w_packed.shape[0]
+    if not C.conv_small_supported(H, W, Cin, Cout, stride) or tuple(w_packed.shape) != (Cout, 9 * Cin):
+        raise ValueError("conv_small: unsupported shape")
+    Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
+    if res is not None and tuple(res.shape) != (B, Ho, Wo, Cout):
+        raise ValueError("conv_small: residual shape")
+    if wd_packed is not None and (stride != 2 or bd is None or tuple(wd_packed.shape) != (Cout, Cin)):
+        raise ValueError("conv_small: downsample needs stride 2, bd and [Cout, Cin] weights")
+    if mf is None:
+        cus = torch.cuda.get_device_properties(x.device).multi_processor_count
+        mf = C.conv_small_pick_mf(B, H, W, Cin, Cout, stride, cus)
+    x = x.contiguous()
+    y = torch.empty(B, Ho, Wo, Cout, dtype=x.dtype, device=x.device)
+    yd = torch.empty_like(y) if wd_packed is not None else None
+    wdf = stream_weight_frag(wd_packed) if wd_packed is not None else None
+    C.conv_small(_ptr(x), _ptr(stream_weight_frag(w_packed)), _ptr(bias.float().contiguous()),
+                 _ptr(None if res is None else res.contiguous()), _ptr(y), B, H, W, Cin, Cout, stride, relu, mf,
+                 _stream(), _ptr(wdf), _ptr(None if bd is None else bd.float().contiguous()), _ptr(yd))
+    return (y, yd) if wd_packed is not None else y
+
+
 def conv3x3_rows28(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, res: torch.Tensor | None = None,
                    relu: bool = True) -> torch.Tensor:
     """Weight-stationary row-streaming 3x3/s1/p1 conv on [B,28,28,128] ->

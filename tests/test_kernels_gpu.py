@@ -470,6 +470,38 @@ def test_conv3x3_s2rows(gpu, B):
     assert (yd.float() - yd0.float()).abs().max().item() < 0.05
 
 
+# every ResNet18/34 3x3 shape at query batches; mf None = the engine's pick
+@pytest.mark.parametrize("HW,Cin,Cout,stride", [(56, 64, 64, 1), (56, 64, 128, 2), (28, 128, 128, 1),
+                                                (28, 128, 256, 2), (14, 256, 256, 1), (14, 256, 512, 2),
+                                                (7, 512, 512, 1)])
+@pytest.mark.parametrize("B,mf", [(1, None), (1, 1), (1, 2), (1, 4), (3, None)])
+def test_conv_small(gpu, HW, Cin, Cout, stride, B, mf):
+    """Query-batch conv (conv_small.hip) vs torch fp32: stride 1 with a
+    residual, stride 2 with the fused 1x1/s2 downsample."""
+    g = torch.Generator().manual_seed(53 + HW + Cin)
+    x = torch.randn(B, Cin, HW, HW, generator=g).bfloat16().float()
+    w = (torch.randn(Cout, Cin, 3, 3, generator=g) / (3 * Cin ** 0.5)).bfloat16().float()
+    bias = torch.randn(Cout, generator=g) * 0.1
+    wp = ops.pack_conv_weight(w, device=gpu)
+    xg = _nhwc(x).bfloat16().to(gpu)
+    if stride == 1:
+        r = torch.randn(B, Cout, HW, HW, generator=g).bfloat16().float()
+        ref = F.relu(F.conv2d(x, w, bias, 1, 1) + r)
+        y = ops.conv_small(xg, wp, bias.to(gpu), _nhwc(r).bfloat16().to(gpu), True, mf=mf)
+        torch.cuda.synchronize()
+        assert _rel(_nchw(y.float().cpu()), ref) < 5e-3, _rel(_nchw(y.float().cpu()), ref)
+    else:
+        wd = (torch.randn(Cout, Cin, 1, 1, generator=g) / Cin ** 0.5).bfloat16().float()
+        bd = torch.randn(Cout, generator=g) * 0.1
+        ref = F.relu(F.conv2d(x, w, bias, 2, 1))
+        ref_d = F.conv2d(x, wd, bd, 2, 0)
+        y, yd = ops.conv_small(xg, wp, bias.to(gpu), None, True, stride=2,
+                               wd_packed=ops.pack_conv_weight(wd, device=gpu), bd=bd.to(gpu), mf=mf)
+        torch.cuda.synchronize()
+        assert _rel(_nchw(y.float().cpu()), ref) < 5e-3, _rel(_nchw(y.float().cpu()), ref)
+        assert _rel(_nchw(yd.float().cpu()), ref_d) < 5e-3, _rel(_nchw(yd.float().cpu()), ref_d)
+
+
 @pytest.mark.parametrize("B,res", [(1, False), (3, True), (2, False)])
 def test_conv3x3_rows28(gpu, B, res):
     """Weight-stationary row-streaming layer2 conv (conv3x3_rows28.hip) vs

@@ -336,3 +336,60 @@ def test_stem_row_rotation_from_permlane_swaps():
     p16 = _permlane16_swap(z, x)
     y = [p16[0][l] if (l & 16) else p16[1][l] for l in range(64)]
     assert y == [(l - 16) % 64 for l in range(64)]
+
+
+def _small_swz(q, ch):
+    return (q & 15) if ch >= 16 else ((q >> 1) & 7)
+
+
+@pytest.mark.parametrize("H,CI,S", [(56, 64, 1), (56, 64, 2), (28, 128, 1), (28, 128, 2), (14, 256, 1),
+                                    (14, 256, 2), (7, 512, 1)])
+@pytest.mark.parametrize("mf", [1, 2, 4])
+def test_conv_small_lds_addressing(H, CI, S, mf):
+    """conv_small.hip: every (pixel, tap, channel chunk) the K loop reads from
+    the staged rows is the input chunk it needs (zero chunk for padding taps,
+    the DMA's source permutation inverted). The ds_read_b128 fragment reads
+    are at most 4-way bank conflicted (stride 2 puts the 16 pixels of a
+    fragment 2 apart; a fragment that wraps an output row jumps): tolerated
+    on this latency-bound query-batch path, where LDS is far from busy."""
+    W = H
+    CH, KPT = CI // 8, CI // 32
+    Ho = (H - 1) // S + 1
+    P = Ho * Ho
+    tp = mf * 16
+    worst = 1
+    tiles = list(range(0, P, tp))
+    for p0 in {tiles[0], tiles[len(tiles) // 2], tiles[-1]}:
+        p1 = min(p0 + tp, P)
+        oh_lo, oh_hi = p0 // Ho, (p1 - 1) // Ho
+        ih_lo, ih_hi = max(0, oh_lo * S - 1), min(H - 1, oh_hi * S + 1)
+        total = (ih_hi - ih_lo + 1) * W * CH
+        # DMA: LDS slot s <- input chunk (row, col, c)
+        staged = {}
+        for s in range(total):
+            q, cp = divmod(s, CH)
+            staged[s] = (ih_lo + q // W, q % W, cp ^ _small_swz(q, CH))
+        assert len(set(staged.values())) == total
+        for t in range(9 * KPT):
+            tap = t // KPT
+            kh, kw = divmod(tap, 3)
+            for f in range(mf):
+                addr = []
+                for l in range(64):
+                    fr, fq = l & 15, l >> 4
+                    c = (t % KPT) * 4 + fq
+                    p = p0 + 16 * f + fr
+                    oh, ow = divmod(p, Ho)
+                    ih, iw = oh * S - 1 + kh, ow * S - 1 + kw
+                    ok = p < p1 and 0 <= ih < H and 0 <= iw < W
+                    if not ok:
+                        addr.append(-16)  # the zero chunk
+                        continue
+                    q = (oh * S - 1 - ih_lo) * W + (ow * S - 1) + kh * W + kw
+                    slot = q * CH + (c ^ _small_swz(q, CH))
+                    assert staged[slot] == (ih, iw, c), (p0, t, f, l)
+                    addr.append(slot * 16)
+                real = [a for a in addr if a >= 0]
+                if real:
+                    worst = max(worst, _b128_ways([a if a >= 0 else real[0] for a in addr]))
+    assert worst <= 4, worst
