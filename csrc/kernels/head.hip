@@ -83,6 +83,42 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int b0 = g * kIPW;
   const int nimg = min(kIPW, a.B - b0);
+  // fc weights of this wave's first tile pair, issued before the pooling so
+  // their latency overlaps it (every wave has at most one tile pair when the
+  // split is <= 8 tiles, and one 512-deep K chunk when C <= 512): one memory
+  // round trip less on the chain pool -> fc -> softmax -> merge
+  const int col = lane & 15, kq = lane >> 4;
+  const int nsplit = a.tiles_per_split * 16;
+  const int n_begin = split * nsplit;
+  const bool pre = a.tiles_per_split <= 8 && C <= 512;
+  bf16x8 pwa[16], pwb[16];
+  float pbv[2][4];
+  auto load_tile_pair = [&](int t, bf16x8* wa, bf16x8* wb, float (*bv)[4], int kc) __attribute__((always_inline)) {
+    const int n0 = n_begin + t * 16;
+    const bool two = t + 4 < a.tiles_per_split && n0 + 64 < a.N;
+    // bias of this lane's 4 (+4) classes, in flight with the weight loads
+    // (loaded after the MFMAs they cost a dependent round trip per tile)
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bv[h][r] = (h == 0 || two) ? a.bias[n_begin + (t + 4 * h) * 16 + kq * 4 + r] : 0.f;
+    const bf16* w0 = a.w + (long)(n0 + col) * a.ldw + kq * 8;
+    const bf16* w1 = w0 + 64L * a.ldw;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int k = kc + 32 * u;
+      if (k < C) {
+        if (a.ko & 2) {
+          wa[u] = bf16x8{};
+          wb[u] = bf16x8{};
+        } else {
+          wa[u] = *(const bf16x8*)(w0 + k);
+          if (two) wb[u] = *(const bf16x8*)(w1 + k);
+        }
+      }
+    }
+  };
+  if (pre && wave < a.tiles_per_split && n_begin + wave * 16 < a.N) load_tile_pair(wave, pwa, pwb, pbv, 0);
   if constexpr (POOLED) {  // the last conv already pooled: bf16 [B, C] rows -> LDS
     const int c8 = C / 8;
     for (int it = tid; it < nimg * c8; it += 256) {
@@ -180,9 +216,6 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
   // K in chunks of 512: the chunk's 16 pooled fragments are read once from
   // LDS, then two tiles' 16 weight fragments each are loaded together so a
   // wave waits on global latency once per tile pair.
-  const int col = lane & 15, kq = lane >> 4;
-  const int nsplit = a.tiles_per_split * 16;
-  const int n_begin = split * nsplit;
   const bool live = col < nimg;
   const bf16* prow = pooled + col * ldp + kq * 8;
   for (int t = wave; t < a.tiles_per_split; t += 8) {
@@ -190,29 +223,21 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
     if (n0 >= a.N) break;
     const bool two = t + 4 < a.tiles_per_split && n0 + 64 < a.N;
     floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-    // bias of this lane's 4 (+4) classes, in flight with the weight loads
-    // (loaded after the MFMAs they cost a dependent round trip per tile)
     float bv[2][4];
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) bv[h][r] = (h == 0 || two) ? a.bias[n_begin + (t + 4 * h) * 16 + kq * 4 + r] : 0.f;
-    const bf16* w0 = a.w + (long)(n0 + col) * a.ldw + kq * 8;
-    const bf16* w1 = w0 + 64L * a.ldw;
     for (int kc = 0; kc < C; kc += 512) {
       bf16x8 pb[16], wa[16], wb[16];
+      if (pre) {  // (t == wave, kc == 0: the prefetched pair)
 #pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        const int k = kc + 32 * u;
-        if (k < C) {
-          if (a.ko & 2) {
-            wa[u] = bf16x8{};
-            wb[u] = bf16x8{};
-          } else {
-            wa[u] = *(const bf16x8*)(w0 + k);
-            if (two) wb[u] = *(const bf16x8*)(w1 + k);
-          }
+        for (int u = 0; u < 16; ++u) {
+          wa[u] = pwa[u];
+          wb[u] = pwb[u];
         }
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) bv[h][r] = pbv[h][r];
+      } else {
+        load_tile_pair(t, wa, wb, bv, kc);
       }
 #pragma unroll
       for (int u = 0; u < 16; ++u) {

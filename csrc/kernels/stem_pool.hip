@@ -149,7 +149,11 @@ struct StemGeom {
 // DBG (timing experiments, tools/stem_knockouts.py): bit 0 no horizontal-pool
 // epilogue (one store of the accumulators per fragment instead), bit 1 no u8
 // conversion, bit 2 no vertical max / output stores, bit 3 no MFMAs
-template <int NF, bool U8, int DBG = 0>
+// CS (channel split, query batches): the workgroup computes 64 / CS of the
+// 64 output channels (blockIdx.y picks which), so a batch too small to
+// fill the CUs with strips runs CS x as many workgroups (each converts the
+// same input rows: cheap next to the MFMAs it no longer does).
+template <int NF, bool U8, int DBG = 0, int CS = 1>
 __global__ __launch_bounds__(256, 2) void stem_conv_pool_kernel(
     StemArgs a) {
   using G = StemGeom<NF>;
@@ -171,6 +175,9 @@ __global__ __launch_bounds__(256, 2) void stem_conv_pool_kernel(
   const int ph0 = (blockIdx.x - b * strips) * a.strip;
   const int T = a.strip / 2;  // steps 1..T emit pooled rows
   const bf16* img = a.x + (long)b * G::Hp * G::Wq * 8;
+  constexpr int NB = 4 / CS;  // 16-channel blocks of this workgroup
+  static_assert(CS == 1 || CS == 2 || CS == 4, "channel split");
+  const int nb0 = CS == 1 ? 0 : blockIdx.y * NB;
 
   // This wave's share of a row list [lo, lo+cnt): rows lo+wave, lo+wave+4, ...
   // (U8: padded row r is image row r-3; rows outside the image are not
@@ -243,15 +250,15 @@ __global__ __launch_bounds__(256, 2) void stem_conv_pool_kernel(
   };
 
   // Weights in registers: wf[n][s] = W[16n + fr][32s + 8fq .. +8].
-  bf16x8 wf[4][7];
+  bf16x8 wf[NB][7];
 #pragma unroll
-  for (int n = 0; n < 4; ++n)
+  for (int n = 0; n < NB; ++n)
 #pragma unroll
     for (int s = 0; s < 7; ++s)
-      wf[n][s] = *(const bf16x8*)(a.w + (n * 16 + fr) * kK + s * 32 + fq * 8);
-  float bs[4];
+      wf[n][s] = *(const bf16x8*)(a.w + ((nb0 + n) * 16 + fr) * kK + s * 32 + fq * 8);
+  float bs[NB];
 #pragma unroll
-  for (int n = 0; n < 4; ++n) bs[n] = a.bias[n * 16 + fr];
+  for (int n = 0; n < NB; ++n) bs[n] = a.bias[(nb0 + n) * 16 + fr];
 
   if (a.stagger && blockIdx.x >= gridDim.x / 2)  // (a wave-uniform scalar loop)
     for (int i = 0; i < a.stagger; ++i) __builtin_amdgcn_s_sleep(32);  // ~2048 cycles each
@@ -288,24 +295,24 @@ __global__ __launch_bounds__(256, 2) void stem_conv_pool_kernel(
 #pragma unroll
         for (int s = 0; s < 7; ++s) rows[s] = ((2 * cr + s) % RING) * RB;
         // per-lane store base: column 2g, channel chunk r/8, element r%8
-        const uint32_t hbase = lds_addr(hrow) + fq * 2 * kHpCol + (fr >> 3) * 16 + (fr & 7) * 2;
-        float prev3[4];  // column 16f+15 of the previous fragment, per channel block
+        const uint32_t hbase = lds_addr(hrow) + fq * 2 * kHpCol + (fr >> 3) * 16 + (fr & 7) * 2 + nb0 * 32;
+        float prev3[NB];  // column 16f+15 of the previous fragment, per channel block
         bf16x8 xf[7];
 #pragma unroll
         for (int s = 0; s < 7; ++s) xf[s] = *(const bf16x8*)(rbase + rows[s]);
 #pragma unroll
         for (int f = 0; f < NF; ++f) {
-          floatx4 acc[4];
+          floatx4 acc[NB];
 #pragma unroll
-          for (int n = 0; n < 4; ++n) acc[n] = floatx4{0.f, 0.f, 0.f, 0.f};
+          for (int n = 0; n < NB; ++n) acc[n] = floatx4{0.f, 0.f, 0.f, 0.f};
           if constexpr (DBG & 8) {
 #pragma unroll
-            for (int n = 0; n < 4; ++n) acc[n][0] = (float)xf[n][0] + (float)wf[n][0][0];
+            for (int n = 0; n < NB; ++n) acc[n][0] = (float)xf[n][0] + (float)wf[n][0][0];
           } else {
 #pragma unroll
           for (int s = 0; s < 7; ++s)
 #pragma unroll
-            for (int n = 0; n < 4; ++n)
+            for (int n = 0; n < NB; ++n)
               acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[s], wf[n][s], acc[n], 0, 0, 0);
           }
           // The next fragment's operands go out before this epilogue so the
@@ -318,7 +325,7 @@ __global__ __launch_bounds__(256, 2) void stem_conv_pool_kernel(
           if constexpr (DBG & 1) {
             float t = 0.f;
 #pragma unroll
-            for (int n = 0; n < 4; ++n) t += acc[n][0] + acc[n][1] + acc[n][2] + acc[n][3];
+            for (int n = 0; n < NB; ++n) t += acc[n][0] + acc[n][1] + acc[n][2] + acc[n][3];
             ds_write_lo16(hbase, __float_as_uint(t), f * 8 * kHpCol);
             continue;
           }
@@ -328,7 +335,7 @@ __global__ __launch_bounds__(256, 2) void stem_conv_pool_kernel(
           // i = 3 value of row g-1, or of row 3 of fragment f-1 when g = 0)
           // and 8f + 2g + 1 (own values only).
 #pragma unroll
-          for (int n = 0; n < 4; ++n) {
+          for (int n = 0; n < NB; ++n) {
             const floatx4 v = acc[n];
             const float src = (f > 0 && fq == 3) ? prev3[n] : v[3];
             float nb = rot_rows_down1(src, lane);
@@ -354,7 +361,8 @@ __global__ __launch_bounds__(256, 2) void stem_conv_pool_kernel(
     lds_barrier();
     if (t > 0 && !(DBG & 4)) {  // vertical 3-max -> pooled rows ph, ph+1
       const int ph = ph0 + 2 * (t - 1);
-      const int per_row = G::PW * 8;
+      constexpr int CG = 8 / CS;  // this workgroup's 8-channel groups
+      const int per_row = G::PW * CG;
       ushort8 m[4];  // 16*PW <= 1024 items: at most 4 per thread, reads issued together
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -362,7 +370,7 @@ __global__ __launch_bounds__(256, 2) void stem_conv_pool_kernel(
         if (it < 2 * per_row) {
           const int pr = it >= per_row;
           const int rem = it - pr * per_row;
-          const int pw = rem >> 3, cg = rem & 7;
+          const int pw = rem / CG, cg = rem % CG + (CS == 1 ? 0 : CG * (int)blockIdx.y);
           const int r1 = 2 * (ph + pr) - 1;
           const int off = pw * kHpCol + cg * 16;
           const ushort8 v1 = *(const ushort8*)(hp + ((r1 + kHp) % kHp) * HPB + off);
@@ -377,7 +385,8 @@ __global__ __launch_bounds__(256, 2) void stem_conv_pool_kernel(
         if (it < 2 * per_row) {
           const int pr = it >= per_row;
           const int rem = it - pr * per_row;
-          *(ushort8*)(a.y + (((long)b * G::PH + ph + pr) * G::PW + (rem >> 3)) * 64 + (rem & 7) * 8) = m[j];
+          *(ushort8*)(a.y + (((long)b * G::PH + ph + pr) * G::PW + rem / CG) * 64 +
+                      (rem % CG + (CS == 1 ? 0 : CG * (int)blockIdx.y)) * 8) = m[j];
         }
       }
     }
@@ -644,7 +653,8 @@ int stem_pool_pick_strip(int B, int PH, int num_cus) {
 }
 
 namespace {
-int g_stem_dbg = 0;  // knock-out variant of the 224x224 u8 kernel (tools/stem_knockouts.py)
+int g_stem_dbg = 0;
+constexpr long kStemSplitCus = 256;  // MI355X CUs: the channel split fills them at query batches  // knock-out variant of the 224x224 u8 kernel (tools/stem_knockouts.py)
 
 void stem_launch(const void* x, const uint8_t* u8, const void* w, const float* bias, void* y, int B, int S, int Wq,
                  int strip, hipStream_t s) {
@@ -706,6 +716,22 @@ void stem_launch(const void* x, const uint8_t* u8, const void* w, const float* b
 #undef DMLC_STEM_ROLES_CASE
     }
   } else if (u8) {
+    // query batches: split the 64 channels over 2 or 4 workgroups when the
+    // strips alone leave most CUs idle (B = 1: 28 strips -> 112 workgroups)
+    // (g_stem_dbg bits 12-13: 1 / 2 / 3 force a split of 1 / 2 / 4)
+    const long wgs = (long)B * (PH / strip);
+    int cs = wgs * 4 <= kStemSplitCus ? 4 : wgs * 2 <= kStemSplitCus ? 2 : 1;
+    if ((g_stem_dbg >> 12) & 3) cs = 1 << (((g_stem_dbg >> 12) & 3) - 1);
+    const dim3 gs(grid.x, cs);
+    switch (NF * 4 + (cs == 4 ? 2 : cs == 2 ? 1 : 0)) {
+      case 7 * 4 + 1: hipLaunchKernelGGL((stem_conv_pool_kernel<7, true, 0, 2>), gs, dim3(256), lds, s, a); break;
+      case 7 * 4 + 2: hipLaunchKernelGGL((stem_conv_pool_kernel<7, true, 0, 4>), gs, dim3(256), lds, s, a); break;
+      default: break;
+    }
+    if (NF == 7 && cs > 1) {
+      DMLC_HIP_CHECK(hipGetLastError());
+      return;
+    }
     switch (NF) {
 #define DMLC_STEM_U8_CASE(F) \
   case F: hipLaunchKernelGGL((stem_conv_pool_kernel<F, true>), grid, dim3(256), lds, s, a); break;

@@ -87,6 +87,9 @@ struct EngineOptions {
   // resnet50_fp8 layer1 identity bottlenecks as one kernel (bottleneck56.hip, compute / memory
   // wave roles): 156-177 vs ~245 us per block, +6% img/s (profiles/r3_bottleneck_v3.txt)
   bool fused_bottleneck = true;
+  // resnet50_fp8 layer3 / layer4 identity bottlenecks as one whole-image kernel
+  // each (bottleneck_img.hip: t1 / t2 in LDS and VGPRs)
+  bool fused_bottleneck_img = true;
   bool ds_into_expand = true;    // ResNet50 layer1.0: the 1x1 downsample computed inside conv3 (one K-concat GEMM)
   bool stream_conv = true;       // direct 3x3 convs with the input resident in LDS (conv3x3_stream.hip)
   bool stream_wreg = true;       // ... with register-streamed weights where available
@@ -188,6 +191,7 @@ class Engine {
   bool ds_fusable(size_t oi, int B) const;     // ops oi, oi+1 = downsample + stride-2 stream conv1
   bool block_fusable(size_t oi, int B) const;  // ops oi, oi+1 = a layer1 basic block -> conv3x3_block
   bool bottleneck_fusable(size_t oi) const;    // ops oi..oi+2 = a layer1 identity bottleneck -> bottleneck56
+  bool bottleneck_img_fusable(size_t oi, int B) const;  // ops oi..oi+2 = a layer3/4 identity bottleneck -> bottleneck_img
   bool bottleneck_head_fusable(size_t oi) const;  // ops oi, oi+1 = layer1.0's reduce + 3x3 -> bottleneck56_head
   bool bottleneck_conv3(const ConvLayer& L) const;  // L is such a block's expand conv (fragment-order weights)
   int ds_expand_op(size_t oi) const;  // ops[oi] = a downsample folded into a later expand conv: that op, or -1

@@ -493,3 +493,42 @@ def test_resnet50_fp8_fused_bottleneck_matches_unfused(gpu):
 def test_unknown_engine_option_is_an_error(gpu):
     with pytest.raises(Exception, match="unknown engine option"):
         InferenceEngine("resnet18", max_batch=1, options={"no_such_path": True})
+
+
+def test_resnet50_fp8_fused_bottleneck_img_matches_unfused(gpu):
+    """resnet50_fp8's layer3 / layer4 identity blocks (layer3.1-3.5,
+    layer4.1-4.2) as one whole-image kernel each (bottleneck_img.hip: conv1
+    e4m3 MFMA over LDS-staged x chunks -> t1 in LDS -> conv2 3x3 -> t2 ->
+    conv3 + residual -> e4m3) vs the three-kernel path (fused_bottleneck_img
+    off): the same e4m3 / bf16 roundings, different accumulation order, so
+    logits agree to a few e4m3 ulps and top-1 on all but near-ties; the fp32
+    reference within the e4m3 model's bar; and the fused kernel is the one
+    that ran (the blocks' conv2 / conv3 ops are empty in the per-op profile)."""
+    model = build("resnet50", seed=71, randomize_bn=True)
+    sd = state_dict_f32(model)
+    g = torch.Generator().manual_seed(72)
+    B = torch.cuda.get_device_properties(gpu).multi_processor_count  # one image per CU: the fused path's batch
+    img = torch.randint(0, 256, (B, 224, 224, 3), generator=g, dtype=torch.uint8)
+    x = img.to(gpu)
+    eng = InferenceEngine("resnet50_fp8", sd, max_batch=B, options={"fused_bottleneck_img": True})
+    ref_eng = InferenceEngine("resnet50_fp8", sd, max_batch=B, options={"fused_bottleneck_img": False})
+    fi, fp, fl = eng.predict(x, return_logits=True, use_graph=False)
+    gi, gp = eng.predict(x)
+    ri, rp, rl = ref_eng.predict(x, return_logits=True, use_graph=False)
+    torch.cuda.synchronize()
+    rel = ((fl - rl).norm() / rl.norm()).item()
+    assert rel < 5e-2, rel
+    p = torch.softmax(rl.float().cpu(), -1)
+    top2 = p.topk(2, -1).values
+    near = (top2[:, 0] - top2[:, 1]) < 5e-2
+    assert torch.all((fi.cpu() == ri.cpu()) | near)
+    assert torch.equal(fi, gi)
+    ref = _ref_logits(model, img[:8])
+    assert ((fl[:8].cpu() - ref).norm() / ref.norm()).item() < 0.15
+    prof = dict(eng._e.profile(x.data_ptr(), B, 224, 224, 0))
+    rprof = dict(ref_eng._e.profile(x.data_ptr(), B, 224, 224, 0))
+    for blk in ["layer3.%d" % i for i in range(1, 6)] + ["layer4.1", "layer4.2"]:
+        fused = prof[blk + ".conv1"] + prof[blk + ".conv2"] + prof[blk + ".conv3"]
+        sep = rprof[blk + ".conv1"] + rprof[blk + ".conv2"] + rprof[blk + ".conv3"]
+        print(blk, "fused", fused, "separate", sep)
+        assert prof[blk + ".conv3"] < 0.6 * rprof[blk + ".conv3"], (blk, prof, rprof)

@@ -240,10 +240,12 @@ def test_stem_conv_pool(gpu, B, S, strip):
 
 
 @pytest.mark.parametrize("B,S,strip", [(3, 224, None), (2, 224, 2), (1, 224, 56), (2, 128, None), (4, 192, 6),
-                                       (1, 256, 8)])
+                                       (1, 256, 8), (1, 224, 2), (1, 224, None)])
 def test_stem_conv_pool_u8(gpu, B, S, strip):
     """Stem with the preprocess fused (u8 images in): bit-identical to the
-    two-kernel path preprocess_u8(paired) -> stem_conv_pool."""
+    two-kernel path preprocess_u8(paired) -> stem_conv_pool. At 224x224 and
+    query batches the strips also split the channels over 2 or 4
+    workgroups (B = 1 strip 2: 4; B = 3: 2)."""
     g = torch.Generator().manual_seed(12)
     img = torch.randint(0, 256, (B, S, S, 3), dtype=torch.uint8, generator=g).to(gpu)
     w = (torch.randn(64, 3, 7, 7, generator=g) / 147 ** 0.5).bfloat16().float()
