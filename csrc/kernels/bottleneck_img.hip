@@ -51,7 +51,7 @@ __device__ __forceinline__ void lds_barrier() {
 }
 
 struct BiArgs {
-  const uint8_t* x;    // [B, P, C] e4m3 (value = e4m3 * res_scale)
+  const uint8_t* x;    // [B, H, H, C] e4m3 (value = e4m3 * res_scale)
   const uint8_t* w1;   // [M][C] e4m3 (per-row scales folded into a1)
   const float* a1;     // [M] s_x * s_w1[n]
   const float* b1;     // [M]
@@ -59,31 +59,40 @@ struct BiArgs {
   const float* b2;     // [M]
   const bf16* w3;      // [C][M] bf16 row-major
   const float* b3;     // [C]
-  uint8_t* y;          // [B, P, C] e4m3
+  uint8_t* y;          // [B, H, H, C] e4m3
   float res_scale;     // s_x
   float out_inv_scale; // 1 / s_y
 };
 
-template <int H, int C, int M>
+// A workgroup owns RS output rows (a strip; RS = H: the whole image) of one
+// image; t1 is computed for those rows plus the halo rows inside the image.
+// Its 8 waves are PG pixel groups x 8/PG channel groups.
+template <int H, int C, int M, int RS, int PG, int KC>
 struct BiGeom {
-  static constexpr int P = H * H;
-  static constexpr int NPF = (P + 15) / 16;    // pixel fragments
-  static constexpr int NFW = M / 8 / 16;       // conv1 / conv2 N fragments per wave
-  static constexpr int NG = NFW / 2;           // ... = perm32 groups per wave
-  static constexpr int C3W = C / 8;            // conv3 channels per wave
-  static constexpr int NG3 = NG;               // conv3 groups per pass
-  static constexpr int NP3 = C3W / (32 * NG3); // conv3 passes
-  static constexpr int KS1 = C / 128;          // conv1 e4m3 K steps
-  static constexpr int NCH = KS1 / 2;          // x chunks of 256 channels (2 K steps)
-  static constexpr int XCB = P * 256;          // bytes per staged x chunk
-  static constexpr int TB = P * M * 2;         // t1 / t2 bytes
-  static constexpr int KPT = M / 32;           // conv2 K steps per tap
-  static constexpr int KS2 = 9 * KPT;          // conv2 K steps
-  static constexpr int KS3 = M / 32;           // conv3 K steps
-  static constexpr int PD = 4;                 // conv2 / conv3 weight ring depth
+  static constexpr int NS = H / RS;                  // strips per image
+  static constexpr int TRM = NS == 1 ? H : RS + 2;   // t1 rows (most)
+  static constexpr int TPX = TRM * H;                // t1 pixels (most)
+  static constexpr int OPX = RS * H;                 // output pixels
+  static constexpr int NA = ((TPX + 15) / 16 + PG - 1) / PG;  // conv1 fragments per pixel group
+  static constexpr int NB = ((OPX + 15) / 16 + PG - 1) / PG;  // conv2 / conv3 fragments per pixel group
+  static constexpr int CGW = 8 / PG;                 // channel groups (waves per pixel group)
+  static constexpr int NFW = M / CGW / 16;           // conv1 / conv2 N fragments per wave
+  static constexpr int NG = NFW / 2;                 // ... = perm32 groups per wave
+  static constexpr int C3W = C / CGW;                // conv3 channels per wave
+  static constexpr int NP3 = C3W / (32 * NG);        // conv3 passes of NG groups
+  static constexpr int KS1 = C / 128;                // conv1 e4m3 K steps
+  static constexpr int KPC = KC / 128;               // ... per staged x chunk
+  static constexpr int NCH = C / KC;                 // x chunks
+  static constexpr int XCB = TPX * KC;               // bytes per staged x chunk
+  static constexpr int TB = TPX * M * 2;             // t1 / t2 bytes
+  static constexpr int KPT = M / 32;                 // conv2 K steps per tap
+  static constexpr int KS2 = 9 * KPT;                // conv2 K steps
+  static constexpr int KS3 = M / 32;                 // conv3 K steps
+  static constexpr int PD = 4;                       // conv2 / conv3 weight ring depth
   static constexpr int ZOFF = TB > 2 * XCB ? TB : 2 * XCB;  // 16 zero bytes
   static constexpr size_t LDS = (size_t)ZOFF + 16;
-  static_assert(NFW % 2 == 0 && C3W % (32 * NG3) == 0 && KS1 % 2 == 0, "shape");
+  static_assert(H % RS == 0 && 8 % PG == 0 && NFW % 2 == 0 && NFW >= 2, "shape");
+  static_assert(C3W % (32 * NG) == 0 && C % KC == 0 && (KC == 128 || KC == 256), "shape");
   static_assert(KS2 % PD == 0 && KS3 % PD == 0, "weight ring period");
   static_assert(LDS <= 160 * 1024, "LDS budget");
 };
@@ -94,8 +103,18 @@ template <int M>
 __device__ __forceinline__ int t_off(int p, int c) {
   return p * (M * 2) + ((c ^ (p & 15)) << 4);
 }
-// staged x chunk: pixel p's 16 chunks of 16 e4m3 channels, the same swizzle
-__device__ __forceinline__ int x_off(int p, int c) { return p * 256 + ((c ^ (p & 15)) << 4); }
+// staged x chunk: pixel p's KC / 16 chunks of 16 e4m3 channels; KC = 256:
+// chunk c at c ^ (p & 15); KC = 128 (two pixels per 256-B bank row): c ^
+// ((p >> 1) & 7). Either way the 16 pixels of a fragment read 16 distinct
+// bank slots.
+template <int KC>
+__device__ __forceinline__ int x_swz(int p) {
+  return KC == 256 ? (p & 15) : ((p >> 1) & 7);
+}
+template <int KC>
+__device__ __forceinline__ int x_off(int p, int c) {
+  return p * KC + ((c ^ x_swz<KC>(p)) << 4);
+}
 
 __device__ __forceinline__ v8i cat8(const uint4& lo, const uint4& hi) {
   return v8i{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
@@ -128,32 +147,41 @@ __device__ __forceinline__ const __attribute__((address_space(1))) T* gl(const T
 // perm32: A-operand row fr of N fragment nf of 32-channel group gg
 __device__ __forceinline__ int perm_ch(int gg, int nf, int fr) { return 32 * gg + 8 * (fr >> 2) + 4 * nf + (fr & 3); }
 
-template <int H, int C, int M>
+template <int H, int C, int M, int RS, int PG, int KC>
 __global__ __launch_bounds__(512, 1) void bottleneck_img_kernel(BiArgs a) {
-  using G = BiGeom<H, C, M>;
-  constexpr int P = G::P, NPF = G::NPF, NFW = G::NFW, NG = G::NG;
+  using G = BiGeom<H, C, M, RS, PG, KC>;
+  constexpr int NA = G::NA, NB = G::NB, NFW = G::NFW, NG = G::NG;
   extern __shared__ __attribute__((aligned(16))) uint4 smem[];
   char* lds = (char*)smem;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = lane & 15, fq = lane >> 4;
-  const uint8_t* xim = a.x + (long)blockIdx.x * P * C;
-  uint8_t* yim = a.y + (long)blockIdx.x * P * C;
+  const int pg = PG == 1 ? 0 : wave / G::CGW;     // pixel group
+  const int cg = PG == 1 ? wave : wave % G::CGW;  // channel group
+  const int b = blockIdx.x / G::NS, strip = blockIdx.x % G::NS;
+  const int r0 = strip * RS;                                     // first output row
+  const int t0 = r0 > 0 ? r0 - 1 : 0;                            // first t1 row
+  const int tpx = ((r0 + RS < H ? r0 + RS + 1 : H) - t0) * H;    // t1 pixels of this strip
+  constexpr int OPX = G::OPX;
+  const uint8_t* xim = a.x + (long)b * H * H * C;
+  uint8_t* yim = a.y + (long)b * H * H * C;
   if (tid == 0) *(uint4*)(lds + G::ZOFF) = make_uint4(0, 0, 0, 0);
 
-  // ======== A. conv1 (e4m3) over staged x chunks ========
-  // chunk i -> buffer i & 1; DMA instruction j: pixels 4j .. 4j+3, lane ->
-  // pixel 4j + (lane >> 4), physical chunk lane & 15
+  // ======== A. conv1 (e4m3) over staged x chunks (t1 pixels of the strip) ========
+  // chunk i -> buffer i & 1. KC = 256: a DMA instruction covers pixels 4j ..
+  // 4j+3 (lane -> pixel 4j + (lane >> 4), physical chunk lane & 15); KC = 128:
+  // pixels 8j .. 8j+7 (lane >> 3, physical chunk lane & 7)
+  constexpr int PPI = 1024 / KC;  // pixels per DMA instruction
+  const char* xt = (const char*)xim + (long)t0 * H * C;
   auto dma_x = [&](int i) __attribute__((always_inline)) {
     char* buf = lds + (i & 1) * G::XCB;
-    for (int j = wave; j < (P + 3) / 4; j += 8) {
-      const int p = 4 * j + (lane >> 4);
-      if (p < P) dma16(xim + (long)p * C + 256 * i + 16 * ((lane & 15) ^ (p & 15)), buf + j * 1024);
+    for (int j = wave; j < (tpx + PPI - 1) / PPI; j += 8) {
+      const int p = PPI * j + lane / (KC / 16);
+      const int pc = lane % (KC / 16);
+      if (p < tpx) dma16(xt + (long)p * C + KC * i + 16 * (pc ^ x_swz<KC>(p)), buf + j * 1024);
     }
   };
-  // this wave's conv1 / conv2 channels: perm32 groups wave * NG .. + NG - 1;
-  // its e4m3 weight fragment of K step ks, N fragment n (32 B per lane)
-  // this wave's conv1 / conv2 channels: perm32 groups wave * NG .. + NG - 1.
+  // this wave's conv1 / conv2 channels: perm32 groups cg * NG .. + NG - 1.
   // Its e4m3 weight fragment of K step ks, N fragment n: 32 B per lane by
   // two buffer loads (per-lane row offset, K step as the scalar offset). The
   // K steps are unrolled, so the scalar offset goes through an empty asm
@@ -163,7 +191,7 @@ __global__ __launch_bounds__(512, 1) void bottleneck_img_kernel(BiArgs a) {
   const __amdgpu_buffer_rsrc_t w1rs = wave_rsrc(a.w1, M * C);
   uint32_t w1vo[NFW];
 #pragma unroll
-  for (int n = 0; n < NFW; ++n) w1vo[n] = (uint32_t)(perm_ch(wave * NG + (n >> 1), n & 1, fr) * C + 32 * fq);
+  for (int n = 0; n < NFW; ++n) w1vo[n] = (uint32_t)(perm_ch(cg * NG + (n >> 1), n & 1, fr) * C + 32 * fq);
   auto w1frag = [&](int ks, int n) __attribute__((always_inline)) {
     int so = 128 * ks;
     asm volatile("" : "+s"(so));
@@ -171,14 +199,15 @@ __global__ __launch_bounds__(512, 1) void bottleneck_img_kernel(BiArgs a) {
     const uint4 hi = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(w1rs, w1vo[n] + 16, so, 0));
     return cat8(lo, hi);
   };
-  floatx4 acc[NPF][NFW];
+  floatx4 acc[NA][NFW];
 #pragma unroll
-  for (int f = 0; f < NPF; ++f)
+  for (int f = 0; f < NA; ++f)
 #pragma unroll
     for (int n = 0; n < NFW; ++n) acc[f][n] = floatx4{0.f, 0.f, 0.f, 0.f};
   dma_x(0);
-  // weights through a 3-deep ring: K step ks + 2 issued while ks computes
-  constexpr int WR = 3;
+  // weights through a 3-deep ring (K step ks + 2 issued while ks computes;
+  // 2-deep when the accumulators leave no room: layer2's 14 fragments)
+  constexpr int WR = NA * NFW > 26 ? 2 : 3;
   v8i wq1[WR][NFW];
 #pragma unroll
   for (int s = 0; s < WR - 1; ++s)
@@ -186,7 +215,7 @@ __global__ __launch_bounds__(512, 1) void bottleneck_img_kernel(BiArgs a) {
     for (int n = 0; n < NFW; ++n) wq1[s][n] = w1frag(s, n);
 #pragma unroll
   for (int ks = 0; ks < G::KS1; ++ks) {
-    const int i = ks >> 1, kk = ks & 1;
+    const int i = ks / G::KPC, kk = ks % G::KPC;
     if (kk == 0) {
       vm_wait<0>();   // chunk i (this wave's DMA) landed (and the weights issued so far)
       lds_barrier();  // every wave's part of chunk i; every wave done with chunk i - 1
@@ -197,18 +226,20 @@ __global__ __launch_bounds__(512, 1) void bottleneck_img_kernel(BiArgs a) {
       for (int n = 0; n < NFW; ++n) wq1[(ks + WR - 1) % WR][n] = w1frag(ks + WR - 1, n);
     }
     const char* buf = lds + (i & 1) * G::XCB;
-    // fragment f's operand; the next one's read while the current one's
-    // MFMAs issue (sched barriers: hoisting every read spilled)
+    // fragment f's operand (chunks 8 kk + 2 fq, +1 of the pixel); the next
+    // one's read while the current one's MFMAs issue (sched barriers:
+    // hoisting every read spilled)
     auto xread = [&](int f) __attribute__((always_inline)) {
-      int p = min(16 * f + fr, P - 1);  // (padding lanes: a real pixel, results unused)
-      asm volatile("" : "+v"(p));       // recomputed per read: hoisted, the addresses stayed live
-      return cat8(*(const uint4*)(buf + x_off(p, 8 * kk + 2 * fq)), *(const uint4*)(buf + x_off(p, 8 * kk + 2 * fq + 1)));
+      int p = min(16 * (pg * NA + f) + fr, tpx - 1);  // (padding lanes: a real pixel, results unused)
+      asm volatile("" : "+v"(p));                     // recomputed per read: hoisted, the addresses stayed live
+      return cat8(*(const uint4*)(buf + x_off<KC>(p, 8 * kk + 2 * fq)),
+                  *(const uint4*)(buf + x_off<KC>(p, 8 * kk + 2 * fq + 1)));
     };
     v8i xn = xread(0);
 #pragma unroll
-    for (int f = 0; f < NPF; ++f) {
+    for (int f = 0; f < NA; ++f) {
       const v8i xv = xn;
-      if (f + 1 < NPF) xn = xread(f + 1);
+      if (f + 1 < NA) xn = xread(f + 1);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int n = 0; n < NFW; ++n)  // formats 0/0 = e4m3; E8M0 scales 127 = 1.0
@@ -220,63 +251,64 @@ __global__ __launch_bounds__(512, 1) void bottleneck_img_kernel(BiArgs a) {
   // (the stores below are conditional on the pixel: unpinned, the compiler
   // sank whole MFMA chains into that branch, with every operand kept live)
 #pragma unroll
-  for (int f = 0; f < NPF; ++f)
+  for (int f = 0; f < NA; ++f)
 #pragma unroll
     for (int n = 0; n < NFW; ++n) asm volatile("" : "+v"(acc[f][n]));
   lds_barrier();  // every wave done with the x buffers: t1 goes over them
   {
+    const auto* a1p = gl(a.a1);
+    const auto* b1p = gl(a.b1);
 #pragma unroll
     for (int j = 0; j < NG; ++j) {
-      const int c0 = 32 * (wave * NG + j) + 8 * fq;  // this lane's 8 channels of group j
+      const int c0 = 32 * (cg * NG + j) + 8 * fq;  // this lane's 8 channels of group j
       float al[8], bi[8];
-      const auto* a1p = gl(a.a1);
-      const auto* b1p = gl(a.b1);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         al[e] = a1p[c0 + e];
         bi[e] = b1p[c0 + e];
       }
 #pragma unroll
-      for (int f = 0; f < NPF; ++f) {
+      for (int f = 0; f < NA; ++f) {
         // (padding pixels: computed, not stored; a `continue` around the
         // whole body made the unrolled loop spill)
-        const int p = 16 * f + fr;
+        const int p = 16 * (pg * NA + f) + fr;
         float v[8];
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] = fmaxf(acc[f][2 * j + (e >> 2)][e & 3] * al[e] + bi[e], 0.f);
         const uint4 pk = pack8(v);
-        if (p < P) *(uint4*)(lds + t_off<M>(p, c0 / 8)) = pk;
+        if (p < tpx) *(uint4*)(lds + t_off<M>(p, c0 / 8)) = pk;
       }
     }
   }
   lds_barrier();
 
   // ======== B. conv2 (3x3, bf16) over t1 ========
-  int qb[NPF], vm[NPF];  // staged pixel of tap (0, 0); taps inside the image (bit 3 kh + kw)
+  // output pixel op of the strip = image pixel (r0 + op / H, op % H); qb: its
+  // t1 pixel at tap (0, 0); vm: taps inside the image (bit 3 kh + kw)
+  int qb[NB], vm[NB];
 #pragma unroll
-  for (int f = 0; f < NPF; ++f) {
-    const int p = 16 * f + fr;
-    const int oh = p / H, ow = p - (p / H) * H;
-    qb[f] = (oh - 1) * H + (ow - 1);
+  for (int f = 0; f < NB; ++f) {
+    const int op = 16 * (pg * NB + f) + fr;
+    const int oh = r0 + op / H, ow = op - (op / H) * H;
+    qb[f] = (oh - 1 - t0) * H + (ow - 1);
     int m = 0;
 #pragma unroll
     for (int kh = 0; kh < 3; ++kh)
 #pragma unroll
       for (int kw = 0; kw < 3; ++kw)
         m |= ((unsigned)(oh - 1 + kh) < (unsigned)H && (unsigned)(ow - 1 + kw) < (unsigned)H) << (kh * 3 + kw);
-    vm[f] = p < P ? m : 0;
+    vm[f] = op < OPX ? m : 0;
   }
-  floatx4 acc2[NPF][NFW];
+  floatx4 acc2[NB][NFW];
 #pragma unroll
-  for (int f = 0; f < NPF; ++f)
+  for (int f = 0; f < NB; ++f)
 #pragma unroll
     for (int n = 0; n < NFW; ++n) acc2[f][n] = floatx4{0.f, 0.f, 0.f, 0.f};
   {
     constexpr int PD = G::PD;
-    // fragment (group wave * NG + (n >> 1), K step ks, nf = n & 1): 1 KB, lane * 16 B
     // fragment-order weights of this wave's groups: byte offset of
-    // (group wave * NG + (n >> 1), K step ks, nf = n & 1) = ((g KS2 + ks) 2 + nf) 1 KB
-    const __amdgpu_buffer_rsrc_t w2rs = wave_rsrc(a.wf2 + (long)wave * NG * G::KS2 * 1024, NG * G::KS2 * 2048);
+    // (group cg * NG + (n >> 1), K step ks, nf = n & 1) = ((g KS2 + ks) 2 + nf) 1 KB
+    const __amdgpu_buffer_rsrc_t w2rs = wave_rsrc(a.wf2 + (long)cg * NG * G::KS2 * 1024, NG * G::KS2 * 2048);
     auto w2 = [&](int ks, int n) __attribute__((always_inline)) {
       int so = ks * 2048;
       asm volatile("" : "+s"(so));  // (see w1frag)
@@ -308,9 +340,9 @@ __global__ __launch_bounds__(512, 1) void bottleneck_img_kernel(BiArgs a) {
           for (int n = 0; n < NFW; ++n) wq[(s + PD - 1) % PD][n] = w2(ks + PD - 1, n);
         }
 #pragma unroll
-        for (int f = 0; f < NPF; ++f) {
+        for (int f = 0; f < NB; ++f) {
           const bf16x8 xb = xn;
-          if (f + 1 < NPF) xn = tread(ks, f + 1);
+          if (f + 1 < NB) xn = tread(ks, f + 1);
           else if (ks + 1 < G::KS2) xn = tread(ks + 1, 0);
           __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -323,36 +355,39 @@ __global__ __launch_bounds__(512, 1) void bottleneck_img_kernel(BiArgs a) {
   }
   // t2 = relu(acc + b2) as bf16, held until every wave is done reading t1
 #pragma unroll
-  for (int f = 0; f < NPF; ++f)
+  for (int f = 0; f < NB; ++f)
 #pragma unroll
     for (int n = 0; n < NFW; ++n) asm volatile("" : "+v"(acc2[f][n]));  // (see phase A)
-  uint4 tv[NPF][NG];
-#pragma unroll
-  for (int j = 0; j < NG; ++j) {
-    const int c0 = 32 * (wave * NG + j) + 8 * fq;
-    float bi[8];
+  uint4 tv[NB][NG];
+  {
     const auto* b2p = gl(a.b2);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) bi[e] = b2p[c0 + e];
+    for (int j = 0; j < NG; ++j) {
+      const int c0 = 32 * (cg * NG + j) + 8 * fq;
+      float bi[8];
 #pragma unroll
-    for (int f = 0; f < NPF; ++f) {
-      float v[8];
+      for (int e = 0; e < 8; ++e) bi[e] = b2p[c0 + e];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = fmaxf(acc2[f][2 * j + (e >> 2)][e & 3] + bi[e], 0.f);
-      tv[f][j] = pack8(v);
+      for (int f = 0; f < NB; ++f) {
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = fmaxf(acc2[f][2 * j + (e >> 2)][e & 3] + bi[e], 0.f);
+        tv[f][j] = pack8(v);
+      }
     }
   }
 #pragma unroll
-  for (int f = 0; f < NPF; ++f)
+  for (int f = 0; f < NB; ++f)
 #pragma unroll
     for (int j = 0; j < NG; ++j) asm volatile("" : "+v"(tv[f][j].x), "+v"(tv[f][j].y), "+v"(tv[f][j].z), "+v"(tv[f][j].w));
   lds_barrier();
+  // t2 at output pixel op (stride M * 2 per pixel, over t1)
 #pragma unroll
   for (int j = 0; j < NG; ++j)
 #pragma unroll
-    for (int f = 0; f < NPF; ++f) {
-      const int p = 16 * f + fr;
-      if (p < P) *(uint4*)(lds + t_off<M>(p, 4 * (wave * NG + j) + fq)) = tv[f][j];
+    for (int f = 0; f < NB; ++f) {
+      const int op = 16 * (pg * NB + f) + fr;
+      if (op < OPX) *(uint4*)(lds + t_off<M>(op, 4 * (cg * NG + j) + fq)) = tv[f][j];
     }
   lds_barrier();
 
@@ -360,20 +395,30 @@ __global__ __launch_bounds__(512, 1) void bottleneck_img_kernel(BiArgs a) {
   {
     constexpr int PD = G::PD;
     const float inv = a.out_inv_scale, rsi = a.res_scale * inv;
+    const uint8_t* xo = xim + (long)r0 * H * C;  // the strip's first output pixel
+    uint8_t* yo = yim + (long)r0 * H * C;
+    const __amdgpu_buffer_rsrc_t w3rs = wave_rsrc(a.w3, C * M * 2);
     for (int pass = 0; pass < G::NP3; ++pass) {
-      const int gg0 = wave * (G::C3W / 32) + pass * G::NG3;  // first 32-channel group of the pass
-      // residual: 8 e4m3 channels 32 gg + 8 fq .. of each pixel, in flight under the MFMAs
-      uint2 rv[NPF][G::NG3];
-      const auto* xr = gl(xim);
+      const int gg0 = cg * (G::C3W / 32) + pass * NG;  // first 32-channel group of the pass
+      // residual: 8 e4m3 channels 32 gg + 8 fq .. of each pixel, loaded at
+      // the start of the pass (in flight under its MFMAs), or after them
+      // when the accumulators leave no room (layer2's 13 fragments: spilled)
+      constexpr bool kEarlyRes = NB * NFW <= 24;
+      uint2 rv[NB][NG];
+      auto load_rv = [&]() __attribute__((always_inline)) {
+        const auto* xr = gl(xo);
 #pragma unroll
-      for (int f = 0; f < NPF; ++f)
+        for (int f = 0; f < NB; ++f)
 #pragma unroll
-        for (int j = 0; j < G::NG3; ++j) {
-          const int p = min(16 * f + fr, P - 1);
-          rv[f][j] = *(const uint2*)(xim + (long)p * C + 32 * (gg0 + j) + 8 * fq);
-        }
+          for (int j = 0; j < NG; ++j) {
+            const int op = min(16 * (pg * NB + f) + fr, OPX - 1);
+            const uint64_t r =
+                *(const __attribute__((address_space(1))) uint64_t*)(xr + (long)op * C + 32 * (gg0 + j) + 8 * fq);
+            rv[f][j] = make_uint2((uint32_t)r, (uint32_t)(r >> 32));
+          }
+      };
+      if constexpr (kEarlyRes) load_rv();
       // w3 rows (perm32) of this pass: per-lane row offset, K step as the scalar offset
-      const __amdgpu_buffer_rsrc_t w3rs = wave_rsrc(a.w3, C * M * 2);
       uint32_t w3vo[NFW];
 #pragma unroll
       for (int n = 0; n < NFW; ++n) w3vo[n] = (uint32_t)((perm_ch(gg0 + (n >> 1), n & 1, fr) * M + 8 * fq) * 2);
@@ -382,9 +427,9 @@ __global__ __launch_bounds__(512, 1) void bottleneck_img_kernel(BiArgs a) {
         asm volatile("" : "+s"(so));  // (see w1frag)
         return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(w3rs, w3vo[n], so, 0));
       };
-      floatx4 c3[NPF][NFW];
+      floatx4 c3[NB][NFW];
 #pragma unroll
-      for (int f = 0; f < NPF; ++f)
+      for (int f = 0; f < NB; ++f)
 #pragma unroll
         for (int n = 0; n < NFW; ++n) c3[f][n] = floatx4{0.f, 0.f, 0.f, 0.f};
       bf16x8 wq[PD][NFW];
@@ -393,9 +438,9 @@ __global__ __launch_bounds__(512, 1) void bottleneck_img_kernel(BiArgs a) {
 #pragma unroll
         for (int n = 0; n < NFW; ++n) wq[s][n] = w3(s, n);
       auto t2read = [&](int ks, int f) __attribute__((always_inline)) {
-        int p = min(16 * f + fr, P - 1);
-        asm volatile("" : "+v"(p));  // (see tread)
-        return *(const bf16x8*)(lds + t_off<M>(p, 4 * ks + fq));
+        int op = min(16 * (pg * NB + f) + fr, OPX - 1);
+        asm volatile("" : "+v"(op));  // (see tread)
+        return *(const bf16x8*)(lds + t_off<M>(op, 4 * ks + fq));
       };
       bf16x8 xn = t2read(0, 0);
       for (int k0 = 0; k0 < G::KS3; k0 += PD) {
@@ -407,9 +452,9 @@ __global__ __launch_bounds__(512, 1) void bottleneck_img_kernel(BiArgs a) {
             for (int n = 0; n < NFW; ++n) wq[(s + PD - 1) % PD][n] = w3(ks + PD - 1, n);
           }
 #pragma unroll
-          for (int f = 0; f < NPF; ++f) {
+          for (int f = 0; f < NB; ++f) {
             const bf16x8 xb = xn;
-            if (f + 1 < NPF) xn = t2read(ks, f + 1);
+            if (f + 1 < NB) xn = t2read(ks, f + 1);
             else if (ks + 1 < G::KS3) xn = t2read(ks + 1, 0);
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -420,19 +465,20 @@ __global__ __launch_bounds__(512, 1) void bottleneck_img_kernel(BiArgs a) {
         }
       }
 #pragma unroll
-      for (int f = 0; f < NPF; ++f)
+      for (int f = 0; f < NB; ++f)
 #pragma unroll
         for (int n = 0; n < NFW; ++n) asm volatile("" : "+v"(c3[f][n]));  // (see phase A)
+      if constexpr (!kEarlyRes) load_rv();
+      const auto* b3p = gl(a.b3);
 #pragma unroll
-      for (int j = 0; j < G::NG3; ++j) {
+      for (int j = 0; j < NG; ++j) {
         const int c0 = 32 * (gg0 + j) + 8 * fq;
         float bs[8];
-        const auto* b3p = gl(a.b3);
 #pragma unroll
         for (int e = 0; e < 8; ++e) bs[e] = b3p[c0 + e] * inv;
 #pragma unroll
-        for (int f = 0; f < NPF; ++f) {
-          const int p = 16 * f + fr;
+        for (int f = 0; f < NB; ++f) {
+          const int op = 16 * (pg * NB + f) + fr;
           float r[8], v[8];
           fp8x4_to_f32(rv[f][j].x, r);
           fp8x4_to_f32(rv[f][j].y, r + 4);
@@ -440,7 +486,7 @@ __global__ __launch_bounds__(512, 1) void bottleneck_img_kernel(BiArgs a) {
           for (int e = 0; e < 8; ++e)
             v[e] = __builtin_amdgcn_fmed3f(c3[f][2 * j + (e >> 2)][e & 3] * inv + bs[e] + r[e] * rsi, 0.f, 448.f);
           const uint2 pk = make_uint2(f32x4_to_fp8_sat(v), f32x4_to_fp8_sat(v + 4));
-          if (p < P) *(uint2*)(yim + (long)p * C + c0) = pk;
+          if (op < OPX) *(uint2*)(yo + (long)op * C + c0) = pk;
         }
       }
     }
@@ -450,7 +496,8 @@ __global__ __launch_bounds__(512, 1) void bottleneck_img_kernel(BiArgs a) {
 }  // namespace
 
 bool bottleneck_img_supported(int H, int W, int C, int M) {
-  return H == W && ((H == 14 && C == 1024 && M == 256) || (H == 7 && C == 2048 && M == 512));
+  return H == W && ((H == 28 && C == 512 && M == 128) || (H == 14 && C == 1024 && M == 256) ||
+                    (H == 7 && C == 2048 && M == 512));
 }
 
 void bottleneck_img(const void* x, const void* w1, const float* a1, const float* b1, const void* wf2, const float* b2,
@@ -475,11 +522,19 @@ void bottleneck_img(const void* x, const void* w1, const float* a1, const float*
   a.y = (uint8_t*)y;
   a.res_scale = res_scale;
   a.out_inv_scale = out_inv_scale;
-  constexpr size_t lds3 = BiGeom<14, 1024, 256>::LDS, lds4 = BiGeom<7, 2048, 512>::LDS;
-  if (H == 14)
-    hipLaunchKernelGGL((bottleneck_img_kernel<14, 1024, 256>), dim3(B), dim3(512), lds3, s, a);
+  // layer2: half-image strips (t1 of 15 rows: 105 KB), 2 pixel groups x 4
+  // channel groups, x staged 128 channels at a time; layer3 / layer4: whole
+  // images, 8 channel groups, 256 channels at a time
+  using G2 = BiGeom<28, 512, 128, 14, 2, 128>;
+  using G3 = BiGeom<14, 1024, 256, 14, 1, 256>;
+  using G4 = BiGeom<7, 2048, 512, 7, 1, 256>;
+  constexpr size_t lds2 = G2::LDS, lds3 = G3::LDS, lds4 = G4::LDS;
+  if (H == 28)
+    hipLaunchKernelGGL((bottleneck_img_kernel<28, 512, 128, 14, 2, 128>), dim3(B * G2::NS), dim3(512), lds2, s, a);
+  else if (H == 14)
+    hipLaunchKernelGGL((bottleneck_img_kernel<14, 1024, 256, 14, 1, 256>), dim3(B), dim3(512), lds3, s, a);
   else
-    hipLaunchKernelGGL((bottleneck_img_kernel<7, 2048, 512>), dim3(B), dim3(512), lds4, s, a);
+    hipLaunchKernelGGL((bottleneck_img_kernel<7, 2048, 512, 7, 1, 256>), dim3(B), dim3(512), lds4, s, a);
   DMLC_HIP_CHECK(hipGetLastError());
 }
 

@@ -496,8 +496,9 @@ def test_unknown_engine_option_is_an_error(gpu):
 
 
 def test_resnet50_fp8_fused_bottleneck_img_matches_unfused(gpu):
-    """resnet50_fp8's layer3 / layer4 identity blocks (layer3.1-3.5,
-    layer4.1-4.2) as one whole-image kernel each (bottleneck_img.hip: conv1
+    """resnet50_fp8's layer2 / layer3 / layer4 identity blocks (layer2.1-2.3
+    as half-image strips, layer3.1-3.5, layer4.1-4.2 as whole images) as one
+    kernel each (bottleneck_img.hip: conv1
     e4m3 MFMA over LDS-staged x chunks -> t1 in LDS -> conv2 3x3 -> t2 ->
     conv3 + residual -> e4m3) vs the three-kernel path (fused_bottleneck_img
     off): the same e4m3 / bf16 roundings, different accumulation order, so
@@ -527,7 +528,7 @@ def test_resnet50_fp8_fused_bottleneck_img_matches_unfused(gpu):
     assert ((fl[:8].cpu() - ref).norm() / ref.norm()).item() < 0.15
     prof = dict(eng._e.profile(x.data_ptr(), B, 224, 224, 0))
     rprof = dict(ref_eng._e.profile(x.data_ptr(), B, 224, 224, 0))
-    for blk in ["layer3.%d" % i for i in range(1, 6)] + ["layer4.1", "layer4.2"]:
+    for blk in ["layer2.%d" % i for i in range(1, 4)] + ["layer3.%d" % i for i in range(1, 6)] + ["layer4.1", "layer4.2"]:
         fused = prof[blk + ".conv1"] + prof[blk + ".conv2"] + prof[blk + ".conv3"]
         sep = rprof[blk + ".conv1"] + rprof[blk + ".conv2"] + rprof[blk + ".conv3"]
         print(blk, "fused", fused, "separate", sep)
