@@ -63,6 +63,9 @@ struct BiArgs {
   float res_scale;     // s_x
   float out_inv_scale; // 1 / s_y
 };
+// DBG (timing knock-outs, tools/bottleneck_img_bench.py; layer3 only): bit 0
+// no conv1 MFMAs, bit 1 no conv2 loop, bit 2 no conv3 loop, bit 3 no residual
+// loads / y stores
 
 // A workgroup owns RS output rows (a strip; RS = H: the whole image) of one
 // image; t1 is computed for those rows plus the halo rows inside the image.
@@ -84,25 +87,25 @@ struct BiGeom {
   static constexpr int KPC = KC / 128;               // ... per staged x chunk
   static constexpr int NCH = C / KC;                 // x chunks
   static constexpr int XCB = TPX * KC;               // bytes per staged x chunk
-  static constexpr int TB = TPX * M * 2;             // t1 / t2 bytes
+  // t1 / t2: a zero-haloed grid of (RS + 2) x (H + 2) pixels (output rows r0
+  // - 1 .. r0 + RS, columns -1 .. H), PXS bytes per pixel: M * 2 + 16, so
+  // consecutive pixels start one 16-B bank slot apart (PXS / 16 = 1 mod 16:
+  // conflict-free fragment reads, no XOR) and every tap / channel offset of
+  // a conv2 or conv3 read is an immediate on one per-fragment address
+  static constexpr int HP = H + 2;
+  static constexpr int PXS = M * 2 + 16;
+  static constexpr int TB = (RS + 2) * HP * PXS;     // t1 / t2 bytes
   static constexpr int KPT = M / 32;                 // conv2 K steps per tap
   static constexpr int KS2 = 9 * KPT;                // conv2 K steps
   static constexpr int KS3 = M / 32;                 // conv3 K steps
   static constexpr int PD = 4;                       // conv2 / conv3 weight ring depth
-  static constexpr int ZOFF = TB > 2 * XCB ? TB : 2 * XCB;  // 16 zero bytes
-  static constexpr size_t LDS = (size_t)ZOFF + 16;
+  static constexpr size_t LDS = (size_t)(TB > 2 * XCB ? TB : 2 * XCB);
   static_assert(H % RS == 0 && 8 % PG == 0 && NFW % 2 == 0 && NFW >= 2, "shape");
   static_assert(C3W % (32 * NG) == 0 && C % KC == 0 && (KC == 128 || KC == 256), "shape");
   static_assert(KS2 % PD == 0 && KS3 % PD == 0, "weight ring period");
   static_assert(LDS <= 160 * 1024, "LDS budget");
 };
 
-// t1 / t2: pixel p's M / 8 chunks of 8 channels, logical chunk c at physical
-// c ^ (p & 15): the 16 pixels of a fragment read 16 distinct bank slots
-template <int M>
-__device__ __forceinline__ int t_off(int p, int c) {
-  return p * (M * 2) + ((c ^ (p & 15)) << 4);
-}
 // staged x chunk: pixel p's KC / 16 chunks of 16 e4m3 channels; KC = 256:
 // chunk c at c ^ (p & 15); KC = 128 (two pixels per 256-B bank row): c ^
 // ((p >> 1) & 7). Either way the 16 pixels of a fragment read 16 distinct
@@ -147,7 +150,7 @@ __device__ __forceinline__ const __attribute__((address_space(1))) T* gl(const T
 // perm32: A-operand row fr of N fragment nf of 32-channel group gg
 __device__ __forceinline__ int perm_ch(int gg, int nf, int fr) { return 32 * gg + 8 * (fr >> 2) + 4 * nf + (fr & 3); }
 
-template <int H, int C, int M, int RS, int PG, int KC>
+template <int H, int C, int M, int RS, int PG, int KC, int DBG = 0>
 __global__ __launch_bounds__(512, 1) void bottleneck_img_kernel(BiArgs a) {
   using G = BiGeom<H, C, M, RS, PG, KC>;
   constexpr int NA = G::NA, NB = G::NB, NFW = G::NFW, NG = G::NG;
@@ -165,7 +168,6 @@ __global__ __launch_bounds__(512, 1) void bottleneck_img_kernel(BiArgs a) {
   constexpr int OPX = G::OPX;
   const uint8_t* xim = a.x + (long)b * H * H * C;
   uint8_t* yim = a.y + (long)b * H * H * C;
-  if (tid == 0) *(uint4*)(lds + G::ZOFF) = make_uint4(0, 0, 0, 0);
 
   // ======== A. conv1 (e4m3) over staged x chunks (t1 pixels of the strip) ========
   // chunk i -> buffer i & 1. KC = 256: a DMA instruction covers pixels 4j ..
@@ -235,16 +237,22 @@ __global__ __launch_bounds__(512, 1) void bottleneck_img_kernel(BiArgs a) {
       return cat8(*(const uint4*)(buf + x_off<KC>(p, 8 * kk + 2 * fq)),
                   *(const uint4*)(buf + x_off<KC>(p, 8 * kk + 2 * fq + 1)));
     };
-    v8i xn = xread(0);
+    // operands XA fragments ahead (see phase B), within the K step
+    constexpr int XA = NFW >= 4 ? 2 : (NA >= 3 ? 3 : NA);  // (4 N fragments: 128 MFMA cycles per fragment)
+    v8i xr[XA];
+#pragma unroll
+    for (int f = 0; f < XA; ++f) xr[f] = xread(f);
 #pragma unroll
     for (int f = 0; f < NA; ++f) {
-      const v8i xv = xn;
-      if (f + 1 < NA) xn = xread(f + 1);
+      const v8i xv = xr[f % XA];
+      if (f + XA < NA) xr[f % XA] = xread(f + XA);
       __builtin_amdgcn_sched_barrier(0);
+      if (!(DBG & 1)) {
 #pragma unroll
-      for (int n = 0; n < NFW; ++n)  // formats 0/0 = e4m3; E8M0 scales 127 = 1.0
-        acc[f][n] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(wq1[ks % WR][n], xv, acc[f][n], 0, 0, 0, 127, 0,
-                                                                     127);
+        for (int n = 0; n < NFW; ++n)  // formats 0/0 = e4m3; E8M0 scales 127 = 1.0
+          acc[f][n] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(wq1[ks % WR][n], xv, acc[f][n], 0, 0, 0, 127, 0,
+                                                                       127);
+      }
       __builtin_amdgcn_sched_barrier(0);
     }
   }
@@ -276,28 +284,43 @@ __global__ __launch_bounds__(512, 1) void bottleneck_img_kernel(BiArgs a) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] = fmaxf(acc[f][2 * j + (e >> 2)][e & 3] * al[e] + bi[e], 0.f);
         const uint4 pk = pack8(v);
-        if (p < tpx) *(uint4*)(lds + t_off<M>(p, c0 / 8)) = pk;
+        // t1 pixel p = image row t0 + p / H -> grid row t0 - r0 + 1 + p / H, column p % H + 1
+        const int gq = (t0 - r0 + 1 + p / H) * G::HP + p % H + 1;
+        if (p < tpx) *(uint4*)(lds + gq * G::PXS + c0 * 2) = pk;
       }
+    }
+  }
+  // the grid's halo (zero padding of conv2): columns 0 and H + 1 of every
+  // row, and the rows above / below the image at its top / bottom strip
+  {
+    constexpr int CPX = G::PXS / 16;  // 16-B chunks per grid pixel
+    const bool top = r0 == 0, bot = r0 + RS == H;
+    const int nrow = (top ? G::HP : 0) + (bot ? G::HP : 0);
+    const int items = (2 * (RS + 2) + nrow) * CPX;
+    for (int it = tid; it < items; it += 512) {
+      const int px = it / CPX, cc = it - px * CPX;
+      int gq;
+      if (px < 2 * (RS + 2)) {
+        gq = (px >> 1) * G::HP + ((px & 1) ? H + 1 : 0);
+      } else {
+        const int k = px - 2 * (RS + 2);
+        gq = (top && k < G::HP) ? k : (RS + 1) * G::HP + (top ? k - G::HP : k);
+      }
+      *(uint4*)(lds + gq * G::PXS + cc * 16) = make_uint4(0, 0, 0, 0);
     }
   }
   lds_barrier();
 
   // ======== B. conv2 (3x3, bf16) over t1 ========
-  // output pixel op of the strip = image pixel (r0 + op / H, op % H); qb: its
-  // t1 pixel at tap (0, 0); vm: taps inside the image (bit 3 kh + kw)
-  int qb[NB], vm[NB];
+  // output pixel op of the strip = image pixel (r0 + op / H, op % H) = grid
+  // pixel (op / H + 1, op % H + 1); gb: byte address of its tap (0, 0) grid
+  // pixel plus this lane's 16-B chunk (padding lanes: a real pixel, results
+  // unused). A tap adds (kh HP + kw) PXS, a K step within it 64 B.
+  int gb[NB];
 #pragma unroll
   for (int f = 0; f < NB; ++f) {
-    const int op = 16 * (pg * NB + f) + fr;
-    const int oh = r0 + op / H, ow = op - (op / H) * H;
-    qb[f] = (oh - 1 - t0) * H + (ow - 1);
-    int m = 0;
-#pragma unroll
-    for (int kh = 0; kh < 3; ++kh)
-#pragma unroll
-      for (int kw = 0; kw < 3; ++kw)
-        m |= ((unsigned)(oh - 1 + kh) < (unsigned)H && (unsigned)(ow - 1 + kw) < (unsigned)H) << (kh * 3 + kw);
-    vm[f] = op < OPX ? m : 0;
+    const int op = min(16 * (pg * NB + f) + fr, OPX - 1);
+    gb[f] = ((op / H) * G::HP + op % H) * G::PXS + fq * 16;
   }
   floatx4 acc2[NB][NFW];
 #pragma unroll
@@ -305,7 +328,8 @@ __global__ __launch_bounds__(512, 1) void bottleneck_img_kernel(BiArgs a) {
 #pragma unroll
     for (int n = 0; n < NFW; ++n) acc2[f][n] = floatx4{0.f, 0.f, 0.f, 0.f};
   {
-    constexpr int PD = G::PD;
+    constexpr int PD = G::PD, KPT = G::KPT;
+    static_assert(KPT % PD == 0, "weight ring aligned to a tap");
     // fragment-order weights of this wave's groups: byte offset of
     // (group cg * NG + (n >> 1), K step ks, nf = n & 1) = ((g KS2 + ks) 2 + nf) 1 KB
     const __amdgpu_buffer_rsrc_t w2rs = wave_rsrc(a.wf2 + (long)cg * NG * G::KS2 * 1024, NG * G::KS2 * 2048);
@@ -320,34 +344,38 @@ __global__ __launch_bounds__(512, 1) void bottleneck_img_kernel(BiArgs a) {
     for (int s = 0; s < PD - 1; ++s)
 #pragma unroll
       for (int n = 0; n < NFW; ++n) wq[s][n] = w2(s, n);
-    // t1 operand of fragment f at K step ks (zero chunk for padding taps)
-    auto tread = [&](int ks, int f) __attribute__((always_inline)) {
-      const int tap = ks / G::KPT;
-      const int c = (ks - tap * G::KPT) * 4 + fq;
-      const int dq = (tap / 3) * H + (tap - 3 * (tap / 3));
-      int q = qb[f] + dq;
-      asm volatile("" : "+v"(q));  // address computed per read (hoisted ones stayed live)
-      const int off = ((vm[f] >> tap) & 1) ? t_off<M>(q, c) : G::ZOFF;
-      return *(const bf16x8*)(lds + off);
-    };
-    bf16x8 xn = tread(0, 0);
-    for (int k0 = 0; k0 < G::KS2; k0 += PD) {
+    // per tap: NB address adds, then KPT K steps whose reads are the tap
+    // address + immediates; (K step, fragment) items in order, the operand of
+    // item i + XD read while item i's MFMAs issue (a fragment's NFW MFMAs do
+    // not cover an LDS read)
+    constexpr int XD = 4;
+    for (int tap = 0; tap < ((DBG & 2) ? 0 : 9); ++tap) {
+      const int toff = ((tap / 3) * G::HP + tap % 3) * G::PXS;
+      int tb[NB];
 #pragma unroll
-      for (int s = 0; s < PD; ++s) {
-        const int ks = k0 + s;
+      for (int f = 0; f < NB; ++f) tb[f] = gb[f] + toff;
+      auto tread = [&](int kc, int f) __attribute__((always_inline)) {
+        return *(const bf16x8*)(lds + tb[f] + kc * 64);
+      };
+      bf16x8 xr[XD];
+#pragma unroll
+      for (int i = 0; i < XD; ++i) xr[i] = tread(i / NB, i % NB);
+#pragma unroll
+      for (int kc = 0; kc < KPT; ++kc) {
+        const int ks = tap * KPT + kc;
         if (ks + PD - 1 < G::KS2) {
 #pragma unroll
-          for (int n = 0; n < NFW; ++n) wq[(s + PD - 1) % PD][n] = w2(ks + PD - 1, n);
+          for (int n = 0; n < NFW; ++n) wq[(kc + PD - 1) % PD][n] = w2(ks + PD - 1, n);
         }
 #pragma unroll
         for (int f = 0; f < NB; ++f) {
-          const bf16x8 xb = xn;
-          if (f + 1 < NB) xn = tread(ks, f + 1);
-          else if (ks + 1 < G::KS2) xn = tread(ks + 1, 0);
+          const int i = kc * NB + f, in = i + XD;  // (compile time)
+          const bf16x8 xb = xr[i % XD];
+          if (in < KPT * NB) xr[i % XD] = tread(in / NB, in % NB);
           __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
           for (int n = 0; n < NFW; ++n)
-            acc2[f][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wq[s][n], xb, acc2[f][n], 0, 0, 0);
+            acc2[f][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wq[kc % PD][n], xb, acc2[f][n], 0, 0, 0);
           __builtin_amdgcn_sched_barrier(0);
         }
       }
@@ -387,7 +415,9 @@ __global__ __launch_bounds__(512, 1) void bottleneck_img_kernel(BiArgs a) {
 #pragma unroll
     for (int f = 0; f < NB; ++f) {
       const int op = 16 * (pg * NB + f) + fr;
-      if (op < OPX) *(uint4*)(lds + t_off<M>(op, 4 * (cg * NG + j) + fq)) = tv[f][j];
+      // t2 at the output pixel's own grid position (its tap (1, 1))
+      const int gq = (op / H + 1) * G::HP + op % H + 1;
+      if (op < OPX) *(uint4*)(lds + gq * G::PXS + (32 * (cg * NG + j) + 8 * fq) * 2) = tv[f][j];
     }
   lds_barrier();
 
@@ -417,7 +447,14 @@ __global__ __launch_bounds__(512, 1) void bottleneck_img_kernel(BiArgs a) {
             rv[f][j] = make_uint2((uint32_t)r, (uint32_t)(r >> 32));
           }
       };
-      if constexpr (kEarlyRes) load_rv();
+      if (DBG & 8) {
+#pragma unroll
+        for (int f = 0; f < NB; ++f)
+#pragma unroll
+          for (int j = 0; j < NG; ++j) rv[f][j] = make_uint2(0, 0);
+      } else if constexpr (kEarlyRes) {
+        load_rv();
+      }
       // w3 rows (perm32) of this pass: per-lane row offset, K step as the scalar offset
       uint32_t w3vo[NFW];
 #pragma unroll
@@ -438,12 +475,15 @@ __global__ __launch_bounds__(512, 1) void bottleneck_img_kernel(BiArgs a) {
 #pragma unroll
         for (int n = 0; n < NFW; ++n) wq[s][n] = w3(s, n);
       auto t2read = [&](int ks, int f) __attribute__((always_inline)) {
-        int op = min(16 * (pg * NB + f) + fr, OPX - 1);
-        asm volatile("" : "+v"(op));  // (see tread)
-        return *(const bf16x8*)(lds + t_off<M>(op, 4 * ks + fq));
+        return *(const bf16x8*)(lds + gb[f] + (G::HP + 1) * G::PXS + ks * 64);
       };
-      bf16x8 xn = t2read(0, 0);
-      for (int k0 = 0; k0 < G::KS3; k0 += PD) {
+      constexpr int XD = 4;  // (see phase B)
+      static_assert((PD * NB) % XD == 0, "operand ring aligned to the unrolled block");
+      bf16x8 xr[XD];
+#pragma unroll
+      for (int i = 0; i < XD; ++i) xr[i] = t2read(i / NB, i % NB);
+#pragma unroll
+      for (int k0 = 0; k0 < ((DBG & 4) ? 0 : G::KS3); k0 += PD) {
 #pragma unroll
         for (int s = 0; s < PD; ++s) {
           const int ks = k0 + s;
@@ -453,9 +493,9 @@ __global__ __launch_bounds__(512, 1) void bottleneck_img_kernel(BiArgs a) {
           }
 #pragma unroll
           for (int f = 0; f < NB; ++f) {
-            const bf16x8 xb = xn;
-            if (f + 1 < NB) xn = t2read(ks, f + 1);
-            else if (ks + 1 < G::KS3) xn = t2read(ks + 1, 0);
+            const int i = s * NB + f, in = i + XD;  // (compile time)
+            const bf16x8 xb = xr[i % XD];
+            if (k0 + in / NB < G::KS3) xr[i % XD] = t2read(k0 + in / NB, in % NB);
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int n = 0; n < NFW; ++n)
@@ -468,7 +508,9 @@ __global__ __launch_bounds__(512, 1) void bottleneck_img_kernel(BiArgs a) {
       for (int f = 0; f < NB; ++f)
 #pragma unroll
         for (int n = 0; n < NFW; ++n) asm volatile("" : "+v"(c3[f][n]));  // (see phase A)
-      if constexpr (!kEarlyRes) load_rv();
+      if constexpr (!kEarlyRes) {
+        if (!(DBG & 8)) load_rv();
+      }
       const auto* b3p = gl(a.b3);
 #pragma unroll
       for (int j = 0; j < NG; ++j) {
@@ -486,7 +528,7 @@ __global__ __launch_bounds__(512, 1) void bottleneck_img_kernel(BiArgs a) {
           for (int e = 0; e < 8; ++e)
             v[e] = __builtin_amdgcn_fmed3f(c3[f][2 * j + (e >> 2)][e & 3] * inv + bs[e] + r[e] * rsi, 0.f, 448.f);
           const uint2 pk = make_uint2(f32x4_to_fp8_sat(v), f32x4_to_fp8_sat(v + 4));
-          if (op < OPX) *(uint2*)(yo + (long)op * C + c0) = pk;
+          if (op < OPX && (!(DBG & 8) || pk.x == 0x12345678u)) *(uint2*)(yo + (long)op * C + c0) = pk;
         }
       }
     }
@@ -502,7 +544,7 @@ bool bottleneck_img_supported(int H, int W, int C, int M) {
 
 void bottleneck_img(const void* x, const void* w1, const float* a1, const float* b1, const void* wf2, const float* b2,
                     const void* w3, const float* b3, void* y, float res_scale, float out_inv_scale, int B, int H, int C,
-                    int M, hipStream_t s) {
+                    int M, hipStream_t s, int dbg) {
   if (B <= 0) return;
   if (!bottleneck_img_supported(H, H, C, M)) throw std::invalid_argument("bottleneck_img: unsupported shape");
   if (!x || !w1 || !a1 || !b1 || !wf2 || !b2 || !w3 || !b3 || !y ||
@@ -531,8 +573,17 @@ void bottleneck_img(const void* x, const void* w1, const float* a1, const float*
   constexpr size_t lds2 = G2::LDS, lds3 = G3::LDS, lds4 = G4::LDS;
   if (H == 28)
     hipLaunchKernelGGL((bottleneck_img_kernel<28, 512, 128, 14, 2, 128>), dim3(B * G2::NS), dim3(512), lds2, s, a);
-  else if (H == 14)
-    hipLaunchKernelGGL((bottleneck_img_kernel<14, 1024, 256, 14, 1, 256>), dim3(B), dim3(512), lds3, s, a);
+  else if (H == 14) {
+    switch (dbg) {
+#define DMLC_BI_DBG(D)                                                                                             \
+  case D:                                                                                                          \
+    hipLaunchKernelGGL((bottleneck_img_kernel<14, 1024, 256, 14, 1, 256, D>), dim3(B), dim3(512), lds3, s, a); \
+    break;
+      DMLC_BI_DBG(1) DMLC_BI_DBG(2) DMLC_BI_DBG(4)
+#undef DMLC_BI_DBG
+      default: hipLaunchKernelGGL((bottleneck_img_kernel<14, 1024, 256, 14, 1, 256>), dim3(B), dim3(512), lds3, s, a);
+    }
+  }
   else
     hipLaunchKernelGGL((bottleneck_img_kernel<7, 2048, 512, 7, 1, 256>), dim3(B), dim3(512), lds4, s, a);
   DMLC_HIP_CHECK(hipGetLastError());

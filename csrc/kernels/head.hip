@@ -39,7 +39,7 @@ namespace {
 
 constexpr int kIPW = 4;         // images per workgroup, pooling in the kernel (one wave each in the softmax)
 constexpr int kIPWPooled = 16;  // images per workgroup on a pooled input (all 16 MFMA columns)
-constexpr int kMaxSplits = 8;   // class splits (workgroups per image group); <= 256 / kIPWPooled
+constexpr int kMaxSplits = 16;  // class splits (workgroups per image group); <= 256 / kIPWPooled
 
 struct HeadArgs {
   const bf16* x;      // [B, HW, C]
@@ -369,7 +369,11 @@ int head_splits_ipw(int B, int N, int num_cus, int ipw) {
   const int groups = (B + ipw - 1) / ipw;
   const int tiles = (N + 15) / 16;
   int ns = 1;
-  while (ns < kMaxSplits && (long)groups * ns * 2 <= num_cus && tiles / (ns * 2) >= 4) ns *= 2;
+  // (query batches: down to one 16-class tile per wave, 16 splits for 1000
+  // classes: the fc is the longest step of the head's chain there)
+  const int min_tiles = B <= ipw ? 2 : 4;
+  while (ns < kMaxSplits && (long)groups * ns * 2 <= num_cus && tiles / (ns * 2) >= min_tiles) ns *= 2;
+  if (B > ipw) ns = std::min(ns, 8);  // (throughput batches: measured with at most 8)
   return ns;
 }
 

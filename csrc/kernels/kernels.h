@@ -189,7 +189,7 @@ void bottleneck56(const void* x, const void* w1, const float* a1, const float* b
 bool bottleneck_img_supported(int H, int W, int C, int M);
 void bottleneck_img(const void* x, const void* w1, const float* a1, const float* b1, const void* wf2, const float* b2,
                     const void* w3, const float* b3, void* y, float res_scale, float out_inv_scale, int B, int H, int C,
-                    int M, hipStream_t s);
+                    int M, hipStream_t s, int dbg = 0);
 // ResNet50 layer1.0's reduce 1x1 (64 -> 64) + 3x3 (64 -> 64) as one kernel
 // (bottleneck56.hip, t1 in LDS): x bf16 [B,56,56,64], w1 bf16 [64][64] (BN
 // folded), b1, wf2 / b2 as above, y = t2 bf16 [B,56,56,64].

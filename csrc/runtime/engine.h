@@ -87,9 +87,11 @@ struct EngineOptions {
   // resnet50_fp8 layer1 identity bottlenecks as one kernel (bottleneck56.hip, compute / memory
   // wave roles): 156-177 vs ~245 us per block, +6% img/s (profiles/r3_bottleneck_v3.txt)
   bool fused_bottleneck = true;
-  // resnet50_fp8 layer3 / layer4 identity bottlenecks as one whole-image kernel
-  // each (bottleneck_img.hip: t1 / t2 in LDS and VGPRs)
-  bool fused_bottleneck_img = true;
+  // resnet50_fp8 layer2-4 identity bottlenecks as one kernel each
+  // (bottleneck_img.hip: t1 / t2 in LDS and VGPRs); off: slower than the
+  // unfused kernels so far (resnet50_fp8 92k vs 111k img/s same box,
+  // profiles/r4_gpu_session_g2.txt)
+  bool fused_bottleneck_img = false;
   bool ds_into_expand = true;    // ResNet50 layer1.0: the 1x1 downsample computed inside conv3 (one K-concat GEMM)
   bool stream_conv = true;       // direct 3x3 convs with the input resident in LDS (conv3x3_stream.hip)
   bool stream_wreg = true;       // ... with register-streamed weights where available
