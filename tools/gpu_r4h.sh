@@ -5,6 +5,11 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 log() { echo "== $*"; }
+log batch-1 latency and head
+timeout -k 10 200 python bench.py --steps 5 --warmup 2 --prime-steps 5 --latency-steps 5 --latency-queries 300 --e2e-queries 0 > gpurun_out/r4h_b1.log 2>&1 || { tail -20 gpurun_out/r4h_b1.log; exit 1; }
+tail -1 gpurun_out/r4h_b1.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print("b1 p50/p95", d["gpu_batch1_latency_p50_ms"], d["gpu_batch1_latency_p95_ms"])'
+timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r4h_b1prof -o run -- python3 bench.py --steps 5 --warmup 2 --prime-steps 5 --latency-steps 5 --latency-queries 100 --e2e-queries 0 > gpurun_out/r4h_b1prof.log 2>&1 || { tail -5 gpurun_out/r4h_b1prof.log; exit 1; }
+python tools/lane_stats.py gpurun_out/r4h_b1prof/run_kernel_trace.csv --lat 10 2>&1 | sed -n '/batch-1/,$p'
 log jobs
 timeout -k 10 120 python tools/make_shards.py --synthetic 1000 --per 250 --out /tmp/shards > gpurun_out/r4h_mk.log 2>&1 || { tail -5 gpurun_out/r4h_mk.log; exit 1; }
 for cfg in "64 4" "128 4"; do
