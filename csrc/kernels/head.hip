@@ -90,7 +90,9 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
   const int col = lane & 15, kq = lane >> 4;
   const int nsplit = a.tiles_per_split * 16;
   const int n_begin = split * nsplit;
-  const bool pre = a.tiles_per_split <= 8 && C <= 512;
+  // (pooled input: its rows arrive in one batch of loads, and the prefetched
+  // weights next to them spilled)
+  const bool pre = !POOLED && a.tiles_per_split <= 8 && C <= 512;
   bf16x8 pwa[16], pwb[16];
   float pbv[2][4];
   auto load_tile_pair = [&](int t, bf16x8* wa, bf16x8* wb, float (*bv)[4], int kc) __attribute__((always_inline)) {
@@ -120,10 +122,23 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
   };
   if (pre && wave < a.tiles_per_split && n_begin + wave * 16 < a.N) load_tile_pair(wave, pwa, pwb, pbv, 0);
   if constexpr (POOLED) {  // the last conv already pooled: bf16 [B, C] rows -> LDS
+    // rows straight into LDS by LDS-DMA (global_load_lds_dwordx4, 1 KB =
+    // 512 channels per wave instruction), all in flight at once: a
+    // load-store loop waited a round trip per row (42 us at resnet50_fp8
+    // b256, C = 2048)
     const int c8 = C / 8;
-    for (int it = tid; it < nimg * c8; it += 256) {
-      const int i = it / c8, cg = it - i * c8;
-      *(uint4*)(pooled + i * ldp + cg * 8) = *(const uint4*)(a.pooled + (long)(b0 + i) * C + cg * 8);
+    if (C % 512 == 0) {
+      const int cpr = C / 512;
+      for (int k = wave; k < nimg * cpr; k += 4) {
+        const int i = k / cpr, jb = k - i * cpr;
+        dma16(a.pooled + (long)(b0 + i) * C + jb * 512 + lane * 8, pooled + i * ldp + jb * 512);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      for (int it = tid; it < nimg * c8; it += 256) {
+        const int i = it / c8, cg = it - i * c8;
+        *(uint4*)(pooled + i * ldp + cg * 8) = *(const uint4*)(a.pooled + (long)(b0 + i) * C + cg * 8);
+      }
     }
     __syncthreads();
   } else {

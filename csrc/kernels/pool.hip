@@ -106,6 +106,70 @@ __global__ __launch_bounds__(256) void avgpool_global_kernel(const void* __restr
   }
 }
 
+// Same result bit for bit (part p = pixels p, p+8, ... summed in order, the 8
+// parts combined in the butterfly order of the shuffle reduce above), with
+// a lane owning 8 channels of one image: a wave reads 512 contiguous
+// channels of a pixel per load, and a lane keeps all 8 part sums, so no
+// shuffles. Loads in blocks of 24 pixels (3 per part) issued together. For
+// batches where the 8-lane kernel's scattered 8-B reads ran at ~1 TB/s
+// (resnet50_fp8 b256: 23 us for 25.7 MB).
+template <bool FP8>
+__global__ __launch_bounds__(256) void avgpool_rows_kernel(const void* __restrict__ xv, bf16* __restrict__ y, int HW,
+                                                           int C, float scale) {
+  const int b = blockIdx.y;
+  const int cg = blockIdx.x * blockDim.x + threadIdx.x;  // 8-channel group
+  if (cg * 8 >= C) return;
+  const float inv = (FP8 ? scale : 1.f) / HW;
+  const long base = (long)b * HW * C + cg * 8;
+  float s[8][8];
+#pragma unroll
+  for (int p = 0; p < 8; ++p)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s[p][j] = 0.f;
+  constexpr int BLK = 24;
+  for (int i0 = 0; i0 < HW; i0 += BLK) {
+    uint4 v[BLK];
+#pragma unroll
+    for (int u = 0; u < BLK; ++u) {
+      const int i = i0 + u;
+      if (i < HW) {
+        if constexpr (FP8) {
+          const uint2 q = *(const uint2*)((const uint8_t*)xv + base + (long)i * C);
+          v[u] = make_uint4(q.x, q.y, 0u, 0u);
+        } else {
+          v[u] = *(const uint4*)((const bf16*)xv + base + (long)i * C);
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < BLK; ++u) {
+      const int i = i0 + u;
+      if (i < HW) {
+        float f[8];
+        if constexpr (FP8) {
+          f[0] = __builtin_amdgcn_cvt_f32_fp8((int)v[u].x, 0);
+          f[1] = __builtin_amdgcn_cvt_f32_fp8((int)v[u].x, 1);
+          f[2] = __builtin_amdgcn_cvt_f32_fp8((int)v[u].x, 2);
+          f[3] = __builtin_amdgcn_cvt_f32_fp8((int)v[u].x, 3);
+          f[4] = __builtin_amdgcn_cvt_f32_fp8((int)v[u].y, 0);
+          f[5] = __builtin_amdgcn_cvt_f32_fp8((int)v[u].y, 1);
+          f[6] = __builtin_amdgcn_cvt_f32_fp8((int)v[u].y, 2);
+          f[7] = __builtin_amdgcn_cvt_f32_fp8((int)v[u].y, 3);
+        } else {
+          unpack8(v[u], f);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s[u & 7][j] += f[j];  // (BLK % 8 == 0: part = i % 8 = u % 8)
+      }
+    }
+  }
+  float o[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+    o[j] = (((s[0][j] + s[1][j]) + (s[2][j] + s[3][j])) + ((s[4][j] + s[5][j]) + (s[6][j] + s[7][j]))) * inv;
+  *(uint4*)(y + ((long)b * C + cg * 8)) = pack8(o);
+}
+
 // torch adaptive_avg_pool2d bin rule: [floor(i*H/Ho), ceil((i+1)*H/Ho)).
 __global__ __launch_bounds__(256) void avgpool_adaptive_kernel(const bf16* __restrict__ x,
                                                                bf16* __restrict__ y, int B, int H,
@@ -156,12 +220,20 @@ void avgpool_global(const void* x, void* y, int B, int HW, int C, hipStream_t s,
   if (C % 8 != 0) throw std::invalid_argument("avgpool_global: C % 8 != 0");
   const long work = (long)B * (C / 8) * 8;
   if (work == 0) return;
-  if (in_fp8)
+  if (B >= 32 && B <= 65535) {  // (throughput batches: lane per 8 channels, contiguous wave reads)
+    const int c8 = C / 8, nt = std::min(c8, 256);
+    const dim3 grid((c8 + nt - 1) / nt, B);
+    if (in_fp8)
+      hipLaunchKernelGGL(avgpool_rows_kernel<true>, grid, dim3(nt), 0, s, x, (bf16*)y, HW, C, scale);
+    else
+      hipLaunchKernelGGL(avgpool_rows_kernel<false>, grid, dim3(nt), 0, s, x, (bf16*)y, HW, C, 1.f);
+  } else if (in_fp8) {
     hipLaunchKernelGGL(avgpool_global_kernel<true>, dim3(grid_for(work)), dim3(256), 0, s, x, (bf16*)y, B, HW, C,
                        scale);
-  else
+  } else {
     hipLaunchKernelGGL(avgpool_global_kernel<false>, dim3(grid_for(work)), dim3(256), 0, s, x, (bf16*)y, B, HW, C,
                        1.f);
+  }
   DMLC_HIP_CHECK(hipGetLastError());
 }
 

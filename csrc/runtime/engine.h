@@ -68,6 +68,7 @@ struct Op {
 // A/B-timed (profiles/). Python: InferenceEngine(..., options={"fused_block":
 // False}); the names are the field names.
 constexpr int kSmallConvMaxB = 4;  // largest batch on the query-batch conv path
+constexpr int kPoolThenHeadB = 32;  // from this batch on an unfused-pool head pools once, then head_pooled
 
 struct EngineOptions {
   bool persistent = true;        // persistent (grid-stride) implicit-GEMM conv grids
