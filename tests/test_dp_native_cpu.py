@@ -183,7 +183,8 @@ def test_calibration_equalises_coordinator_and_worker_forward_times():
     assert out["answers_ok"]
     cal = out["calibration"]
     rounds = cal["rounds"]
-    assert rounds[0]["weight"] == 1.0 and rounds[0]["busy_coord_ms"] > 1.25 * rounds[0]["busy_worker_ms"]
+    # (5.5 vs 4.0 ms expected; > 1.15x leaves room for a loaded host)
+    assert rounds[0]["weight"] == 1.0 and rounds[0]["busy_coord_ms"] > 1.15 * rounds[0]["busy_worker_ms"]
     # equal forward times at c0 * 0.2 + 1.5 = 20 * 0.2 -> c0 = 12.5 (weight 0.625)
     assert 0.55 <= cal["weight"] <= 0.75, rounds
     best = max(rounds, key=lambda r: r["rate"])

@@ -262,7 +262,8 @@ def _coalescing_fleet(devices=1, jobs=("resnet18",), max_per_rank=16, window_us=
 def test_concurrent_single_image_queries_share_forwards(n):
     """n concurrent 1-image queries on one GPU: at most ceil(n / max) forwards,
     every answer exactly once and in order."""
-    f = _coalescing_fleet()
+    # a 200 ms window: starting n threads on a loaded host can take longer than the default 50 ms
+    f = _coalescing_fleet(window_us=200000)
     imgs = _imgs(n, seed=20)
     qs = [("resnet18", i, 1) for i in range(n)]
     out = f.run(imgs, qs, threads=n)
