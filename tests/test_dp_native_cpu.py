@@ -170,8 +170,9 @@ def test_weighted_counts_rejects_raising_the_coordinator():
 
 def test_calibration_equalises_coordinator_and_worker_forward_times():
     """bench.py's calibration on the host fake: the coordinator's forward is
-    slowed by a fixed 1.5 ms per step (standing for the CUs its scatter legs'
-    copy kernels take on a GPU) on top of 0.2 ms per image. Starting from an
+    slowed by a fixed 3 ms per step (standing for the CUs its scatter legs'
+    copy kernels take on a GPU) on top of 0.4 ms per image (sleeps long
+    enough that host scheduling noise stays small next to them). Starting from an
     even split, the calibration rounds converge to the count whose forward
     time matches the other ranks' within 5%, and the timed run then uses it
     (every rank computing the same counts from the gathered times)."""
@@ -179,16 +180,17 @@ def test_calibration_equalises_coordinator_and_worker_forward_times():
     counts = C.dp_weighted_counts(per, world, 1.0)
     pool = np.random.default_rng(5).integers(0, 256, size=(2 * sum(counts), H, W, 3), dtype=np.uint8)
     out = C.dp_host_bench(pool, world, per, coord_weight=1.0, input_mode="scatter", lanes=2, prime=2, warmup=2,
-                          steps=4, latency=1, us_per_image=200, coord_extra_us=1500, calib_rounds=6, calib_steps=4)
+                          steps=4, latency=1, us_per_image=400, coord_extra_us=3000, calib_rounds=6, calib_steps=4)
     assert out["answers_ok"]
     cal = out["calibration"]
     rounds = cal["rounds"]
-    # (5.5 vs 4.0 ms expected; > 1.15x leaves room for a loaded host)
+    # (11 vs 8 ms expected; > 1.15x leaves room for a loaded host)
     assert rounds[0]["weight"] == 1.0 and rounds[0]["busy_coord_ms"] > 1.15 * rounds[0]["busy_worker_ms"]
-    # equal forward times at c0 * 0.2 + 1.5 = 20 * 0.2 -> c0 = 12.5 (weight 0.625)
-    assert 0.55 <= cal["weight"] <= 0.75, rounds
+    # equal forward times at c0 * 0.4 + 3 = 20 * 0.4 -> c0 = 12.5 (weight 0.625)
+    # (host sleeps and thread wake-ups jitter by ~10%: a round can read as balanced a count or two off)
+    assert 0.5 <= cal["weight"] <= 0.85, rounds
     best = max(rounds, key=lambda r: r["rate"])
-    assert abs(best["busy_coord_ms"] / best["busy_worker_ms"] - 1) < 0.12, rounds
+    assert abs(best["busy_coord_ms"] / best["busy_worker_ms"] - 1) < 0.2, rounds
     assert out["counts"][0] == round(per * cal["weight"]) and out["counts"][1:] == [per] * (world - 1)
     assert all(len(s) == 4 and s == out["steps"][0] for s in out["steps"])
 
