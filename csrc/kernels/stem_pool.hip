@@ -24,8 +24,9 @@
 //    lane holds 4 consecutive output columns of one channel.
 //  * Pool: the horizontal 3-max is then mostly lane-local: columns
 //    4g..4g+3 of a lane give pooled columns 2g (plus column 4g-1, fetched
-//    from the lane 16 below with two row-swap permutes) and 2g+1. +bias and ReLU
-//    are applied after the max (both monotone, so they commute with it),
+//    from the lane 16 below with two row-swap permutes) and 2g+1. The bias is
+//    the accumulators' starting value; rounding to bf16 and ReLU are monotone,
+//    so they run first and the max runs on packed bf16 pairs (hpool_packed),
 //    and the results go to a 5-row LDS ring of pooled conv rows ([pw][64 ch],
 //    16-B channel chunks XOR-swizzled by pw so the 4 row groups of a wave
 //    hit different banks). The vertical 3-max over that ring writes two
@@ -130,6 +131,61 @@ __device__ __forceinline__ float rot_rows_down1(float x, int lane) {
   const unsigned z = lane < 32 ? p32[1] : p32[0];
   const auto p16 = __builtin_amdgcn_permlane16_swap(z, u, false, false);
   return __uint_as_float((lane & 16) ? p16[0] : p16[1]);
+}
+
+// Horizontal 3-max + ReLU of one output-column fragment in packed bf16 (the
+// bias is already in the accumulators: they start from it). Lane (r, g) holds
+// columns 16f + 4g + i (i = 0..3) of channel 16n + r. Rounding is monotone and
+// ReLU'd bf16 bits order as unsigned 16-bit integers, so round-then-max equals
+// the fp32 max-then-round: each block converts its 4 values (2 cvt + 2 ReLU),
+// pooled column 8f + 2g + 1 = max(v1, v2, v3) and 8f + 2g = max(v0, v1, nb)
+// come out of two packed u16 maxes over (v0, v1) | (v1, v2) | (nb, v3), and
+// nb (column 16f + 4g - 1: v3 of row g - 1, of row 3 of fragment f-1 for g
+// = 0) moves between lanes as bf16 pairs, two channel blocks per row
+// rotation instead of one fp32 each. 0 is the neutral left pad (values >= 0).
+// 89.6 vs 90.9 us for the role-split stem at B = 256 against the fp32 max +
+// bias-add epilogue (profiles/r4_stem_roles.txt).
+
+template <int NB>
+__device__ __forceinline__ void hpool_packed(const floatx4 (&acc)[NB], uint32_t (&prevq)[(NB + 1) / 2], int lane,
+                                             int fq, uint32_t hbase, const int f, const int off) {
+  typedef unsigned short ushort2v __attribute__((ext_vector_type(2)));
+  uint32_t p01[NB], p23[NB];
+#pragma unroll
+  for (int n = 0; n < NB; ++n) {
+    const float2v a = {acc[n][0], acc[n][1]}, b = {acc[n][2], acc[n][3]};
+    p01[n] = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(
+                                              __builtin_bit_cast(short2v, __builtin_convertvector(a, bf16x2)),
+                                              short2v{0, 0}));
+    p23[n] = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(
+                                              __builtin_bit_cast(short2v, __builtin_convertvector(b, bf16x2)),
+                                              short2v{0, 0}));
+  }
+  constexpr int NQ = (NB + 1) / 2;
+  uint32_t r[NQ];
+#pragma unroll
+  for (int j = 0; j < NQ; ++j) {
+    // (v3 of block 2j, v3 of block 2j+1)
+    const uint32_t q = 2 * j + 1 < NB ? __builtin_amdgcn_perm(p23[2 * j + 1], p23[2 * j], 0x07060302u) : p23[2 * j];
+    const uint32_t src = (f > 0 && fq == 3) ? prevq[j] : q;
+    uint32_t rr = __float_as_uint(rot_rows_down1(__uint_as_float(src), lane));
+    if (f == 0) rr = fq == 0 ? 0u : rr;
+    r[j] = rr;
+    prevq[j] = q;
+  }
+#pragma unroll
+  for (int n = 0; n < NB; ++n) {
+    // (nb, v3): nb from half (n & 1) of the rotated pair (a lone block's pair
+    // carries its v3 in the high half)
+    const uint32_t c = __builtin_amdgcn_perm(p23[n], r[n >> 1], (n & 1) || NB == 1 ? 0x07060302u : 0x07060100u);
+    const uint32_t b12 = __builtin_amdgcn_alignbit(p23[n], p01[n], 16);  // (v1, v2)
+    const ushort2v m = __builtin_elementwise_max(
+        __builtin_elementwise_max(__builtin_bit_cast(ushort2v, p01[n]), __builtin_bit_cast(ushort2v, b12)),
+        __builtin_bit_cast(ushort2v, c));
+    const uint32_t packed = __builtin_bit_cast(uint32_t, m);
+    ds_write_lo16(hbase, packed, off + n * 32);
+    ds_write_hi16(hbase, packed, off + n * 32 + kHpCol);
+  }
 }
 
 // The whole geometry follows from the image size S = 32 NF (NF = output
@@ -296,7 +352,7 @@ __global__ __launch_bounds__(256, 2) void stem_conv_pool_kernel(
         for (int s = 0; s < 7; ++s) rows[s] = ((2 * cr + s) % RING) * RB;
         // per-lane store base: column 2g, channel chunk r/8, element r%8
         const uint32_t hbase = lds_addr(hrow) + fq * 2 * kHpCol + (fr >> 3) * 16 + (fr & 7) * 2 + nb0 * 32;
-        float prev3[NB];  // column 16f+15 of the previous fragment, per channel block
+        uint32_t prevq[(NB + 1) / 2];  // column 16f+15 of the previous fragment, bf16 pairs of channel blocks
         bf16x8 xf[7];
 #pragma unroll
         for (int s = 0; s < 7; ++s) xf[s] = *(const bf16x8*)(rbase + rows[s]);
@@ -304,7 +360,8 @@ __global__ __launch_bounds__(256, 2) void stem_conv_pool_kernel(
         for (int f = 0; f < NF; ++f) {
           floatx4 acc[NB];
 #pragma unroll
-          for (int n = 0; n < NB; ++n) acc[n] = floatx4{0.f, 0.f, 0.f, 0.f};
+          for (int n = 0; n < NB; ++n)
+            acc[n] = floatx4{bs[n], bs[n], bs[n], bs[n]};  // the bias first (hpool_packed)
           if constexpr (DBG & 8) {
 #pragma unroll
             for (int n = 0; n < NB; ++n) acc[n][0] = (float)xf[n][0] + (float)wf[n][0][0];
@@ -329,27 +386,9 @@ __global__ __launch_bounds__(256, 2) void stem_conv_pool_kernel(
             ds_write_lo16(hbase, __float_as_uint(t), f * 8 * kHpCol);
             continue;
           }
-          // Horizontal 3-max over columns (2pw-1, 2pw, 2pw+1), + bias, ReLU.
-          // Lane (r, g) holds columns 16f + 4g + i (i = 0..3) of channel
-          // 16n + r: pooled columns 8f + 2g (needs column 16f + 4g - 1, the
-          // i = 3 value of row g-1, or of row 3 of fragment f-1 when g = 0)
-          // and 8f + 2g + 1 (own values only).
-#pragma unroll
-          for (int n = 0; n < NB; ++n) {
-            const floatx4 v = acc[n];
-            const float src = (f > 0 && fq == 3) ? prev3[n] : v[3];
-            float nb = rot_rows_down1(src, lane);
-            if (f == 0) nb = fq == 0 ? v[0] : nb;  // first image column: no left neighbour
-            float2v p = {fmaxf(fmaxf(nb, v[0]), v[1]), fmaxf(fmaxf(v[1], v[2]), v[3])};
-            p += float2v{bs[n], bs[n]};
-            // ReLU after rounding: bf16 bits as int16, max with 0 (also maps -0 to +0)
-            const short2v q = __builtin_elementwise_max(
-                __builtin_bit_cast(short2v, __builtin_convertvector(p, bf16x2)), short2v{0, 0});
-            const uint32_t packed = __builtin_bit_cast(uint32_t, q);
-            ds_write_lo16(hbase, packed, f * 8 * kHpCol + n * 32);
-            ds_write_hi16(hbase, packed, f * 8 * kHpCol + n * 32 + kHpCol);
-            prev3[n] = v[3];
-          }
+          // horizontal 3-max over columns (2pw-1, 2pw, 2pw+1) + ReLU (the
+          // bias is in the accumulators)
+          hpool_packed<NB>(acc, prevq, lane, fq, hbase, f, f * 8 * kHpCol);
         }
       }
     }
@@ -437,7 +476,11 @@ __device__ __forceinline__ void vm_wait_dyn(int n) {
   }
 }
 
-template <int NF>
+// V (stem_conv_pool_set_dbg bits 24-29): timing knock-outs
+// (tools/stem_roles_ab.py, profiles/r4_stem_roles.txt): 4 no u8 conversion, 8
+// no conv rows, 16 no horizontal-pool epilogue, 32 no raw-row DMA / vertical
+// max / stores (results wrong: timing only)
+template <int NF, int V = 0>
 __global__ __launch_bounds__(512, 1) void stem_roles_kernel(StemArgs a) {
   using G = StemGeom<NF>;
   extern __shared__ __attribute__((aligned(16))) uint4 smem[];
@@ -532,7 +575,7 @@ __global__ __launch_bounds__(512, 1) void stem_roles_kernel(StemArgs a) {
 
   for (int t = 0; t <= T + 1; ++t) {
     if (mfma_wave) {
-      if (t <= T) {
+      if (t <= T && !(V & 8)) {
         const int c0 = 4 * t - 4;
         const int cr = c0 + wave;
         char* hrow = hp + ((cr + kRolesHpRing) % kRolesHpRing) * HPB;
@@ -545,15 +588,15 @@ __global__ __launch_bounds__(512, 1) void stem_roles_kernel(StemArgs a) {
 #pragma unroll
           for (int s = 0; s < 7; ++s) rows[s] = ((2 * cr + s) % kRolesPairRing) * RB;
           const uint32_t hbase = lds_addr(hrow) + fq * 2 * kHpCol + (fr >> 3) * 16 + (fr & 7) * 2;
-          float prev3[4];
+          uint32_t prevq[2];  // v3 of the previous fragment's row 3, as bf16 pairs
           bf16x8 xf[7];
 #pragma unroll
           for (int s = 0; s < 7; ++s) xf[s] = *(const bf16x8*)(rbase + rows[s]);
 #pragma unroll
           for (int f = 0; f < NF; ++f) {
-            floatx4 acc[4];
+            floatx4 acc[4];  // starting from the bias (hpool_packed)
 #pragma unroll
-            for (int n = 0; n < 4; ++n) acc[n] = floatx4{0.f, 0.f, 0.f, 0.f};
+            for (int n = 0; n < 4; ++n) acc[n] = floatx4{bs[n], bs[n], bs[n], bs[n]};
 #pragma unroll
             for (int s = 0; s < 7; ++s)
 #pragma unroll
@@ -563,20 +606,11 @@ __global__ __launch_bounds__(512, 1) void stem_roles_kernel(StemArgs a) {
 #pragma unroll
               for (int s = 0; s < 7; ++s) xf[s] = *(const bf16x8*)(rbase + rows[s] + (f + 1) * 256);
             }
+            if (V & 16) {
 #pragma unroll
-            for (int n = 0; n < 4; ++n) {
-              const floatx4 v = acc[n];
-              const float src = (f > 0 && fq == 3) ? prev3[n] : v[3];
-              float nb = rot_rows_down1(src, lane);
-              if (f == 0) nb = fq == 0 ? v[0] : nb;
-              float2v p = {fmaxf(fmaxf(nb, v[0]), v[1]), fmaxf(fmaxf(v[1], v[2]), v[3])};
-              p += float2v{bs[n], bs[n]};
-              const short2v q = __builtin_elementwise_max(
-                  __builtin_bit_cast(short2v, __builtin_convertvector(p, bf16x2)), short2v{0, 0});
-              const uint32_t packed = __builtin_bit_cast(uint32_t, q);
-              ds_write_lo16(hbase, packed, f * 8 * kHpCol + n * 32);
-              ds_write_hi16(hbase, packed, f * 8 * kHpCol + n * 32 + kHpCol);
-              prev3[n] = v[3];
+              for (int n = 0; n < 4; ++n) asm volatile("" ::"v"(acc[n]));
+            } else {
+              hpool_packed<4>(acc, prevq, lane, fq, hbase, f, f * 8 * kHpCol);
             }
           }
         }
@@ -588,12 +622,12 @@ __global__ __launch_bounds__(512, 1) void stem_roles_kernel(StemArgs a) {
       // are not loaded)
       constexpr int DPR = (UB / 4 + 63) / 64;
       int nwait = 0;
-      if (t + 2 < T) {
+      if (t + 2 < T && !(V & 32)) {
         load_rows(8 * t + 21, 8);
 #pragma unroll
         for (int i = 0; i < 2; ++i) nwait += (8 * t + 21 + hw + 4 * i - 3 < G::S) ? DPR : 0;
       }
-      if (t >= 2) {  // vertical 3-max of step t-1's conv rows -> pooled rows ph, ph+1
+      if (t >= 2 && !(V & 32)) {  // vertical 3-max of step t-1's conv rows -> pooled rows ph, ph+1
         const int ph = 2 * (t - 2);
         constexpr int per_row = G::PW * 8;
         ushort8 m[4];
@@ -623,7 +657,7 @@ __global__ __launch_bounds__(512, 1) void stem_roles_kernel(StemArgs a) {
           nwait += (64 * hw + 256 * j < 2 * per_row) ? 1 : 0;  // a store instruction of this wave
         }
       }
-      if (t < T) convert_rows(8 * t + 5, 8, htid, 256);
+      if (t < T && !(V & 4)) convert_rows(8 * t + 5, 8, htid, 256);
       // step t-1's DMAs (converted at t+1) have landed: everything but this
       // step's DMAs and stores (vmcnt retires in issue order)
       vm_wait_dyn(nwait);
@@ -705,6 +739,23 @@ void stem_launch(const void* x, const uint8_t* u8, const void* w, const float* b
     const size_t lds_roles = (size_t)kRolesPairRing * Wq * 16 + (size_t)kRolesHpRing * a.PW * kHpCol +
                              (size_t)kRolesRawRing * (S * 3 + kU8Pad);
     if (lds_roles > 160 * 1024) throw std::invalid_argument("stem_conv_pool: role-split LDS budget");
+    const int rv = (g_stem_dbg >> 24) & 127;
+    if (NF == 7 && rv) {
+      switch (rv) {
+#define DMLC_STEM_RV_CASE(V) \
+  case V: hipLaunchKernelGGL((stem_roles_kernel<7, V>), dim3(B), dim3(512), lds_roles, s, a); break;
+        DMLC_STEM_RV_CASE(4)
+        DMLC_STEM_RV_CASE(8)
+        DMLC_STEM_RV_CASE(16)
+        DMLC_STEM_RV_CASE(36)
+        DMLC_STEM_RV_CASE(52)
+        DMLC_STEM_RV_CASE(40)
+#undef DMLC_STEM_RV_CASE
+        default: throw std::invalid_argument("stem_conv_pool: unknown role-split variant");
+      }
+      DMLC_HIP_CHECK(hipGetLastError());
+      return;
+    }
     switch (NF) {
 #define DMLC_STEM_ROLES_CASE(F) \
   case F: hipLaunchKernelGGL((stem_roles_kernel<F>), dim3(B), dim3(512), lds_roles, s, a); break;

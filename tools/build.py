@@ -101,6 +101,10 @@ HIPCC_FLAGS = [
     "-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result",
     "-munsafe-fp-atomics",
 ]
+# A/B builds of compiler flags: DMLC_HIPCC_EXTRA for every .hip file except
+# those named in DMLC_HIPCC_EXTRA_SKIP (comma-separated basenames)
+_EXTRA = os.environ.get("DMLC_HIPCC_EXTRA", "").split()
+_EXTRA_SKIP = set(filter(None, os.environ.get("DMLC_HIPCC_EXTRA_SKIP", "").split(",")))
 
 
 # Per-file extra flags. The fused stem's max-pool epilogue works on finite
@@ -133,6 +137,8 @@ def build(jobs: int = 8, verbose: bool = False, node: bool = True) -> None:
         if _stale(o, [s], hdr):
             lang = ["-x", "hip"] if s.endswith(".hip") else []
             extra = HIPCC_FILE_FLAGS.get(os.path.basename(s), [])
+            if s.endswith(".hip") and os.path.basename(s) not in _EXTRA_SKIP:
+                extra = extra + _EXTRA
             remark = [SCRATCH_REMARK] if s.endswith(".hip") else []
             steps.append(["hipcc", *HIPCC_FLAGS, *extra, *lang, *remark, "-c", s, "-o", o])
 
