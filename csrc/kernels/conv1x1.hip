@@ -536,6 +536,7 @@ void conv1x1(const ConvArgs& a, int num_cus, hipStream_t s) {
     case 6: launch_rb<false, true, 1, true>(l); break;    // bf16 -> e4m3 + residual (fp8 expand)
     case 11: launch_rb<true, true, 2, false>(l); break;   // e4m3 -> e4m3 / s2 (fp8 downsample)
     case 3: launch_rb<true, true, 1, false>(l); break;    // e4m3 -> e4m3
+    case 7: launch_rb<true, true, 1, true>(l); break;     // e4m3 -> e4m3 + residual (expand after an e4m3 3x3)
     default: throw std::invalid_argument("conv1x1: unsupported dtype / residual / stride combination");
   }
   DMLC_HIP_CHECK(hipGetLastError());

@@ -48,9 +48,17 @@ struct R28Args {
   const bf16* wf;     // weights, fragment order [4][36][2][64][8] (stream_frag_index, K = 1152)
   const float* bias;  // [128]
   const bf16* res;    // [B, 28, 28, 128] or null
-  bf16* y;            // [B, 28, 28, 128]
+  bf16* y;            // [B, 28, 28, 128] (OUT8: e4m3 bytes)
   int relu;
+  float out_inv_scale;  // OUT8: y = e4m3(relu(v) * out_inv_scale)
 };
+
+// 4 floats (within +-448) -> 4 e4m3 bytes
+__device__ __forceinline__ uint32_t r28_e4m3x4(float a, float b, float c, float d) {
+  int v = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  v = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, v, true);
+  return (uint32_t)v;
+}
 
 constexpr int kH = 28, kW = 28, kC = 128;
 constexpr int kR = 4;                 // output rows per step
@@ -93,8 +101,10 @@ __device__ __forceinline__ void vm_wait_plus(int n) {
 // wave (their AGPR / VGPR split costs ~0.6 register moves per MFMA), or 8
 // waves (two per SIMD) x 16 channels, 144 weight registers, every X fragment
 // read feeding one MFMA instead of two.
-template <bool RES, int DBG = 0, int AH = 1, int NW = 4>
+// OUT8: e4m3 output (ResNet50's layer2 3x3 -> its e4m3 expand conv; NW = 4, no residual)
+template <bool RES, int DBG = 0, int AH = 1, int NW = 4, bool OUT8 = false>
 __global__ __launch_bounds__(64 * NW, 1) void conv3x3_rows28_kernel(R28Args a) {
+  static_assert(!OUT8 || (NW == 4 && !RES), "e4m3 output: the 4-wave form without residual");
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
   constexpr int NF = NW == 4 ? 2 : 1;  // N fragments (16 channels) per wave
   constexpr int NT = 64 * NW;
@@ -288,7 +298,16 @@ __global__ __launch_bounds__(64 * NW, 1) void conv3x3_rows28_kernel(R28Args a) {
 #pragma unroll
             for (int e = 0; e < 8; ++e) v[e] += r[e];
           }
-          *(uint4*)(a.y + obase + (long)(16 * ff + fr) * kC) = pack8_relu(v, a.relu);
+          if constexpr (OUT8) {
+            float q[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              q[e] = fminf(fmaxf((a.relu ? fmaxf(v[e], 0.f) : v[e]) * a.out_inv_scale, -448.f), 448.f);
+            *(uint2*)((uint8_t*)a.y + obase + (long)(16 * ff + fr) * kC) =
+                make_uint2(r28_e4m3x4(q[0], q[1], q[2], q[3]), r28_e4m3x4(q[4], q[5], q[6], q[7]));
+          } else {
+            *(uint4*)(a.y + obase + (long)(16 * ff + fr) * kC) = pack8_relu(v, a.relu);
+          }
         } else {
           if constexpr (RES) {
             const uint2 rr = *(const uint2*)(rp + 8 * nf0);
@@ -337,8 +356,9 @@ bool conv3x3_rows28_supported(int H, int W, int Cin, int Cout) {
 }
 
 void conv3x3_rows28(const void* x, const void* wf, const float* bias, const void* res, void* y, int B, bool relu,
-                    hipStream_t s, int dbg) {
+                    hipStream_t s, int dbg, float out_inv_scale) {
   if (B <= 0) return;
+  if (out_inv_scale > 0.f && (res || dbg)) throw std::invalid_argument("conv3x3_rows28: e4m3 output without residual only");
   if (!x || !wf || !bias || !y ||
       (((uintptr_t)x | (uintptr_t)wf | (uintptr_t)res | (uintptr_t)y) & 15))
     throw std::invalid_argument("conv3x3_rows28: null / misaligned operand");
@@ -350,6 +370,13 @@ void conv3x3_rows28(const void* x, const void* wf, const float* bias, const void
   a.res = (const bf16*)res;
   a.y = (bf16*)y;
   a.relu = relu;
+  a.out_inv_scale = out_inv_scale;
+  if (out_inv_scale > 0.f) {
+    hipLaunchKernelGGL((conv3x3_rows28_kernel<false, 0, 1, 4, true>), dim3(B), dim3(256),
+                       (size_t)R28Ring<1>::kSlotsAlloc * kRB, s, a);
+    DMLC_HIP_CHECK(hipGetLastError());
+    return;
+  }
   const int ah = (dbg == 64 || dbg == 65) ? 2 : 1;
   const size_t lds = (size_t)(ah == 2 ? R28Ring<2>::kSlotsAlloc : R28Ring<1>::kSlotsAlloc) * kRB +
                      (res ? (size_t)kResCh * 16 : 0);  // 90 / 118 KB (two ahead: 123 / 151 KB)

@@ -75,7 +75,20 @@ struct StreamConvArgs {
   // not written (nothing else reads it).
   bf16* pool;
   int store_y;
+  // e4m3 output (ResNet50's bottleneck 3x3 -> its e4m3 expand conv): y holds
+  // round(relu(v) * out_inv_scale) as e4m3 bytes [B, H, W, CO]; 0 = bf16
+  float out_inv_scale;
 };
+
+struct alignas(8) u32x2s {
+  uint32_t x, y;
+};
+// 4 floats (>= -448, <= 448) -> 4 e4m3 bytes
+__device__ __forceinline__ uint32_t e4m3x4(float a, float b, float c, float d) {
+  int v = __builtin_amdgcn_cvt_pk_fp8_f32(fmaxf(a, -448.f), fmaxf(b, -448.f), 0, false);
+  v = __builtin_amdgcn_cvt_pk_fp8_f32(fmaxf(c, -448.f), fmaxf(d, -448.f), v, true);
+  return (uint32_t)v;
+}
 
 // Weight-row permutation inside a wave's 32-row tile: row n = 16nf + r holds
 // channel 8(r>>2) + 4nf + (r&3) of the group, so the lane with accumulator
@@ -494,7 +507,17 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream_kernel(StreamConvArgs a
         for (int e = 0; e < 8; ++e) v[e] += r[e];
       }
       const uint4 packed = pack8_relu(v, relu);
-      if (a.store_y) *(uint4*)(a.y + off) = packed;
+      if (a.out_inv_scale > 0.f) {  // e4m3 bytes at element offset off
+        float q[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) q[e] = fminf((relu ? fmaxf(v[e], 0.f) : v[e]) * a.out_inv_scale, 448.f);
+        u32x2s o;
+        o.x = e4m3x4(q[0], q[1], q[2], q[3]);
+        o.y = e4m3x4(q[4], q[5], q[6], q[7]);
+        *(u32x2s*)((uint8_t*)a.y + off) = o;
+      } else if (a.store_y) {
+        *(uint4*)(a.y + off) = packed;
+      }
       if constexpr (POOLABLE) {
         if (a.pool) {  // the bf16 activation's values, as the unfused avgpool reads them
           float q[8];
@@ -648,8 +671,10 @@ bool conv3x3_stream_uses_frag(int Hin, int Win, int Cin, int Cout, int stride) {
 void conv3x3_stream(const void* x, const void* w, const float* bias, const void* res, void* y, const void* zero,
                     int B, int Hin, int Win, int Cin, int Cout, int stride, bool relu, hipStream_t s,
                     unsigned long long* stamps, const void* wd, const float* bd, void* yd, const void* wfrag,
-                    const void* wdfrag, void* pool, bool store_y) {
+                    const void* wdfrag, void* pool, bool store_y, float out_inv_scale) {
   if (B <= 0) return;
+  if (out_inv_scale > 0.f && (res || pool || yd || !store_y))
+    throw std::invalid_argument("conv3x3_stream: e4m3 output without residual, pool or downsample only");
   if ((pool || !store_y) && !conv3x3_stream_pool_supported(Hin, Win, Cin, Cout, stride))
     throw std::invalid_argument("conv3x3_stream: fused avgpool needs whole-image workgroups");
   if (pool && ((uintptr_t)pool & 15)) throw std::invalid_argument("conv3x3_stream: misaligned pool");
@@ -675,6 +700,7 @@ void conv3x3_stream(const void* x, const void* w, const float* bias, const void*
   a.wdf = (const bf16*)wdfrag;
   a.pool = (bf16*)pool;
   a.store_y = store_y ? 1 : 0;
+  a.out_inv_scale = out_inv_scale > 0.f ? out_inv_scale : 0.f;
   if (wfrag && (!conv3x3_stream_uses_frag(Hin, Win, Cin, Cout, stride) || ((uintptr_t)wfrag & 15) ||
                 (yd && (!wdfrag || ((uintptr_t)wdfrag & 15)))))
     throw std::invalid_argument("conv3x3_stream: no register-weight variant for this call");

@@ -208,7 +208,7 @@ void conv3x3_s2rows(const void* x, const void* wf, const float* bias, const void
 // wf: fragment-order weights (stream_frag_index, K = 1152); res optional.
 bool conv3x3_rows28_supported(int H, int W, int Cin, int Cout);
 void conv3x3_rows28(const void* x, const void* wf, const float* bias, const void* res, void* y, int B, bool relu,
-                    hipStream_t s, int dbg = 0);
+                    hipStream_t s, int dbg = 0, float out_inv_scale = 0.f);  // > 0: e4m3 y, no residual
 // Query-batch 3x3/p1 conv (conv_small.hip) for B <= a few images: one launch
 // per conv, no split-K. x [B,H,W,CI] bf16 NHWC (CI in 64..512), wf: fragment-
 // order weights (stream_frag_index, K = 9 CI), y = relu?(conv + bias (+ res)).
@@ -232,7 +232,9 @@ void conv3x3_stream(const void* x, const void* w, const float* bias, const void*
                     int B, int Hin, int Win, int Cin, int Cout, int stride, bool relu, hipStream_t s,
                     unsigned long long* stamps = nullptr, const void* wd = nullptr, const float* bd = nullptr,
                     void* yd = nullptr, const void* wfrag = nullptr, const void* wdfrag = nullptr,
-                    void* pool = nullptr, bool store_y = true);
+                    void* pool = nullptr, bool store_y = true, float out_inv_scale = 0.f);
+// out_inv_scale > 0: y is e4m3 (relu(v) * out_inv_scale, saturated), no
+// residual / pool / downsample.
 // pool (bf16 [B, Cout]): the global average pool of the output, computed in
 // the epilogue (whole-image workgroups: the 7x7x512 stride-1 conv); with
 // store_y = false the output activation is not written.

@@ -86,6 +86,8 @@ bool EngineOptions::set(const std::string& name, bool v) {
       {"direct13", &EngineOptions::direct13},
       {"direct27", &EngineOptions::direct27},
       {"fork_ds", &EngineOptions::fork_ds},         {"fp8_3x3", &EngineOptions::fp8_3x3},
+      {"fp8_3x3_out", &EngineOptions::fp8_3x3_out},
+      {"fp8_3x3_out_s2", &EngineOptions::fp8_3x3_out_s2},
       {"conv1x1", &EngineOptions::conv1x1},         {"s2rows", &EngineOptions::s2rows},
       {"rows28", &EngineOptions::rows28},           {"stem_roles", &EngineOptions::stem_roles},
       {"igemm_small_m", &EngineOptions::igemm_small_m},
@@ -350,9 +352,10 @@ void Engine::build_alexnet() {
 // 256..2048-channel block outputs and residual paths (where the bytes are:
 // layer1's 56x56x256 tensors dominate the traffic), so every 1x1 expand /
 // reduce conv and downsample reads or writes e4m3. The 3x3 convs keep bf16
-// input and output (EngineOptions::fp8_3x3 makes them e4m3 as well): as bf16 they run
+// input (EngineOptions::fp8_3x3 makes them e4m3 in and out): as bf16 they run
 // the direct stream / row convs (LDS-resident input, register weights),
-// which beat the fp8 implicit GEMM on these shapes. The stem and layer1's
+// which beat the fp8 implicit GEMM on these shapes; those kernels write
+// e4m3 through their epilogue (fp8_3x3_out), so the expand convs read e4m3. The stem and layer1's
 // 64-channel inner convs stay bf16 (Cin = 64 is below the fp8 kernel's
 // 128-channel K-tile).
 void Engine::mark_fp8() {
@@ -367,6 +370,24 @@ void Engine::mark_fp8() {
     if (op.type == OpType::Conv && !convs_[op.conv].fc && shapes_[op.out].C % 128 == 0 &&
         (fp8_3x3 || !near_3x3[op.out]))
       shapes_[op.out].fp8 = true;
+  if (opt_.fp8_3x3_out && !fp8_3x3) {
+    // outputs of 3x3 convs that no 3x3 conv reads (a bottleneck's t2), where
+    // the conv runs on conv3x3_rows28 / conv3x3_stream (e4m3 epilogues)
+    std::vector<bool> in_3x3(shapes_.size(), false);
+    for (const Op& op : ops_)
+      if (op.type == OpType::Conv && !convs_[op.conv].fc && convs_[op.conv].kh == 3) in_3x3[op.in] = true;
+    for (const Op& op : ops_) {
+      if (op.type != OpType::Conv) continue;
+      const ConvLayer& L = convs_[op.conv];
+      const ActShape& is = shapes_[op.in];
+      if (L.fc || L.kh != 3 || L.kw != 3 || L.pad != 1 || op.res >= 0 || in_3x3[op.out] ||
+          shapes_[op.out].C % 128 || shapes_[op.in].fp8)
+        continue;
+      if (conv3x3_rows28_supported(is.H, is.W, is.C, L.cout) ||
+          conv3x3_stream_supported(is.H, is.W, is.C, L.cout, L.stride) || (opt_.fp8_3x3_out_s2 && L.stride == 2))
+        shapes_[op.out].fp8 = true;
+    }
+  }
   for (const Op& op : ops_) {
     if (op.type != OpType::Conv) continue;
     if (op.res >= 0 && shapes_[op.res].fp8 != shapes_[op.out].fp8)
@@ -706,8 +727,10 @@ ConvArgs Engine::conv_args(const Op& op, int B, float* logits) const {
 Engine::ConvPath Engine::conv_path(const Op& op, int B) const {
   const ConvLayer& L = convs_[op.conv];
   const ActShape& is = shapes_[op.in];
-  const bool k3 = !L.fc && !L.pair && !L.fp8 && L.kh == 3 && L.kw == 3 && L.pad == 1 && !shapes_[op.out].f32 &&
-                  !shapes_[op.out].fp8;
+  const bool k3b = !L.fc && !L.pair && !L.fp8 && L.kh == 3 && L.kw == 3 && L.pad == 1 && !shapes_[op.out].f32;
+  const bool k3 = k3b && !shapes_[op.out].fp8;
+  // e4m3 output (fp8_3x3_out): the row / stream kernels' e4m3 epilogue
+  const bool k3o8 = k3b && shapes_[op.out].fp8 && opt_.fp8_3x3_out && op.res < 0;
   // the stream conv runs 1-4 workgroups per image (or image pair): only
   // worth it once the batch fills the CUs
   // 14x14x256 -> 7x7x512 / s2 (layer4.0.conv1) runs 2 rounds of single-image
@@ -725,7 +748,7 @@ Engine::ConvPath Engine::conv_path(const Op& op, int B) const {
       conv_small_supported(is.H, is.W, is.C, L.cout, L.stride) &&
       !(opt_.direct13 && conv3x3_13_supported(is.H, is.W, is.C, L.cout)))  // (AlexNet keeps its fused pools)
     return ConvPath::Small;
-  if (opt_.rows28 && k3 && L.stride == 1 && L.wf_off && 10 * B >= 7 * rounds * num_cus_ &&
+  if (opt_.rows28 && (k3 || k3o8) && L.stride == 1 && L.wf_off && 10 * B >= 7 * rounds * num_cus_ &&
       conv3x3_rows28_supported(is.H, is.W, is.C, L.cout))
     return ConvPath::Rows28;
   if (opt_.direct13 && k3 && L.stride == 1 && L.wf_off && conv3x3_13_supported(is.H, is.W, is.C, L.cout))
@@ -733,7 +756,7 @@ Engine::ConvPath Engine::conv_path(const Op& op, int B) const {
   if (opt_.direct27 && !L.fc && !L.fp8 && L.kh == 5 && L.kw == 5 && L.stride == 1 && L.relu && L.wf_off &&
       L.kpad == 1600 && !shapes_[op.out].f32 && conv5x5_27_supported(is.H, is.W, is.C, L.cout, L.pad))
     return ConvPath::Direct27;
-  if (opt_.stream_conv && k3 && !l4s2 && !l1 && 8 * B >= num_cus_ &&
+  if (opt_.stream_conv && (k3 || k3o8) && !l4s2 && !l1 && 8 * B >= num_cus_ &&
       conv3x3_stream_supported(is.H, is.W, is.C, L.cout, L.stride))
     return ConvPath::Stream;
   if (opt_.row_conv && k3 && L.stride == 1 && conv3x3_rows_supported(is.H, is.W, is.C, L.cout)) return ConvPath::Rows;
@@ -1120,7 +1143,8 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
                            D ? (const float*)((const uint8_t*)warena_ + D->b_off) : nullptr,
                            D ? acts_[yd] : nullptr, wreg ? (const uint8_t*)warena_ + L.wf_off : nullptr,
                            (wreg && D) ? (const uint8_t*)warena_ + D->wf_off : nullptr,
-                           fpool ? acts_[ops_[oi + 1].out] : nullptr, !fpool || trace || evs);
+                           fpool ? acts_[ops_[oi + 1].out] : nullptr, !fpool || trace || evs,
+                           shapes_[op.out].fp8 ? 1.f / shapes_[op.out].scale : 0.f);
             pooled = fpool;
             skip_ds = -1;
             break;
@@ -1183,7 +1207,7 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
           case ConvPath::Rows28:
             conv3x3_rows28(acts_[op.in], (const uint8_t*)warena_ + L.wf_off,
                            (const float*)((const uint8_t*)warena_ + L.b_off), op.res >= 0 ? acts_[op.res] : nullptr,
-                           acts_[op.out], B, L.relu, cs);
+                           acts_[op.out], B, L.relu, cs, 0, shapes_[op.out].fp8 ? 1.f / shapes_[op.out].scale : 0.f);
             break;
           case ConvPath::Rows:
             conv3x3_rows(acts_[op.in], (const uint8_t*)warena_ + L.w_off,

@@ -116,6 +116,13 @@ struct EngineOptions {
   // resnet50_fp8: the 3x3 convs' inputs / outputs in e4m3 too (default bf16:
   // the direct bf16 convs beat the fp8 implicit GEMM on those shapes)
   bool fp8_3x3 = false;
+  // ResNet50 e4m3: the bottleneck 3x3 convs that run on the row / stream
+  // kernels write e4m3 (their bf16 inputs stay), so the expand conv reads e4m3
+  // (117.8-118.1k vs 112.5-112.7k img/s same box, profiles/r4_r50_3x3_e4m3_out.txt)
+  bool fp8_3x3_out = true;
+  // ... and the strided 3x3 convs of layer3.0 / layer4.0 (implicit GEMM with
+  // an e4m3 epilogue instead of the bf16 big-tile kernel)
+  bool fp8_3x3_out_s2 = false;
 
   // Set a field by name; false if there is no such option.
   bool set(const std::string& name, bool value);

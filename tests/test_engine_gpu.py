@@ -93,6 +93,41 @@ def test_engine_resnet50_fp8(gpu):
     assert torch.equal(i2.cpu(), idx.cpu())
 
 
+@pytest.mark.parametrize("B,s2", [(16, False), (256, False), (256, True)])
+def test_resnet50_fp8_3x3_e4m3_out(gpu, B, s2):
+    """fp8_3x3_out: the bottleneck 3x3 convs write e4m3 (a calibrated
+    per-tensor scale; the row / stream kernels' e4m3 epilogue at B = 256, the
+    implicit GEMM at B = 16; s2: the strided ones too, on the implicit GEMM)
+    and the expand convs read it on the e4m3 MFMA. Against fp32 at B = 16 and
+    against the bf16-3x3-output engine at B = 256: the same bar as
+    test_engine_resnet50_fp8."""
+    model = build("resnet50", seed=11, randomize_bn=True)
+    sd = state_dict_f32(model)
+    eng = InferenceEngine("resnet50_fp8", sd, max_batch=B, options={"fp8_3x3_out": True, "fp8_3x3_out_s2": s2})
+    g = torch.Generator().manual_seed(31 + B)
+    img = torch.randint(0, 256, (B, 224, 224, 3), generator=g, dtype=torch.uint8)
+    if B == 16:
+        ref = _ref_logits(model, img)
+    else:
+        base = InferenceEngine("resnet50_fp8", sd, max_batch=B, options={"fp8_3x3_out": False})
+        _, _, ref = base.predict(img.to(gpu), return_logits=True, use_graph=False)
+        ref = ref.cpu()
+    idx, prob, logits = eng.predict(img.to(gpu), return_logits=True, use_graph=False)
+    torch.cuda.synchronize()
+    rel = ((logits.cpu() - ref).norm() / ref.norm()).item()
+    cos = torch.nn.functional.cosine_similarity(logits.cpu(), ref, dim=-1).min().item()
+    agree = (idx.cpu().long() == ref.argmax(-1)).float().mean().item()
+    print(f"resnet50_fp8 fp8_3x3_out B={B} s2={s2}: rel {rel:.4f} min-cos {cos:.4f} top1 agree {agree:.3f}")
+    assert rel < 0.15 and cos > 0.98, (rel, cos)
+    ref_p = torch.softmax(ref, -1)
+    top2 = ref_p.topk(2, -1).values
+    near_tie = (top2[:, 0] - top2[:, 1]) < 5e-2
+    mism = idx.cpu().long() != ref.argmax(-1)
+    assert torch.all(~mism | near_tie), (agree, rel)
+    i2, _ = eng.predict(img.to(gpu), use_graph=True)
+    assert torch.equal(i2.cpu(), idx.cpu())
+
+
 @pytest.mark.parametrize("B", [16, 64])
 def test_resnet50_fp8_fused_head_matches_unfused(gpu, B):
     """The fused head reads ResNet50 e4m3's last activation directly (pool
