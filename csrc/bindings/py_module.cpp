@@ -228,6 +228,12 @@ PYBIND11_MODULE(_C, m) {
      py::arg("b3"), py::arg("y"), py::arg("res_scale"), py::arg("out_inv_scale"), py::arg("B"), py::arg("stream") = 0,
      py::arg("dbg") = 0);
   m.def("conv3x3_s2rows_supported", &conv3x3_s2rows_supported);
+  m.def("conv3x3_s2rows128_supported", &conv3x3_s2rows128_supported);
+  m.def("conv3x3_s2rows128", [](uintptr_t x, uintptr_t wf, uintptr_t bias, uintptr_t y, int B, bool relu,
+                                float out_inv_scale, uintptr_t stream) {
+    conv3x3_s2rows128(P<void>(x), P<void>(wf), P<float>(bias), P<void>(y), B, relu, out_inv_scale, S(stream));
+  }, py::arg("x"), py::arg("wf"), py::arg("bias"), py::arg("y"), py::arg("B"), py::arg("relu"),
+        py::arg("out_inv_scale"), py::arg("stream"));
   m.def("conv3x3_s2rows", [](uintptr_t x, uintptr_t wf, uintptr_t bias, uintptr_t wdf, uintptr_t bd, uintptr_t y,
                              uintptr_t yd, uintptr_t zero, int B, bool relu, uintptr_t stream, int dbg) {
     conv3x3_s2rows(P<void>(x), P<void>(wf), P<float>(bias), P<void>(wdf), P<float>(bd), P<void>(y), P<void>(yd),

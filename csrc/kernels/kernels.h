@@ -201,6 +201,12 @@ void bottleneck56_head(const void* x, const void* w1, const float* b1, const voi
 // weights (stream_frag_index, K = 576 / 64); y = relu?(conv3x3 + bias),
 // yd = downsample + bd.
 bool conv3x3_s2rows_supported(int Hin, int Win, int Cin, int Cout);
+// ResNet50 layer2.0.conv2, 56x56x128 -> 28x28x128 / s2 (conv3x3_s2rows128.hip):
+// one weight-stationary workgroup per image; wf in fragment order; y bf16, or
+// e4m3 (relu(v) * out_inv_scale) when out_inv_scale > 0.
+bool conv3x3_s2rows128_supported(int Hin, int Win, int Cin, int Cout);
+void conv3x3_s2rows128(const void* x, const void* wf, const float* bias, void* y, int B, bool relu,
+                       float out_inv_scale, hipStream_t s);
 void conv3x3_s2rows(const void* x, const void* wf, const float* bias, const void* wdf, const float* bd, void* y,
                     void* yd, const void* zero, int B, bool relu, hipStream_t s, int dbg = 0);
 // Weight-stationary row-streaming 3x3/s1/p1 conv for 28x28x128 -> 128

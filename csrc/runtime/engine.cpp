@@ -89,6 +89,7 @@ bool EngineOptions::set(const std::string& name, bool v) {
       {"fp8_3x3_out", &EngineOptions::fp8_3x3_out},
       {"fp8_3x3_out_s2", &EngineOptions::fp8_3x3_out_s2},
       {"conv1x1", &EngineOptions::conv1x1},         {"s2rows", &EngineOptions::s2rows},
+      {"s2rows128", &EngineOptions::s2rows128},
       {"rows28", &EngineOptions::rows28},           {"stem_roles", &EngineOptions::stem_roles},
       {"igemm_small_m", &EngineOptions::igemm_small_m},
       {"small_conv", &EngineOptions::small_conv},
@@ -1130,6 +1131,15 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
               const uint8_t* wa = (const uint8_t*)warena_;
               conv3x3_s2rows(acts_[op.in], wa + L.wf_off, (const float*)(wa + L.b_off), wa + D->wf_off,
                              (const float*)(wa + D->b_off), acts_[op.out], acts_[yd], zero_, B, L.relu, cs);
+              skip_ds = -1;
+              break;
+            }
+            if (!D && opt_.s2rows128 && op.res < 0 && L.wf_off && L.stride == 2 &&
+                10 * B >= 7 * ((B + num_cus_ - 1) / num_cus_) * num_cus_ &&
+                conv3x3_s2rows128_supported(is.H, is.W, is.C, L.cout)) {
+              const uint8_t* wa = (const uint8_t*)warena_;
+              conv3x3_s2rows128(acts_[op.in], wa + L.wf_off, (const float*)(wa + L.b_off), acts_[op.out], B, L.relu,
+                                shapes_[op.out].fp8 ? 1.f / shapes_[op.out].scale : 0.f, cs);
               skip_ds = -1;
               break;
             }

@@ -546,8 +546,10 @@ def test_resnet50_fp8_fused_bottleneck_img_matches_unfused(gpu):
     B = torch.cuda.get_device_properties(gpu).multi_processor_count  # one image per CU: the fused path's batch
     img = torch.randint(0, 256, (B, 224, 224, 3), generator=g, dtype=torch.uint8)
     x = img.to(gpu)
-    eng = InferenceEngine("resnet50_fp8", sd, max_batch=B, options={"fused_bottleneck_img": True})
-    ref_eng = InferenceEngine("resnet50_fp8", sd, max_batch=B, options={"fused_bottleneck_img": False})
+    # (the fused kernel keeps t2 internal: it pairs with the bf16-t2 graph, fp8_3x3_out off)
+    eng = InferenceEngine("resnet50_fp8", sd, max_batch=B, options={"fused_bottleneck_img": True, "fp8_3x3_out": False})
+    ref_eng = InferenceEngine("resnet50_fp8", sd, max_batch=B,
+                              options={"fused_bottleneck_img": False, "fp8_3x3_out": False})
     fi, fp, fl = eng.predict(x, return_logits=True, use_graph=False)
     gi, gp = eng.predict(x)
     ri, rp, rl = ref_eng.predict(x, return_logits=True, use_graph=False)

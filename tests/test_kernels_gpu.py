@@ -472,6 +472,30 @@ def test_conv3x3_s2rows(gpu, B):
     assert (yd.float() - yd0.float()).abs().max().item() < 0.05
 
 
+@pytest.mark.parametrize("B,out8", [(1, False), (3, False), (2, True)])
+def test_conv3x3_s2rows128(gpu, B, out8):
+    """ResNet50 layer2.0.conv2 row-streaming kernel (conv3x3_s2rows128.hip)
+    vs torch fp32: bf16 output, and e4m3 output (relu(v) * inv_scale,
+    dequantised) against the same reference at e4m3 resolution."""
+    g = torch.Generator().manual_seed(41 + B)
+    x = torch.randn(B, 128, 56, 56, generator=g).bfloat16().float()
+    w = (torch.randn(128, 128, 3, 3, generator=g) / 34).bfloat16().float()
+    bias = torch.randn(128, generator=g) * 0.1
+    ref = F.relu(F.conv2d(x, w, bias, 2, 1))
+    xg = _nhwc(x).bfloat16().to(gpu)
+    wp = ops.pack_conv_weight(w, device=gpu)
+    if not out8:
+        y = ops.conv3x3_s2rows128(xg, wp, bias.to(gpu))
+        torch.cuda.synchronize()
+        assert _rel(_nchw(y.float().cpu()), ref) < 5e-3, _rel(_nchw(y.float().cpu()), ref)
+    else:
+        scale = ref.abs().max().item() / 448.0
+        y8 = ops.conv3x3_s2rows128(xg, wp, bias.to(gpu), out_inv_scale=1.0 / scale)
+        torch.cuda.synchronize()
+        deq = y8.view(torch.float8_e4m3fn).float().cpu() * scale
+        assert _rel(_nchw(deq), ref) < 4e-2, _rel(_nchw(deq), ref)
+
+
 # every ResNet18/34 3x3 shape at query batches; mf None = the engine's pick
 @pytest.mark.parametrize("HW,Cin,Cout,stride", [(56, 64, 64, 1), (56, 64, 128, 2), (28, 128, 128, 1),
                                                 (28, 128, 256, 2), (14, 256, 256, 1), (14, 256, 512, 2),

@@ -262,6 +262,59 @@ def test_s2rows_lds_layout():
     assert {i for i in range(RB // 16) if i not in dst} == {h * HALF // 16 + j for h in range(2) for j in (0, 1, 2, 3, 228, 229, 230, 231)}
 
 
+def test_s2rows128_lds_layout():
+    """conv3x3_s2rows128.hip (ResNet50 layer2.0.conv2): every ds_read_b128 of
+    a 2-row step (4 fragments, the last 8 lanes clamped to pixel 55; 9 taps x
+    4 channel quarters; all 14 steps through the 9-row ring and its 2 guard
+    slots) is conflict free and reads the channels the weight fragment
+    expects; the DMA order of a row covers every (column, channel chunk) once;
+    the ring fits the LDS."""
+    PLANE, RING = 57 * 64, 9
+    RB = 4 * PLANE
+    assert RB % 256 == 0 and (RING + 2) * RB <= 160 * 1024
+    for r0 in range(0, 28, 2):
+        sb = (2 * r0) % RING
+        for f in range(4):
+            for kh in range(3):
+                for kw in range(3):
+                    for q in range(4):
+                        addr = []
+                        for l in range(64):
+                            fr, g = l & 15, l >> 4
+                            p = min(16 * f + fr, 55)
+                            r, c = r0 + p // 28, p % 28
+                            y, x = 2 * r + kh - 1, 2 * c + kw - 1
+                            sl = sb + 2 * (p // 28)
+                            sl = sl - RING if sl >= RING else sl
+                            v = (kw == 2) + 2 * (kh == 2)
+                            s = ((p + (v & 1) + 28 * (v >> 1)) >> 1) & 3
+                            col = (c + (v & 1)) * 64 + ((g ^ s) << 4)
+                            a = sl * RB + col + kh * RB + (29 * 64 if kw == 1 else 0) + q * PLANE
+                            addr.append(a)
+                            slot = a // RB
+                            assert slot < RING + 2
+                            if y >= 0:
+                                assert (slot % RING) == (y + 1) % RING
+                            else:
+                                assert slot == 0  # the zero row (step 0 only)
+                            off = a % RB
+                            qq, j = off // PLANE, off % PLANE
+                            assert qq == q and j // 64 == _s2rows_pos(x)
+                            assert ((j % 64) // 16) ^ _s2rows_swz(y, x) == g
+                        assert _b128_ways(addr) == 1, (r0, f, kh, kw, q)
+    # rows in use at a step (2 r0 - 1 .. 2 r0 + 3) and those DMA'd during it
+    # (2 r0 + 4 .. 2 r0 + 7) occupy 9 distinct slots
+    for r0 in range(0, 26, 2):
+        assert len({(yy + 1) % RING for yy in range(2 * r0 - 1, 2 * r0 + 8)}) == 9
+    seen = set()
+    for q in range(4):
+        for k in range(224):
+            pos, c = 1 + k // 4, k % 4
+            x = 2 * pos - 1 if pos < 29 else 2 * (pos - 29)
+            seen.add((x, 4 * q + (c ^ _s2rows_swz(0, x))))
+    assert seen == {(x, cc) for x in range(56) for cc in range(16)}
+
+
 def test_rows28_lds_layout():
     """conv3x3_rows28.hip: every ds_read_b128 of a 112-pixel step (7
     fragments x 9 taps x 4 channel quarters, all 7 steps, through the
