@@ -224,6 +224,7 @@ int Engine::conv(int in, const std::string& name, const std::string& bn, int cou
   }
   convs_.back().in_act = in;
   const int out = add_act(os);
+  convs_.back().out_act = out;
   Op op{OpType::Conv, in, out, res, (int)convs_.size() - 1, 0, 0, 0, name};
   ops_.push_back(op);
   return out;
@@ -371,6 +372,7 @@ void Engine::mark_fp8() {
     if (op.type == OpType::Conv && !convs_[op.conv].fc && shapes_[op.out].C % 128 == 0 &&
         (fp8_3x3 || !near_3x3[op.out]))
       shapes_[op.out].fp8 = true;
+  chan_act_.assign(shapes_.size(), false);
   if (opt_.fp8_3x3_out && !fp8_3x3) {
     // outputs of 3x3 convs that no 3x3 conv reads (a bottleneck's t2), where
     // the conv runs on conv3x3_rows28 / conv3x3_stream (e4m3 epilogues)
@@ -385,8 +387,10 @@ void Engine::mark_fp8() {
           shapes_[op.out].C % 128 || shapes_[op.in].fp8)
         continue;
       if (conv3x3_rows28_supported(is.H, is.W, is.C, L.cout) ||
-          conv3x3_stream_supported(is.H, is.W, is.C, L.cout, L.stride) || (opt_.fp8_3x3_out_s2 && L.stride == 2))
+          conv3x3_stream_supported(is.H, is.W, is.C, L.cout, L.stride) || (opt_.fp8_3x3_out_s2 && L.stride == 2)) {
         shapes_[op.out].fp8 = true;
+        chan_act_[op.out] = true;
+      }
     }
   }
   for (const Op& op : ops_) {
@@ -433,6 +437,15 @@ void Engine::calibrate(const WeightMap& w) {
     float amax = 0.f;
     for (uint16_t v : a) amax = std::max(amax, std::fabs(bf2f_host(v)));
     shapes_[i].scale = std::max(amax, 1e-6f) / 448.f;
+    if (!chan_act_[i]) continue;
+    // per-channel scales (a channel whose calibration values stay tiny gets
+    // 1/1000 of the tensor's range instead of an unbounded 1 / scale)
+    const int C = shapes_[i].C;
+    std::vector<float> cm(C, 0.f);
+    for (size_t j = 0; j < n; ++j) cm[j % C] = std::max(cm[j % C], std::fabs(bf2f_host(a[j])));
+    shapes_[i].cscale.resize(C);
+    for (int c = 0; c < C; ++c) shapes_[i].cscale[c] = std::max(cm[c], std::max(amax, 1e-6f) * 1e-3f) / 448.f;
+    shapes_[i].scale = 1.f;
   }
 }
 
@@ -531,6 +544,15 @@ void Engine::pack_weights(const WeightMap& w) {
         bias[n] = (float)((double)b.data[n] + ((double)bias[n] - (double)m.data[n]) * s);
       }
     }
+    if (L.out_act >= 0 && !shapes_[L.out_act].cscale.empty()) {
+      // the conv writes e4m3 with per-channel scales: fold 1 / cscale[n] into
+      // its weights and bias (ReLU commutes with a positive scale)
+      const std::vector<float>& cs = shapes_[L.out_act].cscale;
+      for (int n = 0; n < L.cout; ++n) {
+        scale[n] /= cs[n];
+        bias[n] /= cs[n];
+      }
+    }
     std::vector<uint16_t> wbf;
     uint16_t* pw = (uint16_t*)(host.data() + L.w_off);
     if (L.fp8) {  // fold into a bf16 staging copy first, then quantise per row
@@ -589,11 +611,18 @@ void Engine::pack_weights(const WeightMap& w) {
       uint8_t* q = host.data() + L.w_off;
       float* alpha = (float*)(host.data() + L.a_off);
       const float s_in = shapes_[L.in_act].scale;
+      // per-channel input scales (fp8_3x3_out): along K (channel k % Cin)
+      const std::vector<float>& ics = shapes_[L.in_act].cscale;
+      const int cin = shapes_[L.in_act].C;
+      auto wv = [&](int n, int k) {
+        const float v = bf2f_host(pw[(size_t)n * L.kpad + k]);
+        return ics.empty() ? v : v * ics[k % cin];
+      };
       for (int n = 0; n < L.npad; ++n) {
         float amax = 0.f;
-        for (int k = 0; k < L.kpad; ++k) amax = std::max(amax, std::fabs(bf2f_host(pw[(size_t)n * L.kpad + k])));
+        for (int k = 0; k < L.kpad; ++k) amax = std::max(amax, std::fabs(wv(n, k)));
         const float sw = amax > 0.f ? amax / 448.f : 1.f;
-        for (int k = 0; k < L.kpad; ++k) q[(size_t)n * L.kpad + k] = f2e4m3_host(bf2f_host(pw[(size_t)n * L.kpad + k]) / sw);
+        for (int k = 0; k < L.kpad; ++k) q[(size_t)n * L.kpad + k] = f2e4m3_host(wv(n, k) / sw);
         alpha[n] = s_in * sw;
       }
     }

@@ -27,6 +27,10 @@ struct ActShape {
   bool f32 = false;
   bool fp8 = false;   // OCP e4m3 with a per-tensor scale (resnet50_fp8)
   float scale = 1.f;  // value = e4m3 * scale (calibrated)
+  // per-channel e4m3 scales (fp8_3x3_out's t2): value[c] = e4m3 * cscale[c],
+  // folded into the producing conv's weights / bias (1 / cscale) and the
+  // consuming conv's weights (cscale along K); `scale` is then 1
+  std::vector<float> cscale;
   size_t elems_per_image() const { return (size_t)H * W * C; }
   size_t elem_bytes() const { return f32 ? 4 : fp8 ? 1 : 2; }
 };
@@ -44,6 +48,7 @@ struct ConvLayer {
   int npad = 0, kpad = 0;
   size_t w_off = 0, b_off = 0;  // offsets (bytes) into the weight arena
   int in_act = -1;              // activation the conv reads
+  int out_act = -1;             // activation the conv writes
   bool fp8 = false;             // e4m3 weights (input activation is e4m3)
   size_t a_off = 0;             // fp8: alpha[n] = s_in * s_w[n] (fp32 [npad])
   size_t wf_off = 0;            // weights in stream-conv fragment order (0 = none)
@@ -226,6 +231,7 @@ class Engine {
   bool fp8_ = false;  // resnet50_fp8
 
   std::vector<ActShape> shapes_;
+  std::vector<bool> chan_act_;  // activations with per-channel e4m3 scales (mark_fp8 -> calibrate)
   std::vector<ConvLayer> convs_;
   std::vector<Op> ops_;
   int logits_act_ = -1;

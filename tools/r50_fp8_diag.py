@@ -21,10 +21,11 @@ with torch.no_grad():
     mean = torch.tensor([0.485, 0.456, 0.406]).view(1, 3, 1, 1)
     std = torch.tensor([0.229, 0.224, 0.225]).view(1, 3, 1, 1)
     ref = model((img[:16].permute(0, 3, 1, 2).float() / 255 - mean) / std)
-variants = {"default": {}, "no ds_into_expand": {"ds_into_expand": False},
-            "fp8_3x3_out off": {"fp8_3x3_out": False},
-            "fp8_3x3_out off, no ds_into_expand": {"fp8_3x3_out": False, "ds_into_expand": False},
-            "no stream_conv": {"stream_conv": False}}
+variants = {"fp8_3x3_out off": {"fp8_3x3_out": False},
+            "fp8_3x3_out on": {"fp8_3x3_out": True},
+            "fp8_3x3_out on, no ds_into_expand": {"fp8_3x3_out": True, "ds_into_expand": False},
+            "fp8_3x3_out on, no stream_conv": {"fp8_3x3_out": True, "stream_conv": False},
+            "fp8_3x3_out on, strided too": {"fp8_3x3_out": True, "fp8_3x3_out_s2": True}}
 out = {}
 for name, opts in variants.items():
     eng = InferenceEngine("resnet50_fp8", sd, max_batch=B, options=opts)
@@ -36,6 +37,6 @@ for name, opts in variants.items():
         agree = (lg[:16].argmax(-1) == ref.argmax(-1)).float().mean().item()
         out[(name, graph)] = i.cpu()
         print(f"B={B} {name:36s} graph={graph}: rel {rel:.4f} top1 vs fp32 {agree:.3f}", flush=True)
-base = out[("default", True)]
+base = out[("fp8_3x3_out off", True)]
 for k, v in out.items():
-    print(f"  top1 agreement with default/graph: {k}: {(v == base).float().mean().item():.3f}")
+    print(f"  top1 agreement with fp8_3x3_out off (graph): {k}: {(v == base).float().mean().item():.3f}")
