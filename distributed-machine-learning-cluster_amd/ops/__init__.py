@@ -220,6 +220,27 @@ def conv3x3_s2rows(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, 
     return y, yd
 
 
+def conv3x3_s2rows128(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, relu: bool = True,
+                      out_inv_scale: float = 0.0):
+    """ResNet50 layer2.0.conv2, [B,56,56,128] -> [B,28,28,128] stride 2, one
+    row-streaming weight-stationary workgroup per image
+    (conv3x3_s2rows128.hip). Returns bf16, or e4m3 bytes (uint8) of
+    relu?(conv + bias) * out_inv_scale when out_inv_scale > 0."""
+    _need_cuda(x, w_packed, bias)
+    C = native()
+    B, H, W, Cin = x.shape
+    Cout = w_packed.shape[0]
+    if not C.conv3x3_s2rows128_supported(H, W, Cin, Cout) or tuple(w_packed.shape) != (Cout, 9 * Cin):
+        raise ValueError("conv3x3_s2rows128: unsupported shape")
+    x = x.contiguous()
+    dt = torch.uint8 if out_inv_scale > 0 else x.dtype
+    y = torch.empty(B, H // 2, W // 2, Cout, dtype=dt, device=x.device)
+    wf = stream_weight_frag(w_packed)
+    C.conv3x3_s2rows128(_ptr(x), _ptr(wf), _ptr(bias.float().contiguous()), _ptr(y), B, relu, float(out_inv_scale),
+                        _stream())
+    return y
+
+
 def conv_small(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, res: torch.Tensor | None = None,
                relu: bool = True, stride: int = 1, wd_packed: torch.Tensor | None = None,
                bd: torch.Tensor | None = None, mf: int | None = None):
