@@ -126,13 +126,12 @@ struct EngineOptions {
   // the direct bf16 convs beat the fp8 implicit GEMM on those shapes)
   bool fp8_3x3 = false;
   // ResNet50 e4m3: the bottleneck 3x3 convs that run on the row / stream
-  // kernels write e4m3 (their bf16 inputs stay), so the expand conv reads e4m3
-  // (117.8-118.1k vs 112.5-112.7k img/s same box, profiles/r4_r50_3x3_e4m3_out.txt).
-  // Off by default: with one per-tensor scale for t2 the logits move from
-  // 3.1% to 4.5% off fp32 and 1-2 of 16 confident top-1s flip on some
-  // random-init models (tools/r50_fp8_diag.py); per-channel t2 scales folded
-  // into the expand weights are the way to win it back
-  bool fp8_3x3_out = false;
+  // kernels write e4m3 (their bf16 inputs stay), so the expand conv reads e4m3:
+  // 120.8k vs 116.0k img/s same box (profiles/r4_r50_fp8_3x3_out_perchannel.txt).
+  // Per-channel scales folded into the weights (ActShape::cscale): logits 4.2%
+  // vs 3.1% off fp32, top-1 16/16 (one per-tensor scale: 4.5% and 1-2 flips,
+  // profiles/r4_r50_fp8_3x3_out_accuracy.txt)
+  bool fp8_3x3_out = true;
   // ... and the strided 3x3 convs of layer3.0 / layer4.0 (implicit GEMM with
   // an e4m3 epilogue instead of the bf16 big-tile kernel)
   bool fp8_3x3_out_s2 = false;

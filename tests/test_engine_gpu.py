@@ -478,6 +478,15 @@ def test_resnet50_downsample_in_expand_matches_separate(gpu, arch):
     p = torch.softmax(rl.float().cpu(), -1)
     top2 = p.topk(2, -1).values
     near = (top2[:, 0] - top2[:, 1]) < 5e-2
+    if arch.endswith("fp8"):
+        # e4m3 paths that differ in rounding points: a top-1 may flip where the
+        # two leading logits are within a few times the per-image rms logit
+        # difference of the two engines (large-logit random models make the
+        # probability gap a poor tie measure)
+        lg = rl.float().cpu()
+        gap = lg.topk(2, -1).values
+        rms = (fl.float().cpu() - lg).pow(2).mean(-1).sqrt()
+        near = near | ((gap[:, 0] - gap[:, 1]) < 4 * rms)
     assert torch.all((fi.cpu() == ri.cpu()) | near)
     prof = dict(eng._e.profile(x.data_ptr(), 64, 224, 224, 0))
     rprof = dict(ref_eng._e.profile(x.data_ptr(), 64, 224, 224, 0))
