@@ -1,9 +1,11 @@
 #!/usr/bin/env python3
-"""A/B of the role-split ResNet stem (stem_pool.hip stem_roles_kernel<7, V>)
-variants at B=256, 224x224 u8 images: each variant's output must be
-bit-identical to the default's (same arithmetic, only the issue order and the
-helpers' store order differ), then graph-replayed timings, interleaved over
---rounds rounds in one process (tools/conv_bench.py's timer)."""
+"""Knock-out timings of the role-split ResNet stem (stem_pool.hip
+stem_roles_kernel<7, V>, V bits: 4 no u8 conversion, 8 no conv rows, 16 no
+pooling epilogue, 32 no DMA / vertical max / stores) at B=256, 224x224 u8
+images, graph-replayed, interleaved over --rounds rounds in one process
+(tools/conv_bench.py's timer). The variants this tool A/B'd in round 4
+(pipelined operand reloads, rotated helper stores, the packed pooling
+epilogue) are in profiles/r4_stem_roles.txt."""
 import argparse
 import os
 import statistics
@@ -18,10 +20,8 @@ from dmlc import ops  # noqa: E402
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from conv_bench import time_us, warm_gpu  # noqa: E402
 
-NAMES = {0: "default", 1: "pipelined operand reloads", 2: "rotated helper stores", 3: "both",
-         4: "KO u8 conversion", 8: "KO conv rows", 16: "KO h-pool epilogue",
-         36: "MFMA + h-pool only", 52: "MFMA only", 40: "conversion only",
-         64: "packed bf16 pooling"}
+NAMES = {0: "default", 4: "KO u8 conversion", 8: "KO conv rows", 16: "KO h-pool epilogue",
+         36: "MFMA + h-pool only", 52: "MFMA only", 40: "conversion only"}
 KNOCKOUTS = {4, 8, 16, 36, 52, 40}
 
 
@@ -30,7 +30,7 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--variants", default="0,1,2,3")
+    ap.add_argument("--variants", default="0,4,8,16,36,52,40")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     g = torch.Generator().manual_seed(5)
@@ -58,13 +58,6 @@ def main():
         torch.cuda.synchronize()
         same = torch.equal(out.view(torch.int16), ref.view(torch.int16))
         print(f"variant {v} ({NAMES.get(v, '')}): bit-identical to the default: {same}", flush=True)
-        if v & 64:  # bias accumulated from the start: rounding may differ by an ulp
-            d = (out.float() - ref.float()).abs()
-            rel = (d / ref.float().abs().clamp_min(1e-3)).max().item()
-            print(f"  max abs diff {d.max().item():.4g}, max rel {rel:.3g}, differing {(d > 0).float().mean().item():.4%}")
-            if d.max().item() > 0.05 * ref.float().abs().max().item():
-                raise SystemExit(f"variant {v} out of tolerance")
-            continue
         if not same:
             raise SystemExit(f"variant {v} differs: max abs {(out.float() - ref.float()).abs().max().item()}")
     warm_gpu()
