@@ -473,8 +473,11 @@ class HostFleet {
       if (dp::Worker* w = f_->worker(kv.first, d)) dp::host_worker_set_healthy(*w, false);
   }
   // queries: (model, first, count) over `images`; run by `threads` threads.
+  // Queries listed in `bad` fail inside their stage function (as a JPEG of
+  // a bad size does in the GPU executor's stage): only they get an error.
   py::dict run(py::array_t<uint8_t, py::array::c_style> images, std::vector<std::tuple<std::string, int64_t, int64_t>> qs,
-               int threads) {
+               int threads, std::vector<int> bad) {
+    const std::set<int> bad_q(bad.begin(), bad.end());
     const size_t ib = (size_t)H_ * W_ * 3;
     const uint8_t* src = images.data();
     const int64_t total = images.shape(0);
@@ -494,7 +497,9 @@ class HostFleet {
               if (first < 0 || first + count > total) throw std::invalid_argument("query out of range");
               idx[q].assign(count, -1);
               prob[q].assign(count, 0.f);
-              auto stage = [&, first = first](const dp::StageCtx& c, int64_t off, int64_t n) -> const uint8_t* {
+              const bool fails = bad_q.count((int)q) > 0;
+              auto stage = [&, first = first, fails](const dp::StageCtx& c, int64_t off, int64_t n) -> const uint8_t* {
+                if (fails) throw std::runtime_error("stage: bad image size");
                 if (n > c.capacity) throw std::logic_error("stage: more images than the batch holds");
                 std::memcpy(c.batch, src + (size_t)(first + off) * ib, (size_t)n * ib);
                 return (const uint8_t*)c.batch;
@@ -536,6 +541,9 @@ class HostFleet {
     std::map<std::string, std::map<int, int64_t>> fwd;
     for (const auto& kv : f_->partitions()) fwd[kv.first] = f_->forwards(kv.first);
     d["forwards"] = fwd;
+    std::map<std::string, std::map<int, int64_t>> sizes;
+    for (const auto& kv : f_->partitions()) sizes[kv.first] = f_->forward_sizes(kv.first);
+    d["forward_sizes"] = sizes;
     std::lock_guard<std::mutex> g(mu_);
     d["comm_builds"] = comm_builds_;
     d["overlapping_worlds"] = overlaps_;
@@ -707,6 +715,7 @@ class RcclLoop {
 
 void bind_dp(py::module& m) {
   m.def("dp_partition_devices", &dp::partition_devices, py::arg("live"), py::arg("jobs"));
+  m.def("fleet_bucket_batch", &dp::bucket_batch, py::arg("b"), py::arg("max"));
   m.def("host_order_probe", &host_order_probe, py::arg("bad"), py::arg("timeout_ms") = 500);
   m.def("host_multi_world_probe", &host_multi_world_probe, py::arg("timeout_ms") = 2000);
   py::class_<HostFleet>(m, "HostFleet")
@@ -720,7 +729,8 @@ void bind_dp(py::module& m) {
       .def("fail", &HostFleet::fail)
       .def("set_seed", &HostFleet::set_seed)
       .def("fail_next_builds", &HostFleet::fail_next_builds)
-      .def("run", &HostFleet::run, py::arg("images"), py::arg("queries"), py::arg("threads") = 1)
+      .def("run", &HostFleet::run, py::arg("images"), py::arg("queries"), py::arg("threads") = 1,
+           py::arg("bad") = std::vector<int>{})
       .def("state", &HostFleet::state);
   py::class_<RcclLoop>(m, "RcclLoop")
       .def(py::init<int, int>(), py::arg("device") = 0, py::arg("max_ctas") = 0)

@@ -1,5 +1,7 @@
 #include "dp.h"
 
+#include <map>
+
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -38,14 +40,21 @@ class HostWorker : public Worker {
     stamps_.emplace_back();
     return n_events_++;
   }
-  // synchronous "streams": an event's time is the time it was recorded
-  void record(int ev, int) override {
+  // synchronous "streams" with a synthetic device clock per stream: a
+  // forward advances its compute stream's clock by its modelled cost
+  // (delay_us + us_per_image * B + extra_us) and an event reads the clock of
+  // the stream it is recorded on, so elapsed_ms() around a forward is exactly
+  // that cost, whatever the host's sleep and wake-up jitter (the forward
+  // still sleeps for it, so the protocol's real-time overlap is exercised).
+  // The coordinator calibration that reads these times is then deterministic
+  // (its tests used to assert on wall-clock stamps).
+  void record(int ev, int stream) override {
     std::lock_guard<std::mutex> g(mu_);
-    stamps_.at(ev) = std::chrono::steady_clock::now();
+    stamps_.at(ev) = clock_us_[stream];
   }
   double elapsed_ms(int a, int b) override {
     std::lock_guard<std::mutex> g(mu_);
-    return std::chrono::duration<double, std::milli>(stamps_.at(b) - stamps_.at(a)).count();
+    return (double)(stamps_.at(b) - stamps_.at(a)) / 1000.0;
   }
   void wait(int, int) override {}
   bool query(int) override { return true; }
@@ -61,6 +70,10 @@ class HostWorker : public Worker {
     std::memcpy(&w, arena_, 4);
     const int64_t us = delay_us_ + (int64_t)us_per_image_ * B + extra_us_;
     if (us > 0) std::this_thread::sleep_for(std::chrono::microseconds(us));
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      clock_us_[compute_stream(lane)] += us;
+    }
     for (int b = 0; b < B; ++b) {
       const uint8_t* img = images + (size_t)b * bytes_;
       idx[b] = (int32_t)(((uint64_t)host_class_of(img, bytes_, 1 << 30) + w) % (uint64_t)classes_);
@@ -96,7 +109,8 @@ class HostWorker : public Worker {
   std::vector<std::atomic<bool>> busy_;
   uint8_t arena_[16] = {};
   int n_events_ = 0;
-  std::vector<std::chrono::steady_clock::time_point> stamps_;
+  std::vector<int64_t> stamps_;             // synthetic µs, per event
+  std::map<int, int64_t> clock_us_;         // synthetic µs, per stream
   std::mutex mu_;
   std::vector<void*> live_;
 };

@@ -1,5 +1,7 @@
 #include "fleet.h"
 
+#include "cv_wait.h"
+
 #include <algorithm>
 #include <chrono>
 #include <climits>
@@ -70,6 +72,8 @@ struct Fleet::Instance {
   std::atomic<int> outstanding{0};
   std::atomic<int64_t> served{0};
   std::atomic<int64_t> forwards{0};
+  std::mutex sizes_mu;
+  std::map<int, int64_t> sizes;  // direct forwards by (bucketed) batch size
 
   Instance(std::string m, int d, std::unique_ptr<Worker> worker, const FleetOptions& o)
       : model(std::move(m)), device(d), max(o.max_per_rank), ib(o.image_bytes), aux_pi(o.aux_bytes),
@@ -107,7 +111,9 @@ struct Fleet::Instance {
   // stream of small queries cannot starve a scatter), then every lane.
   void claim_all() {
     std::unique_lock<std::mutex> g(mu);
-    cv.wait_for(g, std::chrono::milliseconds(5), [&] { return q.empty() || dead; });
+    const auto until = std::chrono::steady_clock::now() + std::chrono::milliseconds(5);
+    while (!(q.empty() || dead) && cv_wait_until(cv, g, until) != std::cv_status::timeout) {
+    }
     ++claims;  // no new direct forward starts from here on
     cv.wait(g, [&] { return free.size() == lanes.size(); });
   }
@@ -220,6 +226,17 @@ std::map<int, int64_t> Fleet::forwards(const std::string& model) const {
   const Model& m = get(model);
   std::map<int, int64_t> out;
   for (const auto& i : m.inst) out[i->device] += i->forwards.load();
+  return out;
+}
+
+std::map<int, int64_t> Fleet::forward_sizes(const std::string& model) const {
+  std::shared_lock<std::shared_mutex> lk(plan_mu_);
+  const Model& m = get(model);
+  std::map<int, int64_t> out;
+  for (const auto& i : m.inst) {
+    std::lock_guard<std::mutex> g(i->sizes_mu);
+    for (const auto& kv : i->sizes) out[kv.first] += kv.second;
+  }
   return out;
 }
 
@@ -459,14 +476,16 @@ Fleet::Route Fleet::classify(const std::string& model, int64_t n, const StageFn&
   }
 }
 
-namespace {
-// Smallest power of two >= b, at most max (bounded graph set per lane).
-int bucket_of(int b, int max) {
+// Forward batch of b coalesced images: the next power of two up to 64, then
+// the next multiple of 32 (at most max). A bounded set of captured graphs per
+// lane (7 + (max - 64) / 32), and above 64 images a forward pads at most 31
+// (a 129-image forward runs 160, not 256).
+int bucket_batch(int b, int max) {
   int p = 1;
-  while (p < b) p <<= 1;
+  while (p < b && p < 64) p <<= 1;
+  if (b > 64) p = (b + 31) / 32 * 32;
   return std::min(p, max);
 }
-}  // namespace
 
 Fleet::Route Fleet::direct(Model& m, int64_t n, const StageFn& stage, int32_t* idx, float* prob, int prefer) {
   // least outstanding queries; ties rotate so equal load spreads evenly; the
@@ -562,9 +581,19 @@ Fleet::Route Fleet::direct(Model& m, int64_t n, const StageFn& stage, int32_t* i
       auto& L = in.lanes[f.lane];
       const int cs = Worker::compute_stream(f.lane);
       bool issued = false;
+      std::vector<std::pair<Req*, std::exception_ptr>> failed;  // stage errors, published under in.mu
+      auto publish_failed = [&]() {  // holds in.mu
+        for (auto& fr : failed) {
+          fr.first->err = fr.second;
+          fr.first->state = 3;
+        }
+        failed.clear();
+      };
       try {
         w->activate();
         int off = 0;
+        std::vector<Req*> kept;
+        kept.reserve(f.batch.size());
         for (Req* r : f.batch) {
           StageCtx ctx;
           ctx.worker = w;
@@ -579,21 +608,28 @@ Fleet::Route Fleet::direct(Model& m, int64_t n, const StageFn& stage, int32_t* i
             p = (*r->stage)(ctx, r->first, r->n);
           } catch (...) {
             if (!w->healthy()) throw;
-            r->err = std::current_exception();  // this request only
-            r->state = 3;
+            // this request only. Its owner may return (and free it) as soon
+            // as it sees state 3, so the failure is published under in.mu
+            // below and the request leaves this forward's batch now: nothing
+            // here touches it after the publish.
+            failed.emplace_back(r, std::current_exception());
             continue;
           }
           // the lane's own buffer, so the graph key (batch address, bucket) is fixed per lane
           if (p != ctx.batch) w->copy(ctx.batch, p, (size_t)r->n * in.ib, cs);
           r->off = off;
           off += r->n;
+          kept.push_back(r);
         }
+        f.batch.swap(kept);
         if (off > 0) {
-          const int Bf = opt_.bucket_batches ? bucket_of(off, max) : off;
+          const int Bf = opt_.bucket_batches ? bucket_batch(off, max) : off;
           auto* a = (uint8_t*)L.ans;
           w->classify((const uint8_t*)L.batch, Bf, (int32_t*)a, (float*)(a + (size_t)max * 4), f.lane);
           w->copy_d2h(L.ans_host, L.ans, (size_t)max * 8, cs);
           in.forwards++;
+          std::lock_guard<std::mutex> sg(in.sizes_mu);
+          in.sizes[Bf]++;
         }
         w->record(L.ev, cs);
         issued = true;
@@ -601,6 +637,7 @@ Fleet::Route Fleet::direct(Model& m, int64_t n, const StageFn& stage, int32_t* i
         const bool lost = !w->healthy();
         const auto err = std::current_exception();
         g.lock();
+        publish_failed();
         for (Req* r : f.batch)
           if (r->state == 1) {
             r->state = 3;
@@ -614,6 +651,8 @@ Fleet::Route Fleet::direct(Model& m, int64_t n, const StageFn& stage, int32_t* i
         continue;
       }
       g.lock();
+      publish_failed();
+      in.cv.notify_all();  // owners of failed requests
       if (issued) mine.push_back(std::move(f));
     }
     if (!mine.empty()) {  // finish my oldest forward
@@ -659,7 +698,7 @@ Fleet::Route Fleet::direct(Model& m, int64_t n, const StageFn& stage, int32_t* i
     // wait for: a lane, my requests answered by another caller's forward, or
     // the batching window of the oldest queued request
     if (!in.q.empty() && in.claims == 0 && !in.free.empty() && !in.dead)
-      in.cv.wait_until(g, in.q.front()->t0 + window);
+      cv_wait_until(in.cv, g, in.q.front()->t0 + window);
     else
       in.cv.wait(g);
   }

@@ -29,8 +29,8 @@
 //     same way, so its chunks run on several lanes at once (issued together,
 //     synchronised oldest first) instead of one lane with a host sync per
 //     chunk. The batch size of a forward is rounded up to a bucket (1, 2, 4,
-//     ..., max_per_rank), so each lane replays one captured hipGraph per
-//     bucket.
+//     ..., 64, then multiples of 32 up to max_per_rank), so each lane replays
+//     one captured hipGraph per bucket.
 //
 // Invariants:
 //   * partitions are disjoint whenever there are at least as many live GPUs
@@ -64,6 +64,9 @@ namespace dp {
 // job j of J gets [j*n/J, (j+1)*n/J); with n < J job j gets GPU j % n alone.
 std::vector<std::vector<int>> partition_devices(std::vector<int> live, int jobs);
 
+// Forward batch for b coalesced images (FleetOptions::bucket_batches).
+int bucket_batch(int b, int max);
+
 struct FleetOptions {
   int max_per_rank = 256;         // images per GPU per forward (= the CU count: one round of the big-batch kernels)
   size_t image_bytes = 224 * 224 * 3;
@@ -77,8 +80,9 @@ struct FleetOptions {
   // ... except on an idle instance (no forward running): the first request
   // goes at once, later ones batch while it runs.
   bool eager_when_idle = true;
-  // Round a forward's batch up to a power of two (max_per_rank at most): a
-  // bounded set of captured graphs per lane.
+  // Round a forward's batch up to a bucket (bucket_batch(): powers of two to
+  // 64, then multiples of 32, max_per_rank at most): a bounded set of
+  // captured graphs per lane.
   bool bucket_batches = true;
 };
 
@@ -146,6 +150,8 @@ class Fleet {
   // Direct-path forwards run per device for `model` (each may carry several
   // coalesced queries).
   std::map<int, int64_t> forwards(const std::string& model) const;
+  // Direct-path forwards by (bucketed) batch size, over the partition.
+  std::map<int, int64_t> forward_sizes(const std::string& model) const;
   int rebalances() const { return rebalances_.load(); }
   // The instance of `model` on `device` (nullptr if none): tests, hooks.
   Worker* worker(const std::string& model, int device) const;

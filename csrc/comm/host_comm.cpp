@@ -29,6 +29,7 @@
 #include <mutex>
 
 #include "comm.h"
+#include "cv_wait.h"
 
 namespace dmlc {
 namespace comm {
@@ -70,7 +71,7 @@ class HostWorld {
       bool all = true;
       for (Op* o : ops) all &= o->done;
       if (all) break;
-      if (cv_.wait_until(g, deadline) == std::cv_status::timeout) {
+      if (cv_wait_until(cv_, g, deadline) == std::cv_status::timeout) {
         bool all2 = true;
         for (Op* o : ops) all2 &= o->done;
         if (all2) break;

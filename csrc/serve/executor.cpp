@@ -21,6 +21,7 @@
 #include <climits>
 #include <set>
 #include "shard.h"
+#include "../control/common.h"
 #include <fstream>
 #include "../kernels/kernels.h"
 #include <condition_variable>
@@ -203,7 +204,8 @@ class CpuExecutor : public Executor {
 //     arrive, streamed from disk through two pinned buffers on per-GPU side
 //     streams (the read of chunk i+1 overlaps the DMA of chunk i); a shard
 //     query runs on the GPU holding its slice when that GPU is in the model's
-//     partition, reading the slice in place.
+//     partition, reading the slice from that GPU's HBM (one on-device copy
+//     into the lane's batch buffer, no host or xGMI traffic).
 class GpuExecutor : public Executor {
  public:
   GpuExecutor(std::vector<int> devices, int max_batch, size_t cache_bytes, int min_shard, int lanes, int batch_window_us)
@@ -252,23 +254,35 @@ class GpuExecutor : public Executor {
   void set_jobs(const std::vector<std::string>& models) override { fleet_->set_jobs(models); }
   void lose_device(int device) override {
     fleet_->lose(device);
+    {
+      // decoded query images homed on the lost GPU are gone with it (first:
+      // a re-staging failure below must not leave them cached)
+      std::lock_guard<std::mutex> g(cache_mu_);
+      for (auto it = cache_.begin(); it != cache_.end();) {
+        if (it->second.device == device && it->second.pins == 0) {
+          cache_bytes_ -= it->second.bytes;
+          cache_bytes_dev_[device] -= it->second.bytes;
+          lru_.erase(it->second.lru);
+          it = cache_.erase(it);  // (its memory went with the device)
+        } else {
+          ++it;
+        }
+      }
+    }
     // the partitions moved: every staged shard is placed for the new ones now
     std::vector<std::pair<std::string, std::shared_ptr<HbmBlob>>> bs;
     {
       std::lock_guard<std::mutex> g(blob_mu_);
       for (const auto& kv : hbm_blobs_) bs.emplace_back(kv.first, kv.second);
     }
-    for (auto& kv : bs) current_blob(kv.first, kv.second);
-    // decoded query images homed on the lost GPU are gone with it
-    std::lock_guard<std::mutex> g(cache_mu_);
-    for (auto it = cache_.begin(); it != cache_.end();) {
-      if (it->second.device == device && it->second.pins == 0) {
-        cache_bytes_ -= it->second.bytes;
-        cache_bytes_dev_[device] -= it->second.bytes;
-        lru_.erase(it->second.lru);
-        it = cache_.erase(it);  // (its memory went with the device)
-      } else {
-        ++it;
+    for (auto& kv : bs) {
+      try {
+        current_blob(kv.first, kv.second);
+      } catch (const std::exception& e) {
+        // (a missing file, or HBM exhausted while the old and new copies
+        // coexist): the blob stays placed for the old partitions, so the next
+        // query that reads it retries the re-staging
+        DMLC_LOG_WARN("re-staging " << kv.first << " after losing GPU " << device << " failed: " << e.what());
       }
     }
   }
@@ -415,7 +429,7 @@ class GpuExecutor : public Executor {
 
   // SDFS u8 shard replica -> HBM: one full copy per serving partition, each
   // sliced over that partition's GPUs (shard.h shard_placement), so every
-  // model reads the images of its queries in place from a GPU it serves on.
+  // model reads the images of its queries from the HBM of a GPU it serves on.
   void stage_blob(const std::string& key, const std::string& path) override {
     auto b = load_blob(path);
     std::lock_guard<std::mutex> g(blob_mu_);
@@ -717,9 +731,17 @@ class GpuExecutor : public Executor {
       auto it = hbm_blobs_.find(key);
       if (it != hbm_blobs_.end() && it->second != b && ok(*it->second)) return it->second;  // done meanwhile
     }
-    auto nb = load_blob(b->path);
+    auto nb = load_blob(b->path);  // long: the file read and the DMA run without blob_mu_
     std::lock_guard<std::mutex> g(blob_mu_);
-    hbm_blobs_[key] = nb;
+    auto it = hbm_blobs_.find(key);
+    if (it != hbm_blobs_.end() && it->second == b) {
+      it->second = nb;  // still the stale blob we found: replace it
+      return nb;
+    }
+    // stage_blob installed a newer replica meanwhile (keep it; this query
+    // may still read its own fresh copy of the old one), or the key was
+    // dropped: either way nb is not installed and is freed with the query
+    if (it != hbm_blobs_.end() && ok(*it->second)) return it->second;
     return nb;
   }
 
@@ -752,8 +774,12 @@ class GpuExecutor : public Executor {
 
   // Images [first, first + n) of a staged shard through the fleet (no scatter:
   // the slices are already spread over the partition's GPUs; the query
-  // prefers the GPU holding its first image in the model's copy, and reads
-  // it there in place).
+  // prefers the GPU holding its first image in the model's copy). The stage
+  // returns the slice's own HBM address when the range lies in a slice on the
+  // serving GPU, and the fleet then copies it device-to-device into the
+  // lane's batch buffer (Fleet::direct: a coalesced forward's batch address
+  // is fixed per lane, so each lane replays one captured graph per bucket):
+  // n x 150 KB at HBM copy speed, about 1-2 % of a 256-image forward.
   void classify_range(const std::string& model, std::shared_ptr<HbmBlob> b, const std::string& key, int64_t first,
                       int64_t n, int32_t* idx, float* prob) {
     b = current_blob(key, b);
@@ -766,7 +792,7 @@ class GpuExecutor : public Executor {
       const int64_t g0 = first + off;
       auto s = (hipStream_t)c.worker->stream(c.stream);
       if (dense) {
-        for (const auto& pc : b->pieces)  // in place: the whole range in a slice on this GPU
+        for (const auto& pc : b->pieces)  // the whole range in a slice on this GPU (copied into the lane by the fleet)
           if (pc.device == c.device && g0 >= pc.first && g0 + cnt <= pc.first + pc.n)
             return (const uint8_t*)pc.dev + (size_t)(g0 - pc.first) * ib;
         for (int64_t pos = g0; pos < g0 + cnt;) {  // gather the range into the stage buffer

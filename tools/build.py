@@ -204,6 +204,22 @@ def build(jobs: int = 8, verbose: bool = False, node: bool = True) -> None:
                     and "control" + os.sep + "member.cpp" not in s and "serve" + os.sep + "leader.cpp" not in s:
                 fuzz_objs.append(o)
         tsan_objs = [o for o in tsan_objs if not o.endswith("cli_fuzz.cpp.o")]
+
+    # ---- 6. the serving fleet's coalescing path under both sanitizers
+    # (csrc/tests/fleet_stress.cpp over host workers; no HIP)
+    stress = {}
+    if node:
+        fleet_srcs = [os.path.join(CSRC, "tests", "fleet_stress.cpp")] + \
+            [os.path.join(CSRC, "comm", f) for f in ("dp.cpp", "fleet.cpp", "host_comm.cpp")]
+        for tag, flags in (("tsan", ["-O1", "-g", "-std=c++17", "-fsanitize=thread", "-pthread", "-DDMLC_TSAN"]),
+                           ("asan", asan_flags)):
+            objs = []
+            for s in fleet_srcs:
+                o = os.path.join(OBJ, f"fs{tag}_" + os.path.relpath(s, CSRC).replace(os.sep, "_") + ".o")
+                objs.append(o)
+                if _stale(o, [s], hdr):
+                    steps.append(["g++", *flags, "-c", s, "-o", o])
+            stress[os.path.join(BIN, f"dmlc-fleet-stress-{tag}")] = (objs, flags)
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         list(ex.map(lambda c: _run(c, verbose), steps))
     if asan_objs:
@@ -215,6 +231,10 @@ def build(jobs: int = 8, verbose: bool = False, node: bool = True) -> None:
         tsan_exe = os.path.join(BIN, "dmlc-node-tsan")
         if _stale(tsan_exe, tsan_objs, 0):
             _run(["g++", "-fsanitize=thread", "-pthread", *tsan_objs, "-o", tsan_exe], verbose)
+
+    for exe, (objs, flags) in stress.items():
+        if _stale(exe, objs, 0):
+            _run(["g++", *[f for f in flags if f.startswith(("-fsanitize", "-pthread"))], *objs, "-o", exe], verbose)
 
     libgpu = os.path.join(PKG, "libdmlc_gpu.so")
     if _stale(libgpu, gpu_objs, 0):
