@@ -200,6 +200,14 @@ def main():
            "adaptive_window": a.adaptive_window,
            "query_batch": a.batch, "data": data_desc, "prefetch": a.prefetch, "node_gpus": a.node_gpus,
            "source": "shards" if shards else "jpeg",
+           "fast_periods": a.fast_periods,
+           # the node's failure-detection and background-loop periods this run used
+           # (dmlc-node flags; the reference's are 1 s pings / 1 s detector, a 3 s
+           # failure timeout and 3 s loops: src/membership.rs:230,273,289;
+           # src/services.rs:188,201,213,529)
+           "periods_ms": ({"ping": 200, "detect": 200, "fail": 1200, "bg": 500} if a.fast_periods else
+                          {"ping": 1000, "detect": 1000, "fail": 3000, "bg": 3000}),
+           "kill": a.kill,
            "reference": REF, "jobs": []}
     for j in jobs:
         d = [x / 1000 for x in j["durations_us"]]

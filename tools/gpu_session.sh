@@ -70,8 +70,8 @@ for s in "$@"; do
       m=${s#pmc:}
       # shellcheck disable=SC2046
       step "pmc_sq_$m" 120 rocprofv3 --kernel-trace --output-format csv -d "$OUT/pmc_sq_$m" -o p --pmc \
-        SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE \
-        SQ_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE GRBM_COUNT -- $(bench_short "$m")
+        SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_INSTS_VALU_MFMA_MOPS_F8 SQ_INSTS_VALU_MFMA_MOPS_F6F4 SQ_INSTS_MFMA \
+        SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE -- $(bench_short "$m")
       step "pmc_fetch_$m" 120 rocprofv3 --kernel-trace --output-format csv -d "$OUT/pmc_fetch_$m" -o p --pmc \
         FETCH_SIZE -- $(bench_short "$m")
       step "pmc_write_$m" 120 rocprofv3 --kernel-trace --output-format csv -d "$OUT/pmc_write_$m" -o p --pmc \
