@@ -51,6 +51,14 @@ struct R28Args {
   bf16* y;            // [B, 28, 28, 128] (OUT8: e4m3 bytes)
   int relu;
   float out_inv_scale;  // OUT8: y = e4m3(relu(v) * out_inv_scale)
+  // DSX (ResNet18 layer2.0.conv2, ds_into_conv2): the block's 1x1/s2
+  // downsample of its input xds [B, 56, 56, 64] as 2 more K steps of this
+  // conv (K = 1152 + 64), weights wds in fragment order [4][2][2][64][8],
+  // bias bds added to bias: y = relu(conv3x3(x) + b + wds * xds[2y, 2x] + bds),
+  // exactly the residual block's output without the yd round trip
+  const bf16* xds;
+  const bf16* wds;
+  const float* bds;
 };
 
 // 4 floats (within +-448) -> 4 e4m3 bytes
@@ -102,9 +110,12 @@ __device__ __forceinline__ void vm_wait_plus(int n) {
 // waves (two per SIMD) x 16 channels, 144 weight registers, every X fragment
 // read feeding one MFMA instead of two.
 // OUT8: e4m3 output (ResNet50's layer2 3x3 -> its e4m3 expand conv; NW = 4, no residual)
-template <bool RES, int DBG = 0, int AH = 1, int NW = 4, bool OUT8 = false>
+// DSX: see R28Args::xds (4 waves, no residual operand: the downsample is the residual)
+template <bool RES, int DBG = 0, int AH = 1, int NW = 4, bool OUT8 = false, bool DSX = false>
 __global__ __launch_bounds__(64 * NW, 1) void conv3x3_rows28_kernel(R28Args a) {
   static_assert(!OUT8 || (NW == 4 && !RES), "e4m3 output: the 4-wave form without residual");
+  static_assert(!DSX || (NW == 4 && !RES && !OUT8 && AH == 1), "downsample K steps: the 4-wave bf16 form");
+  constexpr int kDS = DSX ? 2 : 0;  // downsample K steps (64 input channels)
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
   constexpr int NF = NW == 4 ? 2 : 1;  // N fragments (16 channels) per wave
   constexpr int NT = 64 * NW;
@@ -160,6 +171,9 @@ __global__ __launch_bounds__(64 * NW, 1) void conv3x3_rows28_kernel(R28Args a) {
   float bs[CPL];
 #pragma unroll
   for (int e = 0; e < CPL; ++e) bs[e] = a.bias[ch0 + 8 * g + 4 * nf0 + e];
+  if constexpr (DSX)
+#pragma unroll
+    for (int e = 0; e < CPL; ++e) bs[e] += a.bds[ch0 + 8 * g + e];
   for (int yy = 0; yy <= 4; ++yy) load_row(yy);
 
   // ---- per-lane constants: fragment f = tile pixels p = 16 f + fr (row
@@ -177,12 +191,17 @@ __global__ __launch_bounds__(64 * NW, 1) void conv3x3_rows28_kernel(R28Args a) {
       col[f][kw] = (c + kw) * 64 + ((g ^ s) << 4);
     }
   }
-  bf16x8 w[kKS][NF];
+  bf16x8 w[kKS + kDS][NF];
 #pragma unroll
   for (int t = 0; t < kKS; ++t)
 #pragma unroll
     for (int nf = 0; nf < NF; ++nf)
       w[t][nf] = *(const bf16x8*)(a.wf + ((((long)cg * kKS + t) * 2 + nf + nf0) * 64 + lane) * 8);
+#pragma unroll
+  for (int t = 0; t < kDS; ++t)
+#pragma unroll
+    for (int nf = 0; nf < NF; ++nf)
+      w[kKS + t][nf] = *(const bf16x8*)(a.wds + ((((long)cg * kDS + t) * 2 + nf) * 64 + lane) * 8);
   // the prologue rows (DMA'd before the weights) have landed; the weights
   // (72 loads, 288 KB per workgroup from L2) may still be in flight: the
   // first step's MFMAs wait for each K step's own fragments (the compiler's
@@ -201,6 +220,23 @@ __global__ __launch_bounds__(64 * NW, 1) void conv3x3_rows28_kernel(R28Args a) {
     // physical chunk c ^ (p & 15), so the epilogue's reads are conflict free.
     // Issued before this step's row DMAs: its wait leaves those in flight.
     const long obase = ((long)b * kH + r0) * kW * kC + ch0 + 8 * g + 4 * nf0;
+    if constexpr (DSX) {
+      // the downsample's input pixels x[2 (r0 + p / 28), 2 (p % 28)] (128 B
+      // each) -> LDS [112 pixels][8 chunks], chunk c at physical c ^ (p & 7):
+      // the B-fragment reads of the 2 downsample K steps are conflict free
+      // (tests/test_layouts_cpu.py)
+      const bf16* ximg = a.xds + (long)b * (2 * kH) * (2 * kW) * 64;
+#pragma unroll
+      for (int j = 0; j < (kMF * 16 * 8 + NT - 1) / NT; ++j) {
+        const int i0 = j * NT + wave * 64;
+        if (i0 < kMF * 16 * 8) {
+          const int i = i0 + lane;
+          const int p = i >> 3, c = (i & 7) ^ (p & 7);
+          const int yy = 2 * (r0 + p / kW), xx = 2 * (p % kW);
+          dma16(ximg + ((long)yy * (2 * kW) + xx) * 64 + 8 * c, resbuf + i0 * 16);
+        }
+      }
+    }
     if constexpr (RES) {
       const bf16* rimg = a.res + ((long)b * kH + r0) * kW * kC;
 #pragma unroll
@@ -274,6 +310,26 @@ __global__ __launch_bounds__(64 * NW, 1) void conv3x3_rows28_kernel(R28Args a) {
         }
       }
       __builtin_amdgcn_sched_barrier(0);
+      if constexpr (DSX) {
+        // this wave's downsample-input DMAs (older than this step's row DMAs)
+        // have landed, and everyone's; then the 2 downsample K steps
+        vm_wait<0>();
+        __builtin_amdgcn_s_barrier();
+#pragma unroll
+        for (int u = 0; u < kDS; ++u) {
+#pragma unroll
+          for (int f = 0; f < PF; ++f) {
+            const int p = 16 * (FB + f) + fr;
+            xc[f] = *(const bf16x8*)(resbuf + p * 128 + (((4 * u + g) ^ (p & 7)) << 4));
+          }
+#pragma unroll
+          for (int f = 0; f < PF; ++f)
+#pragma unroll
+            for (int nf = 0; nf < NF; ++nf)
+              acc[f][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[kKS + u][nf], xc[f], acc[f][nf], 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
       if constexpr (RES && FB == 0) {  // this wave's residual DMAs (older than this step's row DMAs) have landed; and everyone's
         if (AH == 1 || step == 0)
           vm_wait<0>();
@@ -356,14 +412,33 @@ bool conv3x3_rows28_supported(int H, int W, int Cin, int Cout) {
 }
 
 void conv3x3_rows28(const void* x, const void* wf, const float* bias, const void* res, void* y, int B, bool relu,
-                    hipStream_t s, int dbg, float out_inv_scale) {
+                    hipStream_t s, int dbg, float out_inv_scale, const void* xds, const void* wds, const float* bds) {
   if (B <= 0) return;
+  if (xds || wds || bds) {  // the block's downsample as 2 more K steps (ds_into_conv2)
+    if (!xds || !wds || !bds || res || dbg || out_inv_scale > 0.f || !x || !wf || !bias || !y ||
+        (((uintptr_t)x | (uintptr_t)wf | (uintptr_t)xds | (uintptr_t)wds | (uintptr_t)y) & 15))
+      throw std::invalid_argument("conv3x3_rows28: downsample K steps need xds, wds, bds (no residual, bf16 out)");
+    if (x == y || xds == y) throw std::invalid_argument("conv3x3_rows28: in-place not supported");
+    R28Args a{};
+    a.x = (const bf16*)x;
+    a.wf = (const bf16*)wf;
+    a.bias = bias;
+    a.y = (bf16*)y;
+    a.relu = relu;
+    a.xds = (const bf16*)xds;
+    a.wds = (const bf16*)wds;
+    a.bds = bds;
+    const size_t lds = (size_t)R28Ring<1>::kSlotsAlloc * kRB + (size_t)kMF * 16 * 128;
+    hipLaunchKernelGGL((conv3x3_rows28_kernel<false, 0, 1, 4, false, true>), dim3(B), dim3(256), lds, s, a);
+    DMLC_HIP_CHECK(hipGetLastError());
+    return;
+  }
   if (out_inv_scale > 0.f && (res || dbg)) throw std::invalid_argument("conv3x3_rows28: e4m3 output without residual only");
   if (!x || !wf || !bias || !y ||
       (((uintptr_t)x | (uintptr_t)wf | (uintptr_t)res | (uintptr_t)y) & 15))
     throw std::invalid_argument("conv3x3_rows28: null / misaligned operand");
   if (x == y || (res && res == y)) throw std::invalid_argument("conv3x3_rows28: in-place not supported");
-  R28Args a;
+  R28Args a{};
   a.x = (const bf16*)x;
   a.wf = (const bf16*)wf;
   a.bias = bias;

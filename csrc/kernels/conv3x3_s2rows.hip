@@ -64,12 +64,17 @@ constexpr int kSlotsAlloc = kRing + 2;
 constexpr int kRun = 4 * 2 * kW;      // 224 DMA chunks per K-half plane (slots 1..56)
 constexpr int kMF = kR * kW / 16;     // 7 pixel fragments per step
 constexpr int kKT = 18, kCT = 2;      // 3x3 / downsample K steps
-constexpr int kKS = kKT + kCT;
 constexpr int kOffKw1 = kE0 * 64;     // kw = 1 reads slot 29 + c
 
 __device__ __forceinline__ int swz_of(int y, int x) { return ((((y + 1) >> 1) * kW + ((x + 1) >> 1)) >> 1) & 3; }
 
+// DS: also the block's 1x1/s2 downsample (K = 64 more, the yd output). Off
+// (ds_into_conv2): the downsample is a K-extension of the block's conv2
+// (conv3x3_rows28_kernel DSX), so yd is neither written here nor read back
+// there: 51 of the 205 MB this kernel moved at B = 256, and 2 of its 20 K steps.
+template <bool DS>
 __global__ __launch_bounds__(256, 1) void conv3x3_s2rows_kernel(S2Args a) {
+  constexpr int kKS = kKT + (DS ? kCT : 0);
   extern __shared__ __attribute__((aligned(16))) uint4 smem[];
   char* ring = (char*)smem;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -112,7 +117,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3_s2rows_kernel(S2Args a) {
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     bs[e] = a.bias[ch0 + 8 * g + e];
-    bsd[e] = a.bd[ch0 + 8 * g + e];
+    bsd[e] = DS ? a.bd[ch0 + 8 * g + e] : 0.f;
   }
   for (int yy = 0; yy <= 7; ++yy) load_row(yy);
 
@@ -213,13 +218,13 @@ __global__ __launch_bounds__(256, 1) void conv3x3_s2rows_kernel(S2Args a) {
         }
       if (!(a.dbg & 2)) {
         *(uint4*)(a.y + o) = pack8_relu(v, a.relu);
-        *(uint4*)(a.yd + o) = pack8(vd);
+        if constexpr (DS) *(uint4*)(a.yd + o) = pack8(vd);
       }
     }
-    // the next step's rows have landed (the 2 kMF stores just issued may
+    // the next step's rows have landed (the (2) kMF stores just issued may
     // still be in flight: vmcnt retires in order) and every wave is done
     // reading the rows they replace
-    vm_wait<2 * kMF>();
+    vm_wait<(DS ? 2 : 1) * kMF>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
   };
@@ -236,7 +241,9 @@ bool conv3x3_s2rows_supported(int Hin, int Win, int Cin, int Cout) {
 void conv3x3_s2rows(const void* x, const void* wf, const float* bias, const void* wdf, const float* bd, void* y,
                     void* yd, const void* zero, int B, bool relu, hipStream_t s, int dbg) {
   if (B <= 0) return;
-  if (!x || !wf || !bias || !wdf || !bd || !y || !yd || !zero ||
+  if ((wdf == nullptr) != (bd == nullptr) || (wdf == nullptr) != (yd == nullptr))
+    throw std::invalid_argument("conv3x3_s2rows: the downsample needs wdf, bd and yd together");
+  if (!x || !wf || !bias || !y || !zero ||
       (((uintptr_t)x | (uintptr_t)wf | (uintptr_t)wdf | (uintptr_t)y | (uintptr_t)yd | (uintptr_t)zero) & 15))
     throw std::invalid_argument("conv3x3_s2rows: null / misaligned operand");
   S2Args a;
@@ -250,7 +257,10 @@ void conv3x3_s2rows(const void* x, const void* wf, const float* bias, const void
   a.zero = (const bf16*)zero;
   a.relu = relu;
   a.dbg = dbg;
-  hipLaunchKernelGGL(conv3x3_s2rows_kernel, dim3(B), dim3(256), (size_t)kSlotsAlloc * kRB, s, a);
+  if (wdf)
+    hipLaunchKernelGGL(conv3x3_s2rows_kernel<true>, dim3(B), dim3(256), (size_t)kSlotsAlloc * kRB, s, a);
+  else
+    hipLaunchKernelGGL(conv3x3_s2rows_kernel<false>, dim3(B), dim3(256), (size_t)kSlotsAlloc * kRB, s, a);
   DMLC_HIP_CHECK(hipGetLastError());
 }
 

@@ -199,7 +199,8 @@ void bottleneck56_head(const void* x, const void* w1, const float* b1, const voi
 // downsample in one row-streaming, weight-stationary kernel
 // (conv3x3_s2rows.hip): one workgroup per image. wf / wdf: fragment-order
 // weights (stream_frag_index, K = 576 / 64); y = relu?(conv3x3 + bias),
-// yd = downsample + bd.
+// yd = downsample + bd; wdf = bd = yd = null: the conv alone (the downsample
+// then runs inside conv2: conv3x3_rows28's xds).
 bool conv3x3_s2rows_supported(int Hin, int Win, int Cin, int Cout);
 // ResNet50 layer2.0.conv2, 56x56x128 -> 28x28x128 / s2 (conv3x3_s2rows128.hip):
 // one weight-stationary workgroup per image; wf in fragment order; y bf16, or
@@ -213,8 +214,12 @@ void conv3x3_s2rows(const void* x, const void* wf, const float* bias, const void
 // (conv3x3_rows28.hip): one workgroup per image, the weights in registers.
 // wf: fragment-order weights (stream_frag_index, K = 1152); res optional.
 bool conv3x3_rows28_supported(int H, int W, int Cin, int Cout);
+// xds / wds / bds (ds_into_conv2): the block's 1x1/s2 downsample of xds [B, 56,
+// 56, 64] as 2 more K steps (wds fragment order [4][2][2][64][8], K = 64; bds
+// added to bias), instead of a residual read.
 void conv3x3_rows28(const void* x, const void* wf, const float* bias, const void* res, void* y, int B, bool relu,
-                    hipStream_t s, int dbg = 0, float out_inv_scale = 0.f);  // > 0: e4m3 y, no residual
+                    hipStream_t s, int dbg = 0, float out_inv_scale = 0.f, const void* xds = nullptr,
+                    const void* wds = nullptr, const float* bds = nullptr);  // > 0: e4m3 y, no residual
 // Query-batch 3x3/p1 conv (conv_small.hip) for B <= a few images: one launch
 // per conv, no split-K. x [B,H,W,CI] bf16 NHWC (CI in 64..512), wf: fragment-
 // order weights (stream_frag_index, K = 9 CI), y = relu?(conv + bias (+ res)).

@@ -476,7 +476,9 @@ __device__ __forceinline__ void vm_wait_dyn(int n) {
   }
 }
 
-// V (stem_conv_pool_set_dbg bits 24-29): timing knock-outs
+// V bit 1: the raw rows by 16-B LDS-DMA (one instruction per 672-B row
+// instead of three 4-B ones; the u8 images must be 16-B aligned, which the
+// launcher checks). V (stem_conv_pool_set_dbg bits 24-29): timing knock-outs
 // (tools/stem_roles_ab.py, profiles/r4_stem_roles.txt): 4 no u8 conversion, 8
 // no conv rows, 16 no horizontal-pool epilogue, 32 no raw-row DMA / vertical
 // max / stores (results wrong: timing only)
@@ -508,8 +510,13 @@ __global__ __launch_bounds__(512, 1) void stem_roles_kernel(StemArgs a) {
       if (iy < 0 || iy >= G::S) continue;
       const uint8_t* src = uimg + (long)iy * UB;
       char* dst = u8ring + (r % kRolesRawRing) * UBS + kU8Front;
-      for (int c0 = 0; c0 < UB / 4; c0 += 64)
-        if (c0 + lane < UB / 4) dma4(src + (c0 + lane) * 4, dst + c0 * 4);
+      if constexpr (V & 1) {
+        static_assert(UB % 16 == 0 && UB / 16 <= 64 && UBS % 16 == 0 && kU8Front % 16 == 0, "16-B raw rows");
+        if (lane < UB / 16) dma16(src + lane * 16, dst);
+      } else {
+        for (int c0 = 0; c0 < UB / 4; c0 += 64)
+          if (c0 + lane < UB / 4) dma4(src + (c0 + lane) * 4, dst + c0 * 4);
+      }
     }
   };
   // raw rows [lo, lo+cnt) -> paired bf16 rows (stem_conv_pool_kernel's
@@ -620,7 +627,7 @@ __global__ __launch_bounds__(512, 1) void stem_roles_kernel(StemArgs a) {
       // DMA the raw rows step t+2's conversion reads: this wave's rows
       // 8t+21+hw and 8t+25+hw, DPR instructions each (rows outside the image
       // are not loaded)
-      constexpr int DPR = (UB / 4 + 63) / 64;
+      constexpr int DPR = (V & 1) ? 1 : (UB / 4 + 63) / 64;
       int nwait = 0;
       if (t + 2 < T && !(V & 32)) {
         load_rows(8 * t + 21, 8);
@@ -746,6 +753,7 @@ void stem_launch(const void* x, const uint8_t* u8, const void* w, const float* b
   case V: hipLaunchKernelGGL((stem_roles_kernel<7, V>), dim3(B), dim3(512), lds_roles, s, a); break;
         DMLC_STEM_RV_CASE(4)
         DMLC_STEM_RV_CASE(8)
+        DMLC_STEM_RV_CASE(9)
         DMLC_STEM_RV_CASE(16)
         DMLC_STEM_RV_CASE(36)
         DMLC_STEM_RV_CASE(52)
@@ -756,9 +764,12 @@ void stem_launch(const void* x, const uint8_t* u8, const void* w, const float* b
       DMLC_HIP_CHECK(hipGetLastError());
       return;
     }
-    switch (NF) {
+    // 16-B raw-row DMA when the images allow it (g_stem_dbg 2048: force the 4-B form)
+    const bool d16 = !((uintptr_t)u8 & 15) && !(g_stem_dbg & 2048);
+    switch (NF * 2 + (d16 ? 1 : 0)) {
 #define DMLC_STEM_ROLES_CASE(F) \
-  case F: hipLaunchKernelGGL((stem_roles_kernel<F>), dim3(B), dim3(512), lds_roles, s, a); break;
+  case 2 * F: hipLaunchKernelGGL((stem_roles_kernel<F>), dim3(B), dim3(512), lds_roles, s, a); break; \
+  case 2 * F + 1: hipLaunchKernelGGL((stem_roles_kernel<F, 1>), dim3(B), dim3(512), lds_roles, s, a); break;
       DMLC_STEM_ROLES_CASE(4)
       DMLC_STEM_ROLES_CASE(5)
       DMLC_STEM_ROLES_CASE(6)

@@ -78,7 +78,7 @@ bool EngineOptions::set(const std::string& name, bool v) {
       {"fused_preprocess", &EngineOptions::fused_preprocess}, {"row_conv", &EngineOptions::row_conv},
       {"rows_wreg", &EngineOptions::rows_wreg},     {"fused_block", &EngineOptions::fused_block},
       {"fused_bottleneck", &EngineOptions::fused_bottleneck},
-      {"ds_into_expand", &EngineOptions::ds_into_expand},
+      {"ds_into_expand", &EngineOptions::ds_into_expand}, {"ds_into_conv2", &EngineOptions::ds_into_conv2},
       {"stream_conv", &EngineOptions::stream_conv}, {"stream_wreg", &EngineOptions::stream_wreg},
       {"stream_l4s2", &EngineOptions::stream_l4s2}, {"fuse_ds", &EngineOptions::fuse_ds},
       {"bigtile", &EngineOptions::bigtile},         {"fused_pool", &EngineOptions::fused_pool},
@@ -1005,6 +1005,24 @@ int Engine::ds_expand_op(size_t oi) const {
 // the 56x56x64 -> 128 shape: conv3x3_s2rows runs one workgroup per image
 // (59 us at B=256 vs 72 us for the stream conv's 4 rounds of strips,
 // profiles/r2_s2rows.txt); like the fused block only with rounds >= ~70% full.
+// ops[oi] = layer2.0.conv1 on conv3x3_s2rows (its downsample = ops[oi - 1]);
+// the block's conv2 (ops[oi + 1], on conv3x3_rows28) can compute that
+// downsample as 2 more K steps when it is the downsample output's only reader.
+bool Engine::ds_conv2_ok(size_t oi, int B) const {
+  if (!opt_.ds_into_conv2 || oi < 1 || oi + 1 >= ops_.size()) return false;
+  const Op& d = ops_[oi - 1];
+  const Op& c2 = ops_[oi + 1];
+  if (c2.type != OpType::Conv || c2.res != d.out || c2.in != ops_[oi].out) return false;
+  const ConvLayer& L2 = convs_[c2.conv];
+  const ConvLayer& D = convs_[d.conv];
+  if (!L2.wf_off || !D.wf_off || L2.fp8 || shapes_[c2.out].fp8 || conv_path(c2, B) != ConvPath::Rows28) return false;
+  const ActShape& xs = shapes_[d.in];
+  if (xs.H != 56 || xs.W != 56 || xs.C != 64 || xs.fp8 || xs.f32 || L2.cout != 128 || D.cout != 128) return false;
+  for (size_t j = 0; j < ops_.size(); ++j)
+    if (j != oi + 1 && (ops_[j].in == d.out || ops_[j].res == d.out)) return false;
+  return true;
+}
+
 bool Engine::s2rows_ok(const Op& op, const ConvLayer& D, int B) const {
   const ConvLayer& L = convs_[op.conv];
   const ActShape& is = shapes_[op.in];
@@ -1028,6 +1046,7 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
   std::map<int, hipEvent_t> joined;  // activation -> event its side-stream producer recorded
   int skip = 0;                      // ops already done by a fused kernel
   int skip_ds = -1;                  // downsample op left to the next (stream) conv
+  int ds_conv2 = -1;                 // downsample op left to the block's conv2 (ds_into_conv2)
   bool pooled = false;               // the last conv wrote pooled_ (fused avgpool)
   for (size_t oi = 0; oi < ops_.size(); ++oi) {
     const Op& op = ops_[oi];
@@ -1158,8 +1177,14 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
             const bool fpool = cs == s && pool_fusable(oi, B);
             if (D && s2rows_ok(op, *D, B)) {
               const uint8_t* wa = (const uint8_t*)warena_;
-              conv3x3_s2rows(acts_[op.in], wa + L.wf_off, (const float*)(wa + L.b_off), wa + D->wf_off,
-                             (const float*)(wa + D->b_off), acts_[op.out], acts_[yd], zero_, B, L.relu, cs);
+              if (ds_conv2_ok(oi, B)) {  // the downsample runs inside conv2
+                conv3x3_s2rows(acts_[op.in], wa + L.wf_off, (const float*)(wa + L.b_off), nullptr, nullptr,
+                               acts_[op.out], nullptr, zero_, B, L.relu, cs);
+                ds_conv2 = skip_ds;
+              } else {
+                conv3x3_s2rows(acts_[op.in], wa + L.wf_off, (const float*)(wa + L.b_off), wa + D->wf_off,
+                               (const float*)(wa + D->b_off), acts_[op.out], acts_[yd], zero_, B, L.relu, cs);
+              }
               skip_ds = -1;
               break;
             }
@@ -1244,6 +1269,15 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
             break;
           }
           case ConvPath::Rows28:
+            if (ds_conv2 >= 0 && op.res == ops_[ds_conv2].out) {
+              const ConvLayer& D = convs_[ops_[ds_conv2].conv];
+              const uint8_t* wa = (const uint8_t*)warena_;
+              conv3x3_rows28(acts_[op.in], wa + L.wf_off, (const float*)(wa + L.b_off), nullptr, acts_[op.out], B,
+                             L.relu, cs, 0, 0.f, acts_[ops_[ds_conv2].in], wa + D.wf_off,
+                             (const float*)(wa + D.b_off));
+              ds_conv2 = -1;
+              break;
+            }
             conv3x3_rows28(acts_[op.in], (const uint8_t*)warena_ + L.wf_off,
                            (const float*)((const uint8_t*)warena_ + L.b_off), op.res >= 0 ? acts_[op.res] : nullptr,
                            acts_[op.out], B, L.relu, cs, 0, shapes_[op.out].fp8 ? 1.f / shapes_[op.out].scale : 0.f);

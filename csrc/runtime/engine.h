@@ -100,6 +100,10 @@ struct EngineOptions {
   // (it keeps t2 internal)
   bool fused_bottleneck_img = false;
   bool ds_into_expand = true;    // ResNet50 layer1.0: the 1x1 downsample computed inside conv3 (one K-concat GEMM)
+  // ResNet18 layer2.0: the 1x1/s2 downsample as 2 more K steps of conv2
+  // (conv3x3_rows28 DSX) instead of an output of conv3x3_s2rows that conv2
+  // reads back as its residual (51 MB written + 51 MB read at B = 256)
+  bool ds_into_conv2 = true;
   bool stream_conv = true;       // direct 3x3 convs with the input resident in LDS (conv3x3_stream.hip)
   bool stream_wreg = true;       // ... with register-streamed weights where available
   bool stream_l4s2 = true;       // ... also for 14x14x256 -> 512 / s2 (register weights only)
@@ -218,6 +222,7 @@ class Engine {
   bool bottleneck_conv3(const ConvLayer& L) const;  // L is such a block's expand conv (fragment-order weights)
   int ds_expand_op(size_t oi) const;  // ops[oi] = a downsample folded into a later expand conv: that op, or -1
   bool s2rows_ok(const Op& op, const ConvLayer& D, int B) const;  // layer2.0 conv1 + downsample -> conv3x3_s2rows
+  bool ds_conv2_ok(size_t oi, int B) const;  // ... and that downsample as K steps of conv2 (ds_into_conv2)
 
   std::string arch_;
   int device_ = 0;

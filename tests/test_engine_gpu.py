@@ -369,13 +369,15 @@ def test_fused_block_matches_unfused(gpu):
     assert torch.equal(fl, rl) and torch.equal(fi, ri)
 
 
-@pytest.mark.parametrize("option", ["s2rows", "rows28"])
+@pytest.mark.parametrize("option", ["s2rows", "rows28", "ds_into_conv2"])
 def test_weight_stationary_rows_match_stream(gpu, option):
     """ResNet18's layer2 convs as weight-stationary row-streaming kernels
     (s2rows: layer2.0 conv1 + downsample, conv3x3_s2rows.hip; rows28: the
-    stride-1 convs, conv3x3_rows28.hip) vs the stream conv (the option off):
-    different accumulation order, so logits agree to bf16 rounding, not bit
-    for bit."""
+    stride-1 convs, conv3x3_rows28.hip; ds_into_conv2: layer2.0's downsample
+    as 2 more K steps of its conv2 instead of an s2rows output read back as
+    the residual) vs the path with the option off: different accumulation
+    order (and no bf16 rounding of the downsample output), so logits agree to
+    bf16 rounding, not bit for bit."""
     model = build("resnet18", seed=45, randomize_bn=True)
     sd = state_dict_f32(model)
     g = torch.Generator().manual_seed(46)

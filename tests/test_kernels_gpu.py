@@ -257,12 +257,15 @@ def test_stem_conv_pool_u8(gpu, B, S, strip):
     one = ops.stem_conv_pool_u8(img, wp, bias, strip)
     C.stem_conv_pool_set_dbg(512)  # one workgroup per image, MFMA / helper waves: same arithmetic
     try:
-        roles = ops.stem_conv_pool_u8(img, wp, bias, strip)
+        roles = ops.stem_conv_pool_u8(img, wp, bias, strip)  # raw rows by 16-B LDS-DMA (aligned images)
+        C.stem_conv_pool_set_dbg(512 | 2048)  # ... by 4-B LDS-DMA
+        roles4 = ops.stem_conv_pool_u8(img, wp, bias, strip)
     finally:
         C.stem_conv_pool_set_dbg(0)
     torch.cuda.synchronize()
     assert torch.equal(one, two)
     assert torch.equal(roles, two)
+    assert torch.equal(roles4, two)
 
 
 @pytest.mark.parametrize("HW,C,B,res,relu", [(28, 128, 1, False, True), (28, 128, 3, True, True),

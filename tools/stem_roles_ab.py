@@ -20,9 +20,10 @@ from dmlc import ops  # noqa: E402
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from conv_bench import time_us, warm_gpu  # noqa: E402
 
-NAMES = {0: "default", 4: "KO u8 conversion", 8: "KO conv rows", 16: "KO h-pool epilogue",
-         36: "MFMA + h-pool only", 52: "MFMA only", 40: "conversion only"}
-KNOCKOUTS = {4, 8, 16, 36, 52, 40}
+NAMES = {0: "default", 4: "KO u8 conversion", 8: "KO conv rows", 9: "KO conv rows, 16-B raw DMA",
+         16: "KO h-pool epilogue", 36: "MFMA + h-pool only", 52: "MFMA only", 40: "conversion only",
+         -1: "4-B raw-row DMA (round 4)"}
+KNOCKOUTS = {4, 8, 9, 16, 36, 52, 40}
 
 
 def main():
@@ -43,7 +44,7 @@ def main():
     vs = [int(t) for t in args.variants.split(",")]
 
     def run(v):
-        C.stem_conv_pool_set_dbg(v << 24)
+        C.stem_conv_pool_set_dbg(2048 if v == -1 else v << 24)
         try:
             return ops.stem_conv_pool_u8(img, wp, bias, 56)
         finally:
