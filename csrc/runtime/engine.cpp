@@ -79,6 +79,7 @@ bool EngineOptions::set(const std::string& name, bool v) {
       {"rows_wreg", &EngineOptions::rows_wreg},     {"fused_block", &EngineOptions::fused_block},
       {"fused_bottleneck", &EngineOptions::fused_bottleneck},
       {"ds_into_expand", &EngineOptions::ds_into_expand}, {"ds_into_conv2", &EngineOptions::ds_into_conv2},
+      {"fp8_3x3_in", &EngineOptions::fp8_3x3_in},
       {"stream_conv", &EngineOptions::stream_conv}, {"stream_wreg", &EngineOptions::stream_wreg},
       {"stream_l4s2", &EngineOptions::stream_l4s2}, {"fuse_ds", &EngineOptions::fuse_ds},
       {"bigtile", &EngineOptions::bigtile},         {"fused_pool", &EngineOptions::fused_pool},
@@ -392,6 +393,31 @@ void Engine::mark_fp8() {
         chan_act_[op.out] = true;
       }
     }
+    if (opt_.fp8_3x3_in) {
+      // ... and their e4m3 input t1 where the e4m3 3x3 kernel runs the conv:
+      // t1 is written by a 1x1 conv and read by nothing else
+      for (const Op& op : ops_) {
+        if (op.type != OpType::Conv) continue;
+        const ConvLayer& L = convs_[op.conv];
+        const ActShape& is = shapes_[op.in];
+        if (L.fc || L.kh != 3 || L.kw != 3 || L.pad != 1 || L.stride != 1 || op.res >= 0 || !chan_act_[op.out] ||
+            is.fp8 || is.f32 || !conv3x3_stream8_supported(is.H, is.W, is.C, L.cout))
+          continue;
+        int producers = 0, readers = 0;
+        bool from_1x1 = false;
+        for (const Op& o : ops_) {
+          if (o.type == OpType::Conv && o.out == op.in) {
+            ++producers;
+            const ConvLayer& P = convs_[o.conv];
+            from_1x1 = !P.fc && P.kh == 1 && P.kw == 1 && P.stride == 1 && o.res < 0;
+          }
+          if (o.in == op.in || o.res == op.in) ++readers;
+        }
+        if (producers != 1 || !from_1x1 || readers != 1) continue;
+        shapes_[op.in].fp8 = true;
+        chan_act_[op.in] = true;
+      }
+    }
   }
   for (const Op& op : ops_) {
     if (op.type != OpType::Conv) continue;
@@ -491,6 +517,12 @@ void Engine::pack_weights(const WeightMap& w) {
         conv5x5_27_supported(shapes_[L.in_act].H, shapes_[L.in_act].W, shapes_[L.in_act].C, L.cout, L.pad)) {
       L.wf_off = off;  // fragment-order copy for conv5x5_27.hip
       off = align_up(off + (size_t)L.cout * L.kpad * 2, 256);
+    }
+    if (L.fp8 && !L.fc && L.in_act >= 0 && L.kh == 3 && L.kw == 3 && L.stride == 1 && L.pad == 1 &&
+        L.kpad == 9 * L.cin && conv3x3_stream8_supported(shapes_[L.in_act].H, shapes_[L.in_act].W,
+                                                         shapes_[L.in_act].C, L.cout)) {
+      L.wf_off = off;  // e4m3 fragment-order copy for conv3x3_stream8.hip
+      off = align_up(off + (size_t)L.cout * L.kpad, 256);
     }
     if (bottleneck_conv3(L)) {  // fragment-order copy for bottleneck56.hip's expand conv
       L.wf_off = off;
@@ -624,6 +656,20 @@ void Engine::pack_weights(const WeightMap& w) {
         const float sw = amax > 0.f ? amax / 448.f : 1.f;
         for (int k = 0; k < L.kpad; ++k) q[(size_t)n * L.kpad + k] = f2e4m3_host(wv(n, k) / sw);
         alpha[n] = s_in * sw;
+      }
+      if (L.wf_off) {  // conv3x3_stream8's fragment order of the e4m3 weights
+        uint8_t* pf = host.data() + L.wf_off;
+        const int KT = L.kpad / 128;
+        for (int j = 0; j < L.cout / 32; ++j)
+          for (int t = 0; t < KT; ++t)
+            for (int nf = 0; nf < 2; ++nf)
+              for (int h = 0; h < 2; ++h)
+                for (int ln = 0; ln < 64; ++ln) {
+                  const int fq = ln >> 4, r = 16 * nf + (ln & 15);
+                  const int n = 32 * j + 8 * ((r & 15) >> 2) + 4 * (r >> 4) + (r & 3);  // perm32
+                  const int k0 = 128 * t + 32 * fq + 16 * (h ^ (fq & 1));
+                  std::memcpy(pf + conv3x3_stream8_frag_offset(j, t, nf, h, ln, KT), q + (size_t)n * L.kpad + k0, 16);
+                }
       }
     }
   }
@@ -783,6 +829,11 @@ Engine::ConvPath Engine::conv_path(const Op& op, int B) const {
     return ConvPath::Rows28;
   if (opt_.direct13 && k3 && L.stride == 1 && L.wf_off && conv3x3_13_supported(is.H, is.W, is.C, L.cout))
     return ConvPath::Direct13;
+  // e4m3 in and out (fp8_3x3_in): whole images per workgroup, once the batch
+  // fills the CUs (query batches: the e4m3 implicit GEMM)
+  if (L.fp8 && !L.fc && L.kh == 3 && L.kw == 3 && L.stride == 1 && L.pad == 1 && L.wf_off && op.res < 0 &&
+      shapes_[op.out].fp8 && 4 * B >= num_cus_ && conv3x3_stream8_supported(is.H, is.W, is.C, L.cout))
+    return ConvPath::Stream8;
   if (opt_.direct27 && !L.fc && !L.fp8 && L.kh == 5 && L.kw == 5 && L.stride == 1 && L.relu && L.wf_off &&
       L.kpad == 1600 && !shapes_[op.out].f32 && conv5x5_27_supported(is.H, is.W, is.C, L.cout, L.pad))
     return ConvPath::Direct27;
@@ -1266,6 +1317,12 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
                        D ? wa + D->wf_off : nullptr, D ? (const float*)(wa + D->b_off) : nullptr,
                        D ? acts_[yd] : nullptr);
             skip_ds = -1;
+            break;
+          }
+          case ConvPath::Stream8: {
+            const uint8_t* wa = (const uint8_t*)warena_;
+            conv3x3_stream8(acts_[op.in], wa + L.wf_off, (const float*)(wa + L.a_off), (const float*)(wa + L.b_off),
+                            acts_[op.out], zero_, B, is.H, is.W, is.C, L.cout, L.relu, 1.f / shapes_[op.out].scale, cs);
             break;
           }
           case ConvPath::Rows28:

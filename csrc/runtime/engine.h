@@ -139,6 +139,10 @@ struct EngineOptions {
   // ... and the strided 3x3 convs of layer3.0 / layer4.0 (implicit GEMM with
   // an e4m3 epilogue instead of the bf16 big-tile kernel)
   bool fp8_3x3_out_s2 = false;
+  // ResNet50 e4m3: the stride-1 bottleneck 3x3 convs of layer3 / layer4 also
+  // READ e4m3 (t1 written by the reduce 1x1 with per-channel scales) and run
+  // on the e4m3 MFMA (conv3x3_stream8.hip: 2x the bf16 rate); needs fp8_3x3_out
+  bool fp8_3x3_in = true;
 
   // Set a field by name; false if there is no such option.
   bool set(const std::string& name, bool value);
@@ -209,7 +213,7 @@ class Engine {
   void run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* idx, float* prob,
                float* logits, hipStream_t s, std::vector<hipEvent_t>* evs, bool trace);
   ConvArgs conv_args(const Op& op, int B, float* logits) const;
-  enum class ConvPath { Stream, Rows, Rows28, Direct13, Direct27, OneByOne, BigTile, Igemm, Small };
+  enum class ConvPath { Stream, Rows, Rows28, Direct13, Direct27, OneByOne, BigTile, Igemm, Small, Stream8 };
   ConvPath conv_path(const Op& op, int B) const;
   bool side_safe(int B) const;
   bool head_fusable(size_t oi) const;

@@ -405,6 +405,50 @@ def conv2d_fp8(x: torch.Tensor, w_q: torch.Tensor, alpha: torch.Tensor, cout: in
     return y
 
 
+def stream8_weight_frag(w_q: torch.Tensor, cout: int) -> torch.Tensor:
+    """e4m3 packed conv weights [Npad, K] (pack_conv_weight_fp8) -> the e4m3
+    3x3 conv's fragment order (conv3x3_stream8.hip): [Cout/32][K/128][2 nf][2
+    h][64 lanes][16 B], lane l of (group g, K-tile t, nf, h) holding
+    W[32g + perm32(16nf + (l & 15))][128t + 32fq + 16(h ^ (fq & 1)) + 0..15],
+    fq = l >> 4 (the odd-fq half swap matches the kernel's X reads)."""
+    w = w_q[:cout].view(torch.uint8)
+    K = w.shape[1]
+    n = torch.arange(32)
+    perm = 8 * ((n & 15) >> 2) + 4 * (n >> 4) + (n & 3)
+    lane = torch.arange(64)
+    fq = lane >> 4
+    G, T = cout // 32, K // 128
+    g = torch.arange(G).view(G, 1, 1, 1, 1, 1)
+    t = torch.arange(T).view(1, T, 1, 1, 1, 1)
+    nf = torch.arange(2).view(1, 1, 2, 1, 1, 1)
+    h = torch.arange(2).view(1, 1, 1, 2, 1, 1)
+    ln = lane.view(1, 1, 1, 1, 64, 1)
+    e = torch.arange(16).view(1, 1, 1, 1, 1, 16)
+    row = 32 * g + perm[16 * nf + (ln & 15)]
+    col = 128 * t + 32 * (ln >> 4) + 16 * (h ^ ((ln >> 4) & 1)) + e
+    del fq
+    row, col = torch.broadcast_tensors(row, col)
+    return w[row.to(w.device), col.to(w.device)].contiguous()
+
+
+def conv3x3_stream8(x: torch.Tensor, w_q: torch.Tensor, alpha: torch.Tensor, bias: torch.Tensor, relu: bool = True,
+                    out_scale: float = 1.0, frag: torch.Tensor | None = None) -> torch.Tensor:
+    """e4m3 3x3/s1/p1 conv (conv3x3_stream8.hip) on e4m3 NHWC [B,14,14,256] or
+    [B,7,7,512]: e4m3(relu?(acc * alpha + bias) / out_scale) with acc = conv
+    of the e4m3 values. w_q / alpha: pack_conv_weight_fp8 (alpha = s_x * s_w)."""
+    _need_cuda(x, w_q, alpha, bias)
+    C = native()
+    B, H, W, Cin = x.shape
+    cout = Cin
+    if x.dtype != FP8 or not C.conv3x3_stream8_supported(H, W, Cin, cout) or w_q.shape[1] != 9 * Cin:
+        raise ValueError("conv3x3_stream8: unsupported shape / dtype")
+    wf = stream8_weight_frag(w_q, cout) if frag is None else frag
+    y = torch.empty(B, H, W, cout, dtype=FP8, device=x.device)
+    C.conv3x3_stream8(_ptr(x.contiguous()), _ptr(wf), _ptr(alpha.float().contiguous()), _ptr(bias.float().contiguous()),
+                      _ptr(y), _ptr(_zero_page(x.device)), B, H, W, Cin, cout, relu, 1.0 / out_scale, _stream())
+    return y
+
+
 def maxpool2d(x: torch.Tensor, k: int = 3, stride: int = 2, pad: int = 1) -> torch.Tensor:
     _need_cuda(x)
     C = native()

@@ -581,3 +581,53 @@ def test_resnet50_fp8_fused_bottleneck_img_matches_unfused(gpu):
         sep = rprof[blk + ".conv1"] + rprof[blk + ".conv2"] + rprof[blk + ".conv3"]
         print(blk, "fused", fused, "separate", sep)
         assert prof[blk + ".conv3"] < 0.6 * rprof[blk + ".conv3"], (blk, prof, rprof)
+
+
+def test_resnet50_fp8_bench_config_b256_matches_fp32(gpu):
+    """The exact resnet50_fp8 bench configuration — B = 256, default options
+    (layers 2-4 on e4m3; e4m3 3x3 inputs on conv3x3_stream8 for layers 3-4 and
+    e4m3 3x3 outputs), graph-replayed — against fp32 torch.nn on the first 16
+    images: logits within 6% relative L2 and top-1 identical except on
+    near-ties."""
+    model = build("resnet50", seed=11, randomize_bn=True)
+    sd = state_dict_f32(model)
+    eng = InferenceEngine("resnet50_fp8", sd, max_batch=256)
+    g = torch.Generator().manual_seed(91)
+    img = torch.randint(0, 256, (256, 224, 224, 3), generator=g, dtype=torch.uint8)
+    idx, prob, logits = eng.predict(img.to(gpu), return_logits=True, use_graph=True)
+    i2, p2 = eng.predict(img.to(gpu), use_graph=True)  # the bench's graph (no logits output)
+    torch.cuda.synchronize()
+    assert torch.equal(i2, idx)
+    ref = _ref_logits(model, img[:16])
+    lg = logits[:16].cpu()
+    rel = ((lg - ref).norm() / ref.norm()).item()
+    cos = torch.nn.functional.cosine_similarity(lg, ref, dim=-1).min().item()
+    print(f"resnet50_fp8 bench config b256 vs fp32 (16 images): rel {rel:.4f} min-cos {cos:.4f}")
+    assert rel < 0.06 and cos > 0.99, (rel, cos)
+    top2 = torch.softmax(ref, -1).topk(2, -1).values
+    near_tie = (top2[:, 0] - top2[:, 1]) < 5e-2
+    mism = idx[:16].cpu().long() != ref.argmax(-1)
+    assert torch.all(~mism | near_tie), mism.sum().item()
+
+
+@pytest.mark.parametrize("B", [64, 256])
+def test_resnet50_fp8_3x3_in_matches_bf16_in(gpu, B):
+    """fp8_3x3_in: layer3/4's stride-1 bottleneck 3x3 convs read e4m3 t1
+    (per-channel scales, written by the reduce 1x1) on conv3x3_stream8 vs the
+    same engine with those convs on bf16 inputs (conv3x3_stream): one more
+    e4m3 rounding per block, so the logits differ by a few percent and top-1
+    agrees except on near-ties."""
+    model = build("resnet50", seed=15, randomize_bn=True)
+    sd = state_dict_f32(model)
+    eng = InferenceEngine("resnet50_fp8", sd, max_batch=B)
+    base = InferenceEngine("resnet50_fp8", sd, max_batch=B, options={"fp8_3x3_in": False})
+    g = torch.Generator().manual_seed(93 + B)
+    img = torch.randint(0, 256, (B, 224, 224, 3), generator=g, dtype=torch.uint8).to(gpu)
+    i, _, lg = eng.predict(img, return_logits=True)
+    ri, _, rl = base.predict(img, return_logits=True)
+    torch.cuda.synchronize()
+    rel = ((lg - rl).norm() / rl.norm()).item()
+    print(f"fp8_3x3_in B={B}: rel {rel:.4f} vs bf16 3x3 inputs")
+    assert rel < 0.05, rel
+    top2 = torch.softmax(rl.float(), -1).topk(2, -1).values
+    assert torch.all((i == ri) | ((top2[:, 0] - top2[:, 1]) < 5e-2))

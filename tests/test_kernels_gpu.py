@@ -666,3 +666,32 @@ def test_softmax_top1(gpu):
     torch.cuda.synchronize()
     assert torch.equal(idx.cpu().long(), pi)
     assert torch.allclose(prob.cpu(), pv, rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("B,H,C", [(3, 14, 256), (2, 7, 512), (3, 7, 512), (40, 14, 256)])
+def test_conv3x3_stream8(gpu, B, H, C):
+    """The e4m3 3x3/s1 conv (conv3x3_stream8.hip, block-scaled e4m3 MFMA) vs
+    fp32 torch on the same e4m3 operands (dequantised): the only difference is
+    the output's e4m3 rounding (3 mantissa bits, <= 1/16 relative), so the
+    dequantised output is within 0.04 relative L2 and no element is more than
+    one e4m3 step off the exactly rounded fp32 result. Odd batches leave the
+    7x7 kernel's last workgroup one image short."""
+    g = torch.Generator().manual_seed(100 + B + C)
+    x = torch.randn(B, H, H, C, generator=g).clamp_min(0)  # post-ReLU t1
+    sx = x.abs().max().item() / ops.FP8_MAX
+    xq = ops.quantize_fp8(x, sx)
+    w = torch.randn(C, C, 3, 3, generator=g) / (9 * C) ** 0.5
+    wq, sw = ops.pack_conv_weight_fp8(w)
+    bias = torch.randn(C, generator=g) * 0.05
+    alpha = sx * sw
+    wd = (wq.float()[:C, :9 * C] * sw[:C, None]).view(C, 3, 3, C).permute(0, 3, 1, 2)
+    ref = F.relu(F.conv2d(xq.float().permute(0, 3, 1, 2) * sx, wd, bias, padding=1)).permute(0, 2, 3, 1)
+    out_scale = ref.abs().max().item() / ops.FP8_MAX
+    y = ops.conv3x3_stream8(xq.to(gpu), wq.to(gpu), alpha.to(gpu), bias.to(gpu), relu=True, out_scale=out_scale)
+    torch.cuda.synchronize()
+    got = y.float().cpu() * out_scale
+    assert _rel(got, ref) < 0.04, _rel(got, ref)
+    exact = ops.quantize_fp8(ref, out_scale).float() * out_scale
+    # one e4m3 step at most (accumulation order moves values across a rounding boundary)
+    step = (exact.abs() / 8).clamp_min(out_scale * 2 ** -9)
+    assert ((got - exact).abs() <= step * 1.01).float().mean().item() == 1.0

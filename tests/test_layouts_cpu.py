@@ -446,3 +446,59 @@ def test_conv_small_lds_addressing(H, CI, S, mf):
                 if real:
                     worst = max(worst, _b128_ways([a if a >= 0 else real[0] for a in addr]))
     assert worst <= 4, worst
+
+
+@pytest.mark.parametrize("H,CI,IMG", [(14, 256, 1), (7, 512, 2)])
+def test_stream8_lds_layout(H, CI, IMG):
+    """conv3x3_stream8.hip (e4m3 3x3): the staged image (logical chunk pair m
+    of staged pixel q at physical pair m ^ (q & 7)) read back through the
+    kernel's per-lane offsets reproduces every lane's 32 input channels in the
+    weight packing's order (odd fq: second 16 first), and both 16-B reads of
+    every X fragment are bank-conflict free for every tap and K-tile."""
+    W, CPX = H, CI // 16
+    npx = IMG * H * W
+    torch.manual_seed(0)
+    img = torch.randint(0, 256, (npx, CI), dtype=torch.uint8)
+    lds = torch.zeros(npx * CI + CI, dtype=torch.uint8)  # + the zero pixel
+    for q in range(npx):  # staging: physical chunk pc holds logical ((pc>>1) ^ (q&7)) << 1 | (pc&1)
+        for pc in range(CPX):
+            lc = (((pc >> 1) ^ (q & 7)) << 1) | (pc & 1)
+            lds[q * CI + 16 * pc: q * CI + 16 * pc + 16] = img[q, 16 * lc: 16 * lc + 16]
+    ZB = npx * CI
+    nfrag = (npx + 15) // 16
+    for tap in range(9):
+        kh, kw = divmod(tap, 3)
+        ktap = (kh - 1) * W + (kw - 1)
+        for cc in range(CI // 128):
+            for f in range(nfrag):
+                a0, a1, want = [], [], []
+                for lane in range(64):
+                    fr, fq = lane & 15, lane >> 4
+                    p = min(16 * f + fr, npx - 1)
+                    ii, pi = divmod(p, H * W)
+                    r, c = divmod(pi, W)
+                    inside = 0 <= r + kh - 1 < H and 0 <= c + kw - 1 < W
+                    xa = ((ii * H + r) * W + c) * CI + ktap * CI if inside else ZB
+                    u = fq ^ ((fr + ktap) & 7)
+                    tsw0 = (u << 5) | ((fq & 1) << 4)
+                    a0.append(xa + (tsw0 ^ (cc << 7)))
+                    a1.append(xa + ((tsw0 ^ 16) ^ (cc << 7)))
+                    got = torch.cat([lds[a0[-1]:a0[-1] + 16], lds[a1[-1]:a1[-1] + 16]])
+                    if inside and 16 * f + fr < npx:
+                        q = p + ktap
+                        ch = 128 * cc + 32 * fq
+                        exp = img[q, ch:ch + 32]
+                        if fq & 1:
+                            exp = torch.cat([exp[16:], exp[:16]])
+                        assert torch.equal(got, exp), (tap, cc, f, lane)
+                    elif not inside:
+                        assert not got.any()
+                # conflicts: only among in-image lanes (border lanes all read the zero pixel)
+                live = [l for l in range(64) if a0[l] < ZB]
+                for addr in (a0, a1):
+                    for grp in _B128_GROUPS:
+                        slots = {}
+                        for l in grp:
+                            if l in live:
+                                slots.setdefault((addr[l] // 16) % 16, set()).add(addr[l])
+                        assert all(len(v) == 1 for v in slots.values()), (tap, cc, f)
