@@ -68,8 +68,8 @@ def test_engine_resnet50_fp8(gpu):
     """ResNet50 with layers 2-4 on the block-scaled e4m3 MFMA (per-channel
     weight scales, per-tensor activation scales calibrated at load) vs the
     fp32 reference: e4m3 keeps 3 mantissa bits, so the bar is looser than the
-    bf16 engine's: logits within 15% (relative L2) and top-1 agreement on
-    all but near-ties."""
+    bf16 engine's: logits within 7% (relative L2; 4.8% measured, round 5) and
+    top-1 agreement on all but near-ties."""
     model = build("resnet50", seed=11, randomize_bn=True)
     sd = state_dict_f32(model)
     eng = InferenceEngine("resnet50_fp8", sd, max_batch=16)
@@ -82,7 +82,7 @@ def test_engine_resnet50_fp8(gpu):
     cos = torch.nn.functional.cosine_similarity(logits.cpu(), ref, dim=-1).min().item()
     agree = (idx.cpu().long() == ref.argmax(-1)).float().mean().item()
     print(f"resnet50_fp8 vs fp32: rel {rel:.4f} min-cos {cos:.4f} top1 agree {agree:.3f}")
-    assert rel < 0.15 and cos > 0.98, (rel, cos)
+    assert rel < 0.07 and cos > 0.995, (rel, cos)
     ref_p = torch.softmax(ref, -1)
     top2 = ref_p.topk(2, -1).values
     near_tie = (top2[:, 0] - top2[:, 1]) < 5e-2
@@ -118,7 +118,7 @@ def test_resnet50_fp8_3x3_e4m3_out(gpu, B, s2):
     cos = torch.nn.functional.cosine_similarity(logits.cpu(), ref, dim=-1).min().item()
     agree = (idx.cpu().long() == ref.argmax(-1)).float().mean().item()
     print(f"resnet50_fp8 fp8_3x3_out B={B} s2={s2}: rel {rel:.4f} min-cos {cos:.4f} top1 agree {agree:.3f}")
-    assert rel < 0.15 and cos > 0.98, (rel, cos)
+    assert rel < 0.07 and cos > 0.995, (rel, cos)
     ref_p = torch.softmax(ref, -1)
     top2 = ref_p.topk(2, -1).values
     near_tie = (top2[:, 0] - top2[:, 1]) < 5e-2
