@@ -231,12 +231,13 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv3x3_stream8_frag_offset", &conv3x3_stream8_frag_offset);
   m.def("conv3x3_stream8_set_variant", &conv3x3_stream8_set_variant);
   m.def("conv3x3_stream8", [](uintptr_t x, uintptr_t wf, uintptr_t alpha, uintptr_t bias, uintptr_t y, uintptr_t zero,
-                              int B, int H, int W, int Cin, int Cout, bool relu, float out_inv_scale, uintptr_t stream) {
+                              int B, int H, int W, int Cin, int Cout, int stride, bool relu, float out_inv_scale,
+                              uintptr_t stream) {
     conv3x3_stream8(P<void>(x), P<void>(wf), P<float>(alpha), P<float>(bias), P<void>(y), P<void>(zero), B, H, W, Cin,
-                    Cout, relu, out_inv_scale, S(stream));
+                    Cout, stride, relu, out_inv_scale, S(stream));
   }, py::arg("x"), py::arg("wf"), py::arg("alpha"), py::arg("bias"), py::arg("y"), py::arg("zero"), py::arg("B"),
-        py::arg("H"), py::arg("W"), py::arg("Cin"), py::arg("Cout"), py::arg("relu"), py::arg("out_inv_scale"),
-        py::arg("stream") = 0);
+        py::arg("H"), py::arg("W"), py::arg("Cin"), py::arg("Cout"), py::arg("stride"), py::arg("relu"),
+        py::arg("out_inv_scale"), py::arg("stream") = 0);
   m.def("conv3x3_s2rows_supported", &conv3x3_s2rows_supported);
   m.def("conv3x3_s2rows128_supported", &conv3x3_s2rows128_supported);
   m.def("conv3x3_s2rows128", [](uintptr_t x, uintptr_t wf, uintptr_t bias, uintptr_t y, int B, bool relu,

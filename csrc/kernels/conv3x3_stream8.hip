@@ -51,20 +51,28 @@ struct Stream8Args {
   float out_inv_scale;  // y = e4m3(relu(v) * out_inv_scale)
 };
 
-template <int H, int W, int CI, int IMG>
+// Geometry: output H x W, stride S; a workgroup owns HS output rows of one
+// image (PARTS = H / HS > 1, stride 2 only) or IMG whole images.
+template <int H, int W, int CI, int HS, int IMG, int S>
 struct Stream8Geom {
-  static constexpr int XR = IMG * H;          // staged rows
-  static constexpr int PXB = CI;              // bytes per staged pixel
-  static constexpr int ROWB = W * PXB;
-  static constexpr int ZB = XR * ROWB;        // the zero pixel
+  static constexpr int PARTS = H / HS;
+  static_assert(PARTS == 1 || (IMG == 1 && S == 2), "strips: one image, stride 2");
+  static constexpr int HI = S * H, WI = S * W;   // input rows / columns
+  // staged rows: whole images, or the strip's input rows 2 r0 - 1 .. 2 (r0 +
+  // HS - 1) + 1 (stride 2 never reads below the image)
+  static constexpr int XR = PARTS == 1 ? IMG * HI : (S * (HS - 1) + 3 < HI ? S * (HS - 1) + 3 : HI);
+  static constexpr int PXB = CI;                 // bytes per staged pixel
+  static constexpr int ROWB = WI * PXB;
+  static constexpr int ZB = XR * ROWB;           // the zero pixel
   static constexpr int LDS = ZB + PXB;
-  static constexpr int CH = XR * W * (CI / 16);  // 16-B chunks staged
+  static constexpr int CH = XR * WI * (CI / 16);  // 16-B chunks staged (at most)
 };
 
-template <int H, int W, int CI, int CO, int IMG, int NSP, int WM, int NG, int PD>
+template <int H, int W, int CI, int CO, int HS, int IMG, int NSP, int WM, int NG, int PD, int S>
 __global__ __launch_bounds__(512, 1) void conv3x3_stream8_kernel(Stream8Args a) {
-  using G = Stream8Geom<H, W, CI, IMG>;
-  constexpr int NPIX = IMG * H * W;          // output pixels per workgroup
+  using G = Stream8Geom<H, W, CI, HS, IMG, S>;
+  constexpr int PARTS = G::PARTS, HI = G::HI, WI = G::WI;
+  constexpr int NPIX = IMG * HS * W;         // output pixels per workgroup
   constexpr int MFT = (NPIX + 15) / 16;      // pixel fragments (the last one partly padding)
   constexpr int MF = (MFT + WM - 1) / WM;    // per wave
   constexpr int WN = 32 * NG;                // channels per wave
@@ -77,6 +85,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream8_kernel(Stream8Args a) 
   static_assert(CT % PD == 0, "the ring slot of K-tile tap * CT + cc is cc % PD: compile-time register indices");
   static_assert(G::CH % 64 == 0, "whole DMA instructions");
   static_assert(G::LDS <= 160 * 1024, "LDS budget");
+  static_assert(S == 1 || (S == 2 && WI % 2 == 0), "stride");
 
   extern __shared__ __attribute__((aligned(16))) uint4 smem[];
   char* xs = (char*)smem;
@@ -84,21 +93,38 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream8_kernel(Stream8Args a) 
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave % WM, wc = wave / WM;
   const int fr = lane & 15, fq = lane >> 4;
-  const int ns = blockIdx.x % NSP, bg = blockIdx.x / NSP;
+  const int ns = blockIdx.x % NSP, rest = blockIdx.x / NSP;
+  const int bg = rest / PARTS, part = rest - bg * PARTS;
   const int b = bg * IMG, nimg = min(IMG, a.B - b);
-  const int npix = nimg * H * W;
+  const int r0 = part * HS;                                  // first output row
+  const int rs = PARTS == 1 ? 0 : max(S * r0 - 1, 0);        // first staged input row
+  const int nrows = PARTS == 1 ? nimg * HI : min(S * (r0 + HS - 1) + 1, HI - 1) - rs + 1;
+  const int npix = IMG == 1 ? NPIX : nimg * HS * W;
   const int ch0 = ns * (CO / NSP) + wc * WN;
-  const uint8_t* img = a.x + (long)b * H * W * CI;
+  const uint8_t* img = a.x + (long)b * HI * WI * CI;
 
-  // ---- stage the images (one flat run of 16-B chunks): logical chunk pair m
-  // of staged pixel q (= its row * W + x, the key K) at physical pair
-  // m ^ (q & 7), each chunk keeping its half
-  const int nchunks = nimg * H * W * CPX;
+  // ---- stage the input rows (one flat run of 16-B chunks; stride 2: each
+  // row's even columns first, then its odd ones). The key K of a staged
+  // pixel is chosen so that for output pixel p at tap (kh, kw) it is p + a
+  // tap constant, consecutive along a fragment even where it wraps a row:
+  //   stride 1 (whole images): K = staged row * W + x;
+  //   stride 2: K = image * H * W + (((y + 1) >> 1) - r0) * W + ((x + 1) >> 1).
+  // Logical chunk pair m of a staged pixel sits at physical pair m ^ (K & 7),
+  // each chunk keeping its half.
   for (int k0 = wave * 64; k0 < G::CH; k0 += 512) {
     const int ci = k0 + lane;
-    const int q = ci / CPX, pc = ci - q * CPX;  // staged pixel, physical chunk
-    const int lc = ((((pc >> 1) ^ (q & 7)) << 1) | (pc & 1));  // logical chunk at physical pc
-    const uint8_t* src = ci < nchunks ? img + (long)q * CI + 16 * lc : a.zero;
+    const int i = ci / (WI * CPX), rem = ci - i * (WI * CPX);
+    const int q = rem / CPX, pc = rem - q * CPX;  // physical column, chunk
+    const int x = S == 1 ? q : (q < WI / 2 ? 2 * q : 2 * (q - WI / 2) + 1);
+    int K;
+    if constexpr (S == 1) {
+      K = i * W + x;
+    } else {
+      const int ii = PARTS == 1 ? i / HI : 0, y = PARTS == 1 ? i - ii * HI : rs + i;
+      K = ii * (H * W) + (((y + 1) >> 1) - r0) * W + ((x + 1) >> 1);
+    }
+    const int lc = ((((pc >> 1) ^ (K & 7)) << 1) | (pc & 1));  // logical chunk at physical pc
+    const uint8_t* src = i < nrows ? img + ((long)(rs + i) * WI + x) * CI + 16 * lc : a.zero;
     dma16(src, xs + k0 * 16);
   }
   if (wave == 0 && lane < CPX) dma16(a.zero, xs + G::ZB);
@@ -120,15 +146,17 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream8_kernel(Stream8Args a) 
     for (int nf = 0; nf < NF; ++nf) wq[t][nf] = wfrag(t, nf);
 
   // ---- per-lane pixel constants: xoff = the staged offset of the tap-(1,1)
-  // pixel | flags for the image's first / last row and column (their outside
-  // taps read the zero pixel)
+  // input pixel | flags for the image's first / last row and column (their
+  // outside taps read the zero pixel; stride 2 never leaves the image at the
+  // bottom or right)
   int xoff[MF];
 #pragma unroll
   for (int f = 0; f < MF; ++f) {
     const int p = min(16 * (wm * MF + f) + fr, npix - 1);
-    const int pi = p % (H * W), ii = p / (H * W), prow = pi / W, pcol = pi - prow * W;
-    xoff[f] = ((ii * H + prow) * W + pcol) * G::PXB | (prow == 0 ? 1 : 0) | (prow == H - 1 ? 2 : 0) |
-              (pcol == 0 ? 4 : 0) | (pcol == W - 1 ? 8 : 0);
+    const int pi = p % (HS * W), ii = p / (HS * W), prow = pi / W, pcol = pi - prow * W, r = r0 + prow;
+    const int row = ii * HI + S * r - rs;  // (stride 2: even input column 2 pcol sits at slot pcol)
+    xoff[f] = (row * WI + pcol) * G::PXB | (r == 0 ? 1 : 0) | (S == 1 && r == H - 1 ? 2 : 0) | (pcol == 0 ? 4 : 0) |
+              (S == 1 && pcol == W - 1 ? 8 : 0);
     asm volatile("" : "+v"(xoff[f]));
   }
   floatx4 acc[MF][NF];
@@ -144,10 +172,12 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream8_kernel(Stream8Args a) 
   auto set_tap = [&](int tap) __attribute__((always_inline)) {
     const int kh = tap / 3, kw = tap - kh * 3;
     const int tm = (kh == 0 ? 1 : 0) | (kh == 2 ? 2 : 0) | (kw == 0 ? 4 : 0) | (kw == 2 ? 8 : 0);
-    const int toff = ((kh - 1) * W + (kw - 1)) * G::PXB;
+    // staged column offset of tap column kw (stride 2: odd columns start at WI / 2)
+    const int dq = S == 1 ? kw - 1 : (kw == 0 ? WI / 2 - 1 : kw == 1 ? 0 : WI / 2);
+    const int toff = ((kh - 1) * WI + dq) * G::PXB;
 #pragma unroll
     for (int f = 0; f < MF; ++f) xa[f] = (xoff[f] & tm) ? G::ZB : (xoff[f] & ~15) + toff;
-    const int ktap = (kh - 1) * W + (kw - 1);
+    const int ktap = S == 1 ? (kh - 1) * W + (kw - 1) : (kh == 2 ? W : 0) + (kw == 2 ? 1 : 0);
     const int u = fq ^ ((fr + ktap) & 7);
     tsw0 = (u << 5) | ((fq & 1) << 4);
     tsw1 = tsw0 ^ 16;
@@ -208,7 +238,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream8_kernel(Stream8Args a) 
       bs[j][e] = a.bias[ch0 + 32 * j + 8 * fq + e];
     }
   const float inv = a.out_inv_scale;
-  const long base = (long)b * H * W * CO + ch0 + 8 * fq;
+  const long base = ((long)b * H + r0) * W * CO + ch0 + 8 * fq;
 #pragma unroll
   for (int f = 0; f < MF; ++f) {
     const int p = 16 * (wm * MF + f) + fr;
@@ -232,11 +262,11 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream8_kernel(Stream8Args a) 
   }
 }
 
-template <int H, int W, int CI, int CO, int IMG, int NSP, int WM, int NG, int PD>
+template <int H, int W, int CI, int CO, int HS, int IMG, int NSP, int WM, int NG, int PD, int S>
 void launch8(const Stream8Args& a, hipStream_t s) {
-  using G = Stream8Geom<H, W, CI, IMG>;
-  const int grid = (a.B + IMG - 1) / IMG * NSP;
-  hipLaunchKernelGGL((conv3x3_stream8_kernel<H, W, CI, CO, IMG, NSP, WM, NG, PD>), dim3(grid), dim3(512),
+  using G = Stream8Geom<H, W, CI, HS, IMG, S>;
+  const int grid = (a.B + IMG - 1) / IMG * (H / HS) * NSP;
+  hipLaunchKernelGGL((conv3x3_stream8_kernel<H, W, CI, CO, HS, IMG, NSP, WM, NG, PD, S>), dim3(grid), dim3(512),
                      (size_t)G::LDS, s, a);
 }
 
@@ -246,8 +276,12 @@ int g_stream8_variant = 0;
 
 void conv3x3_stream8_set_variant(int v) { g_stream8_variant = v; }
 
-bool conv3x3_stream8_supported(int Hin, int Win, int Cin, int Cout) {
-  return Cin == Cout && ((Hin == 14 && Win == 14 && Cin == 256) || (Hin == 7 && Win == 7 && Cin == 512));
+bool conv3x3_stream8_supported(int Hin, int Win, int Cin, int Cout, int stride) {
+  if (Cin != Cout) return false;
+  if (stride == 1) return (Hin == 14 && Win == 14 && Cin == 256) || (Hin == 7 && Win == 7 && Cin == 512);
+  // ResNet50 layer3.0 / layer4.0 conv2 (the bottleneck's strided 3x3)
+  if (stride == 2) return (Hin == 28 && Win == 28 && Cin == 256) || (Hin == 14 && Win == 14 && Cin == 512);
+  return false;
 }
 
 // Byte offset of the 16 weight bytes lane `lane` loads for (32-channel group
@@ -260,9 +294,11 @@ size_t conv3x3_stream8_frag_offset(int j, int t, int nf, int h, int lane, int KT
 }
 
 void conv3x3_stream8(const void* x, const void* wf, const float* alpha, const float* bias, void* y, const void* zero,
-                     int B, int Hin, int Win, int Cin, int Cout, bool relu, float out_inv_scale, hipStream_t s) {
+                     int B, int Hin, int Win, int Cin, int Cout, int stride, bool relu, float out_inv_scale,
+                     hipStream_t s) {
   if (B <= 0) return;
-  if (!conv3x3_stream8_supported(Hin, Win, Cin, Cout)) throw std::invalid_argument("conv3x3_stream8: unsupported shape");
+  if (!conv3x3_stream8_supported(Hin, Win, Cin, Cout, stride))
+    throw std::invalid_argument("conv3x3_stream8: unsupported shape");
   if (!x || !wf || !alpha || !bias || !y || !zero || (((uintptr_t)x | (uintptr_t)wf | (uintptr_t)zero) & 15) ||
       ((uintptr_t)y & 7) || !(out_inv_scale > 0.f))
     throw std::invalid_argument("conv3x3_stream8: null / misaligned operand or no output scale");
@@ -278,16 +314,23 @@ void conv3x3_stream8(const void* x, const void* wf, const float* alpha, const fl
   a.relu = relu;
   a.out_inv_scale = out_inv_scale;
   const int v = g_stream8_variant;
-  if (Cin == 256) {
+  if (stride == 2 && Cin == 256) {
+    // layer3.0.conv2 (28x28x256 -> 14x14): half an image (7 output rows, 15
+    // staged rows = 105 KB) x all 256 channels, 8 groups of 32
+    launch8<14, 14, 256, 256, 7, 1, 1, 1, 1, 2, 2>(a, s);
+  } else if (stride == 2) {
+    // layer4.0.conv2 (14x14x512 -> 7x7): one image (98 KB) x half the channels
+    launch8<7, 7, 512, 512, 7, 1, 2, 1, 1, 2, 2>(a, s);
+  } else if (Cin == 256) {
     // layer3: one image x half the channels per workgroup (2 pixel halves x 4
     // groups of 32; 188 VGPRs). All 256 channels per workgroup (4 groups of
     // 64 per wave) spills at any ring depth.
-    launch8<14, 14, 256, 256, 1, 2, 2, 1, 2>(a, s);
+    launch8<14, 14, 256, 256, 14, 1, 2, 2, 1, 2, 1>(a, s);
   } else {  // layer4: two images x half the channels, 8 groups of 32 (variant bit 2: a 2-deep weight ring)
     if (v & 2)
-      launch8<7, 7, 512, 512, 2, 2, 1, 1, 2>(a, s);
+      launch8<7, 7, 512, 512, 7, 2, 2, 1, 1, 2, 1>(a, s);
     else
-      launch8<7, 7, 512, 512, 2, 2, 1, 1, 4>(a, s);
+      launch8<7, 7, 512, 512, 7, 2, 2, 1, 1, 4, 1>(a, s);
   }
   DMLC_HIP_CHECK(hipGetLastError());
 }

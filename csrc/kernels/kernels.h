@@ -237,15 +237,16 @@ void conv_small(const void* x, const void* wf, const float* bias, const void* re
 // stride 2 on 56x56x64 -> 128 and 28x28x128 -> 256. Hin/Win are the input
 // dims; same operand layouts as conv2d_igemm.
 bool conv3x3_stream_supported(int Hin, int Win, int Cin, int Cout, int stride = 1);
-// e4m3 3x3 / s1 / p1 conv on the block-scaled e4m3 MFMA (conv3x3_stream8.hip):
-// ResNet50's layer3 / layer4 bottleneck 3x3 convs with e4m3 t1 in and e4m3 t2
-// out. x [B, H, W, C] e4m3; wf: e4m3 weights [CO][9 C] (k = tap * C + c) in
+// e4m3 3x3 / p1 conv, stride 1 or 2, on the block-scaled e4m3 MFMA
+// (conv3x3_stream8.hip): ResNet50's layer3 / layer4 bottleneck 3x3 convs with
+// e4m3 t1 in and e4m3 t2 out. x [B, H, W, C] e4m3; wf: e4m3 weights [CO][9 C] (k = tap * C + c) in
 // the order of conv3x3_stream8_frag_offset (KT = 9 C / 128); y = e4m3(
 // relu?(acc * alpha + bias) * out_inv_scale) [B, H, W, CO].
-bool conv3x3_stream8_supported(int Hin, int Win, int Cin, int Cout);
+bool conv3x3_stream8_supported(int Hin, int Win, int Cin, int Cout, int stride = 1);
 size_t conv3x3_stream8_frag_offset(int j, int t, int nf, int h, int lane, int KT);
 void conv3x3_stream8(const void* x, const void* wf, const float* alpha, const float* bias, void* y, const void* zero,
-                     int B, int Hin, int Win, int Cin, int Cout, bool relu, float out_inv_scale, hipStream_t s);
+                     int B, int Hin, int Win, int Cin, int Cout, int stride, bool relu, float out_inv_scale,
+                     hipStream_t s);
 void conv3x3_stream8_set_variant(int v);  // A/B hook (0 = the defaults)
 // Stride 2 may also compute the block's 1x1/s2 downsample conv (wd [Cout,
 // Cin], bias bd, no ReLU) from the same resident input into yd.

@@ -400,9 +400,10 @@ void Engine::mark_fp8() {
         if (op.type != OpType::Conv) continue;
         const ConvLayer& L = convs_[op.conv];
         const ActShape& is = shapes_[op.in];
-        if (L.fc || L.kh != 3 || L.kw != 3 || L.pad != 1 || L.stride != 1 || op.res >= 0 || !chan_act_[op.out] ||
-            is.fp8 || is.f32 || !conv3x3_stream8_supported(is.H, is.W, is.C, L.cout))
+        if (L.fc || L.kh != 3 || L.kw != 3 || L.pad != 1 || op.res >= 0 || is.fp8 || is.f32 ||
+            shapes_[op.out].f32 || in_3x3[op.out] || !conv3x3_stream8_supported(is.H, is.W, is.C, L.cout, L.stride))
           continue;
+        if (!chan_act_[op.out] && (L.stride == 1 || shapes_[op.out].fp8)) continue;
         int producers = 0, readers = 0;
         bool from_1x1 = false;
         for (const Op& o : ops_) {
@@ -416,6 +417,9 @@ void Engine::mark_fp8() {
         if (producers != 1 || !from_1x1 || readers != 1) continue;
         shapes_[op.in].fp8 = true;
         chan_act_[op.in] = true;
+        // (a strided one's t2: e4m3 out too, per-channel scales, as the stride-1 ones')
+        shapes_[op.out].fp8 = true;
+        chan_act_[op.out] = true;
       }
     }
   }
@@ -518,9 +522,9 @@ void Engine::pack_weights(const WeightMap& w) {
       L.wf_off = off;  // fragment-order copy for conv5x5_27.hip
       off = align_up(off + (size_t)L.cout * L.kpad * 2, 256);
     }
-    if (L.fp8 && !L.fc && L.in_act >= 0 && L.kh == 3 && L.kw == 3 && L.stride == 1 && L.pad == 1 &&
-        L.kpad == 9 * L.cin && conv3x3_stream8_supported(shapes_[L.in_act].H, shapes_[L.in_act].W,
-                                                         shapes_[L.in_act].C, L.cout)) {
+    if (L.fp8 && !L.fc && L.in_act >= 0 && L.kh == 3 && L.kw == 3 && L.pad == 1 && L.kpad == 9 * L.cin &&
+        conv3x3_stream8_supported(shapes_[L.in_act].H, shapes_[L.in_act].W, shapes_[L.in_act].C, L.cout,
+                                  L.stride)) {
       L.wf_off = off;  // e4m3 fragment-order copy for conv3x3_stream8.hip
       off = align_up(off + (size_t)L.cout * L.kpad, 256);
     }
@@ -831,8 +835,8 @@ Engine::ConvPath Engine::conv_path(const Op& op, int B) const {
     return ConvPath::Direct13;
   // e4m3 in and out (fp8_3x3_in): whole images per workgroup, once the batch
   // fills the CUs (query batches: the e4m3 implicit GEMM)
-  if (L.fp8 && !L.fc && L.kh == 3 && L.kw == 3 && L.stride == 1 && L.pad == 1 && L.wf_off && op.res < 0 &&
-      shapes_[op.out].fp8 && 4 * B >= num_cus_ && conv3x3_stream8_supported(is.H, is.W, is.C, L.cout))
+  if (L.fp8 && !L.fc && L.kh == 3 && L.kw == 3 && L.pad == 1 && L.wf_off && op.res < 0 && shapes_[op.out].fp8 &&
+      4 * B >= num_cus_ && conv3x3_stream8_supported(is.H, is.W, is.C, L.cout, L.stride))
     return ConvPath::Stream8;
   if (opt_.direct27 && !L.fc && !L.fp8 && L.kh == 5 && L.kw == 5 && L.stride == 1 && L.relu && L.wf_off &&
       L.kpad == 1600 && !shapes_[op.out].f32 && conv5x5_27_supported(is.H, is.W, is.C, L.cout, L.pad))
@@ -1322,7 +1326,8 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
           case ConvPath::Stream8: {
             const uint8_t* wa = (const uint8_t*)warena_;
             conv3x3_stream8(acts_[op.in], wa + L.wf_off, (const float*)(wa + L.a_off), (const float*)(wa + L.b_off),
-                            acts_[op.out], zero_, B, is.H, is.W, is.C, L.cout, L.relu, 1.f / shapes_[op.out].scale, cs);
+                            acts_[op.out], zero_, B, is.H, is.W, is.C, L.cout, L.stride, L.relu,
+                            1.f / shapes_[op.out].scale, cs);
             break;
           }
           case ConvPath::Rows28:

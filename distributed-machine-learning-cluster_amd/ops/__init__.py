@@ -432,20 +432,22 @@ def stream8_weight_frag(w_q: torch.Tensor, cout: int) -> torch.Tensor:
 
 
 def conv3x3_stream8(x: torch.Tensor, w_q: torch.Tensor, alpha: torch.Tensor, bias: torch.Tensor, relu: bool = True,
-                    out_scale: float = 1.0, frag: torch.Tensor | None = None) -> torch.Tensor:
-    """e4m3 3x3/s1/p1 conv (conv3x3_stream8.hip) on e4m3 NHWC [B,14,14,256] or
-    [B,7,7,512]: e4m3(relu?(acc * alpha + bias) / out_scale) with acc = conv
-    of the e4m3 values. w_q / alpha: pack_conv_weight_fp8 (alpha = s_x * s_w)."""
+                    out_scale: float = 1.0, frag: torch.Tensor | None = None, stride: int = 1) -> torch.Tensor:
+    """e4m3 3x3/p1 conv (conv3x3_stream8.hip) on e4m3 NHWC: stride 1 on
+    [B,14,14,256] / [B,7,7,512], stride 2 on [B,28,28,256] / [B,14,14,512]:
+    e4m3(relu?(acc * alpha + bias) / out_scale) with acc = conv of the e4m3
+    values. w_q / alpha: pack_conv_weight_fp8 (alpha = s_x * s_w)."""
     _need_cuda(x, w_q, alpha, bias)
     C = native()
     B, H, W, Cin = x.shape
     cout = Cin
-    if x.dtype != FP8 or not C.conv3x3_stream8_supported(H, W, Cin, cout) or w_q.shape[1] != 9 * Cin:
+    if x.dtype != FP8 or not C.conv3x3_stream8_supported(H, W, Cin, cout, stride) or w_q.shape[1] != 9 * Cin:
         raise ValueError("conv3x3_stream8: unsupported shape / dtype")
     wf = stream8_weight_frag(w_q, cout) if frag is None else frag
-    y = torch.empty(B, H, W, cout, dtype=FP8, device=x.device)
+    y = torch.empty(B, H // stride, W // stride, cout, dtype=FP8, device=x.device)
     C.conv3x3_stream8(_ptr(x.contiguous()), _ptr(wf), _ptr(alpha.float().contiguous()), _ptr(bias.float().contiguous()),
-                      _ptr(y), _ptr(_zero_page(x.device)), B, H, W, Cin, cout, relu, 1.0 / out_scale, _stream())
+                      _ptr(y), _ptr(_zero_page(x.device)), B, H, W, Cin, cout, stride, relu, 1.0 / out_scale,
+                      _stream())
     return y
 
 

@@ -668,14 +668,16 @@ def test_softmax_top1(gpu):
     assert torch.allclose(prob.cpu(), pv, rtol=1e-4, atol=1e-6)
 
 
-@pytest.mark.parametrize("B,H,C", [(3, 14, 256), (2, 7, 512), (3, 7, 512), (40, 14, 256)])
-def test_conv3x3_stream8(gpu, B, H, C):
+@pytest.mark.parametrize("B,H,C,S", [(3, 14, 256, 1), (2, 7, 512, 1), (3, 7, 512, 1), (40, 14, 256, 1),
+                                     (3, 28, 256, 2), (2, 14, 512, 2)])
+def test_conv3x3_stream8(gpu, B, H, C, S):
     """The e4m3 3x3/s1 conv (conv3x3_stream8.hip, block-scaled e4m3 MFMA) vs
     fp32 torch on the same e4m3 operands (dequantised): the only difference is
     the output's e4m3 rounding (3 mantissa bits, <= 1/16 relative), so the
     dequantised output is within 0.04 relative L2 and no element is more than
     one e4m3 step off the exactly rounded fp32 result. Odd batches leave the
-    7x7 kernel's last workgroup one image short."""
+    7x7 kernel's last workgroup one image short; stride 2 (ResNet50 layer3.0 /
+    layer4.0 conv2) runs half-image strips on 28x28x256."""
     g = torch.Generator().manual_seed(100 + B + C)
     x = torch.randn(B, H, H, C, generator=g).clamp_min(0)  # post-ReLU t1
     sx = x.abs().max().item() / ops.FP8_MAX
@@ -685,9 +687,10 @@ def test_conv3x3_stream8(gpu, B, H, C):
     bias = torch.randn(C, generator=g) * 0.05
     alpha = sx * sw
     wd = (wq.float()[:C, :9 * C] * sw[:C, None]).view(C, 3, 3, C).permute(0, 3, 1, 2)
-    ref = F.relu(F.conv2d(xq.float().permute(0, 3, 1, 2) * sx, wd, bias, padding=1)).permute(0, 2, 3, 1)
+    ref = F.relu(F.conv2d(xq.float().permute(0, 3, 1, 2) * sx, wd, bias, stride=S, padding=1)).permute(0, 2, 3, 1)
     out_scale = ref.abs().max().item() / ops.FP8_MAX
-    y = ops.conv3x3_stream8(xq.to(gpu), wq.to(gpu), alpha.to(gpu), bias.to(gpu), relu=True, out_scale=out_scale)
+    y = ops.conv3x3_stream8(xq.to(gpu), wq.to(gpu), alpha.to(gpu), bias.to(gpu), relu=True, out_scale=out_scale,
+                            stride=S)
     torch.cuda.synchronize()
     got = y.float().cpu() * out_scale
     assert _rel(got, ref) < 0.04, _rel(got, ref)

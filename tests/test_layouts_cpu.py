@@ -502,3 +502,68 @@ def test_stream8_lds_layout(H, CI, IMG):
                             if l in live:
                                 slots.setdefault((addr[l] // 16) % 16, set()).add(addr[l])
                         assert all(len(v) == 1 for v in slots.values()), (tap, cc, f)
+
+
+@pytest.mark.parametrize("H,CI,HS", [(14, 256, 7), (7, 512, 7)])
+def test_stream8_stride2_lds_layout(H, CI, HS):
+    """conv3x3_stream8.hip at stride 2 (ResNet50 layer3.0 / layer4.0 conv2):
+    staged input rows with each row's even columns first, chunk pairs keyed
+    by K = (((y + 1) >> 1) - r0) * W + ((x + 1) >> 1); the kernel's tap
+    offsets read every lane's 32 channels of input pixel (2r + kh - 1,
+    2c + kw - 1) (odd fq: second 16 first) and both reads are conflict free."""
+    W = H
+    HI, WI, CPX = 2 * H, 2 * W, CI // 16
+    torch.manual_seed(1)
+    img = torch.randint(0, 256, (HI, WI, CI), dtype=torch.uint8)
+    for part in range(H // HS):
+        r0 = part * HS
+        rs = max(2 * r0 - 1, 0)
+        nrows = min(2 * (r0 + HS - 1) + 1, HI - 1) - rs + 1
+        lds = torch.zeros(nrows * WI * CI + CI, dtype=torch.uint8)
+        ZB = nrows * WI * CI
+        for i in range(nrows):
+            y = rs + i
+            for q in range(WI):
+                x = 2 * q if q < WI // 2 else 2 * (q - WI // 2) + 1
+                K = (((y + 1) >> 1) - r0) * W + ((x + 1) >> 1)
+                for pc in range(CPX):
+                    lc = (((pc >> 1) ^ (K & 7)) << 1) | (pc & 1)
+                    o = (i * WI + q) * CI + 16 * pc
+                    lds[o:o + 16] = img[y, x, 16 * lc:16 * lc + 16]
+        npix = HS * W
+        for tap in range(9):
+            kh, kw = divmod(tap, 3)
+            dq = WI // 2 - 1 if kw == 0 else (0 if kw == 1 else WI // 2)
+            toff = ((kh - 1) * WI + dq) * CI
+            ktap = (W if kh == 2 else 0) + (1 if kw == 2 else 0)
+            for cc in range(CI // 128):
+                for f in range((npix + 15) // 16):
+                    a0, a1 = [], []
+                    for lane in range(64):
+                        fr, fq = lane & 15, lane >> 4
+                        p = min(16 * f + fr, npix - 1)
+                        prow, pcol = divmod(p, W)
+                        r = r0 + prow
+                        inside = not ((r == 0 and kh == 0) or (pcol == 0 and kw == 0))
+                        xa = ((2 * r - rs) * WI + pcol) * CI + toff if inside else ZB
+                        u = fq ^ ((fr + ktap) & 7)
+                        t0 = (u << 5) | ((fq & 1) << 4)
+                        a0.append(xa + (t0 ^ (cc << 7)))
+                        a1.append(xa + ((t0 ^ 16) ^ (cc << 7)))
+                        got = torch.cat([lds[a0[-1]:a0[-1] + 16], lds[a1[-1]:a1[-1] + 16]])
+                        if inside and 16 * f + fr < npix:
+                            ch = 128 * cc + 32 * fq
+                            exp = img[2 * r + kh - 1, 2 * pcol + kw - 1, ch:ch + 32]
+                            if fq & 1:
+                                exp = torch.cat([exp[16:], exp[:16]])
+                            assert torch.equal(got, exp), (part, tap, cc, f, lane)
+                        elif not inside:
+                            assert not got.any()
+                    live = [l for l in range(64) if a0[l] < ZB]
+                    for addr in (a0, a1):
+                        for grp in _B128_GROUPS:
+                            slots = {}
+                            for l in grp:
+                                if l in live:
+                                    slots.setdefault((addr[l] // 16) % 16, set()).add(addr[l])
+                            assert all(len(v) == 1 for v in slots.values()), (part, tap, cc, f)
