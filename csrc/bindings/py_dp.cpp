@@ -243,6 +243,169 @@ py::dict dp_host_bench(py::array_t<uint8_t, py::array::c_style> pool, int world,
   return out;
 }
 
+py::dict group_stats(const dp::Group::Stats& st) {
+  py::dict d;
+  d["images"] = st.images;
+  d["steps"] = st.steps;
+  d["recoveries"] = st.recoveries;
+  d["redone_images"] = st.redone_images;
+  return d;
+}
+
+// ------------------------------------------------------------------ loopback
+// bench.py's per-rank call sequence (stage, prime, calibrate, timed runs,
+// an unpipelined run) on `world` virtual ranks of ONE GPU: rank r is a
+// dp::Runner over its own HIP worker (engines[r] + lanes - 1 copies, its own
+// streams and slots) and the device-loopback communicators (stream-ordered
+// device copies, comm::device_loopback_world), one thread per rank as one
+// process per GPU would be. `pool`: the coordinator's device pool of two
+// global batches. Returns every step's gathered answers from rank 0.
+py::dict dp_loopback_bench(std::vector<Engine*> engines, uintptr_t pool, int per_rank, double coord_weight,
+                           const std::string& input_mode, int lanes, int prime, int steps, int unpipelined,
+                           int calib_rounds, int calib_steps, int image_size) {
+  const int world = (int)engines.size();
+  if (world < 1) throw std::invalid_argument("dp_loopback_bench: no engines");
+  const bool scatter = input_mode == "scatter";
+  if (!scatter && input_mode != "staged") throw std::invalid_argument("input_mode: scatter | staged");
+  const int S = image_size;
+  const size_t ib = (size_t)S * S * 3;
+  const auto counts0 = dp::weighted_counts(per_rank, world, coord_weight);
+  int64_t G = 0;
+  for (int c : counts0) G += c;
+  const uint8_t* src = (const uint8_t*)pool;
+  auto cin = comm::device_loopback_world(world), cout = comm::device_loopback_world(world);
+  // every rank's runner, built here (engine copies allocate), driven below by one thread each
+  std::vector<std::vector<std::unique_ptr<Engine>>> lane_engines(world);
+  std::vector<std::unique_ptr<dp::Runner>> runners;
+  for (int r = 0; r < world; ++r) {
+    Engine* e = engines[r];
+    e->reserve(per_rank);
+    std::vector<Engine*> more;
+    for (int l = 1; l < lanes; ++l) {
+      lane_engines[r].push_back(std::make_unique<Engine>(*e, e->device()));
+      lane_engines[r].back()->copy_weights_from(*e);
+      lane_engines[r].back()->reserve(std::max(e->max_batch(), per_rank));
+      more.push_back(lane_engines[r].back().get());
+    }
+    runners.push_back(std::make_unique<dp::Runner>(dp::make_hip_worker(e, S, S, true, more),
+                                                   world > 1 ? std::move(cin[r]) : nullptr,
+                                                   world > 1 ? std::move(cout[r]) : nullptr, world, r, counts0,
+                                                   scatter, ib, 20000));
+  }
+  std::vector<std::string> errs(world);
+  std::vector<std::vector<int64_t>> done(world);
+  std::vector<int64_t> ans_step;
+  std::vector<std::vector<int32_t>> ans_idx;
+  std::vector<std::vector<float>> ans_prob;
+  std::vector<int> final_counts;
+  dp::Runner::Calibration calib;
+  ThreadAllGather ag(world);
+  runners[0]->set_step_hook([&](int64_t step, const int32_t* i, const float* p, int64_t n) {
+    ans_step.push_back(step);
+    ans_idx.emplace_back(i, i + n);
+    ans_prob.emplace_back(p, p + n);
+  });
+  {
+    py::gil_scoped_release nogil;
+    std::vector<std::thread> ts;
+    for (int r = 0; r < world; ++r)
+      ts.emplace_back([&, r] {
+        uint8_t* mine = nullptr;
+        try {
+          dp::Runner& run = *runners[r];
+          run.worker()->activate();
+          const uint8_t* p = r == 0 ? src : nullptr;
+          int64_t np = r == 0 ? 2 * G : 0;
+          if (!scatter) {  // staged: two per-rank batches at a stride of max_per_rank images, in this rank's HBM
+            DMLC_HIP_CHECK(hipMalloc(&mine, (size_t)2 * run.max_per_rank() * ib));
+            for (int k = 0; k < 2; ++k)
+              run.stage(r == 0 ? src + (size_t)k * G * ib : nullptr, mine + (size_t)k * run.max_per_rank() * ib);
+            p = mine;
+            np = 2 * run.max_per_rank();
+          }
+          std::vector<int64_t> d;
+          d.push_back(run.run(p, np, 0, prime).steps);
+          if (calib_rounds > 0) {
+            auto c = run.calibrate(p, np, prime, calib_steps, calib_rounds, 0.05, [&](double x) { return ag(r, x); });
+            if (r == 0) calib = c;
+          }
+          int64_t first = prime + (calib_rounds > 0 ? calib.steps : 0);
+          (void)first;
+          d.push_back(run.run(p, np, 1000, steps).steps);
+          d.push_back(run.run(p, np, 1000 + steps, unpipelined, /*pipelined=*/false).steps);
+          run.worker()->sync_all();
+          done[r] = d;
+          if (r == 0) final_counts = run.counts();
+        } catch (const std::exception& e) {
+          errs[r] = e.what();
+        }
+        if (mine) (void)hipFree(mine);
+      });
+    for (auto& t : ts) t.join();
+  }
+  for (int r = 0; r < world; ++r)
+    if (!errs[r].empty()) throw std::runtime_error("rank " + std::to_string(r) + ": " + errs[r]);
+  runners.clear();
+  py::list steps_out;
+  for (size_t k = 0; k < ans_step.size(); ++k) {
+    steps_out.append(py::make_tuple(ans_step[k], py::array_t<int32_t>(ans_idx[k].size(), ans_idx[k].data()),
+                                    py::array_t<float>(ans_prob[k].size(), ans_prob[k].data())));
+  }
+  py::dict out;
+  out["runs"] = done;
+  out["counts"] = final_counts;
+  out["answers"] = steps_out;
+  out["calibration"] = DpRunner::calib_dict(calib);
+  return out;
+}
+
+// dp::Group (one process driving several GPUs: the serving fleet's scatter)
+// over `engines` as its members on ONE GPU and device-loopback
+// communicators; fail_member >= 1 is lost after fail_after steps (its
+// communicator operations fail) and the group rebuilds over the survivors.
+py::dict dp_loopback_group(std::vector<Engine*> engines, uintptr_t images, int64_t n, int max_per_rank,
+                           int fail_member, int64_t fail_after, int repeats, int image_size) {
+  const int S = image_size;
+  std::vector<std::unique_ptr<dp::Worker>> owned;
+  std::vector<dp::Worker*> ws;
+  for (Engine* e : engines) {
+    e->reserve(max_per_rank);
+    owned.push_back(dp::make_hip_worker(e, S, S, true));
+    ws.push_back(owned.back().get());
+  }
+  std::vector<std::vector<int>> builds;
+  auto factory = [&builds](const std::vector<int>& members) {
+    builds.push_back(members);
+    return comm::device_loopback_world((int)members.size());
+  };
+  py::array_t<int32_t> idx(n), commits(n);
+  py::array_t<float> prob(n);
+  int32_t* pi = idx.mutable_data();
+  float* pp = prob.mutable_data();
+  int32_t* pc = commits.mutable_data();
+  dp::Group::Stats st;
+  std::vector<int> members;
+  {
+    py::gil_scoped_release nogil;
+    dp::Group g(ws, factory, max_per_rank, (size_t)S * S * 3, 20000);
+    if (fail_member >= 0) g.fail(fail_member, fail_after, /*abrupt=*/true);
+    for (int k = 0; k < std::max(1, repeats); ++k) {
+      std::fill(pi, pi + n, -1);
+      std::fill(pc, pc + n, 0);
+      st = g.classify((const uint8_t*)images, n, pi, pp, -1, pc);
+    }
+    members = g.members();
+  }
+  py::dict out;
+  out["idx"] = idx;
+  out["prob"] = prob;
+  out["commits"] = commits;
+  out["stats"] = group_stats(st);
+  out["members"] = members;
+  out["builds"] = builds;
+  return out;
+}
+
 // ------------------------------------------------------------------ group
 class DpGroupPy {
  public:
@@ -716,6 +879,13 @@ class RcclLoop {
 void bind_dp(py::module& m) {
   m.def("dp_partition_devices", &dp::partition_devices, py::arg("live"), py::arg("jobs"));
   m.def("fleet_bucket_batch", &dp::bucket_batch, py::arg("b"), py::arg("max"));
+  m.def("dp_loopback_bench", &dp_loopback_bench, py::arg("engines"), py::arg("pool"), py::arg("per_rank"),
+        py::arg("coord_weight") = 1.0, py::arg("input_mode") = "scatter", py::arg("lanes") = 2, py::arg("prime") = 4,
+        py::arg("steps") = 50, py::arg("unpipelined") = 4, py::arg("calib_rounds") = 0, py::arg("calib_steps") = 4,
+        py::arg("image_size") = 224);
+  m.def("dp_loopback_group", &dp_loopback_group, py::arg("engines"), py::arg("images"), py::arg("n"),
+        py::arg("max_per_rank"), py::arg("fail_member") = -1, py::arg("fail_after") = 0, py::arg("repeats") = 1,
+        py::arg("image_size") = 224);
   m.def("host_order_probe", &host_order_probe, py::arg("bad"), py::arg("timeout_ms") = 500);
   m.def("host_multi_world_probe", &host_multi_world_probe, py::arg("timeout_ms") = 2000);
   py::class_<HostFleet>(m, "HostFleet")

@@ -94,6 +94,35 @@ std::unique_ptr<Comm> rccl_init_rank(const std::string& unique_id, int nranks, i
 std::vector<std::unique_ptr<Comm>> rccl_init_all(const std::vector<int>& devices);
 
 // ------------------------------------------------------------------ host fake
+// The data plane of an in-process fake world: how a matched send's bytes
+// reach its receive. The host fake copies host memory at match time; the
+// device loopback (loopback_comm.cpp) enqueues stream-ordered device copies.
+class FakeDataPlane {
+ public:
+  virtual ~FakeDataPlane() = default;
+  virtual std::string name() const = 0;
+  // An operation is posted (its group ends) on stream s: a token for the
+  // stream's position there (nullptr when positions do not matter).
+  virtual void* mark(Stream s) = 0;
+  // A send (posted at smark on ss) meets its receive (rmark on rs): move the
+  // bytes after both positions, and order later work on both streams after
+  // the move (RCCL: both kernels complete together).
+  virtual void move(const void* sbuf, void* rbuf, size_t bytes, void* smark, Stream ss, void* rmark, Stream rs) = 0;
+  // A copy within one rank, in stream order (a broadcast root's own buffer).
+  virtual void local_copy(void* dst, const void* src, size_t bytes, Stream s) = 0;
+  // The token of a matched, failed or withdrawn operation is no longer needed.
+  virtual void release(void* mark) = 0;
+};
+// `n` communicators of one fake world over data plane `dp` (host_world: the
+// host-memory plane).
+std::vector<std::unique_ptr<Comm>> fake_world(int n, int timeout_ms, std::shared_ptr<FakeDataPlane> dp);
+// The device loopback plane (loopback_comm.cpp, HIP): n virtual ranks whose
+// buffers are device memory of the current device, a matched send/recv
+// becoming hipMemcpyAsync on the world's copy stream between events recorded
+// on the two ranks' streams. Matching stays the host fake's rendezvous rule,
+// so a single-GPU test runs the multi-rank protocol with real streams,
+// events and slot reuse (tests/test_dp_loopback_gpu.py).
+std::vector<std::unique_ptr<Comm>> device_loopback_world(int n, int timeout_ms = 20000);
 class HostWorld;  // shared mailbox state of one fake communicator
 // `n` host communicators of one fake world; rank i = result[i]. Operations
 // may be driven from one thread per rank or from one thread for all ranks.

@@ -481,6 +481,7 @@ Group::Group(std::vector<Worker*> workers, CommFactory make_comms, int max_per_r
       timeout_ms_(timeout_ms) {
   if (workers_.empty()) throw std::invalid_argument("dp::Group: no workers");
   lost_.assign(workers_.size(), false);
+  killed_.assign(workers_.size(), false);
   fail_at_.assign(workers_.size(), -1);
   fail_abrupt_.assign(workers_.size(), false);
   for (size_t i = 0; i < workers_.size(); ++i) {
@@ -526,7 +527,10 @@ void Group::kill_now(int m) {
   if (m <= 0 || m >= (int)workers_.size()) throw std::invalid_argument("dp::Group::kill_now: bad member");
   auto it = std::find(members_.begin(), members_.end(), m);
   if (it == members_.end()) return;
-  host_worker_set_healthy(*workers_[m], false);
+  // (a host worker also fails its forwards; a HIP worker on the device
+  // loopback loses only its communicator operations)
+  if (dynamic_cast<HostWorker*>(workers_[m])) host_worker_set_healthy(*workers_[m], false);
+  killed_[m] = true;
   const int rank = (int)(it - members_.begin());
   if (!cin_.empty()) {
     comm::host_kill(*cin_[0], rank);
@@ -633,7 +637,7 @@ Group::Stats Group::classify(const uint8_t* src, int64_t n, int32_t* idx, float*
       lost.push_back(e.member);
     } catch (const comm::CommError&) {
       for (int m : members_)
-        if (!workers_[m]->healthy()) lost.push_back(m);
+        if (!workers_[m]->healthy() || killed_[m]) lost.push_back(m);
       if (lost.empty()) throw;  // not attributable to a lost GPU
     }
     if (std::find(lost.begin(), lost.end(), members_.front()) != lost.end())
@@ -644,6 +648,7 @@ Group::Stats Group::classify(const uint8_t* src, int64_t n, int32_t* idx, float*
     for (auto& c : cout_) c->abort();
     for (int m : members_)
       if (std::find(lost.begin(), lost.end(), m) == lost.end()) workers_[m]->sync_all();
+      else if (killed_[m]) workers_[m]->sync_all_noexcept();  // a killed HIP worker's GPU is fine: drain it
     for (int m : lost) lost_[m] = true;
     members_.erase(std::remove_if(members_.begin(), members_.end(), [&](int m) { return lost_[m]; }),
                    members_.end());

@@ -294,6 +294,7 @@ class Group {
   std::vector<std::unique_ptr<Rank>> ranks_;  // one per worker (index = worker)
   std::vector<std::unique_ptr<Comm>> cin_, cout_;
   std::vector<bool> lost_;
+  std::vector<bool> killed_;  // kill_now()ed: its communicator operations fail, whatever its worker says
   std::vector<int64_t> fail_at_;  // per worker: steps still to issue before it is lost (-1: never)
   std::vector<bool> fail_abrupt_;
   int min_per_rank_ = 1;

@@ -43,14 +43,32 @@ struct Op {
   const void* sbuf = nullptr;
   void* rbuf = nullptr;
   size_t bytes = 0;
+  Stream stream = nullptr;  // the rank's stream (data planes that order by stream)
+  void* mark = nullptr;     // the data plane's token for the stream position at post
   bool done = false;
   std::string error;  // set with done = true on failure
+};
+
+// host memory: the bytes move at match time
+class HostPlane : public FakeDataPlane {
+ public:
+  std::string name() const override { return "host"; }
+  void* mark(Stream) override { return nullptr; }
+  void move(const void* sbuf, void* rbuf, size_t bytes, void*, Stream, void*, Stream) override {
+    if (bytes) std::memcpy(rbuf, sbuf, bytes);
+  }
+  void local_copy(void* dst, const void* src, size_t bytes, Stream) override {
+    if (bytes && dst != src) std::memcpy(dst, src, bytes);
+  }
+  void release(void*) override {}
 };
 }  // namespace
 
 class HostWorld {
  public:
-  HostWorld(int n, int timeout_ms) : n_(n), timeout_ms_(timeout_ms), dead_(n, false) {}
+  HostWorld(int n, int timeout_ms, std::shared_ptr<FakeDataPlane> dp)
+      : n_(n), timeout_ms_(timeout_ms), dead_(n, false), dp_(std::move(dp)) {}
+  FakeDataPlane& plane() { return *dp_; }
 
   // Post every op (matching what it can), then wait for all of them.
   // Throws CommError on failure or timeout (after withdrawing unmatched ops).
@@ -123,6 +141,7 @@ class HostWorld {
  private:
   using Key = std::pair<int, int>;  // (src, dst)
   void post(Op* o) {
+    o->mark = dp_->mark(o->stream);
     if (aborted_) return fail(o, "host comm: communicator aborted");
     if (dead_[o->self] || dead_[o->peer])
       return fail(o, "host comm: rank " + std::to_string(dead_[o->self] ? o->self : o->peer) + " is lost");
@@ -142,7 +161,10 @@ class HostWorld {
         fail(r, e);
         return;
       }
-      if (s->bytes) std::memcpy(r->rbuf, s->sbuf, s->bytes);
+      dp_->move(s->sbuf, r->rbuf, s->bytes, s->mark, s->stream, r->mark, r->stream);
+      dp_->release(s->mark);
+      dp_->release(r->mark);
+      s->mark = r->mark = nullptr;
       s->done = r->done = true;
       cv_.notify_all();
       return;
@@ -150,6 +172,8 @@ class HostWorld {
     mine.push_back(o);
   }
   void fail(Op* o, const std::string& e) {
+    dp_->release(o->mark);
+    o->mark = nullptr;
     o->done = true;
     o->error = e;
     cv_.notify_all();
@@ -161,6 +185,8 @@ class HostWorld {
         for (auto it = q.begin(); it != q.end(); ++it)
           if (*it == o) {
             q.erase(it);
+            dp_->release(o->mark);
+            o->mark = nullptr;
             return;
           }
       }
@@ -187,6 +213,7 @@ class HostWorld {
   std::map<Key, std::deque<Op*>> sends_, recvs_;  // posted, unmatched, FIFO per pair
   std::vector<bool> dead_;
   bool aborted_ = false;
+  std::shared_ptr<FakeDataPlane> dp_;
 };
 
 namespace {
@@ -231,7 +258,7 @@ class HostComm : public Comm {
   HostComm(std::shared_ptr<HostWorld> w, int rank) : w_(std::move(w)), rank_(rank) {}
   int rank() const override { return rank_; }
   int size() const override { return w_->size(); }
-  std::string backend() const override { return "host"; }
+  std::string backend() const override { return w_->plane().name(); }
 
   void group_start() override { ++t_depth; }
   void group_end() override {
@@ -241,21 +268,23 @@ class HostComm : public Comm {
     ops.swap(t_ops);
     run_ops(ops);
   }
-  void send(const void* buf, size_t bytes, int peer, Stream) override {
+  void send(const void* buf, size_t bytes, int peer, Stream s) override {
     Op o;
     o.is_send = true;
     o.self = rank_;
     o.peer = check_peer(peer);
     o.sbuf = buf;
     o.bytes = bytes;
+    o.stream = s;
     post(o);
   }
-  void recv(void* buf, size_t bytes, int peer, Stream) override {
+  void recv(void* buf, size_t bytes, int peer, Stream s) override {
     Op o;
     o.self = rank_;
     o.peer = check_peer(peer);
     o.rbuf = buf;
     o.bytes = bytes;
+    o.stream = s;
     post(o);
   }
   void broadcast(const void* sendbuf, void* recvbuf, size_t bytes, int root, Stream s) override {
@@ -263,7 +292,7 @@ class HostComm : public Comm {
     if (rank_ == root) {
       for (int r = 0; r < size(); ++r)
         if (r != root) send(sendbuf, bytes, r, s);
-      if (recvbuf != sendbuf && bytes) std::memcpy(recvbuf, sendbuf, bytes);
+      w_->plane().local_copy(recvbuf, sendbuf, bytes, s);
     } else {
       recv(recvbuf, bytes, root, s);
     }
@@ -293,12 +322,17 @@ class HostComm : public Comm {
 
 }  // namespace
 
-std::vector<std::unique_ptr<Comm>> host_world(int n, int timeout_ms) {
-  if (n < 1) throw std::invalid_argument("host_world: n must be >= 1");
-  auto w = std::make_shared<HostWorld>(n, timeout_ms);
+std::vector<std::unique_ptr<Comm>> fake_world(int n, int timeout_ms, std::shared_ptr<FakeDataPlane> dp) {
+  if (n < 1) throw std::invalid_argument("fake_world: n must be >= 1");
+  if (!dp) throw std::invalid_argument("fake_world: no data plane");
+  auto w = std::make_shared<HostWorld>(n, timeout_ms, std::move(dp));
   std::vector<std::unique_ptr<Comm>> out;
   for (int r = 0; r < n; ++r) out.push_back(std::make_unique<HostComm>(w, r));
   return out;
+}
+
+std::vector<std::unique_ptr<Comm>> host_world(int n, int timeout_ms) {
+  return fake_world(n, timeout_ms, std::make_shared<HostPlane>());
 }
 
 void host_kill(Comm& c, int rank) {

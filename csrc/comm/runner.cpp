@@ -70,9 +70,10 @@ PipelineResult Runner::run(const uint8_t* pool, int64_t pool_images, int64_t fir
     p.src = has_pool ? pool + (size_t)((step % nb) * per) * ib_ : nullptr;
     return p;
   };
-  auto on_result = [&](const StepPlan&, const int32_t* i, const float* pr) {
+  auto on_result = [&](const StepPlan& p, const int32_t* i, const float* pr) {
     last_idx_.assign(i, i + G);
     last_prob_.assign(pr, pr + G);
+    if (hook_) hook_(p.step, i, pr, G);
   };
   return run_pipeline({r_.get()}, first, n, plan, on_result, timeout_ms_, pipelined);
 }

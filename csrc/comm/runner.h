@@ -77,6 +77,11 @@ class Runner {
   int64_t global_batch() const;
   const std::vector<int32_t>& last_idx() const { return last_idx_; }
   const std::vector<float>& last_prob() const { return last_prob_; }
+  // Called on the coordinator with every step's gathered answers (step,
+  // idx, prob, global batch) as run() commits them (tests: every step, not
+  // only the last, is checked).
+  using StepHook = std::function<void(int64_t step, const int32_t* idx, const float* prob, int64_t n)>;
+  void set_step_hook(StepHook h) { hook_ = std::move(h); }
 
  private:
   std::unique_ptr<Worker> w_;
@@ -90,6 +95,7 @@ class Runner {
   std::unique_ptr<Rank> r_;
   std::vector<int32_t> last_idx_;
   std::vector<float> last_prob_;
+  StepHook hook_;
 };
 
 }  // namespace dp
