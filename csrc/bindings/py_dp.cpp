@@ -329,8 +329,6 @@ py::dict dp_loopback_bench(std::vector<Engine*> engines, uintptr_t pool, int per
             auto c = run.calibrate(p, np, prime, calib_steps, calib_rounds, 0.05, [&](double x) { return ag(r, x); });
             if (r == 0) calib = c;
           }
-          int64_t first = prime + (calib_rounds > 0 ? calib.steps : 0);
-          (void)first;
           d.push_back(run.run(p, np, 1000, steps).steps);
           d.push_back(run.run(p, np, 1000 + steps, unpipelined, /*pipelined=*/false).steps);
           run.worker()->sync_all();

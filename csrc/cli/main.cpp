@@ -452,6 +452,7 @@ int run_node(const Args& a) {
     lc.bind_host = mc.bind_host;
     lc.replication = a.geti("rf", 4);
     lc.bg_ms = a.geti("bg-ms", 3000);
+    lc.standby_copy_ms = a.geti("standby-copy-ms", 250);
     lc.query_interval_ms = a.geti("query-interval-ms", 500);
     lc.query_batch = a.geti("query-batch", 1);
     lc.max_inflight = a.geti("max-inflight", 32);
@@ -525,7 +526,7 @@ int main(int argc, char** argv) {
     std::cout << "usage: dmlc-node [--host H] [--port P] [--leaders h:p,...] [--workdir D] [--dataset D]\n"
                  "                 [--labels F] [--models name=path,...] [--executor auto|gpu|cpu] [--device N]\n"
                  "                 [--gpus N | --devices a,b,...] [--min-shard 32] [--lanes 2]\n"
-                 "                 [--rf 4] [--ping-ms 1000] [--fail-ms 3000] [--bg-ms 3000]\n"
+                 "                 [--rf 4] [--ping-ms 1000] [--fail-ms 3000] [--bg-ms 3000] [--standby-copy-ms 250]\n"
                  "                 [--query-interval-ms 500] [--adaptive-window 0] [--query-batch 1] [--jobs resnet18,alexnet]\n"
                  "                 [--join h:p] [--daemon] [--stay] [--quiet-predictions] [--new-conn-per-query]\n"
                  "                 [--max-attempts 3]\n"

@@ -3,6 +3,7 @@
 #include "../runtime/trace.h"
 
 #include <dirent.h>
+#include <poll.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -13,6 +14,7 @@
 #include "../serve/shard.h"
 
 #include "common.h"
+#include "../comm/cv_wait.h"
 
 namespace dmlc {
 namespace ctl {
@@ -98,6 +100,7 @@ void MemberService::start(int base_port) {
   register_handlers();
   server_->start();
   checker_ = std::thread([this] { leader_check_loop(); });
+  if (!cfg_.leader_candidates.empty()) watcher_ = std::thread([this] { leader_watch_loop(); });
   replicator_ = std::thread([this] { replica_loop(); });
 }
 
@@ -218,6 +221,9 @@ void MemberService::stop() {
   if (stop_.exchange(true)) return;
   { std::lock_guard<std::mutex> g(rq_mu_); }  // a waiter is past its predicate check or asleep: no lost wakeup
   rq_cv_.notify_all();
+  { std::lock_guard<std::mutex> g(wake_mu_); }
+  wake_cv_.notify_all();
+  if (watcher_.joinable()) watcher_.join();
   if (replicator_.joinable()) replicator_.join();
   if (checker_.joinable()) checker_.join();
   if (prefetcher_.joinable()) prefetcher_.join();
@@ -511,8 +517,14 @@ bool MemberService::check_leader(const std::string& addr) {
 
 void MemberService::leader_check_loop() {
   while (!stop_.load()) {
-    for (int slept = 0; slept < cfg_.check_ms && !stop_.load(); slept += 50)
-      std::this_thread::sleep_for(std::chrono::milliseconds(50));
+    {
+      // one check period, or earlier when the watch saw the leader's connection close
+      std::unique_lock<std::mutex> lk(wake_mu_);
+      const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(cfg_.check_ms);
+      while (!wake_ && !stop_.load() && cv_wait_until(wake_cv_, lk, deadline) != std::cv_status::timeout) {
+      }
+      wake_ = false;
+    }
     if (stop_.load() || cfg_.leader_candidates.empty()) break;
     std::string cur = leader_address();
     if (check_leader(cur)) continue;
@@ -532,6 +544,49 @@ void MemberService::leader_check_loop() {
         break;
       }
     }
+  }
+}
+
+void MemberService::leader_watch_loop() {
+  // The reference finds a dead leader only by its periodic check
+  // (src/services.rs:527-545: one check period of detection on average, a
+  // whole one at worst). The check stays (it also catches a hung leader whose
+  // socket is open), but a crashed or stopped leader's kernel closes its
+  // sockets at once: an idle connection to it turns that close into an
+  // immediate check. A connection dropped for any other reason only costs one
+  // extra check.
+  while (!stop_.load()) {
+    const std::string cur = leader_address();
+    Fd fd;
+    try {
+      fd = tcp_connect(host_of(cur), leader_port(port_of(cur)), 1000);
+    } catch (const std::exception&) {
+    }
+    bool closed = false;
+    while (fd && !stop_.load() && leader_address() == cur) {
+      pollfd p{fd.get(), POLLIN | POLLRDHUP, 0};
+      const int r = ::poll(&p, 1, 100);
+      if (r < 0 && errno != EINTR) break;
+      if (r > 0) {  // the leader never writes on this connection: readable = closed or reset
+        closed = true;
+        break;
+      }
+    }
+    if (stop_.load()) break;
+    // Only the close of an established connection wakes the checker: a leader
+    // not reachable yet (nodes still starting) is left to the periodic check,
+    // as in the reference, so the pointer never moves off a leader that is
+    // still coming up.
+    if (closed) {
+      {
+        std::lock_guard<std::mutex> g(wake_mu_);
+        wake_ = true;
+      }
+      wake_cv_.notify_all();
+    }
+    if (!fd || closed)  // no reconnect storm at an unreachable leader
+      for (int i = 0; i < 4 && !stop_.load() && leader_address() == cur; ++i)
+        std::this_thread::sleep_for(std::chrono::milliseconds(50));
   }
 }
 

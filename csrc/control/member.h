@@ -112,6 +112,7 @@ class MemberService {
   std::string query_image(const std::string& id) const;
   void register_handlers();
   void leader_check_loop();
+  void leader_watch_loop();
   bool check_leader(const std::string& addr);
 
   MemberConfig cfg_;
@@ -126,6 +127,13 @@ class MemberService {
   std::string leader_;
   std::atomic<bool> stop_{false};
   std::thread checker_;
+  // Leader watch: an idle TCP connection to the current leader's RPC port
+  // whose close (the leader's process died or stopped) wakes the checker at
+  // once instead of at its next period.
+  std::thread watcher_;
+  std::mutex wake_mu_;
+  std::condition_variable wake_cv_;
+  bool wake_ = false;  // under wake_mu_
   std::thread prefetcher_;
   std::atomic<bool> prefetching_{false};
   std::atomic<int> prefetched_{0};

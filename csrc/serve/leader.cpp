@@ -749,16 +749,37 @@ void LeaderService::assign_loop() {
 }
 
 void LeaderService::succession_loop() {
+  // The member's leader check (every bg period, src/services.rs:527-545) moves
+  // the leader pointer; a standby that finds itself pointed at takes over at
+  // once (the pointer is a local read, polled every 50 ms) instead of at its
+  // own next bg tick, which added up to a whole further period to a
+  // coordinator fail-over (5.5 s mean with the reference's periods, trials of
+  // 3.3-6.8 s: profiles/r5_recovery_refperiods_leader_before.json). The
+  // standby copy of the job state runs every standby_copy_ms.
   std::string last = member_->leader_address();
+  const auto copy_period = std::chrono::milliseconds(std::max(50, cfg_.standby_copy_ms));
+  auto next_copy = std::chrono::steady_clock::now() + copy_period;
   while (!stop_.load()) {
-    sleep_bg();
+    std::this_thread::sleep_for(std::chrono::milliseconds(50));
     if (stop_.load()) break;
     const std::string leader = member_->leader_address();
-    if (last != self_ && leader == self_) {
+    const bool took_over = last != self_ && leader == self_;
+    if (!took_over && std::chrono::steady_clock::now() < next_copy) {
+      last = leader;
+      continue;
+    }
+    next_copy = std::chrono::steady_clock::now() + copy_period;
+    if (took_over) {
       bool resume;
       {
         std::lock_guard<std::mutex> g(mu_);
         resume = !jobs_.empty() && !jobs_[0].durations_us.empty();
+      }
+      {
+        // the previous leader's node was unreachable (that is what moved the
+        // pointer): no queries to its member until membership has decided
+        std::lock_guard<std::mutex> g(rng_mu_);
+        bench_until_[last] = steady_us() + (int64_t)cfg_.bg_ms * 1000;
       }
       DMLC_LOG_WARN("became leader" << (resume ? "; resuming jobs" : ""));
       if (resume) predict();

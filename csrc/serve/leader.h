@@ -46,6 +46,11 @@ struct LeaderConfig {
   std::string bind_host = "0.0.0.0";
   int replication = 4;
   int bg_ms = 3000;
+  // A standby copies the leader's job progress this often (incremental: the
+  // queries completed since its last copy). The reference copies at its
+  // background period; answers completed after the last copy are redone by a
+  // successor, and show up as part of the fail-over gap.
+  int standby_copy_ms = 250;
   int query_interval_ms = 500;
   int query_batch = 1;
   int max_inflight = 32;

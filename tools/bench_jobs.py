@@ -205,8 +205,11 @@ def main():
            # (dmlc-node flags; the reference's are 1 s pings / 1 s detector, a 3 s
            # failure timeout and 3 s loops: src/membership.rs:230,273,289;
            # src/services.rs:188,201,213,529)
-           "periods_ms": ({"ping": 200, "detect": 200, "fail": 1200, "bg": 500} if a.fast_periods else
-                          {"ping": 1000, "detect": 1000, "fail": 3000, "bg": 3000}),
+           # (standby_copy: the standby leader's job-state copy, --standby-copy-ms;
+           # the reference copies at its 3 s loop period)
+           "periods_ms": ({"ping": 200, "detect": 200, "fail": 1200, "bg": 500, "standby_copy": 250}
+                          if a.fast_periods else
+                          {"ping": 1000, "detect": 1000, "fail": 3000, "bg": 3000, "standby_copy": 250}),
            "kill": a.kill,
            "reference": REF, "jobs": []}
     for j in jobs:

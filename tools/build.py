@@ -182,8 +182,10 @@ def build(jobs: int = 8, verbose: bool = False, node: bool = True) -> None:
             o = os.path.join(OBJ, "tsan_" + os.path.relpath(s, CSRC).replace(os.sep, "_") + ".o")
             tsan_objs.append(o)
             if _stale(o, [s], hdr):
+                # (DMLC_TSAN: timed condition waits on the system clock, which
+                # GCC 11's TSan intercepts: csrc/comm/cv_wait.h)
                 steps.append(["g++", "-O1", "-g", "-std=c++17", "-fPIC", "-fsanitize=thread", "-pthread",
-                              "-DDMLC_NO_ROCTX", "-c", s, "-o", o])
+                              "-DDMLC_NO_ROCTX", "-DDMLC_TSAN", "-c", s, "-o", o])
 
     # ---- 5. AddressSanitizer + UBSan builds: the node (same sources as the
     # TSan build) and the parser fuzzer (csrc/cli/fuzz.cpp)

@@ -63,6 +63,10 @@ def main():
                "std_s": round(statistics.stdev(xs), 3) if len(xs) > 1 else None,
                "reference": {"mean_s": ref_mean, "std_s": ref_std, "trials": ref_trials,
                              "source": "CS425MP4Report.pdf p.3 (10 VMs)"},
+               "mechanisms": "a member's idle TCP watch on the leader's RPC port wakes its leader check as soon "
+                             "as the leader's connections close (a crashed process); the new leader benches the "
+                             "old one's member at take-over; standby job-state copies every 250 ms "
+                             "(csrc/control/member.cpp leader_watch_loop, csrc/serve/leader.cpp succession_loop)",
                "runs": runs}
         path = os.path.join(a.out_dir, f"{a.tag}_{kind}.json")
         with open(path, "w") as f:
