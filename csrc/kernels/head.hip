@@ -75,9 +75,15 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   constexpr int kIPW = IPW;
   const int C = a.C;
-  const int ldp = C + 8;  // pooled row stride (elements): rows 16 B apart in bank space
+  // pooled row stride (elements): C + 16, rows 32 B apart in bank space, so
+  // the fc's fragment reads (lane: image lane & 15, 16-B chunk lane >> 4) are
+  // conflict free for 4 and for 16 images (C + 8 was 2-way at 16;
+  // tests/test_layouts_cpu.py::test_head_lds_layout)
+  const int ldp = C + 16;
   bf16* pooled = (bf16*)smem;                                // [kIPW][ldp]
-  float* lg = (float*)(smem + kIPW * ldp * 2);  // [kIPW][tiles_per_split*16]
+  // logits of the split: row stride nsplit + 4 floats, stored as one 16-B
+  // chunk per lane (the 8 lanes of a store group: 8 images at 4-dword steps)
+  float* lg = (float*)(smem + kIPW * ldp * 2);  // [kIPW][tiles_per_split*16 + 4]
   float* red = lg;  // pooling partials [TPG][kIPW][C] fp32 (dead before lg is written)
   const int g = blockIdx.x, split = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -89,6 +95,7 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
   // round trip less on the chain pool -> fc -> softmax -> merge
   const int col = lane & 15, kq = lane >> 4;
   const int nsplit = a.tiles_per_split * 16;
+  const int lgs = nsplit + 4;
   const int n_begin = split * nsplit;
   // (pooled input: its rows arrive in one batch of loads, and the prefetched
   // weights next to them spilled)
@@ -272,13 +279,14 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
         if (h == 1 && !two) break;
         const floatx4 acc = h ? acc1 : acc0;
         const int tt = t + 4 * h;
+        floatx4 v;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int n = n_begin + tt * 16 + kq * 4 + r;
-          const float v = acc[r] + bv[h][r];
-          if (n < a.N) a.logits[(long)(b0 + col) * a.N + n] = v;
-          lg[col * nsplit + tt * 16 + kq * 4 + r] = v;
+          v[r] = acc[r] + bv[h][r];
+          if (n < a.N) a.logits[(long)(b0 + col) * a.N + n] = v[r];
         }
+        *(floatx4*)(lg + col * lgs + tt * 16 + kq * 4) = v;
       }
     }
   }
@@ -296,7 +304,7 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
   int bi = 0x7fffffff;
   if (img_live)
     for (int n = n_begin + li; n < n_end; n += TPI) {
-      const float v = lg[im * nsplit + (n - n_begin)];
+      const float v = lg[im * lgs + (n - n_begin)];
       if (v > best) {
         best = v;
         bi = n;
@@ -312,7 +320,7 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
     }
   }
   if (img_live)
-    for (int n = n_begin + li; n < n_end; n += TPI) s += __expf(lg[im * nsplit + (n - n_begin)] - best);
+    for (int n = n_begin + li; n < n_end; n += TPI) s += __expf(lg[im * lgs + (n - n_begin)] - best);
 #pragma unroll
   for (int o = TPI / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
   if (a.NS == 1) {
@@ -435,8 +443,8 @@ void head_fused(const void* x, const void* w, const float* bias, int B, int HW, 
   a.ko = 0;
   a.scale = scale;
   const int c8 = C / 8, tpg = c8 >= 256 ? 1 : c8 >= 128 ? 2 : c8 >= 64 ? 4 : 8;
-  const size_t lds = (size_t)kIPW * (C + 8) * 2 +
-                     std::max((size_t)kIPW * a.tiles_per_split * 16 * 4, (size_t)tpg * kIPW * C * 4);
+  const size_t lds = (size_t)kIPW * (C + 16) * 2 +
+                     std::max((size_t)kIPW * (a.tiles_per_split * 16 + 4) * 4, (size_t)tpg * kIPW * C * 4);
   if (lds > 160 * 1024) throw std::invalid_argument("head_fused: LDS budget exceeded");
   if (in_fp8) {  // ResNet50 e4m3: the last bottleneck's output pooled straight from e4m3
     if (tpg != 1) throw std::invalid_argument("head_fused: e4m3 input needs C >= 2048");
@@ -484,7 +492,7 @@ void head_pooled(const void* pooled, const void* w, const float* bias, int B, in
   a.N = N;
   a.ldw = ldw;
   a.ko = ko;
-  const size_t lds = (size_t)ipw * (C + 8) * 2 + (size_t)ipw * a.tiles_per_split * 16 * 4;
+  const size_t lds = (size_t)ipw * (C + 16) * 2 + (size_t)ipw * (a.tiles_per_split * 16 + 4) * 4;
   if (lds > 160 * 1024) throw std::invalid_argument("head_pooled: LDS budget exceeded");
   hipLaunchKernelGGL((head_kernel<1, kIPWPooled, true>), dim3(groups, ns), dim3(256), lds, s, a);
   DMLC_HIP_CHECK(hipGetLastError());

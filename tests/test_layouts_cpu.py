@@ -567,3 +567,153 @@ def test_stream8_stride2_lds_layout(H, CI, HS):
                                 if l in live:
                                     slots.setdefault((addr[l] // 16) % 16, set()).add(addr[l])
                             assert all(len(v) == 1 for v in slots.values()), (part, tap, cc, f)
+
+
+def _b32_store_ways(addr, groups=((0, 32), (32, 64))):
+    """ds_write_b16/b32: two 32-lane groups, bank (a/4) mod 32; lanes on one
+    dword (the two halves of a b16 pair) are one access."""
+    worst = 1
+    for lo, hi in groups:
+        banks = {}
+        for l in range(lo, hi):
+            banks.setdefault((addr[l] // 4) % 32, set()).add(addr[l] // 4)
+        worst = max(worst, max(len(v) for v in banks.values()))
+    return worst
+
+
+def test_stem_hpool_store_layout():
+    """stem_pool.hip hpool_packed: lane (fr, g) of column fragment f stores
+    channel 16n + fr of pooled columns 8f + 2g (low half) and 8f + 2g + 1
+    (high half, +kHpCol) at hbase = g*2*kHpCol + (fr>>3)*16 + (fr&7)*2 plus
+    the immediates f*8*kHpCol + n*32. Every (pooled column, channel) of a
+    pooled conv row is written exactly once, at pw*kHpCol + 2c, which is
+    where the vertical max reads 16-B channel chunks; no ds_write_b16 of the
+    epilogue has two distinct dwords on one bank (4 row groups 288 B = 8
+    banks apart)."""
+    kHpCol, PW, NF, NB = 144, 56, 7, 4
+    seen = {}
+    for f in range(NF):
+        for n in range(NB):
+            for hi in range(2):
+                addr = []
+                for l in range(64):
+                    fr, g = l & 15, l >> 4
+                    a = g * 2 * kHpCol + (fr >> 3) * 16 + (fr & 7) * 2 + f * 8 * kHpCol + n * 32 + hi * kHpCol
+                    pw, c = 8 * f + 2 * g + hi, 16 * n + fr
+                    assert a == pw * kHpCol + 2 * c
+                    assert (pw, c) not in seen
+                    seen[(pw, c)] = a
+                    addr.append(a)
+                assert _b32_store_ways(addr) == 1, (f, n, hi)
+    assert set(seen) == {(pw, c) for pw in range(PW) for c in range(64)}
+    assert max(seen.values()) + 2 <= PW * kHpCol  # inside one pooled row
+
+
+def test_stem_vertical_max_reads():
+    """stem_pool.hip vertical 3-max (helper waves, 256 threads): item it ->
+    pooled row pr = it >= per_row, column pw, channel chunk cg, 16-B reads at
+    pw*kHpCol + cg*16 of three conv rows; the items of the two pooled rows
+    cover every (pw, cg) once each, a wave never straddles the two rows, and
+    the reads are 2-way bank conflicted (8 columns of 144 B per 16-lane
+    group), pinned here: on the helper waves, off the MFMA waves' path
+    (profiles/r4_stem_roles.txt: the helpers finish inside the MFMA phase)."""
+    kHpCol, PW = 144, 56
+    per_row = PW * 8
+    assert per_row % 64 == 0
+    items = set()
+    worst = 1
+    for j in range(4):
+        for w in range(4):
+            addr = []
+            for l in range(64):
+                it = w * 64 + l + j * 256
+                if it >= 2 * per_row:
+                    addr.append(None)
+                    continue
+                pr = it >= per_row
+                rem = it - pr * per_row
+                pw, cg = rem >> 3, rem & 7
+                items.add((pr, pw, cg))
+                addr.append(pw * kHpCol + cg * 16)
+            live = [a for a in addr if a is not None]
+            if live:
+                worst = max(worst, _b128_ways([a if a is not None else live[0] for a in addr]))
+    assert items == {(pr, pw, cg) for pr in range(2) for pw in range(PW) for cg in range(8)}
+    assert worst == 2
+
+
+def test_stem_convert_store_layout():
+    """stem_pool.hip convert_rows (helpers): item it = (row, k) writes paired
+    chunks 4k .. 4k+3 of its row (16 B each: pixels 8k-3+2q, 8k-2+2q as
+    [r g b r g b 0 0]); every chunk of the rows converted is written exactly
+    once and holds the pixel pair the MFMA waves' window reads (chunk p =
+    padded pixels 2p, 2p+1, padded column = image column + 3). The
+    ds_write_b128 stores are 4-way bank conflicted (64-B per-lane stride),
+    pinned here: helper waves, 8 stores per item."""
+    S = 224
+    need = ((112 - 1) * 6 + 26) // 3
+    Wr = ((max(S + 6, need)) + 7) // 8 * 8
+    Wq = Wr // 2
+    G4 = (Wq + 3) // 4
+    RB = Wq * 16
+    rows = 8
+    written = {}
+    for it in range(rows * G4):
+        r, k = divmod(it, G4)
+        for q in range(4):
+            chunk = 4 * k + q
+            if chunk >= Wq:
+                continue
+            assert (r, chunk) not in written
+            # pixels of the chunk: ix = 8k - 3 + i for i = 2q, 2q + 1
+            written[(r, chunk)] = (8 * k - 3 + 2 * q, 8 * k - 3 + 2 * q + 1)
+    assert set(written) == {(r, c) for r in range(rows) for c in range(Wq)}
+    for (r, c), (p0, p1) in written.items():
+        assert (p0 + 3, p1 + 3) == (2 * c, 2 * c + 1)  # padded columns of pair chunk c
+    worst = 1
+    for t0 in range(0, rows * G4, 64):
+        for q in range(4):
+            addr = []
+            for l in range(64):
+                it = min(t0 + l, rows * G4 - 1)
+                r, k = divmod(it, G4)
+                addr.append((r % 13) * RB + (4 * k + q) * 16)
+            banks = {}
+            for grp in [list(range(i, i + 8)) for i in range(0, 64, 8)]:  # ds_write_b128: 8 x 8 contiguous
+                for l in grp:
+                    banks.setdefault((grp[0], (addr[l] // 4) % 32), set()).add(addr[l])
+            worst = max(worst, max(len(v) for v in banks.values()))
+    assert worst <= 4, worst
+
+
+@pytest.mark.parametrize("C,ipw", [(512, 4), (512, 16), (2048, 16), (2048, 4)])
+def test_head_lds_layout(C, ipw):
+    """head.hip: pooled rows at a (C + 16)-element stride; the fc's B-operand
+    read (lane: image col = lane & 15, 16-B chunk kq = lane >> 4, K offset k)
+    is conflict free for every K step with 4 live images (head_fused) and 16
+    (head_pooled); the logits store (one 16-B chunk per lane at col*lgs +
+    16tt + 4kq, lgs = nsplit + 4) is conflict free in its 8-lane groups and
+    the per-image softmax reads (consecutive classes) cover each image's
+    split exactly."""
+    ldp = C + 16
+    for k in range(0, C, 32):
+        addr = []
+        for l in range(64):
+            col, kq = l & 15, l >> 4
+            addr.append(col * ldp * 2 + kq * 16 + 2 * k if col < ipw else None)
+        live = [a for a in addr if a is not None]
+        assert _b128_ways([a if a is not None else live[0] for a in addr]) == 1, k
+    for nsplit in (64, 128, 256, 1008):
+        lgs = nsplit + 4
+        for tt in range(0, nsplit // 16):
+            addr = [(l & 15) * lgs * 4 + (tt * 16 + (l >> 4) * 4) * 4 for l in range(64)]
+            for g0 in range(0, 64, 8):  # ds_write_b128: 8 x 8 contiguous, bank (a/4) mod 32
+                banks = {}
+                for l in range(g0, g0 + 8):
+                    if (l & 15) >= ipw:
+                        continue
+                    for d in range(4):
+                        banks.setdefault((addr[l] // 4 + d) % 32, set()).add(addr[l])
+                assert max((len(v) for v in banks.values()), default=1) == 1, (nsplit, tt, g0)
+        slots = {(l & 15, tt * 16 + (l >> 4) * 4 + r) for tt in range(nsplit // 16) for l in range(64) for r in range(4)}
+        assert slots == {(c, n) for c in range(16) for n in range(nsplit)}
