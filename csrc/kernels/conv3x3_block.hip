@@ -71,7 +71,7 @@ constexpr int kSteps = kH / kR + 2;    // 16
 // without waiting for the DMA too).
 // DBG (tools/block_bench.py knock-outs): bit 0 no x-row DMA in the loop, bit 1
 // no residual loads, bit 2 no y stores (results wrong, timing only)
-template <bool PROD, int PD, int DMA_KS, int DBG = 0>
+template <bool PROD, int PD, int DMA_KS, int DBG = 0, bool EP = false>
 __device__ __forceinline__ void block_role(const BlockArgs& a, char* xring, char* tring, int rw, int lane) {
   const int wm = rw & 1, wn = rw >> 1;
   const int fr = lane & 15, g = lane >> 4;
@@ -184,10 +184,16 @@ __device__ __forceinline__ void block_role(const BlockArgs& a, char* xring, char
         }
       }
       floatx4 acc[kMF][2];
+      // EP: the bias is the first MFMA's accumulator input (no zeroing, no
+      // bias adds in the epilogue)
+      const floatx4 bv[2] = {floatx4{bs[0][0], bs[0][1], bs[0][2], bs[0][3]},
+                             floatx4{bs[1][0], bs[1][1], bs[1][2], bs[1][3]}};
+      if constexpr (!EP) {
 #pragma unroll
-      for (int f = 0; f < kMF; ++f)
+        for (int f = 0; f < kMF; ++f)
 #pragma unroll
-        for (int nf = 0; nf < 2; ++nf) acc[f][nf] = floatx4{0.f, 0.f, 0.f, 0.f};
+          for (int nf = 0; nf < 2; ++nf) acc[f][nf] = floatx4{0.f, 0.f, 0.f, 0.f};
+      }
       bf16x8 xc[kMF], xn[kMF];
       auto load_k = [&](int ks, bf16x8* xd) __attribute__((always_inline)) {
         const int tap = ks >> 1, h = ks & 1;
@@ -211,7 +217,8 @@ __device__ __forceinline__ void block_role(const BlockArgs& a, char* xring, char
         for (int f = 0; f < kMF; ++f)
 #pragma unroll
           for (int nf = 0; nf < 2; ++nf)
-            acc[f][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wq[ks % PD][nf], xc[f], acc[f][nf], 0, 0, 0);
+            acc[f][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wq[ks % PD][nf], xc[f],
+                                                                 (EP && ks == 0) ? bv[nf] : acc[f][nf], 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
         if (ks + 1 < kKS) {
 #pragma unroll
@@ -219,6 +226,48 @@ __device__ __forceinline__ void block_role(const BlockArgs& a, char* xring, char
         }
       }
       // ---- epilogue: lane holds channels wn*32 + 8g .. +7 of pixel (row, col)
+      // EP: ~17 VALU per fragment instead of ~41 (the epilogues of both roles
+      // meet at the step barrier with the matrix cores idle, and an MFMA
+      // leaves its SIMD 8 of its 16 cycles for other vector instructions):
+      // bias already in the accumulators, the residual added from its bf16
+      // pairs by v_dot2c_f32_bf16 (x.lo * 1 + x.hi * 0: exact), ReLU and the
+      // padding rows' zeros on the packed bf16 words
+      if constexpr (EP) {
+        typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+        // (bf16 1.0 = 0x3f80 in the low / high half, kept in registers: the
+        // compiler turned the constant pair into the inline constant 1.0,
+        // which the hardware reads as the f32 bits 0x3f800000 = (0, 1))
+        uint32_t slo = 0x00003f80u, shi = 0x3f800000u;
+        asm volatile("" : "+v"(slo), "+v"(shi));
+        const bf16x2v sel_lo = __builtin_bit_cast(bf16x2v, slo), sel_hi = __builtin_bit_cast(bf16x2v, shi);
+#pragma unroll
+        for (int f = 0; f < kMF; ++f) {
+          const int p = wm * (kR * kW / 2) + 16 * f + fr;
+          float v[8];
+#pragma unroll
+          for (int nf = 0; nf < 2; ++nf)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[4 * nf + i] = acc[f][nf][i];
+          if constexpr (PROD) {
+            const int row = base + p / kW, col = p % kW;
+            const bool outside = (unsigned)row >= (unsigned)kH;
+            const int q = col + 1;
+            const uint4 pk = relu_bf16x8(pack8(v));
+            *(uint4*)(tring + ((row + kRing) % kRing) * kSlot + wn * kHalf + q * 64 + ((g ^ ((q >> 1) & 3)) << 4)) =
+                outside ? make_uint4(0, 0, 0, 0) : pk;
+          } else {
+            const uint32_t rw4[4] = {rres[f].x, rres[f].y, rres[f].z, rres[f].w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const bf16x2v rp = __builtin_bit_cast(bf16x2v, rw4[i]);
+              v[2 * i] = __builtin_amdgcn_fdot2_f32_bf16(rp, sel_lo, v[2 * i], false);
+              v[2 * i + 1] = __builtin_amdgcn_fdot2_f32_bf16(rp, sel_hi, v[2 * i + 1], false);
+            }
+            const uint4 pk = relu_bf16x8(pack8(v));
+            if (!(DBG & 4) || pk.x == 0x12345678u) *(uint4*)(a.y + obase + (long)p * kC + wn * 32 + 8 * g) = pk;
+          }
+        }
+      } else
 #pragma unroll
       for (int f = 0; f < kMF; ++f) {
         const int p = wm * (kR * kW / 2) + 16 * f + fr;
@@ -438,7 +487,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_block_ws_kernel(BlockArgs a) {
     block_role_ws<false>(a, xring, tring, wave & 3, lane);
 }
 
-template <int PD, int DMA_KS, int DBG = 0>
+template <int PD, int DMA_KS, int DBG = 0, bool EP = true>
 __global__ __launch_bounds__(512, 1) void conv3x3_block_kernel(BlockArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint4 smem[];
   char* xring = (char*)smem;
@@ -451,9 +500,9 @@ __global__ __launch_bounds__(512, 1) void conv3x3_block_kernel(BlockArgs a) {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   if (wave < 4)
-    block_role<true, PD, DMA_KS, DBG>(a, xring, tring, wave & 3, lane);
+    block_role<true, PD, DMA_KS, DBG, EP>(a, xring, tring, wave & 3, lane);
   else
-    block_role<false, PD, DMA_KS, DBG>(a, xring, tring, wave & 3, lane);
+    block_role<false, PD, DMA_KS, DBG, EP>(a, xring, tring, wave & 3, lane);
 }
 
 }  // namespace
@@ -478,12 +527,13 @@ void conv3x3_block(const void* x, const void* wf1, const float* bias1, const voi
   const size_t lds = (size_t)2 * kRing * kSlot;  // 148.5 KB
   // PD 6: 5 K steps of weight lookahead (PD 3 and a mid-step DMA measured
   // the same, 116-120 us at B=256); tools/block_bench.py
-  switch (dbg) {  // knock-outs / variants for tools/block_bench.py
+  switch (dbg) {  // knock-outs / variants for tools/block_bench.py (32: the round-4 epilogue, bias adds + unpacked residual)
     case 1: hipLaunchKernelGGL((conv3x3_block_kernel<6, 0, 1>), dim3(B), dim3(512), lds, s, a); break;
     case 2: hipLaunchKernelGGL((conv3x3_block_kernel<6, 0, 2>), dim3(B), dim3(512), lds, s, a); break;
     case 4: hipLaunchKernelGGL((conv3x3_block_kernel<6, 0, 4>), dim3(B), dim3(512), lds, s, a); break;
     case 7: hipLaunchKernelGGL((conv3x3_block_kernel<6, 0, 7>), dim3(B), dim3(512), lds, s, a); break;
     case 16: hipLaunchKernelGGL(conv3x3_block_ws_kernel, dim3(B), dim3(512), lds, s, a); break;
+    case 32: hipLaunchKernelGGL((conv3x3_block_kernel<6, 0, 0, false>), dim3(B), dim3(512), lds, s, a); break;
     default: hipLaunchKernelGGL((conv3x3_block_kernel<6, 0>), dim3(B), dim3(512), lds, s, a);
   }
   DMLC_HIP_CHECK(hipGetLastError());

@@ -290,11 +290,12 @@ __global__ __launch_bounds__(64 * NW, 1) void conv3x3_rows28_kernel(R28Args a) {
     // registers, the weights reused)
     auto pass = [&](auto fb_, auto fe_) __attribute__((always_inline)) {
       constexpr int FB = decltype(fb_)::value, FE = decltype(fe_)::value, PF = FE - FB;
-      floatx4 acc[PF][NF];
+      // the bias is the first MFMA's accumulator input (no zeroing, no bias
+      // adds in the epilogue, which with one wave per SIMD runs with the
+      // matrix core idle)
+      floatx4 acc[PF][NF], bv[NF];
 #pragma unroll
-      for (int f = 0; f < PF; ++f)
-#pragma unroll
-        for (int nf = 0; nf < NF; ++nf) acc[f][nf] = floatx4{0.f, 0.f, 0.f, 0.f};
+      for (int nf = 0; nf < NF; ++nf) bv[nf] = floatx4{bs[4 * nf], bs[4 * nf + 1], bs[4 * nf + 2], bs[4 * nf + 3]};
       bf16x8 xc[PF];
 #pragma unroll
       for (int f = 0; f < PF; ++f) xc[f] = xread(0, FB + f);
@@ -305,7 +306,7 @@ __global__ __launch_bounds__(64 * NW, 1) void conv3x3_rows28_kernel(R28Args a) {
           __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
           for (int nf = 0; nf < NF; ++nf)
-            acc[f][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[t][nf], xc[f], acc[f][nf], 0, 0, 0);
+            acc[f][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[t][nf], xc[f], t == 0 ? bv[nf] : acc[f][nf], 0, 0, 0);
           if (t + 1 < kKS && !(DBG & 2)) xc[f] = xread(t + 1, FB + f);
         }
       }
@@ -345,14 +346,25 @@ __global__ __launch_bounds__(64 * NW, 1) void conv3x3_rows28_kernel(R28Args a) {
 #pragma unroll
         for (int nf = 0; nf < NF; ++nf)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) v[4 * nf + i] = acc[f][nf][i] + bs[4 * nf + i];
+          for (int i = 0; i < 4; ++i) v[4 * nf + i] = acc[f][nf][i];
         const char* rp = resbuf + (16 * ff + fr) * 256 + (((4 * cg + g) ^ fr) << 4);
         if constexpr (NW == 4) {
           if constexpr (RES) {
-            float r[8];
-            unpack8(*(const uint4*)rp, r);
+            // residual bf16 pairs added by v_dot2c_f32_bf16 (pair . (1, 0) /
+            // (0, 1): exact), one VALU per channel instead of an unpack and
+            // an add; the selectors live in registers (as an inline constant
+            // the pair (1, 0) became f32 1.0 = (0, 1): conv3x3_block.hip)
+            typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+            uint32_t slo = 0x00003f80u, shi = 0x3f800000u;
+            asm volatile("" : "+v"(slo), "+v"(shi));
+            const uint4 rr = *(const uint4*)rp;
+            const uint32_t rw4[4] = {rr.x, rr.y, rr.z, rr.w};
 #pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] += r[e];
+            for (int i = 0; i < 4; ++i) {
+              const bf16x2v pr = __builtin_bit_cast(bf16x2v, rw4[i]);
+              v[2 * i] = __builtin_amdgcn_fdot2_f32_bf16(pr, __builtin_bit_cast(bf16x2v, slo), v[2 * i], false);
+              v[2 * i + 1] = __builtin_amdgcn_fdot2_f32_bf16(pr, __builtin_bit_cast(bf16x2v, shi), v[2 * i + 1], false);
+            }
           }
           if constexpr (OUT8) {
             float q[8];

@@ -355,7 +355,10 @@ def test_fused_pool_head_matches_unfused(gpu):
 def test_fused_block_matches_unfused(gpu):
     """ResNet18's layer1 blocks as one kernel each (conv3x3_block.hip) vs two
     row convs per block (options fused_block=False): same MFMA order and bf16
-    intermediate, so the logits are bit-identical."""
+    intermediate; the fused block starts its accumulators from the bias and
+    adds the residual by v_dot2c_f32_bf16 (rounding differently from the row
+    convs' bias-after / unpacked-residual epilogue, which the kernel test pins
+    bit for bit as variant 32), so the logits agree to bf16 rounding."""
     model = build("resnet18", seed=43, randomize_bn=True)
     sd = state_dict_f32(model)
     g = torch.Generator().manual_seed(44)
@@ -366,7 +369,9 @@ def test_fused_block_matches_unfused(gpu):
     ri, rp, rl = ref_eng.predict(img, return_logits=True)
     fi, fp, fl = eng.predict(img, return_logits=True)
     torch.cuda.synchronize()
-    assert torch.equal(fl, rl) and torch.equal(fi, ri)
+    rel = ((fl.float() - rl.float()).norm() / rl.float().norm()).item()
+    assert rel < 1e-2, rel
+    assert (fi == ri).float().mean().item() > 0.95
 
 
 @pytest.mark.parametrize("option", ["s2rows", "rows28", "ds_into_conv2"])

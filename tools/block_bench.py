@@ -50,7 +50,19 @@ def main():
     zero = ops._zero_page(dev)
     P = ops._ptr
 
+    ref = None
     for dbg in (int(d) for d in args.dbg.split(",")):
+        if dbg in (0, 16, 32):  # result-preserving variants: compare with the first one
+            C.conv3x3_block(P(x), P(wf1), P(b1), P(wf2), P(b2), P(y), P(zero), args.batch, ops._stream(), dbg)
+            torch.cuda.synchronize()
+            if ref is None:
+                ref = y.float().clone()
+            else:
+                d = (y.float() - ref).abs()
+                print(f"dbg={dbg}: max abs diff vs the first variant {d.max().item():.4g} "
+                      f"(max |ref| {ref.abs().max().item():.3g}, bf16 ulps differing "
+                      f"{(d > 0).float().mean().item() * 100:.3f}%)", flush=True)
+
         def block():
             for _ in range(args.reps):
                 C.conv3x3_block(P(x), P(wf1), P(b1), P(wf2), P(b2), P(y), P(zero), args.batch, ops._stream(), dbg)

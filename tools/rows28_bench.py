@@ -68,7 +68,8 @@ def main():
             ("stream", stream(None)), ("stream+res", stream(r))]
     if args.dbg:
         runs += [("no DMA", rows(None, 1)), ("no LDS rd", rows(None, 2)), ("no DMA wait", rows(None, 16)),
-                 ("DMA row 0", rows(None, 32)), ("prologue", rows(None, 8))]
+                 ("DMA row 0", rows(None, 32)), ("prologue", rows(None, 8)), ("no epilogue", rows(None, 4)),
+                 ("no DMA,LDS,epi", rows(None, 7))]
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from conv_bench import warm_gpu
     warm_gpu()
