@@ -135,7 +135,7 @@ struct StreamGeom {
 };
 
 template <int H, int W, int CI, int CO, int HS, int IMG, int NSP, int WM, int S, int ND, bool DS, bool WR,
-          int PD = 4, int NG = 1, int PRIO = 0, int CW = 0>
+          int PD = 4, int NG = 1, int PRIO = 0>
 __global__ __launch_bounds__(512, 1) void conv3x3_stream_kernel(StreamConvArgs a) {
   using G = StreamGeom<H, W, CI, HS, IMG, S, ND>;
   constexpr int BK = 32;                     // K-tile depth = one MFMA k-step
@@ -389,14 +389,9 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream_kernel(StreamConvArgs a
       // everything but the two weight reads just issued: the X fragments (read
       // during the previous K-tile) have landed. One wait instead of the
       // compiler's one per fragment.
-      // CW (register weights): a counted wait per fragment instead. The reads
-      // complete in order and fragment f's read has MF - 1 younger ones in
-      // flight when its MFMAs start (f + 1 .. MF - 1 of the previous tile,
-      // 0 .. f - 1 of this one), so the wave never drains its LDS queue.
-      if constexpr (!(WR && CW)) __builtin_amdgcn_s_waitcnt(0xC07F | ((WR ? 0 : NF) << 8));
+      __builtin_amdgcn_s_waitcnt(0xC07F | ((WR ? 0 : NF) << 8));
 #pragma unroll
       for (int f = 0; f < MF; ++f) {
-        if constexpr (WR && CW) __builtin_amdgcn_s_waitcnt(0xC07F | ((MF - 1) << 8));
 #pragma unroll
         for (int nf = 0; nf < NF; ++nf)
           acc[f][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(WR ? wq[cc % PD][nf] : wf[nf], xf[f], acc[f][nf], 0, 0,
@@ -432,10 +427,9 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream_kernel(StreamConvArgs a
       const int cn = cc + 1 == CT ? 0 : cc + 1;
       bf16x8 wn[NF];
       if constexpr (!WR) wread(wn, st1);
-      if constexpr (!(WR && CW)) __builtin_amdgcn_s_waitcnt(0xC07F | ((WR ? 0 : NF) << 8));
+      __builtin_amdgcn_s_waitcnt(0xC07F | ((WR ? 0 : NF) << 8));
 #pragma unroll
       for (int f = 0; f < MF; ++f) {
-        if constexpr (WR && CW) __builtin_amdgcn_s_waitcnt(0xC07F | ((MF - 1) << 8));
 #pragma unroll
         for (int nf = 0; nf < NF; ++nf)
           accd[f][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(WR ? wq[cc % PD][nf] : wf[nf], xf[f], accd[f][nf], 0,
@@ -595,7 +589,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream_kernel(StreamConvArgs a
 }
 
 template <int H, int W, int CI, int CO, int HS, int IMG, int NSP, int WM, int S, bool WR = false, int PD = 4,
-          int NG = 1, int PRIO = 0, int CW = 0>
+          int NG = 1, int PRIO = 0>
 void launch_stream(const StreamConvArgs& a, hipStream_t s) {
   using G = StreamGeom<H, W, CI, HS, IMG, S, 3>;
   constexpr size_t lds = WR ? (size_t)G::XBYTES : G::LDS;
@@ -604,12 +598,12 @@ void launch_stream(const StreamConvArgs& a, hipStream_t s) {
   if constexpr (WR) {
     if constexpr (S == 2) {
       if (a.yd) {
-        hipLaunchKernelGGL((conv3x3_stream_kernel<H, W, CI, CO, HS, IMG, NSP, WM, S, 3, true, true, PD, NG, PRIO, CW>),
+        hipLaunchKernelGGL((conv3x3_stream_kernel<H, W, CI, CO, HS, IMG, NSP, WM, S, 3, true, true, PD, NG, PRIO>),
                            dim3(grid), dim3(512), lds, s, a);
         return;
       }
     }
-      hipLaunchKernelGGL((conv3x3_stream_kernel<H, W, CI, CO, HS, IMG, NSP, WM, S, 3, false, true, PD, NG, PRIO, CW>),
+      hipLaunchKernelGGL((conv3x3_stream_kernel<H, W, CI, CO, HS, IMG, NSP, WM, S, 3, false, true, PD, NG, PRIO>),
                          dim3(grid), dim3(512), lds, s, a);
     return;
   } else {
@@ -631,8 +625,7 @@ void launch_stream(const StreamConvArgs& a, hipStream_t s) {
 // per wave (NG 2); 4 = the stride-2 14x14x256 one with one (NG 1, half the
 // channels per workgroup); 8 = the 7x7x512 stride-1 register-weight kernel
 // with an 8-deep weight ring (16 deep spills); 32 = waves 4-7 at priority 1 in
-// the register-weight kernels of layers 3-4; 64 = counted per-fragment LDS
-// waits in the register-weight kernels (CW).
+// the register-weight kernels of layers 3-4.
 std::atomic<int> g_stream_variant{0};
 
 }  // namespace
@@ -721,8 +714,6 @@ void conv3x3_stream(const void* x, const void* w, const float* bias, const void*
   else if (stride == 1 && Cin == 256 && wfrag) {  // layer3, register weights, 2 pixel halves x 4 groups of 64 channels
     if (g_stream_variant & 1)
       launch_stream<14, 14, 256, 256, 14, 1, 1, 2, 1, true, 2, 2>(a, s);
-    else if (g_stream_variant & 64)
-      launch_stream<14, 14, 256, 256, 14, 1, 1, 2, 1, true, 2, 2, 0, 1>(a, s);
     else if (g_stream_variant & 32)
       launch_stream<14, 14, 256, 256, 14, 1, 1, 2, 1, true, 4, 2, 1>(a, s);
     else
@@ -735,8 +726,6 @@ void conv3x3_stream(const void* x, const void* w, const float* bias, const void*
     // pixel halves 58.7 us, 1 image x 8 groups 60.9 us vs 53.0 us)
     if (g_stream_variant & 8)
       launch_stream<7, 7, 512, 512, 7, 2, 2, 1, 1, true, 8>(a, s);
-    else if (g_stream_variant & 64)
-      launch_stream<7, 7, 512, 512, 7, 2, 2, 1, 1, true, 4, 1, 0, 1>(a, s);
     else if (g_stream_variant & 32)
       launch_stream<7, 7, 512, 512, 7, 2, 2, 1, 1, true, 4, 1, 1>(a, s);
     else
@@ -756,8 +745,6 @@ void conv3x3_stream(const void* x, const void* w, const float* bias, const void*
     // for the 7 of a half image): 50.7 vs 49.4 us at B = 256, not used
     if (g_stream_variant & 2)
       launch_stream<14, 14, 128, 256, 7, 1, 1, 2, 2, true, 4, 2>(a, s);
-    else if (g_stream_variant & 64)
-      launch_stream<14, 14, 128, 256, 7, 1, 1, 1, 2, true, 4, 1, 0, 1>(a, s);
     else
       launch_stream<14, 14, 128, 256, 7, 1, 1, 1, 2, true>(a, s);
   }
@@ -769,8 +756,6 @@ void conv3x3_stream(const void* x, const void* w, const float* bias, const void*
     // workgroup, 32 per wave (variant bit 4; profiles/r3_stream_s2_ng2.txt)
     if (g_stream_variant & 4)
       launch_stream<7, 7, 256, 512, 7, 1, 2, 1, 2, true>(a, s);
-    else if (g_stream_variant & 64)
-      launch_stream<7, 7, 256, 512, 7, 1, 1, 1, 2, true, 4, 2, 0, 1>(a, s);
     else if (g_stream_variant & 32)
       launch_stream<7, 7, 256, 512, 7, 1, 1, 1, 2, true, 4, 2, 1>(a, s);
     else

@@ -599,42 +599,6 @@ __global__ __launch_bounds__(512, 1) void stem_roles_kernel(StemArgs a) {
           bf16x8 xf[7];
 #pragma unroll
           for (int s = 0; s < 7; ++s) xf[s] = *(const bf16x8*)(rbase + rows[s]);
-          if constexpr ((V & 64) != 0) {
-            // Pooling epilogue one fragment behind: fragment f's 28 MFMAs
-            // are issued interleaved with fragment f-1's epilogue (VALU,
-            // row rotations, 16-bit LDS stores). In-order issue otherwise
-            // leaves the matrix core idle for the whole epilogue of every
-            // fragment: the role-split MFMA waves share no SIMD with another
-            // MFMA wave (28 of the stem's 90 us, profiles/r4_stem_roles.txt).
-            floatx4 acc[2][4];
-#pragma unroll
-            for (int f = 0; f <= NF; ++f) {
-              if (f < NF) {
-#pragma unroll
-                for (int n = 0; n < 4; ++n) acc[f & 1][n] = floatx4{bs[n], bs[n], bs[n], bs[n]};
-#pragma unroll
-                for (int s = 0; s < 7; ++s)
-#pragma unroll
-                  for (int n = 0; n < 4; ++n)
-                    acc[f & 1][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[s], wf[n][s], acc[f & 1][n], 0, 0, 0);
-              }
-              if (f > 0) hpool_packed<4>(acc[(f - 1) & 1], prevq, lane, fq, hbase, f - 1, (f - 1) * 8 * kHpCol);
-              if (f + 1 < NF) {
-#pragma unroll
-                for (int s = 0; s < 7; ++s) xf[s] = *(const bf16x8*)(rbase + rows[s] + (f + 1) * 256);
-              }
-              if (f < NF && f > 0) {
-                // 28 MFMAs, each followed by up to 3 VALU ops of the epilogue
-                // and, every 4th, one of its 8 LDS stores
-#pragma unroll
-                for (int i = 0; i < 28; ++i) {
-                  __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                  __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
-                  if ((i & 3) == 3) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
-                }
-              }
-            }
-          } else {
 #pragma unroll
           for (int f = 0; f < NF; ++f) {
             floatx4 acc[4];  // starting from the bias (hpool_packed)
@@ -655,7 +619,6 @@ __global__ __launch_bounds__(512, 1) void stem_roles_kernel(StemArgs a) {
             } else {
               hpool_packed<4>(acc, prevq, lane, fq, hbase, f, f * 8 * kHpCol);
             }
-          }
           }
         }
       }
@@ -795,8 +758,6 @@ void stem_launch(const void* x, const uint8_t* u8, const void* w, const float* b
         DMLC_STEM_RV_CASE(36)
         DMLC_STEM_RV_CASE(52)
         DMLC_STEM_RV_CASE(40)
-        DMLC_STEM_RV_CASE(64)
-        DMLC_STEM_RV_CASE(65)
 #undef DMLC_STEM_RV_CASE
         default: throw std::invalid_argument("stem_conv_pool: unknown role-split variant");
       }
