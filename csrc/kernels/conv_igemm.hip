@@ -48,6 +48,15 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef const __attribute__((address_space(1))) void* gbl_ptr_t;
 
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+// e4m3 tiles: a lane's fragment is chunks 2fq and 2fq + 1 of its row, and
+// with the bf16 swizzle rows 0 and 4 of a 16-lane read group met on one bank
+// (45.7% of the fp8 kernel's LDS cycles were conflicts,
+// profiles/r5_roofline_resnet50_fp8.txt); (row >> 1) & 5 gives every group
+// of both reads 16 distinct bank slots (tests/test_layouts_cpu.py)
+template <bool IN8>
+__device__ __forceinline__ int swzk(int row, int chunk) {
+  return IN8 ? chunk ^ ((row >> 1) & 5) : swz(row, chunk);
+}
 
 typedef int v8i __attribute__((ext_vector_type(8)));
 __device__ __forceinline__ v8i cat8(uint4 lo, uint4 hi) {
@@ -168,7 +177,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a, int kt_p
 #pragma unroll
     for (int p = 0; p < PA; ++p) {
       const int r = wave * (BM / 4) + p * 8 + lrow;
-      const int lc = swz(r, pchunk);
+      const int lc = swzk<IN8>(r, pchunk);
       lcA[p] = lc;
       const int m = m0_ + r;
       if (m < M) {
@@ -195,7 +204,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a, int kt_p
 #pragma unroll
     for (int p = 0; p < PB; ++p) {
       const int r = wave * (BN / 4) + p * 8 + lrow;
-      wboff[p] = (n0_ + r) * a.Kpad + swz(r, pchunk) * CE;
+      wboff[p] = (n0_ + r) * a.Kpad + swzk<IN8>(r, pchunk) * CE;
     }
   };
   setup_rows(m0, n0);
@@ -255,12 +264,12 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a, int kt_p
 #pragma unroll
       for (int i = 0; i < TN; ++i) {
         const int r = wn * WTN + i * 16 + fr;
-        af[i] = cat8(sb[A_CH + r * 8 + swz(r, 2 * fq)], sb[A_CH + r * 8 + swz(r, 2 * fq + 1)]);
+        af[i] = cat8(sb[A_CH + r * 8 + swzk<IN8>(r, 2 * fq)], sb[A_CH + r * 8 + swzk<IN8>(r, 2 * fq + 1)]);
       }
 #pragma unroll
       for (int j = 0; j < TM; ++j) {
         const int r = wm * WTM + j * 16 + fr;
-        bm[j] = cat8(sb[r * 8 + swz(r, 2 * fq)], sb[r * 8 + swz(r, 2 * fq + 1)]);
+        bm[j] = cat8(sb[r * 8 + swzk<IN8>(r, 2 * fq)], sb[r * 8 + swzk<IN8>(r, 2 * fq + 1)]);
       }
 #pragma unroll
       for (int i = 0; i < TN; ++i)
@@ -275,12 +284,12 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a, int kt_p
 #pragma unroll
       for (int i = 0; i < TN; ++i) {
         const int r = wn * WTN + i * 16 + fr;
-        af[i] = __builtin_bit_cast(bf16x8, sb[A_CH + r * 8 + swz(r, ks * 4 + fq)]);
+        af[i] = __builtin_bit_cast(bf16x8, sb[A_CH + r * 8 + swzk<IN8>(r, ks * 4 + fq)]);
       }
 #pragma unroll
       for (int j = 0; j < TM; ++j) {
         const int r = wm * WTM + j * 16 + fr;
-        bm[j] = __builtin_bit_cast(bf16x8, sb[r * 8 + swz(r, ks * 4 + fq)]);
+        bm[j] = __builtin_bit_cast(bf16x8, sb[r * 8 + swzk<IN8>(r, ks * 4 + fq)]);
       }
 #pragma unroll
       for (int i = 0; i < TN; ++i)

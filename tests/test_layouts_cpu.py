@@ -717,3 +717,23 @@ def test_head_lds_layout(C, ipw):
                 assert max((len(v) for v in banks.values()), default=1) == 1, (nsplit, tt, g0)
         slots = {(l & 15, tt * 16 + (l >> 4) * 4 + r) for tt in range(nsplit // 16) for l in range(64) for r in range(4)}
         assert slots == {(c, n) for c in range(16) for n in range(nsplit)}
+
+
+@pytest.mark.parametrize("in8", [False, True])
+def test_igemm_fragment_reads_conflict_free(in8):
+    """conv_igemm.hip: 128-B LDS rows, physical chunk = logical ^ h(row) with
+    h = (row >> 1) & 7 (bf16: lane (fr, fq) reads chunk 4 ks + fq of row fr)
+    or (row >> 1) & 5 (e4m3: chunks 2 fq and 2 fq + 1, two reads); every
+    ds_read_b128 of a 16-row fragment is bank-conflict free (the e4m3 tiles
+    with the bf16 swizzle were 2-way: 45.7% conflict cycles measured)."""
+    h = (lambda r: (r >> 1) & 5) if in8 else (lambda r: (r >> 1) & 7)
+    reads = [(lambda fq, s=s: 2 * fq + s) for s in range(2)] if in8 else \
+        [(lambda fq, ks=ks: 4 * ks + fq) for ks in range(2)]
+    for base in (0, 16, 32, 48):  # fragments start at 16-row multiples
+        for rd in reads:
+            addr = []
+            for l in range(64):
+                fr, fq = l & 15, l >> 4
+                r = base + fr
+                addr.append(r * 128 + ((rd(fq) ^ h(r)) << 4))
+            assert _b128_ways(addr) == 1, (base, in8)
