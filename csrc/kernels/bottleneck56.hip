@@ -109,10 +109,7 @@ __device__ __forceinline__ uint32_t f32x4_to_fp8(const float* f) {
 }
 
 __device__ __forceinline__ void fp8x4_to_f32(uint32_t u, float* f) {
-  f[0] = __builtin_amdgcn_cvt_f32_fp8((int)u, 0);
-  f[1] = __builtin_amdgcn_cvt_f32_fp8((int)u, 1);
-  f[2] = __builtin_amdgcn_cvt_f32_fp8((int)u, 2);
-  f[3] = __builtin_amdgcn_cvt_f32_fp8((int)u, 3);
+  e4m3x4_to_f32(u, f);
 }
 
 // 16-B global load the compiler does not track: its wait is the kernel's own

@@ -19,6 +19,17 @@ __device__ __forceinline__ float bf2f(bf16 v) { return (float)v; }
 __device__ __forceinline__ bf16 f2bf(float v) { return (bf16)v; }  // v_cvt_pk_bf16_f32 (RNE)
 
 // Unpack / pack 8 bf16 held in a uint4 (16 B) register quad.
+// 4 e4m3 bytes -> 4 floats (exact) with the packed converts: two
+// v_cvt_pk_f32_fp8 (bytes 0-1, 2-3) instead of four v_cvt_f32_fp8
+__device__ __forceinline__ void e4m3x4_to_f32(uint32_t u, float* f) {
+  typedef float f32x2v __attribute__((ext_vector_type(2)));
+  const f32x2v lo = __builtin_amdgcn_cvt_pk_f32_fp8((int)u, false);
+  const f32x2v hi = __builtin_amdgcn_cvt_pk_f32_fp8((int)u, true);
+  f[0] = lo.x;
+  f[1] = lo.y;
+  f[2] = hi.x;
+  f[3] = hi.y;
+}
 __device__ __forceinline__ void unpack8(const uint4& u, float* f) {
   const uint32_t w[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll

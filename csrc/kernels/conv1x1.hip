@@ -65,10 +65,7 @@ __device__ __forceinline__ void pin(T& v) {
 
 
 __device__ __forceinline__ void fp8x4_to_f32(uint32_t u, float* f) {
-  f[0] = __builtin_amdgcn_cvt_f32_fp8((int)u, 0);
-  f[1] = __builtin_amdgcn_cvt_f32_fp8((int)u, 1);
-  f[2] = __builtin_amdgcn_cvt_f32_fp8((int)u, 2);
-  f[3] = __builtin_amdgcn_cvt_f32_fp8((int)u, 3);
+  e4m3x4_to_f32(u, f);
 }
 // values already within +-448
 __device__ __forceinline__ uint32_t f32x4_to_fp8_sat(const float* f) {

@@ -193,14 +193,8 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
               float f[8];
               if constexpr (FP8) {
                 const int lo8 = (int)v[pp][u].x, hi8 = (int)v[pp][u].y;
-                f[0] = __builtin_amdgcn_cvt_f32_fp8(lo8, 0);
-                f[1] = __builtin_amdgcn_cvt_f32_fp8(lo8, 1);
-                f[2] = __builtin_amdgcn_cvt_f32_fp8(lo8, 2);
-                f[3] = __builtin_amdgcn_cvt_f32_fp8(lo8, 3);
-                f[4] = __builtin_amdgcn_cvt_f32_fp8(hi8, 0);
-                f[5] = __builtin_amdgcn_cvt_f32_fp8(hi8, 1);
-                f[6] = __builtin_amdgcn_cvt_f32_fp8(hi8, 2);
-                f[7] = __builtin_amdgcn_cvt_f32_fp8(hi8, 3);
+                e4m3x4_to_f32((uint32_t)lo8, f);
+                e4m3x4_to_f32((uint32_t)hi8, f + 4);
               } else {
                 unpack8(v[pp][u], f);
               }

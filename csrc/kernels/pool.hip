@@ -73,14 +73,8 @@ __global__ __launch_bounds__(256) void avgpool_global_kernel(const void* __restr
         if (i < HW) {
           if constexpr (FP8) {
             const uint2 q = *(const uint2*)((const uint8_t*)xv + base + (long)i * C);
-            f[u][0] = __builtin_amdgcn_cvt_f32_fp8((int)q.x, 0);
-            f[u][1] = __builtin_amdgcn_cvt_f32_fp8((int)q.x, 1);
-            f[u][2] = __builtin_amdgcn_cvt_f32_fp8((int)q.x, 2);
-            f[u][3] = __builtin_amdgcn_cvt_f32_fp8((int)q.x, 3);
-            f[u][4] = __builtin_amdgcn_cvt_f32_fp8((int)q.y, 0);
-            f[u][5] = __builtin_amdgcn_cvt_f32_fp8((int)q.y, 1);
-            f[u][6] = __builtin_amdgcn_cvt_f32_fp8((int)q.y, 2);
-            f[u][7] = __builtin_amdgcn_cvt_f32_fp8((int)q.y, 3);
+            e4m3x4_to_f32((uint32_t)q.x, f[u]);
+            e4m3x4_to_f32((uint32_t)q.y, f[u] + 4);
           } else {
             unpack8(*(const uint4*)((const bf16*)xv + base + (long)i * C), f[u]);
           }
@@ -147,14 +141,8 @@ __global__ __launch_bounds__(256) void avgpool_rows_kernel(const void* __restric
       if (i < HW) {
         float f[8];
         if constexpr (FP8) {
-          f[0] = __builtin_amdgcn_cvt_f32_fp8((int)v[u].x, 0);
-          f[1] = __builtin_amdgcn_cvt_f32_fp8((int)v[u].x, 1);
-          f[2] = __builtin_amdgcn_cvt_f32_fp8((int)v[u].x, 2);
-          f[3] = __builtin_amdgcn_cvt_f32_fp8((int)v[u].x, 3);
-          f[4] = __builtin_amdgcn_cvt_f32_fp8((int)v[u].y, 0);
-          f[5] = __builtin_amdgcn_cvt_f32_fp8((int)v[u].y, 1);
-          f[6] = __builtin_amdgcn_cvt_f32_fp8((int)v[u].y, 2);
-          f[7] = __builtin_amdgcn_cvt_f32_fp8((int)v[u].y, 3);
+          e4m3x4_to_f32((uint32_t)v[u].x, f);
+          e4m3x4_to_f32((uint32_t)v[u].y, f + 4);
         } else {
           unpack8(v[u], f);
         }
