@@ -259,9 +259,15 @@ struct Compute {
       const int v = s0 + i * kSlot;
       return v >= kRing * kSlot ? v - kRing * kSlot : v;
     };
+    // the bias is the accumulators' starting value; ReLU on the packed bf16
+    float b2v[8];
+    load8(cst + 2 * kM + 32 * wn + 8 * g, b2v);
     floatx4 acc[kMF][2];
 #pragma unroll
-    for (int f = 0; f < kMF; ++f) acc[f][0] = acc[f][1] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int f = 0; f < kMF; ++f) {
+      acc[f][0] = floatx4{b2v[0], b2v[1], b2v[2], b2v[3]};
+      acc[f][1] = floatx4{b2v[4], b2v[5], b2v[6], b2v[7]};
+    }
     bf16x8 xc[kMF], xn[kMF];
     auto load_k = [&](int ks, bf16x8* xd) __attribute__((always_inline)) {
       const int tap = ks >> 1, h = ks & 1;
@@ -293,14 +299,12 @@ struct Compute {
         for (int f = 0; f < kMF; ++f) xc[f] = xn[f];
       }
     }
-    float b2v[8];
-    load8(cst + 2 * kM + 32 * wn + 8 * g, b2v);
 #pragma unroll
     for (int f = 0; f < kMF; ++f) {
       float v[8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = fmaxf(acc[f][e >> 2][e & 3] + b2v[e], 0.f);
-      *(uint4*)(t2 + t2_off(112 * wm + 16 * f + fr, 4 * wn + g)) = pack8(v);
+      for (int e = 0; e < 8; ++e) v[e] = acc[f][e >> 2][e & 3];
+      *(uint4*)(t2 + t2_off(112 * wm + 16 * f + fr, 4 * wn + g)) = relu_bf16x8(pack8(v));
     }
   }
 };
@@ -348,6 +352,24 @@ struct Memory {
           w3[P][ks][nf] =
               *(const bf16x8*)((const char*)a.wf3 + ((grp * 2 + ks) * 2 + nf0) * 1024 + ((g << 4) | r0) * 16);
         }
+    // 1 / s_y folded into the conv3 weights once (re-rounded to bf16), and
+    // the bias (x 1 / s_y) is the MFMAs' accumulator input: an output value
+    // is then one fma (the residual), one med3 and a quarter of a packed
+    // convert, where it was two fma (conv3 is K = 64: its epilogue is most
+    // of the kernel's VALU, which shares the SIMDs with the compute waves)
+    const float inv = a.out_inv_scale;
+#pragma unroll
+    for (int P = 0; P < 2; ++P)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int nf = 0; nf < 4; ++nf) {
+          float wv[8];
+          unpack8(__builtin_bit_cast(uint4, w3[P][ks][nf]), wv);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) wv[e] *= inv;
+          w3[P][ks][nf] = __builtin_bit_cast(bf16x8, pack8(wv));
+        }
   }
 
   // x rows 4j+1 .. 4j+4 (clamped into the image: rows outside it feed t1
@@ -389,10 +411,9 @@ struct Memory {
 #pragma unroll
     for (int P = 0; P < 2; ++P) {
       const int c3 = 128 * cb + 64 * P + 16 * g;  // this lane's 16 channels
-      // 1 / s_y folded into the bias and the residual scale: an output value
-      // is two fma, one med3 (ReLU and the e4m3 saturation) and a quarter of
-      // a packed convert (the memory waves' VALU shares the SIMDs with the
-      // compute waves' MFMAs)
+      // 1 / s_y folded into the weights (constructor), the bias and the
+      // residual scale: an output value is one fma, one med3 (ReLU and the
+      // e4m3 saturation) and a quarter of a packed convert
       const float inv = a.out_inv_scale, rsi = a.res_scale * inv;
       float b3v[16];
       load8(cst + 3 * kM + c3, b3v);
@@ -407,7 +428,8 @@ struct Memory {
         for (int ks = 0; ks < 2; ++ks) xt[ks] = *(const bf16x8*)(t2 + t2_off(p, 4 * ks + g));
         floatx4 acc[4];
 #pragma unroll
-        for (int nf = 0; nf < 4; ++nf) acc[nf] = floatx4{0.f, 0.f, 0.f, 0.f};
+        for (int nf = 0; nf < 4; ++nf)
+          acc[nf] = floatx4{b3v[4 * nf], b3v[4 * nf + 1], b3v[4 * nf + 2], b3v[4 * nf + 3]};
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -421,8 +443,7 @@ struct Memory {
           fp8x4_to_f32(rw[h], rf);
 #pragma unroll
           for (int i = 0; i < 4; ++i)
-            v[i] = __builtin_amdgcn_fmed3f(__builtin_fmaf(rf[i], rsi, __builtin_fmaf(acc[h][i], inv, b3v[4 * h + i])),
-                                           0.f, 448.f);
+            v[i] = __builtin_amdgcn_fmed3f(__builtin_fmaf(rf[i], rsi, acc[h][i]), 0.f, 448.f);
           q[h] = f32x4_to_fp8_sat(v);
         }
         if (!(a.dbg & 4))  // non-temporal y stores (L2 kept for the x re-reads); dbg bit 2: plain stores
