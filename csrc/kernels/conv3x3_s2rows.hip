@@ -173,9 +173,9 @@ __global__ __launch_bounds__(256, 1) void conv3x3_s2rows_kernel(S2Args a) {
 #pragma unroll
     for (int f = 0; f < kMF; ++f)
 #pragma unroll
-      for (int nf = 0; nf < 2; ++nf) {
-        acc[f][nf] = floatx4{0.f, 0.f, 0.f, 0.f};
-        accd[f][nf] = floatx4{0.f, 0.f, 0.f, 0.f};
+      for (int nf = 0; nf < 2; ++nf) {  // the biases are the accumulators' starting values
+        acc[f][nf] = floatx4{bs[4 * nf], bs[4 * nf + 1], bs[4 * nf + 2], bs[4 * nf + 3]};
+        if constexpr (DS) accd[f][nf] = floatx4{bsd[4 * nf], bsd[4 * nf + 1], bsd[4 * nf + 2], bsd[4 * nf + 3]};
       }
     // K step t: tap = t >> 1 (downsample steps: tap 4 = (1, 1)), K-half h = t & 1
     auto xread = [&](int t, int f) __attribute__((always_inline)) {
@@ -213,8 +213,8 @@ __global__ __launch_bounds__(256, 1) void conv3x3_s2rows_kernel(S2Args a) {
       for (int nf = 0; nf < 2; ++nf)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          v[4 * nf + i] = acc[f][nf][i] + bs[4 * nf + i];
-          vd[4 * nf + i] = accd[f][nf][i] + bsd[4 * nf + i];
+          v[4 * nf + i] = acc[f][nf][i];
+          vd[4 * nf + i] = DS ? accd[f][nf][i] : 0.f;
         }
       if (!(a.dbg & 2)) {
         *(uint4*)(a.y + o) = pack8_relu(v, a.relu);

@@ -135,11 +135,11 @@ __device__ __forceinline__ float rot_rows_down1(float x, int lane) {
 
 // Horizontal 3-max + ReLU of one output-column fragment in packed bf16 (the
 // bias is already in the accumulators: they start from it). Lane (r, g) holds
-// columns 16f + 4g + i (i = 0..3) of channel 16n + r. Rounding is monotone and
-// ReLU'd bf16 bits order as unsigned 16-bit integers, so round-then-max equals
-// the fp32 max-then-round: each block converts its 4 values (2 cvt + 2 ReLU),
-// pooled column 8f + 2g + 1 = max(v1, v2, v3) and 8f + 2g = max(v0, v1, nb)
-// come out of two packed u16 maxes over (v0, v1) | (v1, v2) | (nb, v3), and
+// columns 16f + 4g + i (i = 0..3) of channel 16n + r. Rounding is monotone,
+// so round-then-max equals the fp32 max-then-round: each block converts its 4
+// values (2 cvt), pooled column 8f + 2g + 1 = max(v1, v2, v3) and 8f + 2g =
+// max(v0, v1, nb) come out of two packed i16 maxes over (v0, v1) | (v1, v2) |
+// (nb, v3) and one ReLU, and
 // nb (column 16f + 4g - 1: v3 of row g - 1, of row 3 of fragment f-1 for g
 // = 0) moves between lanes as bf16 pairs, two channel blocks per row
 // rotation instead of one fp32 each. 0 is the neutral left pad (values >= 0).
@@ -149,17 +149,12 @@ __device__ __forceinline__ float rot_rows_down1(float x, int lane) {
 template <int NB>
 __device__ __forceinline__ void hpool_packed(const floatx4 (&acc)[NB], uint32_t (&prevq)[(NB + 1) / 2], int lane,
                                              int fq, uint32_t hbase, const int f, const int off) {
-  typedef unsigned short ushort2v __attribute__((ext_vector_type(2)));
   uint32_t p01[NB], p23[NB];
 #pragma unroll
-  for (int n = 0; n < NB; ++n) {
+  for (int n = 0; n < NB; ++n) {  // (no ReLU yet: see below)
     const float2v a = {acc[n][0], acc[n][1]}, b = {acc[n][2], acc[n][3]};
-    p01[n] = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(
-                                              __builtin_bit_cast(short2v, __builtin_convertvector(a, bf16x2)),
-                                              short2v{0, 0}));
-    p23[n] = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(
-                                              __builtin_bit_cast(short2v, __builtin_convertvector(b, bf16x2)),
-                                              short2v{0, 0}));
+    p01[n] = __builtin_bit_cast(uint32_t, __builtin_convertvector(a, bf16x2));
+    p23[n] = __builtin_bit_cast(uint32_t, __builtin_convertvector(b, bf16x2));
   }
   constexpr int NQ = (NB + 1) / 2;
   uint32_t r[NQ];
@@ -179,9 +174,18 @@ __device__ __forceinline__ void hpool_packed(const floatx4 (&acc)[NB], uint32_t 
     // carries its v3 in the high half)
     const uint32_t c = __builtin_amdgcn_perm(p23[n], r[n >> 1], (n & 1) || NB == 1 ? 0x07060302u : 0x07060100u);
     const uint32_t b12 = __builtin_amdgcn_alignbit(p23[n], p01[n], 16);  // (v1, v2)
-    const ushort2v m = __builtin_elementwise_max(
-        __builtin_elementwise_max(__builtin_bit_cast(ushort2v, p01[n]), __builtin_bit_cast(ushort2v, b12)),
-        __builtin_bit_cast(ushort2v, c));
+    // signed 16-bit max on the raw bf16 bits: exact whenever the window's
+    // maximum is >= 0 (non-negative bf16 order as int16 and above every
+    // negative one); when all three are negative it returns some negative
+    // value, which the ReLU after the max turns into 0 = relu(max) anyway.
+    // One ReLU per pair of pooled columns instead of two per block of four
+    // conv columns; the 0 left pad stays neutral (relu(max(0, a, b)) =
+    // relu(max(a, b)))
+    const short2v m = __builtin_elementwise_max(
+        __builtin_elementwise_max(
+            __builtin_elementwise_max(__builtin_bit_cast(short2v, p01[n]), __builtin_bit_cast(short2v, b12)),
+            __builtin_bit_cast(short2v, c)),
+        short2v{0, 0});
     const uint32_t packed = __builtin_bit_cast(uint32_t, m);
     ds_write_lo16(hbase, packed, off + n * 32);
     ds_write_hi16(hbase, packed, off + n * 32 + kHpCol);
