@@ -32,6 +32,7 @@
 #include "common.h"
 #include "kernels.h"
 
+#include <cstdlib>
 #include <type_traits>
 
 namespace dmlc {
@@ -111,11 +112,16 @@ __device__ __forceinline__ void vm_wait_plus(int n) {
 // read feeding one MFMA instead of two.
 // OUT8: e4m3 output (ResNet50's layer2 3x3 -> its e4m3 expand conv; NW = 4, no residual)
 // DSX: see R28Args::xds (4 waves, no residual operand: the downsample is the residual)
-template <bool RES, int DBG = 0, int AH = 1, int NW = 4, bool OUT8 = false, bool DSX = false>
+template <bool RES, int DBG = 0, int AH = 1, int NW = 4, bool OUT8 = false, bool DSX = false, bool R2 = true>
 __global__ __launch_bounds__(64 * NW, 1) void conv3x3_rows28_kernel(R28Args a) {
   static_assert(!OUT8 || (NW == 4 && !RES), "e4m3 output: the 4-wave form without residual");
   static_assert(!DSX || (NW == 4 && !RES && !OUT8 && AH == 1), "downsample K steps: the 4-wave bf16 form");
   constexpr int kDS = DSX ? 2 : 0;  // downsample K steps (64 input channels)
+  // RES2: the residual is DMA'd one step ahead into two LDS buffers, so the
+  // epilogue reads it with no wait and no workgroup barrier of its own (the
+  // previous step's end-of-step wait covered it)
+  constexpr bool RES2 = RES && AH == 1 && NW == 4 && R2;
+  constexpr int kRB2 = kResCh * 16;  // 28672 B per residual buffer
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
   constexpr int NF = NW == 4 ? 2 : 1;  // N fragments (16 channels) per wave
   constexpr int NT = 64 * NW;
@@ -174,7 +180,49 @@ __global__ __launch_bounds__(64 * NW, 1) void conv3x3_rows28_kernel(R28Args a) {
   if constexpr (DSX)
 #pragma unroll
     for (int e = 0; e < CPL; ++e) bs[e] += a.bds[ch0 + 8 * g + e];
+  // DSX: the downsample's input pixels x[2 (r0 + p / 28), 2 (p % 28)] of
+  // step s (128 B each) -> LDS buffer s & 1 [112 pixels][8 chunks], chunk c
+  // at physical c ^ (p & 7): the B-fragment reads of the 2 downsample K steps
+  // are conflict free (tests/test_layouts_cpu.py). DMA'd one step ahead, so
+  // the downsample K steps open a step's K loop with no wait of their own
+  constexpr int kDSB = kMF * 16 * 8 * 16;  // 14336 B per buffer
+  auto ds_dma = [&](int st) __attribute__((always_inline)) {
+    const bf16* ximg = a.xds + (long)b * (2 * kH) * (2 * kW) * 64;
+    const int r0s = st * kR;
+    char* dst = resbuf + (st & 1) * kDSB;
+    // (an opaque lane id: hoisted out of the step loop, the per-lane part of
+    // these addresses stayed live across the K loop and spilled)
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+#pragma unroll
+    for (int j = 0; j < (kMF * 16 * 8 + NT - 1) / NT; ++j) {
+      const int i0 = j * NT + wave * 64;
+      if (i0 < kMF * 16 * 8) {
+        const int i = i0 + ln;
+        const int p = i >> 3, c = (i & 7) ^ (p & 7);
+        const int yy = 2 * (r0s + p / kW), xx = 2 * (p % kW);
+        dma16(ximg + ((long)yy * (2 * kW) + xx) * 64 + 8 * c, dst + i0 * 16);
+      }
+    }
+  };
+  auto res_dma = [&](int st, char* dst) __attribute__((always_inline)) {
+    const bf16* rimg = a.res + ((long)b * kH + st * kR) * kW * kC;
+    int ln = lane;  // (opaque: see ds_dma)
+    asm volatile("" : "+v"(ln));
+#pragma unroll
+    for (int j = 0; j < (kResCh + NT - 1) / NT; ++j) {
+      const int i0 = j * NT + wave * 64;
+      if (i0 < kResCh) {  // (wave-uniform: kResCh is a multiple of 64)
+        const int i = i0 + ln;
+        const int p = i >> 4, c = i & 15;
+        dma16(rimg + (long)p * kC + 8 * (c ^ (p & 15)), dst + i0 * 16);
+      }
+    }
+  };
+  if constexpr (DSX) ds_dma(0);  // (older than the rows: the prologue's wait covers it)
+  if constexpr (RES2) res_dma(0, resbuf);
   for (int yy = 0; yy <= 4; ++yy) load_row(yy);
+  __builtin_amdgcn_sched_barrier(0);  // (the staging arithmetic is dead before the 304 weight registers load)
 
   // ---- per-lane constants: fragment f = tile pixels p = 16 f + fr (row
   // p / 28 of the step, column p % 28). col[f][kw]: in-row byte offset of
@@ -220,34 +268,12 @@ __global__ __launch_bounds__(64 * NW, 1) void conv3x3_rows28_kernel(R28Args a) {
     // physical chunk c ^ (p & 15), so the epilogue's reads are conflict free.
     // Issued before this step's row DMAs: its wait leaves those in flight.
     const long obase = ((long)b * kH + r0) * kW * kC + ch0 + 8 * g + 4 * nf0;
-    if constexpr (DSX) {
-      // the downsample's input pixels x[2 (r0 + p / 28), 2 (p % 28)] (128 B
-      // each) -> LDS [112 pixels][8 chunks], chunk c at physical c ^ (p & 7):
-      // the B-fragment reads of the 2 downsample K steps are conflict free
-      // (tests/test_layouts_cpu.py)
-      const bf16* ximg = a.xds + (long)b * (2 * kH) * (2 * kW) * 64;
-#pragma unroll
-      for (int j = 0; j < (kMF * 16 * 8 + NT - 1) / NT; ++j) {
-        const int i0 = j * NT + wave * 64;
-        if (i0 < kMF * 16 * 8) {
-          const int i = i0 + lane;
-          const int p = i >> 3, c = (i & 7) ^ (p & 7);
-          const int yy = 2 * (r0 + p / kW), xx = 2 * (p % kW);
-          dma16(ximg + ((long)yy * (2 * kW) + xx) * 64 + 8 * c, resbuf + i0 * 16);
-        }
-      }
-    }
-    if constexpr (RES) {
-      const bf16* rimg = a.res + ((long)b * kH + r0) * kW * kC;
-#pragma unroll
-      for (int j = 0; j < (kResCh + NT - 1) / NT; ++j) {
-        const int i0 = j * NT + wave * 64;
-        if (i0 < kResCh) {  // (wave-uniform: kResCh is a multiple of 64)
-          const int i = i0 + lane;
-          const int p = i >> 4, c = i & 15;
-          dma16(rimg + (long)p * kC + 8 * (c ^ (p & 15)), resbuf + i0 * 16);
-        }
-      }
+    if constexpr (DSX)  // the next step's downsample input (this step's landed during the last one)
+      if (step + 1 < kSteps) ds_dma(step + 1);
+    if constexpr (RES2) {  // the next step's residual
+      if (step + 1 < kSteps) res_dma(step + 1, resbuf + ((step + 1) & 1) * kRB2);
+    } else if constexpr (RES) {
+      res_dma(step, resbuf);
     }
     // rows of step + AH (step 0 also issues those of steps 1 .. AH - 1)
     int ndma = 0;
@@ -312,16 +338,16 @@ __global__ __launch_bounds__(64 * NW, 1) void conv3x3_rows28_kernel(R28Args a) {
       }
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (DSX) {
-        // this wave's downsample-input DMAs (older than this step's row DMAs)
-        // have landed, and everyone's; then the 2 downsample K steps
-        vm_wait<0>();
-        __builtin_amdgcn_s_barrier();
+        // the 2 downsample K steps on this step's x[2y, 2x], DMA'd during the
+        // previous step (its end-of-step wait and barrier covered it: no wait
+        // and no workgroup barrier here)
+        const char* dsb = resbuf + (step & 1) * kDSB;
 #pragma unroll
         for (int u = 0; u < kDS; ++u) {
 #pragma unroll
           for (int f = 0; f < PF; ++f) {
             const int p = 16 * (FB + f) + fr;
-            xc[f] = *(const bf16x8*)(resbuf + p * 128 + (((4 * u + g) ^ (p & 7)) << 4));
+            xc[f] = *(const bf16x8*)(dsb + p * 128 + (((4 * u + g) ^ (p & 7)) << 4));
           }
 #pragma unroll
           for (int f = 0; f < PF; ++f)
@@ -331,7 +357,7 @@ __global__ __launch_bounds__(64 * NW, 1) void conv3x3_rows28_kernel(R28Args a) {
         }
         __builtin_amdgcn_sched_barrier(0);
       }
-      if constexpr (RES && FB == 0) {  // this wave's residual DMAs (older than this step's row DMAs) have landed; and everyone's
+      if constexpr (RES && !RES2 && FB == 0) {  // this wave's residual DMAs (older than this step's row DMAs) have landed; and everyone's
         if (AH == 1 || step == 0)
           vm_wait<0>();
         else
@@ -347,7 +373,7 @@ __global__ __launch_bounds__(64 * NW, 1) void conv3x3_rows28_kernel(R28Args a) {
         for (int nf = 0; nf < NF; ++nf)
 #pragma unroll
           for (int i = 0; i < 4; ++i) v[4 * nf + i] = acc[f][nf][i];
-        const char* rp = resbuf + (16 * ff + fr) * 256 + (((4 * cg + g) ^ fr) << 4);
+        const char* rp = resbuf + (RES2 ? (step & 1) * kRB2 : 0) + (16 * ff + fr) * 256 + (((4 * cg + g) ^ fr) << 4);
         if constexpr (NW == 4) {
           if constexpr (RES) {
             // residual bf16 pairs added by v_dot2c_f32_bf16 (pair . (1, 0) /
@@ -440,7 +466,7 @@ void conv3x3_rows28(const void* x, const void* wf, const float* bias, const void
     a.xds = (const bf16*)xds;
     a.wds = (const bf16*)wds;
     a.bds = bds;
-    const size_t lds = (size_t)R28Ring<1>::kSlotsAlloc * kRB + (size_t)kMF * 16 * 128;
+    const size_t lds = (size_t)R28Ring<1>::kSlotsAlloc * kRB + 2 * (size_t)kMF * 16 * 128;  // two downsample-input buffers
     hipLaunchKernelGGL((conv3x3_rows28_kernel<false, 0, 1, 4, false, true>), dim3(B), dim3(256), lds, s, a);
     DMLC_HIP_CHECK(hipGetLastError());
     return;
@@ -465,9 +491,14 @@ void conv3x3_rows28(const void* x, const void* wf, const float* bias, const void
     return;
   }
   const int ah = (dbg == 64 || dbg == 65) ? 2 : 1;
+  // (the default residual form double-buffers the residual one step ahead)
+  // (DMLC_ROWS28_RES1=1: the round-4 single residual buffer, A/B)
+  static const bool res1 = getenv("DMLC_ROWS28_RES1") && atoi(getenv("DMLC_ROWS28_RES1"));
+  const bool res2 = res && ah == 1 && dbg != 129 && !res1;
   const size_t lds = (size_t)(ah == 2 ? R28Ring<2>::kSlotsAlloc : R28Ring<1>::kSlotsAlloc) * kRB +
-                     (res ? (size_t)kResCh * 16 : 0);  // 90 / 118 KB (two ahead: 123 / 151 KB)
+                     (res ? (size_t)(res2 ? 2 : 1) * kResCh * 16 : 0);  // 90 / 146 KB (two ahead: 123 / 151 KB)
   static_assert(R28Ring<2>::kSlotsAlloc * kRB + kResCh * 16 <= 160 * 1024, "LDS budget");
+  static_assert(R28Ring<1>::kSlotsAlloc * kRB + 2 * kResCh * 16 <= 160 * 1024, "LDS budget");
   switch (dbg) {
     case 64: hipLaunchKernelGGL((conv3x3_rows28_kernel<false, 0, 2>), dim3(B), dim3(256), lds, s, a); break;
     case 65: hipLaunchKernelGGL((conv3x3_rows28_kernel<true, 0, 2>), dim3(B), dim3(256), lds, s, a); break;
@@ -481,7 +512,9 @@ void conv3x3_rows28(const void* x, const void* wf, const float* bias, const void
     case 16: hipLaunchKernelGGL((conv3x3_rows28_kernel<false, 16>), dim3(B), dim3(256), lds, s, a); break;
     case 32: hipLaunchKernelGGL((conv3x3_rows28_kernel<false, 32>), dim3(B), dim3(256), lds, s, a); break;
     default:
-      if (res)
+      if (res && !res2)
+        hipLaunchKernelGGL((conv3x3_rows28_kernel<true, 0, 1, 4, false, false, false>), dim3(B), dim3(256), lds, s, a);
+      else if (res)
         hipLaunchKernelGGL(conv3x3_rows28_kernel<true>, dim3(B), dim3(256), lds, s, a);
       else
         hipLaunchKernelGGL(conv3x3_rows28_kernel<false>, dim3(B), dim3(256), lds, s, a);
