@@ -1,8 +1,9 @@
 // Direct 3x3 / stride 1 / pad 1 convolution on the block-scaled e4m3 MFMA
 // (v_mfma_scale_f32_16x16x128_f8f6f4, unit block scales), e4m3 in and out:
-// ResNet50's bottleneck 3x3 convs of layer3 (14x14x256) and layer4
-// (7x7x512), whose input t1 comes from the reduce 1x1 conv and whose output t2
-// feeds the e4m3 expand conv (resnet50_fp8, EngineOptions::fp8_3x3_in).
+// ResNet50's bottleneck 3x3 convs of layer2 (28x28x128), layer3 (14x14x256)
+// and layer4 (7x7x512), whose input t1 comes from the reduce 1x1 conv and
+// whose output t2 feeds the e4m3 expand conv (resnet50_fp8,
+// EngineOptions::fp8_3x3_in).
 //
 // Reference equivalent: Bottleneck.conv2 + bn2 + relu of tch::vision::resnet50
 // (BASELINE config 5: the model zoo path of src/services.rs:513-524, run per
@@ -25,7 +26,10 @@
 //    same half swap, so the dot product is unchanged): in every 16-lane
 //    group of a ds_read_b128 the 8 lanes of one fq read 8 distinct pairs and
 //    the two fq take opposite halves, so the reads are bank-conflict free
-//    (tests/test_layouts_cpu.py);
+//    (tests/test_layouts_cpu.py). 128-channel pixels (128 B, half a bank
+//    row) key the pair by (K >> 1) & 3 instead: K's parity picks the window
+//    half, and the 8 lanes of one fq (4 + 4 consecutive K, or 8) cover the 8
+//    values of K & 7 once;
 //  * epilogue: v = acc * alpha[n] + bias[n] (alpha = the per-channel e4m3
 //    weight scale x the input scale; t2's per-channel output scales are
 //    folded into both), ReLU, e4m3 (saturated at 448), 8 consecutive
@@ -52,15 +56,19 @@ struct Stream8Args {
 };
 
 // Geometry: output H x W, stride S; a workgroup owns HS output rows of one
-// image (PARTS = H / HS > 1, stride 2 only) or IMG whole images.
+// image (PARTS = H / HS > 1: stride 2, or two halves at stride 1) or IMG
+// whole images.
 template <int H, int W, int CI, int HS, int IMG, int S>
 struct Stream8Geom {
   static constexpr int PARTS = H / HS;
-  static_assert(PARTS == 1 || (IMG == 1 && S == 2), "strips: one image, stride 2");
+  static_assert(PARTS == 1 || IMG == 1, "strips: one image");
   static constexpr int HI = S * H, WI = S * W;   // input rows / columns
-  // staged rows: whole images, or the strip's input rows 2 r0 - 1 .. 2 (r0 +
-  // HS - 1) + 1 (stride 2 never reads below the image)
-  static constexpr int XR = PARTS == 1 ? IMG * HI : (S * (HS - 1) + 3 < HI ? S * (HS - 1) + 3 : HI);
+  // staged rows: whole images, the strip's input rows 2 r0 - 1 .. 2 (r0 +
+  // HS - 1) + 1 (stride 2 never reads below the image), or a strip and its
+  // halo rows inside the image (stride 1)
+  static constexpr int XR = PARTS == 1 ? IMG * HI
+                            : S == 1   ? HS + (PARTS > 2 ? 2 : 1)
+                                       : (S * (HS - 1) + 3 < HI ? S * (HS - 1) + 3 : HI);
   static constexpr int PXB = CI;                 // bytes per staged pixel
   static constexpr int ROWB = WI * PXB;
   static constexpr int ZB = XR * ROWB;           // the zero pixel
@@ -81,9 +89,10 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream8_kernel(Stream8Args a) 
   constexpr int KT = 9 * CT;                 // K-tiles
   constexpr int CPX = CI / 16;               // 16-B chunks per pixel
   static_assert(CO == 8 / WM * WN * NSP, "channel split");
-  static_assert(CI % 128 == 0 && CPX >= 16, "e4m3 pixels of >= 256 B (whole bank rows)");
-  static_assert(CT % PD == 0, "the ring slot of K-tile tap * CT + cc is cc % PD: compile-time register indices");
-  static_assert(G::CH % 64 == 0, "whole DMA instructions");
+  static_assert(CI % 128 == 0 && (CPX >= 16 || CPX == 8), "e4m3 pixels of 128 B or >= 256 B (whole bank rows)");
+  // ring slot of K-tile t = tap * CT + cc: cc % PD (tap loop rolled), or t % PD
+  // (CT = 1: the 9 taps unrolled): compile-time register indices either way
+  static_assert(CT == 1 || CT % PD == 0, "weight ring depth");
   static_assert(G::LDS <= 160 * 1024, "LDS budget");
   static_assert(S == 1 || (S == 2 && WI % 2 == 0), "stride");
 
@@ -102,6 +111,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream8_kernel(Stream8Args a) 
   const int npix = IMG == 1 ? NPIX : nimg * HS * W;
   const int ch0 = ns * (CO / NSP) + wc * WN;
   const uint8_t* img = a.x + (long)b * HI * WI * CI;
+  // chunk-pair key of staged pixel K (see the header)
+  auto pswz = [](int k) __attribute__((always_inline)) { return CPX >= 16 ? (k & 7) : ((k >> 1) & 3); };
 
   // ---- stage the input rows (one flat run of 16-B chunks; stride 2: each
   // row's even columns first, then its odd ones). The key K of a staged
@@ -123,9 +134,9 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream8_kernel(Stream8Args a) 
       const int ii = PARTS == 1 ? i / HI : 0, y = PARTS == 1 ? i - ii * HI : rs + i;
       K = ii * (H * W) + (((y + 1) >> 1) - r0) * W + ((x + 1) >> 1);
     }
-    const int lc = ((((pc >> 1) ^ (K & 7)) << 1) | (pc & 1));  // logical chunk at physical pc
+    const int lc = ((((pc >> 1) ^ pswz(K)) << 1) | (pc & 1));  // logical chunk at physical pc
     const uint8_t* src = i < nrows ? img + ((long)(rs + i) * WI + x) * CI + 16 * lc : a.zero;
-    dma16(src, xs + k0 * 16);
+    if (G::CH % 64 == 0 || ci < G::CH) dma16(src, xs + k0 * 16);
   }
   if (wave == 0 && lane < CPX) dma16(a.zero, xs + G::ZB);
 
@@ -166,8 +177,10 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream8_kernel(Stream8Args a) 
     for (int nf = 0; nf < NF; ++nf) acc[f][nf] = floatx4{0.f, 0.f, 0.f, 0.f};
 
   // tap (kh, kw): fragment bases xa[f]; lane offsets of the two reads: pair
-  // ((fq + 4 cc) ^ (K & 7)) with K = p + ktap (p & 15 == fr for real pixels),
-  // first the half fq & 1, then the other
+  // ((fq + 4 cc) ^ pswz(K)) with K = p + kb + ktap (p & 15 == fr for real
+  // pixels; kb: a stride-1 half image's staged rows start r0 - rs rows above
+  // its first output row), first the half fq & 1, then the other
+  const int kb = S == 1 ? (r0 - rs) * W : 0;
   int xa[MF], tsw0 = 0, tsw1 = 0;
   auto set_tap = [&](int tap) __attribute__((always_inline)) {
     const int kh = tap / 3, kw = tap - kh * 3;
@@ -178,7 +191,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream8_kernel(Stream8Args a) 
 #pragma unroll
     for (int f = 0; f < MF; ++f) xa[f] = (xoff[f] & tm) ? G::ZB : (xoff[f] & ~15) + toff;
     const int ktap = S == 1 ? (kh - 1) * W + (kw - 1) : (kh == 2 ? W : 0) + (kw == 2 ? 1 : 0);
-    const int u = fq ^ ((fr + ktap) & 7);
+    const int u = fq ^ pswz(fr + kb + ktap);
     tsw0 = (u << 5) | ((fq & 1) << 4);
     tsw1 = tsw0 ^ 16;
   };
@@ -195,30 +208,36 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream8_kernel(Stream8Args a) 
   v8i xf[MF];
 #pragma unroll
   for (int f = 0; f < MF; ++f) xf[f] = xread(f, 0);
-  for (int tap = 0; tap < 9; ++tap) {
+  // K-tile t = tap * CT + cc, its weights in ring slot `slot`
+  auto ktile = [&](const int tap, const int cc, const int slot) __attribute__((always_inline)) {
+    const int t = tap * CT + cc;
+    if (t + PD - 1 < KT)
 #pragma unroll
-    for (int cc = 0; cc < CT; ++cc) {
-      const int t = tap * CT + cc;
-      if (t + PD - 1 < KT)
+      for (int nf = 0; nf < NF; ++nf) wq[(slot + PD - 1) % PD][nf] = wfrag(t + PD - 1, nf);
+    if (cc + 1 == CT && tap + 1 < 9) set_tap(tap + 1);
+    const int cn = cc + 1 == CT ? 0 : cc + 1;
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // the X fragments read during the previous K-tile
 #pragma unroll
-        for (int nf = 0; nf < NF; ++nf) wq[(cc + PD - 1) % PD][nf] = wfrag(t + PD - 1, nf);
-      if (cc + 1 == CT && tap + 1 < 9) set_tap(tap + 1);
-      const int cn = cc + 1 == CT ? 0 : cc + 1;
-      __builtin_amdgcn_s_waitcnt(0xC07F);  // the X fragments read during the previous K-tile
+    for (int f = 0; f < MF; ++f) {
 #pragma unroll
-      for (int f = 0; f < MF; ++f) {
-#pragma unroll
-        for (int nf = 0; nf < NF; ++nf)
-          acc[f][nf] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(wq[cc % PD][nf], xf[f], acc[f][nf], 0, 0, 0,
-                                                                         127, 0, 127);
-        if (t + 1 < KT) xf[f] = xread(f, cn);
-      }
-#pragma unroll
-      for (int f = 0; f < MF; ++f) {
-        __builtin_amdgcn_sched_group_barrier(0x008, NF, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-      }
+      for (int nf = 0; nf < NF; ++nf)
+        acc[f][nf] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(wq[slot][nf], xf[f], acc[f][nf], 0, 0, 0, 127,
+                                                                       0, 127);
+      if (t + 1 < KT) xf[f] = xread(f, cn);
     }
+#pragma unroll
+    for (int f = 0; f < MF; ++f) {
+      __builtin_amdgcn_sched_group_barrier(0x008, NF, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+    }
+  };
+  if constexpr (CT == 1) {
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) ktile(tap, 0, tap % PD);
+  } else {
+    for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+      for (int cc = 0; cc < CT; ++cc) ktile(tap, cc, cc % PD);
   }
 
   // every MFMA done here: pinned, the compiler cannot sink the last K-tile's
@@ -278,9 +297,13 @@ void conv3x3_stream8_set_variant(int v) { g_stream8_variant = v; }
 
 bool conv3x3_stream8_supported(int Hin, int Win, int Cin, int Cout, int stride) {
   if (Cin != Cout) return false;
-  if (stride == 1) return (Hin == 14 && Win == 14 && Cin == 256) || (Hin == 7 && Win == 7 && Cin == 512);
-  // ResNet50 layer3.0 / layer4.0 conv2 (the bottleneck's strided 3x3)
-  if (stride == 2) return (Hin == 28 && Win == 28 && Cin == 256) || (Hin == 14 && Win == 14 && Cin == 512);
+  if (stride == 1)
+    return (Hin == 28 && Win == 28 && Cin == 128) || (Hin == 14 && Win == 14 && Cin == 256) ||
+           (Hin == 7 && Win == 7 && Cin == 512);
+  // ResNet50 layer2.0 / layer3.0 / layer4.0 conv2 (the bottleneck's strided 3x3)
+  if (stride == 2)
+    return (Hin == 56 && Win == 56 && Cin == 128) || (Hin == 28 && Win == 28 && Cin == 256) ||
+           (Hin == 14 && Win == 14 && Cin == 512);
   return false;
 }
 
@@ -314,19 +337,36 @@ void conv3x3_stream8(const void* x, const void* wf, const float* alpha, const fl
   a.relu = relu;
   a.out_inv_scale = out_inv_scale;
   const int v = g_stream8_variant;
-  if (stride == 2 && Cin == 256) {
+  if (stride == 2 && Cin == 128) {
+    // layer2.0.conv2 (56x56x128 -> 28x28): 4 output rows (9 staged rows of
+    // 128-B pixels = 63 KB; 104 VGPRs: two workgroups per CU, one's staging
+    // under the other's MFMAs) x all 128 channels, 4 pixel quarters x 2 groups
+    // of 64. Variant 4: 7-row strips (105 KB, 164 VGPRs, one per CU):
+    // 1927 vs 1923 us per resnet50_fp8 b256 forward (profiles/r5_stream8_layer2.txt)
+    if (v & 4)
+      launch8<28, 28, 128, 128, 7, 1, 1, 4, 2, 2, 2>(a, s);
+    else
+      launch8<28, 28, 128, 128, 4, 1, 1, 4, 2, 2, 2>(a, s);
+  } else if (stride == 2 && Cin == 256) {
     // layer3.0.conv2 (28x28x256 -> 14x14): half an image (7 output rows, 15
     // staged rows = 105 KB) x all 256 channels, 8 groups of 32
     launch8<14, 14, 256, 256, 7, 1, 1, 1, 1, 2, 2>(a, s);
   } else if (stride == 2) {
     // layer4.0.conv2 (14x14x512 -> 7x7): one image (98 KB) x half the channels
     launch8<7, 7, 512, 512, 7, 1, 2, 1, 1, 2, 2>(a, s);
+  } else if (Cin == 128) {
+    // layer2 (28x28x128): half an image (14 output rows + a halo row, 54 KB)
+    // x all 128 channels, 4 pixel quarters x 2 groups of 64 (the whole image,
+    // 100 KB, per workgroup would stage it once per channel half)
+    // (4-row strips, 108 VGPRs, two workgroups per CU: 1955 vs 1927 us per
+    // resnet50_fp8 b256 forward, profiles/r5_stream8_layer2.txt)
+    launch8<28, 28, 128, 128, 14, 1, 1, 4, 2, 2, 1>(a, s);
   } else if (Cin == 256) {
     // layer3: one image x half the channels per workgroup (2 pixel halves x 4
     // groups of 32; 188 VGPRs). All 256 channels per workgroup (4 groups of
     // 64 per wave) spills at any ring depth.
     launch8<14, 14, 256, 256, 14, 1, 2, 2, 1, 2, 1>(a, s);
-  } else {  // layer4: two images x half the channels, 8 groups of 32 (variant bit 2: a 2-deep weight ring)
+  } else {  // layer4: two images x half the channels, 8 groups of 32 (variant 2: a 2-deep weight ring)
     if (v & 2)
       launch8<7, 7, 512, 512, 7, 2, 2, 1, 1, 2, 1>(a, s);
     else

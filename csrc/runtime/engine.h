@@ -139,9 +139,11 @@ struct EngineOptions {
   // ... and the strided 3x3 convs of layer3.0 / layer4.0 (implicit GEMM with
   // an e4m3 epilogue instead of the bf16 big-tile kernel)
   bool fp8_3x3_out_s2 = false;
-  // ResNet50 e4m3: the stride-1 bottleneck 3x3 convs of layer3 / layer4 also
-  // READ e4m3 (t1 written by the reduce 1x1 with per-channel scales) and run
-  // on the e4m3 MFMA (conv3x3_stream8.hip: 2x the bf16 rate); needs fp8_3x3_out
+  // ResNet50 e4m3: the bottleneck 3x3 convs of layer2 / layer3 / layer4 (and
+  // the strided ones of layer2.0 / 3.0 / 4.0) also READ e4m3 (t1 written by
+  // the reduce 1x1 with per-channel scales) and run on the e4m3 MFMA
+  // (conv3x3_stream8.hip: 2x the bf16 rate; layer2: 142.7 -> 144.3 k img/s
+  // from 135.4 k, profiles/r5_stream8_layer2.txt); needs fp8_3x3_out
   bool fp8_3x3_in = true;
 
   // Set a field by name; false if there is no such option.

@@ -680,7 +680,8 @@ def test_softmax_top1(gpu):
 
 
 @pytest.mark.parametrize("B,H,C,S", [(3, 14, 256, 1), (2, 7, 512, 1), (3, 7, 512, 1), (40, 14, 256, 1),
-                                     (3, 28, 256, 2), (2, 14, 512, 2)])
+                                     (3, 28, 256, 2), (2, 14, 512, 2), (3, 28, 128, 1), (1, 28, 128, 1),
+                                     (2, 56, 128, 2)])
 def test_conv3x3_stream8(gpu, B, H, C, S):
     """The e4m3 3x3/s1 conv (conv3x3_stream8.hip, block-scaled e4m3 MFMA) vs
     fp32 torch on the same e4m3 operands (dequantised): the only difference is
@@ -688,7 +689,9 @@ def test_conv3x3_stream8(gpu, B, H, C, S):
     dequantised output is within 0.04 relative L2 and no element is more than
     one e4m3 step off the exactly rounded fp32 result. Odd batches leave the
     7x7 kernel's last workgroup one image short; stride 2 (ResNet50 layer3.0 /
-    layer4.0 conv2) runs half-image strips on 28x28x256."""
+    layer4.0 conv2) runs half-image strips on 28x28x256 (layer2.0 conv2:
+    quarter-image strips of 56x56x128); layer2 (28x28x128) half images with a
+    halo row and 128-B pixels."""
     g = torch.Generator().manual_seed(100 + B + C)
     x = torch.randn(B, H, H, C, generator=g).clamp_min(0)  # post-ReLU t1
     sx = x.abs().max().item() / ops.FP8_MAX
@@ -702,6 +705,16 @@ def test_conv3x3_stream8(gpu, B, H, C, S):
     out_scale = ref.abs().max().item() / ops.FP8_MAX
     y = ops.conv3x3_stream8(xq.to(gpu), wq.to(gpu), alpha.to(gpu), bias.to(gpu), relu=True, out_scale=out_scale,
                             stride=S)
+    if C == 128 and S == 2:  # layer2.0's other strip height (variant 4): same sums, same bits
+        Cn = dmlc.native()
+        Cn.conv3x3_stream8_set_variant(4)
+        try:
+            y2 = ops.conv3x3_stream8(xq.to(gpu), wq.to(gpu), alpha.to(gpu), bias.to(gpu), relu=True,
+                                     out_scale=out_scale, stride=S)
+        finally:
+            Cn.conv3x3_stream8_set_variant(0)
+        torch.cuda.synchronize()
+        assert torch.equal(y.view(torch.uint8), y2.view(torch.uint8))
     torch.cuda.synchronize()
     got = y.float().cpu() * out_scale
     assert _rel(got, ref) < 0.04, _rel(got, ref)

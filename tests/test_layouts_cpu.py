@@ -504,15 +504,83 @@ def test_stream8_lds_layout(H, CI, IMG):
                         assert all(len(v) == 1 for v in slots.values()), (tap, cc, f)
 
 
-@pytest.mark.parametrize("H,CI,HS", [(14, 256, 7), (7, 512, 7)])
+@pytest.mark.parametrize("HS", [14])
+def test_stream8_half_image_lds_layout(HS):
+    """conv3x3_stream8.hip on ResNet50 layer2 (28x28x128, stride 1): a
+    workgroup stages a strip of HS output rows plus its halo rows inside the
+    image (rows rs = max(r0 - 1, 0) .. min(r0 + HS, 27)); 128-B pixels key chunk pair m of
+    staged pixel K = i * W + x at m ^ ((K >> 1) & 3). The kernel's tap
+    offsets (K = p + (r0 - rs) * W + ktap) read every lane's 32 channels
+    (odd fq: second 16 first), zero-pixel taps read zeros, and both 16-B reads
+    of every X fragment are bank-conflict free."""
+    H = W = 28
+    CI = 128
+    CPX = CI // 16
+    torch.manual_seed(2)
+    img = torch.randint(1, 256, (H, W, CI), dtype=torch.uint8)
+    for part in range(H // HS):
+        r0 = part * HS
+        rs = max(r0 - 1, 0)
+        nrows = min(r0 + HS, H - 1) - rs + 1
+        assert nrows <= HS + (2 if H // HS > 2 else 1)
+        lds = torch.zeros(nrows * W * CI + CI, dtype=torch.uint8)
+        ZB = nrows * W * CI
+        for i in range(nrows):
+            for x in range(W):
+                K = i * W + x
+                for pc in range(CPX):
+                    lc = (((pc >> 1) ^ ((K >> 1) & 3)) << 1) | (pc & 1)
+                    o = (i * W + x) * CI + 16 * pc
+                    lds[o:o + 16] = img[rs + i, x, 16 * lc:16 * lc + 16]
+        npix = HS * W
+        kb = (r0 - rs) * W
+        for tap in range(9):
+            kh, kw = divmod(tap, 3)
+            ktap = (kh - 1) * W + (kw - 1)
+            for f in range((npix + 15) // 16):
+                a0, a1 = [], []
+                for lane in range(64):
+                    fr, fq = lane & 15, lane >> 4
+                    p = min(16 * f + fr, npix - 1)
+                    prow, pcol = divmod(p, W)
+                    r = r0 + prow
+                    inside = 0 <= r + kh - 1 < H and 0 <= pcol + kw - 1 < W
+                    xa = ((r - rs) * W + pcol) * CI + ktap * CI if inside else ZB
+                    u = fq ^ (((fr + kb + ktap) >> 1) & 3)
+                    t0 = (u << 5) | ((fq & 1) << 4)
+                    a0.append(xa + t0)
+                    a1.append(xa + (t0 ^ 16))
+                    got = torch.cat([lds[a0[-1]:a0[-1] + 16], lds[a1[-1]:a1[-1] + 16]])
+                    if inside and 16 * f + fr < npix:
+                        exp = img[r + kh - 1, pcol + kw - 1, 32 * fq:32 * fq + 32]
+                        if fq & 1:
+                            exp = torch.cat([exp[16:], exp[:16]])
+                        assert torch.equal(got, exp), (part, tap, f, lane)
+                    elif not inside:
+                        assert not got.any()
+                live = [l for l in range(64) if a0[l] < ZB and 16 * f + (l & 15) < npix]
+                for addr in (a0, a1):
+                    for grp in _B128_GROUPS:
+                        slots = {}
+                        for l in grp:
+                            if l in live:
+                                slots.setdefault((addr[l] // 16) % 16, set()).add(addr[l])
+                        assert all(len(v) == 1 for v in slots.values()), (part, tap, f)
+
+
+@pytest.mark.parametrize("H,CI,HS", [(14, 256, 7), (7, 512, 7), (28, 128, 4), (28, 128, 7)])
 def test_stream8_stride2_lds_layout(H, CI, HS):
-    """conv3x3_stream8.hip at stride 2 (ResNet50 layer3.0 / layer4.0 conv2):
-    staged input rows with each row's even columns first, chunk pairs keyed
-    by K = (((y + 1) >> 1) - r0) * W + ((x + 1) >> 1); the kernel's tap
-    offsets read every lane's 32 channels of input pixel (2r + kh - 1,
-    2c + kw - 1) (odd fq: second 16 first) and both reads are conflict free."""
+    """conv3x3_stream8.hip at stride 2 (ResNet50 layer2.0 / layer3.0 / layer4.0
+    conv2): staged input rows with each row's even columns first, chunk pairs
+    keyed by K = (((y + 1) >> 1) - r0) * W + ((x + 1) >> 1) (pair m at m ^ (K
+    & 7), 128-B pixels m ^ ((K >> 1) & 3)); the kernel's tap offsets read
+    every lane's 32 channels of input pixel (2r + kh - 1, 2c + kw - 1) (odd fq:
+    second 16 first) and both reads are conflict free."""
     W = H
     HI, WI, CPX = 2 * H, 2 * W, CI // 16
+
+    def pswz(k):
+        return k & 7 if CPX >= 16 else (k >> 1) & 3
     torch.manual_seed(1)
     img = torch.randint(0, 256, (HI, WI, CI), dtype=torch.uint8)
     for part in range(H // HS):
@@ -527,7 +595,7 @@ def test_stream8_stride2_lds_layout(H, CI, HS):
                 x = 2 * q if q < WI // 2 else 2 * (q - WI // 2) + 1
                 K = (((y + 1) >> 1) - r0) * W + ((x + 1) >> 1)
                 for pc in range(CPX):
-                    lc = (((pc >> 1) ^ (K & 7)) << 1) | (pc & 1)
+                    lc = (((pc >> 1) ^ pswz(K)) << 1) | (pc & 1)
                     o = (i * WI + q) * CI + 16 * pc
                     lds[o:o + 16] = img[y, x, 16 * lc:16 * lc + 16]
         npix = HS * W
@@ -546,7 +614,7 @@ def test_stream8_stride2_lds_layout(H, CI, HS):
                         r = r0 + prow
                         inside = not ((r == 0 and kh == 0) or (pcol == 0 and kw == 0))
                         xa = ((2 * r - rs) * WI + pcol) * CI + toff if inside else ZB
-                        u = fq ^ ((fr + ktap) & 7)
+                        u = fq ^ pswz(fr + ktap)
                         t0 = (u << 5) | ((fq & 1) << 4)
                         a0.append(xa + (t0 ^ (cc << 7)))
                         a1.append(xa + ((t0 ^ 16) ^ (cc << 7)))
