@@ -391,6 +391,11 @@ int head_splits_ipw(int B, int N, int num_cus, int ipw) {
   const int min_tiles = B <= ipw ? 2 : 4;
   while (ns < kMaxSplits && (long)groups * ns * 2 <= num_cus && tiles / (ns * 2) >= min_tiles) ns *= 2;
   if (B > ipw) ns = std::min(ns, 8);  // (throughput batches: measured with at most 8)
+  // pooled head at throughput batches: 16 splits while that stays within one
+  // workgroup per CU (B = 256: 16 image groups x 16), each workgroup streaming
+  // half the fc weights of an 8-way split: ResNet50 (C = 2048) 18.2 vs 23.4 us,
+  // ResNet18 (C = 512) 10.4 vs 11.2 us (tools/head_bench.py, profiles/r5_head_splits.txt)
+  if (ipw == kIPWPooled && B > ipw && (long)groups * kMaxSplits <= num_cus && tiles >= 2 * kMaxSplits) ns = kMaxSplits;
   return ns;
 }
 

@@ -1,14 +1,16 @@
 #!/usr/bin/env python3
 """Time the pooled classifier head (head.hip) alone: graph-replayed launches,
 per-launch GPU time, by class split count and knock-out bits (ko 2: no fc
-weight loads). usage: python tools/head_bench.py"""
+weight loads). usage: python tools/head_bench.py [K (512: ResNet18, 2048:
+ResNet50)]"""
 import sys, os
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
 import dmlc
 
 C = dmlc.native()
-B, K, N, NP = 256, 512, 1000, 1008
+B, N, NP = 256, 1000, 1008
+K = int(sys.argv[1]) if len(sys.argv) > 1 else 512
 dev = torch.device("cuda", 0)
 pooled = torch.randn(B, K, device=dev).to(torch.bfloat16)
 w = (torch.randn(NP, K, device=dev) * 0.05).to(torch.bfloat16)
@@ -39,7 +41,7 @@ def run(ns, ko, reps=200):
 
 
 ref = torch.softmax(pooled.float() @ w[:N].float().t() + bias[:N], -1)
-for ns in (0, 2, 4, 8):
+for ns in (0, 4, 8, 16):
     us = run(ns, 0)
     ok = torch.equal(idx.long().cpu(), ref.argmax(-1).cpu())
     print(f"ns={ns or 'auto'}: {us:.2f} us/launch  top1 ok={ok}  (ko=2: {run(ns, 2):.2f} us)")
