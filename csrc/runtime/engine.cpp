@@ -354,12 +354,13 @@ void Engine::build_alexnet() {
 // resnet50_fp8: conv outputs with a multiple of 128 channels are e4m3: the
 // 256..2048-channel block outputs and residual paths (where the bytes are:
 // layer1's 56x56x256 tensors dominate the traffic), so every 1x1 expand /
-// reduce conv and downsample reads or writes e4m3. The 3x3 convs keep bf16
-// input (EngineOptions::fp8_3x3 makes them e4m3 in and out): as bf16 they run
-// the direct stream / row convs (LDS-resident input, register weights),
-// which beat the fp8 implicit GEMM on these shapes; those kernels write
-// e4m3 through their epilogue (fp8_3x3_out), so the expand convs read e4m3. The stem and layer1's
-// 64-channel inner convs stay bf16 (Cin = 64 is below the fp8 kernel's
+// reduce conv and downsample reads or writes e4m3. The bottleneck 3x3 convs
+// of layers 2-4 then read e4m3 too and run on the e4m3 MFMA
+// (conv3x3_stream8.hip, fp8_3x3_in: their t1 gets per-channel scales from the
+// reduce 1x1) and write e4m3 (fp8_3x3_out), so the expand convs read e4m3.
+// (EngineOptions::fp8_3x3 instead marks every 3x3 conv's input and output
+// e4m3 for the fp8 implicit GEMM: slower, off.) The stem and layer1's
+// 64-channel inner convs stay bf16 (Cin = 64 is below the fp8 kernels'
 // 128-channel K-tile).
 void Engine::mark_fp8() {
   const bool fp8_3x3 = opt_.fp8_3x3;

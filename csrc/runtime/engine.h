@@ -126,8 +126,9 @@ struct EngineOptions {
   // sibling conv1 by 10-12 us and adds ~10 us of fork/join gaps per block:
   // profiles/r1_fork_ds_timeline.txt); kept to test the side-stream path
   bool fork_ds = false;
-  // resnet50_fp8: the 3x3 convs' inputs / outputs in e4m3 too (default bf16:
-  // the direct bf16 convs beat the fp8 implicit GEMM on those shapes)
+  // resnet50_fp8: every 3x3 conv's input and output in e4m3 on the fp8
+  // implicit GEMM (off: slower than the default, where the bottleneck 3x3s of
+  // layers 2-4 read and write e4m3 on conv3x3_stream8: fp8_3x3_in / _out below)
   bool fp8_3x3 = false;
   // ResNet50 e4m3: the bottleneck 3x3 convs that run on the row / stream
   // kernels write e4m3 (their bf16 inputs stay), so the expand conv reads e4m3:
