@@ -655,8 +655,12 @@ int conv_pick_split_k(const ConvArgs& a, int num_cus) {
   // tiles): 8 K slices (two rounds of workgroups) beat the one-round pick --
   // classifier.1 55 -> 47 us, classifier.6 28 -> 23 us at B=256; 16 is slower
   // again (profiles/r3_alexnet_fc_splitk.txt)
-  if (a.H == 1 && a.W == 1 && a.KH == 1 && a.KW == 1 && a.Kpad >= 4096) s = std::max(s, 8);
-  s = std::min(s, k_tiles / 8);
+  const bool fc = a.H == 1 && a.W == 1 && a.KH == 1 && a.KW == 1 && a.Kpad >= 4096;
+  if (fc) s = std::max(s, 8);
+  // (fc layers may take K slices of 4 K-tiles: classifier.6, 16 tiles at
+  // B = 256, 22.0 -> 20.2 us with 16 slices; tools/fc_bench.py,
+  // profiles/r5_fc_splitk.txt)
+  s = std::min(s, k_tiles / (fc ? 4 : 8));
   s = std::min(s, 16);
   return std::max(s, 1);
 }
