@@ -290,6 +290,7 @@ PYBIND11_MODULE(_C, m) {
     mfma_fp8_probe(P<void>(a), P<void>(b), P<float>(d), S(stream));
   });
   m.def("head_ws_bytes", &head_ws_bytes);
+  m.def("head_pooled_splits", &head_pooled_splits);
   m.def("head_pooled", [](uintptr_t pooled, uintptr_t w, uintptr_t bias, int B, int C, int N, int ldw, int Npad,
                           uintptr_t logits, uintptr_t idx, uintptr_t prob, uintptr_t ws, size_t ws_bytes, int num_cus,
                           uintptr_t stream, int ns, int ko) {

@@ -401,6 +401,8 @@ int head_splits_ipw(int B, int N, int num_cus, int ipw) {
 
 int head_splits(int B, int N, int num_cus) { return head_splits_ipw(B, N, num_cus, kIPW); }
 
+int head_pooled_splits(int B, int N, int num_cus) { return head_splits_ipw(B, N, num_cus, kIPWPooled); }
+
 size_t head_ws_bytes(int max_batch) {
   // partials for up to kMaxSplits splits, then the group counters at the very end
   const size_t groups = (max_batch + kIPW - 1) / kIPW;

@@ -305,6 +305,8 @@ void mfma_fp8_probe(const void* a, const void* b, float* d, hipStream_t s);
 // ws: head_ws_bytes(max_batch) bytes, zeroed once at allocation.
 bool head_supported(int C, int N, int ldw, int Npad);
 int head_splits(int B, int N, int num_cus);
+// class splits of head_pooled (16 images per workgroup) when not overridden
+int head_pooled_splits(int B, int N, int num_cus);
 size_t head_ws_bytes(int max_batch);
 void head_fused(const void* x, const void* w, const float* bias, int B, int HW, int C, int N, int ldw, int Npad,
                 float* logits, int32_t* idx, float* prob, void* ws, size_t ws_bytes, int num_cus, hipStream_t s,

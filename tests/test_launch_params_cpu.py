@@ -1,0 +1,22 @@
+"""Host-side launch-parameter choices of the GPU kernels (no GPU needed: the
+native module's host functions run on the CPU)."""
+import pytest
+
+import dmlc
+
+C = dmlc.native()
+CUS = 256  # MI355X
+
+
+@pytest.mark.parametrize("B,ns", [(1, 16), (16, 16), (64, 16), (256, 16), (512, 8), (1024, 4)])
+def test_head_pooled_splits(B, ns):
+    """head_pooled's class-split count for 1000 classes: 16 splits while the
+    grid (16 images per workgroup x splits) stays within one workgroup per CU
+    (ResNet18 / ResNet50 at B = 256: 256 workgroups; profiles/r5_head_splits.txt),
+    fewer once the image groups alone fill the CUs."""
+    got = C.head_pooled_splits(B, 1000, CUS)
+    assert got == ns
+    groups = (B + 15) // 16
+    assert groups * got <= max(CUS, groups)  # never more than one round of workgroups
+    # the workspace sized for the largest split count holds the partials and counters
+    assert C.head_ws_bytes(B) >= B * got * 16 + groups * 4
