@@ -72,7 +72,10 @@ struct Stream8Geom {
   static constexpr int PXB = CI;                 // bytes per staged pixel
   static constexpr int ROWB = WI * PXB;
   static constexpr int ZB = XR * ROWB;           // the zero pixel
-  static constexpr int LDS = ZB + PXB;
+  // (128-B pixels: two zero pixels, the window half a real pixel of the same
+  // K parity would use, so border lanes keep their bank slots)
+  static constexpr int ZBYTES = PXB >= 256 ? PXB : 256;
+  static constexpr int LDS = ZB + ZBYTES;
   static constexpr int CH = XR * WI * (CI / 16);  // 16-B chunks staged (at most)
 };
 
@@ -138,7 +141,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream8_kernel(Stream8Args a) 
     const uint8_t* src = i < nrows ? img + ((long)(rs + i) * WI + x) * CI + 16 * lc : a.zero;
     if (G::CH % 64 == 0 || ci < G::CH) dma16(src, xs + k0 * 16);
   }
-  if (wave == 0 && lane < CPX) dma16(a.zero, xs + G::ZB);
+  if (wave == 0 && lane < G::ZBYTES / 16) dma16(a.zero, xs + G::ZB);
 
   // ---- weights: fragment (group j, K-tile t, nf, half h) = 1 KB, lane l's
   // 16 B at l * 16 (conv3x3_stream8_frag_offset); this wave's NG groups are
@@ -188,9 +191,14 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream8_kernel(Stream8Args a) 
     // staged column offset of tap column kw (stride 2: odd columns start at WI / 2)
     const int dq = S == 1 ? kw - 1 : (kw == 0 ? WI / 2 - 1 : kw == 1 ? 0 : WI / 2);
     const int toff = ((kh - 1) * WI + dq) * G::PXB;
-#pragma unroll
-    for (int f = 0; f < MF; ++f) xa[f] = (xoff[f] & tm) ? G::ZB : (xoff[f] & ~15) + toff;
     const int ktap = S == 1 ? (kh - 1) * W + (kw - 1) : (kh == 2 ? W : 0) + (kw == 2 ? 1 : 0);
+    // 128-B pixels: a real pixel's window half is its staged column's parity,
+    // K's parity (stride 2: flipped for kw != 1, the odd columns staged after
+    // the even ones); border lanes read the zero pixel in that half, so they
+    // keep the bank slots the swizzle gives their K
+    const int zh = CPX >= 16 ? 0 : (((fr + kb + ktap) & 1) ^ (S == 2 && kw != 1 ? 1 : 0));
+#pragma unroll
+    for (int f = 0; f < MF; ++f) xa[f] = (xoff[f] & tm) ? G::ZB + zh * 128 : (xoff[f] & ~15) + toff;
     const int u = fq ^ pswz(fr + kb + ktap);
     tsw0 = (u << 5) | ((fq & 1) << 4);
     tsw1 = tsw0 ^ 16;

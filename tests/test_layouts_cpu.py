@@ -493,8 +493,9 @@ def test_stream8_lds_layout(H, CI, IMG):
                         assert torch.equal(got, exp), (tap, cc, f, lane)
                     elif not inside:
                         assert not got.any()
-                # conflicts: only among in-image lanes (border lanes all read the zero pixel)
-                live = [l for l in range(64) if a0[l] < ZB]
+                # conflicts among every real pixel's lanes, border lanes (zero
+                # pixel, their own chunk offsets) included
+                live = [l for l in range(64) if 16 * f + (l & 15) < npx]
                 for addr in (a0, a1):
                     for grp in _B128_GROUPS:
                         slots = {}
@@ -523,7 +524,7 @@ def test_stream8_half_image_lds_layout(HS):
         rs = max(r0 - 1, 0)
         nrows = min(r0 + HS, H - 1) - rs + 1
         assert nrows <= HS + (2 if H // HS > 2 else 1)
-        lds = torch.zeros(nrows * W * CI + CI, dtype=torch.uint8)
+        lds = torch.zeros(nrows * W * CI + 256, dtype=torch.uint8)  # + two zero pixels
         ZB = nrows * W * CI
         for i in range(nrows):
             for x in range(W):
@@ -545,7 +546,8 @@ def test_stream8_half_image_lds_layout(HS):
                     prow, pcol = divmod(p, W)
                     r = r0 + prow
                     inside = 0 <= r + kh - 1 < H and 0 <= pcol + kw - 1 < W
-                    xa = ((r - rs) * W + pcol) * CI + ktap * CI if inside else ZB
+                    zh = (fr + kb + ktap) & 1  # the zero pixel in the window half of the lane's K parity
+                    xa = ((r - rs) * W + pcol) * CI + ktap * CI if inside else ZB + 128 * zh
                     u = fq ^ (((fr + kb + ktap) >> 1) & 3)
                     t0 = (u << 5) | ((fq & 1) << 4)
                     a0.append(xa + t0)
@@ -558,7 +560,7 @@ def test_stream8_half_image_lds_layout(HS):
                         assert torch.equal(got, exp), (part, tap, f, lane)
                     elif not inside:
                         assert not got.any()
-                live = [l for l in range(64) if a0[l] < ZB and 16 * f + (l & 15) < npix]
+                live = [l for l in range(64) if 16 * f + (l & 15) < npix]  # border lanes included
                 for addr in (a0, a1):
                     for grp in _B128_GROUPS:
                         slots = {}
@@ -587,7 +589,7 @@ def test_stream8_stride2_lds_layout(H, CI, HS):
         r0 = part * HS
         rs = max(2 * r0 - 1, 0)
         nrows = min(2 * (r0 + HS - 1) + 1, HI - 1) - rs + 1
-        lds = torch.zeros(nrows * WI * CI + CI, dtype=torch.uint8)
+        lds = torch.zeros(nrows * WI * CI + max(CI, 256), dtype=torch.uint8)  # + the zero pixel(s)
         ZB = nrows * WI * CI
         for i in range(nrows):
             y = rs + i
@@ -613,7 +615,10 @@ def test_stream8_stride2_lds_layout(H, CI, HS):
                         prow, pcol = divmod(p, W)
                         r = r0 + prow
                         inside = not ((r == 0 and kh == 0) or (pcol == 0 and kw == 0))
-                        xa = ((2 * r - rs) * WI + pcol) * CI + toff if inside else ZB
+                        # (128-B pixels: the zero pixel in the window half a real pixel of this
+                        # K would use: K's parity, flipped for kw != 1)
+                        zh = ((fr + ktap) & 1) ^ (1 if kw != 1 else 0) if CPX < 16 else 0
+                        xa = ((2 * r - rs) * WI + pcol) * CI + toff if inside else ZB + 128 * zh
                         u = fq ^ pswz(fr + ktap)
                         t0 = (u << 5) | ((fq & 1) << 4)
                         a0.append(xa + (t0 ^ (cc << 7)))
@@ -627,7 +632,7 @@ def test_stream8_stride2_lds_layout(H, CI, HS):
                             assert torch.equal(got, exp), (part, tap, cc, f, lane)
                         elif not inside:
                             assert not got.any()
-                    live = [l for l in range(64) if a0[l] < ZB]
+                    live = [l for l in range(64) if 16 * f + (l & 15) < npix]  # border lanes included
                     for addr in (a0, a1):
                         for grp in _B128_GROUPS:
                             slots = {}
