@@ -334,6 +334,17 @@ PYBIND11_MODULE(_C, m) {
   });
 
   // ---------------------------------------------------------------- engine
+  // host-only packing audit: [(layer, kind, off, bytes)], arena bytes
+  m.def("pack_audit", [](const std::string& arch, const py::dict& weights, const std::map<std::string, bool>& options,
+                         int num_classes, int image_size) {
+    size_t total = 0;
+    const auto regs = Engine::pack_audit(arch, to_weight_map(weights), engine_options(options), &total,
+                                         num_classes, image_size);
+    py::list out;
+    for (const auto& r : regs) out.append(py::make_tuple(r.layer, r.kind, r.off, r.bytes));
+    return py::make_tuple(out, total);
+  }, py::arg("arch"), py::arg("weights"), py::arg("options") = std::map<std::string, bool>{},
+     py::arg("num_classes") = 1000, py::arg("image_size") = 224);
   py::class_<Engine>(m, "Engine")
       .def(py::init([](const std::string& arch, const py::dict& weights, int device, int num_classes,
                        int image_size, const std::map<std::string, bool>& options) {

@@ -112,26 +112,50 @@ Engine::Engine(const std::string& arch, const WeightMap& weights, int device, in
   hipDeviceProp_t prop;
   DMLC_HIP_CHECK(hipGetDeviceProperties(&prop, device_));
   num_cus_ = prop.multiProcessorCount;
+  build_graph(weights, true);
+  pack_weights(weights);
+  init_device();
+}
 
-  if (arch == "resnet18")
+Engine::Engine(HostOnly, const std::string& arch, const WeightMap& weights, int num_classes, int image_size,
+               const EngineOptions& options)
+    : arch_(arch), device_(-1), num_classes_(num_classes), image_size_(image_size), opt_(options) {
+  if (num_classes % 4 != 0) throw std::invalid_argument("num_classes must be a multiple of 4");
+  build_graph(weights, false);
+}
+
+void Engine::build_graph(const WeightMap& weights, bool calibrate_on_device) {
+  if (arch_ == "resnet18")
     build_resnet({2, 2, 2, 2}, false);
-  else if (arch == "resnet34")
+  else if (arch_ == "resnet34")
     build_resnet({3, 4, 6, 3}, false);
-  else if (arch == "resnet50")
+  else if (arch_ == "resnet50")
     build_resnet({3, 4, 6, 3}, true);
-  else if (arch == "resnet50_fp8") {
+  else if (arch_ == "resnet50_fp8") {
     fp8_ = true;
     build_resnet({3, 4, 6, 3}, true);
     mark_fp8();
-    calibrate(weights);
+    if (calibrate_on_device) {
+      calibrate(weights);
+    } else {  // host-only audit: unit scales, same layout
+      for (size_t i = 0; i < shapes_.size(); ++i)
+        if (shapes_[i].fp8 && chan_act_[i]) shapes_[i].cscale.assign(shapes_[i].C, 1.f);
+    }
   }
-  else if (arch == "alexnet")
+  else if (arch_ == "alexnet")
     build_alexnet();
   else
-    throw std::invalid_argument("unknown arch: " + arch);
+    throw std::invalid_argument("unknown arch: " + arch_);
+}
 
-  pack_weights(weights);
-  init_device();
+std::vector<PackRegion> Engine::pack_audit(const std::string& arch, const WeightMap& weights,
+                                           const EngineOptions& options, size_t* total, int num_classes,
+                                           int image_size) {
+  Engine e(HostOnly{}, arch, weights, num_classes, image_size, options);
+  std::vector<PackRegion> regions;
+  const std::vector<uint8_t> host = e.pack_host(weights, &regions);
+  if (total) *total = host.size();
+  return regions;
 }
 
 // Same graph, packing and calibration as `src`, on another device, with an
@@ -180,6 +204,7 @@ void Engine::init_device() {
 }
 
 Engine::~Engine() {
+  if (device_ < 0) return;  // host-only (pack_audit): nothing on a device
   hipSetDevice(device_);
   for (auto& kv : graphs_) hipGraphExecDestroy(kv.second);
   if (!acts_.empty() && acts_[0]) hipFree(acts_[0]);
@@ -480,7 +505,38 @@ void Engine::calibrate(const WeightMap& w) {
   }
 }
 
+namespace {
+
+// A layer's region of the host weight image: every write is bounds-checked
+// against the size the layout pass gave it, so a packing order that writes
+// past its region fails at load instead of corrupting its neighbours.
+struct RegionRef {
+  uint8_t* base = nullptr;
+  size_t bytes = 0;
+  const std::string* layer = nullptr;
+  const char* kind = "";
+  template <class T>
+  T& at(size_t i) const {
+    if ((i + 1) * sizeof(T) > bytes)
+      throw std::runtime_error("pack_weights: write past the " + std::string(kind) + " region of " + *layer);
+    return reinterpret_cast<T*>(base)[i];
+  }
+  void copy(size_t off, const void* src, size_t n) const {
+    if (off + n > bytes)
+      throw std::runtime_error("pack_weights: copy past the " + std::string(kind) + " region of " + *layer);
+    std::memcpy(base + off, src, n);
+  }
+};
+
+}  // namespace
+
 void Engine::pack_weights(const WeightMap& w) {
+  const std::vector<uint8_t> host = pack_host(w, nullptr);
+  DMLC_HIP_CHECK(hipMalloc(&warena_, weight_bytes_));
+  DMLC_HIP_CHECK(hipMemcpy(warena_, host.data(), weight_bytes_, hipMemcpyHostToDevice));
+}
+
+std::vector<uint8_t> Engine::pack_host(const WeightMap& w, std::vector<PackRegion>* regions) {
   // Layout pass.
   size_t off = 0;
   for (auto& L : convs_) {
@@ -496,6 +552,7 @@ void Engine::pack_weights(const WeightMap& w) {
       off = align_up(off + (size_t)L.npad * 4, 256);
     }
     L.wf_off = 0;
+    L.wf_bytes = 0;
     // (3x3 convs the register-weight stream conv runs, and the 1x1/s2
     // downsample it fuses next to a stride-2 one)
     // (and every 3x3/p1 conv and 1x1/s2 downsample the query-batch conv can
@@ -516,26 +573,31 @@ void Engine::pack_weights(const WeightMap& w) {
           (conv3x3_rows_supported(shapes_[L.in_act].H, shapes_[L.in_act].W, shapes_[L.in_act].C, L.cout) ||
            conv3x3_13_supported(shapes_[L.in_act].H, shapes_[L.in_act].W, shapes_[L.in_act].C, L.cout)))))) {
       L.wf_off = off;  // fragment-order copy for the register-weight stream conv
-      off = align_up(off + (size_t)L.cout * L.kpad * 2, 256);
+      L.wf_bytes = (size_t)L.cout * L.kpad * 2;
+      off = align_up(off + L.wf_bytes, 256);
     }
     if (!L.fp8 && !L.fc && L.in_act >= 0 && L.kh == 5 && L.kw == 5 && L.stride == 1 &&
         conv5x5_27_supported(shapes_[L.in_act].H, shapes_[L.in_act].W, shapes_[L.in_act].C, L.cout, L.pad)) {
       L.wf_off = off;  // fragment-order copy for conv5x5_27.hip
-      off = align_up(off + (size_t)L.cout * L.kpad * 2, 256);
+      L.wf_bytes = (size_t)L.cout * L.kpad * 2;
+      off = align_up(off + L.wf_bytes, 256);
     }
     if (L.fp8 && !L.fc && L.in_act >= 0 && L.kh == 3 && L.kw == 3 && L.pad == 1 && L.kpad == 9 * L.cin &&
         conv3x3_stream8_supported(shapes_[L.in_act].H, shapes_[L.in_act].W, shapes_[L.in_act].C, L.cout,
                                   L.stride)) {
       L.wf_off = off;  // e4m3 fragment-order copy for conv3x3_stream8.hip
-      off = align_up(off + (size_t)L.cout * L.kpad, 256);
+      L.wf_bytes = (size_t)L.cout * L.kpad;
+      off = align_up(off + L.wf_bytes, 256);
     }
     if (bottleneck_conv3(L)) {  // fragment-order copy for bottleneck56.hip's expand conv
       L.wf_off = off;
-      off = align_up(off + (size_t)L.cout * L.kpad * 2, 256);
+      L.wf_bytes = (size_t)L.cout * L.kpad * 2;
+      off = align_up(off + L.wf_bytes, 256);
     }
     if (L.alex_stem) {  // paired-chunk K order for alex_stem.hip
       L.wf_off = off;
-      off = align_up(off + (size_t)L.cout * kAlexStemK * 2, 256);
+      L.wf_bytes = (size_t)L.cout * kAlexStemK * 2;
+      off = align_up(off + L.wf_bytes, 256);
     }
   }
   // bottleneck expand convs that can take their stride-1 downsample as a
@@ -562,6 +624,12 @@ void Engine::pack_weights(const WeightMap& w) {
   }
   weight_bytes_ = off;
   std::vector<uint8_t> host(off, 0);
+  auto region = [&](const ConvLayer& L, const char* kind, size_t roff, size_t bytes) {
+    if (roff + bytes > host.size())
+      throw std::runtime_error("pack_weights: " + std::string(kind) + " region of " + L.name + " past the arena");
+    if (regions) regions->push_back(PackRegion{L.name, kind, roff, bytes});
+    return RegionRef{host.data() + roff, bytes, &L.name, kind};
+  };
   for (auto& L : convs_) {
     const HostTensor& W = need(w, L.name + ".weight");
     const HostTensor* cb = maybe(w, L.name + ".bias");
@@ -590,13 +658,18 @@ void Engine::pack_weights(const WeightMap& w) {
         bias[n] /= cs[n];
       }
     }
+    const RegionRef rw = region(L, "w", L.w_off, (size_t)L.npad * L.kpad * (L.fp8 ? 1 : 2));
+    const RegionRef rb = region(L, "b", L.b_off, (size_t)L.npad * 4);
+    const RegionRef rf = L.wf_off ? region(L, "wf", L.wf_off, L.wf_bytes) : RegionRef{};
     std::vector<uint16_t> wbf;
-    uint16_t* pw = (uint16_t*)(host.data() + L.w_off);
+    RegionRef rwbf = rw;  // bf16 weights [npad][kpad]
     if (L.fp8) {  // fold into a bf16 staging copy first, then quantise per row
       wbf.assign((size_t)L.npad * L.kpad, 0);
-      pw = wbf.data();
+      rwbf.base = (uint8_t*)wbf.data();
+      rwbf.bytes = wbf.size() * 2;
+      rwbf.kind = "bf16 staging";
     }
-    float* pb = (float*)(host.data() + L.b_off);
+    auto pw = [&](size_t i) -> uint16_t& { return rwbf.at<uint16_t>(i); };
     if (!L.fc) {
       if (W.shape.size() != 4 || W.shape[0] != L.cout || W.shape[1] != L.cin || W.shape[2] != L.kh ||
           W.shape[3] != L.kw)
@@ -613,7 +686,7 @@ void Engine::pack_weights(const WeightMap& w) {
                 k = (size_t)i * ((L.kw * 3 + 7) / 8) * 8 + j * 3 + c;
               else
                 k = (size_t)(i * L.kw + j) * L.cin_eff + c;
-              pw[(size_t)n * L.kpad + k] = f2bf_host(v);
+              pw((size_t)n * L.kpad + k) = f2bf_host(v);
             }
     } else {
       if (W.shape.size() != 2 || W.shape[0] != L.cout || W.shape[1] != L.cin)
@@ -626,44 +699,42 @@ void Engine::pack_weights(const WeightMap& w) {
             const int c = k / (H * Wd), hw = k % (H * Wd);
             dst = hw * C + c;
           }
-          pw[(size_t)n * L.kpad + dst] = f2bf_host(W.data[(size_t)n * L.cin + k] * scale[n]);
+          pw((size_t)n * L.kpad + dst) = f2bf_host(W.data[(size_t)n * L.cin + k] * scale[n]);
         }
     }
-    for (int n = 0; n < L.cout; ++n) pb[n] = bias[n];
+    for (int n = 0; n < L.cout; ++n) rb.at<float>(n) = bias[n];
     if (L.alex_stem) {
-      uint16_t* pf = (uint16_t*)(host.data() + L.wf_off);
       for (int n = 0; n < L.cout; ++n)
         for (int c = 0; c < L.cin; ++c)
           for (int i = 0; i < L.kh; ++i)
             for (int j = 0; j < L.kw; ++j)
-              pf[(size_t)n * kAlexStemK + alex_stem_k(i, j, c)] =
+              rf.at<uint16_t>((size_t)n * kAlexStemK + alex_stem_k(i, j, c)) =
                   f2bf_host(W.data[(((size_t)n * L.cin + c) * L.kh + i) * L.kw + j] * scale[n]);
-    } else if (L.wf_off) {
-      uint16_t* pf = (uint16_t*)(host.data() + L.wf_off);
+    } else if (L.wf_off && !L.fp8) {  // bf16 fragment order (e4m3 layers: stream8's order, below)
       for (int n = 0; n < L.cout; ++n)
-        for (int k = 0; k < L.kpad; ++k) pf[stream_frag_index(n, k, L.kpad)] = pw[(size_t)n * L.kpad + k];
+        for (int k = 0; k < L.kpad; ++k) rf.at<uint16_t>(stream_frag_index(n, k, L.kpad)) = pw((size_t)n * L.kpad + k);
     }
     if (L.fp8) {
       // e4m3 weights with a per-output-channel scale; alpha = s_in * s_w[n]
-      uint8_t* q = host.data() + L.w_off;
-      float* alpha = (float*)(host.data() + L.a_off);
+      const RegionRef& q = rw;
+      const RegionRef alpha = region(L, "alpha", L.a_off, (size_t)L.npad * 4);
       const float s_in = shapes_[L.in_act].scale;
       // per-channel input scales (fp8_3x3_out): along K (channel k % Cin)
       const std::vector<float>& ics = shapes_[L.in_act].cscale;
       const int cin = shapes_[L.in_act].C;
       auto wv = [&](int n, int k) {
-        const float v = bf2f_host(pw[(size_t)n * L.kpad + k]);
+        const float v = bf2f_host(pw((size_t)n * L.kpad + k));
         return ics.empty() ? v : v * ics[k % cin];
       };
       for (int n = 0; n < L.npad; ++n) {
         float amax = 0.f;
         for (int k = 0; k < L.kpad; ++k) amax = std::max(amax, std::fabs(wv(n, k)));
         const float sw = amax > 0.f ? amax / 448.f : 1.f;
-        for (int k = 0; k < L.kpad; ++k) q[(size_t)n * L.kpad + k] = f2e4m3_host(wv(n, k) / sw);
-        alpha[n] = s_in * sw;
+        for (int k = 0; k < L.kpad; ++k) q.at<uint8_t>((size_t)n * L.kpad + k) = f2e4m3_host(wv(n, k) / sw);
+        alpha.at<float>(n) = s_in * sw;
       }
       if (L.wf_off) {  // conv3x3_stream8's fragment order of the e4m3 weights
-        uint8_t* pf = host.data() + L.wf_off;
+        const uint8_t* qb = q.base;
         const int KT = L.kpad / 128;
         for (int j = 0; j < L.cout / 32; ++j)
           for (int t = 0; t < KT; ++t)
@@ -673,7 +744,7 @@ void Engine::pack_weights(const WeightMap& w) {
                   const int fq = ln >> 4, r = 16 * nf + (ln & 15);
                   const int n = 32 * j + 8 * ((r & 15) >> 2) + 4 * (r >> 4) + (r & 3);  // perm32
                   const int k0 = 128 * t + 32 * fq + 16 * (h ^ (fq & 1));
-                  std::memcpy(pf + conv3x3_stream8_frag_offset(j, t, nf, h, ln, KT), q + (size_t)n * L.kpad + k0, 16);
+                  rf.copy(conv3x3_stream8_frag_offset(j, t, nf, h, ln, KT), qb + (size_t)n * L.kpad + k0, 16);
                 }
       }
     }
@@ -682,20 +753,19 @@ void Engine::pack_weights(const WeightMap& w) {
     if (L.cat_ds < 0) continue;
     const ConvLayer& D = convs_[L.cat_ds];
     const int K = L.kpad + D.kpad;
-    uint16_t* cw = (uint16_t*)(host.data() + L.cat_off);
+    const RegionRef cw = region(L, "cat", L.cat_off, (size_t)L.npad * K * 2);
     const uint16_t* w3 = (const uint16_t*)(host.data() + L.w_off);
     const uint16_t* wd = (const uint16_t*)(host.data() + D.w_off);
     for (int n = 0; n < L.npad; ++n) {
-      std::copy(w3 + (size_t)n * L.kpad, w3 + (size_t)(n + 1) * L.kpad, cw + (size_t)n * K);
-      std::copy(wd + (size_t)n * D.kpad, wd + (size_t)(n + 1) * D.kpad, cw + (size_t)n * K + L.kpad);
+      cw.copy((size_t)n * K * 2, w3 + (size_t)n * L.kpad, (size_t)L.kpad * 2);
+      cw.copy(((size_t)n * K + L.kpad) * 2, wd + (size_t)n * D.kpad, (size_t)D.kpad * 2);
     }
-    float* cb = (float*)(host.data() + L.cat_b_off);
+    const RegionRef cb = region(L, "cat_b", L.cat_b_off, (size_t)L.npad * 4);
     const float* b3 = (const float*)(host.data() + L.b_off);
     const float* bd = (const float*)(host.data() + D.b_off);
-    for (int n = 0; n < L.npad; ++n) cb[n] = b3[n] + bd[n];
+    for (int n = 0; n < L.npad; ++n) cb.at<float>(n) = b3[n] + bd[n];
   }
-  DMLC_HIP_CHECK(hipMalloc(&warena_, weight_bytes_));
-  DMLC_HIP_CHECK(hipMemcpy(warena_, host.data(), weight_bytes_, hipMemcpyHostToDevice));
+  return host;
 }
 
 void Engine::reserve(int max_batch) {

@@ -52,6 +52,7 @@ struct ConvLayer {
   bool fp8 = false;             // e4m3 weights (input activation is e4m3)
   size_t a_off = 0;             // fp8: alpha[n] = s_in * s_w[n] (fp32 [npad])
   size_t wf_off = 0;            // weights in stream-conv fragment order (0 = none)
+  size_t wf_bytes = 0;          // ... and the size of that region
   // bottleneck expand conv with its stride-1 downsample folded in (conv1x1 x2):
   // [cout][kpad + ds kpad] bf16 = [W3 | Wd] and bias b3 + bd (0 = none)
   int cat_ds = -1;              // convs_ index of that downsample
@@ -151,6 +152,12 @@ struct EngineOptions {
   bool set(const std::string& name, bool value);
 };
 
+// One region of the packed weight arena (Engine::pack_audit).
+struct PackRegion {
+  std::string layer, kind;  // kind: w | b | alpha | wf | cat | cat_b
+  size_t off = 0, bytes = 0;
+};
+
 class Engine {
  public:
   // arch: resnet18 | resnet34 | resnet50 | alexnet | resnet50_fp8 (layers 2-4
@@ -167,6 +174,14 @@ class Engine {
   void copy_weights_from(const Engine& src);
   ~Engine();
   Engine& operator=(const Engine&) = delete;
+  // Host-only packing audit (no device is touched): build `arch`'s graph,
+  // pack its weights into the host image with every write bounds-checked
+  // against the region the layout pass gave it (std::runtime_error on a write
+  // outside it), and return the regions. e4m3 activation scales are 1
+  // instead of calibrated. *total = the arena size.
+  static std::vector<PackRegion> pack_audit(const std::string& arch, const WeightMap& weights,
+                                            const EngineOptions& options, size_t* total,
+                                            int num_classes = 1000, int image_size = 224);
   void* weight_arena() const { return warena_; }
 
   const std::string& arch() const { return arch_; }
@@ -209,7 +224,12 @@ class Engine {
   int fc(int in, const std::string& name, int cout, bool relu, bool last);
   void build_resnet(const std::vector<int>& blocks, bool bottleneck);
   void build_alexnet();
+  struct HostOnly {};
+  Engine(HostOnly, const std::string& arch, const WeightMap& weights, int num_classes, int image_size,
+         const EngineOptions& options);
+  void build_graph(const WeightMap& weights, bool calibrate_on_device);
   void pack_weights(const WeightMap& w);
+  std::vector<uint8_t> pack_host(const WeightMap& w, std::vector<PackRegion>* regions);
   void init_device();
   void mark_fp8();
   void calibrate(const WeightMap& w);
