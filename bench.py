@@ -58,13 +58,14 @@ if ROOT not in sys.path:
 
 REF_MEAN_LATENCY_MS = 158.94  # ResNet18, CS425MP4Report.pdf p.2 §1a
 REF_STREAM_IMG_S = 1000.0 / REF_MEAN_LATENCY_MS
-# rank 0's share in scatter mode (it also runs the 7 send legs): its forward
-# next to RCCL kernels is ~1.2x slower (profiles/r2_rccl_interference.txt).
-# That was measured with one rank; at N > 1 bench.py starts from it and
-# calibrates (--coord-weight auto, csrc/comm/runner.h Runner::calibrate):
-# rounds of pipelined steps, every rank's forward time all-gathered, rank 0's
-# count re-solved until its forward time matches the slowest other rank's.
-COORD_WEIGHT = 0.85
+# rank 0's share in scatter mode (it also runs the N-1 send legs, and RCCL's
+# copy kernels next to its forward slow it: ~1.2x measured with one rank,
+# profiles/r2_rccl_interference.txt). No multi-GPU measurement exists to seed
+# it with, so at N > 1 bench.py starts from an even split and calibrates
+# (--coord-weight auto, csrc/comm/runner.h Runner::calibrate): rounds of
+# pipelined steps, every rank's forward time all-gathered, rank 0's count
+# re-solved until its forward time matches the slowest other rank's.
+COORD_WEIGHT = 1.0
 
 
 def pct(xs, q):
@@ -98,6 +99,15 @@ def spawn_ranks(n: int) -> int:
     return rc
 
 
+def preflight(n_gpus: int, local_rank: int | None = None) -> None:
+    """Enough GPUs for the ranks (torch.cuda.device_count() does not
+    initialise the GPU, so the spawning parent may call it)."""
+    import torch
+    n = torch.cuda.device_count()
+    if n < n_gpus or (local_rank is not None and local_rank >= n):
+        raise SystemExit(f"bench.py: --gpus {n_gpus} (local rank {local_rank}) but {n} GPU(s) visible")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -124,9 +134,21 @@ def main():
     ap.add_argument("--profile-ops", action="store_true", help="print per-op times of one eager forward")
     ap.add_argument("--e2e-queries", type=int, default=200,
                     help="queries through a dmlc-node cluster for the reference-definition query latency (0: skip)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no GPU: every rank a process with a host worker (a forward of B images takes "
+                         "B x --dry-us-per-image of modelled time, + --dry-coord-extra-us on rank 0 for its send "
+                         "legs) on the cross-process socket communicator; the rest of the path (spawn, gloo, "
+                         "unique ids, calibration all-gather, per-rank max, JSON) is the real one")
+    ap.add_argument("--dry-us-per-image", type=int, default=4)
+    ap.add_argument("--dry-coord-extra-us", type=int, default=200)
+    ap.add_argument("--image-size", type=int, default=224, help="(--dry-run only; the models take 224)")
     args = ap.parse_args()
+    dry = args.dry_run
+    S = args.image_size if dry else 224
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        if not dry:
+            preflight(args.gpus)
         sys.exit(spawn_ranks(args.gpus))
 
     import torch
@@ -137,8 +159,12 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    if dry:
+        dev = torch.device("cpu")
+    else:
+        preflight(args.gpus, local_rank)
+        torch.cuda.set_device(local_rank)
+        dev = torch.device("cuda", local_rank)
     if world > 1:
         # CPU side channel only: unique ids, barriers, max of the timed region
         dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -150,16 +176,19 @@ def main():
     C = dmlc.native()
     B = args.batch
     scatter = args.input_mode == "scatter"  # per-step RCCL scatter (staged: once, before timing)
-    # Random-init weights (the reference's .ot files are LFS stubs); every
-    # rank builds the same seeded model.
-    sd = state_dict_f32(build(args.model, seed=0))
     opts = {k: bool(int(v)) for k, v in (o.split("=", 1) for o in args.engine_opt)}
-    eng = InferenceEngine(args.model, sd, device=local_rank, max_batch=B, options=opts)
     use_graph = not args.no_graph
+    eng = sd = None
+    if not dry:
+        # Random-init weights (the reference's .ot files are LFS stubs); every
+        # rank builds the same seeded model.
+        sd = state_dict_f32(build(args.model, seed=0))
+        eng = InferenceEngine(args.model, sd, device=local_rank, max_batch=B, options=opts)
 
     ids = [b"", b""]
     if world > 1:
-        box = [[C.rccl_unique_id(), C.rccl_unique_id()] if rank == 0 else None]
+        new_id = C.socket_unique_id if dry else C.rccl_unique_id
+        box = [[new_id(), new_id()] if rank == 0 else None]
         dist.broadcast_object_list(box, src=0)
         ids = box[0]
     auto_weight = args.coord_weight == "auto" and world > 1 and scatter
@@ -169,10 +198,19 @@ def main():
         coord_weight = float(args.coord_weight)
     if not scatter:
         coord_weight = 1.0  # nothing to send per step: an even split
-    runner = C.DpRunner(eng._e, world, rank, ids[0], ids[1], B, scatter=scatter, use_graph=use_graph,
-                        lanes=args.lanes, coord_weight=coord_weight)
+    if dry:
+        runner = C.DpRunner.host(world, rank, ids[0], ids[1], B, scatter=scatter, image_size=S, lanes=args.lanes,
+                                 coord_weight=coord_weight, us_per_image=args.dry_us_per_image,
+                                 coord_extra_us=args.dry_coord_extra_us)
+    else:
+        runner = C.DpRunner(eng._e, world, rank, ids[0], ids[1], B, scatter=scatter, use_graph=use_graph,
+                            lanes=args.lanes, coord_weight=coord_weight)
     counts = runner.counts  # images per rank per step (sum = B * world)
     M = runner.max_per_rank
+
+    def sync():
+        if not dry:
+            torch.cuda.synchronize()
 
     # Input pool: two global batches of distinct synthetic images, in the
     # coordinator's HBM (scatter), staged from there into every rank's HBM
@@ -182,24 +220,25 @@ def main():
     n_pool = 0
     if args.input_mode == "staged":
         n_pool = 2 * M  # two per-rank batches at a stride of max_per_rank images
-        pool = torch.empty((n_pool, 224, 224, 3), dtype=torch.uint8, device=dev)
-        src = torch.randint(0, 256, (2, world * B, 224, 224, 3), dtype=torch.uint8, device=dev,
+        pool = torch.empty((n_pool, S, S, 3), dtype=torch.uint8, device=dev)
+        src = torch.randint(0, 256, (2, world * B, S, S, 3), dtype=torch.uint8, device=dev,
                             generator=g) if rank == 0 else None
-        torch.cuda.synchronize()
+        sync()
         for k in range(2):  # batch k: rank r's shard = its count's images of src[k]
             runner.stage(src[k].data_ptr() if rank == 0 else 0, pool[k * M].data_ptr())
+        staged_src = src if dry else None  # (dry run: rank 0 checks the answers against it)
         del src
     elif rank == 0 or not scatter:
         n_pool = 2 * (B * world if scatter else M)
-        pool = torch.randint(0, 256, (n_pool, 224, 224, 3), dtype=torch.uint8, device=dev, generator=g)
+        pool = torch.randint(0, 256, (n_pool, S, S, 3), dtype=torch.uint8, device=dev, generator=g)
     pool_ptr = pool.data_ptr() if pool is not None else 0
-    torch.cuda.synchronize()
+    sync()
 
     def barrier():
-        torch.cuda.synchronize()
+        sync()
         if world > 1:
             dist.barrier()
-        torch.cuda.synchronize()
+        sync()
 
     # Setup: prime the pipeline (hipGraph capture of every slot, RCCL
     # channels, and ~35 ms of load so the GPU leaves its idle clocks; a fixed
@@ -239,18 +278,32 @@ def main():
     batch_lat = lat["step_ms"]
     barrier()
 
+    answers_checked = False
     if rank == 0:
         idx, prob = runner.last_results()
         assert len(idx) == sum(counts)
         assert min(idx) >= 0 and max(idx) < 1000, "bad class ids"
         assert min(prob) > 0 and max(prob) <= 1.0001, "bad probabilities"
+        if dry and args.input_mode != "local":
+            # the host worker's answer is a function of the image's bytes
+            # (csrc/comm/dp.h make_host_worker): the last step's gathered
+            # answers must be those of the images that step was given
+            G = sum(counts)
+            last = args.warmup + args.steps + args.latency_steps - 1
+            if scatter:
+                imgs = pool[:(n_pool // G) * G].view(-1, G, S, S, 3)[last % (n_pool // G)]
+            else:
+                imgs = staged_src[last % 2][:G]
+            want = (imgs.reshape(G, -1).sum(1, dtype=torch.int64) % 1000).tolist()
+            assert list(idx) == want, "dry run: gathered answers do not match their images"
+            answers_checked = True
 
     # Batch-1 GPU-only latency (hipGraph replay of preprocess+forward+top-1
     # for one HBM-resident image, host-timed including the D2H of the
     # answer). Not the reference's query definition (which includes the RPC
     # and the JPEG decode): that one is tools/bench_jobs.py's.
     qlat = []
-    if rank == 0 and args.latency_queries > 0:
+    if rank == 0 and args.latency_queries > 0 and not dry:
         q_eng = InferenceEngine(args.model, sd, device=local_rank, max_batch=1, options=opts)
         qimg = pool[:1].contiguous()
         qout = (torch.empty(1, dtype=torch.int32, device=dev), torch.empty(1, dtype=torch.float32, device=dev))
@@ -266,7 +319,7 @@ def main():
     # decode + resize + forward + top-1, one query at a time) through a
     # one-node dmlc-node cluster on this GPU.
     e2e = None
-    if rank == 0 and args.e2e_queries > 0:
+    if rank == 0 and args.e2e_queries > 0 and not dry:
         try:
             from dmlc.serve.e2e import query_latency
             e2e = query_latency(args.e2e_queries, args.model if args.model in ("resnet18", "alexnet") else "resnet18",
@@ -275,14 +328,15 @@ def main():
             print(f"# e2e query latency failed: {ex}", file=sys.stderr)
 
     ops_profile = None
-    if rank == 0 and args.profile_ops:
+    if rank == 0 and args.profile_ops and not dry:
         ops_profile = eng.profile(pool[:B].contiguous())
 
     if rank == 0:
         n_img = sum(counts) * args.steps
         value = n_img / elapsed
         res = {
-            "metric": "images/sec (whole node) + p50/p95 query latency, "
+            "metric": ("DRY RUN (host workers, no GPU): " if dry else "")
+                      + "images/sec (whole node) + p50/p95 query latency, "
                       + ("ResNet18" if args.model == "resnet18" else args.model) + " ImageNet",
             "value": round(value, 1),
             "unit": "images/s",
@@ -294,7 +348,9 @@ def main():
             "scaling": "weak",
             "vs_baseline": round(value / REF_STREAM_IMG_S, 1) if args.model == "resnet18" else None,
             "dtype": "fp8" if args.model.endswith("_fp8") else "bf16",
-            "data": "synthetic u8 224x224x3 images, random-init weights; "
+            "data": (f"DRY RUN: host workers ({args.dry_us_per_image} us/image modelled, +{args.dry_coord_extra_us} "
+                     f"us per forward on rank 0), socket communicator; synthetic u8 {S}x{S}x3 images; " if dry
+                     else "synthetic u8 224x224x3 images, random-init weights; ")
                     + {"staged": "generated on rank 0, shards scattered to the ranks' HBM over RCCL before timing",
                        "scatter": "HBM-resident on rank 0, scattered over RCCL every step",
                        "local": "generated in every rank's HBM"}[args.input_mode],
@@ -307,10 +363,11 @@ def main():
                 "coord_weight": round(coord_weight, 4),
                 "coord_weight_mode": "calibrated" if calibration else ("fixed" if world > 1 else "n/a"),
                 "seq_len": None,
-                "image_size": 224,
+                "image_size": S,
                 "parallelism": f"dp{world}",
                 "input_mode": args.input_mode,
-                "comm": "native RCCL grouped send/recv (csrc/comm/runner.h), shards + answers on separate communicators"
+                "comm": ("socket (dry run) " if dry else "native RCCL ")
+                        + "grouped send/recv (csrc/comm/runner.h), shards + answers on separate communicators"
                     + ("" if scatter else "; per step: answers only"),
                 "rccl_ranks": world,
                 "hipgraph": use_graph,
@@ -332,8 +389,11 @@ def main():
             "vs_baseline_latency": round(REF_MEAN_LATENCY_MS / e2e["mean_ms"], 1) if e2e else None,
             "gpu_batch1_latency_p50_ms": round(pct(qlat, 50), 4) if qlat else None,
             "gpu_batch1_latency_p95_ms": round(pct(qlat, 95), 4) if qlat else None,
-            "tflops_effective": round(value * eng.gflop_per_image / 1e3, 1),
+            "tflops_effective": round(value * eng.gflop_per_image / 1e3, 1) if eng else None,
+            "dry_run": dry,
         }
+        if dry:
+            res["answers_checked"] = answers_checked
         if calibration:
             res["calibration"] = [{k: (round(v, 4) if isinstance(v, float) else v) for k, v in r.items()}
                                   for r in calibration["rounds"]]

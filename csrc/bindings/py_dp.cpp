@@ -60,6 +60,27 @@ class DpRunner {
                                       std::move(cout), world, rank, counts, scatter, (size_t)S_ * S_ * 3, timeout_ms,
                                       slots);
   }
+  // bench.py --dry-run: the same rank on a host worker (a classify of B
+  // images takes B x us_per_image (+ extra_us on the coordinator, the modelled
+  // cost of its scatter legs) of synthetic device time, csrc/comm/dp.h) and
+  // the cross-process socket communicator (comm::socket_init_rank), one
+  // process per rank exactly as on the GPUs.
+  DpRunner(int world, int rank, const std::string& id_in, const std::string& id_out, int max_per_rank, bool scatter,
+           int image_size, int timeout_ms, int lanes, int slots, double coord_weight, int us_per_image,
+           int coord_extra_us)
+      : S_(image_size) {
+    if (lanes < 1 || lanes > dp::Worker::kMaxLanes) throw std::invalid_argument("DpRunner: lanes must be 1..4");
+    const auto counts = dp::weighted_counts(max_per_rank, world, coord_weight);
+    std::unique_ptr<comm::Comm> cin, cout;
+    if (world > 1) {
+      const int to = timeout_ms > 0 ? timeout_ms : 20000;
+      cin = comm::socket_init_rank(id_in, world, rank, to);
+      cout = comm::socket_init_rank(id_out, world, rank, to);
+    }
+    r_ = std::make_unique<dp::Runner>(
+        dp::make_host_worker(rank, S_, S_, 1000, lanes, 0, 0, us_per_image, rank == 0 ? coord_extra_us : 0),
+        std::move(cin), std::move(cout), world, rank, counts, scatter, (size_t)S_ * S_ * 3, timeout_ms, slots);
+  }
   ~DpRunner() {
     r_.reset();
     lanes_.clear();
@@ -906,6 +927,7 @@ void bind_dp(py::module& m) {
            py::arg("legs") = 7);
   m.def("rccl_loopback", &rccl_loopback, py::arg("device") = 0, py::arg("bytes") = 1 << 20, py::arg("max_ctas") = 0);
   m.def("rccl_unique_id", []() { return py::bytes(comm::rccl_unique_id()); });
+  m.def("socket_unique_id", []() { return py::bytes(comm::socket_unique_id()); });
   m.def("dp_shard_counts", &dp::shard_counts);
   m.def("dp_weighted_counts", &dp::weighted_counts, py::arg("per_rank"), py::arg("world"), py::arg("coord_weight"));
   m.def("dp_host_bench", &dp_host_bench, py::arg("pool"), py::arg("world"), py::arg("per_rank"),
@@ -937,6 +959,18 @@ void bind_dp(py::module& m) {
            py::arg("max_per_rank"), py::arg("scatter") = true, py::arg("image_size") = 224,
            py::arg("use_graph") = true, py::arg("timeout_ms") = -1, py::arg("lanes") = 1, py::arg("slots") = 0,
            py::arg("coord_weight") = 1.0, py::arg("counts") = std::vector<int>{}, py::keep_alive<1, 2>())
+      .def_static("host",
+                  [](int world, int rank, py::bytes id_in, py::bytes id_out, int max_per_rank, bool scatter,
+                     int image_size, int timeout_ms, int lanes, int slots, double coord_weight, int us_per_image,
+                     int coord_extra_us) {
+                    return std::unique_ptr<DpRunner>(new DpRunner(world, rank, std::string(id_in), std::string(id_out),
+                                                                  max_per_rank, scatter, image_size, timeout_ms, lanes,
+                                                                  slots, coord_weight, us_per_image, coord_extra_us));
+                  },
+                  py::arg("world"), py::arg("rank"), py::arg("id_in"), py::arg("id_out"), py::arg("max_per_rank"),
+                  py::arg("scatter") = true, py::arg("image_size") = 224, py::arg("timeout_ms") = 60000,
+                  py::arg("lanes") = 2, py::arg("slots") = 0, py::arg("coord_weight") = 1.0,
+                  py::arg("us_per_image") = 4, py::arg("coord_extra_us") = 0)
       .def("run", &DpRunner::run, py::arg("pool"), py::arg("pool_images"), py::arg("first"), py::arg("n"),
            py::arg("pipelined") = true)
       .def("last_results", &DpRunner::last_results)

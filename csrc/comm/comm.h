@@ -93,6 +93,14 @@ std::unique_ptr<Comm> rccl_init_rank(const std::string& unique_id, int nranks, i
 // result[i] is rank i on devices[i].
 std::vector<std::unique_ptr<Comm>> rccl_init_all(const std::vector<int>& devices);
 
+// ------------------------------------------------------------------ sockets
+// Cross-process host communicator over loopback TCP (socket_comm.cpp): the
+// process-per-rank shape of RCCL (a unique id from rank 0 handed out over a
+// side channel, one rank per process) with the host fake's rendezvous, FIFO
+// and grouping rules. bench.py --dry-run runs its multi-process path on it.
+std::string socket_unique_id();
+std::unique_ptr<Comm> socket_init_rank(const std::string& unique_id, int nranks, int rank, int timeout_ms = 20000);
+
 // ------------------------------------------------------------------ host fake
 // The data plane of an in-process fake world: how a matched send's bytes
 // reach its receive. The host fake copies host memory at match time; the
