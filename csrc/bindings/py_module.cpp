@@ -251,15 +251,6 @@ PYBIND11_MODULE(_C, m) {
                    P<void>(zero), B, relu, S(stream), dbg);
   }, py::arg("x"), py::arg("wf"), py::arg("bias"), py::arg("wdf"), py::arg("bd"), py::arg("y"), py::arg("yd"),
         py::arg("zero"), py::arg("B"), py::arg("relu"), py::arg("stream"), py::arg("dbg") = 0);
-  m.def("bottleneck_img_supported", &bottleneck_img_supported);
-  m.def("bottleneck_img", [](uintptr_t x, uintptr_t w1, uintptr_t a1, uintptr_t b1, uintptr_t wf2, uintptr_t b2,
-                             uintptr_t w3, uintptr_t b3, uintptr_t y, float res_scale, float out_inv_scale, int B, int H,
-                             int C, int M, uintptr_t stream, int dbg) {
-    bottleneck_img(P<void>(x), P<void>(w1), P<float>(a1), P<float>(b1), P<void>(wf2), P<float>(b2), P<void>(w3),
-                   P<float>(b3), P<void>(y), res_scale, out_inv_scale, B, H, C, M, S(stream), dbg);
-  }, py::arg("x"), py::arg("w1"), py::arg("a1"), py::arg("b1"), py::arg("wf2"), py::arg("b2"), py::arg("w3"),
-        py::arg("b3"), py::arg("y"), py::arg("res_scale"), py::arg("out_inv_scale"), py::arg("B"), py::arg("H"),
-        py::arg("C"), py::arg("M"), py::arg("stream") = 0, py::arg("dbg") = 0);
   m.def("conv_small_supported", &conv_small_supported);
   m.def("conv_small_pick_mf", &conv_small_pick_mf);
   m.def("conv_small_set_mf", &conv_small_set_mf);
@@ -273,10 +264,10 @@ PYBIND11_MODULE(_C, m) {
         py::arg("stream"), py::arg("wdf") = 0, py::arg("bd") = 0, py::arg("yd") = 0);
   m.def("conv3x3_rows28_supported", &conv3x3_rows28_supported);
   m.def("conv3x3_rows28", [](uintptr_t x, uintptr_t wf, uintptr_t bias, uintptr_t res, uintptr_t y, int B, bool relu,
-                             uintptr_t stream, int dbg) {
-    conv3x3_rows28(P<void>(x), P<void>(wf), P<float>(bias), P<void>(res), P<void>(y), B, relu, S(stream), dbg);
+                             uintptr_t stream) {
+    conv3x3_rows28(P<void>(x), P<void>(wf), P<float>(bias), P<void>(res), P<void>(y), B, relu, S(stream));
   }, py::arg("x"), py::arg("wf"), py::arg("bias"), py::arg("res"), py::arg("y"), py::arg("B"), py::arg("relu"),
-        py::arg("stream"), py::arg("dbg") = 0);
+        py::arg("stream"));
   m.def("stem_conv_pool_u8", [](uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y, int B, int S_, int strip,
                                 uintptr_t stream) {
     stem_conv_pool_u8(P<uint8_t>(x), P<void>(w), P<float>(bias), P<void>(y), B, S_, strip, S(stream));

@@ -450,10 +450,10 @@ bool conv3x3_rows28_supported(int H, int W, int Cin, int Cout) {
 }
 
 void conv3x3_rows28(const void* x, const void* wf, const float* bias, const void* res, void* y, int B, bool relu,
-                    hipStream_t s, int dbg, float out_inv_scale, const void* xds, const void* wds, const float* bds) {
+                    hipStream_t s, float out_inv_scale, const void* xds, const void* wds, const float* bds) {
   if (B <= 0) return;
   if (xds || wds || bds) {  // the block's downsample as 2 more K steps (ds_into_conv2)
-    if (!xds || !wds || !bds || res || dbg || out_inv_scale > 0.f || !x || !wf || !bias || !y ||
+    if (!xds || !wds || !bds || res || out_inv_scale > 0.f || !x || !wf || !bias || !y ||
         (((uintptr_t)x | (uintptr_t)wf | (uintptr_t)xds | (uintptr_t)wds | (uintptr_t)y) & 15))
       throw std::invalid_argument("conv3x3_rows28: downsample K steps need xds, wds, bds (no residual, bf16 out)");
     if (x == y || xds == y) throw std::invalid_argument("conv3x3_rows28: in-place not supported");
@@ -471,7 +471,7 @@ void conv3x3_rows28(const void* x, const void* wf, const float* bias, const void
     DMLC_HIP_CHECK(hipGetLastError());
     return;
   }
-  if (out_inv_scale > 0.f && (res || dbg)) throw std::invalid_argument("conv3x3_rows28: e4m3 output without residual only");
+  if (out_inv_scale > 0.f && res) throw std::invalid_argument("conv3x3_rows28: e4m3 output without residual only");
   if (!x || !wf || !bias || !y ||
       (((uintptr_t)x | (uintptr_t)wf | (uintptr_t)res | (uintptr_t)y) & 15))
     throw std::invalid_argument("conv3x3_rows28: null / misaligned operand");
@@ -490,35 +490,13 @@ void conv3x3_rows28(const void* x, const void* wf, const float* bias, const void
     DMLC_HIP_CHECK(hipGetLastError());
     return;
   }
-  const int ah = (dbg == 64 || dbg == 65) ? 2 : 1;
-  // (the default residual form double-buffers the residual one step ahead)
-  // (DMLC_ROWS28_RES1=1: the round-4 single residual buffer, A/B)
-  static const bool res1 = getenv("DMLC_ROWS28_RES1") && atoi(getenv("DMLC_ROWS28_RES1"));
-  const bool res2 = res && ah == 1 && dbg != 129 && !res1;
-  const size_t lds = (size_t)(ah == 2 ? R28Ring<2>::kSlotsAlloc : R28Ring<1>::kSlotsAlloc) * kRB +
-                     (res ? (size_t)(res2 ? 2 : 1) * kResCh * 16 : 0);  // 90 / 146 KB (two ahead: 123 / 151 KB)
-  static_assert(R28Ring<2>::kSlotsAlloc * kRB + kResCh * 16 <= 160 * 1024, "LDS budget");
+  // (the residual is double-buffered one step ahead: RES2)
+  const size_t lds = (size_t)R28Ring<1>::kSlotsAlloc * kRB + (res ? (size_t)2 * kResCh * 16 : 0);  // 90 / 151 KB
   static_assert(R28Ring<1>::kSlotsAlloc * kRB + 2 * kResCh * 16 <= 160 * 1024, "LDS budget");
-  switch (dbg) {
-    case 64: hipLaunchKernelGGL((conv3x3_rows28_kernel<false, 0, 2>), dim3(B), dim3(256), lds, s, a); break;
-    case 65: hipLaunchKernelGGL((conv3x3_rows28_kernel<true, 0, 2>), dim3(B), dim3(256), lds, s, a); break;
-    case 128: hipLaunchKernelGGL((conv3x3_rows28_kernel<false, 0, 1, 8>), dim3(B), dim3(512), lds, s, a); break;
-    case 129: hipLaunchKernelGGL((conv3x3_rows28_kernel<true, 0, 1, 8>), dim3(B), dim3(512), lds, s, a); break;
-    case 1: hipLaunchKernelGGL((conv3x3_rows28_kernel<false, 1>), dim3(B), dim3(256), lds, s, a); break;
-    case 2: hipLaunchKernelGGL((conv3x3_rows28_kernel<false, 2>), dim3(B), dim3(256), lds, s, a); break;
-    case 4: hipLaunchKernelGGL((conv3x3_rows28_kernel<false, 4>), dim3(B), dim3(256), lds, s, a); break;
-    case 7: hipLaunchKernelGGL((conv3x3_rows28_kernel<false, 7>), dim3(B), dim3(256), lds, s, a); break;
-    case 8: hipLaunchKernelGGL((conv3x3_rows28_kernel<false, 8>), dim3(B), dim3(256), lds, s, a); break;
-    case 16: hipLaunchKernelGGL((conv3x3_rows28_kernel<false, 16>), dim3(B), dim3(256), lds, s, a); break;
-    case 32: hipLaunchKernelGGL((conv3x3_rows28_kernel<false, 32>), dim3(B), dim3(256), lds, s, a); break;
-    default:
-      if (res && !res2)
-        hipLaunchKernelGGL((conv3x3_rows28_kernel<true, 0, 1, 4, false, false, false>), dim3(B), dim3(256), lds, s, a);
-      else if (res)
-        hipLaunchKernelGGL(conv3x3_rows28_kernel<true>, dim3(B), dim3(256), lds, s, a);
-      else
-        hipLaunchKernelGGL(conv3x3_rows28_kernel<false>, dim3(B), dim3(256), lds, s, a);
-  }
+  if (res)
+    hipLaunchKernelGGL(conv3x3_rows28_kernel<true>, dim3(B), dim3(256), lds, s, a);
+  else
+    hipLaunchKernelGGL(conv3x3_rows28_kernel<false>, dim3(B), dim3(256), lds, s, a);
   DMLC_HIP_CHECK(hipGetLastError());
 }
 

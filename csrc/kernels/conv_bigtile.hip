@@ -111,14 +111,10 @@ __device__ __forceinline__ void wait_younger(int y) {
   vm_wait<0>();
 }
 
-// DBG (DMLC_BT_DEBUG=<bits> at first launch selects the instrumented build):
-// 1 skip in-loop DMA, 2 skip MFMA, 4 skip epilogue, 8 skip prologue DMA,
-// 16 skip output stores, 32 per-workgroup phase stamps into a.ws.
-template <int BM, int BN, int WM, int WN, int NS, bool DBG>
+template <int BM, int BN, int WM, int WN, int NS>
 __global__ __launch_bounds__(512, 1) void conv_bt_kernel(ConvArgs a, int k_tiles, int tiles, int splits,
                                                          float* __restrict__ slabs, unsigned* __restrict__ flags,
-                                                         unsigned* __restrict__ err, int dbg_bits) {
-  const int dbg = DBG ? dbg_bits : 0;
+                                                         unsigned* __restrict__ err) {
   constexpr int BK = 32;    // bf16 per pipeline sub-tile (one 64-B LDS row)
   constexpr int ROWB = 64;
   constexpr int PA = BM / 128, PB = BN / 128;  // rows staged per lane (8 waves x 16 rows per DMA instruction)
@@ -135,16 +131,6 @@ __global__ __launch_bounds__(512, 1) void conv_bt_kernel(ConvArgs a, int k_tiles
 
   extern __shared__ __attribute__((aligned(16))) uint4 smem[];
 
-  // debug (DMLC_BT_DEBUG & 32): per-workgroup phase stamps (100 MHz clock) into a.ws
-  unsigned long long* stamps = (dbg & 32) && a.ws ? (unsigned long long*)a.ws + blockIdx.x * 4 : nullptr;
-  // (a stamp consumed only at the end would stay a pending scalar-memory op
-  // through the K loop: it shares lgkmcnt with the LDS reads and completes out
-  // of order, which turns every counted LDS wait into lgkmcnt(0))
-  unsigned long long t_start = 0;
-  if (stamps) {
-    t_start = __builtin_amdgcn_s_memrealtime();
-    asm volatile("" ::"s"(t_start));
-  }
   int tile, slice;
   if (!bt_unit(blockIdx.x, tiles, splits, tile, slice)) return;
   tile = __builtin_amdgcn_readfirstlane(tile);  // provably uniform: scalar buffer descriptors, no waterfall loops
@@ -273,7 +259,6 @@ __global__ __launch_bounds__(512, 1) void conv_bt_kernel(ConvArgs a, int k_tiles
   };
 #pragma unroll
   for (int s2 = 0; s2 < D; ++s2) {
-    if (dbg & 8) break;
     const int tn = k0 + s2;
     const bool valid = tn < k1;
     const int tap = tn / ctiles, c0 = (tn - tap * ctiles) * BK, kh = tap / a.KW, kw = tap - kh * a.KW;
@@ -282,18 +267,13 @@ __global__ __launch_bounds__(512, 1) void conv_bt_kernel(ConvArgs a, int k_tiles
     for (int g = 0; g < G; ++g) issue_one(g, sbase, (kh * a.W + kw) * a.Cin + c0, kh, kw, valid, w + tn * BK);
   }
   int st = 0;
-  unsigned long long t_first = 0;
   for (int t = k0; t < k1; ++t) {
     vm_wait<(D - 1) * G>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (stamps && t == k0) {
-      t_first = __builtin_amdgcn_s_memrealtime();
-      asm volatile("" ::"s"(t_first));
-    }
     const int tn = t + D;
-    const bool valid = tn < k1 && !(dbg & 1);
+    const bool valid = tn < k1;
     const int tap = tn / ctiles, c0 = (tn - tap * ctiles) * BK, kh = tap / a.KW, kw = tap - kh * a.KW;
     const int off = (kh * a.W + kw) * a.Cin + c0;
     char* rbase = (char*)smem + (st == 0 ? NS - 1 : st - 1) * STAGE_B;
@@ -307,25 +287,20 @@ __global__ __launch_bounds__(512, 1) void conv_bt_kernel(ConvArgs a, int k_tiles
 #pragma unroll
     for (int i = 0; i < TN; ++i) {
       if (i < G) issue_one(i, rbase, off, kh, kw, valid, wt);
-      if (!(dbg & 2)) {
 #pragma unroll
-        for (int j = 0; j < TM; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bm[j], acc[i][j], 0, 0, 0);
-      }
+      for (int j = 0; j < TM; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bm[j], acc[i][j], 0, 0, 0);
     }
-    if constexpr (!DBG) {
-      // pin the order: fragment reads, then (1 DMA, TM MFMAs) x TN
-      __builtin_amdgcn_sched_group_barrier(0x100, TN + TM, 0);
+    // pin the order: fragment reads, then (1 DMA, TM MFMAs) x TN
+    __builtin_amdgcn_sched_group_barrier(0x100, TN + TM, 0);
 #pragma unroll
-      for (int i = 0; i < TN; ++i) {
-        if (i < G) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, TM, 0);
-      }
+    for (int i = 0; i < TN; ++i) {
+      if (i < G) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, TM, 0);
     }
     st = st == NS - 1 ? 0 : st + 1;
   }
 
-  const unsigned long long t_loop = stamps ? __builtin_amdgcn_s_memrealtime() : 0;
   const int nslot = splits - 1;
   if (slice == 0 && splits > 1 && tid == 0) {
     for (int s2 = 1; s2 < splits; ++s2) {
@@ -350,7 +325,6 @@ __global__ __launch_bounds__(512, 1) void conv_bt_kernel(ConvArgs a, int k_tiles
   // the bf16 output 128. Heads add the slabs (slice order: deterministic),
   // bias and residual, apply ReLU and store 16 B; contributors store fp32
   // (sc1, write-through) and raise their flag.
-  if (dbg & 4) return;
   static_assert(WTN == 64 && WTM % 64 == 0, "epilogue staging assumes 64-column wave tiles");
   __syncthreads();  // every wave is done reading the operand stages (and the head's flags matched)
   float* wl = (float*)smem + wave * (64 * 64);
@@ -407,10 +381,7 @@ __global__ __launch_bounds__(512, 1) void conv_bt_kernel(ConvArgs a, int k_tiles
         for (int e = 0; e < 8; ++e) v[e] += r[e];
       }
       const uint4 pv = pack8_relu(v, a.relu);
-      if (dbg & 16)
-        asm volatile("" ::"v"(pv.x), "v"(pv.y), "v"(pv.z), "v"(pv.w));
-      else
-        *(uint4*)((bf16*)a.y + o) = pv;
+      *(uint4*)((bf16*)a.y + o) = pv;
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next half overwrites
   }
@@ -418,13 +389,6 @@ __global__ __launch_bounds__(512, 1) void conv_bt_kernel(ConvArgs a, int k_tiles
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains before the signal
     __syncthreads();
     if (tid == 0) __hip_atomic_store(flags + tile * nslot + slice - 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  if (stamps && tid == 0) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    stamps[0] = t_start;
-    stamps[1] = t_first;
-    stamps[2] = t_loop;
-    stamps[3] = __builtin_amdgcn_s_memrealtime();
   }
 }
 
@@ -716,20 +680,13 @@ void conv2d_bigtile(const ConvArgs& a, int cfg, int splits, void* ws, size_t ws_
   float* slabs = ws ? (float*)((char*)ws + kHeader) : nullptr;
   // operand stages (64-B rows), or the epilogue's 8 x 16 KB fp32 staging if larger
   const size_t lds = std::max((size_t)c.ns * (c.bm + c.bn) * 64, (size_t)8 * 64 * 64 * 4);
-  static const int dbg = std::getenv("DMLC_BT_DEBUG") ? std::atoi(std::getenv("DMLC_BT_DEBUG")) : 0;
   const dim3 g((unsigned)grid), b(512);
-  if (cfg == 0 && dbg)
-    hipLaunchKernelGGL((conv_bt_kernel<256, 256, 2, 4, 4, true>), g, b, lds, s, a, k_tiles, (int)tiles, splits, slabs,
-                       flags, err, dbg);
-  else if (cfg == 0)
-    hipLaunchKernelGGL((conv_bt_kernel<256, 256, 2, 4, 4, false>), g, b, lds, s, a, k_tiles, (int)tiles, splits, slabs,
-                       flags, err, 0);
-  else if (dbg)
-    hipLaunchKernelGGL((conv_bt_kernel<256, 128, 4, 2, 5, true>), g, b, lds, s, a, k_tiles, (int)tiles, splits, slabs,
-                       flags, err, dbg);
+  if (cfg == 0)
+    hipLaunchKernelGGL((conv_bt_kernel<256, 256, 2, 4, 4>), g, b, lds, s, a, k_tiles, (int)tiles, splits, slabs,
+                       flags, err);
   else
-    hipLaunchKernelGGL((conv_bt_kernel<256, 128, 4, 2, 5, false>), g, b, lds, s, a, k_tiles, (int)tiles, splits, slabs,
-                       flags, err, 0);
+    hipLaunchKernelGGL((conv_bt_kernel<256, 128, 4, 2, 5>), g, b, lds, s, a, k_tiles, (int)tiles, splits, slabs,
+                       flags, err);
   DMLC_HIP_CHECK(hipGetLastError());
 }
 

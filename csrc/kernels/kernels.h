@@ -181,15 +181,6 @@ bool bottleneck56_supported(int H, int W, int C, int Cm);
 void bottleneck56(const void* x, const void* w1, const float* a1, const float* b1, const void* wf2, const float* b2,
                   const void* wf3, const float* b3, void* y, float res_scale, float out_inv_scale, int B,
                   hipStream_t s, int dbg = 0);
-// ResNet50 identity bottleneck on whole-image workgroups (bottleneck_img.hip):
-// layer3 (H = 14, C = 1024, M = 256) and layer4 (H = 7, C = 2048, M = 512) of
-// resnet50_fp8. x, y e4m3 [B,H,H,C]; w1 e4m3 [M][C] with a1 = s_x * s_w1;
-// wf2 fragment-order bf16 (stream_frag_index, K = 9M); w3 bf16 [C][M];
-// y = relu(conv3(relu(conv2(relu(conv1(x))))) + x) / s_y.
-bool bottleneck_img_supported(int H, int W, int C, int M);
-void bottleneck_img(const void* x, const void* w1, const float* a1, const float* b1, const void* wf2, const float* b2,
-                    const void* w3, const float* b3, void* y, float res_scale, float out_inv_scale, int B, int H, int C,
-                    int M, hipStream_t s, int dbg = 0);
 // ResNet50 layer1.0's reduce 1x1 (64 -> 64) + 3x3 (64 -> 64) as one kernel
 // (bottleneck56.hip, t1 in LDS): x bf16 [B,56,56,64], w1 bf16 [64][64] (BN
 // folded), b1, wf2 / b2 as above, y = t2 bf16 [B,56,56,64].
@@ -218,7 +209,7 @@ bool conv3x3_rows28_supported(int H, int W, int Cin, int Cout);
 // 56, 64] as 2 more K steps (wds fragment order [4][2][2][64][8], K = 64; bds
 // added to bias), instead of a residual read.
 void conv3x3_rows28(const void* x, const void* wf, const float* bias, const void* res, void* y, int B, bool relu,
-                    hipStream_t s, int dbg = 0, float out_inv_scale = 0.f, const void* xds = nullptr,
+                    hipStream_t s, float out_inv_scale = 0.f, const void* xds = nullptr,
                     const void* wds = nullptr, const float* bds = nullptr);  // > 0: e4m3 y, no residual
 // Query-batch 3x3/p1 conv (conv_small.hip) for B <= a few images: one launch
 // per conv, no split-K. x [B,H,W,CI] bf16 NHWC (CI in 64..512), wf: fragment-

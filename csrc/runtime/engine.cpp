@@ -94,7 +94,6 @@ bool EngineOptions::set(const std::string& name, bool v) {
       {"rows28", &EngineOptions::rows28},           {"stem_roles", &EngineOptions::stem_roles},
       {"igemm_small_m", &EngineOptions::igemm_small_m},
       {"small_conv", &EngineOptions::small_conv},
-      {"fused_bottleneck_img", &EngineOptions::fused_bottleneck_img},
   };
   for (const auto& f : fields)
     if (name == f.first) {
@@ -1036,48 +1035,6 @@ bool Engine::bottleneck_fusable(size_t oi) const {
   return true;
 }
 
-// ops[oi..oi+2] = conv1 (1x1 C -> M, e4m3 in, bf16 out) + conv2 (3x3 M -> M,
-// bf16) + conv3 (1x1 M -> C, bf16 in, + the block input, e4m3 out) of a
-// resnet50_fp8 layer3 / layer4 identity block, the intermediates read by
-// nothing else: one bottleneck_img kernel per block.
-bool Engine::bottleneck_img_fusable(size_t oi, int B) const {
-  if (!opt_.fused_bottleneck_img || !fp8_ || oi + 2 >= ops_.size()) return false;
-  // one workgroup per image: only with rounds of images >= ~70% full (as the
-  // ResNet18 block kernel)
-  const int rounds = (B + num_cus_ - 1) / num_cus_;
-  if (10 * B < 7 * rounds * num_cus_) return false;
-  const Op& c1 = ops_[oi];
-  const Op& c2 = ops_[oi + 1];
-  const Op& c3 = ops_[oi + 2];
-  if (c1.type != OpType::Conv || c2.type != OpType::Conv || c3.type != OpType::Conv) return false;
-  if (c1.side || c2.side || c3.side || c2.in != c1.out || c3.in != c2.out || c1.res >= 0 || c2.res >= 0 ||
-      c3.res != c1.in)
-    return false;
-  const ConvLayer& L1 = convs_[c1.conv];
-  const ConvLayer& L2 = convs_[c2.conv];
-  const ConvLayer& L3 = convs_[c3.conv];
-  const ActShape& xs = shapes_[c1.in];
-  const int C = xs.C, M = L1.cout;
-  if (!xs.fp8 || !shapes_[c3.out].fp8 || shapes_[c1.out].fp8 || shapes_[c2.out].fp8) return false;
-  if (!bottleneck_img_supported(xs.H, xs.W, C, M)) return false;
-  if (!L1.fp8 || L1.fc || L1.kh != 1 || L1.kw != 1 || L1.stride != 1 || !L1.relu || L1.kpad != C || L1.npad != M)
-    return false;
-  if (L2.fp8 || L2.kh != 3 || L2.kw != 3 || L2.stride != 1 || L2.pad != 1 || !L2.relu || L2.cout != M ||
-      !L2.wf_off || L2.kpad != 9 * M)
-    return false;
-  if (L3.fp8 || L3.fc || L3.kh != 1 || L3.kw != 1 || L3.stride != 1 || !L3.relu || L3.cout != C || L3.kpad != M ||
-      L3.npad != C)
-    return false;
-  for (size_t j = 0; j < ops_.size(); ++j) {
-    if (j != oi + 1 && (ops_[j].in == c1.out || ops_[j].res == c1.out)) return false;
-    if (j != oi + 2 && (ops_[j].in == c2.out || ops_[j].res == c2.out)) return false;
-  }
-  return true;
-}
-
-// ops[oi..oi+1] = conv1 (1x1 64 -> 64) + conv2 (3x3 64 -> 64) on a bf16
-// 56x56x64 input (ResNet50 layer1.0: the stem's output), conv1's output read
-// by conv2 alone: one bottleneck56_head kernel, t1 kept in LDS.
 bool Engine::bottleneck_head_fusable(size_t oi) const {
   if (!opt_.fused_bottleneck || oi + 1 >= ops_.size()) return false;
   const Op& c1 = ops_[oi];
@@ -1263,17 +1220,6 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
           skip = 2;
           break;
         }
-        if (cs == s && bottleneck_img_fusable(oi, B)) {
-          const ConvLayer& L2 = convs_[ops_[oi + 1].conv];
-          const ConvLayer& L3 = convs_[ops_[oi + 2].conv];
-          const uint8_t* wa = (const uint8_t*)warena_;
-          bottleneck_img(acts_[op.in], wa + L.w_off, (const float*)(wa + L.a_off), (const float*)(wa + L.b_off),
-                         wa + L2.wf_off, (const float*)(wa + L2.b_off), wa + L3.w_off, (const float*)(wa + L3.b_off),
-                         acts_[ops_[oi + 2].out], shapes_[op.in].scale, 1.f / shapes_[ops_[oi + 2].out].scale, B,
-                         shapes_[op.in].H, shapes_[op.in].C, L.cout, s);
-          skip = 2;
-          break;
-        }
         if (cs == s && bottleneck_head_fusable(oi)) {
           const ConvLayer& L2 = convs_[ops_[oi + 1].conv];
           const uint8_t* wa = (const uint8_t*)warena_;
@@ -1406,14 +1352,14 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
               const ConvLayer& D = convs_[ops_[ds_conv2].conv];
               const uint8_t* wa = (const uint8_t*)warena_;
               conv3x3_rows28(acts_[op.in], wa + L.wf_off, (const float*)(wa + L.b_off), nullptr, acts_[op.out], B,
-                             L.relu, cs, 0, 0.f, acts_[ops_[ds_conv2].in], wa + D.wf_off,
+                             L.relu, cs, 0.f, acts_[ops_[ds_conv2].in], wa + D.wf_off,
                              (const float*)(wa + D.b_off));
               ds_conv2 = -1;
               break;
             }
             conv3x3_rows28(acts_[op.in], (const uint8_t*)warena_ + L.wf_off,
                            (const float*)((const uint8_t*)warena_ + L.b_off), op.res >= 0 ? acts_[op.res] : nullptr,
-                           acts_[op.out], B, L.relu, cs, 0, shapes_[op.out].fp8 ? 1.f / shapes_[op.out].scale : 0.f);
+                           acts_[op.out], B, L.relu, cs, shapes_[op.out].fp8 ? 1.f / shapes_[op.out].scale : 0.f);
             break;
           case ConvPath::Rows:
             conv3x3_rows(acts_[op.in], (const uint8_t*)warena_ + L.w_off,

@@ -94,12 +94,6 @@ struct EngineOptions {
   // resnet50_fp8 layer1 identity bottlenecks as one kernel (bottleneck56.hip, compute / memory
   // wave roles): 156-177 vs ~245 us per block, +6% img/s (profiles/r3_bottleneck_v3.txt)
   bool fused_bottleneck = true;
-  // resnet50_fp8 layer2-4 identity bottlenecks as one kernel each
-  // (bottleneck_img.hip: t1 / t2 in LDS and VGPRs); off: slower than the
-  // unfused kernels so far (resnet50_fp8 92k vs 111k img/s same box,
-  // profiles/r4_gpu_session_g2.txt); engages only with fp8_3x3_out off
-  // (it keeps t2 internal)
-  bool fused_bottleneck_img = false;
   bool ds_into_expand = true;    // ResNet50 layer1.0: the 1x1 downsample computed inside conv3 (one K-concat GEMM)
   // ResNet18 layer2.0: the 1x1/s2 downsample as 2 more K steps of conv2
   // (conv3x3_rows28 DSX) instead of an output of conv3x3_s2rows that conv2
@@ -244,7 +238,6 @@ class Engine {
   bool ds_fusable(size_t oi, int B) const;     // ops oi, oi+1 = downsample + stride-2 stream conv1
   bool block_fusable(size_t oi, int B) const;  // ops oi, oi+1 = a layer1 basic block -> conv3x3_block
   bool bottleneck_fusable(size_t oi) const;    // ops oi..oi+2 = a layer1 identity bottleneck -> bottleneck56
-  bool bottleneck_img_fusable(size_t oi, int B) const;  // ops oi..oi+2 = a layer3/4 identity bottleneck -> bottleneck_img
   bool bottleneck_head_fusable(size_t oi) const;  // ops oi, oi+1 = layer1.0's reduce + 3x3 -> bottleneck56_head
   bool bottleneck_conv3(const ConvLayer& L) const;  // L is such a block's expand conv (fragment-order weights)
   int ds_expand_op(size_t oi) const;  // ops[oi] = a downsample folded into a later expand conv: that op, or -1

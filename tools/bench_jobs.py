@@ -64,6 +64,24 @@ def recovery_s(jobs, t_fail_us):
     return max(0.0, (max(after) - base) / 1e6)
 
 
+def resume_s(jobs, t_fail_us, window_s=5.0, slack=3.0):
+    """Time from the failure to the first completion from which answers flow
+    normally again: every gap in the following window_s is at most `slack` x
+    the median gap before the failure (the report's "time to resume normal
+    operation", measured from the failure instant)."""
+    done = sorted(d for j in jobs for d in j["done_us"] if d > 0)
+    before = [b - a for a, b in zip(done, done[1:]) if b < t_fail_us]
+    if not before:
+        return None
+    lim = slack * statistics.median(before)
+    after = [d for d in done if d > t_fail_us]
+    for i, t in enumerate(after):
+        win = [x for x in after[i:] if x <= t + window_s * 1e6]
+        if len(win) >= 2 and all(b - a <= lim for a, b in zip(win, win[1:])):
+            return (t - t_fail_us) / 1e6
+    return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--nodes", type=int, default=4)
@@ -75,6 +93,11 @@ def main():
     ap.add_argument("--adaptive-window", type=int, default=0,
                     help="closed-loop rate: queries in flight per member (0 = fixed --interval-ms tick)")
     ap.add_argument("--kill", choices=["none", "member", "leader"], default="none")
+    ap.add_argument("--fail-mode", choices=["kill", "stop"], default="kill",
+                    help="kill: SIGKILL the victim's process (the kernel closes its sockets: peers see a FIN); "
+                         "stop: SIGSTOP it (a hung node: sockets stay open, nothing answers, no FIN or RST)")
+    ap.add_argument("--standby-copy-ms", type=int, default=250,
+                    help="dmlc-node --standby-copy-ms (the reference copies job state at its 3 s loop period)")
     ap.add_argument("--fast-periods", action="store_true", help="200 ms pings, 1.2 s failure timeout, 500 ms loops")
     ap.add_argument("--port", type=int, default=21000)
     ap.add_argument("--out", default="")
@@ -127,7 +150,8 @@ def main():
     models = ",".join(f"{m}={p}" for m, p in ck.items())
     extra = ["--job-limit", str(a.images), "--query-interval-ms", str(a.interval_ms), "--query-batch",
              str(a.batch), "--quiet-predictions", "--max-batch", str(max(a.max_batch, a.batch)),
-             "--adaptive-window", str(a.adaptive_window)] + (["--prefetch"] if a.prefetch else [])
+             "--adaptive-window", str(a.adaptive_window), "--standby-copy-ms", str(a.standby_copy_ms)] + \
+        (["--prefetch"] if a.prefetch else [])
     cl = LocalCluster(a.nodes, a.port, os.path.join(root, "c"), lab, n_leaders=2, executor=a.executor,
                       dataset=ds, models=models, fast=a.fast_periods, extra=extra)
     if a.kill == "member" and a.nodes < 3:
@@ -181,8 +205,11 @@ def main():
             if a.kill != "none" and t_fail is None and counts and min(counts) >= a.images * 0.3:
                 victim = nodes[0] if a.kill == "leader" else nodes[-1]
                 t_fail = time.time()
-                victim.kill()
-                print(f"# killed {a.kill} {victim.address} at {t_fail - t_predict:.2f}s", file=sys.stderr)
+                if a.fail_mode == "stop":
+                    victim.freeze()
+                else:
+                    victim.kill()
+                print(f"# {a.fail_mode} {a.kill} {victim.address} at {t_fail - t_predict:.2f}s", file=sys.stderr)
             if len(counts) == 2 and min(counts) >= a.images:
                 break
             if int(time.time() - t_predict) % 10 == 0:  # progress (a silent run looks hung)
@@ -209,7 +236,9 @@ def main():
            # the reference copies at its 3 s loop period)
            "periods_ms": ({"ping": 200, "detect": 200, "fail": 1200, "bg": 500, "standby_copy": 250}
                           if a.fast_periods else
-                          {"ping": 1000, "detect": 1000, "fail": 3000, "bg": 3000, "standby_copy": 250}),
+                          {"ping": 1000, "detect": 1000, "fail": 3000, "bg": 3000,
+                           "standby_copy": a.standby_copy_ms}),
+           "fail_mode": a.fail_mode,
            "kill": a.kill,
            "reference": REF, "jobs": []}
     for j in jobs:
@@ -238,6 +267,8 @@ def main():
     res["second_job_first_result_ms"] = round((fd[-1] - fd[0]) / 1000, 3)
     if t_fail is not None:
         res[f"{a.kill}_failure_recovery_s"] = round(recovery_s(jobs, t_fail * 1e6), 3)
+        rs = resume_s(jobs, t_fail * 1e6)
+        res[f"{a.kill}_failure_resume_s"] = round(rs, 3) if rs is not None else None
     line = json.dumps(res)
     print(line)
     if a.out:

@@ -77,9 +77,8 @@ def _run(cmd: list[str], verbose: bool) -> None:
 # (one epilogue edit took the fused ResNet18 block from 103 to 190 us with 372
 # bytes/lane of it) fails the build instead of shipping.
 SCRATCH_REMARK = "-Rpass-analysis=kernel-resource-usage"
-# known and accepted: the fused ResNet50 bottleneck (off by default, at parity
-# with the unfused path) keeps 2 registers in scratch, and the bf16 ResNet50's
-# K = 128 expand conv with residual (conv1x1 RB 256 / NW 64) 5
+# known and accepted: the bf16 ResNet50's K = 128 expand conv with residual
+# (conv1x1 RB 256 / NW 64) keeps 5 registers in scratch
 SCRATCH_ALLOWED = {"kernels_conv1x1.hip.o": 20}
 
 
