@@ -311,13 +311,13 @@ void handle_line(Node& n, const std::string& line) {
       }
     } else if (c == "jobs") {
       if (t.size() != 1) return err_line("Invalid jobs command!");
-      Reader r(n.call_leader(L_JOBS, "", 30000));
+      Reader r(n.call_leader(L_JOBS, "", 5000));
       const uint32_t k = r.u32();
       for (uint32_t i = 0; i < k; ++i) out_line(format_job_report((int)i + 1, read_job(r)));
     } else if (c == "jobs-dump") {
       // machine-readable job state (per-query latency and completion time)
       if (t.size() != 2) return err_line("Invalid jobs-dump command!");
-      Reader r(n.call_leader(L_JOBS, "", 30000));
+      Reader r(n.call_leader(L_JOBS, "", 5000));
       const uint32_t k = r.u32();
       std::ofstream f(absolutize(t[1]));
       f << "[";
@@ -336,7 +336,7 @@ void handle_line(Node& n, const std::string& line) {
       out_line("dumped " + std::to_string(k) + " jobs");
     } else if (c == "assign") {
       if (t.size() != 1) return err_line("Invalid assign command!");
-      Reader r(n.call_leader(L_JOBS, "", 30000));
+      Reader r(n.call_leader(L_JOBS, "", 5000));
       const uint32_t k = r.u32();
       for (uint32_t i = 0; i < k; ++i) {
         const Job j = read_job(r);
@@ -440,6 +440,7 @@ int run_node(const Args& a) {
   mcfg.dataset_dir = a.get("dataset", "test_files/imagenet_1k/train");
   mcfg.leader_candidates = leaders;
   mcfg.check_ms = a.geti("bg-ms", 3000);
+  mcfg.watch_ms = a.geti("watch-ms", 250);
   mcfg.hbm_replicas = !a.has("no-hbm-replicas");
   n->member = std::make_unique<MemberService>(mcfg, n->ms.get(), std::move(ex), labels);
   n->member->start(n->base_port);
@@ -461,6 +462,8 @@ int run_node(const Args& a) {
     lc.print_predictions = !a.has("quiet-predictions");
     lc.new_conn_per_query = a.has("new-conn-per-query");
     lc.max_attempts = a.geti("max-attempts", 3);
+    lc.query_timeout_ms = a.geti("query-timeout-ms", 120000);
+    lc.query_timeout_min_ms = a.geti("query-timeout-min-ms", 1000);
     lc.job_models.clear();
     for (const auto& m : split(a.get("jobs", "resnet18,alexnet"), ','))
       if (!trim(m).empty()) lc.job_models.push_back(trim(m));
@@ -529,7 +532,8 @@ int main(int argc, char** argv) {
                  "                 [--rf 4] [--ping-ms 1000] [--fail-ms 3000] [--bg-ms 3000] [--standby-copy-ms 250]\n"
                  "                 [--query-interval-ms 500] [--adaptive-window 0] [--query-batch 1] [--jobs resnet18,alexnet]\n"
                  "                 [--join h:p] [--daemon] [--stay] [--quiet-predictions] [--new-conn-per-query]\n"
-                 "                 [--max-attempts 3]\n"
+                 "                 [--max-attempts 3] [--watch-ms 250] [--query-timeout-ms 120000]\n"
+                 "                 [--query-timeout-min-ms 1000]\n"
                  "                 [--max-batch 256] [--batch-window-us 200] [--hbm-cache-mb 4096] [--prefetch]\n"
                  "       dmlc-node selftest\n"
                  "       dmlc-node classify --model M --weights W.ot --labels L --image I.JPEG [--executor cpu|gpu]\n";

@@ -100,7 +100,7 @@ void MemberService::start(int base_port) {
   register_handlers();
   server_->start();
   checker_ = std::thread([this] { leader_check_loop(); });
-  if (!cfg_.leader_candidates.empty()) watcher_ = std::thread([this] { leader_watch_loop(); });
+  if (!cfg_.leader_candidates.empty() && cfg_.watch_ms > 0) watcher_ = std::thread([this] { leader_watch_loop(); });
   replicator_ = std::thread([this] { replica_loop(); });
 }
 
@@ -505,9 +505,10 @@ void MemberService::register_handlers() {
   });
 }
 
-bool MemberService::check_leader(const std::string& addr) {
+bool MemberService::check_leader(const std::string& addr, int timeout_ms) {
   try {
-    const std::string resp = RpcClient::shared().call(host_of(addr), leader_port(port_of(addr)), L_ALIVE, "", 2000);
+    const std::string resp =
+        RpcClient::shared().call(host_of(addr), leader_port(port_of(addr)), L_ALIVE, "", timeout_ms);
     Reader r(resp);
     return r.boolean();
   } catch (const std::exception&) {
@@ -517,17 +518,23 @@ bool MemberService::check_leader(const std::string& addr) {
 
 void MemberService::leader_check_loop() {
   while (!stop_.load()) {
+    bool woken;
     {
-      // one check period, or earlier when the watch saw the leader's connection close
+      // one check period, or earlier when the heartbeat saw the leader fail
       std::unique_lock<std::mutex> lk(wake_mu_);
       const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(cfg_.check_ms);
       while (!wake_ && !stop_.load() && cv_wait_until(wake_cv_, lk, deadline) != std::cv_status::timeout) {
       }
+      woken = wake_;
       wake_ = false;
     }
     if (stop_.load() || cfg_.leader_candidates.empty()) break;
     std::string cur = leader_address();
-    if (check_leader(cur)) continue;
+    // (woken: the heartbeat has already seen this leader miss: confirm with
+    // the heartbeat's timeout; with the heartbeat on, the periodic check
+    // waits at most 1 s, so it never holds the checker past a wake for long)
+    if (check_leader(cur, woken || cfg_.watch_ms > 0 ? std::max(woken ? 100 : 1000, 3 * cfg_.watch_ms) : 2000))
+      continue;
     // Advance through the candidate list (wrapping, unlike the reference),
     // at most one full round per check period.
     const auto& c = cfg_.leader_candidates;
@@ -550,43 +557,59 @@ void MemberService::leader_check_loop() {
 void MemberService::leader_watch_loop() {
   // The reference finds a dead leader only by its periodic check
   // (src/services.rs:527-545: one check period of detection on average, a
-  // whole one at worst). The check stays (it also catches a hung leader whose
-  // socket is open), but a crashed or stopped leader's kernel closes its
-  // sockets at once: an idle connection to it turns that close into an
-  // immediate check. A connection dropped for any other reason only costs one
-  // extra check.
+  // whole one at worst). The check stays; this heartbeat shortens detection:
+  // an L_ALIVE probe every watch_ms on the pooled connection. A refused or
+  // closed connection (a crashed process: its kernel sent a FIN or RST) wakes
+  // the checker at once, a hung leader (sockets open, nothing answers) once a
+  // probe times out; the checker confirms with a probe of its own before it
+  // moves the pointer. Only a probe failure after one that succeeded counts
+  // (a leader still coming up is left to the periodic check, as in the
+  // reference), and wakes are at most one per second: a busy leader that
+  // drops a probe costs one extra check (2 s timeout), never a storm.
+  using clock = std::chrono::steady_clock;
+  const int timeout = std::max(100, 3 * cfg_.watch_ms);
+  std::string cur;
+  bool seen_up = false;
+  int missed = 0;
+  auto last_wake = clock::now() - std::chrono::seconds(10);
   while (!stop_.load()) {
-    const std::string cur = leader_address();
-    Fd fd;
-    try {
-      fd = tcp_connect(host_of(cur), leader_port(port_of(cur)), 1000);
-    } catch (const std::exception&) {
+    const std::string now_leader = leader_address();
+    if (now_leader != cur) {  // a new leader: start over
+      cur = now_leader;
+      seen_up = false;
+      missed = 0;
     }
-    bool closed = false;
-    while (fd && !stop_.load() && leader_address() == cur) {
-      pollfd p{fd.get(), POLLIN | POLLRDHUP, 0};
-      const int r = ::poll(&p, 1, 100);
-      if (r < 0 && errno != EINTR) break;
-      if (r > 0) {  // the leader never writes on this connection: readable = closed or reset
-        closed = true;
-        break;
-      }
+    const auto t0 = clock::now();
+    bool ok = false, refused = false;
+    try {
+      const std::string resp =
+          RpcClient::shared().call(host_of(cur), leader_port(port_of(cur)), L_ALIVE, "", timeout);
+      Reader r(resp);
+      ok = r.boolean();
+    } catch (const std::exception& e) {
+      // a timeout takes the whole timeout; a closed / refused connection fails at once
+      refused = clock::now() - t0 < std::chrono::milliseconds(timeout / 2);
     }
     if (stop_.load()) break;
-    // Only the close of an established connection wakes the checker: a leader
-    // not reachable yet (nodes still starting) is left to the periodic check,
-    // as in the reference, so the pointer never moves off a leader that is
-    // still coming up.
-    if (closed) {
-      {
-        std::lock_guard<std::mutex> g(wake_mu_);
-        wake_ = true;
+    if (ok) {
+      seen_up = true;
+      missed = 0;
+    } else if (seen_up && leader_address() == cur) {
+      ++missed;
+      if (clock::now() - last_wake >= std::chrono::seconds(1)) {
+        last_wake = clock::now();
+        {
+          std::lock_guard<std::mutex> g(wake_mu_);
+          wake_ = true;
+        }
+        wake_cv_.notify_all();
+        DMLC_LOG_INFO("leader " << cur << " missed " << missed << " heartbeat(s)" << (refused ? " (connection closed)" : "")
+                                << "; checking now");
       }
-      wake_cv_.notify_all();
     }
-    if (!fd || closed)  // no reconnect storm at an unreachable leader
-      for (int i = 0; i < 4 && !stop_.load() && leader_address() == cur; ++i)
-        std::this_thread::sleep_for(std::chrono::milliseconds(50));
+    const auto next = t0 + std::chrono::milliseconds(cfg_.watch_ms);
+    while (!stop_.load() && clock::now() < next && leader_address() == cur)
+      std::this_thread::sleep_for(std::chrono::milliseconds(20));
   }
 }
 

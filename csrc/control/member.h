@@ -37,6 +37,10 @@ struct MemberConfig {
   std::string dataset_dir;  // imagenet_1k/train layout: <dir>/<wnid>/<file>.JPEG
   std::vector<std::string> leader_candidates;  // base addresses "host:port", in order
   int check_ms = 3000;
+  // leader heartbeat: an L_ALIVE probe of the current leader every watch_ms
+  // (timeout 3 x watch_ms); a closed connection or a missed probe wakes the
+  // leader check at once (0: off, the periodic check alone)
+  int watch_ms = 250;
   int chunk_bytes = 8 << 20;
   bool hbm_replicas = true;  // stage received u8-shard replicas into the executor's blob store (HBM)
 };
@@ -113,7 +117,7 @@ class MemberService {
   void register_handlers();
   void leader_check_loop();
   void leader_watch_loop();
-  bool check_leader(const std::string& addr);
+  bool check_leader(const std::string& addr, int timeout_ms = 2000);
 
   MemberConfig cfg_;
   MembershipService* ms_;
@@ -127,8 +131,9 @@ class MemberService {
   std::string leader_;
   std::atomic<bool> stop_{false};
   std::thread checker_;
-  // Leader watch: an idle TCP connection to the current leader's RPC port
-  // whose close (the leader's process died or stopped) wakes the checker at
+  // Leader watch: a heartbeat to the current leader (MemberConfig::watch_ms)
+  // whose failure (the leader's process died: its connections close; or it
+  // hangs: probes time out with the sockets still open) wakes the checker at
   // once instead of at its next period.
   std::thread watcher_;
   std::mutex wake_mu_;

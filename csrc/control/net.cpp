@@ -134,7 +134,7 @@ void send_all(int fd, const void* p, size_t n) {
     ssize_t w = ::send(fd, c, n, MSG_NOSIGNAL);
     if (w < 0) {
       if (errno == EINTR) continue;
-      throw NetError(std::string("send: ") + strerror(errno));
+      throw NetError(std::string("send: ") + strerror(errno), errno == EAGAIN || errno == EWOULDBLOCK);
     }
     c += w;
     n -= (size_t)w;
@@ -152,7 +152,7 @@ bool recv_all(int fd, void* p, size_t n) {
     }
     if (r < 0) {
       if (errno == EINTR) continue;
-      throw NetError(std::string("recv: ") + strerror(errno));
+      throw NetError(std::string("recv: ") + strerror(errno), errno == EAGAIN || errno == EWOULDBLOCK);
     }
     got += (size_t)r;
   }

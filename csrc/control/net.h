@@ -9,9 +9,10 @@ namespace dmlc {
 namespace ctl {
 
 struct NetError : std::exception {
-  explicit NetError(std::string m) : msg(std::move(m)) {}
+  explicit NetError(std::string m, bool timeout = false) : msg(std::move(m)), timed_out(timeout) {}
   const char* what() const noexcept override { return msg.c_str(); }
   std::string msg;
+  bool timed_out = false;  // a send / recv deadline passed (the peer is there but silent)
 };
 
 // "host:port" -> sockaddr_in (IPv4; hostnames resolved with getaddrinfo).

@@ -1,5 +1,13 @@
 #include "rpc.h"
 
+#include <cerrno>
+
+#include <cstring>
+
+#include <chrono>
+
+#include <poll.h>
+
 #include <sys/socket.h>
 #include <unistd.h>
 
@@ -119,7 +127,7 @@ RpcClient& RpcClient::shared() {
 }
 
 std::string RpcClient::call(const std::string& host, int port, uint16_t method, const std::string& payload,
-                            int timeout_ms, bool fresh) {
+                            int timeout_ms, bool fresh, const std::function<bool()>& alive) {
   const std::string key = host + ":" + std::to_string(port);
   std::string body;
   body.append((const char*)&method, 2);
@@ -148,9 +156,23 @@ std::string RpcClient::call(const std::string& host, int port, uint16_t method, 
     std::string resp;
     try {
       write_frame(conn.get(), body);
+      if (alive) {  // wait for the reply's first bytes in slices, asking the failure detector between them
+        const auto t_end = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms);
+        for (;;) {
+          pollfd p{conn.get(), POLLIN, 0};
+          const int r = ::poll(&p, 1, 250);
+          if (r > 0) break;
+          if (r < 0 && errno != EINTR) throw NetError(std::string("poll: ") + strerror(errno));
+          if (std::chrono::steady_clock::now() >= t_end) throw NetError("reply timed out", true);
+          if (!alive()) throw NetError("peer declared failed while waiting for its reply", true);
+        }
+      }
       if (!read_frame(conn.get(), &resp)) throw NetError("connection closed");
-    } catch (const NetError&) {
-      if (pooled) continue;  // stale pooled socket: retry once fresh
+    } catch (const NetError& e) {
+      // a stale pooled socket (peer restarted: closed / reset) gets one retry
+      // on a fresh connection; a deadline that passed does not (a hung peer
+      // would otherwise cost the caller twice its timeout)
+      if (pooled && !e.timed_out) continue;
       throw;
     }
     if (resp.empty()) throw RpcError("empty response");

@@ -63,8 +63,12 @@ class RpcClient {
   // fresh: a new TCP connection for this call, closed after it (the
   // reference's per-query connect, src/services.rs:420,583-588; the default
   // reuses pooled connections).
+  // alive (optional): polled every 250 ms while the reply has not started
+  // arriving; the call gives up (NetError, timed_out) as soon as it returns
+  // false: the caller's failure detector has declared the peer dead, so a
+  // hung peer costs the call that long instead of its whole timeout.
   std::string call(const std::string& host, int port, uint16_t method, const std::string& payload,
-                   int timeout_ms = 10000, bool fresh = false);
+                   int timeout_ms = 10000, bool fresh = false, const std::function<bool()>& alive = nullptr);
   void drop(const std::string& host, int port);  // close pooled connections
   void clear();
 

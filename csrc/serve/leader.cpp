@@ -59,6 +59,7 @@ void LeaderService::start(int base_port) {
   loops_.emplace_back([this] { rereplicate_loop(); });
   loops_.emplace_back([this] { assign_loop(); });
   loops_.emplace_back([this] { succession_loop(); });
+  loops_.emplace_back([this] { standby_copy_loop(); });
 }
 
 void LeaderService::stop() {
@@ -633,12 +634,19 @@ void LeaderService::query(size_t j, const std::string& model, Id target, Range r
   for (int attempt = 0; attempt < 4 && !stop_.load(); ++attempt) {
     bool transport = false;
     std::string why;
+    int deadline = 0;
     try {
       // the reference connects anew for every query (src/services.rs:420); by
       // default the pooled connection is reused (--new-conn-per-query: fresh)
-      const std::string resp = RpcClient::shared().call(tgt.host(), member_port(tgt.port()),
-                                                        sg ? M_PREDICT_RANGE : M_PREDICT, w.data(), 120000,
-                                                        cfg_.new_conn_per_query);
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        deadline = query_timeout(j);
+      }
+      // (a member the failure detector declares dead ends the wait early:
+      // before the job has a latency history its deadline is the ceiling)
+      const std::string resp = RpcClient::shared().call(
+          tgt.host(), member_port(tgt.port()), sg ? M_PREDICT_RANGE : M_PREDICT, w.data(), deadline,
+          cfg_.new_conn_per_query, [this, &tgt] { return ms_->active_ids().count(tgt) > 0; });
       Reader r(resp);
       if (r.boolean()) {
         const uint32_t m = r.u32();
@@ -661,7 +669,8 @@ void LeaderService::query(size_t j, const std::string& model, Id target, Range r
       transport = true;
       why = e.what();
     }
-    DMLC_LOG_WARN("predict " << model << " on " << tgt.address << " failed: " << why << "; benched");
+    DMLC_LOG_WARN("predict " << model << " on " << tgt.address << " failed: " << why << " (deadline " << deadline
+                             << " ms); benched");
     tried.insert(tgt.address);
     {
       std::lock_guard<std::mutex> g(rng_mu_);
@@ -749,30 +758,25 @@ void LeaderService::assign_loop() {
 }
 
 void LeaderService::succession_loop() {
-  // The member's leader check (every bg period, src/services.rs:527-545) moves
-  // the leader pointer; a standby that finds itself pointed at takes over at
-  // once (the pointer is a local read, polled every 50 ms) instead of at its
-  // own next bg tick, which added up to a whole further period to a
-  // coordinator fail-over (5.5 s mean with the reference's periods, trials of
-  // 3.3-6.8 s: profiles/r5_recovery_refperiods_leader_before.json). The
-  // standby copy of the job state runs every standby_copy_ms.
+  // The member's leader check (every bg period, src/services.rs:527-545, or at
+  // once when its heartbeat sees the leader miss) moves the leader pointer; a
+  // standby that finds itself pointed at takes over at once (the pointer is a
+  // local read, polled every 50 ms) instead of at its own next bg tick, which
+  // added up to a whole further period to a coordinator fail-over (5.5 s mean
+  // with the reference's periods, trials of 3.3-6.8 s:
+  // profiles/r5_recovery_refperiods_leader_before.json). The job-state copy
+  // runs in its own loop (standby_copy_loop), so a copy call stuck on a hung
+  // leader never delays the take-over.
   std::string last = member_->leader_address();
-  const auto copy_period = std::chrono::milliseconds(std::max(50, cfg_.standby_copy_ms));
-  auto next_copy = std::chrono::steady_clock::now() + copy_period;
   while (!stop_.load()) {
     std::this_thread::sleep_for(std::chrono::milliseconds(50));
     if (stop_.load()) break;
     const std::string leader = member_->leader_address();
-    const bool took_over = last != self_ && leader == self_;
-    if (!took_over && std::chrono::steady_clock::now() < next_copy) {
-      last = leader;
-      continue;
-    }
-    next_copy = std::chrono::steady_clock::now() + copy_period;
-    if (took_over) {
+    if (last != self_ && leader == self_) {
       bool resume;
       {
         std::lock_guard<std::mutex> g(mu_);
+        leading_ = true;
         resume = !jobs_.empty() && !jobs_[0].durations_us.empty();
       }
       {
@@ -784,37 +788,74 @@ void LeaderService::succession_loop() {
       DMLC_LOG_WARN("became leader" << (resume ? "; resuming jobs" : ""));
       if (resume) predict();
     } else if (leader != self_) {
-      try {  // standby: copy job progress AND the SDFS directory from the leader
-        // incremental: only the queries completed since the last copy move
-        // (the per-query vectors grow with every query; re-sending them all
-        // each period made the copy cost grow with the job)
-        Writer req;
-        {
-          std::lock_guard<std::mutex> g(mu_);
-          req.u32((uint32_t)jobs_.size());
-          for (const auto& j : jobs_) req.u32((uint32_t)std::min(j.durations_us.size(), j.done_us.size()));
-        }
-        const std::string resp =
-            RpcClient::shared().call(host_of(leader), leader_port(port_of(leader)), L_STATE, req.data(), 5000);
-        Reader r(resp);
-        const uint32_t nj = r.u32();
-        std::lock_guard<std::mutex> g(mu_);
-        std::vector<Job> js = jobs_;
-        bool aligned = nj == js.size();
-        for (uint32_t i = 0; i < nj; ++i) {
-          Job tmp;
-          Job& dst = aligned ? js[i] : tmp;
-          if (!read_job_delta(r, dst)) aligned = false;
-        }
-        Directory d = read_directory(r);
-        if (aligned) jobs_ = std::move(js);
-        else for (auto& j : jobs_) j.durations_us.clear(), j.done_us.clear();  // full copy next time
-        dir_ = std::move(d);
-      } catch (const std::exception&) {
-      }
+      std::lock_guard<std::mutex> g(mu_);
+      leading_ = false;
     }
     last = leader;
   }
+}
+
+void LeaderService::standby_copy_loop() {
+  // A standby copies the leader's job progress every standby_copy_ms
+  // (incremental: only the queries completed since the last copy move; the
+  // per-query vectors grow with every query, so re-sending them all each
+  // period made the copy cost grow with the job) and the SDFS directory every
+  // bg period (the reference's copy period; it changes only on put / delete /
+  // re-replication, so copying it at the job-progress rate was 12x the state
+  // traffic and leader-mutex time for nothing: ADVICE r5).
+  const auto copy_period = std::chrono::milliseconds(std::max(50, cfg_.standby_copy_ms));
+  const auto dir_period = std::chrono::milliseconds(std::max(cfg_.bg_ms, cfg_.standby_copy_ms));
+  auto next_dir = std::chrono::steady_clock::now();
+  while (!stop_.load()) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (auto t = t0; !stop_.load() && t < t0 + copy_period; t = std::chrono::steady_clock::now())
+      std::this_thread::sleep_for(std::chrono::milliseconds(std::min<int64_t>(50, cfg_.standby_copy_ms)));
+    if (stop_.load()) break;
+    const std::string leader = member_->leader_address();
+    if (leader == self_) continue;
+    const bool want_dir = std::chrono::steady_clock::now() >= next_dir;
+    try {
+      Writer req;
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        req.u32((uint32_t)jobs_.size());
+        for (const auto& j : jobs_) req.u32((uint32_t)std::min(j.durations_us.size(), j.done_us.size()));
+      }
+      req.boolean(want_dir);
+      // (a copy waits at most one copy period: a hung leader stalls only this loop)
+      const std::string resp = RpcClient::shared().call(host_of(leader), leader_port(port_of(leader)), L_STATE,
+                                                        req.data(), std::max(1000, cfg_.standby_copy_ms));
+      Reader r(resp);
+      const uint32_t nj = r.u32();
+      std::lock_guard<std::mutex> g(mu_);
+      if (leading_) continue;  // took over meanwhile: this node's own progress is the truth now
+      std::vector<Job> js = jobs_;
+      bool aligned = nj == js.size();
+      for (uint32_t i = 0; i < nj; ++i) {
+        Job tmp;
+        Job& dst = aligned ? js[i] : tmp;
+        if (!read_job_delta(r, dst)) aligned = false;
+      }
+      const bool has_dir = r.boolean();
+      if (has_dir) {
+        dir_ = read_directory(r);
+        next_dir = std::chrono::steady_clock::now() + dir_period;
+      }
+      if (aligned) jobs_ = std::move(js);
+      else for (auto& j : jobs_) j.durations_us.clear(), j.done_us.clear();  // full copy next time
+    } catch (const std::exception&) {
+    }
+  }
+}
+
+int LeaderService::query_timeout(size_t j) const {
+  const auto& d = jobs_[j].durations_us;
+  if (d.size() < 20) return cfg_.query_timeout_ms;
+  std::vector<int64_t> recent(d.end() - (ptrdiff_t)std::min<size_t>(d.size(), 256), d.end());
+  const size_t k = recent.size() * 99 / 100;
+  std::nth_element(recent.begin(), recent.begin() + (ptrdiff_t)k, recent.end());
+  const int64_t ms = recent[k] / 100;  // 10 x p99 (us -> ms)
+  return (int)std::max<int64_t>(cfg_.query_timeout_min_ms, std::min<int64_t>(cfg_.query_timeout_ms, ms));
 }
 
 void LeaderService::register_handlers() {
@@ -937,11 +978,13 @@ void LeaderService::register_handlers() {
       const uint32_t n = r.u32();
       for (uint32_t i = 0; i < n; ++i) have.push_back(r.u32());
     }
+    const bool want_dir = r.left() >= 1 ? r.boolean() : true;
     Writer w;
     std::lock_guard<std::mutex> g(mu_);
     w.u32((uint32_t)jobs_.size());
     for (size_t i = 0; i < jobs_.size(); ++i) write_job_delta(w, jobs_[i], i < have.size() ? have[i] : 0);
-    write_directory(w, dir_);
+    w.boolean(want_dir);
+    if (want_dir) write_directory(w, dir_);
     return w.take();
   });
 }

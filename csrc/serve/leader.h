@@ -59,6 +59,13 @@ struct LeaderConfig {
   bool print_predictions = true;
   bool new_conn_per_query = false;  // the reference's per-query TCP connect (src/services.rs:420)
   int max_attempts = 3;  // sends of one query (across members and requeues) before it is dropped
+  // A query's RPC deadline: 10 x the job's recent p99 query time, within
+  // [query_timeout_min_ms, query_timeout_ms] (query_timeout_ms until 20
+  // queries have completed). A hung member (its socket open, nothing
+  // answering) then costs a query about that long before it is sent
+  // elsewhere, not the fixed ceiling.
+  int query_timeout_ms = 120000;
+  int query_timeout_min_ms = 1000;
   std::vector<std::string> job_models = {"resnet18", "alexnet"};
 };
 
@@ -109,6 +116,8 @@ class LeaderService {
   void rereplicate_loop();
   void assign_loop();
   void succession_loop();
+  void standby_copy_loop();
+  int query_timeout(size_t j) const;  // under mu_
   void sleep_bg();
 
   LeaderConfig cfg_;
@@ -122,6 +131,7 @@ class LeaderService {
   std::vector<Job> jobs_;
   std::vector<bool> running_;
   std::atomic<bool> stop_{false};
+  bool leading_ = false;  // took over as leader (the standby copy stops applying), under mu_
   std::vector<std::thread> loops_;
   std::mutex runners_mu_;
   std::vector<std::thread> runners_;

@@ -106,6 +106,13 @@ class NodeProcess:
             os.killpg(self.proc.pid, signal.SIGKILL)
             self.proc.wait(timeout=10)
 
+    def freeze(self) -> None:
+        """A hung node (failure tests): SIGSTOP the process group. Its sockets
+        stay open and nothing answers: peers see no FIN or RST, only silence.
+        kill() still ends it."""
+        if self.proc.poll() is None:
+            os.killpg(self.proc.pid, signal.SIGSTOP)
+
     def stop(self) -> None:
         if self.proc.poll() is None:
             try:

@@ -180,6 +180,49 @@ def test_predict_jobs_assign_and_leader_failover(env, tmp_path):
         assert "Model: resnet18" in rep and "Model: alexnet" in rep and "ms p95" in rep
 
 
+@pytest.mark.parametrize("victim", ["leader", "member"])
+def test_hung_node_failover(env, tmp_path, victim):
+    """A node that hangs (SIGSTOP: its sockets stay open, nothing answers, no
+    FIN or RST) instead of crashing, with the reference's periods (1 s pings,
+    3 s failure timeout, 3 s loops): a hung leader is found by the members'
+    heartbeat (csrc/control/member.cpp leader_watch_loop) and the standby
+    takes over and resumes the jobs; a hung member costs a query its adaptive
+    deadline (csrc/serve/leader.cpp query_timeout), then the query goes to
+    another member. Either way answers flow again within a few seconds and
+    both jobs finish."""
+    models = f"resnet18={env['models']['resnet18']},alexnet={env['models']['alexnet']}"
+    base = 19700 if victim == "leader" else 19800
+    cl = LocalCluster(4, base, str(tmp_path / "c"), env["labels"], n_leaders=2, executor="cpu",
+                      dataset=env["dataset"], models=models, fast=False,
+                      extra=["--job-limit", "48", "--query-interval-ms", "250", "--quiet-predictions",
+                             "--standby-copy-ms", "3000"])
+    with cl:
+        n = cl.nodes
+        time.sleep(4.0)  # one assignment round at the reference's 3 s period
+        n[3].cmd("predict")
+        time.sleep(4.0)
+        before = _job_counts(n[3])
+        assert len(before) == 2 and all(c[1] > 0 for c in before), before
+        hung = n[0] if victim == "leader" else n[2]
+        t0 = time.time()
+        hung.freeze()
+        deadline = t0 + 90
+        counts, resumed = [], None
+        while time.time() < deadline:
+            try:
+                counts = _job_counts(n[3])
+            except Exception:  # noqa: BLE001  (leader switch in progress, or the hung leader timed out)
+                counts = []
+            if resumed is None and len(counts) == 2 and sum(c[1] for c in counts) > sum(c[1] for c in before) + 4:
+                resumed = time.time() - t0
+            if len(counts) == 2 and all(c[1] >= 48 for c in counts):
+                break
+            time.sleep(0.5)
+        assert len(counts) == 2 and all(c[1] >= 48 for c in counts), counts
+        assert resumed is not None and resumed < 15, resumed
+        hung.kill()
+
+
 def test_adaptive_rate_jobs(env, tmp_path):
     """--adaptive-window: no tick, each job keeps a window of queries in flight
     per assigned member (least-outstanding routing), so with a 10 s tick set

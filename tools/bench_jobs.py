@@ -64,20 +64,22 @@ def recovery_s(jobs, t_fail_us):
     return max(0.0, (max(after) - base) / 1e6)
 
 
-def resume_s(jobs, t_fail_us, window_s=5.0, slack=3.0):
+def resume_s(jobs, t_fail_us, window_s=3.0, frac=0.75):
     """Time from the failure to the first completion from which answers flow
-    normally again: every gap in the following window_s is at most `slack` x
-    the median gap before the failure (the report's "time to resume normal
+    at the normal rate again: at least `frac` of the pre-failure completion
+    rate over the following window_s (the report's "time to resume normal
     operation", measured from the failure instant)."""
     done = sorted(d for j in jobs for d in j["done_us"] if d > 0)
-    before = [b - a for a, b in zip(done, done[1:]) if b < t_fail_us]
-    if not before:
+    pre = [d for d in done if t_fail_us - 10e6 <= d < t_fail_us]
+    if len(pre) < 2 or pre[-1] <= pre[0]:
         return None
-    lim = slack * statistics.median(before)
+    rate = (len(pre) - 1) / ((pre[-1] - pre[0]) / 1e6)  # completions per second before the failure
     after = [d for d in done if d > t_fail_us]
     for i, t in enumerate(after):
-        win = [x for x in after[i:] if x <= t + window_s * 1e6]
-        if len(win) >= 2 and all(b - a <= lim for a, b in zip(win, win[1:])):
+        if t + window_s * 1e6 > done[-1]:
+            break  # too close to the end of the jobs to judge
+        n = sum(1 for x in after[i:] if x < t + window_s * 1e6)
+        if n >= frac * rate * window_s:
             return (t - t_fail_us) / 1e6
     return None
 
@@ -96,6 +98,7 @@ def main():
     ap.add_argument("--fail-mode", choices=["kill", "stop"], default="kill",
                     help="kill: SIGKILL the victim's process (the kernel closes its sockets: peers see a FIN); "
                          "stop: SIGSTOP it (a hung node: sockets stay open, nothing answers, no FIN or RST)")
+    ap.add_argument("--keep-logs", action="store_true", help="write every node's console to <tmp root>/node<port>.log")
     ap.add_argument("--standby-copy-ms", type=int, default=250,
                     help="dmlc-node --standby-copy-ms (the reference copies job state at its 3 s loop period)")
     ap.add_argument("--fast-periods", action="store_true", help="200 ms pings, 1.2 s failure timeout, 500 ms loops")
@@ -222,6 +225,11 @@ def main():
             nd.stop()
         for nd in nodes:
             nd.kill()
+        if a.keep_logs:  # every node's console output, for failure timelines
+            for nd in nodes:
+                with open(os.path.join(root, f"node{nd.port}.log"), "w") as f:
+                    f.write(nd.output())
+            print(f"# node logs in {root}", file=sys.stderr)
     res = {"bench": "two concurrent predict jobs through the control plane", "nodes": a.nodes,
            "executor": a.executor, "gpus": ngpu, "images_per_job": a.images, "query_interval_ms": a.interval_ms,
            "adaptive_window": a.adaptive_window,
@@ -266,6 +274,7 @@ def main():
     res["second_job_start_ms"] = round((st[-1] - st[0]) / 1000, 3)
     res["second_job_first_result_ms"] = round((fd[-1] - fd[0]) / 1000, 3)
     if t_fail is not None:
+        res["t_fail_unix_s"] = round(t_fail, 3)
         res[f"{a.kill}_failure_recovery_s"] = round(recovery_s(jobs, t_fail * 1e6), 3)
         rs = resume_s(jobs, t_fail * 1e6)
         res[f"{a.kill}_failure_resume_s"] = round(rs, 3) if rs is not None else None

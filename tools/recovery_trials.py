@@ -65,8 +65,8 @@ def main():
                              + (" (coordinator)" if kind == "leader" else " (a non-coordinator member)"),
                "definition": "longest gap between consecutive query completions (either job) after the failure, "
                              "minus the median gap before it (tools/bench_jobs.py recovery_s)",
-               "definition_resume": "time from the failure to the first completion after which every gap for 5 s "
-                                    "is <= 3x the median gap before it (tools/bench_jobs.py resume_s)",
+               "definition_resume": "time from the failure to the first completion from which the next 3 s hold at "
+                                    "least 75% of the pre-failure completion rate (tools/bench_jobs.py resume_s)",
                "fail_mode": a.fail_mode,
                "resume_trials": ys, "resume_mean_s": round(statistics.mean(ys), 3) if ys else None,
                "resume_std_s": round(statistics.stdev(ys), 3) if len(ys) > 1 else None,
