@@ -269,9 +269,12 @@ PYBIND11_MODULE(_C, m) {
   }, py::arg("x"), py::arg("wf"), py::arg("bias"), py::arg("res"), py::arg("y"), py::arg("B"), py::arg("relu"),
         py::arg("stream"));
   m.def("stem_conv_pool_u8", [](uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y, int B, int S_, int strip,
-                                uintptr_t stream) {
-    stem_conv_pool_u8(P<uint8_t>(x), P<void>(w), P<float>(bias), P<void>(y), B, S_, strip, S(stream));
-  });
+                                uintptr_t stream, uintptr_t w_dense) {
+    stem_conv_pool_u8(P<uint8_t>(x), P<void>(w), P<float>(bias), P<void>(y), B, S_, strip, S(stream),
+                      P<void>(w_dense));
+  }, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("y"), py::arg("B"), py::arg("S"), py::arg("strip"),
+        py::arg("stream"), py::arg("w_dense") = 0);
+  m.def("stem_dense_k_index", &stem_dense_k_index);
   m.def("stem_conv_pool_set_dbg", &stem_conv_pool_set_dbg);
   m.def("stem_conv_pool", [](uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y, int B, int S_, int Wq,
                              int strip, uintptr_t stream) {

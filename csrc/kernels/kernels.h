@@ -275,10 +275,23 @@ void stem_conv_pool(const void* x, const void* w, const float* bias, void* y, in
 // Same stem with the preprocess fused: u8 HWC SxS images [B, S, S, 3] in
 // (already at the target size: the identity case of preprocess_u8), the
 // paired bf16 rows built in LDS with preprocess_u8's exact arithmetic.
+// w_dense (optional, 16-B aligned): the same weights in dense-K order
+// [64][kStemDenseK] (stem_dense_k_index); with it the one-image-per-workgroup
+// kernel runs 5 K steps a fragment instead of 7 (stem_pool.hip, V & 2).
 // timing knock-outs of the 224x224 u8 stem (0 = off; see stem_pool.hip DBG)
 void stem_conv_pool_set_dbg(int dbg);
 void stem_conv_pool_u8(const uint8_t* x, const void* w, const float* bias, void* y, int B, int S, int strip,
-                       hipStream_t s);
+                       hipStream_t s, const void* w_dense = nullptr);
+constexpr int kStemDenseK = 160;
+// dense-K slot of tap (dy, dx, c) of the 7x7x3 stem: K index k holds dword
+// D = 16 (k / 32) + 4 ((k % 8) / 2) + (k % 32) / 8 of the kernel rows' 22-element
+// windows (7 px x rgb + 1 pad) concatenated, element 2 D + k % 2. Returns the
+// k of element (dy, 3 dx + c).
+inline int stem_dense_k_index(int dy, int dx, int c) {
+  const int E = 22 * dy + 3 * dx + c, D = E / 2, h = E % 2;
+  const int s = D / 16, i = (D % 16) / 4, fq = D % 4;
+  return 32 * s + 8 * fq + 2 * i + h;
+}
 // AlexNet features.0-2 fused (alex_stem.hip): u8 [B, 224, 224, 3] ->
 // normalise -> conv 11x11/s4/p2 + bias -> ReLU -> maxpool 3x3/s2 ->
 // [B, 27, 27, 64] bf16. w: [64][544] bf16 in alex_stem_k order.

@@ -66,6 +66,7 @@ constexpr int kRingU8 = 13;
 constexpr int kU8Front = 16, kU8Pad = 80;
 constexpr int kHp = 5;     // horizontally pooled conv rows: carried halo + 4
 constexpr int kK = 224;    // 7 kernel rows x 4 chunks x 8
+constexpr int kKD = 160;   // dense K: 7 kernel rows x 22 (7 px x rgb + 1 pad) -> 5 x 32
 // Pooled-row LDS layout: [pw][64 ch] with a 144-B column stride (128 + 16 pad):
 // the 4 row groups of a wave write columns 2 apart = 288 B = 8 banks apart,
 // so the 16-bit stores are conflict-free and every address is a per-lane
@@ -77,6 +78,7 @@ struct StemArgs {
   const uint8_t* u8;  // fused preprocess: u8 HWC images [B, S, S, 3] (x unused)
   int S;
   const bf16* w;      // [64, 224]
+  const bf16* w2;     // [64, 160] dense-K order (stem_roles_kernel<.., V & 2>), may be null
   const float* bias;  // [64]
   bf16* y;            // [B, PH, PW, 64]
   int Hp, Wq, PH, PW, strip;
@@ -486,11 +488,28 @@ __device__ __forceinline__ void vm_wait_dyn(int n) {
 // (tools/stem_roles_ab.py, profiles/r4_stem_roles.txt): 4 no u8 conversion, 8
 // no conv rows, 16 no horizontal-pool epilogue, 32 no raw-row DMA / vertical
 // max / stores (results wrong: timing only)
+//
+// V bit 2: dense K. The paired rows above hold [r g b r g b 0 0] chunks and
+// a kernel row takes one 32-wide K step of 8 pixels: 7 x 32 = 224 K for 147
+// taps (66% of the MFMAs useful). Dense rows hold the padded row as plain
+// [px][rgb] bf16 (3 * (S + 6) elements, 48 B per 8 pixels: helper stores at
+// a 48-B lane stride, conflict-free), and K runs over the 7 kernel rows'
+// 22-element windows (7 px x rgb + 1 zero-weight slot) concatenated: 154 of
+// 160 = 5 K steps, 20 MFMAs a fragment instead of 28. Lane (fr, fq) of K
+// step s holds dword D = 16 s + 4 i + fq (i = 0..3) of that concatenation:
+// kernel row D / 11, window dword D % 11, so each operand is four
+// ds_read_b32 at per-lane addresses computed once per conv row (a dword
+// never straddles two rows; 6 of the 20 dword slots put some lanes in the
+// next row). Weights: stem_dense_k_index (kernels.h), [64][160].
 template <int NF, int V = 0>
 __global__ __launch_bounds__(512, 1) void stem_roles_kernel(StemArgs a) {
   using G = StemGeom<NF>;
   extern __shared__ __attribute__((aligned(16))) uint4 smem[];
-  constexpr int RB = G::Wq * 16;      // bytes per paired row
+  constexpr bool DK = (V & 2) != 0;
+  constexpr int NG = 4 * NF + 1;      // dense rows: 8-pixel groups of the S + 6 padded pixels
+  static_assert(NG * 8 >= G::S + 6, "dense row groups");
+  constexpr int RB = DK ? NG * 48 : G::Wq * 16;  // bytes per paired / dense row
+  static_assert(!DK || 12 * (16 * NF - 1) + 4 * 13 + 4 <= RB, "dense window reads stay in the row");
   constexpr int UB = G::S * 3;        // bytes per raw image row
   constexpr int UBS = UB + kU8Pad;    // raw ring slot
   constexpr int HPB = G::PW * kHpCol;  // bytes per horizontally pooled conv row
@@ -526,6 +545,39 @@ __global__ __launch_bounds__(512, 1) void stem_roles_kernel(StemArgs a) {
   // raw rows [lo, lo+cnt) -> paired bf16 rows (stem_conv_pool_kernel's
   // convert_rows, over nthr threads)
   auto convert_rows = [&](int lo, int cnt, int t0, int nthr) __attribute__((always_inline)) {
+    if constexpr (DK) {
+      // item = (row, group g): padded pixels 8g .. 8g+7 (image columns 8g-3 ..
+      // 8g+4) -> 24 bf16 at byte 48 g of the dense row, three 16-B stores
+      const int items = cnt * NG;
+      for (int it = t0; it < items; it += nthr) {
+        const int r = lo + it / NG;
+        const int g = it - (it / NG) * NG;
+        if (r < 0) continue;
+        const int iy = r - 3;
+        const bool row_in = iy >= 0 && iy < G::S;
+        const char* srow = u8ring + (r % kRolesRawRing) * UBS + kU8Front;
+        const int A = 24 * g - 12;
+        uint32_t d[7];
+#pragma unroll
+        for (int j = 0; j < 7; ++j) d[j] = row_in ? *(const uint32_t*)(srow + A + 4 * j) : 0u;
+        float v[24];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int ix = 8 * g - 3 + i;
+          const bool in = row_in && ix >= 0 && ix < G::S;
+#pragma unroll
+          for (int c = 0; c < 3; ++c) {
+            const int idx = 3 + 3 * i + c;
+            const float cv = (float)((d[idx >> 2] >> (8 * (idx & 3))) & 0xffu);
+            v[3 * i + c] = in ? imagenet_norm(c, cv) : 0.f;
+          }
+        }
+        char* drow = ring + (r % kRolesPairRing) * RB + g * 48;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) *(uint4*)(drow + q * 16) = pack8(v + 8 * q);
+      }
+      return;
+    }
     const int G4 = (G::Wq + 3) / 4;
     const int items = cnt * G4;
     for (int it = t0; it < items; it += nthr) {
@@ -561,13 +613,16 @@ __global__ __launch_bounds__(512, 1) void stem_roles_kernel(StemArgs a) {
     }
   };
 
-  bf16x8 wf[4][7];
+  constexpr int KS = DK ? kKD / 32 : 7;  // K steps a fragment
+  bf16x8 wf[4][KS];
   float bs[4];
   if (mfma_wave) {
 #pragma unroll
     for (int n = 0; n < 4; ++n)
 #pragma unroll
-      for (int s = 0; s < 7; ++s) wf[n][s] = *(const bf16x8*)(a.w + (n * 16 + fr) * kK + s * 32 + fq * 8);
+      for (int s = 0; s < KS; ++s)
+        wf[n][s] = DK ? *(const bf16x8*)(a.w2 + (n * 16 + fr) * kKD + s * 32 + fq * 8)
+                      : *(const bf16x8*)(a.w + (n * 16 + fr) * kK + s * 32 + fq * 8);
 #pragma unroll
     for (int n = 0; n < 4; ++n) bs[n] = a.bias[n * 16 + fr];
   }
@@ -593,6 +648,73 @@ __global__ __launch_bounds__(512, 1) void stem_roles_kernel(StemArgs a) {
         if (cr < 0) {
           if (wave == 3)
             for (int o = lane * 16; o < HPB; o += 64 * 16) *(uint4*)(hrow + o) = make_uint4(0, 0, 0, 0);
+        } else if constexpr (DK) {
+          // per-lane operand addresses of this conv row: dword slot j = 4 s + i
+          // holds concatenated dword D = 4 j + fq (kernel row D / 11); fragment
+          // f adds 16 * 12 * f bytes (an immediate)
+          int sl[7];
+#pragma unroll
+          for (int dy = 0; dy < 7; ++dy) sl[dy] = ((2 * cr + dy) % kRolesPairRing) * RB;
+          const int lane_off = 12 * fr + 4 * fq;
+          int ad[20];
+#pragma unroll
+          for (int j = 0; j < 20; ++j) {
+            const int dy0 = (4 * j) / 11, d0 = (4 * j) % 11, t = 11 - d0;
+            // (j = 19: dwords 77..79 are zero-weight slots: they read on in
+            // kernel row 6, finite data inside the row)
+            if (t >= 4 || j == 19)
+              ad[j] = lane_off + sl[dy0] + 4 * d0;
+            else
+              ad[j] = lane_off + (fq < t ? sl[dy0] + 4 * d0 : sl[dy0 + 1] - 4 * t);
+          }
+          const uint32_t hbase = lds_addr(hrow) + fq * 2 * kHpCol + (fr >> 3) * 16 + (fr & 7) * 2;
+          uint32_t prevq[2];
+          using u32x4 = uint32_t __attribute__((ext_vector_type(4)));
+          // opaque per-slot addresses: one base register each, so the loads
+          // are not merged into ds_read2 pairs across K steps / fragments
+          // (which land in the wrong registers and cost moves)
+#pragma unroll
+          for (int j = 0; j < 20; ++j) asm volatile("" : "+v"(ad[j]));
+          u32x4 xq[KS], nx[KS];
+#pragma unroll
+          for (int s = 0; s < KS; ++s)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) xq[s][i] = *(const uint32_t*)(ring + ad[4 * s + i]);
+          // Software pipeline, one scheduling region per fragment f: the
+          // operand loads of f + 1, the MFMAs of f, and the pooling epilogue of
+          // f - 1 (its accumulators long complete: no hazard waits, its VALU
+          // and LDS stores fill the MFMA issue gaps)
+          floatx4 acc[2][4];
+#pragma unroll
+          for (int f = 0; f <= NF; ++f) {
+            if (f + 1 < NF) {
+#pragma unroll
+              for (int s = 0; s < KS; ++s)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) nx[s][i] = *(const uint32_t*)(ring + ad[4 * s + i] + (f + 1) * 192);
+            }
+            if (f < NF) {
+#pragma unroll
+              for (int n = 0; n < 4; ++n) acc[f & 1][n] = floatx4{bs[n], bs[n], bs[n], bs[n]};
+#pragma unroll
+              for (int s = 0; s < KS; ++s)
+#pragma unroll
+                for (int n = 0; n < 4; ++n)
+                  acc[f & 1][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, xq[s]),
+                                                                          wf[n][s], acc[f & 1][n], 0, 0, 0);
+            }
+            if (f > 0) {
+              if (V & 16) {
+#pragma unroll
+                for (int n = 0; n < 4; ++n) asm volatile("" ::"v"(acc[(f - 1) & 1][n]));
+              } else {
+                hpool_packed<4>(acc[(f - 1) & 1], prevq, lane, fq, hbase, f - 1, (f - 1) * 8 * kHpCol);
+              }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int s = 0; s < KS; ++s) xq[s] = nx[s];
+          }
         } else {
           const char* rbase = ring + (fr + fq) * 16;
           int rows[7];
@@ -701,8 +823,8 @@ namespace {
 int g_stem_dbg = 0;
 constexpr long kStemSplitCus = 256;  // MI355X CUs: the channel split fills them at query batches  // knock-out variant of the 224x224 u8 kernel (tools/stem_knockouts.py)
 
-void stem_launch(const void* x, const uint8_t* u8, const void* w, const float* bias, void* y, int B, int S, int Wq,
-                 int strip, hipStream_t s) {
+void stem_launch(const void* x, const uint8_t* u8, const void* w, const void* w2, const float* bias, void* y, int B,
+                 int S, int Wq, int strip, hipStream_t s) {
   if (B <= 0) return;
   const int Ho = S / 2, PH = Ho / 2;
   const int NF = Ho / 16;
@@ -710,13 +832,14 @@ void stem_launch(const void* x, const uint8_t* u8, const void* w, const float* b
   if (Wq != stem_row_width(S, 3, 7, 2) / 2) throw std::invalid_argument("stem_conv_pool: bad paired row width");
   if (strip < 2 || strip % 2 || PH % strip) throw std::invalid_argument("stem_conv_pool: bad strip");
   if ((!x && !u8) || !w || !bias || !y || ((uintptr_t)x & 15) || ((uintptr_t)u8 & 3) || ((uintptr_t)w & 15) ||
-      ((uintptr_t)y & 15))
+      ((uintptr_t)y & 15) || ((uintptr_t)w2 & 15))
     throw std::invalid_argument("stem_conv_pool: null / misaligned operand");
   StemArgs a;
   a.x = (const bf16*)x;
   a.u8 = u8;
   a.S = S;
   a.w = (const bf16*)w;
+  a.w2 = (const bf16*)w2;
   a.bias = bias;
   a.y = (bf16*)y;
   a.Hp = S + 6;
@@ -751,6 +874,7 @@ void stem_launch(const void* x, const uint8_t* u8, const void* w, const float* b
                              (size_t)kRolesRawRing * (S * 3 + kU8Pad);
     if (lds_roles > 160 * 1024) throw std::invalid_argument("stem_conv_pool: role-split LDS budget");
     const int rv = (g_stem_dbg >> 24) & 127;
+    if ((rv & 2) && !w2) throw std::invalid_argument("stem_conv_pool: dense-K variant without dense weights");
     if (NF == 7 && rv) {
       switch (rv) {
 #define DMLC_STEM_RV_CASE(V) \
@@ -762,6 +886,12 @@ void stem_launch(const void* x, const uint8_t* u8, const void* w, const float* b
         DMLC_STEM_RV_CASE(36)
         DMLC_STEM_RV_CASE(52)
         DMLC_STEM_RV_CASE(40)
+        DMLC_STEM_RV_CASE(1)
+        DMLC_STEM_RV_CASE(3)
+        DMLC_STEM_RV_CASE(7)
+        DMLC_STEM_RV_CASE(19)
+        DMLC_STEM_RV_CASE(43)
+        DMLC_STEM_RV_CASE(55)
 #undef DMLC_STEM_RV_CASE
         default: throw std::invalid_argument("stem_conv_pool: unknown role-split variant");
       }
@@ -770,6 +900,20 @@ void stem_launch(const void* x, const uint8_t* u8, const void* w, const float* b
     }
     // 16-B raw-row DMA when the images allow it (g_stem_dbg 2048: force the 4-B form)
     const bool d16 = !((uintptr_t)u8 & 15) && !(g_stem_dbg & 2048);
+    if (d16 && w2) {  // dense K (the engine packs both weight orders)
+      switch (NF) {
+#define DMLC_STEM_DENSE_CASE(F) \
+  case F: hipLaunchKernelGGL((stem_roles_kernel<F, 3>), dim3(B), dim3(512), lds_roles, s, a); break;
+        DMLC_STEM_DENSE_CASE(4)
+        DMLC_STEM_DENSE_CASE(5)
+        DMLC_STEM_DENSE_CASE(6)
+        DMLC_STEM_DENSE_CASE(7)
+        DMLC_STEM_DENSE_CASE(8)
+#undef DMLC_STEM_DENSE_CASE
+      }
+      DMLC_HIP_CHECK(hipGetLastError());
+      return;
+    }
     switch (NF * 2 + (d16 ? 1 : 0)) {
 #define DMLC_STEM_ROLES_CASE(F) \
   case 2 * F: hipLaunchKernelGGL((stem_roles_kernel<F>), dim3(B), dim3(512), lds_roles, s, a); break; \
@@ -829,13 +973,13 @@ void stem_conv_pool_set_dbg(int dbg) { g_stem_dbg = dbg; }
 void stem_conv_pool(const void* x, const void* w, const float* bias, void* y, int B, int S, int Wq, int strip,
                     hipStream_t s) {
   if (!x) throw std::invalid_argument("stem_conv_pool: null input");
-  stem_launch(x, nullptr, w, bias, y, B, S, Wq, strip, s);
+  stem_launch(x, nullptr, w, nullptr, bias, y, B, S, Wq, strip, s);
 }
 
 void stem_conv_pool_u8(const uint8_t* x, const void* w, const float* bias, void* y, int B, int S, int strip,
-                       hipStream_t s) {
+                       hipStream_t s, const void* w_dense) {
   if (!x) throw std::invalid_argument("stem_conv_pool_u8: null input");
-  stem_launch(nullptr, x, w, bias, y, B, S, stem_row_width(S, 3, 7, 2) / 2, strip, s);
+  stem_launch(nullptr, x, w, w_dense, bias, y, B, S, stem_row_width(S, 3, 7, 2) / 2, strip, s);
 }
 
 }  // namespace dmlc

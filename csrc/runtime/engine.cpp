@@ -92,6 +92,7 @@ bool EngineOptions::set(const std::string& name, bool v) {
       {"conv1x1", &EngineOptions::conv1x1},         {"s2rows", &EngineOptions::s2rows},
       {"s2rows128", &EngineOptions::s2rows128},
       {"rows28", &EngineOptions::rows28},           {"stem_roles", &EngineOptions::stem_roles},
+      {"stem_dense", &EngineOptions::stem_dense},
       {"igemm_small_m", &EngineOptions::igemm_small_m},
       {"small_conv", &EngineOptions::small_conv},
   };
@@ -593,6 +594,11 @@ std::vector<uint8_t> Engine::pack_host(const WeightMap& w, std::vector<PackRegio
       L.wf_bytes = (size_t)L.cout * L.kpad * 2;
       off = align_up(off + L.wf_bytes, 256);
     }
+    if (L.stem_pool) {  // dense-K order for the one-image-per-workgroup stem (stem_dense_k_index)
+      L.wf_off = off;
+      L.wf_bytes = (size_t)L.cout * kStemDenseK * 2;
+      off = align_up(off + L.wf_bytes, 256);
+    }
     if (L.alex_stem) {  // paired-chunk K order for alex_stem.hip
       L.wf_off = off;
       L.wf_bytes = (size_t)L.cout * kAlexStemK * 2;
@@ -702,7 +708,14 @@ std::vector<uint8_t> Engine::pack_host(const WeightMap& w, std::vector<PackRegio
         }
     }
     for (int n = 0; n < L.cout; ++n) rb.at<float>(n) = bias[n];
-    if (L.alex_stem) {
+    if (L.stem_pool) {
+      for (int n = 0; n < L.cout; ++n)
+        for (int c = 0; c < L.cin; ++c)
+          for (int i = 0; i < L.kh; ++i)
+            for (int j = 0; j < L.kw; ++j)
+              rf.at<uint16_t>((size_t)n * kStemDenseK + stem_dense_k_index(i, j, c)) =
+                  f2bf_host(W.data[(((size_t)n * L.cin + c) * L.kh + i) * L.kw + j] * scale[n]);
+    } else if (L.alex_stem) {
       for (int n = 0; n < L.cout; ++n)
         for (int c = 0; c < L.cin; ++c)
           for (int i = 0; i < L.kh; ++i)
@@ -1403,7 +1416,7 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
                             (const float*)((const uint8_t*)warena_ + L.b_off), acts_[op.out], B, image_size_,
                             opt_.stem_roles ? stem_pool_u8_pick_strip(B, shapes_[op.out].H, num_cus_)
                                             : stem_pool_pick_strip(B, shapes_[op.out].H, num_cus_),
-                            s);
+                            s, opt_.stem_dense && L.wf_off ? (const uint8_t*)warena_ + L.wf_off : nullptr);
           break;
         }
         stem_conv_pool(acts_[op.in], (const uint8_t*)warena_ + L.w_off,

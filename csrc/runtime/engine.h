@@ -110,6 +110,7 @@ struct EngineOptions {
                                  // walking its rows (conv3x3_s2rows.hip), B >= 0.7 x CUs
   bool rows28 = true;            // layer2's stride-1 convs the same way (conv3x3_rows28.hip), B >= 0.7 x CUs
   bool stem_roles = true;        // u8 stem: one workgroup per image with MFMA / helper waves once B >= CUs
+  bool stem_dense = true;        // ... with the dense-K weight order (5 K steps a fragment instead of 7)
   bool bigtile = true;           // 8-wave big-tile split-K convs where picked (not on the ResNet18 b256 path)
   bool conv1x1 = true;           // weight-stationary 1x1 convs (conv1x1.hip: ResNet50 bottlenecks)
   bool fused_pool = true;        // the last conv's epilogue computes the global average pool

@@ -524,6 +524,26 @@ def pack_stem_pool_weight(w: torch.Tensor, scale: torch.Tensor | None = None, de
     return out.to(device) if device is not None else out
 
 
+def pack_stem_dense_weight(w: torch.Tensor, scale: torch.Tensor | None = None, device=None) -> torch.Tensor:
+    """[64, 3, 7, 7] fp32 -> bf16 [64, 160] in the dense-K order of the
+    one-image-per-workgroup stem (stem_pool.hip V & 2): the 7 kernel rows'
+    22-element windows (kw-major rgb + 1 zero slot) concatenated as dwords D,
+    K index k = 32 s + 8 fq + 2 i + h for element 2 D + h, D = 16 s + 4 i + fq."""
+    cout, cin, kh, kw = w.shape
+    if (cout, cin, kh, kw) != (64, 3, 7, 7):
+        raise ValueError("stem_conv_pool packs a [64, 3, 7, 7] weight")
+    w = w.float()
+    if scale is not None:
+        w = w * scale.float().view(-1, 1, 1, 1)
+    cat = torch.zeros(64, 7, 22)
+    cat[:, :, :21] = w.permute(0, 2, 3, 1).reshape(64, 7, 21)  # [n, kh, kw*3 + c]
+    cat = torch.cat([cat.reshape(64, 154), torch.zeros(64, 6)], 1)  # element E = 2 D + h
+    k = torch.arange(160)
+    D = 16 * (k // 32) + 4 * ((k % 8) // 2) + (k % 32) // 8
+    out = cat[:, 2 * D + k % 2].to(torch.bfloat16)
+    return out.to(device) if device is not None else out
+
+
 def stem_conv_pool(x_paired: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, size: int = 224,
                    strip: int | None = None) -> torch.Tensor:
     """Fused conv7x7/s2 + bias + ReLU + maxpool3x3/s2/p1 on the paired image
@@ -543,10 +563,12 @@ def stem_conv_pool(x_paired: torch.Tensor, w_packed: torch.Tensor, bias: torch.T
 
 
 def stem_conv_pool_u8(images: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor,
-                      strip: int | None = None) -> torch.Tensor:
+                      strip: int | None = None, w_dense: torch.Tensor | None = None) -> torch.Tensor:
     """The fused stem with the preprocess fused too: u8 [B, S, S, 3] images
     (already at the model size) -> [B, S/4, S/4, 64]. Same values as
-    ``stem_conv_pool(preprocess_u8(images, S, 3, paired=True), ...)``."""
+    ``stem_conv_pool(preprocess_u8(images, S, 3, paired=True), ...)`` (up to
+    fp32 summation order with ``w_dense``: pack_stem_dense_weight of the same
+    weights, which the one-image-per-workgroup kernel then uses)."""
     _need_cuda(images, w_packed, bias)
     if images.dtype != torch.uint8 or images.dim() != 4 or images.shape[-1] != 3 or images.shape[1] != images.shape[2]:
         raise ValueError("stem_conv_pool_u8 expects uint8 [B, S, S, 3]")
@@ -556,8 +578,12 @@ def stem_conv_pool_u8(images: torch.Tensor, w_packed: torch.Tensor, bias: torch.
     if strip is None:
         strip = C.stem_pool_u8_pick_strip(B, ph, torch.cuda.get_device_properties(images.device).multi_processor_count)
     y = torch.empty(B, ph, ph, 64, device=images.device, dtype=torch.bfloat16)
+    if w_dense is not None:
+        _need_cuda(w_dense)
+        if w_dense.shape != (64, 160) or w_dense.dtype != torch.bfloat16 or not w_dense.is_contiguous():
+            raise ValueError("w_dense must be pack_stem_dense_weight's contiguous bf16 [64, 160]")
     C.stem_conv_pool_u8(_ptr(images.contiguous()), _ptr(w_packed.contiguous()), _ptr(bias.float().contiguous()),
-                        _ptr(y), B, S, strip, _stream())
+                        _ptr(y), B, S, strip, _stream(), _ptr(w_dense) if w_dense is not None else 0)
     return y
 
 

@@ -253,19 +253,29 @@ def test_stem_conv_pool_u8(gpu, B, S, strip):
     wp = ops.pack_stem_pool_weight(w, device=gpu)
     C = dmlc.native()
     pairs = C.stem_row_width(S, 3, 7, 2) // 2
+    wd = ops.pack_stem_dense_weight(w, device=gpu)
     two = ops.stem_conv_pool(ops.preprocess_u8(img, S, 3, 2 * pairs, paired=True), wp, bias, S, strip)
     one = ops.stem_conv_pool_u8(img, wp, bias, strip)
     C.stem_conv_pool_set_dbg(512)  # one workgroup per image, MFMA / helper waves: same arithmetic
     try:
         roles = ops.stem_conv_pool_u8(img, wp, bias, strip)  # raw rows by 16-B LDS-DMA (aligned images)
-        C.stem_conv_pool_set_dbg(512 | 2048)  # ... by 4-B LDS-DMA
-        roles4 = ops.stem_conv_pool_u8(img, wp, bias, strip)
+        # dense K (5 K steps a fragment): the same products summed in another order
+        dense = ops.stem_conv_pool_u8(img, wp, bias, strip, w_dense=wd)
+        zeroed = ops.stem_conv_pool_u8(img, wp, bias, strip, w_dense=torch.zeros_like(wd))  # it reads w_dense
+        C.stem_conv_pool_set_dbg(512 | 2048)  # ... by 4-B LDS-DMA (the paired kernel: no dense form)
+        roles4 = ops.stem_conv_pool_u8(img, wp, bias, strip, w_dense=wd)
     finally:
         C.stem_conv_pool_set_dbg(0)
     torch.cuda.synchronize()
     assert torch.equal(one, two)
     assert torch.equal(roles, two)
     assert torch.equal(roles4, two)
+    # fp32 sums in a different order, then one bf16 rounding: at most one
+    # bf16 ulp apart, and only where a sum lands near a rounding boundary
+    d, t = dense.float(), two.float()
+    assert (d - t).abs().le(t.abs() * 2.0 ** -7 + 1e-6).all(), (d - t).abs().max().item()
+    assert (d != t).float().mean().item() < 0.05
+    assert torch.equal(zeroed, F.relu(bias).bfloat16().view(1, 1, 1, 64).expand_as(zeroed))
 
 
 @pytest.mark.parametrize("HW,C,B,res,relu", [(28, 128, 1, False, True), (28, 128, 3, True, True),

@@ -8,6 +8,7 @@ import pytest
 import torch
 import torch.nn.functional as F
 
+import dmlc
 from dmlc import ops
 
 
@@ -757,6 +758,100 @@ def test_stem_convert_store_layout():
                     banks.setdefault((grp[0], (addr[l] // 4) % 32), set()).add(addr[l])
             worst = max(worst, max(len(v) for v in banks.values()))
     assert worst <= 4, worst
+
+
+def _dense_stem_addr(fr, fq, j, RB=1392):
+    """stem_pool.hip dense-K operand address of lane (fr, fq), dword slot j
+    (= 4 s + i), fragment 0, with kernel row dy's slot at dy * RB (the ring
+    only moves the slot bases)."""
+    dy0, d0 = (4 * j) // 11, (4 * j) % 11
+    t = 11 - d0
+    lane_off = 12 * fr + 4 * fq
+    if t >= 4 or j == 19:
+        return lane_off + dy0 * RB + 4 * d0
+    return lane_off + (dy0 * RB + 4 * d0 if fq < t else (dy0 + 1) * RB - 4 * t)
+
+
+@pytest.mark.parametrize("S", [128, 224, 256])
+def test_stem_dense_layout(S):
+    """Dense-K stem (stem_pool.hip stem_roles_kernel V & 2): the dense row
+    holds padded pixel p (image column p - 3) channel c at element 3p + c;
+    every operand dword a lane reads is the pair of window elements its K
+    slots name (kernel row D / 11, elements 2 (D % 11), +1 of output column
+    ox's 22-element window starting at element 6 ox), zero-weight slots read
+    inside the row, and the weight order (pack_stem_dense_weight, the
+    engine's stem_dense_k_index) puts tap (dy, dx, c) at that K."""
+    NF = S // 32
+    NG = 4 * NF + 1
+    RB = NG * 48
+    Ho = S // 2
+    assert NG * 8 >= S + 6
+    g = torch.Generator().manual_seed(3)
+    w = torch.randn(64, 3, 7, 7, generator=g)
+    wd = ops.pack_stem_dense_weight(w).float()
+    wb = w.bfloat16().float()
+    C = dmlc.native()
+    seen = set()
+    for k in range(160):
+        s, fq, i, h = k // 32, (k % 32) // 8, (k % 8) // 2, k % 2
+        D = 16 * s + 4 * i + fq
+        E = 2 * D + h
+        dy, e = E // 22, E % 22
+        if D >= 77 or e == 21:
+            assert wd[:, k].abs().max() == 0
+            continue
+        dx, c = e // 3, e % 3
+        assert C.stem_dense_k_index(dy, dx, c) == k
+        assert torch.equal(wd[:, k], wb[:, c, dy, dx])
+        seen.add((dy, dx, c))
+    assert len(seen) == 147
+    for f in range(NF):
+        for fr in range(16):
+            ox = 16 * f + fr
+            for fq in range(4):
+                for j in range(20):
+                    a = _dense_stem_addr(fr, fq, j, RB) + 192 * f
+                    row, off = divmod(a, RB)
+                    D = 4 * j + fq
+                    assert 0 <= off and off + 4 <= RB and a % 4 == 0
+                    if D >= 77:
+                        assert row == 6
+                        continue
+                    assert row == D // 11 and off // 2 == 6 * ox + 2 * (D % 11)
+    assert 6 * (Ho - 1) + 21 < 3 * (S + 6) <= NG * 24
+
+
+def test_stem_dense_lds_conflicts():
+    """Dense-K stem LDS traffic: the helpers' conversion stores (lane =
+    8-pixel group g: three 16-B stores at 48 g + 16 q) and the MFMA waves'
+    operand reads (ds_read_b32, every dword slot) are bank-conflict free:
+    the 48-B lane stride puts 16 lanes on 16 distinct 4-bank groups, and the
+    operand dwords of a slot are 3 fr + fq + const (overlapping windows: equal
+    addresses broadcast) -- 1-way except the slots that straddle two kernel
+    rows, pinned at 2-way."""
+    worst = 1
+    for t0 in range(0, 8 * 29, 64):
+        for q in range(3):
+            addr = [48 * ((t0 + l) % 29) + 16 * q + 1392 * ((t0 + l) // 29) for l in range(64)]
+            worst = max(worst, _b128_ways(addr))
+            for grp in [list(range(i, i + 8)) for i in range(0, 64, 8)]:  # 8-lane write groups, 32 banks
+                banks = {}
+                for l in grp:
+                    for b in range(addr[l] // 4, addr[l] // 4 + 4):
+                        banks.setdefault(b % 32, set()).add(addr[l])
+                worst = max(worst, max(len(v) for v in banks.values()))
+    assert worst == 1
+    ways = []
+    for j in range(20):
+        banks = {}
+        for l in range(64):
+            a = _dense_stem_addr(l & 15, l >> 4, j)
+            banks.setdefault((a // 4) % 64, set()).add(a)
+        ways.append(max(len(v) for v in banks.values()))
+    straddle = [j for j in range(20) if 11 - (4 * j) % 11 < 4 and j != 19]
+    assert straddle == [2, 5, 8, 13, 16]
+    assert all(ways[j] == 1 for j in range(20) if j not in straddle), ways
+    assert max(ways) <= 2, ways
 
 
 @pytest.mark.parametrize("C,ipw", [(512, 4), (512, 16), (2048, 16), (2048, 4)])
