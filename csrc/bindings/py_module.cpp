@@ -214,19 +214,18 @@ PYBIND11_MODULE(_C, m) {
         py::arg("wfrag") = 0);
   m.def("conv3x3_block_supported", &conv3x3_block_supported);
   m.def("conv3x3_block", [](uintptr_t x, uintptr_t wf1, uintptr_t b1, uintptr_t wf2, uintptr_t b2, uintptr_t y,
-                            uintptr_t zero, int B, uintptr_t stream, int dbg) {
+                            uintptr_t zero, int B, uintptr_t stream) {
     conv3x3_block(P<void>(x), P<void>(wf1), P<float>(b1), P<void>(wf2), P<float>(b2), P<void>(y), P<void>(zero), B,
-                  S(stream), dbg);
+                  S(stream));
   }, py::arg("x"), py::arg("wf1"), py::arg("b1"), py::arg("wf2"), py::arg("b2"), py::arg("y"), py::arg("zero"),
-        py::arg("B"), py::arg("stream"), py::arg("dbg") = 0);
+        py::arg("B"), py::arg("stream"));
   m.def("bottleneck56", [](uintptr_t x, uintptr_t w1, uintptr_t a1, uintptr_t b1, uintptr_t wf2, uintptr_t b2,
                            uintptr_t wf3, uintptr_t b3, uintptr_t y, float res_scale, float out_inv_scale, int B,
-                           uintptr_t stream, int dbg) {
+                           uintptr_t stream) {
     bottleneck56(P<void>(x), P<void>(w1), P<float>(a1), P<float>(b1), P<void>(wf2), P<float>(b2), P<void>(wf3),
-                 P<float>(b3), P<void>(y), res_scale, out_inv_scale, B, S(stream), dbg);
+                 P<float>(b3), P<void>(y), res_scale, out_inv_scale, B, S(stream));
   }, py::arg("x"), py::arg("w1"), py::arg("a1"), py::arg("b1"), py::arg("wf2"), py::arg("b2"), py::arg("wf3"),
-     py::arg("b3"), py::arg("y"), py::arg("res_scale"), py::arg("out_inv_scale"), py::arg("B"), py::arg("stream") = 0,
-     py::arg("dbg") = 0);
+     py::arg("b3"), py::arg("y"), py::arg("res_scale"), py::arg("out_inv_scale"), py::arg("B"), py::arg("stream") = 0);
   m.def("conv3x3_stream8_supported", &conv3x3_stream8_supported);
   m.def("conv3x3_stream8_frag_offset", &conv3x3_stream8_frag_offset);
   m.def("conv3x3_stream8_set_variant", &conv3x3_stream8_set_variant);
@@ -246,11 +245,11 @@ PYBIND11_MODULE(_C, m) {
   }, py::arg("x"), py::arg("wf"), py::arg("bias"), py::arg("y"), py::arg("B"), py::arg("relu"),
         py::arg("out_inv_scale"), py::arg("stream"));
   m.def("conv3x3_s2rows", [](uintptr_t x, uintptr_t wf, uintptr_t bias, uintptr_t wdf, uintptr_t bd, uintptr_t y,
-                             uintptr_t yd, uintptr_t zero, int B, bool relu, uintptr_t stream, int dbg) {
+                             uintptr_t yd, uintptr_t zero, int B, bool relu, uintptr_t stream) {
     conv3x3_s2rows(P<void>(x), P<void>(wf), P<float>(bias), P<void>(wdf), P<float>(bd), P<void>(y), P<void>(yd),
-                   P<void>(zero), B, relu, S(stream), dbg);
+                   P<void>(zero), B, relu, S(stream));
   }, py::arg("x"), py::arg("wf"), py::arg("bias"), py::arg("wdf"), py::arg("bd"), py::arg("y"), py::arg("yd"),
-        py::arg("zero"), py::arg("B"), py::arg("relu"), py::arg("stream"), py::arg("dbg") = 0);
+        py::arg("zero"), py::arg("B"), py::arg("relu"), py::arg("stream"));
   m.def("conv_small_supported", &conv_small_supported);
   m.def("conv_small_pick_mf", &conv_small_pick_mf);
   m.def("conv_small_set_mf", &conv_small_set_mf);

@@ -62,8 +62,6 @@ struct BnArgs {
   uint8_t* y;          // [B, 56, 56, 256] e4m3
   float res_scale;     // s_x
   float out_inv_scale; // 1 / s_y
-  int dbg;             // experiments (tools/bottleneck_bench.py): bit 0 no y stores (kept live), bit 1 no
-                       // residual loads, bit 2 plain (not non-temporal) y stores
 };
 
 constexpr int kH = 56, kW = 56, kC = 256, kM = 64;
@@ -404,10 +402,7 @@ struct Memory {
 #pragma unroll
     for (int f = 0; f < kMF; ++f)
 #pragma unroll
-      for (int P = 0; P < 2; ++P) {
-        pin(rv[f][P]);
-        if (a.dbg & 2) rv[f][P] = u32x4{0, 0, 0, 0};
-      }
+      for (int P = 0; P < 2; ++P) pin(rv[f][P]);
 #pragma unroll
     for (int P = 0; P < 2; ++P) {
       const int c3 = 128 * cb + 64 * P + 16 * g;  // this lane's 16 channels
@@ -446,10 +441,8 @@ struct Memory {
             v[i] = __builtin_amdgcn_fmed3f(__builtin_fmaf(rf[i], rsi, acc[h][i]), 0.f, 448.f);
           q[h] = f32x4_to_fp8_sat(v);
         }
-        if (!(a.dbg & 4))  // non-temporal y stores (L2 kept for the x re-reads); dbg bit 2: plain stores
-          __builtin_nontemporal_store(u32x4{q[0], q[1], q[2], q[3]}, (u32x4*)(yim + pix(k, f) + c3));
-        else if (!(a.dbg & 1) || q[0] == 0x12345678u)
-          *(uint4*)(yim + pix(k, f) + c3) = make_uint4(q[0], q[1], q[2], q[3]);
+        // non-temporal y stores (L2 kept for the x re-reads)
+        __builtin_nontemporal_store(u32x4{q[0], q[1], q[2], q[3]}, (u32x4*)(yim + pix(k, f) + c3));
       }
     }
   }
@@ -513,8 +506,7 @@ __global__ __launch_bounds__(512, 1) void bottleneck56_kernel(BnArgs a) {
       }
       if (k < kSteps) m.load_rv(k);
       if (dma) {  // the DMA has landed (the stores and the next residual may be in flight)
-        if (a.dbg & 1) vm_wait<0>();
-        else if (k >= 1) vm_wait<kST + Memory::kRL>();
+        if (k >= 1) vm_wait<kST + Memory::kRL>();
         else vm_wait<Memory::kRL>();
       }
       lds_barrier();  // S2
@@ -630,7 +622,7 @@ bool bottleneck56_supported(int H, int W, int C, int Cm) { return H == kH && W =
 
 void bottleneck56(const void* x, const void* w1, const float* a1, const float* b1, const void* wf2, const float* b2,
                   const void* wf3, const float* b3, void* y, float res_scale, float out_inv_scale, int B,
-                  hipStream_t s, int dbg) {
+                  hipStream_t s) {
   if (B <= 0) return;
   if (!x || !w1 || !a1 || !b1 || !wf2 || !b2 || !wf3 || !b3 || !y ||
       (((uintptr_t)x | (uintptr_t)w1 | (uintptr_t)wf2 | (uintptr_t)wf3 | (uintptr_t)y) & 15))
@@ -648,7 +640,6 @@ void bottleneck56(const void* x, const void* w1, const float* a1, const float* b
   a.y = (uint8_t*)y;
   a.res_scale = res_scale;
   a.out_inv_scale = out_inv_scale;
-  a.dbg = dbg;
   hipLaunchKernelGGL(bottleneck56_kernel, dim3(B), dim3(512), kLds, s, a);
   DMLC_HIP_CHECK(hipGetLastError());
 }

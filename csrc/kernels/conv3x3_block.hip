@@ -69,9 +69,7 @@ constexpr int kSteps = kH / kR + 2;    // 16
 // DMA_KS: K step at which producers issue the next step's x-row DMA (vmcnt
 // retires in order: a weight load issued after the DMA cannot be waited on
 // without waiting for the DMA too).
-// DBG (tools/block_bench.py knock-outs): bit 0 no x-row DMA in the loop, bit 1
-// no residual loads, bit 2 no y stores (results wrong, timing only)
-template <bool PROD, int PD, int DMA_KS, int DBG = 0, bool EP = false>
+template <bool PROD, int PD, int DMA_KS>
 __device__ __forceinline__ void block_role(const BlockArgs& a, char* xring, char* tring, int rw, int lane) {
   const int wm = rw & 1, wn = rw >> 1;
   const int fr = lane & 15, g = lane >> 4;
@@ -158,7 +156,7 @@ __device__ __forceinline__ void block_role(const BlockArgs& a, char* xring, char
     // producers: DMA the new x rows of the next producer step (its t rows
     // nb..nb+3 need x rows nb-1..nb+4; up to nb are here already)
     auto issue_dma = [&]() __attribute__((always_inline)) {
-      if (PROD && !(DBG & 1) && step + 1 <= kH / kR) {
+      if (PROD && step + 1 <= kH / kR) {
         const int nb = step == 0 ? 1 : base + 4;
         for (int r = nb + 1; r <= nb + 4; ++r)
           if (r >= 6) load_row(r);
@@ -180,20 +178,14 @@ __device__ __forceinline__ void block_role(const BlockArgs& a, char* xring, char
 #pragma unroll
         for (int f = 0; f < kMF; ++f) {
           const int p = wm * (kR * kW / 2) + 16 * f + fr;
-          rres[f] = (DBG & 2) ? make_uint4(0, 0, 0, 0) : *(const uint4*)(a.x + obase + (long)p * kC + wn * 32 + 8 * g);
+          rres[f] = *(const uint4*)(a.x + obase + (long)p * kC + wn * 32 + 8 * g);
         }
       }
       floatx4 acc[kMF][2];
-      // EP: the bias is the first MFMA's accumulator input (no zeroing, no
-      // bias adds in the epilogue)
+      // the bias is the first MFMA's accumulator input (no zeroing, no bias
+      // adds in the epilogue)
       const floatx4 bv[2] = {floatx4{bs[0][0], bs[0][1], bs[0][2], bs[0][3]},
                              floatx4{bs[1][0], bs[1][1], bs[1][2], bs[1][3]}};
-      if constexpr (!EP) {
-#pragma unroll
-        for (int f = 0; f < kMF; ++f)
-#pragma unroll
-          for (int nf = 0; nf < 2; ++nf) acc[f][nf] = floatx4{0.f, 0.f, 0.f, 0.f};
-      }
       bf16x8 xc[kMF], xn[kMF];
       auto load_k = [&](int ks, bf16x8* xd) __attribute__((always_inline)) {
         const int tap = ks >> 1, h = ks & 1;
@@ -218,7 +210,7 @@ __device__ __forceinline__ void block_role(const BlockArgs& a, char* xring, char
 #pragma unroll
           for (int nf = 0; nf < 2; ++nf)
             acc[f][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wq[ks % PD][nf], xc[f],
-                                                                 (EP && ks == 0) ? bv[nf] : acc[f][nf], 0, 0, 0);
+                                                                 ks == 0 ? bv[nf] : acc[f][nf], 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
         if (ks + 1 < kKS) {
 #pragma unroll
@@ -226,13 +218,13 @@ __device__ __forceinline__ void block_role(const BlockArgs& a, char* xring, char
         }
       }
       // ---- epilogue: lane holds channels wn*32 + 8g .. +7 of pixel (row, col)
-      // EP: ~17 VALU per fragment instead of ~41 (the epilogues of both roles
+      // ~17 VALU per fragment instead of ~41 (the epilogues of both roles
       // meet at the step barrier with the matrix cores idle, and an MFMA
       // leaves its SIMD 8 of its 16 cycles for other vector instructions):
       // bias already in the accumulators, the residual added from its bf16
       // pairs by v_dot2c_f32_bf16 (x.lo * 1 + x.hi * 0: exact), ReLU and the
       // padding rows' zeros on the packed bf16 words
-      if constexpr (EP) {
+      {
         typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
         // (bf16 1.0 = 0x3f80 in the low / high half, kept in registers: the
         // compiler turned the constant pair into the inline constant 1.0,
@@ -264,34 +256,8 @@ __device__ __forceinline__ void block_role(const BlockArgs& a, char* xring, char
               v[2 * i + 1] = __builtin_amdgcn_fdot2_f32_bf16(rp, sel_hi, v[2 * i + 1], false);
             }
             const uint4 pk = relu_bf16x8(pack8(v));
-            if (!(DBG & 4) || pk.x == 0x12345678u) *(uint4*)(a.y + obase + (long)p * kC + wn * 32 + 8 * g) = pk;
+            *(uint4*)(a.y + obase + (long)p * kC + wn * 32 + 8 * g) = pk;
           }
-        }
-      } else
-#pragma unroll
-      for (int f = 0; f < kMF; ++f) {
-        const int p = wm * (kR * kW / 2) + 16 * f + fr;
-        float v[8];
-#pragma unroll
-        for (int nf = 0; nf < 2; ++nf)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) v[4 * nf + i] = acc[f][nf][i] + bs[nf][i];
-        if constexpr (PROD) {
-          const int row = base + p / kW, col = p % kW;
-          // t row -1 / 56 is conv2's zero padding
-          const bool outside = (unsigned)row >= (unsigned)kH;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = outside ? 0.f : fmaxf(v[e], 0.f);
-          const int q = col + 1;  // staged column; channels wn*32 + 8g: K half wn, chunk g
-          *(uint4*)(tring + ((row + kRing) % kRing) * kSlot + wn * kHalf + q * 64 + ((g ^ ((q >> 1) & 3)) << 4)) =
-              pack8(v);
-        } else {
-          float r[8];
-          unpack8(rres[f], r);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e] + r[e], 0.f);
-          const uint4 pk = pack8(v);
-          if (!(DBG & 4) || pk.x == 0x12345678u) *(uint4*)(a.y + obase + (long)p * kC + wn * 32 + 8 * g) = pk;
         }
       }
     }
@@ -303,191 +269,7 @@ __device__ __forceinline__ void block_role(const BlockArgs& a, char* xring, char
   }
 }
 
-// ---- Weight-stationary roles (WS): each wave holds its 32 output channels'
-// weights for the whole K (18 K steps x 2 N fragments = 144 VGPRs, loaded
-// once per workgroup) instead of streaming them from L2 every step. The loop
-// then has no weight loads at all, so nothing queues behind the x-row DMA,
-// the residual loads or the y stores in the in-order vmcnt (the cause of the
-// 25-28 us of non-overlapped memory time per block in the streamed-weight
-// version, profiles/r3_block_knockouts.txt), and the L2 serves ~147 KB per
-// workgroup instead of ~4.4 MB. To fit beside the weights, a step's 7 pixel
-// fragments run as two passes (4 + 3 fragments: half the accumulator and X
-// registers), X fragments single-buffered (each re-read right after its
-// MFMAs); the consumer's residual for a pass is loaded at the pass's start
-// and lands during its K loop.
-template <bool PROD>
-__device__ __forceinline__ void block_role_ws(const BlockArgs& a, char* xring, char* tring, int rw, int lane) {
-  const int wm = rw & 1, wn = rw >> 1;
-  const int fr = lane & 15, g = lane >> 4;
-  const int b = blockIdx.x;
-  const bf16* img = a.x + (long)b * kH * kW * kC;
-
-  auto load_row = [&](int r) __attribute__((always_inline)) {
-    char* dst = xring + ((r + kRing) % kRing) * kSlot + 64 + rw * 1024;
-    const int k = rw * 64 + lane;
-    const int q = 1 + (k >> 2), c = k & 3;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      if (k < kRun) {
-        if (r < kH)
-          dma16(img + ((long)r * kW + (q - 1)) * kC + 8 * (4 * h + (c ^ ((q >> 1) & 3))), dst + h * kHalf);
-        else
-          *(uint4*)(dst + h * kHalf + lane * 16) = make_uint4(0, 0, 0, 0);
-      }
-    }
-  };
-  if constexpr (PROD)
-    for (int r = 0; r <= 5; ++r) load_row(r);
-
-  // all 18 K steps x 2 N fragments of this wave's weights (after the row
-  // DMAs: the compiler's waits on them cover the older DMAs too)
-  const __amdgpu_buffer_rsrc_t wrs =
-      wave_rsrc((PROD ? a.wf1 : a.wf2) + (long)wn * kKS * 2 * 64 * 8, kKS * 2 * 1024);
-  bf16x8 wreg[kKS][2];
-#pragma unroll
-  for (int ks = 0; ks < kKS; ++ks)
-#pragma unroll
-    for (int nf = 0; nf < 2; ++nf)
-      wreg[ks][nf] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, lane * 16, (ks * 2 + nf) * 1024, 0));
-  const float* bias = PROD ? a.bias1 : a.bias2;
-
-  vm_wait<0>();
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-
-  const char* src_ring = PROD ? xring : tring;
-  for (int step = 0; step < kSteps; ++step) {
-    const bool work = PROD ? (step <= kH / kR && (step > 0 || wm == 1)) : step >= 2;
-    const int base = PROD ? (step == 0 ? -3 : 4 * (step - 1) + 1) : 4 * (step - 2);
-    if (PROD && step + 1 <= kH / kR) {  // the next producer step's new x rows
-      const int nb = step == 0 ? 1 : base + 4;
-      for (int r = nb + 1; r <= nb + 4; ++r)
-        if (r >= 6) load_row(r);
-    }
-    if (work) {
-      const int rb = base + 2 * wm - 1 + 2 * kRing;
-      const int rs0 = (rb % kRing) * kSlot, rs1 = ((rb + 1) % kRing) * kSlot;
-      const int rs2 = ((rb + 2) % kRing) * kSlot, rs3 = ((rb + 3) % kRing) * kSlot;
-      // by value: a select between by-reference captures became a select of
-      // their stack addresses and a load through it (scratch)
-      auto rsl = [=](int j) __attribute__((always_inline)) { return j == 0 ? rs0 : j == 1 ? rs1 : j == 2 ? rs2 : rs3; };
-      const long obase = ((long)b * kH + base) * kW * kC;
-      // fragments [FB, FE) of the step: K loop, then their epilogue
-      auto pass = [&](auto fb_, auto fe_) __attribute__((always_inline)) {
-        constexpr int FB = decltype(fb_)::value, FE = decltype(fe_)::value, PF = FE - FB;
-        // per-lane geometry recomputed every pass from an opaque copy of the
-        // lane id: hoisted out of the step loop it stayed live (with 64-bit
-        // output addresses) across both passes and spilled
-        int lo = lane;
-        asm volatile("" : "+v"(lo));
-        const int fr = lo & 15, g = lo >> 4;
-        int hi1 = 0, colf[PF];
-#pragma unroll
-        for (int f = 0; f < PF; ++f) {
-          const int p = wm * (kR * kW / 2) + 16 * (FB + f) + fr;
-          hi1 |= (p / kW - 2 * wm) << f;
-          colf[f] = p % kW;
-        }
-        uint4 rres[PROD ? 1 : PF];
-        if constexpr (!PROD) {
-#pragma unroll
-          for (int f = 0; f < PF; ++f) {
-            const int p = wm * (kR * kW / 2) + 16 * (FB + f) + fr;
-            rres[f] = *(const uint4*)(a.x + obase + (long)p * kC + wn * 32 + 8 * g);
-          }
-        }
-        // ta[f]: fragment f's ring offset for the current tap (K half 0; half
-        // 1 is +kHalf, an immediate), recomputed by volatile asm where a new
-        // tap starts so the compiler neither hoists nor keeps all 9 taps'
-        // addresses live (the weights hold 144 registers)
-        int ta[PF];
-        auto set_tap = [&](int tap, int f) __attribute__((always_inline)) {
-          const int kh = tap / 3, kw = tap % 3;
-          const int r_lo = rsl(kh), r_hi = rsl(kh + 1);
-          const int ro = ((hi1 >> f) & 1) ? r_hi : r_lo;
-          int q = colf[f] + kw;
-          asm volatile("" : "+v"(q));  // column -> chunk offset computed here, not kept per tap
-          const int cq = q * 64 + ((g ^ ((q >> 1) & 3)) << 4);
-          asm volatile("v_add_u32 %0, %1, %2" : "=v"(ta[f]) : "v"(ro), "v"(cq));
-        };
-        auto xread = [&](int ks, int f) __attribute__((always_inline)) {
-          if ((ks & 1) == 0) set_tap(ks >> 1, f);
-          return *(const bf16x8*)(src_ring + ta[f] + (ks & 1) * kHalf);
-        };
-        floatx4 acc[PF][2];
-#pragma unroll
-        for (int f = 0; f < PF; ++f)
-#pragma unroll
-          for (int nf = 0; nf < 2; ++nf) acc[f][nf] = floatx4{0.f, 0.f, 0.f, 0.f};
-        bf16x8 xc[PF];
-#pragma unroll
-        for (int f = 0; f < PF; ++f) xc[f] = xread(0, f);
-#pragma unroll
-        for (int ks = 0; ks < kKS; ++ks) {
-#pragma unroll
-          for (int f = 0; f < PF; ++f) {
-            __builtin_amdgcn_sched_barrier(0);  // keep the issue order: no early reads piling up registers
-#pragma unroll
-            for (int nf = 0; nf < 2; ++nf)
-              acc[f][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wreg[ks][nf], xc[f], acc[f][nf], 0, 0, 0);
-            if (ks + 1 < kKS) xc[f] = xread(ks + 1, f);
-          }
-        }
-        float bs[8];
-#pragma unroll
-        for (int nf = 0; nf < 2; ++nf)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) bs[4 * nf + i] = bias[wn * 32 + 8 * g + 4 * nf + i];
-#pragma unroll
-        for (int f = 0; f < PF; ++f) {
-          const int p = wm * (kR * kW / 2) + 16 * (FB + f) + fr;
-          float v[8];
-#pragma unroll
-          for (int nf = 0; nf < 2; ++nf)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) v[4 * nf + i] = acc[f][nf][i] + bs[4 * nf + i];
-          if constexpr (PROD) {
-            const int row = base + p / kW, col = p % kW;
-            const bool outside = (unsigned)row >= (unsigned)kH;
-            const int q = col + 1;
-            *(uint4*)(tring + ((row + kRing) % kRing) * kSlot + wn * kHalf + q * 64 + ((g ^ ((q >> 1) & 3)) << 4)) =
-                outside ? make_uint4(0, 0, 0, 0) : relu_bf16x8(pack8(v));
-          } else {
-            float r[8];
-            // unpacked only here (hoisted, the 8 floats per fragment stayed live through the K loop)
-            asm volatile("" : "+v"(rres[f].x), "+v"(rres[f].y), "+v"(rres[f].z), "+v"(rres[f].w));
-            unpack8(rres[f], r);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] += r[e];
-            *(uint4*)(a.y + obase + (long)p * kC + wn * 32 + 8 * g) = relu_bf16x8(pack8(v));
-          }
-        }
-      };
-      pass(std::integral_constant<int, 0>{}, std::integral_constant<int, 4>{});
-      pass(std::integral_constant<int, 4>{}, std::integral_constant<int, kMF>{});
-    }
-    if constexpr (PROD) vm_wait<0>();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-  }
-}
-
-__global__ __launch_bounds__(512, 1) void conv3x3_block_ws_kernel(BlockArgs a) {
-  extern __shared__ __attribute__((aligned(16))) uint4 smem[];
-  char* xring = (char*)smem;
-  char* tring = xring + kRing * kSlot;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  for (int i = tid; i < 2 * kRing * kSlot / 16; i += 512) ((uint4*)xring)[i] = make_uint4(0, 0, 0, 0);
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  if (wave < 4)
-    block_role_ws<true>(a, xring, tring, wave & 3, lane);
-  else
-    block_role_ws<false>(a, xring, tring, wave & 3, lane);
-}
-
-template <int PD, int DMA_KS, int DBG = 0, bool EP = true>
+template <int PD, int DMA_KS>
 __global__ __launch_bounds__(512, 1) void conv3x3_block_kernel(BlockArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint4 smem[];
   char* xring = (char*)smem;
@@ -500,9 +282,9 @@ __global__ __launch_bounds__(512, 1) void conv3x3_block_kernel(BlockArgs a) {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   if (wave < 4)
-    block_role<true, PD, DMA_KS, DBG, EP>(a, xring, tring, wave & 3, lane);
+    block_role<true, PD, DMA_KS>(a, xring, tring, wave & 3, lane);
   else
-    block_role<false, PD, DMA_KS, DBG, EP>(a, xring, tring, wave & 3, lane);
+    block_role<false, PD, DMA_KS>(a, xring, tring, wave & 3, lane);
 }
 
 }  // namespace
@@ -510,7 +292,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_block_kernel(BlockArgs a) {
 bool conv3x3_block_supported(int H, int W, int C) { return H == kH && W == kW && C == kC; }
 
 void conv3x3_block(const void* x, const void* wf1, const float* bias1, const void* wf2, const float* bias2, void* y,
-                   const void* zero, int B, hipStream_t s, int dbg) {
+                   const void* zero, int B, hipStream_t s) {
   if (B <= 0) return;
   if (!x || !wf1 || !wf2 || !bias1 || !bias2 || !y || !zero ||
       (((uintptr_t)x | (uintptr_t)wf1 | (uintptr_t)wf2 | (uintptr_t)y | (uintptr_t)zero) & 15))
@@ -527,15 +309,7 @@ void conv3x3_block(const void* x, const void* wf1, const float* bias1, const voi
   const size_t lds = (size_t)2 * kRing * kSlot;  // 148.5 KB
   // PD 6: 5 K steps of weight lookahead (PD 3 and a mid-step DMA measured
   // the same, 116-120 us at B=256); tools/block_bench.py
-  switch (dbg) {  // knock-outs / variants for tools/block_bench.py (32: the round-4 epilogue, bias adds + unpacked residual)
-    case 1: hipLaunchKernelGGL((conv3x3_block_kernel<6, 0, 1>), dim3(B), dim3(512), lds, s, a); break;
-    case 2: hipLaunchKernelGGL((conv3x3_block_kernel<6, 0, 2>), dim3(B), dim3(512), lds, s, a); break;
-    case 4: hipLaunchKernelGGL((conv3x3_block_kernel<6, 0, 4>), dim3(B), dim3(512), lds, s, a); break;
-    case 7: hipLaunchKernelGGL((conv3x3_block_kernel<6, 0, 7>), dim3(B), dim3(512), lds, s, a); break;
-    case 16: hipLaunchKernelGGL(conv3x3_block_ws_kernel, dim3(B), dim3(512), lds, s, a); break;
-    case 32: hipLaunchKernelGGL((conv3x3_block_kernel<6, 0, 0, false>), dim3(B), dim3(512), lds, s, a); break;
-    default: hipLaunchKernelGGL((conv3x3_block_kernel<6, 0>), dim3(B), dim3(512), lds, s, a);
-  }
+  hipLaunchKernelGGL((conv3x3_block_kernel<6, 0>), dim3(B), dim3(512), lds, s, a);
   DMLC_HIP_CHECK(hipGetLastError());
 }
 

@@ -74,15 +74,11 @@ constexpr int kR = 4;                 // output rows per step
 constexpr int kSteps = kH / kR;       // 7
 constexpr int kPlane = 30 * 64;       // one channel quarter of a staged row: 1920 B
 constexpr int kRB = 4 * kPlane;       // 7680 B per staged row
-// Input rows are DMA'd AH steps ahead: rows r0 - 1 .. r0 + 4 in use + 4 AH
-// in flight. One step ahead (the default, 10-row ring) measured faster than
-// two (14-row ring): 48.2-48.9 vs 51.5-52.0 us at B = 256 with warm clocks
-// (profiles/r3_rows28_ahead.txt).
-template <int AH>
-struct R28Ring {
-  static constexpr int kRing = 6 + 4 * AH;
-  static constexpr int kSlotsAlloc = kRing + 2;  // + guard copies of slots 0, 1
-};
+// Input rows are DMA'd one step ahead: rows r0 - 1 .. r0 + 4 in use + 4 in
+// flight (10-row ring; two steps ahead, a 14-row ring, measured slower: 48.2-48.9
+// vs 51.5-52.0 us at B = 256 with warm clocks, profiles/r3_rows28_ahead.txt).
+constexpr int kRing = 10;
+constexpr int kSlotsAlloc = kRing + 2;  // + guard copies of slots 0, 1
 constexpr int kRun = 4 * kW;          // 112 DMA chunks per quarter plane (slots 1..28)
 constexpr int kMF = kR * kW / 16;     // 7 pixel fragments per step
 constexpr int kKS = 9 * kC / 32;      // 36 K steps
@@ -90,43 +86,22 @@ constexpr int kResCh = kMF * 16 * 16;  // residual chunks per step (112 pixels x
 
 __device__ __forceinline__ int swz_of(int y, int x) { return ((kW * y + x) >> 1) & 3; }
 
-// s_waitcnt vmcnt(base + n) for a wave-uniform runtime n in [0, 24]
-template <int BASE>
-__device__ __forceinline__ void vm_wait_plus(int n) {
-  switch (n) {
-#define DMLC_VMW(N) \
-  case N: vm_wait<BASE + N>(); break;
-    DMLC_VMW(0) DMLC_VMW(1) DMLC_VMW(2) DMLC_VMW(3) DMLC_VMW(4) DMLC_VMW(5) DMLC_VMW(6) DMLC_VMW(7) DMLC_VMW(8)
-    DMLC_VMW(9) DMLC_VMW(10) DMLC_VMW(11) DMLC_VMW(12) DMLC_VMW(13) DMLC_VMW(14) DMLC_VMW(15) DMLC_VMW(16)
-    DMLC_VMW(17) DMLC_VMW(18) DMLC_VMW(19) DMLC_VMW(20) DMLC_VMW(21) DMLC_VMW(22) DMLC_VMW(23) DMLC_VMW(24)
-#undef DMLC_VMW
-    default: vm_wait<BASE>(); break;  // never: counts above 24 do not occur (wait longer)
-  }
-}
-
-// DBG (experiments): bit 0 no row DMA in the loop, bit 1 no LDS reads in the
-// K loop, bit 2 no epilogue, bit 3 prologue only
-// NW: 4 waves (one per SIMD) x 32 output channels, 288 weight registers per
-// wave (their AGPR / VGPR split costs ~0.6 register moves per MFMA), or 8
-// waves (two per SIMD) x 16 channels, 144 weight registers, every X fragment
-// read feeding one MFMA instead of two.
-// OUT8: e4m3 output (ResNet50's layer2 3x3 -> its e4m3 expand conv; NW = 4, no residual)
-// DSX: see R28Args::xds (4 waves, no residual operand: the downsample is the residual)
-template <bool RES, int DBG = 0, int AH = 1, int NW = 4, bool OUT8 = false, bool DSX = false, bool R2 = true>
-__global__ __launch_bounds__(64 * NW, 1) void conv3x3_rows28_kernel(R28Args a) {
-  static_assert(!OUT8 || (NW == 4 && !RES), "e4m3 output: the 4-wave form without residual");
-  static_assert(!DSX || (NW == 4 && !RES && !OUT8 && AH == 1), "downsample K steps: the 4-wave bf16 form");
+// 4 waves (one per SIMD) x 32 output channels, 288 weight registers per wave
+// (their AGPR / VGPR split costs ~0.6 register moves per MFMA; 8 waves x 16
+// channels measured slower, profiles/r3_rows28_ahead.txt).
+// OUT8: e4m3 output (ResNet50's layer2 3x3 -> its e4m3 expand conv; no residual)
+// DSX: see R28Args::xds (no residual operand: the downsample is the residual)
+// RES: the residual is DMA'd one step ahead into two LDS buffers, so the
+// epilogue reads it with no wait and no workgroup barrier of its own (the
+// previous step's end-of-step wait covered it)
+template <bool RES, bool OUT8 = false, bool DSX = false>
+__global__ __launch_bounds__(256, 1) void conv3x3_rows28_kernel(R28Args a) {
+  static_assert(!OUT8 || !RES, "e4m3 output: no residual");
+  static_assert(!DSX || (!RES && !OUT8), "downsample K steps: the bf16 form");
   constexpr int kDS = DSX ? 2 : 0;  // downsample K steps (64 input channels)
-  // RES2: the residual is DMA'd one step ahead into two LDS buffers, so the
-  // epilogue reads it with no wait and no workgroup barrier of its own (the
-  // previous step's end-of-step wait covered it)
-  constexpr bool RES2 = RES && AH == 1 && NW == 4 && R2;
   constexpr int kRB2 = kResCh * 16;  // 28672 B per residual buffer
-  static_assert(NW == 4 || NW == 8, "4 or 8 waves");
-  constexpr int NF = NW == 4 ? 2 : 1;  // N fragments (16 channels) per wave
-  constexpr int NT = 64 * NW;
-  constexpr int kRing = R28Ring<AH>::kRing, kSlotsAlloc = R28Ring<AH>::kSlotsAlloc;
-  static_assert(AH == 1 || AH == 2, "rows DMA'd one or two steps ahead");
+  constexpr int NF = 2;  // N fragments (16 channels) per wave
+  constexpr int NT = 256;
   extern __shared__ __attribute__((aligned(16))) uint4 smem[];
   char* ring = (char*)smem;
   char* resbuf = ring + kSlotsAlloc * kRB;  // RES: [112 pixels][16 chunks]
@@ -141,20 +116,19 @@ __global__ __launch_bounds__(64 * NW, 1) void conv3x3_rows28_kernel(R28Args a) {
   __builtin_amdgcn_s_barrier();
   // input row yy -> ring slot (yy + 1) % kRing (+ guard slot kRing / kRing+1
   // for slots 0 / 1); wave w stages quarter plane w & 3: chunks 0..63 and
-  // 64..111 of its run (NW = 8: wave w the half w >> 2). Row 28 (below the image) reuses a slot: its run is
-  // written as zeros. row_dmas(yy) = the DMA instructions load_row(yy) issues
-  // (wave-uniform; the vmcnt waits below count them).
+  // 64..111 of its run. Row 28 (below the image) reuses a slot: its run is
+  // written as zeros.
   const int qp = wave & 3;  // the quarter plane this wave stages
   auto load_row = [&](int yy) __attribute__((always_inline)) {
     const int slot = (yy + 1) % kRing;
     char* dst = ring + qp * kPlane + 64;
 #pragma unroll
-    for (int i0 = NW == 8 ? 64 * (wave >> 2) : 0; i0 < kRun; i0 += 64 * (NW / 4)) {
+    for (int i0 = 0; i0 < kRun; i0 += 64) {
       const int k = i0 + lane;
       const int x = k >> 2, c = k & 3;
       if (k < kRun) {
         if (yy < kH) {
-          const bf16* src = img + ((long)((DBG & 32) ? 0 : yy) * kW + x) * kC + 32 * qp + 8 * (c ^ swz_of(yy, x));
+          const bf16* src = img + ((long)yy * kW + x) * kC + 32 * qp + 8 * (c ^ swz_of(yy, x));
           dma16(src, dst + slot * kRB + i0 * 16);
           if (slot < 2) dma16(src, dst + (slot + kRing) * kRB + i0 * 16);
         } else {
@@ -164,19 +138,15 @@ __global__ __launch_bounds__(64 * NW, 1) void conv3x3_rows28_kernel(R28Args a) {
       }
     }
   };
-  auto row_dmas = [&](int yy) __attribute__((always_inline)) {
-    return yy < kH ? ((yy + 1) % kRing < 2 ? 2 : 1) * (NW == 4 ? 2 : 1) : 0;
-  };
   // this lane's 8 output channels ch0 + 8g .. +7 (weight rows permuted,
-  // perm32; NW = 8: the 4 channels ch0 + 8g + 4 nf0 .. +3 of fragment nf0 of
-  // 32-channel group wave / 2); loaded before the row DMAs so the prologue
-  // wait below can leave exactly the weight loads in flight
-  const int cg = NW == 4 ? wave : wave >> 1, nf0 = NW == 4 ? 0 : wave & 1;
+  // perm32); loaded before the row DMAs so the prologue wait below can leave
+  // exactly the weight loads in flight
+  const int cg = wave;
   const int ch0 = cg * 32;
   constexpr int CPL = 4 * NF;  // output channels per lane
   float bs[CPL];
 #pragma unroll
-  for (int e = 0; e < CPL; ++e) bs[e] = a.bias[ch0 + 8 * g + 4 * nf0 + e];
+  for (int e = 0; e < CPL; ++e) bs[e] = a.bias[ch0 + 8 * g + e];
   if constexpr (DSX)
 #pragma unroll
     for (int e = 0; e < CPL; ++e) bs[e] += a.bds[ch0 + 8 * g + e];
@@ -220,7 +190,7 @@ __global__ __launch_bounds__(64 * NW, 1) void conv3x3_rows28_kernel(R28Args a) {
     }
   };
   if constexpr (DSX) ds_dma(0);  // (older than the rows: the prologue's wait covers it)
-  if constexpr (RES2) res_dma(0, resbuf);
+  if constexpr (RES) res_dma(0, resbuf);
   for (int yy = 0; yy <= 4; ++yy) load_row(yy);
   __builtin_amdgcn_sched_barrier(0);  // (the staging arithmetic is dead before the 304 weight registers load)
 
@@ -244,7 +214,7 @@ __global__ __launch_bounds__(64 * NW, 1) void conv3x3_rows28_kernel(R28Args a) {
   for (int t = 0; t < kKS; ++t)
 #pragma unroll
     for (int nf = 0; nf < NF; ++nf)
-      w[t][nf] = *(const bf16x8*)(a.wf + ((((long)cg * kKS + t) * 2 + nf + nf0) * 64 + lane) * 8);
+      w[t][nf] = *(const bf16x8*)(a.wf + ((((long)cg * kKS + t) * 2 + nf) * 64 + lane) * 8);
 #pragma unroll
   for (int t = 0; t < kDS; ++t)
 #pragma unroll
@@ -267,24 +237,14 @@ __global__ __launch_bounds__(64 * NW, 1) void conv3x3_rows28_kernel(R28Args a) {
     // loop; registers are full of weights): 16-B chunk c of pixel p at
     // physical chunk c ^ (p & 15), so the epilogue's reads are conflict free.
     // Issued before this step's row DMAs: its wait leaves those in flight.
-    const long obase = ((long)b * kH + r0) * kW * kC + ch0 + 8 * g + 4 * nf0;
+    const long obase = ((long)b * kH + r0) * kW * kC + ch0 + 8 * g;
     if constexpr (DSX)  // the next step's downsample input (this step's landed during the last one)
       if (step + 1 < kSteps) ds_dma(step + 1);
-    if constexpr (RES2) {  // the next step's residual
+    if constexpr (RES)  // the next step's residual
       if (step + 1 < kSteps) res_dma(step + 1, resbuf + ((step + 1) & 1) * kRB2);
-    } else if constexpr (RES) {
-      res_dma(step, resbuf);
-    }
-    // rows of step + AH (step 0 also issues those of steps 1 .. AH - 1)
-    int ndma = 0;
-    if (!(DBG & 1)) {
-      const int s_lo = step == 0 ? 1 : step + AH, s_hi = step + AH;
-      for (int s2 = s_lo; s2 <= s_hi && s2 < kSteps; ++s2)
-        for (int yy = 4 * s2 + 1; yy <= 4 * s2 + 4; ++yy) {
-          load_row(yy);
-          ndma += row_dmas(yy);
-        }
-    }
+    // the rows of the next step
+    if (step + 1 < kSteps)
+      for (int yy = 4 * step + 5; yy <= 4 * step + 8; ++yy) load_row(yy);
     // ring slot of kernel row 0 of each fragment (+ kh rows: immediate, guard slots)
     int rowoff[kMF];
 #pragma unroll
@@ -311,11 +271,9 @@ __global__ __launch_bounds__(64 * NW, 1) void conv3x3_rows28_kernel(R28Args a) {
       if (q == 0) tap_addr(tap, f);
       return *(const bf16x8*)(ring + tb[f] + (tap / 3) * kRB + q * kPlane);
     };
-    // fragments [FB, FE) of the step: the K loop, then their epilogue (NW = 8
-    // runs the step as two such passes: half the accumulator and operand
-    // registers, the weights reused)
-    auto pass = [&](auto fb_, auto fe_) __attribute__((always_inline)) {
-      constexpr int FB = decltype(fb_)::value, FE = decltype(fe_)::value, PF = FE - FB;
+    // the step's fragments: the K loop, then their epilogue
+    {
+      constexpr int FB = 0, PF = kMF;
       // the bias is the first MFMA's accumulator input (no zeroing, no bias
       // adds in the epilogue, which with one wave per SIMD runs with the
       // matrix core idle)
@@ -333,7 +291,7 @@ __global__ __launch_bounds__(64 * NW, 1) void conv3x3_rows28_kernel(R28Args a) {
 #pragma unroll
           for (int nf = 0; nf < NF; ++nf)
             acc[f][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[t][nf], xc[f], t == 0 ? bv[nf] : acc[f][nf], 0, 0, 0);
-          if (t + 1 < kKS && !(DBG & 2)) xc[f] = xread(t + 1, FB + f);
+          if (t + 1 < kKS) xc[f] = xread(t + 1, FB + f);
         }
       }
       __builtin_amdgcn_sched_barrier(0);
@@ -357,24 +315,17 @@ __global__ __launch_bounds__(64 * NW, 1) void conv3x3_rows28_kernel(R28Args a) {
         }
         __builtin_amdgcn_sched_barrier(0);
       }
-      if constexpr (RES && !RES2 && FB == 0) {  // this wave's residual DMAs (older than this step's row DMAs) have landed; and everyone's
-        if (AH == 1 || step == 0)
-          vm_wait<0>();
-        else
-          vm_wait_plus<0>(ndma);
-        __builtin_amdgcn_s_barrier();
-      }
       // ---- epilogue: lane holds channels ch0 + 8g .. +7 of tile pixel 16 f + fr
 #pragma unroll
-      for (int f = 0; f < ((DBG & 4) ? 0 : PF); ++f) {
+      for (int f = 0; f < PF; ++f) {
         const int ff = FB + f;
         float v[8];
 #pragma unroll
         for (int nf = 0; nf < NF; ++nf)
 #pragma unroll
           for (int i = 0; i < 4; ++i) v[4 * nf + i] = acc[f][nf][i];
-        const char* rp = resbuf + (RES2 ? (step & 1) * kRB2 : 0) + (16 * ff + fr) * 256 + (((4 * cg + g) ^ fr) << 4);
-        if constexpr (NW == 4) {
+        const char* rp = resbuf + (RES ? (step & 1) * kRB2 : 0) + (16 * ff + fr) * 256 + (((4 * cg + g) ^ fr) << 4);
+        {
           if constexpr (RES) {
             // residual bf16 pairs added by v_dot2c_f32_bf16 (pair . (1, 0) /
             // (0, 1): exact), one VALU per channel instead of an unpack and
@@ -402,45 +353,19 @@ __global__ __launch_bounds__(64 * NW, 1) void conv3x3_rows28_kernel(R28Args a) {
           } else {
             *(uint4*)(a.y + obase + (long)(16 * ff + fr) * kC) = pack8_relu(v, a.relu);
           }
-        } else {
-          if constexpr (RES) {
-            const uint2 rr = *(const uint2*)(rp + 8 * nf0);
-            float r[8];
-            unpack8(make_uint4(rr.x, rr.y, 0u, 0u), r);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] += r[e];
-          }
-          v[4] = v[5] = v[6] = v[7] = 0.f;
-          const uint4 pk = pack8_relu(v, a.relu);
-          *(uint2*)(a.y + obase + (long)(16 * ff + fr) * kC) = make_uint2(pk.x, pk.y);
         }
       }
-    };
-    if constexpr (NW == 4) {
-      pass(std::integral_constant<int, 0>{}, std::integral_constant<int, kMF>{});
-    } else {
-      pass(std::integral_constant<int, 0>{}, std::integral_constant<int, 4>{});
-      pass(std::integral_constant<int, 4>{}, std::integral_constant<int, kMF>{});
     }
     // the next step's rows have landed and every wave is done with the rows
-    // they replace. vmcnt retires in order; younger than those rows: AH = 1
-    // this step's kMF stores; AH = 2 the previous step's stores, this step's
-    // row DMAs and stores (step 0: its K loop already drained every load,
-    // the compiler's waits on the weights; RES: the residual wait before the
-    // epilogue covered them, and this step's row DMAs stay in flight)
-    if constexpr (!(DBG & 16)) {
-      if (AH == 1 || step == 0)
-        vm_wait<kMF>();
-      else if (!RES)
-        vm_wait_plus<2 * kMF>(ndma);
-    }
+    // they replace. vmcnt retires in order; younger than those rows: this
+    // step's kMF stores (step 0: its K loop already drained every load, the
+    // compiler's waits on the weights)
+    vm_wait<kMF>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
   };
-  if constexpr (!(DBG & 8)) {
-    step_body(0);
-    for (int step = 1; step < kSteps; ++step) step_body(step);
-  }
+  step_body(0);
+  for (int step = 1; step < kSteps; ++step) step_body(step);
 }
 
 }  // namespace
@@ -466,8 +391,8 @@ void conv3x3_rows28(const void* x, const void* wf, const float* bias, const void
     a.xds = (const bf16*)xds;
     a.wds = (const bf16*)wds;
     a.bds = bds;
-    const size_t lds = (size_t)R28Ring<1>::kSlotsAlloc * kRB + 2 * (size_t)kMF * 16 * 128;  // two downsample-input buffers
-    hipLaunchKernelGGL((conv3x3_rows28_kernel<false, 0, 1, 4, false, true>), dim3(B), dim3(256), lds, s, a);
+    const size_t lds = (size_t)kSlotsAlloc * kRB + 2 * (size_t)kMF * 16 * 128;  // two downsample-input buffers
+    hipLaunchKernelGGL((conv3x3_rows28_kernel<false, false, true>), dim3(B), dim3(256), lds, s, a);
     DMLC_HIP_CHECK(hipGetLastError());
     return;
   }
@@ -485,14 +410,14 @@ void conv3x3_rows28(const void* x, const void* wf, const float* bias, const void
   a.relu = relu;
   a.out_inv_scale = out_inv_scale;
   if (out_inv_scale > 0.f) {
-    hipLaunchKernelGGL((conv3x3_rows28_kernel<false, 0, 1, 4, true>), dim3(B), dim3(256),
-                       (size_t)R28Ring<1>::kSlotsAlloc * kRB, s, a);
+    hipLaunchKernelGGL((conv3x3_rows28_kernel<false, true>), dim3(B), dim3(256),
+                       (size_t)kSlotsAlloc * kRB, s, a);
     DMLC_HIP_CHECK(hipGetLastError());
     return;
   }
-  // (the residual is double-buffered one step ahead: RES2)
-  const size_t lds = (size_t)R28Ring<1>::kSlotsAlloc * kRB + (res ? (size_t)2 * kResCh * 16 : 0);  // 90 / 151 KB
-  static_assert(R28Ring<1>::kSlotsAlloc * kRB + 2 * kResCh * 16 <= 160 * 1024, "LDS budget");
+  // (the residual is double-buffered one step ahead)
+  const size_t lds = (size_t)kSlotsAlloc * kRB + (res ? (size_t)2 * kResCh * 16 : 0);  // 90 / 151 KB
+  static_assert(kSlotsAlloc * kRB + 2 * kResCh * 16 <= 160 * 1024, "LDS budget");
   if (res)
     hipLaunchKernelGGL(conv3x3_rows28_kernel<true>, dim3(B), dim3(256), lds, s, a);
   else

@@ -50,7 +50,6 @@ struct S2Args {
   bf16* yd;           // [B, 28, 28, 128]
   const bf16* zero;
   int relu;
-  int dbg;  // experiment: bit 0 no loop DMA, bit 1 no stores
 };
 
 constexpr int kHI = 56, kWI = 56, kCI = 64, kH = 28, kW = 28, kCO = 128;
@@ -158,7 +157,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3_s2rows_kernel(S2Args a) {
   // whole weight load back in front of the first MFMA
   auto step_body = [&](const int step) __attribute__((always_inline)) {
     const int r0 = step * kR;  // first output row; input rows 2 r0 - 1 .. 2 r0 + 7
-    if (step + 1 < kSteps && !(a.dbg & 1))
+    if (step + 1 < kSteps)
       for (int yy = 2 * r0 + 8; yy <= 2 * r0 + 15; ++yy) load_row(yy);
     // ring slot of kernel row 0 of every fragment (+ kh rows: immediate, guard slots)
     const int sb = (2 * r0) % kRing;
@@ -216,10 +215,8 @@ __global__ __launch_bounds__(256, 1) void conv3x3_s2rows_kernel(S2Args a) {
           v[4 * nf + i] = acc[f][nf][i];
           vd[4 * nf + i] = DS ? accd[f][nf][i] : 0.f;
         }
-      if (!(a.dbg & 2)) {
-        *(uint4*)(a.y + o) = pack8_relu(v, a.relu);
-        if constexpr (DS) *(uint4*)(a.yd + o) = pack8(vd);
-      }
+      *(uint4*)(a.y + o) = pack8_relu(v, a.relu);
+      if constexpr (DS) *(uint4*)(a.yd + o) = pack8(vd);
     }
     // the next step's rows have landed (the (2) kMF stores just issued may
     // still be in flight: vmcnt retires in order) and every wave is done
@@ -239,7 +236,7 @@ bool conv3x3_s2rows_supported(int Hin, int Win, int Cin, int Cout) {
 }
 
 void conv3x3_s2rows(const void* x, const void* wf, const float* bias, const void* wdf, const float* bd, void* y,
-                    void* yd, const void* zero, int B, bool relu, hipStream_t s, int dbg) {
+                    void* yd, const void* zero, int B, bool relu, hipStream_t s) {
   if (B <= 0) return;
   if ((wdf == nullptr) != (bd == nullptr) || (wdf == nullptr) != (yd == nullptr))
     throw std::invalid_argument("conv3x3_s2rows: the downsample needs wdf, bd and yd together");
@@ -256,7 +253,6 @@ void conv3x3_s2rows(const void* x, const void* wf, const float* bias, const void
   a.yd = (bf16*)yd;
   a.zero = (const bf16*)zero;
   a.relu = relu;
-  a.dbg = dbg;
   if (wdf)
     hipLaunchKernelGGL(conv3x3_s2rows_kernel<true>, dim3(B), dim3(256), (size_t)kSlotsAlloc * kRB, s, a);
   else

@@ -156,7 +156,7 @@ void conv3x3_rows(const void* x, const void* w, const float* bias, const void* r
 // in LDS. wf1/wf2: fragment-order weights (stream_frag_index, K = 576).
 bool conv3x3_block_supported(int H, int W, int C);
 void conv3x3_block(const void* x, const void* wf1, const float* bias1, const void* wf2, const float* bias2, void* y,
-                   const void* zero, int B, hipStream_t s, int dbg = 0);
+                   const void* zero, int B, hipStream_t s);
 // Direct 3x3/s1/p1 conv on 13x13 images, the whole image in LDS
 // (conv3x3_13.hip): AlexNet features.6/.8/.10 (192->384, 384->256,
 // 256->256). wf: fragment-order weights (stream_frag_index, K = 9 Cin).
@@ -180,7 +180,7 @@ void conv5x5_27(const void* x, const void* wf, const float* bias, void* y, const
 bool bottleneck56_supported(int H, int W, int C, int Cm);
 void bottleneck56(const void* x, const void* w1, const float* a1, const float* b1, const void* wf2, const float* b2,
                   const void* wf3, const float* b3, void* y, float res_scale, float out_inv_scale, int B,
-                  hipStream_t s, int dbg = 0);
+                  hipStream_t s);
 // ResNet50 layer1.0's reduce 1x1 (64 -> 64) + 3x3 (64 -> 64) as one kernel
 // (bottleneck56.hip, t1 in LDS): x bf16 [B,56,56,64], w1 bf16 [64][64] (BN
 // folded), b1, wf2 / b2 as above, y = t2 bf16 [B,56,56,64].
@@ -200,7 +200,7 @@ bool conv3x3_s2rows128_supported(int Hin, int Win, int Cin, int Cout);
 void conv3x3_s2rows128(const void* x, const void* wf, const float* bias, void* y, int B, bool relu,
                        float out_inv_scale, hipStream_t s);
 void conv3x3_s2rows(const void* x, const void* wf, const float* bias, const void* wdf, const float* bd, void* y,
-                    void* yd, const void* zero, int B, bool relu, hipStream_t s, int dbg = 0);
+                    void* yd, const void* zero, int B, bool relu, hipStream_t s);
 // Weight-stationary row-streaming 3x3/s1/p1 conv for 28x28x128 -> 128
 // (conv3x3_rows28.hip): one workgroup per image, the weights in registers.
 // wf: fragment-order weights (stream_frag_index, K = 1152); res optional.
@@ -278,7 +278,8 @@ void stem_conv_pool(const void* x, const void* w, const float* bias, void* y, in
 // w_dense (optional, 16-B aligned): the same weights in dense-K order
 // [64][kStemDenseK] (stem_dense_k_index); with it the one-image-per-workgroup
 // kernel runs 5 K steps a fragment instead of 7 (stem_pool.hip, V & 2).
-// timing knock-outs of the 224x224 u8 stem (0 = off; see stem_pool.hip DBG)
+// test hooks (0 = off): 512 forces the one-image-per-workgroup kernel, 2048
+// its 4-B raw-row DMA form
 void stem_conv_pool_set_dbg(int dbg);
 void stem_conv_pool_u8(const uint8_t* x, const void* w, const float* bias, void* y, int B, int S, int strip,
                        hipStream_t s, const void* w_dense = nullptr);

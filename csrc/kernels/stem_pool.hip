@@ -208,14 +208,11 @@ struct StemGeom {
   static_assert(24 * ((Wq + 3) / 4) - 8 - 3 * S <= kU8Pad - kU8Front, "raw ring pad");
 };
 
-// DBG (timing experiments, tools/stem_knockouts.py): bit 0 no horizontal-pool
-// epilogue (one store of the accumulators per fragment instead), bit 1 no u8
-// conversion, bit 2 no vertical max / output stores, bit 3 no MFMAs
 // CS (channel split, query batches): the workgroup computes 64 / CS of the
 // 64 output channels (blockIdx.y picks which), so a batch too small to
 // fill the CUs with strips runs CS x as many workgroups (each converts the
 // same input rows: cheap next to the MFMAs it no longer does).
-template <int NF, bool U8, int DBG = 0, int CS = 1>
+template <int NF, bool U8, int CS = 1>
 __global__ __launch_bounds__(256, 2) void stem_conv_pool_kernel(
     StemArgs a) {
   using G = StemGeom<NF>;
@@ -368,29 +365,17 @@ __global__ __launch_bounds__(256, 2) void stem_conv_pool_kernel(
 #pragma unroll
           for (int n = 0; n < NB; ++n)
             acc[n] = floatx4{bs[n], bs[n], bs[n], bs[n]};  // the bias first (hpool_packed)
-          if constexpr (DBG & 8) {
-#pragma unroll
-            for (int n = 0; n < NB; ++n) acc[n][0] = (float)xf[n][0] + (float)wf[n][0][0];
-          } else {
 #pragma unroll
           for (int s = 0; s < 7; ++s)
 #pragma unroll
             for (int n = 0; n < NB; ++n)
               acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[s], wf[n][s], acc[n], 0, 0, 0);
-          }
           // The next fragment's operands go out before this epilogue so the
           // reads land under it.
           if (f + 1 < NF) {
 #pragma unroll
             for (int s = 0; s < 7; ++s)
               xf[s] = *(const bf16x8*)(rbase + rows[s] + (f + 1) * 256);
-          }
-          if constexpr (DBG & 1) {
-            float t = 0.f;
-#pragma unroll
-            for (int n = 0; n < NB; ++n) t += acc[n][0] + acc[n][1] + acc[n][2] + acc[n][3];
-            ds_write_lo16(hbase, __float_as_uint(t), f * 8 * kHpCol);
-            continue;
           }
           // horizontal 3-max over columns (2pw-1, 2pw, 2pw+1) + ReLU (the
           // bias is in the accumulators)
@@ -404,7 +389,7 @@ __global__ __launch_bounds__(256, 2) void stem_conv_pool_kernel(
     // the u8 conversion share one phase (they touch disjoint LDS).
     vm_wait<0>();
     lds_barrier();
-    if (t > 0 && !(DBG & 4)) {  // vertical 3-max -> pooled rows ph, ph+1
+    if (t > 0) {  // vertical 3-max -> pooled rows ph, ph+1
       const int ph = ph0 + 2 * (t - 1);
       constexpr int CG = 8 / CS;  // this workgroup's 8-channel groups
       const int per_row = G::PW * CG;
@@ -438,7 +423,7 @@ __global__ __launch_bounds__(256, 2) void stem_conv_pool_kernel(
     if constexpr (U8) {
       // the next step's raw rows landed; the paired rows they replace were
       // last read by this step's MFMAs (before the barrier above)
-      if (t < T && !(DBG & 2)) convert_rows(2 * c0 + 13, 8);
+      if (t < T) convert_rows(2 * c0 + 13, 8);
     }
     // the next step's MFMAs overwrite pooled rows read above and read the
     // converted rows
@@ -484,10 +469,8 @@ __device__ __forceinline__ void vm_wait_dyn(int n) {
 
 // V bit 1: the raw rows by 16-B LDS-DMA (one instruction per 672-B row
 // instead of three 4-B ones; the u8 images must be 16-B aligned, which the
-// launcher checks). V (stem_conv_pool_set_dbg bits 24-29): timing knock-outs
-// (tools/stem_roles_ab.py, profiles/r4_stem_roles.txt): 4 no u8 conversion, 8
-// no conv rows, 16 no horizontal-pool epilogue, 32 no raw-row DMA / vertical
-// max / stores (results wrong: timing only)
+// launcher checks). (Knock-out timings of the phases: profiles/r4_stem_roles.txt,
+// profiles/r6_stem_dense.txt.)
 //
 // V bit 2: dense K. The paired rows above hold [r g b r g b 0 0] chunks and
 // a kernel row takes one 32-wide K step of 8 pixels: 7 x 32 = 224 K for 147
@@ -641,7 +624,7 @@ __global__ __launch_bounds__(512, 1) void stem_roles_kernel(StemArgs a) {
 
   for (int t = 0; t <= T + 1; ++t) {
     if (mfma_wave) {
-      if (t <= T && !(V & 8)) {
+      if (t <= T) {
         const int c0 = 4 * t - 4;
         const int cr = c0 + wave;
         char* hrow = hp + ((cr + kRolesHpRing) % kRolesHpRing) * HPB;
@@ -704,12 +687,7 @@ __global__ __launch_bounds__(512, 1) void stem_roles_kernel(StemArgs a) {
                                                                           wf[n][s], acc[f & 1][n], 0, 0, 0);
             }
             if (f > 0) {
-              if (V & 16) {
-#pragma unroll
-                for (int n = 0; n < 4; ++n) asm volatile("" ::"v"(acc[(f - 1) & 1][n]));
-              } else {
-                hpool_packed<4>(acc[(f - 1) & 1], prevq, lane, fq, hbase, f - 1, (f - 1) * 8 * kHpCol);
-              }
+              hpool_packed<4>(acc[(f - 1) & 1], prevq, lane, fq, hbase, f - 1, (f - 1) * 8 * kHpCol);
             }
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -739,12 +717,7 @@ __global__ __launch_bounds__(512, 1) void stem_roles_kernel(StemArgs a) {
 #pragma unroll
               for (int s = 0; s < 7; ++s) xf[s] = *(const bf16x8*)(rbase + rows[s] + (f + 1) * 256);
             }
-            if (V & 16) {
-#pragma unroll
-              for (int n = 0; n < 4; ++n) asm volatile("" ::"v"(acc[n]));
-            } else {
-              hpool_packed<4>(acc, prevq, lane, fq, hbase, f, f * 8 * kHpCol);
-            }
+            hpool_packed<4>(acc, prevq, lane, fq, hbase, f, f * 8 * kHpCol);
           }
         }
       }
@@ -755,12 +728,12 @@ __global__ __launch_bounds__(512, 1) void stem_roles_kernel(StemArgs a) {
       // are not loaded)
       constexpr int DPR = (V & 1) ? 1 : (UB / 4 + 63) / 64;
       int nwait = 0;
-      if (t + 2 < T && !(V & 32)) {
+      if (t + 2 < T) {
         load_rows(8 * t + 21, 8);
 #pragma unroll
         for (int i = 0; i < 2; ++i) nwait += (8 * t + 21 + hw + 4 * i - 3 < G::S) ? DPR : 0;
       }
-      if (t >= 2 && !(V & 32)) {  // vertical 3-max of step t-1's conv rows -> pooled rows ph, ph+1
+      if (t >= 2) {  // vertical 3-max of step t-1's conv rows -> pooled rows ph, ph+1
         const int ph = 2 * (t - 2);
         constexpr int per_row = G::PW * 8;
         ushort8 m[4];
@@ -790,7 +763,7 @@ __global__ __launch_bounds__(512, 1) void stem_roles_kernel(StemArgs a) {
           nwait += (64 * hw + 256 * j < 2 * per_row) ? 1 : 0;  // a store instruction of this wave
         }
       }
-      if (t < T && !(V & 4)) convert_rows(8 * t + 5, 8, htid, 256);
+      if (t < T) convert_rows(8 * t + 5, 8, htid, 256);
       // step t-1's DMAs (converted at t+1) have landed: everything but this
       // step's DMAs and stores (vmcnt retires in issue order)
       vm_wait_dyn(nwait);
@@ -821,7 +794,7 @@ int stem_pool_pick_strip(int B, int PH, int num_cus) {
 
 namespace {
 int g_stem_dbg = 0;
-constexpr long kStemSplitCus = 256;  // MI355X CUs: the channel split fills them at query batches  // knock-out variant of the 224x224 u8 kernel (tools/stem_knockouts.py)
+constexpr long kStemSplitCus = 256;  // MI355X CUs: the channel split fills them at query batches
 
 void stem_launch(const void* x, const uint8_t* u8, const void* w, const void* w2, const float* bias, void* y, int B,
                  int S, int Wq, int strip, hipStream_t s) {
@@ -847,57 +820,17 @@ void stem_launch(const void* x, const uint8_t* u8, const void* w, const void* w2
   a.PH = PH;
   a.PW = PH;
   a.strip = strip;
-  // g_stem_dbg: bits 0-7 knock-outs, 512 force the role-split kernel, 1024
-  // forbid it, bits 16+ stagger + 1 (0 = the default)
-  a.stagger = (g_stem_dbg >> 16) ? (g_stem_dbg >> 16) - 1 : ((long)B * (PH / strip) >= 512 ? kStemStagger : 0);
+  // g_stem_dbg (tests): 512 force the role-split kernel, 2048 its 4-B raw-row DMA
+  a.stagger = (long)B * (PH / strip) >= 512 ? kStemStagger : 0;
   const size_t lds = u8 ? (size_t)kRingU8 * Wq * 16 + (size_t)kHp * a.PW * kHpCol + (size_t)kRingU8 * (S * 3 + kU8Pad)
                         : (size_t)kRing * Wq * 16 + (size_t)kHp * a.PW * kHpCol;
   const dim3 grid(B * (PH / strip));
-  if (u8 && NF == 7 && (g_stem_dbg & 255)) {
-    switch (g_stem_dbg & 255) {
-#define DMLC_STEM_DBG_CASE(D) \
-  case D: hipLaunchKernelGGL((stem_conv_pool_kernel<7, true, D>), grid, dim3(256), lds, s, a); break;
-      DMLC_STEM_DBG_CASE(1)
-      DMLC_STEM_DBG_CASE(2)
-      DMLC_STEM_DBG_CASE(4)
-      DMLC_STEM_DBG_CASE(6)
-      DMLC_STEM_DBG_CASE(7)
-      DMLC_STEM_DBG_CASE(8)
-      DMLC_STEM_DBG_CASE(14)
-#undef DMLC_STEM_DBG_CASE
-      default: throw std::invalid_argument("stem_conv_pool: unknown debug variant");
-    }
-  } else if (u8 && ((g_stem_dbg & 512) || (strip == PH && !(g_stem_dbg & 1024)))) {
+  if (u8 && ((g_stem_dbg & 512) || strip == PH)) {
     // one workgroup per image, role-split waves (stem_pool_u8_pick_strip picks
     // strip = PH once the batch gives every CU an image)
     const size_t lds_roles = (size_t)kRolesPairRing * Wq * 16 + (size_t)kRolesHpRing * a.PW * kHpCol +
                              (size_t)kRolesRawRing * (S * 3 + kU8Pad);
     if (lds_roles > 160 * 1024) throw std::invalid_argument("stem_conv_pool: role-split LDS budget");
-    const int rv = (g_stem_dbg >> 24) & 127;
-    if ((rv & 2) && !w2) throw std::invalid_argument("stem_conv_pool: dense-K variant without dense weights");
-    if (NF == 7 && rv) {
-      switch (rv) {
-#define DMLC_STEM_RV_CASE(V) \
-  case V: hipLaunchKernelGGL((stem_roles_kernel<7, V>), dim3(B), dim3(512), lds_roles, s, a); break;
-        DMLC_STEM_RV_CASE(4)
-        DMLC_STEM_RV_CASE(8)
-        DMLC_STEM_RV_CASE(9)
-        DMLC_STEM_RV_CASE(16)
-        DMLC_STEM_RV_CASE(36)
-        DMLC_STEM_RV_CASE(52)
-        DMLC_STEM_RV_CASE(40)
-        DMLC_STEM_RV_CASE(1)
-        DMLC_STEM_RV_CASE(3)
-        DMLC_STEM_RV_CASE(7)
-        DMLC_STEM_RV_CASE(19)
-        DMLC_STEM_RV_CASE(43)
-        DMLC_STEM_RV_CASE(55)
-#undef DMLC_STEM_RV_CASE
-        default: throw std::invalid_argument("stem_conv_pool: unknown role-split variant");
-      }
-      DMLC_HIP_CHECK(hipGetLastError());
-      return;
-    }
     // 16-B raw-row DMA when the images allow it (g_stem_dbg 2048: force the 4-B form)
     const bool d16 = !((uintptr_t)u8 & 15) && !(g_stem_dbg & 2048);
     if (d16 && w2) {  // dense K (the engine packs both weight orders)
@@ -928,14 +861,12 @@ void stem_launch(const void* x, const uint8_t* u8, const void* w, const void* w2
   } else if (u8) {
     // query batches: split the 64 channels over 2 or 4 workgroups when the
     // strips alone leave most CUs idle (B = 1: 28 strips -> 112 workgroups)
-    // (g_stem_dbg bits 12-13: 1 / 2 / 3 force a split of 1 / 2 / 4)
     const long wgs = (long)B * (PH / strip);
-    int cs = wgs * 4 <= kStemSplitCus ? 4 : wgs * 2 <= kStemSplitCus ? 2 : 1;
-    if ((g_stem_dbg >> 12) & 3) cs = 1 << (((g_stem_dbg >> 12) & 3) - 1);
+    const int cs = wgs * 4 <= kStemSplitCus ? 4 : wgs * 2 <= kStemSplitCus ? 2 : 1;
     const dim3 gs(grid.x, cs);
     switch (NF * 4 + (cs == 4 ? 2 : cs == 2 ? 1 : 0)) {
-      case 7 * 4 + 1: hipLaunchKernelGGL((stem_conv_pool_kernel<7, true, 0, 2>), gs, dim3(256), lds, s, a); break;
-      case 7 * 4 + 2: hipLaunchKernelGGL((stem_conv_pool_kernel<7, true, 0, 4>), gs, dim3(256), lds, s, a); break;
+      case 7 * 4 + 1: hipLaunchKernelGGL((stem_conv_pool_kernel<7, true, 2>), gs, dim3(256), lds, s, a); break;
+      case 7 * 4 + 2: hipLaunchKernelGGL((stem_conv_pool_kernel<7, true, 4>), gs, dim3(256), lds, s, a); break;
       default: break;
     }
     if (NF == 7 && cs > 1) {

@@ -180,7 +180,7 @@ def conv3x3_rows(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, re
 
 
 def conv3x3_block(x: torch.Tensor, w1_packed: torch.Tensor, b1: torch.Tensor, w2_packed: torch.Tensor,
-                  b2: torch.Tensor, variant: int = 0) -> torch.Tensor:
+                  b2: torch.Tensor) -> torch.Tensor:
     """A whole 56x56x64 basic block (conv3x3_block.hip) on NHWC bf16:
     relu(conv2(relu(conv1(x) + b1)) + b2 + x), the intermediate kept in LDS
     (rounded to bf16 like a stored activation). w*_packed: conv2d packed
@@ -194,7 +194,7 @@ def conv3x3_block(x: torch.Tensor, w1_packed: torch.Tensor, b1: torch.Tensor, w2
     y = torch.empty_like(x)
     wf1, wf2 = stream_weight_frag(w1_packed), stream_weight_frag(w2_packed)
     C.conv3x3_block(_ptr(x), _ptr(wf1), _ptr(b1.float().contiguous()), _ptr(wf2), _ptr(b2.float().contiguous()),
-                    _ptr(y), _ptr(_zero_page(x.device)), B, _stream(), variant)
+                    _ptr(y), _ptr(_zero_page(x.device)), B, _stream())
     return y
 
 

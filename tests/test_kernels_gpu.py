@@ -438,8 +438,11 @@ def test_conv3x3_rows(gpu, B, strip, res):
 @pytest.mark.parametrize("B", [1, 3])
 def test_conv3x3_block(gpu, B):
     """Fused layer1 basic block (conv3x3_block.hip: conv1 producer waves ->
-    LDS -> conv2 consumer waves + residual) vs torch fp32, and bit-identical
-    to two register-weight row convs (same MFMA order, bf16 intermediate)."""
+    LDS -> conv2 consumer waves + residual) vs torch fp32, and vs two
+    register-weight row convs: the block starts its accumulators from the
+    bias and adds the residual by v_dot2c_f32_bf16, the row convs add both
+    after the K loop, so the two round differently (the bf16 intermediate
+    too): within a few bf16 steps of each other, equally close to fp32."""
     g = torch.Generator().manual_seed(31)
     x = torch.randn(B, 64, 56, 56, generator=g).bfloat16().float()
     w1 = (torch.randn(64, 64, 3, 3, generator=g) / 24).bfloat16().float()
@@ -453,21 +456,12 @@ def test_conv3x3_block(gpu, B):
     y = ops.conv3x3_block(xg, wp1, b1.to(gpu), wp2, b2.to(gpu))
     tg = ops.conv3x3_rows(xg, wp1, b1.to(gpu), None, True, frag=True)
     y2 = ops.conv3x3_rows(tg, wp2, b2.to(gpu), xg, True, frag=True)
-    y_ws = ops.conv3x3_block(xg, wp1, b1.to(gpu), wp2, b2.to(gpu), variant=16)  # weight-stationary roles
-    # variant 32: the round-4 epilogue (bias added after the K loop, residual
-    # unpacked): bit-identical to the row convs; the default starts the
-    # accumulators from the bias and adds the residual by v_dot2c_f32_bf16,
-    # so it rounds differently (the bf16 intermediate too): within a few bf16
-    # steps of it, equally close to fp32
-    y_old = ops.conv3x3_block(xg, wp1, b1.to(gpu), wp2, b2.to(gpu), variant=32)
     torch.cuda.synchronize()
     got = _nchw(y.float().cpu())
     assert _rel(got, ref) < 5e-3, _rel(got, ref)
-    assert torch.equal(y_old, y2)
-    assert torch.equal(y_ws, y_old)
-    assert abs(_rel(got, ref) - _rel(_nchw(y_old.float().cpu()), ref)) < 1e-3
-    d = (y.float() - y_old.float()).abs()
-    tol = y_old.float().abs() * 2.0 ** -5 + 2e-3 * y_old.float().abs().max()
+    assert abs(_rel(got, ref) - _rel(_nchw(y2.float().cpu()), ref)) < 1e-3
+    d = (y.float() - y2.float()).abs()
+    tol = y2.float().abs() * 2.0 ** -5 + 2e-3 * y2.float().abs().max()
     assert (d <= tol).all(), (d - tol).max()
     assert (d > 0).float().mean() < 5e-2
 

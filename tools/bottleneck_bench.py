@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Microbenchmark of the fused ResNet50 layer1 bottleneck (bottleneck56.hip)
-at B=256 with parts knocked out (--dbg bits, see BnArgs::dbg): event-timed,
-median over --iters event pairs of --reps launches each. Random operands
+at B=256: event-timed, median over --iters event pairs of --reps launches
+each (its phase knock-outs: profiles/r3_bottleneck_*.txt). Random operands
 (timing only; numerics are tests/test_engine_gpu.py's)."""
 import argparse
 import os
@@ -19,7 +19,6 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--iters", type=int, default=15)
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--dbg", default="0,1,2,4,3,7")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     B = args.batch
@@ -40,10 +39,10 @@ def main():
     C = dmlc.native()
     P = [t.data_ptr() for t in (x, w1, a1, b1, wf2, b2, wf3, b3, y)]
     torch.cuda.synchronize()
-    for dbg in (int(d) for d in args.dbg.split(",")):
+    for _rnd in range(2):  # two passes: the spread between them is the noise
         def run():
             for _ in range(args.reps):
-                C.bottleneck56(*P, 1.0, 1.0, B, 0, dbg)
+                C.bottleneck56(*P, 1.0, 1.0, B, 0)
         run()
         torch.cuda.synchronize()
         ts = []
@@ -54,7 +53,7 @@ def main():
             e1.record()
             e1.synchronize()
             ts.append(e0.elapsed_time(e1) * 1e3 / args.reps)
-        print(f"dbg={dbg:2d}  {statistics.median(ts):8.1f} us", flush=True)
+        print(f"bottleneck56  {statistics.median(ts):8.1f} us", flush=True)
 
 
 if __name__ == "__main__":

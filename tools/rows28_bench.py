@@ -33,7 +33,6 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--reps", type=int, default=10)
-    ap.add_argument("--dbg", action="store_true", help="also time the experiment variants")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     g = torch.Generator().manual_seed(1)
@@ -50,10 +49,10 @@ def main():
     P = ops._ptr
     flop = 2 * B * 28 * 28 * 128 * 1152
 
-    def rows(res, dbg=0):
+    def rows(res):
         def run():
             for _ in range(args.reps):
-                C.conv3x3_rows28(P(x), P(wf), P(b1), P(res), P(y), B, True, ops._stream(), dbg)
+                C.conv3x3_rows28(P(x), P(wf), P(b1), P(res), P(y), B, True, ops._stream())
         return run
 
     def stream(res):
@@ -63,13 +62,7 @@ def main():
                                  ops._stream())
         return run
 
-    runs = [("rows28", rows(None)), ("rows28+res", rows(r)), ("ahead2", rows(None, 64)), ("ahead2+res", rows(r, 65)),
-            ("8 waves", rows(None, 128)), ("8 waves+res", rows(r, 129)),
-            ("stream", stream(None)), ("stream+res", stream(r))]
-    if args.dbg:
-        runs += [("no DMA", rows(None, 1)), ("no LDS rd", rows(None, 2)), ("no DMA wait", rows(None, 16)),
-                 ("DMA row 0", rows(None, 32)), ("prologue", rows(None, 8)), ("no epilogue", rows(None, 4)),
-                 ("no DMA,LDS,epi", rows(None, 7))]
+    runs = [("rows28", rows(None)), ("rows28+res", rows(r)), ("stream", stream(None)), ("stream+res", stream(r))]
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from conv_bench import warm_gpu
     warm_gpu()

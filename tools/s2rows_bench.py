@@ -33,7 +33,6 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--reps", type=int, default=10, help="launches per timed event pair")
-    ap.add_argument("--dbg", action="store_true", help="also time the no-DMA / no-store experiment variants")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     g = torch.Generator().manual_seed(1)
@@ -52,10 +51,10 @@ def main():
     P = ops._ptr
     flop = 2 * B * 28 * 28 * 128 * (576 + 64)
 
-    def rows(dbg=0):
+    def rows():
         def run():
             for _ in range(args.reps):
-                C.conv3x3_s2rows(P(x), P(wf), P(b1), P(wdf), P(bd), P(y), P(yd), P(zero), B, True, ops._stream(), dbg)
+                C.conv3x3_s2rows(P(x), P(wf), P(b1), P(wdf), P(bd), P(y), P(yd), P(zero), B, True, ops._stream())
         return run
 
     def stream():
@@ -64,8 +63,6 @@ def main():
                              P(wdp), P(bd), P(yd))
 
     runs = [("s2rows", rows()), ("stream+ds", stream)]
-    if args.dbg:
-        runs += [("no DMA", rows(1)), ("no stores", rows(2)), ("neither", rows(3))]
     for name, fn in runs:
         fn()
         torch.cuda.synchronize()
