@@ -23,11 +23,11 @@
 //    groups), stored as one 16-B (bf16) / 8-B (e4m3) write.
 //
 // vmcnt retires in issue order and the compiler cannot see the asm loads, so
-// every wait is explicit: per block a wave issues RES (residual loads), DMA
-// (S-1 blocks ahead; dummy zero-page loads past the end keep the count
-// uniform) and ST (stores); the block's DMA has landed when at most
-// (S-1)(ST+RES+DMA) newer operations are outstanding, its residual when at
-// most DMA are. Only M % BM == 0 is supported (BM = 64, 32 for 1-KB rows: no
+// every wait is explicit: per block a wave issues RES (the next block's
+// residual loads), DMA (S-1 blocks ahead; dummy zero-page loads past the end
+// keep the counts uniform) and ST (stores); the block's DMA has landed when at
+// most (S-1)(ST+RES+DMA) newer operations are outstanding, its residual when
+// at most 2 DMA + ST + RES are. Only M % BM == 0 is supported (BM = 64, 32 for 1-KB rows: no
 // partial blocks, so every wave issues the same instruction counts).
 #include "common.h"
 #include "kernels.h"
@@ -252,34 +252,48 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void conv1x1_kernel(C1Arg
   typedef typename std::conditional<
       OUT8, typename std::conditional<(CPL == 16), u32x4, typename std::conditional<(CPL == 8), u32x2, uint32_t>::type>::type,
       typename std::conditional<(CPL == 8), u32x4, u32x2>::type>::type RV;
-  RV rv[NPF][NG];
+  // PRE (e4m3 output with a residual): the residual of a block is loaded one
+  // block ahead, into the other of two register sets (the block loop is
+  // unrolled by two so each set stays in fixed registers), so its latency
+  // hides under a whole block, not just the block's own MFMAs. (bf16: the
+  // 64-channel forms have no registers for a second set; each block loads
+  // its own residual with its DMA.)
+  constexpr bool PRE = RES && OUT8 && (WV == 8 || RB <= 256);  // (the 4-wave 512-B form: no registers either)
+  RV rv0[NPF][NG], rv1[NPF][NG];
+  auto load_res = [&](int blk, RV (&rv)[NPF][NG]) __attribute__((always_inline)) {
+    const bool live = blk < a.nblocks;  // (past the end: the zero page, so every wave issues RT loads)
+#pragma unroll
+    for (int pf = 0; pf < NPF; ++pf)
+#pragma unroll
+      for (int j = 0; j < NG; ++j) {
+        const void* p = live ? (const void*)res_ptr(blk, pf, j) : a.zero;
+        if constexpr (OUT8 && CPL == 16) rv[pf][j] = gload16(p);
+        else if constexpr (OUT8 && CPL == 8) rv[pf][j] = gload8(p);
+        else if constexpr (OUT8) rv[pf][j] = gload4(p);
+        else if constexpr (CPL == 8) rv[pf][j] = gload16(p);
+        else rv[pf][j] = gload8(p);
+      }
+  };
 
-  // prologue: blocks 0 .. S-2 of this workgroup
+  // prologue: the first block's residual, then blocks 0 .. S-2's rows
+  if constexpr (PRE) load_res(mstart, rv0);
 #pragma unroll
   for (int s = 0; s < S - 1; ++s) issue_dma(mstart + s * mstride, s);
 
-  int it = 0;
-  for (int blk = mstart; blk < a.nblocks; blk += mstride, ++it) {
+  // per block a wave issues R [RT] (PRE: the next block's), D(block + S-1)
+  // [DT], then after the MFMAs its stores [ST]. The block's rows have landed
+  // when at most N1 = (S-1)(RT+DT+ST) newer operations are outstanding; its
+  // residual when at most 2 DT + ST + RT (PRE: issued one block earlier,
+  // after D(block + S-2)) / DT are.
+  auto block = [&](int blk, int it, RV (&rv)[NPF][NG], RV (&rvn)[NPF][NG]) __attribute__((always_inline)) {
     const int st = it % S;
     lds_barrier();  // every wave is done with stage (it-1) % S: the DMA below reuses it
-    if constexpr (RES) {
-#pragma unroll
-      for (int pf = 0; pf < NPF; ++pf)
-#pragma unroll
-        for (int j = 0; j < NG; ++j) {
-          const void* p = res_ptr(blk, pf, j);
-          if constexpr (OUT8 && CPL == 16) rv[pf][j] = gload16(p);
-          else if constexpr (OUT8 && CPL == 8) rv[pf][j] = gload8(p);
-          else if constexpr (OUT8) rv[pf][j] = gload4(p);
-          else if constexpr (CPL == 8) rv[pf][j] = gload16(p);
-          else rv[pf][j] = gload8(p);
-        }
-    }
+    if constexpr (PRE) load_res(blk + mstride, rvn);
+    else if constexpr (RES) load_res(blk, rv);
     issue_dma(blk + (S - 1) * mstride, (it + S - 1) % S);
-    if (it < S - 1) vm_wait<DT>();  // prologue blocks: only this DMA may stay in flight
+    if (it < S - 1) vm_wait<PRE ? RT + DT : DT>();  // prologue blocks: only this block's issues may stay in flight
     else vm_wait<N1>();
     lds_barrier();  // every wave's share of block blk's rows has landed
-
     // ---- MFMAs: acc[pf][f] = D[channel ch(f, 4g+i)][pixel 16pf + fr]
     const char* sb = stages + st * STAGE;
     floatx4 acc[NPF][NF];
@@ -317,7 +331,11 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void conv1x1_kernel(C1Arg
 
     // ---- epilogue
     if constexpr (RES) {
-      vm_wait<DT>();  // this block's residual (only the DMA issued after it may be in flight)
+      if constexpr (PRE) {
+        if (it >= S - 1) vm_wait<2 * DT + ST + RT>();  // this block's residual (earlier blocks: waited above)
+      } else {
+        vm_wait<DT>();  // this block's residual (only the DMA issued after it may be in flight)
+      }
 #pragma unroll
       for (int pf = 0; pf < NPF; ++pf)
 #pragma unroll
@@ -386,6 +404,15 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void conv1x1_kernel(C1Arg
         }
       }
     }
+  };
+  int it = 0;
+  if constexpr (PRE) {
+    for (int blk = mstart; blk < a.nblocks; blk += 2 * mstride, it += 2) {
+      block(blk, it, rv0, rv1);
+      if (blk + mstride < a.nblocks) block(blk + mstride, it + 1, rv1, rv0);
+    }
+  } else {
+    for (int blk = mstart; blk < a.nblocks; blk += mstride, ++it) block(blk, it, rv0, rv0);
   }
   vm_wait<0>();  // no LDS-DMA may outlive the workgroup
 }

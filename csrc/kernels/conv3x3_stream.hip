@@ -712,10 +712,8 @@ void conv3x3_stream(const void* x, const void* w, const float* bias, const void*
   else if (stride == 1 && Cin == 128)  // layer2: half an image (15 x 28 x 256 B = 105 KB)
     launch_stream<28, 28, 128, 128, 14, 1, 1, 2, 1>(a, s);
   else if (stride == 1 && Cin == 256 && wfrag) {  // layer3, register weights, 2 pixel halves x 4 groups of 64 channels
-    if (g_stream_variant & 1)
+    if (g_stream_variant & 1)  // (tests: a 2-deep weight ring, the same MFMA order)
       launch_stream<14, 14, 256, 256, 14, 1, 1, 2, 1, true, 2, 2>(a, s);
-    else if (g_stream_variant & 32)
-      launch_stream<14, 14, 256, 256, 14, 1, 1, 2, 1, true, 4, 2, 1>(a, s);
     else
       launch_stream<14, 14, 256, 256, 14, 1, 1, 2, 1, true, 4, 2>(a, s);
   }
@@ -724,12 +722,7 @@ void conv3x3_stream(const void* x, const void* w, const float* bias, const void*
   else if (stride == 1 && wfrag) {  // layer4, weights in fragment order straight into VGPRs
     // (two 64-channel groups per wave measured slower here: 2 images x 2
     // pixel halves 58.7 us, 1 image x 8 groups 60.9 us vs 53.0 us)
-    if (g_stream_variant & 8)
-      launch_stream<7, 7, 512, 512, 7, 2, 2, 1, 1, true, 8>(a, s);
-    else if (g_stream_variant & 32)
-      launch_stream<7, 7, 512, 512, 7, 2, 2, 1, 1, true, 4, 1, 1>(a, s);
-    else
-      launch_stream<7, 7, 512, 512, 7, 2, 2, 1, 1, true>(a, s);
+    launch_stream<7, 7, 512, 512, 7, 2, 2, 1, 1, true>(a, s);
   }
   else if (stride == 1)  // layer4: two whole images x half the output channels (2 x 49 x 1 KB = 98 KB)
     launch_stream<7, 7, 512, 512, 7, 2, 2, 1, 1>(a, s);
@@ -756,8 +749,6 @@ void conv3x3_stream(const void* x, const void* w, const float* bias, const void*
     // workgroup, 32 per wave (variant bit 4; profiles/r3_stream_s2_ng2.txt)
     if (g_stream_variant & 4)
       launch_stream<7, 7, 256, 512, 7, 1, 2, 1, 2, true>(a, s);
-    else if (g_stream_variant & 32)
-      launch_stream<7, 7, 256, 512, 7, 1, 1, 1, 2, true, 4, 2, 1>(a, s);
     else
       launch_stream<7, 7, 256, 512, 7, 1, 1, 1, 2, true, 4, 2>(a, s);
   }

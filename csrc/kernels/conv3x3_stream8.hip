@@ -374,11 +374,8 @@ void conv3x3_stream8(const void* x, const void* wf, const float* alpha, const fl
     // groups of 32; 188 VGPRs). All 256 channels per workgroup (4 groups of
     // 64 per wave) spills at any ring depth.
     launch8<14, 14, 256, 256, 14, 1, 2, 2, 1, 2, 1>(a, s);
-  } else {  // layer4: two images x half the channels, 8 groups of 32 (variant 2: a 2-deep weight ring)
-    if (v & 2)
-      launch8<7, 7, 512, 512, 7, 2, 2, 1, 1, 2, 1>(a, s);
-    else
-      launch8<7, 7, 512, 512, 7, 2, 2, 1, 1, 4, 1>(a, s);
+  } else {  // layer4: two images x half the channels, 8 groups of 32
+    launch8<7, 7, 512, 512, 7, 2, 2, 1, 1, 4, 1>(a, s);
   }
   DMLC_HIP_CHECK(hipGetLastError());
 }

@@ -238,7 +238,7 @@ size_t conv3x3_stream8_frag_offset(int j, int t, int nf, int h, int lane, int KT
 void conv3x3_stream8(const void* x, const void* wf, const float* alpha, const float* bias, void* y, const void* zero,
                      int B, int Hin, int Win, int Cin, int Cout, int stride, bool relu, float out_inv_scale,
                      hipStream_t s);
-void conv3x3_stream8_set_variant(int v);  // A/B hook (0 = the defaults)
+void conv3x3_stream8_set_variant(int v);  // test hook (0 = the defaults; 4: 7-row strips at layer2.0.conv2)
 // Stride 2 may also compute the block's 1x1/s2 downsample conv (wd [Cout,
 // Cin], bias bd, no ReLU) from the same resident input into yd.
 void conv3x3_stream(const void* x, const void* w, const float* bias, const void* res, void* y, const void* zero,
@@ -255,7 +255,9 @@ bool conv3x3_stream_pool_supported(int Hin, int Win, int Cin, int Cout, int stri
 // wfrag: the same weights in fragment order (stream_weight_frag_layout), used
 // by the variants that load weights straight into VGPRs (7x7x512 stride 1)
 bool conv3x3_stream_uses_frag(int Hin, int Win, int Cin, int Cout, int stride);
-// A/B tuning hook (tools/conv_bench.py): picks alternative register-weight kernels
+// test / A/B hook (tests/test_kernels_gpu.py, tools/conv_bench.py), 0 = the
+// defaults: bit 0 a 2-deep weight ring (14x14x256), bit 1 two channel groups a
+// wave (14x14 128 -> 256 / s2), bit 2 32 channels a wave (7x7 256 -> 512 / s2)
 void conv3x3_stream_set_variant(int v);
 // [Cout, K] row-major bf16 -> fragment order [Cout/32][K/32][2][64][8]:
 // dst index of (n, k) for n < Cout, k < K (Cout % 32 == 0, K % 32 == 0)
