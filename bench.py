@@ -180,6 +180,9 @@ def main():
     use_graph = not args.no_graph
     eng = sd = None
     if not dry:
+        # one compute lane: the stream convs' workgroup start stagger (set
+        # before any graph captures the launches; csrc/kernels/stagger.hip)
+        C.kernel_stagger_for_lanes(args.lanes)
         # Random-init weights (the reference's .ot files are LFS stubs); every
         # rank builds the same seeded model.
         sd = state_dict_f32(build(args.model, seed=0))

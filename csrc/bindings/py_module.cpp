@@ -275,6 +275,9 @@ PYBIND11_MODULE(_C, m) {
         py::arg("stream"), py::arg("w_dense") = 0);
   m.def("stem_dense_k_index", &stem_dense_k_index);
   m.def("stem_conv_pool_set_dbg", &stem_conv_pool_set_dbg);
+  m.def("kernel_stagger", &kernel_stagger);
+  m.def("kernel_stagger_set", &kernel_stagger_set);
+  m.def("kernel_stagger_for_lanes", &kernel_stagger_for_lanes);
   m.def("stem_conv_pool", [](uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y, int B, int S_, int Wq,
                              int strip, uintptr_t stream) {
     stem_conv_pool(P<void>(x), P<void>(w), P<float>(bias), P<void>(y), B, S_, Wq, strip, S(stream));

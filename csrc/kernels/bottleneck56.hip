@@ -62,6 +62,7 @@ struct BnArgs {
   uint8_t* y;          // [B, 56, 56, 256] e4m3
   float res_scale;     // s_x
   float out_inv_scale; // 1 / s_y
+  int stagger;         // start_stagger (common.h)
 };
 
 constexpr int kH = 56, kW = 56, kC = 256, kM = 64;
@@ -463,6 +464,7 @@ __global__ __launch_bounds__(512, 1) void bottleneck56_kernel(BnArgs a) {
   float* cst = (float*)(xb + kXB);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  start_stagger(a.stagger);
   // zero the t1 ring (its pad columns stay zero for the whole kernel); the
   // per-channel constants -> LDS
   for (int i = tid; i < kRing * kSlot / 16; i += 512) ((uint4*)ring)[i] = make_uint4(0, 0, 0, 0);
@@ -574,6 +576,7 @@ __global__ __launch_bounds__(512, 1) void bottleneck56_head_kernel(BnArgs a) {
   float* cst = (float*)(xb + kXBh);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  start_stagger(a.stagger);
   for (int i = tid; i < kRing * kSlot / 16; i += 512) ((uint4*)ring)[i] = make_uint4(0, 0, 0, 0);
   if (tid < kM) {
     cst[tid] = 1.f;  // (no conv1 alpha: bf16 weights carry the BN scale)
@@ -629,6 +632,7 @@ void bottleneck56(const void* x, const void* w1, const float* a1, const float* b
     throw std::invalid_argument("bottleneck56: null / misaligned operand");
   if (x == y) throw std::invalid_argument("bottleneck56: in-place not supported (the residual is re-read)");
   BnArgs a;
+  a.stagger = kernel_stagger(kStagBottleneck);
   a.x = (const uint8_t*)x;
   a.w1 = (const uint8_t*)w1;
   a.a1 = a1;
@@ -651,6 +655,7 @@ void bottleneck56_head(const void* x, const void* w1, const float* b1, const voi
     throw std::invalid_argument("bottleneck56_head: null / misaligned operand");
   if (x == y) throw std::invalid_argument("bottleneck56_head: in-place not supported");
   BnArgs a = {};
+  a.stagger = kernel_stagger(kStagBottleneck);
   a.x = (const uint8_t*)x;
   a.w1 = (const uint8_t*)w1;
   a.b1 = b1;

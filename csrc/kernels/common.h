@@ -15,6 +15,17 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 constexpr int kWave = 64;
 
+// Workgroup start stagger (launch tuning, kernels.h kernel_stagger): a
+// workgroup on an odd CU of its XCD (workgroups are dealt to the 8 XCDs
+// round-robin, then to CUs in order) starts n x ~2048 cycles late. With one
+// workgroup per CU every workgroup otherwise runs its HBM-bound prologue, its
+// MFMA loop and its store-bound epilogue in step with all the others; offset
+// halves overlap one half's memory phase with the other half's MFMAs.
+__device__ __forceinline__ void start_stagger(int n) {
+  if (n && ((blockIdx.x >> 3) & 1))  // (a wave-uniform scalar loop)
+    for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(32);
+}
+
 __device__ __forceinline__ float bf2f(bf16 v) { return (float)v; }
 __device__ __forceinline__ bf16 f2bf(float v) { return (bf16)v; }  // v_cvt_pk_bf16_f32 (RNE)
 

@@ -123,6 +123,7 @@ struct C1Args {
   float res_scale, out_inv_scale;
   const void* x2;  // second input (K chunks cpr1 .. CPR-1 of a pixel), or null
   int cpr1;        // 16-B chunks of a pixel from x
+  int stagger;     // start_stagger (common.h)
 };
 
 // pixels per block: 64, or 32 for 1-KB input rows (stage = BM x RB bytes)
@@ -159,6 +160,7 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void conv1x1_kernel(C1Arg
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  start_stagger(a.stagger);
   const int fr = lane & 15, g = lane >> 4;
   // block id -> (slice, first block): the slices of one M block on one XCD
   const int wgid = blockIdx.x;
@@ -536,6 +538,7 @@ void conv1x1(const ConvArgs& a, int num_cus, hipStream_t s) {
   c.N = a.N;
   c.Kpad = a.Kpad;
   c.relu = a.relu;
+  c.stagger = kernel_stagger(kStagConv1x1);
   c.res_scale = a.res_scale;
   c.out_inv_scale = a.out_inv_scale;
   c.nslices = a.N / (pk.wv * pk.nw);

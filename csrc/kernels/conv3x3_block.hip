@@ -50,6 +50,7 @@ struct BlockArgs {
   const float* bias2;  // [64]
   bf16* y;             // [B, 56, 56, 64]
   const bf16* zero;    // >= 16 zero bytes
+  int stagger;         // start_stagger (common.h)
 };
 
 constexpr int kH = 56, kW = 56, kC = 64;
@@ -276,6 +277,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_block_kernel(BlockArgs a) {
   char* tring = xring + kRing * kSlot;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  start_stagger(a.stagger);
   // zero both rings (pad columns stay zero; x row -1 is the zeroed slot 9;
   // t halo rows are written as zeros), before any x-row DMA lands
   for (int i = tid; i < 2 * kRing * kSlot / 16; i += 512) ((uint4*)xring)[i] = make_uint4(0, 0, 0, 0);
@@ -306,6 +308,7 @@ void conv3x3_block(const void* x, const void* wf1, const float* bias1, const voi
   a.bias2 = bias2;
   a.y = (bf16*)y;
   a.zero = (const bf16*)zero;
+  a.stagger = kernel_stagger(kStagBlock);
   const size_t lds = (size_t)2 * kRing * kSlot;  // 148.5 KB
   // PD 6: 5 K steps of weight lookahead (PD 3 and a mid-step DMA measured
   // the same, 116-120 us at B=256); tools/block_bench.py

@@ -60,6 +60,7 @@ struct R28Args {
   const bf16* xds;
   const bf16* wds;
   const float* bds;
+  int stagger;  // start_stagger (common.h)
 };
 
 // 4 floats (within +-448) -> 4 e4m3 bytes
@@ -107,6 +108,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3_rows28_kernel(R28Args a) {
   char* resbuf = ring + kSlotsAlloc * kRB;  // RES: [112 pixels][16 chunks]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  start_stagger(a.stagger);
   const int fr = lane & 15, g = lane >> 4;
   const int b = blockIdx.x;
   const bf16* img = a.x + (long)b * kH * kW * kC;
@@ -391,6 +393,7 @@ void conv3x3_rows28(const void* x, const void* wf, const float* bias, const void
     a.xds = (const bf16*)xds;
     a.wds = (const bf16*)wds;
     a.bds = bds;
+    a.stagger = kernel_stagger(kStagRows28);
     const size_t lds = (size_t)kSlotsAlloc * kRB + 2 * (size_t)kMF * 16 * 128;  // two downsample-input buffers
     hipLaunchKernelGGL((conv3x3_rows28_kernel<false, false, true>), dim3(B), dim3(256), lds, s, a);
     DMLC_HIP_CHECK(hipGetLastError());
@@ -409,6 +412,7 @@ void conv3x3_rows28(const void* x, const void* wf, const float* bias, const void
   a.y = (bf16*)y;
   a.relu = relu;
   a.out_inv_scale = out_inv_scale;
+  a.stagger = kernel_stagger(kStagRows28);
   if (out_inv_scale > 0.f) {
     hipLaunchKernelGGL((conv3x3_rows28_kernel<false, true>), dim3(B), dim3(256),
                        (size_t)kSlotsAlloc * kRB, s, a);

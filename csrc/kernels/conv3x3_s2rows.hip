@@ -50,6 +50,7 @@ struct S2Args {
   bf16* yd;           // [B, 28, 28, 128]
   const bf16* zero;
   int relu;
+  int stagger;  // start_stagger (common.h)
 };
 
 constexpr int kHI = 56, kWI = 56, kCI = 64, kH = 28, kW = 28, kCO = 128;
@@ -78,6 +79,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3_s2rows_kernel(S2Args a) {
   char* ring = (char*)smem;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  start_stagger(a.stagger);
   const int fr = lane & 15, g = lane >> 4;
   const int b = blockIdx.x;
   const bf16* img = a.x + (long)b * kHI * kWI * kCI;
@@ -244,6 +246,7 @@ void conv3x3_s2rows(const void* x, const void* wf, const float* bias, const void
       (((uintptr_t)x | (uintptr_t)wf | (uintptr_t)wdf | (uintptr_t)y | (uintptr_t)yd | (uintptr_t)zero) & 15))
     throw std::invalid_argument("conv3x3_s2rows: null / misaligned operand");
   S2Args a;
+  a.stagger = kernel_stagger(kStagS2rows);
   a.x = (const bf16*)x;
   a.wf = (const bf16*)wf;
   a.wdf = (const bf16*)wdf;

@@ -78,6 +78,7 @@ struct StreamConvArgs {
   // e4m3 output (ResNet50's bottleneck 3x3 -> its e4m3 expand conv): y holds
   // round(relu(v) * out_inv_scale) as e4m3 bytes [B, H, W, CO]; 0 = bf16
   float out_inv_scale;
+  int stagger;  // start_stagger (common.h)
 };
 
 struct alignas(8) u32x2s {
@@ -195,6 +196,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream_kernel(StreamConvArgs a
   // counted LDS wait into lgkmcnt(0): consume them here.
   const int relu = a.relu;
   asm volatile("" ::"s"(relu));
+  start_stagger(a.stagger);
   unsigned long long t_start = 0, t_first = 0;
   if (a.stamps) {
     t_start = __builtin_amdgcn_s_memrealtime();
@@ -693,6 +695,7 @@ void conv3x3_stream(const void* x, const void* w, const float* bias, const void*
   a.B = B;
   a.relu = relu;
   a.stamps = stamps;
+  a.stagger = kernel_stagger(kStagStream);
   a.wd = (const bf16*)wd;
   a.bd = bd;
   a.yd = (bf16*)yd;

@@ -53,6 +53,7 @@ struct Stream8Args {
   int B;
   int relu;
   float out_inv_scale;  // y = e4m3(relu(v) * out_inv_scale)
+  int stagger;          // start_stagger (common.h)
 };
 
 // Geometry: output H x W, stride S; a workgroup owns HS output rows of one
@@ -103,6 +104,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream8_kernel(Stream8Args a) 
   char* xs = (char*)smem;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  start_stagger(a.stagger);
   const int wm = wave % WM, wc = wave / WM;
   const int fr = lane & 15, fq = lane >> 4;
   const int ns = blockIdx.x % NSP, rest = blockIdx.x / NSP;
@@ -344,6 +346,7 @@ void conv3x3_stream8(const void* x, const void* wf, const float* alpha, const fl
   a.B = B;
   a.relu = relu;
   a.out_inv_scale = out_inv_scale;
+  a.stagger = kernel_stagger(kStagStream8);
   const int v = g_stream8_variant;
   if (stride == 2 && Cin == 128) {
     // layer2.0.conv2 (56x56x128 -> 28x28): 4 output rows (9 staged rows of

@@ -283,6 +283,16 @@ void stem_conv_pool(const void* x, const void* w, const float* bias, void* y, in
 // test hooks (0 = off): 512 forces the one-image-per-workgroup kernel, 2048
 // its 4-B raw-row DMA form
 void stem_conv_pool_set_dbg(int dbg);
+// Workgroup start stagger per kernel family (common.h start_stagger): the
+// launchers pass kernel_stagger(k) to their kernels. kernel_stagger_set is the
+// A/B hook (tools/engine_ab.py); n < 0 restores the default.
+enum StaggerKernel { kStagStream = 0, kStagBlock, kStagRows28, kStagS2rows, kStagStem, kStagStream8, kStagConv1x1,
+                     kStagBottleneck, kStagCount };
+int kernel_stagger(int k);
+void kernel_stagger_set(int k, int n);
+// The process's compute-lane count (bench.py, dmlc-node --lanes): one lane
+// staggers the stream convs (stagger.hip), more lanes use the defaults.
+void kernel_stagger_for_lanes(int lanes);
 void stem_conv_pool_u8(const uint8_t* x, const void* w, const float* bias, void* y, int B, int S, int strip,
                        hipStream_t s, const void* w_dense = nullptr);
 constexpr int kStemDenseK = 160;

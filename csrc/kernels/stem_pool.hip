@@ -89,6 +89,7 @@ struct StemArgs {
   // matrix pipes idle. 100.9 -> 93.0 us at B = 256 with 2
   // (profiles/r3_stem_knockouts.txt).
   int stagger;
+  int rstagger;  // the one-image-per-workgroup kernel: start_stagger (common.h)
 };
 constexpr int kStemStagger = 2;
 
@@ -503,6 +504,7 @@ __global__ __launch_bounds__(512, 1) void stem_roles_kernel(StemArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  start_stagger(a.rstagger);
   const bool mfma_wave = wave < 4;
   const int hw = wave & 3, htid = tid & 255;  // helper wave / thread index among the helpers
   const int fr = lane & 15, fq = lane >> 4;
@@ -822,6 +824,7 @@ void stem_launch(const void* x, const uint8_t* u8, const void* w, const void* w2
   a.strip = strip;
   // g_stem_dbg (tests): 512 force the role-split kernel, 2048 its 4-B raw-row DMA
   a.stagger = (long)B * (PH / strip) >= 512 ? kStemStagger : 0;
+  a.rstagger = kernel_stagger(kStagStem);
   const size_t lds = u8 ? (size_t)kRingU8 * Wq * 16 + (size_t)kHp * a.PW * kHpCol + (size_t)kRingU8 * (S * 3 + kU8Pad)
                         : (size_t)kRing * Wq * 16 + (size_t)kHp * a.PW * kHpCol;
   const dim3 grid(B * (PH / strip));

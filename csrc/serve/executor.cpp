@@ -212,6 +212,7 @@ class GpuExecutor : public Executor {
       : devices_(std::move(devices)), max_batch_(max_batch), lanes_(std::max(1, std::min(lanes, 4))),
         cache_cap_(cache_bytes) {
     if (devices_.empty()) throw std::invalid_argument("GpuExecutor: no devices");
+    kernel_stagger_for_lanes(lanes_);  // (one lane: the stream convs staggered, stagger.hip)
     for (int d : devices_) cache_bytes_dev_[d] = 0;
     if (devices_.size() > 1) enable_peers();
     for (int i = 0; i < kStagers; ++i) free_stagers_.push_back(std::make_shared<Stager>());

@@ -10,7 +10,9 @@ every non-default variant are checked bit-identical to the default first
   python tools/engine_ab.py --model resnet18 --variants "stream=0;stream=64"
 
 Hooks: stream (conv3x3_stream_set_variant), stream8 (conv3x3_stream8_set_variant),
-stem (stem_conv_pool_set_dbg), comma-separated within a variant."""
+stem (stem_conv_pool_set_dbg), stag_<family>=N (kernel_stagger_set: workgroup
+start stagger of stream / block / rows28 / s2rows / stem / stream8 / conv1x1 /
+bottleneck kernels), comma-separated within a variant."""
 import argparse
 import os
 import statistics
@@ -28,13 +30,16 @@ from conv_bench import time_us, warm_gpu  # noqa: E402
 
 HOOKS = {"stream": "conv3x3_stream_set_variant", "stream8": "conv3x3_stream8_set_variant",
          "stem": "stem_conv_pool_set_dbg"}
+# workgroup start stagger per kernel family (kernels.h StaggerKernel): stag_<family>=N
+STAG = {"stag_stream": 0, "stag_block": 1, "stag_rows28": 2, "stag_s2rows": 3, "stag_stem": 4, "stag_stream8": 5,
+        "stag_conv1x1": 6, "stag_bottleneck": 7}
 
 
 def parse(spec):
     out = {}
     for kv in filter(None, spec.split(",")):
         k, v = kv.split("=")
-        if k not in HOOKS:
+        if k not in HOOKS and k not in STAG:
             raise SystemExit(f"unknown hook {k} (known: {', '.join(HOOKS)})")
         out[k] = int(v, 0)
     return out
@@ -60,12 +65,18 @@ def main():
     def run(spec):
         hooks = parse(spec)
         for k, v in hooks.items():
-            getattr(C, HOOKS[k])(v)
+            if k in STAG:
+                C.kernel_stagger_set(STAG[k], v)
+            else:
+                getattr(C, HOOKS[k])(v)
         try:
             return eng.predict(img, use_graph=False)
         finally:
             for k in hooks:
-                getattr(C, HOOKS[k])(0)
+                if k in STAG:
+                    C.kernel_stagger_set(STAG[k], -1)
+                else:
+                    getattr(C, HOOKS[k])(0)
 
     ref = [t.clone() for t in run("")]
     torch.cuda.synchronize()
