@@ -21,6 +21,7 @@
 //     pending and later operation with CommError.
 // One progress thread per communicator owns all its socket I/O (poll over the
 // peer connections and a wake-up pipe), so several threads may post.
+#include <cerrno>
 #include <arpa/inet.h>
 #include <fcntl.h>
 #include <netinet/in.h>
@@ -106,6 +107,7 @@ int accept_until(int lfd, Clock::time_point deadline) {
     const int r = poll(&p, 1, std::min(ms, 200));
     if (r > 0) {
       const int fd = accept4(lfd, nullptr, nullptr, SOCK_CLOEXEC);
+      if (fd < 0 && (errno == EINTR || errno == ECONNABORTED)) continue;
       if (fd < 0) sys_fail("accept");
       set_nodelay(fd);
       return fd;
@@ -119,6 +121,7 @@ void write_all(int fd, const void* p, size_t n) {
   const char* c = (const char*)p;
   while (n) {
     const ssize_t k = ::send(fd, c, n, MSG_NOSIGNAL);
+    if (k < 0 && errno == EINTR) continue;
     if (k <= 0) sys_fail("bootstrap send");
     c += k;
     n -= (size_t)k;
@@ -128,6 +131,7 @@ void read_all(int fd, void* p, size_t n) {
   char* c = (char*)p;
   while (n) {
     const ssize_t k = ::recv(fd, c, n, 0);
+    if (k < 0 && errno == EINTR) continue;
     if (k <= 0) throw CommError("socket comm: bootstrap peer closed");
     c += k;
     n -= (size_t)k;
@@ -297,7 +301,7 @@ class SocketWorld {
       Out& m = p.outq.front();
       if (m.hdr_done < sizeof(m.hdr)) {
         const ssize_t k = ::send(p.fd, (const char*)m.hdr + m.hdr_done, sizeof(m.hdr) - m.hdr_done, MSG_NOSIGNAL);
-        if (k < 0) return errno == EAGAIN || errno == EWOULDBLOCK;
+        if (k < 0) return errno == EAGAIN || errno == EWOULDBLOCK || errno == EINTR;
         m.hdr_done += (size_t)k;
         if (m.hdr_done < sizeof(m.hdr)) return true;
       }
@@ -305,7 +309,7 @@ class SocketWorld {
         const uint64_t n = m.data->bytes;
         while (m.body_done < n) {
           const ssize_t k = ::send(p.fd, (const char*)m.data->sbuf + m.body_done, n - m.body_done, MSG_NOSIGNAL);
-          if (k < 0) return errno == EAGAIN || errno == EWOULDBLOCK;
+          if (k < 0) return errno == EAGAIN || errno == EWOULDBLOCK || errno == EINTR;
           m.body_done += (size_t)k;
         }
         finish(m.data, "");
@@ -325,7 +329,7 @@ class SocketWorld {
           const size_t want = p.in_data ? n - p.in_body_done : std::min<uint64_t>(sizeof(sink), n - p.in_body_done);
           const ssize_t k = ::recv(p.fd, dst, want, 0);
           if (k == 0) return false;
-          if (k < 0) return errno == EAGAIN || errno == EWOULDBLOCK;
+          if (k < 0) return errno == EAGAIN || errno == EWOULDBLOCK || errno == EINTR;
           p.in_body_done += (size_t)k;
         }
         if (p.in_data) finish(p.in_data, "");
@@ -335,7 +339,7 @@ class SocketWorld {
       }
       const ssize_t k = ::recv(p.fd, (char*)p.in_hdr + p.in_hdr_done, sizeof(p.in_hdr) - p.in_hdr_done, 0);
       if (k == 0) return false;
-      if (k < 0) return errno == EAGAIN || errno == EWOULDBLOCK;
+      if (k < 0) return errno == EAGAIN || errno == EWOULDBLOCK || errno == EINTR;
       p.in_hdr_done += (size_t)k;
       if (p.in_hdr_done < sizeof(p.in_hdr)) continue;
       p.in_hdr_done = 0;
