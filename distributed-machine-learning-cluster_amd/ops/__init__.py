@@ -9,7 +9,6 @@ Layout conventions: activations are bf16 NHWC; conv/linear weights are packed
 """
 from __future__ import annotations
 
-import os
 
 import torch
 
@@ -115,11 +114,6 @@ def conv2d(x: torch.Tensor, w_packed: torch.Tensor, cout: int, kh: int, kw: int,
         bt_ws = _bigtile_ws(x.device, C.conv_bigtile_ws_bytes(slabs))
         bt_bytes = bt_ws.numel()
     ws = None
-    if tile >= C.CONV_BIGTILE0 and int(os.environ.get("DMLC_BT_DEBUG", "0")) & 32:
-        global BT_STAMPS  # per-workgroup phase stamps of the last launch (debug)
-        if BT_STAMPS is None:
-            BT_STAMPS = torch.zeros(1 << 16, dtype=torch.int64, device=x.device)
-        ws = BT_STAMPS
     if split_k > 1:
         ws = torch.empty(split_k * B * Ho * Wo * w_packed.shape[0], device=x.device, dtype=torch.float32)
     C.conv2d(x=_ptr(x.contiguous()), w=_ptr(w_packed), bias=_ptr(bias), res=_ptr(res), y=_ptr(out), B=B, H=H,
@@ -132,6 +126,15 @@ def conv2d(x: torch.Tensor, w_packed: torch.Tensor, cout: int, kh: int, kw: int,
 
 _BT_WS: dict = {}
 BT_STAMPS = None
+_PHASE_STAMPS = False
+
+
+def set_phase_stamps(on: bool) -> None:
+    """Record per-workgroup phase stamps (start / prologue / loop / epilogue,
+    100 MHz) of every following conv3x3_stream launch into BT_STAMPS (a
+    measurement hook for tools/conv_bench.py; off by default)."""
+    global _PHASE_STAMPS
+    _PHASE_STAMPS = bool(on)
 
 
 def _bigtile_ws(device: torch.device, nbytes: int) -> torch.Tensor:
@@ -330,7 +333,7 @@ def conv3x3_stream(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, 
         raise ValueError("conv3x3_stream: unsupported shape")
     y = torch.empty(B, H // stride, W // stride, Cout, dtype=x.dtype, device=x.device)
     stamps = 0
-    if int(os.environ.get("DMLC_BT_DEBUG", "0")) & 32:  # per-workgroup phase stamps (debug)
+    if _PHASE_STAMPS:  # per-workgroup phase stamps of the stream conv (tools/conv_bench.py --stamps)
         global BT_STAMPS
         if BT_STAMPS is None:
             BT_STAMPS = torch.zeros(1 << 16, dtype=torch.int64, device=x.device)

@@ -101,7 +101,9 @@ def main():
     ap.add_argument("--split", type=int, default=1, help="split-K factor (big-tile configs 11/12: K slices, 1 = auto)")
     ap.add_argument("--variants", default="0", help="register-weight stream conv variants to time (A/B hook)")
     ap.add_argument("--ref", action="store_true", help="also time hipBLASLt GEMM and MIOpen conv on each shape")
+    ap.add_argument("--stamps", action="store_true", help="per-workgroup phase stamps of the stream convs")
     a = ap.parse_args()
+    ops.set_phase_stamps(a.stamps)
     dev = torch.device("cuda", 0)
     B = a.batch
     tiles = [] if a.tiles == "none" else [int(t) for t in a.tiles.split(",")]
@@ -130,9 +132,6 @@ def main():
                                        split_k=(a.split if a.split != 1 else 0) if t in (11, 12) else a.split)
                 us = time_us(f, a.iters)
                 row.append(f"tile{t}={us:7.1f}us {flops/us/1e6:6.0f}TF")
-                if t >= 11 and ops.BT_STAMPS is not None:
-                    f()
-                    row.append(_stamps())
             except Exception as e:  # noqa: BLE001
                 row.append(f"tile{t}=ERR({e})")
         if name in ("l2", "l3", "l4", "l2.c1", "l3.c1", "l4.c1"):  # direct conv, streamed weights (conv3x3_stream.hip)
