@@ -122,6 +122,15 @@ PYBIND11_MODULE(_C, m) {
           conv1x1(a, prop.multiProcessorCount, S(stream));
           return;
         }
+        if (tile == kConv1x1Tile + 2) {  // fully connected (fc_gemm.hip); split_k 0: fc_gemm_splits
+          a.tile = -1;
+          hipDeviceProp_t prop;
+          int dev = 0;
+          DMLC_HIP_CHECK(hipGetDevice(&dev));
+          DMLC_HIP_CHECK(hipGetDeviceProperties(&prop, dev));
+          fc_gemm(a, split_k > 0 ? split_k : fc_gemm_splits(a, prop.multiProcessorCount), S(stream));
+          return;
+        }
         if (tile == kConv1x1Tile + 1) {  // support query only (no launch): raises if unsupported
           a.tile = -1;
           if (!conv1x1_supported(a)) throw std::invalid_argument("conv1x1: unsupported shape");
@@ -167,6 +176,14 @@ PYBIND11_MODULE(_C, m) {
       });
   m.attr("CONV_BIGTILE0") = kConvBigTile0;
   m.attr("CONV_1X1") = kConv1x1Tile;
+  m.attr("CONV_FC") = kConv1x1Tile + 2;
+  m.def("fc_gemm_splits", [](int M, int Kpad, int Npad, int num_cus) {
+    ConvArgs a;
+    a.B = M;
+    a.Kpad = Kpad;
+    a.Npad = Npad;
+    return fc_gemm_splits(a, num_cus);
+  });
   m.def("maxpool2d", [](uintptr_t x, uintptr_t y, int B, int H, int W, int C, int k, int stride,
                         int pad, uintptr_t stream) {
     maxpool2d(P<void>(x), P<void>(y), B, H, W, C, conv_out_dim(H, k, stride, pad),

@@ -738,11 +738,13 @@ void conv2d_igemm(const ConvArgs& a, hipStream_t s) {
     case 9: launch_cfg<128, 64, 2, 2, 3>(b, splits, kt_per, k_tiles, s); break;
     default: launch_cfg<64, 128, 2, 2, 3>(b, splits, kt_per, k_tiles, s); break;
   }
-  if (splits > 1) {
-    const int blocks = (int)std::min<long>((M * (a.N / 4) + 255) / 256, 4096);
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, s, b, (int)M, splits);
-    DMLC_HIP_CHECK(hipGetLastError());
-  }
+  if (splits > 1) splitk_reduce(b, M, splits, s);
+}
+
+void splitk_reduce(const ConvArgs& a, long M, int splits, hipStream_t s) {
+  const int blocks = (int)std::min<long>((M * (a.N / 4) + 255) / 256, 4096);
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, s, a, (int)M, splits);
+  DMLC_HIP_CHECK(hipGetLastError());
 }
 
 }  // namespace dmlc

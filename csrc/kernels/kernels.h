@@ -73,6 +73,15 @@ int conv_npad(int N);
 size_t conv_splitk_ws_elems(const ConvArgs& a);
 int conv_pick_split_k(const ConvArgs& a, int num_cus);
 void conv2d_igemm(const ConvArgs& a, hipStream_t s);
+// The split-K reduction (+ bias, residual, ReLU, bf16 / fp32 out) of `splits`
+// fp32 partial slices [splits][M][Npad] in a.ws.
+void splitk_reduce(const ConvArgs& a, long M, int splits, hipStream_t s);
+// Fully connected layers at M = B <= 256 (fc_gemm.hip): all rows x 128
+// columns x one K slice per workgroup, register-staged LDS tiles, fp32
+// partials reduced by splitk_reduce (so a.ws is required even at 1 slice).
+bool fc_gemm_supported(const ConvArgs& a);
+int fc_gemm_splits(const ConvArgs& a, int num_cus);  // K slices for ~one workgroup per CU
+void fc_gemm(const ConvArgs& a, int splits, hipStream_t s);
 
 // Big-tile conv (conv_bigtile.hip): 8-wave 256x256 (cfg 0, Npad % 256 == 0)
 // or 256x128 (cfg 1, Npad == 128) tiles, bf16 in/out, no stem/fp8, with an

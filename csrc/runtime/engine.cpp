@@ -93,6 +93,7 @@ bool EngineOptions::set(const std::string& name, bool v) {
       {"s2rows128", &EngineOptions::s2rows128},
       {"rows28", &EngineOptions::rows28},           {"stem_roles", &EngineOptions::stem_roles},
       {"stem_dense", &EngineOptions::stem_dense},
+      {"fc_gemm", &EngineOptions::fc_gemm},
       {"igemm_small_m", &EngineOptions::igemm_small_m},
       {"small_conv", &EngineOptions::small_conv},
   };
@@ -933,6 +934,10 @@ Engine::ConvPath Engine::conv_path(const Op& op, int B) const {
     a.split_k = 1;
     if (conv1x1_supported(a)) return ConvPath::OneByOne;
   }
+  if (opt_.fc_gemm && L.fc && !L.fp8) {
+    const ConvArgs a = conv_args(op, B, nullptr);
+    if (fc_gemm_supported(a) && (size_t)B * L.npad <= ws_elems_) return ConvPath::Fc;
+  }
   if (opt_.bigtile && conv_bigtile_pick(conv_args(op, B, nullptr), num_cus_) >= 0) return ConvPath::BigTile;
   return ConvPath::Igemm;
 }
@@ -1400,6 +1405,19 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
             ConvArgs a = conv_args(op, B, logits);
             if (cs != s) a.split_k = 1;  // the split-K workspace belongs to the main stream
             conv2d_igemm(a, cs);
+            break;
+          }
+          case ConvPath::Fc: {
+            ConvArgs a = conv_args(op, B, logits);
+            if (cs != s) {  // (its partials need the main stream's split-K workspace)
+              a.split_k = 1;
+              conv2d_igemm(a, cs);
+              break;
+            }
+            int sp = fc_gemm_splits(a, num_cus_);
+            while (sp > 1 && ((size_t)sp * B * a.Npad > ws_elems_ || (a.Kpad / 64) % sp)) --sp;
+            a.ws = ws_;
+            fc_gemm(a, sp, cs);
             break;
           }
         }

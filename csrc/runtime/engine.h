@@ -110,6 +110,7 @@ struct EngineOptions {
                                  // walking its rows (conv3x3_s2rows.hip), B >= 0.7 x CUs
   bool rows28 = true;            // layer2's stride-1 convs the same way (conv3x3_rows28.hip), B >= 0.7 x CUs
   bool stem_roles = true;        // u8 stem: one workgroup per image with MFMA / helper waves once B >= CUs
+  bool fc_gemm = true;           // fully connected layers at B <= 256 on fc_gemm.hip (else the implicit GEMM)
   bool stem_dense = true;        // ... with the dense-K weight order (5 K steps a fragment instead of 7)
   bool bigtile = true;           // 8-wave big-tile split-K convs where picked (not on the ResNet18 b256 path)
   bool conv1x1 = true;           // weight-stationary 1x1 convs (conv1x1.hip: ResNet50 bottlenecks)
@@ -231,7 +232,7 @@ class Engine {
   void run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* idx, float* prob,
                float* logits, hipStream_t s, std::vector<hipEvent_t>* evs, bool trace);
   ConvArgs conv_args(const Op& op, int B, float* logits) const;
-  enum class ConvPath { Stream, Rows, Rows28, Direct13, Direct27, OneByOne, BigTile, Igemm, Small, Stream8 };
+  enum class ConvPath { Stream, Rows, Rows28, Direct13, Direct27, OneByOne, BigTile, Igemm, Small, Stream8, Fc };
   ConvPath conv_path(const Op& op, int B) const;
   bool side_safe(int B) const;
   bool head_fusable(size_t oi) const;

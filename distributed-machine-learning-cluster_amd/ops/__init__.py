@@ -81,11 +81,29 @@ def stem_image(x_nhwc3: torch.Tensor, pad: int, row_width: int) -> torch.Tensor:
     return out.contiguous()
 
 
+def fc(x: torch.Tensor, w_packed: torch.Tensor, cout: int, bias: torch.Tensor | None = None, relu: bool = False,
+       out_f32: bool = False, splits: int = 0) -> torch.Tensor:
+    """Fully connected layer at M <= 256 rows on fc_gemm.hip: x bf16 [M, K]
+    (K = w_packed.shape[1], a multiple of 64), w_packed [Npad, K] (Npad % 128
+    == 0) -> [M, cout] bf16 (fp32 with out_f32). splits: K slices (0: the
+    engine's choice), fp32 partials reduced with the bias and ReLU."""
+    _need_cuda(x, w_packed, bias)
+    C = native()
+    M, K = x.shape
+    if K != w_packed.shape[1]:
+        raise ValueError("fc: x's K must equal the packed weight's K")
+    if splits <= 0:
+        splits = C.fc_gemm_splits(M, K, w_packed.shape[0], torch.cuda.get_device_properties(x.device).multi_processor_count)
+    ws = torch.empty(splits * M * w_packed.shape[0], device=x.device, dtype=torch.float32)
+    return conv2d(x.contiguous().view(M, 1, 1, K), w_packed, cout, 1, 1, bias=bias, relu=relu, out_f32=out_f32,
+                  split_k=splits, tile=C.CONV_FC, ws=ws).view(M, cout)
+
+
 def conv2d(x: torch.Tensor, w_packed: torch.Tensor, cout: int, kh: int, kw: int, stride: int = 1,
            pad: int = 0, bias: torch.Tensor | None = None, res: torch.Tensor | None = None,
            relu: bool = False, out_f32: bool = False, split_k: int = 1, tile: int = -1,
            out: torch.Tensor | None = None, stem: bool = False, out_hw: tuple | None = None,
-           max_blocks: int = 0) -> torch.Tensor:
+           max_blocks: int = 0, ws: torch.Tensor | None = None) -> torch.Tensor:
     """Implicit-GEMM conv on MFMA. x: bf16 NHWC [B,H,W,Cin] (Cin % 64 == 0),
     or with ``stem`` the padded packed RGB image (``stem_image``) plus the
     output size ``out_hw`` (the padding is already in the image).
@@ -113,8 +131,7 @@ def conv2d(x: torch.Tensor, w_packed: torch.Tensor, cout: int, kh: int, kw: int,
         slabs = -(-B * Ho * Wo // bm) * (w_packed.shape[0] // bn) * (bt_splits - 1)
         bt_ws = _bigtile_ws(x.device, C.conv_bigtile_ws_bytes(slabs))
         bt_bytes = bt_ws.numel()
-    ws = None
-    if split_k > 1:
+    if ws is None and split_k > 1:
         ws = torch.empty(split_k * B * Ho * Wo * w_packed.shape[0], device=x.device, dtype=torch.float32)
     C.conv2d(x=_ptr(x.contiguous()), w=_ptr(w_packed), bias=_ptr(bias), res=_ptr(res), y=_ptr(out), B=B, H=H,
              W=W, Cin=Cin, KH=kh, KW=kw, stride=stride, pad=pad, N=cout, Npad=w_packed.shape[0],

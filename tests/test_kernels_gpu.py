@@ -435,6 +435,29 @@ def test_conv3x3_rows(gpu, B, strip, res):
     assert torch.equal(y2, y)
 
 
+@pytest.mark.parametrize("M,K,N,relu,f32,splits", [(256, 9216, 4096, True, False, 0), (256, 4096, 4096, True, False, 0),
+                                                   (256, 4096, 1000, False, True, 0), (3, 9216, 4096, True, False, 0),
+                                                   (200, 1024, 256, True, False, 1), (64, 4096, 1000, False, True, 4)])
+def test_fc_gemm(gpu, M, K, N, relu, f32, splits):
+    """Fully connected layers on fc_gemm.hip (AlexNet's classifier shapes at
+    B = 256, a query batch, a ragged M, one and several K slices) vs torch
+    fp32 on the same bf16 operands; the zero-page rows past M stay out of
+    the result."""
+    g = torch.Generator().manual_seed(41)
+    x = torch.randn(M, K, generator=g).bfloat16().float()
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).bfloat16().float()
+    b = torch.randn(N, generator=g) * 0.1
+    ref = x @ w.t() + b
+    if relu:
+        ref = F.relu(ref)
+    wp = ops.pack_conv_weight(w.view(N, K, 1, 1), device=gpu)
+    assert wp.shape[1] == K and wp.shape[0] % 128 == 0
+    y = ops.fc(x.bfloat16().to(gpu), wp, N, bias=b.to(gpu), relu=relu, out_f32=f32, splits=splits)
+    torch.cuda.synchronize()
+    assert y.shape == (M, N) and y.dtype == (torch.float32 if f32 else torch.bfloat16)
+    assert _rel(y.float().cpu(), ref) < 5e-3, _rel(y.float().cpu(), ref)
+
+
 @pytest.mark.parametrize("B", [1, 3])
 def test_conv3x3_block(gpu, B):
     """Fused layer1 basic block (conv3x3_block.hip: conv1 producer waves ->
