@@ -305,14 +305,37 @@ void kernel_stagger_for_lanes(int lanes);
 void stem_conv_pool_u8(const uint8_t* x, const void* w, const float* bias, void* y, int B, int S, int strip,
                        hipStream_t s, const void* w_dense = nullptr);
 constexpr int kStemDenseK = 160;
-// dense-K slot of tap (dy, dx, c) of the 7x7x3 stem: K index k holds dword
-// D = 16 (k / 32) + 4 ((k % 8) / 2) + (k % 32) / 8 of the kernel rows' 22-element
-// windows (7 px x rgb + 1 pad) concatenated, element 2 D + k % 2. Returns the
-// k of element (dy, 3 dx + c).
+// Dense-K stem operand map. A kernel row's window is 22 bf16 (7 px x rgb + 1
+// zero-weight slot) = 11 dwords u; K index k = 32 s + 8 fq + 2 i + h is
+// element h of the dword that lane group fq reads in dword slot j = 4 s + i
+// (K step s). Each slot pairs, in each 32-lane half (fq 0/1, fq 2/3), the same
+// dword u of an even and an odd kernel row, which the kernel places 16 banks
+// apart (stem_pool.hip): 18 of the 20 ds_read_b32 slots are bank-conflict
+// free (the 7th row has no odd partner; 3 of its dwords take the zero-weight
+// pad slots' partners, the other 8 pair up in slots 18 and 19). Slots 0..14:
+// row pair (2 (j / 5), 2 (j / 5) + 1), dwords 2 (j % 5) + (fq >> 1); 15..19:
+// the u = 10 dwords of rows 0..5, then row 6 (against row 5 under zero
+// weights for u = 0..2).
+struct StemDenseCell {
+  int dy, u;
+  bool pad;  // zero weights (reads a real dword)
+};
+constexpr StemDenseCell stem_dense_cell(int j, int fq) {
+  if (j < 15) return {2 * (j / 5) + (fq & 1), 2 * (j % 5) + (fq >> 1), false};
+  const int hp = 2 * (j - 15) + (fq >> 1), m = fq & 1;
+  if (hp < 3) return {2 * hp + m, 10, false};
+  if (hp < 6) return {m ? 5 : 6, hp - 3, m == 1};
+  return {6, 3 + 2 * (hp - 6) + m, false};
+}
+// the K index of tap (dy, dx, c) (element 3 dx + c of kernel row dy's window)
 inline int stem_dense_k_index(int dy, int dx, int c) {
-  const int E = 22 * dy + 3 * dx + c, D = E / 2, h = E % 2;
-  const int s = D / 16, i = (D % 16) / 4, fq = D % 4;
-  return 32 * s + 8 * fq + 2 * i + h;
+  const int e = 3 * dx + c, u = e / 2, h = e % 2;
+  for (int j = 0; j < 20; ++j)
+    for (int fq = 0; fq < 4; ++fq) {
+      const StemDenseCell cell = stem_dense_cell(j, fq);
+      if (!cell.pad && cell.dy == dy && cell.u == u) return 32 * (j / 4) + 8 * fq + 2 * (j % 4) + h;
+    }
+  return -1;
 }
 // AlexNet features.0-2 fused (alex_stem.hip): u8 [B, 224, 224, 3] ->
 // normalise -> conv 11x11/s4/p2 + bias -> ReLU -> maxpool 3x3/s2 ->

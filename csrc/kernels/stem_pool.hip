@@ -115,6 +115,10 @@ __device__ __forceinline__ void ds_write_hi16(uint32_t addr, uint32_t v, const i
   asm volatile("ds_write_b16_d16_hi %0, %1 offset:%2" ::"v"(addr), "v"(v), "i"(off));
 }
 
+__device__ __forceinline__ void ds_write32(uint32_t addr, uint32_t v, const int off) {
+  asm volatile("ds_write_b32 %0, %1 offset:%2" ::"v"(addr), "v"(v), "i"(off));
+}
+
 __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -149,9 +153,19 @@ __device__ __forceinline__ float rot_rows_down1(float x, int lane) {
 // 89.6 vs 90.9 us for the role-split stem at B = 256 against the fp32 max +
 // bias-add epilogue (profiles/r4_stem_roles.txt).
 
-template <int NB>
+//
+// PAIR: channel pairs as 32-bit stores, one per block instead of two 16-bit
+// ones (LDS store cycles are per instruction): lanes fr and fr ^ 1 swap
+// their packed pair (DPP quad_perm [1,0,3,2]); the even lane stores channels
+// (fr, fr + 1) of the first pooled column, the odd one channels (fr - 1, fr)
+// of the second. hbase is then the pair base (hpool_pair_base), psel the
+// lane's v_perm selector (hpool_pair_sel).
+__device__ __forceinline__ uint32_t hpool_pair_sel(int fr) { return (fr & 1) ? 0x03020706u : 0x05040100u; }
+
+template <int NB, bool PAIR = false>
 __device__ __forceinline__ void hpool_packed(const floatx4 (&acc)[NB], uint32_t (&prevq)[(NB + 1) / 2], int lane,
-                                             int fq, uint32_t hbase, const int f, const int off) {
+                                             int fq, uint32_t hbase, const int f, const int off,
+                                             uint32_t psel = 0) {
   uint32_t p01[NB], p23[NB];
 #pragma unroll
   for (int n = 0; n < NB; ++n) {  // (no ReLU yet: see below)
@@ -190,8 +204,13 @@ __device__ __forceinline__ void hpool_packed(const floatx4 (&acc)[NB], uint32_t 
             __builtin_bit_cast(short2v, c)),
         short2v{0, 0});
     const uint32_t packed = __builtin_bit_cast(uint32_t, m);
-    ds_write_lo16(hbase, packed, off + n * 32);
-    ds_write_hi16(hbase, packed, off + n * 32 + kHpCol);
+    if constexpr (PAIR) {
+      const uint32_t other = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)packed, 0xB1, 0xF, 0xF, false);
+      ds_write32(hbase, __builtin_amdgcn_perm(other, packed, psel), off + n * 32);
+    } else {
+      ds_write_lo16(hbase, packed, off + n * 32);
+      ds_write_hi16(hbase, packed, off + n * 32 + kHpCol);
+    }
   }
 }
 
@@ -478,13 +497,17 @@ __device__ __forceinline__ void vm_wait_dyn(int n) {
 // taps (66% of the MFMAs useful). Dense rows hold the padded row as plain
 // [px][rgb] bf16 (3 * (S + 6) elements, 48 B per 8 pixels: helper stores at
 // a 48-B lane stride, conflict-free), and K runs over the 7 kernel rows'
-// 22-element windows (7 px x rgb + 1 zero-weight slot) concatenated: 154 of
-// 160 = 5 K steps, 20 MFMAs a fragment instead of 28. Lane (fr, fq) of K
-// step s holds dword D = 16 s + 4 i + fq (i = 0..3) of that concatenation:
-// kernel row D / 11, window dword D % 11, so each operand is four
-// ds_read_b32 at per-lane addresses computed once per conv row (a dword
-// never straddles two rows; 6 of the 20 dword slots put some lanes in the
-// next row). Weights: stem_dense_k_index (kernels.h), [64][160].
+// 22-element windows (7 px x rgb + 1 zero-weight slot): 154 of 160 = 5 K
+// steps, 20 MFMAs a fragment instead of 28. Each operand is four ds_read_b32
+// (one window dword each) at per-lane addresses computed once per conv row;
+// which dword a lane group reads in which slot is stem_dense_cell
+// (kernels.h): in every 32-lane half the same dword of an even and an odd
+// kernel row, and odd rows sit 64 B (16 banks) further into their ring slot
+// (slots a multiple of 128 B), so the two halves' 3 fr + u dword patterns
+// never share a bank (18 of 20 slots; a lane pattern over one bank window
+// costs the ds_read_b32 2 cycles a half-wave instead of 1). The pooling
+// epilogue stores channel pairs (hpool_packed<.., true>). Weights:
+// stem_dense_k_index (kernels.h), [64][160].
 template <int NF, int V = 0>
 __global__ __launch_bounds__(512, 1) void stem_roles_kernel(StemArgs a) {
   using G = StemGeom<NF>;
@@ -493,13 +516,19 @@ __global__ __launch_bounds__(512, 1) void stem_roles_kernel(StemArgs a) {
   constexpr int NG = 4 * NF + 1;      // dense rows: 8-pixel groups of the S + 6 padded pixels
   static_assert(NG * 8 >= G::S + 6, "dense row groups");
   constexpr int RB = DK ? NG * 48 : G::Wq * 16;  // bytes per paired / dense row
-  static_assert(!DK || 12 * (16 * NF - 1) + 4 * 13 + 4 <= RB, "dense window reads stay in the row");
+  // ring slot stride: dense slots a multiple of 128 B with room for the odd
+  // rows' 64-B offset (within the paired rows' LDS budget of the launcher)
+  constexpr int RBS = DK ? (RB + 64 + 127) / 128 * 128 : RB;
+  static_assert(RBS <= G::Wq * 16, "dense ring within the launcher's LDS budget");
+  static_assert(!DK || 12 * (16 * NF - 1) + 4 * 10 + 4 <= RB, "dense window reads stay in the row");
   constexpr int UB = G::S * 3;        // bytes per raw image row
   constexpr int UBS = UB + kU8Pad;    // raw ring slot
   constexpr int HPB = G::PW * kHpCol;  // bytes per horizontally pooled conv row
   constexpr int T = G::PH / 2;
   char* ring = (char*)smem;
-  char* hp = ring + kRolesPairRing * RB;
+  char* hp = ring + kRolesPairRing * RBS;
+  // byte offset of padded row r (>= 0) in the paired / dense ring
+  auto row_off = [](int r) __attribute__((always_inline)) { return (r % kRolesPairRing) * RBS + (DK ? 64 * (r & 1) : 0); };
   char* u8ring = hp + kRolesHpRing * HPB;
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -557,7 +586,7 @@ __global__ __launch_bounds__(512, 1) void stem_roles_kernel(StemArgs a) {
             v[3 * i + c] = in ? imagenet_norm(c, cv) : 0.f;
           }
         }
-        char* drow = ring + (r % kRolesPairRing) * RB + g * 48;
+        char* drow = ring + row_off(r) + g * 48;
 #pragma unroll
         for (int q = 0; q < 3; ++q) *(uint4*)(drow + q * 16) = pack8(v + 8 * q);
       }
@@ -589,7 +618,7 @@ __global__ __launch_bounds__(512, 1) void stem_roles_kernel(StemArgs a) {
           v[8 * (i >> 1) + 3 * (i & 1) + c] = in ? nv : 0.f;
         }
       }
-      char* drow = ring + (r % kRolesPairRing) * RB;
+      char* drow = ring + row_off(r);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         v[8 * q + 6] = v[8 * q + 7] = 0.f;
@@ -634,37 +663,41 @@ __global__ __launch_bounds__(512, 1) void stem_roles_kernel(StemArgs a) {
           if (wave == 3)
             for (int o = lane * 16; o < HPB; o += 64 * 16) *(uint4*)(hrow + o) = make_uint4(0, 0, 0, 0);
         } else if constexpr (DK) {
-          // per-lane operand addresses of this conv row: dword slot j = 4 s + i
-          // holds concatenated dword D = 4 j + fq (kernel row D / 11); fragment
-          // f adds 16 * 12 * f bytes (an immediate)
-          int sl[7];
+          // per-lane operand addresses of this conv row (stem_dense_cell):
+          // slots 0..14 from one base per kernel-row pair plus an immediate,
+          // 15..19 one register each; fragment f adds 16 * 12 * f bytes
+          // (wave-uniform slot bases as separate values, not an array: a
+          // lane-selected index into one would go through scratch)
+          const int lane_off = 12 * fr;
+          auto cell_off = [&](int j, int c) __attribute__((always_inline)) {
+            const StemDenseCell cell = stem_dense_cell(j, c);
+            return row_off(2 * cr + cell.dy) + 4 * cell.u;
+          };
+          int ad[8];
 #pragma unroll
-          for (int dy = 0; dy < 7; ++dy) sl[dy] = ((2 * cr + dy) % kRolesPairRing) * RB;
-          const int lane_off = 12 * fr + 4 * fq;
-          int ad[20];
+          for (int rp = 0; rp < 3; ++rp)
+            ad[rp] = lane_off + 4 * (fq >> 1) + ((fq & 1) ? row_off(2 * cr + 2 * rp + 1) : row_off(2 * cr + 2 * rp));
 #pragma unroll
-          for (int j = 0; j < 20; ++j) {
-            const int dy0 = (4 * j) / 11, d0 = (4 * j) % 11, t = 11 - d0;
-            // (j = 19: dwords 77..79 are zero-weight slots: they read on in
-            // kernel row 6, finite data inside the row)
-            if (t >= 4 || j == 19)
-              ad[j] = lane_off + sl[dy0] + 4 * d0;
-            else
-              ad[j] = lane_off + (fq < t ? sl[dy0] + 4 * d0 : sl[dy0 + 1] - 4 * t);
+          for (int q = 0; q < 5; ++q) {
+            const int v0 = cell_off(15 + q, 0), v1 = cell_off(15 + q, 1), v2 = cell_off(15 + q, 2),
+                      v3 = cell_off(15 + q, 3);
+            ad[3 + q] = lane_off + (fq == 0 ? v0 : fq == 1 ? v1 : fq == 2 ? v2 : v3);
           }
-          const uint32_t hbase = lds_addr(hrow) + fq * 2 * kHpCol + (fr >> 3) * 16 + (fr & 7) * 2;
+          const uint32_t hbase =
+              lds_addr(hrow) + fq * 2 * kHpCol + (fr >> 3) * 16 + (fr & 6) * 2 + (fr & 1) * kHpCol;
+          const uint32_t psel = hpool_pair_sel(fr);
           uint32_t prevq[2];
           using u32x4 = uint32_t __attribute__((ext_vector_type(4)));
-          // opaque per-slot addresses: one base register each, so the loads
-          // are not merged into ds_read2 pairs across K steps / fragments
-          // (which land in the wrong registers and cost moves)
+          // opaque bases, so the compiler does not re-derive (and re-merge)
+          // the addresses across K steps / fragments
 #pragma unroll
-          for (int j = 0; j < 20; ++j) asm volatile("" : "+v"(ad[j]));
+          for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(ad[j]));
+          auto slot = [&](int j) __attribute__((always_inline)) { return j < 15 ? ad[j / 5] + 8 * (j % 5) : ad[j - 12]; };
           u32x4 xq[KS], nx[KS];
 #pragma unroll
           for (int s = 0; s < KS; ++s)
 #pragma unroll
-            for (int i = 0; i < 4; ++i) xq[s][i] = *(const uint32_t*)(ring + ad[4 * s + i]);
+            for (int i = 0; i < 4; ++i) xq[s][i] = *(const uint32_t*)(ring + slot(4 * s + i));
           // Software pipeline, one scheduling region per fragment f: the
           // operand loads of f + 1, the MFMAs of f, and the pooling epilogue of
           // f - 1 (its accumulators long complete: no hazard waits, its VALU
@@ -676,7 +709,7 @@ __global__ __launch_bounds__(512, 1) void stem_roles_kernel(StemArgs a) {
 #pragma unroll
               for (int s = 0; s < KS; ++s)
 #pragma unroll
-                for (int i = 0; i < 4; ++i) nx[s][i] = *(const uint32_t*)(ring + ad[4 * s + i] + (f + 1) * 192);
+                for (int i = 0; i < 4; ++i) nx[s][i] = *(const uint32_t*)(ring + slot(4 * s + i) + (f + 1) * 192);
             }
             if (f < NF) {
 #pragma unroll
@@ -689,7 +722,7 @@ __global__ __launch_bounds__(512, 1) void stem_roles_kernel(StemArgs a) {
                                                                           wf[n][s], acc[f & 1][n], 0, 0, 0);
             }
             if (f > 0) {
-              hpool_packed<4>(acc[(f - 1) & 1], prevq, lane, fq, hbase, f - 1, (f - 1) * 8 * kHpCol);
+              hpool_packed<4, true>(acc[(f - 1) & 1], prevq, lane, fq, hbase, f - 1, (f - 1) * 8 * kHpCol, psel);
             }
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -699,7 +732,7 @@ __global__ __launch_bounds__(512, 1) void stem_roles_kernel(StemArgs a) {
           const char* rbase = ring + (fr + fq) * 16;
           int rows[7];
 #pragma unroll
-          for (int s = 0; s < 7; ++s) rows[s] = ((2 * cr + s) % kRolesPairRing) * RB;
+          for (int s = 0; s < 7; ++s) rows[s] = row_off(2 * cr + s);
           const uint32_t hbase = lds_addr(hrow) + fq * 2 * kHpCol + (fr >> 3) * 16 + (fr & 7) * 2;
           uint32_t prevq[2];  // v3 of the previous fragment's row 3, as bf16 pairs
           bf16x8 xf[7];

@@ -544,23 +544,40 @@ def pack_stem_pool_weight(w: torch.Tensor, scale: torch.Tensor | None = None, de
     return out.to(device) if device is not None else out
 
 
+def stem_dense_cell(j: int, fq: int) -> tuple[int, int, bool]:
+    """(kernel row dy, window dword u, zero-weight pad) that lane group fq
+    reads in dword slot j of the dense-K stem: kernels.h stem_dense_cell."""
+    if j < 15:
+        return 2 * (j // 5) + (fq & 1), 2 * (j % 5) + (fq >> 1), False
+    hp, m = 2 * (j - 15) + (fq >> 1), fq & 1
+    if hp < 3:
+        return 2 * hp + m, 10, False
+    if hp < 6:
+        return (5 if m else 6), hp - 3, m == 1
+    return 6, 3 + 2 * (hp - 6) + m, False
+
+
 def pack_stem_dense_weight(w: torch.Tensor, scale: torch.Tensor | None = None, device=None) -> torch.Tensor:
     """[64, 3, 7, 7] fp32 -> bf16 [64, 160] in the dense-K order of the
-    one-image-per-workgroup stem (stem_pool.hip V & 2): the 7 kernel rows'
-    22-element windows (kw-major rgb + 1 zero slot) concatenated as dwords D,
-    K index k = 32 s + 8 fq + 2 i + h for element 2 D + h, D = 16 s + 4 i + fq."""
+    one-image-per-workgroup stem (stem_pool.hip V & 2): K index k = 32 s +
+    8 fq + 2 i + h holds element 2 u + h of kernel row dy's 22-element window
+    (kw-major rgb + 1 zero slot), (dy, u) = stem_dense_cell(4 s + i, fq);
+    pad slots and element 21 are zero."""
     cout, cin, kh, kw = w.shape
     if (cout, cin, kh, kw) != (64, 3, 7, 7):
         raise ValueError("stem_conv_pool packs a [64, 3, 7, 7] weight")
     w = w.float()
     if scale is not None:
         w = w * scale.float().view(-1, 1, 1, 1)
-    cat = torch.zeros(64, 7, 22)
-    cat[:, :, :21] = w.permute(0, 2, 3, 1).reshape(64, 7, 21)  # [n, kh, kw*3 + c]
-    cat = torch.cat([cat.reshape(64, 154), torch.zeros(64, 6)], 1)  # element E = 2 D + h
-    k = torch.arange(160)
-    D = 16 * (k // 32) + 4 * ((k % 8) // 2) + (k % 32) // 8
-    out = cat[:, 2 * D + k % 2].to(torch.bfloat16)
+    win = torch.zeros(64, 7, 22)
+    win[:, :, :21] = w.permute(0, 2, 3, 1).reshape(64, 7, 21)  # [n, kh, kw*3 + c]
+    out = torch.zeros(64, 160)
+    for k in range(160):
+        s, fq, i, h = k // 32, (k % 32) // 8, (k % 8) // 2, k % 2
+        dy, u, pad = stem_dense_cell(4 * s + i, fq)
+        if not pad:
+            out[:, k] = win[:, dy, 2 * u + h]
+    out = out.to(torch.bfloat16)
     return out.to(device) if device is not None else out
 
 

@@ -760,32 +760,44 @@ def test_stem_convert_store_layout():
     assert worst <= 4, worst
 
 
+def _dense_rbs(RB):
+    """stem_pool.hip dense ring slot stride: a multiple of 128 B with room for
+    the odd rows' 64-B offset."""
+    return (RB + 64 + 127) // 128 * 128
+
+
 def _dense_stem_addr(fr, fq, j, RB=1392):
     """stem_pool.hip dense-K operand address of lane (fr, fq), dword slot j
-    (= 4 s + i), fragment 0, with kernel row dy's slot at dy * RB (the ring
-    only moves the slot bases)."""
-    dy0, d0 = (4 * j) // 11, (4 * j) % 11
-    t = 11 - d0
-    lane_off = 12 * fr + 4 * fq
-    if t >= 4 or j == 19:
-        return lane_off + dy0 * RB + 4 * d0
-    return lane_off + (dy0 * RB + 4 * d0 if fq < t else (dy0 + 1) * RB - 4 * t)
+    (= 4 s + i), fragment 0, with kernel row dy in ring slot dy (the ring only
+    moves the slot bases by multiples of 128 B; conv row 0, so the absolute
+    row's parity is dy's): slot dy * RBS, odd rows 64 B further, window dword
+    u of output column fr at 12 fr + 4 u (kernels.h stem_dense_cell)."""
+    dy, u, _ = ops.stem_dense_cell(j, fq)
+    return dy * _dense_rbs(RB) + 64 * (dy & 1) + 12 * fr + 4 * u
 
 
 @pytest.mark.parametrize("S", [128, 224, 256])
 def test_stem_dense_layout(S):
     """Dense-K stem (stem_pool.hip stem_roles_kernel V & 2): the dense row
     holds padded pixel p (image column p - 3) channel c at element 3p + c;
-    every operand dword a lane reads is the pair of window elements its K
-    slots name (kernel row D / 11, elements 2 (D % 11), +1 of output column
-    ox's 22-element window starting at element 6 ox), zero-weight slots read
-    inside the row, and the weight order (pack_stem_dense_weight, the
-    engine's stem_dense_k_index) puts tap (dy, dx, c) at that K."""
+    stem_dense_cell covers every (kernel row, window dword) exactly once plus
+    3 zero-weight pads, every operand dword a lane reads is the pair of window
+    elements its K slots name (elements 2u, 2u + 1 of output column ox's
+    window starting at element 6 ox), inside the row, and the weight order
+    (pack_stem_dense_weight, the engine's stem_dense_k_index) puts tap
+    (dy, dx, c) at that K."""
     NF = S // 32
     NG = 4 * NF + 1
     RB = NG * 48
+    RBS = _dense_rbs(RB)
+    Wq = (((max(S + 6, ((S // 2 - 1) * 6 + 26) // 3)) + 7) // 8 * 8) // 2
+    assert RBS <= Wq * 16  # the launcher's LDS budget (paired rows)
     Ho = S // 2
     assert NG * 8 >= S + 6
+    cells = [ops.stem_dense_cell(j, fq) for j in range(20) for fq in range(4)]
+    real = [(dy, u) for dy, u, pad in cells if not pad]
+    assert sorted(real) == [(dy, u) for dy in range(7) for u in range(11)]
+    assert sum(pad for _, _, pad in cells) == 3
     g = torch.Generator().manual_seed(3)
     w = torch.randn(64, 3, 7, 7, generator=g)
     wd = ops.pack_stem_dense_weight(w).float()
@@ -794,10 +806,9 @@ def test_stem_dense_layout(S):
     seen = set()
     for k in range(160):
         s, fq, i, h = k // 32, (k % 32) // 8, (k % 8) // 2, k % 2
-        D = 16 * s + 4 * i + fq
-        E = 2 * D + h
-        dy, e = E // 22, E % 22
-        if D >= 77 or e == 21:
+        dy, u, pad = ops.stem_dense_cell(4 * s + i, fq)
+        e = 2 * u + h
+        if pad or e == 21:
             assert wd[:, k].abs().max() == 0
             continue
         dx, c = e // 3, e % 3
@@ -811,28 +822,36 @@ def test_stem_dense_layout(S):
             for fq in range(4):
                 for j in range(20):
                     a = _dense_stem_addr(fr, fq, j, RB) + 192 * f
-                    row, off = divmod(a, RB)
-                    D = 4 * j + fq
+                    row, off = divmod(a, RBS)
+                    off -= 64 * (row & 1)
+                    dy, u, _ = ops.stem_dense_cell(j, fq)
                     assert 0 <= off and off + 4 <= RB and a % 4 == 0
-                    if D >= 77:
-                        assert row == 6
-                        continue
-                    assert row == D // 11 and off // 2 == 6 * ox + 2 * (D % 11)
+                    assert row == dy and off // 2 == 6 * ox + 2 * u
     assert 6 * (Ho - 1) + 21 < 3 * (S + 6) <= NG * 24
 
 
 def test_stem_dense_lds_conflicts():
-    """Dense-K stem LDS traffic: the helpers' conversion stores (lane =
-    8-pixel group g: three 16-B stores at 48 g + 16 q) and the MFMA waves'
-    operand reads (ds_read_b32, every dword slot) are bank-conflict free:
-    the 48-B lane stride puts 16 lanes on 16 distinct 4-bank groups, and the
-    operand dwords of a slot are 3 fr + fq + const (overlapping windows: equal
-    addresses broadcast) -- 1-way except the slots that straddle two kernel
-    rows, pinned at 2-way."""
+    """Dense-K stem LDS traffic. The helpers' conversion stores (lane =
+    8-pixel group g: three 16-B stores at 48 g + 16 q of its row; ds_write_b128,
+    8-lane groups over 32 banks) are conflict free within a row and at most
+    2-way in the groups that cross into an odd row (8 + 1 LDS-array cycles
+    under the store's ~13-cycle data transfer: no cost). The MFMA waves' operand
+    reads (ds_read_b32: lanes 0-31 and 32-63 each one LDS cycle over 32 banks,
+    bank (a/4) mod 32) are conflict free in 18 of the 20 dword slots: each half
+    pairs dword u of an even and an odd kernel row, 16 banks apart, against
+    the 3 fr + u lane pattern; slots 18, 19 (row 6 against itself) are 2-way.
+    The pooling epilogue's channel-pair stores (ds_write_b32, 2 x 32 lanes)
+    are at most 2-way, which costs a 32-bit store nothing (its data transfer
+    takes the 2 cycles), and cover every (pooled column, channel) of a
+    fragment once."""
+    RB, RBS = 1392, _dense_rbs(1392)
     worst = 1
     for t0 in range(0, 8 * 29, 64):
         for q in range(3):
-            addr = [48 * ((t0 + l) % 29) + 16 * q + 1392 * ((t0 + l) // 29) for l in range(64)]
+            addr = []
+            for l in range(64):
+                r, g = divmod(t0 + l, 29)
+                addr.append((r % 21) * RBS + 64 * (r & 1) + 48 * g + 16 * q)
             worst = max(worst, _b128_ways(addr))
             for grp in [list(range(i, i + 8)) for i in range(0, 64, 8)]:  # 8-lane write groups, 32 banks
                 banks = {}
@@ -840,18 +859,31 @@ def test_stem_dense_lds_conflicts():
                     for b in range(addr[l] // 4, addr[l] // 4 + 4):
                         banks.setdefault(b % 32, set()).add(addr[l])
                 worst = max(worst, max(len(v) for v in banks.values()))
-    assert worst == 1
+    assert worst <= 2
     ways = []
     for j in range(20):
+        w = 1
+        for half in (range(0, 32), range(32, 64)):
+            banks = {}
+            for l in half:
+                a = _dense_stem_addr(l & 15, l >> 4, j, RB) + 192 * 3
+                banks.setdefault((a // 4) % 32, set()).add(a)
+            w = max(w, max(len(v) for v in banks.values()))
+        ways.append(w)
+    assert ways[:18] == [1] * 18, ways
+    assert ways[18:] == [2, 2], ways
+    kHpCol = 144
+    cover = set()
+    for half in (range(0, 32), range(32, 64)):
         banks = {}
-        for l in range(64):
-            a = _dense_stem_addr(l & 15, l >> 4, j)
-            banks.setdefault((a // 4) % 64, set()).add(a)
-        ways.append(max(len(v) for v in banks.values()))
-    straddle = [j for j in range(20) if 11 - (4 * j) % 11 < 4 and j != 19]
-    assert straddle == [2, 5, 8, 13, 16]
-    assert all(ways[j] == 1 for j in range(20) if j not in straddle), ways
-    assert max(ways) <= 2, ways
+        for l in half:
+            fr, fq = l & 15, l >> 4
+            a = fq * 2 * kHpCol + (fr >> 3) * 16 + (fr & 6) * 2 + (fr & 1) * kHpCol
+            col, byte = divmod(a, kHpCol)
+            cover.update({(col, byte // 2), (col, byte // 2 + 1)})
+            banks.setdefault((a // 4) % 32, set()).add(a)
+        assert max(len(v) for v in banks.values()) <= 2
+    assert cover == {(col, c) for col in range(8) for c in range(16)}
 
 
 @pytest.mark.parametrize("C,ipw", [(512, 4), (512, 16), (2048, 16), (2048, 4)])
