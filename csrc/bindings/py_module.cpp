@@ -292,6 +292,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("stream"), py::arg("w_dense") = 0);
   m.def("stem_dense_k_index", &stem_dense_k_index);
   m.def("stem_conv_pool_set_dbg", &stem_conv_pool_set_dbg);
+  m.def("stem_conv_pool_set_stamps", [](uintptr_t p) { stem_conv_pool_set_stamps((void*)p); });
   m.def("kernel_stagger", &kernel_stagger);
   m.def("kernel_stagger_set", &kernel_stagger_set);
   m.def("kernel_stagger_for_lanes", &kernel_stagger_for_lanes);

@@ -292,6 +292,11 @@ void stem_conv_pool(const void* x, const void* w, const float* bias, void* y, in
 // test hooks (0 = off): 512 forces the one-image-per-workgroup kernel, 2048
 // its 4-B raw-row DMA form
 void stem_conv_pool_set_dbg(int dbg);
+// measurement hook: per-step phase stamps of the one-image-per-workgroup
+// stem's first 16 workgroups into p ([16][PH/2 + 2][4] uint64, 100 MHz:
+// step start, MFMA phase done, helper work issued, helper waits done), or
+// null (off)
+void stem_conv_pool_set_stamps(void* p);
 // Workgroup start stagger per kernel family (common.h start_stagger): the
 // launchers pass kernel_stagger(k) to their kernels. kernel_stagger_set is the
 // A/B hook (tools/engine_ab.py); n < 0 restores the default.

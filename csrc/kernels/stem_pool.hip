@@ -90,7 +90,12 @@ struct StemArgs {
   // (profiles/r3_stem_knockouts.txt).
   int stagger;
   int rstagger;  // the one-image-per-workgroup kernel: start_stagger (common.h)
+  // measurement hook (stem_conv_pool_set_stamps): per-step phase stamps of
+  // the one-image-per-workgroup kernel's first kStemStampWgs workgroups
+  // (100 MHz), or null
+  unsigned long long* stamps;
 };
+constexpr int kStemStampWgs = 16;
 constexpr int kStemStagger = 2;
 
 template <int N>
@@ -113,10 +118,6 @@ __device__ __forceinline__ void ds_write_lo16(uint32_t addr, uint32_t v, const i
 }
 __device__ __forceinline__ void ds_write_hi16(uint32_t addr, uint32_t v, const int off) {
   asm volatile("ds_write_b16_d16_hi %0, %1 offset:%2" ::"v"(addr), "v"(v), "i"(off));
-}
-
-__device__ __forceinline__ void ds_write32(uint32_t addr, uint32_t v, const int off) {
-  asm volatile("ds_write_b32 %0, %1 offset:%2" ::"v"(addr), "v"(v), "i"(off));
 }
 
 __device__ __forceinline__ void lds_barrier() {
@@ -153,19 +154,10 @@ __device__ __forceinline__ float rot_rows_down1(float x, int lane) {
 // 89.6 vs 90.9 us for the role-split stem at B = 256 against the fp32 max +
 // bias-add epilogue (profiles/r4_stem_roles.txt).
 
-//
-// PAIR: channel pairs as 32-bit stores, one per block instead of two 16-bit
-// ones (LDS store cycles are per instruction): lanes fr and fr ^ 1 swap
-// their packed pair (DPP quad_perm [1,0,3,2]); the even lane stores channels
-// (fr, fr + 1) of the first pooled column, the odd one channels (fr - 1, fr)
-// of the second. hbase is then the pair base (hpool_pair_base), psel the
-// lane's v_perm selector (hpool_pair_sel).
-__device__ __forceinline__ uint32_t hpool_pair_sel(int fr) { return (fr & 1) ? 0x03020706u : 0x05040100u; }
 
-template <int NB, bool PAIR = false>
+template <int NB>
 __device__ __forceinline__ void hpool_packed(const floatx4 (&acc)[NB], uint32_t (&prevq)[(NB + 1) / 2], int lane,
-                                             int fq, uint32_t hbase, const int f, const int off,
-                                             uint32_t psel = 0) {
+                                             int fq, uint32_t hbase, const int f, const int off) {
   uint32_t p01[NB], p23[NB];
 #pragma unroll
   for (int n = 0; n < NB; ++n) {  // (no ReLU yet: see below)
@@ -204,13 +196,40 @@ __device__ __forceinline__ void hpool_packed(const floatx4 (&acc)[NB], uint32_t 
             __builtin_bit_cast(short2v, c)),
         short2v{0, 0});
     const uint32_t packed = __builtin_bit_cast(uint32_t, m);
-    if constexpr (PAIR) {
-      const uint32_t other = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)packed, 0xB1, 0xF, 0xF, false);
-      ds_write32(hbase, __builtin_amdgcn_perm(other, packed, psel), off + n * 32);
-    } else {
-      ds_write_lo16(hbase, packed, off + n * 32);
-      ds_write_hi16(hbase, packed, off + n * 32 + kHpCol);
-    }
+    ds_write_lo16(hbase, packed, off + n * 32);
+    ds_write_hi16(hbase, packed, off + n * 32 + kHpCol);
+  }
+}
+
+// The same epilogue without the cross-lane exchange (the dense-K stem when
+// its LDS has room for an edge ring): pooled column 2G (G = the lane's
+// 4-column group) is stored without its left neighbour, as
+// relu(max(v0, v1)), and the lane stores relu(v3) of its group into the edge
+// ring ([G][64 ch], same 144-B stride); the helpers' vertical pass takes
+// max(., edge[G - 1]) for even pooled columns. Per block: 2 cvt, alignbit, 3
+// packed max, and -- 3 16-bit stores instead of the row rotation's ~12
+// instructions per pair of blocks (the stem's MFMA waves are issue-bound:
+// profiles/r6_stem_dense.txt).
+template <int NB>
+__device__ __forceinline__ void hpool_edge(const floatx4 (&acc)[NB], uint32_t hbase, uint32_t ebase, const int off,
+                                           const int eoff) {
+#pragma unroll
+  for (int n = 0; n < NB; ++n) {
+    const float2v a = {acc[n][0], acc[n][1]}, b = {acc[n][2], acc[n][3]};
+    const uint32_t p01 = __builtin_bit_cast(uint32_t, __builtin_convertvector(a, bf16x2));
+    const uint32_t p23 = __builtin_bit_cast(uint32_t, __builtin_convertvector(b, bf16x2));
+    const uint32_t b12 = __builtin_amdgcn_alignbit(p23, p01, 16);  // (v1, v2)
+    // (relu v2, relu v3): signed 16-bit max on bf16 bits, exact against 0
+    const short2v r23 = __builtin_elementwise_max(__builtin_bit_cast(short2v, p23), short2v{0, 0});
+    const uint32_t c = __builtin_bit_cast(uint32_t, r23) & 0xffff0000u;  // (0, relu v3)
+    // lo = max(v0, v1, 0), hi = max(v1, v2, relu v3) = relu(max(v1, v2, v3))
+    const short2v m = __builtin_elementwise_max(
+        __builtin_elementwise_max(__builtin_bit_cast(short2v, p01), __builtin_bit_cast(short2v, b12)),
+        __builtin_bit_cast(short2v, c));
+    const uint32_t packed = __builtin_bit_cast(uint32_t, m);
+    ds_write_lo16(hbase, packed, off + n * 32);
+    ds_write_hi16(hbase, packed, off + n * 32 + kHpCol);
+    ds_write_hi16(ebase, __builtin_bit_cast(uint32_t, r23), eoff + n * 32);
   }
 }
 
@@ -506,30 +525,51 @@ __device__ __forceinline__ void vm_wait_dyn(int n) {
 // (slots a multiple of 128 B), so the two halves' 3 fr + u dword patterns
 // never share a bank (18 of 20 slots; a lane pattern over one bank window
 // costs the ds_read_b32 2 cycles a half-wave instead of 1). The pooling
-// epilogue stores channel pairs (hpool_packed<.., true>). Weights:
-// stem_dense_k_index (kernels.h), [64][160].
+// epilogue skips the cross-lane neighbour column when the edge ring fits
+// (hpool_edge; RolesLds::EDGE). Weights: stem_dense_k_index (kernels.h),
+// [64][160].
+//
+// LDS layout of the role-split stem (kernel and launcher): paired / dense
+// ring, hp ring, edge ring (dense K, where it fits in 160 KB: S <= 224), raw
+// ring.
+template <int NF, bool DK>
+struct RolesLds {
+  using G = StemGeom<NF>;
+  static constexpr int NG = 4 * NF + 1;            // dense rows: 8-pixel groups of the S + 6 padded pixels
+  static constexpr int RB = DK ? NG * 48 : G::Wq * 16;  // bytes per paired / dense row
+  // ring slot stride: dense slots a multiple of 128 B with room for the odd
+  // rows' 64-B offset
+  static constexpr int RBS = DK ? (RB + 64 + 127) / 128 * 128 : RB;
+  static constexpr int HPB = G::PW * kHpCol;       // bytes per horizontally pooled conv row
+  static constexpr int EPB = G::PW / 2 * kHpCol;   // edge row: relu(v3) per 4-column group
+  static constexpr int UBS = G::S * 3 + kU8Pad;    // raw ring slot
+  static constexpr int base = kRolesPairRing * RBS + kRolesHpRing * HPB + kRolesRawRing * UBS;
+  static constexpr bool EDGE = DK && base + kRolesHpRing * EPB <= 160 * 1024;
+  static constexpr int bytes = base + (EDGE ? kRolesHpRing * EPB : 0);
+  static_assert(bytes <= 160 * 1024, "role-split LDS budget");
+};
+
 template <int NF, int V = 0>
 __global__ __launch_bounds__(512, 1) void stem_roles_kernel(StemArgs a) {
   using G = StemGeom<NF>;
   extern __shared__ __attribute__((aligned(16))) uint4 smem[];
   constexpr bool DK = (V & 2) != 0;
-  constexpr int NG = 4 * NF + 1;      // dense rows: 8-pixel groups of the S + 6 padded pixels
+  using L = RolesLds<NF, DK>;
+  constexpr int NG = L::NG;
   static_assert(NG * 8 >= G::S + 6, "dense row groups");
-  constexpr int RB = DK ? NG * 48 : G::Wq * 16;  // bytes per paired / dense row
-  // ring slot stride: dense slots a multiple of 128 B with room for the odd
-  // rows' 64-B offset (within the paired rows' LDS budget of the launcher)
-  constexpr int RBS = DK ? (RB + 64 + 127) / 128 * 128 : RB;
-  static_assert(RBS <= G::Wq * 16, "dense ring within the launcher's LDS budget");
+  constexpr int RB = L::RB, RBS = L::RBS;
+  constexpr bool EDGE = L::EDGE;
   static_assert(!DK || 12 * (16 * NF - 1) + 4 * 10 + 4 <= RB, "dense window reads stay in the row");
   constexpr int UB = G::S * 3;        // bytes per raw image row
-  constexpr int UBS = UB + kU8Pad;    // raw ring slot
-  constexpr int HPB = G::PW * kHpCol;  // bytes per horizontally pooled conv row
+  constexpr int UBS = L::UBS;         // raw ring slot
+  constexpr int HPB = L::HPB, EPB = L::EPB;
   constexpr int T = G::PH / 2;
   char* ring = (char*)smem;
   char* hp = ring + kRolesPairRing * RBS;
+  char* edge = hp + kRolesHpRing * HPB;  // (EDGE only)
   // byte offset of padded row r (>= 0) in the paired / dense ring
   auto row_off = [](int r) __attribute__((always_inline)) { return (r % kRolesPairRing) * RBS + (DK ? 64 * (r & 1) : 0); };
-  char* u8ring = hp + kRolesHpRing * HPB;
+  char* u8ring = edge + (EDGE ? kRolesHpRing * EPB : 0);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -653,15 +693,25 @@ __global__ __launch_bounds__(512, 1) void stem_roles_kernel(StemArgs a) {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
 
+  // stamps[(b * (T + 2) + t) * 4 + k]: k = 0 step start / 1 MFMA phase done
+  // (wave 0), 2 helper work issued / 3 helper waits done (wave 4)
+  unsigned long long* stp = (a.stamps && b < kStemStampWgs && (wave == 0 || wave == 4) && lane == 0)
+                                ? a.stamps + (long)b * (T + 2) * 4
+                                : nullptr;
   for (int t = 0; t <= T + 1; ++t) {
+    if (stp && wave == 0) stp[4 * t] = __builtin_amdgcn_s_memrealtime();
     if (mfma_wave) {
       if (t <= T) {
         const int c0 = 4 * t - 4;
         const int cr = c0 + wave;
         char* hrow = hp + ((cr + kRolesHpRing) % kRolesHpRing) * HPB;
+        char* erow = edge + ((cr + kRolesHpRing) % kRolesHpRing) * EPB;  // (EDGE only)
         if (cr < 0) {
-          if (wave == 3)
+          if (wave == 3) {
             for (int o = lane * 16; o < HPB; o += 64 * 16) *(uint4*)(hrow + o) = make_uint4(0, 0, 0, 0);
+            if constexpr (EDGE)
+              for (int o = lane * 16; o < EPB; o += 64 * 16) *(uint4*)(erow + o) = make_uint4(0, 0, 0, 0);
+          }
         } else if constexpr (DK) {
           // per-lane operand addresses of this conv row (stem_dense_cell):
           // slots 0..14 from one base per kernel-row pair plus an immediate,
@@ -683,9 +733,8 @@ __global__ __launch_bounds__(512, 1) void stem_roles_kernel(StemArgs a) {
                       v3 = cell_off(15 + q, 3);
             ad[3 + q] = lane_off + (fq == 0 ? v0 : fq == 1 ? v1 : fq == 2 ? v2 : v3);
           }
-          const uint32_t hbase =
-              lds_addr(hrow) + fq * 2 * kHpCol + (fr >> 3) * 16 + (fr & 6) * 2 + (fr & 1) * kHpCol;
-          const uint32_t psel = hpool_pair_sel(fr);
+          const uint32_t hbase = lds_addr(hrow) + fq * 2 * kHpCol + (fr >> 3) * 16 + (fr & 7) * 2;
+          const uint32_t ebase = lds_addr(erow) + fq * kHpCol + (fr >> 3) * 16 + (fr & 7) * 2;
           uint32_t prevq[2];
           using u32x4 = uint32_t __attribute__((ext_vector_type(4)));
           // opaque bases, so the compiler does not re-derive (and re-merge)
@@ -722,7 +771,10 @@ __global__ __launch_bounds__(512, 1) void stem_roles_kernel(StemArgs a) {
                                                                           wf[n][s], acc[f & 1][n], 0, 0, 0);
             }
             if (f > 0) {
-              hpool_packed<4, true>(acc[(f - 1) & 1], prevq, lane, fq, hbase, f - 1, (f - 1) * 8 * kHpCol, psel);
+              if constexpr (EDGE)
+                hpool_edge<4>(acc[(f - 1) & 1], hbase, ebase, (f - 1) * 8 * kHpCol, (f - 1) * 4 * kHpCol);
+              else
+                hpool_packed<4>(acc[(f - 1) & 1], prevq, lane, fq, hbase, f - 1, (f - 1) * 8 * kHpCol);
             }
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -756,6 +808,7 @@ __global__ __launch_bounds__(512, 1) void stem_roles_kernel(StemArgs a) {
           }
         }
       }
+      if (stp) stp[4 * t + 1] = __builtin_amdgcn_s_memrealtime();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     } else {
       // DMA the raw rows step t+2's conversion reads: this wave's rows
@@ -785,6 +838,17 @@ __global__ __launch_bounds__(512, 1) void stem_roles_kernel(StemArgs a) {
             const ushort8 v2 = *(const ushort8*)(hp + ((r1 + 1) % kRolesHpRing) * HPB + off);
             const ushort8 v3 = *(const ushort8*)(hp + ((r1 + 2) % kRolesHpRing) * HPB + off);
             m[j] = __builtin_elementwise_max(__builtin_elementwise_max(v1, v2), v3);
+            if constexpr (EDGE) {
+              // even pooled column 2G: its left conv column 4G - 1 = relu(v3)
+              // of group G - 1 (hpool_edge); none left of G = 0 (zero pad)
+              if (!(pw & 1) && pw > 0) {
+                const int eo = (pw / 2 - 1) * kHpCol + cg * 16;
+                const ushort8 e1 = *(const ushort8*)(edge + ((r1 + kRolesHpRing) % kRolesHpRing) * EPB + eo);
+                const ushort8 e2 = *(const ushort8*)(edge + ((r1 + 1) % kRolesHpRing) * EPB + eo);
+                const ushort8 e3 = *(const ushort8*)(edge + ((r1 + 2) % kRolesHpRing) * EPB + eo);
+                m[j] = __builtin_elementwise_max(m[j], __builtin_elementwise_max(__builtin_elementwise_max(e1, e2), e3));
+              }
+            }
           }
         }
 #pragma unroll
@@ -801,8 +865,10 @@ __global__ __launch_bounds__(512, 1) void stem_roles_kernel(StemArgs a) {
       if (t < T) convert_rows(8 * t + 5, 8, htid, 256);
       // step t-1's DMAs (converted at t+1) have landed: everything but this
       // step's DMAs and stores (vmcnt retires in issue order)
+      if (stp) stp[4 * t + 2] = __builtin_amdgcn_s_memrealtime();
       vm_wait_dyn(nwait);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (stp) stp[4 * t + 3] = __builtin_amdgcn_s_memrealtime();
     }
     __builtin_amdgcn_s_barrier();
   }
@@ -829,6 +895,7 @@ int stem_pool_pick_strip(int B, int PH, int num_cus) {
 
 namespace {
 int g_stem_dbg = 0;
+unsigned long long* g_stem_stamps = nullptr;
 constexpr long kStemSplitCus = 256;  // MI355X CUs: the channel split fills them at query batches
 
 void stem_launch(const void* x, const uint8_t* u8, const void* w, const void* w2, const float* bias, void* y, int B,
@@ -858,21 +925,19 @@ void stem_launch(const void* x, const uint8_t* u8, const void* w, const void* w2
   // g_stem_dbg (tests): 512 force the role-split kernel, 2048 its 4-B raw-row DMA
   a.stagger = (long)B * (PH / strip) >= 512 ? kStemStagger : 0;
   a.rstagger = kernel_stagger(kStagStem);
+  a.stamps = g_stem_stamps;
   const size_t lds = u8 ? (size_t)kRingU8 * Wq * 16 + (size_t)kHp * a.PW * kHpCol + (size_t)kRingU8 * (S * 3 + kU8Pad)
                         : (size_t)kRing * Wq * 16 + (size_t)kHp * a.PW * kHpCol;
   const dim3 grid(B * (PH / strip));
   if (u8 && ((g_stem_dbg & 512) || strip == PH)) {
     // one workgroup per image, role-split waves (stem_pool_u8_pick_strip picks
     // strip = PH once the batch gives every CU an image)
-    const size_t lds_roles = (size_t)kRolesPairRing * Wq * 16 + (size_t)kRolesHpRing * a.PW * kHpCol +
-                             (size_t)kRolesRawRing * (S * 3 + kU8Pad);
-    if (lds_roles > 160 * 1024) throw std::invalid_argument("stem_conv_pool: role-split LDS budget");
     // 16-B raw-row DMA when the images allow it (g_stem_dbg 2048: force the 4-B form)
     const bool d16 = !((uintptr_t)u8 & 15) && !(g_stem_dbg & 2048);
     if (d16 && w2) {  // dense K (the engine packs both weight orders)
       switch (NF) {
 #define DMLC_STEM_DENSE_CASE(F) \
-  case F: hipLaunchKernelGGL((stem_roles_kernel<F, 3>), dim3(B), dim3(512), lds_roles, s, a); break;
+  case F: hipLaunchKernelGGL((stem_roles_kernel<F, 3>), dim3(B), dim3(512), (RolesLds<F, true>::bytes), s, a); break;
         DMLC_STEM_DENSE_CASE(4)
         DMLC_STEM_DENSE_CASE(5)
         DMLC_STEM_DENSE_CASE(6)
@@ -885,8 +950,12 @@ void stem_launch(const void* x, const uint8_t* u8, const void* w, const void* w2
     }
     switch (NF * 2 + (d16 ? 1 : 0)) {
 #define DMLC_STEM_ROLES_CASE(F) \
-  case 2 * F: hipLaunchKernelGGL((stem_roles_kernel<F>), dim3(B), dim3(512), lds_roles, s, a); break; \
-  case 2 * F + 1: hipLaunchKernelGGL((stem_roles_kernel<F, 1>), dim3(B), dim3(512), lds_roles, s, a); break;
+  case 2 * F: \
+    hipLaunchKernelGGL((stem_roles_kernel<F>), dim3(B), dim3(512), (RolesLds<F, false>::bytes), s, a); \
+    break; \
+  case 2 * F + 1: \
+    hipLaunchKernelGGL((stem_roles_kernel<F, 1>), dim3(B), dim3(512), (RolesLds<F, false>::bytes), s, a); \
+    break;
       DMLC_STEM_ROLES_CASE(4)
       DMLC_STEM_ROLES_CASE(5)
       DMLC_STEM_ROLES_CASE(6)
@@ -936,6 +1005,7 @@ void stem_launch(const void* x, const uint8_t* u8, const void* w, const void* w2
 }  // namespace
 
 void stem_conv_pool_set_dbg(int dbg) { g_stem_dbg = dbg; }
+void stem_conv_pool_set_stamps(void* p) { g_stem_stamps = (unsigned long long*)p; }
 
 void stem_conv_pool(const void* x, const void* w, const float* bias, void* y, int B, int S, int Wq, int strip,
                     hipStream_t s) {

@@ -840,10 +840,11 @@ def test_stem_dense_lds_conflicts():
     bank (a/4) mod 32) are conflict free in 18 of the 20 dword slots: each half
     pairs dword u of an even and an odd kernel row, 16 banks apart, against
     the 3 fr + u lane pattern; slots 18, 19 (row 6 against itself) are 2-way.
-    The pooling epilogue's channel-pair stores (ds_write_b32, 2 x 32 lanes)
-    are at most 2-way, which costs a 32-bit store nothing (its data transfer
-    takes the 2 cycles), and cover every (pooled column, channel) of a
-    fragment once."""
+    The pooling epilogue (hpool_edge) stores, per lane (channel fr of block
+    n, 4-column group G = 4 f + fq), pooled columns 2G, 2G + 1 into the hp
+    row and relu(v3) into the edge row: together they cover every (pooled
+    column, channel) and (group, channel) of a fragment once, at most 2-way
+    per 32-lane half."""
     RB, RBS = 1392, _dense_rbs(1392)
     worst = 1
     for t0 in range(0, 8 * 29, 64):
@@ -873,17 +874,21 @@ def test_stem_dense_lds_conflicts():
     assert ways[:18] == [1] * 18, ways
     assert ways[18:] == [2, 2], ways
     kHpCol = 144
-    cover = set()
+    hcov, ecov = set(), set()
     for half in (range(0, 32), range(32, 64)):
-        banks = {}
+        hb, eb = {}, {}
         for l in half:
             fr, fq = l & 15, l >> 4
-            a = fq * 2 * kHpCol + (fr >> 3) * 16 + (fr & 6) * 2 + (fr & 1) * kHpCol
-            col, byte = divmod(a, kHpCol)
-            cover.update({(col, byte // 2), (col, byte // 2 + 1)})
-            banks.setdefault((a // 4) % 32, set()).add(a)
-        assert max(len(v) for v in banks.values()) <= 2
-    assert cover == {(col, c) for col in range(8) for c in range(16)}
+            h = fq * 2 * kHpCol + (fr >> 3) * 16 + (fr & 7) * 2  # lo16 at h, hi16 at h + kHpCol
+            e = fq * kHpCol + (fr >> 3) * 16 + (fr & 7) * 2
+            for a in (h, h + kHpCol):
+                hcov.add(divmod(a, kHpCol))
+                hb.setdefault((a // 4) % 32, set()).add(a // 4)
+            ecov.add(divmod(e, kHpCol))
+            eb.setdefault((e // 4) % 32, set()).add(e // 4)
+        assert max(len(v) for v in hb.values()) <= 2 and max(len(v) for v in eb.values()) <= 2
+    assert hcov == {(col, 2 * c) for col in range(8) for c in range(16)}
+    assert ecov == {(g, 2 * c) for g in range(4) for c in range(16)}
 
 
 @pytest.mark.parametrize("C,ipw", [(512, 4), (512, 16), (2048, 16), (2048, 4)])

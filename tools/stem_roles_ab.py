@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--variants", default="paired,dense,paired4")
+    ap.add_argument("--stamps", action="store_true",
+                    help="per-step phase stamps of each variant (stem_conv_pool_set_stamps), after the timing")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     g = torch.Generator().manual_seed(5)
@@ -68,6 +70,33 @@ def main():
     for v in vs:
         print(f"{v:8s} median {statistics.median(res[v]):7.1f} us  all {' '.join(f'{t:.1f}' for t in res[v])}",
               flush=True)
+    if args.stamps:
+        steps = 56 // 2 + 2
+        for v in vs:
+            st = torch.zeros(16 * steps * 4, dtype=torch.int64, device=dev)
+            for _ in range(3):  # (the last launch's stamps, warm)
+                C.stem_conv_pool_set_stamps(st.data_ptr())
+                run(v)
+                C.stem_conv_pool_set_stamps(0)
+            torch.cuda.synchronize()
+            a = st.view(16, steps, 4).double().cpu() * 10e-3  # 100 MHz ticks -> us
+            t0 = a[:, 0, 0].view(16, 1)
+            start = a[:, :, 0] - t0
+            mfma = a[:, :, 1] - a[:, :, 0]
+            helper = a[:, :, 2] - a[:, :, 0]
+            hwait = a[:, :, 3] - a[:, :, 2]
+            step = torch.cat([start[:, 1:] - start[:, :-1], torch.zeros(16, 1)], 1)
+
+            def med(x, j):
+                return x[:, j].median().item()
+
+            print(f"{v}: per-step medians over 16 workgroups (us): step t / step length / MFMA wave 0 phase / "
+                  "helper wave 4 work issued / helper waits", flush=True)
+            for j in range(steps):
+                print(f"  t={j:2d} start {med(start, j):6.2f} len {med(step, j):5.2f} mfma {med(mfma, j):5.2f} "
+                      f"helper {med(helper, j):5.2f} wait {med(hwait, j):5.2f}")
+            end = a[:, steps - 1, 3] - a[:, 0, 0]
+            print(f"  total (start to last helper wait) median {end.median().item():.2f} us", flush=True)
 
 
 if __name__ == "__main__":
