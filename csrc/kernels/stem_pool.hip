@@ -227,9 +227,13 @@ __device__ __forceinline__ void hpool_edge(const floatx4 (&acc)[NB], uint32_t hb
         __builtin_elementwise_max(__builtin_bit_cast(short2v, p01), __builtin_bit_cast(short2v, b12)),
         __builtin_bit_cast(short2v, c));
     const uint32_t packed = __builtin_bit_cast(uint32_t, m);
-    ds_write_lo16(hbase, packed, off + n * 32);
-    ds_write_hi16(hbase, packed, off + n * 32 + kHpCol);
-    ds_write_hi16(ebase, __builtin_bit_cast(uint32_t, r23), eoff + n * 32);
+    // compiler-visible stores (its lgkmcnt waits then count them: inline-asm
+    // stores issued after the next fragment's operand loads made its waits
+    // drain those loads; the MFMA waves have no DMA in flight)
+    typedef __attribute__((address_space(3))) uint16_t lds_u16;
+    *(lds_u16*)(uintptr_t)(hbase + off + n * 32) = (uint16_t)packed;
+    *(lds_u16*)(uintptr_t)(hbase + off + n * 32 + kHpCol) = (uint16_t)(packed >> 16);
+    *(lds_u16*)(uintptr_t)(ebase + eoff + n * 32) = (uint16_t)(__builtin_bit_cast(uint32_t, r23) >> 16);
   }
 }
 
