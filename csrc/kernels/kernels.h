@@ -77,8 +77,8 @@ void conv2d_igemm(const ConvArgs& a, hipStream_t s);
 // fp32 partial slices [splits][M][Npad] in a.ws.
 void splitk_reduce(const ConvArgs& a, long M, int splits, hipStream_t s);
 // Fully connected layers at M = B <= 256 (fc_gemm.hip): all rows x 128
-// columns x one K slice per workgroup, register-staged LDS tiles, fp32
-// partials reduced by splitk_reduce (so a.ws is required even at 1 slice).
+// columns x one K slice per workgroup, tiles through a 3-slot LDS-DMA ring,
+// fp32 partials reduced by splitk_reduce (so a.ws is required even at 1 slice).
 bool fc_gemm_supported(const ConvArgs& a);
 int fc_gemm_splits(const ConvArgs& a, int num_cus);  // K slices for ~one workgroup per CU
 void fc_gemm(const ConvArgs& a, int splits, hipStream_t s);

@@ -605,11 +605,18 @@ __global__ __launch_bounds__(512, 1) void stem_roles_kernel(StemArgs a) {
   auto convert_rows = [&](int lo, int cnt, int t0, int nthr) __attribute__((always_inline)) {
     if constexpr (DK) {
       // item = (row, group g): padded pixels 8g .. 8g+7 (image columns 8g-3 ..
-      // 8g+4) -> 24 bf16 at byte 48 g of the dense row, three 16-B stores
+      // 8g+4) -> 24 bf16 at byte 48 g of the dense row, three 16-B stores.
+      // Items of the inner groups 1 .. NG-2 (every pixel inside the image
+      // columns) come first and convert without per-element selects; the 2
+      // edge groups of each row (zero padding, per element) last, on the last
+      // lanes, so only one helper wave takes that path.
+      constexpr int NI = NG - 2;
       const int items = cnt * NG;
       for (int it = t0; it < items; it += nthr) {
-        const int r = lo + it / NG;
-        const int g = it - (it / NG) * NG;
+        const bool inner = it < cnt * NI;
+        const int e = it - cnt * NI;
+        const int r = lo + (inner ? it / NI : e >> 1);
+        const int g = inner ? 1 + it % NI : ((e & 1) ? NG - 1 : 0);
         if (r < 0) continue;
         const int iy = r - 3;
         const bool row_in = iy >= 0 && iy < G::S;
@@ -617,17 +624,25 @@ __global__ __launch_bounds__(512, 1) void stem_roles_kernel(StemArgs a) {
         const int A = 24 * g - 12;
         uint32_t d[7];
 #pragma unroll
-        for (int j = 0; j < 7; ++j) d[j] = row_in ? *(const uint32_t*)(srow + A + 4 * j) : 0u;
+        for (int j = 0; j < 7; ++j) d[j] = *(const uint32_t*)(srow + A + 4 * j);
         float v[24];
+        if (inner && row_in) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int ix = 8 * g - 3 + i;
-          const bool in = row_in && ix >= 0 && ix < G::S;
+          for (int i = 0; i < 24; ++i) {
+            const int idx = 3 + i;
+            v[i] = imagenet_norm(i % 3, (float)((d[idx >> 2] >> (8 * (idx & 3))) & 0xffu));
+          }
+        } else {
 #pragma unroll
-          for (int c = 0; c < 3; ++c) {
-            const int idx = 3 + 3 * i + c;
-            const float cv = (float)((d[idx >> 2] >> (8 * (idx & 3))) & 0xffu);
-            v[3 * i + c] = in ? imagenet_norm(c, cv) : 0.f;
+          for (int i = 0; i < 8; ++i) {
+            const int ix = 8 * g - 3 + i;
+            const bool in = row_in && ix >= 0 && ix < G::S;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+              const int idx = 3 + 3 * i + c;
+              const float cv = (float)((d[idx >> 2] >> (8 * (idx & 3))) & 0xffu);
+              v[3 * i + c] = in ? imagenet_norm(c, cv) : 0.f;
+            }
           }
         }
         char* drow = ring + row_off(r) + g * 48;
