@@ -241,10 +241,19 @@ struct Compute {
       }
       const int r = 4 * j + 1 + 2 * wm + ((geo.hi >> f) & 1);
       const bool outside = (unsigned)r >= (unsigned)kH;
+      // scale + bias as v_pk_fma_f32 on channel pairs, ReLU on the packed
+      // bf16 (relu_bf16x8), rows outside the image zeroed on the packed words
       float v[8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = outside ? 0.f : fmaxf(acc[e >> 2][e & 3] * a1v[e] + b1v[e], 0.f);
-      *(uint4*)(ring + ((r + kRing) % kRing) * kSlot + t1_off(geo.col[f] + 1, wn, g)) = pack8(v);
+      for (int e = 0; e < 8; e += 2) {
+        const f32x2 q = __builtin_elementwise_fma(f32x2{acc[e >> 2][e & 3], acc[e >> 2][(e & 3) + 1]},
+                                                  f32x2{a1v[e], a1v[e + 1]}, f32x2{b1v[e], b1v[e + 1]});
+        v[e] = q.x;
+        v[e + 1] = q.y;
+      }
+      const uint4 pk = relu_bf16x8(pack8(v));
+      *(uint4*)(ring + ((r + kRing) % kRing) * kSlot + t1_off(geo.col[f] + 1, wn, g)) =
+          outside ? make_uint4(0, 0, 0, 0) : pk;
     }
   }
 
@@ -438,8 +447,12 @@ struct Memory {
           float v[4], rf[4];
           fp8x4_to_f32(rw[h], rf);
 #pragma unroll
-          for (int i = 0; i < 4; ++i)
-            v[i] = __builtin_amdgcn_fmed3f(__builtin_fmaf(rf[i], rsi, acc[h][i]), 0.f, 448.f);
+          for (int i = 0; i < 4; i += 2) {  // the residual as v_pk_fma_f32
+            const f32x2 q = __builtin_elementwise_fma(f32x2{rf[i], rf[i + 1]}, f32x2{rsi, rsi},
+                                                      f32x2{acc[h][i], acc[h][i + 1]});
+            v[i] = __builtin_amdgcn_fmed3f(q.x, 0.f, 448.f);
+            v[i + 1] = __builtin_amdgcn_fmed3f(q.y, 0.f, 448.f);
+          }
           q[h] = f32x4_to_fp8_sat(v);
         }
         // non-temporal y stores (L2 kept for the x re-reads)

@@ -349,10 +349,20 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void conv1x1_kernel(C1Arg
 #pragma unroll
       for (int j = 0; j < NG; ++j) {
         float v[CPL];
+        // channel pairs (2e, 2e+1) sit in consecutive accumulator registers:
+        // scale + bias (and the e4m3 residual below) as v_pk_fma_f32, two
+        // channels an instruction
 #pragma unroll
-        for (int e = 0; e < CPL; ++e) {
-          const float raw = W16 ? acc[pf][4 * j + (e >> 2)][e & 3] : NF >= 2 ? acc[pf][2 * j + (e >> 2)][e & 3] : acc[pf][0][e];
-          v[e] = IN8 || OUT8 ? __builtin_fmaf(raw, al[j][e], bs[j][e]) : raw + bs[j][e];
+        for (int e = 0; e < CPL; e += 2) {
+          const floatx4& q = W16 ? acc[pf][4 * j + (e >> 2)] : NF >= 2 ? acc[pf][2 * j + (e >> 2)] : acc[pf][0];
+          const f32x2 raw = {q[e & 3], q[(e & 3) + 1]};
+          f32x2 r;
+          if constexpr (IN8 || OUT8)
+            r = __builtin_elementwise_fma(raw, f32x2{al[j][e], al[j][e + 1]}, f32x2{bs[j][e], bs[j][e + 1]});
+          else
+            r = raw + f32x2{bs[j][e], bs[j][e + 1]};
+          v[e] = r.x;
+          v[e + 1] = r.y;
         }
         if constexpr (RES) {
           float rf[CPL];
@@ -369,7 +379,11 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void conv1x1_kernel(C1Arg
               fp8x4_to_f32(rv[pf][j], rf);
             }
 #pragma unroll
-            for (int e = 0; e < CPL; ++e) v[e] = __builtin_fmaf(rf[e], rsc, v[e]);
+            for (int e = 0; e < CPL; e += 2) {
+              const f32x2 r = __builtin_elementwise_fma(f32x2{rf[e], rf[e + 1]}, f32x2{rsc, rsc}, f32x2{v[e], v[e + 1]});
+              v[e] = r.x;
+              v[e + 1] = r.y;
+            }
           } else {
             if constexpr (CPL == 8) {
               const u32x4 q = rv[pf][j];

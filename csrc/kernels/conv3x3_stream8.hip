@@ -257,16 +257,22 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream8_kernel(Stream8Args a) 
   for (int f = 0; f < MF; ++f)
 #pragma unroll
     for (int nf = 0; nf < NF; ++nf) asm volatile("" : "+v"(acc[f][nf]));
-  // ---- epilogue: lane holds channels ch0 + 32 j + 8 fq .. +7 of its pixel
-  float al[NG][8], bs[NG][8];
+  // ---- epilogue: lane holds channels ch0 + 32 j + 8 fq .. +7 of its pixel.
+  // The 1 / s_out quantisation scale (> 0) is folded into alpha and the bias,
+  // so a value costs half a v_pk_fma_f32 (channel pairs sit in consecutive
+  // accumulator registers) and one med3 (ReLU and the +-448 saturation
+  // together)
+  const float inv = a.out_inv_scale;
+  const float lo_clamp = a.relu ? 0.f : -448.f;
+  f32x2 al[NG][4], bs[NG][4];
 #pragma unroll
   for (int j = 0; j < NG; ++j)
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      al[j][e] = a.alpha[ch0 + 32 * j + 8 * fq + e];
-      bs[j][e] = a.bias[ch0 + 32 * j + 8 * fq + e];
+    for (int e = 0; e < 4; ++e) {
+      const int c = ch0 + 32 * j + 8 * fq + 2 * e;
+      al[j][e] = f32x2{a.alpha[c], a.alpha[c + 1]} * inv;
+      bs[j][e] = f32x2{a.bias[c], a.bias[c + 1]} * inv;
     }
-  const float inv = a.out_inv_scale;
   const long base = ((long)b * H + r0) * W * CO + ch0 + 8 * fq;
 #pragma unroll
   for (int f = 0; f < MF; ++f) {
@@ -277,11 +283,13 @@ __global__ __launch_bounds__(512, 1) void conv3x3_stream8_kernel(Stream8Args a) 
       float q[8];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        q[e] = acc[f][2 * j][e] * al[j][e] + bs[j][e];
-        q[4 + e] = acc[f][2 * j + 1][e] * al[j][4 + e] + bs[j][4 + e];
+        const floatx4& ac = acc[f][2 * j + (e >> 1)];
+        const f32x2 r = __builtin_elementwise_fma(f32x2{ac[2 * (e & 1)], ac[2 * (e & 1) + 1]}, al[j][e], bs[j][e]);
+        q[2 * e] = r.x;
+        q[2 * e + 1] = r.y;
       }
 #pragma unroll
-      for (int e = 0; e < 8; ++e) q[e] = __builtin_amdgcn_fmed3f((a.relu ? fmaxf(q[e], 0.f) : q[e]) * inv, -448.f, 448.f);
+      for (int e = 0; e < 8; ++e) q[e] = __builtin_amdgcn_fmed3f(q[e], lo_clamp, 448.f);
       int lo = __builtin_amdgcn_cvt_pk_fp8_f32(q[0], q[1], 0, false);
       lo = __builtin_amdgcn_cvt_pk_fp8_f32(q[2], q[3], lo, true);
       int hi = __builtin_amdgcn_cvt_pk_fp8_f32(q[4], q[5], 0, false);
