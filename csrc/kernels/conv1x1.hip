@@ -124,6 +124,14 @@ struct C1Args {
   const void* x2;  // second input (K chunks cpr1 .. CPR-1 of a pixel), or null
   int cpr1;        // 16-B chunks of a pixel from x
   int stagger;     // start_stagger (common.h)
+  // CH (chained reduce): the next bottleneck's reduce conv on this conv's
+  // output block, read back from LDS: y2 = e4m3(relu(w2 x y * alpha2 + bias2) * out_inv_scale2)
+  const void* w2;       // [N2][N] e4m3
+  const float* alpha2;  // [N2]
+  const float* bias2;   // [N2]
+  void* y2;             // [M, N2] e4m3
+  int N2, relu2;
+  float out_inv_scale2;
 };
 
 // pixels per block: 64, or 32 for 1-KB input rows (stage = BM x RB bytes)
@@ -133,8 +141,16 @@ constexpr int block_m() { return RB <= 512 ? 64 : 32; }
 // WV waves per workgroup: 4 (two workgroups per CU, <= 64 weight VGPRs per
 // wave) or 8 (one per CU, <= 128 weight VGPRs per wave: twice the channels
 // per wave and per workgroup, so a wide layer restages its input for fewer
-// channel slices)
-template <bool IN8, bool OUT8, int RB, int NW, int S2, bool RES, int S, int WV>
+// channel slices).
+//
+// CH (chained reduce, ResNet50 e4m3 layer2): this conv is a bottleneck's
+// expand conv (e4m3, residual, all N = 512 output channels in one
+// workgroup) and the next bottleneck's reduce conv (512 -> 128, e4m3, ReLU)
+// runs on each finished 64-pixel output block while it is still on chip: the
+// block goes to LDS next to its y store, and every wave computes 16 reduce
+// channels from it (weights in 32 more VGPRs, 4 K steps). The reduce conv's
+// separate launch re-read all of y from HBM (102.8 MB at B = 256).
+template <bool IN8, bool OUT8, int RB, int NW, int S2, bool RES, int S, int WV, bool CH = false>
 __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void conv1x1_kernel(C1Args a) {
   constexpr int kBM = block_m<RB>();
   constexpr int CPR = RB / 16;              // 16-B chunks per staged pixel row
@@ -150,13 +166,17 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void conv1x1_kernel(C1Arg
   constexpr int STAGE = kBM * RB;
   constexpr int DT = STAGE / 16 / 64 / WV;  // DMA instructions per wave per block
   constexpr int RT = RES ? NPF * NG : 0;    // residual loads per wave per block
-  constexpr int ST = NPF * NG;              // stores per wave per block
+  constexpr int NP2 = CH ? WV * NW : 0;     // chained reduce: its K (= N, e4m3 bytes per pixel)
+  constexpr int KS2 = NP2 / 128;            // its K steps
+  constexpr int ST = NPF * NG + (CH ? NPF : 0);  // stores per wave per block (+ the reduce's)
   constexpr int N1 = (S - 1) * (ST + RT + DT);
   static_assert(DT >= 1 && KS >= 1, "tile");
+  static_assert(!CH || (IN8 && OUT8 && RES && W16 && NG == 1 && NP2 == 512 && S2 == 1), "chained reduce form");
   using WFrag = typename std::conditional<IN8, v8i, bf16x8>::type;
 
   extern __shared__ __attribute__((aligned(16))) uint4 smem[];
   char* stages = (char*)smem;
+  char* ybuf = stages + S * STAGE;  // CH: the output block, [kBM][NP2] chunk-swizzled (c ^ (p & 15))
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -214,6 +234,27 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void conv1x1_kernel(C1Arg
       bs[j][e] = a.bias[n] * osc;
       al[j][e] = (IN8 ? a.alpha[n] : 1.f) * osc;
     }
+
+  // CH: the reduce conv's weights (channel 16 wave + fr, k = 128 ks + 32 g ..
+  // +32 at lane (fr, g)) and constants (lane channels 16 wave + 4 g .. +3)
+  v8i wf2[CH ? KS2 : 1];
+  f32x2 al2[2], bs2[2];
+  const float relu_lo2 = a.relu2 ? 0.f : -448.f;
+  if constexpr (CH) {
+    const uint8_t* row = (const uint8_t*)a.w2 + (size_t)(wave * 16 + fr) * NP2;
+#pragma unroll
+    for (int ks = 0; ks < KS2; ++ks) {
+      const uint4 lo = *(const uint4*)(row + ks * 128 + g * 32);
+      const uint4 hi = *(const uint4*)(row + ks * 128 + g * 32 + 16);
+      wf2[ks] = v8i{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+    }
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int n = wave * 16 + 4 * g + 2 * e;
+      al2[e] = f32x2{a.alpha2[n], a.alpha2[n + 1]} * a.out_inv_scale2;
+      bs2[e] = f32x2{a.bias2[n], a.bias2[n + 1]} * a.out_inv_scale2;
+    }
+  }
 
   // ---- staging: block m -> stage buffer (pixel p's RB bytes, chunk-swizzled)
   const long rowstride_in = (long)a.cpr1 * 16;  // x's pixel stride (all of K without x2)
@@ -404,10 +445,15 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void conv1x1_kernel(C1Arg
         if constexpr (OUT8) {  // (already scaled by 1 / s_out)
 #pragma unroll
           for (int e = 0; e < CPL; ++e) v[e] = __builtin_amdgcn_fmed3f(v[e], relu_lo, 448.f);
-          if constexpr (CPL == 16)
-            *(uint4*)yp = make_uint4(f32x4_to_fp8_sat(v), f32x4_to_fp8_sat(v + 4), f32x4_to_fp8_sat(v + 8),
-                                     f32x4_to_fp8_sat(v + 12));
-          else if constexpr (CPL == 8) *(uint2*)yp = make_uint2(f32x4_to_fp8_sat(v), f32x4_to_fp8_sat(v + 4));
+          if constexpr (CPL == 16) {
+            const uint4 q4 = make_uint4(f32x4_to_fp8_sat(v), f32x4_to_fp8_sat(v + 4), f32x4_to_fp8_sat(v + 8),
+                                        f32x4_to_fp8_sat(v + 12));
+            *(uint4*)yp = q4;
+            if constexpr (CH) {  // and into the chained reduce's input block
+              const int p = pf * 16 + fr, c = n >> 4;
+              *(uint4*)(ybuf + p * NP2 + ((c ^ (p & 15)) << 4)) = q4;
+            }
+          } else if constexpr (CPL == 8) *(uint2*)yp = make_uint2(f32x4_to_fp8_sat(v), f32x4_to_fp8_sat(v + 4));
           else *(uint32_t*)yp = f32x4_to_fp8_sat(v);
         } else if constexpr (CPL == 8) {
           *(uint4*)yp = pack8_relu(v, a.relu);  // ReLU on the packed bf16
@@ -418,6 +464,42 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void conv1x1_kernel(C1Arg
           }
           *(uint2*)yp = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
         }
+      }
+    }
+    if constexpr (CH) {
+      // ---- chained reduce on the block (every wave's share of it is in
+      // ybuf after the barrier; the next block's ybuf writes come after its
+      // two barriers, so one buffer suffices)
+      lds_barrier();
+      floatx4 acc2[NPF];
+#pragma unroll
+      for (int pf = 0; pf < NPF; ++pf) acc2[pf] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS2; ++ks) {
+        v8i xb[NPF];
+#pragma unroll
+        for (int pf = 0; pf < NPF; ++pf) {
+          const int p = pf * 16 + fr, c0 = ks * 8 + 2 * g;
+          const char* row = ybuf + p * NP2;
+          const uint4 lo = *(const uint4*)(row + ((c0 ^ (p & 15)) << 4));
+          const uint4 hi = *(const uint4*)(row + (((c0 + 1) ^ (p & 15)) << 4));
+          xb[pf] = v8i{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+        }
+#pragma unroll
+        for (int pf = 0; pf < NPF; ++pf)
+          acc2[pf] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(wf2[ks], xb[pf], acc2[pf], 0, 0, 0, 127, 0, 127);
+      }
+#pragma unroll
+      for (int pf = 0; pf < NPF; ++pf) {
+        const long m = (long)blk * kBM + pf * 16 + fr;
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const f32x2 r = __builtin_elementwise_fma(f32x2{acc2[pf][2 * e], acc2[pf][2 * e + 1]}, al2[e], bs2[e]);
+          v[2 * e] = __builtin_amdgcn_fmed3f(r.x, relu_lo2, 448.f);
+          v[2 * e + 1] = __builtin_amdgcn_fmed3f(r.y, relu_lo2, 448.f);
+        }
+        *(uint32_t*)((uint8_t*)a.y2 + m * a.N2 + wave * 16 + 4 * g) = f32x4_to_fp8_sat(v);
       }
     }
   };
@@ -526,6 +608,58 @@ void launch_rb(const L1& l) {
 }  // namespace
 
 bool conv1x1_supported(const ConvArgs& a) { return pick(a).nw > 0; }
+
+bool conv1x1_chain_supported(const ConvArgs& a, const ConvArgs& r) {
+  const Pick pk = pick(a);
+  // the expand conv: e4m3 in and out, residual, 128-B input rows, all 512
+  // channels in one 8-wave workgroup; the reduce conv: 1x1 / stride 1 on its
+  // output (K = 512 e4m3), 128 e4m3 output channels = 16 per wave
+  return pk.nw == 64 && pk.wv == 8 && pk.rb == 128 && a.N == 512 && a.in_fp8 && a.out_fp8 && a.res && !a.x2 &&
+         a.stride == 1 && conv1x1_supported(r) && r.in_fp8 && r.out_fp8 && !r.res && !r.x2 && r.stride == 1 &&
+         r.Kpad == a.N && r.Cin == a.N && r.N == 128 && r.ldo == 128 && r.B == a.B && r.H == a.Ho && r.W == a.Wo &&
+         r.alpha && r.bias && r.w && r.y;
+}
+
+void conv1x1_chain(const ConvArgs& a, const ConvArgs& r, int num_cus, hipStream_t s) {
+  if (!conv1x1_chain_supported(a, r)) throw std::invalid_argument("conv1x1_chain: unsupported pair");
+  if (!a.x || !a.w || !a.bias || !a.y || !a.zero || !a.alpha ||
+      (((uintptr_t)a.x | (uintptr_t)a.w | (uintptr_t)a.y | (uintptr_t)a.res | (uintptr_t)r.w | (uintptr_t)r.y) & 15))
+    throw std::invalid_argument("conv1x1_chain: null / misaligned operand");
+  C1Args c{};
+  c.x = a.x;
+  c.x2 = nullptr;
+  c.cpr1 = a.Cin / 16;
+  c.w = a.w;
+  c.bias = a.bias;
+  c.alpha = a.alpha;
+  c.res = a.res;
+  c.y = a.y;
+  c.zero = a.zero;
+  c.B = a.B;
+  c.H = a.H;
+  c.W = a.W;
+  c.Ho = a.Ho;
+  c.Wo = a.Wo;
+  c.N = a.N;
+  c.Kpad = a.Kpad;
+  c.relu = a.relu;
+  c.stagger = kernel_stagger(kStagConv1x1);
+  c.res_scale = a.res_scale;
+  c.out_inv_scale = a.out_inv_scale;
+  c.nslices = 1;
+  c.nblocks = (int)((long)a.B * a.Ho * a.Wo / 64);
+  c.w2 = r.w;
+  c.alpha2 = r.alpha;
+  c.bias2 = r.bias;
+  c.y2 = r.y;
+  c.N2 = r.N;
+  c.relu2 = r.relu;
+  c.out_inv_scale2 = r.out_inv_scale;
+  const int q = std::max(1, std::min((c.nblocks + 7) / 8, num_cus / 8));
+  const size_t lds = 3 * 64 * 128 + 64 * 512;
+  hipLaunchKernelGGL((conv1x1_kernel<true, true, 128, 64, 1, true, 3, 8, true>), dim3(8 * q), dim3(512), lds, s, c);
+  DMLC_HIP_CHECK(hipGetLastError());
+}
 
 void conv1x1(const ConvArgs& a, int num_cus, hipStream_t s) {
   const Pick pk = pick(a);

@@ -100,6 +100,11 @@ constexpr int kConvBigTile0 = 11;
 constexpr int kConv1x1Tile = 100;
 bool conv1x1_supported(const ConvArgs& a);
 void conv1x1(const ConvArgs& a, int num_cus, hipStream_t s);
+// ResNet50 e4m3 layer2: an expand conv (e4m3, residual, N = 512) and the next
+// bottleneck's reduce conv r (1x1, K = 512 -> 128) on its output, one launch
+// (the reduce input never goes back to HBM; conv1x1.hip CH form)
+bool conv1x1_chain_supported(const ConvArgs& a, const ConvArgs& r);
+void conv1x1_chain(const ConvArgs& a, const ConvArgs& r, int num_cus, hipStream_t s);
 int conv_bigtile_pick(const ConvArgs& a, int num_cus);  // engine's choice: config, or -1 (old kernel)
 int conv_bigtile_splits(const ConvArgs& a, int cfg, int num_cus);
 long conv_bigtile_slabs(const ConvArgs& a, int cfg, int splits);

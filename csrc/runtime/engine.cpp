@@ -79,6 +79,7 @@ bool EngineOptions::set(const std::string& name, bool v) {
       {"rows_wreg", &EngineOptions::rows_wreg},     {"fused_block", &EngineOptions::fused_block},
       {"fused_bottleneck", &EngineOptions::fused_bottleneck},
       {"ds_into_expand", &EngineOptions::ds_into_expand}, {"ds_into_conv2", &EngineOptions::ds_into_conv2},
+      {"chain_1x1", &EngineOptions::chain_1x1},
       {"fp8_3x3_in", &EngineOptions::fp8_3x3_in},
       {"stream_conv", &EngineOptions::stream_conv}, {"stream_wreg", &EngineOptions::stream_wreg},
       {"stream_l4s2", &EngineOptions::stream_l4s2}, {"fuse_ds", &EngineOptions::fuse_ds},
@@ -1124,6 +1125,24 @@ bool Engine::ds_conv2_ok(size_t oi, int B) const {
   return true;
 }
 
+// ops[oi] is a bottleneck's expand conv (1x1, residual) and ops[oi + 1] the
+// next bottleneck's reduce conv on its output, both on conv1x1.hip, in a form
+// conv1x1_chain runs as one launch (ResNet50 e4m3 layer2.0-2.2 -> 2.1-2.3).
+// The expand output keeps its other reader (the next expand's residual).
+bool Engine::chain_ok(size_t oi, int B) const {
+  if (!opt_.chain_1x1 || oi + 1 >= ops_.size() || acts_.empty()) return false;
+  const Op& e = ops_[oi];
+  const Op& r = ops_[oi + 1];
+  if (e.type != OpType::Conv || r.type != OpType::Conv || e.res < 0 || r.in != e.out || r.res >= 0 || e.side ||
+      r.side)
+    return false;
+  if (conv_path(e, B) != ConvPath::OneByOne || conv_path(r, B) != ConvPath::OneByOne) return false;
+  if (convs_[e.conv].cat_off) return false;  // (an expand with its downsample as a second K block)
+  ConvArgs a = conv_args(e, B, nullptr), ra = conv_args(r, B, nullptr);
+  a.split_k = ra.split_k = 1;
+  return conv1x1_chain_supported(a, ra);
+}
+
 bool Engine::s2rows_ok(const Op& op, const ConvLayer& D, int B) const {
   const ConvLayer& L = convs_[op.conv];
   const ActShape& is = shapes_[op.in];
@@ -1227,6 +1246,13 @@ void Engine::run_ops(const uint8_t* images, int B, int Hin, int Win, int32_t* id
             conv1x1(a, num_cus_, cs);
             break;
           }
+        }
+        if (cs == s && chain_ok(oi, B)) {
+          ConvArgs a = conv_args(op, B, logits), ra = conv_args(ops_[oi + 1], B, logits);
+          a.split_k = ra.split_k = 1;
+          conv1x1_chain(a, ra, num_cus_, cs);
+          skip = 1;
+          break;
         }
         if (cs == s && bottleneck_fusable(oi)) {
           const ConvLayer& L2 = convs_[ops_[oi + 1].conv];

@@ -114,6 +114,10 @@ struct EngineOptions {
   bool stem_dense = true;        // ... with the dense-K weight order (5 K steps a fragment instead of 7)
   bool bigtile = true;           // 8-wave big-tile split-K convs where picked (not on the ResNet18 b256 path)
   bool conv1x1 = true;           // weight-stationary 1x1 convs (conv1x1.hip: ResNet50 bottlenecks)
+  // resnet50_fp8 layer2: an expand conv and the next bottleneck's reduce conv
+  // on its output in one launch (conv1x1_chain: the reduce reads the output
+  // blocks from LDS instead of 102.8 MB back from HBM at B = 256)
+  bool chain_1x1 = true;
   bool fused_pool = true;        // the last conv's epilogue computes the global average pool
   bool fused_head = true;        // avgpool + fc + softmax / top-1 in one kernel (head.hip)
   bool direct13 = true;          // AlexNet's 13x13 3x3 convs with the image resident in LDS (conv3x3_13.hip)
@@ -244,7 +248,8 @@ class Engine {
   bool bottleneck_conv3(const ConvLayer& L) const;  // L is such a block's expand conv (fragment-order weights)
   int ds_expand_op(size_t oi) const;  // ops[oi] = a downsample folded into a later expand conv: that op, or -1
   bool s2rows_ok(const Op& op, const ConvLayer& D, int B) const;  // layer2.0 conv1 + downsample -> conv3x3_s2rows
-  bool ds_conv2_ok(size_t oi, int B) const;  // ... and that downsample as K steps of conv2 (ds_into_conv2)
+  bool ds_conv2_ok(size_t oi, int B) const;
+  bool chain_ok(size_t oi, int B) const;  // ops[oi] (expand) + ops[oi + 1] (reduce) as one conv1x1_chain  // ... and that downsample as K steps of conv2 (ds_into_conv2)
 
   std::string arch_;
   int device_ = 0;

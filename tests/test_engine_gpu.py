@@ -588,6 +588,32 @@ def test_resnet50_fp8_fused_bottleneck_matches_unfused(gpu):
         assert prof[blk + ".conv3"] < 0.6 * rprof[blk + ".conv3"], (blk, prof, rprof)
 
 
+@pytest.mark.parametrize("B", [32, 256])
+def test_resnet50_fp8_chain_1x1_matches_unchained(gpu, B):
+    """resnet50_fp8 layer2: each expand conv with the next bottleneck's reduce
+    conv on its output in one launch (conv1x1_chain: the reduce reads the
+    output blocks from LDS) vs two launches. Same MFMA instruction per 128-K
+    step, same K order, same epilogue arithmetic: the logits are bit-identical;
+    and the chained path is the one that ran (the reduce ops it absorbs take
+    no kernel time of their own)."""
+    model = build("resnet50", seed=71, randomize_bn=True)
+    sd = state_dict_f32(model)
+    g = torch.Generator().manual_seed(72)
+    x = torch.randint(0, 256, (B, 224, 224, 3), generator=g, dtype=torch.uint8).to(gpu)
+    eng = InferenceEngine("resnet50_fp8", sd, max_batch=B, options={"chain_1x1": True})
+    ref_eng = InferenceEngine("resnet50_fp8", sd, max_batch=B, options={"chain_1x1": False})
+    ci, cp, cl = eng.predict(x, return_logits=True, use_graph=False)
+    gi, gp = eng.predict(x)
+    ri, rp, rl = ref_eng.predict(x, return_logits=True, use_graph=False)
+    torch.cuda.synchronize()
+    assert torch.equal(cl, rl), ((cl - rl).abs().max().item(), (rl.norm()).item())
+    assert torch.equal(ci, ri) and torch.equal(ci, gi)
+    prof = dict(eng._e.profile(x.data_ptr(), B, 224, 224, 0))
+    rprof = dict(ref_eng._e.profile(x.data_ptr(), B, 224, 224, 0))
+    for blk in ("layer2.1", "layer2.2", "layer2.3"):
+        assert prof[blk + ".conv1"] < 0.6 * rprof[blk + ".conv1"], (blk, prof, rprof)
+
+
 def test_unknown_engine_option_is_an_error(gpu):
     with pytest.raises(Exception, match="unknown engine option"):
         InferenceEngine("resnet18", max_batch=1, options={"no_such_path": True})
