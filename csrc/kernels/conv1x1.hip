@@ -168,8 +168,11 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void conv1x1_kernel(C1Arg
   constexpr int RT = RES ? NPF * NG : 0;    // residual loads per wave per block
   constexpr int NP2 = CH ? WV * NW : 0;     // chained reduce: its K (= N, e4m3 bytes per pixel)
   constexpr int KS2 = NP2 / 128;            // its K steps
-  constexpr int ST = NPF * NG + (CH ? NPF : 0);  // stores per wave per block (+ the reduce's)
-  constexpr int N1 = (S - 1) * (ST + RT + DT);
+  constexpr int ST2 = CH ? NPF : 0;         // the chained reduce's stores (of the previous block)
+  constexpr int ST = NPF * NG + ST2;        // stores per wave per block
+  // (CH: the previous block's reduce stores are issued after this block's
+  // R and D, so one more ST2 sits between a block's DMA and its wait)
+  constexpr int N1 = (S - 1) * (ST + RT + DT) + ST2;
   static_assert(DT >= 1 && KS >= 1, "tile");
   static_assert(!CH || (IN8 && OUT8 && RES && W16 && NG == 1 && NP2 == 512 && S2 == 1), "chained reduce form");
   using WFrag = typename std::conditional<IN8, v8i, bf16x8>::type;
@@ -302,6 +305,7 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void conv1x1_kernel(C1Arg
   // 64-channel forms have no registers for a second set; each block loads
   // its own residual with its DMA.)
   constexpr bool PRE = RES && OUT8 && (WV == 8 || RB <= 256);  // (the 4-wave 512-B form: no registers either)
+  static_assert(!CH || PRE, "the chained reduce form loads its residual a block ahead");
   RV rv0[NPF][NG], rv1[NPF][NG];
   auto load_res = [&](int blk, RV (&rv)[NPF][NG]) __attribute__((always_inline)) {
     const bool live = blk < a.nblocks;  // (past the end: the zero page, so every wave issues RT loads)
@@ -323,6 +327,44 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void conv1x1_kernel(C1Arg
 #pragma unroll
   for (int s = 0; s < S - 1; ++s) issue_dma(mstart + s * mstride, s);
 
+  // ---- CH: the chained reduce of block blk from ybuf (issued at the start of
+  // the next block, between its loads and its DMA wait, so it runs under
+  // that latency; every wave wrote its share of ybuf before the barrier that
+  // opens that block, and none writes ybuf again before the block's second
+  // barrier: one buffer suffices)
+  auto reduce = [&](int blk) __attribute__((always_inline)) {
+    floatx4 acc2[NPF];
+#pragma unroll
+    for (int pf = 0; pf < NPF; ++pf) acc2[pf] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KS2; ++ks) {
+      v8i xb[NPF];
+#pragma unroll
+      for (int pf = 0; pf < NPF; ++pf) {
+        const int p = pf * 16 + fr, c0 = ks * 8 + 2 * g;
+        const char* row = ybuf + p * NP2;
+        const uint4 lo = *(const uint4*)(row + ((c0 ^ (p & 15)) << 4));
+        const uint4 hi = *(const uint4*)(row + (((c0 + 1) ^ (p & 15)) << 4));
+        xb[pf] = v8i{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+      }
+#pragma unroll
+      for (int pf = 0; pf < NPF; ++pf)
+        acc2[pf] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(wf2[ks], xb[pf], acc2[pf], 0, 0, 0, 127, 0, 127);
+    }
+#pragma unroll
+    for (int pf = 0; pf < NPF; ++pf) {
+      const long m = (long)blk * kBM + pf * 16 + fr;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const f32x2 r = __builtin_elementwise_fma(f32x2{acc2[pf][2 * e], acc2[pf][2 * e + 1]}, al2[e], bs2[e]);
+        v[2 * e] = __builtin_amdgcn_fmed3f(r.x, relu_lo2, 448.f);
+        v[2 * e + 1] = __builtin_amdgcn_fmed3f(r.y, relu_lo2, 448.f);
+      }
+      *(uint32_t*)((uint8_t*)a.y2 + m * a.N2 + wave * 16 + 4 * g) = f32x4_to_fp8_sat(v);
+    }
+  };
+
   // per block a wave issues R [RT] (PRE: the next block's), D(block + S-1)
   // [DT], then after the MFMAs its stores [ST]. The block's rows have landed
   // when at most N1 = (S-1)(RT+DT+ST) newer operations are outstanding; its
@@ -334,8 +376,17 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void conv1x1_kernel(C1Arg
     if constexpr (PRE) load_res(blk + mstride, rvn);
     else if constexpr (RES) load_res(blk, rv);
     issue_dma(blk + (S - 1) * mstride, (it + S - 1) % S);
-    if (it < S - 1) vm_wait<PRE ? RT + DT : DT>();  // prologue blocks: only this block's issues may stay in flight
-    else vm_wait<N1>();
+    if constexpr (CH) {
+      if (it > 0) reduce(blk - mstride);
+    }
+    if (it < S - 1) {  // prologue blocks: only this block's issues (CH: + the reduce stores) may stay in flight
+      if (CH && it > 0) vm_wait<(PRE ? RT + DT : DT) + ST2>();
+      else vm_wait<PRE ? RT + DT : DT>();
+    } else if (CH && it == S - 1) {
+      vm_wait<N1 - ST2>();  // (block 0 had no reduce to issue)
+    } else {
+      vm_wait<N1>();
+    }
     lds_barrier();  // every wave's share of block blk's rows has landed
     // ---- MFMAs: acc[pf][f] = D[channel ch(f, 4g+i)][pixel 16pf + fr]
     const char* sb = stages + st * STAGE;
@@ -375,7 +426,7 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void conv1x1_kernel(C1Arg
     // ---- epilogue
     if constexpr (RES) {
       if constexpr (PRE) {
-        if (it >= S - 1) vm_wait<2 * DT + ST + RT>();  // this block's residual (earlier blocks: waited above)
+        if (it >= S - 1) vm_wait<2 * DT + ST + RT + ST2>();  // this block's residual (earlier blocks: waited above)
       } else {
         vm_wait<DT>();  // this block's residual (only the DMA issued after it may be in flight)
       }
@@ -466,42 +517,6 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void conv1x1_kernel(C1Arg
         }
       }
     }
-    if constexpr (CH) {
-      // ---- chained reduce on the block (every wave's share of it is in
-      // ybuf after the barrier; the next block's ybuf writes come after its
-      // two barriers, so one buffer suffices)
-      lds_barrier();
-      floatx4 acc2[NPF];
-#pragma unroll
-      for (int pf = 0; pf < NPF; ++pf) acc2[pf] = floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int ks = 0; ks < KS2; ++ks) {
-        v8i xb[NPF];
-#pragma unroll
-        for (int pf = 0; pf < NPF; ++pf) {
-          const int p = pf * 16 + fr, c0 = ks * 8 + 2 * g;
-          const char* row = ybuf + p * NP2;
-          const uint4 lo = *(const uint4*)(row + ((c0 ^ (p & 15)) << 4));
-          const uint4 hi = *(const uint4*)(row + (((c0 + 1) ^ (p & 15)) << 4));
-          xb[pf] = v8i{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
-        }
-#pragma unroll
-        for (int pf = 0; pf < NPF; ++pf)
-          acc2[pf] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(wf2[ks], xb[pf], acc2[pf], 0, 0, 0, 127, 0, 127);
-      }
-#pragma unroll
-      for (int pf = 0; pf < NPF; ++pf) {
-        const long m = (long)blk * kBM + pf * 16 + fr;
-        float v[4];
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          const f32x2 r = __builtin_elementwise_fma(f32x2{acc2[pf][2 * e], acc2[pf][2 * e + 1]}, al2[e], bs2[e]);
-          v[2 * e] = __builtin_amdgcn_fmed3f(r.x, relu_lo2, 448.f);
-          v[2 * e + 1] = __builtin_amdgcn_fmed3f(r.y, relu_lo2, 448.f);
-        }
-        *(uint32_t*)((uint8_t*)a.y2 + m * a.N2 + wave * 16 + 4 * g) = f32x4_to_fp8_sat(v);
-      }
-    }
   };
   int it = 0;
   if constexpr (PRE) {
@@ -511,6 +526,14 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void conv1x1_kernel(C1Arg
     }
   } else {
     for (int blk = mstart; blk < a.nblocks; blk += mstride, ++it) block(blk, it, rv0, rv0);
+  }
+  if constexpr (CH) {
+    if (it > 0) {  // the last block's reduce
+      lds_barrier();
+      int last = mstart;
+      while (last + mstride < a.nblocks) last += mstride;
+      reduce(last);
+    }
   }
   vm_wait<0>();  // no LDS-DMA may outlive the workgroup
 }
