@@ -305,6 +305,22 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("head_ws_bytes", &head_ws_bytes);
   m.def("head_pooled_splits", &head_pooled_splits);
+  m.def("conv1x1_plan", [](bool in8, bool out8, int rb, int nw, bool res, int s, int wv, bool ch) {
+    const C1Plan p = conv1x1_plan(in8, out8, rb, nw, res, s, wv, ch);
+    py::dict d;
+    d["s"] = p.s;
+    d["dt"] = p.dt;
+    d["rt"] = p.rt;
+    d["st"] = p.st;
+    d["st2"] = p.st2;
+    d["pre"] = p.pre;
+    d["n1"] = p.n1;
+    d["n1_first"] = p.n1_first;
+    d["pro_wait"] = p.pro_wait;
+    d["pro_wait_ch"] = p.pro_wait_ch;
+    d["res_wait"] = p.res_wait;
+    return d;
+  });
   m.def("head_pooled", [](uintptr_t pooled, uintptr_t w, uintptr_t bias, int B, int C, int N, int ldw, int Npad,
                           uintptr_t logits, uintptr_t idx, uintptr_t prob, uintptr_t ws, size_t ws_bytes, int num_cus,
                           uintptr_t stream, int ns, int ko) {

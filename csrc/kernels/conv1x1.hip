@@ -138,6 +138,44 @@ struct C1Args {
 template <int RB>
 constexpr int block_m() { return RB <= 512 ? 64 : 32; }
 
+}  // namespace
+
+// The block loop's vector-memory plan (kernels.h C1Plan): operation counts per
+// wave per block and every s_waitcnt vmcnt threshold, computed once here for
+// the kernel's template constants and for the host (conv1x1_plan:
+// tests/test_conv1x1_vmcnt_cpu.py replays the kernel's issue order against it).
+constexpr C1Plan c1_plan(bool in8, bool out8, int rb, int nw, bool res, int s, int wv, bool ch) {
+  C1Plan p{};
+  const int bm = rb <= 512 ? 64 : 32;
+  const int nf = nw / 16;
+  const bool w16 = out8 && nf >= 4;
+  const int ng = w16 ? nf / 4 : nf >= 2 ? nf / 2 : 1;
+  const int npf = bm / 16;
+  p.s = s;
+  p.dt = bm * rb / 16 / 64 / wv;
+  p.rt = res ? npf * ng : 0;
+  p.st2 = ch ? npf : 0;
+  p.st = npf * ng + p.st2;
+  p.pre = res && out8 && (wv == 8 || rb <= 256);
+  // block it's rows were DMA'd S-1 blocks earlier; everything issued since:
+  // (S-1) blocks of R + D + stores, and (CH) one more set of reduce stores
+  // (the previous block's, issued after this block's R and D)
+  p.n1 = (s - 1) * (p.st + p.rt + p.dt) + p.st2;
+  p.n1_first = p.n1 - p.st2;  // CH, block S-1: block 0 issued no reduce stores
+  p.pro_wait = p.pre ? p.rt + p.dt : p.dt;  // blocks < S-1: only this block's R, D in flight
+  p.pro_wait_ch = p.pro_wait + p.st2;       // ... and (CH, it > 0) the reduce stores after them
+  // PRE: block it's residual came with block it-1's R, before D(it-1), its
+  // stores, R(it), D(it) and (CH) the reduce stores of it-2 and it-1
+  p.res_wait = p.pre ? 2 * p.dt + p.st + p.rt + p.st2 : p.dt;
+  return p;
+}
+
+C1Plan conv1x1_plan(bool in8, bool out8, int rb, int nw, bool res, int s, int wv, bool ch) {
+  return c1_plan(in8, out8, rb, nw, res, s, wv, ch);
+}
+
+namespace {
+
 // WV waves per workgroup: 4 (two workgroups per CU, <= 64 weight VGPRs per
 // wave) or 8 (one per CU, <= 128 weight VGPRs per wave: twice the channels
 // per wave and per workgroup, so a wide layer restages its input for fewer
@@ -164,15 +202,16 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void conv1x1_kernel(C1Arg
   constexpr int CPL = W16 ? 16 : NF >= 2 ? 8 : 4;          // channels per lane per group
   constexpr int NPF = kBM / 16;             // pixel fragments per block
   constexpr int STAGE = kBM * RB;
-  constexpr int DT = STAGE / 16 / 64 / WV;  // DMA instructions per wave per block
-  constexpr int RT = RES ? NPF * NG : 0;    // residual loads per wave per block
+  constexpr C1Plan P = c1_plan(IN8, OUT8, RB, NW, RES, S, WV, CH);
+  constexpr int DT = P.dt;                  // DMA instructions per wave per block
+  constexpr int RT = P.rt;                  // residual loads per wave per block
   constexpr int NP2 = CH ? WV * NW : 0;     // chained reduce: its K (= N, e4m3 bytes per pixel)
   constexpr int KS2 = NP2 / 128;            // its K steps
-  constexpr int ST2 = CH ? NPF : 0;         // the chained reduce's stores (of the previous block)
-  constexpr int ST = NPF * NG + ST2;        // stores per wave per block
+  constexpr int ST2 = P.st2;                // the chained reduce's stores (of the previous block)
+  constexpr int ST = P.st;                  // stores per wave per block
   // (CH: the previous block's reduce stores are issued after this block's
   // R and D, so one more ST2 sits between a block's DMA and its wait)
-  constexpr int N1 = (S - 1) * (ST + RT + DT) + ST2;
+  constexpr int N1 = P.n1;
   static_assert(DT >= 1 && KS >= 1, "tile");
   static_assert(!CH || (IN8 && OUT8 && RES && W16 && NG == 1 && NP2 == 512 && S2 == 1), "chained reduce form");
   using WFrag = typename std::conditional<IN8, v8i, bf16x8>::type;
@@ -304,7 +343,7 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void conv1x1_kernel(C1Arg
   // hides under a whole block, not just the block's own MFMAs. (bf16: the
   // 64-channel forms have no registers for a second set; each block loads
   // its own residual with its DMA.)
-  constexpr bool PRE = RES && OUT8 && (WV == 8 || RB <= 256);  // (the 4-wave 512-B form: no registers either)
+  constexpr bool PRE = P.pre;  // (RES && OUT8 && (WV == 8 || RB <= 256): the 4-wave 512-B form has no registers either)
   static_assert(!CH || PRE, "the chained reduce form loads its residual a block ahead");
   RV rv0[NPF][NG], rv1[NPF][NG];
   auto load_res = [&](int blk, RV (&rv)[NPF][NG]) __attribute__((always_inline)) {
@@ -380,10 +419,10 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void conv1x1_kernel(C1Arg
       if (it > 0) reduce(blk - mstride);
     }
     if (it < S - 1) {  // prologue blocks: only this block's issues (CH: + the reduce stores) may stay in flight
-      if (CH && it > 0) vm_wait<(PRE ? RT + DT : DT) + ST2>();
-      else vm_wait<PRE ? RT + DT : DT>();
+      if (CH && it > 0) vm_wait<P.pro_wait_ch>();
+      else vm_wait<P.pro_wait>();
     } else if (CH && it == S - 1) {
-      vm_wait<N1 - ST2>();  // (block 0 had no reduce to issue)
+      vm_wait<P.n1_first>();  // (block 0 had no reduce to issue)
     } else {
       vm_wait<N1>();
     }
@@ -426,9 +465,9 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void conv1x1_kernel(C1Arg
     // ---- epilogue
     if constexpr (RES) {
       if constexpr (PRE) {
-        if (it >= S - 1) vm_wait<2 * DT + ST + RT + ST2>();  // this block's residual (earlier blocks: waited above)
+        if (it >= S - 1) vm_wait<P.res_wait>();  // this block's residual (earlier blocks: waited above)
       } else {
-        vm_wait<DT>();  // this block's residual (only the DMA issued after it may be in flight)
+        vm_wait<P.res_wait>();  // this block's residual (only the DMA issued after it may be in flight)
       }
 #pragma unroll
       for (int pf = 0; pf < NPF; ++pf)

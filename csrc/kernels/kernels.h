@@ -104,6 +104,16 @@ void conv1x1(const ConvArgs& a, int num_cus, hipStream_t s);
 // bottleneck's reduce conv r (1x1, K = 512 -> 128) on its output, one launch
 // (the reduce input never goes back to HBM; conv1x1.hip CH form)
 bool conv1x1_chain_supported(const ConvArgs& a, const ConvArgs& r);
+// conv1x1.hip's block-loop vmcnt plan for one kernel form (in8 / out8, staged
+// row bytes rb, channels per wave nw, residual, stages s, waves wv, chained
+// reduce): per-wave operation counts per block (DMA dt, residual rt, stores st
+// of which st2 are the chained reduce's) and every wait's threshold.
+struct C1Plan {
+  int s, dt, rt, st, st2;
+  bool pre;  // residual loaded one block ahead
+  int n1, n1_first, pro_wait, pro_wait_ch, res_wait;
+};
+C1Plan conv1x1_plan(bool in8, bool out8, int rb, int nw, bool res, int s, int wv, bool ch);
 void conv1x1_chain(const ConvArgs& a, const ConvArgs& r, int num_cus, hipStream_t s);
 int conv_bigtile_pick(const ConvArgs& a, int num_cus);  // engine's choice: config, or -1 (old kernel)
 int conv_bigtile_splits(const ConvArgs& a, int cfg, int num_cus);
