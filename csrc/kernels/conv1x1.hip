@@ -27,8 +27,11 @@
 // residual loads), DMA (S-1 blocks ahead; dummy zero-page loads past the end
 // keep the counts uniform) and ST (stores); the block's DMA has landed when at
 // most (S-1)(ST+RES+DMA) newer operations are outstanding, its residual when
-// at most 2 DMA + ST + RES are. Only M % BM == 0 is supported (BM = 64, 32 for 1-KB rows: no
-// partial blocks, so every wave issues the same instruction counts).
+// at most 2 DMA + ST + RES are (the chained form's reduce stores, issued with
+// the next block, add to both; every threshold comes from c1_plan below and
+// is replayed against this issue order in tests/test_conv1x1_vmcnt_cpu.py).
+// Only M % BM == 0 is supported (BM = 64, 32 for 1-KB rows: no partial
+// blocks, so every wave issues the same instruction counts).
 #include "common.h"
 #include "kernels.h"
 
@@ -405,10 +408,11 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void conv1x1_kernel(C1Arg
   };
 
   // per block a wave issues R [RT] (PRE: the next block's), D(block + S-1)
-  // [DT], then after the MFMAs its stores [ST]. The block's rows have landed
-  // when at most N1 = (S-1)(RT+DT+ST) newer operations are outstanding; its
-  // residual when at most 2 DT + ST + RT (PRE: issued one block earlier,
-  // after D(block + S-2)) / DT are.
+  // [DT], (CH) the previous block's reduce stores [ST2], then after the MFMAs
+  // its stores [ST - ST2]. The block's rows have landed when at most N1 =
+  // (S-1)(RT+DT+ST) + ST2 newer operations are outstanding; its residual when
+  // at most 2 DT + ST + RT + ST2 (PRE: issued one block earlier, after
+  // D(block + S-2)) / DT are (C1Plan).
   auto block = [&](int blk, int it, RV (&rv)[NPF][NG], RV (&rvn)[NPF][NG]) __attribute__((always_inline)) {
     const int st = it % S;
     lds_barrier();  // every wave is done with stage (it-1) % S: the DMA below reuses it
