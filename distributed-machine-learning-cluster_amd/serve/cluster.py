@@ -55,8 +55,13 @@ class NodeProcess:
                 self.lines.append(line.rstrip("\n"))
 
     def send(self, line: str) -> None:
-        self.proc.stdin.write(line + "\n")
-        self.proc.stdin.flush()
+        try:
+            self.proc.stdin.write(line + "\n")
+            self.proc.stdin.flush()
+        except BrokenPipeError as e:  # the node exited: say how, with its last output
+            rc = self.proc.wait(timeout=5)
+            raise RuntimeError(f"node {self.address} exited (rc {rc}) before {line!r}; output:\n"
+                               f"{self.output()[-4000:]}") from e
 
     def mark(self) -> int:
         with self._lock:

@@ -191,7 +191,7 @@ def test_hung_node_failover(env, tmp_path, victim):
     another member. Either way answers flow again within a few seconds and
     both jobs finish."""
     models = f"resnet18={env['models']['resnet18']},alexnet={env['models']['alexnet']}"
-    base = 19700 if victim == "leader" else 19800
+    base = 21000 if victim == "leader" else 21100  # (ports no other test uses: the suite runs in parallel)
     cl = LocalCluster(4, base, str(tmp_path / "c"), env["labels"], n_leaders=2, executor="cpu",
                       dataset=env["dataset"], models=models, fast=False,
                       extra=["--job-limit", "48", "--query-interval-ms", "250", "--quiet-predictions",
