@@ -139,6 +139,26 @@ void test_stats() {
   CHECK(rep.find("2 total, 2.000 ms avg") != std::string::npos);
 }
 
+// The take-over's resume decision on a standby's copy (LeaderService::
+// succession_loop): job 0 issued queries but had no answer yet when the copy
+// was taken, job 1 had answers; the started stamp travels in the delta copy.
+void test_resume_decision() {
+  Job a, b;
+  a.model_name = "resnet18";
+  b.model_name = "alexnet";
+  CHECK(!jobs_running({a, b}));
+  a.started_us = 123;
+  b.add_result(true, 1000);
+  CHECK(jobs_running({a, Job{}}));
+  CHECK(jobs_running({Job{}, b}));
+  Writer w;
+  write_job_delta(w, a, 0);
+  Reader r(w.data());
+  Job copy;
+  CHECK(read_job_delta(r, copy));
+  CHECK(copy.started_us == 123 && copy.durations_us.empty() && jobs_running({copy, Job{}}));
+}
+
 void test_table() {
   const std::string t = make_table({"a", "bb"}, {{"xyz", "1"}});
   CHECK(t == "+-----+----+\n| a   | bb |\n+-----+----+\n| xyz | 1  |\n+-----+----+");
@@ -152,6 +172,7 @@ int run_selftest() {
   test_codec();
   test_sdfs_naming();
   test_stats();
+  test_resume_decision();
   test_table();
   std::printf("selftest: %d passed, %d failed\n", g_pass, g_fail);
   return g_fail == 0 ? 0 : 1;

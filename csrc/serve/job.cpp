@@ -91,6 +91,12 @@ bool read_job_delta(Reader& r, Job& j) {
   return true;
 }
 
+bool jobs_running(const std::vector<Job>& jobs) {
+  for (const auto& j : jobs)
+    if (j.started_us != 0 || !j.durations_us.empty()) return true;
+  return false;
+}
+
 Job read_job(Reader& r) {
   Job j;
   j.model_name = r.str();

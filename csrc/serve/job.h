@@ -53,6 +53,9 @@ void write_job_delta(Writer& w, const Job& j, uint32_t from);
 // Applies a delta onto `j` (which holds `from` entries); false if `j` does
 // not line up (the standby then asks for everything again).
 bool read_job_delta(Reader& r, Job& j);
+// A standby that takes over resumes the jobs when its copy shows them
+// running: any job that issued a query or has a completed one.
+bool jobs_running(const std::vector<Job>& jobs);
 
 struct LatencyStats {
   size_t count = 0;

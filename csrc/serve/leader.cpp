@@ -780,8 +780,7 @@ void LeaderService::succession_loop() {
         // resume when the copy shows the jobs running: any job that issued or
         // finished a query (not only job 0's completions: a copy taken before
         // the first job's first answer would otherwise leave both jobs stopped)
-        resume = false;
-        for (const auto& j : jobs_) resume = resume || j.started_us != 0 || !j.durations_us.empty();
+        resume = jobs_running(jobs_);
       }
       {
         // the previous leader's node was unreachable (that is what moved the
