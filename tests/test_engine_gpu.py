@@ -588,7 +588,7 @@ def test_resnet50_fp8_fused_bottleneck_matches_unfused(gpu):
         assert prof[blk + ".conv3"] < 0.6 * rprof[blk + ".conv3"], (blk, prof, rprof)
 
 
-@pytest.mark.parametrize("B", [32, 256])
+@pytest.mark.parametrize("B", [4, 12, 32, 256])
 def test_resnet50_fp8_chain_1x1_matches_unchained(gpu, B):
     """resnet50_fp8 layer2: each expand conv with the next bottleneck's reduce
     conv on its output in one launch (conv1x1_chain: the reduce reads the
@@ -608,6 +608,8 @@ def test_resnet50_fp8_chain_1x1_matches_unchained(gpu, B):
     torch.cuda.synchronize()
     assert torch.equal(cl, rl), ((cl - rl).abs().max().item(), (rl.norm()).item())
     assert torch.equal(ci, ri) and torch.equal(ci, gi)
+    if B < 32:  # (ragged persistent grids: workgroups with one block or none; timing is launch-bound)
+        return
     prof = dict(eng._e.profile(x.data_ptr(), B, 224, 224, 0))
     rprof = dict(ref_eng._e.profile(x.data_ptr(), B, 224, 224, 0))
     for blk in ("layer2.1", "layer2.2", "layer2.3"):
